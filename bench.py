@@ -1,0 +1,248 @@
+#!/usr/bin/env python
+"""Benchmark: ODE RHS evals/s at |E|≈1.2M, d=128 (BASELINE.json `metric`).
+
+Workload (BASELINE.json configs[2], the config the metric is quoted on):
+G-arxiv synthetic graph — N = 169,343 nodes, E' = 1,200,000 edges (RMAT +
+self loops, rw-normalised), C = 128 fp32 features — integrated with rk4
+(torchdiffeq rk4_alt_step_func, 4 RHS evaluations per step) through the drop-in
+LaplacianODEFunc (function='laplacian', block='constant', add_source=False:
+src/best_params.py:7 for ogbn-arxiv).  A "step" is one rk4 step: 4 RHS
+evaluations (K1, gnpde_spmm_rhs_f32) + 4 fused stage combinations.
+
+value = RHS evaluations per second over the whole job (all ranks), inputs
+resident in HBM.  Multi-GPU: one process per GPU, each integrating its own
+G-arxiv graph (the reference's batch axis; independent objects, no data-path
+collective) -> "scaling": "weak"; the time is the max over ranks.
+
+Extra objects on the JSON line:
+  roofline      K1 achieved GB/s (algorithmic bytes / mean per-launch time from
+                HIP events on the launch stream) vs the 8 TB/s HBM peak;
+  cpu_baseline  the CPU oracle (scipy CSR, fp32) on a bounded sample, rank 0, N=1;
+  attention     the transformer RHS (config C4 shape: C=128, h=2, att=32) in
+                reference (fork scaled_dot) and per_edge modes.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "graph-neural-pde_amd"))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def lap_bytes(N, E, C, add_source=False):
+    """Algorithmic HBM bytes of one Laplacian RHS:
+    gathered x rows 4EC + x_i read & f write 8NC + col/weight 8E + rowptr 4(N+1)."""
+    return 4 * E * C + 8 * N * C + 8 * E + 4 * (N + 1) + (4 * N * C if add_source else 0)
+
+
+def attn_bytes(N, E, C, att, mode):
+    """Algorithmic bytes of one attention RHS.  per_edge: projection
+    4NC + 8N*att, stats+aggregation 4N*att + 4E*att + 4EC + 8NC + 4E + 4(N+1);
+    reference: the k gather is replaced by the key-sum pass 4N*att + 4N."""
+    base = 4 * N * C + 8 * N * att + 4 * N * att + 4 * E * C + 8 * N * C + 4 * E + 4 * (N + 1)
+    return base + (4 * E * att if mode == "per_edge" else 4 * N * att + 4 * N)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--nodes", type=int, default=169343)
+    p.add_argument("--edges", type=int, default=1200000)
+    p.add_argument("--dim", type=int, default=128)
+    p.add_argument("--step-size", type=float, default=0.25)
+    p.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU-baseline sample")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-attention", action="store_true")
+    p.add_argument("--rhs-only", action="store_true", help="time K RHS calls only (for rocprof runs)")
+    return p.parse_args()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    import gnpde
+    from gnpde import ops, synthetic
+    from gnpde.integrator import _Combine, _fixed_step
+
+    N, E, C = args.nodes, args.edges, args.dim
+    ei, w = synthetic.rw_graph(N, E, seed=rank, device=dev)
+    x = synthetic.features(1, N, C, seed=1 + rank, device=dev)
+    opt = {'hidden_dim': C, 'block': 'constant', 'function': 'laplacian', 'add_source': False,
+           'no_alpha_sigmoid': False, 'max_nfe': 10 ** 9, 'multi_modal': False}
+    func = gnpde.LaplacianODEFunc(C, C, opt, dev).to(dev)
+    func.edge_index, func.edge_weight = ei, w
+    combine = _Combine()
+    h = args.step_size
+
+    # instrument the K1 launches with HIP events on the launch (current) stream
+    events = []
+    orig_spmm = ops.spmm_rhs
+
+    def timed_spmm(*a, **k):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        out = orig_spmm(*a, **k)
+        e.record()
+        events.append((s, e))
+        return out
+
+    def run_steps(n, y):
+        for i in range(n):
+            if args.rhs_only:
+                y = func(None, y) if i == 0 else func(None, y)
+            else:
+                y = _fixed_step('rk4', func, i * h, h, (i + 1) * h, y, combine)
+        return y
+
+    with torch.no_grad():
+        g = func.graph_for(x)  # once per graph: CSR + plan (outside the timed region)
+        y = run_steps(args.warmup, x)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        ops.spmm_rhs = timed_spmm
+        import gnpde.function_laplacian_diffusion as fld
+        fld.ops.spmm_rhs = timed_spmm
+        t0 = time.perf_counter()
+        y = run_steps(args.steps, x)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        ops.spmm_rhs = orig_spmm
+        fld.ops.spmm_rhs = orig_spmm
+    assert torch.isfinite(y).all()
+    k1_ms = sum(s.elapsed_time(e) for s, e in events) / max(len(events), 1)
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t)
+    rhs_per_step = 1 if args.rhs_only else 4
+    total_rhs = world * args.steps * rhs_per_step
+    value = total_rhs / elapsed
+    ms_per_step = elapsed * 1e3 / args.steps
+    nbytes = lap_bytes(N, E, C)
+    achieved = nbytes / (k1_ms * 1e-3) / 1e9
+
+    traffic = None
+    tp = os.path.join(ROOT, "profiles", "k1_traffic.json")
+    if os.path.exists(tp):
+        with open(tp) as fh:
+            tj = json.load(fh)
+        if tj.get("nodes") == N and tj.get("edges") == E and tj.get("dim") == C:
+            traffic = tj.get("hbm_bytes_per_launch")
+
+    result = {
+        "metric": "ODE RHS evals/s (and ms/step) at |E|≈1.2M, d=128; achieved HBM GB/s vs roofline",
+        "value": round(value, 2),
+        "unit": "RHS evals/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (seeded RMAT G-arxiv graph per rank, N(0,1) features)",
+        "config": {"workload": "G-arxiv laplacian RHS, rk4 (configs[2])", "nodes": N, "edges": E, "dim": C,
+                   "method": "rk4", "step_size": h, "rhs_per_step": rhs_per_step, "global_batch": world,
+                   "parallelism": "replicas%d" % world, "chunk": g.chunk,
+                   "hub_rows": g.csr.plan.n_heavy},
+        "rhs_ms": round(k1_ms, 4),
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "kernel": "gnpde_spmm_rhs_f32 (agg_kernel + hub fixup)",
+                     "algorithmic_bytes_per_launch": nbytes},
+    }
+
+    if not args.no_attention and rank == 0:
+        result["attention"] = bench_attention(g, x, dev, ops)
+
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(ei, w, x, N, E, C, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(result))
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def bench_attention(g, x, dev, ops, reps=20):
+    C = x.shape[-1]
+    heads, att = 2, 32
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(2)
+    Wq, Wk = [torch.randn(att, C, generator=gen, device=dev) * 0.1 for _ in range(2)]
+    bq, bk = [torch.randn(att, generator=gen, device=dev) * 0.1 for _ in range(2)]
+    alpha = torch.tensor(0.0, device=dev)
+    out = {"config": "C=%d heads=%d attention_dim=%d (configs[3] shape, fp32)" % (C, heads, att)}
+    for mode, norm_idx in (("reference", 1), ("reference", 0), ("per_edge", 0), ("per_edge", 1)):
+        def once():
+            ns = ops.node_scores(g, x, Wq, bq, Wk, bk, heads, 'scaled_dot', mode)
+            m, rl = ops.softmax_stats(g, ns, norm_idx)
+            return ops.attn_rhs(g, ns, m, rl, norm_idx, x, alpha=alpha)
+        with torch.no_grad():
+            g.csc if norm_idx == 1 else None
+            for _ in range(3):
+                once()
+            torch.cuda.synchronize()
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(reps):
+                once()
+            e.record()
+            torch.cuda.synchronize()
+        ms = s.elapsed_time(e) / reps
+        nb = attn_bytes(g.N, g.nnz, C, att, mode)
+        gbs = nb / (ms * 1e-3) / 1e9
+        out["%s_norm%d" % (mode, norm_idx)] = {"rhs_ms": round(ms, 4), "achieved_GBs": round(gbs, 1),
+                                               "frac": round(gbs / HBM_PEAK_GBS, 4), "algorithmic_bytes": nb}
+    return out
+
+
+def cpu_baseline(ei, w, x, N, E, C, budget_s):
+    """The oracle's prepared-CSR Laplacian RHS (scipy, fp32, single thread) on a
+    bounded sample of the same workload: as many RHS evaluations as fit in
+    ~budget_s seconds (at least 3)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+    import gnpde_oracle as O
+    ein, wn, xn = ei.cpu().numpy(), w.cpu().numpy(), x.cpu().numpy()
+    lap = O.LaplacianCSR(ein, wn, N)
+    y = lap.rhs(xn, 0.0)  # warm
+    n, t0 = 0, time.perf_counter()
+    while True:
+        y = lap.rhs(xn, 0.0)
+        n += 1
+        el = time.perf_counter() - t0
+        if (el > budget_s and n >= 3) or n >= 1000:
+            break
+    assert np.isfinite(y).all()
+    return {"value": round(n / el, 3), "unit": "RHS evals/s", "cores": 1, "kind": "port",
+            "sample": "%d full G-arxiv Laplacian RHS evaluations (N=%d, E'=%d, C=%d) in %.1f s; oracle "
+                      "LaplacianCSR (scipy CSR @ x, fp32, single-threaded), %s" % (n, N, E, C, el,
+                                                                                  os.uname().machine)}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,246 @@
+// aggregate.hpp — the gather-aggregate engine shared by the Laplacian RHS (K1)
+// and the attention RHS (K3): one wavefront per work item (a whole CSR row or a
+// chunk of a hub row), rows of x gathered with 16-byte loads, the RHS epilogue
+// fused, hub-row chunks summed in plan order by a fixup pass (deterministic, no
+// float atomics).
+#pragma once
+#include "common.hpp"
+
+namespace gnpde {
+
+// ------------------------------------------------------------------ weight policies
+// Plain per-edge weights (Laplacian RHS, function_laplacian_diffusion.py:54-57).
+struct PlainWeights {
+  const float* __restrict__ w;
+  __device__ __forceinline__ float operator()(int /*row*/, int p, int /*c*/) const { return w[p]; }
+};
+
+// Scores of one (src, dst) pair for one head (function_transformer_attention.py:246-259).
+__device__ __forceinline__ float pair_score(int mode, const float* __restrict__ qi, const float* __restrict__ kj,
+                                            int dk, float p0, float p1) {
+  if (mode == GNPDE_SCORE_DOT) {
+    float s = 0.f;
+    for (int d = 0; d < dk; ++d) s = fmaf(qi[d], kj[d], s);
+    return s * rsqrtf((float)dk) ;
+  } else if (mode == GNPDE_SCORE_EXP_KERNEL) {
+    float s = 0.f;
+    for (int d = 0; d < dk; ++d) {
+      const float t = qi[d] - kj[d];
+      s = fmaf(t, t, s);
+    }
+    return p0 * p0 * expf(-(s / (2.0f * p1 * p1)));
+  } else {  // cosine / pearson: torch>=1.12 CosineSimilarity, each operand / max(norm, eps)
+    float mq = 0.f, mk = 0.f;
+    if (mode == GNPDE_SCORE_PEARSON) {
+      for (int d = 0; d < dk; ++d) { mq += qi[d]; mk += kj[d]; }
+      mq /= (float)dk;
+      mk /= (float)dk;
+    }
+    float nq = 0.f, nk = 0.f, dot = 0.f;
+    for (int d = 0; d < dk; ++d) {
+      const float a = qi[d] - mq, b = kj[d] - mk;
+      nq = fmaf(a, a, nq);
+      nk = fmaf(b, b, nk);
+      dot = fmaf(a, b, dot);
+    }
+    const float den = fmaxf(sqrtf(nq), 1e-5f) * fmaxf(sqrtf(nk), 1e-5f);
+    return dot / den;
+  }
+}
+
+struct ScoreArgs {
+  int mode;
+  int H;
+  int dk;
+  const double* __restrict__ cs;  // [R,H] reference-mode node scores (fp64)
+  const float* __restrict__ q;    // [R,ldqk] per-edge modes
+  const float* __restrict__ k;
+  int64_t ldqk;
+  float p0, p1;
+
+  // score of edge src->dst, head h, as double (exact for the fp32 modes)
+  __device__ __forceinline__ double score(int src, int dst, int h) const {
+    if (mode == GNPDE_SCORE_REFERENCE) return cs[(int64_t)src * H + h];
+    return (double)pair_score(mode, q + (int64_t)src * ldqk + h * dk, k + (int64_t)dst * ldqk + h * dk, dk, p0, p1);
+  }
+};
+
+// Attention weights: w_e = (1/H) sum_h exp(s_e,h - m[g,h]) * rl[g,h]
+// (utils.softmax :116-127, then attention.mean(dim=2), function_transformer_attention.py:34)
+struct AttnWeights {
+  ScoreArgs sa;
+  int norm_idx;                   // group: 0 = src (row), 1 = dst (col)
+  const double* __restrict__ m;   // [R,H]
+  const float* __restrict__ rl;   // [R,H]
+  float invH;
+  __device__ __forceinline__ float operator()(int row, int /*p*/, int c) const {
+    const int g = norm_idx == 0 ? row : c;
+    float w = 0.f;
+    for (int h = 0; h < sa.H; ++h) {
+      const double s = sa.score(row, c, h);
+      const float z = expf((float)(s - m[(int64_t)g * sa.H + h]));
+      w = fmaf(z, rl[(int64_t)g * sa.H + h], w);
+    }
+    return w * invH;
+  }
+};
+
+// ------------------------------------------------------------------ aggregation kernel
+// Lane layout: lane = g*GL + gl; GROUPS = 64/GL edges are gathered side by side,
+// each by a group of GL lanes covering the C columns with VEC-wide loads
+// (NCH column passes).  U edges per group are in flight per iteration.
+template <int VEC, int GL, int NCH, int U, class WP>
+__global__ __launch_bounds__(256) void agg_kernel(const int4* __restrict__ items, int n_items,
+                                                   const int* __restrict__ col, WP wp, int C, Epi ep,
+                                                   float* __restrict__ partials) {
+  constexpr int G = kWave / GL;
+  const int lane = threadIdx.x & 63;
+  const int wid = uniform(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
+  if (wid >= n_items) return;
+  const int4 it = items[wid];
+  const int row = uniform(it.x), beg = uniform(it.y), end = uniform(it.z), slot = uniform(it.w);
+  const int g = lane / GL, gl = lane % GL;
+
+  float acc[NCH][VEC];
+#pragma unroll
+  for (int ch = 0; ch < NCH; ++ch)
+#pragma unroll
+    for (int t = 0; t < VEC; ++t) acc[ch][t] = 0.f;
+
+  for (int e0 = beg; e0 < end; e0 += kWave) {
+    const int n = min(kWave, end - e0);
+    int mc = 0;
+    float mw = 0.f;
+    if (lane < n) {
+      mc = col[e0 + lane];
+      mw = wp(row, e0 + lane, mc);
+    }
+    for (int j = 0; j < n; j += G * U) {
+      float v[U][NCH][VEC];
+      float ww[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int jj = j + u * G + g;
+        const int sl = jj < n ? jj : 0;
+        const int c = __shfl(mc, sl);
+        const float wsl = __shfl(mw, sl);
+        ww[u] = jj < n ? wsl : 0.f;
+        const float* __restrict__ xr = ep.x + (int64_t)c * ep.ldx;
+#pragma unroll
+        for (int ch = 0; ch < NCH; ++ch) {
+          const int cc = (ch * GL + gl) * VEC;
+          if (jj < n && cc < C) {
+            load_vec<VEC>(xr + cc, v[u][ch]);
+          } else {
+#pragma unroll
+            for (int t = 0; t < VEC; ++t) v[u][ch][t] = 0.f;
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int ch = 0; ch < NCH; ++ch)
+#pragma unroll
+          for (int t = 0; t < VEC; ++t) acc[ch][t] = fmaf(ww[u], v[u][ch][t], acc[ch][t]);
+    }
+  }
+  // combine the G edge groups
+#pragma unroll
+  for (int o = GL; o < kWave; o <<= 1)
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch)
+#pragma unroll
+      for (int t = 0; t < VEC; ++t) acc[ch][t] += __shfl_xor(acc[ch][t], o);
+
+  if (g != 0) return;
+  if (slot >= 0) {
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch) {
+      const int cc = (ch * GL + gl) * VEC;
+      if (cc < C) store_vec<VEC>(partials + (int64_t)slot * C + cc, acc[ch]);
+    }
+    return;
+  }
+  const float a = (ep.flags & GNPDE_EPI_RHS) ? epi_alpha(ep) : 1.f;
+  const float b = (ep.flags & GNPDE_ADD_SOURCE) ? *ep.beta : 0.f;
+#pragma unroll
+  for (int ch = 0; ch < NCH; ++ch) {
+    const int cc = (ch * GL + gl) * VEC;
+    if (cc < C) epilogue_store<VEC>(ep, row, cc, acc[ch], a, b);
+  }
+}
+
+// Hub rows: sum the chunk partials in plan order, then the epilogue.
+template <int VEC>
+__global__ __launch_bounds__(256) void agg_fixup_kernel(const int4* __restrict__ heavy, int n_heavy, int C, Epi ep,
+                                                         const float* __restrict__ partials) {
+  const int lane = threadIdx.x & 63;
+  const int wid = uniform(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
+  if (wid >= n_heavy) return;
+  const int4 hv = heavy[wid];
+  const int row = uniform(hv.x), first = uniform(hv.y), nch = uniform(hv.z);
+  const float a = (ep.flags & GNPDE_EPI_RHS) ? epi_alpha(ep) : 1.f;
+  const float b = (ep.flags & GNPDE_ADD_SOURCE) ? *ep.beta : 0.f;
+  for (int cc = lane * VEC; cc < C; cc += kWave * VEC) {
+    float s[VEC];
+#pragma unroll
+    for (int t = 0; t < VEC; ++t) s[t] = 0.f;
+    for (int c = 0; c < nch; ++c) {
+      float v[VEC];
+      load_vec<VEC>(partials + (int64_t)(first + c) * C + cc, v);
+#pragma unroll
+      for (int t = 0; t < VEC; ++t) s[t] += v[t];
+    }
+    epilogue_store<VEC>(ep, row, cc, s, a, b);
+  }
+}
+
+template <int VEC, int GL, int NCH, int U, class WP>
+static int launch_agg_cfg(const int4* items, int64_t n_items, const int4* heavy, int64_t n_heavy, const int* col,
+                          const WP& wp, int C, const Epi& ep, float* partials, hipStream_t s) {
+  if (n_items > 0) {
+    const int64_t grid = ceil_div(n_items, kWavesPerBlock);
+    agg_kernel<VEC, GL, NCH, U, WP><<<(unsigned)grid, kBlock, 0, s>>>(items, (int)n_items, col, wp, C, ep, partials);
+    GNPDE_LAUNCH_CHECK();
+  }
+  if (n_heavy > 0) {
+    const int64_t grid = ceil_div(n_heavy, kWavesPerBlock);
+    agg_fixup_kernel<VEC><<<(unsigned)grid, kBlock, 0, s>>>(heavy, (int)n_heavy, C, ep, partials);
+    GNPDE_LAUNCH_CHECK();
+  }
+  return GNPDE_OK;
+}
+
+template <int VEC, class WP>
+static int launch_agg_vec(const int4* items, int64_t n_items, const int4* heavy, int64_t n_heavy, const int* col,
+                          const WP& wp, int C, const Epi& ep, float* partials, hipStream_t s) {
+  const int lanes = (int)ceil_div(C, VEC);
+  if (lanes <= 16) return launch_agg_cfg<VEC, 16, 1, 4>(items, n_items, heavy, n_heavy, col, wp, C, ep, partials, s);
+  if (lanes <= 32) return launch_agg_cfg<VEC, 32, 1, 4>(items, n_items, heavy, n_heavy, col, wp, C, ep, partials, s);
+  if (lanes <= 64) return launch_agg_cfg<VEC, 64, 1, 4>(items, n_items, heavy, n_heavy, col, wp, C, ep, partials, s);
+  if (lanes <= 128) return launch_agg_cfg<VEC, 64, 2, 2>(items, n_items, heavy, n_heavy, col, wp, C, ep, partials, s);
+  if (lanes <= 256) return launch_agg_cfg<VEC, 64, 4, 2>(items, n_items, heavy, n_heavy, col, wp, C, ep, partials, s);
+  if (lanes <= 512) return launch_agg_cfg<VEC, 64, 8, 1>(items, n_items, heavy, n_heavy, col, wp, C, ep, partials, s);
+  set_error("aggregate: C=%d too wide (max %d)", C, 512 * VEC);
+  return GNPDE_EUNSUPPORTED;
+}
+
+template <class WP>
+static int launch_agg(const int32_t* items, int64_t n_items, const int32_t* heavy, int64_t n_heavy,
+                      const int32_t* col, const WP& wp, int64_t C, const Epi& ep, float* partials, hipStream_t s) {
+  const bool src_ok4 = !(ep.flags & GNPDE_ADD_SOURCE) || (ep.ldx0 % 4 == 0 && aligned16(ep.x0));
+  const bool src_ok2 = !(ep.flags & GNPDE_ADD_SOURCE) || (ep.ldx0 % 2 == 0 && aligned8(ep.x0));
+  const bool v4 = C % 4 == 0 && ep.ldx % 4 == 0 && ep.ldf % 4 == 0 && aligned16(ep.x) && aligned16(ep.f) && src_ok4 &&
+                  (partials == nullptr || aligned16(partials));
+  const bool v2 = C % 2 == 0 && ep.ldx % 2 == 0 && ep.ldf % 2 == 0 && aligned8(ep.x) && aligned8(ep.f) && src_ok2 &&
+                  (partials == nullptr || aligned8(partials));
+  const int4* it = reinterpret_cast<const int4*>(items);
+  const int4* hv = reinterpret_cast<const int4*>(heavy);
+  const int c = (int)C;
+  if (v4) return launch_agg_vec<4>(it, n_items, hv, n_heavy, col, wp, c, ep, partials, s);
+  if (v2) return launch_agg_vec<2>(it, n_items, hv, n_heavy, col, wp, c, ep, partials, s);
+  return launch_agg_vec<1>(it, n_items, hv, n_heavy, col, wp, c, ep, partials, s);
+}
+
+}  // namespace gnpde

@@ -1,0 +1,138 @@
+// common.hpp — shared helpers for the gnpde HIP kernels (gfx950 / CDNA4, wave64).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <string>
+
+#include "../../include/gnpde.h"
+
+namespace gnpde {
+
+// ------------------------------------------------------------------ error plumbing
+void set_error(const char* fmt, ...);
+
+#define GNPDE_REQUIRE(cond, code, ...)      \
+  do {                                      \
+    if (!(cond)) {                          \
+      ::gnpde::set_error(__VA_ARGS__);      \
+      return (code);                        \
+    }                                       \
+  } while (0)
+
+#define GNPDE_HIP(call)                                                                 \
+  do {                                                                                  \
+    hipError_t e_ = (call);                                                             \
+    if (e_ != hipSuccess) {                                                             \
+      ::gnpde::set_error("%s failed: %s (%s:%d)", #call, hipGetErrorString(e_), __FILE__, \
+                         __LINE__);                                                     \
+      return GNPDE_EHIP;                                                                \
+    }                                                                                   \
+  } while (0)
+
+#define GNPDE_LAUNCH_CHECK() GNPDE_HIP(hipGetLastError())
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+inline bool aligned8(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 7u) == 0; }
+
+constexpr int kWave = 64;          // CDNA wavefront width
+constexpr int kBlock = 256;        // 4 waves per workgroup
+constexpr int kWavesPerBlock = kBlock / kWave;
+constexpr float kSoftmaxEps = 1e-16f;  // utils.softmax denominator epsilon, src/utils.py:124-125
+
+// ------------------------------------------------------------------ vector loads
+template <int VEC>
+__device__ __forceinline__ void load_vec(const float* __restrict__ p, float (&v)[VEC]) {
+  if constexpr (VEC == 4) {
+    const float4 t = *reinterpret_cast<const float4*>(p);
+    v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+  } else if constexpr (VEC == 2) {
+    const float2 t = *reinterpret_cast<const float2*>(p);
+    v[0] = t.x; v[1] = t.y;
+  } else {
+    v[0] = *p;
+  }
+}
+
+template <int VEC>
+__device__ __forceinline__ void store_vec(float* __restrict__ p, const float (&v)[VEC]) {
+  if constexpr (VEC == 4) {
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  } else if constexpr (VEC == 2) {
+    *reinterpret_cast<float2*>(p) = make_float2(v[0], v[1]);
+  } else {
+    *p = v[0];
+  }
+}
+
+__device__ __forceinline__ int uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// butterfly reductions over the 64 lanes of a wavefront
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  return v;
+}
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
+  return v;
+}
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// RHS epilogue scalars (device scalars: no host sync, graph-capturable)
+struct Epi {
+  const float* x;
+  int64_t ldx;
+  const float* x0;
+  int64_t ldx0;
+  const float* alpha;
+  const float* beta;
+  int flags;
+  float* f;
+  int64_t ldf;
+};
+
+__device__ __forceinline__ float epi_alpha(const Epi& e) {
+  const float a = *e.alpha;
+  return (e.flags & GNPDE_ALPHA_SIGMOID) ? 1.0f / (1.0f + expf(-a)) : a;
+}
+
+// f = a*(ax - x) [+ b*x0]  (function_laplacian_diffusion.py:69-77) or f = ax
+template <int VEC>
+__device__ __forceinline__ void epilogue_store(const Epi& e, int64_t row, int cc, const float (&ax)[VEC],
+                                               float a, float b) {
+  float o[VEC];
+  if (e.flags & GNPDE_EPI_RHS) {
+    float xr[VEC];
+    load_vec<VEC>(e.x + row * e.ldx + cc, xr);
+#pragma unroll
+    for (int t = 0; t < VEC; ++t) o[t] = a * (ax[t] - xr[t]);
+    if (e.flags & GNPDE_ADD_SOURCE) {
+      float x0r[VEC];
+      load_vec<VEC>(e.x0 + row * e.ldx0 + cc, x0r);
+#pragma unroll
+      for (int t = 0; t < VEC; ++t) o[t] = o[t] + b * x0r[t];
+    }
+  } else {
+#pragma unroll
+    for (int t = 0; t < VEC; ++t) o[t] = ax[t];
+  }
+  store_vec<VEC>(e.f + row * e.ldf + cc, o);
+}
+
+inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+}  // namespace gnpde

@@ -1,0 +1,116 @@
+// linear.hip — the dense node projections of the attention RHS (Q and K of
+// SpGraphTransAttentionLayer, function_transformer_attention.py:224-225) on the
+// CDNA4 matrix cores: exact-f32 v_mfma_f32_32x32x2_f32 (one f32 fma chain per
+// output, same numerics as an fp32 GEMM with a different summation order).
+//
+// Tile: one wavefront = 32 rows x 64 output columns (two 32x32 accumulators),
+// 4 wavefronts per workgroup = 128 rows; blockIdx.y walks 64-column slices of
+// the output.  The K (= C) reduction is split between the two lane halves of
+// the MFMA: half h covers k in [h*Kh, h*Kh + Kh), Kh = ceil(K/2), so each lane
+// streams a contiguous run of its own x row (16-byte loads when K % 8 == 0).
+// W^T for the slice is staged once per workgroup in LDS as [k][64 columns].
+#include "common.hpp"
+
+namespace gnpde {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int kLinRowsPerWave = 32;
+constexpr int kLinCols = 64;
+
+template <bool VEC4>
+__global__ __launch_bounds__(256) void linear_mfma_kernel(const float* __restrict__ x, int R, int K, int64_t ldx,
+                                                           const float* __restrict__ W,
+                                                           const float* __restrict__ bias, int Nout, int split,
+                                                           float* __restrict__ out_a, int64_t lda,
+                                                           float* __restrict__ out_b, int64_t ldb) {
+  extern __shared__ __attribute__((aligned(16))) float wt[];  // [2*Kh][64]
+  const int Kh = (K + 1) >> 1;
+  const int col0 = blockIdx.y * kLinCols;
+  // stage W^T slice: wt[k'][j] = W[col0 + j][k(k')], k' = h*Kh + s  ->  k = k' (k' < K) else 0
+  for (int t = threadIdx.x; t < 2 * Kh * kLinCols; t += blockDim.x) {
+    const int kk = t / kLinCols, j = t - kk * kLinCols;
+    const int n = col0 + j;
+    wt[t] = (kk < K && n < Nout) ? W[(int64_t)n * K + kk] : 0.f;
+  }
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const int r32 = lane & 31, h = lane >> 5;
+  const int row0 = (blockIdx.x * kWavesPerBlock + wv) * kLinRowsPerWave;
+  if (row0 >= R) return;
+  const int my_row = min(row0 + r32, R - 1);
+  const float* __restrict__ xr = x + (int64_t)my_row * ldx;
+  const int kbase = h * Kh;
+
+  f32x16 acc0 = {0}, acc1 = {0};
+  for (int s0 = 0; s0 < Kh; s0 += 4) {
+    float a[4];
+    if constexpr (VEC4) {
+      const float4 t = *reinterpret_cast<const float4*>(xr + kbase + s0);
+      a[0] = t.x; a[1] = t.y; a[2] = t.z; a[3] = t.w;
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int k = kbase + s0 + i;
+        a[i] = (s0 + i < Kh && k < K) ? xr[k] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (s0 + i < Kh) {
+        const float* wrow = wt + (kbase + s0 + i) * kLinCols;
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], wrow[r32], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], wrow[32 + r32], acc1, 0, 0, 0);
+      }
+    }
+  }
+  // C/D layout (32x32): col = lane&31, row = (reg&3) + 8*(reg>>2) + 4*(lane>>5)
+#pragma unroll
+  for (int tile = 0; tile < 2; ++tile) {
+    const int n = col0 + tile * 32 + r32;
+    if (n >= Nout) continue;
+    const float bv = bias ? bias[n] : 0.f;
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const int row = row0 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+      if (row >= R) continue;
+      const float val = (tile == 0 ? acc0[reg] : acc1[reg]) + bv;
+      if (n < split)
+        out_a[(int64_t)row * lda + n] = val;
+      else
+        out_b[(int64_t)row * ldb + (n - split)] = val;
+    }
+  }
+}
+
+}  // namespace gnpde
+
+using namespace gnpde;
+
+extern "C" int gnpde_linear_f32(const float* x, int64_t R, int64_t K, int64_t ldx, const float* W, const float* bias,
+                                int64_t Nout, int64_t split, float* out_a, int64_t lda, float* out_b, int64_t ldb,
+                                void* stream) {
+  GNPDE_REQUIRE(x && W && out_a, GNPDE_EINVAL, "linear: NULL pointer");
+  GNPDE_REQUIRE(R >= 0 && R < INT32_MAX && K >= 1 && ldx >= K && Nout >= 1, GNPDE_EINVAL, "linear: bad sizes");
+  GNPDE_REQUIRE(split >= 0 && split <= Nout, GNPDE_EINVAL, "linear: bad split");
+  GNPDE_REQUIRE(split == Nout || out_b != nullptr, GNPDE_EINVAL, "linear: out_b is NULL");
+  GNPDE_REQUIRE(lda >= split && (split == Nout || ldb >= Nout - split), GNPDE_EINVAL, "linear: bad ld");
+  const int64_t Kh = (K + 1) / 2;
+  const size_t shm = sizeof(float) * (size_t)(2 * Kh * kLinCols);
+  GNPDE_REQUIRE(shm <= 160 * 1024, GNPDE_EUNSUPPORTED, "linear: K=%lld too large for the LDS slice",
+                (long long)K);
+  if (R == 0) return GNPDE_OK;
+  const dim3 grid((unsigned)ceil_div(R, kWavesPerBlock * kLinRowsPerWave), (unsigned)ceil_div(Nout, kLinCols));
+  const bool vec4 = (K % 8 == 0) && (ldx % 4 == 0) && aligned16(x);
+  hipStream_t s = as_stream(stream);
+  if (vec4)
+    linear_mfma_kernel<true><<<grid, kBlock, shm, s>>>(x, (int)R, (int)K, ldx, W, bias, (int)Nout, (int)split, out_a,
+                                                      lda, out_b, ldb);
+  else
+    linear_mfma_kernel<false><<<grid, kBlock, shm, s>>>(x, (int)R, (int)K, ldx, W, bias, (int)Nout, (int)split, out_a,
+                                                       lda, out_b, ldb);
+  GNPDE_LAUNCH_CHECK();
+  return GNPDE_OK;
+}

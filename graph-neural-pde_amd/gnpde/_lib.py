@@ -1,0 +1,106 @@
+"""ctypes binding of libgnpde.so (the C ABI declared in include/gnpde.h).
+
+The library is built in-tree by ``make -C graph-neural-pde_amd`` (or
+``__graft_entry__.build()``).  There is no fallback: if the shared object is
+missing or fails to load, every call raises.  This binding is exactly what a
+maintainer of the reference would add next to ``src/utils.py`` to reach the
+native path (INTEGRATION.md shows it).
+"""
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("GNPDE_LIB", os.path.join(_HERE, "libgnpde.so"))
+
+c_i32p = ctypes.POINTER(ctypes.c_int32)
+c_i64p = ctypes.POINTER(ctypes.c_int64)
+_vp = ctypes.c_void_p
+_i64 = ctypes.c_int64
+_int = ctypes.c_int
+_f32 = ctypes.c_float
+_f64 = ctypes.c_double
+_size = ctypes.c_size_t
+
+# name -> (restype, argtypes); every entry point of include/gnpde.h
+SIGNATURES = {
+    "gnpde_abi_version": (_int, []),
+    "gnpde_last_error": (ctypes.c_char_p, []),
+    "gnpde_csr_workspace_bytes": (_size, [_i64, _i64, _i64]),
+    "gnpde_csr_build": (_int, [_vp, _i64, _i64, _i64, _int, _vp, _vp, _vp, _vp, _size, _vp]),
+    "gnpde_gather_weights_f32": (_int, [_vp, _i64, _int, _vp, _vp, _vp]),
+    "gnpde_indegree_i32": (_int, [_vp, _i64, _i64, _vp, _vp]),
+    "gnpde_plan_workspace_bytes": (_size, [_i64]),
+    "gnpde_plan_build": (_int, [_vp, _i64, ctypes.c_int32, _vp, _i64, _vp, _i64, c_i64p, c_i64p, c_i64p, _vp,
+                                _size, _vp]),
+    "gnpde_spmm_rhs_f32": (_int, [_vp, _i64, _vp, _i64, _vp, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _int, _vp,
+                                  _i64, _vp, _vp]),
+    "gnpde_linear_f32": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _vp]),
+    "gnpde_keysum_workspace_bytes": (_size, [_i64, _i64, _i64, _i64]),
+    "gnpde_ref_scores_f32": (_int, [_vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _vp, _vp,
+                                    _size, _vp]),
+    "gnpde_softmax_stats_f32": (_int, [_vp, _i64, _vp, _i64, _vp, _int, _int, _i64, _i64, _vp, _vp, _vp, _i64, _f32,
+                                       _f32, _vp, _vp, _vp, _vp]),
+    "gnpde_attn_rhs_f32": (_int, [_vp, _i64, _vp, _i64, _vp, _int, _int, _i64, _i64, _vp, _vp, _vp, _i64, _f32, _f32,
+                                  _vp, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _int, _vp, _i64, _vp, _vp]),
+    "gnpde_edge_attention_f32": (_int, [_vp, _i64, _vp, _vp, _int, _int, _i64, _i64, _vp, _vp, _vp, _i64, _f32, _f32,
+                                        _vp, _vp, _vp, _vp]),
+    "gnpde_rk_combine_f32": (_int, [_i64, _vp, _int, ctypes.POINTER(_vp), ctypes.POINTER(_f64), _f64, _vp, _vp]),
+}
+
+# constants mirrored from include/gnpde.h
+ABI_VERSION = 1
+EPI_PLAIN = 0
+EPI_RHS = 1
+ALPHA_SIGMOID = 2
+ADD_SOURCE = 4
+SCORE_REFERENCE = 0
+SCORE_DOT = 1
+SCORE_EXP_KERNEL = 2
+SCORE_COSINE = 3
+SCORE_PEARSON = 4
+
+_lock = threading.Lock()
+_lib = None
+
+
+class GnpdeError(RuntimeError):
+    pass
+
+
+def load():
+    """Load libgnpde.so once; raise GnpdeError (no fallback) if unavailable."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise GnpdeError(
+                "libgnpde.so not found at %s: build it with `make -C graph-neural-pde_amd` or "
+                "`python -c 'import __graft_entry__ as g; g.build()'`" % LIB_PATH)
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        ver = lib.gnpde_abi_version()
+        if ver != ABI_VERSION:
+            raise GnpdeError("libgnpde ABI version %d != expected %d" % (ver, ABI_VERSION))
+        _lib = lib
+        return lib
+
+
+def call(name, *args):
+    """Invoke an entry point; raise GnpdeError with gnpde_last_error() on failure."""
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if rc != 0:
+        msg = lib.gnpde_last_error().decode(errors="replace")
+        raise GnpdeError("%s failed (rc=%d): %s" % (name, rc, msg))
+    return rc
+
+
+def fn(name):
+    return getattr(load(), name)

@@ -1,0 +1,193 @@
+"""Drop-in ODEFunc / ODEblock base classes (reference src/base_classes.py).
+
+Same constructor signatures, attribute contract and state_dict keys as the
+reference, so ``GNN.__init__`` (src/GNN.py:12-15) and the torchdiffeq-style
+loop use them unchanged:
+
+* ``ODEFunc(opt, device)`` — src/base_classes.py:193-211: attributes
+  ``edge_index``, ``edge_weight``, ``attention_weights``, ``x0``, ``nfe``,
+  parameters ``alpha_train``, ``beta_train`` (0-d, init 0), ``alpha_sc``,
+  ``beta_sc``.  Adds a per-graph CSR cache: the first RHS call after
+  ``edge_index`` changes builds the device CSR + plan once; every later call
+  reuses it.
+* ``ODEblock(odefunc, regularization_fns, opt, device, t)`` —
+  src/base_classes.py:110-175: ``odefunc``, ``reg_odefunc.odefunc``,
+  ``train_integrator``/``test_integrator``, ``set_x0``, ``set_tol``,
+  ``reset_tol``, ``reset_graph_data``, ``set_time``.
+* ``GraphData`` — src/base_classes.py:177-190.
+"""
+import torch
+from torch import nn
+
+from . import ops
+from .integrator import odeint, odeint_adjoint
+from .utils import get_rw_adj, gcn_norm_fill_val
+
+
+class GraphData(object):
+    def __init__(self):
+        super(GraphData, self).__init__()
+        self.edge_index = None
+        self.edge_attr = None
+        self.num_nodes = None
+
+    def new_graph(self, edge_index, num_nodes, edge_attr=None):
+        self.edge_index = edge_index
+        self.edge_attr = edge_attr
+        self.num_nodes = num_nodes
+
+    def __repr__(self):
+        return self.__class__.__name__
+
+
+def _tensor_key(t):
+    if t is None:
+        return None
+    return (t.data_ptr(), t._version, tuple(t.shape), t.dtype, str(t.device))
+
+
+class ODEFunc(nn.Module):
+    """Base RHS module (src/base_classes.py:193-211)."""
+
+    def __init__(self, opt, device):
+        super(ODEFunc, self).__init__()
+        self.opt = opt
+        self.device = device
+        self.edge_index = None
+        self.edge_weight = None
+        self.attention_weights = None
+        self.alpha_train = nn.Parameter(torch.tensor(0.0))
+        self.beta_train = nn.Parameter(torch.tensor(0.0))
+        self.x0 = None
+        self.nfe = 0
+        self.alpha_sc = nn.Parameter(torch.ones(1))
+        self.beta_sc = nn.Parameter(torch.ones(1))
+        self._graph = None
+        self._graph_key = None
+        self._w_cache = {}
+
+    def graph_for(self, x):
+        """Device CSR of ``self.edge_index`` for node count x.shape[1] (cached)."""
+        if self.edge_index is None:
+            raise RuntimeError("%s: edge_index is not set (the ODE block sets it in reset_graph_data)" %
+                               self.__class__.__name__)
+        key = (_tensor_key(self.edge_index), int(x.shape[1]))
+        if self._graph is None or key != self._graph_key:
+            chunk = int(self.opt.get('gnpde_chunk', ops.DEFAULT_CHUNK)) if isinstance(self.opt, dict) else \
+                ops.DEFAULT_CHUNK
+            self._graph = ops.GraphCSR(self.edge_index, int(x.shape[1]), chunk=chunk)
+            self._graph_key = key
+            self._w_cache = {}
+        return self._graph
+
+    def csr_weights(self, g, w, tag, transpose=False):
+        """COO-order weights (or [B,E,h] attention -> head mean) in CSR (or CSC) order,
+        cached per tensor version."""
+        tag = (tag, transpose)
+        key = (tag, _tensor_key(w))
+        hit = self._w_cache.get(tag)
+        if hit is not None and hit[0] == key:
+            return hit[1]
+        wc = g.gather_weights(w.detach().float() if w.dtype != torch.float32 else w.detach(), transpose=transpose)
+        self._w_cache[tag] = (key, wc)
+        return wc
+
+    def __repr__(self):
+        return self.__class__.__name__
+
+
+class RegularizedODEfunc(nn.Module):
+    """Holder with the reference's ``reg_odefunc.odefunc`` attribute path
+    (src/regularized_ODE_function.py).  The kinetic-energy / Jacobian
+    regularisers are OUT OF SCOPE (off by default, broken in the fork)."""
+
+    def __init__(self, odefunc, regularization_fns):
+        super(RegularizedODEfunc, self).__init__()
+        self.odefunc = odefunc
+        self.regularization_fns = regularization_fns
+
+    def forward(self, t, state):
+        raise NotImplementedError("gnpde: ODE regularisation terms are out of scope (SURVEY.md §2 row 12)")
+
+
+class ODEblock(nn.Module):
+    """src/base_classes.py:110-175."""
+
+    def __init__(self, odefunc, regularization_fns, opt, device, t):
+        super(ODEblock, self).__init__()
+        self.opt = opt
+        self.t = t
+        self.device = device
+        self.aug_dim = 2 if opt.get('augment', False) else 1
+        self.odefunc = odefunc(self.aug_dim * opt['hidden_dim'], self.aug_dim * opt['hidden_dim'], opt, device)
+        self.nreg = len(regularization_fns)
+        self.reg_odefunc = RegularizedODEfunc(self.odefunc, regularization_fns)
+        self.train_integrator = odeint_adjoint if opt.get('adjoint', False) else odeint
+        self.test_integrator = None
+        self.set_tol()
+        self._prep_key = None
+        self._prep = None
+
+    def set_x0(self, x0):
+        self.odefunc.x0 = x0.clone().detach()
+        self.reg_odefunc.odefunc.x0 = x0.clone().detach()
+
+    def set_tol(self):
+        self.atol = self.opt.get('tol_scale', 1) * 1e-7
+        self.rtol = self.opt.get('tol_scale', 1) * 1e-9
+        if self.opt.get('adjoint', False):
+            self.atol_adjoint = self.opt.get('tol_scale_adjoint', 1) * 1e-7
+            self.rtol_adjoint = self.opt.get('tol_scale_adjoint', 1) * 1e-9
+
+    def reset_tol(self):
+        self.atol = 1e-7
+        self.rtol = 1e-9
+        self.atol_adjoint = 1e-7
+        self.rtol_adjoint = 1e-9
+
+    def reset_graph_data(self, data, dtype, y=None):
+        """src/base_classes.py:147-167 with the intended normalisation semantics
+        (gnpde.utils): self-loops (weight self_loop_weight) + rw (norm_dim=1) or
+        symmetric gcn normalisation.  The reference's second
+        add_remaining_self_loops (:160-162) is a no-op once every node has a
+        loop and is skipped.  Cached on (edge_index, edge_attr) identity, so a
+        model that passes the same graph every forward prepares it once."""
+        if data is not None:
+            key = (_tensor_key(data.edge_index), _tensor_key(data.edge_attr), int(data.num_nodes),
+                   self.opt.get('data_norm', 'rw'), float(self.opt.get('self_loop_weight', 0)), dtype)
+            if key != self._prep_key:
+                self.num_nodes = data.num_nodes
+                if self.opt.get('data_norm', 'rw') == 'rw':
+                    edge_index, edge_weight = get_rw_adj(data.edge_index, edge_weight=data.edge_attr, norm_dim=1,
+                                                         fill_value=self.opt['self_loop_weight'],
+                                                         num_nodes=data.num_nodes, dtype=dtype)
+                else:
+                    edge_index, edge_weight = gcn_norm_fill_val(data.edge_index, edge_weight=data.edge_attr,
+                                                                fill_value=self.opt['self_loop_weight'],
+                                                                num_nodes=data.num_nodes, dtype=dtype)
+                dev = self.device if self.device is not None else edge_index.device
+                self._prep = (edge_index.to(dev), edge_weight.to(dev))
+                self._prep_key = key
+            edge_index, edge_weight = self._prep
+            self.data_edge_index = edge_index
+            self.odefunc.edge_index = edge_index
+            self.odefunc.edge_weight = edge_weight
+            self.reg_odefunc.odefunc.edge_index = edge_index
+            self.reg_odefunc.odefunc.edge_weight = edge_weight
+        self.odefunc.y = y
+
+    def set_time(self, time):
+        self.t = torch.tensor([0, time]).to(self.device)
+
+    def _integrate(self, x, options):
+        if self.training and self.nreg > 0:
+            raise NotImplementedError("gnpde: ODE regularisation terms are out of scope (SURVEY.md §2 row 12)")
+        integrator = self.train_integrator if self.training else self.test_integrator
+        t = self.t.type_as(x)
+        state_dt = integrator(self.odefunc, x, t, method=self.opt['method'], options=options, atol=self.atol,
+                              rtol=self.rtol)
+        return state_dt[1]
+
+    def __repr__(self):
+        return self.__class__.__name__ + '( Time Interval ' + str(self.t[0].item()) + ' -> ' + \
+            str(self.t[1].item()) + ")"

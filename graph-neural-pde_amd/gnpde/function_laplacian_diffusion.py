@@ -1,0 +1,112 @@
+"""Drop-in LaplacianODEFunc (reference src/function_laplacian_diffusion.py:15-77).
+
+``forward(t, x)`` computes ``f = sigma(alpha_train) * (A x - x) [+ beta_train * x0]``
+with one HIP launch (K1, gnpde_spmm_rhs_f32): CSR gather-aggregate with the
+epilogue fused.  The weight source follows ``opt['block']`` exactly as the
+reference (:45-57): 'attention' -> head-mean of ``attention_weights [B,E,h]``,
+'mixed'/'hard_attention' -> ``attention_weights [B,E]``, otherwise
+``edge_weight [B,E]``.  Duplicated edges are summed, as the reference's
+COO -> to_dense does.
+
+Gradients: x, alpha_train and beta_train are differentiable (backward = the
+same K1 kernel over the CSC for A^T, plus two reductions); gradients with
+respect to the edge weights are SURVEY §8(f) next-1 and raise.
+"""
+import torch
+from torch import nn
+
+from . import ops
+from .base_classes import ODEFunc
+from .utils import MaxNFEException
+
+
+class _LaplacianRHS(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, alpha_train, beta_train, g, w_csr, w_csc_fn, x0, alpha_sigmoid, add_source):
+        f = ops.spmm_rhs(g, w_csr, x, x0=x0, alpha=alpha_train.detach(), beta=beta_train.detach(), rhs=True,
+                         alpha_sigmoid=alpha_sigmoid, add_source=add_source)
+        ctx.save_for_backward(x, alpha_train, beta_train)
+        ctx.g, ctx.w_csr, ctx.w_csc_fn, ctx.x0 = g, w_csr, w_csc_fn, x0
+        ctx.alpha_sigmoid, ctx.add_source = alpha_sigmoid, add_source
+        return f
+
+    @staticmethod
+    def backward(ctx, gf):
+        x, alpha_train, beta_train = ctx.saved_tensors
+        gf = gf.contiguous()
+        g = ctx.g
+        gx = ga = gb = None
+        if ctx.needs_input_grad[0]:
+            # d/dx [a (A x - x)] applied to gf = a (A^T gf - gf): K1 over the CSC
+            gx = ops.spmm_rhs(g, ctx.w_csc_fn(), gf, alpha=alpha_train.detach(), rhs=True,
+                              alpha_sigmoid=ctx.alpha_sigmoid, transpose=True)
+        if ctx.needs_input_grad[1]:
+            one = torch.ones((), dtype=torch.float32, device=x.device)
+            d = ops.spmm_rhs(g, ctx.w_csr, x.detach(), alpha=one, rhs=True, alpha_sigmoid=False)  # A x - x
+            s = (gf.double() * d.double()).sum().to(alpha_train.dtype)
+            if ctx.alpha_sigmoid:
+                sg = torch.sigmoid(alpha_train.detach())
+                s = s * sg * (1 - sg)
+            ga = s.reshape(alpha_train.shape)
+        if ctx.needs_input_grad[2]:
+            if ctx.add_source:
+                gb = (gf.double() * ctx.x0.double()).sum().to(beta_train.dtype).reshape(beta_train.shape)
+            else:
+                gb = torch.zeros_like(beta_train)
+        return gx, ga, gb, None, None, None, None, None, None
+
+
+class LaplacianODEFunc(ODEFunc):
+
+    # currently requires in_features = out_features (as the reference)
+    def __init__(self, in_features, out_features, opt, device):
+        super(LaplacianODEFunc, self).__init__(opt, device)
+        self.in_features = in_features
+        self.out_features = out_features
+        # unused by the RHS; kept for state_dict compatibility (:24-27)
+        self.w = nn.Parameter(torch.eye(opt['hidden_dim']))
+        self.d = nn.Parameter(torch.zeros(opt['hidden_dim']) + 1)
+        self.alpha_sc = nn.Parameter(torch.ones(1))
+        self.beta_sc = nn.Parameter(torch.ones(1))
+        if opt.get('multi_modal', False):
+            raise NotImplementedError("gnpde: multi_modal is broken in the reference (torch.nn.softmax, "
+                                      "function_laplacian_diffusion.py:63) and out of scope")
+
+    def _weights_tensor(self):
+        blk = self.opt.get('block', 'constant')
+        if blk == 'attention':
+            w, tag = self.attention_weights, 'att_mean'
+        elif blk in ('mixed', 'hard_attention'):
+            w, tag = self.attention_weights, 'att'
+        else:
+            w, tag = self.edge_weight, 'w'
+        if w is None:
+            raise RuntimeError("LaplacianODEFunc: %s weights are not set for block=%r" % (tag, blk))
+        if torch.is_grad_enabled() and w.requires_grad:
+            raise NotImplementedError("gnpde: gradients with respect to edge/attention weights are SURVEY §8(f) "
+                                      "next-1; call under torch.no_grad() or detach the weights")
+        return w, tag
+
+    def sparse_multiply(self, x):
+        """A x (src/function_laplacian_diffusion.py:39-58) — K1 without the epilogue."""
+        g = self.graph_for(x)
+        w, tag = self._weights_tensor()
+        return ops.spmm_rhs(g, self.csr_weights(g, w, tag), x, rhs=False)
+
+    def forward(self, t, x):  # the t param is needed by the ODE solver.
+        if self.nfe > self.opt["max_nfe"]:
+            raise MaxNFEException
+        self.nfe += 1
+        g = self.graph_for(x)
+        w, tag = self._weights_tensor()
+        w_csr = self.csr_weights(g, w, tag)
+        add_source = bool(self.opt.get('add_source', False))
+        if add_source and self.x0 is None:
+            raise RuntimeError("LaplacianODEFunc: add_source needs x0 (ODEblock.set_x0)")
+        alpha_sigmoid = not self.opt.get('no_alpha_sigmoid', False)
+        x0 = self.x0 if add_source else None
+        if x0 is not None and x0.dtype != torch.float32:
+            x0 = x0.float()
+        return _LaplacianRHS.apply(x, self.alpha_train, self.beta_train, g, w_csr,
+                                   lambda: self.csr_weights(g, w, tag, transpose=True), x0, alpha_sigmoid,
+                                   add_source)

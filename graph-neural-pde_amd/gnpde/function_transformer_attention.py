@@ -1,0 +1,166 @@
+"""Drop-in ODEFuncTransformerAtt and SpGraphTransAttentionLayer
+(reference src/function_transformer_attention.py:9-270).
+
+Per RHS evaluation the reference projects Q/K/V, gathers q[src] and k[dst],
+forms an [B,h,E,E] score matmul, runs utils.softmax and densifies the
+head-mean attention into [B,N,N] for a dense matmul.  Here one RHS is:
+
+1. node scores — reference ``scaled_dot`` (the fork's global key sum,
+   :249 = ``q_src . (sum_e' k_dst(e')) / sqrt(dk)``) needs no
+   per-edge work at all: an indegree-weighted column sum of x (fp64), a tiny
+   key projection, and one fp64 GEMV per node (gnpde_ref_scores_f32).  The
+   per-edge modes (``score_mode='per_edge'`` scaled_dot = upstream GRAND, and
+   exp_kernel / cosine_sim / pearson, :246-259) project Q|K with the MFMA
+   kernel (gnpde_linear_f32);
+2. grouped softmax statistics (max, 1/sum-exp) per source (norm_idx 0) or
+   destination (norm_idx 1) node (gnpde_softmax_stats_f32);
+3. weighted aggregation with the head-mean weights recomputed on the fly and
+   the RHS epilogue fused (gnpde_attn_rhs_f32).
+
+V and Wout are dead when ``mix_features=False`` (:33-41) and are never
+computed; the parameters exist for state_dict compatibility.  Settings the
+fork cannot execute (``mix_features`` :23-31, ``square_plus`` :264,
+``multi_modal`` :171/222, beltrami+exp_kernel :164-167) raise
+NotImplementedError.  ``reweight_attention`` is a no-op in the fork (the
+layer's ``edge_weights`` is captured as None at construction, :15 / :261) and
+is a no-op here.  Inference only: training-mode forwards with grad enabled
+raise (backward kernels are SURVEY §8(f) next-1).
+"""
+import torch
+from torch import nn
+
+from . import ops
+from .base_classes import ODEFunc, _tensor_key
+from .utils import MaxNFEException
+
+
+def _check_supported(opt):
+    if opt.get('mix_features', False):
+        raise NotImplementedError("gnpde: mix_features=True is broken in the reference "
+                                  "(function_transformer_attention.py:29-31 uses a tuple as a tensor)")
+    if opt.get('square_plus', False):
+        raise NotImplementedError("gnpde: square_plus is broken in the reference (utils.squareplus called "
+                                  "without num_nodes, :264) and not implemented")
+    if opt.get('multi_modal', False):
+        raise NotImplementedError("gnpde: multi_modal is broken in the reference and out of scope")
+    if opt.get('beltrami', False) and opt.get('attention_type', 'scaled_dot') == 'exp_kernel':
+        raise NotImplementedError("gnpde: the beltrami exp_kernel branch slices nodes instead of features in the "
+                                  "reference (:166-167) and is not implemented")
+
+
+class SpGraphTransAttentionLayer(nn.Module):
+    """src/function_transformer_attention.py:65-270 (standard branch)."""
+
+    def __init__(self, in_features, out_features, opt, device, concat=True, edge_weights=None):
+        super(SpGraphTransAttentionLayer, self).__init__()
+        self.in_features = in_features
+        self.out_features = out_features
+        self.alpha = opt.get('leaky_relu_slope', 0.2)
+        self.concat = concat
+        self.device = device
+        self.opt = opt
+        self.h = int(opt['heads'])
+        self.edge_weights = edge_weights
+        self.attention_dim = opt.get('attention_dim', out_features)
+        assert self.attention_dim % self.h == 0, \
+            "Number of heads ({}) must be a factor of the dimension size ({})".format(self.h, self.attention_dim)
+        self.d_k = self.attention_dim // self.h
+        _check_supported(opt)
+        if opt.get('attention_type', 'scaled_dot') == "exp_kernel":
+            self.output_var = nn.Parameter(torch.ones(1))
+            self.lengthscale = nn.Parameter(torch.ones(1))
+        self.Q = nn.Linear(in_features, self.attention_dim)
+        self.init_weights(self.Q)
+        self.V = nn.Linear(in_features, self.attention_dim)
+        self.init_weights(self.V)
+        self.K = nn.Linear(in_features, self.attention_dim)
+        self.init_weights(self.K)
+        self.activation = nn.Sigmoid()
+        self.Wout = nn.Linear(self.d_k, in_features)
+        self.init_weights(self.Wout)
+        self._graph = None
+        self._graph_key = None
+
+    def init_weights(self, m):
+        """Constant 1e-5 init (:153-157)."""
+        if type(m) == nn.Linear:
+            nn.init.constant_(m.weight, 1e-5)
+
+    @property
+    def score_mode(self):
+        return self.opt.get('attention_score_mode', 'reference')
+
+    def _score_params(self):
+        if self.opt.get('attention_type', 'scaled_dot') == 'exp_kernel':
+            # p0 = output_var, p1 = lengthscale: read once per call (host sync of 2 scalars)
+            return float(self.output_var.detach()), float(self.lengthscale.detach())
+        return 1.0, 1.0
+
+    def graph_for(self, x, edge):
+        key = (_tensor_key(edge), int(x.shape[1]))
+        if self._graph is None or key != self._graph_key:
+            self._graph = ops.GraphCSR(edge, int(x.shape[1]), chunk=int(self.opt.get('gnpde_chunk',
+                                                                                      ops.DEFAULT_CHUNK)))
+            self._graph_key = key
+        return self._graph
+
+    def node_scores(self, g, x):
+        if self.training and torch.is_grad_enabled():
+            raise NotImplementedError("gnpde: attention backward kernels are SURVEY §8(f) next-1; use eval mode "
+                                      "or torch.no_grad()")
+        p0, p1 = self._score_params()
+        return ops.node_scores(g, x, self.Q.weight.detach(), self.Q.bias.detach(), self.K.weight.detach(),
+                               self.K.bias.detach(), self.h, self.opt.get('attention_type', 'scaled_dot'),
+                               self.score_mode, p0, p1)
+
+    def forward(self, x, edge, y=None):
+        """Returns (attention [B,E,h], (None, None)): the per-edge softmax
+        attention of :265-266 in COO order.  ``values`` (V(x), prods) is not
+        materialised (dead for mix_features=False)."""
+        g = self.graph_for(x, edge)
+        ns = self.node_scores(g, x)
+        norm_idx = int(self.opt['attention_norm_idx'])
+        m, rl = ops.softmax_stats(g, ns, norm_idx)
+        return ops.edge_attention(g, ns, m, rl, norm_idx), (None, None)
+
+    def __repr__(self):
+        return self.__class__.__name__ + ' (' + str(self.in_features) + ' -> ' + str(self.out_features) + ')'
+
+
+class ODEFuncTransformerAtt(ODEFunc):
+    """src/function_transformer_attention.py:9-62."""
+
+    def __init__(self, in_features, out_features, opt, device):
+        super(ODEFuncTransformerAtt, self).__init__(opt, device)
+        self.in_features = in_features
+        self.out_features = out_features
+        self.multihead_att_layer = SpGraphTransAttentionLayer(in_features, out_features, opt, device,
+                                                              edge_weights=self.edge_weight)
+        if device is not None:
+            self.multihead_att_layer = self.multihead_att_layer.to(device)
+        self.y = None
+
+    def multiply_attention(self, x, attention, v=None):
+        """A_mean x with attention [B,E,h] given explicitly (:20-42)."""
+        g = self.graph_for(x)
+        w = g.gather_weights(attention.detach().float())
+        return ops.spmm_rhs(g, w, x, rhs=False)
+
+    def forward(self, t, x):  # t is needed when called by the integrator
+        if self.nfe > self.opt["max_nfe"]:
+            raise MaxNFEException
+        self.nfe += 1
+        g = self.graph_for(x)
+        lay = self.multihead_att_layer
+        ns = lay.node_scores(g, x)
+        norm_idx = int(self.opt['attention_norm_idx'])
+        m, rl = ops.softmax_stats(g, ns, norm_idx)
+        add_source = bool(self.opt.get('add_source', False))
+        if add_source and self.x0 is None:
+            raise RuntimeError("ODEFuncTransformerAtt: add_source needs x0 (ODEblock.set_x0)")
+        return ops.attn_rhs(g, ns, m, rl, norm_idx, x, x0=self.x0 if add_source else None,
+                            alpha=self.alpha_train.detach(), beta=self.beta_train.detach(), rhs=True,
+                            alpha_sigmoid=not self.opt.get('no_alpha_sigmoid', False), add_source=add_source)
+
+    def __repr__(self):
+        return self.__class__.__name__ + ' (' + str(self.in_features) + ' -> ' + str(self.out_features) + ')'

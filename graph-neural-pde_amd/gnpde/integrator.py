@@ -1,0 +1,281 @@
+"""Bundled ODE integrator with torchdiffeq's calling convention.
+
+The reference integrates with ``torchdiffeq.odeint`` (src/block_constant.py:46-51,
+src/block_transformer_attention.py:40-52); torchdiffeq (README.md:29 pins 0.2.1,
+requirements.txt:20 0.1.1) is not installed in this image, so the solver loop
+is restated here from its published algorithm (torchdiffeq 0.2.x):
+
+* fixed grid (``euler``, ``midpoint``, ``rk4``): ``FixedGridODESolver`` with
+  ``_grid_constructor_from_step_size`` (niters = ceil((t1-t0)/h + 1), the last
+  grid point snapped to t1) and linear interpolation onto the requested times;
+  rk4 is ``rk4_alt_step_func`` (the 3/8 rule);
+* ``dopri5``: ``RKAdaptiveStepsizeODESolver`` with the Dormand-Prince-Shampine
+  tableau, ``_select_initial_step``, the RMS error norm, the
+  safety 0.9 / ifactor 10 / dfactor 0.2 controller and 4th-order dense output
+  (``_interp_fit`` with the DPS mid-point coefficients) at the requested times.
+
+Stage combinations ``y0 + dt * sum_j b_j k_j`` are single fused HIP passes
+(gnpde_rk_combine_f32).  The RHS calls are whatever ``func`` is (the gnpde
+ODEFuncs run entirely in HIP).  Parity of integrated values is UNPINNED: the
+reference's tests only check shapes.
+"""
+import math
+
+import torch
+
+from . import ops
+
+# Dormand-Prince-Shampine (torchdiffeq dopri5.py)
+_DP_ALPHA = [1 / 5, 3 / 10, 4 / 5, 8 / 9, 1., 1.]
+_DP_BETA = [
+    [1 / 5],
+    [3 / 40, 9 / 40],
+    [44 / 45, -56 / 15, 32 / 9],
+    [19372 / 6561, -25360 / 2187, 64448 / 6561, -212 / 729],
+    [9017 / 3168, -355 / 33, 46732 / 5247, 49 / 176, -5103 / 18656],
+    [35 / 384, 0, 500 / 1113, 125 / 192, -2187 / 6784, 11 / 84],
+]
+_DP_C_SOL = [35 / 384, 0, 500 / 1113, 125 / 192, -2187 / 6784, 11 / 84, 0]
+_DP_C_ERROR = [
+    35 / 384 - 1951 / 21600,
+    0,
+    500 / 1113 - 22642 / 50085,
+    125 / 192 - 451 / 720,
+    -2187 / 6784 - -12231 / 42400,
+    11 / 84 - 649 / 6300,
+    -1. / 60.,
+]
+_DP_C_MID = [
+    6025192743 / 30085553152 / 2, 0, 51252292925 / 65400821598 / 2, -2691868925 / 45128329728 / 2,
+    187940372067 / 1594534317056 / 2, -1776094331 / 19743644256 / 2, 11237099 / 235043384 / 2,
+]
+
+FIXED_METHODS = ('euler', 'midpoint', 'rk4')
+ADAPTIVE_METHODS = ('dopri5',)
+
+
+class _Combine(object):
+    """y0 + scale * sum_j c_j k_j on the device (fused HIP pass)."""
+
+    def __call__(self, y0, ks, coefs, scale):
+        return ops.rk_combine(y0, ks, coefs, scale).view(ks[0].shape)
+
+
+def _torch_combine(y0, ks, coefs, scale):
+    """Host-logic testing aid only (tests inject it for CPU oracle funcs)."""
+    acc = torch.zeros_like(ks[0]) if y0 is None else y0.clone()
+    for k, c in zip(ks, coefs):
+        acc = acc + (scale * c) * k
+    return acc
+
+
+def _rms_norm(t):
+    return t.abs().pow(2).mean().sqrt()
+
+
+def fixed_grid(t, step_size):
+    """torchdiffeq ``_grid_constructor_from_step_size`` (dtype of t)."""
+    start_time, end_time = t[0], t[-1]
+    niters = torch.ceil((end_time - start_time) / step_size + 1).item()
+    t_infer = torch.arange(0, niters, dtype=t.dtype, device=t.device) * step_size + start_time
+    t_infer[-1] = t[-1]
+    return t_infer
+
+
+def _linear_interp(t0, t1, y0, y1, t):
+    if t == t0:
+        return y0
+    if t == t1:
+        return y1
+    slope = (t - t0) / (t1 - t0)
+    return y0 + slope * (y1 - y0)
+
+
+def _fixed_step(method, func, t0, dt, t1, y0, combine):
+    """Returns y1 = y0 + dy (one grid step)."""
+    if method == 'euler':
+        f0 = func(t0, y0)
+        return combine(y0, [f0], [1.0], dt)
+    if method == 'midpoint':
+        f0 = func(t0, y0)
+        y_mid = combine(y0, [f0], [0.5], dt)
+        f_mid = func(t0 + 0.5 * dt, y_mid)
+        return combine(y0, [f_mid], [1.0], dt)
+    if method == 'rk4':  # rk4_alt_step_func (3/8 rule)
+        k1 = func(t0, y0)
+        k2 = func(t0 + dt / 3.0, combine(y0, [k1], [1.0 / 3.0], dt))
+        k3 = func(t0 + dt * 2.0 / 3.0, combine(y0, [k1, k2], [-1.0 / 3.0, 1.0], dt))
+        k4 = func(t1, combine(y0, [k1, k2, k3], [1.0, -1.0, 1.0], dt))
+        return combine(y0, [k1, k2, k3, k4], [0.125, 0.375, 0.375, 0.125], dt)
+    raise ValueError(method)
+
+
+def odeint_fixed(func, y0, t, method, step_size=None, combine=None):
+    combine = combine or _Combine()
+    grid = t if step_size is None else fixed_grid(t, step_size)
+    if not (bool(grid[0] == t[0]) and bool(grid[-1] == t[-1])):
+        raise AssertionError("time grid does not cover t")
+    grid_h = [float(v) for v in grid.tolist()]
+    t_h = [float(v) for v in t.tolist()]
+    solution = [y0]
+    j = 1
+    yc = y0
+    for ta, tb in zip(grid_h[:-1], grid_h[1:]):
+        dt = tb - ta
+        y1 = _fixed_step(method, func, ta, dt, tb, yc, combine)
+        while j < len(t_h) and tb >= t_h[j]:
+            solution.append(_linear_interp(ta, tb, yc, y1, t_h[j]))
+            j += 1
+        yc = y1
+    return torch.stack(solution, 0)
+
+
+class _Dopri5(object):
+    """torchdiffeq RKAdaptiveStepsizeODESolver restated for dopri5."""
+    order = 5
+
+    def __init__(self, func, y0, rtol, atol, combine, first_step=None, safety=0.9, ifactor=10.0, dfactor=0.2,
+                 max_num_steps=2 ** 31 - 1, norm=_rms_norm):
+        dtype = torch.promote_types(torch.float64, y0.dtype)
+        dev = y0.device
+        self.func, self.y0, self.combine, self.norm = func, y0, combine, norm
+        self.dtype = dtype
+        self.rtol = torch.as_tensor(rtol, dtype=dtype, device=dev)
+        self.atol = torch.as_tensor(atol, dtype=dtype, device=dev)
+        self.safety = torch.as_tensor(safety, dtype=dtype, device=dev)
+        self.ifactor = torch.as_tensor(ifactor, dtype=dtype, device=dev)
+        self.dfactor = torch.as_tensor(dfactor, dtype=dtype, device=dev)
+        self.first_step = None if first_step is None else torch.as_tensor(first_step, dtype=dtype, device=dev)
+        self.max_num_steps = max_num_steps
+        self.n_steps = 0
+
+    def _select_initial_step(self, t0, f0):
+        y0, rtol, atol, norm, func = self.y0, self.rtol, self.atol, self.norm, self.func
+        dtype, dev = y0.dtype, y0.device
+        t_dtype = t0.dtype
+        scale = atol + torch.abs(y0) * rtol
+        d0 = norm(y0 / scale).abs()
+        d1 = norm(f0 / scale).abs()
+        if d0 < 1e-5 or d1 < 1e-5:
+            h0 = torch.tensor(1e-6, dtype=dtype, device=dev)
+        else:
+            h0 = 0.01 * d0 / d1
+        h0 = h0.abs()
+        y1 = y0 + h0 * f0
+        f1 = func(t0.to(dtype) + h0, y1)
+        d2 = torch.abs(norm((f1 - f0) / scale) / h0)
+        if d1 <= 1e-15 and d2 <= 1e-15:
+            h1 = torch.max(torch.tensor(1e-6, dtype=dtype, device=dev), h0 * 1e-3)
+        else:
+            h1 = (0.01 / max(d1, d2)) ** (1. / float(self.order))
+        h1 = h1.abs()
+        return torch.min(100 * h0, h1).to(t_dtype)
+
+    def _optimal_step_size(self, last_step, error_ratio):
+        if error_ratio == 0:
+            return last_step * self.ifactor
+        dfactor = self.dfactor
+        if error_ratio < 1:
+            dfactor = torch.ones((), dtype=last_step.dtype, device=last_step.device)
+        error_ratio = error_ratio.type_as(last_step)
+        exponent = torch.tensor(self.order, dtype=last_step.dtype, device=last_step.device).reciprocal()
+        factor = torch.min(self.ifactor, torch.max(self.safety / error_ratio ** exponent, dfactor))
+        return last_step * factor
+
+    def _step(self, y0, f0, t0, dt):
+        dtf = float(dt)
+        t0f = float(t0)
+        k = [f0]
+        yi = y0
+        for i, (a_i, beta_i) in enumerate(zip(_DP_ALPHA, _DP_BETA)):
+            ti = t0f + dtf if a_i == 1. else t0f + a_i * dtf
+            yi = self.combine(y0, k, beta_i, dtf)
+            k.append(self.func(ti, yi))
+        # c_sol == beta[-1] and c_sol[-1] == 0 for dopri5: y1 is the last stage input
+        y1 = yi
+        f1 = k[-1]
+        y1_error = self.combine(None, k, _DP_C_ERROR, dtf)
+        return y1, f1, y1_error, k
+
+    def _interp(self, y0, y1, k, dt, t0, t1, t):
+        dtf = float(dt)
+        y_mid = self.combine(y0, k, _DP_C_MID, dtf)
+        f0, f1 = k[0], k[-1]
+        a = 2 * dtf * (f1 - f0) - 8 * (y1 + y0) + 16 * y_mid
+        b = dtf * (5 * f0 - 3 * f1) + 18 * y0 + 14 * y1 - 32 * y_mid
+        c = dtf * (f1 - 4 * f0) - 11 * y0 - 5 * y1 + 16 * y_mid
+        d = dtf * f0
+        e = y0
+        x = float((t - t0) / (t1 - t0))
+        total = e + x * d
+        xp = x
+        for coeff in (c, b, a):
+            xp = xp * x
+            total = total + xp * coeff
+        return total
+
+    def integrate(self, t):
+        t = t.to(self.dtype)
+        solution = [self.y0]
+        t0 = t[0]
+        f0 = self.func(t0, self.y0)
+        dt = self._select_initial_step(t0, f0) if self.first_step is None else self.first_step
+        y, f = self.y0, f0
+        t_prev, t_cur = t0, t0
+        last = None  # (y_prev, y_cur, k, dt) of the last accepted step
+        for i in range(1, len(t)):
+            next_t = t[i]
+            while next_t > t_cur:
+                if not bool(t_cur + dt > t_cur):
+                    raise AssertionError('underflow in dt {}'.format(float(dt)))
+                if self.n_steps >= self.max_num_steps:
+                    raise AssertionError('max_num_steps exceeded ({}>={})'.format(self.n_steps, self.max_num_steps))
+                y1, f1, y1_err, k = self._step(y, f, t_cur, dt)
+                error_tol = self.atol + self.rtol * torch.max(y.abs(), y1.abs())
+                error_ratio = self.norm(y1_err / error_tol).abs()
+                if error_ratio <= 1:
+                    last = (y, y1, k, dt)
+                    t_prev, t_cur = t_cur, t_cur + dt
+                    y, f = y1, f1
+                dt = self._optimal_step_size(dt, error_ratio)
+                self.n_steps += 1
+            if last is None or next_t == t_cur:
+                solution.append(y)
+            else:
+                y_prev, y_cur, k, dts = last
+                solution.append(self._interp(y_prev, y_cur, k, dts, t_prev, t_cur, next_t))
+        return torch.stack(solution, 0)
+
+
+def odeint(func, y0, t, rtol=1e-7, atol=1e-9, method=None, options=None, combine=None):
+    """torchdiffeq.odeint(func, y0, t, rtol, atol, method, options) -> [len(t), *y0.shape]."""
+    method = method or 'dopri5'
+    options = dict(options or {})
+    if combine is None:
+        if not y0.is_cuda:
+            raise RuntimeError("gnpde.odeint: y0 must be a ROCm device tensor (stage combinations run in HIP)")
+        combine = _Combine()
+    if not isinstance(t, torch.Tensor):
+        t = torch.as_tensor(t)
+    if t.dim() != 1 or len(t) < 2:
+        raise ValueError("t must be a 1-D tensor with at least two time points")
+    if method in FIXED_METHODS:
+        return odeint_fixed(func, y0, t, method, options.get('step_size'), combine)
+    if method in ADAPTIVE_METHODS:
+        solver = _Dopri5(func, y0, rtol, atol, combine, first_step=options.get('first_step'),
+                         max_num_steps=options.get('max_num_steps', 2 ** 31 - 1))
+        out = solver.integrate(t)
+        odeint.last_n_steps = solver.n_steps
+        return out
+    raise NotImplementedError("gnpde.odeint: method %r not supported (supported: %s)" %
+                              (method, ', '.join(FIXED_METHODS + ADAPTIVE_METHODS)))
+
+
+odeint.last_n_steps = 0
+
+
+def odeint_adjoint(*args, **kwargs):
+    raise NotImplementedError("gnpde: adjoint integration needs the backward kernels (SURVEY §8(f) next-1)")
+
+
+__all__ = ['odeint', 'odeint_adjoint', 'fixed_grid', 'FIXED_METHODS', 'ADAPTIVE_METHODS', 'math']

@@ -1,0 +1,348 @@
+"""Tensor-level wrappers over the C ABI (include/gnpde.h).
+
+Everything here runs on the GPU through libgnpde.so; there is no CPU path.
+Tensors must live on a ROCm device; every launch goes onto torch's current
+stream, so the calls compose with torch ops and are hipGraph-capturable (the
+graph build / plan functions are once-per-graph and synchronous).
+
+Layout: node features [B,N,C] fp32 row-major, viewed as
+[R=B*N, C]; graphs are block-diagonal over the batch as an int32 CSR
+(rowptr[R+1], col[nnz] global node ids, perm[nnz] CSR pos -> COO edge id).
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+
+DEFAULT_CHUNK = 256  # hub-splitting threshold (edges per wavefront work item)
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def _stream(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def _require_gpu(t, name, dtype=None):
+    if not isinstance(t, torch.Tensor):
+        raise TypeError("%s must be a torch.Tensor" % name)
+    if not t.is_cuda:
+        raise RuntimeError("gnpde: %s must be a ROCm device tensor (the native path has no CPU fallback); got %s"
+                           % (name, t.device))
+    if dtype is not None and t.dtype != dtype:
+        raise TypeError("gnpde: %s must be %s, got %s" % (name, dtype, t.dtype))
+
+
+def _rows(x, name):
+    """[B,N,C] or [R,C] fp32 -> contiguous [R,C] view."""
+    _require_gpu(x, name, torch.float32)
+    x = x.contiguous()
+    return x.reshape(-1, x.shape[-1])
+
+
+# --------------------------------------------------------------------------- graph
+class Plan(object):
+    """Wavefront work items over a grouped CSR (gnpde_plan_build)."""
+
+    def __init__(self, items, heavy, n_items, n_heavy, n_slots, chunk):
+        self.items, self.heavy = items, heavy
+        self.n_items, self.n_heavy, self.n_slots = n_items, n_heavy, n_slots
+        self.chunk = chunk
+
+
+class GroupedCSR(object):
+    """Edges grouped by one endpoint: key_row 0 -> aggregation CSR (by source),
+    key_row 1 -> CSC (by destination)."""
+
+    def __init__(self, rowptr, col, perm, R, nnz, key_row, plan):
+        self.rowptr, self.col, self.perm = rowptr, col, perm
+        self.R, self.nnz, self.key_row, self.plan = R, nnz, key_row, plan
+
+
+def validate_edge_index(edge_index, num_nodes):
+    _require_gpu(edge_index, "edge_index", torch.int64)
+    if edge_index.dim() != 3 or edge_index.shape[1] != 2:
+        raise ValueError("edge_index must be [B,2,E], got %s" % (tuple(edge_index.shape),))
+    if edge_index.numel():
+        lo, hi = int(edge_index.min()), int(edge_index.max())  # once per graph
+        if lo < 0 or hi >= num_nodes:
+            raise IndexError("edge_index values must be in [0, %d), got [%d, %d]" % (num_nodes, lo, hi))
+
+
+def build_plan(rowptr, R, nnz, chunk=DEFAULT_CHUNK):
+    dev = rowptr.device
+    cap_items = R + 2 * (nnz // chunk) + 2
+    cap_heavy = nnz // chunk + 2
+    items = torch.empty(cap_items * 4, dtype=torch.int32, device=dev)
+    heavy = torch.empty(cap_heavy * 4, dtype=torch.int32, device=dev)
+    ws_bytes = _lib.fn("gnpde_plan_workspace_bytes")(R)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    n_it, n_hv, n_sl = ctypes.c_int64(0), ctypes.c_int64(0), ctypes.c_int64(0)
+    _lib.call("gnpde_plan_build", _ptr(rowptr), R, chunk, _ptr(items), cap_items, _ptr(heavy), cap_heavy,
+              ctypes.byref(n_it), ctypes.byref(n_hv), ctypes.byref(n_sl), _ptr(ws), ws_bytes, _stream(dev))
+    return Plan(items, heavy, n_it.value, n_hv.value, n_sl.value, chunk)
+
+
+def build_grouped(edge_index, num_nodes, key_row, chunk=DEFAULT_CHUNK):
+    """COO [B,2,E] -> block-diagonal CSR grouped by edge_index[:, key_row] (+ plan)."""
+    B, _, E = edge_index.shape
+    N = int(num_nodes)
+    R, nnz = B * N, B * E
+    dev = edge_index.device
+    ei = edge_index.contiguous()
+    rowptr = torch.empty(R + 1, dtype=torch.int32, device=dev)
+    col = torch.empty(max(nnz, 1), dtype=torch.int32, device=dev)
+    perm = torch.empty(max(nnz, 1), dtype=torch.int32, device=dev)
+    ws_bytes = _lib.fn("gnpde_csr_workspace_bytes")(B, E, N)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    _lib.call("gnpde_csr_build", _ptr(ei), B, E, N, key_row, _ptr(rowptr), _ptr(col), _ptr(perm), _ptr(ws), ws_bytes,
+              _stream(dev))
+    plan = build_plan(rowptr, R, nnz, chunk)
+    return GroupedCSR(rowptr, col, perm, R, nnz, key_row, plan)
+
+
+class GraphCSR(object):
+    """All per-graph device structures the RHS needs, built once and reused by
+    every RHS evaluation (the reference rebuilds a dense [B,N,N] per call)."""
+
+    def __init__(self, edge_index, num_nodes, chunk=DEFAULT_CHUNK, validate=True):
+        if validate:
+            validate_edge_index(edge_index, num_nodes)
+        self.edge_index = edge_index
+        self.B, _, self.E = edge_index.shape
+        self.N = int(num_nodes)
+        self.R = self.B * self.N
+        self.nnz = self.B * self.E
+        self.chunk = chunk
+        self.csr = build_grouped(edge_index, self.N, 0, chunk)
+        self._csc = None
+        self._indeg = None
+
+    @property
+    def csc(self):
+        if self._csc is None:
+            self._csc = build_grouped(self.edge_index, self.N, 1, self.chunk)
+        return self._csc
+
+    @property
+    def indeg(self):
+        if self._indeg is None:
+            deg = torch.empty(self.R, dtype=torch.int32, device=self.edge_index.device)
+            _lib.call("gnpde_indegree_i32", _ptr(self.csr.col), self.nnz, self.R, _ptr(deg),
+                      _stream(deg.device))
+            self._indeg = deg
+        return self._indeg
+
+    def gather_weights(self, w, transpose=False):
+        """COO-order weights [B,E] or attention [B,E,h] -> CSR-order [nnz] (head mean);
+        transpose=True gives CSC order."""
+        _require_gpu(w, "edge weights", torch.float32)
+        w = w.contiguous()
+        if w.dim() == 2:
+            H = 1
+        elif w.dim() == 3:
+            H = w.shape[2]
+        else:
+            raise ValueError("weights must be [B,E] or [B,E,h]")
+        if w.shape[0] != self.B or w.shape[1] != self.E:
+            raise ValueError("weights shape %s does not match edge_index [%d,2,%d]" % (tuple(w.shape), self.B,
+                                                                                        self.E))
+        out = torch.empty(max(self.nnz, 1), dtype=torch.float32, device=w.device)
+        perm = self.csc.perm if transpose else self.csr.perm
+        _lib.call("gnpde_gather_weights_f32", _ptr(w), self.nnz, H, _ptr(perm), _ptr(out),
+                  _stream(w.device))
+        return out
+
+
+# --------------------------------------------------------------------------- epilogue helpers
+def _flags(rhs, alpha_sigmoid, add_source):
+    f = 0
+    if rhs:
+        f |= _lib.EPI_RHS
+        if alpha_sigmoid:
+            f |= _lib.ALPHA_SIGMOID
+        if add_source:
+            f |= _lib.ADD_SOURCE
+    return f
+
+
+def _scalar(t, name, dev):
+    if t is None:
+        return None
+    if not isinstance(t, torch.Tensor):
+        t = torch.tensor(float(t), dtype=torch.float32, device=dev)
+    _require_gpu(t, name)
+    if t.dtype != torch.float32:
+        t = t.float()
+    return t.reshape(1).contiguous()
+
+
+def spmm_rhs(g, w_csr, x, x0=None, alpha=None, beta=None, rhs=True, alpha_sigmoid=True, add_source=False,
+             out=None, transpose=False):
+    """K1: f = a*(A x - x) [+ b*x0] (or A x with rhs=False).  x [B,N,C] fp32.
+
+    transpose=True aggregates over the CSC instead (A^T x; ``w_csr`` must then
+    be in CSC order) — the backward of the RHS with respect to x."""
+    shape = x.shape
+    xr = _rows(x, "x")
+    C = xr.shape[1]
+    if xr.shape[0] != g.R:
+        raise ValueError("x has %d rows, graph has %d" % (xr.shape[0], g.R))
+    dev = xr.device
+    a = _scalar(alpha, "alpha", dev) if rhs else None
+    if rhs and a is None:
+        raise ValueError("spmm_rhs: alpha required")
+    b = _scalar(beta, "beta", dev) if add_source else None
+    x0r = _rows(x0, "x0") if add_source else None
+    if out is None:
+        out = torch.empty_like(xr)
+    grouped = g.csc if transpose else g.csr
+    plan = grouped.plan
+    partials = torch.empty(plan.n_slots * C, dtype=torch.float32, device=dev) if plan.n_slots else None
+    _lib.call("gnpde_spmm_rhs_f32", _ptr(plan.items), plan.n_items, _ptr(plan.heavy), plan.n_heavy, _ptr(grouped.col),
+              _ptr(w_csr), C, _ptr(xr), C, _ptr(x0r), C, _ptr(a), _ptr(b), _flags(rhs, alpha_sigmoid, add_source),
+              _ptr(out), C, _ptr(partials), _stream(dev))
+    return out.view(shape)
+
+
+# --------------------------------------------------------------------------- attention
+SCORE_MODES = {
+    ('scaled_dot', 'reference'): _lib.SCORE_REFERENCE,
+    ('scaled_dot', 'per_edge'): _lib.SCORE_DOT,
+    ('exp_kernel', 'reference'): _lib.SCORE_EXP_KERNEL,
+    ('exp_kernel', 'per_edge'): _lib.SCORE_EXP_KERNEL,
+    ('cosine_sim', 'reference'): _lib.SCORE_COSINE,
+    ('cosine_sim', 'per_edge'): _lib.SCORE_COSINE,
+    ('pearson', 'reference'): _lib.SCORE_PEARSON,
+    ('pearson', 'per_edge'): _lib.SCORE_PEARSON,
+}
+
+
+def linear(x, W, bias=None, split=None):
+    """MFMA projection: x [R,K] @ W[Nout,K]^T + bias -> (out[:, :split], out[:, split:])."""
+    xr = _rows(x, "x")
+    _require_gpu(W, "W", torch.float32)
+    W = W.contiguous()
+    Nout, K = W.shape
+    if xr.shape[1] != K:
+        raise ValueError("linear: x has %d columns, W expects %d" % (xr.shape[1], K))
+    if bias is not None:
+        _require_gpu(bias, "bias", torch.float32)
+        bias = bias.contiguous()
+    split = Nout if split is None else int(split)
+    R = xr.shape[0]
+    out_a = torch.empty(R, split, dtype=torch.float32, device=xr.device)
+    out_b = torch.empty(R, Nout - split, dtype=torch.float32, device=xr.device) if split < Nout else None
+    _lib.call("gnpde_linear_f32", _ptr(xr), R, K, K, _ptr(W), _ptr(bias), Nout, split, _ptr(out_a), max(split, 1),
+              _ptr(out_b), max(Nout - split, 1), _stream(xr.device))
+    return out_a, out_b
+
+
+class NodeScores(object):
+    """Per-RHS node-level operands of the attention scores."""
+
+    def __init__(self, mode, heads, dk, cs=None, q=None, k=None, p0=1.0, p1=1.0):
+        self.mode, self.heads, self.dk = mode, heads, dk
+        self.cs, self.q, self.k = cs, q, k
+        self.p0, self.p1 = float(p0), float(p1)
+        self.ldqk = q.shape[1] if q is not None else 1
+
+
+def node_scores(g, x, Wq, bq, Wk, bk, heads, attention_type='scaled_dot', score_mode='reference',
+                output_var=1.0, lengthscale=1.0):
+    """Q/K-side work of SpGraphTransAttentionLayer.forward (function_transformer_attention.py:224-259)."""
+    mode = SCORE_MODES[(attention_type, score_mode)]
+    xr = _rows(x, "x")
+    att = Wq.shape[0]
+    if att % heads:
+        raise ValueError("attention_dim %d not divisible by heads %d" % (att, heads))
+    dk = att // heads
+    if mode == _lib.SCORE_REFERENCE:
+        B, N, C = g.B, g.N, xr.shape[1]
+        cs = torch.empty(g.R, heads, dtype=torch.float64, device=xr.device)
+        ws_bytes = _lib.fn("gnpde_keysum_workspace_bytes")(B, N, C, att)
+        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=xr.device)
+        for name, t in (("Wq", Wq), ("bq", bq), ("Wk", Wk), ("bk", bk)):
+            _require_gpu(t, name, torch.float32)
+        _lib.call("gnpde_ref_scores_f32", _ptr(xr), B, N, C, C, _ptr(g.indeg), _ptr(Wq.contiguous()),
+                  _ptr(bq.contiguous()), _ptr(Wk.contiguous()), _ptr(bk.contiguous()), att, heads, _ptr(cs), _ptr(ws),
+                  ws_bytes, _stream(xr.device))
+        return NodeScores(mode, heads, dk, cs=cs)
+    W = torch.cat([Wq, Wk], 0)
+    b = torch.cat([bq, bk], 0) if bq is not None else None
+    q, k = linear(xr, W, b, split=att)
+    return NodeScores(mode, heads, dk, q=q, k=k, p0=output_var, p1=lengthscale)
+
+
+def softmax_stats(g, ns, norm_idx):
+    """m, rl [R,h]: per-group max and reciprocal sum-exp (utils.softmax, src/utils.py:116-127)."""
+    grouped = g.csr if norm_idx == 0 else g.csc
+    plan = grouped.plan
+    dev = grouped.col.device
+    H = ns.heads
+    m = torch.empty(g.R, H, dtype=torch.float64, device=dev)
+    rl = torch.empty(g.R, H, dtype=torch.float32, device=dev)
+    partials = torch.empty(plan.n_slots * 2 * H, dtype=torch.float64, device=dev) if plan.n_slots else None
+    _lib.call("gnpde_softmax_stats_f32", _ptr(plan.items), plan.n_items, _ptr(plan.heavy), plan.n_heavy,
+              _ptr(grouped.col), int(norm_idx == 1), ns.mode, H, ns.dk, _ptr(ns.cs), _ptr(ns.q), _ptr(ns.k), ns.ldqk,
+              ns.p0, ns.p1, _ptr(m), _ptr(rl), _ptr(partials), _stream(dev))
+    return m, rl
+
+
+def attn_rhs(g, ns, m, rl, norm_idx, x, x0=None, alpha=None, beta=None, rhs=True, alpha_sigmoid=True,
+             add_source=False, out=None):
+    """K3 aggregation: f = a*(A_att x - x) [+ b x0], A_att = head-mean softmax weights."""
+    shape = x.shape
+    xr = _rows(x, "x")
+    C = xr.shape[1]
+    dev = xr.device
+    a = _scalar(alpha, "alpha", dev) if rhs else None
+    b = _scalar(beta, "beta", dev) if add_source else None
+    x0r = _rows(x0, "x0") if add_source else None
+    if out is None:
+        out = torch.empty_like(xr)
+    plan = g.csr.plan
+    partials = torch.empty(plan.n_slots * C, dtype=torch.float32, device=dev) if plan.n_slots else None
+    _lib.call("gnpde_attn_rhs_f32", _ptr(plan.items), plan.n_items, _ptr(plan.heavy), plan.n_heavy, _ptr(g.csr.col),
+              int(norm_idx), ns.mode, ns.heads, ns.dk, _ptr(ns.cs), _ptr(ns.q), _ptr(ns.k), ns.ldqk, ns.p0, ns.p1,
+              _ptr(m), _ptr(rl), C, _ptr(xr), C, _ptr(x0r), C, _ptr(a), _ptr(b), _flags(rhs, alpha_sigmoid, add_source),
+              _ptr(out), C, _ptr(partials), _stream(dev))
+    return out.view(shape)
+
+
+def edge_attention(g, ns, m, rl, norm_idx):
+    """attention [B,E,h] in COO order (SpGraphTransAttentionLayer.forward's first output)."""
+    dev = g.csr.col.device
+    att = torch.empty(g.B, g.E, ns.heads, dtype=torch.float32, device=dev)
+    plan = g.csr.plan
+    _lib.call("gnpde_edge_attention_f32", _ptr(plan.items), plan.n_items, _ptr(g.csr.col), _ptr(g.csr.perm),
+              int(norm_idx), ns.mode, ns.heads, ns.dk, _ptr(ns.cs), _ptr(ns.q), _ptr(ns.k), ns.ldqk, ns.p0, ns.p1,
+              _ptr(m), _ptr(rl), _ptr(att), _stream(dev))
+    return att
+
+
+# --------------------------------------------------------------------------- solver glue
+def rk_combine(y0, ks, coefs, scale, out=None):
+    """out = y0 + scale * sum_j coefs[j] * ks[j]  (one fused pass; y0=None means 0)."""
+    ref = y0 if y0 is not None else ks[0]
+    _require_gpu(ref, "y0", torch.float32)
+    if y0 is not None:
+        y0 = y0.contiguous()
+    if out is None:
+        out = torch.empty_like(ref, memory_format=torch.contiguous_format)
+    nk = len(ks)
+    kp = (ctypes.c_void_p * max(nk, 1))()
+    cf = (ctypes.c_double * max(nk, 1))()
+    keep = []
+    for j, (k, c) in enumerate(zip(ks, coefs)):
+        _require_gpu(k, "k%d" % j, torch.float32)
+        k = k.contiguous()
+        keep.append(k)
+        kp[j] = k.data_ptr()
+        cf[j] = float(c)
+    _lib.call("gnpde_rk_combine_f32", ref.numel(), _ptr(y0), nk, kp, cf, float(scale), _ptr(out),
+              _stream(ref.device))
+    return out

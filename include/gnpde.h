@@ -1,0 +1,179 @@
+/*
+ * gnpde.h — C ABI of the MI355X-native GRAND/BLEND ODE right-hand side.
+ *
+ * One shared library, libgnpde.so (graph-neural-pde_amd/gnpde/), built with
+ * `hipcc --offload-arch=gfx950`.  Plain pointers and sizes only; no torch
+ * types.  Every device pointer is owned by the caller (the Python host passes
+ * torch tensors' data_ptr()); the library never allocates device memory and
+ * keeps no state besides its kernels.  Every call enqueues on the caller's
+ * `stream` (a hipStream_t passed as void*; NULL = legacy default stream) and
+ * never synchronises, except gnpde_plan_build, which is documented as a
+ * once-per-graph synchronous call.  All calls are graph-capturable except
+ * gnpde_plan_build.
+ *
+ * Return codes: 0 ok, GNPDE_EINVAL (-1) invalid argument, GNPDE_EHIP (-2) HIP
+ * runtime error, GNPDE_EUNSUPPORTED (-3) unsupported shape/dtype.  The message
+ * of the last failure on the calling thread is returned by gnpde_last_error().
+ *
+ * Reference interfaces replaced (alimt1992/graph-neural-pde @ 2025-01-17):
+ *   - the per-RHS COO->dense->matmul of LaplacianODEFunc.sparse_multiply,
+ *     src/function_laplacian_diffusion.py:39-58, and of
+ *     ODEFuncTransformerAtt.multiply_attention, src/function_transformer_attention.py:33-41;
+ *   - the RHS epilogue f = sigma(alpha)(ax - x) [+ beta x0],
+ *     src/function_laplacian_diffusion.py:69-77, src/function_transformer_attention.py:52-59;
+ *   - SpGraphTransAttentionLayer.forward's Q/K projections, gathers, scaled_dot
+ *     score and edge softmax, src/function_transformer_attention.py:224-266 and
+ *     utils.softmax, src/utils.py:116-127;
+ *   - the torchdiffeq stage combinations y0 + dt*sum(b_j k_j) the solver does
+ *     between RHS calls (src/block_constant.py:46-51 calls odeint).
+ *
+ * Layout: graphs are block-diagonal over the batch: global node id
+ * r = b*N + n (b < B, n < N), R = B*N rows.  Node features are row-major
+ * [R, C] with leading dimension ld (elements).  A "CSR" here is rowptr[R+1],
+ * col[nnz] (global node ids), perm[nnz] (CSR position -> COO edge id b*E+e).
+ * Grouping by source (edge_index[:,0]) gives the aggregation CSR; grouping by
+ * destination (edge_index[:,1]) gives the CSC used for destination-grouped
+ * softmax (attention_norm_idx = 1).
+ */
+#ifndef GNPDE_H_
+#define GNPDE_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GNPDE_ABI_VERSION 1
+
+#define GNPDE_OK 0
+#define GNPDE_EINVAL (-1)
+#define GNPDE_EHIP (-2)
+#define GNPDE_EUNSUPPORTED (-3)
+
+/* flags for the RHS epilogue */
+#define GNPDE_EPI_PLAIN 0          /* f = ax                                   */
+#define GNPDE_EPI_RHS 1            /* f = a*(ax - x) [+ b*x0]                  */
+#define GNPDE_ALPHA_SIGMOID 2      /* a = sigmoid(*alpha) instead of *alpha    */
+#define GNPDE_ADD_SOURCE 4         /* add b*x0 (b = *beta)                      */
+
+/* score modes of the attention RHS (function_transformer_attention.py:246-259) */
+#define GNPDE_SCORE_REFERENCE 0    /* fork scaled_dot: q_src . (sum_e' k_dst(e')) / sqrt(dk)      */
+#define GNPDE_SCORE_DOT 1          /* per-edge scaled_dot: q_src . k_dst / sqrt(dk) (upstream)    */
+#define GNPDE_SCORE_EXP_KERNEL 2   /* ov^2 exp(-|q_src - k_dst|^2 / (2 ls^2))                     */
+#define GNPDE_SCORE_COSINE 3       /* cosine similarity, eps 1e-5                                 */
+#define GNPDE_SCORE_PEARSON 4      /* centred cosine similarity                                   */
+
+int gnpde_abi_version(void);
+const char* gnpde_last_error(void);
+
+/* ---------------------------------------------------------------- graph build
+ * COO edge_index [B,2,E] (int64, values in [0,N) — caller-validated) -> CSR
+ * grouped by row `key_row` (0 = source, 1 = destination).  Stable: inside a
+ * row, edges keep their COO order.  Replaces the per-call index building of
+ * function_laplacian_diffusion.py:41-44 (done once per graph here).         */
+size_t gnpde_csr_workspace_bytes(int64_t B, int64_t E, int64_t N);
+int gnpde_csr_build(const int64_t* edge_index, int64_t B, int64_t E, int64_t N, int key_row,
+                    int32_t* rowptr, int32_t* col, int32_t* perm,
+                    void* workspace, size_t workspace_bytes, void* stream);
+
+/* w_out[p] = mean_{h<H} w_in[perm[p]*H + h]  (H = 1: plain permutation).
+ * Head-mean of attention weights, function_laplacian_diffusion.py:45-49.    */
+int gnpde_gather_weights_f32(const float* w_in, int64_t nnz, int H, const int32_t* perm, float* w_out,
+                             void* stream);
+
+/* deg[r] = #{p : idx[p] == r}, r < R (memset + integer atomics: deterministic).
+ * With idx = the aggregation CSR's col this is the in-degree used by the
+ * reference-mode key sum.                                                   */
+int gnpde_indegree_i32(const int32_t* idx, int64_t nnz, int64_t R, int32_t* deg, void* stream);
+
+/* ---------------------------------------------------------------- work plan
+ * Splits rows with more than `chunk` edges into balanced chunks so that one
+ * power-law hub does not serialise a wavefront.  items[n_items] is int4
+ * {row, edge_begin, edge_end, slot} (slot = -1: the item owns its row;
+ * slot >= 0: partial-sum slot); heavy[n_heavy] is int4 {row, first_slot,
+ * n_chunks, 0}.  Capacity: items >= R + 2*nnz/chunk + 1, heavy >= nnz/chunk + 1.
+ * SYNCHRONOUS (copies the two counts to the host); call once per graph.     */
+int gnpde_plan_build(const int32_t* rowptr, int64_t R, int32_t chunk,
+                     int32_t* items, int64_t items_capacity, int32_t* heavy, int64_t heavy_capacity,
+                     int64_t* n_items, int64_t* n_heavy, int64_t* n_slots,
+                     void* workspace, size_t workspace_bytes, void* stream);
+size_t gnpde_plan_workspace_bytes(int64_t R);
+
+/* ---------------------------------------------------------------- K1: SpMM RHS
+ * ax[r,:] = sum_{p in row r} w[p] * x[col[p],:]
+ * f[r,:]  = ax                                  (flags & 1 == 0)
+ *         = a*(ax - x[r,:]) [+ b*x0[r,:]]        (GNPDE_EPI_RHS)
+ * a = *alpha or sigmoid(*alpha), b = *beta: device scalars (no host sync).
+ * partials: n_slots*C floats of scratch (NULL if n_slots == 0).
+ * Replaces function_laplacian_diffusion.py:39-77 per RHS evaluation.        */
+int gnpde_spmm_rhs_f32(const int32_t* items, int64_t n_items, const int32_t* heavy, int64_t n_heavy,
+                       const int32_t* col, const float* w, int64_t C,
+                       const float* x, int64_t ldx, const float* x0, int64_t ldx0,
+                       const float* alpha, const float* beta, int flags,
+                       float* f, int64_t ldf, float* partials, void* stream);
+
+/* ---------------------------------------------------------------- attention
+ * Node-level projection (MFMA, v_mfma_f32_32x32x2_f32):
+ *   out[r, j] = sum_k x[r,k] * W[j,k] + bias[j], j < Nout; columns [0, split)
+ *   go to out_a (ld lda), [split, Nout) to out_b (ld ldb).
+ * Replaces the nn.Linear Q/K of function_transformer_attention.py:224-225.  */
+int gnpde_linear_f32(const float* x, int64_t R, int64_t K, int64_t ldx, const float* W, const float* bias,
+                     int64_t Nout, int64_t split, float* out_a, int64_t lda, float* out_b, int64_t ldb,
+                     void* stream);
+
+/* Reference-mode node scores (fork scaled_dot, function_transformer_attention.py:249):
+ *   S_b = Wk * (sum_n indeg(n) x_n) + (sum_n indeg(n)) bk    (fp64)
+ *   cs[r,h] = (q_r,h . S_b,h) / sqrt(dk),  q = Wq x + bq      (fp64 out)
+ * indeg: in-degree per global node (int32, R); ws: gnpde_keysum_workspace_bytes.  */
+size_t gnpde_keysum_workspace_bytes(int64_t B, int64_t N, int64_t C, int64_t att);
+int gnpde_ref_scores_f32(const float* x, int64_t B, int64_t N, int64_t C, int64_t ldx, const int32_t* indeg,
+                         const float* Wq, const float* bq, const float* Wk, const float* bk,
+                         int64_t att, int64_t heads, double* cs, void* workspace, size_t workspace_bytes,
+                         void* stream);
+
+/* Destination- or source-grouped softmax statistics over a grouped CSR
+ * (items from gnpde_plan_build over the CSC for norm_idx=1, the CSR for
+ * norm_idx=0; gidx = the OTHER endpoint of each edge):
+ * m[g,h] = max_e s_e,h (fp64), rl[g,h] = 1/(sum_e exp(s_e,h - m) + 1e-16).
+ * partials: 2*heads doubles per plan slot.
+ * Edge scores by `mode` from cs (REFERENCE) or q/k (per-edge modes).
+ * Restates utils.softmax, src/utils.py:116-127.                              */
+int gnpde_softmax_stats_f32(const int32_t* items, int64_t n_items, const int32_t* heavy, int64_t n_heavy,
+                            const int32_t* gidx, int group_is_dst, int mode, int64_t heads, int64_t dk,
+                            const double* cs, const float* q, const float* k, int64_t ldqk,
+                            float score_p0, float score_p1,
+                            double* m, float* rl, double* partials, void* stream);
+
+/* Attention aggregation + RHS epilogue over the aggregation CSR:
+ *   w_e = (1/h) sum_h exp(s_e,h - m[g(e),h]) * rl[g(e),h],  g = src (norm_idx 0) or dst (1)
+ *   ax  = sum_e w_e x[dst(e)],  f = epilogue(ax)   (multiply_attention :33-41, forward :52-59) */
+int gnpde_attn_rhs_f32(const int32_t* items, int64_t n_items, const int32_t* heavy, int64_t n_heavy,
+                       const int32_t* col, int norm_idx, int mode, int64_t heads, int64_t dk,
+                       const double* cs, const float* q, const float* k, int64_t ldqk,
+                       float score_p0, float score_p1, const double* m, const float* rl,
+                       int64_t C, const float* x, int64_t ldx, const float* x0, int64_t ldx0,
+                       const float* alpha, const float* beta, int flags,
+                       float* f, int64_t ldf, float* partials, void* stream);
+
+/* Per-edge, per-head attention in COO order (the [B,E,h] `attention` that
+ * SpGraphTransAttentionLayer.forward returns, function_transformer_attention.py:265-267):
+ *   att[perm[p]*heads + h] = exp(s_p,h - m[g,h]) * rl[g,h]  over the aggregation CSR. */
+int gnpde_edge_attention_f32(const int32_t* items, int64_t n_items, const int32_t* col, const int32_t* perm,
+                             int norm_idx, int mode, int64_t heads, int64_t dk,
+                             const double* cs, const float* q, const float* k, int64_t ldqk,
+                             float score_p0, float score_p1, const double* m, const float* rl,
+                             float* att, void* stream);
+
+/* ---------------------------------------------------------------- solver glue
+ * out[i] = y0[i] + scale * sum_{j<nk} coef[j] * k_j[i]   (nk <= 8; y0 may be NULL = 0)
+ * One pass for a Runge-Kutta stage input or step update (torchdiffeq
+ * rk4_alt_step_func / _runge_kutta_step combinations).                      */
+int gnpde_rk_combine_f32(int64_t n, const float* y0, int nk, const float* const* ks, const double* coef,
+                         double scale, float* out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GNPDE_H_ */

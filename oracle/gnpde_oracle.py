@@ -1,0 +1,358 @@
+"""CPU oracle for the GRAND/BLEND ODE right-hand side — TEST INFRASTRUCTURE ONLY.
+
+This module is the checker, never the product.  Only ``tests/``,
+``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may import
+it.  The shipped path (``graph-neural-pde_amd/gnpde``) never imports it and has
+no CPU fallback.
+
+It restates, in float64 numpy, the arithmetic of the reference hot path
+(alimt1992/graph-neural-pde @ 2025-01-17).  Every function cites the reference
+lines it follows.  Parity is PINNED: ``tests/test_oracle_golden.py`` checks
+every function below against the golden vectors in ``tests/golden/`` that
+``tests/golden/gen_golden.py`` produced by running the reference modules
+themselves (float64), plus the reference tests' known answers
+(test/test_utils.py:62-79, test/test_function_laplacian_diffusion.py:56-86,
+test/test_transformer_attention.py:98-106).  Exceptions, documented in
+DESIGN.md §Parity: the graph-normalisation helpers (the fork's versions crash
+on batched input, SURVEY §0.5 — pinned by the KATs only), the ``per_edge``
+score mode (upstream GRAND semantics, not in the fork: parity unpinned) and the
+integrators (torchdiffeq is absent; no reference test checks integrated values:
+parity unpinned).
+
+Layout conventions (same as the reference): ``edge_index [B,2,E]`` int64 with
+row 0 = source / aggregating node and row 1 = destination / gathered node;
+node features ``x [B,N,C]``; per-edge weights ``[B,E]`` or ``[B,E,h]``.
+"""
+import numpy as np
+
+try:  # scipy is only a speed-up for the aggregation at large sizes
+    import scipy.sparse as _sp
+except Exception:  # pragma: no cover
+    _sp = None
+
+
+def _as64(a):
+    return np.asarray(a, dtype=np.float64)
+
+
+def _sigmoid(a):
+    return 1.0 / (1.0 + np.exp(-a))
+
+
+# --------------------------------------------------------------------------- aggregation
+def aggregate(edge_index, w, x):
+    """``ax[b,i,:] = sum_{e: edge[b,0,e]=i} w[b,e] * x[b, edge[b,1,e], :]``.
+
+    Restates the sparse-COO -> to_dense -> matmul of
+    src/function_laplacian_diffusion.py:39-58 (and
+    src/function_transformer_attention.py:34-41); duplicates are summed, as
+    ``to_dense`` sums coalesced duplicates.
+    """
+    edge_index = np.asarray(edge_index)
+    w = _as64(w)
+    x = _as64(x)
+    B, N, C = x.shape
+    out = np.zeros((B, N, C))
+    for b in range(B):
+        src, dst = edge_index[b, 0], edge_index[b, 1]
+        if _sp is not None:
+            A = _sp.coo_matrix((w[b], (src, dst)), shape=(N, N)).tocsr()
+            out[b] = A @ x[b]
+        else:
+            np.add.at(out[b], src, w[b][:, None] * x[b][dst])
+    return out
+
+
+def alpha_value(alpha_train, no_alpha_sigmoid):
+    """src/function_laplacian_diffusion.py:69-72 / src/function_transformer_attention.py:52-55."""
+    a = float(alpha_train)
+    return a if no_alpha_sigmoid else float(_sigmoid(a))
+
+
+def rhs_epilogue(ax, x, x0, alpha_train, beta_train, add_source, no_alpha_sigmoid):
+    """``f = alpha*(ax - x) [+ beta_train * x0]`` — function_laplacian_diffusion.py:69-77."""
+    f = alpha_value(alpha_train, no_alpha_sigmoid) * (ax - _as64(x))
+    if add_source:
+        f = f + float(beta_train) * _as64(x0)
+    return f
+
+
+def laplacian_weights(block, edge_weight=None, attention_weights=None):
+    """Weight source by ``opt['block']`` — function_laplacian_diffusion.py:45-57."""
+    if block == 'attention':
+        return _as64(attention_weights).mean(axis=2)
+    if block in ('mixed', 'hard_attention'):
+        return _as64(attention_weights)
+    return _as64(edge_weight)
+
+
+def laplacian_rhs(edge_index, x, x0, alpha_train, beta_train, block='constant', edge_weight=None,
+                  attention_weights=None, add_source=False, no_alpha_sigmoid=False):
+    """LaplacianODEFunc.forward — src/function_laplacian_diffusion.py:60-77."""
+    w = laplacian_weights(block, edge_weight, attention_weights)
+    ax = aggregate(edge_index, w, x)
+    return rhs_epilogue(ax, x, x0, alpha_train, beta_train, add_source, no_alpha_sigmoid)
+
+
+# --------------------------------------------------------------------------- edge softmax
+def edge_softmax(src, index, num_nodes=None):
+    """utils.softmax — src/utils.py:116-127.
+
+    ``out = exp(s - max_g s) / (sum_g exp(s - max_g s) + 1e-16)`` with groups
+    ``g = index[b, e]`` per batch element, broadcast over the head axis.
+    """
+    src = _as64(src)
+    index = np.asarray(index)
+    B, E, H = src.shape
+    if num_nodes is None:
+        num_nodes = int(index.max()) + 1 if index.size else 0
+    out = np.empty_like(src)
+    for b in range(B):
+        mx = np.full((num_nodes, H), -np.inf)
+        np.maximum.at(mx, index[b], src[b])
+        ex = np.exp(src[b] - mx[index[b]])
+        sm = np.zeros((num_nodes, H))
+        np.add.at(sm, index[b], ex)
+        out[b] = ex / (sm[index[b]] + 1e-16)
+    return out
+
+
+def squareplus(src, index, num_nodes=None):
+    """utils.squareplus — src/utils.py:129-140 (intended call with num_nodes).
+
+    Per batch element: ``out = (s' + sqrt(s'^2 + 4))/2`` with ``s' = s - max(s)``
+    (max over all edges and heads of that element), normalised per group.
+    """
+    src = _as64(src)
+    index = np.asarray(index)
+    B, E, H = src.shape
+    if num_nodes is None:
+        num_nodes = int(index.max()) + 1
+    out = np.empty_like(src)
+    for b in range(B):
+        s = src[b] - src[b].max()
+        s = (s + np.sqrt(s * s + 4.0)) / 2.0
+        sm = np.zeros((num_nodes, H))
+        np.add.at(sm, index[b], s)
+        out[b] = s / (sm[index[b]] + 1e-16)
+    return out
+
+
+# --------------------------------------------------------------------------- attention scores
+def project(x, W, b):
+    """nn.Linear(x) = x W^T + b — function_transformer_attention.py:224-226."""
+    return _as64(x) @ _as64(W).T + _as64(b)
+
+
+def split_heads(q, heads):
+    """view(B,N,h,d_k).transpose(2,3) -> [B,N,d_k,h] — function_transformer_attention.py:230-238."""
+    B, N, A = q.shape
+    return q.reshape(B, N, heads, A // heads).transpose(0, 1, 3, 2)
+
+
+def attention_scores(x, edge_index, Wq, bq, Wk, bk, heads, attention_type='scaled_dot', score_mode='reference',
+                     output_var=1.0, lengthscale=1.0):
+    """``prods [B,E,h]`` — function_transformer_attention.py:218-259 (standard, non-beltrami branch).
+
+    score_mode='reference' restates the fork's scaled_dot (:249) exactly:
+    ``sum(matmul(src[B,h,E,dk], dst_k[B,h,dk,E] / sqrt(dk)), dim=3)``, which
+    equals ``q_src(e),h . (sum_e' k_dst(e'),h) / sqrt(dk)`` — one global key-sum
+    per (batch, head), computed here in O(E*d).  score_mode='per_edge' is the
+    upstream-GRAND ``q_src . k_dst / sqrt(dk)`` (not in the fork: unpinned).
+    exp_kernel (:246-247), cosine_sim (:250-252, torch>=1.12 CosineSimilarity:
+    each operand divided by max(norm, eps)), pearson (:253-259) are per-edge.
+    """
+    edge_index = np.asarray(edge_index)
+    q = split_heads(project(x, Wq, bq), heads)  # [B,N,dk,h]
+    k = split_heads(project(x, Wk, bk), heads)
+    B = q.shape[0]
+    dk = q.shape[2]
+    out = []
+    for b in range(B):
+        src = q[b][edge_index[b, 0]]  # [E,dk,h]
+        dst = k[b][edge_index[b, 1]]
+        if attention_type == 'scaled_dot':
+            if score_mode == 'reference':
+                ksum = dst.sum(axis=0)  # [dk,h]
+                p = (src * ksum[None]).sum(axis=1) / np.sqrt(dk)
+            else:
+                p = (src * dst).sum(axis=1) / np.sqrt(dk)
+        elif attention_type == 'exp_kernel':
+            p = output_var ** 2 * np.exp(-((src - dst) ** 2).sum(axis=1) / (2 * lengthscale ** 2))
+        elif attention_type in ('cosine_sim', 'pearson'):
+            if attention_type == 'pearson':
+                src = src - src.mean(axis=1, keepdims=True)
+                dst = dst - dst.mean(axis=1, keepdims=True)
+            eps = 1e-5
+            ns = np.maximum(np.sqrt((src ** 2).sum(axis=1, keepdims=True)), eps)
+            nd = np.maximum(np.sqrt((dst ** 2).sum(axis=1, keepdims=True)), eps)
+            p = ((src / ns) * (dst / nd)).sum(axis=1)
+        else:
+            raise ValueError(attention_type)
+        out.append(p)
+    return np.stack(out, 0)
+
+
+def transformer_attention(x, edge_index, Wq, bq, Wk, bk, heads, norm_idx, attention_type='scaled_dot',
+                          score_mode='reference', square_plus=False, output_var=1.0, lengthscale=1.0):
+    """SpGraphTransAttentionLayer.forward -> attention [B,E,h] — function_transformer_attention.py:159-267."""
+    prods = attention_scores(x, edge_index, Wq, bq, Wk, bk, heads, attention_type, score_mode, output_var,
+                             lengthscale)
+    index = np.asarray(edge_index)[:, norm_idx, :]
+    if square_plus:
+        return squareplus(prods, index)
+    return edge_softmax(prods, index)
+
+
+def transformer_rhs(edge_index, x, x0, Wq, bq, Wk, bk, heads, norm_idx, alpha_train, beta_train,
+                    attention_type='scaled_dot', score_mode='reference', add_source=False, no_alpha_sigmoid=False,
+                    square_plus=False, output_var=1.0, lengthscale=1.0):
+    """ODEFuncTransformerAtt.forward — function_transformer_attention.py:44-59 with
+    multiply_attention (mix_features=False, :33-41): head-mean weights x aggregation."""
+    att = transformer_attention(x, edge_index, Wq, bq, Wk, bk, heads, norm_idx, attention_type, score_mode,
+                                square_plus, output_var, lengthscale)
+    ax = aggregate(edge_index, att.mean(axis=2), x)
+    return rhs_epilogue(ax, x, x0, alpha_train, beta_train, add_source, no_alpha_sigmoid)
+
+
+# --------------------------------------------------------------------------- graph preparation
+def add_remaining_self_loops(edge_index, edge_weight, fill_value, num_nodes):
+    """Intended semantics of src/utils.py:16-42 (the fork's batched rewrite
+    corrupts the edge set): upstream GRAND / PyG
+    ``add_remaining_self_loops`` applied per batch element — non-loop edges are
+    kept in order, then one loop per node whose weight is the node's existing
+    loop weight (last one wins) or ``fill_value``.  Returns lists per batch
+    element (counts may differ)."""
+    edge_index = np.asarray(edge_index)
+    B, _, E = edge_index.shape
+    if edge_weight is None:
+        edge_weight = np.ones((B, E))
+    out_e, out_w = [], []
+    for b in range(B):
+        row, col = edge_index[b]
+        w = _as64(edge_weight[b])
+        mask = row != col
+        loop_w = np.full(num_nodes, float(fill_value))
+        inv = ~mask
+        loop_w[row[inv]] = w[inv]
+        ei = np.concatenate([edge_index[b][:, mask], np.stack([np.arange(num_nodes)] * 2)], axis=1)
+        out_e.append(ei)
+        out_w.append(np.concatenate([w[mask], loop_w]))
+    return out_e, out_w
+
+
+def get_rw_adj(edge_index, edge_weight=None, norm_dim=1, fill_value=0.0, num_nodes=None):
+    """Intended semantics of src/utils.py:215-233 pinned by test/test_utils.py:62-79:
+    dense result == sklearn ``normalize(A + s*I, 'l1', axis = 0 if norm_dim==1 else 1)``."""
+    edge_index = np.asarray(edge_index)
+    B, _, E = edge_index.shape
+    if num_nodes is None:
+        num_nodes = int(edge_index.max()) + 1
+    if edge_weight is None:
+        edge_weight = np.ones((B, E))
+    if fill_value != 0:
+        eis, ws = add_remaining_self_loops(edge_index, edge_weight, fill_value, num_nodes)
+    else:
+        eis = [edge_index[b] for b in range(B)]
+        ws = [_as64(edge_weight[b]) for b in range(B)]
+    out_w = []
+    for ei, w in zip(eis, ws):
+        idx = ei[0] if norm_dim == 0 else ei[1]
+        deg = np.zeros(num_nodes)
+        np.add.at(deg, idx, w)
+        with np.errstate(divide='ignore'):
+            inv = 1.0 / deg
+        out_w.append(inv[idx] * w)
+    return eis, out_w
+
+
+def gcn_norm_fill_val(edge_index, edge_weight=None, fill_value=0.0, num_nodes=None):
+    """Intended semantics of src/utils.py:177-194 (test/test_function_laplacian_diffusion.py:73-85,
+    test/test_ICML_gnn.py): ``D^-1/2 (A + s*I) D^-1/2`` with deg over the column index, inf -> 0."""
+    edge_index = np.asarray(edge_index)
+    B, _, E = edge_index.shape
+    if num_nodes is None:
+        num_nodes = int(edge_index.max()) + 1
+    if edge_weight is None:
+        edge_weight = np.ones((B, E))
+    if int(fill_value) != 0:
+        eis, ws = add_remaining_self_loops(edge_index, edge_weight, fill_value, num_nodes)
+    else:
+        eis = [edge_index[b] for b in range(B)]
+        ws = [_as64(edge_weight[b]) for b in range(B)]
+    out_w = []
+    for ei, w in zip(eis, ws):
+        deg = np.zeros(num_nodes)
+        np.add.at(deg, ei[1], w)
+        with np.errstate(divide='ignore'):
+            dis = deg ** -0.5
+        dis[np.isinf(dis)] = 0.0
+        out_w.append(dis[ei[0]] * w * dis[ei[1]])
+    return eis, out_w
+
+
+def to_dense(edge_index_b, w_b, num_nodes):
+    """Dense [N,N] of one batch element (duplicates summed) — utils.to_dense_adj :102-113."""
+    A = np.zeros((num_nodes, num_nodes))
+    np.add.at(A, (edge_index_b[0], edge_index_b[1]), w_b)
+    return A
+
+
+# --------------------------------------------------------------------------- integrators
+def fixed_grid(t0, t1, step_size):
+    """torchdiffeq FixedGridODESolver grid (0.2.x ``_grid_constructor_from_step_size``):
+    ``niters = ceil((t1-t0)/h + 1)``, ``t = arange(niters)*h + t0``, last point := t1.
+    Computed in float32, the dtype the reference's ``t.type_as(x)`` gives
+    (src/block_constant.py:23)."""
+    t0 = np.float32(t0)
+    t1 = np.float32(t1)
+    h = np.float32(step_size)
+    niters = int(np.ceil(np.float32((t1 - t0) / h) + np.float32(1)))
+    grid = np.arange(niters, dtype=np.float32) * h + t0
+    grid[-1] = t1
+    return grid
+
+
+def odeint_fixed(func, y0, t0, t1, method, step_size):
+    """euler / rk4 (torchdiffeq ``rk4_alt_step_func``, 3/8 rule) over the fixed grid;
+    parity unpinned."""
+    y = _as64(y0)
+    grid = fixed_grid(t0, t1, step_size)
+    for ta, tb in zip(grid[:-1], grid[1:]):
+        dt = float(tb) - float(ta)
+        if method == 'euler':
+            y = y + dt * func(float(ta), y)
+        elif method == 'rk4':
+            k1 = func(float(ta), y)
+            k2 = func(float(ta) + dt / 3.0, y + dt * k1 / 3.0)
+            k3 = func(float(ta) + dt * 2.0 / 3.0, y + dt * (k2 - k1 / 3.0))
+            k4 = func(float(tb), y + dt * (k1 - k2 + k3))
+            y = y + (k1 + 3.0 * (k2 + k3) + k4) * dt * 0.125
+        else:
+            raise ValueError(method)
+    return y
+
+
+# --------------------------------------------------------------------------- prepared CSR (timed CPU baseline)
+class LaplacianCSR(object):
+    """The Laplacian RHS with the COO -> CSR conversion done once (scipy), so the
+    CPU baseline times the steady-state RHS the way the GPU path is timed.
+    Same arithmetic as ``laplacian_rhs`` (function_laplacian_diffusion.py:39-77);
+    float32 storage and arithmetic, like the reference's fp32 runs."""
+
+    def __init__(self, edge_index, w, num_nodes, dtype=np.float32):
+        edge_index = np.asarray(edge_index)
+        self.B = edge_index.shape[0]
+        self.N = int(num_nodes)
+        self.A = [_sp.coo_matrix((np.asarray(w[b], dtype), (edge_index[b, 0], edge_index[b, 1])),
+                                 shape=(self.N, self.N)).tocsr() for b in range(self.B)]
+        self.dtype = dtype
+
+    def rhs(self, x, alpha, x0=None, beta=0.0, add_source=False, no_alpha_sigmoid=False):
+        a = self.dtype(alpha_value(alpha, no_alpha_sigmoid))
+        out = np.empty_like(x)
+        for b in range(self.B):
+            out[b] = a * (self.A[b] @ x[b] - x[b])
+            if add_source:
+                out[b] += self.dtype(beta) * x0[b]
+        return out

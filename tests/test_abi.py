@@ -1,0 +1,83 @@
+"""The C-ABI library loads, exports every symbol include/gnpde.h declares, and
+rejects bad arguments with an error code + message before touching the GPU
+(these calls validate on the host, so they run without a device)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from conftest import ROOT
+
+import gnpde
+from gnpde import _lib
+
+HEADER = os.path.join(ROOT, "include", "gnpde.h")
+
+
+def declared_symbols():
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(gnpde_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_header_declares_the_entry_points():
+    syms = declared_symbols()
+    for must in ("gnpde_csr_build", "gnpde_spmm_rhs_f32", "gnpde_attn_rhs_f32", "gnpde_softmax_stats_f32",
+                 "gnpde_linear_f32", "gnpde_ref_scores_f32", "gnpde_rk_combine_f32", "gnpde_last_error"):
+        assert must in syms
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _lib.load()
+    missing = [s for s in declared_symbols() if not hasattr(lib, s)]
+    assert not missing, missing
+
+
+def test_binding_covers_every_declared_symbol():
+    assert sorted(_lib.SIGNATURES) == declared_symbols()
+
+
+def test_abi_version():
+    assert _lib.load().gnpde_abi_version() == _lib.ABI_VERSION == 1
+
+
+def test_library_is_gfx950_code_object():
+    data = open(_lib.LIB_PATH, "rb").read()
+    assert b"gfx950" in data
+
+
+def test_errors_are_reported_not_raised():
+    lib = _lib.load()
+    vp = ctypes.c_void_p
+    # C = 0 -> EINVAL before any launch
+    rc = lib.gnpde_spmm_rhs_f32(vp(0), 0, vp(0), 0, vp(0), vp(0), 0, vp(0), 0, vp(0), 0, vp(0), vp(0), 0, vp(0), 0,
+                                vp(0), vp(0))
+    assert rc == -1
+    assert b"C must be" in lib.gnpde_last_error()
+    rc = lib.gnpde_linear_f32(vp(0), 10, 4, 4, vp(0), vp(0), 8, 8, vp(0), 8, vp(0), 0, vp(0))
+    assert rc == -1 and b"NULL" in lib.gnpde_last_error()
+    rc = lib.gnpde_csr_build(vp(0), 1, 10, 5, 2, vp(0), vp(0), vp(0), vp(0), 0, vp(0))
+    assert rc == -1 and b"key_row" in lib.gnpde_last_error()
+    rc = lib.gnpde_softmax_stats_f32(vp(0), 0, vp(0), 0, vp(0), 0, 0, 17, 1, vp(0), vp(0), vp(0), 1,
+                                     ctypes.c_float(1), ctypes.c_float(1), vp(0), vp(0), vp(0), vp(0))
+    assert rc == -3 and b"heads" in lib.gnpde_last_error()
+    rc = lib.gnpde_rk_combine_f32(16, vp(0), 9, None, None, ctypes.c_double(1.0), vp(1), vp(0))
+    assert rc == -3
+
+
+def test_python_wrapper_raises_with_message():
+    with pytest.raises(_lib.GnpdeError, match="rc=-1"):
+        _lib.call("gnpde_linear_f32", ctypes.c_void_p(0), 10, 4, 4, ctypes.c_void_p(0), ctypes.c_void_p(0), 8, 8,
+                  ctypes.c_void_p(0), 8, ctypes.c_void_p(0), 0, ctypes.c_void_p(0))
+
+
+def test_workspace_size_queries():
+    lib = _lib.load()
+    assert lib.gnpde_csr_workspace_bytes(1, 1000, 100) >= 3 * 4000
+    assert lib.gnpde_plan_workspace_bytes(100) >= 6 * 404
+    assert lib.gnpde_keysum_workspace_bytes(2, 1000, 64, 32) > 0
+
+
+def test_package_exposes_library_path():
+    assert gnpde.native_library_path().endswith("libgnpde.so")

@@ -1,0 +1,444 @@
+"""GPU parity: the HIP path (through the C ABI, via the drop-in classes and
+gnpde.ops) against the reference's golden vectors and the CPU oracle.
+
+Tolerances (north star: "within 1e-5 rel fp32"): RHS outputs
+max|f - f_ref| / max|f_ref| <= 1e-5 against float64 goldens / oracle;
+attention weights max abs diff <= 2e-5; integer structures (CSR, plans)
+bit-exact; repeated runs bit-identical (no float atomics anywhere).
+"""
+import glob
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import gnpde
+import gnpde_oracle as O
+from conftest import GOLDEN
+from gnpde import ops, synthetic
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+RTOL = 1e-5
+
+FIXTURES = sorted(glob.glob(os.path.join(GOLDEN, "*.npz")))
+
+
+def load(path):
+    d = np.load(path, allow_pickle=False)
+    return d, json.loads(str(d["meta"]))
+
+
+def rel(a, b):
+    a = a.detach().double().cpu().numpy() if isinstance(a, torch.Tensor) else np.asarray(a, np.float64)
+    den = max(np.abs(b).max(), 1e-30)
+    return np.abs(a - b).max() / den
+
+
+def T(a, dtype=None):
+    t = torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+    return t if dtype is None else t.to(dtype)
+
+
+OPT = {'self_loop_weight': 1, 'leaky_relu_slope': 0.2, 'heads': 2, 'attention_norm_idx': 0, 'add_source': False,
+       'hidden_dim': 6, 'block': 'constant', 'function': 'laplacian', 'augment': False, 'adjoint': False,
+       'tol_scale': 1, 'time': 1, 'method': 'euler', 'no_alpha_sigmoid': False, 'reweight_attention': False,
+       'step_size': 1, 'beltrami': False, 'attention_type': 'scaled_dot', 'square_plus': False, 'max_nfe': 100000,
+       'data_norm': 'rw', 'max_iters': 1000, 'multi_modal': False, 'mix_features': False, 'attention_dim': 16}
+
+
+def make_laplacian(d, m):
+    C = m["C"]
+    opt = dict(OPT, hidden_dim=C, block=m["block"], add_source=m["add_source"], no_alpha_sigmoid=m["no_alpha_sigmoid"],
+               heads=m["heads"])
+    func = gnpde.LaplacianODEFunc(C, C, opt, DEV).to(DEV)
+    with torch.no_grad():
+        func.alpha_train.fill_(float(d["alpha_train"]))
+        func.beta_train.fill_(float(d["beta_train"]))
+    func.edge_index = T(d["edge_index"])
+    if m["block"] == "constant":
+        func.edge_weight = T(d["weights"])
+    else:
+        func.attention_weights = T(d["weights"])
+    func.x0 = T(d["x0"])
+    return func
+
+
+def make_transformer(d, m, score_mode="reference"):
+    C = m["C"]
+    opt = dict(OPT, hidden_dim=C, heads=m["heads"], attention_dim=m["attention_dim"],
+               attention_norm_idx=m["attention_norm_idx"], attention_type=m["attention_type"],
+               add_source=m["add_source"], no_alpha_sigmoid=m["no_alpha_sigmoid"], function='transformer',
+               attention_score_mode=score_mode)
+    func = gnpde.ODEFuncTransformerAtt(C, C, opt, DEV).to(DEV)
+    lay = func.multihead_att_layer
+    with torch.no_grad():
+        func.alpha_train.fill_(float(d["alpha_train"]))
+        func.beta_train.fill_(float(d["beta_train"]))
+        lay.Q.weight.copy_(T(d["Wq"]))
+        lay.Q.bias.copy_(T(d["bq"]))
+        lay.K.weight.copy_(T(d["Wk"]))
+        lay.K.bias.copy_(T(d["bk"]))
+        if m["attention_type"] == "exp_kernel":
+            lay.output_var.fill_(m["output_var"])
+            lay.lengthscale.fill_(m["lengthscale"])
+    func.eval()
+    func.edge_index = T(d["edge_index"])
+    func.x0 = T(d["x0"])
+    return func
+
+
+# ---------------------------------------------------------------- golden vectors
+@pytest.mark.parametrize("path", [p for p in FIXTURES if os.path.basename(p).startswith("lap_")],
+                         ids=os.path.basename)
+def test_laplacian_rhs_golden(path):
+    d, m = load(path)
+    func = make_laplacian(d, m)
+    with torch.no_grad():
+        f = func(torch.tensor(0.0), T(d["x"]))
+    assert f.shape == d["f"].shape
+    assert rel(f, d["f"]) <= RTOL
+
+
+@pytest.mark.parametrize("path", [p for p in FIXTURES if os.path.basename(p).startswith("att_")],
+                         ids=os.path.basename)
+def test_transformer_rhs_golden(path):
+    d, m = load(path)
+    func = make_transformer(d, m)
+    with torch.no_grad():
+        f = func(torch.tensor(0.0), T(d["x"]))
+        att, _ = func.multihead_att_layer(T(d["x"]), func.edge_index)
+    assert att.shape == d["attention"].shape
+    assert np.abs(att.double().cpu().numpy() - d["attention"]).max() <= 2e-5
+    if np.abs(d["f"]).max() == 0:
+        assert float(f.abs().max()) < 1e-6
+    else:
+        assert rel(f, d["f"]) <= RTOL
+
+
+def test_kat_symmetric_attention_exactly_half():
+    """test/test_transformer_attention.py:98-106."""
+    d, m = load(os.path.join(GOLDEN, "att_kat_symmetric.npz"))
+    func = make_transformer(d, m)
+    with torch.no_grad():
+        att, _ = func.multihead_att_layer(T(d["x"]), func.edge_index)
+    assert torch.all(att == 0.5)
+
+
+# ---------------------------------------------------------------- random graphs with hubs (plan split path)
+def hub_graph(N, E, seed, B=1, hub_frac=0.15):
+    """Random graph where node 0 (and node 1 as destination) receive a large
+    share of the edges, so rows/columns exceed the 256-edge chunk."""
+    rng = np.random.default_rng(seed)
+    ei = rng.integers(0, N, size=(B, 2, E))
+    nh = int(hub_frac * E)
+    ei[:, 0, :nh] = 0
+    ei[:, 1, nh:2 * nh] = 1
+    for b in range(B):
+        p = rng.permutation(E)
+        ei[b] = ei[b][:, p]
+    return ei
+
+
+@pytest.mark.parametrize("C", [1, 3, 7, 16, 64, 80, 128, 162, 256, 512])
+def test_spmm_rhs_vs_oracle_with_hubs(C):
+    N, E = 3000, 40000
+    ei = hub_graph(N, E, seed=C)
+    rng = np.random.default_rng(C + 1)
+    w = rng.uniform(0.1, 1, size=(1, E)).astype(np.float32)
+    x = rng.standard_normal((1, N, C)).astype(np.float32)
+    x0 = rng.standard_normal((1, N, C)).astype(np.float32)
+    g = ops.GraphCSR(T(ei), N)
+    assert g.csr.plan.n_heavy >= 1 and g.csc.plan.n_heavy >= 1
+    wc = g.gather_weights(T(w))
+    alpha, beta = torch.tensor(0.37, device=DEV), torch.tensor(-0.8, device=DEV)
+    f = ops.spmm_rhs(g, wc, T(x), T(x0), alpha, beta, add_source=True)
+    want = O.laplacian_rhs(ei, x, x0, 0.37, -0.8, edge_weight=w, add_source=True)
+    assert rel(f, want) <= RTOL
+    ax = ops.spmm_rhs(g, wc, T(x), rhs=False)
+    assert rel(ax, O.aggregate(ei, w, x)) <= RTOL
+    # transpose (CSC) aggregation = A^T x
+    wt = g.gather_weights(T(w), transpose=True)
+    atx = ops.spmm_rhs(g, wt, T(x), rhs=False, transpose=True)
+    assert rel(atx, O.aggregate(ei[:, ::-1, :], w, x)) <= RTOL
+
+
+def test_csr_structures_exact():
+    N, E, B = 500, 6000, 2
+    ei = hub_graph(N, E, seed=3, B=B)
+    g = ops.GraphCSR(T(ei), N, chunk=64)
+    rowptr = g.csr.rowptr.cpu().numpy()
+    col = g.csr.col.cpu().numpy()
+    perm = g.csr.perm.cpu().numpy()
+    src = (np.arange(B)[:, None] * N + ei[:, 0]).reshape(-1)
+    dst = (np.arange(B)[:, None] * N + ei[:, 1]).reshape(-1)
+    order = np.argsort(src, kind="stable")
+    assert np.array_equal(perm, order)
+    assert np.array_equal(col, dst[order])
+    assert np.array_equal(rowptr, np.searchsorted(src[order], np.arange(B * N + 1), side="left"))
+    # plan covers every edge exactly once, chunks <= 64 edges, hubs split
+    items = g.csr.plan.items[:4 * g.csr.plan.n_items].view(-1, 4).cpu().numpy()
+    cover = np.zeros(B * E, np.int64)
+    for r, b0, b1, slot in items:
+        assert b1 - b0 <= 64 and rowptr[r] <= b0 <= b1 <= rowptr[r + 1]
+        cover[b0:b1] += 1
+    assert np.all(cover == 1)
+    assert len(np.unique(items[:, 0])) == B * N  # every row has an item (empty rows too)
+    deg = g.indeg.cpu().numpy()
+    assert np.array_equal(deg, np.bincount(dst, minlength=B * N))
+
+
+def test_empty_graph_and_isolated_rows():
+    N, C = 50, 8
+    x = torch.randn(1, N, C, device=DEV)
+    g = ops.GraphCSR(torch.zeros(1, 2, 0, dtype=torch.int64, device=DEV), N)
+    f = ops.spmm_rhs(g, torch.zeros(1, device=DEV), x, alpha=torch.tensor(0.0, device=DEV))
+    assert torch.allclose(f, -0.5 * x)  # sigma(0) * (0 - x)
+
+
+def test_bit_reproducible():
+    N, E, C = 4000, 60000, 128
+    ei = hub_graph(N, E, seed=11)
+    g = ops.GraphCSR(T(ei), N)
+    w = torch.rand(1, E, device=DEV)
+    x = torch.randn(1, N, C, device=DEV)
+    wc = g.gather_weights(w)
+    a = ops.spmm_rhs(g, wc, x, alpha=torch.tensor(0.1, device=DEV))
+    b = ops.spmm_rhs(g, wc, x, alpha=torch.tensor(0.1, device=DEV))
+    assert torch.equal(a, b)
+
+
+# ---------------------------------------------------------------- attention: per-edge modes, hubs
+@pytest.mark.parametrize("attention_type", ["scaled_dot", "exp_kernel", "cosine_sim", "pearson"])
+@pytest.mark.parametrize("norm_idx", [0, 1])
+def test_attention_rhs_per_edge_vs_oracle(attention_type, norm_idx):
+    N, E, C, h, att = 2000, 30000, 48, 4, 32
+    ei = hub_graph(N, E, seed=norm_idx + 5)
+    rng = np.random.default_rng(9)
+    x = rng.standard_normal((1, N, C)).astype(np.float32)
+    x0 = rng.standard_normal((1, N, C)).astype(np.float32)
+    Wq, Wk = [(rng.standard_normal((att, C)) * 0.1).astype(np.float32) for _ in range(2)]
+    bq, bk = [(rng.standard_normal(att) * 0.1).astype(np.float32) for _ in range(2)]
+    g = ops.GraphCSR(T(ei), N)
+    ns = ops.node_scores(g, T(x), T(Wq), T(bq), T(Wk), T(bk), h, attention_type, 'per_edge', 1.3, 0.8)
+    m, rl = ops.softmax_stats(g, ns, norm_idx)
+    f = ops.attn_rhs(g, ns, m, rl, norm_idx, T(x), T(x0), torch.tensor(0.3, device=DEV),
+                     torch.tensor(0.6, device=DEV), add_source=True)
+    want = O.transformer_rhs(ei, x, x0, Wq, bq, Wk, bk, h, norm_idx, 0.3, 0.6, attention_type=attention_type,
+                             score_mode='per_edge', add_source=True, output_var=1.3, lengthscale=0.8)
+    assert rel(f, want) <= RTOL
+    a = ops.edge_attention(g, ns, m, rl, norm_idx)
+    wa = O.transformer_attention(x, ei, Wq, bq, Wk, bk, h, norm_idx, attention_type, 'per_edge', output_var=1.3,
+                                 lengthscale=0.8)
+    assert np.abs(a.double().cpu().numpy() - wa).max() <= 2e-5
+
+
+@pytest.mark.parametrize("norm_idx", [0, 1])
+@pytest.mark.parametrize("heads,att", [(1, 8), (2, 32), (8, 128), (16, 32)])
+def test_attention_rhs_reference_mode_vs_oracle(norm_idx, heads, att):
+    N, E, C, B = 1500, 20000, 40, 2
+    ei = hub_graph(N, E, seed=heads, B=B)
+    rng = np.random.default_rng(heads + att)
+    x = rng.standard_normal((B, N, C)).astype(np.float32)
+    Wq, Wk = [(rng.standard_normal((att, C)) * 0.02).astype(np.float32) for _ in range(2)]
+    bq, bk = [(rng.standard_normal(att) * 0.02).astype(np.float32) for _ in range(2)]
+    g = ops.GraphCSR(T(ei), N)
+    ns = ops.node_scores(g, T(x), T(Wq), T(bq), T(Wk), T(bk), heads)
+    m, rl = ops.softmax_stats(g, ns, norm_idx)
+    f = ops.attn_rhs(g, ns, m, rl, norm_idx, T(x), alpha=torch.tensor(-0.2, device=DEV))
+    want = O.transformer_rhs(ei, x, None, Wq, bq, Wk, bk, heads, norm_idx, -0.2, 0.0)
+    assert rel(f, want) <= RTOL
+
+
+# ---------------------------------------------------------------- MFMA projection
+@pytest.mark.parametrize("R,K,Nout,split", [(1, 4, 8, 4), (1000, 128, 64, 32), (5003, 80, 256, 128),
+                                            (777, 162, 64, 32), (64, 7, 33, 33), (4096, 256, 128, 64)])
+def test_linear_mfma_vs_fp64(R, K, Nout, split):
+    x = torch.randn(R, K, device=DEV)
+    W = torch.randn(Nout, K, device=DEV) * 0.1
+    b = torch.randn(Nout, device=DEV)
+    qa, qb = ops.linear(x, W, b, split)
+    want = (x.double() @ W.double().T + b.double())
+    got = torch.cat([qa, qb], 1) if qb is not None else qa
+    err = (got.double() - want).abs().max() / want.abs().max()
+    assert err < 2e-6
+
+
+# ---------------------------------------------------------------- solver glue
+def test_rk_combine():
+    y0 = torch.randn(1000003, device=DEV)
+    ks = [torch.randn_like(y0) for _ in range(7)]
+    c = [0.1, -0.5, 0.25, 1.0, 2.0, -3.0, 0.5]
+    out = ops.rk_combine(y0, ks, c, 0.3)
+    want = y0.double() + 0.3 * sum(ci * k.double() for ci, k in zip(c, ks))
+    assert (out.double() - want).abs().max() < 1e-5
+    out4 = ops.rk_combine(y0[:1000000], [k[:1000000] for k in ks[:2]], c[:2], 1.0)
+    assert torch.allclose(out4, y0[:1000000] + 0.1 * ks[0][:1000000] - 0.5 * ks[1][:1000000], atol=1e-6)
+    err = ops.rk_combine(None, ks[:3], c[:3], 2.0)
+    assert torch.allclose(err, 2.0 * (0.1 * ks[0] - 0.5 * ks[1] + 0.25 * ks[2]), atol=1e-5)
+
+
+# ---------------------------------------------------------------- ODE blocks end to end
+def _prep_oracle(ei, N, fill=1.0):
+    eis, ws = O.get_rw_adj(ei, norm_dim=1, fill_value=fill, num_nodes=N)
+    return np.stack(eis, 0), np.stack(ws, 0)
+
+
+@pytest.mark.parametrize("method,step", [("euler", 0.1), ("rk4", 0.25)])
+def test_constant_block_integration_vs_oracle(method, step):
+    N, E, C = 2708, 10556, 80  # Cora-sized
+    rng = np.random.default_rng(4)
+    ei = rng.integers(0, N, size=(1, 2, E))
+    x = rng.standard_normal((1, N, C)).astype(np.float32)
+    opt = dict(OPT, hidden_dim=C, method=method, step_size=step, add_source=True, time=1.0)
+    blk = gnpde.ConstantODEblock(gnpde.LaplacianODEFunc, [], opt, DEV, t=torch.tensor([0, 1])).to(DEV)
+    with torch.no_grad():
+        blk.odefunc.alpha_train.fill_(0.5)
+        blk.odefunc.beta_train.fill_(0.25)
+    blk.eval()
+    data = gnpde.GraphData()
+    data.new_graph(T(ei), N)
+    blk.set_x0(T(x))
+    with torch.no_grad():
+        z = blk(T(x), data)
+    eo, wo = _prep_oracle(ei, N)
+    f = lambda t, y: O.laplacian_rhs(eo, y, x, 0.5, 0.25, edge_weight=wo, add_source=True)  # noqa: E731
+    want = O.odeint_fixed(f, x, 0.0, 1.0, method, step)
+    assert rel(z, want) <= RTOL
+    assert blk.odefunc.nfe == (10 if method == "euler" else 16)
+
+
+def test_constant_block_dopri5_vs_exact():
+    """dopri5 on the linear diffusion ODE vs expm (integrated-value parity is unpinned
+    against the reference; this checks the solver converges to the exact flow)."""
+    import scipy.linalg
+    N, E, C = 300, 1500, 8
+    rng = np.random.default_rng(8)
+    ei = rng.integers(0, N, size=(1, 2, E))
+    x = rng.standard_normal((1, N, C)).astype(np.float32)
+    opt = dict(OPT, hidden_dim=C, method='dopri5', tol_scale=100.0)
+    blk = gnpde.ConstantODEblock(gnpde.LaplacianODEFunc, [], opt, DEV, t=torch.tensor([0, 1])).to(DEV).eval()
+    data = gnpde.GraphData()
+    data.new_graph(T(ei), N)
+    with torch.no_grad():
+        z = blk(T(x), data)
+    eo, wo = _prep_oracle(ei, N)
+    A = O.to_dense(eo[0], wo[0], N)
+    M = 0.5 * (A - np.eye(N))
+    want = scipy.linalg.expm(M) @ x[0].astype(np.float64)
+    assert rel(z[0], want) <= 1e-4
+
+
+def test_attention_block_vs_oracle():
+    N, E, C, h, att = 1000, 6000, 32, 4, 32
+    rng = np.random.default_rng(12)
+    ei = rng.integers(0, N, size=(1, 2, E))
+    x = rng.standard_normal((1, N, C)).astype(np.float32)
+    opt = dict(OPT, hidden_dim=C, heads=h, attention_dim=att, block='attention', attention_norm_idx=1,
+               method='rk4', step_size=0.5)
+    blk = gnpde.AttODEblock(gnpde.LaplacianODEFunc, [], opt, DEV, t=torch.tensor([0, 1])).to(DEV).eval()
+    Wq, Wk = [(rng.standard_normal((att, C)) * 0.05).astype(np.float32) for _ in range(2)]
+    bq, bk = [(rng.standard_normal(att) * 0.05).astype(np.float32) for _ in range(2)]
+    with torch.no_grad():
+        lay = blk.multihead_att_layer
+        lay.Q.weight.copy_(T(Wq))
+        lay.Q.bias.copy_(T(bq))
+        lay.K.weight.copy_(T(Wk))
+        lay.K.bias.copy_(T(bk))
+    data = gnpde.GraphData()
+    data.new_graph(T(ei), N)
+    with torch.no_grad():
+        z = blk(T(x), data)
+    eo, wo = _prep_oracle(ei, N)
+    attn = O.transformer_attention(x, eo, Wq, bq, Wk, bk, h, 1)
+    f = lambda t, y: O.laplacian_rhs(eo, y, None, 0.0, 0.0, block='attention', attention_weights=attn)  # noqa
+    want = O.odeint_fixed(f, x, 0.0, 1.0, 'rk4', 0.5)
+    assert rel(z, want) <= RTOL
+
+
+def test_transformer_function_in_block_dopri5_runs():
+    """function=transformer, method=dopri5 (config C2 shape, small)."""
+    N, E, C = 400, 2000, 16
+    rng = np.random.default_rng(13)
+    ei = rng.integers(0, N, size=(1, 2, E))
+    x = torch.randn(1, N, C, device=DEV)
+    opt = dict(OPT, hidden_dim=C, heads=8, attention_dim=32, function='transformer', attention_norm_idx=1,
+               method='dopri5', tol_scale=1000.0)
+    blk = gnpde.ConstantODEblock(gnpde.ODEFuncTransformerAtt, [], opt, DEV, t=torch.tensor([0, 1])).to(DEV).eval()
+    data = gnpde.GraphData()
+    data.new_graph(T(ei), N)
+    with torch.no_grad():
+        z = blk(x, data)
+    assert z.shape == x.shape and torch.isfinite(z).all()
+
+
+# ---------------------------------------------------------------- backward (x, alpha, beta)
+def test_laplacian_backward_vs_oracle():
+    N, E, C = 1200, 15000, 24
+    ei = hub_graph(N, E, seed=21)
+    rng = np.random.default_rng(22)
+    w = rng.uniform(0.1, 1, size=(1, E)).astype(np.float32)
+    x = rng.standard_normal((1, N, C)).astype(np.float32)
+    x0 = rng.standard_normal((1, N, C)).astype(np.float32)
+    gout = rng.standard_normal((1, N, C)).astype(np.float32)
+    func = gnpde.LaplacianODEFunc(C, C, dict(OPT, hidden_dim=C, add_source=True), DEV).to(DEV)
+    with torch.no_grad():
+        func.alpha_train.fill_(0.3)
+        func.beta_train.fill_(0.7)
+    func.edge_index = T(ei)
+    func.edge_weight = T(w)
+    func.x0 = T(x0)
+    xt = T(x).requires_grad_(True)
+    f = func(0, xt)
+    f.backward(T(gout))
+    a = 1 / (1 + np.exp(-0.3))
+    gx_want = a * (O.aggregate(ei[:, ::-1, :], w, gout) - gout)
+    assert rel(xt.grad, gx_want) <= RTOL
+    d = O.aggregate(ei, w, x) - x
+    ga_want = (gout * d).sum() * a * (1 - a)
+    assert abs(float(func.alpha_train.grad) - ga_want) / abs(ga_want) < 1e-5
+    gb_want = (gout * x0).sum()
+    assert abs(float(func.beta_train.grad) - gb_want) / abs(gb_want) < 1e-5
+
+
+# ---------------------------------------------------------------- full-size properties (G-arxiv)
+def test_arxiv_scale_rhs_vs_oracle_and_properties():
+    N, E, C = synthetic.ARXIV_N, synthetic.ARXIV_E, 128
+    ei, w = synthetic.rw_graph(N, E, seed=0, device=DEV)
+    x = synthetic.features(1, N, C, seed=1, device=DEV)
+    g = ops.GraphCSR(ei, N)
+    assert g.csr.plan.n_heavy > 0  # RMAT hubs exercise the split path
+    wc = g.gather_weights(w)
+    f = ops.spmm_rhs(g, wc, x, alpha=torch.tensor(0.0, device=DEV))
+    ein, wn, xn = ei.cpu().numpy(), w.cpu().numpy(), x.cpu().numpy()
+    want = O.laplacian_rhs(ein, xn, None, 0.0, 0.0, edge_weight=wn)
+    assert rel(f, want) <= RTOL
+    # column-stochastic rw normalisation: column sums of A x equal those of x
+    ax = ops.spmm_rhs(g, wc, x, rhs=False)
+    assert torch.allclose(ax.double().sum(1), x.double().sum(1), rtol=1e-4, atol=1e-2)
+    # linearity
+    x2 = synthetic.features(1, N, C, seed=2, device=DEV)
+    lhs = ops.spmm_rhs(g, wc, x + 2 * x2, rhs=False)
+    rhs_ = ax + 2 * ops.spmm_rhs(g, wc, x2, rhs=False)
+    assert (lhs - rhs_).abs().max() / rhs_.abs().max() < 1e-5
+
+
+def test_arxiv_scale_attention_vs_oracle():
+    N, E, C, h, att = synthetic.ARXIV_N, synthetic.ARXIV_E, 128, 2, 32
+    ei, _ = synthetic.rw_graph(N, E, seed=0, device=DEV)
+    x = synthetic.features(1, N, C, seed=1, device=DEV)
+    gen = torch.Generator(device=DEV)
+    gen.manual_seed(2)
+    Wq, Wk = [torch.randn(att, C, generator=gen, device=DEV) * 0.1 for _ in range(2)]
+    bq, bk = [torch.randn(att, generator=gen, device=DEV) * 0.1 for _ in range(2)]
+    g = ops.GraphCSR(ei, N)
+    ein, xn = ei.cpu().numpy(), x.cpu().numpy()
+    npw = [t.cpu().numpy() for t in (Wq, bq, Wk, bk)]
+    for mode, norm_idx in (("per_edge", 0), ("reference", 1)):
+        ns = ops.node_scores(g, x, Wq, bq, Wk, bk, h, 'scaled_dot', mode)
+        m, rl = ops.softmax_stats(g, ns, norm_idx)
+        f = ops.attn_rhs(g, ns, m, rl, norm_idx, x, alpha=torch.tensor(0.0, device=DEV))
+        want = O.transformer_rhs(ein, xn, None, *npw, h, norm_idx, 0.0, 0.0, score_mode=mode)
+        assert rel(f, want) <= RTOL, mode

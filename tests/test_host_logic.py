@@ -1,0 +1,169 @@
+"""Host-side logic of the drop-in layer, on CPU: registry, constructor/attribute
+contract, state_dict keys, the no-fallback guarantee, graph normalisation
+(intended semantics, pinned by the reference's KATs) and the bundled
+integrator's control logic (with a torch stage combiner injected — the product
+path always combines on the GPU)."""
+import numpy as np
+import pytest
+import torch
+
+import gnpde
+import gnpde_oracle as O
+from gnpde import integrator as gode
+from gnpde import utils as gu
+
+OPT = {'self_loop_weight': 1, 'leaky_relu_slope': 0.2, 'heads': 2, 'attention_norm_idx': 0, 'add_source': False,
+       'hidden_dim': 6, 'block': 'constant', 'function': 'laplacian', 'augment': False, 'adjoint': False,
+       'tol_scale': 1, 'time': 1, 'method': 'euler', 'no_alpha_sigmoid': False, 'reweight_attention': False,
+       'step_size': 1, 'beltrami': False, 'attention_type': 'scaled_dot', 'square_plus': False, 'max_nfe': 1000,
+       'data_norm': 'rw', 'max_iters': 1000, 'multi_modal': False, 'mix_features': False, 'attention_dim': 16}
+
+
+def test_registry_matches_reference_names():
+    assert gnpde.set_function(dict(OPT, function='laplacian')) is gnpde.LaplacianODEFunc
+    assert gnpde.set_function(dict(OPT, function='transformer')) is gnpde.ODEFuncTransformerAtt
+    assert gnpde.set_block(dict(OPT, block='constant')) is gnpde.ConstantODEblock
+    assert gnpde.set_block(dict(OPT, block='attention')) is gnpde.AttODEblock
+    with pytest.raises(NotImplementedError):
+        gnpde.set_block(dict(OPT, block='mixed'))
+    with pytest.raises(NotImplementedError):
+        gnpde.set_function(dict(OPT, function='GAT'))
+    from gnpde.model_configurations import BlockNotDefined, FunctionNotDefined
+    with pytest.raises(BlockNotDefined):
+        gnpde.set_block(dict(OPT, block='nope'))
+    with pytest.raises(FunctionNotDefined):
+        gnpde.set_function(dict(OPT, function='nope'))
+
+
+def test_state_dict_keys_match_reference_layout():
+    blk = gnpde.ConstantODEblock(gnpde.LaplacianODEFunc, [], OPT, None, t=torch.tensor([0, 1]))
+    keys = set(blk.state_dict().keys())
+    for k in ('odefunc.alpha_train', 'odefunc.beta_train', 'odefunc.w', 'odefunc.d', 'odefunc.alpha_sc',
+              'odefunc.beta_sc', 'reg_odefunc.odefunc.alpha_train'):
+        assert k in keys
+    tr = gnpde.ODEFuncTransformerAtt(6, 6, OPT, None)
+    keys = set(tr.state_dict().keys())
+    for k in ('multihead_att_layer.Q.weight', 'multihead_att_layer.K.bias', 'multihead_att_layer.V.weight',
+              'multihead_att_layer.Wout.weight', 'alpha_train'):
+        assert k in keys
+    assert float(tr.multihead_att_layer.Q.weight[0, 0].detach()) == pytest.approx(1e-5)
+
+
+def test_attention_block_contract():
+    blk = gnpde.AttODEblock(gnpde.LaplacianODEFunc, [], dict(OPT, block='attention'), None,
+                            t=torch.tensor([0, 1]))
+    assert isinstance(blk.multihead_att_layer, gnpde.SpGraphTransAttentionLayer)
+    assert blk.test_integrator is gnpde.odeint and blk.atol == 1e-7 and blk.rtol == 1e-9
+
+
+def test_no_cpu_fallback():
+    func = gnpde.LaplacianODEFunc(2, 2, dict(OPT, hidden_dim=2), None)
+    func.edge_index = torch.tensor([[[0, 1, 2, 1], [1, 0, 1, 2]]])
+    func.edge_weight = torch.ones(1, 4)
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        func(0, torch.ones(1, 3, 2))
+    with pytest.raises(RuntimeError, match="ROCm device"):
+        gnpde.odeint(lambda t, y: y, torch.ones(3), torch.tensor([0., 1.]), method='euler')
+
+
+def test_unsupported_settings_raise():
+    for bad in (dict(mix_features=True), dict(square_plus=True), dict(multi_modal=True),
+                dict(beltrami=True, attention_type='exp_kernel')):
+        with pytest.raises(NotImplementedError):
+            gnpde.ODEFuncTransformerAtt(6, 6, dict(OPT, **bad), None)
+
+
+def test_max_nfe_guard():
+    func = gnpde.LaplacianODEFunc(2, 2, dict(OPT, hidden_dim=2, max_nfe=3), None)
+    func.nfe = 4
+    with pytest.raises(gnpde.MaxNFEException):
+        func(0, torch.ones(1, 3, 2))
+
+
+@pytest.mark.parametrize("self_loop", [0, 0.3, 1, 3.2])
+@pytest.mark.parametrize("norm_dim", [0, 1])
+def test_get_rw_adj_kat(self_loop, norm_dim):
+    """test/test_utils.py:62-79 against gnpde.utils (torch, intended semantics)."""
+    from sklearn.preprocessing import normalize
+    edge = torch.tensor([[[0, 2, 2, 1], [1, 0, 1, 2]]])
+    ei, w = gu.get_rw_adj(edge, norm_dim=norm_dim, fill_value=self_loop, num_nodes=3)
+    got = O.to_dense(ei[0].numpy(), w[0].numpy(), 3)
+    base = O.to_dense(edge[0].numpy(), np.ones(4), 3)
+    assert np.allclose(got, normalize(base + np.identity(3) * self_loop, norm='l1', axis=0 if norm_dim == 1 else 1))
+
+
+def test_gcn_norm_kat():
+    edge = torch.tensor([[[0, 1, 2, 1], [1, 0, 1, 2]]])
+    ei, w = gu.gcn_norm_fill_val(edge, fill_value=1, num_nodes=3)
+    aug = O.to_dense(edge[0].numpy(), np.ones(4), 3) + np.identity(3)
+    deg = np.sqrt(aug.sum(axis=1))
+    assert np.allclose(O.to_dense(ei[0].numpy(), w[0].numpy(), 3), aug / deg[:, None] / deg[None, :])
+
+
+def test_add_remaining_self_loops_matches_oracle():
+    rng = np.random.default_rng(0)
+    ei = rng.integers(0, 9, size=(2, 2, 30))
+    ei[:, 1, :5] = ei[:, 0, :5]  # some existing loops
+    w = rng.uniform(size=(2, 30)).astype(np.float32)
+    oe, ow = O.add_remaining_self_loops(ei, w, 0.5, 9)
+    for b in range(2):
+        te, tw = gu.add_remaining_self_loops(torch.from_numpy(ei[b:b + 1]), torch.from_numpy(w[b:b + 1]), 0.5, 9)
+        assert np.array_equal(te[0].numpy(), oe[b]) and np.allclose(tw[0].numpy(), ow[b])
+    if oe[0].shape[1] != oe[1].shape[1]:
+        with pytest.raises(ValueError, match="equal counts"):
+            gu.add_remaining_self_loops(torch.from_numpy(ei), torch.from_numpy(w), 0.5, 9)
+
+
+def test_utils_softmax_matches_oracle():
+    rng = np.random.default_rng(1)
+    src = rng.standard_normal((2, 100, 3))
+    idx = rng.integers(0, 12, size=(2, 100))
+    got = gu.softmax(torch.from_numpy(src), torch.from_numpy(idx)).numpy()
+    assert np.abs(got - O.edge_softmax(src, idx)).max() < 1e-14
+
+
+# ---------------------------------------------------------------- integrator control logic
+def test_fixed_grid_constructor():
+    t = torch.tensor([0.0, 1.0])
+    assert gode.fixed_grid(t, 0.1).tolist() == pytest.approx(O.fixed_grid(0, 1, 0.1).tolist())
+    assert len(gode.fixed_grid(torch.tensor([0.0, 3.0]), 0.25)) == 13
+
+
+@pytest.mark.parametrize("method,tol", [("euler", 0.02), ("midpoint", 2e-3), ("rk4", 1e-6)])
+def test_fixed_solvers_linear_ode(method, tol):
+    f = lambda t, y: -y  # noqa: E731
+    y0 = torch.ones(4, dtype=torch.float64)
+    out = gode.odeint(f, y0, torch.tensor([0.0, 1.0], dtype=torch.float64), method=method,
+                      options=dict(step_size=0.1), combine=gode._torch_combine)
+    assert out.shape == (2, 4)
+    assert torch.allclose(out[1], torch.full((4,), np.exp(-1.0), dtype=torch.float64), atol=tol)
+
+
+def test_rk4_matches_oracle_integrator():
+    rng = np.random.default_rng(2)
+    A = rng.standard_normal((5, 5)) * 0.3
+    f_np = lambda t, y: y @ A.T  # noqa: E731
+    f_t = lambda t, y: y @ torch.from_numpy(A).T  # noqa: E731
+    y0 = rng.standard_normal(5)
+    want = O.odeint_fixed(f_np, y0, 0.0, 2.0, "rk4", 0.25)
+    got = gode.odeint(f_t, torch.from_numpy(y0), torch.tensor([0.0, 2.0]), method='rk4',
+                      options=dict(step_size=0.25), combine=gode._torch_combine)[1].numpy()
+    assert np.allclose(got, want, rtol=1e-12, atol=1e-12)
+
+
+def test_dopri5_accuracy_and_step_control():
+    f = lambda t, y: -2.0 * y  # noqa: E731
+    y0 = torch.ones(3, dtype=torch.float64)
+    out = gode.odeint(f, y0, torch.tensor([0.0, 0.5, 1.0]), method='dopri5', rtol=1e-9, atol=1e-10,
+                      combine=gode._torch_combine)
+    assert torch.allclose(out[1], torch.full((3,), np.exp(-1.0), dtype=torch.float64), atol=1e-8)
+    assert torch.allclose(out[2], torch.full((3,), np.exp(-2.0), dtype=torch.float64), atol=1e-8)
+    n_tight = gode.odeint.last_n_steps
+    gode.odeint(f, y0, torch.tensor([0.0, 1.0]), method='dopri5', rtol=1e-4, atol=1e-5, combine=gode._torch_combine)
+    assert gode.odeint.last_n_steps < n_tight
+
+
+def test_unknown_method_raises():
+    with pytest.raises(NotImplementedError):
+        gode.odeint(lambda t, y: y, torch.ones(2), torch.tensor([0., 1.]), method='implicit_adams',
+                    combine=gode._torch_combine)
