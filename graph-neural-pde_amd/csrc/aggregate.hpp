@@ -15,76 +15,6 @@ struct PlainWeights {
   __device__ __forceinline__ float operator()(int /*row*/, int p, int /*c*/) const { return w[p]; }
 };
 
-// Scores of one (src, dst) pair for one head (function_transformer_attention.py:246-259).
-__device__ __forceinline__ float pair_score(int mode, const float* __restrict__ qi, const float* __restrict__ kj,
-                                            int dk, float p0, float p1) {
-  if (mode == GNPDE_SCORE_DOT) {
-    float s = 0.f;
-    for (int d = 0; d < dk; ++d) s = fmaf(qi[d], kj[d], s);
-    return s * rsqrtf((float)dk) ;
-  } else if (mode == GNPDE_SCORE_EXP_KERNEL) {
-    float s = 0.f;
-    for (int d = 0; d < dk; ++d) {
-      const float t = qi[d] - kj[d];
-      s = fmaf(t, t, s);
-    }
-    return p0 * p0 * expf(-(s / (2.0f * p1 * p1)));
-  } else {  // cosine / pearson: torch>=1.12 CosineSimilarity, each operand / max(norm, eps)
-    float mq = 0.f, mk = 0.f;
-    if (mode == GNPDE_SCORE_PEARSON) {
-      for (int d = 0; d < dk; ++d) { mq += qi[d]; mk += kj[d]; }
-      mq /= (float)dk;
-      mk /= (float)dk;
-    }
-    float nq = 0.f, nk = 0.f, dot = 0.f;
-    for (int d = 0; d < dk; ++d) {
-      const float a = qi[d] - mq, b = kj[d] - mk;
-      nq = fmaf(a, a, nq);
-      nk = fmaf(b, b, nk);
-      dot = fmaf(a, b, dot);
-    }
-    const float den = fmaxf(sqrtf(nq), 1e-5f) * fmaxf(sqrtf(nk), 1e-5f);
-    return dot / den;
-  }
-}
-
-struct ScoreArgs {
-  int mode;
-  int H;
-  int dk;
-  const double* __restrict__ cs;  // [R,H] reference-mode node scores (fp64)
-  const float* __restrict__ q;    // [R,ldqk] per-edge modes
-  const float* __restrict__ k;
-  int64_t ldqk;
-  float p0, p1;
-
-  // score of edge src->dst, head h, as double (exact for the fp32 modes)
-  __device__ __forceinline__ double score(int src, int dst, int h) const {
-    if (mode == GNPDE_SCORE_REFERENCE) return cs[(int64_t)src * H + h];
-    return (double)pair_score(mode, q + (int64_t)src * ldqk + h * dk, k + (int64_t)dst * ldqk + h * dk, dk, p0, p1);
-  }
-};
-
-// Attention weights: w_e = (1/H) sum_h exp(s_e,h - m[g,h]) * rl[g,h]
-// (utils.softmax :116-127, then attention.mean(dim=2), function_transformer_attention.py:34)
-struct AttnWeights {
-  ScoreArgs sa;
-  int norm_idx;                   // group: 0 = src (row), 1 = dst (col)
-  const double* __restrict__ m;   // [R,H]
-  const float* __restrict__ rl;   // [R,H]
-  float invH;
-  __device__ __forceinline__ float operator()(int row, int /*p*/, int c) const {
-    const int g = norm_idx == 0 ? row : c;
-    float w = 0.f;
-    for (int h = 0; h < sa.H; ++h) {
-      const double s = sa.score(row, c, h);
-      const float z = expf((float)(s - m[(int64_t)g * sa.H + h]));
-      w = fmaf(z, rl[(int64_t)g * sa.H + h], w);
-    }
-    return w * invH;
-  }
-};
-
 // ------------------------------------------------------------------ aggregation kernel
 // Lane layout: lane = g*GL + gl; GROUPS = 64/GL edges are gathered side by side,
 // each by a group of GL lanes covering the C columns with VEC-wide loads
@@ -171,28 +101,44 @@ __global__ __launch_bounds__(256) void agg_kernel(const int4* __restrict__ items
   }
 }
 
-// Hub rows: sum the chunk partials in plan order, then the epilogue.
-template <int VEC>
+// Hub rows: sum the chunk partials, then the epilogue.  GL lanes cover the
+// columns; the 64/GL lane groups take chunks g, g+G, ... and are combined by a
+// fixed xor tree (deterministic).
+template <int VEC, int GL>
 __global__ __launch_bounds__(256) void agg_fixup_kernel(const int4* __restrict__ heavy, int n_heavy, int C, Epi ep,
                                                          const float* __restrict__ partials) {
+  constexpr int G = kWave / GL;
   const int lane = threadIdx.x & 63;
   const int wid = uniform(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
   if (wid >= n_heavy) return;
   const int4 hv = heavy[wid];
   const int row = uniform(hv.x), first = uniform(hv.y), nch = uniform(hv.z);
+  const int g = lane / GL, gl = lane % GL;
   const float a = (ep.flags & GNPDE_EPI_RHS) ? epi_alpha(ep) : 1.f;
   const float b = (ep.flags & GNPDE_ADD_SOURCE) ? *ep.beta : 0.f;
-  for (int cc = lane * VEC; cc < C; cc += kWave * VEC) {
+  for (int c0 = 0; c0 < C; c0 += GL * VEC) {
+    const int cc = c0 + gl * VEC;
+    const bool live = cc < C;
     float s[VEC];
 #pragma unroll
     for (int t = 0; t < VEC; ++t) s[t] = 0.f;
-    for (int c = 0; c < nch; ++c) {
+#pragma unroll 4
+    for (int c = g; c < nch; c += G) {
       float v[VEC];
-      load_vec<VEC>(partials + (int64_t)(first + c) * C + cc, v);
+      if (live) {
+        load_vec<VEC>(partials + (int64_t)(first + c) * C + cc, v);
+      } else {
+#pragma unroll
+        for (int t = 0; t < VEC; ++t) v[t] = 0.f;
+      }
 #pragma unroll
       for (int t = 0; t < VEC; ++t) s[t] += v[t];
     }
-    epilogue_store<VEC>(ep, row, cc, s, a, b);
+#pragma unroll
+    for (int o = GL; o < kWave; o <<= 1)
+#pragma unroll
+      for (int t = 0; t < VEC; ++t) s[t] += __shfl_xor(s[t], o);
+    if (g == 0 && live) epilogue_store<VEC>(ep, row, cc, s, a, b);
   }
 }
 
@@ -206,7 +152,7 @@ static int launch_agg_cfg(const int4* items, int64_t n_items, const int4* heavy,
   }
   if (n_heavy > 0) {
     const int64_t grid = ceil_div(n_heavy, kWavesPerBlock);
-    agg_fixup_kernel<VEC><<<(unsigned)grid, kBlock, 0, s>>>(heavy, (int)n_heavy, C, ep, partials);
+    agg_fixup_kernel<VEC, GL><<<(unsigned)grid, kBlock, 0, s>>>(heavy, (int)n_heavy, C, ep, partials);
     GNPDE_LAUNCH_CHECK();
   }
   return GNPDE_OK;

@@ -73,6 +73,18 @@ __global__ void gather_weights_kernel(const float* __restrict__ w, int64_t nnz, 
   }
 }
 
+// rowidx[p] = r such that rowptr[r] <= p < rowptr[r+1]  (upper_bound - 1)
+__global__ void rowidx_kernel(const int32_t* __restrict__ rowptr, int64_t R, int64_t nnz, int32_t* __restrict__ rowidx) {
+  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < nnz; p += (int64_t)gridDim.x * blockDim.x) {
+    int64_t lo = 0, hi = R;  // find last r with rowptr[r] <= p
+    while (lo < hi) {
+      const int64_t mid = (lo + hi + 1) >> 1;
+      if (rowptr[mid] <= p) lo = mid; else hi = mid - 1;
+    }
+    rowidx[p] = (int32_t)lo;
+  }
+}
+
 __global__ void count_kernel(const int32_t* __restrict__ idx, int64_t n, int32_t* __restrict__ cnt) {
   for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < n; p += (int64_t)gridDim.x * blockDim.x)
     atomicAdd(&cnt[idx[p]], 1);
@@ -190,6 +202,15 @@ int gnpde_gather_weights_f32(const float* w_in, int64_t nnz, int H, const int32_
   if (nnz == 0) return GNPDE_OK;
   GNPDE_REQUIRE(w_in && perm && w_out, GNPDE_EINVAL, "gather_weights: NULL pointer");
   gather_weights_kernel<<<grid_for(nnz), 256, 0, as_stream(stream)>>>(w_in, nnz, H, perm, w_out);
+  GNPDE_LAUNCH_CHECK();
+  return GNPDE_OK;
+}
+
+int gnpde_csr_rowidx(const int32_t* rowptr, int64_t R, int64_t nnz, int32_t* rowidx, void* stream) {
+  GNPDE_REQUIRE(R >= 1 && nnz >= 0, GNPDE_EINVAL, "csr_rowidx: bad sizes");
+  if (nnz == 0) return GNPDE_OK;
+  GNPDE_REQUIRE(rowptr && rowidx, GNPDE_EINVAL, "csr_rowidx: NULL pointer");
+  rowidx_kernel<<<grid_for(nnz), 256, 0, as_stream(stream)>>>(rowptr, R, nnz, rowidx);
   GNPDE_LAUNCH_CHECK();
   return GNPDE_OK;
 }

@@ -1,23 +1,45 @@
 // rhs.hip — per-RHS-evaluation kernels: the Laplacian SpMM RHS (K1), the
-// attention RHS (K3: softmax statistics + weighted aggregation) and the
-// reference-mode key-sum node scores.
+// attention RHS pieces (grouped softmax statistics, edge-parallel head-mean
+// weights, per-edge attention) and the reference-mode key-sum node scores.
 #include "aggregate.hpp"
+#include "scores.hpp"
 
 namespace gnpde {
 
 // ------------------------------------------------------------------ softmax statistics
-// One wavefront per plan item over a grouped CSR (group g = the item's row).
-// Lane per edge; per head an online (max, sum-exp) over 64-edge blocks.
-template <int MAXH>
+// GL lanes per plan item (64/GL items per wavefront).  Every lane keeps an
+// online (max, sum-exp) per head over its strided edges; the GL partial states
+// are merged by a fixed xor tree (deterministic).
+__device__ __forceinline__ void online_push(double& M, float& L, double s) {
+  if (s > M) {
+    L = (M == -INFINITY ? 0.f : L * expf((float)(M - s))) + 1.f;
+    M = s;
+  } else {
+    L += expf((float)(s - M));
+  }
+}
+
+__device__ __forceinline__ void online_merge(double& M, float& L, double M2, float L2) {
+  const double Mn = fmax(M, M2);
+  if (Mn == -INFINITY) return;
+  const float a = (M == -INFINITY) ? 0.f : L * expf((float)(M - Mn));
+  const float b = (M2 == -INFINITY) ? 0.f : L2 * expf((float)(M2 - Mn));
+  L = a + b;
+  M = Mn;
+}
+
+template <int MAXH, int GL>
 __global__ __launch_bounds__(256) void stats_kernel(const int4* __restrict__ items, int n_items,
                                                      const int* __restrict__ gidx, int group_is_dst, ScoreArgs sa,
                                                      double* __restrict__ m_out, float* __restrict__ rl_out,
                                                      double* __restrict__ partials) {
+  constexpr int G = kWave / GL;
   const int lane = threadIdx.x & 63;
-  const int wid = uniform(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
-  if (wid >= n_items) return;
-  const int4 it = items[wid];
-  const int g = uniform(it.x), beg = uniform(it.y), end = uniform(it.z), slot = uniform(it.w);
+  const int g = lane / GL, gl = lane % GL;
+  const int item = (blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * G + g;
+  const bool live = item < n_items;
+  const int4 it = live ? items[item] : make_int4(0, 0, 0, -1);
+  const int grp = it.x, beg = it.y, end = it.z, slot = it.w;
   const int H = sa.H;
   double M[MAXH];
   float L[MAXH];
@@ -26,33 +48,31 @@ __global__ __launch_bounds__(256) void stats_kernel(const int4* __restrict__ ite
     M[h] = -INFINITY;
     L[h] = 0.f;
   }
-  for (int e0 = beg; e0 < end; e0 += kWave) {
-    const int n = min(kWave, end - e0);
-    const bool live = lane < n;
-    const int o = live ? gidx[e0 + lane] : 0;
-    const int src = group_is_dst ? o : g;
-    const int dst = group_is_dst ? g : o;
+  for (int p = beg + gl; p < end; p += GL) {
+    const int o = gidx[p];
+    const int src = group_is_dst ? o : grp;
+    const int dst = group_is_dst ? grp : o;
+#pragma unroll
+    for (int h = 0; h < MAXH; ++h)
+      if (h < H) online_push(M[h], L[h], sa.score(src, dst, h));
+  }
+#pragma unroll
+  for (int o = 1; o < GL; o <<= 1) {
 #pragma unroll
     for (int h = 0; h < MAXH; ++h) {
-      if (h < H) {
-        const double s = live ? sa.score(src, dst, h) : -INFINITY;
-        const double bm = wave_max(s);
-        const double mn = fmax(M[h], bm);
-        const float z = live ? expf((float)(s - mn)) : 0.f;
-        const float bs = wave_sum(z);
-        L[h] = (M[h] == -INFINITY ? 0.f : L[h] * expf((float)(M[h] - mn))) + bs;
-        M[h] = mn;
-      }
+      const double M2 = __shfl_xor(M[h], o);
+      const float L2 = __shfl_xor(L[h], o);
+      online_merge(M[h], L[h], M2, L2);
     }
   }
-  if (lane != 0) return;
+  if (!live || gl != 0) return;
   for (int h = 0; h < H && h < MAXH; ++h) {
     if (slot >= 0) {
       partials[(int64_t)slot * 2 * H + h] = M[h];
       partials[(int64_t)slot * 2 * H + H + h] = (double)L[h];
     } else {
-      m_out[(int64_t)g * H + h] = M[h];
-      rl_out[(int64_t)g * H + h] = 1.0f / (L[h] + kSoftmaxEps);
+      m_out[(int64_t)grp * H + h] = M[h];
+      rl_out[(int64_t)grp * H + h] = 1.0f / (L[h] + kSoftmaxEps);
     }
   }
 }
@@ -67,86 +87,127 @@ __global__ __launch_bounds__(256) void stats_fixup_kernel(const int4* __restrict
   const int4 hv = heavy[i];
   const int g = hv.x, first = hv.y, nch = hv.z;
   double M = -INFINITY;
-  for (int c = 0; c < nch; ++c) M = fmax(M, partials[(int64_t)(first + c) * 2 * H + h]);
   float L = 0.f;
-  for (int c = 0; c < nch; ++c) {
-    const double mc = partials[(int64_t)(first + c) * 2 * H + h];
-    const float lc = (float)partials[(int64_t)(first + c) * 2 * H + H + h];
-    if (mc != -INFINITY) L += lc * expf((float)(mc - M));
-  }
+  for (int c = 0; c < nch; ++c)
+    online_merge(M, L, partials[(int64_t)(first + c) * 2 * H + h], (float)partials[(int64_t)(first + c) * 2 * H + H + h]);
   m_out[(int64_t)g * H + h] = M;
   rl_out[(int64_t)g * H + h] = 1.0f / (L + kSoftmaxEps);
 }
 
-// ------------------------------------------------------------------ per-edge attention (COO order)
-__global__ __launch_bounds__(256) void edge_attention_kernel(const int4* __restrict__ items, int n_items,
-                                                              const int* __restrict__ col,
-                                                              const int* __restrict__ perm, int norm_idx,
-                                                              ScoreArgs sa, const double* __restrict__ m,
-                                                              const float* __restrict__ rl, float* __restrict__ att) {
-  const int lane = threadIdx.x & 63;
-  const int wid = uniform(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
-  if (wid >= n_items) return;
-  const int4 it = items[wid];
-  const int row = uniform(it.x), beg = uniform(it.y), end = uniform(it.z);
+// ------------------------------------------------------------------ edge-parallel weights
+// w[p] = (sum_h exp(s_p,h - m[g,h]) * rl[g,h]) / H   (softmax, then mean over heads)
+__global__ __launch_bounds__(256) void attn_weights_kernel(const int* __restrict__ rowidx, const int* __restrict__ col,
+                                                            int64_t nnz, int norm_idx, ScoreArgs sa,
+                                                            const double* __restrict__ m,
+                                                            const float* __restrict__ rl, float* __restrict__ w) {
   const int H = sa.H;
-  for (int p = beg + lane; p < end; p += kWave) {
-    const int c = col[p];
-    const int g = norm_idx == 0 ? row : c;
+  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < nnz; p += (int64_t)gridDim.x * blockDim.x) {
+    const int r = rowidx[p], c = col[p];
+    const int64_t g = norm_idx == 0 ? r : c;
+    float acc = 0.f;
+    for (int h = 0; h < H; ++h) {
+      const double s = sa.score(r, c, h);
+      acc += expf((float)(s - m[g * H + h])) * rl[g * H + h];
+    }
+    w[p] = acc / (float)H;
+  }
+}
+
+// att[perm[p]*H + h] = exp(s_p,h - m[g,h]) * rl[g,h]   (COO order, per head)
+__global__ __launch_bounds__(256) void edge_attention_kernel(const int* __restrict__ rowidx,
+                                                              const int* __restrict__ col,
+                                                              const int* __restrict__ perm, int64_t nnz,
+                                                              int norm_idx, ScoreArgs sa,
+                                                              const double* __restrict__ m,
+                                                              const float* __restrict__ rl, float* __restrict__ att) {
+  const int H = sa.H;
+  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < nnz; p += (int64_t)gridDim.x * blockDim.x) {
+    const int r = rowidx[p], c = col[p];
+    const int64_t g = norm_idx == 0 ? r : c;
     const int64_t e = perm[p];
     for (int h = 0; h < H; ++h) {
-      const double s = sa.score(row, c, h);
-      att[e * H + h] = expf((float)(s - m[(int64_t)g * H + h])) * rl[(int64_t)g * H + h];
+      const double s = sa.score(r, c, h);
+      att[e * H + h] = expf((float)(s - m[g * H + h])) * rl[g * H + h];
     }
   }
 }
 
 // ------------------------------------------------------------------ reference-mode key sum
-// partial column sums of indeg-weighted x over row tiles, fp64:
-//   part[b][tile][c] = sum_{n in tile} indeg[b*N+n] * x[b*N+n][c];  part[..][C] = sum indeg
-constexpr int kKeysumRows = 128;
-
+// part[b][tile][c] = sum_{n in tile} indeg[b*N+n] * x[b*N+n][c]  (fp64), part[..][C] = sum indeg.
+// TPR threads per row, RPB = 256/TPR rows in flight per block iteration.
+template <int VEC>
 __global__ __launch_bounds__(256) void keysum_partial_kernel(const float* __restrict__ x, int64_t N, int C,
                                                               int64_t ldx, const int* __restrict__ indeg,
-                                                              int ntiles, double* __restrict__ part) {
+                                                              int rows_per_tile, int TPR, int ntiles,
+                                                              double* __restrict__ part) {
+  extern __shared__ __attribute__((aligned(16))) double red[];  // [RPB][C+1]
   const int tile = blockIdx.x, b = blockIdx.y;
-  const int64_t n0 = (int64_t)tile * kKeysumRows;
-  const int64_t n1 = min<int64_t>(N, n0 + kKeysumRows);
+  const int RPB = blockDim.x / TPR;
+  const int rs = threadIdx.x / TPR, t = threadIdx.x % TPR;
+  const int64_t n0 = (int64_t)tile * rows_per_tile;
+  const int64_t n1 = min<int64_t>(N, n0 + rows_per_tile);
+  const int64_t base = (int64_t)b * N;
+  for (int c0 = t * VEC; c0 < C; c0 += TPR * VEC) {
+    double acc[VEC];
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) acc[i] = 0.0;
+#pragma unroll 4
+    for (int64_t n = n0 + rs; n < n1; n += RPB) {
+      const double d = (double)indeg[base + n];
+      float v[VEC];
+      load_vec<VEC>(x + (base + n) * ldx + c0, v);
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) acc[i] = fma(d, (double)v[i], acc[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) red[rs * (C + 1) + c0 + i] = acc[i];
+  }
+  if (t == 0) {
+    double ds = 0.0;
+    for (int64_t n = n0 + rs; n < n1; n += RPB) ds += (double)indeg[base + n];
+    red[rs * (C + 1) + C] = ds;
+  }
+  __syncthreads();
   double* out = part + ((int64_t)b * ntiles + tile) * (C + 1);
   for (int c = threadIdx.x; c <= C; c += blockDim.x) {
     double s = 0.0;
-    for (int64_t n = n0; n < n1; ++n) {
-      const int64_t r = (int64_t)b * N + n;
-      const double d = (double)indeg[r];
-      s += (c < C) ? d * (double)x[r * ldx + c] : d;
-    }
+    for (int r = 0; r < RPB; ++r) s += red[r * (C + 1) + c];
     out[c] = s;
   }
 }
 
-// per batch element: Xbar, S = Wk Xbar + E bk, U[c,h] = sum_{d in h} Wq[d,c] S[d] / sqrt(dk), v[h]
-__global__ __launch_bounds__(256) void keysum_finish_kernel(const double* __restrict__ part, int ntiles, int C,
+// xbar[b][c] = sum over tiles (4 interleaved subsets + fixed-order combine)
+__global__ __launch_bounds__(256) void keysum_tiles_kernel(const double* __restrict__ part, int ntiles, int C,
+                                                            double* __restrict__ xbar) {
+  __shared__ double red[4][64];
+  const int b = blockIdx.y;
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int sub = threadIdx.x >> 6;
+  double s = 0.0;
+  if (c <= C)
+    for (int t = sub; t < ntiles; t += 4) s += part[((int64_t)b * ntiles + t) * (C + 1) + c];
+  red[sub][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (sub == 0 && c <= C) xbar[(int64_t)b * (C + 1) + c] = ((red[0][c & 63] + red[1][c & 63]) + red[2][c & 63]) +
+                                                         red[3][c & 63];
+}
+
+// per batch element: S = Wk xbar + E bk;  U[c,h] = sum_{d in h} Wq[d,c] S[d] / sqrt(dk);  v[h] = bq_h . S_h / sqrt(dk)
+__global__ __launch_bounds__(256) void keysum_finish_kernel(const double* __restrict__ xbar, int C,
                                                              const float* __restrict__ Wq,
                                                              const float* __restrict__ bq,
                                                              const float* __restrict__ Wk,
                                                              const float* __restrict__ bk, int att, int H,
                                                              double* __restrict__ U, double* __restrict__ v) {
-  extern __shared__ __attribute__((aligned(16))) double sm[];
-  double* xbar = sm;             // C+1
-  double* S = sm + (C + 1);      // att
+  extern __shared__ __attribute__((aligned(16))) double S[];  // att
   const int b = blockIdx.x;
-  const double* pb = part + (int64_t)b * ntiles * (C + 1);
-  for (int c = threadIdx.x; c <= C; c += blockDim.x) {
+  const double* xb = xbar + (int64_t)b * (C + 1);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int d = wv; d < att; d += kWavesPerBlock) {
     double s = 0.0;
-    for (int t = 0; t < ntiles; ++t) s += pb[(int64_t)t * (C + 1) + c];
-    xbar[c] = s;
-  }
-  __syncthreads();
-  const double esum = xbar[C];
-  for (int d = threadIdx.x; d < att; d += blockDim.x) {
-    double s = esum * (double)bk[d];
-    for (int c = 0; c < C; ++c) s += (double)Wk[(int64_t)d * C + c] * xbar[c];
-    S[d] = s;
+    for (int c = lane; c < C; c += kWave) s = fma((double)Wk[(int64_t)d * C + c], xb[c], s);
+    s = wave_sum(s);
+    if (lane == 0) S[d] = s + xb[C] * (double)bk[d];
   }
   __syncthreads();
   const int dk = att / H;
@@ -154,53 +215,65 @@ __global__ __launch_bounds__(256) void keysum_finish_kernel(const double* __rest
   for (int t = threadIdx.x; t < C * H; t += blockDim.x) {
     const int c = t / H, h = t - c * H;
     double s = 0.0;
-    for (int d = h * dk; d < (h + 1) * dk; ++d) s += (double)Wq[(int64_t)d * C + c] * S[d];
+    for (int d = h * dk; d < (h + 1) * dk; ++d) s = fma((double)Wq[(int64_t)d * C + c], S[d], s);
     U[((int64_t)b * C + c) * H + h] = s * inv;
   }
   for (int h = threadIdx.x; h < H; h += blockDim.x) {
     double s = 0.0;
-    for (int d = h * dk; d < (h + 1) * dk; ++d) s += (double)bq[d] * S[d];
+    for (int d = h * dk; d < (h + 1) * dk; ++d) s = fma((double)bq[d], S[d], s);
     v[(int64_t)b * H + h] = s * inv;
   }
 }
 
-// cs[r,h] = x_r . U[b,:,h] + v[b,h]  (fp64), one wavefront per row
-template <int MAXH>
+// cs[r,h] = x_r . U[b,:,h] + v[b,h]  (fp64 accumulation), GL lanes per row
+template <int VEC, int GL, int MAXH>
 __global__ __launch_bounds__(256) void node_scores_kernel(const float* __restrict__ x, int64_t R, int64_t N, int C,
                                                            int64_t ldx, int H, const double* __restrict__ U,
                                                            const double* __restrict__ v, double* __restrict__ cs) {
+  constexpr int G = kWave / GL;
   const int lane = threadIdx.x & 63;
-  const int64_t nw = (int64_t)gridDim.x * kWavesPerBlock;
-  for (int64_t r = uniform(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)); r < R; r += nw) {
-    const int64_t b = r / N;
+  const int g = lane / GL, gl = lane % GL;
+  const int64_t nrows_step = (int64_t)gridDim.x * kWavesPerBlock * G;
+  for (int64_t r0 = (int64_t)(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * G; r0 < R; r0 += nrows_step) {
+    const int64_t r = r0 + g;
+    const bool live = r < R;
+    const int64_t rr = live ? r : R - 1;
+    const int64_t b = rr / N;
     double acc[MAXH];
 #pragma unroll
     for (int h = 0; h < MAXH; ++h) acc[h] = 0.0;
-    for (int c = lane; c < C; c += kWave) {
-      const double xv = (double)x[r * ldx + c];
-      const double* u = U + (b * C + c) * H;
+    for (int c0 = gl * VEC; c0 < C; c0 += GL * VEC) {
+      float xv[VEC];
+      load_vec<VEC>(x + rr * ldx + c0, xv);
 #pragma unroll
-      for (int h = 0; h < MAXH; ++h)
-        if (h < H) acc[h] = fma(xv, u[h], acc[h]);
+      for (int i = 0; i < VEC; ++i) {
+        const double* u = U + (b * C + c0 + i) * H;
+#pragma unroll
+        for (int h = 0; h < MAXH; ++h)
+          if (h < H) acc[h] = fma((double)xv[i], u[h], acc[h]);
+      }
     }
 #pragma unroll
-    for (int h = 0; h < MAXH; ++h) {
-      if (h < H) {
-        const double s = wave_sum(acc[h]);
-        if (lane == 0) cs[r * H + h] = s + v[b * H + h];
-      }
+    for (int o = 1; o < GL; o <<= 1)
+#pragma unroll
+      for (int h = 0; h < MAXH; ++h) acc[h] += __shfl_xor(acc[h], o);
+    if (live && gl == 0) {
+#pragma unroll
+      for (int h = 0; h < MAXH; ++h)
+        if (h < H) cs[r * H + h] = acc[h] + v[b * H + h];
     }
   }
 }
 
+// ------------------------------------------------------------------ host helpers
 static int check_score_args(int mode, int64_t heads, int64_t dk, const double* cs, const float* q, const float* k) {
   GNPDE_REQUIRE(heads >= 1 && heads <= 16, GNPDE_EUNSUPPORTED, "attention: heads=%lld not in [1,16]",
                 (long long)heads);
-  GNPDE_REQUIRE(mode >= GNPDE_SCORE_REFERENCE && mode <= GNPDE_SCORE_PEARSON, GNPDE_EINVAL,
+  GNPDE_REQUIRE(mode >= GNPDE_SCORE_REFERENCE && mode <= GNPDE_SCORE_UNIFORM, GNPDE_EINVAL,
                 "attention: unknown score mode %d", mode);
   if (mode == GNPDE_SCORE_REFERENCE) {
     GNPDE_REQUIRE(cs != nullptr, GNPDE_EINVAL, "attention: reference mode needs cs");
-  } else {
+  } else if (mode != GNPDE_SCORE_UNIFORM) {
     GNPDE_REQUIRE(q != nullptr && k != nullptr && dk >= 1, GNPDE_EINVAL, "attention: per-edge mode needs q, k, dk");
   }
   return GNPDE_OK;
@@ -249,6 +322,65 @@ static int check_epi(const Epi& e, int64_t C, int64_t n_heavy, const void* parti
   return GNPDE_OK;
 }
 
+static int pow2_at_least(int v, int cap) {
+  int p = 1;
+  while (p < v && p < cap) p <<= 1;
+  return p;
+}
+
+constexpr int kKeysumTilesTarget = 1024;
+
+static int keysum_vec(int64_t C, const float* x, int64_t ldx) {
+  if (C % 4 == 0 && ldx % 4 == 0 && aligned16(x)) return 4;
+  if (C % 2 == 0 && ldx % 2 == 0 && aligned8(x)) return 2;
+  return 1;
+}
+
+// tiles of rows for the partial column sums (independent of the vector width)
+static void keysum_tiles(int64_t B, int64_t N, int* rows_per_tile, int* ntiles) {
+  const int64_t per_batch = std::max<int64_t>(1, kKeysumTilesTarget / B);
+  const int64_t rpt = std::max<int64_t>(ceil_div(N, per_batch), 1);
+  *rows_per_tile = (int)rpt;
+  *ntiles = (int)ceil_div(N, rpt);
+}
+
+template <int MAXH>
+static void launch_stats(unsigned grid, int GL, hipStream_t s, const int4* it, int n, const int* gidx, int gid,
+                         const ScoreArgs& sa, double* m, float* rl, double* partials) {
+  if (GL == 8)
+    stats_kernel<MAXH, 8><<<grid, kBlock, 0, s>>>(it, n, gidx, gid, sa, m, rl, partials);
+  else
+    stats_kernel<MAXH, 64><<<grid, kBlock, 0, s>>>(it, n, gidx, gid, sa, m, rl, partials);
+}
+
+template <int VEC, int GL>
+static void launch_node_scores(unsigned grid, hipStream_t s, const float* x, int64_t R, int64_t N, int C, int64_t ldx,
+                               int H, const double* U, const double* v, double* cs) {
+  if (H <= 1)
+    node_scores_kernel<VEC, GL, 1><<<grid, kBlock, 0, s>>>(x, R, N, C, ldx, H, U, v, cs);
+  else if (H <= 2)
+    node_scores_kernel<VEC, GL, 2><<<grid, kBlock, 0, s>>>(x, R, N, C, ldx, H, U, v, cs);
+  else if (H <= 4)
+    node_scores_kernel<VEC, GL, 4><<<grid, kBlock, 0, s>>>(x, R, N, C, ldx, H, U, v, cs);
+  else if (H <= 8)
+    node_scores_kernel<VEC, GL, 8><<<grid, kBlock, 0, s>>>(x, R, N, C, ldx, H, U, v, cs);
+  else
+    node_scores_kernel<VEC, GL, 16><<<grid, kBlock, 0, s>>>(x, R, N, C, ldx, H, U, v, cs);
+}
+
+template <int VEC>
+static void launch_node_scores_vec(unsigned grid, int GL, hipStream_t s, const float* x, int64_t R, int64_t N, int C,
+                                   int64_t ldx, int H, const double* U, const double* v, double* cs) {
+  if (GL <= 8)
+    launch_node_scores<VEC, 8>(grid, s, x, R, N, C, ldx, H, U, v, cs);
+  else if (GL <= 16)
+    launch_node_scores<VEC, 16>(grid, s, x, R, N, C, ldx, H, U, v, cs);
+  else if (GL <= 32)
+    launch_node_scores<VEC, 32>(grid, s, x, R, N, C, ldx, H, U, v, cs);
+  else
+    launch_node_scores<VEC, 64>(grid, s, x, R, N, C, ldx, H, U, v, cs);
+}
+
 }  // namespace gnpde
 
 using namespace gnpde;
@@ -281,17 +413,18 @@ int gnpde_softmax_stats_f32(const int32_t* items, int64_t n_items, const int32_t
   const ScoreArgs sa = make_score_args(mode, heads, dk, cs, q, k, ldqk, score_p0, score_p1);
   hipStream_t s = as_stream(stream);
   const int4* it = reinterpret_cast<const int4*>(items);
-  const unsigned grid = (unsigned)ceil_div(n_items, kWavesPerBlock);
+  const int GL = 8;  // lanes per item
+  const unsigned grid = (unsigned)ceil_div(n_items, (int64_t)kWavesPerBlock * (kWave / GL));
   if (heads <= 1)
-    stats_kernel<1><<<grid, kBlock, 0, s>>>(it, (int)n_items, gidx, group_is_dst, sa, m, rl, partials);
+    launch_stats<1>(grid, GL, s, it, (int)n_items, gidx, group_is_dst, sa, m, rl, partials);
   else if (heads <= 2)
-    stats_kernel<2><<<grid, kBlock, 0, s>>>(it, (int)n_items, gidx, group_is_dst, sa, m, rl, partials);
+    launch_stats<2>(grid, GL, s, it, (int)n_items, gidx, group_is_dst, sa, m, rl, partials);
   else if (heads <= 4)
-    stats_kernel<4><<<grid, kBlock, 0, s>>>(it, (int)n_items, gidx, group_is_dst, sa, m, rl, partials);
+    launch_stats<4>(grid, GL, s, it, (int)n_items, gidx, group_is_dst, sa, m, rl, partials);
   else if (heads <= 8)
-    stats_kernel<8><<<grid, kBlock, 0, s>>>(it, (int)n_items, gidx, group_is_dst, sa, m, rl, partials);
+    launch_stats<8>(grid, GL, s, it, (int)n_items, gidx, group_is_dst, sa, m, rl, partials);
   else
-    stats_kernel<16><<<grid, kBlock, 0, s>>>(it, (int)n_items, gidx, group_is_dst, sa, m, rl, partials);
+    launch_stats<16>(grid, GL, s, it, (int)n_items, gidx, group_is_dst, sa, m, rl, partials);
   GNPDE_LAUNCH_CHECK();
   if (n_heavy > 0) {
     const unsigned g2 = (unsigned)ceil_div(n_heavy * heads, kBlock);
@@ -302,51 +435,45 @@ int gnpde_softmax_stats_f32(const int32_t* items, int64_t n_items, const int32_t
   return GNPDE_OK;
 }
 
-int gnpde_attn_rhs_f32(const int32_t* items, int64_t n_items, const int32_t* heavy, int64_t n_heavy,
-                       const int32_t* col, int norm_idx, int mode, int64_t heads, int64_t dk, const double* cs,
-                       const float* q, const float* k, int64_t ldqk, float score_p0, float score_p1, const double* m,
-                       const float* rl, int64_t C, const float* x, int64_t ldx, const float* x0, int64_t ldx0,
-                       const float* alpha, const float* beta, int flags, float* f, int64_t ldf, float* partials,
-                       void* stream) {
+static unsigned edge_grid(int64_t nnz) { return (unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(nnz, kBlock), 16384)); }
+
+int gnpde_attn_weights_f32(const int32_t* rowidx, const int32_t* col, int64_t nnz, int norm_idx, int mode,
+                           int64_t heads, int64_t dk, const double* cs, const float* q, const float* k, int64_t ldqk,
+                           float score_p0, float score_p1, const double* m, const float* rl, float* w_out,
+                           void* stream) {
   int rc = check_score_args(mode, heads, dk, cs, q, k);
   if (rc) return rc;
-  const Epi ep = make_epi(x, ldx, x0, ldx0, alpha, beta, flags, f, ldf);
-  rc = check_epi(ep, C, n_heavy, partials);
-  if (rc) return rc;
-  GNPDE_REQUIRE(norm_idx == 0 || norm_idx == 1, GNPDE_EINVAL, "attn_rhs: norm_idx must be 0 or 1");
-  GNPDE_REQUIRE(m && rl, GNPDE_EINVAL, "attn_rhs: NULL m/rl");
-  GNPDE_REQUIRE(n_items == 0 || (items && col), GNPDE_EINVAL, "attn_rhs: NULL plan/col");
-  AttnWeights wp;
-  wp.sa = make_score_args(mode, heads, dk, cs, q, k, ldqk, score_p0, score_p1);
-  wp.norm_idx = norm_idx;
-  wp.m = m;
-  wp.rl = rl;
-  wp.invH = 1.0f / (float)heads;
-  return launch_agg(items, n_items, heavy, n_heavy, col, wp, C, ep, partials, as_stream(stream));
+  GNPDE_REQUIRE(norm_idx == 0 || norm_idx == 1, GNPDE_EINVAL, "attn_weights: norm_idx must be 0 or 1");
+  if (nnz == 0) return GNPDE_OK;
+  GNPDE_REQUIRE(rowidx && col && m && rl && w_out, GNPDE_EINVAL, "attn_weights: NULL pointer");
+  const ScoreArgs sa = make_score_args(mode, heads, dk, cs, q, k, ldqk, score_p0, score_p1);
+  attn_weights_kernel<<<edge_grid(nnz), kBlock, 0, as_stream(stream)>>>(rowidx, col, nnz, norm_idx, sa, m, rl, w_out);
+  GNPDE_LAUNCH_CHECK();
+  return GNPDE_OK;
 }
 
-int gnpde_edge_attention_f32(const int32_t* items, int64_t n_items, const int32_t* col, const int32_t* perm,
+int gnpde_edge_attention_f32(const int32_t* rowidx, const int32_t* col, const int32_t* perm, int64_t nnz,
                              int norm_idx, int mode, int64_t heads, int64_t dk, const double* cs, const float* q,
                              const float* k, int64_t ldqk, float score_p0, float score_p1, const double* m,
                              const float* rl, float* att, void* stream) {
   int rc = check_score_args(mode, heads, dk, cs, q, k);
   if (rc) return rc;
   GNPDE_REQUIRE(norm_idx == 0 || norm_idx == 1, GNPDE_EINVAL, "edge_attention: norm_idx must be 0 or 1");
-  if (n_items == 0) return GNPDE_OK;
-  GNPDE_REQUIRE(items && col && perm && m && rl && att, GNPDE_EINVAL, "edge_attention: NULL pointer");
+  if (nnz == 0) return GNPDE_OK;
+  GNPDE_REQUIRE(rowidx && col && perm && m && rl && att, GNPDE_EINVAL, "edge_attention: NULL pointer");
   const ScoreArgs sa = make_score_args(mode, heads, dk, cs, q, k, ldqk, score_p0, score_p1);
-  const unsigned grid = (unsigned)ceil_div(n_items, kWavesPerBlock);
-  edge_attention_kernel<<<grid, kBlock, 0, as_stream(stream)>>>(reinterpret_cast<const int4*>(items), (int)n_items,
-                                                                col, perm, norm_idx, sa, m, rl, att);
+  edge_attention_kernel<<<edge_grid(nnz), kBlock, 0, as_stream(stream)>>>(rowidx, col, perm, nnz, norm_idx, sa, m,
+                                                                          rl, att);
   GNPDE_LAUNCH_CHECK();
   return GNPDE_OK;
 }
 
 size_t gnpde_keysum_workspace_bytes(int64_t B, int64_t N, int64_t C, int64_t att) {
   (void)att;
-  const int64_t ntiles = ceil_div(N, kKeysumRows);
+  int rpt, ntiles;
+  keysum_tiles(B, N, &rpt, &ntiles);
   const int64_t H = 16;  // upper bound on heads
-  return sizeof(double) * (size_t)(B * ntiles * (C + 1) + B * C * H + B * H) + 256;
+  return sizeof(double) * (size_t)(B * ntiles * (C + 1) + B * (C + 1) + B * C * H + B * H) + 256;
 }
 
 int gnpde_ref_scores_f32(const float* x, int64_t B, int64_t N, int64_t C, int64_t ldx, const int32_t* indeg,
@@ -358,30 +485,42 @@ int gnpde_ref_scores_f32(const float* x, int64_t B, int64_t N, int64_t C, int64_
                 "ref_scores: heads must divide attention_dim and be <= 16");
   GNPDE_REQUIRE(workspace_bytes >= gnpde_keysum_workspace_bytes(B, N, C, att), GNPDE_EINVAL,
                 "ref_scores: workspace too small");
-  GNPDE_REQUIRE(C + 1 + att <= 6000, GNPDE_EUNSUPPORTED, "ref_scores: C + attention_dim too large");
+  GNPDE_REQUIRE(att <= 8192, GNPDE_EUNSUPPORTED, "ref_scores: attention_dim too large");
   hipStream_t s = as_stream(stream);
-  const int ntiles = (int)ceil_div(N, kKeysumRows);
+  const int vec = keysum_vec(C, x, ldx);
+  const int tpr = pow2_at_least((int)ceil_div(C, vec), 256);
+  int rpt, ntiles;
+  keysum_tiles(B, N, &rpt, &ntiles);
   double* part = static_cast<double*>(workspace);
-  double* U = part + B * ntiles * (C + 1);
+  double* xbar = part + B * ntiles * (C + 1);
+  double* U = xbar + B * (C + 1);
   double* v = U + B * C * heads;
-  keysum_partial_kernel<<<dim3(ntiles, (unsigned)B), kBlock, 0, s>>>(x, N, (int)C, ldx, indeg, ntiles, part);
+  const int rpb = kBlock / tpr;
+  const size_t shm = sizeof(double) * (size_t)rpb * (C + 1);
+  GNPDE_REQUIRE(shm <= 64 * 1024, GNPDE_EUNSUPPORTED, "ref_scores: C too large");
+  const dim3 g1((unsigned)ntiles, (unsigned)B);
+  if (vec == 4)
+    keysum_partial_kernel<4><<<g1, kBlock, shm, s>>>(x, N, (int)C, ldx, indeg, rpt, tpr, ntiles, part);
+  else if (vec == 2)
+    keysum_partial_kernel<2><<<g1, kBlock, shm, s>>>(x, N, (int)C, ldx, indeg, rpt, tpr, ntiles, part);
+  else
+    keysum_partial_kernel<1><<<g1, kBlock, shm, s>>>(x, N, (int)C, ldx, indeg, rpt, tpr, ntiles, part);
   GNPDE_LAUNCH_CHECK();
-  const size_t shm = sizeof(double) * (size_t)(C + 1 + att);
-  keysum_finish_kernel<<<(unsigned)B, kBlock, shm, s>>>(part, ntiles, (int)C, Wq, bq, Wk, bk, (int)att, (int)heads,
-                                                        U, v);
+  keysum_tiles_kernel<<<dim3((unsigned)ceil_div(C + 1, 64), (unsigned)B), kBlock, 0, s>>>(part, ntiles, (int)C, xbar);
+  GNPDE_LAUNCH_CHECK();
+  keysum_finish_kernel<<<(unsigned)B, kBlock, sizeof(double) * (size_t)att, s>>>(xbar, (int)C, Wq, bq, Wk, bk, (int)att,
+                                                                               (int)heads, U, v);
   GNPDE_LAUNCH_CHECK();
   const int64_t R = B * N;
-  const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(R, kWavesPerBlock), 8192);
-  if (heads <= 1)
-    node_scores_kernel<1><<<grid, kBlock, 0, s>>>(x, R, N, (int)C, ldx, (int)heads, U, v, cs);
-  else if (heads <= 2)
-    node_scores_kernel<2><<<grid, kBlock, 0, s>>>(x, R, N, (int)C, ldx, (int)heads, U, v, cs);
-  else if (heads <= 4)
-    node_scores_kernel<4><<<grid, kBlock, 0, s>>>(x, R, N, (int)C, ldx, (int)heads, U, v, cs);
-  else if (heads <= 8)
-    node_scores_kernel<8><<<grid, kBlock, 0, s>>>(x, R, N, (int)C, ldx, (int)heads, U, v, cs);
+  const int GL = std::min(64, pow2_at_least((int)ceil_div(C, vec), 64));
+  const int rows_per_block = kWavesPerBlock * (kWave / std::max(GL, 8));
+  const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(R, rows_per_block), 8192);
+  if (vec == 4)
+    launch_node_scores_vec<4>(grid, GL, s, x, R, N, (int)C, ldx, (int)heads, U, v, cs);
+  else if (vec == 2)
+    launch_node_scores_vec<2>(grid, GL, s, x, R, N, (int)C, ldx, (int)heads, U, v, cs);
   else
-    node_scores_kernel<16><<<grid, kBlock, 0, s>>>(x, R, N, (int)C, ldx, (int)heads, U, v, cs);
+    launch_node_scores_vec<1>(grid, GL, s, x, R, N, (int)C, ldx, (int)heads, U, v, cs);
   GNPDE_LAUNCH_CHECK();
   return GNPDE_OK;
 }

@@ -41,10 +41,11 @@ SIGNATURES = {
                                     _size, _vp]),
     "gnpde_softmax_stats_f32": (_int, [_vp, _i64, _vp, _i64, _vp, _int, _int, _i64, _i64, _vp, _vp, _vp, _i64, _f32,
                                        _f32, _vp, _vp, _vp, _vp]),
-    "gnpde_attn_rhs_f32": (_int, [_vp, _i64, _vp, _i64, _vp, _int, _int, _i64, _i64, _vp, _vp, _vp, _i64, _f32, _f32,
-                                  _vp, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _int, _vp, _i64, _vp, _vp]),
-    "gnpde_edge_attention_f32": (_int, [_vp, _i64, _vp, _vp, _int, _int, _i64, _i64, _vp, _vp, _vp, _i64, _f32, _f32,
+    "gnpde_attn_weights_f32": (_int, [_vp, _vp, _i64, _int, _int, _i64, _i64, _vp, _vp, _vp, _i64, _f32, _f32, _vp,
+                                      _vp, _vp, _vp]),
+    "gnpde_edge_attention_f32": (_int, [_vp, _vp, _vp, _i64, _int, _int, _i64, _i64, _vp, _vp, _vp, _i64, _f32, _f32,
                                         _vp, _vp, _vp, _vp]),
+    "gnpde_csr_rowidx": (_int, [_vp, _i64, _i64, _vp, _vp]),
     "gnpde_rk_combine_f32": (_int, [_i64, _vp, _int, ctypes.POINTER(_vp), ctypes.POINTER(_f64), _f64, _vp, _vp]),
 }
 
@@ -59,6 +60,7 @@ SCORE_DOT = 1
 SCORE_EXP_KERNEL = 2
 SCORE_COSINE = 3
 SCORE_PEARSON = 4
+SCORE_UNIFORM = 5
 
 _lock = threading.Lock()
 _lib = None

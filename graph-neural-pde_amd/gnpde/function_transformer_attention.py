@@ -14,8 +14,10 @@ head-mean attention into [B,N,N] for a dense matmul.  Here one RHS is:
    kernel (gnpde_linear_f32);
 2. grouped softmax statistics (max, 1/sum-exp) per source (norm_idx 0) or
    destination (norm_idx 1) node (gnpde_softmax_stats_f32);
-3. weighted aggregation with the head-mean weights recomputed on the fly and
-   the RHS epilogue fused (gnpde_attn_rhs_f32).
+3. edge-parallel head-mean weights (gnpde_attn_weights_f32), then the K1
+   gather-aggregate with the RHS epilogue fused (gnpde_spmm_rhs_f32).  With
+   the fork scaled_dot and norm_idx 0 every score of a source group is equal,
+   so the weights are 1/outdeg for any x: computed once per graph.
 
 V and Wout are dead when ``mix_features=False`` (:33-41) and are never
 computed; the parameters exist for state_dict compatibility.  Settings the
@@ -46,6 +48,12 @@ def _check_supported(opt):
     if opt.get('beltrami', False) and opt.get('attention_type', 'scaled_dot') == 'exp_kernel':
         raise NotImplementedError("gnpde: the beltrami exp_kernel branch slices nodes instead of features in the "
                                   "reference (:166-167) and is not implemented")
+
+
+def _check_inference(module):
+    if module.training and torch.is_grad_enabled():
+        raise NotImplementedError("gnpde: attention backward kernels are SURVEY §8(f) next-1; use eval mode or "
+                                  "torch.no_grad()")
 
 
 class SpGraphTransAttentionLayer(nn.Module):
@@ -80,6 +88,7 @@ class SpGraphTransAttentionLayer(nn.Module):
         self.init_weights(self.Wout)
         self._graph = None
         self._graph_key = None
+        self._uniform = None  # (graph, NodeScores, m, rl, csr weights) for the uniform fast path
 
     def init_weights(self, m):
         """Constant 1e-5 init (:153-157)."""
@@ -104,10 +113,30 @@ class SpGraphTransAttentionLayer(nn.Module):
             self._graph_key = key
         return self._graph
 
+    def is_uniform(self, norm_idx):
+        """Fork scaled_dot + source-grouped softmax: all scores of a group are equal,
+        so the attention is 1/outdeg whatever x — graph-only, cached."""
+        return (self.score_mode == 'reference' and norm_idx == 0 and
+                self.opt.get('attention_type', 'scaled_dot') == 'scaled_dot')
+
+    def scores_and_stats(self, g, x, norm_idx):
+        """(NodeScores, m, rl) for this RHS evaluation."""
+        if self.is_uniform(norm_idx):
+            if self._uniform is None or self._uniform[0] is not g:
+                ns = ops.uniform_scores(self.h)
+                m, rl = ops.softmax_stats(g, ns, 0)
+                self._uniform = (g, ns, m, rl, ops.attn_weights(g, ns, m, rl, 0))
+            return self._uniform[1:4]
+        ns = self.node_scores(g, x)
+        m, rl = ops.softmax_stats(g, ns, norm_idx)
+        return ns, m, rl
+
+    def uniform_weights(self, g):
+        self.scores_and_stats(g, None, 0)
+        return self._uniform[4]
+
     def node_scores(self, g, x):
-        if self.training and torch.is_grad_enabled():
-            raise NotImplementedError("gnpde: attention backward kernels are SURVEY §8(f) next-1; use eval mode "
-                                      "or torch.no_grad()")
+        _check_inference(self)
         p0, p1 = self._score_params()
         return ops.node_scores(g, x, self.Q.weight.detach(), self.Q.bias.detach(), self.K.weight.detach(),
                                self.K.bias.detach(), self.h, self.opt.get('attention_type', 'scaled_dot'),
@@ -118,9 +147,8 @@ class SpGraphTransAttentionLayer(nn.Module):
         attention of :265-266 in COO order.  ``values`` (V(x), prods) is not
         materialised (dead for mix_features=False)."""
         g = self.graph_for(x, edge)
-        ns = self.node_scores(g, x)
         norm_idx = int(self.opt['attention_norm_idx'])
-        m, rl = ops.softmax_stats(g, ns, norm_idx)
+        ns, m, rl = self.scores_and_stats(g, x, norm_idx)
         return ops.edge_attention(g, ns, m, rl, norm_idx), (None, None)
 
     def __repr__(self):
@@ -150,17 +178,19 @@ class ODEFuncTransformerAtt(ODEFunc):
         if self.nfe > self.opt["max_nfe"]:
             raise MaxNFEException
         self.nfe += 1
+        _check_inference(self)
         g = self.graph_for(x)
         lay = self.multihead_att_layer
-        ns = lay.node_scores(g, x)
         norm_idx = int(self.opt['attention_norm_idx'])
-        m, rl = ops.softmax_stats(g, ns, norm_idx)
         add_source = bool(self.opt.get('add_source', False))
         if add_source and self.x0 is None:
             raise RuntimeError("ODEFuncTransformerAtt: add_source needs x0 (ODEblock.set_x0)")
-        return ops.attn_rhs(g, ns, m, rl, norm_idx, x, x0=self.x0 if add_source else None,
-                            alpha=self.alpha_train.detach(), beta=self.beta_train.detach(), rhs=True,
-                            alpha_sigmoid=not self.opt.get('no_alpha_sigmoid', False), add_source=add_source)
+        kw = dict(x0=self.x0 if add_source else None, alpha=self.alpha_train.detach(), beta=self.beta_train.detach(),
+                  rhs=True, alpha_sigmoid=not self.opt.get('no_alpha_sigmoid', False), add_source=add_source)
+        if lay.is_uniform(norm_idx):
+            return ops.spmm_rhs(g, lay.uniform_weights(g), x, **kw)
+        ns, m, rl = lay.scores_and_stats(g, x, norm_idx)
+        return ops.attn_rhs(g, ns, m, rl, norm_idx, x, **kw)
 
     def __repr__(self):
         return self.__class__.__name__ + ' (' + str(self.in_features) + ' -> ' + str(self.out_features) + ')'

@@ -16,6 +16,7 @@ import torch
 from . import _lib
 
 DEFAULT_CHUNK = 256  # hub-splitting threshold (edges per wavefront work item)
+STATS_CHUNK = 64     # items of the softmax-statistics kernel (8 lanes per item)
 
 
 def _ptr(t):
@@ -60,6 +61,24 @@ class GroupedCSR(object):
     def __init__(self, rowptr, col, perm, R, nnz, key_row, plan):
         self.rowptr, self.col, self.perm = rowptr, col, perm
         self.R, self.nnz, self.key_row, self.plan = R, nnz, key_row, plan
+        self._rowidx = None
+        self._stats_plan = None
+
+    @property
+    def rowidx(self):
+        """Row of every CSR position (edge-parallel kernels)."""
+        if self._rowidx is None:
+            ri = torch.empty(max(self.nnz, 1), dtype=torch.int32, device=self.rowptr.device)
+            _lib.call("gnpde_csr_rowidx", _ptr(self.rowptr), self.R, self.nnz, _ptr(ri), _stream(ri.device))
+            self._rowidx = ri
+        return self._rowidx
+
+    @property
+    def stats_plan(self):
+        """Plan with small chunks for the 8-lanes-per-group statistics kernel."""
+        if self._stats_plan is None:
+            self._stats_plan = build_plan(self.rowptr, self.R, self.nnz, STATS_CHUNK)
+        return self._stats_plan
 
 
 def validate_edge_index(edge_index, num_nodes):
@@ -277,10 +296,19 @@ def node_scores(g, x, Wq, bq, Wk, bk, heads, attention_type='scaled_dot', score_
     return NodeScores(mode, heads, dk, q=q, k=k, p0=output_var, p1=lengthscale)
 
 
+def uniform_scores(heads):
+    """Source-grouped softmax of the fork's scaled_dot: every score of a source
+    row is q_i . S / sqrt(dk), identical within the group, so softmax gives
+    exp(0)/(outdeg + 1e-16) whatever x, Q and K are.  The
+    weights depend on the graph only and are computed once per graph."""
+    return NodeScores(_lib.SCORE_UNIFORM, heads, 1)
+
+
 def softmax_stats(g, ns, norm_idx):
-    """m, rl [R,h]: per-group max and reciprocal sum-exp (utils.softmax, src/utils.py:116-127)."""
+    """m [R,h] fp64, rl [R,h]: per-group max and 1/(sum-exp + 1e-16)
+    (utils.softmax, src/utils.py:116-127)."""
     grouped = g.csr if norm_idx == 0 else g.csc
-    plan = grouped.plan
+    plan = grouped.stats_plan
     dev = grouped.col.device
     H = ns.heads
     m = torch.empty(g.R, H, dtype=torch.float64, device=dev)
@@ -292,35 +320,32 @@ def softmax_stats(g, ns, norm_idx):
     return m, rl
 
 
+def attn_weights(g, ns, m, rl, norm_idx):
+    """Head-mean softmax weights in aggregation-CSR order [nnz]."""
+    dev = g.csr.col.device
+    w = torch.empty(max(g.nnz, 1), dtype=torch.float32, device=dev)
+    _lib.call("gnpde_attn_weights_f32", _ptr(g.csr.rowidx), _ptr(g.csr.col), g.nnz, int(norm_idx), ns.mode, ns.heads,
+              ns.dk, _ptr(ns.cs), _ptr(ns.q), _ptr(ns.k), ns.ldqk, ns.p0, ns.p1, _ptr(m), _ptr(rl), _ptr(w),
+              _stream(dev))
+    return w
+
+
 def attn_rhs(g, ns, m, rl, norm_idx, x, x0=None, alpha=None, beta=None, rhs=True, alpha_sigmoid=True,
              add_source=False, out=None):
-    """K3 aggregation: f = a*(A_att x - x) [+ b x0], A_att = head-mean softmax weights."""
-    shape = x.shape
-    xr = _rows(x, "x")
-    C = xr.shape[1]
-    dev = xr.device
-    a = _scalar(alpha, "alpha", dev) if rhs else None
-    b = _scalar(beta, "beta", dev) if add_source else None
-    x0r = _rows(x0, "x0") if add_source else None
-    if out is None:
-        out = torch.empty_like(xr)
-    plan = g.csr.plan
-    partials = torch.empty(plan.n_slots * C, dtype=torch.float32, device=dev) if plan.n_slots else None
-    _lib.call("gnpde_attn_rhs_f32", _ptr(plan.items), plan.n_items, _ptr(plan.heavy), plan.n_heavy, _ptr(g.csr.col),
-              int(norm_idx), ns.mode, ns.heads, ns.dk, _ptr(ns.cs), _ptr(ns.q), _ptr(ns.k), ns.ldqk, ns.p0, ns.p1,
-              _ptr(m), _ptr(rl), C, _ptr(xr), C, _ptr(x0r), C, _ptr(a), _ptr(b), _flags(rhs, alpha_sigmoid, add_source),
-              _ptr(out), C, _ptr(partials), _stream(dev))
-    return out.view(shape)
+    """K3: f = a*(A_att x - x) [+ b x0], A_att = head-mean softmax weights
+    (edge-parallel weights, then the K1 gather-aggregate with the fused epilogue)."""
+    w = attn_weights(g, ns, m, rl, norm_idx)
+    return spmm_rhs(g, w, x, x0=x0, alpha=alpha, beta=beta, rhs=rhs, alpha_sigmoid=alpha_sigmoid,
+                    add_source=add_source, out=out)
 
 
 def edge_attention(g, ns, m, rl, norm_idx):
     """attention [B,E,h] in COO order (SpGraphTransAttentionLayer.forward's first output)."""
     dev = g.csr.col.device
     att = torch.empty(g.B, g.E, ns.heads, dtype=torch.float32, device=dev)
-    plan = g.csr.plan
-    _lib.call("gnpde_edge_attention_f32", _ptr(plan.items), plan.n_items, _ptr(g.csr.col), _ptr(g.csr.perm),
-              int(norm_idx), ns.mode, ns.heads, ns.dk, _ptr(ns.cs), _ptr(ns.q), _ptr(ns.k), ns.ldqk, ns.p0, ns.p1,
-              _ptr(m), _ptr(rl), _ptr(att), _stream(dev))
+    _lib.call("gnpde_edge_attention_f32", _ptr(g.csr.rowidx), _ptr(g.csr.col), _ptr(g.csr.perm), g.nnz, int(norm_idx),
+              ns.mode, ns.heads, ns.dk, _ptr(ns.cs), _ptr(ns.q), _ptr(ns.k), ns.ldqk, ns.p0, ns.p1, _ptr(m), _ptr(rl),
+              _ptr(att), _stream(dev))
     return att
 
 

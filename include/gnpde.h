@@ -64,6 +64,8 @@ extern "C" {
 #define GNPDE_SCORE_EXP_KERNEL 2   /* ov^2 exp(-|q_src - k_dst|^2 / (2 ls^2))                     */
 #define GNPDE_SCORE_COSINE 3       /* cosine similarity, eps 1e-5                                 */
 #define GNPDE_SCORE_PEARSON 4      /* centred cosine similarity                                   */
+#define GNPDE_SCORE_UNIFORM 5      /* every score 0: the fork's scaled_dot under source-grouped    */
+                                   /* softmax (norm_idx 0), where all scores of a group are equal  */
 
 int gnpde_abi_version(void);
 const char* gnpde_last_error(void);
@@ -77,6 +79,10 @@ size_t gnpde_csr_workspace_bytes(int64_t B, int64_t E, int64_t N);
 int gnpde_csr_build(const int64_t* edge_index, int64_t B, int64_t E, int64_t N, int key_row,
                     int32_t* rowptr, int32_t* col, int32_t* perm,
                     void* workspace, size_t workspace_bytes, void* stream);
+
+/* rowidx[p] = the row of CSR position p (once per graph; drives the
+ * edge-parallel attention-weight kernels).                                   */
+int gnpde_csr_rowidx(const int32_t* rowptr, int64_t R, int64_t nnz, int32_t* rowidx, void* stream);
 
 /* w_out[p] = mean_{h<H} w_in[perm[p]*H + h]  (H = 1: plain permutation).
  * Head-mean of attention weights, function_laplacian_diffusion.py:45-49.    */
@@ -139,6 +145,7 @@ int gnpde_ref_scores_f32(const float* x, int64_t B, int64_t N, int64_t C, int64_
  * m[g,h] = max_e s_e,h (fp64), rl[g,h] = 1/(sum_e exp(s_e,h - m) + 1e-16).
  * partials: 2*heads doubles per plan slot.
  * Edge scores by `mode` from cs (REFERENCE) or q/k (per-edge modes).
+ * Groups of 8 lanes per item: plan it with a small chunk (e.g. 64).
  * Restates utils.softmax, src/utils.py:116-127.                              */
 int gnpde_softmax_stats_f32(const int32_t* items, int64_t n_items, const int32_t* heavy, int64_t n_heavy,
                             const int32_t* gidx, int group_is_dst, int mode, int64_t heads, int64_t dk,
@@ -146,21 +153,20 @@ int gnpde_softmax_stats_f32(const int32_t* items, int64_t n_items, const int32_t
                             float score_p0, float score_p1,
                             double* m, float* rl, double* partials, void* stream);
 
-/* Attention aggregation + RHS epilogue over the aggregation CSR:
- *   w_e = (1/h) sum_h exp(s_e,h - m[g(e),h]) * rl[g(e),h],  g = src (norm_idx 0) or dst (1)
- *   ax  = sum_e w_e x[dst(e)],  f = epilogue(ax)   (multiply_attention :33-41, forward :52-59) */
-int gnpde_attn_rhs_f32(const int32_t* items, int64_t n_items, const int32_t* heavy, int64_t n_heavy,
-                       const int32_t* col, int norm_idx, int mode, int64_t heads, int64_t dk,
-                       const double* cs, const float* q, const float* k, int64_t ldqk,
-                       float score_p0, float score_p1, const double* m, const float* rl,
-                       int64_t C, const float* x, int64_t ldx, const float* x0, int64_t ldx0,
-                       const float* alpha, const float* beta, int flags,
-                       float* f, int64_t ldf, float* partials, void* stream);
+/* Head-mean attention weights in aggregation-CSR order (edge-parallel):
+ *   w[p] = (1/h) sum_h exp(s_p,h - m[g,h]) * rl[g,h],  g = src (norm_idx 0) or dst (1)
+ * (utils.softmax then attention.mean(dim=2), function_transformer_attention.py:34).
+ * The attention RHS is then gnpde_spmm_rhs_f32 with these weights
+ * (multiply_attention :33-41 + forward :52-59).                              */
+int gnpde_attn_weights_f32(const int32_t* rowidx, const int32_t* col, int64_t nnz, int norm_idx, int mode,
+                           int64_t heads, int64_t dk, const double* cs, const float* q, const float* k, int64_t ldqk,
+                           float score_p0, float score_p1, const double* m, const float* rl, float* w_out,
+                           void* stream);
 
 /* Per-edge, per-head attention in COO order (the [B,E,h] `attention` that
  * SpGraphTransAttentionLayer.forward returns, function_transformer_attention.py:265-267):
  *   att[perm[p]*heads + h] = exp(s_p,h - m[g,h]) * rl[g,h]  over the aggregation CSR. */
-int gnpde_edge_attention_f32(const int32_t* items, int64_t n_items, const int32_t* col, const int32_t* perm,
+int gnpde_edge_attention_f32(const int32_t* rowidx, const int32_t* col, const int32_t* perm, int64_t nnz,
                              int norm_idx, int mode, int64_t heads, int64_t dk,
                              const double* cs, const float* q, const float* k, int64_t ldqk,
                              float score_p0, float score_p1, const double* m, const float* rl,

@@ -23,7 +23,7 @@ def declared_symbols():
 
 def test_header_declares_the_entry_points():
     syms = declared_symbols()
-    for must in ("gnpde_csr_build", "gnpde_spmm_rhs_f32", "gnpde_attn_rhs_f32", "gnpde_softmax_stats_f32",
+    for must in ("gnpde_csr_build", "gnpde_spmm_rhs_f32", "gnpde_attn_weights_f32", "gnpde_softmax_stats_f32",
                  "gnpde_linear_f32", "gnpde_ref_scores_f32", "gnpde_rk_combine_f32", "gnpde_last_error"):
         assert must in syms
 
