@@ -18,20 +18,45 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 constexpr int kLinRowsPerWave = 32;
 constexpr int kLinCols = 64;
 
+constexpr int kLinChunk = 16;        // k-steps per half per prefetch chunk
+constexpr int kLinLdsStride = kLinCols + 1;
+
+template <bool VEC4>
+__device__ __forceinline__ void lin_load_chunk(const float* __restrict__ xr, int kbase, int s0, int Kh, int K,
+                                               float (&a)[kLinChunk]) {
+  if constexpr (VEC4) {
+#pragma unroll
+    for (int i = 0; i < kLinChunk; i += 4) {
+      if (s0 + i < Kh) {
+        const float4 t = *reinterpret_cast<const float4*>(xr + kbase + s0 + i);
+        a[i] = t.x; a[i + 1] = t.y; a[i + 2] = t.z; a[i + 3] = t.w;
+      } else {
+        a[i] = a[i + 1] = a[i + 2] = a[i + 3] = 0.f;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < kLinChunk; ++i) {
+      const int k = kbase + s0 + i;
+      a[i] = (s0 + i < Kh && k < K) ? xr[k] : 0.f;
+    }
+  }
+}
+
 template <bool VEC4>
 __global__ __launch_bounds__(256) void linear_mfma_kernel(const float* __restrict__ x, int R, int K, int64_t ldx,
                                                            const float* __restrict__ W,
                                                            const float* __restrict__ bias, int Nout, int split,
                                                            float* __restrict__ out_a, int64_t lda,
                                                            float* __restrict__ out_b, int64_t ldb) {
-  extern __shared__ __attribute__((aligned(16))) float wt[];  // [2*Kh][64]
+  extern __shared__ __attribute__((aligned(16))) float wt[];  // [2*Kh][65]
   const int Kh = (K + 1) >> 1;
   const int col0 = blockIdx.y * kLinCols;
-  // stage W^T slice: wt[k'][j] = W[col0 + j][k(k')], k' = h*Kh + s  ->  k = k' (k' < K) else 0
+  // stage W^T slice (coalesced along k): wt[k][j] = W[col0 + j][k]
   for (int t = threadIdx.x; t < 2 * Kh * kLinCols; t += blockDim.x) {
-    const int kk = t / kLinCols, j = t - kk * kLinCols;
+    const int j = t / (2 * Kh), kk = t - j * (2 * Kh);
     const int n = col0 + j;
-    wt[t] = (kk < K && n < Nout) ? W[(int64_t)n * K + kk] : 0.f;
+    wt[kk * kLinLdsStride + j] = (kk < K && n < Nout) ? W[(int64_t)n * K + kk] : 0.f;
   }
   __syncthreads();
 
@@ -45,26 +70,20 @@ __global__ __launch_bounds__(256) void linear_mfma_kernel(const float* __restric
   const int kbase = h * Kh;
 
   f32x16 acc0 = {0}, acc1 = {0};
-  for (int s0 = 0; s0 < Kh; s0 += 4) {
-    float a[4];
-    if constexpr (VEC4) {
-      const float4 t = *reinterpret_cast<const float4*>(xr + kbase + s0);
-      a[0] = t.x; a[1] = t.y; a[2] = t.z; a[3] = t.w;
-    } else {
+  float a_cur[kLinChunk], a_nxt[kLinChunk];
+  lin_load_chunk<VEC4>(xr, kbase, 0, Kh, K, a_cur);
+  for (int s0 = 0; s0 < Kh; s0 += kLinChunk) {
+    if (s0 + kLinChunk < Kh) lin_load_chunk<VEC4>(xr, kbase, s0 + kLinChunk, Kh, K, a_nxt);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int k = kbase + s0 + i;
-        a[i] = (s0 + i < Kh && k < K) ? xr[k] : 0.f;
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < kLinChunk; ++i) {
       if (s0 + i < Kh) {
-        const float* wrow = wt + (kbase + s0 + i) * kLinCols;
-        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], wrow[r32], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], wrow[32 + r32], acc1, 0, 0, 0);
+        const float* wrow = wt + (kbase + s0 + i) * kLinLdsStride;
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a_cur[i], wrow[r32], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a_cur[i], wrow[32 + r32], acc1, 0, 0, 0);
       }
     }
+#pragma unroll
+    for (int i = 0; i < kLinChunk; ++i) a_cur[i] = a_nxt[i];
   }
   // C/D layout (32x32): col = lane&31, row = (reg&3) + 8*(reg>>2) + 4*(lane>>5)
 #pragma unroll
@@ -98,7 +117,7 @@ extern "C" int gnpde_linear_f32(const float* x, int64_t R, int64_t K, int64_t ld
   GNPDE_REQUIRE(split == Nout || out_b != nullptr, GNPDE_EINVAL, "linear: out_b is NULL");
   GNPDE_REQUIRE(lda >= split && (split == Nout || ldb >= Nout - split), GNPDE_EINVAL, "linear: bad ld");
   const int64_t Kh = (K + 1) / 2;
-  const size_t shm = sizeof(float) * (size_t)(2 * Kh * kLinCols);
+  const size_t shm = sizeof(float) * (size_t)(2 * Kh * kLinLdsStride);
   GNPDE_REQUIRE(shm <= 160 * 1024, GNPDE_EUNSUPPORTED, "linear: K=%lld too large for the LDS slice",
                 (long long)K);
   if (R == 0) return GNPDE_OK;

@@ -77,21 +77,31 @@ __global__ __launch_bounds__(256) void stats_kernel(const int4* __restrict__ ite
   }
 }
 
-// Hub groups: combine the chunks' (max, sum) pairs in plan order.
+// Hub groups: one wavefront per (group, head); lanes merge strided chunks, then a
+// fixed xor tree (deterministic).
 __global__ __launch_bounds__(256) void stats_fixup_kernel(const int4* __restrict__ heavy, int n_heavy, int H,
                                                            const double* __restrict__ partials,
                                                            double* __restrict__ m_out, float* __restrict__ rl_out) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= n_heavy * H) return;
-  const int i = t / H, h = t - i * H;
+  const int lane = threadIdx.x & 63;
+  const int wid = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+  if (wid >= n_heavy * H) return;
+  const int i = wid / H, h = wid - i * H;
   const int4 hv = heavy[i];
   const int g = hv.x, first = hv.y, nch = hv.z;
   double M = -INFINITY;
   float L = 0.f;
-  for (int c = 0; c < nch; ++c)
+  for (int c = lane; c < nch; c += kWave)
     online_merge(M, L, partials[(int64_t)(first + c) * 2 * H + h], (float)partials[(int64_t)(first + c) * 2 * H + H + h]);
-  m_out[(int64_t)g * H + h] = M;
-  rl_out[(int64_t)g * H + h] = 1.0f / (L + kSoftmaxEps);
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const double M2 = __shfl_xor(M, o);
+    const float L2 = __shfl_xor(L, o);
+    online_merge(M, L, M2, L2);
+  }
+  if (lane == 0) {
+    m_out[(int64_t)g * H + h] = M;
+    rl_out[(int64_t)g * H + h] = 1.0f / (L + kSoftmaxEps);
+  }
 }
 
 // ------------------------------------------------------------------ edge-parallel weights
@@ -128,6 +138,74 @@ __global__ __launch_bounds__(256) void edge_attention_kernel(const int* __restri
     for (int h = 0; h < H; ++h) {
       const double s = sa.score(r, c, h);
       att[e * H + h] = expf((float)(s - m[g * H + h])) * rl[g * H + h];
+    }
+  }
+}
+
+// ------------------------------------------------------------------ team-mode kernels (per-edge q/k scores)
+// T lanes per edge / group (T = H * S, S = dk/VEC lanes per head), 64/T teams per
+// wavefront; lane t holds VEC consecutive elements of the att-wide q/k rows and
+// ends with its own head's score.  Head leaders (t % S == 0) own the per-head state.
+struct Team {
+  int T, S;
+};
+
+template <int VEC>
+__global__ __launch_bounds__(256) void stats_team_kernel(const int4* __restrict__ items, int n_items,
+                                                          const int* __restrict__ gidx, int group_is_dst, ScoreArgs sa,
+                                                          Team tm, double* __restrict__ m_out,
+                                                          float* __restrict__ rl_out, double* __restrict__ partials) {
+  const int lane = threadIdx.x & 63;
+  const int T = tm.T, S = tm.S, tpw = kWave / T;
+  const int team = lane / T, t = lane % T, h = t / S;
+  const int item = (blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * tpw + team;
+  const bool live = item < n_items && team < tpw;
+  const int4 it = live ? items[item] : make_int4(0, 0, 0, -1);
+  const int grp = it.x, beg = it.y, end = it.z, slot = it.w;
+  double M = -INFINITY;
+  float L = 0.f;
+  for (int p = beg; p < end; p += 2) {
+    const bool two = p + 1 < end;
+    const int o0 = gidx[p];
+    const int o1 = two ? gidx[p + 1] : o0;
+    const float s0 = team_score<VEC>(sa, group_is_dst ? o0 : grp, group_is_dst ? grp : o0, t, S);
+    const float s1 = team_score<VEC>(sa, group_is_dst ? o1 : grp, group_is_dst ? grp : o1, t, S);
+    online_push(M, L, (double)s0);
+    if (two) online_push(M, L, (double)s1);
+  }
+  if (!live || (t % S) != 0) return;
+  const int H = sa.H;
+  if (slot >= 0) {
+    partials[(int64_t)slot * 2 * H + h] = M;
+    partials[(int64_t)slot * 2 * H + H + h] = (double)L;
+  } else {
+    m_out[(int64_t)grp * H + h] = M;
+    rl_out[(int64_t)grp * H + h] = 1.0f / (L + kSoftmaxEps);
+  }
+}
+
+template <int VEC, bool COO>
+__global__ __launch_bounds__(256) void attn_team_kernel(const int* __restrict__ rowidx, const int* __restrict__ col,
+                                                         const int* __restrict__ perm, int64_t nnz, int norm_idx,
+                                                         ScoreArgs sa, Team tm, const double* __restrict__ m,
+                                                         const float* __restrict__ rl, float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int T = tm.T, S = tm.S, tpw = kWave / T;
+  const int team = lane / T, t = lane % T, h = t / S;
+  const int H = sa.H;
+  if (team >= tpw) return;
+  const int64_t nteams = (int64_t)gridDim.x * kWavesPerBlock * tpw;
+  for (int64_t p = (int64_t)(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * tpw + team; p < nnz; p += nteams) {
+    const int r = rowidx[p], c = col[p];
+    const int64_t g = norm_idx == 0 ? r : c;
+    const float s = team_score<VEC>(sa, r, c, t, S);
+    const bool leader = (t % S) == 0;
+    float term = leader ? expf((float)((double)s - m[g * H + h])) * rl[g * H + h] : 0.f;
+    if (COO) {
+      if (leader) out[(int64_t)perm[p] * H + h] = term;
+    } else {
+      for (int o = S; o < T; o <<= 1) term += __shfl_xor(term, o);
+      if (t == 0) out[p] = term / (float)H;
     }
   }
 }
@@ -176,20 +254,26 @@ __global__ __launch_bounds__(256) void keysum_partial_kernel(const float* __rest
   }
 }
 
-// xbar[b][c] = sum over tiles (4 interleaved subsets + fixed-order combine)
+// xbar[b][c] = sum over tiles: 16 columns x 16 interleaved tile subsets per block,
+// subsets combined in a fixed order.
 __global__ __launch_bounds__(256) void keysum_tiles_kernel(const double* __restrict__ part, int ntiles, int C,
                                                             double* __restrict__ xbar) {
-  __shared__ double red[4][64];
+  __shared__ double red[16][17];
   const int b = blockIdx.y;
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int sub = threadIdx.x >> 6;
+  const int cl = threadIdx.x & 15, sub = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + cl;
   double s = 0.0;
-  if (c <= C)
-    for (int t = sub; t < ntiles; t += 4) s += part[((int64_t)b * ntiles + t) * (C + 1) + c];
-  red[sub][threadIdx.x & 63] = s;
+  if (c <= C) {
+#pragma unroll 4
+    for (int t = sub; t < ntiles; t += 16) s += part[((int64_t)b * ntiles + t) * (C + 1) + c];
+  }
+  red[sub][cl] = s;
   __syncthreads();
-  if (sub == 0 && c <= C) xbar[(int64_t)b * (C + 1) + c] = ((red[0][c & 63] + red[1][c & 63]) + red[2][c & 63]) +
-                                                         red[3][c & 63];
+  if (sub == 0 && c <= C) {
+    double a = 0.0;
+    for (int k = 0; k < 16; ++k) a += red[k][cl];
+    xbar[(int64_t)b * (C + 1) + c] = a;
+  }
 }
 
 // per batch element: S = Wk xbar + E bk;  U[c,h] = sum_{d in h} Wq[d,c] S[d] / sqrt(dk);  v[h] = bq_h . S_h / sqrt(dk)
@@ -328,7 +412,7 @@ static int pow2_at_least(int v, int cap) {
   return p;
 }
 
-constexpr int kKeysumTilesTarget = 1024;
+constexpr int kKeysumTilesTarget = 512;
 
 static int keysum_vec(int64_t C, const float* x, int64_t ldx) {
   if (C % 4 == 0 && ldx % 4 == 0 && aligned16(x)) return 4;
@@ -381,6 +465,30 @@ static void launch_node_scores_vec(unsigned grid, int GL, hipStream_t s, const f
     launch_node_scores<VEC, 64>(grid, s, x, R, N, C, ldx, H, U, v, cs);
 }
 
+// team geometry for the per-edge modes: VEC = 4, S = dk/4, T = H*S, both powers
+// of two, T <= 64; otherwise lane mode (T = 0).
+static Team team_geometry(const ScoreArgs& sa) {
+  Team tm{0, 0};
+  if (sa.mode != GNPDE_SCORE_DOT && sa.mode != GNPDE_SCORE_EXP_KERNEL && sa.mode != GNPDE_SCORE_COSINE &&
+      sa.mode != GNPDE_SCORE_PEARSON)
+    return tm;
+  if (sa.dk % 4 != 0 || sa.ldqk % 4 != 0 || !aligned16(sa.q) || !aligned16(sa.k)) return tm;
+  const int S = sa.dk / 4, T = sa.H * S;
+  if ((S & (S - 1)) || (T & (T - 1)) || T > kWave) return tm;
+  tm.T = T;
+  tm.S = S;
+  return tm;
+}
+
+static unsigned edge_grid(int64_t nnz) {
+  return (unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(nnz, kBlock), 16384));
+}
+
+static unsigned team_grid(int64_t nnz, const Team& tm) {
+  const int64_t per_block = (int64_t)kWavesPerBlock * (kWave / tm.T);
+  return (unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(nnz, per_block), 32768));
+}
+
 }  // namespace gnpde
 
 using namespace gnpde;
@@ -413,6 +521,12 @@ int gnpde_softmax_stats_f32(const int32_t* items, int64_t n_items, const int32_t
   const ScoreArgs sa = make_score_args(mode, heads, dk, cs, q, k, ldqk, score_p0, score_p1);
   hipStream_t s = as_stream(stream);
   const int4* it = reinterpret_cast<const int4*>(items);
+  const Team tm = team_geometry(sa);
+  if (tm.T > 0) {
+    const unsigned grid = (unsigned)ceil_div(n_items, (int64_t)kWavesPerBlock * (kWave / tm.T));
+    stats_team_kernel<4><<<grid, kBlock, 0, s>>>(it, (int)n_items, gidx, group_is_dst, sa, tm, m, rl, partials);
+    GNPDE_LAUNCH_CHECK();
+  } else {
   const int GL = 8;  // lanes per item
   const unsigned grid = (unsigned)ceil_div(n_items, (int64_t)kWavesPerBlock * (kWave / GL));
   if (heads <= 1)
@@ -426,16 +540,15 @@ int gnpde_softmax_stats_f32(const int32_t* items, int64_t n_items, const int32_t
   else
     launch_stats<16>(grid, GL, s, it, (int)n_items, gidx, group_is_dst, sa, m, rl, partials);
   GNPDE_LAUNCH_CHECK();
+  }
   if (n_heavy > 0) {
-    const unsigned g2 = (unsigned)ceil_div(n_heavy * heads, kBlock);
+    const unsigned g2 = (unsigned)ceil_div(n_heavy * heads, kWavesPerBlock);
     stats_fixup_kernel<<<g2, kBlock, 0, s>>>(reinterpret_cast<const int4*>(heavy), (int)n_heavy, (int)heads, partials,
                                              m, rl);
     GNPDE_LAUNCH_CHECK();
   }
   return GNPDE_OK;
 }
-
-static unsigned edge_grid(int64_t nnz) { return (unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(nnz, kBlock), 16384)); }
 
 int gnpde_attn_weights_f32(const int32_t* rowidx, const int32_t* col, int64_t nnz, int norm_idx, int mode,
                            int64_t heads, int64_t dk, const double* cs, const float* q, const float* k, int64_t ldqk,
@@ -447,7 +560,13 @@ int gnpde_attn_weights_f32(const int32_t* rowidx, const int32_t* col, int64_t nn
   if (nnz == 0) return GNPDE_OK;
   GNPDE_REQUIRE(rowidx && col && m && rl && w_out, GNPDE_EINVAL, "attn_weights: NULL pointer");
   const ScoreArgs sa = make_score_args(mode, heads, dk, cs, q, k, ldqk, score_p0, score_p1);
-  attn_weights_kernel<<<edge_grid(nnz), kBlock, 0, as_stream(stream)>>>(rowidx, col, nnz, norm_idx, sa, m, rl, w_out);
+  const Team tm = team_geometry(sa);
+  if (tm.T > 0)
+    attn_team_kernel<4, false><<<team_grid(nnz, tm), kBlock, 0, as_stream(stream)>>>(rowidx, col, nullptr, nnz, norm_idx,
+                                                                                    sa, tm, m, rl, w_out);
+  else
+    attn_weights_kernel<<<edge_grid(nnz), kBlock, 0, as_stream(stream)>>>(rowidx, col, nnz, norm_idx, sa, m, rl,
+                                                                          w_out);
   GNPDE_LAUNCH_CHECK();
   return GNPDE_OK;
 }
@@ -462,8 +581,13 @@ int gnpde_edge_attention_f32(const int32_t* rowidx, const int32_t* col, const in
   if (nnz == 0) return GNPDE_OK;
   GNPDE_REQUIRE(rowidx && col && perm && m && rl && att, GNPDE_EINVAL, "edge_attention: NULL pointer");
   const ScoreArgs sa = make_score_args(mode, heads, dk, cs, q, k, ldqk, score_p0, score_p1);
-  edge_attention_kernel<<<edge_grid(nnz), kBlock, 0, as_stream(stream)>>>(rowidx, col, perm, nnz, norm_idx, sa, m,
-                                                                          rl, att);
+  const Team tm = team_geometry(sa);
+  if (tm.T > 0)
+    attn_team_kernel<4, true><<<team_grid(nnz, tm), kBlock, 0, as_stream(stream)>>>(rowidx, col, perm, nnz, norm_idx, sa,
+                                                                                   tm, m, rl, att);
+  else
+    edge_attention_kernel<<<edge_grid(nnz), kBlock, 0, as_stream(stream)>>>(rowidx, col, perm, nnz, norm_idx, sa, m,
+                                                                            rl, att);
   GNPDE_LAUNCH_CHECK();
   return GNPDE_OK;
 }
@@ -506,7 +630,7 @@ int gnpde_ref_scores_f32(const float* x, int64_t B, int64_t N, int64_t C, int64_
   else
     keysum_partial_kernel<1><<<g1, kBlock, shm, s>>>(x, N, (int)C, ldx, indeg, rpt, tpr, ntiles, part);
   GNPDE_LAUNCH_CHECK();
-  keysum_tiles_kernel<<<dim3((unsigned)ceil_div(C + 1, 64), (unsigned)B), kBlock, 0, s>>>(part, ntiles, (int)C, xbar);
+  keysum_tiles_kernel<<<dim3((unsigned)ceil_div(C + 1, 16), (unsigned)B), kBlock, 0, s>>>(part, ntiles, (int)C, xbar);
   GNPDE_LAUNCH_CHECK();
   keysum_finish_kernel<<<(unsigned)B, kBlock, sizeof(double) * (size_t)att, s>>>(xbar, (int)C, Wq, bq, Wk, bk, (int)att,
                                                                                (int)heads, U, v);

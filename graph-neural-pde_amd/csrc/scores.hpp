@@ -1,16 +1,23 @@
 // scores.hpp — attention edge scores (function_transformer_attention.py:246-259).
+//
+// Two evaluation shapes:
+//  * lane mode: one lane evaluates a whole (src, dst) pair for one head
+//    (reference / uniform modes: a node-score gather; fallback for odd dk);
+//  * team mode: T lanes cooperate on one edge, lane t holding VEC consecutive
+//    elements of the att-wide q/k rows (coalesced 16-byte gathers); the S =
+//    dk/VEC lanes of a head reduce with xor shuffles, so every lane ends with
+//    its own head's score.
 #pragma once
 #include "common.hpp"
 
 namespace gnpde {
 
-// Scores of one (src, dst) pair for one head (function_transformer_attention.py:246-259).
 __device__ __forceinline__ float pair_score(int mode, const float* __restrict__ qi, const float* __restrict__ kj,
                                             int dk, float p0, float p1) {
   if (mode == GNPDE_SCORE_DOT) {
     float s = 0.f;
     for (int d = 0; d < dk; ++d) s = fmaf(qi[d], kj[d], s);
-    return s * rsqrtf((float)dk) ;
+    return s * rsqrtf((float)dk);
   } else if (mode == GNPDE_SCORE_EXP_KERNEL) {
     float s = 0.f;
     for (int d = 0; d < dk; ++d) {
@@ -21,7 +28,10 @@ __device__ __forceinline__ float pair_score(int mode, const float* __restrict__ 
   } else {  // cosine / pearson: torch>=1.12 CosineSimilarity, each operand / max(norm, eps)
     float mq = 0.f, mk = 0.f;
     if (mode == GNPDE_SCORE_PEARSON) {
-      for (int d = 0; d < dk; ++d) { mq += qi[d]; mk += kj[d]; }
+      for (int d = 0; d < dk; ++d) {
+        mq += qi[d];
+        mk += kj[d];
+      }
       mq /= (float)dk;
       mk /= (float)dk;
     }
@@ -47,12 +57,69 @@ struct ScoreArgs {
   int64_t ldqk;
   float p0, p1;
 
-  // score of edge src->dst, head h, as double (exact for the fp32 modes)
+  // lane mode: score of edge src->dst, head h, as double (exact for the fp32 modes)
   __device__ __forceinline__ double score(int src, int dst, int h) const {
     if (mode == GNPDE_SCORE_REFERENCE) return cs[(int64_t)src * H + h];
     if (mode == GNPDE_SCORE_UNIFORM) return 0.0;
     return (double)pair_score(mode, q + (int64_t)src * ldqk + h * dk, k + (int64_t)dst * ldqk + h * dk, dk, p0, p1);
   }
 };
+
+// sum over the S lanes of a head segment (S a power of two, segments aligned)
+__device__ __forceinline__ float seg_sum(float v, int S) {
+  for (int o = 1; o < S; o <<= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// team mode: lane t (< T) of the team covers elements [t*VEC, t*VEC+VEC) of the
+// att-wide rows; returns the score of the lane's head (all S lanes agree).
+template <int VEC>
+__device__ __forceinline__ float team_score(const ScoreArgs& sa, int src, int dst, int t, int S) {
+  float q[VEC], k[VEC];
+  load_vec<VEC>(sa.q + (int64_t)src * sa.ldqk + t * VEC, q);
+  load_vec<VEC>(sa.k + (int64_t)dst * sa.ldqk + t * VEC, k);
+  const float dk = (float)sa.dk;
+  if (sa.mode == GNPDE_SCORE_DOT) {
+    float a = 0.f;
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) a = fmaf(q[i], k[i], a);
+    return seg_sum(a, S) * rsqrtf(dk);
+  }
+  if (sa.mode == GNPDE_SCORE_EXP_KERNEL) {
+    float a = 0.f;
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) {
+      const float d = q[i] - k[i];
+      a = fmaf(d, d, a);
+    }
+    a = seg_sum(a, S);
+    return sa.p0 * sa.p0 * expf(-(a / (2.0f * sa.p1 * sa.p1)));
+  }
+  if (sa.mode == GNPDE_SCORE_PEARSON) {
+    float sq = 0.f, sk = 0.f;
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) {
+      sq += q[i];
+      sk += k[i];
+    }
+    const float mq = seg_sum(sq, S) / dk, mk = seg_sum(sk, S) / dk;
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) {
+      q[i] -= mq;
+      k[i] -= mk;
+    }
+  }
+  float nq = 0.f, nk = 0.f, dot = 0.f;
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) {
+    nq = fmaf(q[i], q[i], nq);
+    nk = fmaf(k[i], k[i], nk);
+    dot = fmaf(q[i], k[i], dot);
+  }
+  nq = seg_sum(nq, S);
+  nk = seg_sum(nk, S);
+  dot = seg_sum(dot, S);
+  return dot / (fmaxf(sqrtf(nq), 1e-5f) * fmaxf(sqrtf(nk), 1e-5f));
+}
 
 }  // namespace gnpde

@@ -89,6 +89,7 @@ class SpGraphTransAttentionLayer(nn.Module):
         self._graph = None
         self._graph_key = None
         self._uniform = None  # (graph, NodeScores, m, rl, csr weights) for the uniform fast path
+        self._wcat = None     # (param versions, ([Wq;Wk], [bq;bk]))
 
     def init_weights(self, m):
         """Constant 1e-5 init (:153-157)."""
@@ -138,9 +139,16 @@ class SpGraphTransAttentionLayer(nn.Module):
     def node_scores(self, g, x):
         _check_inference(self)
         p0, p1 = self._score_params()
+        wcat = None
+        if self.score_mode != 'reference' or self.opt.get('attention_type', 'scaled_dot') != 'scaled_dot':
+            key = tuple(_tensor_key(t) for t in (self.Q.weight, self.Q.bias, self.K.weight, self.K.bias))
+            if self._wcat is None or self._wcat[0] != key:  # [Wq; Wk] for the fused MFMA projection
+                self._wcat = (key, (torch.cat([self.Q.weight.detach(), self.K.weight.detach()], 0).contiguous(),
+                                    torch.cat([self.Q.bias.detach(), self.K.bias.detach()], 0).contiguous()))
+            wcat = self._wcat[1]
         return ops.node_scores(g, x, self.Q.weight.detach(), self.Q.bias.detach(), self.K.weight.detach(),
                                self.K.bias.detach(), self.h, self.opt.get('attention_type', 'scaled_dot'),
-                               self.score_mode, p0, p1)
+                               self.score_mode, p0, p1, wcat=wcat)
 
     def forward(self, x, edge, y=None):
         """Returns (attention [B,E,h], (None, None)): the per-edge softmax

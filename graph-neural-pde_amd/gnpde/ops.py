@@ -271,7 +271,7 @@ class NodeScores(object):
 
 
 def node_scores(g, x, Wq, bq, Wk, bk, heads, attention_type='scaled_dot', score_mode='reference',
-                output_var=1.0, lengthscale=1.0):
+                output_var=1.0, lengthscale=1.0, wcat=None):
     """Q/K-side work of SpGraphTransAttentionLayer.forward (function_transformer_attention.py:224-259)."""
     mode = SCORE_MODES[(attention_type, score_mode)]
     xr = _rows(x, "x")
@@ -290,8 +290,11 @@ def node_scores(g, x, Wq, bq, Wk, bk, heads, attention_type='scaled_dot', score_
                   _ptr(bq.contiguous()), _ptr(Wk.contiguous()), _ptr(bk.contiguous()), att, heads, _ptr(cs), _ptr(ws),
                   ws_bytes, _stream(xr.device))
         return NodeScores(mode, heads, dk, cs=cs)
-    W = torch.cat([Wq, Wk], 0)
-    b = torch.cat([bq, bk], 0) if bq is not None else None
+    if wcat is not None:
+        W, b = wcat
+    else:
+        W = torch.cat([Wq, Wk], 0)
+        b = torch.cat([bq, bk], 0) if bq is not None else None
     q, k = linear(xr, W, b, split=att)
     return NodeScores(mode, heads, dk, q=q, k=k, p0=output_var, p1=lengthscale)
 
