@@ -177,9 +177,26 @@ static int launch_agg(const int32_t* items, int64_t n_items, const int32_t* heav
                       const int32_t* col, const WP& wp, int64_t C, const Epi& ep, float* partials, hipStream_t s) {
   const bool src_ok4 = !(ep.flags & GNPDE_ADD_SOURCE) || (ep.ldx0 % 4 == 0 && aligned16(ep.x0));
   const bool src_ok2 = !(ep.flags & GNPDE_ADD_SOURCE) || (ep.ldx0 % 2 == 0 && aligned8(ep.x0));
-  const bool v4 = C % 4 == 0 && ep.ldx % 4 == 0 && ep.ldf % 4 == 0 && aligned16(ep.x) && aligned16(ep.f) && src_ok4 &&
+  bool st4 = true, st2 = true;
+  auto chk = [&](const void* p) {
+    if (p) {
+      st4 = st4 && aligned16(p);
+      st2 = st2 && aligned8(p);
+    }
+  };
+  if (ep.has_stage) {
+    chk(ep.st.f_out);
+    for (int i = 0; i < ep.st.n_out; ++i) {
+      chk(ep.st.o[i].out);
+      chk(ep.st.o[i].base);
+      for (int j = 0; j < ep.st.o[i].nk; ++j) chk(ep.st.o[i].k[j]);
+    }
+  } else {
+    chk(ep.f);
+  }
+  const bool v4 = C % 4 == 0 && ep.ldx % 4 == 0 && ep.ldf % 4 == 0 && aligned16(ep.x) && st4 && src_ok4 &&
                   (partials == nullptr || aligned16(partials));
-  const bool v2 = C % 2 == 0 && ep.ldx % 2 == 0 && ep.ldf % 2 == 0 && aligned8(ep.x) && aligned8(ep.f) && src_ok2 &&
+  const bool v2 = C % 2 == 0 && ep.ldx % 2 == 0 && ep.ldf % 2 == 0 && aligned8(ep.x) && st2 && src_ok2 &&
                   (partials == nullptr || aligned8(partials));
   const int4* it = reinterpret_cast<const int4*>(items);
   const int4* hv = reinterpret_cast<const int4*>(heavy);

@@ -103,6 +103,8 @@ struct Epi {
   int flags;
   float* f;
   int64_t ldf;
+  int has_stage;
+  gnpde_stage_epilogue_t st;
 };
 
 __device__ __forceinline__ float epi_alpha(const Epi& e) {
@@ -110,14 +112,15 @@ __device__ __forceinline__ float epi_alpha(const Epi& e) {
   return (e.flags & GNPDE_ALPHA_SIGMOID) ? 1.0f / (1.0f + expf(-a)) : a;
 }
 
-// f = a*(ax - x) [+ b*x0]  (function_laplacian_diffusion.py:69-77) or f = ax
+// f = a*(ax - x) [+ b*x0]  (function_laplacian_diffusion.py:69-77) or f = ax,
+// then either store f or emit the fused Runge-Kutta stage outputs.
 template <int VEC>
 __device__ __forceinline__ void epilogue_store(const Epi& e, int64_t row, int cc, const float (&ax)[VEC],
                                                float a, float b) {
-  float o[VEC];
-  if (e.flags & GNPDE_EPI_RHS) {
-    float xr[VEC];
-    load_vec<VEC>(e.x + row * e.ldx + cc, xr);
+  float o[VEC], xr[VEC];
+  const bool need_x = (e.flags & GNPDE_EPI_RHS) != 0;
+  if (need_x) load_vec<VEC>(e.x + row * e.ldx + cc, xr);
+  if (need_x) {
 #pragma unroll
     for (int t = 0; t < VEC; ++t) o[t] = a * (ax[t] - xr[t]);
     if (e.flags & GNPDE_ADD_SOURCE) {
@@ -130,7 +133,36 @@ __device__ __forceinline__ void epilogue_store(const Epi& e, int64_t row, int cc
 #pragma unroll
     for (int t = 0; t < VEC; ++t) o[t] = ax[t];
   }
-  store_vec<VEC>(e.f + row * e.ldf + cc, o);
+  if (!e.has_stage) {
+    store_vec<VEC>(e.f + row * e.ldf + cc, o);
+    return;
+  }
+  const int64_t off = row * e.ldf + cc;
+  if (e.st.f_out) store_vec<VEC>(e.st.f_out + off, o);
+  for (int i = 0; i < e.st.n_out; ++i) {
+    const gnpde_stage_out_t& so = e.st.o[i];
+    float r[VEC];
+    if (so.base == nullptr) {
+#pragma unroll
+      for (int t = 0; t < VEC; ++t) r[t] = 0.f;
+    } else if (need_x && so.base == e.x && e.ldx == e.ldf) {
+#pragma unroll
+      for (int t = 0; t < VEC; ++t) r[t] = so.cb * xr[t];
+    } else {
+      load_vec<VEC>(so.base + off, r);
+#pragma unroll
+      for (int t = 0; t < VEC; ++t) r[t] = so.cb * r[t];
+    }
+    for (int j = 0; j < so.nk; ++j) {
+      float kv[VEC];
+      load_vec<VEC>(so.k[j] + off, kv);
+#pragma unroll
+      for (int t = 0; t < VEC; ++t) r[t] = fmaf(so.c[j], kv[t], r[t]);
+    }
+#pragma unroll
+    for (int t = 0; t < VEC; ++t) r[t] = fmaf(so.cf, o[t], r[t]);
+    store_vec<VEC>(so.out + off, r);
+  }
 }
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }

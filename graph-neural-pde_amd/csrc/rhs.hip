@@ -379,8 +379,10 @@ static ScoreArgs make_score_args(int mode, int64_t heads, int64_t dk, const doub
 }
 
 static Epi make_epi(const float* x, int64_t ldx, const float* x0, int64_t ldx0, const float* alpha, const float* beta,
-                    int flags, float* f, int64_t ldf) {
+                    int flags, float* f, int64_t ldf, const gnpde_stage_epilogue_t* stage = nullptr) {
   Epi e;
+  e.has_stage = stage != nullptr;
+  if (stage) e.st = *stage;
   e.x = x;
   e.ldx = ldx;
   e.x0 = x0;
@@ -395,7 +397,17 @@ static Epi make_epi(const float* x, int64_t ldx, const float* x0, int64_t ldx0, 
 
 static int check_epi(const Epi& e, int64_t C, int64_t n_heavy, const void* partials) {
   GNPDE_REQUIRE(C >= 1, GNPDE_EINVAL, "rhs: C must be >= 1");
-  GNPDE_REQUIRE(e.x && e.f, GNPDE_EINVAL, "rhs: NULL x or f");
+  GNPDE_REQUIRE(e.x && (e.f || e.has_stage), GNPDE_EINVAL, "rhs: NULL x or f");
+  if (e.has_stage) {
+    GNPDE_REQUIRE(e.st.n_out >= 0 && e.st.n_out <= GNPDE_STAGE_MAX_OUT, GNPDE_EINVAL, "rhs: stage n_out out of range");
+    GNPDE_REQUIRE(e.st.f_out || e.st.n_out > 0, GNPDE_EINVAL, "rhs: stage epilogue stores nothing");
+    for (int i = 0; i < e.st.n_out; ++i) {
+      GNPDE_REQUIRE(e.st.o[i].out && e.st.o[i].nk >= 0 && e.st.o[i].nk <= GNPDE_STAGE_MAX_K, GNPDE_EINVAL,
+                    "rhs: bad stage output %d", i);
+      for (int j = 0; j < e.st.o[i].nk; ++j)
+        GNPDE_REQUIRE(e.st.o[i].k[j] != nullptr, GNPDE_EINVAL, "rhs: stage output %d k[%d] is NULL", i, j);
+    }
+  }
   GNPDE_REQUIRE(e.ldx >= C && e.ldf >= C, GNPDE_EINVAL, "rhs: leading dimension < C");
   if (e.flags & GNPDE_EPI_RHS) GNPDE_REQUIRE(e.alpha != nullptr, GNPDE_EINVAL, "rhs: NULL alpha");
   if (e.flags & GNPDE_ADD_SOURCE) {
@@ -498,8 +510,8 @@ extern "C" {
 int gnpde_spmm_rhs_f32(const int32_t* items, int64_t n_items, const int32_t* heavy, int64_t n_heavy,
                        const int32_t* col, const float* w, int64_t C, const float* x, int64_t ldx, const float* x0,
                        int64_t ldx0, const float* alpha, const float* beta, int flags, float* f, int64_t ldf,
-                       float* partials, void* stream) {
-  const Epi ep = make_epi(x, ldx, x0, ldx0, alpha, beta, flags, f, ldf);
+                       float* partials, const gnpde_stage_epilogue_t* stage, void* stream) {
+  const Epi ep = make_epi(x, ldx, x0, ldx0, alpha, beta, flags, f, ldf, stage);
   int rc = check_epi(ep, C, n_heavy, partials);
   if (rc) return rc;
   GNPDE_REQUIRE(n_items >= 0 && n_items < INT32_MAX && n_heavy >= 0, GNPDE_EINVAL, "spmm_rhs: bad item counts");

@@ -13,6 +13,21 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GNPDE_LIB", os.path.join(_HERE, "libgnpde.so"))
 
+STAGE_MAX_OUT = 2
+STAGE_MAX_K = 2
+
+
+class StageOut(ctypes.Structure):
+    """gnpde_stage_out_t: out = cb*base + cf*f + sum_j c[j]*k[j]."""
+    _fields_ = [("out", ctypes.c_void_p), ("base", ctypes.c_void_p), ("cb", ctypes.c_float), ("cf", ctypes.c_float),
+                ("nk", ctypes.c_int), ("k", ctypes.c_void_p * STAGE_MAX_K), ("c", ctypes.c_float * STAGE_MAX_K)]
+
+
+class StageEpilogue(ctypes.Structure):
+    """gnpde_stage_epilogue_t (include/gnpde.h)."""
+    _fields_ = [("f_out", ctypes.c_void_p), ("n_out", ctypes.c_int), ("o", StageOut * STAGE_MAX_OUT)]
+
+
 c_i32p = ctypes.POINTER(ctypes.c_int32)
 c_i64p = ctypes.POINTER(ctypes.c_int64)
 _vp = ctypes.c_void_p
@@ -34,7 +49,7 @@ SIGNATURES = {
     "gnpde_plan_build": (_int, [_vp, _i64, ctypes.c_int32, _vp, _i64, _vp, _i64, c_i64p, c_i64p, c_i64p, _vp,
                                 _size, _vp]),
     "gnpde_spmm_rhs_f32": (_int, [_vp, _i64, _vp, _i64, _vp, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _int, _vp,
-                                  _i64, _vp, _vp]),
+                                  _i64, _vp, ctypes.POINTER(StageEpilogue), _vp]),
     "gnpde_linear_f32": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _vp]),
     "gnpde_keysum_workspace_bytes": (_size, [_i64, _i64, _i64, _i64]),
     "gnpde_ref_scores_f32": (_int, [_vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _vp, _vp,

@@ -93,6 +93,20 @@ class LaplacianODEFunc(ODEFunc):
         w, tag = self._weights_tensor()
         return ops.spmm_rhs(g, self.csr_weights(g, w, tag), x, rhs=False)
 
+    def rhs_stage(self, t, x, stage):
+        """forward(t, x) with the solver's stage combination fused into the K1
+        epilogue (gnpde.integrator, no-grad fixed-grid solvers)."""
+        if self.nfe > self.opt["max_nfe"]:
+            raise MaxNFEException
+        self.nfe += 1
+        g = self.graph_for(x)
+        w, tag = self._weights_tensor()
+        add_source = bool(self.opt.get('add_source', False))
+        x0 = self.x0 if add_source else None
+        ops.spmm_rhs(g, self.csr_weights(g, w, tag), x, x0=x0, alpha=self.alpha_train.detach(),
+                     beta=self.beta_train.detach(), rhs=True, alpha_sigmoid=not self.opt.get('no_alpha_sigmoid', False),
+                     add_source=add_source, stage=stage)
+
     def forward(self, t, x):  # the t param is needed by the ODE solver.
         if self.nfe > self.opt["max_nfe"]:
             raise MaxNFEException

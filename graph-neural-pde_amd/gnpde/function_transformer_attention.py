@@ -182,7 +182,15 @@ class ODEFuncTransformerAtt(ODEFunc):
         w = g.gather_weights(attention.detach().float())
         return ops.spmm_rhs(g, w, x, rhs=False)
 
+    def rhs_stage(self, t, x, stage):
+        """forward(t, x) with the solver's stage combination fused into the
+        aggregation epilogue (gnpde.integrator, no-grad fixed-grid solvers)."""
+        self._rhs(x, stage)
+
     def forward(self, t, x):  # t is needed when called by the integrator
+        return self._rhs(x, None)
+
+    def _rhs(self, x, stage):
         if self.nfe > self.opt["max_nfe"]:
             raise MaxNFEException
         self.nfe += 1
@@ -194,7 +202,8 @@ class ODEFuncTransformerAtt(ODEFunc):
         if add_source and self.x0 is None:
             raise RuntimeError("ODEFuncTransformerAtt: add_source needs x0 (ODEblock.set_x0)")
         kw = dict(x0=self.x0 if add_source else None, alpha=self.alpha_train.detach(), beta=self.beta_train.detach(),
-                  rhs=True, alpha_sigmoid=not self.opt.get('no_alpha_sigmoid', False), add_source=add_source)
+                  rhs=True, alpha_sigmoid=not self.opt.get('no_alpha_sigmoid', False), add_source=add_source,
+                  stage=stage)
         if lay.is_uniform(norm_idx):
             return ops.spmm_rhs(g, lay.uniform_weights(g), x, **kw)
         ns, m, rl = lay.scores_and_stats(g, x, norm_idx)

@@ -55,9 +55,13 @@ ADAPTIVE_METHODS = ('dopri5',)
 
 
 class _Combine(object):
-    """y0 + scale * sum_j c_j k_j on the device (fused HIP pass)."""
+    """y0 + scale * sum_j c_j k_j on the device (fused HIP pass).  When autograd
+    has to see the combination (grad enabled and an operand requires grad) it
+    is written with torch ops so gradients flow through the solver."""
 
     def __call__(self, y0, ks, coefs, scale):
+        if torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in [y0] + list(ks)):
+            return _torch_combine(y0, ks, coefs, scale)
         return ops.rk_combine(y0, ks, coefs, scale).view(ks[0].shape)
 
 
@@ -110,8 +114,57 @@ def _fixed_step(method, func, t0, dt, t1, y0, combine):
     raise ValueError(method)
 
 
+def _fusable(func, y0, combine):
+    """The RHS can emit the stage combinations itself (gnpde ODEFuncs, no autograd)."""
+    return (isinstance(combine, _Combine) and hasattr(func, 'rhs_stage') and y0.is_cuda and
+            y0.dtype == torch.float32 and not torch.is_grad_enabled())
+
+
+def _fused_step(method, func, t0, dt, t1, y0, ws):
+    """One grid step with the stage combinations fused into the RHS epilogues
+    (gnpde_stage_epilogue_t): same arithmetic as _fixed_step, ~7 fewer passes
+    over the state per rk4 step and no separate combine launches."""
+    y0 = y0.contiguous()
+    if method == 'euler':
+        y1 = torch.empty_like(y0)
+        func.rhs_stage(t0, y0, ops.Stage(outs=[(y1, y0, 1.0, dt, [])]))
+        return y1
+    if method == 'midpoint':
+        ym = ws.get('a', y0)
+        y1 = torch.empty_like(y0)
+        func.rhs_stage(t0, y0, ops.Stage(outs=[(ym, y0, 1.0, 0.5 * dt, [])]))
+        func.rhs_stage(t0 + 0.5 * dt, ym, ops.Stage(outs=[(y1, y0, 1.0, dt, [])]))
+        return y1
+    if method == 'rk4':  # rk4_alt_step_func (3/8 rule) with a running accumulator
+        ya, yb, yc, k1 = ws.get('a', y0), ws.get('b', y0), ws.get('c', y0), ws.get('k1', y0)
+        acc = torch.empty_like(y0)
+        # k1 = f(y0):  ya = y0 + dt/3 k1;  acc = y0 + dt/8 k1
+        func.rhs_stage(t0, y0, ops.Stage(f_out=k1, outs=[(ya, y0, 1.0, dt / 3.0, []), (acc, y0, 1.0, dt * 0.125, [])]))
+        # k2 = f(ya):  yb = y0 + dt (k2 - k1/3);  acc += 3dt/8 k2
+        func.rhs_stage(t0 + dt / 3.0, ya, ops.Stage(outs=[(yb, y0, 1.0, dt, [(k1, -dt / 3.0)]),
+                                                          (acc, acc, 1.0, dt * 0.375, [])]))
+        # k3 = f(yb):  yc = y0 + dt (k1 - k2 + k3) = 2 y0 - yb + 2dt/3 k1 + dt k3;  acc += 3dt/8 k3
+        func.rhs_stage(t0 + dt * 2.0 / 3.0, yb, ops.Stage(outs=[(yc, yb, -1.0, dt, [(y0, 2.0), (k1, dt * 2.0 / 3.0)]),
+                                                                (acc, acc, 1.0, dt * 0.375, [])]))
+        # k4 = f(yc):  y1 = acc + dt/8 k4
+        func.rhs_stage(t1, yc, ops.Stage(outs=[(acc, acc, 1.0, dt * 0.125, [])]))
+        return acc
+    raise ValueError(method)
+
+
+class _Workspace(dict):
+    def get(self, name, like):
+        t = dict.get(self, name)
+        if t is None or t.shape != like.shape or t.device != like.device:
+            t = torch.empty_like(like, memory_format=torch.contiguous_format)
+            self[name] = t
+        return t
+
+
 def odeint_fixed(func, y0, t, method, step_size=None, combine=None):
     combine = combine or _Combine()
+    fused = _fusable(func, y0, combine)
+    ws = _Workspace()
     grid = t if step_size is None else fixed_grid(t, step_size)
     if not (bool(grid[0] == t[0]) and bool(grid[-1] == t[-1])):
         raise AssertionError("time grid does not cover t")
@@ -122,7 +175,8 @@ def odeint_fixed(func, y0, t, method, step_size=None, combine=None):
     yc = y0
     for ta, tb in zip(grid_h[:-1], grid_h[1:]):
         dt = tb - ta
-        y1 = _fixed_step(method, func, ta, dt, tb, yc, combine)
+        y1 = _fused_step(method, func, ta, dt, tb, yc, ws) if fused else _fixed_step(method, func, ta, dt, tb, yc,
+                                                                                      combine)
         while j < len(t_h) and tb >= t_h[j]:
             solution.append(_linear_interp(ta, tb, yc, y1, t_h[j]))
             j += 1

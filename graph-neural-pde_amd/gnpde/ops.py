@@ -199,12 +199,57 @@ def _scalar(t, name, dev):
     return t.reshape(1).contiguous()
 
 
+class Stage(object):
+    """Fused Runge-Kutta stage outputs of one RHS evaluation (gnpde_stage_epilogue_t):
+    ``f_out`` receives f (optional); each entry of ``outs`` is
+    (out, base, cb, cf, [(k_j, c_j), ...]) meaning out = cb*base + cf*f + sum_j c_j*k_j.
+    ``base`` may be None, the RHS input x, or ``out`` itself (in place).  No
+    output may alias the RHS input."""
+
+    def __init__(self, f_out=None, outs=()):
+        self.f_out = f_out
+        self.outs = list(outs)
+
+    def tensors(self):
+        ts = [self.f_out] if self.f_out is not None else []
+        for out, base, _cb, _cf, ks in self.outs:
+            ts.append(out)
+            if base is not None:
+                ts.append(base)
+            ts.extend(k for k, _ in ks)
+        return ts
+
+    def struct(self, x_input):
+        if len(self.outs) > _lib.STAGE_MAX_OUT:
+            raise ValueError("at most %d stage outputs" % _lib.STAGE_MAX_OUT)
+        st = _lib.StageEpilogue()
+        st.f_out = self.f_out.data_ptr() if self.f_out is not None else None
+        st.n_out = len(self.outs)
+        for i, (out, base, cb, cf, ks) in enumerate(self.outs):
+            if len(ks) > _lib.STAGE_MAX_K:
+                raise ValueError("at most %d k terms per stage output" % _lib.STAGE_MAX_K)
+            if out.data_ptr() == x_input.data_ptr():
+                raise ValueError("a stage output may not alias the RHS input")
+            o = st.o[i]
+            o.out = out.data_ptr()
+            o.base = base.data_ptr() if base is not None else None
+            o.cb = float(cb)
+            o.cf = float(cf)
+            o.nk = len(ks)
+            for j, (k, c) in enumerate(ks):
+                o.k[j] = k.data_ptr()
+                o.c[j] = float(c)
+        return st
+
+
 def spmm_rhs(g, w_csr, x, x0=None, alpha=None, beta=None, rhs=True, alpha_sigmoid=True, add_source=False,
-             out=None, transpose=False):
+             out=None, transpose=False, stage=None):
     """K1: f = a*(A x - x) [+ b*x0] (or A x with rhs=False).  x [B,N,C] fp32.
 
     transpose=True aggregates over the CSC instead (A^T x; ``w_csr`` must then
-    be in CSC order) — the backward of the RHS with respect to x."""
+    be in CSC order) — the backward of the RHS with respect to x.
+    stage: a ``Stage`` -> the fused Runge-Kutta outputs are written instead of f
+    (returns None)."""
     shape = x.shape
     xr = _rows(x, "x")
     C = xr.shape[1]
@@ -216,15 +261,22 @@ def spmm_rhs(g, w_csr, x, x0=None, alpha=None, beta=None, rhs=True, alpha_sigmoi
         raise ValueError("spmm_rhs: alpha required")
     b = _scalar(beta, "beta", dev) if add_source else None
     x0r = _rows(x0, "x0") if add_source else None
-    if out is None:
+    st = None
+    if stage is not None:
+        for t in stage.tensors():
+            _require_gpu(t, "stage tensor", torch.float32)
+            if not t.is_contiguous() or t.numel() != xr.numel():
+                raise ValueError("stage tensors must be contiguous and shaped like x")
+        st = ctypes.byref(stage.struct(xr))
+    elif out is None:
         out = torch.empty_like(xr)
     grouped = g.csc if transpose else g.csr
     plan = grouped.plan
     partials = torch.empty(plan.n_slots * C, dtype=torch.float32, device=dev) if plan.n_slots else None
     _lib.call("gnpde_spmm_rhs_f32", _ptr(plan.items), plan.n_items, _ptr(plan.heavy), plan.n_heavy, _ptr(grouped.col),
               _ptr(w_csr), C, _ptr(xr), C, _ptr(x0r), C, _ptr(a), _ptr(b), _flags(rhs, alpha_sigmoid, add_source),
-              _ptr(out), C, _ptr(partials), _stream(dev))
-    return out.view(shape)
+              _ptr(out), C, _ptr(partials), st, _stream(dev))
+    return None if stage is not None else out.view(shape)
 
 
 # --------------------------------------------------------------------------- attention
@@ -334,12 +386,12 @@ def attn_weights(g, ns, m, rl, norm_idx):
 
 
 def attn_rhs(g, ns, m, rl, norm_idx, x, x0=None, alpha=None, beta=None, rhs=True, alpha_sigmoid=True,
-             add_source=False, out=None):
+             add_source=False, out=None, stage=None):
     """K3: f = a*(A_att x - x) [+ b x0], A_att = head-mean softmax weights
     (edge-parallel weights, then the K1 gather-aggregate with the fused epilogue)."""
     w = attn_weights(g, ns, m, rl, norm_idx)
     return spmm_rhs(g, w, x, x0=x0, alpha=alpha, beta=beta, rhs=rhs, alpha_sigmoid=alpha_sigmoid,
-                    add_source=add_source, out=out)
+                    add_source=add_source, out=out, stage=stage)
 
 
 def edge_attention(g, ns, m, rl, norm_idx):

@@ -107,18 +107,49 @@ int gnpde_plan_build(const int32_t* rowptr, int64_t R, int32_t chunk,
                      void* workspace, size_t workspace_bytes, void* stream);
 size_t gnpde_plan_workspace_bytes(int64_t R);
 
+/* ---------------------------------------------------------------- fused solver epilogue
+ * Optional stage outputs of the RHS kernels, so a Runge-Kutta stage combination
+ * y0 + dt*sum_j b_j k_j is produced by the same pass that computes k_i (no
+ * separate read of k_i, no extra launch).  With f = the RHS value of row r:
+ *   f_out[r]    = f                                       (f_out may be NULL)
+ *   o[i].out[r] = cb*base[r] + cf*f + sum_{j<nk} c[j]*k[j][r]   for i < n_out
+ * base may be NULL (0), equal to the RHS input x (the row already read by the
+ * epilogue is reused) or equal to o[i].out (in-place accumulation).  Every
+ * array has the leading dimension ldf of the RHS output.  No output may alias
+ * the RHS input x (other rows of x are still being gathered).                */
+#define GNPDE_STAGE_MAX_OUT 2
+#define GNPDE_STAGE_MAX_K 2
+typedef struct {
+  float* out;
+  const float* base;
+  float cb;
+  float cf;
+  int nk;
+  const float* k[GNPDE_STAGE_MAX_K];
+  float c[GNPDE_STAGE_MAX_K];
+} gnpde_stage_out_t;
+
+typedef struct {
+  float* f_out;
+  int n_out;
+  gnpde_stage_out_t o[GNPDE_STAGE_MAX_OUT];
+} gnpde_stage_epilogue_t;
+
 /* ---------------------------------------------------------------- K1: SpMM RHS
  * ax[r,:] = sum_{p in row r} w[p] * x[col[p],:]
  * f[r,:]  = ax                                  (flags & 1 == 0)
  *         = a*(ax - x[r,:]) [+ b*x0[r,:]]        (GNPDE_EPI_RHS)
  * a = *alpha or sigmoid(*alpha), b = *beta: device scalars (no host sync).
  * partials: n_slots*C floats of scratch (NULL if n_slots == 0).
+ * stage: NULL -> f[r,:] is stored to f; otherwise the stage epilogue above
+ * decides what is stored (f is ignored).
  * Replaces function_laplacian_diffusion.py:39-77 per RHS evaluation.        */
 int gnpde_spmm_rhs_f32(const int32_t* items, int64_t n_items, const int32_t* heavy, int64_t n_heavy,
                        const int32_t* col, const float* w, int64_t C,
                        const float* x, int64_t ldx, const float* x0, int64_t ldx0,
                        const float* alpha, const float* beta, int flags,
-                       float* f, int64_t ldf, float* partials, void* stream);
+                       float* f, int64_t ldf, float* partials, const gnpde_stage_epilogue_t* stage,
+                       void* stream);
 
 /* ---------------------------------------------------------------- attention
  * Node-level projection (MFMA, v_mfma_f32_32x32x2_f32):

@@ -52,9 +52,14 @@ def test_errors_are_reported_not_raised():
     vp = ctypes.c_void_p
     # C = 0 -> EINVAL before any launch
     rc = lib.gnpde_spmm_rhs_f32(vp(0), 0, vp(0), 0, vp(0), vp(0), 0, vp(0), 0, vp(0), 0, vp(0), vp(0), 0, vp(0), 0,
-                                vp(0), vp(0))
+                                vp(0), None, vp(0))
     assert rc == -1
     assert b"C must be" in lib.gnpde_last_error()
+    st = _lib.StageEpilogue()
+    st.n_out = 3
+    rc = lib.gnpde_spmm_rhs_f32(vp(0), 0, vp(0), 0, vp(0), vp(0), 4, vp(16), 4, vp(0), 0, vp(0), vp(0), 0, vp(0), 4,
+                                vp(0), ctypes.byref(st), vp(0))
+    assert rc == -1 and b"n_out" in lib.gnpde_last_error()
     rc = lib.gnpde_linear_f32(vp(0), 10, 4, 4, vp(0), vp(0), 8, 8, vp(0), 8, vp(0), 0, vp(0))
     assert rc == -1 and b"NULL" in lib.gnpde_last_error()
     rc = lib.gnpde_csr_build(vp(0), 1, 10, 5, 2, vp(0), vp(0), vp(0), vp(0), 0, vp(0))
@@ -72,6 +77,13 @@ def test_python_wrapper_raises_with_message():
                   ctypes.c_void_p(0), 8, ctypes.c_void_p(0), 0, ctypes.c_void_p(0))
 
 
+def test_stage_struct_layout_matches_header():
+    # gnpde_stage_out_t: out, base (8 B each), cb, cf, nk (4 B each), k[2] (8 B, aligned), c[2]
+    assert ctypes.sizeof(_lib.StageOut) == 8 + 8 + 4 + 4 + 4 + 4 + 16 + 8
+    assert _lib.StageOut.k.offset == 32
+    assert ctypes.sizeof(_lib.StageEpilogue) == 8 + 8 + 2 * ctypes.sizeof(_lib.StageOut)
+
+
 def test_workspace_size_queries():
     lib = _lib.load()
     assert lib.gnpde_csr_workspace_bytes(1, 1000, 100) >= 3 * 4000
@@ -81,3 +93,20 @@ def test_workspace_size_queries():
 
 def test_package_exposes_library_path():
     assert gnpde.native_library_path().endswith("libgnpde.so")
+
+
+def test_c_header_struct_layout_with_gcc(tmp_path):
+    """The ctypes mirror of gnpde_stage_epilogue_t matches what a C compiler lays out."""
+    import shutil
+    import subprocess
+    if shutil.which("gcc") is None:
+        pytest.skip("gcc not available")
+    src = tmp_path / "layout.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "gnpde.h"\nint main(void){'
+                   'printf("%zu %zu %zu %zu\\n", sizeof(gnpde_stage_out_t), offsetof(gnpde_stage_out_t, k),'
+                   'offsetof(gnpde_stage_out_t, c), sizeof(gnpde_stage_epilogue_t));return 0;}\n')
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    got = [int(v) for v in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()]
+    assert got == [ctypes.sizeof(_lib.StageOut), _lib.StageOut.k.offset, _lib.StageOut.c.offset,
+                   ctypes.sizeof(_lib.StageEpilogue)]

@@ -280,6 +280,41 @@ def test_rk_combine():
     assert torch.allclose(err, 2.0 * (0.1 * ks[0] - 0.5 * ks[1] + 0.25 * ks[2]), atol=1e-5)
 
 
+# ---------------------------------------------------------------- fused stage epilogues
+@pytest.mark.parametrize("C", [7, 162, 128])
+@pytest.mark.parametrize("method", ["euler", "midpoint", "rk4"])
+def test_fused_stage_epilogue_matches_unfused(C, method):
+    from gnpde import integrator as gi
+    N, E = 2500, 30000
+    ei = hub_graph(N, E, seed=C)
+    rng = np.random.default_rng(C)
+    w = rng.uniform(0.1, 1, size=(1, E)).astype(np.float32)
+    func = gnpde.LaplacianODEFunc(C, C, dict(OPT, hidden_dim=C, add_source=True), DEV).to(DEV)
+    with torch.no_grad():
+        func.alpha_train.fill_(0.2)
+        func.beta_train.fill_(0.4)
+    func.edge_index, func.edge_weight = T(ei), T(w)
+    x = torch.randn(1, N, C, device=DEV)
+    func.x0 = torch.randn(1, N, C, device=DEV)
+    with torch.no_grad():
+        ws = gi._Workspace()
+        y_f = x
+        y_u = x
+        for i in range(3):
+            y_f = gi._fused_step(method, func, 0.1 * i, 0.1, 0.1 * (i + 1), y_f, ws)
+            y_u = gi._fixed_step(method, func, 0.1 * i, 0.1, 0.1 * (i + 1), y_u, gi._Combine())
+    assert (y_f - y_u).abs().max() / y_u.abs().max() < 2e-6
+
+
+def test_stage_output_may_not_alias_input():
+    N, C = 100, 8
+    g = ops.GraphCSR(T(np.zeros((1, 2, 5), np.int64)), N)
+    x = torch.randn(1, N, C, device=DEV)
+    with pytest.raises(ValueError, match="alias"):
+        ops.spmm_rhs(g, torch.ones(5, device=DEV), x, alpha=torch.tensor(0.0, device=DEV),
+                     stage=ops.Stage(outs=[(x, x, 1.0, 0.1, [])]))
+
+
 # ---------------------------------------------------------------- ODE blocks end to end
 def _prep_oracle(ei, N, fill=1.0):
     eis, ws = O.get_rw_adj(ei, norm_dim=1, fill_value=fill, num_nodes=N)
