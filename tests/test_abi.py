@@ -60,6 +60,15 @@ def test_errors_are_reported_not_raised():
     rc = lib.gnpde_spmm_rhs_f32(vp(0), 0, vp(0), 0, vp(0), vp(0), 4, vp(16), 4, vp(0), 0, vp(0), vp(0), 0, vp(0), 4,
                                 vp(0), ctypes.byref(st), vp(0))
     assert rc == -1 and b"n_out" in lib.gnpde_last_error()
+    # a well-formed stage struct passes validation (no items -> nothing launched):
+    # catches a library built against a stale header layout
+    st = _lib.StageEpilogue()
+    st.n_out = 1
+    st.o[0].out, st.o[0].cb, st.o[0].cf, st.o[0].nk = 4096, 1.0, 0.5, 1
+    st.o[0].k[0], st.o[0].c[0] = 8192, 2.0
+    rc = lib.gnpde_spmm_rhs_f32(vp(0), 0, vp(0), 0, vp(0), vp(0), 4, vp(16), 4, vp(0), 0, vp(32), vp(0), 1, vp(0), 4,
+                                vp(0), ctypes.byref(st), vp(0))
+    assert rc == 0, lib.gnpde_last_error()
     rc = lib.gnpde_linear_f32(vp(0), 10, 4, 4, vp(0), vp(0), 8, 8, vp(0), 8, vp(0), 0, vp(0))
     assert rc == -1 and b"NULL" in lib.gnpde_last_error()
     rc = lib.gnpde_csr_build(vp(0), 1, 10, 5, 2, vp(0), vp(0), vp(0), vp(0), 0, vp(0))
