@@ -16,20 +16,40 @@ struct PlainWeights {
 };
 
 // ------------------------------------------------------------------ aggregation kernel
-// Lane layout: lane = g*GL + gl; GROUPS = 64/GL edges are gathered side by side,
-// each by a group of GL lanes covering the C columns with VEC-wide loads
-// (NCH column passes).  U edges per group are in flight per iteration.
-template <int VEC, int GL, int NCH, int U, class WP>
+// Lane layout: RPW row slots of SL = 64/RPW lanes per wavefront (one plan item
+// each); inside a slot lane = g*GL + gl: G = SL/GL edges are gathered side by
+// side, each by a group of GL lanes covering the C columns with VEC-wide loads
+// (NCH column passes); U edges per group are in flight per iteration.  The
+// epilogue operands (x_r, x0_r, stage inputs) are loaded before the gathers
+// when NCH <= 2 (PRE) so their latency overlaps the aggregation.
+template <int VEC, int GL, int NCH, int U, int RPW, class WP>
 __global__ __launch_bounds__(256) void agg_kernel(const int4* __restrict__ items, int n_items,
                                                    const int* __restrict__ col, WP wp, int C, Epi ep,
                                                    float* __restrict__ partials) {
-  constexpr int G = kWave / GL;
+  constexpr int SL = kWave / RPW;
+  constexpr int G = SL / GL;
+  constexpr bool PRE = NCH <= 2;
   const int lane = threadIdx.x & 63;
+  const int rs = lane / SL, sl = lane % SL;
+  const int g = sl / GL, gl = sl % GL;
   const int wid = uniform(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
-  if (wid >= n_items) return;
-  const int4 it = items[wid];
-  const int row = uniform(it.x), beg = uniform(it.y), end = uniform(it.z), slot = uniform(it.w);
-  const int g = lane / GL, gl = lane % GL;
+  const int item = wid * RPW + rs;
+  if (wid * RPW >= n_items) return;
+  const bool live = item < n_items;
+  const int4 it = live ? items[item] : make_int4(0, 0, 0, -1);
+  const int row = it.x, beg = it.y, end = it.z, slot = it.w;
+  const bool owner = live && slot < 0 && g == 0;
+
+  EpiPre<VEC> pre[PRE ? NCH : 1];
+  if constexpr (PRE) {
+    if (owner) {
+#pragma unroll
+      for (int ch = 0; ch < NCH; ++ch) {
+        const int cc = (ch * GL + gl) * VEC;
+        if (cc < C) epi_prefetch<VEC>(ep, row, cc, pre[ch]);
+      }
+    }
+  }
 
   float acc[NCH][VEC];
 #pragma unroll
@@ -37,13 +57,13 @@ __global__ __launch_bounds__(256) void agg_kernel(const int4* __restrict__ items
 #pragma unroll
     for (int t = 0; t < VEC; ++t) acc[ch][t] = 0.f;
 
-  for (int e0 = beg; e0 < end; e0 += kWave) {
-    const int n = min(kWave, end - e0);
+  for (int e0 = beg; e0 < end; e0 += SL) {
+    const int n = min(SL, end - e0);
     int mc = 0;
     float mw = 0.f;
-    if (lane < n) {
-      mc = col[e0 + lane];
-      mw = wp(row, e0 + lane, mc);
+    if (sl < n) {
+      mc = col[e0 + sl];
+      mw = wp(row, e0 + sl, mc);
     }
     for (int j = 0; j < n; j += G * U) {
       float v[U][NCH][VEC];
@@ -51,9 +71,9 @@ __global__ __launch_bounds__(256) void agg_kernel(const int4* __restrict__ items
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int jj = j + u * G + g;
-        const int sl = jj < n ? jj : 0;
-        const int c = __shfl(mc, sl);
-        const float wsl = __shfl(mw, sl);
+        const int src = rs * SL + (jj < n ? jj : 0);
+        const int c = __shfl(mc, src);
+        const float wsl = __shfl(mw, src);
         ww[u] = jj < n ? wsl : 0.f;
         const float* __restrict__ xr = ep.x + (int64_t)c * ep.ldx;
 #pragma unroll
@@ -75,15 +95,15 @@ __global__ __launch_bounds__(256) void agg_kernel(const int4* __restrict__ items
           for (int t = 0; t < VEC; ++t) acc[ch][t] = fmaf(ww[u], v[u][ch][t], acc[ch][t]);
     }
   }
-  // combine the G edge groups
+  // combine the G edge groups of each slot
 #pragma unroll
-  for (int o = GL; o < kWave; o <<= 1)
+  for (int o = GL; o < SL; o <<= 1)
 #pragma unroll
     for (int ch = 0; ch < NCH; ++ch)
 #pragma unroll
       for (int t = 0; t < VEC; ++t) acc[ch][t] += __shfl_xor(acc[ch][t], o);
 
-  if (g != 0) return;
+  if (!live || g != 0) return;
   if (slot >= 0) {
 #pragma unroll
     for (int ch = 0; ch < NCH; ++ch) {
@@ -97,7 +117,12 @@ __global__ __launch_bounds__(256) void agg_kernel(const int4* __restrict__ items
 #pragma unroll
   for (int ch = 0; ch < NCH; ++ch) {
     const int cc = (ch * GL + gl) * VEC;
-    if (cc < C) epilogue_store<VEC>(ep, row, cc, acc[ch], a, b);
+    if (cc < C) {
+      if constexpr (PRE)
+        epi_finish<VEC>(ep, row, cc, acc[ch], a, b, pre[ch]);
+      else
+        epilogue_store<VEC>(ep, row, cc, acc[ch], a, b);
+    }
   }
 }
 
@@ -142,12 +167,13 @@ __global__ __launch_bounds__(256) void agg_fixup_kernel(const int4* __restrict__
   }
 }
 
-template <int VEC, int GL, int NCH, int U, class WP>
+template <int VEC, int GL, int NCH, int U, int RPW, class WP>
 static int launch_agg_cfg(const int4* items, int64_t n_items, const int4* heavy, int64_t n_heavy, const int* col,
                           const WP& wp, int C, const Epi& ep, float* partials, hipStream_t s) {
   if (n_items > 0) {
-    const int64_t grid = ceil_div(n_items, kWavesPerBlock);
-    agg_kernel<VEC, GL, NCH, U, WP><<<(unsigned)grid, kBlock, 0, s>>>(items, (int)n_items, col, wp, C, ep, partials);
+    const int64_t grid = ceil_div(n_items, (int64_t)kWavesPerBlock * RPW);
+    agg_kernel<VEC, GL, NCH, U, RPW, WP><<<(unsigned)grid, kBlock, 0, s>>>(items, (int)n_items, col, wp, C, ep,
+                                                                           partials);
     GNPDE_LAUNCH_CHECK();
   }
   if (n_heavy > 0) {
@@ -158,16 +184,29 @@ static int launch_agg_cfg(const int4* items, int64_t n_items, const int4* heavy,
   return GNPDE_OK;
 }
 
+// Experiment knob (not part of the ABI contract): GNPDE_AGG_VARIANT selects an
+// alternative lane geometry for the dominant 32-lane (C = 128 fp32) case.
+int agg_variant();
+
 template <int VEC, class WP>
 static int launch_agg_vec(const int4* items, int64_t n_items, const int4* heavy, int64_t n_heavy, const int* col,
                           const WP& wp, int C, const Epi& ep, float* partials, hipStream_t s) {
   const int lanes = (int)ceil_div(C, VEC);
-  if (lanes <= 16) return launch_agg_cfg<VEC, 16, 1, 4>(items, n_items, heavy, n_heavy, col, wp, C, ep, partials, s);
-  if (lanes <= 32) return launch_agg_cfg<VEC, 32, 1, 4>(items, n_items, heavy, n_heavy, col, wp, C, ep, partials, s);
-  if (lanes <= 64) return launch_agg_cfg<VEC, 64, 1, 4>(items, n_items, heavy, n_heavy, col, wp, C, ep, partials, s);
-  if (lanes <= 128) return launch_agg_cfg<VEC, 64, 2, 2>(items, n_items, heavy, n_heavy, col, wp, C, ep, partials, s);
-  if (lanes <= 256) return launch_agg_cfg<VEC, 64, 4, 2>(items, n_items, heavy, n_heavy, col, wp, C, ep, partials, s);
-  if (lanes <= 512) return launch_agg_cfg<VEC, 64, 8, 1>(items, n_items, heavy, n_heavy, col, wp, C, ep, partials, s);
+  if (lanes <= 16) return launch_agg_cfg<VEC, 16, 1, 4, 1>(items, n_items, heavy, n_heavy, col, wp, C, ep, partials, s);
+  if (lanes <= 32) {
+    switch (agg_variant()) {
+      case 1: return launch_agg_cfg<VEC, 32, 1, 4, 2>(items, n_items, heavy, n_heavy, col, wp, C, ep, partials, s);
+      case 2: return launch_agg_cfg<VEC, 32, 1, 2, 1>(items, n_items, heavy, n_heavy, col, wp, C, ep, partials, s);
+      case 3: return launch_agg_cfg<VEC, 16, 2, 2, 1>(items, n_items, heavy, n_heavy, col, wp, C, ep, partials, s);
+      case 4: return launch_agg_cfg<VEC, 32, 1, 8, 1>(items, n_items, heavy, n_heavy, col, wp, C, ep, partials, s);
+      case 5: return launch_agg_cfg<VEC, 16, 2, 2, 2>(items, n_items, heavy, n_heavy, col, wp, C, ep, partials, s);
+      default: return launch_agg_cfg<VEC, 32, 1, 4, 1>(items, n_items, heavy, n_heavy, col, wp, C, ep, partials, s);
+    }
+  }
+  if (lanes <= 64) return launch_agg_cfg<VEC, 64, 1, 4, 1>(items, n_items, heavy, n_heavy, col, wp, C, ep, partials, s);
+  if (lanes <= 128) return launch_agg_cfg<VEC, 64, 2, 2, 1>(items, n_items, heavy, n_heavy, col, wp, C, ep, partials, s);
+  if (lanes <= 256) return launch_agg_cfg<VEC, 64, 4, 2, 1>(items, n_items, heavy, n_heavy, col, wp, C, ep, partials, s);
+  if (lanes <= 512) return launch_agg_cfg<VEC, 64, 8, 1, 1>(items, n_items, heavy, n_heavy, col, wp, C, ep, partials, s);
   set_error("aggregate: C=%d too wide (max %d)", C, 512 * VEC);
   return GNPDE_EUNSUPPORTED;
 }

@@ -112,22 +112,48 @@ __device__ __forceinline__ float epi_alpha(const Epi& e) {
   return (e.flags & GNPDE_ALPHA_SIGMOID) ? 1.0f / (1.0f + expf(-a)) : a;
 }
 
+// Epilogue operands of one row slice, loaded ahead of the aggregation so their
+// latency overlaps the gathers (they depend only on the row).
+template <int VEC>
+struct EpiPre {
+  float xr[VEC];
+  float x0r[VEC];
+  float base[GNPDE_STAGE_MAX_OUT][VEC];
+  float kv[GNPDE_STAGE_MAX_OUT][GNPDE_STAGE_MAX_K][VEC];
+};
+
+template <int VEC>
+__device__ __forceinline__ void epi_prefetch(const Epi& e, int64_t row, int cc, EpiPre<VEC>& p) {
+  const bool need_x = (e.flags & GNPDE_EPI_RHS) != 0;
+  if (need_x) load_vec<VEC>(e.x + row * e.ldx + cc, p.xr);
+  if (e.flags & GNPDE_ADD_SOURCE) load_vec<VEC>(e.x0 + row * e.ldx0 + cc, p.x0r);
+  if (!e.has_stage) return;
+  const int64_t off = row * e.ldf + cc;
+#pragma unroll
+  for (int i = 0; i < GNPDE_STAGE_MAX_OUT; ++i) {
+    if (i < e.st.n_out) {
+      const gnpde_stage_out_t& so = e.st.o[i];
+      if (so.base != nullptr && !(need_x && so.base == e.x && e.ldx == e.ldf)) load_vec<VEC>(so.base + off, p.base[i]);
+#pragma unroll
+      for (int j = 0; j < GNPDE_STAGE_MAX_K; ++j)
+        if (j < so.nk) load_vec<VEC>(so.k[j] + off, p.kv[i][j]);
+    }
+  }
+}
+
 // f = a*(ax - x) [+ b*x0]  (function_laplacian_diffusion.py:69-77) or f = ax,
 // then either store f or emit the fused Runge-Kutta stage outputs.
 template <int VEC>
-__device__ __forceinline__ void epilogue_store(const Epi& e, int64_t row, int cc, const float (&ax)[VEC],
-                                               float a, float b) {
-  float o[VEC], xr[VEC];
+__device__ __forceinline__ void epi_finish(const Epi& e, int64_t row, int cc, const float (&ax)[VEC], float a,
+                                           float b, const EpiPre<VEC>& p) {
+  float o[VEC];
   const bool need_x = (e.flags & GNPDE_EPI_RHS) != 0;
-  if (need_x) load_vec<VEC>(e.x + row * e.ldx + cc, xr);
   if (need_x) {
 #pragma unroll
-    for (int t = 0; t < VEC; ++t) o[t] = a * (ax[t] - xr[t]);
+    for (int t = 0; t < VEC; ++t) o[t] = a * (ax[t] - p.xr[t]);
     if (e.flags & GNPDE_ADD_SOURCE) {
-      float x0r[VEC];
-      load_vec<VEC>(e.x0 + row * e.ldx0 + cc, x0r);
 #pragma unroll
-      for (int t = 0; t < VEC; ++t) o[t] = o[t] + b * x0r[t];
+      for (int t = 0; t < VEC; ++t) o[t] = o[t] + b * p.x0r[t];
     }
   } else {
 #pragma unroll
@@ -139,7 +165,9 @@ __device__ __forceinline__ void epilogue_store(const Epi& e, int64_t row, int cc
   }
   const int64_t off = row * e.ldf + cc;
   if (e.st.f_out) store_vec<VEC>(e.st.f_out + off, o);
-  for (int i = 0; i < e.st.n_out; ++i) {
+#pragma unroll
+  for (int i = 0; i < GNPDE_STAGE_MAX_OUT; ++i) {
+    if (i >= e.st.n_out) break;
     const gnpde_stage_out_t& so = e.st.o[i];
     float r[VEC];
     if (so.base == nullptr) {
@@ -147,22 +175,30 @@ __device__ __forceinline__ void epilogue_store(const Epi& e, int64_t row, int cc
       for (int t = 0; t < VEC; ++t) r[t] = 0.f;
     } else if (need_x && so.base == e.x && e.ldx == e.ldf) {
 #pragma unroll
-      for (int t = 0; t < VEC; ++t) r[t] = so.cb * xr[t];
+      for (int t = 0; t < VEC; ++t) r[t] = so.cb * p.xr[t];
     } else {
-      load_vec<VEC>(so.base + off, r);
 #pragma unroll
-      for (int t = 0; t < VEC; ++t) r[t] = so.cb * r[t];
+      for (int t = 0; t < VEC; ++t) r[t] = so.cb * p.base[i][t];
     }
-    for (int j = 0; j < so.nk; ++j) {
-      float kv[VEC];
-      load_vec<VEC>(so.k[j] + off, kv);
 #pragma unroll
-      for (int t = 0; t < VEC; ++t) r[t] = fmaf(so.c[j], kv[t], r[t]);
+    for (int j = 0; j < GNPDE_STAGE_MAX_K; ++j) {
+      if (j < so.nk) {
+#pragma unroll
+        for (int t = 0; t < VEC; ++t) r[t] = fmaf(so.c[j], p.kv[i][j][t], r[t]);
+      }
     }
 #pragma unroll
     for (int t = 0; t < VEC; ++t) r[t] = fmaf(so.cf, o[t], r[t]);
     store_vec<VEC>(so.out + off, r);
   }
+}
+
+template <int VEC>
+__device__ __forceinline__ void epilogue_store(const Epi& e, int64_t row, int cc, const float (&ax)[VEC], float a,
+                                               float b) {
+  EpiPre<VEC> p;
+  epi_prefetch<VEC>(e, row, cc, p);
+  epi_finish<VEC>(e, row, cc, ax, a, b, p);
 }
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }

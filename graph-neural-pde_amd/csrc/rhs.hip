@@ -4,7 +4,17 @@
 #include "aggregate.hpp"
 #include "scores.hpp"
 
+#include <cstdlib>
+
 namespace gnpde {
+
+int agg_variant() {
+  static const int v = [] {
+    const char* e = std::getenv("GNPDE_AGG_VARIANT");
+    return e ? std::atoi(e) : 0;
+  }();
+  return v;
+}
 
 // ------------------------------------------------------------------ softmax statistics
 // GL lanes per plan item (64/GL items per wavefront).  Every lane keeps an
