@@ -43,6 +43,15 @@ def lap_bytes(N, E, C, add_source=False):
     return 4 * E * C + 8 * N * C + 8 * E + 4 * (N + 1) + (4 * N * C if add_source else 0)
 
 
+def rk4_fused_step_bytes(N, E, C):
+    """Algorithmic bytes of one rk4 step with the stage combinations fused into
+    the four K1 epilogues (gnpde.integrator._fused_step): 4 x (gathers 4EC +
+    indices 8E + rowptr 4(N+1) + input row 4NC) + 15 state passes of 4NC
+    (stage 1 writes ya, acc, k1; stage 2 reads y0, k1, acc, writes yb, acc;
+    stage 3 reads y0, k1, acc, writes yc, acc; stage 4 reads acc, writes acc)."""
+    return 4 * (4 * E * C + 8 * E + 4 * (N + 1) + 4 * N * C) + 15 * 4 * N * C
+
+
 def attn_bytes(N, E, C, att, mode):
     """Algorithmic bytes of one attention RHS.  per_edge: projection
     4NC + 8N*att, stats+aggregation 4N*att + 4E*att + 4EC + 8NC + 4E + 4(N+1);
@@ -63,7 +72,8 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU-baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-attention", action="store_true")
-    p.add_argument("--rhs-only", action="store_true", help="time K RHS calls only (for rocprof runs)")
+    p.add_argument("--rhs-only", action="store_true", help="time K plain RHS calls instead of rk4 steps")
+    p.add_argument("--rhs-plain-reps", type=int, default=20, help="plain-RHS launches timed after the steps")
     return p.parse_args()
 
 
@@ -141,8 +151,34 @@ def main():
     total_rhs = world * args.steps * rhs_per_step
     value = total_rhs / elapsed
     ms_per_step = elapsed * 1e3 / args.steps
-    nbytes = lap_bytes(N, E, C)
+    if args.rhs_only:
+        nbytes = lap_bytes(N, E, C)
+        kname = "agg_kernel<4,32,1,4,1,false,PlainWeights> (+ agg_fixup_kernel<4,32,false>)"
+    else:
+        nbytes = rk4_fused_step_bytes(N, E, C) / 4.0
+        kname = "agg_kernel<4,32,1,4,1,true,PlainWeights> (+ agg_fixup_kernel<4,32,true>): K1 with fused rk4 stage"
     achieved = nbytes / (k1_ms * 1e-3) / 1e9
+
+    # the plain RHS (no fused stage) on the same graph, for the per-RHS roofline
+    plain = None
+    if args.rhs_plain_reps > 0:
+        with torch.no_grad():
+            wc = func.csr_weights(g, w, 'w')
+            out = torch.empty_like(x).view(-1, C)
+            for _ in range(3):
+                orig_spmm(g, wc, x, alpha=func.alpha_train.detach(), out=out)
+            torch.cuda.synchronize()
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(args.rhs_plain_reps):
+                orig_spmm(g, wc, x, alpha=func.alpha_train.detach(), out=out)
+            e.record()
+            torch.cuda.synchronize()
+        pms = s.elapsed_time(e) / args.rhs_plain_reps
+        pb = lap_bytes(N, E, C)
+        plain = {"rhs_ms": round(pms, 4), "achieved": round(pb / (pms * 1e-3) / 1e9, 1),
+                 "frac": round(pb / (pms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "algorithmic_bytes": pb,
+                 "kernel": "agg_kernel<4,32,1,4,1,false,PlainWeights> (+ fixup)"}
 
     traffic = None
     tp = os.path.join(ROOT, "profiles", "k1_traffic.json")
@@ -150,7 +186,7 @@ def main():
         with open(tp) as fh:
             tj = json.load(fh)
         if tj.get("nodes") == N and tj.get("edges") == E and tj.get("dim") == C:
-            traffic = tj.get("hbm_bytes_per_launch")
+            traffic = tj.get("fused_step_launch" if not args.rhs_only else "plain_launch", {}).get("hbm_bytes")
 
     result = {
         "metric": "ODE RHS evals/s (and ms/step) at |E|≈1.2M, d=128; achieved HBM GB/s vs roofline",
@@ -172,8 +208,9 @@ def main():
         "rhs_ms": round(k1_ms, 4),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "kernel": "gnpde_spmm_rhs_f32 (agg_kernel + hub fixup)",
-                     "algorithmic_bytes_per_launch": nbytes},
+                     "kernel": kname, "algorithmic_bytes_per_launch": int(nbytes),
+                     "launch_ms": round(k1_ms, 4), "launches": len(events)},
+        "rhs_plain": plain,
     }
 
     if not args.no_attention and rank == 0:

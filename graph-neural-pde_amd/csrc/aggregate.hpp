@@ -22,7 +22,7 @@ struct PlainWeights {
 // (NCH column passes); U edges per group are in flight per iteration.  The
 // epilogue operands (x_r, x0_r, stage inputs) are loaded before the gathers
 // when NCH <= 2 (PRE) so their latency overlaps the aggregation.
-template <int VEC, int GL, int NCH, int U, int RPW, class WP>
+template <int VEC, int GL, int NCH, int U, int RPW, bool STG, class WP>
 __global__ __launch_bounds__(256) void agg_kernel(const int4* __restrict__ items, int n_items,
                                                    const int* __restrict__ col, WP wp, int C, Epi ep,
                                                    float* __restrict__ partials) {
@@ -46,7 +46,7 @@ __global__ __launch_bounds__(256) void agg_kernel(const int4* __restrict__ items
 #pragma unroll
       for (int ch = 0; ch < NCH; ++ch) {
         const int cc = (ch * GL + gl) * VEC;
-        if (cc < C) epi_prefetch<VEC>(ep, row, cc, pre[ch]);
+        if (cc < C) epi_prefetch<VEC, STG>(ep, row, cc, pre[ch]);
       }
     }
   }
@@ -119,9 +119,9 @@ __global__ __launch_bounds__(256) void agg_kernel(const int4* __restrict__ items
     const int cc = (ch * GL + gl) * VEC;
     if (cc < C) {
       if constexpr (PRE)
-        epi_finish<VEC>(ep, row, cc, acc[ch], a, b, pre[ch]);
+        epi_finish<VEC, STG>(ep, row, cc, acc[ch], a, b, pre[ch]);
       else
-        epilogue_store<VEC>(ep, row, cc, acc[ch], a, b);
+        epilogue_store<VEC, STG>(ep, row, cc, acc[ch], a, b);
     }
   }
 }
@@ -129,7 +129,7 @@ __global__ __launch_bounds__(256) void agg_kernel(const int4* __restrict__ items
 // Hub rows: sum the chunk partials, then the epilogue.  GL lanes cover the
 // columns; the 64/GL lane groups take chunks g, g+G, ... and are combined by a
 // fixed xor tree (deterministic).
-template <int VEC, int GL>
+template <int VEC, int GL, bool STG>
 __global__ __launch_bounds__(256) void agg_fixup_kernel(const int4* __restrict__ heavy, int n_heavy, int C, Epi ep,
                                                          const float* __restrict__ partials) {
   constexpr int G = kWave / GL;
@@ -163,22 +163,27 @@ __global__ __launch_bounds__(256) void agg_fixup_kernel(const int4* __restrict__
     for (int o = GL; o < kWave; o <<= 1)
 #pragma unroll
       for (int t = 0; t < VEC; ++t) s[t] += __shfl_xor(s[t], o);
-    if (g == 0 && live) epilogue_store<VEC>(ep, row, cc, s, a, b);
+    if (g == 0 && live) epilogue_store<VEC, STG>(ep, row, cc, s, a, b);
   }
 }
 
 template <int VEC, int GL, int NCH, int U, int RPW, class WP>
 static int launch_agg_cfg(const int4* items, int64_t n_items, const int4* heavy, int64_t n_heavy, const int* col,
                           const WP& wp, int C, const Epi& ep, float* partials, hipStream_t s) {
+  const unsigned grid = (unsigned)ceil_div(n_items, (int64_t)kWavesPerBlock * RPW);
+  const unsigned gfix = (unsigned)ceil_div(n_heavy, kWavesPerBlock);
   if (n_items > 0) {
-    const int64_t grid = ceil_div(n_items, (int64_t)kWavesPerBlock * RPW);
-    agg_kernel<VEC, GL, NCH, U, RPW, WP><<<(unsigned)grid, kBlock, 0, s>>>(items, (int)n_items, col, wp, C, ep,
-                                                                           partials);
+    if (ep.has_stage)
+      agg_kernel<VEC, GL, NCH, U, RPW, true, WP><<<grid, kBlock, 0, s>>>(items, (int)n_items, col, wp, C, ep, partials);
+    else
+      agg_kernel<VEC, GL, NCH, U, RPW, false, WP><<<grid, kBlock, 0, s>>>(items, (int)n_items, col, wp, C, ep, partials);
     GNPDE_LAUNCH_CHECK();
   }
   if (n_heavy > 0) {
-    const int64_t grid = ceil_div(n_heavy, kWavesPerBlock);
-    agg_fixup_kernel<VEC, GL><<<(unsigned)grid, kBlock, 0, s>>>(heavy, (int)n_heavy, C, ep, partials);
+    if (ep.has_stage)
+      agg_fixup_kernel<VEC, GL, true><<<gfix, kBlock, 0, s>>>(heavy, (int)n_heavy, C, ep, partials);
+    else
+      agg_fixup_kernel<VEC, GL, false><<<gfix, kBlock, 0, s>>>(heavy, (int)n_heavy, C, ep, partials);
     GNPDE_LAUNCH_CHECK();
   }
   return GNPDE_OK;
@@ -197,9 +202,6 @@ static int launch_agg_vec(const int4* items, int64_t n_items, const int4* heavy,
     switch (agg_variant()) {
       case 1: return launch_agg_cfg<VEC, 32, 1, 4, 2>(items, n_items, heavy, n_heavy, col, wp, C, ep, partials, s);
       case 2: return launch_agg_cfg<VEC, 32, 1, 2, 1>(items, n_items, heavy, n_heavy, col, wp, C, ep, partials, s);
-      case 3: return launch_agg_cfg<VEC, 16, 2, 2, 1>(items, n_items, heavy, n_heavy, col, wp, C, ep, partials, s);
-      case 4: return launch_agg_cfg<VEC, 32, 1, 8, 1>(items, n_items, heavy, n_heavy, col, wp, C, ep, partials, s);
-      case 5: return launch_agg_cfg<VEC, 16, 2, 2, 2>(items, n_items, heavy, n_heavy, col, wp, C, ep, partials, s);
       default: return launch_agg_cfg<VEC, 32, 1, 4, 1>(items, n_items, heavy, n_heavy, col, wp, C, ep, partials, s);
     }
   }

@@ -122,12 +122,12 @@ struct EpiPre {
   float kv[GNPDE_STAGE_MAX_OUT][GNPDE_STAGE_MAX_K][VEC];
 };
 
-template <int VEC>
+template <int VEC, bool STG>
 __device__ __forceinline__ void epi_prefetch(const Epi& e, int64_t row, int cc, EpiPre<VEC>& p) {
   const bool need_x = (e.flags & GNPDE_EPI_RHS) != 0;
   if (need_x) load_vec<VEC>(e.x + row * e.ldx + cc, p.xr);
   if (e.flags & GNPDE_ADD_SOURCE) load_vec<VEC>(e.x0 + row * e.ldx0 + cc, p.x0r);
-  if (!e.has_stage) return;
+  if constexpr (!STG) return;
   const int64_t off = row * e.ldf + cc;
 #pragma unroll
   for (int i = 0; i < GNPDE_STAGE_MAX_OUT; ++i) {
@@ -143,7 +143,7 @@ __device__ __forceinline__ void epi_prefetch(const Epi& e, int64_t row, int cc, 
 
 // f = a*(ax - x) [+ b*x0]  (function_laplacian_diffusion.py:69-77) or f = ax,
 // then either store f or emit the fused Runge-Kutta stage outputs.
-template <int VEC>
+template <int VEC, bool STG>
 __device__ __forceinline__ void epi_finish(const Epi& e, int64_t row, int cc, const float (&ax)[VEC], float a,
                                            float b, const EpiPre<VEC>& p) {
   float o[VEC];
@@ -159,7 +159,7 @@ __device__ __forceinline__ void epi_finish(const Epi& e, int64_t row, int cc, co
 #pragma unroll
     for (int t = 0; t < VEC; ++t) o[t] = ax[t];
   }
-  if (!e.has_stage) {
+  if constexpr (!STG) {
     store_vec<VEC>(e.f + row * e.ldf + cc, o);
     return;
   }
@@ -193,12 +193,12 @@ __device__ __forceinline__ void epi_finish(const Epi& e, int64_t row, int cc, co
   }
 }
 
-template <int VEC>
+template <int VEC, bool STG>
 __device__ __forceinline__ void epilogue_store(const Epi& e, int64_t row, int cc, const float (&ax)[VEC], float a,
                                                float b) {
   EpiPre<VEC> p;
-  epi_prefetch<VEC>(e, row, cc, p);
-  epi_finish<VEC>(e, row, cc, ax, a, b, p);
+  epi_prefetch<VEC, STG>(e, row, cc, p);
+  epi_finish<VEC, STG>(e, row, cc, ax, a, b, p);
 }
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
