@@ -317,7 +317,8 @@ def odeint(func, y0, t, rtol=1e-7, atol=1e-9, method=None, options=None, combine
         return odeint_fixed(func, y0, t, method, options.get('step_size'), combine)
     if method in ADAPTIVE_METHODS:
         solver = _Dopri5(func, y0, rtol, atol, combine, first_step=options.get('first_step'),
-                         max_num_steps=options.get('max_num_steps', 2 ** 31 - 1))
+                         max_num_steps=options.get('max_num_steps', 2 ** 31 - 1),
+                         norm=options.get('norm', _rms_norm))
         out = solver.integrate(t)
         odeint.last_n_steps = solver.n_steps
         return out

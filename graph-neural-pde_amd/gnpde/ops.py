@@ -219,11 +219,13 @@ class Stage(object):
             ts.extend(k for k, _ in ks)
         return ts
 
-    def struct(self, x_input):
+    def struct(self, x_input, shift=0):
+        """ctypes struct; every pointer is moved back by ``shift`` bytes (row-block
+        buffers addressed with global row ids, dist.RowShardedLaplacian)."""
         if len(self.outs) > _lib.STAGE_MAX_OUT:
             raise ValueError("at most %d stage outputs" % _lib.STAGE_MAX_OUT)
         st = _lib.StageEpilogue()
-        st.f_out = self.f_out.data_ptr() if self.f_out is not None else None
+        st.f_out = self.f_out.data_ptr() - shift if self.f_out is not None else None
         st.n_out = len(self.outs)
         for i, (out, base, cb, cf, ks) in enumerate(self.outs):
             if len(ks) > _lib.STAGE_MAX_K:
@@ -231,13 +233,13 @@ class Stage(object):
             if out.data_ptr() == x_input.data_ptr():
                 raise ValueError("a stage output may not alias the RHS input")
             o = st.o[i]
-            o.out = out.data_ptr()
-            o.base = base.data_ptr() if base is not None else None
+            o.out = out.data_ptr() - shift
+            o.base = base.data_ptr() - shift if base is not None else None
             o.cb = float(cb)
             o.cf = float(cf)
             o.nk = len(ks)
             for j, (k, c) in enumerate(ks):
-                o.k[j] = k.data_ptr()
+                o.k[j] = k.data_ptr() - shift
                 o.c[j] = float(c)
         return st
 
@@ -277,6 +279,36 @@ def spmm_rhs(g, w_csr, x, x0=None, alpha=None, beta=None, rhs=True, alpha_sigmoi
               _ptr(w_csr), C, _ptr(xr), C, _ptr(x0r), C, _ptr(a), _ptr(b), _flags(rhs, alpha_sigmoid, add_source),
               _ptr(out), C, _ptr(partials), st, _stream(dev))
     return None if stage is not None else out.view(shape)
+
+
+def spmm_rhs_rows(g, plan, w_csr, x_src, x_rows, row0, x0=None, alpha=None, beta=None, alpha_sigmoid=True,
+                  add_source=False, stage=None, out=None):
+    """K1 over a row block: ``plan`` covers rows [row0, row0 + n) with global row
+    ids; gathers read ``x_src`` (all rows, global order); the block's own state
+    ``x_rows`` [n, C], ``x0`` and the outputs are local buffers addressed through
+    pointers shifted back by row0 rows (never dereferenced outside the block).
+    The epilogue's x_r comes from x_src[row], which holds the same values."""
+    xs = _rows(x_src, "x_src")
+    xl = _rows(x_rows, "x_rows")
+    C = xs.shape[1]
+    dev = xs.device
+    shift = int(row0) * C * 4
+    sp = lambda t: ctypes.c_void_p(t.data_ptr() - shift) if t is not None else ctypes.c_void_p(0)  # noqa: E731
+    a = _scalar(alpha, "alpha", dev)
+    b = _scalar(beta, "beta", dev) if add_source else None
+    x0r = _rows(x0, "x0") if add_source else None
+    st = None
+    if stage is not None:
+        for t in stage.tensors():
+            _require_gpu(t, "stage tensor", torch.float32)
+        st = ctypes.byref(stage.struct(xs, shift))
+    elif out is None:
+        out = torch.empty_like(xl)
+    partials = torch.empty(plan.n_slots * C, dtype=torch.float32, device=dev) if plan.n_slots else None
+    _lib.call("gnpde_spmm_rhs_f32", _ptr(plan.items), plan.n_items, _ptr(plan.heavy), plan.n_heavy, _ptr(g.csr.col),
+              _ptr(w_csr), C, _ptr(xs), C, sp(x0r), C, _ptr(a), _ptr(b), _flags(True, alpha_sigmoid, add_source),
+              sp(out) if out is not None else ctypes.c_void_p(0), C, _ptr(partials), st, _stream(dev))
+    return None if stage is not None else out.view(x_rows.shape)
 
 
 # --------------------------------------------------------------------------- attention

@@ -1,0 +1,91 @@
+"""Worker bodies of tests/test_dist_gloo.py (module-level so mp.spawn can pickle them)."""
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+for p in (os.path.join(ROOT, "graph-neural-pde_amd"), os.path.join(ROOT, "oracle"), HERE):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+
+def problem(seed=0, N=61, E=400, C=10, B=1):
+    rng = np.random.default_rng(seed)
+    ei = rng.integers(0, N, size=(B, 2, E))
+    w = rng.uniform(0.1, 1.0, size=(B, E))
+    x = rng.standard_normal((B, N, C))
+    A = np.zeros((B * N, B * N))
+    for b in range(B):
+        np.add.at(A, (b * N + ei[b, 0], b * N + ei[b, 1]), w[b])
+    return ei, w, x, A
+
+
+def reference(A, x, alpha, method, t1, step, **kw):
+    from gnpde import integrator as gi
+    At = torch.from_numpy(A)
+    f = lambda t, y: alpha * (y @ At.T - y)  # noqa: E731  (y as [C, R]^T trick below)
+    y0 = torch.from_numpy(x.reshape(-1, x.shape[-1]))
+    fr = lambda t, y: alpha * (At @ y - y)  # noqa: E731
+    del f
+    out = gi.odeint(fr, y0, torch.tensor([0.0, t1], dtype=torch.float64), method=method,
+                    options=dict(step_size=step, **kw), combine=gi._torch_combine, rtol=1e-8, atol=1e-10)
+    return out[1].numpy(), gi.odeint.last_n_steps
+
+
+def _init(rank, world, port):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+
+def rows_worker(rank, world, port, method, q):
+    _init(rank, world, port)
+    try:
+        from gnpde import dist as gd, integrator as gi
+        ei, w, x, A = problem()
+        alpha = 0.6
+        R, C = A.shape[0], x.shape[-1]
+        At = torch.from_numpy(A)
+
+        def local_rhs(t, y_full, r0, r1, y_local):
+            f = torch.zeros_like(y_local)
+            f[:r1 - r0] = alpha * (At[r0:r1] @ y_full[:R] - y_full[r0:r1])
+            return f
+
+        sh = gd.RowShardedLaplacian(torch.from_numpy(ei), torch.from_numpy(w), x.shape[1], alpha, local_rhs=local_rhs)
+        y0 = sh.scatter(torch.from_numpy(x.reshape(R, C)))
+        y = gi.odeint(sh, y0, torch.tensor([0.0, 1.0], dtype=torch.float64), method=method,
+                      options=dict(step_size=0.25), combine=gi._torch_combine)[1]
+        full = sh.unpad(sh.gather(y)).numpy()
+        want, _ = reference(A, x, alpha, method, 1.0, 0.25)
+        q.put((rank, float(np.abs(full - want).max()), sh.nfe, [list(b) for b in sh.blocks]))
+    finally:
+        dist.destroy_process_group()
+
+
+def cols_worker(rank, world, port, method, q):
+    _init(rank, world, port)
+    try:
+        from gnpde import dist as gd, integrator as gi
+        ei, w, x, A = problem(seed=1, C=11)
+        alpha = 0.45
+        R, C = A.shape[0], x.shape[-1]
+        At = torch.from_numpy(A)
+        sh = gd.ColumnShardedLaplacian(torch.from_numpy(ei), torch.from_numpy(w), x.shape[1], C, alpha,
+                                       local_rhs=lambda t, xl: alpha * (At @ xl - xl))
+        xl = sh.split(torch.from_numpy(x.reshape(R, C)))
+        opts = dict(step_size=0.25)
+        if method == "dopri5":
+            opts["norm"] = sh.global_rms_norm
+        y = gi.odeint(sh, xl, torch.tensor([0.0, 1.0], dtype=torch.float64), method=method, options=opts,
+                      combine=gi._torch_combine, rtol=1e-8, atol=1e-10)[1]
+        steps = gi.odeint.last_n_steps
+        full = sh.gather(y).numpy()
+        want, want_steps = reference(A, x, alpha, method, 1.0, 0.25)
+        q.put((rank, float(np.abs(full - want).max()), steps, want_steps if method == "dopri5" else steps))
+    finally:
+        dist.destroy_process_group()

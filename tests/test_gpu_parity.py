@@ -315,6 +315,31 @@ def test_stage_output_may_not_alias_input():
                      stage=ops.Stage(outs=[(x, x, 1.0, 0.1, [])]))
 
 
+# ---------------------------------------------------------------- row-block RHS (dist.RowShardedLaplacian)
+def test_row_block_rhs_matches_full_rows():
+    from gnpde import dist as gd
+    from gnpde import integrator as gi
+    N, E, C = 3000, 40000, 64
+    ei = hub_graph(N, E, seed=31)
+    rng = np.random.default_rng(31)
+    w = T(rng.uniform(0.1, 1, size=(1, E)).astype(np.float32))
+    x = torch.randn(N, C, device=DEV)
+    g = ops.GraphCSR(T(ei), N)
+    wc = g.gather_weights(w)
+    alpha = torch.tensor(0.3, device=DEV)
+    full = ops.spmm_rhs(g, wc, x, alpha=alpha)
+    for r0, r1 in ((0, 1000), (1000, 2217), (2217, 3000)):
+        plan = gd._local_plan(g.csr, r0, r1, ops.DEFAULT_CHUNK)
+        loc = ops.spmm_rhs_rows(g, plan, wc, x, x[r0:r1].contiguous(), r0, alpha=alpha)
+        assert torch.equal(loc, full[r0:r1])
+        # fused stage through shifted pointers: out = x_rows + 0.5 f
+        out = torch.empty(r1 - r0, C, device=DEV)
+        ops.spmm_rhs_rows(g, plan, wc, x, x[r0:r1].contiguous(), r0, alpha=alpha,
+                          stage=ops.Stage(outs=[(out, x[r0:r1].contiguous(), 1.0, 0.5, [])]))
+        assert torch.allclose(out, x[r0:r1] + 0.5 * full[r0:r1], atol=1e-6)
+    del gi
+
+
 # ---------------------------------------------------------------- ODE blocks end to end
 def _prep_oracle(ei, N, fill=1.0):
     eis, ws = O.get_rw_adj(ei, norm_dim=1, fill_value=fill, num_nodes=N)
