@@ -237,6 +237,10 @@ def bench_sharded(args, world, rank, dev):
     import gnpde
     from gnpde import dist as gd, synthetic
     N, E, C, h = args.nodes, args.edges, args.dim, args.step_size
+    if not dist.is_initialized():  # single process: a world of one
+        import random
+        dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % random.randint(20000, 40000), rank=0,
+                                world_size=1, device_id=dev)
     ei, w = synthetic.rw_graph(N, E, seed=0, device=dev)
     x = synthetic.features(1, N, C, seed=1, device=dev)
     alpha = torch.zeros((), device=dev)
@@ -279,9 +283,8 @@ def bench_sharded(args, world, rank, dev):
             "data": "synthetic (seeded RMAT G-arxiv graph, N(0,1) features)",
             "config": {"workload": "G-arxiv laplacian RHS, rk4, one graph sharded (%s)" % args.mode, "nodes": N,
                        "edges": E, "dim": C, "method": "rk4", "parallelism": "%s%d" % (args.mode, world)}}))
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
+    dist.barrier()
+    dist.destroy_process_group()
 
 
 def bench_attention(g, x, dev, ops, reps=20):
