@@ -356,3 +356,49 @@ class LaplacianCSR(object):
             if add_source:
                 out[b] += self.dtype(beta) * x0[b]
         return out
+
+
+# --------------------------------------------------------------------------- C restatement (timed baseline)
+class COracle(object):
+    """ctypes view of oracle/build/liboracle.so (oracle/c/rhs_oracle.c): the
+    Laplacian RHS in fp32 over a CSR built once, OpenMP over rows."""
+
+    def __init__(self, path=None):
+        import ctypes
+        import os
+        path = path or os.path.join(os.path.dirname(os.path.abspath(__file__)), "build", "liboracle.so")
+        self.lib = ctypes.CDLL(path)
+        vp, i64 = ctypes.c_void_p, ctypes.c_int64
+        self.lib.gnpde_oracle_csr.argtypes = [vp, i64, i64, i64, vp, vp, vp, vp]
+        self.lib.gnpde_oracle_laplacian_rhs.argtypes = [vp, vp, vp, i64, i64, vp, vp, ctypes.c_float,
+                                                        ctypes.c_float, ctypes.c_int, ctypes.c_int, vp,
+                                                        ctypes.c_int]
+        self.ct = ctypes
+
+    def csr(self, edge_index, w, num_nodes):
+        ei = np.ascontiguousarray(edge_index, dtype=np.int64)
+        B, _, E = ei.shape
+        R = B * int(num_nodes)
+        rowptr = np.empty(R + 1, np.int64)
+        col = np.empty(max(B * E, 1), np.int32)
+        wc = np.empty(max(B * E, 1), np.float32)
+        wf = np.ascontiguousarray(w, dtype=np.float32).reshape(-1)
+        p = lambda a: a.ctypes.data_as(self.ct.c_void_p)  # noqa: E731
+        rc = self.lib.gnpde_oracle_csr(p(ei), B, E, int(num_nodes), p(wf), p(rowptr), p(col), p(wc))
+        if rc != 0:
+            raise ValueError("gnpde_oracle_csr failed (%d)" % rc)
+        return rowptr, col, wc
+
+    def laplacian_rhs(self, csr, x, alpha_train, x0=None, beta_train=0.0, no_alpha_sigmoid=False, add_source=False,
+                      nthreads=0):
+        rowptr, col, wc = csr
+        x = np.ascontiguousarray(x, dtype=np.float32)
+        C = x.shape[-1]
+        R = x.size // C
+        f = np.empty_like(x)
+        x0a = np.ascontiguousarray(x0, dtype=np.float32) if add_source else x
+        p = lambda a: a.ctypes.data_as(self.ct.c_void_p)  # noqa: E731
+        self.lib.gnpde_oracle_laplacian_rhs(p(rowptr), p(col), p(wc), R, C, p(x), p(x0a), float(alpha_train),
+                                            float(beta_train), int(no_alpha_sigmoid), int(add_source), p(f),
+                                            int(nthreads))
+        return f
