@@ -21,6 +21,7 @@ constexpr int kLinCols = 64;
 constexpr int kLinChunk = 16;        // k-steps per half per prefetch chunk
 constexpr int kLinLdsStride = kLinCols + 1;
 
+// A chunk of kLinChunk k-steps of this lane's half row (zeros past Kh / K).
 template <bool VEC4>
 __device__ __forceinline__ void lin_load_chunk(const float* __restrict__ xr, int kbase, int s0, int Kh, int K,
                                                float (&a)[kLinChunk]) {
@@ -43,20 +44,25 @@ __device__ __forceinline__ void lin_load_chunk(const float* __restrict__ xr, int
   }
 }
 
+// K split between the MFMA lane halves: half h covers k = h*Kh + s, s < Kh.
+// The LDS image of W^T has Khp = roundup(Kh, kLinChunk) rows per half (zero
+// padded), so the MFMA loop runs whole chunks with no per-step guard.
 template <bool VEC4>
 __global__ __launch_bounds__(256) void linear_mfma_kernel(const float* __restrict__ x, int R, int K, int64_t ldx,
                                                            const float* __restrict__ W,
                                                            const float* __restrict__ bias, int Nout, int split,
                                                            float* __restrict__ out_a, int64_t lda,
                                                            float* __restrict__ out_b, int64_t ldb) {
-  extern __shared__ __attribute__((aligned(16))) float wt[];  // [2*Kh][65]
+  extern __shared__ __attribute__((aligned(16))) float wt[];  // [2*Khp][65]
   const int Kh = (K + 1) >> 1;
+  const int Khp = (Kh + kLinChunk - 1) / kLinChunk * kLinChunk;
   const int col0 = blockIdx.y * kLinCols;
-  // stage W^T slice (coalesced along k): wt[k][j] = W[col0 + j][k]
-  for (int t = threadIdx.x; t < 2 * Kh * kLinCols; t += blockDim.x) {
-    const int j = t / (2 * Kh), kk = t - j * (2 * Kh);
+  for (int t = threadIdx.x; t < 2 * Khp * kLinCols; t += blockDim.x) {
+    const int j = t / (2 * Khp), kr = t - j * (2 * Khp);  // kr = h*Khp + s
+    const int h = kr / Khp, sidx = kr - h * Khp;
+    const int k = h * Kh + sidx;
     const int n = col0 + j;
-    wt[kk * kLinLdsStride + j] = (kk < K && n < Nout) ? W[(int64_t)n * K + kk] : 0.f;
+    wt[kr * kLinLdsStride + j] = (sidx < Kh && k < K && n < Nout) ? W[(int64_t)n * K + k] : 0.f;
   }
   __syncthreads();
 
@@ -68,19 +74,24 @@ __global__ __launch_bounds__(256) void linear_mfma_kernel(const float* __restric
   const int my_row = min(row0 + r32, R - 1);
   const float* __restrict__ xr = x + (int64_t)my_row * ldx;
   const int kbase = h * Kh;
+  const float* __restrict__ wbase = wt + h * Khp * kLinLdsStride;
 
   f32x16 acc0 = {0}, acc1 = {0};
   float a_cur[kLinChunk], a_nxt[kLinChunk];
   lin_load_chunk<VEC4>(xr, kbase, 0, Kh, K, a_cur);
-  for (int s0 = 0; s0 < Kh; s0 += kLinChunk) {
-    if (s0 + kLinChunk < Kh) lin_load_chunk<VEC4>(xr, kbase, s0 + kLinChunk, Kh, K, a_nxt);
+  for (int s0 = 0; s0 < Khp; s0 += kLinChunk) {
+    if (s0 + kLinChunk < Khp) lin_load_chunk<VEC4>(xr, kbase, s0 + kLinChunk, Kh, K, a_nxt);
+    float b0[kLinChunk], b1[kLinChunk];
 #pragma unroll
     for (int i = 0; i < kLinChunk; ++i) {
-      if (s0 + i < Kh) {
-        const float* wrow = wt + (kbase + s0 + i) * kLinLdsStride;
-        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a_cur[i], wrow[r32], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a_cur[i], wrow[32 + r32], acc1, 0, 0, 0);
-      }
+      const float* wrow = wbase + (s0 + i) * kLinLdsStride;
+      b0[i] = wrow[r32];
+      b1[i] = wrow[32 + r32];
+    }
+#pragma unroll
+    for (int i = 0; i < kLinChunk; ++i) {
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a_cur[i], b0[i], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a_cur[i], b1[i], acc1, 0, 0, 0);
     }
 #pragma unroll
     for (int i = 0; i < kLinChunk; ++i) a_cur[i] = a_nxt[i];
@@ -117,7 +128,8 @@ extern "C" int gnpde_linear_f32(const float* x, int64_t R, int64_t K, int64_t ld
   GNPDE_REQUIRE(split == Nout || out_b != nullptr, GNPDE_EINVAL, "linear: out_b is NULL");
   GNPDE_REQUIRE(lda >= split && (split == Nout || ldb >= Nout - split), GNPDE_EINVAL, "linear: bad ld");
   const int64_t Kh = (K + 1) / 2;
-  const size_t shm = sizeof(float) * (size_t)(2 * Kh * kLinLdsStride);
+  const int64_t Khp = (Kh + kLinChunk - 1) / kLinChunk * kLinChunk;
+  const size_t shm = sizeof(float) * (size_t)(2 * Khp * kLinLdsStride);
   GNPDE_REQUIRE(shm <= 160 * 1024, GNPDE_EUNSUPPORTED, "linear: K=%lld too large for the LDS slice",
                 (long long)K);
   if (R == 0) return GNPDE_OK;

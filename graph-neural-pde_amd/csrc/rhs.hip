@@ -286,7 +286,11 @@ __global__ __launch_bounds__(256) void keysum_tiles_kernel(const double* __restr
   }
 }
 
-// per batch element: S = Wk xbar + E bk;  U[c,h] = sum_{d in h} Wq[d,c] S[d] / sqrt(dk);  v[h] = bq_h . S_h / sqrt(dk)
+// per batch element: S = Wk xbar + E bk (recomputed per block into LDS: att
+// dot products of length C), then this block's slice of
+// U[c,h] = sum_{d in h} Wq[d,c] S[d] / sqrt(dk) and, in block 0, v[h] = bq_h . S_h / sqrt(dk).
+constexpr int kFinishPairs = 256;  // (c,h) pairs per block
+
 __global__ __launch_bounds__(256) void keysum_finish_kernel(const double* __restrict__ xbar, int C,
                                                              const float* __restrict__ Wq,
                                                              const float* __restrict__ bq,
@@ -294,7 +298,7 @@ __global__ __launch_bounds__(256) void keysum_finish_kernel(const double* __rest
                                                              const float* __restrict__ bk, int att, int H,
                                                              double* __restrict__ U, double* __restrict__ v) {
   extern __shared__ __attribute__((aligned(16))) double S[];  // att
-  const int b = blockIdx.x;
+  const int b = blockIdx.y;
   const double* xb = xbar + (int64_t)b * (C + 1);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   for (int d = wv; d < att; d += kWavesPerBlock) {
@@ -306,56 +310,72 @@ __global__ __launch_bounds__(256) void keysum_finish_kernel(const double* __rest
   __syncthreads();
   const int dk = att / H;
   const double inv = 1.0 / sqrt((double)dk);
-  for (int t = threadIdx.x; t < C * H; t += blockDim.x) {
+  const int t = blockIdx.x * kFinishPairs + threadIdx.x;
+  if (t < C * H) {
     const int c = t / H, h = t - c * H;
     double s = 0.0;
     for (int d = h * dk; d < (h + 1) * dk; ++d) s = fma((double)Wq[(int64_t)d * C + c], S[d], s);
     U[((int64_t)b * C + c) * H + h] = s * inv;
   }
-  for (int h = threadIdx.x; h < H; h += blockDim.x) {
+  if (blockIdx.x == 0 && threadIdx.x < H) {
+    const int h = threadIdx.x;
     double s = 0.0;
     for (int d = h * dk; d < (h + 1) * dk; ++d) s = fma((double)bq[d], S[d], s);
     v[(int64_t)b * H + h] = s * inv;
   }
 }
 
-// cs[r,h] = x_r . U[b,:,h] + v[b,h]  (fp64 accumulation), GL lanes per row
+// cs[r,h] = x_r . U[b,:,h] + v[b,h]  (fp64 accumulation), GL lanes per row,
+// 64/GL rows per wavefront, every load of the row issued before the FMAs.
 template <int VEC, int GL, int MAXH>
 __global__ __launch_bounds__(256) void node_scores_kernel(const float* __restrict__ x, int64_t R, int64_t N, int C,
                                                            int64_t ldx, int H, const double* __restrict__ U,
                                                            const double* __restrict__ v, double* __restrict__ cs) {
   constexpr int G = kWave / GL;
+  constexpr int NP = 4;  // column passes held in flight (C <= NP*GL*VEC handled in one sweep)
   const int lane = threadIdx.x & 63;
   const int g = lane / GL, gl = lane % GL;
-  const int64_t nrows_step = (int64_t)gridDim.x * kWavesPerBlock * G;
-  for (int64_t r0 = (int64_t)(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * G; r0 < R; r0 += nrows_step) {
-    const int64_t r = r0 + g;
-    const bool live = r < R;
-    const int64_t rr = live ? r : R - 1;
-    const int64_t b = rr / N;
-    double acc[MAXH];
+  const int64_t r = (int64_t)(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * G + g;
+  const bool live = r < R;
+  const int64_t rr = live ? r : R - 1;
+  const int64_t b = rr / N;
+  double acc[MAXH];
 #pragma unroll
-    for (int h = 0; h < MAXH; ++h) acc[h] = 0.0;
-    for (int c0 = gl * VEC; c0 < C; c0 += GL * VEC) {
-      float xv[VEC];
-      load_vec<VEC>(x + rr * ldx + c0, xv);
+  for (int h = 0; h < MAXH; ++h) acc[h] = 0.0;
+  for (int c00 = 0; c00 < C; c00 += NP * GL * VEC) {
+    float xv[NP][VEC];
 #pragma unroll
-      for (int i = 0; i < VEC; ++i) {
-        const double* u = U + (b * C + c0 + i) * H;
+    for (int p = 0; p < NP; ++p) {
+      const int c0 = c00 + (p * GL + gl) * VEC;
+      if (c0 < C) {
+        load_vec<VEC>(x + rr * ldx + c0, xv[p]);
+      } else {
 #pragma unroll
-        for (int h = 0; h < MAXH; ++h)
-          if (h < H) acc[h] = fma((double)xv[i], u[h], acc[h]);
+        for (int i = 0; i < VEC; ++i) xv[p][i] = 0.f;
       }
     }
 #pragma unroll
-    for (int o = 1; o < GL; o <<= 1)
+    for (int p = 0; p < NP; ++p) {
+      const int c0 = c00 + (p * GL + gl) * VEC;
+      if (c0 < C) {
 #pragma unroll
-      for (int h = 0; h < MAXH; ++h) acc[h] += __shfl_xor(acc[h], o);
-    if (live && gl == 0) {
+        for (int i = 0; i < VEC; ++i) {
+          const double* u = U + (b * C + c0 + i) * H;
 #pragma unroll
-      for (int h = 0; h < MAXH; ++h)
-        if (h < H) cs[r * H + h] = acc[h] + v[b * H + h];
+          for (int h = 0; h < MAXH; ++h)
+            if (h < H) acc[h] = fma((double)xv[p][i], u[h], acc[h]);
+        }
+      }
     }
+  }
+#pragma unroll
+  for (int o = 1; o < GL; o <<= 1)
+#pragma unroll
+    for (int h = 0; h < MAXH; ++h) acc[h] += __shfl_xor(acc[h], o);
+  if (live && gl == 0) {
+#pragma unroll
+    for (int h = 0; h < MAXH; ++h)
+      if (h < H) cs[r * H + h] = acc[h] + v[b * H + h];
   }
 }
 
@@ -654,13 +674,14 @@ int gnpde_ref_scores_f32(const float* x, int64_t B, int64_t N, int64_t C, int64_
   GNPDE_LAUNCH_CHECK();
   keysum_tiles_kernel<<<dim3((unsigned)ceil_div(C + 1, 16), (unsigned)B), kBlock, 0, s>>>(part, ntiles, (int)C, xbar);
   GNPDE_LAUNCH_CHECK();
-  keysum_finish_kernel<<<(unsigned)B, kBlock, sizeof(double) * (size_t)att, s>>>(xbar, (int)C, Wq, bq, Wk, bk, (int)att,
-                                                                               (int)heads, U, v);
+  keysum_finish_kernel<<<dim3((unsigned)ceil_div(C * heads, kFinishPairs), (unsigned)B), kBlock,
+                         sizeof(double) * (size_t)att, s>>>(xbar, (int)C, Wq, bq, Wk, bk, (int)att, (int)heads, U, v);
   GNPDE_LAUNCH_CHECK();
   const int64_t R = B * N;
-  const int GL = std::min(64, pow2_at_least((int)ceil_div(C, vec), 64));
-  const int rows_per_block = kWavesPerBlock * (kWave / std::max(GL, 8));
-  const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(R, rows_per_block), 8192);
+  // lanes per row: enough for the row in <= 4 VEC-wide passes, at least 8
+  const int GL = std::max(8, std::min(64, pow2_at_least((int)ceil_div(ceil_div(C, vec), 4), 64)));
+  const int rows_per_block = kWavesPerBlock * (kWave / GL);
+  const unsigned grid = (unsigned)ceil_div(R, rows_per_block);
   if (vec == 4)
     launch_node_scores_vec<4>(grid, GL, s, x, R, N, (int)C, ldx, (int)heads, U, v, cs);
   else if (vec == 2)
