@@ -55,7 +55,11 @@ def rk4_fused_step_bytes(N, E, C):
 def attn_bytes(N, E, C, att, mode):
     """Algorithmic bytes of one attention RHS.  per_edge: projection
     4NC + 8N*att, stats+aggregation 4N*att + 4E*att + 4EC + 8NC + 4E + 4(N+1);
-    reference: the k gather is replaced by the key-sum pass 4N*att + 4N."""
+    reference: the k gather is replaced by the key-sum pass 4N*att + 4N; uniform: see below."""
+    if mode == "uniform":
+        # fork scaled_dot with norm_idx=0: weights 1/outdeg are graph-only and cached, so one RHS is the
+        # aggregation alone (CSR 4(N+1) + 4E, weights 4E, gathers 4EC, own row 4NC, f 4NC)
+        return 4 * (N + 1) + 8 * E + 4 * E * C + 8 * N * C
     base = 4 * N * C + 8 * N * att + 4 * N * att + 4 * E * C + 8 * N * C + 4 * E + 4 * (N + 1)
     return base + (4 * E * att if mode == "per_edge" else 4 * N * att + 4 * N)
 
@@ -319,7 +323,7 @@ def bench_attention(g, x, dev, ops, reps=20):
             e.record()
             torch.cuda.synchronize()
         ms = s.elapsed_time(e) / reps
-        nb = attn_bytes(g.N, g.nnz, C, att, mode)
+        nb = attn_bytes(g.N, g.nnz, C, att, "uniform" if (mode, norm_idx) == ("reference", 0) else mode)
         gbs = nb / (ms * 1e-3) / 1e9
         out["%s_norm%d" % (mode, norm_idx)] = {"rhs_ms": round(ms, 4), "achieved_GBs": round(gbs, 1),
                                                "frac": round(gbs / HBM_PEAK_GBS, 4), "algorithmic_bytes": nb}

@@ -20,6 +20,8 @@ constexpr int kLinCols = 64;
 
 constexpr int kLinChunk = 16;        // k-steps per half per prefetch chunk
 constexpr int kLinLdsStride = kLinCols + 1;
+constexpr int kLinStageCols = kLinCols / kWavesPerBlock;  // W^T columns staged per wavefront
+constexpr int kOutOfRange = 0x7ffffff0;                    // buffer offset past any W (reads 0)
 
 // A chunk of kLinChunk k-steps of this lane's half row (zeros past Kh / K).
 template <bool VEC4>
@@ -57,12 +59,29 @@ __global__ __launch_bounds__(256) void linear_mfma_kernel(const float* __restric
   const int Kh = (K + 1) >> 1;
   const int Khp = (Kh + kLinChunk - 1) / kLinChunk * kLinChunk;
   const int col0 = blockIdx.y * kLinCols;
-  for (int t = threadIdx.x; t < 2 * Khp * kLinCols; t += blockDim.x) {
-    const int j = t / (2 * Khp), kr = t - j * (2 * Khp);  // kr = h*Khp + s
-    const int h = kr / Khp, sidx = kr - h * Khp;
-    const int k = h * Kh + sidx;
-    const int n = col0 + j;
-    wt[kr * kLinLdsStride + j] = (sidx < Kh && k < K && n < Nout) ? W[(int64_t)n * K + k] : 0.f;
+  // Stage W^T: wave wv fills columns j = wv + 4*jj, lanes walk the k rows
+  // (coalesced along k).  Buffer loads with 32-bit offsets: a padding element
+  // (k past the half, n past Nout) gets an out-of-range offset and reads 0, so
+  // all kLinStageCols loads issue back to back with no branch or 64-bit select.
+  {
+    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(W), 0, Nout * K * (int)sizeof(float), 0x00020000);
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (int kr = lane; kr < 2 * Khp; kr += kWave) {
+      const int hh = kr >= Khp ? 1 : 0;
+      const int sidx = kr - hh * Khp;
+      const int k = hh * Kh + sidx;
+      const bool kok = sidx < Kh && k < K;
+      float val[kLinStageCols];
+#pragma unroll
+      for (int jj = 0; jj < kLinStageCols; ++jj) {
+        const int n = col0 + wv + kWavesPerBlock * jj;
+        const int off = (kok && n < Nout) ? (n * K + k) * (int)sizeof(float) : kOutOfRange;
+        val[jj] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(wr, off, 0, 0));
+      }
+#pragma unroll
+      for (int jj = 0; jj < kLinStageCols; ++jj) wt[kr * kLinLdsStride + wv + kWavesPerBlock * jj] = val[jj];
+    }
   }
   __syncthreads();
 
@@ -125,6 +144,7 @@ extern "C" int gnpde_linear_f32(const float* x, int64_t R, int64_t K, int64_t ld
   GNPDE_REQUIRE(x && W && out_a, GNPDE_EINVAL, "linear: NULL pointer");
   GNPDE_REQUIRE(R >= 0 && R < INT32_MAX && K >= 1 && ldx >= K && Nout >= 1, GNPDE_EINVAL, "linear: bad sizes");
   GNPDE_REQUIRE(split >= 0 && split <= Nout, GNPDE_EINVAL, "linear: bad split");
+  GNPDE_REQUIRE(Nout * K * (int64_t)sizeof(float) < kOutOfRange, GNPDE_EUNSUPPORTED, "linear: W larger than 2 GB");
   GNPDE_REQUIRE(split == Nout || out_b != nullptr, GNPDE_EINVAL, "linear: out_b is NULL");
   GNPDE_REQUIRE(lda >= split && (split == Nout || ldb >= Nout - split), GNPDE_EINVAL, "linear: bad ld");
   const int64_t Kh = (K + 1) / 2;

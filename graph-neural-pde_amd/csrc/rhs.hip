@@ -160,6 +160,13 @@ struct Team {
   int T, S;
 };
 
+// Team-mode softmax statistics: one team of T lanes per work item.  The
+// item's own row (q of the source group, or k of the destination group) is
+// loaded once; the other endpoints' indices come in T at a time (one per
+// lane, then broadcast with shuffles) and kTeamEdges rows are in flight
+// together.  Edges are pushed in CSR order, as the lane-mode kernel does.
+constexpr int kTeamEdges = 4;
+
 template <int VEC>
 __global__ __launch_bounds__(256) void stats_team_kernel(const int4* __restrict__ items, int n_items,
                                                           const int* __restrict__ gidx, int group_is_dst, ScoreArgs sa,
@@ -172,16 +179,29 @@ __global__ __launch_bounds__(256) void stats_team_kernel(const int4* __restrict_
   const bool live = item < n_items && team < tpw;
   const int4 it = live ? items[item] : make_int4(0, 0, 0, -1);
   const int grp = it.x, beg = it.y, end = it.z, slot = it.w;
+  float own[VEC];
+  team_row<VEC>(sa, group_is_dst ? sa.k : sa.q, grp, t, own);
   double M = -INFINITY;
   float L = 0.f;
-  for (int p = beg; p < end; p += 2) {
-    const bool two = p + 1 < end;
-    const int o0 = gidx[p];
-    const int o1 = two ? gidx[p + 1] : o0;
-    const float s0 = team_score<VEC>(sa, group_is_dst ? o0 : grp, group_is_dst ? grp : o0, t, S);
-    const float s1 = team_score<VEC>(sa, group_is_dst ? o1 : grp, group_is_dst ? grp : o1, t, S);
-    online_push(M, L, (double)s0);
-    if (two) online_push(M, L, (double)s1);
+  for (int p0 = beg; p0 < end; p0 += T) {
+    const int cnt = min(T, end - p0);
+    const int mine = gidx[p0 + min(t, cnt - 1)];
+    for (int j = 0; j < cnt; j += kTeamEdges) {
+      float other[kTeamEdges][VEC];
+#pragma unroll
+      for (int u = 0; u < kTeamEdges; ++u) {
+        const int o = __shfl(mine, team * T + min(j + u, cnt - 1));
+        team_row<VEC>(sa, group_is_dst ? sa.q : sa.k, o, t, other[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < kTeamEdges; ++u) {
+        if (j + u < cnt) {
+          const float s = group_is_dst ? team_score_regs<VEC>(sa, other[u], own, S)
+                                       : team_score_regs<VEC>(sa, own, other[u], S);
+          online_push(M, L, (double)s);
+        }
+      }
+    }
   }
   if (!live || (t % S) != 0) return;
   const int H = sa.H;
@@ -194,6 +214,9 @@ __global__ __launch_bounds__(256) void stats_team_kernel(const int4* __restrict_
   }
 }
 
+// Team-mode attention weights: a team takes T consecutive edges (indices
+// loaded one per lane, coalesced), then evaluates them kTeamEdges at a time
+// with the q/k rows and the group's softmax statistics all in flight.
 template <int VEC, bool COO>
 __global__ __launch_bounds__(256) void attn_team_kernel(const int* __restrict__ rowidx, const int* __restrict__ col,
                                                          const int* __restrict__ perm, int64_t nnz, int norm_idx,
@@ -204,18 +227,42 @@ __global__ __launch_bounds__(256) void attn_team_kernel(const int* __restrict__ 
   const int team = lane / T, t = lane % T, h = t / S;
   const int H = sa.H;
   if (team >= tpw) return;
+  const bool leader = (t % S) == 0;
   const int64_t nteams = (int64_t)gridDim.x * kWavesPerBlock * tpw;
-  for (int64_t p = (int64_t)(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * tpw + team; p < nnz; p += nteams) {
-    const int r = rowidx[p], c = col[p];
-    const int64_t g = norm_idx == 0 ? r : c;
-    const float s = team_score<VEC>(sa, r, c, t, S);
-    const bool leader = (t % S) == 0;
-    float term = leader ? expf((float)((double)s - m[g * H + h])) * rl[g * H + h] : 0.f;
-    if (COO) {
-      if (leader) out[(int64_t)perm[p] * H + h] = term;
-    } else {
-      for (int o = S; o < T; o <<= 1) term += __shfl_xor(term, o);
-      if (t == 0) out[p] = term / (float)H;
+  for (int64_t p0 = ((int64_t)(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * tpw + team) * T; p0 < nnz;
+       p0 += nteams * T) {
+    const int cnt = (int)min((int64_t)T, nnz - p0);
+    const int64_t pm = p0 + min(t, cnt - 1);
+    const int my_r = rowidx[pm], my_c = col[pm];
+    const int my_dst = COO ? perm[pm] : 0;
+    for (int j = 0; j < cnt; j += kTeamEdges) {
+      float qv[kTeamEdges][VEC], kv[kTeamEdges][VEC];
+      double mv[kTeamEdges];
+      float rv[kTeamEdges];
+#pragma unroll
+      for (int u = 0; u < kTeamEdges; ++u) {
+        const int src = team * T + min(j + u, cnt - 1);
+        const int r = __shfl(my_r, src), c = __shfl(my_c, src);
+        team_row<VEC>(sa, sa.q, r, t, qv[u]);
+        team_row<VEC>(sa, sa.k, c, t, kv[u]);
+        const int64_t g = norm_idx == 0 ? r : c;
+        mv[u] = m[g * H + h];
+        rv[u] = rl[g * H + h];
+      }
+#pragma unroll
+      for (int u = 0; u < kTeamEdges; ++u) {
+        const int dst = COO ? __shfl(my_dst, team * T + min(j + u, cnt - 1)) : 0;
+        if (j + u < cnt) {
+          const float s = team_score_regs<VEC>(sa, qv[u], kv[u], S);
+          float term = leader ? expf((float)((double)s - mv[u])) * rv[u] : 0.f;
+          if (COO) {
+            if (leader) out[(int64_t)dst * H + h] = term;
+          } else {
+            for (int o = S; o < T; o <<= 1) term += __shfl_xor(term, o);
+            if (t == 0) out[p0 + j + u] = term / (float)H;
+          }
+        }
+      }
     }
   }
 }
@@ -289,14 +336,16 @@ __global__ __launch_bounds__(256) void keysum_tiles_kernel(const double* __restr
 // per batch element: S = Wk xbar + E bk (recomputed per block into LDS: att
 // dot products of length C), then this block's slice of
 // U[c,h] = sum_{d in h} Wq[d,c] S[d] / sqrt(dk) and, in block 0, v[h] = bq_h . S_h / sqrt(dk).
+// U is stored padded as [B][Cp][Hp] (zeros past C and H) so node_scores reads
+// it with compile-time offsets and no clamping; v as [B][Hp].
 constexpr int kFinishPairs = 256;  // (c,h) pairs per block
 
 __global__ __launch_bounds__(256) void keysum_finish_kernel(const double* __restrict__ xbar, int C,
                                                              const float* __restrict__ Wq,
                                                              const float* __restrict__ bq,
                                                              const float* __restrict__ Wk,
-                                                             const float* __restrict__ bk, int att, int H,
-                                                             double* __restrict__ U, double* __restrict__ v) {
+                                                             const float* __restrict__ bk, int att, int H, int Cp,
+                                                             int Hp, double* __restrict__ U, double* __restrict__ v) {
   extern __shared__ __attribute__((aligned(16))) double S[];  // att
   const int b = blockIdx.y;
   const double* xb = xbar + (int64_t)b * (C + 1);
@@ -311,71 +360,164 @@ __global__ __launch_bounds__(256) void keysum_finish_kernel(const double* __rest
   const int dk = att / H;
   const double inv = 1.0 / sqrt((double)dk);
   const int t = blockIdx.x * kFinishPairs + threadIdx.x;
-  if (t < C * H) {
-    const int c = t / H, h = t - c * H;
+  if (t < Cp * Hp) {
+    const int c = t / Hp, h = t - c * Hp;
     double s = 0.0;
-    for (int d = h * dk; d < (h + 1) * dk; ++d) s = fma((double)Wq[(int64_t)d * C + c], S[d], s);
-    U[((int64_t)b * C + c) * H + h] = s * inv;
+    if (c < C && h < H)
+      for (int d = h * dk; d < (h + 1) * dk; ++d) s = fma((double)Wq[(int64_t)d * C + c], S[d], s);
+    U[(int64_t)b * Cp * Hp + t] = s * inv;
   }
-  if (blockIdx.x == 0 && threadIdx.x < H) {
+  if (blockIdx.x == 0 && threadIdx.x < Hp) {
     const int h = threadIdx.x;
     double s = 0.0;
-    for (int d = h * dk; d < (h + 1) * dk; ++d) s = fma((double)bq[d], S[d], s);
-    v[(int64_t)b * H + h] = s * inv;
+    if (h < H)
+      for (int d = h * dk; d < (h + 1) * dk; ++d) s = fma((double)bq[d], S[d], s);
+    v[(int64_t)b * Hp + h] = s * inv;
   }
 }
 
-// cs[r,h] = x_r . U[b,:,h] + v[b,h]  (fp64 accumulation), GL lanes per row,
-// 64/GL rows per wavefront, every load of the row issued before the FMAs.
-template <int VEC, int GL, int MAXH>
-__global__ __launch_bounds__(256) void node_scores_kernel(const float* __restrict__ x, int64_t R, int64_t N, int C,
-                                                           int64_t ldx, int H, const double* __restrict__ U,
-                                                           const double* __restrict__ v, double* __restrict__ cs) {
-  constexpr int G = kWave / GL;
-  constexpr int NP = 4;  // column passes held in flight (C <= NP*GL*VEC handled in one sweep)
-  const int lane = threadIdx.x & 63;
-  const int g = lane / GL, gl = lane % GL;
-  const int64_t r = (int64_t)(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * G + g;
-  const bool live = r < R;
-  const int64_t rr = live ? r : R - 1;
-  const int64_t b = rr / N;
-  double acc[MAXH];
+// cs[b*N+n, h] = x_{b,n} . U[b,:,h] + v[b,h]  (fp64 accumulation).
+// GL lanes per row, G = 64/GL rows per wavefront step; each lane owns NPV
+// columns of a chunk of CW = GL*NPV columns.  When the row fits one chunk (the
+// usual case) the lane's slice of U[b] stays in registers for every row the
+// wave visits and the next row's x slice is prefetched while the current one
+// is reduced.  U is padded ([Cp][Hp], Cp = nch*CW, Hp = MAXH), so its loads
+// take compile-time offsets from one lane base; x loads past C (ragged last
+// chunk only) are clamped and zeroed.  No load sits behind a branch.
+constexpr int kNodeScoreURegs = 32;  // doubles of U held per lane
+
+template <int MAXH>
+constexpr int node_scores_npv() { return kNodeScoreURegs / MAXH; }
+
+template <int VEC, int NP, int GL, bool CLAMP>
+__device__ __forceinline__ void ns_load_x(const float* __restrict__ xrow, int cbase, int gl, int C,
+                                          float (&xv)[NP][VEC]) {
 #pragma unroll
-  for (int h = 0; h < MAXH; ++h) acc[h] = 0.0;
-  for (int c00 = 0; c00 < C; c00 += NP * GL * VEC) {
-    float xv[NP][VEC];
+  for (int p = 0; p < NP; ++p) {
+    const int c0 = cbase + (p * GL + gl) * VEC;
+    if constexpr (CLAMP) {
+      const bool ok = c0 < C;  // C % VEC == 0 (host)
+      float t[VEC];
+      load_vec<VEC>(xrow + (ok ? c0 : 0), t);
 #pragma unroll
-    for (int p = 0; p < NP; ++p) {
-      const int c0 = c00 + (p * GL + gl) * VEC;
-      if (c0 < C) {
-        load_vec<VEC>(x + rr * ldx + c0, xv[p]);
-      } else {
-#pragma unroll
-        for (int i = 0; i < VEC; ++i) xv[p][i] = 0.f;
-      }
-    }
-#pragma unroll
-    for (int p = 0; p < NP; ++p) {
-      const int c0 = c00 + (p * GL + gl) * VEC;
-      if (c0 < C) {
-#pragma unroll
-        for (int i = 0; i < VEC; ++i) {
-          const double* u = U + (b * C + c0 + i) * H;
-#pragma unroll
-          for (int h = 0; h < MAXH; ++h)
-            if (h < H) acc[h] = fma((double)xv[p][i], u[h], acc[h]);
-        }
-      }
+      for (int i = 0; i < VEC; ++i) xv[p][i] = ok ? t[i] : 0.f;
+    } else {
+      load_vec<VEC>(xrow + c0, xv[p]);
     }
   }
+}
+
+template <int VEC, int NP, int GL, int MAXH>
+__device__ __forceinline__ void ns_load_u(const double* __restrict__ Ub, int cbase, int gl,
+                                          double (&u)[NP][VEC][MAXH]) {
+  const double* __restrict__ base = Ub + (int64_t)(cbase + gl * VEC) * MAXH;
+#pragma unroll
+  for (int p = 0; p < NP; ++p)
+#pragma unroll
+    for (int i = 0; i < VEC; ++i)
+#pragma unroll
+      for (int h = 0; h < MAXH; ++h) u[p][i][h] = base[(p * GL * VEC + i) * MAXH + h];
+}
+
+template <int VEC, int NP, int MAXH>
+__device__ __forceinline__ void ns_dot(const float (&xv)[NP][VEC], const double (&u)[NP][VEC][MAXH],
+                                       double (&acc)[MAXH]) {
+#pragma unroll
+  for (int p = 0; p < NP; ++p)
+#pragma unroll
+    for (int i = 0; i < VEC; ++i)
+#pragma unroll
+      for (int h = 0; h < MAXH; ++h) acc[h] = fma((double)xv[p][i], u[p][i][h], acc[h]);
+}
+
+template <int GL, int MAXH>
+__device__ __forceinline__ void ns_store(double (&acc)[MAXH], const double (&vb)[MAXH], int gl, int H, bool live,
+                                         double* __restrict__ out) {
 #pragma unroll
   for (int o = 1; o < GL; o <<= 1)
 #pragma unroll
     for (int h = 0; h < MAXH; ++h) acc[h] += __shfl_xor(acc[h], o);
-  if (live && gl == 0) {
+  if (gl == 0 && live) {
 #pragma unroll
     for (int h = 0; h < MAXH; ++h)
-      if (h < H) cs[r * H + h] = acc[h] + v[b * H + h];
+      if (h < H) out[h] = acc[h] + vb[h];
+  }
+}
+
+template <int VEC, int GL, int MAXH, bool CLAMP>
+__device__ __forceinline__ void ns_rows_resident(const float* __restrict__ xb, const double* __restrict__ Ub,
+                                                 const double (&vb)[MAXH], double* __restrict__ csb, int64_t N,
+                                                 int64_t n0, int64_t n1, int C, int64_t ldx, int H, int g, int gl,
+                                                 int wv) {
+  constexpr int G = kWave / GL;
+  constexpr int NP = node_scores_npv<MAXH>() / VEC;
+  const int64_t step = (int64_t)kWavesPerBlock * G;
+  double u[NP][VEC][MAXH];
+  ns_load_u<VEC, NP, GL, MAXH>(Ub, 0, gl, u);
+  float xc[NP][VEC];
+  int64_t nb = n0 + wv * G;
+  ns_load_x<VEC, NP, GL, CLAMP>(xb + min(nb + g, N - 1) * ldx, 0, gl, C, xc);
+  for (; nb < n1; nb += step) {
+    const int64_t nr = nb + g;
+    float xn[NP][VEC];
+    ns_load_x<VEC, NP, GL, CLAMP>(xb + min(nr + step, N - 1) * ldx, 0, gl, C, xn);
+    double acc[MAXH];
+#pragma unroll
+    for (int h = 0; h < MAXH; ++h) acc[h] = 0.0;
+    ns_dot<VEC, NP, MAXH>(xc, u, acc);
+    ns_store<GL, MAXH>(acc, vb, gl, H, nr < n1, csb + nr * H);
+#pragma unroll
+    for (int p = 0; p < NP; ++p)
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) xc[p][i] = xn[p][i];
+  }
+}
+
+template <int VEC, int GL, int MAXH>
+__global__ __launch_bounds__(256) void node_scores_kernel(const float* __restrict__ x, int64_t B, int64_t N, int C,
+                                                           int64_t ldx, int H, int nch, const double* __restrict__ U,
+                                                           const double* __restrict__ v, double* __restrict__ cs,
+                                                           int64_t rows_per_block) {
+  constexpr int G = kWave / GL;
+  constexpr int NPV = node_scores_npv<MAXH>();
+  constexpr int NP = NPV / VEC;
+  constexpr int CW = GL * NPV;
+  static_assert(NP >= 1, "node_scores: VEC wider than the per-lane column budget");
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int g = lane / GL, gl = lane % GL;
+  const int64_t n0 = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t n1 = min(N, n0 + rows_per_block);
+  const int64_t step = (int64_t)kWavesPerBlock * G;
+  const bool ragged = C != nch * CW;
+  for (int64_t b = blockIdx.y; b < B; b += gridDim.y) {
+    const double* __restrict__ Ub = U + b * nch * CW * MAXH;
+    const float* __restrict__ xb = x + b * N * ldx;
+    double* __restrict__ csb = cs + b * N * H;
+    double vb[MAXH];
+#pragma unroll
+    for (int h = 0; h < MAXH; ++h) vb[h] = v[b * MAXH + h];
+    if (nch == 1) {
+      if (ragged)
+        ns_rows_resident<VEC, GL, MAXH, true>(xb, Ub, vb, csb, N, n0, n1, C, ldx, H, g, gl, wv);
+      else
+        ns_rows_resident<VEC, GL, MAXH, false>(xb, Ub, vb, csb, N, n0, n1, C, ldx, H, g, gl, wv);
+    } else {
+      for (int64_t nb = n0 + wv * G; nb < n1; nb += step) {
+        const int64_t nr = nb + g;
+        const float* xrow = xb + min(nr, N - 1) * ldx;
+        double acc[MAXH];
+#pragma unroll
+        for (int h = 0; h < MAXH; ++h) acc[h] = 0.0;
+        for (int ch = 0; ch < nch; ++ch) {
+          double u[NP][VEC][MAXH];
+          float xc[NP][VEC];
+          ns_load_x<VEC, NP, GL, true>(xrow, ch * CW, gl, C, xc);
+          ns_load_u<VEC, NP, GL, MAXH>(Ub, ch * CW, gl, u);
+          ns_dot<VEC, NP, MAXH>(xc, u, acc);
+        }
+        ns_store<GL, MAXH>(acc, vb, gl, H, nr < n1, csb + nr * H);
+      }
+    }
   }
 }
 
@@ -479,32 +621,64 @@ static void launch_stats(unsigned grid, int GL, hipStream_t s, const int4* it, i
     stats_kernel<MAXH, 64><<<grid, kBlock, 0, s>>>(it, n, gidx, gid, sa, m, rl, partials);
 }
 
-template <int VEC, int GL>
-static void launch_node_scores(unsigned grid, hipStream_t s, const float* x, int64_t R, int64_t N, int C, int64_t ldx,
-                               int H, const double* U, const double* v, double* cs) {
-  if (H <= 1)
-    node_scores_kernel<VEC, GL, 1><<<grid, kBlock, 0, s>>>(x, R, N, C, ldx, H, U, v, cs);
-  else if (H <= 2)
-    node_scores_kernel<VEC, GL, 2><<<grid, kBlock, 0, s>>>(x, R, N, C, ldx, H, U, v, cs);
-  else if (H <= 4)
-    node_scores_kernel<VEC, GL, 4><<<grid, kBlock, 0, s>>>(x, R, N, C, ldx, H, U, v, cs);
-  else if (H <= 8)
-    node_scores_kernel<VEC, GL, 8><<<grid, kBlock, 0, s>>>(x, R, N, C, ldx, H, U, v, cs);
-  else
-    node_scores_kernel<VEC, GL, 16><<<grid, kBlock, 0, s>>>(x, R, N, C, ldx, H, U, v, cs);
+// node_scores geometry: VEC, MAXH (= Hp), lanes per row GL (8..64) so one
+// chunk of CW = GL*NPV columns covers the row when it can, nch chunks.
+struct NsGeom {
+  int vec, maxh, GL, CW, nch;
+};
+
+static NsGeom ns_geometry(int vec, int64_t C, int64_t H) {
+  NsGeom g;
+  g.maxh = H <= 1 ? 1 : H <= 2 ? 2 : H <= 4 ? 4 : H <= 8 ? 8 : 16;
+  const int npv = kNodeScoreURegs / g.maxh;
+  g.vec = (vec == 4 && npv >= 4) ? 4 : 1;
+  g.GL = std::max(8, pow2_at_least((int)ceil_div(C, npv), 64));
+  g.CW = g.GL * npv;
+  g.nch = (int)ceil_div(C, g.CW);
+  return g;
 }
 
-template <int VEC>
-static void launch_node_scores_vec(unsigned grid, int GL, hipStream_t s, const float* x, int64_t R, int64_t N, int C,
-                                   int64_t ldx, int H, const double* U, const double* v, double* cs) {
-  if (GL <= 8)
-    launch_node_scores<VEC, 8>(grid, s, x, R, N, C, ldx, H, U, v, cs);
-  else if (GL <= 16)
-    launch_node_scores<VEC, 16>(grid, s, x, R, N, C, ldx, H, U, v, cs);
-  else if (GL <= 32)
-    launch_node_scores<VEC, 32>(grid, s, x, R, N, C, ldx, H, U, v, cs);
+template <int VEC, int MAXH>
+static void launch_node_scores(dim3 grid, const NsGeom& ge, hipStream_t s, const float* x, int64_t B, int64_t N, int C,
+                               int64_t ldx, int H, const double* U, const double* v, double* cs, int64_t rpb) {
+  const int n = ge.nch;
+  if (ge.GL <= 8)
+    node_scores_kernel<VEC, 8, MAXH><<<grid, kBlock, 0, s>>>(x, B, N, C, ldx, H, n, U, v, cs, rpb);
+  else if (ge.GL <= 16)
+    node_scores_kernel<VEC, 16, MAXH><<<grid, kBlock, 0, s>>>(x, B, N, C, ldx, H, n, U, v, cs, rpb);
+  else if (ge.GL <= 32)
+    node_scores_kernel<VEC, 32, MAXH><<<grid, kBlock, 0, s>>>(x, B, N, C, ldx, H, n, U, v, cs, rpb);
   else
-    launch_node_scores<VEC, 64>(grid, s, x, R, N, C, ldx, H, U, v, cs);
+    node_scores_kernel<VEC, 64, MAXH><<<grid, kBlock, 0, s>>>(x, B, N, C, ldx, H, n, U, v, cs, rpb);
+}
+
+// rows per block sized for ~4096 wavefronts over the whole launch (16 per CU)
+static void launch_node_scores_any(hipStream_t s, const NsGeom& ge, const float* x, int64_t B, int64_t N, int C,
+                                   int64_t ldx, int H, const double* U, const double* v, double* cs) {
+  const int G = kWave / ge.GL;
+  const int64_t groups = ceil_div(N, (int64_t)G);
+  const int64_t waves_per_batch = std::max<int64_t>(1, 4096 / B);
+  const int64_t iters = std::max<int64_t>(1, ceil_div(groups, waves_per_batch));
+  const int64_t rpb = (int64_t)kWavesPerBlock * G * iters;
+  const dim3 grid((unsigned)ceil_div(N, rpb), (unsigned)std::min<int64_t>(B, 65535));
+#define GNPDE_NS(V, M) launch_node_scores<V, M>(grid, ge, s, x, B, N, C, ldx, H, U, v, cs, rpb)
+  if (ge.vec == 4) {
+    switch (ge.maxh) {
+      case 1: GNPDE_NS(4, 1); break;
+      case 2: GNPDE_NS(4, 2); break;
+      case 4: GNPDE_NS(4, 4); break;
+      default: GNPDE_NS(4, 8); break;
+    }
+  } else {
+    switch (ge.maxh) {
+      case 1: GNPDE_NS(1, 1); break;
+      case 2: GNPDE_NS(1, 2); break;
+      case 4: GNPDE_NS(1, 4); break;
+      case 8: GNPDE_NS(1, 8); break;
+      default: GNPDE_NS(1, 16); break;
+    }
+  }
+#undef GNPDE_NS
 }
 
 // team geometry for the per-edge modes: VEC = 4, S = dk/4, T = H*S, both powers
@@ -526,8 +700,9 @@ static unsigned edge_grid(int64_t nnz) {
   return (unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(nnz, kBlock), 16384));
 }
 
+// a block takes kWavesPerBlock * 64 consecutive edges per pass (T per team)
 static unsigned team_grid(int64_t nnz, const Team& tm) {
-  const int64_t per_block = (int64_t)kWavesPerBlock * (kWave / tm.T);
+  const int64_t per_block = (int64_t)kWavesPerBlock * (kWave / tm.T) * tm.T;
   return (unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(nnz, per_block), 32768));
 }
 
@@ -638,8 +813,9 @@ size_t gnpde_keysum_workspace_bytes(int64_t B, int64_t N, int64_t C, int64_t att
   (void)att;
   int rpt, ntiles;
   keysum_tiles(B, N, &rpt, &ntiles);
-  const int64_t H = 16;  // upper bound on heads
-  return sizeof(double) * (size_t)(B * ntiles * (C + 1) + B * (C + 1) + B * C * H + B * H) + 256;
+  const int64_t H = 16;                                // upper bound on heads (padded Hp <= 16)
+  const int64_t Cp = std::max<int64_t>(256, 2 * C);    // >= the padded U rows of ns_geometry
+  return sizeof(double) * (size_t)(B * ntiles * (C + 1) + B * (C + 1) + B * Cp * H + B * H) + 256;
 }
 
 int gnpde_ref_scores_f32(const float* x, int64_t B, int64_t N, int64_t C, int64_t ldx, const int32_t* indeg,
@@ -659,8 +835,12 @@ int gnpde_ref_scores_f32(const float* x, int64_t B, int64_t N, int64_t C, int64_
   keysum_tiles(B, N, &rpt, &ntiles);
   double* part = static_cast<double*>(workspace);
   double* xbar = part + B * ntiles * (C + 1);
+  const NsGeom ge = ns_geometry(vec, C, heads);
+  const int64_t Cp = (int64_t)ge.nch * ge.CW, Hp = ge.maxh;
   double* U = xbar + B * (C + 1);
-  double* v = U + B * C * heads;
+  double* v = U + B * Cp * Hp;
+  GNPDE_REQUIRE((size_t)((char*)(v + B * Hp) - (char*)workspace) <= workspace_bytes, GNPDE_EUNSUPPORTED,
+                "ref_scores: padded U does not fit the workspace");
   const int rpb = kBlock / tpr;
   const size_t shm = sizeof(double) * (size_t)rpb * (C + 1);
   GNPDE_REQUIRE(shm <= 64 * 1024, GNPDE_EUNSUPPORTED, "ref_scores: C too large");
@@ -674,20 +854,11 @@ int gnpde_ref_scores_f32(const float* x, int64_t B, int64_t N, int64_t C, int64_
   GNPDE_LAUNCH_CHECK();
   keysum_tiles_kernel<<<dim3((unsigned)ceil_div(C + 1, 16), (unsigned)B), kBlock, 0, s>>>(part, ntiles, (int)C, xbar);
   GNPDE_LAUNCH_CHECK();
-  keysum_finish_kernel<<<dim3((unsigned)ceil_div(C * heads, kFinishPairs), (unsigned)B), kBlock,
-                         sizeof(double) * (size_t)att, s>>>(xbar, (int)C, Wq, bq, Wk, bk, (int)att, (int)heads, U, v);
+  keysum_finish_kernel<<<dim3((unsigned)ceil_div(Cp * Hp, kFinishPairs), (unsigned)B), kBlock,
+                         sizeof(double) * (size_t)att, s>>>(xbar, (int)C, Wq, bq, Wk, bk, (int)att, (int)heads,
+                                                            (int)Cp, (int)Hp, U, v);
   GNPDE_LAUNCH_CHECK();
-  const int64_t R = B * N;
-  // lanes per row: enough for the row in <= 4 VEC-wide passes, at least 8
-  const int GL = std::max(8, std::min(64, pow2_at_least((int)ceil_div(ceil_div(C, vec), 4), 64)));
-  const int rows_per_block = kWavesPerBlock * (kWave / GL);
-  const unsigned grid = (unsigned)ceil_div(R, rows_per_block);
-  if (vec == 4)
-    launch_node_scores_vec<4>(grid, GL, s, x, R, N, (int)C, ldx, (int)heads, U, v, cs);
-  else if (vec == 2)
-    launch_node_scores_vec<2>(grid, GL, s, x, R, N, (int)C, ldx, (int)heads, U, v, cs);
-  else
-    launch_node_scores_vec<1>(grid, GL, s, x, R, N, (int)C, ldx, (int)heads, U, v, cs);
+  launch_node_scores_any(s, ge, x, B, N, (int)C, ldx, (int)heads, U, v, cs);
   GNPDE_LAUNCH_CHECK();
   return GNPDE_OK;
 }

@@ -73,11 +73,11 @@ __device__ __forceinline__ float seg_sum(float v, int S) {
 
 // team mode: lane t (< T) of the team covers elements [t*VEC, t*VEC+VEC) of the
 // att-wide rows; returns the score of the lane's head (all S lanes agree).
+// Score from the lane's slices already in registers (q of the source, k of
+// the destination); the loads are left to the caller so several edges' rows
+// can be in flight at once.
 template <int VEC>
-__device__ __forceinline__ float team_score(const ScoreArgs& sa, int src, int dst, int t, int S) {
-  float q[VEC], k[VEC];
-  load_vec<VEC>(sa.q + (int64_t)src * sa.ldqk + t * VEC, q);
-  load_vec<VEC>(sa.k + (int64_t)dst * sa.ldqk + t * VEC, k);
+__device__ __forceinline__ float team_score_regs(const ScoreArgs& sa, float (&q)[VEC], float (&k)[VEC], int S) {
   const float dk = (float)sa.dk;
   if (sa.mode == GNPDE_SCORE_DOT) {
     float a = 0.f;
@@ -120,6 +120,20 @@ __device__ __forceinline__ float team_score(const ScoreArgs& sa, int src, int ds
   nk = seg_sum(nk, S);
   dot = seg_sum(dot, S);
   return dot / (fmaxf(sqrtf(nq), 1e-5f) * fmaxf(sqrtf(nk), 1e-5f));
+}
+
+template <int VEC>
+__device__ __forceinline__ void team_row(const ScoreArgs& sa, const float* __restrict__ base, int node, int t,
+                                         float (&v)[VEC]) {
+  load_vec<VEC>(base + (int64_t)node * sa.ldqk + t * VEC, v);
+}
+
+template <int VEC>
+__device__ __forceinline__ float team_score(const ScoreArgs& sa, int src, int dst, int t, int S) {
+  float q[VEC], k[VEC];
+  team_row<VEC>(sa, sa.q, src, t, q);
+  team_row<VEC>(sa, sa.k, dst, t, k);
+  return team_score_regs<VEC>(sa, q, k, S);
 }
 
 }  // namespace gnpde

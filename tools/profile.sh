@@ -13,7 +13,7 @@ BARGS=${BENCH_ARGS:---no-cpu-baseline}
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_${TAG}_trace -o run -- \
   python3 $R/bench.py $BARGS > $OUT/prof_${TAG}_trace.log 2>&1
 rc=$?; echo "trace rc=$rc"; tail -3 $OUT/prof_${TAG}_trace.log; if fatal $rc; then exit $rc; fi
-for ctr in ${PMCS:-FETCH_SIZE WRITE_SIZE}; do
+for ctr in ${PMCS-FETCH_SIZE WRITE_SIZE}; do
   timeout -k 10 600 rocprofv3 --pmc $ctr --kernel-include-regex "${KREGEX:-agg_kernel}" --output-format csv \
     -d $OUT/prof_${TAG}_pmc_$ctr -o run -- python3 $R/bench.py --no-cpu-baseline --no-attention --steps 5 --warmup 2 --rhs-plain-reps 5 \
     > $OUT/prof_${TAG}_pmc_$ctr.log 2>&1
