@@ -165,7 +165,16 @@ struct Team {
 // loaded once; the other endpoints' indices come in T at a time (one per
 // lane, then broadcast with shuffles) and kTeamEdges rows are in flight
 // together.  Edges are pushed in CSR order, as the lane-mode kernel does.
+// Loop trip counts are wave-uniform (maxima over the wave's teams), so every
+// shuffle runs with the whole wavefront active; a team past its own edges
+// computes throw-away scores and pushes nothing.
 constexpr int kTeamEdges = 4;
+
+__device__ __forceinline__ int wave_max_int(int v) {
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) v = max(v, __shfl_xor(v, o));
+  return v;
+}
 
 template <int VEC>
 __global__ __launch_bounds__(256) void stats_team_kernel(const int4* __restrict__ items, int n_items,
@@ -176,31 +185,35 @@ __global__ __launch_bounds__(256) void stats_team_kernel(const int4* __restrict_
   const int T = tm.T, S = tm.S, tpw = kWave / T;
   const int team = lane / T, t = lane % T, h = t / S;
   const int item = (blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * tpw + team;
-  const bool live = item < n_items && team < tpw;
+  const bool live = item < n_items;
   const int4 it = live ? items[item] : make_int4(0, 0, 0, -1);
   const int grp = it.x, beg = it.y, end = it.z, slot = it.w;
   float own[VEC];
   team_row<VEC>(sa, group_is_dst ? sa.k : sa.q, grp, t, own);
+  const float* __restrict__ other_base = group_is_dst ? sa.q : sa.k;
   double M = -INFINITY;
   float L = 0.f;
-  for (int p0 = beg; p0 < end; p0 += T) {
-    const int cnt = min(T, end - p0);
-    const int mine = gidx[p0 + min(t, cnt - 1)];
-    for (int j = 0; j < cnt; j += kTeamEdges) {
+  const int rounds = wave_max_int((end - beg + T - 1) / T);
+  for (int r = 0; r < rounds; ++r) {
+    const int p0 = beg + r * T;
+    const int cnt = max(0, min(T, end - p0));
+    int mine = 0;
+    if (cnt > 0) mine = gidx[p0 + min(t, cnt - 1)];
+    const int jmax = wave_max_int(cnt);
+    for (int j = 0; j < jmax; j += kTeamEdges) {
       float other[kTeamEdges][VEC];
 #pragma unroll
       for (int u = 0; u < kTeamEdges; ++u) {
-        const int o = __shfl(mine, team * T + min(j + u, cnt - 1));
-        team_row<VEC>(sa, group_is_dst ? sa.q : sa.k, o, t, other[u]);
+        const int o = __shfl(mine, team * T + max(0, min(j + u, cnt - 1)));
+        team_row<VEC>(sa, other_base, o, t, other[u]);
       }
+      float s[kTeamEdges];
 #pragma unroll
-      for (int u = 0; u < kTeamEdges; ++u) {
-        if (j + u < cnt) {
-          const float s = group_is_dst ? team_score_regs<VEC>(sa, other[u], own, S)
-                                       : team_score_regs<VEC>(sa, own, other[u], S);
-          online_push(M, L, (double)s);
-        }
-      }
+      for (int u = 0; u < kTeamEdges; ++u)
+        s[u] = group_is_dst ? team_score_regs<VEC>(sa, other[u], own, S) : team_score_regs<VEC>(sa, own, other[u], S);
+#pragma unroll
+      for (int u = 0; u < kTeamEdges; ++u)
+        if (j + u < cnt) online_push(M, L, (double)s[u]);
     }
   }
   if (!live || (t % S) != 0) return;
@@ -216,7 +229,8 @@ __global__ __launch_bounds__(256) void stats_team_kernel(const int4* __restrict_
 
 // Team-mode attention weights: a team takes T consecutive edges (indices
 // loaded one per lane, coalesced), then evaluates them kTeamEdges at a time
-// with the q/k rows and the group's softmax statistics all in flight.
+// with the q/k rows and the group's softmax statistics all in flight.  Trip
+// counts are wave-uniform, as in stats_team_kernel.
 template <int VEC, bool COO>
 __global__ __launch_bounds__(256) void attn_team_kernel(const int* __restrict__ rowidx, const int* __restrict__ col,
                                                          const int* __restrict__ perm, int64_t nnz, int norm_idx,
@@ -226,23 +240,30 @@ __global__ __launch_bounds__(256) void attn_team_kernel(const int* __restrict__ 
   const int T = tm.T, S = tm.S, tpw = kWave / T;
   const int team = lane / T, t = lane % T, h = t / S;
   const int H = sa.H;
-  if (team >= tpw) return;
   const bool leader = (t % S) == 0;
-  const int64_t nteams = (int64_t)gridDim.x * kWavesPerBlock * tpw;
-  for (int64_t p0 = ((int64_t)(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * tpw + team) * T; p0 < nnz;
-       p0 += nteams * T) {
-    const int cnt = (int)min((int64_t)T, nnz - p0);
-    const int64_t pm = p0 + min(t, cnt - 1);
-    const int my_r = rowidx[pm], my_c = col[pm];
-    const int my_dst = COO ? perm[pm] : 0;
-    for (int j = 0; j < cnt; j += kTeamEdges) {
+  const int64_t wave_first = (int64_t)(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * tpw * T;
+  const int64_t sweep = (int64_t)gridDim.x * kWavesPerBlock * tpw * T;
+  for (int64_t w0 = wave_first; w0 < nnz; w0 += sweep) {
+    const int64_t p0 = w0 + (int64_t)team * T;
+    const int cnt = (int)max((int64_t)0, min((int64_t)T, nnz - p0));
+    int my_r = 0, my_c = 0, my_dst = 0;
+    if (cnt > 0) {
+      const int64_t pm = p0 + min(t, cnt - 1);
+      my_r = rowidx[pm];
+      my_c = col[pm];
+      if (COO) my_dst = perm[pm];
+    }
+    const int jmax = wave_max_int(cnt);
+    for (int j = 0; j < jmax; j += kTeamEdges) {
       float qv[kTeamEdges][VEC], kv[kTeamEdges][VEC];
       double mv[kTeamEdges];
       float rv[kTeamEdges];
+      int dst[kTeamEdges];
 #pragma unroll
       for (int u = 0; u < kTeamEdges; ++u) {
-        const int src = team * T + min(j + u, cnt - 1);
+        const int src = team * T + max(0, min(j + u, cnt - 1));
         const int r = __shfl(my_r, src), c = __shfl(my_c, src);
+        dst[u] = COO ? __shfl(my_dst, src) : 0;
         team_row<VEC>(sa, sa.q, r, t, qv[u]);
         team_row<VEC>(sa, sa.k, c, t, kv[u]);
         const int64_t g = norm_idx == 0 ? r : c;
@@ -251,16 +272,13 @@ __global__ __launch_bounds__(256) void attn_team_kernel(const int* __restrict__ 
       }
 #pragma unroll
       for (int u = 0; u < kTeamEdges; ++u) {
-        const int dst = COO ? __shfl(my_dst, team * T + min(j + u, cnt - 1)) : 0;
-        if (j + u < cnt) {
-          const float s = team_score_regs<VEC>(sa, qv[u], kv[u], S);
-          float term = leader ? expf((float)((double)s - mv[u])) * rv[u] : 0.f;
-          if (COO) {
-            if (leader) out[(int64_t)dst * H + h] = term;
-          } else {
-            for (int o = S; o < T; o <<= 1) term += __shfl_xor(term, o);
-            if (t == 0) out[p0 + j + u] = term / (float)H;
-          }
+        const float s = team_score_regs<VEC>(sa, qv[u], kv[u], S);
+        float term = leader ? expf((float)((double)s - mv[u])) * rv[u] : 0.f;
+        if (COO) {
+          if (leader && j + u < cnt) out[(int64_t)dst[u] * H + h] = term;
+        } else {
+          for (int o = S; o < T; o <<= 1) term += __shfl_xor(term, o);
+          if (t == 0 && j + u < cnt) out[p0 + j + u] = term / (float)H;
         }
       }
     }
@@ -683,8 +701,17 @@ static void launch_node_scores_any(hipStream_t s, const NsGeom& ge, const float*
 
 // team geometry for the per-edge modes: VEC = 4, S = dk/4, T = H*S, both powers
 // of two, T <= 64; otherwise lane mode (T = 0).
+static bool team_mode_enabled() {  // GNPDE_TEAM=0 forces lane mode (diagnostics)
+  static const bool on = [] {
+    const char* e = std::getenv("GNPDE_TEAM");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 static Team team_geometry(const ScoreArgs& sa) {
   Team tm{0, 0};
+  if (!team_mode_enabled()) return tm;
   if (sa.mode != GNPDE_SCORE_DOT && sa.mode != GNPDE_SCORE_EXP_KERNEL && sa.mode != GNPDE_SCORE_COSINE &&
       sa.mode != GNPDE_SCORE_PEARSON)
     return tm;

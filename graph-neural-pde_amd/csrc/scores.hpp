@@ -75,9 +75,17 @@ __device__ __forceinline__ float seg_sum(float v, int S) {
 // att-wide rows; returns the score of the lane's head (all S lanes agree).
 // Score from the lane's slices already in registers (q of the source, k of
 // the destination); the loads are left to the caller so several edges' rows
-// can be in flight at once.
+// can be in flight at once.  The shuffles of seg_sum must run with every lane
+// of the wavefront active (callers keep these calls out of divergent code).
 template <int VEC>
-__device__ __forceinline__ float team_score_regs(const ScoreArgs& sa, float (&q)[VEC], float (&k)[VEC], int S) {
+__device__ __forceinline__ float team_score_regs(const ScoreArgs& sa, const float (&qin)[VEC], const float (&kin)[VEC],
+                                                 int S) {
+  float q[VEC], k[VEC];
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) {
+    q[i] = qin[i];
+    k[i] = kin[i];
+  }
   const float dk = (float)sa.dk;
   if (sa.mode == GNPDE_SCORE_DOT) {
     float a = 0.f;

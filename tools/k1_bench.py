@@ -46,7 +46,8 @@ def main():
         ws = gi._Workspace()
         t_step = timeit(lambda: gi._fused_step('rk4', func, 0.0, 0.25, 0.25, x, ws), 20)
         t_step_unfused = timeit(lambda: gi._fixed_step('rk4', func, 0.0, 0.25, 0.25, x, gi._Combine()), 10)
-    print(json.dumps({"variant": int(os.environ.get("GNPDE_AGG_VARIANT", "0")), "N": N, "E": E, "C": C,
+    print(json.dumps({"variant": int(os.environ.get("GNPDE_AGG_VARIANT", "0")),
+                      "bpc": os.environ.get("GNPDE_AGG_BPC", "auto"), "N": N, "E": E, "C": C,
                       "rhs_us": round(t_rhs, 2), "rk4_fused_us": round(t_step, 1),
                       "rk4_unfused_us": round(t_step_unfused, 1),
                       "rhs_GBs": round((4 * E * C + 8 * N * C + 8 * E + 4 * (N + 1)) / t_rhs / 1e3, 1)}))
