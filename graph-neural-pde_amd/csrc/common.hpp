@@ -203,4 +203,27 @@ __device__ __forceinline__ void epilogue_store(const Epi& e, int64_t row, int cc
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
+// ------------------------------------------------------------------ buffer memory ops
+// Raw buffer loads/stores take a 32-bit byte offset from a wave-uniform base,
+// and the hardware drops an access at or past num_records: a lane with nothing
+// to load or store passes kBufNone, so predicated accesses need no branch.
+// That matters on gfx9, where stores count in vmcnt: a store under a branch
+// makes the compiler's later waits conservative (vmcnt(0)), which serialises
+// every following store and load behind it.  Byte offsets must stay below
+// kBufRecords (callers check their buffer sizes).
+constexpr uint32_t kBufRecords = 0xffffff00u;
+constexpr uint32_t kBufNone = 0xfffffff0u;
+constexpr int kWaitVm0 = 0x0f70;  // s_waitcnt vmcnt(0) (expcnt, lgkmcnt at max)
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)kBufRecords, 0x00020000);
+}
+__device__ __forceinline__ void buf_store_f32(__amdgpu_buffer_rsrc_t r, uint32_t off, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, off, 0, 0);
+}
+__device__ __forceinline__ void buf_store_f64(__amdgpu_buffer_rsrc_t r, uint32_t off, double v) {
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, off, 0, 0);
+}
+
 }  // namespace gnpde

@@ -59,6 +59,19 @@ __global__ __launch_bounds__(256) void linear_mfma_kernel(const float* __restric
   const int Kh = (K + 1) >> 1;
   const int Khp = (Kh + kLinChunk - 1) / kLinChunk * kLinChunk;
   const int col0 = blockIdx.y * kLinCols;
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const int r32 = lane & 31, h = lane >> 5;
+  const int row0 = (blockIdx.x * kWavesPerBlock + wv) * kLinRowsPerWave;
+  const bool wave_live = row0 < R;  // no early return: every wave takes part in the staging barrier
+  const int my_row = min(row0 + r32, R - 1);
+  const float* __restrict__ xr = x + (int64_t)my_row * ldx;
+  const int kbase = h * Kh;
+
+  // this wave's first chunk of x goes out before the W^T staging
+  float a_cur[kLinChunk], a_nxt[kLinChunk];
+  lin_load_chunk<VEC4>(xr, kbase, 0, Kh, K, a_cur);
+
   // Stage W^T: wave wv fills columns j = wv + 4*jj, lanes walk the k rows
   // (coalesced along k).  Buffer loads with 32-bit offsets: a padding element
   // (k past the half, n past Nout) gets an out-of-range offset and reads 0, so
@@ -66,7 +79,6 @@ __global__ __launch_bounds__(256) void linear_mfma_kernel(const float* __restric
   {
     const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float*>(W), 0, Nout * K * (int)sizeof(float), 0x00020000);
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     for (int kr = lane; kr < 2 * Khp; kr += kWave) {
       const int hh = kr >= Khp ? 1 : 0;
       const int sidx = kr - hh * Khp;
@@ -84,20 +96,13 @@ __global__ __launch_bounds__(256) void linear_mfma_kernel(const float* __restric
     }
   }
   __syncthreads();
+  // Explicit: the loop head then sees no pending load, so the compiler's merge
+  // there does not make every chunk wait for the next chunk's prefetch.
+  __builtin_amdgcn_s_waitcnt(kWaitVm0);
+  if (!wave_live) return;
 
-  const int lane = threadIdx.x & 63;
-  const int wv = threadIdx.x >> 6;
-  const int r32 = lane & 31, h = lane >> 5;
-  const int row0 = (blockIdx.x * kWavesPerBlock + wv) * kLinRowsPerWave;
-  if (row0 >= R) return;
-  const int my_row = min(row0 + r32, R - 1);
-  const float* __restrict__ xr = x + (int64_t)my_row * ldx;
-  const int kbase = h * Kh;
   const float* __restrict__ wbase = wt + h * Khp * kLinLdsStride;
-
   f32x16 acc0 = {0}, acc1 = {0};
-  float a_cur[kLinChunk], a_nxt[kLinChunk];
-  lin_load_chunk<VEC4>(xr, kbase, 0, Kh, K, a_cur);
   for (int s0 = 0; s0 < Khp; s0 += kLinChunk) {
     if (s0 + kLinChunk < Khp) lin_load_chunk<VEC4>(xr, kbase, s0 + kLinChunk, Kh, K, a_nxt);
     float b0[kLinChunk], b1[kLinChunk];
@@ -115,21 +120,43 @@ __global__ __launch_bounds__(256) void linear_mfma_kernel(const float* __restric
 #pragma unroll
     for (int i = 0; i < kLinChunk; ++i) a_cur[i] = a_nxt[i];
   }
-  // C/D layout (32x32): col = lane&31, row = (reg&3) + 8*(reg>>2) + 4*(lane>>5)
+
+  // Epilogue.  C/D layout (32x32): col = lane&31, row = (reg&3) + 8*(reg>>2) + 4*(lane>>5).
+  // Each lane owns one column per tile: its bias, destination (out_a or
+  // out_b) and stride are fixed up front; a whole in-range tile stores with
+  // no branch (a conditional store would make every later wait drain vmcnt,
+  // stores included, serialising them).
+  float bv[2];
+  float* dst[2];
+  int64_t ld[2];
 #pragma unroll
   for (int tile = 0; tile < 2; ++tile) {
     const int n = col0 + tile * 32 + r32;
-    if (n >= Nout) continue;
-    const float bv = bias ? bias[n] : 0.f;
+    const int nc = n < Nout ? n : 0;
+    const float bb = bias ? bias[nc] : 0.f;
+    bv[tile] = n < Nout ? bb : 0.f;
+    const bool to_a = n < split;
+    dst[tile] = to_a ? out_a + nc : out_b + (nc - split);
+    ld[tile] = to_a ? lda : ldb;
+  }
+  const bool full = row0 + kLinRowsPerWave <= R && col0 + kLinCols <= Nout;
+  if (full) {
 #pragma unroll
     for (int reg = 0; reg < 16; ++reg) {
       const int row = row0 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
-      if (row >= R) continue;
-      const float val = (tile == 0 ? acc0[reg] : acc1[reg]) + bv;
-      if (n < split)
-        out_a[(int64_t)row * lda + n] = val;
-      else
-        out_b[(int64_t)row * ldb + (n - split)] = val;
+      dst[0][(int64_t)row * ld[0]] = acc0[reg] + bv[0];
+      dst[1][(int64_t)row * ld[1]] = acc1[reg] + bv[1];
+    }
+  } else {
+#pragma unroll
+    for (int tile = 0; tile < 2; ++tile) {
+      const int n = col0 + tile * 32 + r32;
+      if (n >= Nout) continue;
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const int row = row0 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+        if (row < R) dst[tile][(int64_t)row * ld[tile]] = (tile == 0 ? acc0[reg] : acc1[reg]) + bv[tile];
+      }
     }
   }
 }

@@ -241,6 +241,7 @@ __global__ __launch_bounds__(256) void attn_team_kernel(const int* __restrict__ 
   const int team = lane / T, t = lane % T, h = t / S;
   const int H = sa.H;
   const bool leader = (t % S) == 0;
+  const __amdgpu_buffer_rsrc_t rout = buf_rsrc(out);
   const int64_t wave_first = (int64_t)(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * tpw * T;
   const int64_t sweep = (int64_t)gridDim.x * kWavesPerBlock * tpw * T;
   for (int64_t w0 = wave_first; w0 < nnz; w0 += sweep) {
@@ -275,10 +276,12 @@ __global__ __launch_bounds__(256) void attn_team_kernel(const int* __restrict__ 
         const float s = team_score_regs<VEC>(sa, qv[u], kv[u], S);
         float term = leader ? expf((float)((double)s - mv[u])) * rv[u] : 0.f;
         if (COO) {
-          if (leader && j + u < cnt) out[(int64_t)dst[u] * H + h] = term;
+          const bool st = leader && j + u < cnt;
+          buf_store_f32(rout, st ? (uint32_t)(((int64_t)dst[u] * H + h) * 4) : kBufNone, term);
         } else {
           for (int o = S; o < T; o <<= 1) term += __shfl_xor(term, o);
-          if (t == 0 && j + u < cnt) out[p0 + j + u] = term / (float)H;
+          const bool st = t == 0 && j + u < cnt;
+          buf_store_f32(rout, st ? (uint32_t)((p0 + j + u) * 4) : kBufNone, term / (float)H);
         }
       }
     }
@@ -448,23 +451,24 @@ __device__ __forceinline__ void ns_dot(const float (&xv)[NP][VEC], const double 
       for (int h = 0; h < MAXH; ++h) acc[h] = fma((double)xv[p][i], u[p][i][h], acc[h]);
 }
 
+// reduce over the GL lanes of a row and store cs[row, :H] from lane gl == 0
+// (branch-free buffer stores; other lanes and heads past H pass kBufNone)
 template <int GL, int MAXH>
 __device__ __forceinline__ void ns_store(double (&acc)[MAXH], const double (&vb)[MAXH], int gl, int H, bool live,
-                                         double* __restrict__ out) {
+                                         __amdgpu_buffer_rsrc_t rcs, int64_t row) {
 #pragma unroll
   for (int o = 1; o < GL; o <<= 1)
 #pragma unroll
     for (int h = 0; h < MAXH; ++h) acc[h] += __shfl_xor(acc[h], o);
-  if (gl == 0 && live) {
+  const bool st = gl == 0 && live;
 #pragma unroll
-    for (int h = 0; h < MAXH; ++h)
-      if (h < H) out[h] = acc[h] + vb[h];
-  }
+  for (int h = 0; h < MAXH; ++h)
+    buf_store_f64(rcs, (st && h < H) ? (uint32_t)((row * H + h) * 8) : kBufNone, acc[h] + vb[h]);
 }
 
 template <int VEC, int GL, int MAXH, bool CLAMP>
 __device__ __forceinline__ void ns_rows_resident(const float* __restrict__ xb, const double* __restrict__ Ub,
-                                                 const double (&vb)[MAXH], double* __restrict__ csb, int64_t N,
+                                                 const double (&vb)[MAXH], __amdgpu_buffer_rsrc_t rcs, int64_t N,
                                                  int64_t n0, int64_t n1, int C, int64_t ldx, int H, int g, int gl,
                                                  int wv) {
   constexpr int G = kWave / GL;
@@ -483,7 +487,7 @@ __device__ __forceinline__ void ns_rows_resident(const float* __restrict__ xb, c
 #pragma unroll
     for (int h = 0; h < MAXH; ++h) acc[h] = 0.0;
     ns_dot<VEC, NP, MAXH>(xc, u, acc);
-    ns_store<GL, MAXH>(acc, vb, gl, H, nr < n1, csb + nr * H);
+    ns_store<GL, MAXH>(acc, vb, gl, H, nr < n1, rcs, nr);
 #pragma unroll
     for (int p = 0; p < NP; ++p)
 #pragma unroll
@@ -510,15 +514,15 @@ __global__ __launch_bounds__(256) void node_scores_kernel(const float* __restric
   for (int64_t b = blockIdx.y; b < B; b += gridDim.y) {
     const double* __restrict__ Ub = U + b * nch * CW * MAXH;
     const float* __restrict__ xb = x + b * N * ldx;
-    double* __restrict__ csb = cs + b * N * H;
+    const __amdgpu_buffer_rsrc_t rcs = buf_rsrc(cs + b * N * H);
     double vb[MAXH];
 #pragma unroll
     for (int h = 0; h < MAXH; ++h) vb[h] = v[b * MAXH + h];
     if (nch == 1) {
       if (ragged)
-        ns_rows_resident<VEC, GL, MAXH, true>(xb, Ub, vb, csb, N, n0, n1, C, ldx, H, g, gl, wv);
+        ns_rows_resident<VEC, GL, MAXH, true>(xb, Ub, vb, rcs, N, n0, n1, C, ldx, H, g, gl, wv);
       else
-        ns_rows_resident<VEC, GL, MAXH, false>(xb, Ub, vb, csb, N, n0, n1, C, ldx, H, g, gl, wv);
+        ns_rows_resident<VEC, GL, MAXH, false>(xb, Ub, vb, rcs, N, n0, n1, C, ldx, H, g, gl, wv);
     } else {
       for (int64_t nb = n0 + wv * G; nb < n1; nb += step) {
         const int64_t nr = nb + g;
@@ -533,7 +537,7 @@ __global__ __launch_bounds__(256) void node_scores_kernel(const float* __restric
           ns_load_u<VEC, NP, GL, MAXH>(Ub, ch * CW, gl, u);
           ns_dot<VEC, NP, MAXH>(xc, u, acc);
         }
-        ns_store<GL, MAXH>(acc, vb, gl, H, nr < n1, csb + nr * H);
+        ns_store<GL, MAXH>(acc, vb, gl, H, nr < n1, rcs, nr);
       }
     }
   }
@@ -804,7 +808,8 @@ int gnpde_attn_weights_f32(const int32_t* rowidx, const int32_t* col, int64_t nn
   if (nnz == 0) return GNPDE_OK;
   GNPDE_REQUIRE(rowidx && col && m && rl && w_out, GNPDE_EINVAL, "attn_weights: NULL pointer");
   const ScoreArgs sa = make_score_args(mode, heads, dk, cs, q, k, ldqk, score_p0, score_p1);
-  const Team tm = team_geometry(sa);
+  Team tm = team_geometry(sa);
+  if ((uint64_t)nnz * 4 >= kBufRecords) tm.T = 0;  // buffer-store offsets are 32-bit
   if (tm.T > 0)
     attn_team_kernel<4, false><<<team_grid(nnz, tm), kBlock, 0, as_stream(stream)>>>(rowidx, col, nullptr, nnz, norm_idx,
                                                                                     sa, tm, m, rl, w_out);
@@ -825,7 +830,8 @@ int gnpde_edge_attention_f32(const int32_t* rowidx, const int32_t* col, const in
   if (nnz == 0) return GNPDE_OK;
   GNPDE_REQUIRE(rowidx && col && perm && m && rl && att, GNPDE_EINVAL, "edge_attention: NULL pointer");
   const ScoreArgs sa = make_score_args(mode, heads, dk, cs, q, k, ldqk, score_p0, score_p1);
-  const Team tm = team_geometry(sa);
+  Team tm = team_geometry(sa);
+  if ((uint64_t)nnz * heads * 4 >= kBufRecords) tm.T = 0;  // buffer-store offsets are 32-bit
   if (tm.T > 0)
     attn_team_kernel<4, true><<<team_grid(nnz, tm), kBlock, 0, as_stream(stream)>>>(rowidx, col, perm, nnz, norm_idx, sa,
                                                                                    tm, m, rl, att);
@@ -855,6 +861,7 @@ int gnpde_ref_scores_f32(const float* x, int64_t B, int64_t N, int64_t C, int64_
   GNPDE_REQUIRE(workspace_bytes >= gnpde_keysum_workspace_bytes(B, N, C, att), GNPDE_EINVAL,
                 "ref_scores: workspace too small");
   GNPDE_REQUIRE(att <= 8192, GNPDE_EUNSUPPORTED, "ref_scores: attention_dim too large");
+  GNPDE_REQUIRE((uint64_t)N * heads * 8 < kBufRecords, GNPDE_EUNSUPPORTED, "ref_scores: N*heads too large");
   hipStream_t s = as_stream(stream);
   const int vec = keysum_vec(C, x, ldx);
   const int tpr = pow2_at_least((int)ceil_div(C, vec), 256);
