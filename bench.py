@@ -46,10 +46,10 @@ def lap_bytes(N, E, C, add_source=False):
 def rk4_fused_step_bytes(N, E, C):
     """Algorithmic bytes of one rk4 step with the stage combinations fused into
     the four K1 epilogues (gnpde.integrator._fused_step): 4 x (gathers 4EC +
-    indices 8E + rowptr 4(N+1) + input row 4NC) + 15 state passes of 4NC
-    (stage 1 writes ya, acc, k1; stage 2 reads y0, k1, acc, writes yb, acc;
-    stage 3 reads y0, k1, acc, writes yc, acc; stage 4 reads acc, writes acc)."""
-    return 4 * (4 * E * C + 8 * E + 4 * (N + 1) + 4 * N * C) + 15 * 4 * N * C
+    indices 8E + rowptr 4(N+1) + input row 4NC) + 8 state passes of 4NC
+    (stage 1 writes x2; stage 2 reads y, writes x3; stage 3 reads x2, writes
+    x4; stage 4 reads x3 and y, writes y1)."""
+    return 4 * (4 * E * C + 8 * E + 4 * (N + 1) + 4 * N * C) + 8 * 4 * N * C
 
 
 def attn_bytes(N, E, C, att, mode):

@@ -135,20 +135,22 @@ def _fused_step(method, func, t0, dt, t1, y0, ws):
         func.rhs_stage(t0, y0, ops.Stage(outs=[(ym, y0, 1.0, 0.5 * dt, [])]))
         func.rhs_stage(t0 + 0.5 * dt, ym, ops.Stage(outs=[(y1, y0, 1.0, dt, [])]))
         return y1
-    if method == 'rk4':  # rk4_alt_step_func (3/8 rule) with a running accumulator
-        ya, yb, yc, k1 = ws.get('a', y0), ws.get('b', y0), ws.get('c', y0), ws.get('k1', y0)
-        acc = torch.empty_like(y0)
-        # k1 = f(y0):  ya = y0 + dt/3 k1;  acc = y0 + dt/8 k1
-        func.rhs_stage(t0, y0, ops.Stage(f_out=k1, outs=[(ya, y0, 1.0, dt / 3.0, []), (acc, y0, 1.0, dt * 0.125, [])]))
-        # k2 = f(ya):  yb = y0 + dt (k2 - k1/3);  acc += 3dt/8 k2
-        func.rhs_stage(t0 + dt / 3.0, ya, ops.Stage(outs=[(yb, y0, 1.0, dt, [(k1, -dt / 3.0)]),
-                                                          (acc, acc, 1.0, dt * 0.375, [])]))
-        # k3 = f(yb):  yc = y0 + dt (k1 - k2 + k3) = 2 y0 - yb + 2dt/3 k1 + dt k3;  acc += 3dt/8 k3
-        func.rhs_stage(t0 + dt * 2.0 / 3.0, yb, ops.Stage(outs=[(yc, yb, -1.0, dt, [(y0, 2.0), (k1, dt * 2.0 / 3.0)]),
-                                                                (acc, acc, 1.0, dt * 0.375, [])]))
-        # k4 = f(yc):  y1 = acc + dt/8 k4
-        func.rhs_stage(t1, yc, ops.Stage(outs=[(acc, acc, 1.0, dt * 0.125, [])]))
-        return acc
+    if method == 'rk4':
+        # rk4_alt_step_func (3/8 rule).  With x2 = y + dt k1/3 the stage inputs
+        # and the result are affine in rows the epilogue already holds (its own
+        # input row comes for free), so no k_i is ever stored:
+        #   x3 = y + dt (k2 - k1/3)      = 2 y  - x2 + dt k2
+        #   x4 = y + dt (k1 - k2 + k3)   = 2 x2 - x3 + dt k3
+        #   y1 = y + dt/8 (k1 + 3k2 + 3k3 + k4) = (6 x3 + 3 x4 - y + dt k4) / 8
+        # 8 state passes per step besides the gathers (one write per stage,
+        # reads of y, x2, y + x3), where storing k's and an accumulator takes 15.
+        x2, x3, x4 = ws.get('a', y0), ws.get('b', y0), ws.get('c', y0)
+        y1 = torch.empty_like(y0)
+        func.rhs_stage(t0, y0, ops.Stage(outs=[(x2, y0, 1.0, dt / 3.0, [])]))
+        func.rhs_stage(t0 + dt / 3.0, x2, ops.Stage(outs=[(x3, x2, -1.0, dt, [(y0, 2.0)])]))
+        func.rhs_stage(t0 + dt * 2.0 / 3.0, x3, ops.Stage(outs=[(x4, x3, -1.0, dt, [(x2, 2.0)])]))
+        func.rhs_stage(t1, x4, ops.Stage(outs=[(y1, x4, 0.375, dt * 0.125, [(x3, 0.75), (y0, -0.125)])]))
+        return y1
     raise ValueError(method)
 
 
