@@ -213,9 +213,9 @@ static int launch_agg_vec(const int4* items, int64_t n_items, const int4* heavy,
   return GNPDE_EUNSUPPORTED;
 }
 
-template <class WP>
-static int launch_agg(const int32_t* items, int64_t n_items, const int32_t* heavy, int64_t n_heavy,
-                      const int32_t* col, const WP& wp, int64_t C, const Epi& ep, float* partials, hipStream_t s) {
+// Widest vector (4, 2 or 1 floats) every operand of the aggregation and its
+// epilogue allows: C, the leading dimensions and all pointers must agree.
+inline int epi_vec_width(const Epi& ep, int64_t C, const void* partials) {
   const bool src_ok4 = !(ep.flags & GNPDE_ADD_SOURCE) || (ep.ldx0 % 4 == 0 && aligned16(ep.x0));
   const bool src_ok2 = !(ep.flags & GNPDE_ADD_SOURCE) || (ep.ldx0 % 2 == 0 && aligned8(ep.x0));
   bool st4 = true, st2 = true;
@@ -235,16 +235,26 @@ static int launch_agg(const int32_t* items, int64_t n_items, const int32_t* heav
   } else {
     chk(ep.f);
   }
-  const bool v4 = C % 4 == 0 && ep.ldx % 4 == 0 && ep.ldf % 4 == 0 && aligned16(ep.x) && st4 && src_ok4 &&
-                  (partials == nullptr || aligned16(partials));
-  const bool v2 = C % 2 == 0 && ep.ldx % 2 == 0 && ep.ldf % 2 == 0 && aligned8(ep.x) && st2 && src_ok2 &&
-                  (partials == nullptr || aligned8(partials));
+  if (C % 4 == 0 && ep.ldx % 4 == 0 && ep.ldf % 4 == 0 && aligned16(ep.x) && st4 && src_ok4 &&
+      (partials == nullptr || aligned16(partials)))
+    return 4;
+  if (C % 2 == 0 && ep.ldx % 2 == 0 && ep.ldf % 2 == 0 && aligned8(ep.x) && st2 && src_ok2 &&
+      (partials == nullptr || aligned8(partials)))
+    return 2;
+  return 1;
+}
+
+template <class WP>
+static int launch_agg(const int32_t* items, int64_t n_items, const int32_t* heavy, int64_t n_heavy,
+                      const int32_t* col, const WP& wp, int64_t C, const Epi& ep, float* partials, hipStream_t s) {
   const int4* it = reinterpret_cast<const int4*>(items);
   const int4* hv = reinterpret_cast<const int4*>(heavy);
   const int c = (int)C;
-  if (v4) return launch_agg_vec<4>(it, n_items, hv, n_heavy, col, wp, c, ep, partials, s);
-  if (v2) return launch_agg_vec<2>(it, n_items, hv, n_heavy, col, wp, c, ep, partials, s);
-  return launch_agg_vec<1>(it, n_items, hv, n_heavy, col, wp, c, ep, partials, s);
+  switch (epi_vec_width(ep, C, partials)) {
+    case 4: return launch_agg_vec<4>(it, n_items, hv, n_heavy, col, wp, c, ep, partials, s);
+    case 2: return launch_agg_vec<2>(it, n_items, hv, n_heavy, col, wp, c, ep, partials, s);
+    default: return launch_agg_vec<1>(it, n_items, hv, n_heavy, col, wp, c, ep, partials, s);
+  }
 }
 
 }  // namespace gnpde

@@ -1,0 +1,357 @@
+// attention.hip — K2: edge-block segmented softmax of the attention RHS.
+//
+// One RHS of the transformer function needs, per edge e = (i -> j) and head h,
+//   s_e,h   = score(q_i, k_j)                           (SDDMM)
+//   a_e,h   = exp(s_e,h - max_g s) / (sum_g exp(. - max) + 1e-16)   over the group g
+//             of e (its source i for attention_norm_idx 0, its destination j for 1)
+//   w_e     = (1/H) sum_h a_e,h                          (head mean)
+// and then ax_i = sum_e w_e x_j (K1, aggregate.hpp).  Reference:
+//   SpGraphTransAttentionLayer.forward  src/function_transformer_attention.py:218-266
+//   utils.softmax                       src/utils.py:116-127
+//   multiply_attention head mean        src/function_transformer_attention.py:33-41
+//
+// Work decomposition (why not one group per wavefront): the graphs are
+// power-law with a mean degree of ~7, so a wavefront per group leaves most
+// lanes idle and serialises one dependent gather chain per few edges.  Here a
+// wavefront takes an ITEM = a range of at most EB (<= 64) consecutive edges of
+// the grouped CSR:
+//   * a block of consecutive whole groups, packed greedily up to EB edges
+//     (gnpde_seg_plan_build, once per graph), or
+//   * a chunk of EB edges of a longer group (slot >= 0: partial statistics,
+//     merged by the stats fixup of rhs.hip).
+// Lane e of the wavefront owns edge e0 + e.  Scores are computed in the team
+// layout (T = H*dk/4 lanes per edge, 16-byte q/k slices, up to kSegRounds
+// rounds of 64/T edges, kSegBatch rounds of rows in flight together), moved to
+// lane layout one head at a time, and the per-group max and sum-exp come from
+// segmented inclusive scans over the lanes built from DPP row shifts and row
+// broadcasts (VALU only, fixed order: deterministic), read back at the
+// group's last lane.  (A design that also fused the x aggregation into this pass measured
+// slower than this kernel + K1: the score latency in front of the gathers
+// costs more than the 8 bytes per edge of weights)
+//
+// Outputs (OUT): kSegWeights = head-mean weights w[p] in grouped-CSR order
+// (norm_idx 0, where the grouped CSR IS the aggregation CSR), chunk items ->
+// partials; kSegStats = group statistics m[g,h] (fp64 max), rl[g,h] =
+// 1/(sum + 1e-16) (norm_idx 1 over the CSC, read by the edge-parallel weight
+// kernels of rhs.hip), chunk items -> partials; kSegChunkWeights = weights of
+// the chunk items from the merged statistics of their group.
+#include <type_traits>
+
+#include "aggregate.hpp"
+#include "rhs_host.hpp"
+
+namespace gnpde {
+
+constexpr int kSegRounds = 8;       // team rounds per item: EB = min(64, 8 * 64/T) edges
+constexpr int kSegBatch = 4;        // rounds whose q/k slices are in flight together
+
+enum { kSegWeights = 0, kSegStats = 1, kSegChunkWeights = 2 };
+
+// ------------------------------------------------------------------ DPP cross-lane steps
+// gfx9 DPP controls: row_shr:n (from lane - n inside a 16-lane row), row_bcast:15
+// (lane 15 of each row to the next row), row_bcast:31 (lane 31 to rows 2-3).
+// Lanes without a source keep `old`.  VALU only: no LDS-pipe permutes.
+constexpr int kDppRowShr = 0x110;
+constexpr int kDppBcast15 = 0x142;
+constexpr int kDppBcast31 = 0x143;
+constexpr int kDppQuadXor1 = 0xB1;  // quad_perm [1,0,3,2]
+constexpr int kDppQuadXor2 = 0x4E;  // quad_perm [2,3,0,1]
+
+template <int CTRL, int ROWS>
+__device__ __forceinline__ int dpp_i(int old, int v) {
+  return __builtin_amdgcn_update_dpp(old, v, CTRL, ROWS, 0xf, false);
+}
+template <int CTRL, int ROWS>
+__device__ __forceinline__ float dpp_f(float old, float v) {
+  return __builtin_bit_cast(float, dpp_i<CTRL, ROWS>(__builtin_bit_cast(int, old), __builtin_bit_cast(int, v)));
+}
+template <int CTRL, int ROWS>
+__device__ __forceinline__ double dpp_d(double old, double v) {
+  const long long o = __builtin_bit_cast(long long, old), x = __builtin_bit_cast(long long, v);
+  const int lo = dpp_i<CTRL, ROWS>((int)o, (int)x);
+  const int hi = dpp_i<CTRL, ROWS>((int)(o >> 32), (int)(x >> 32));
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
+}
+template <int CTRL, int ROWS, class V>
+__device__ __forceinline__ V dpp(V old, V v) {
+  if constexpr (sizeof(V) == 8) return dpp_d<CTRL, ROWS>(old, v);
+  else return dpp_f<CTRL, ROWS>(old, v);
+}
+
+// The six steps of a wave-wide inclusive scan: row_shr 1,2,4,8, then
+// row_bcast15 into rows 1 and 3, then row_bcast31 into rows 2 and 3.
+// seg_flags: bit k set when the source lane of step k is in the same group.
+__device__ __forceinline__ unsigned seg_flags(int grp) {
+  unsigned f = 0;
+  f |= (dpp_i<kDppRowShr + 1, 0xf>(-1, grp) == grp) ? 1u : 0u;
+  f |= (dpp_i<kDppRowShr + 2, 0xf>(-1, grp) == grp) ? 2u : 0u;
+  f |= (dpp_i<kDppRowShr + 4, 0xf>(-1, grp) == grp) ? 4u : 0u;
+  f |= (dpp_i<kDppRowShr + 8, 0xf>(-1, grp) == grp) ? 8u : 0u;
+  f |= (dpp_i<kDppBcast15, 0xa>(-1, grp) == grp) ? 16u : 0u;
+  f |= (dpp_i<kDppBcast31, 0xc>(-1, grp) == grp) ? 32u : 0u;
+  return f;
+}
+
+template <bool MAX, class V>
+__device__ __forceinline__ V seg_scan(V v, unsigned f) {
+  const V id = MAX ? (V)-INFINITY : (V)0;
+  auto op = [](V a, V b) { return MAX ? (a > b ? a : b) : a + b; };
+  V u;
+  u = dpp<kDppRowShr + 1, 0xf>(id, v);
+  if (f & 1u) v = op(v, u);
+  u = dpp<kDppRowShr + 2, 0xf>(id, v);
+  if (f & 2u) v = op(v, u);
+  u = dpp<kDppRowShr + 4, 0xf>(id, v);
+  if (f & 4u) v = op(v, u);
+  u = dpp<kDppRowShr + 8, 0xf>(id, v);
+  if (f & 8u) v = op(v, u);
+  u = dpp<kDppBcast15, 0xa>(id, v);
+  if (f & 16u) v = op(v, u);
+  u = dpp<kDppBcast31, 0xc>(id, v);
+  if (f & 32u) v = op(v, u);
+  return v;
+}
+
+// sum over the S lanes of a head segment: DPP quad permutes for the first two
+// steps, LDS permutes beyond (S <= 16)
+__device__ __forceinline__ float head_sum(float v, int S) {
+  if (S >= 2) v += dpp_f<kDppQuadXor1, 0xf>(0.f, v);
+  if (S >= 4) v += dpp_f<kDppQuadXor2, 0xf>(0.f, v);
+  for (int o = 4; o < S; o <<= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// team_score_regs with the DPP head reduction (scaled_dot; other modes as in scores.hpp)
+__device__ __forceinline__ float seg_team_score(const ScoreArgs& sa, const float (&q)[4], const float (&k)[4], int S) {
+  if (sa.mode == GNPDE_SCORE_DOT) {
+    float a = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a = fmaf(q[i], k[i], a);
+    return head_sum(a, S) * rsqrtf((float)sa.dk);
+  }
+  return team_score_regs<4>(sa, q, k, S);
+}
+
+template <bool REF, int OUT>
+__global__ __launch_bounds__(256) void seg_softmax_kernel(const int4* __restrict__ items, int n_items,
+                                                           const int* __restrict__ rowptr,
+                                                           const int* __restrict__ rowidx,
+                                                           const int* __restrict__ gidx, int group_is_dst,
+                                                           ScoreArgs sa, Team tm, float* __restrict__ w,
+                                                           double* __restrict__ m, float* __restrict__ rl,
+                                                           double* __restrict__ partials) {
+  using S_t = typename std::conditional<REF, double, float>::type;
+  const int lane = threadIdx.x & 63;
+  const int item = uniform(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
+  if (item >= n_items) return;
+  const int4 it = items[item];
+  const int e0 = uniform(it.x), e1 = uniform(it.y), slot = uniform(it.z);
+  const int n = e1 - e0;
+  if (n <= 0) return;
+  const bool live = lane < n;
+  const int p = e0 + min(lane, n - 1);
+  const int grp = rowidx[p];
+  const int oth = gidx[p];
+  const int src = group_is_dst ? oth : grp;
+  const int dst = group_is_dst ? grp : oth;
+  const int seg_end = min(rowptr[grp + 1], e1) - 1 - e0;  // last lane of this lane's group inside the item
+  const unsigned same = seg_flags(grp) & (live ? 0x3fu : 0u);  // all lanes run the DPP steps
+
+  // team-layout scores (per-edge modes): lane (team, t) holds the score of edge
+  // r*ER + team for head t/S; the q and k slices of kSegBatch rounds are in flight together
+  const int T = REF ? 1 : tm.T, S = REF ? 1 : tm.S, ER = kWave / T;
+  const int team = lane / T, t = lane % T;
+  float sc[REF ? 1 : kSegRounds];
+  if constexpr (!REF) {
+#pragma unroll
+    for (int b = 0; b < kSegRounds; b += kSegBatch) {
+      if (b * ER < n) {
+        float qv[kSegBatch][4], kv[kSegBatch][4];
+#pragma unroll
+        for (int r = 0; r < kSegBatch; ++r) {
+          if ((b + r) * ER < n) {
+            const int sl = min((b + r) * ER + team, n - 1);
+            team_row<4>(sa, sa.q, __shfl(src, sl), t, qv[r]);
+            team_row<4>(sa, sa.k, __shfl(dst, sl), t, kv[r]);
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < kSegBatch; ++r)
+          if ((b + r) * ER < n) sc[b + r] = seg_team_score(sa, qv[r], kv[r], S);  // full-wave cross-lane ops
+      }
+    }
+  }
+  const int round_of_lane = lane / ER, team_src = (lane % ER) * T;
+
+  const int H = sa.H;
+  float wsum = 0.f;
+  for (int h = 0; h < H; ++h) {
+    S_t v;
+    if constexpr (REF) {
+      v = live ? sa.cs[(int64_t)src * H + h] : -INFINITY;
+    } else {
+      v = -INFINITY;
+#pragma unroll
+      for (int r = 0; r < kSegRounds; ++r) {
+        if (r * ER < n) {
+          const float x = __shfl(sc[r], team_src + h * S);
+          if (round_of_lane == r) v = x;
+        }
+      }
+      if (!live) v = -INFINITY;
+    }
+    if constexpr (OUT == kSegChunkWeights) {
+      const int64_t gi = (int64_t)grp * H + h;
+      wsum += live ? expf((float)((double)v - m[gi])) * rl[gi] : 0.f;
+    } else {
+      const S_t M = __shfl(seg_scan<true>(v, same), seg_end);
+      const float e = live ? expf((float)(v - M)) : 0.f;
+      const float Ls = __shfl(seg_scan<false>(e, same), seg_end);
+      if (slot >= 0) {  // chunk of a long group: one segment, partial statistics
+        if (lane == 0) {
+          partials[(int64_t)slot * 2 * H + h] = (double)M;
+          partials[(int64_t)slot * 2 * H + H + h] = (double)Ls;
+        }
+      } else if constexpr (OUT == kSegWeights) {
+        wsum += e / (Ls + kSoftmaxEps);
+      } else {
+        if (live && lane == seg_end) {
+          m[(int64_t)grp * H + h] = (double)M;
+          rl[(int64_t)grp * H + h] = 1.0f / (Ls + kSoftmaxEps);
+        }
+      }
+    }
+  }
+  if constexpr (OUT == kSegWeights || OUT == kSegChunkWeights) {
+    if (live && (OUT == kSegChunkWeights || slot < 0)) w[p] = wsum / (float)H;
+  }
+}
+
+template <bool REF, int OUT>
+static int launch_seg(const int4* items, int64_t n, const int* rowptr, const int* rowidx, const int* gidx, int gid,
+                      const ScoreArgs& sa, const Team& tm, float* w, double* m, float* rl, double* partials,
+                      hipStream_t s) {
+  if (n <= 0) return GNPDE_OK;
+  seg_softmax_kernel<REF, OUT><<<(unsigned)ceil_div(n, kWavesPerBlock), kBlock, 0, s>>>(
+      items, (int)n, rowptr, rowidx, gidx, gid, sa, tm, w, m, rl, partials);
+  GNPDE_LAUNCH_CHECK();
+  return GNPDE_OK;
+}
+
+}  // namespace gnpde
+
+using namespace gnpde;
+
+extern "C" {
+
+int gnpde_seg_block_edges(int mode, int64_t heads, int64_t dk) {
+  if (mode == GNPDE_SCORE_REFERENCE || mode == GNPDE_SCORE_UNIFORM) return kWave;
+  if (heads < 1 || dk < 4 || dk % 4 != 0) return 0;
+  const int64_t S = dk / 4, T = heads * S;
+  if ((S & (S - 1)) || (T & (T - 1)) || T > kWave) return 0;
+  return (int)std::min<int64_t>(kWave, kSegRounds * (kWave / T));
+}
+
+int gnpde_seg_plan_build(const int32_t* rowptr, int64_t R, int32_t eb, int32_t* items, int64_t items_capacity,
+                         int32_t* chunk_items, int64_t chunks_capacity, int32_t* heavy, int64_t heavy_capacity,
+                         int64_t* n_items, int64_t* n_chunks, int64_t* n_heavy) {
+  GNPDE_REQUIRE(rowptr && items && chunk_items && heavy && n_items && n_chunks && n_heavy, GNPDE_EINVAL,
+                "seg_plan_build: NULL pointer");
+  GNPDE_REQUIRE(R >= 0 && eb >= 1 && eb <= kWave, GNPDE_EINVAL, "seg_plan_build: bad R / eb");
+  int64_t ni = 0, nc = 0, nh = 0;
+  int64_t b0 = -1, b1 = -1, bg = -1;  // the open block [b0, b1), first group bg
+  auto close = [&]() -> bool {
+    if (b0 < 0) return true;
+    if (ni >= items_capacity) return false;
+    int32_t* o = items + 4 * ni++;
+    o[0] = (int32_t)b0; o[1] = (int32_t)b1; o[2] = -1; o[3] = (int32_t)bg;
+    b0 = -1;
+    return true;
+  };
+  for (int64_t r = 0; r < R; ++r) {
+    const int64_t s0 = rowptr[r], s1 = rowptr[r + 1], d = s1 - s0;
+    GNPDE_REQUIRE(d >= 0, GNPDE_EINVAL, "seg_plan_build: rowptr not monotone at %lld", (long long)r);
+    if (d == 0) continue;  // empty groups: no edges, nothing to compute
+    if (d > eb) {          // long group: eb-edge chunks with partial statistics
+      GNPDE_REQUIRE(close(), GNPDE_EINVAL, "seg_plan_build: items capacity");
+      const int64_t nch = (d + eb - 1) / eb;
+      GNPDE_REQUIRE(nc + nch <= chunks_capacity && nh < heavy_capacity, GNPDE_EINVAL, "seg_plan_build: chunk capacity");
+      int32_t* hv = heavy + 4 * nh++;
+      hv[0] = (int32_t)r; hv[1] = (int32_t)nc; hv[2] = (int32_t)nch; hv[3] = 0;
+      for (int64_t c = 0; c < nch; ++c) {
+        int32_t* o = chunk_items + 4 * nc;
+        o[0] = (int32_t)(s0 + c * eb); o[1] = (int32_t)std::min(s1, s0 + (c + 1) * eb); o[2] = (int32_t)nc;
+        o[3] = (int32_t)r;
+        ++nc;
+      }
+      continue;
+    }
+    if (b0 >= 0 && s1 - b0 <= eb) {  // non-empty groups are contiguous in edge order
+      b1 = s1;
+      continue;
+    }
+    GNPDE_REQUIRE(close(), GNPDE_EINVAL, "seg_plan_build: items capacity");
+    b0 = s0;
+    b1 = s1;
+    bg = r;
+  }
+  GNPDE_REQUIRE(close(), GNPDE_EINVAL, "seg_plan_build: items capacity");
+  *n_items = ni;
+  *n_chunks = nc;
+  *n_heavy = nh;
+  return GNPDE_OK;
+}
+
+int gnpde_seg_softmax_f32(const int32_t* items, int64_t n_items, const int32_t* chunk_items, int64_t n_chunk_items,
+                          const int32_t* heavy, int64_t n_heavy, const int32_t* rowptr, const int32_t* rowidx,
+                          const int32_t* gidx, int group_is_dst, int out_kind, int mode, int64_t heads, int64_t dk,
+                          const double* cs, const float* q, const float* k, int64_t ldqk, float score_p0,
+                          float score_p1, float* w, double* m, float* rl, double* partials, void* stream) {
+  int rc = check_score_args(mode, heads, dk, cs, q, k);
+  if (rc) return rc;
+  GNPDE_REQUIRE(out_kind == 0 || out_kind == 1, GNPDE_EINVAL, "seg_softmax: out_kind must be 0 (weights) or 1 (stats)");
+  GNPDE_REQUIRE(mode != GNPDE_SCORE_UNIFORM, GNPDE_EUNSUPPORTED, "seg_softmax: uniform scores need no softmax pass");
+  GNPDE_REQUIRE(!(mode == GNPDE_SCORE_REFERENCE && out_kind == 0), GNPDE_EUNSUPPORTED,
+                "seg_softmax: reference scores grouped by source are uniform");
+  GNPDE_REQUIRE(n_items >= 0 && n_chunk_items >= 0 && n_heavy >= 0 && n_items + n_chunk_items < INT32_MAX,
+                GNPDE_EINVAL, "seg_softmax: bad item counts");
+  GNPDE_REQUIRE(gnpde_seg_block_edges(mode, heads, dk) > 0, GNPDE_EUNSUPPORTED,
+                "seg_softmax: per-edge scores need dk %% 4 == 0 and power-of-two dk/4, heads*dk/4 <= 64");
+  if (n_items + n_chunk_items == 0) return GNPDE_OK;
+  GNPDE_REQUIRE(rowptr && rowidx && gidx, GNPDE_EINVAL, "seg_softmax: NULL graph arrays");
+  GNPDE_REQUIRE(n_items == 0 || items, GNPDE_EINVAL, "seg_softmax: NULL items");
+  GNPDE_REQUIRE(n_chunk_items == 0 || (chunk_items && heavy && n_heavy > 0 && partials && m && rl), GNPDE_EINVAL,
+                "seg_softmax: chunk items need heavy, partials and m/rl scratch");
+  if (out_kind == 0) GNPDE_REQUIRE(w != nullptr, GNPDE_EINVAL, "seg_softmax: NULL w");
+  if (out_kind == 1) GNPDE_REQUIRE(m && rl, GNPDE_EINVAL, "seg_softmax: NULL m/rl");
+  const ScoreArgs sa = make_score_args(mode, heads, dk, cs, q, k, ldqk, score_p0, score_p1);
+  Team tm{1, 1};
+  if (mode != GNPDE_SCORE_REFERENCE) {
+    tm = team_geometry(sa);
+    GNPDE_REQUIRE(tm.T > 0, GNPDE_EUNSUPPORTED, "seg_softmax: q/k must be 16-byte aligned with ldqk %% 4 == 0");
+  }
+  hipStream_t s = as_stream(stream);
+  const int4* it = reinterpret_cast<const int4*>(items);
+  const int4* ch = reinterpret_cast<const int4*>(chunk_items);
+  const int4* hv = reinterpret_cast<const int4*>(heavy);
+  const bool ref = mode == GNPDE_SCORE_REFERENCE;
+#define GNPDE_SEG(R, O, ITEMS, N) \
+  launch_seg<R, O>(ITEMS, N, rowptr, rowidx, gidx, group_is_dst, sa, tm, w, m, rl, partials, s)
+  if (out_kind == 0) {
+    rc = GNPDE_SEG(false, kSegWeights, it, n_items);
+    if (!rc) rc = GNPDE_SEG(false, kSegWeights, ch, n_chunk_items);
+  } else if (ref) {
+    rc = GNPDE_SEG(true, kSegStats, it, n_items);
+    if (!rc) rc = GNPDE_SEG(true, kSegStats, ch, n_chunk_items);
+  } else {
+    rc = GNPDE_SEG(false, kSegStats, it, n_items);
+    if (!rc) rc = GNPDE_SEG(false, kSegStats, ch, n_chunk_items);
+  }
+  if (rc || n_chunk_items == 0) return rc;
+  rc = launch_stats_fixup(hv, n_heavy, (int)heads, partials, m, rl, s);
+  if (rc || out_kind == 1) return rc;
+  return GNPDE_SEG(false, kSegChunkWeights, ch, n_chunk_items);
+#undef GNPDE_SEG
+}
+
+}  // extern "C"

@@ -2,9 +2,7 @@
 // attention RHS pieces (grouped softmax statistics, edge-parallel head-mean
 // weights, per-edge attention) and the reference-mode key-sum node scores.
 #include "aggregate.hpp"
-#include "scores.hpp"
-
-#include <cstdlib>
+#include "rhs_host.hpp"
 
 namespace gnpde {
 
@@ -20,24 +18,6 @@ int agg_variant() {
 // GL lanes per plan item (64/GL items per wavefront).  Every lane keeps an
 // online (max, sum-exp) per head over its strided edges; the GL partial states
 // are merged by a fixed xor tree (deterministic).
-__device__ __forceinline__ void online_push(double& M, float& L, double s) {
-  if (s > M) {
-    L = (M == -INFINITY ? 0.f : L * expf((float)(M - s))) + 1.f;
-    M = s;
-  } else {
-    L += expf((float)(s - M));
-  }
-}
-
-__device__ __forceinline__ void online_merge(double& M, float& L, double M2, float L2) {
-  const double Mn = fmax(M, M2);
-  if (Mn == -INFINITY) return;
-  const float a = (M == -INFINITY) ? 0.f : L * expf((float)(M - Mn));
-  const float b = (M2 == -INFINITY) ? 0.f : L2 * expf((float)(M2 - Mn));
-  L = a + b;
-  M = Mn;
-}
-
 template <int MAXH, int GL>
 __global__ __launch_bounds__(256) void stats_kernel(const int4* __restrict__ items, int n_items,
                                                      const int* __restrict__ gidx, int group_is_dst, ScoreArgs sa,
@@ -114,6 +94,15 @@ __global__ __launch_bounds__(256) void stats_fixup_kernel(const int4* __restrict
   }
 }
 
+int launch_stats_fixup(const int4* heavy, int64_t n_heavy, int H, const double* partials, double* m, float* rl,
+                       hipStream_t s) {
+  if (n_heavy <= 0) return GNPDE_OK;
+  const unsigned g2 = (unsigned)ceil_div(n_heavy * H, kWavesPerBlock);
+  stats_fixup_kernel<<<g2, kBlock, 0, s>>>(heavy, (int)n_heavy, H, partials, m, rl);
+  GNPDE_LAUNCH_CHECK();
+  return GNPDE_OK;
+}
+
 // ------------------------------------------------------------------ edge-parallel weights
 // w[p] = (sum_h exp(s_p,h - m[g,h]) * rl[g,h]) / H   (softmax, then mean over heads)
 __global__ __launch_bounds__(256) void attn_weights_kernel(const int* __restrict__ rowidx, const int* __restrict__ col,
@@ -153,13 +142,6 @@ __global__ __launch_bounds__(256) void edge_attention_kernel(const int* __restri
 }
 
 // ------------------------------------------------------------------ team-mode kernels (per-edge q/k scores)
-// T lanes per edge / group (T = H * S, S = dk/VEC lanes per head), 64/T teams per
-// wavefront; lane t holds VEC consecutive elements of the att-wide q/k rows and
-// ends with its own head's score.  Head leaders (t % S == 0) own the per-head state.
-struct Team {
-  int T, S;
-};
-
 // Team-mode softmax statistics: one team of T lanes per work item.  The
 // item's own row (q of the source group, or k of the destination group) is
 // loaded once; the other endpoints' indices come in T at a time (one per
@@ -169,12 +151,6 @@ struct Team {
 // shuffle runs with the whole wavefront active; a team past its own edges
 // computes throw-away scores and pushes nothing.
 constexpr int kTeamEdges = 4;
-
-__device__ __forceinline__ int wave_max_int(int v) {
-#pragma unroll
-  for (int o = 1; o < kWave; o <<= 1) v = max(v, __shfl_xor(v, o));
-  return v;
-}
 
 template <int VEC>
 __global__ __launch_bounds__(256) void stats_team_kernel(const int4* __restrict__ items, int n_items,
@@ -544,74 +520,6 @@ __global__ __launch_bounds__(256) void node_scores_kernel(const float* __restric
 }
 
 // ------------------------------------------------------------------ host helpers
-static int check_score_args(int mode, int64_t heads, int64_t dk, const double* cs, const float* q, const float* k) {
-  GNPDE_REQUIRE(heads >= 1 && heads <= 16, GNPDE_EUNSUPPORTED, "attention: heads=%lld not in [1,16]",
-                (long long)heads);
-  GNPDE_REQUIRE(mode >= GNPDE_SCORE_REFERENCE && mode <= GNPDE_SCORE_UNIFORM, GNPDE_EINVAL,
-                "attention: unknown score mode %d", mode);
-  if (mode == GNPDE_SCORE_REFERENCE) {
-    GNPDE_REQUIRE(cs != nullptr, GNPDE_EINVAL, "attention: reference mode needs cs");
-  } else if (mode != GNPDE_SCORE_UNIFORM) {
-    GNPDE_REQUIRE(q != nullptr && k != nullptr && dk >= 1, GNPDE_EINVAL, "attention: per-edge mode needs q, k, dk");
-  }
-  return GNPDE_OK;
-}
-
-static ScoreArgs make_score_args(int mode, int64_t heads, int64_t dk, const double* cs, const float* q,
-                                 const float* k, int64_t ldqk, float p0, float p1) {
-  ScoreArgs sa;
-  sa.mode = mode;
-  sa.H = (int)heads;
-  sa.dk = (int)dk;
-  sa.cs = cs;
-  sa.q = q;
-  sa.k = k;
-  sa.ldqk = ldqk;
-  sa.p0 = p0;
-  sa.p1 = p1;
-  return sa;
-}
-
-static Epi make_epi(const float* x, int64_t ldx, const float* x0, int64_t ldx0, const float* alpha, const float* beta,
-                    int flags, float* f, int64_t ldf, const gnpde_stage_epilogue_t* stage = nullptr) {
-  Epi e;
-  e.has_stage = stage != nullptr;
-  if (stage) e.st = *stage;
-  e.x = x;
-  e.ldx = ldx;
-  e.x0 = x0;
-  e.ldx0 = ldx0;
-  e.alpha = alpha;
-  e.beta = beta;
-  e.flags = flags;
-  e.f = f;
-  e.ldf = ldf;
-  return e;
-}
-
-static int check_epi(const Epi& e, int64_t C, int64_t n_heavy, const void* partials) {
-  GNPDE_REQUIRE(C >= 1, GNPDE_EINVAL, "rhs: C must be >= 1");
-  GNPDE_REQUIRE(e.x && (e.f || e.has_stage), GNPDE_EINVAL, "rhs: NULL x or f");
-  if (e.has_stage) {
-    GNPDE_REQUIRE(e.st.n_out >= 0 && e.st.n_out <= GNPDE_STAGE_MAX_OUT, GNPDE_EINVAL, "rhs: stage n_out out of range");
-    GNPDE_REQUIRE(e.st.f_out || e.st.n_out > 0, GNPDE_EINVAL, "rhs: stage epilogue stores nothing");
-    for (int i = 0; i < e.st.n_out; ++i) {
-      GNPDE_REQUIRE(e.st.o[i].out && e.st.o[i].nk >= 0 && e.st.o[i].nk <= GNPDE_STAGE_MAX_K, GNPDE_EINVAL,
-                    "rhs: bad stage output %d", i);
-      for (int j = 0; j < e.st.o[i].nk; ++j)
-        GNPDE_REQUIRE(e.st.o[i].k[j] != nullptr, GNPDE_EINVAL, "rhs: stage output %d k[%d] is NULL", i, j);
-    }
-  }
-  GNPDE_REQUIRE(e.ldx >= C && e.ldf >= C, GNPDE_EINVAL, "rhs: leading dimension < C");
-  if (e.flags & GNPDE_EPI_RHS) GNPDE_REQUIRE(e.alpha != nullptr, GNPDE_EINVAL, "rhs: NULL alpha");
-  if (e.flags & GNPDE_ADD_SOURCE) {
-    GNPDE_REQUIRE(e.flags & GNPDE_EPI_RHS, GNPDE_EINVAL, "rhs: ADD_SOURCE needs EPI_RHS");
-    GNPDE_REQUIRE(e.x0 && e.beta && e.ldx0 >= C, GNPDE_EINVAL, "rhs: ADD_SOURCE needs x0, beta, ldx0 >= C");
-  }
-  GNPDE_REQUIRE(n_heavy == 0 || partials != nullptr, GNPDE_EINVAL, "rhs: hub rows need a partials buffer");
-  return GNPDE_OK;
-}
-
 static int pow2_at_least(int v, int cap) {
   int p = 1;
   while (p < v && p < cap) p <<= 1;
@@ -703,30 +611,6 @@ static void launch_node_scores_any(hipStream_t s, const NsGeom& ge, const float*
 #undef GNPDE_NS
 }
 
-// team geometry for the per-edge modes: VEC = 4, S = dk/4, T = H*S, both powers
-// of two, T <= 64; otherwise lane mode (T = 0).
-static bool team_mode_enabled() {  // GNPDE_TEAM=0 forces lane mode (diagnostics)
-  static const bool on = [] {
-    const char* e = std::getenv("GNPDE_TEAM");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
-static Team team_geometry(const ScoreArgs& sa) {
-  Team tm{0, 0};
-  if (!team_mode_enabled()) return tm;
-  if (sa.mode != GNPDE_SCORE_DOT && sa.mode != GNPDE_SCORE_EXP_KERNEL && sa.mode != GNPDE_SCORE_COSINE &&
-      sa.mode != GNPDE_SCORE_PEARSON)
-    return tm;
-  if (sa.dk % 4 != 0 || sa.ldqk % 4 != 0 || !aligned16(sa.q) || !aligned16(sa.k)) return tm;
-  const int S = sa.dk / 4, T = sa.H * S;
-  if ((S & (S - 1)) || (T & (T - 1)) || T > kWave) return tm;
-  tm.T = T;
-  tm.S = S;
-  return tm;
-}
-
 static unsigned edge_grid(int64_t nnz) {
   return (unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(nnz, kBlock), 16384));
 }
@@ -789,13 +673,7 @@ int gnpde_softmax_stats_f32(const int32_t* items, int64_t n_items, const int32_t
     launch_stats<16>(grid, GL, s, it, (int)n_items, gidx, group_is_dst, sa, m, rl, partials);
   GNPDE_LAUNCH_CHECK();
   }
-  if (n_heavy > 0) {
-    const unsigned g2 = (unsigned)ceil_div(n_heavy * heads, kWavesPerBlock);
-    stats_fixup_kernel<<<g2, kBlock, 0, s>>>(reinterpret_cast<const int4*>(heavy), (int)n_heavy, (int)heads, partials,
-                                             m, rl);
-    GNPDE_LAUNCH_CHECK();
-  }
-  return GNPDE_OK;
+  return launch_stats_fixup(reinterpret_cast<const int4*>(heavy), n_heavy, (int)heads, partials, m, rl, s);
 }
 
 int gnpde_attn_weights_f32(const int32_t* rowidx, const int32_t* col, int64_t nnz, int norm_idx, int mode,

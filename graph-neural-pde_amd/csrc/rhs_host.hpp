@@ -1,0 +1,103 @@
+// rhs_host.hpp — host-side argument checks and packing shared by the RHS
+// translation units (rhs.hip: K1 and the unfused attention pieces;
+// attention.hip: the fused attention RHS).
+#pragma once
+#include <cstdlib>
+
+#include "scores.hpp"
+
+namespace gnpde {
+
+inline int check_score_args(int mode, int64_t heads, int64_t dk, const double* cs, const float* q, const float* k) {
+  GNPDE_REQUIRE(heads >= 1 && heads <= 16, GNPDE_EUNSUPPORTED, "attention: heads=%lld not in [1,16]",
+                (long long)heads);
+  GNPDE_REQUIRE(mode >= GNPDE_SCORE_REFERENCE && mode <= GNPDE_SCORE_UNIFORM, GNPDE_EINVAL,
+                "attention: unknown score mode %d", mode);
+  if (mode == GNPDE_SCORE_REFERENCE) {
+    GNPDE_REQUIRE(cs != nullptr, GNPDE_EINVAL, "attention: reference mode needs cs");
+  } else if (mode != GNPDE_SCORE_UNIFORM) {
+    GNPDE_REQUIRE(q != nullptr && k != nullptr && dk >= 1, GNPDE_EINVAL, "attention: per-edge mode needs q, k, dk");
+  }
+  return GNPDE_OK;
+}
+
+inline ScoreArgs make_score_args(int mode, int64_t heads, int64_t dk, const double* cs, const float* q,
+                                 const float* k, int64_t ldqk, float p0, float p1) {
+  ScoreArgs sa;
+  sa.mode = mode;
+  sa.H = (int)heads;
+  sa.dk = (int)dk;
+  sa.cs = cs;
+  sa.q = q;
+  sa.k = k;
+  sa.ldqk = ldqk;
+  sa.p0 = p0;
+  sa.p1 = p1;
+  return sa;
+}
+
+inline Epi make_epi(const float* x, int64_t ldx, const float* x0, int64_t ldx0, const float* alpha, const float* beta,
+                    int flags, float* f, int64_t ldf, const gnpde_stage_epilogue_t* stage = nullptr) {
+  Epi e;
+  e.has_stage = stage != nullptr;
+  if (stage) e.st = *stage;
+  e.x = x;
+  e.ldx = ldx;
+  e.x0 = x0;
+  e.ldx0 = ldx0;
+  e.alpha = alpha;
+  e.beta = beta;
+  e.flags = flags;
+  e.f = f;
+  e.ldf = ldf;
+  return e;
+}
+
+inline int check_epi(const Epi& e, int64_t C, int64_t n_heavy, const void* partials) {
+  GNPDE_REQUIRE(C >= 1, GNPDE_EINVAL, "rhs: C must be >= 1");
+  GNPDE_REQUIRE(e.x && (e.f || e.has_stage), GNPDE_EINVAL, "rhs: NULL x or f");
+  if (e.has_stage) {
+    GNPDE_REQUIRE(e.st.n_out >= 0 && e.st.n_out <= GNPDE_STAGE_MAX_OUT, GNPDE_EINVAL, "rhs: stage n_out out of range");
+    GNPDE_REQUIRE(e.st.f_out || e.st.n_out > 0, GNPDE_EINVAL, "rhs: stage epilogue stores nothing");
+    for (int i = 0; i < e.st.n_out; ++i) {
+      GNPDE_REQUIRE(e.st.o[i].out && e.st.o[i].nk >= 0 && e.st.o[i].nk <= GNPDE_STAGE_MAX_K, GNPDE_EINVAL,
+                    "rhs: bad stage output %d", i);
+      for (int j = 0; j < e.st.o[i].nk; ++j)
+        GNPDE_REQUIRE(e.st.o[i].k[j] != nullptr, GNPDE_EINVAL, "rhs: stage output %d k[%d] is NULL", i, j);
+    }
+  }
+  GNPDE_REQUIRE(e.ldx >= C && e.ldf >= C, GNPDE_EINVAL, "rhs: leading dimension < C");
+  if (e.flags & GNPDE_EPI_RHS) GNPDE_REQUIRE(e.alpha != nullptr, GNPDE_EINVAL, "rhs: NULL alpha");
+  if (e.flags & GNPDE_ADD_SOURCE) {
+    GNPDE_REQUIRE(e.flags & GNPDE_EPI_RHS, GNPDE_EINVAL, "rhs: ADD_SOURCE needs EPI_RHS");
+    GNPDE_REQUIRE(e.x0 && e.beta && e.ldx0 >= C, GNPDE_EINVAL, "rhs: ADD_SOURCE needs x0, beta, ldx0 >= C");
+  }
+  GNPDE_REQUIRE(n_heavy == 0 || partials != nullptr, GNPDE_EINVAL, "rhs: hub rows need a partials buffer");
+  return GNPDE_OK;
+}
+
+// team geometry for the per-edge modes: VEC = 4, S = dk/4, T = H*S, both powers
+// of two, T <= 64; otherwise lane mode (T = 0).
+inline bool team_mode_enabled() {  // GNPDE_TEAM=0 forces lane mode (diagnostics)
+  static const bool on = [] {
+    const char* e = std::getenv("GNPDE_TEAM");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+inline Team team_geometry(const ScoreArgs& sa) {
+  Team tm{0, 0};
+  if (!team_mode_enabled()) return tm;
+  if (sa.mode != GNPDE_SCORE_DOT && sa.mode != GNPDE_SCORE_EXP_KERNEL && sa.mode != GNPDE_SCORE_COSINE &&
+      sa.mode != GNPDE_SCORE_PEARSON)
+    return tm;
+  if (sa.dk % 4 != 0 || sa.ldqk % 4 != 0 || !aligned16(sa.q) || !aligned16(sa.k)) return tm;
+  const int S = sa.dk / 4, T = sa.H * S;
+  if ((S & (S - 1)) || (T & (T - 1)) || T > kWave) return tm;
+  tm.T = T;
+  tm.S = S;
+  return tm;
+}
+
+}  // namespace gnpde

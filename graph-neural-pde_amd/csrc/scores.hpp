@@ -47,6 +47,66 @@ __device__ __forceinline__ float pair_score(int mode, const float* __restrict__ 
   }
 }
 
+// ------------------------------------------------------------------ online softmax state
+// (max, sum-exp) pushed one score at a time and merged pairwise in a fixed
+// order (deterministic).  fp64 max for the reference mode's fp64 node scores;
+// the float twin serves the fp32 per-edge scores of the fused kernel.
+__device__ __forceinline__ void online_push(double& M, float& L, double s) {
+  if (s > M) {
+    L = (M == -INFINITY ? 0.f : L * expf((float)(M - s))) + 1.f;
+    M = s;
+  } else {
+    L += expf((float)(s - M));
+  }
+}
+
+__device__ __forceinline__ void online_merge(double& M, float& L, double M2, float L2) {
+  const double Mn = fmax(M, M2);
+  if (Mn == -INFINITY) return;
+  const float a = (M == -INFINITY) ? 0.f : L * expf((float)(M - Mn));
+  const float b = (M2 == -INFINITY) ? 0.f : L2 * expf((float)(M2 - Mn));
+  L = a + b;
+  M = Mn;
+}
+
+__device__ __forceinline__ void online_push(float& M, float& L, float s) {
+  if (s > M) {
+    L = (M == -INFINITY ? 0.f : L * expf(M - s)) + 1.f;
+    M = s;
+  } else {
+    L += expf(s - M);
+  }
+}
+
+__device__ __forceinline__ void online_merge(float& M, float& L, float M2, float L2) {
+  const float Mn = fmaxf(M, M2);
+  if (Mn == -INFINITY) return;
+  const float a = (M == -INFINITY) ? 0.f : L * expf(M - Mn);
+  const float b = (M2 == -INFINITY) ? 0.f : L2 * expf(M2 - Mn);
+  L = a + b;
+  M = Mn;
+}
+
+// ------------------------------------------------------------------ team layout (per-edge q/k scores)
+// T lanes per edge / group (T = H * S, S = dk/VEC lanes per head), 64/T teams per
+// wavefront; lane t holds VEC consecutive elements of the att-wide q/k rows and
+// ends with its own head's score.  Head leaders (t % S == 0) own the per-head state.
+struct Team {
+  int T, S;
+};
+
+__device__ __forceinline__ int wave_max_int(int v) {
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) v = max(v, __shfl_xor(v, o));
+  return v;
+}
+
+// Hub groups of the statistics kernels: merge the per-chunk (max, sum-exp)
+// partials [slot][2H] (max as fp64, then sum) into m[g,h], rl[g,h] = 1/(sum + 1e-16).
+// heavy: int4 {group, first_slot, n_chunks, 0}.  Defined in rhs.hip.
+int launch_stats_fixup(const int4* heavy, int64_t n_heavy, int H, const double* partials, double* m, float* rl,
+                       hipStream_t s);
+
 struct ScoreArgs {
   int mode;
   int H;

@@ -60,12 +60,21 @@ SIGNATURES = {
                                       _vp, _vp, _vp]),
     "gnpde_edge_attention_f32": (_int, [_vp, _vp, _vp, _i64, _int, _int, _i64, _i64, _vp, _vp, _vp, _i64, _f32, _f32,
                                         _vp, _vp, _vp, _vp]),
+    "gnpde_seg_block_edges": (_int, [_int, _i64, _i64]),
+    "gnpde_seg_plan_build": (_int, [_vp, _i64, ctypes.c_int32, _vp, _i64, _vp, _i64, _vp, _i64, c_i64p, c_i64p,
+                                    c_i64p]),
+    "gnpde_seg_softmax_f32": (_int, [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _int, _int, _int, _i64, _i64,
+                                     _vp, _vp, _vp, _i64, _f32, _f32, _vp, _vp, _vp, _vp, _vp]),
     "gnpde_csr_rowidx": (_int, [_vp, _i64, _i64, _vp, _vp]),
     "gnpde_rk_combine_f32": (_int, [_i64, _vp, _int, ctypes.POINTER(_vp), ctypes.POINTER(_f64), _f64, _vp, _vp]),
 }
 
 # constants mirrored from include/gnpde.h
 ABI_VERSION = 1
+OK = 0
+EINVAL = -1
+EHIP = -2
+EUNSUPPORTED = -3
 EPI_PLAIN = 0
 EPI_RHS = 1
 ALPHA_SIGMOID = 2
@@ -111,10 +120,18 @@ def load():
 
 def call(name, *args):
     """Invoke an entry point; raise GnpdeError with gnpde_last_error() on failure."""
-    lib = load()
-    rc = getattr(lib, name)(*args)
+    return check(call_rc(name, *args), name)
+
+
+def call_rc(name, *args):
+    """Invoke an entry point and return its status code (for callers that
+    handle GNPDE_EUNSUPPORTED by choosing another device path)."""
+    return getattr(load(), name)(*args)
+
+
+def check(rc, name):
     if rc != 0:
-        msg = lib.gnpde_last_error().decode(errors="replace")
+        msg = load().gnpde_last_error().decode(errors="replace")
         raise GnpdeError("%s failed (rc=%d): %s" % (name, rc, msg))
     return rc
 

@@ -12,12 +12,16 @@ head-mean attention into [B,N,N] for a dense matmul.  Here one RHS is:
    per-edge modes (``score_mode='per_edge'`` scaled_dot = upstream GRAND, and
    exp_kernel / cosine_sim / pearson, :246-259) project Q|K with the MFMA
    kernel (gnpde_linear_f32);
-2. grouped softmax statistics (max, 1/sum-exp) per source (norm_idx 0) or
-   destination (norm_idx 1) node (gnpde_softmax_stats_f32);
-3. edge-parallel head-mean weights (gnpde_attn_weights_f32), then the K1
-   gather-aggregate with the RHS epilogue fused (gnpde_spmm_rhs_f32).  With
-   the fork scaled_dot and norm_idx 0 every score of a source group is equal,
-   so the weights are 1/outdeg for any x: computed once per graph.
+2. norm_idx 1: destination-grouped softmax statistics (max, 1/sum-exp)
+   over the CSC (K2, gnpde_seg_softmax_f32);
+3. head-mean softmax weights in aggregation-CSR order: for norm_idx 0 the
+   edge-block segmented-softmax kernel K2 computes them straight from the
+   scores (SDDMM + segmented max/sum-exp + head mean in one pass, no [E,h]
+   tensor); for norm_idx 1 an edge-parallel pass over the statistics of
+   step 2 (gnpde_attn_weights_f32); then the K1 gather-aggregate with the RHS /
+   Runge-Kutta epilogue fused (gnpde_spmm_rhs_f32).  With the fork scaled_dot
+   and norm_idx 0 every score of a source group is equal, so the weights are
+   1/outdeg for any x: computed once per graph.
 
 V and Wout are dead when ``mix_features=False`` (:33-41) and are never
 computed; the parameters exist for state_dict compatibility.  Settings the
@@ -206,7 +210,10 @@ class ODEFuncTransformerAtt(ODEFunc):
                   stage=stage)
         if lay.is_uniform(norm_idx):
             return ops.spmm_rhs(g, lay.uniform_weights(g), x, **kw)
-        ns, m, rl = lay.scores_and_stats(g, x, norm_idx)
+        ns = lay.node_scores(g, x)
+        # destination-grouped softmax needs its statistics over the CSC first;
+        # source-grouped weights come straight from the scores (K2)
+        m, rl = ops.softmax_stats(g, ns, 1) if norm_idx == 1 else (None, None)
         return ops.attn_rhs(g, ns, m, rl, norm_idx, x, **kw)
 
     def __repr__(self):

@@ -11,6 +11,7 @@ Layout: node features [B,N,C] fp32 row-major, viewed as
 """
 import ctypes
 
+import numpy as np
 import torch
 
 from . import _lib
@@ -63,6 +64,7 @@ class GroupedCSR(object):
         self.R, self.nnz, self.key_row, self.plan = R, nnz, key_row, plan
         self._rowidx = None
         self._stats_plan = None
+        self._seg_plans = {}
 
     @property
     def rowidx(self):
@@ -72,6 +74,13 @@ class GroupedCSR(object):
             _lib.call("gnpde_csr_rowidx", _ptr(self.rowptr), self.R, self.nnz, _ptr(ri), _stream(ri.device))
             self._rowidx = ri
         return self._rowidx
+
+    def seg_plan(self, eb):
+        """Edge-block plan of the segmented-softmax kernel (K2) for blocks of at
+        most ``eb`` edges (SegPlan), built once per grouped CSR and block size."""
+        if eb not in self._seg_plans:
+            self._seg_plans[eb] = build_seg_plan(self.rowptr, eb)
+        return self._seg_plans[eb]
 
     @property
     def stats_plan(self):
@@ -103,6 +112,42 @@ def build_plan(rowptr, R, nnz, chunk=DEFAULT_CHUNK):
     _lib.call("gnpde_plan_build", _ptr(rowptr), R, chunk, _ptr(items), cap_items, _ptr(heavy), cap_heavy,
               ctypes.byref(n_it), ctypes.byref(n_hv), ctypes.byref(n_sl), _ptr(ws), ws_bytes, _stream(dev))
     return Plan(items, heavy, n_it.value, n_hv.value, n_sl.value, chunk)
+
+
+class SegPlan(object):
+    """Work items of gnpde_seg_softmax_f32 (include/gnpde.h): ``items`` int4
+    {e_begin, e_end, -1, first_group} — consecutive whole groups packed greedily
+    up to ``eb`` edges — and ``chunk_items`` {e_begin, e_end, slot, group}
+    covering groups of more than eb edges in eb-edge chunks, ``heavy`` {group,
+    first_slot, n_chunks, 0} per long group."""
+
+    def __init__(self, eb, items, n_items, chunk_items, n_chunk, heavy, n_heavy):
+        self.eb = eb
+        self.items, self.n_items = items, n_items
+        self.chunk_items, self.n_chunk = chunk_items, n_chunk
+        self.heavy, self.n_heavy = heavy, n_heavy
+        self.n_slots = n_chunk
+
+
+def build_seg_plan(rowptr, eb):
+    """gnpde_seg_plan_build on a host copy of rowptr (once per graph and block size)."""
+    rp = np.ascontiguousarray(rowptr.cpu().numpy().astype(np.int32))
+    R = rp.shape[0] - 1
+    nnz = int(rp[-1])
+    cap_i, cap_c, cap_h = max(R, 1), nnz // eb + R + 1, nnz // eb + 2
+    items = np.zeros((cap_i, 4), np.int32)
+    chunks = np.zeros((cap_c, 4), np.int32)
+    heavy = np.zeros((cap_h, 4), np.int32)
+    ni, nc, nh = ctypes.c_int64(0), ctypes.c_int64(0), ctypes.c_int64(0)
+    _lib.call("gnpde_seg_plan_build", rp.ctypes.data, R, eb, items.ctypes.data, cap_i, chunks.ctypes.data, cap_c,
+              heavy.ctypes.data, cap_h, ctypes.byref(ni), ctypes.byref(nc), ctypes.byref(nh))
+    dev = rowptr.device
+
+    def dev32(a, n):
+        return torch.from_numpy(np.ascontiguousarray(a[:max(n, 1)]).reshape(-1)).to(dev)
+
+    return SegPlan(eb, dev32(items, ni.value), ni.value, dev32(chunks, nc.value), nc.value, dev32(heavy, nh.value),
+                   nh.value)
 
 
 def build_grouped(edge_index, num_nodes, key_row, chunk=DEFAULT_CHUNK):
@@ -391,9 +436,45 @@ def uniform_scores(heads):
     return NodeScores(_lib.SCORE_UNIFORM, heads, 1)
 
 
-def softmax_stats(g, ns, norm_idx):
+def _seg_call(g, ns, norm_idx, out_kind):
+    """K2 (gnpde_seg_softmax_f32) over the grouped CSR of the softmax groups:
+    out_kind 0 -> head-mean weights in aggregation-CSR order (norm_idx 0 only);
+    1 -> (m, rl).  NotImplemented when the shape is outside the kernel."""
+    if ns.mode == _lib.SCORE_UNIFORM or (ns.mode == _lib.SCORE_REFERENCE and out_kind == 0):
+        return NotImplemented
+    eb = _lib.fn("gnpde_seg_block_edges")(ns.mode, ns.heads, ns.dk)
+    if eb <= 0:
+        return NotImplemented
+    if ns.q is not None and (ns.ldqk % 4 or ns.q.data_ptr() % 16 or ns.k.data_ptr() % 16):
+        return NotImplemented
+    grouped = g.csr if norm_idx == 0 else g.csc
+    plan = grouped.seg_plan(eb)
+    dev = grouped.col.device
+    H = ns.heads
+    need_stats = out_kind == 1 or plan.n_chunk > 0
+    m = torch.empty(g.R, H, dtype=torch.float64, device=dev) if need_stats else None
+    rl = torch.empty(g.R, H, dtype=torch.float32, device=dev) if need_stats else None
+    partials = torch.empty(plan.n_slots * 2 * H, dtype=torch.float64, device=dev) if plan.n_slots else None
+    w = torch.empty(max(g.nnz, 1), dtype=torch.float32, device=dev) if out_kind == 0 else None
+    rc = _lib.call_rc("gnpde_seg_softmax_f32", _ptr(plan.items), plan.n_items, _ptr(plan.chunk_items), plan.n_chunk,
+                      _ptr(plan.heavy), plan.n_heavy, _ptr(grouped.rowptr), _ptr(grouped.rowidx), _ptr(grouped.col),
+                      int(norm_idx == 1), out_kind, ns.mode, H, ns.dk, _ptr(ns.cs), _ptr(ns.q), _ptr(ns.k), ns.ldqk,
+                      ns.p0, ns.p1, _ptr(w), _ptr(m), _ptr(rl), _ptr(partials), _stream(dev))
+    if rc == _lib.EUNSUPPORTED:
+        return NotImplemented
+    _lib.check(rc, "gnpde_seg_softmax_f32")
+    return w if out_kind == 0 else (m, rl)
+
+
+def softmax_stats(g, ns, norm_idx, seg=True):
     """m [R,h] fp64, rl [R,h]: per-group max and 1/(sum-exp + 1e-16)
-    (utils.softmax, src/utils.py:116-127)."""
+    (utils.softmax, src/utils.py:116-127).  seg=True: the edge-block kernel K2;
+    shapes outside it (and seg=False) use the per-group kernels
+    (gnpde_softmax_stats_f32)."""
+    if seg:
+        r = _seg_call(g, ns, norm_idx, 1)
+        if r is not NotImplemented:
+            return r
     grouped = g.csr if norm_idx == 0 else g.csc
     plan = grouped.stats_plan
     dev = grouped.col.device
@@ -407,8 +488,17 @@ def softmax_stats(g, ns, norm_idx):
     return m, rl
 
 
-def attn_weights(g, ns, m, rl, norm_idx):
-    """Head-mean softmax weights in aggregation-CSR order [nnz]."""
+def attn_weights(g, ns, m, rl, norm_idx, seg=True):
+    """Head-mean softmax weights in aggregation-CSR order [nnz].  norm_idx 0:
+    K2 computes them straight from the scores (m, rl unused, may be None);
+    norm_idx 1 (and shapes outside K2): edge-parallel from the group
+    statistics (gnpde_attn_weights_f32)."""
+    if seg and norm_idx == 0:
+        w = _seg_call(g, ns, 0, 0)
+        if w is not NotImplemented:
+            return w
+    if m is None:
+        m, rl = softmax_stats(g, ns, norm_idx, seg=seg)
     dev = g.csr.col.device
     w = torch.empty(max(g.nnz, 1), dtype=torch.float32, device=dev)
     _lib.call("gnpde_attn_weights_f32", _ptr(g.csr.rowidx), _ptr(g.csr.col), g.nnz, int(norm_idx), ns.mode, ns.heads,
@@ -418,10 +508,10 @@ def attn_weights(g, ns, m, rl, norm_idx):
 
 
 def attn_rhs(g, ns, m, rl, norm_idx, x, x0=None, alpha=None, beta=None, rhs=True, alpha_sigmoid=True,
-             add_source=False, out=None, stage=None):
-    """K3: f = a*(A_att x - x) [+ b x0], A_att = head-mean softmax weights
-    (edge-parallel weights, then the K1 gather-aggregate with the fused epilogue)."""
-    w = attn_weights(g, ns, m, rl, norm_idx)
+             add_source=False, out=None, stage=None, seg=True):
+    """K2 + K1: f = a*(A_att x - x) [+ b x0], A_att = head-mean softmax weights
+    (m, rl: destination statistics for norm_idx 1, or None to compute them)."""
+    w = attn_weights(g, ns, m, rl, norm_idx, seg=seg)
     return spmm_rhs(g, w, x, x0=x0, alpha=alpha, beta=beta, rhs=rhs, alpha_sigmoid=alpha_sigmoid,
                     add_source=add_source, out=out, stage=stage)
 

@@ -194,6 +194,37 @@ int gnpde_attn_weights_f32(const int32_t* rowidx, const int32_t* col, int64_t nn
                            float score_p0, float score_p1, const double* m, const float* rl, float* w_out,
                            void* stream);
 
+/* K2: edge-block segmented softmax over a grouped CSR (the aggregation CSR
+ * for norm_idx 0, the CSC for norm_idx 1; gidx = the other endpoint, rowidx =
+ * the group of every position, group_is_dst as in gnpde_softmax_stats_f32).
+ * One wavefront per item = at most EB consecutive edges (EB =
+ * gnpde_seg_block_edges(mode, heads, dk); 0 means unsupported): items are
+ * int4 {e_begin, e_end, -1, first_group} covering consecutive whole groups
+ * (packed greedily up to EB edges); chunk_items {e_begin, e_end, slot, group}
+ * split groups of degree > EB, heavy {group, first_slot, n_chunks, 0} lists
+ * those groups (partials: 2*heads doubles per slot; m/rl scratch).
+ * gnpde_seg_plan_build builds them from a HOST copy of rowptr into HOST
+ * arrays (plain C++, once per graph; capacities: items >= R, chunk_items >=
+ * nnz/eb + R, heavy >= nnz/eb + 1).
+ *   out_kind 0: w[p] = (1/H) sum_h softmax_p,h in grouped order (per-edge
+ *               modes with norm_idx 0: the aggregation weights of K1);
+ *   out_kind 1: m[g,h] = max (fp64), rl[g,h] = 1/(sum exp(s - m) + 1e-16).
+ * Per-group max and sum come from segmented scans across the lanes (fixed
+ * order, deterministic).  Restates utils.softmax, src/utils.py:116-127, with
+ * the scores of function_transformer_attention.py:246-259 and the head mean of
+ * :34.  Returns GNPDE_EUNSUPPORTED for shapes outside the kernel (dk % 4 != 0,
+ * non-power-of-two teams, uniform scores, reference scores with out_kind 0).  */
+int gnpde_seg_block_edges(int mode, int64_t heads, int64_t dk);
+int gnpde_seg_plan_build(const int32_t* rowptr, int64_t R, int32_t eb, int32_t* items, int64_t items_capacity,
+                         int32_t* chunk_items, int64_t chunks_capacity, int32_t* heavy, int64_t heavy_capacity,
+                         int64_t* n_items, int64_t* n_chunks, int64_t* n_heavy);
+int gnpde_seg_softmax_f32(const int32_t* items, int64_t n_items, const int32_t* chunk_items, int64_t n_chunk_items,
+                          const int32_t* heavy, int64_t n_heavy, const int32_t* rowptr, const int32_t* rowidx,
+                          const int32_t* gidx, int group_is_dst, int out_kind, int mode, int64_t heads, int64_t dk,
+                          const double* cs, const float* q, const float* k, int64_t ldqk,
+                          float score_p0, float score_p1, float* w, double* m, float* rl, double* partials,
+                          void* stream);
+
 /* Per-edge, per-head attention in COO order (the [B,E,h] `attention` that
  * SpGraphTransAttentionLayer.forward returns, function_transformer_attention.py:265-267):
  *   att[perm[p]*heads + h] = exp(s_p,h - m[g,h]) * rl[g,h]  over the aggregation CSR. */

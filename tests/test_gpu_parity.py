@@ -252,6 +252,134 @@ def test_attention_rhs_reference_mode_vs_oracle(norm_idx, heads, att):
     assert rel(f, want) <= RTOL
 
 
+# ---------------------------------------------------------------- K2: edge-block segmented softmax
+def _attn_case(N, E, C, h, att, seed, B=1, hub_frac=0.15, wscale=0.1):
+    ei = hub_graph(N, E, seed=seed, B=B, hub_frac=hub_frac)
+    rng = np.random.default_rng(seed + 100)
+    x = rng.standard_normal((B, N, C)).astype(np.float32)
+    x0 = rng.standard_normal((B, N, C)).astype(np.float32)
+    Wq, Wk = [(rng.standard_normal((att, C)) * wscale).astype(np.float32) for _ in range(2)]
+    bq, bk = [(rng.standard_normal(att) * wscale).astype(np.float32) for _ in range(2)]
+    return ei, x, x0, Wq, bq, Wk, bk
+
+
+def _check_seg_plan(grouped, eb):
+    """Items tile every edge exactly once; whole-group items never split a group."""
+    plan = grouped.seg_plan(eb)
+    rp = grouped.rowptr.cpu().numpy()
+    it = plan.items.cpu().numpy().reshape(-1, 4)[:plan.n_items]
+    ch = plan.chunk_items.cpu().numpy().reshape(-1, 4)[:plan.n_chunk]
+    spans = np.concatenate([it[:, :2], ch[:, :2]])
+    spans = spans[np.argsort(spans[:, 0])]
+    assert (spans[:, 1] - spans[:, 0] <= eb).all() and (spans[:, 1] > spans[:, 0]).all()
+    assert spans[0, 0] == 0 and spans[-1, 1] == rp[-1] and (spans[1:, 0] == spans[:-1, 1]).all()
+    starts = set(rp.tolist())
+    assert all(b in starts and e in starts for b, e in it[:, :2])
+
+
+@pytest.mark.parametrize("C,h,att", [(128, 2, 32), (162, 2, 32), (80, 8, 128), (64, 4, 64), (256, 1, 16),
+                                     (16, 16, 64)])
+@pytest.mark.parametrize("norm_idx", [0, 1])
+def test_seg_softmax_attention_vs_per_group_kernels_and_oracle(C, h, att, norm_idx):
+    """Groups of 1..~4k edges: packed blocks, single-group items and chunked
+    long groups; the K2 path and the per-group kernels both match the oracle."""
+    N, E = 1500, 24000
+    ei, x, x0, Wq, bq, Wk, bk = _attn_case(N, E, C, h, att, seed=C + h + norm_idx)
+    g = ops.GraphCSR(T(ei), N)
+    ns = ops.node_scores(g, T(x), T(Wq), T(bq), T(Wk), T(bk), h, 'scaled_dot', 'per_edge')
+    eb = ops._lib.fn("gnpde_seg_block_edges")(ns.mode, h, att // h)
+    grouped = g.csr if norm_idx == 0 else g.csc
+    _check_seg_plan(grouped, eb)
+    assert grouped.seg_plan(eb).n_chunk > 0
+    kw = dict(alpha=torch.tensor(0.3, device=DEV), beta=torch.tensor(-0.7, device=DEV), add_source=True)
+    f = ops.attn_rhs(g, ns, None, None, norm_idx, T(x), T(x0), **kw)
+    fu = ops.attn_rhs(g, ns, None, None, norm_idx, T(x), T(x0), seg=False, **kw)
+    want = O.transformer_rhs(ei, x, x0, Wq, bq, Wk, bk, h, norm_idx, 0.3, -0.7, score_mode='per_edge',
+                             add_source=True)
+    assert rel(f, want) <= RTOL
+    assert rel(fu, want) <= RTOL
+    f2 = ops.attn_rhs(g, ns, None, None, norm_idx, T(x), T(x0), **kw)
+    assert torch.equal(f, f2)  # deterministic
+    m, rl = ops.softmax_stats(g, ns, norm_idx)
+    a = ops.edge_attention(g, ns, m, rl, norm_idx)
+    wa = O.transformer_attention(x, ei, Wq, bq, Wk, bk, h, norm_idx, 'scaled_dot', 'per_edge')
+    assert np.abs(a.double().cpu().numpy() - wa).max() <= 2e-5
+
+
+@pytest.mark.parametrize("heads,att", [(1, 8), (2, 32), (8, 128), (16, 32), (3, 24)])
+def test_seg_softmax_reference_norm1(heads, att):
+    N, E, C, B = 1200, 16000, 80, 2
+    ei, x, _, Wq, bq, Wk, bk = _attn_case(N, E, C, heads, att, seed=heads, B=B, wscale=0.02)
+    g = ops.GraphCSR(T(ei), N)
+    ns = ops.node_scores(g, T(x), T(Wq), T(bq), T(Wk), T(bk), heads)
+    _check_seg_plan(g.csc, 64)
+    m, rl = ops.softmax_stats(g, ns, 1)
+    m2, rl2 = ops.softmax_stats(g, ns, 1, seg=False)
+    deg = np.diff(g.csc.rowptr.cpu().numpy())
+    nz = torch.from_numpy(deg > 0).to(DEV)
+    assert torch.equal(m[nz], m2[nz])
+    assert torch.allclose(rl[nz], rl2[nz], rtol=2e-6, atol=0)
+    f = ops.attn_rhs(g, ns, m, rl, 1, T(x), alpha=torch.tensor(0.25, device=DEV))
+    want = O.transformer_rhs(ei, x, None, Wq, bq, Wk, bk, heads, 1, 0.25, 0.0)
+    assert rel(f, want) <= RTOL
+
+
+@pytest.mark.parametrize("attention_type", ["exp_kernel", "cosine_sim", "pearson"])
+@pytest.mark.parametrize("norm_idx", [0, 1])
+def test_seg_softmax_other_scores(attention_type, norm_idx):
+    N, E, C, h, att = 1000, 12000, 96, 2, 32
+    ei, x, _, Wq, bq, Wk, bk = _attn_case(N, E, C, h, att, seed=3)
+    g = ops.GraphCSR(T(ei), N)
+    ns = ops.node_scores(g, T(x), T(Wq), T(bq), T(Wk), T(bk), h, attention_type, 'per_edge', 1.3, 0.8)
+    f = ops.attn_rhs(g, ns, None, None, norm_idx, T(x), alpha=torch.tensor(0.1, device=DEV))
+    want = O.transformer_rhs(ei, x, None, Wq, bq, Wk, bk, h, norm_idx, 0.1, 0.0, attention_type=attention_type,
+                             score_mode='per_edge', output_var=1.3, lengthscale=0.8)
+    assert rel(f, want) <= RTOL
+
+
+@pytest.mark.parametrize("C,h,att", [(7, 2, 32), (128, 3, 24), (64, 1, 2)])
+def test_attention_shapes_outside_seg_kernel_use_per_group_kernels(C, h, att):
+    """dk % 4 != 0 and non-power-of-two teams run the per-group kernels."""
+    N, E = 600, 5000
+    ei, x, _, Wq, bq, Wk, bk = _attn_case(N, E, C, h, att, seed=C)
+    g = ops.GraphCSR(T(ei), N)
+    ns = ops.node_scores(g, T(x), T(Wq), T(bq), T(Wk), T(bk), h, 'scaled_dot', 'per_edge')
+    if ops._lib.fn("gnpde_seg_block_edges")(ns.mode, h, att // h) > 0:
+        pytest.skip("shape is inside K2")
+    assert ops._seg_call(g, ns, 0, 0) is NotImplemented
+    f = ops.attn_rhs(g, ns, None, None, 0, T(x), alpha=torch.tensor(0.0, device=DEV))
+    want = O.transformer_rhs(ei, x, None, Wq, bq, Wk, bk, h, 0, 0.0, 0.0, score_mode='per_edge')
+    assert rel(f, want) <= RTOL
+
+
+@pytest.mark.parametrize("method", ["euler", "rk4"])
+@pytest.mark.parametrize("mode,norm_idx", [("per_edge", 0), ("reference", 1)])
+def test_attention_stage_epilogue(method, mode, norm_idx):
+    """The transformer RHS inside the fused fixed-grid integrator (stage
+    combinations in K1's epilogue) equals the unfused integrator."""
+    from gnpde import integrator as gi
+    N, E, C, h, att = 1500, 20000, 64, 2, 32
+    ei, x, _, Wq, bq, Wk, bk = _attn_case(N, E, C, h, att, seed=11, wscale=0.05)
+    opt = dict(OPT, hidden_dim=C, heads=h, attention_dim=att, attention_norm_idx=norm_idx, function='transformer',
+               attention_score_mode=mode)
+    func = gnpde.ODEFuncTransformerAtt(C, C, opt, DEV).to(DEV).eval()
+    with torch.no_grad():
+        lay = func.multihead_att_layer
+        lay.Q.weight.copy_(T(Wq))
+        lay.Q.bias.copy_(T(bq))
+        lay.K.weight.copy_(T(Wk))
+        lay.K.bias.copy_(T(bk))
+        func.alpha_train.fill_(0.3)
+    func.edge_index = T(ei)
+    with torch.no_grad():
+        ws = gi._Workspace()
+        y_f = y_u = T(x)
+        for i in range(2):
+            y_f = gi._fused_step(method, func, 0.1 * i, 0.1, 0.1 * (i + 1), y_f, ws)
+            y_u = gi._fixed_step(method, func, 0.1 * i, 0.1, 0.1 * (i + 1), y_u, gi._Combine())
+    assert (y_f - y_u).abs().max() / y_u.abs().max() < 2e-6
+
+
 # ---------------------------------------------------------------- MFMA projection
 @pytest.mark.parametrize("R,K,Nout,split", [(1, 4, 8, 4), (1000, 128, 64, 32), (5003, 80, 256, 128),
                                             (777, 162, 64, 32), (64, 7, 33, 33), (4096, 256, 128, 64)])

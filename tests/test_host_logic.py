@@ -167,3 +167,42 @@ def test_unknown_method_raises():
     with pytest.raises(NotImplementedError):
         gode.odeint(lambda t, y: y, torch.ones(2), torch.tensor([0., 1.]), method='implicit_adams',
                     combine=gode._torch_combine)
+
+
+# ---------------------------------------------------------------- K2 edge-block plan (host C++, no GPU)
+@pytest.mark.parametrize("eb", [8, 32, 64])
+def test_seg_plan_build_tiles_edges(eb):
+    """gnpde_seg_plan_build: items and chunks tile every edge once, whole-group
+    items hold consecutive whole groups within eb edges, chunks split only
+    groups longer than eb, and heavy lists exactly those groups."""
+    import ctypes
+    from gnpde import _lib
+    rng = np.random.default_rng(eb)
+    deg = rng.integers(0, 12, size=3000)
+    deg[rng.integers(0, 3000, size=40)] = rng.integers(eb + 1, 5 * eb, size=40)
+    deg[:5] = 0
+    rp = np.zeros(len(deg) + 1, np.int32)
+    rp[1:] = np.cumsum(deg)
+    R, nnz = len(deg), int(rp[-1])
+    cap_i, cap_c, cap_h = R, nnz // eb + R + 1, nnz // eb + 2
+    items, chunks, heavy = (np.zeros((c, 4), np.int32) for c in (cap_i, cap_c, cap_h))
+    ni, nc, nh = ctypes.c_int64(0), ctypes.c_int64(0), ctypes.c_int64(0)
+    _lib.call("gnpde_seg_plan_build", rp.ctypes.data, R, eb, items.ctypes.data, cap_i, chunks.ctypes.data, cap_c,
+              heavy.ctypes.data, cap_h, ctypes.byref(ni), ctypes.byref(nc), ctypes.byref(nh))
+    it, ch, hv = items[:ni.value], chunks[:nc.value], heavy[:nh.value]
+    spans = np.concatenate([it[:, :2], ch[:, :2]])
+    spans = spans[np.argsort(spans[:, 0])]
+    assert spans[0, 0] == 0 and spans[-1, 1] == nnz and (spans[1:, 0] == spans[:-1, 1]).all()
+    assert ((spans[:, 1] - spans[:, 0]) <= eb).all() and ((spans[:, 1] - spans[:, 0]) > 0).all()
+    starts = set(rp.tolist())
+    assert all(b in starts and e in starts for b, e in it[:, :2])
+    assert (it[:, 2] == -1).all() and (rp[it[:, 3]] == it[:, 0]).all()
+    assert sorted(hv[:, 0].tolist()) == np.nonzero(deg > eb)[0].tolist()
+    assert (ch[:, 2] == np.arange(len(ch))).all()
+    for g, first, n, _ in hv:
+        assert (ch[first:first + n, 3] == g).all() and ch[first, 0] == rp[g] and ch[first + n - 1, 1] == rp[g + 1]
+    # greedy packing: no two consecutive whole-group items could have been merged
+    for a, b in zip(it[:-1], it[1:]):
+        if a[1] == b[0]:
+            first_len = rp[b[3] + 1] - b[0]
+            assert a[1] - a[0] + first_len > eb
