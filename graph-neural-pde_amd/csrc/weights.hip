@@ -1,0 +1,141 @@
+// weights.hip — edge-weight producers of the mixed and hard-attention ODE blocks.
+//
+// Both blocks integrate the same Laplacian RHS (K1) as the constant block; they
+// differ only in where its edge weights come from, once per forward:
+//   * MixedODEblock.get_mixed_attention   src/block_mixed.py:29-33
+//       w = mean_h(att) * (1 - sigmoid(gamma)) + edge_weight * sigmoid(gamma)
+//   * HardAttODEblock.forward             src/block_transformer_hard_attention.py:37-60
+//       eval : w = mean_h(att)
+//       train: keep edges whose mean attention exceeds the (1 - att_samp_pct)
+//              quantile, then renormalise per softmax group (:32-35).
+// All three are short elementwise / per-group passes over E weights.
+#include <hipcub/hipcub.hpp>
+
+#include "common.hpp"
+
+namespace gnpde {
+
+// out[i] = mean_h att[i*H + h]  [ * (1 - s) + ew[i] * s,  s = sigmoid(*gamma) ]
+__global__ void mix_weights_kernel(const float* __restrict__ att, int H, const float* __restrict__ ew,
+                                   const float* __restrict__ gamma, int64_t n, float* __restrict__ out) {
+  float s = 0.f;
+  if (gamma) s = 1.f / (1.f + expf(-gamma[0]));  // torch.sigmoid in fp32
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    float m;
+    if (H == 1) {
+      m = att[i];
+    } else {
+      float a = 0.f;
+      for (int h = 0; h < H; ++h) a += att[i * H + h];
+      m = a / (float)H;  // attention.mean(dim=2), fp32
+    }
+    out[i] = gamma ? m * (1.f - s) + ew[i] * s : m;
+  }
+}
+
+// One wavefront per group (row of a grouped CSR): the group's sum in a fixed
+// order (lane-strided partial sums, then a butterfly), then
+// w_out[e] = w_in[e] / (sum + 1e-16) for every COO edge e = perm[p] of the row.
+__global__ void group_normalize_kernel(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ perm,
+                                       int64_t R, const float* __restrict__ w_in, float* __restrict__ w_out) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / kWave;
+  const int64_t nwaves = (int64_t)gridDim.x * blockDim.x / kWave;
+  for (int64_t r = wave; r < R; r += nwaves) {
+    const int b = rowptr[r], e = rowptr[r + 1];
+    float s = 0.f;
+    for (int p = b + lane; p < e; p += kWave) s += w_in[perm[p]];
+    s = wave_sum(s);
+    const float den = s + kSoftmaxEps;
+    for (int p = b + lane; p < e; p += kWave) {
+      const int i = perm[p];
+      w_out[i] = w_in[i] / den;
+    }
+  }
+}
+
+// torch.quantile(v, q) (linear interpolation) on a sorted copy:
+// rank = q*(n-1) in fp32, lo = floor, hi = ceil, w = rank - lo,
+// lerp(a, b, w) = w < 0.5 ? a + w (b - a) : b - (b - a)(1 - w)   (ATen's lerp).
+__global__ void quantile_pick_kernel(const float* __restrict__ sorted, int64_t n, float q, float* __restrict__ out) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  const float rank = q * (float)(n - 1);
+  int64_t lo = (int64_t)rank;
+  int64_t hi = (int64_t)ceilf(rank);
+  if (lo < 0) lo = 0;
+  if (hi > n - 1) hi = n - 1;
+  if (lo > n - 1) lo = n - 1;
+  const float w = rank - (float)lo;
+  const float a = sorted[lo], b = sorted[hi];
+  out[0] = (fabsf(w) < 0.5f) ? a + w * (b - a) : b - (b - a) * (1.f - w);
+}
+
+static int grid_for_n(int64_t n, int block = 256, int cap = 4096) {
+  int64_t g = ceil_div(n, block);
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (int)g;
+}
+
+static size_t align_up256(size_t v) { return (v + 255) / 256 * 256; }
+
+static size_t sort_keys_bytes(int64_t n) {
+  size_t bytes = 0;
+  (void)hipcub::DeviceRadixSort::SortKeys(nullptr, bytes, (const float*)nullptr, (float*)nullptr, (int)n);
+  return bytes;
+}
+
+}  // namespace gnpde
+
+using namespace gnpde;
+
+extern "C" {
+
+int gnpde_mix_weights_f32(const float* att, int H, const float* ew, const float* gamma, int64_t n, float* out,
+                          void* stream) {
+  GNPDE_REQUIRE(H >= 1 && n >= 0, GNPDE_EINVAL, "mix_weights: bad sizes H=%d n=%lld", H, (long long)n);
+  GNPDE_REQUIRE((gamma == nullptr) == (ew == nullptr), GNPDE_EINVAL,
+                "mix_weights: gamma and edge_weight must both be set or both be NULL");
+  if (n == 0) return GNPDE_OK;
+  GNPDE_REQUIRE(att && out, GNPDE_EINVAL, "mix_weights: NULL pointer");
+  mix_weights_kernel<<<grid_for_n(n), 256, 0, as_stream(stream)>>>(att, H, ew, gamma, n, out);
+  GNPDE_LAUNCH_CHECK();
+  return GNPDE_OK;
+}
+
+int gnpde_group_normalize_f32(const int32_t* rowptr, const int32_t* perm, int64_t R, int64_t nnz, const float* w_in,
+                              float* w_out, void* stream) {
+  GNPDE_REQUIRE(R >= 1 && nnz >= 0, GNPDE_EINVAL, "group_normalize: bad sizes");
+  GNPDE_REQUIRE(w_in != w_out, GNPDE_EINVAL, "group_normalize: in-place is not supported");
+  if (nnz == 0) return GNPDE_OK;
+  GNPDE_REQUIRE(rowptr && perm && w_in && w_out, GNPDE_EINVAL, "group_normalize: NULL pointer");
+  const int64_t blocks = ceil_div(R, (int64_t)kWavesPerBlock);
+  group_normalize_kernel<<<(int)(blocks < 8192 ? blocks : 8192), kBlock, 0, as_stream(stream)>>>(rowptr, perm, R,
+                                                                                                   w_in, w_out);
+  GNPDE_LAUNCH_CHECK();
+  return GNPDE_OK;
+}
+
+size_t gnpde_quantile_workspace_bytes(int64_t n) {
+  const int64_t m = n > 0 ? n : 1;
+  return align_up256(sizeof(float) * (size_t)m) + align_up256(sort_keys_bytes(m));
+}
+
+int gnpde_quantile_f32(const float* v, int64_t n, double q, float* out, void* workspace, size_t workspace_bytes,
+                       void* stream) {
+  GNPDE_REQUIRE(n >= 1 && n < (int64_t)INT32_MAX, GNPDE_EINVAL, "quantile: n=%lld out of range", (long long)n);
+  GNPDE_REQUIRE(q >= 0.0 && q <= 1.0, GNPDE_EINVAL, "quantile: q=%g outside [0, 1]", q);
+  GNPDE_REQUIRE(v && out && workspace, GNPDE_EINVAL, "quantile: NULL pointer");
+  GNPDE_REQUIRE(workspace_bytes >= gnpde_quantile_workspace_bytes(n), GNPDE_EINVAL, "quantile: workspace too small");
+  hipStream_t s = as_stream(stream);
+  char* ws = static_cast<char*>(workspace);
+  float* sorted = reinterpret_cast<float*>(ws);
+  const size_t a = align_up256(sizeof(float) * (size_t)n);
+  size_t tmp_bytes = workspace_bytes - a;
+  GNPDE_HIP(hipcub::DeviceRadixSort::SortKeys(ws + a, tmp_bytes, v, sorted, (int)n, 0, 32, s));
+  quantile_pick_kernel<<<1, 64, 0, s>>>(sorted, n, (float)q, out);
+  GNPDE_LAUNCH_CHECK();
+  return GNPDE_OK;
+}
+
+}  // extern "C"

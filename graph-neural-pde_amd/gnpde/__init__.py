@@ -8,6 +8,8 @@ C ABI of include/gnpde.h (libgnpde.so, loaded by gnpde._lib with no fallback).
 from . import _lib, ops  # noqa: F401
 from .base_classes import GraphData, ODEblock, ODEFunc  # noqa: F401
 from .block_constant import ConstantODEblock  # noqa: F401
+from .block_mixed import MixedODEblock  # noqa: F401
+from .block_transformer_hard_attention import HardAttODEblock  # noqa: F401
 from .block_transformer_attention import AttODEblock  # noqa: F401
 from .function_laplacian_diffusion import LaplacianODEFunc  # noqa: F401
 from .function_transformer_attention import ODEFuncTransformerAtt, SpGraphTransAttentionLayer  # noqa: F401

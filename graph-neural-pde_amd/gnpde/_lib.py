@@ -45,6 +45,10 @@ SIGNATURES = {
     "gnpde_csr_build": (_int, [_vp, _i64, _i64, _i64, _int, _vp, _vp, _vp, _vp, _size, _vp]),
     "gnpde_gather_weights_f32": (_int, [_vp, _i64, _int, _vp, _vp, _vp]),
     "gnpde_indegree_i32": (_int, [_vp, _i64, _i64, _vp, _vp]),
+    "gnpde_mix_weights_f32": (_int, [_vp, _int, _vp, _vp, _i64, _vp, _vp]),
+    "gnpde_group_normalize_f32": (_int, [_vp, _vp, _i64, _i64, _vp, _vp, _vp]),
+    "gnpde_quantile_workspace_bytes": (_size, [_i64]),
+    "gnpde_quantile_f32": (_int, [_vp, _i64, _f64, _vp, _vp, _size, _vp]),
     "gnpde_plan_workspace_bytes": (_size, [_i64]),
     "gnpde_plan_build": (_int, [_vp, _i64, ctypes.c_int32, _vp, _i64, _vp, _i64, c_i64p, c_i64p, c_i64p, _vp,
                                 _size, _vp]),

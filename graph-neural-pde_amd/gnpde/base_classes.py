@@ -67,15 +67,17 @@ class ODEFunc(nn.Module):
         self._w_cache = {}
 
     def graph_for(self, x):
-        """Device CSR of ``self.edge_index`` for node count x.shape[1] (cached)."""
+        """Device CSR of ``self.edge_index`` for node count x.shape[1] (or x, an
+        int node count) — cached per edge_index tensor version."""
         if self.edge_index is None:
             raise RuntimeError("%s: edge_index is not set (the ODE block sets it in reset_graph_data)" %
                                self.__class__.__name__)
-        key = (_tensor_key(self.edge_index), int(x.shape[1]))
+        n = x if isinstance(x, int) else int(x.shape[1])
+        key = (_tensor_key(self.edge_index), n)
         if self._graph is None or key != self._graph_key:
             chunk = int(self.opt.get('gnpde_chunk', ops.DEFAULT_CHUNK)) if isinstance(self.opt, dict) else \
                 ops.DEFAULT_CHUNK
-            self._graph = ops.GraphCSR(self.edge_index, int(x.shape[1]), chunk=chunk)
+            self._graph = ops.GraphCSR(self.edge_index, n, chunk=chunk)
             self._graph_key = key
             self._w_cache = {}
         return self._graph

@@ -1,0 +1,94 @@
+"""Drop-in HardAttODEblock (reference src/block_transformer_hard_attention.py:6-99).
+
+Eval (:58-60): the RHS integrates over the full graph with the head-mean of
+the block-level attention — one HIP pass (gnpde_mix_weights_f32) then K1.
+
+Training (:42-57): edges whose mean attention exceeds the (1 - att_samp_pct)
+quantile are kept and their weights renormalised per softmax group (:32-35);
+the RHS then integrates over the sampled graph.  The threshold is a device
+radix sort + torch.quantile's interpolation (gnpde_quantile_f32), the
+renormalisation a fixed-order per-group pass (gnpde_group_normalize_f32); the
+edge compaction is a torch boolean index on the device.  The sampling runs
+under no_grad exactly as in the reference, so training differentiates the RHS
+through x, alpha_train and beta_train only — which the Laplacian backward
+provides.
+
+The fork's training branch cannot run as written (SURVEY.md §0.5 family): it
+indexes the batched [B,2,E] edge list with ``mask.T`` (:54) and takes
+``edge_index[attention_norm_idx]`` along the batch axis (:33).  This module
+follows the upstream single-graph semantics (B = 1; ``index`` = source row
+for attention_norm_idx 0, destination row for 1); parity for that branch is
+against the oracle only.  ``use_flux`` broadcasts [B,1,E] against [1,1,C]
+(:46-50) and is broken for E != C: it raises.
+"""
+import torch
+
+from . import ops
+from .base_classes import ODEblock
+from .function_transformer_attention import SpGraphTransAttentionLayer
+from .integrator import odeint, odeint_adjoint
+
+
+class HardAttODEblock(ODEblock):
+    def __init__(self, odefunc, regularization_fns, opt, device, t=torch.tensor([0, 1]), gamma=0.5):
+        super(HardAttODEblock, self).__init__(odefunc, regularization_fns, opt, device, t)
+        assert opt['att_samp_pct'] > 0 and opt['att_samp_pct'] <= 1, "attention sampling threshold must be in (0,1]"
+        self.device = device
+        self.train_integrator = odeint_adjoint if opt.get('adjoint', False) else odeint
+        self.test_integrator = odeint
+        self.set_tol()
+        if opt['function'] not in {'GAT', 'transformer'}:
+            self.multihead_att_layer = SpGraphTransAttentionLayer(opt['hidden_dim'], opt['hidden_dim'], opt, device,
+                                                                  edge_weights=self.odefunc.edge_weight)
+            if device is not None:
+                self.multihead_att_layer = self.multihead_att_layer.to(device)
+
+    def get_attention_weights(self, x):
+        if self.opt['function'] not in {'GAT', 'transformer'}:
+            attention, values = self.multihead_att_layer(x, self.data_edge_index)
+        else:
+            attention, values = self.odefunc.multihead_att_layer(x, self.data_edge_index)
+        return attention
+
+    def renormalise_attention(self, attention):
+        """attention [B,E'] over odefunc.edge_index / (its group sum + 1e-16) (:32-35)."""
+        g = self.odefunc.graph_for(int(self.num_nodes))
+        grouped = g.csr if int(self.opt['attention_norm_idx']) == 0 else g.csc
+        return ops.group_normalize(grouped, attention.reshape(-1)).reshape(attention.shape)
+
+    def sample_edges(self, x):
+        """Training-mode attention sampling (:42-57): (edge_index [1,2,E'], weights [1,E'])."""
+        if self.opt.get('use_flux', False):
+            raise NotImplementedError("gnpde: use_flux is broken in the reference (broadcasts [B,1,E] against "
+                                      "[1,1,C], block_transformer_hard_attention.py:46-50)")
+        ei = self.data_edge_index
+        if ei.shape[0] != 1:
+            raise NotImplementedError("gnpde: hard-attention sampling keeps a different edge count per graph; "
+                                      "the reference's batched branch is broken (:54) and only B = 1 is supported")
+        with torch.no_grad():
+            mean_att = ops.mix_weights(self.get_attention_weights(x))
+            threshold = ops.quantile(mean_att, 1 - self.opt['att_samp_pct'])
+            mask = mean_att[0] > threshold
+            edge_index = ei[:, :, mask]
+            self.odefunc.edge_index = edge_index
+            weights = self.renormalise_attention(mean_att[:, mask])
+        print('retaining {} of {} edges'.format(edge_index.shape[2], ei.shape[2]))
+        return edge_index, weights
+
+    def forward(self, x, graph_data, y=None):
+        self.reset_graph_data(graph_data, x.dtype, y)
+        if self.training:
+            edge_index, weights = self.sample_edges(x)
+            self.odefunc.edge_index = edge_index
+            self.odefunc.attention_weights = weights
+        else:
+            self.odefunc.edge_index = self.data_edge_index
+            self.odefunc.attention_weights = ops.mix_weights(self.get_attention_weights(x))
+        self.reg_odefunc.odefunc.edge_index = self.odefunc.edge_index
+        self.reg_odefunc.odefunc.edge_weight = self.odefunc.edge_weight
+        self.reg_odefunc.odefunc.attention_weights = self.odefunc.attention_weights
+        return self._integrate(x, {'step_size': self.opt.get('step_size')})
+
+    def __repr__(self):
+        return self.__class__.__name__ + '( Time Interval ' + str(self.t[0].item()) + ' -> ' + \
+            str(self.t[1].item()) + ")"

@@ -1,13 +1,15 @@
 """Drop-in registry (reference src/model_configurations.py:17-44): the plugin
 point ``GNN.__init__`` uses (src/GNN.py:12-15).
 
-Built here: block 'constant', 'attention'; function
-'laplacian', 'transformer'.  The other names the reference registers are
-SURVEY §8(f) next-4 ('mixed', 'hard_attention') or out of scope
-('rewire_attention', 'GAT') and raise NotImplementedError naming the reason,
-rather than silently falling back to a different model.
+Built here: block 'constant', 'attention', 'mixed',
+'hard_attention'; function 'laplacian', 'transformer'.  The other names the
+reference registers are out of scope ('rewire_attention', 'GAT') and raise
+NotImplementedError naming the reason, rather than silently falling back to a
+different model.
 """
 from .block_constant import ConstantODEblock
+from .block_mixed import MixedODEblock
+from .block_transformer_hard_attention import HardAttODEblock
 from .block_transformer_attention import AttODEblock
 from .function_laplacian_diffusion import LaplacianODEFunc
 from .function_transformer_attention import ODEFuncTransformerAtt
@@ -22,16 +24,18 @@ class FunctionNotDefined(Exception):
 
 
 _PENDING_BLOCKS = {
-    'mixed': 'SURVEY §8(f) next-4 (same RHS kernel, different weight producer)',
-    'hard_attention': 'SURVEY §8(f) next-4 (same RHS kernel, different weight producer)',
     'rewire_attention': 'out of scope (graph surgery between forwards, SURVEY §2 row 9)',
 }
 
 
 def set_block(opt):
     ode_str = opt['block']
+    if ode_str == 'mixed':
+        return MixedODEblock
     if ode_str == 'attention':
         return AttODEblock
+    if ode_str == 'hard_attention':
+        return HardAttODEblock
     if ode_str == 'constant':
         return ConstantODEblock
     if ode_str in _PENDING_BLOCKS:

@@ -221,6 +221,63 @@ class GraphCSR(object):
         return out
 
 
+# --------------------------------------------------------------------------- block weight producers
+def mix_weights(att, edge_weight=None, gamma=None):
+    """COO-order [B,E] weights from attention [B,E,h] (or [B,E]):
+    mean_h(att) [* (1 - sigmoid(gamma)) + edge_weight * sigmoid(gamma)]
+    (MixedODEblock.get_mixed_attention, src/block_mixed.py:29-33; gamma=None:
+    the plain head mean of src/block_transformer_hard_attention.py:42,60)."""
+    _require_gpu(att, "attention", torch.float32)
+    att = att.contiguous()
+    if att.dim() == 2:
+        H = 1
+    elif att.dim() == 3:
+        H = att.shape[2]
+    else:
+        raise ValueError("attention must be [B,E] or [B,E,h]")
+    B, E = att.shape[0], att.shape[1]
+    if (gamma is None) != (edge_weight is None):
+        raise ValueError("mix_weights: gamma and edge_weight go together")
+    if edge_weight is not None:
+        _require_gpu(edge_weight, "edge_weight", torch.float32)
+        edge_weight = edge_weight.contiguous()
+        if tuple(edge_weight.shape) != (B, E):
+            raise ValueError("edge_weight shape %s != [%d,%d]" % (tuple(edge_weight.shape), B, E))
+        gamma = _scalar(gamma, "gamma", att.device)
+    out = torch.empty(B, E, dtype=torch.float32, device=att.device)
+    _lib.call("gnpde_mix_weights_f32", _ptr(att), H, _ptr(edge_weight), _ptr(gamma), B * E, _ptr(out),
+              _stream(att.device))
+    return out
+
+
+def group_normalize(grouped, w):
+    """w[e] / (sum of w over e's group + 1e-16) in COO order, groups = rows of
+    ``grouped`` (HardAttODEblock.renormalise_attention,
+    src/block_transformer_hard_attention.py:32-35)."""
+    _require_gpu(w, "weights", torch.float32)
+    w = w.contiguous()
+    if w.numel() != grouped.nnz:
+        raise ValueError("group_normalize: %d weights for %d edges" % (w.numel(), grouped.nnz))
+    out = torch.empty_like(w)
+    _lib.call("gnpde_group_normalize_f32", _ptr(grouped.rowptr), _ptr(grouped.perm), grouped.R, grouped.nnz,
+              _ptr(w), _ptr(out), _stream(w.device))
+    return out
+
+
+def quantile(v, q):
+    """torch.quantile(v, q) (linear interpolation) as a device scalar [1]."""
+    _require_gpu(v, "values", torch.float32)
+    v = v.contiguous().reshape(-1)
+    n = v.numel()
+    if n == 0:
+        raise ValueError("quantile of an empty tensor")
+    ws_bytes = _lib.fn("gnpde_quantile_workspace_bytes")(n)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=v.device)
+    out = torch.empty(1, dtype=torch.float32, device=v.device)
+    _lib.call("gnpde_quantile_f32", _ptr(v), n, float(q), _ptr(out), _ptr(ws), ws_bytes, _stream(v.device))
+    return out
+
+
 # --------------------------------------------------------------------------- epilogue helpers
 def _flags(rhs, alpha_sigmoid, add_source):
     f = 0

@@ -89,6 +89,29 @@ int gnpde_csr_rowidx(const int32_t* rowptr, int64_t R, int64_t nnz, int32_t* row
 int gnpde_gather_weights_f32(const float* w_in, int64_t nnz, int H, const int32_t* perm, float* w_out,
                              void* stream);
 
+/* ---------------------------------------------------------------- block weight producers
+ * out[i] = mean_{h<H} att[i*H + h]  (H = 1: copy), and when gamma != NULL
+ * out[i] = mean * (1 - sigmoid(*gamma)) + ew[i] * sigmoid(*gamma)  (COO order,
+ * n = B*E).  gamma is a device scalar (pre-sigmoid).  Replaces
+ * MixedODEblock.get_mixed_attention, src/block_mixed.py:29-33, and the
+ * head mean of HardAttODEblock.forward, src/block_transformer_hard_attention.py:42,60. */
+int gnpde_mix_weights_f32(const float* att, int H, const float* ew, const float* gamma, int64_t n, float* out,
+                          void* stream);
+
+/* w_out[e] = w_in[e] / (sum of w_in over e's group + 1e-16), groups = the rows
+ * of a grouped CSR (rowptr[R+1], perm[nnz] = CSR position -> COO edge id),
+ * COO order in and out; fixed summation order (deterministic).  Replaces
+ * HardAttODEblock.renormalise_attention, src/block_transformer_hard_attention.py:32-35. */
+int gnpde_group_normalize_f32(const int32_t* rowptr, const int32_t* perm, int64_t R, int64_t nnz, const float* w_in,
+                              float* w_out, void* stream);
+
+/* *out = torch.quantile(v[0:n], q) (linear interpolation; rank q*(n-1) in
+ * fp32, ATen's lerp) written to DEVICE memory; radix sort into the workspace.
+ * The attention-sampling threshold of src/block_transformer_hard_attention.py:52. */
+size_t gnpde_quantile_workspace_bytes(int64_t n);
+int gnpde_quantile_f32(const float* v, int64_t n, double q, float* out, void* workspace, size_t workspace_bytes,
+                       void* stream);
+
 /* deg[r] = #{p : idx[p] == r}, r < R (memset + integer atomics: deterministic).
  * With idx = the aggregation CSR's col this is the in-degree used by the
  * reference-mode key sum.                                                   */

@@ -94,6 +94,55 @@ def laplacian_rhs(edge_index, x, x0, alpha_train, beta_train, block='constant', 
     return rhs_epilogue(ax, x, x0, alpha_train, beta_train, add_source, no_alpha_sigmoid)
 
 
+# --------------------------------------------------------------------------- block weight producers
+def mixed_attention(attention, edge_weight, gamma):
+    """MixedODEblock.get_mixed_attention — src/block_mixed.py:29-33:
+    ``attention.mean(dim=2) * (1 - sigmoid(gamma)) + edge_weight * sigmoid(gamma)``."""
+    g = float(_sigmoid(float(gamma)))
+    return _as64(attention).mean(axis=2) * (1.0 - g) + _as64(edge_weight) * g
+
+
+def quantile_f32(v, q):
+    """torch.quantile(v, q) with linear interpolation, restated in float32 as
+    ATen computes it (sort; rank = q*(n-1) in the input dtype; lerp with ATen's
+    two-sided formula) — the threshold of src/block_transformer_hard_attention.py:52."""
+    s = np.sort(np.asarray(v, dtype=np.float32).reshape(-1))
+    n = s.size
+    rank = np.float32(q) * np.float32(n - 1)
+    lo = int(np.floor(rank))
+    hi = int(np.ceil(rank))
+    w = np.float32(rank - np.float32(lo))
+    a, b = s[lo], s[hi]
+    if abs(w) < 0.5:
+        return np.float32(a + w * (b - a))
+    return np.float32(b - (b - a) * (np.float32(1) - w))
+
+
+def group_normalize(w, index, num_nodes):
+    """HardAttODEblock.renormalise_attention (upstream single-graph semantics) —
+    src/block_transformer_hard_attention.py:32-35: ``w / (scatter_sum(w, index)[index] + 1e-16)``."""
+    w = _as64(w)
+    sums = np.zeros(num_nodes)
+    np.add.at(sums, np.asarray(index), w)
+    return w / (sums[np.asarray(index)] + 1e-16)
+
+
+def hard_attention_sample(edge_index, attention, att_samp_pct, norm_idx, num_nodes):
+    """Training-mode attention sampling of HardAttODEblock.forward —
+    src/block_transformer_hard_attention.py:42-57 (B = 1, use_flux off):
+    keep edges whose head-mean attention exceeds the (1 - att_samp_pct)
+    quantile; renormalise the kept weights per group of row ``norm_idx``.
+    Returns (edge_index [1,2,E'], weights [1,E'])."""
+    mean_att = np.asarray(attention, dtype=np.float32)
+    if mean_att.ndim == 3:
+        mean_att = (mean_att.sum(axis=2, dtype=np.float32) / np.float32(mean_att.shape[2])).astype(np.float32)
+    thr = quantile_f32(mean_att, 1 - att_samp_pct)
+    mask = mean_att[0] > thr
+    ei = np.asarray(edge_index)[:, :, mask]
+    w = group_normalize(mean_att[0, mask], ei[0, norm_idx], num_nodes)
+    return ei, w[None, :]
+
+
 # --------------------------------------------------------------------------- edge softmax
 def edge_softmax(src, index, num_nodes=None):
     """utils.softmax — src/utils.py:116-127.

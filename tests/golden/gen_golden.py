@@ -94,6 +94,7 @@ sys.path.insert(0, REF_SRC)
 import function_laplacian_diffusion as ref_lap  # noqa: E402
 import function_transformer_attention as ref_att  # noqa: E402
 import utils as ref_utils  # noqa: E402
+import block_mixed as ref_mixed  # noqa: E402  (module import only; the block's __init__ needs torchdiffeq)
 
 # test/test_params.py:5-16 (the reference tests' shared OPT dict), restated as data.
 BASE_OPT = {
@@ -233,6 +234,41 @@ def run_softmax(name, rng, B, E, H, n_nodes):
     return name
 
 
+# --------------------------------------------------------------------------- mixed block weights
+def run_mixed(name, rng, B, E, H, gamma):
+    """MixedODEblock.get_mixed_attention (src/block_mixed.py:29-33), called
+    unbound on a namespace holding exactly the attributes it reads (the block
+    itself cannot be constructed: its __init__ imports torchdiffeq)."""
+    att = f32(rng.uniform(0.0, 1.0, (B, E, H)))
+    ew = f32(rng.uniform(0.0, 1.0, (B, E)))
+    gamma = float(np.float32(gamma))
+    out = {}
+    for dt, tag in ((torch.float64, 'w'), (torch.float32, 'w_ref32')):
+        att_t = torch.from_numpy(att).to(dt)
+        ns = types.SimpleNamespace(gamma=torch.tensor([gamma], dtype=dt),
+                                   odefunc=types.SimpleNamespace(edge_weight=torch.from_numpy(ew).to(dt)),
+                                   get_attention_weights=lambda x, a=att_t: a)
+        with torch.no_grad():
+            out[tag] = ref_mixed.MixedODEblock.get_mixed_attention(ns, None).numpy()
+    meta = dict(kind='mixed', B=B, E=E, H=H)
+    np.savez_compressed(os.path.join(OUT_DIR, name + '.npz'), meta=json.dumps(meta), attention=att, edge_weight=ew,
+                        gamma=f32(gamma), w=out['w'], w_ref32=out['w_ref32'])
+    return name
+
+
+def main_blocks():
+    """Fixtures of the mixed block's weight producer (separate seed, so the
+    fixtures of main() are untouched)."""
+    rng = np.random.default_rng(20250118)
+    made = [run_mixed('mixed_w_b1_h1', rng, 1, 500, 1, 0.0), run_mixed('mixed_w_b2_h4', rng, 2, 700, 4, -0.7),
+            run_mixed('mixed_w_b1_h8', rng, 1, 300, 8, 1.3)]
+    path = os.path.join(OUT_DIR, 'MANIFEST.json')
+    have = json.load(open(path))
+    with open(path, 'w') as fh:
+        json.dump(sorted(set(have) | set(made)), fh, indent=1)
+    print('wrote', len(made), 'fixtures to', OUT_DIR)
+
+
 def main():
     rng = np.random.default_rng(20250117)
     made = []
@@ -277,4 +313,7 @@ def main():
 
 
 if __name__ == '__main__':
-    main()
+    if len(sys.argv) > 1 and sys.argv[1] == 'blocks':
+        main_blocks()
+    else:
+        main()

@@ -24,8 +24,10 @@ def test_registry_matches_reference_names():
     assert gnpde.set_function(dict(OPT, function='transformer')) is gnpde.ODEFuncTransformerAtt
     assert gnpde.set_block(dict(OPT, block='constant')) is gnpde.ConstantODEblock
     assert gnpde.set_block(dict(OPT, block='attention')) is gnpde.AttODEblock
+    assert gnpde.set_block(dict(OPT, block='mixed')) is gnpde.MixedODEblock
+    assert gnpde.set_block(dict(OPT, block='hard_attention')) is gnpde.HardAttODEblock
     with pytest.raises(NotImplementedError):
-        gnpde.set_block(dict(OPT, block='mixed'))
+        gnpde.set_block(dict(OPT, block='rewire_attention'))
     with pytest.raises(NotImplementedError):
         gnpde.set_function(dict(OPT, function='GAT'))
     from gnpde.model_configurations import BlockNotDefined, FunctionNotDefined
@@ -54,6 +56,27 @@ def test_attention_block_contract():
                             t=torch.tensor([0, 1]))
     assert isinstance(blk.multihead_att_layer, gnpde.SpGraphTransAttentionLayer)
     assert blk.test_integrator is gnpde.odeint and blk.atol == 1e-7 and blk.rtol == 1e-9
+
+
+def test_mixed_block_contract():
+    """test/test_block_mixed.py:57-66: gamma initialised to 0, Laplacian odefunc, attention layer."""
+    blk = gnpde.MixedODEblock(gnpde.LaplacianODEFunc, [], dict(OPT, block='mixed', heads=1), None,
+                              t=torch.tensor([0, 1]))
+    assert isinstance(blk.odefunc, gnpde.LaplacianODEFunc)
+    assert blk.gamma.item() == 0.0 and tuple(blk.gamma.shape) == (1,)
+    assert isinstance(blk.multihead_att_layer, gnpde.SpGraphTransAttentionLayer)
+    assert 'gamma' in blk.state_dict() and 'multihead_att_layer.Q.weight' in blk.state_dict()
+
+
+def test_hard_attention_block_contract():
+    opt = dict(OPT, block='hard_attention', att_samp_pct=0.5)
+    blk = gnpde.HardAttODEblock(gnpde.LaplacianODEFunc, [], opt, None, t=torch.tensor([0, 1]))
+    assert isinstance(blk.multihead_att_layer, gnpde.SpGraphTransAttentionLayer)
+    tr = gnpde.HardAttODEblock(gnpde.ODEFuncTransformerAtt, [], dict(opt, function='transformer'), None,
+                               t=torch.tensor([0, 1]))
+    assert not hasattr(tr, 'multihead_att_layer')  # uses the odefunc's layer (:21-23, :29)
+    with pytest.raises(AssertionError):
+        gnpde.HardAttODEblock(gnpde.LaplacianODEFunc, [], dict(opt, att_samp_pct=0.0), None, t=torch.tensor([0, 1]))
 
 
 def test_no_cpu_fallback():

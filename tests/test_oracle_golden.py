@@ -53,7 +53,8 @@ def test_fixture_manifest():
     assert len(names) >= 20
 
 
-@pytest.mark.parametrize("path", [p for p in FIXTURES if "softmax" not in p], ids=os.path.basename)
+@pytest.mark.parametrize("path", [p for p in FIXTURES if os.path.basename(p).startswith(("lap_", "att_"))],
+                         ids=os.path.basename)
 def test_oracle_rhs_matches_reference(path):
     d, m = load(path)
     f = oracle_rhs(d, m)
@@ -80,6 +81,44 @@ def test_oracle_attention_matches_reference(path):
 def test_oracle_softmax_matches_reference(path):
     d, _ = load(path)
     assert np.abs(O.edge_softmax(d["src"], d["index"]) - d["out"]).max() < 1e-15
+
+
+@pytest.mark.parametrize("path", [p for p in FIXTURES if os.path.basename(p).startswith("mixed_")],
+                         ids=os.path.basename)
+def test_oracle_mixed_attention_matches_reference(path):
+    """MixedODEblock.get_mixed_attention (src/block_mixed.py:29-33), reference fp64 run."""
+    d, _ = load(path)
+    w = O.mixed_attention(d["attention"], d["edge_weight"], d["gamma"])
+    assert np.abs(w - d["w"]).max() < 1e-14
+    assert np.abs(d["w_ref32"] - d["w"]).max() < 1e-6
+
+
+@pytest.mark.parametrize("n", [1, 2, 7, 1000, 4097])
+@pytest.mark.parametrize("q", [0.0, 0.1, 0.25, 0.5, 0.9, 1.0])
+def test_oracle_quantile_matches_torch(n, q):
+    """torch.quantile (the threshold of src/block_transformer_hard_attention.py:52), in-container torch."""
+    torch = pytest.importorskip("torch")
+    v = np.random.default_rng(n).standard_normal(n).astype(np.float32)
+    want = float(torch.quantile(torch.from_numpy(v), q))
+    assert float(O.quantile_f32(v, q)) == want
+
+
+@pytest.mark.parametrize("norm_idx", [0, 1])
+def test_oracle_hard_attention_sample(norm_idx):
+    """Kept edges exceed the quantile threshold, each group of the kept graph sums to 1."""
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(3 + norm_idx)
+    N, E = 50, 600
+    ei = rng.integers(0, N, size=(1, 2, E))
+    att = rng.uniform(0, 1, (1, E, 2)).astype(np.float32)
+    ei2, w = O.hard_attention_sample(ei, att, 0.4, norm_idx, N)
+    mean = att.mean(axis=2)
+    thr = float(torch.quantile(torch.from_numpy(mean), 0.6))
+    assert ei2.shape[2] == int((mean[0] > thr).sum()) and 0 < ei2.shape[2] < E
+    sums = np.zeros(N)
+    np.add.at(sums, ei2[0, norm_idx], w[0])
+    live = np.unique(ei2[0, norm_idx])
+    assert np.allclose(sums[live], 1.0, atol=1e-12)
 
 
 def test_reference_fp32_within_tolerance_of_fp64():
