@@ -57,7 +57,10 @@ __global__ void group_normalize_kernel(const int32_t* __restrict__ rowptr, const
 // torch.quantile(v, q) (linear interpolation) on a sorted copy:
 // rank = q*(n-1) in fp32, lo = floor, hi = ceil, w = rank - lo,
 // lerp(a, b, w) = w < 0.5 ? a + w (b - a) : b - (b - a)(1 - w)   (ATen's lerp).
+// No FMA contraction here: the threshold must equal torch.quantile bit for bit
+// (the sampling mask is a strict comparison against it).
 __global__ void quantile_pick_kernel(const float* __restrict__ sorted, int64_t n, float q, float* __restrict__ out) {
+#pragma clang fp contract(off)
   if (blockIdx.x != 0 || threadIdx.x != 0) return;
   const float rank = q * (float)(n - 1);
   int64_t lo = (int64_t)rank;

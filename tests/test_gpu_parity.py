@@ -647,7 +647,8 @@ def test_mix_weights_golden(path):
 @pytest.mark.parametrize("n", [1, 2, 5, 1000, 65537, 1200000])
 @pytest.mark.parametrize("q", [0.0, 0.3, 0.5, 0.95, 1.0])
 def test_quantile_kernel_matches_torch_quantile(n, q):
-    """Bit-exact against torch.quantile (CPU) — including ties (values on a coarse grid)."""
+    """Bit-exact against the oracle's restatement of torch.quantile (no FMA) — including
+    ties (values on a coarse grid) — and within 1 ulp of the host torch.quantile."""
     rng = np.random.default_rng(n)
     v = rng.standard_normal(n).astype(np.float32)
     if n > 100:
@@ -655,8 +656,9 @@ def test_quantile_kernel_matches_torch_quantile(n, q):
     want = np.float32(O.quantile_f32(v, q))
     got = ops.quantile(T(v), q).cpu().numpy()[0]
     assert got == want
-    if n <= 16_000_000 and n >= 1:
-        assert got == np.float32(torch.quantile(torch.from_numpy(v), q).item())
+    # torch's own CPU quantile may contract its lerp into an FMA (host-dependent): within 1 ulp
+    tq = np.float32(torch.quantile(torch.from_numpy(v), q).item())
+    assert abs(float(got) - float(tq)) <= float(np.spacing(np.abs(tq)))
 
 
 @pytest.mark.parametrize("norm_idx", [0, 1])
