@@ -9,10 +9,65 @@
 namespace gnpde {
 
 // ------------------------------------------------------------------ weight policies
+// A policy splits the weight of CSR position p (row, destination c) into
+// load() — the raw operands, issued with the column index — and finish() —
+// the arithmetic, run once the first gathers of x are in flight, so the
+// weight's memory latency overlaps the row gathers instead of preceding them.
+//
 // Plain per-edge weights (Laplacian RHS, function_laplacian_diffusion.py:54-57).
 struct PlainWeights {
   const float* __restrict__ w;
-  __device__ __forceinline__ float operator()(int /*row*/, int p, int /*c*/) const { return w[p]; }
+  struct Raw {
+    float w;
+  };
+  __device__ __forceinline__ Raw load(int /*row*/, int p, int /*c*/) const { return Raw{w[p]}; }
+  __device__ __forceinline__ float finish(int /*row*/, const Raw& r) const { return r.w; }
+};
+
+// Reference-mode (fork scaled_dot) attention under destination-grouped softmax
+// (attention_norm_idx 1), head-mean taken on the fly: the score of an edge is
+// the node score cs[row, h] of its source (the aggregating row), the group
+// statistics m, rl belong to its destination c.  Same arithmetic, in the same
+// order, as attn_weights_kernel (rhs.hip), so fusing it into K1 changes no
+// bit; it saves the separate weights pass and its [nnz] round trip.
+// MAXH > 0: heads <= MAXH, the per-edge statistics are loaded up front;
+// MAXH == 0: any heads <= 16, loaded in finish().
+template <int MAXH>
+struct RefDstSoftmaxWeights {
+  const double* __restrict__ cs;
+  const double* __restrict__ m;
+  const float* __restrict__ rl;
+  int H;
+  struct Raw {
+    double mm[MAXH > 0 ? MAXH : 1];
+    float rr[MAXH > 0 ? MAXH : 1];
+    int c;
+  };
+  __device__ __forceinline__ Raw load(int /*row*/, int /*p*/, int c) const {
+    Raw r;
+    r.c = c;
+    if constexpr (MAXH > 0) {
+#pragma unroll
+      for (int h = 0; h < MAXH; ++h) {
+        const int hh = h < H ? h : 0;
+        r.mm[h] = m[(int64_t)c * H + hh];
+        r.rr[h] = rl[(int64_t)c * H + hh];
+      }
+    }
+    return r;
+  }
+  __device__ __forceinline__ float finish(int row, const Raw& r) const {
+    float acc = 0.f;
+    if constexpr (MAXH > 0) {
+#pragma unroll
+      for (int h = 0; h < MAXH; ++h)
+        if (h < H) acc += expf((float)(cs[(int64_t)row * H + h] - r.mm[h])) * r.rr[h];
+    } else {
+      for (int h = 0; h < H; ++h)
+        acc += expf((float)(cs[(int64_t)row * H + h] - m[(int64_t)r.c * H + h])) * rl[(int64_t)r.c * H + h];
+    }
+    return acc / (float)H;
+  }
 };
 
 // ------------------------------------------------------------------ aggregation kernel
@@ -60,21 +115,22 @@ __global__ __launch_bounds__(256) void agg_kernel(const int4* __restrict__ items
   for (int e0 = beg; e0 < end; e0 += SL) {
     const int n = min(SL, end - e0);
     int mc = 0;
-    float mw = 0.f;
+    typename WP::Raw raw{};
     if (sl < n) {
       mc = col[e0 + sl];
-      mw = wp(row, e0 + sl, mc);
+      raw = wp.load(row, e0 + sl, mc);
     }
+    float mw = 0.f;
     for (int j = 0; j < n; j += G * U) {
       float v[U][NCH][VEC];
       float ww[U];
+      int srcl[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int jj = j + u * G + g;
         const int src = rs * SL + (jj < n ? jj : 0);
+        srcl[u] = src;
         const int c = __shfl(mc, src);
-        const float wsl = __shfl(mw, src);
-        ww[u] = jj < n ? wsl : 0.f;
         const float* __restrict__ xr = ep.x + (int64_t)c * ep.ldx;
 #pragma unroll
         for (int ch = 0; ch < NCH; ++ch) {
@@ -86,6 +142,14 @@ __global__ __launch_bounds__(256) void agg_kernel(const int4* __restrict__ items
             for (int t = 0; t < VEC; ++t) v[u][ch][t] = 0.f;
           }
         }
+      }
+      // the weights of this batch of edges, finished while its first gathers are in flight
+      if (j == 0 && sl < n) mw = wp.finish(row, raw);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int jj = j + u * G + g;
+        const float wsl = __shfl(mw, srcl[u]);
+        ww[u] = jj < n ? wsl : 0.f;
       }
 #pragma unroll
       for (int u = 0; u < U; ++u)

@@ -283,7 +283,7 @@ __global__ __launch_bounds__(256) void keysum_partial_kernel(const float* __rest
     double acc[VEC];
 #pragma unroll
     for (int i = 0; i < VEC; ++i) acc[i] = 0.0;
-#pragma unroll 4
+#pragma unroll 8
     for (int64_t n = n0 + rs; n < n1; n += RPB) {
       const double d = (double)indeg[base + n];
       float v[VEC];
@@ -308,69 +308,99 @@ __global__ __launch_bounds__(256) void keysum_partial_kernel(const float* __rest
   }
 }
 
-// xbar[b][c] = sum over tiles: 16 columns x 16 interleaved tile subsets per block,
-// subsets combined in a fixed order.
+// xbar[b][c] = sum over tiles: kTileCols columns x kTileSubs interleaved tile
+// subsets per block (every subset's loads issued together), subsets combined
+// in a fixed order (deterministic).
+constexpr int kTileCols = 4;
+constexpr int kTileSubs = 64;
+
 __global__ __launch_bounds__(256) void keysum_tiles_kernel(const double* __restrict__ part, int ntiles, int C,
                                                             double* __restrict__ xbar) {
-  __shared__ double red[16][17];
+  __shared__ double red[kWavesPerBlock][kTileCols + 1];
   const int b = blockIdx.y;
-  const int cl = threadIdx.x & 15, sub = threadIdx.x >> 4;
-  const int c = blockIdx.x * 16 + cl;
+  const int cl = threadIdx.x % kTileCols, sub = threadIdx.x / kTileCols;
+  const int c = blockIdx.x * kTileCols + cl;
   double s = 0.0;
   if (c <= C) {
-#pragma unroll 4
-    for (int t = sub; t < ntiles; t += 16) s += part[((int64_t)b * ntiles + t) * (C + 1) + c];
+#pragma unroll 16
+    for (int t = sub; t < ntiles; t += kTileSubs) s += part[((int64_t)b * ntiles + t) * (C + 1) + c];
   }
-  red[sub][cl] = s;
+  // fixed tree: the 16 subsets of a wavefront by xor shuffles, then the 4 wavefronts
+#pragma unroll
+  for (int o = kTileCols; o < kWave; o <<= 1) s += __shfl_xor(s, o);
+  const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x >> 6;
+  if (lane < kTileCols) red[wv][lane] = s;
   __syncthreads();
-  if (sub == 0 && c <= C) {
+  if (threadIdx.x < kTileCols && c <= C) {
     double a = 0.0;
-    for (int k = 0; k < 16; ++k) a += red[k][cl];
+#pragma unroll
+    for (int k = 0; k < kWavesPerBlock; ++k) a += red[k][cl];
     xbar[(int64_t)b * (C + 1) + c] = a;
   }
 }
 
-// per batch element: S = Wk xbar + E bk (recomputed per block into LDS: att
-// dot products of length C), then this block's slice of
-// U[c,h] = sum_{d in h} Wq[d,c] S[d] / sqrt(dk) and, in block 0, v[h] = bq_h . S_h / sqrt(dk).
-// U is stored padded as [B][Cp][Hp] (zeros past C and H) so node_scores reads
-// it with compile-time offsets and no clamping; v as [B][Hp].
-constexpr int kFinishPairs = 256;  // (c,h) pairs per block
+// Per batch element b, from xbar = sum_n indeg(n) x_n (and xbar[C] = E):
+//   S[d]   = Wk[d,:] . xbar + E bk[d]                    (the fork's global key sum, :249)
+//   U[c,h] = sum_{d in head h} Wq[d,c] S[d] / sqrt(dk)   (padded [Cp][Hp], zeros past C, H)
+//   v[h]   = bq_h . S_h / sqrt(dk)
+// so that cs[n,h] = x_n . U[:,h] + v[h] = q_{n,h} . S_h / sqrt(dk).  Computed by
+// every node-score workgroup into its own LDS (a few KFLOP, operands from L2):
+// no single-workgroup launch between the key sum and the node scores.
+struct KeyProj {
+  const double* __restrict__ xbar;  // [B][C+1]
+  const float* __restrict__ Wq;
+  const float* __restrict__ bq;
+  const float* __restrict__ Wk;
+  const float* __restrict__ bk;
+  int att;
+};
 
-__global__ __launch_bounds__(256) void keysum_finish_kernel(const double* __restrict__ xbar, int C,
-                                                             const float* __restrict__ Wq,
-                                                             const float* __restrict__ bq,
-                                                             const float* __restrict__ Wk,
-                                                             const float* __restrict__ bk, int att, int H, int Cp,
-                                                             int Hp, double* __restrict__ U, double* __restrict__ v) {
-  extern __shared__ __attribute__((aligned(16))) double S[];  // att
-  const int b = blockIdx.y;
-  const double* xb = xbar + (int64_t)b * (C + 1);
+constexpr int kFinishRows = 8;  // rows of Wk per wavefront pass (independent loads in flight)
+
+__device__ void key_projection_lds(const KeyProj& kp, int64_t b, int C, int H, int Cp, int Hp, double* S, double* U,
+                                   double* v) {
+  const double* xb = kp.xbar + b * (C + 1);
+  const int att = kp.att;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  for (int d = wv; d < att; d += kWavesPerBlock) {
-    double s = 0.0;
-    for (int c = lane; c < C; c += kWave) s = fma((double)Wk[(int64_t)d * C + c], xb[c], s);
-    s = wave_sum(s);
-    if (lane == 0) S[d] = s + xb[C] * (double)bk[d];
+  for (int d0 = wv * kFinishRows; d0 < att; d0 += kWavesPerBlock * kFinishRows) {
+    double sacc[kFinishRows];
+#pragma unroll
+    for (int j = 0; j < kFinishRows; ++j) sacc[j] = 0.0;
+    for (int c = lane; c < C; c += kWave) {
+      const double xv = xb[c];
+#pragma unroll
+      for (int j = 0; j < kFinishRows; ++j) {
+        const int d = min(d0 + j, att - 1);
+        sacc[j] = fma((double)kp.Wk[(int64_t)d * C + c], xv, sacc[j]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kFinishRows; ++j) {
+      const double t = wave_sum(sacc[j]);
+      if (lane == 0 && d0 + j < att) S[d0 + j] = t + xb[C] * (double)kp.bk[d0 + j];
+    }
   }
   __syncthreads();
   const int dk = att / H;
   const double inv = 1.0 / sqrt((double)dk);
-  const int t = blockIdx.x * kFinishPairs + threadIdx.x;
-  if (t < Cp * Hp) {
-    const int c = t / Hp, h = t - c * Hp;
-    double s = 0.0;
-    if (c < C && h < H)
-      for (int d = h * dk; d < (h + 1) * dk; ++d) s = fma((double)Wq[(int64_t)d * C + c], S[d], s);
-    U[(int64_t)b * Cp * Hp + t] = s * inv;
+  // pair t -> (h = t / Cp, c = t % Cp): consecutive threads read consecutive Wq columns
+  for (int t = threadIdx.x; t < Cp * Hp; t += blockDim.x) {
+    const int h = t / Cp, c = t - h * Cp;
+    double a = 0.0;
+    if (c < C && h < H) {
+#pragma unroll 16
+      for (int d = h * dk; d < (h + 1) * dk; ++d) a = fma((double)kp.Wq[(int64_t)d * C + c], S[d], a);
+    }
+    U[c * Hp + h] = a * inv;
   }
-  if (blockIdx.x == 0 && threadIdx.x < Hp) {
+  if (threadIdx.x < Hp) {
     const int h = threadIdx.x;
-    double s = 0.0;
+    double a = 0.0;
     if (h < H)
-      for (int d = h * dk; d < (h + 1) * dk; ++d) s = fma((double)bq[d], S[d], s);
-    v[(int64_t)b * Hp + h] = s * inv;
+      for (int d = h * dk; d < (h + 1) * dk; ++d) a = fma((double)kp.bq[d], S[d], a);
+    v[h] = a * inv;
   }
+  __syncthreads();
 }
 
 // cs[b*N+n, h] = x_{b,n} . U[b,:,h] + v[b,h]  (fp64 accumulation).
@@ -473,9 +503,9 @@ __device__ __forceinline__ void ns_rows_resident(const float* __restrict__ xb, c
 
 template <int VEC, int GL, int MAXH>
 __global__ __launch_bounds__(256) void node_scores_kernel(const float* __restrict__ x, int64_t B, int64_t N, int C,
-                                                           int64_t ldx, int H, int nch, const double* __restrict__ U,
-                                                           const double* __restrict__ v, double* __restrict__ cs,
-                                                           int64_t rows_per_block) {
+                                                           int64_t ldx, int H, int nch, KeyProj kp,
+                                                           double* __restrict__ cs, int64_t rows_per_block) {
+  extern __shared__ __attribute__((aligned(16))) double ns_lds[];  // S[att_pad] | U[Cp][MAXH] | v[MAXH]
   constexpr int G = kWave / GL;
   constexpr int NPV = node_scores_npv<MAXH>();
   constexpr int NP = NPV / VEC;
@@ -487,13 +517,18 @@ __global__ __launch_bounds__(256) void node_scores_kernel(const float* __restric
   const int64_t n1 = min(N, n0 + rows_per_block);
   const int64_t step = (int64_t)kWavesPerBlock * G;
   const bool ragged = C != nch * CW;
+  const int Cp = nch * CW;
+  double* S = ns_lds;
+  double* Ub = ns_lds + ((kp.att + 1) & ~1);
+  double* vl = Ub + Cp * MAXH;
   for (int64_t b = blockIdx.y; b < B; b += gridDim.y) {
-    const double* __restrict__ Ub = U + b * nch * CW * MAXH;
+    if (b != blockIdx.y) __syncthreads();  // the previous element's U is no longer read
+    key_projection_lds(kp, b, C, H, Cp, MAXH, S, Ub, vl);
     const float* __restrict__ xb = x + b * N * ldx;
     const __amdgpu_buffer_rsrc_t rcs = buf_rsrc(cs + b * N * H);
     double vb[MAXH];
 #pragma unroll
-    for (int h = 0; h < MAXH; ++h) vb[h] = v[b * MAXH + h];
+    for (int h = 0; h < MAXH; ++h) vb[h] = vl[h];
     if (nch == 1) {
       if (ragged)
         ns_rows_resident<VEC, GL, MAXH, true>(xb, Ub, vb, rcs, N, n0, n1, C, ldx, H, g, gl, wv);
@@ -526,7 +561,7 @@ static int pow2_at_least(int v, int cap) {
   return p;
 }
 
-constexpr int kKeysumTilesTarget = 512;
+constexpr int kKeysumTilesTarget = 1024;
 
 static int keysum_vec(int64_t C, const float* x, int64_t ldx) {
   if (C % 4 == 0 && ldx % 4 == 0 && aligned16(x)) return 4;
@@ -568,30 +603,35 @@ static NsGeom ns_geometry(int vec, int64_t C, int64_t H) {
   return g;
 }
 
+static size_t ns_lds_bytes(const NsGeom& ge, int att) {
+  return sizeof(double) * (size_t)(((att + 1) & ~1) + (int64_t)ge.nch * ge.CW * ge.maxh + ge.maxh);
+}
+
 template <int VEC, int MAXH>
 static void launch_node_scores(dim3 grid, const NsGeom& ge, hipStream_t s, const float* x, int64_t B, int64_t N, int C,
-                               int64_t ldx, int H, const double* U, const double* v, double* cs, int64_t rpb) {
+                               int64_t ldx, int H, const KeyProj& kp, double* cs, int64_t rpb) {
   const int n = ge.nch;
+  const size_t shm = ns_lds_bytes(ge, kp.att);
   if (ge.GL <= 8)
-    node_scores_kernel<VEC, 8, MAXH><<<grid, kBlock, 0, s>>>(x, B, N, C, ldx, H, n, U, v, cs, rpb);
+    node_scores_kernel<VEC, 8, MAXH><<<grid, kBlock, shm, s>>>(x, B, N, C, ldx, H, n, kp, cs, rpb);
   else if (ge.GL <= 16)
-    node_scores_kernel<VEC, 16, MAXH><<<grid, kBlock, 0, s>>>(x, B, N, C, ldx, H, n, U, v, cs, rpb);
+    node_scores_kernel<VEC, 16, MAXH><<<grid, kBlock, shm, s>>>(x, B, N, C, ldx, H, n, kp, cs, rpb);
   else if (ge.GL <= 32)
-    node_scores_kernel<VEC, 32, MAXH><<<grid, kBlock, 0, s>>>(x, B, N, C, ldx, H, n, U, v, cs, rpb);
+    node_scores_kernel<VEC, 32, MAXH><<<grid, kBlock, shm, s>>>(x, B, N, C, ldx, H, n, kp, cs, rpb);
   else
-    node_scores_kernel<VEC, 64, MAXH><<<grid, kBlock, 0, s>>>(x, B, N, C, ldx, H, n, U, v, cs, rpb);
+    node_scores_kernel<VEC, 64, MAXH><<<grid, kBlock, shm, s>>>(x, B, N, C, ldx, H, n, kp, cs, rpb);
 }
 
 // rows per block sized for ~4096 wavefronts over the whole launch (16 per CU)
 static void launch_node_scores_any(hipStream_t s, const NsGeom& ge, const float* x, int64_t B, int64_t N, int C,
-                                   int64_t ldx, int H, const double* U, const double* v, double* cs) {
+                                   int64_t ldx, int H, const KeyProj& kp, double* cs) {
   const int G = kWave / ge.GL;
   const int64_t groups = ceil_div(N, (int64_t)G);
   const int64_t waves_per_batch = std::max<int64_t>(1, 4096 / B);
   const int64_t iters = std::max<int64_t>(1, ceil_div(groups, waves_per_batch));
   const int64_t rpb = (int64_t)kWavesPerBlock * G * iters;
   const dim3 grid((unsigned)ceil_div(N, rpb), (unsigned)std::min<int64_t>(B, 65535));
-#define GNPDE_NS(V, M) launch_node_scores<V, M>(grid, ge, s, x, B, N, C, ldx, H, U, v, cs, rpb)
+#define GNPDE_NS(V, M) launch_node_scores<V, M>(grid, ge, s, x, B, N, C, ldx, H, kp, cs, rpb)
   if (ge.vec == 4) {
     switch (ge.maxh) {
       case 1: GNPDE_NS(4, 1); break;
@@ -637,6 +677,26 @@ int gnpde_spmm_rhs_f32(const int32_t* items, int64_t n_items, const int32_t* hea
   GNPDE_REQUIRE(n_items >= 0 && n_items < INT32_MAX && n_heavy >= 0, GNPDE_EINVAL, "spmm_rhs: bad item counts");
   GNPDE_REQUIRE(n_items == 0 || (items && col && w), GNPDE_EINVAL, "spmm_rhs: NULL plan/col/w");
   PlainWeights wp{w};
+  return launch_agg(items, n_items, heavy, n_heavy, col, wp, C, ep, partials, as_stream(stream));
+}
+
+int gnpde_attn_ref_rhs_f32(const int32_t* items, int64_t n_items, const int32_t* heavy, int64_t n_heavy,
+                           const int32_t* col, const double* cs, const double* m, const float* rl, int64_t heads,
+                           int64_t C, const float* x, int64_t ldx, const float* x0, int64_t ldx0, const float* alpha,
+                           const float* beta, int flags, float* f, int64_t ldf, float* partials,
+                           const gnpde_stage_epilogue_t* stage, void* stream) {
+  const Epi ep = make_epi(x, ldx, x0, ldx0, alpha, beta, flags, f, ldf, stage);
+  int rc = check_epi(ep, C, n_heavy, partials);
+  if (rc) return rc;
+  GNPDE_REQUIRE(heads >= 1 && heads <= 16, GNPDE_EUNSUPPORTED, "attn_ref_rhs: heads=%lld not in [1,16]",
+                (long long)heads);
+  GNPDE_REQUIRE(n_items >= 0 && n_items < INT32_MAX && n_heavy >= 0, GNPDE_EINVAL, "attn_ref_rhs: bad item counts");
+  GNPDE_REQUIRE(n_items == 0 || (items && col && cs && m && rl), GNPDE_EINVAL, "attn_ref_rhs: NULL plan/col/cs/m/rl");
+  if (heads <= 2) {
+    RefDstSoftmaxWeights<2> wp{cs, m, rl, (int)heads};
+    return launch_agg(items, n_items, heavy, n_heavy, col, wp, C, ep, partials, as_stream(stream));
+  }
+  RefDstSoftmaxWeights<0> wp{cs, m, rl, (int)heads};
   return launch_agg(items, n_items, heavy, n_heavy, col, wp, C, ep, partials, as_stream(stream));
 }
 
@@ -724,9 +784,7 @@ size_t gnpde_keysum_workspace_bytes(int64_t B, int64_t N, int64_t C, int64_t att
   (void)att;
   int rpt, ntiles;
   keysum_tiles(B, N, &rpt, &ntiles);
-  const int64_t H = 16;                                // upper bound on heads (padded Hp <= 16)
-  const int64_t Cp = std::max<int64_t>(256, 2 * C);    // >= the padded U rows of ns_geometry
-  return sizeof(double) * (size_t)(B * ntiles * (C + 1) + B * (C + 1) + B * Cp * H + B * H) + 256;
+  return sizeof(double) * (size_t)(B * ntiles * (C + 1) + B * (C + 1)) + 256;
 }
 
 int gnpde_ref_scores_f32(const float* x, int64_t B, int64_t N, int64_t C, int64_t ldx, const int32_t* indeg,
@@ -738,7 +796,7 @@ int gnpde_ref_scores_f32(const float* x, int64_t B, int64_t N, int64_t C, int64_
                 "ref_scores: heads must divide attention_dim and be <= 16");
   GNPDE_REQUIRE(workspace_bytes >= gnpde_keysum_workspace_bytes(B, N, C, att), GNPDE_EINVAL,
                 "ref_scores: workspace too small");
-  GNPDE_REQUIRE(att <= 8192, GNPDE_EUNSUPPORTED, "ref_scores: attention_dim too large");
+  GNPDE_REQUIRE(att <= 4096, GNPDE_EUNSUPPORTED, "ref_scores: attention_dim too large");
   GNPDE_REQUIRE((uint64_t)N * heads * 8 < kBufRecords, GNPDE_EUNSUPPORTED, "ref_scores: N*heads too large");
   hipStream_t s = as_stream(stream);
   const int vec = keysum_vec(C, x, ldx);
@@ -748,11 +806,9 @@ int gnpde_ref_scores_f32(const float* x, int64_t B, int64_t N, int64_t C, int64_
   double* part = static_cast<double*>(workspace);
   double* xbar = part + B * ntiles * (C + 1);
   const NsGeom ge = ns_geometry(vec, C, heads);
-  const int64_t Cp = (int64_t)ge.nch * ge.CW, Hp = ge.maxh;
-  double* U = xbar + B * (C + 1);
-  double* v = U + B * Cp * Hp;
-  GNPDE_REQUIRE((size_t)((char*)(v + B * Hp) - (char*)workspace) <= workspace_bytes, GNPDE_EUNSUPPORTED,
-                "ref_scores: padded U does not fit the workspace");
+  GNPDE_REQUIRE(ns_lds_bytes(ge, (int)att) <= 64 * 1024, GNPDE_EUNSUPPORTED,
+                "ref_scores: key projection (attention_dim %lld, C %lld) does not fit the LDS", (long long)att,
+                (long long)C);
   const int rpb = kBlock / tpr;
   const size_t shm = sizeof(double) * (size_t)rpb * (C + 1);
   GNPDE_REQUIRE(shm <= 64 * 1024, GNPDE_EUNSUPPORTED, "ref_scores: C too large");
@@ -764,13 +820,11 @@ int gnpde_ref_scores_f32(const float* x, int64_t B, int64_t N, int64_t C, int64_
   else
     keysum_partial_kernel<1><<<g1, kBlock, shm, s>>>(x, N, (int)C, ldx, indeg, rpt, tpr, ntiles, part);
   GNPDE_LAUNCH_CHECK();
-  keysum_tiles_kernel<<<dim3((unsigned)ceil_div(C + 1, 16), (unsigned)B), kBlock, 0, s>>>(part, ntiles, (int)C, xbar);
+  keysum_tiles_kernel<<<dim3((unsigned)ceil_div(C + 1, kTileCols), (unsigned)B), kBlock, 0, s>>>(part, ntiles, (int)C,
+                                                                                                 xbar);
   GNPDE_LAUNCH_CHECK();
-  keysum_finish_kernel<<<dim3((unsigned)ceil_div(Cp * Hp, kFinishPairs), (unsigned)B), kBlock,
-                         sizeof(double) * (size_t)att, s>>>(xbar, (int)C, Wq, bq, Wk, bk, (int)att, (int)heads,
-                                                            (int)Cp, (int)Hp, U, v);
-  GNPDE_LAUNCH_CHECK();
-  launch_node_scores_any(s, ge, x, B, N, (int)C, ldx, (int)heads, U, v, cs);
+  const KeyProj kp{xbar, Wq, bq, Wk, bk, (int)att};
+  launch_node_scores_any(s, ge, x, B, N, (int)C, ldx, (int)heads, kp, cs);
   GNPDE_LAUNCH_CHECK();
   return GNPDE_OK;
 }

@@ -377,10 +377,26 @@ def spmm_rhs(g, w_csr, x, x0=None, alpha=None, beta=None, rhs=True, alpha_sigmoi
     grouped = g.csc if transpose else g.csr
     plan = grouped.plan
     partials = torch.empty(plan.n_slots * C, dtype=torch.float32, device=dev) if plan.n_slots else None
-    _lib.call("gnpde_spmm_rhs_f32", _ptr(plan.items), plan.n_items, _ptr(plan.heavy), plan.n_heavy, _ptr(grouped.col),
-              _ptr(w_csr), C, _ptr(xr), C, _ptr(x0r), C, _ptr(a), _ptr(b), _flags(rhs, alpha_sigmoid, add_source),
-              _ptr(out), C, _ptr(partials), st, _stream(dev))
+    epi = (C, _ptr(xr), C, _ptr(x0r), C, _ptr(a), _ptr(b), _flags(rhs, alpha_sigmoid, add_source), _ptr(out), C,
+           _ptr(partials), st, _stream(dev))
+    if isinstance(w_csr, RefDstWeights):
+        if transpose:
+            raise ValueError("on-the-fly attention weights aggregate over the CSR only")
+        _lib.call("gnpde_attn_ref_rhs_f32", _ptr(plan.items), plan.n_items, _ptr(plan.heavy), plan.n_heavy,
+                  _ptr(grouped.col), _ptr(w_csr.cs), _ptr(w_csr.m), _ptr(w_csr.rl), w_csr.heads, *epi)
+    else:
+        _lib.call("gnpde_spmm_rhs_f32", _ptr(plan.items), plan.n_items, _ptr(plan.heavy), plan.n_heavy,
+                  _ptr(grouped.col), _ptr(w_csr), *epi)
     return None if stage is not None else out.view(shape)
+
+
+class RefDstWeights(object):
+    """Weights K1 computes on the fly (gnpde_attn_ref_rhs_f32): the fork's
+    scaled_dot under destination-grouped softmax, head-mean per edge from the
+    node scores cs [R,h] and the CSC statistics m [R,h], rl [R,h]."""
+
+    def __init__(self, cs, m, rl, heads):
+        self.cs, self.m, self.rl, self.heads = cs, m, rl, int(heads)
 
 
 def spmm_rhs_rows(g, plan, w_csr, x_src, x_rows, row0, x0=None, alpha=None, beta=None, alpha_sigmoid=True,
@@ -565,9 +581,17 @@ def attn_weights(g, ns, m, rl, norm_idx, seg=True):
 
 
 def attn_rhs(g, ns, m, rl, norm_idx, x, x0=None, alpha=None, beta=None, rhs=True, alpha_sigmoid=True,
-             add_source=False, out=None, stage=None, seg=True):
+             add_source=False, out=None, stage=None, seg=True, fuse=True):
     """K2 + K1: f = a*(A_att x - x) [+ b x0], A_att = head-mean softmax weights
-    (m, rl: destination statistics for norm_idx 1, or None to compute them)."""
+    (m, rl: destination statistics for norm_idx 1, or None to compute them).
+    Reference scores under norm_idx 1 (fuse=True): the weights are computed
+    inside K1 from (cs, m, rl) — same bits as the separate weights pass."""
+    if fuse and norm_idx == 1 and ns.mode == _lib.SCORE_REFERENCE:
+        if m is None:
+            m, rl = softmax_stats(g, ns, 1, seg=seg)
+        w = RefDstWeights(ns.cs, m, rl, ns.heads)
+        return spmm_rhs(g, w, x, x0=x0, alpha=alpha, beta=beta, rhs=rhs, alpha_sigmoid=alpha_sigmoid,
+                        add_source=add_source, out=out, stage=stage)
     w = attn_weights(g, ns, m, rl, norm_idx, seg=seg)
     return spmm_rhs(g, w, x, x0=x0, alpha=alpha, beta=beta, rhs=rhs, alpha_sigmoid=alpha_sigmoid,
                     add_source=add_source, out=out, stage=stage)

@@ -174,6 +174,20 @@ int gnpde_spmm_rhs_f32(const int32_t* items, int64_t n_items, const int32_t* hea
                        float* f, int64_t ldf, float* partials, const gnpde_stage_epilogue_t* stage,
                        void* stream);
 
+/* K1 with the attention weights computed on the fly for the fork's scaled_dot
+ * (reference score mode) under destination-grouped softmax (attention_norm_idx
+ * 1): w_p = mean_h exp(cs[row,h] - m[col_p,h]) * rl[col_p,h], cs [R,H] fp64 node
+ * scores (gnpde_ref_scores_f32), m [R,H] fp64 / rl [R,H] group statistics
+ * (gnpde_softmax_stats_f32 / gnpde_seg_softmax_f32 over the CSC).  Equals
+ * gnpde_attn_weights_f32 + gnpde_spmm_rhs_f32 bit for bit, in one pass:
+ * ODEFuncTransformerAtt.forward, function_transformer_attention.py:44-59.
+ * Other arguments as gnpde_spmm_rhs_f32.                                     */
+int gnpde_attn_ref_rhs_f32(const int32_t* items, int64_t n_items, const int32_t* heavy, int64_t n_heavy,
+                           const int32_t* col, const double* cs, const double* m, const float* rl, int64_t heads,
+                           int64_t C, const float* x, int64_t ldx, const float* x0, int64_t ldx0, const float* alpha,
+                           const float* beta, int flags, float* f, int64_t ldf, float* partials,
+                           const gnpde_stage_epilogue_t* stage, void* stream);
+
 /* ---------------------------------------------------------------- attention
  * Node-level projection (MFMA, v_mfma_f32_32x32x2_f32):
  *   out[r, j] = sum_k x[r,k] * W[j,k] + bias[j], j < Nout; columns [0, split)
@@ -186,7 +200,10 @@ int gnpde_linear_f32(const float* x, int64_t R, int64_t K, int64_t ldx, const fl
 /* Reference-mode node scores (fork scaled_dot, function_transformer_attention.py:249):
  *   S_b = Wk * (sum_n indeg(n) x_n) + (sum_n indeg(n)) bk    (fp64)
  *   cs[r,h] = (q_r,h . S_b,h) / sqrt(dk),  q = Wq x + bq      (fp64 out)
- * indeg: in-degree per global node (int32, R); ws: gnpde_keysum_workspace_bytes.  */
+ * indeg: in-degree per global node (int32, R); ws: gnpde_keysum_workspace_bytes.
+ * Three launches: indegree-weighted column sums (fp64 row tiles), the fixed-order
+ * tile reduction, then the node scores, whose workgroups each form S_b and
+ * U = Wq^T S / sqrt(dk) in LDS.  attention_dim <= 4096.                      */
 size_t gnpde_keysum_workspace_bytes(int64_t B, int64_t N, int64_t C, int64_t att);
 int gnpde_ref_scores_f32(const float* x, int64_t B, int64_t N, int64_t C, int64_t ldx, const int32_t* indeg,
                          const float* Wq, const float* bq, const float* Wk, const float* bk,

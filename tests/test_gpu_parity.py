@@ -322,6 +322,9 @@ def test_seg_softmax_reference_norm1(heads, att):
     f = ops.attn_rhs(g, ns, m, rl, 1, T(x), alpha=torch.tensor(0.25, device=DEV))
     want = O.transformer_rhs(ei, x, None, Wq, bq, Wk, bk, heads, 1, 0.25, 0.0)
     assert rel(f, want) <= RTOL
+    # weights computed inside K1 (gnpde_attn_ref_rhs_f32) == separate weights pass + K1, bit for bit
+    f_unfused = ops.attn_rhs(g, ns, m, rl, 1, T(x), alpha=torch.tensor(0.25, device=DEV), fuse=False)
+    assert torch.equal(f, f_unfused)
 
 
 @pytest.mark.parametrize("attention_type", ["exp_kernel", "cosine_sim", "pearson"])
