@@ -9,6 +9,9 @@
 // the MFMA: half h covers k in [h*Kh, h*Kh + Kh), Kh = ceil(K/2), so each lane
 // streams a contiguous run of its own x row (16-byte loads when K % 8 == 0).
 // W^T for the slice is staged once per workgroup in LDS as [k][64 columns].
+#include <algorithm>
+#include <cstdlib>
+
 #include "common.hpp"
 
 namespace gnpde {
@@ -46,6 +49,32 @@ __device__ __forceinline__ void lin_load_chunk(const float* __restrict__ xr, int
   }
 }
 
+// Stage W^T for the 64-column slice at col0 into LDS [2*Khp][65]: wave wv
+// fills columns j = wv + 4*jj, lanes walk the k rows (coalesced along k).
+// Buffer loads with 32-bit offsets: a padding element (k past the half, n past
+// Nout) gets an out-of-range offset and reads 0, so all kLinStageCols loads
+// issue back to back with no branch or 64-bit select.
+__device__ __forceinline__ void lin_stage_wt(const float* __restrict__ W, int K, int Nout, int Kh, int Khp, int col0,
+                                             int lane, int wv, float* __restrict__ wt) {
+  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(W), 0, Nout * K * (int)sizeof(float), 0x00020000);
+  for (int kr = lane; kr < 2 * Khp; kr += kWave) {
+    const int hh = kr >= Khp ? 1 : 0;
+    const int sidx = kr - hh * Khp;
+    const int k = hh * Kh + sidx;
+    const bool kok = sidx < Kh && k < K;
+    float val[kLinStageCols];
+#pragma unroll
+    for (int jj = 0; jj < kLinStageCols; ++jj) {
+      const int n = col0 + wv + kWavesPerBlock * jj;
+      const int off = (kok && n < Nout) ? (n * K + k) * (int)sizeof(float) : kOutOfRange;
+      val[jj] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(wr, off, 0, 0));
+    }
+#pragma unroll
+    for (int jj = 0; jj < kLinStageCols; ++jj) wt[kr * kLinLdsStride + wv + kWavesPerBlock * jj] = val[jj];
+  }
+}
+
 // K split between the MFMA lane halves: half h covers k = h*Kh + s, s < Kh.
 // The LDS image of W^T has Khp = roundup(Kh, kLinChunk) rows per half (zero
 // padded), so the MFMA loop runs whole chunks with no per-step guard.
@@ -72,29 +101,7 @@ __global__ __launch_bounds__(256) void linear_mfma_kernel(const float* __restric
   float a_cur[kLinChunk], a_nxt[kLinChunk];
   lin_load_chunk<VEC4>(xr, kbase, 0, Kh, K, a_cur);
 
-  // Stage W^T: wave wv fills columns j = wv + 4*jj, lanes walk the k rows
-  // (coalesced along k).  Buffer loads with 32-bit offsets: a padding element
-  // (k past the half, n past Nout) gets an out-of-range offset and reads 0, so
-  // all kLinStageCols loads issue back to back with no branch or 64-bit select.
-  {
-    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(W), 0, Nout * K * (int)sizeof(float), 0x00020000);
-    for (int kr = lane; kr < 2 * Khp; kr += kWave) {
-      const int hh = kr >= Khp ? 1 : 0;
-      const int sidx = kr - hh * Khp;
-      const int k = hh * Kh + sidx;
-      const bool kok = sidx < Kh && k < K;
-      float val[kLinStageCols];
-#pragma unroll
-      for (int jj = 0; jj < kLinStageCols; ++jj) {
-        const int n = col0 + wv + kWavesPerBlock * jj;
-        const int off = (kok && n < Nout) ? (n * K + k) * (int)sizeof(float) : kOutOfRange;
-        val[jj] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(wr, off, 0, 0));
-      }
-#pragma unroll
-      for (int jj = 0; jj < kLinStageCols; ++jj) wt[kr * kLinLdsStride + wv + kWavesPerBlock * jj] = val[jj];
-    }
-  }
+  lin_stage_wt(W, K, Nout, Kh, Khp, col0, lane, wv, wt);
   __syncthreads();
   // Explicit: the loop head then sees no pending load, so the compiler's merge
   // there does not make every chunk wait for the next chunk's prefetch.
@@ -161,9 +168,121 @@ __global__ __launch_bounds__(256) void linear_mfma_kernel(const float* __restric
   }
 }
 
+
+// Persistent variant for K <= 2*16*NCH, K % 8 == 0 (the usual attention widths): each
+// workgroup stages its W^T slice ONCE and its wavefronts walk 32-row tiles
+// (tile, tile + 4*gridDim.x, ...).  x of the current tile sits in registers
+// (NCH*16 values per lane); as soon as chunk c has gone through the MFMAs its
+// registers are reloaded with chunk c of the NEXT tile, so every load has
+// (NCH - 1) chunks of matrix work to arrive in, with one x buffer.
+template <bool VEC4, int NCH>
+__global__ __launch_bounds__(256, 2) void linear_mfma_tiles_kernel(const float* __restrict__ x, int R, int K,
+                                                                    int64_t ldx, const float* __restrict__ W,
+                                                                    const float* __restrict__ bias, int Nout,
+                                                                    int split, float* __restrict__ out_a,
+                                                                    int64_t lda, float* __restrict__ out_b,
+                                                                    int64_t ldb) {
+  constexpr int KS = NCH * kLinChunk;  // k-steps per half (Khp)
+  extern __shared__ __attribute__((aligned(16))) float wt[];  // [2*KS][65]
+  const int Kh = (K + 1) >> 1;
+  const int col0 = blockIdx.y * kLinCols;
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const int r32 = lane & 31, h = lane >> 5;
+  const int kbase = h * Kh;
+  const int ntiles = (R + kLinRowsPerWave - 1) / kLinRowsPerWave;
+  const int step = gridDim.x * kWavesPerBlock;
+  int tile = blockIdx.x * kWavesPerBlock + wv;
+
+  // the wave's first tile goes out before the W^T staging
+  float a[NCH][kLinChunk];
+  {
+    const float* __restrict__ xr = x + (int64_t)min(min(tile, ntiles - 1) * kLinRowsPerWave + r32, R - 1) * ldx;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) lin_load_chunk<VEC4>(xr, kbase, c * kLinChunk, Kh, K, a[c]);
+  }
+  lin_stage_wt(W, K, Nout, Kh, KS, col0, lane, wv, wt);
+  __syncthreads();
+  if (tile >= ntiles) return;
+
+  // per-lane epilogue constants (one output column per accumulator tile)
+  float bv[2];
+  float* dst[2];
+  int64_t ld[2];
+#pragma unroll
+  for (int tt = 0; tt < 2; ++tt) {
+    const int n = col0 + tt * 32 + r32;
+    const int nc = n < Nout ? n : 0;
+    const float bb = bias ? bias[nc] : 0.f;
+    bv[tt] = n < Nout ? bb : 0.f;
+    const bool to_a = n < split;
+    dst[tt] = to_a ? out_a + nc : out_b + (nc - split);
+    ld[tt] = to_a ? lda : ldb;
+  }
+  const bool cols_full = col0 + kLinCols <= Nout;
+  const float* __restrict__ wbase = wt + h * KS * kLinLdsStride;
+
+  for (; tile < ntiles; tile += step) {
+    // next tile (clamped: the last iteration re-reads a valid row, no branch)
+    const int nt = min(tile + step, ntiles - 1);
+    const float* __restrict__ xn = x + (int64_t)min(nt * kLinRowsPerWave + r32, R - 1) * ldx;
+    f32x16 acc0 = {0}, acc1 = {0};
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      float b0[kLinChunk], b1[kLinChunk];
+#pragma unroll
+      for (int i = 0; i < kLinChunk; ++i) {
+        const float* wrow = wbase + (c * kLinChunk + i) * kLinLdsStride;
+        b0[i] = wrow[r32];
+        b1[i] = wrow[32 + r32];
+      }
+#pragma unroll
+      for (int i = 0; i < kLinChunk; ++i) {
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[c][i], b0[i], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[c][i], b1[i], acc1, 0, 0, 0);
+      }
+      lin_load_chunk<VEC4>(xn, kbase, c * kLinChunk, Kh, K, a[c]);
+      // keep chunks in program order: hoisting later chunks' LDS reads (or the
+      // next tile's loads into fresh registers) would spill
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // C/D layout (32x32): col = lane&31, row = (reg&3) + 8*(reg>>2) + 4*(lane>>5)
+    const int row0 = tile * kLinRowsPerWave;
+    if (row0 + kLinRowsPerWave <= R && cols_full) {
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const int row = row0 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+        dst[0][(int64_t)row * ld[0]] = acc0[reg] + bv[0];
+        dst[1][(int64_t)row * ld[1]] = acc1[reg] + bv[1];
+      }
+    } else {
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt) {
+        const int n = col0 + tt * 32 + r32;
+        if (n >= Nout) continue;
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+          const int row = row0 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+          if (row < R) dst[tt][(int64_t)row * ld[tt]] = (tt == 0 ? acc0[reg] : acc1[reg]) + bv[tt];
+        }
+      }
+    }
+  }
+}
+
 }  // namespace gnpde
 
 using namespace gnpde;
+
+// Experiment knob (not part of the ABI contract): GNPDE_LINEAR=1 forces the
+// per-tile (non-persistent) projection kernel.
+static int linear_variant() {
+  static const int v = [] {
+    const char* e = std::getenv("GNPDE_LINEAR");
+    return e ? std::atoi(e) : 0;
+  }();
+  return v;
+}
 
 extern "C" int gnpde_linear_f32(const float* x, int64_t R, int64_t K, int64_t ldx, const float* W, const float* bias,
                                 int64_t Nout, int64_t split, float* out_a, int64_t lda, float* out_b, int64_t ldb,
@@ -180,9 +299,33 @@ extern "C" int gnpde_linear_f32(const float* x, int64_t R, int64_t K, int64_t ld
   GNPDE_REQUIRE(shm <= 160 * 1024, GNPDE_EUNSUPPORTED, "linear: K=%lld too large for the LDS slice",
                 (long long)K);
   if (R == 0) return GNPDE_OK;
-  const dim3 grid((unsigned)ceil_div(R, kWavesPerBlock * kLinRowsPerWave), (unsigned)ceil_div(Nout, kLinCols));
   const bool vec4 = (K % 8 == 0) && (ldx % 4 == 0) && aligned16(x);
   hipStream_t s = as_stream(stream);
+  const int nch = (int)(Khp / kLinChunk);
+  if (vec4 && nch <= 6 && linear_variant() == 0) {
+    // persistent tiles: about 2 workgroups per CU, tiles spread evenly over the wavefronts
+    const int64_t ntiles = ceil_div(R, kLinRowsPerWave);
+    const int64_t slices = ceil_div(Nout, kLinCols);
+    const int64_t max_waves = std::max<int64_t>(kWavesPerBlock, 2048 / slices);
+    const int64_t per_wave = ceil_div(ntiles, max_waves);
+    const int64_t blocks = ceil_div(ceil_div(ntiles, per_wave), kWavesPerBlock);
+    const dim3 gt((unsigned)blocks, (unsigned)slices);
+#define GNPDE_LIN_T(N) \
+  linear_mfma_tiles_kernel<true, N><<<gt, kBlock, shm, s>>>(x, (int)R, (int)K, ldx, W, bias, (int)Nout, (int)split, \
+                                                             out_a, lda, out_b, ldb)
+    switch (nch) {
+      case 1: GNPDE_LIN_T(1); break;
+      case 2: GNPDE_LIN_T(2); break;
+      case 3: GNPDE_LIN_T(3); break;
+      case 4: GNPDE_LIN_T(4); break;
+      case 5: GNPDE_LIN_T(5); break;
+      default: GNPDE_LIN_T(6); break;
+    }
+#undef GNPDE_LIN_T
+    GNPDE_LAUNCH_CHECK();
+    return GNPDE_OK;
+  }
+  const dim3 grid((unsigned)ceil_div(R, kWavesPerBlock * kLinRowsPerWave), (unsigned)ceil_div(Nout, kLinCols));
   if (vec4)
     linear_mfma_kernel<true><<<grid, kBlock, shm, s>>>(x, (int)R, (int)K, ldx, W, bias, (int)Nout, (int)split, out_a,
                                                       lda, out_b, ldb);

@@ -385,7 +385,10 @@ def test_attention_stage_epilogue(method, mode, norm_idx):
 
 # ---------------------------------------------------------------- MFMA projection
 @pytest.mark.parametrize("R,K,Nout,split", [(1, 4, 8, 4), (1000, 128, 64, 32), (5003, 80, 256, 128),
-                                            (777, 162, 64, 32), (64, 7, 33, 33), (4096, 256, 128, 64)])
+                                            (777, 162, 64, 32), (64, 7, 33, 33), (4096, 256, 128, 64),
+                                            # persistent-tile kernel: 1..6 chunks per half, ragged tiles/columns
+                                            (33, 8, 64, 32), (3001, 48, 96, 40), (100003, 96, 64, 32),
+                                            (169343, 128, 64, 32), (2049, 160, 130, 65), (999, 192, 64, 64)])
 def test_linear_mfma_vs_fp64(R, K, Nout, split):
     x = torch.randn(R, K, device=DEV)
     W = torch.randn(Nout, K, device=DEV) * 0.1
