@@ -120,18 +120,22 @@ def _fusable(func, y0, combine):
             y0.dtype == torch.float32 and not torch.is_grad_enabled())
 
 
-def _fused_step(method, func, t0, dt, t1, y0, ws):
+RHS_PER_STEP = {'euler': 1, 'midpoint': 2, 'rk4': 4}
+
+
+def _fused_step(method, func, t0, dt, t1, y0, ws, out=None):
     """One grid step with the stage combinations fused into the RHS epilogues
     (gnpde_stage_epilogue_t): same arithmetic as _fixed_step, ~7 fewer passes
-    over the state per rk4 step and no separate combine launches."""
+    over the state per rk4 step and no separate combine launches.  ``out``:
+    the buffer that receives y1 (default: a new tensor)."""
     y0 = y0.contiguous()
     if method == 'euler':
-        y1 = torch.empty_like(y0)
+        y1 = torch.empty_like(y0) if out is None else out
         func.rhs_stage(t0, y0, ops.Stage(outs=[(y1, y0, 1.0, dt, [])]))
         return y1
     if method == 'midpoint':
         ym = ws.get('a', y0)
-        y1 = torch.empty_like(y0)
+        y1 = torch.empty_like(y0) if out is None else out
         func.rhs_stage(t0, y0, ops.Stage(outs=[(ym, y0, 1.0, 0.5 * dt, [])]))
         func.rhs_stage(t0 + 0.5 * dt, ym, ops.Stage(outs=[(y1, y0, 1.0, dt, [])]))
         return y1
@@ -145,7 +149,7 @@ def _fused_step(method, func, t0, dt, t1, y0, ws):
         # 8 state passes per step besides the gathers (one write per stage,
         # reads of y, x2, y + x3), where storing k's and an accumulator takes 15.
         x2, x3, x4 = ws.get('a', y0), ws.get('b', y0), ws.get('c', y0)
-        y1 = torch.empty_like(y0)
+        y1 = torch.empty_like(y0) if out is None else out
         func.rhs_stage(t0, y0, ops.Stage(outs=[(x2, y0, 1.0, dt / 3.0, [])]))
         func.rhs_stage(t0 + dt / 3.0, x2, ops.Stage(outs=[(x3, x2, -1.0, dt, [(y0, 2.0)])]))
         func.rhs_stage(t0 + dt * 2.0 / 3.0, x3, ops.Stage(outs=[(x4, x3, -1.0, dt, [(x2, 2.0)])]))
@@ -163,7 +167,62 @@ class _Workspace(dict):
         return t
 
 
-def odeint_fixed(func, y0, t, method, step_size=None, combine=None):
+# Graph replay of fixed-grid steps (hipGraph through torch.cuda.CUDAGraph):
+# worth it once a few steps share one dt; capture itself costs host time.
+GRAPH_MIN_STEPS = 6
+# Set to a list to receive (start_event, end_event, n_rhs) per graph replay
+# (bench.py's per-launch roofline timing); None in normal use.
+replay_events = None
+
+
+class _StepGraphs(object):
+    """Two captured grid steps with a fixed dt, ping-ponging between two state
+    buffers (bufs[0] -> bufs[1] and back), so a step costs one hipGraphLaunch
+    and no copy of the state.  The RHS and its stage epilogues are the same
+    launches as the eager fused step (same kernels, same arguments, same bits).
+    Every per-graph structure (CSR, plans, cached weights) is built by the
+    eager step that precedes capture, so nothing synchronises inside it."""
+
+    def __init__(self, method, func, dt, like, ws):
+        self.bufs = [torch.empty_like(like, memory_format=torch.contiguous_format) for _ in range(2)]
+        self.graphs = []
+        self.n_rhs = RHS_PER_STEP[method]
+        pool = None
+        for i in range(2):
+            g = torch.cuda.CUDAGraph()
+            nfe = getattr(func, 'nfe', None)
+            with torch.cuda.graph(g, pool=pool):
+                _fused_step(method, func, 0.0, dt, dt, self.bufs[i], ws, out=self.bufs[1 - i])
+            if nfe is not None:
+                func.nfe = nfe  # capture records launches, it evaluates nothing
+            pool = g.pool()
+            self.graphs.append(g)
+
+    def step(self, func, i):
+        """Replay bufs[i] -> bufs[1-i]; counts the RHS evaluations like the eager calls."""
+        if hasattr(func, 'nfe'):
+            func.nfe += self.n_rhs
+        if replay_events is not None:
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            self.graphs[i].replay()
+            e.record()
+            replay_events.append((s, e, self.n_rhs))
+        else:
+            self.graphs[i].replay()
+        return self.bufs[1 - i]
+
+
+def _nfe_headroom(func, n):
+    """True when n more RHS calls cannot trip the MaxNFEException guard (the
+    eager path raises at the exact call, as the reference does)."""
+    opt = getattr(func, 'opt', None)
+    if not hasattr(func, 'nfe') or not isinstance(opt, dict) or 'max_nfe' not in opt:
+        return True
+    return func.nfe + n - 1 <= opt['max_nfe']
+
+
+def odeint_fixed(func, y0, t, method, step_size=None, combine=None, graph=None):
     combine = combine or _Combine()
     fused = _fusable(func, y0, combine)
     ws = _Workspace()
@@ -172,15 +231,31 @@ def odeint_fixed(func, y0, t, method, step_size=None, combine=None):
         raise AssertionError("time grid does not cover t")
     grid_h = [float(v) for v in grid.tolist()]
     t_h = [float(v) for v in t.tolist()]
+    steps = list(zip(grid_h[:-1], grid_h[1:]))
+    if graph is None:
+        graph = len(steps) >= GRAPH_MIN_STEPS
+    graphs = None
     solution = [y0]
     j = 1
     yc = y0
-    for ta, tb in zip(grid_h[:-1], grid_h[1:]):
+    for n, (ta, tb) in enumerate(steps):
         dt = tb - ta
-        y1 = _fused_step(method, func, ta, dt, tb, yc, ws) if fused else _fixed_step(method, func, ta, dt, tb, yc,
-                                                                                      combine)
+        if fused and graph and n >= 1 and graphs is None and dt == steps[0][1] - steps[0][0] and \
+                len(steps) - n >= 2:
+            graphs = (_StepGraphs(method, func, dt, yc, ws), dt)
+            graphs[0].bufs[0].copy_(yc)
+            gi = 0
+        if graphs is not None and dt == graphs[1] and _nfe_headroom(func, graphs[0].n_rhs):
+            y1 = graphs[0].step(func, gi)
+            gi = 1 - gi
+        elif fused:
+            y1 = _fused_step(method, func, ta, dt, tb, yc, ws)
+        else:
+            y1 = _fixed_step(method, func, ta, dt, tb, yc, combine)
         while j < len(t_h) and tb >= t_h[j]:
-            solution.append(_linear_interp(ta, tb, yc, y1, t_h[j]))
+            v = _linear_interp(ta, tb, yc, y1, t_h[j])
+            # graph buffers are overwritten by later replays
+            solution.append(v.clone() if graphs is not None and any(v is b for b in graphs[0].bufs) else v)
             j += 1
         yc = y1
     return torch.stack(solution, 0)
@@ -316,7 +391,7 @@ def odeint(func, y0, t, rtol=1e-7, atol=1e-9, method=None, options=None, combine
     if t.dim() != 1 or len(t) < 2:
         raise ValueError("t must be a 1-D tensor with at least two time points")
     if method in FIXED_METHODS:
-        return odeint_fixed(func, y0, t, method, options.get('step_size'), combine)
+        return odeint_fixed(func, y0, t, method, options.get('step_size'), combine, graph=options.get('gnpde_graph'))
     if method in ADAPTIVE_METHODS:
         solver = _Dopri5(func, y0, rtol, atol, combine, first_step=options.get('first_step'),
                          max_num_steps=options.get('max_num_steps', 2 ** 31 - 1),

@@ -770,3 +770,64 @@ def test_hard_attention_block_training_sampling_vs_oracle(norm_idx):
     z.sum().backward()
     assert xt.grad is not None and torch.isfinite(xt.grad).all()
     assert blk.odefunc.alpha_train.grad is not None
+
+
+# ---------------------------------------------------------------- hipGraph replay of fixed-grid steps
+@pytest.mark.parametrize("method", ["euler", "midpoint", "rk4"])
+def test_graph_replay_matches_eager_bitwise(method):
+    """odeint over many equal steps replays two captured steps (hipGraph); the
+    result, every requested time point and the nfe count equal the eager path's."""
+    N, E, C = 3000, 20000, 64
+    rng = np.random.default_rng(61)
+    ei = rng.integers(0, N, size=(1, 2, E))
+    ei[0, 0, :700] = 5  # hub row: the fixup kernel is captured too
+    x = T(rng.standard_normal((1, N, C)).astype(np.float32))
+    opt = dict(OPT, hidden_dim=C, add_source=True, max_nfe=10 ** 6)
+    eo, wo = _prep_oracle(ei, N)
+    outs = []
+    for graph in (False, True):
+        func = gnpde.LaplacianODEFunc(C, C, opt, DEV).to(DEV)
+        func.edge_index, func.edge_weight, func.x0 = T(eo), T(wo).float(), x.clone()
+        with torch.no_grad():
+            func.alpha_train.fill_(0.3)
+            func.beta_train.fill_(-0.2)
+            t = torch.tensor([0.0, 0.35, 1.0, 2.0], device=DEV)
+            z = gnpde.odeint(func, x, t, method=method, options={'step_size': 0.05, 'gnpde_graph': graph})
+        torch.cuda.synchronize()
+        outs.append((z, func.nfe))
+    (z0, n0), (z1, n1) = outs
+    assert n0 == n1 == 40 * {'euler': 1, 'midpoint': 2, 'rk4': 4}[method]
+    assert torch.equal(z0, z1)
+
+
+def test_graph_replay_attention_rhs_matches_eager():
+    """The transformer RHS (reference scores, norm_idx 1: key sum, node scores,
+    CSC statistics, fused-weight K1) replayed from a graph equals the eager run."""
+    N, E, C, h, att = 2000, 12000, 32, 2, 16
+    rng = np.random.default_rng(62)
+    ei = rng.integers(0, N, size=(1, 2, E))
+    x = T(rng.standard_normal((1, N, C)).astype(np.float32))
+    opt = dict(OPT, hidden_dim=C, heads=h, attention_dim=att, function='transformer', attention_norm_idx=1)
+    res = []
+    for graph in (False, True):
+        func = gnpde.ODEFuncTransformerAtt(C, C, opt, DEV).to(DEV)
+        _set_qk(func.multihead_att_layer, np.random.default_rng(63), C, att)
+        func.edge_index = T(ei)
+        with torch.no_grad():
+            z = gnpde.odeint(func, x, torch.tensor([0.0, 1.0], device=DEV), method='rk4',
+                             options={'step_size': 0.1, 'gnpde_graph': graph})
+        torch.cuda.synchronize()
+        res.append(z)
+    assert torch.equal(res[0], res[1])
+
+
+def test_graph_replay_respects_max_nfe():
+    N, E, C = 500, 3000, 16
+    rng = np.random.default_rng(64)
+    ei = rng.integers(0, N, size=(1, 2, E))
+    func = gnpde.LaplacianODEFunc(C, C, dict(OPT, hidden_dim=C, max_nfe=37), DEV).to(DEV)
+    func.edge_index, func.edge_weight = T(ei), T(rng.uniform(0, 1, (1, E)).astype(np.float32))
+    with torch.no_grad(), pytest.raises(gnpde.MaxNFEException):
+        gnpde.odeint(func, T(rng.standard_normal((1, N, C)).astype(np.float32)),
+                     torch.tensor([0.0, 5.0], device=DEV), method='rk4', options={'step_size': 0.1})
+    assert func.nfe == 38  # raised at the call after nfe passed max_nfe, as the eager reference does
