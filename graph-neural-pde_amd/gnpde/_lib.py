@@ -72,6 +72,13 @@ SIGNATURES = {
     "gnpde_seg_softmax_f32": (_int, [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _int, _int, _int, _i64, _i64,
                                      _vp, _vp, _vp, _i64, _f32, _f32, _vp, _vp, _vp, _vp, _vp]),
     "gnpde_csr_rowidx": (_int, [_vp, _i64, _i64, _vp, _vp]),
+    "gnpde_sddmm_f32": (_int, [_vp, _vp, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _vp, _int, _int, _vp, _vp]),
+    "gnpde_softmax_backward_f32": (_int, [_vp, _vp, _i64, _i64, _int, _vp, _vp, _vp, _vp]),
+    "gnpde_segment_sum_f64": (_int, [_vp, _vp, _i64, _i64, _int, _vp, _vp, _vp]),
+    "gnpde_wcolsum_workspace_bytes": (_size, [_i64, _i64, _i64, _int]),
+    "gnpde_wcolsum_f64": (_int, [_vp, _i64, _i64, _i64, _i64, _vp, _int, _vp, _vp, _size, _vp]),
+    "gnpde_score_input_grad_f32": (_int, [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _int, _vp, _i64, _int, _vp]),
+    "gnpde_gather_head_f32": (_int, [_vp, _i64, _int, _int, _vp, _f32, _vp, _vp]),
     "gnpde_rk_combine_f32": (_int, [_i64, _vp, _int, ctypes.POINTER(_vp), ctypes.POINTER(_f64), _f64, _vp, _vp]),
 }
 

@@ -83,7 +83,9 @@ class HardAttODEblock(ODEblock):
             self.odefunc.attention_weights = weights
         else:
             self.odefunc.edge_index = self.data_edge_index
-            self.odefunc.attention_weights = ops.mix_weights(self.get_attention_weights(x))
+            att = self.get_attention_weights(x)
+            # head mean (:60); with autograd recording the torch mean keeps the attention's graph
+            self.odefunc.attention_weights = att.mean(dim=2) if att.requires_grad else ops.mix_weights(att)
         self.reg_odefunc.odefunc.edge_index = self.odefunc.edge_index
         self.reg_odefunc.odefunc.edge_weight = self.odefunc.edge_weight
         self.reg_odefunc.odefunc.attention_weights = self.odefunc.attention_weights

@@ -8,9 +8,12 @@ reference (:45-57): 'attention' -> head-mean of ``attention_weights [B,E,h]``,
 ``edge_weight [B,E]``.  Duplicated edges are summed, as the reference's
 COO -> to_dense does.
 
-Gradients: x, alpha_train and beta_train are differentiable (backward = the
-same K1 kernel over the CSC for A^T, plus two reductions); gradients with
-respect to the edge weights are SURVEY §8(f) next-1 and raise.
+Gradients: x (the same K1 over the CSC for A^T),
+alpha_train / beta_train (two reductions) and the edge weights — whichever
+tensor the block handed over (edge_weight [B,E], or attention_weights [B,E] /
+[B,E,h] whose head mean is taken): an SDDMM g_w[e] = a <gf[src], x[dst]>
+(gnpde_sddmm_f32) written straight into the COO layout of that tensor, so
+autograd carries it on into the attention that produced it.
 """
 import torch
 from torch import nn
@@ -22,12 +25,13 @@ from .utils import MaxNFEException
 
 class _LaplacianRHS(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, alpha_train, beta_train, g, w_csr, w_csc_fn, x0, alpha_sigmoid, add_source):
+    def forward(ctx, x, alpha_train, beta_train, w_src, g, w_csr, w_csc_fn, x0, alpha_sigmoid, add_source):
         f = ops.spmm_rhs(g, w_csr, x, x0=x0, alpha=alpha_train.detach(), beta=beta_train.detach(), rhs=True,
                          alpha_sigmoid=alpha_sigmoid, add_source=add_source)
         ctx.save_for_backward(x, alpha_train, beta_train)
         ctx.g, ctx.w_csr, ctx.w_csc_fn, ctx.x0 = g, w_csr, w_csc_fn, x0
         ctx.alpha_sigmoid, ctx.add_source = alpha_sigmoid, add_source
+        ctx.w_heads = w_src.shape[2] if w_src.dim() == 3 else 1
         return f
 
     @staticmethod
@@ -53,7 +57,12 @@ class _LaplacianRHS(torch.autograd.Function):
                 gb = (gf.double() * ctx.x0.double()).sum().to(beta_train.dtype).reshape(beta_train.shape)
             else:
                 gb = torch.zeros_like(beta_train)
-        return gx, ga, gb, None, None, None, None, None, None
+        gw = None
+        if ctx.needs_input_grad[3]:
+            # d f[src] / d w_e = a x[dst]  ->  g_w[e] = a <gf[src], x[dst]> (/ heads for a head mean)
+            gw = ops.sddmm(g, gf, x.detach(), heads=ctx.w_heads, alpha=alpha_train.detach(),
+                           alpha_sigmoid=ctx.alpha_sigmoid)
+        return gx, ga, gb, gw, None, None, None, None, None, None
 
 
 class LaplacianODEFunc(ODEFunc):
@@ -82,9 +91,6 @@ class LaplacianODEFunc(ODEFunc):
             w, tag = self.edge_weight, 'w'
         if w is None:
             raise RuntimeError("LaplacianODEFunc: %s weights are not set for block=%r" % (tag, blk))
-        if torch.is_grad_enabled() and w.requires_grad:
-            raise NotImplementedError("gnpde: gradients with respect to edge/attention weights are SURVEY §8(f) "
-                                      "next-1; call under torch.no_grad() or detach the weights")
         return w, tag
 
     def sparse_multiply(self, x):
@@ -121,6 +127,6 @@ class LaplacianODEFunc(ODEFunc):
         x0 = self.x0 if add_source else None
         if x0 is not None and x0.dtype != torch.float32:
             x0 = x0.float()
-        return _LaplacianRHS.apply(x, self.alpha_train, self.beta_train, g, w_csr,
+        return _LaplacianRHS.apply(x, self.alpha_train, self.beta_train, w, g, w_csr,
                                    lambda: self.csr_weights(g, w, tag, transpose=True), x0, alpha_sigmoid,
                                    add_source)

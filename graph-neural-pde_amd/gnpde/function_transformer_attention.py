@@ -29,8 +29,18 @@ fork cannot execute (``mix_features`` :23-31, ``square_plus`` :264,
 ``multi_modal`` :171/222, beltrami+exp_kernel :164-167) raise
 NotImplementedError.  ``reweight_attention`` is a no-op in the fork (the
 layer's ``edge_weights`` is captured as None at construction, :15 / :261) and
-is a no-op here.  Inference only: training-mode forwards with grad enabled
-raise (backward kernels are SURVEY §8(f) next-1).
+is a no-op here.
+
+Gradients: with autograd recording, the layer's forward
+is ``_EdgeAttention`` — the same forward kernels, plus a backward made of graph
+passes (backward.hip): edge-softmax backward per group, then for the fork's
+scaled_dot the node-score / key-sum chain rule (segment sums, fp64 weighted
+column sums, a few [att, C] products) and for the per-edge scaled_dot two K1
+aggregations per head (q side over the CSR, k side over the CSC) and the
+projection backward (MFMA projection for d/dx, library GEMM for d/dW).  The
+transformer ODEFunc then composes it with the Laplacian RHS autograd
+(function_laplacian_diffusion._LaplacianRHS), whose weight gradient is an
+SDDMM.  exp_kernel / cosine_sim / pearson have no backward (raise).
 """
 import torch
 from torch import nn
@@ -54,10 +64,95 @@ def _check_supported(opt):
                                   "reference (:166-167) and is not implemented")
 
 
-def _check_inference(module):
-    if module.training and torch.is_grad_enabled():
-        raise NotImplementedError("gnpde: attention backward kernels are SURVEY §8(f) next-1; use eval mode or "
-                                  "torch.no_grad()")
+def _needs_grad(*ts):
+    return torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in ts)
+
+
+class _EdgeAttention(torch.autograd.Function):
+    """attention [B,E,h] (COO) = SpGraphTransAttentionLayer.forward's first
+    output as a function of (x, Wq, bq, Wk, bk); backward in graph passes."""
+
+    @staticmethod
+    def forward(ctx, x, Wq, bq, Wk, bk, layer, g, norm_idx):
+        ns, m, rl = layer.scores_and_stats(g, x.detach(), norm_idx)
+        att = ops.edge_attention(g, ns, m, rl, norm_idx)
+        ctx.save_for_backward(x, Wq, bq, Wk, bk, att)
+        ctx.layer, ctx.g, ctx.norm_idx, ctx.ns = layer, g, norm_idx, ns
+        return att
+
+    @staticmethod
+    def backward(ctx, g_att):
+        x, Wq, bq, Wk, bk, att = ctx.saved_tensors
+        g, ns, norm_idx = ctx.g, ctx.ns, ctx.norm_idx
+        grouped = g.csr if norm_idx == 0 else g.csc
+        gs = ops.softmax_backward(grouped, att, g_att.float())
+        if ns.mode == ops._lib.SCORE_UNIFORM:
+            # every score of a softmax group is the same node score: the attention does not move
+            return (torch.zeros_like(x), torch.zeros_like(Wq), torch.zeros_like(bq), torch.zeros_like(Wk),
+                    torch.zeros_like(bk), None, None, None)
+        if ns.mode == ops._lib.SCORE_REFERENCE:
+            grads = _reference_score_backward(g, ns, gs, x.detach(), Wq.detach(), bq.detach(), Wk.detach(),
+                                              bk.detach())
+        elif ns.mode == ops._lib.SCORE_DOT:
+            grads = _dot_score_backward(g, ns, gs, x.detach(), Wq.detach(), Wk.detach())
+        else:
+            raise NotImplementedError("gnpde: no backward for attention_type %r (scaled_dot only)" %
+                                      ctx.layer.opt.get('attention_type'))
+        return grads + (None, None, None)
+
+
+def _reference_score_backward(g, ns, gs, x, Wq, bq, Wk, bk):
+    """Chain rule of the fork's scaled_dot (function_transformer_attention.py:249):
+    s[e,h] = cs[src(e),h], cs[n,h] = q_{n,h} . S_h / sqrt(dk), q = Wq x + bq,
+    S = Wk xbar + E bk, xbar = sum_n indeg(n) x_n.  Graph passes in HIP; the
+    [att, C]-sized products in fp64 torch."""
+    B, N, H, dk = g.B, g.N, ns.heads, ns.dk
+    att_dim = H * dk
+    C = x.shape[-1]
+    inv = 1.0 / float(dk) ** 0.5
+    gcs = ops.segment_sum(g.csr, gs)                           # [R,H]: edges gather the score of their source
+    xbar = ops.wcolsum(x, B, N, g.indeg.double().view(-1, 1))[:, 0, :]    # [B,C+1]
+    y = ops.wcolsum(x, B, N, gcs)                              # [B,H,C+1]
+    Wq64, bq64, Wk64, bk64 = Wq.double(), bq.double(), Wk.double(), bk.double()
+    S = xbar[:, :C] @ Wk64.t() + xbar[:, C:] * bk64            # [B,att]
+    Sh = S.view(B, H, dk)
+    Wqh = Wq64.view(H, dk, C)
+    U = inv * torch.einsum('hdc,bhd->bch', Wqh, Sh)            # [B,C,H]
+    gU = y[:, :, :C].transpose(1, 2)                           # [B,C,H]
+    gv = y[:, :, C]                                            # [B,H]
+    g_Wq = inv * torch.einsum('bhd,bch->hdc', Sh, gU).reshape(att_dim, C)
+    g_bq = inv * torch.einsum('bhd,bh->hd', Sh, gv).reshape(att_dim)
+    gS = inv * (torch.einsum('hdc,bch->bhd', Wqh, gU) + bq64.view(H, dk)[None] * gv[:, :, None])
+    gS = gS.reshape(B, att_dim)
+    g_Wk = gS.t() @ xbar[:, :C]
+    g_bk = gS.t() @ xbar[:, C]
+    gxbar = gS @ Wk64                                          # [B,C]
+    gx = ops.score_input_grad(gcs, U, g.indeg, gxbar, B, N, C).view(x.shape)
+    return (gx, g_Wq.to(Wq.dtype), g_bq.to(bq.dtype), g_Wk.to(Wk.dtype), g_bk.to(bk.dtype))
+
+
+def _dot_score_backward(g, ns, gs, x, Wq, Wk):
+    """Per-edge scaled_dot s[e,h] = q[src,h] . k[dst,h] / sqrt(dk): per head, g_q
+    aggregates g_s k[dst] over the CSR and g_k aggregates g_s q[src] over the
+    CSC (K1 with per-head weights), then the projection backward."""
+    H, dk = ns.heads, ns.dk
+    inv = 1.0 / float(dk) ** 0.5
+    R = g.R
+    xr = x.reshape(R, -1)
+    gqk = torch.empty(R, 2 * H * dk, dtype=torch.float32, device=x.device)
+    for h in range(H):
+        cols = slice(h * dk, (h + 1) * dk)
+        kh = ns.k[:, cols].contiguous()
+        qh = ns.q[:, cols].contiguous()
+        gqk[:, cols] = ops.spmm_rhs(g, ops.gather_head(g.csr, gs, h, inv), kh, rhs=False)
+        gqk[:, H * dk + h * dk:H * dk + (h + 1) * dk] = ops.spmm_rhs(g, ops.gather_head(g.csc, gs, h, inv), qh,
+                                                                     rhs=False, transpose=True)
+    W = torch.cat([Wq, Wk], 0)                                 # [2att, C]
+    gx, _ = ops.linear(gqk, W.t().contiguous())                # gx = [g_q | g_k] [Wq; Wk]
+    gW = gqk.t() @ xr                                          # [2att, C] (library GEMM)
+    gb = gqk.sum(0)
+    att_dim = H * dk
+    return (gx.view(x.shape), gW[:att_dim], gb[:att_dim], gW[att_dim:], gb[att_dim:])
 
 
 class SpGraphTransAttentionLayer(nn.Module):
@@ -141,7 +236,6 @@ class SpGraphTransAttentionLayer(nn.Module):
         return self._uniform[4]
 
     def node_scores(self, g, x):
-        _check_inference(self)
         p0, p1 = self._score_params()
         wcat = None
         if self.score_mode != 'reference' or self.opt.get('attention_type', 'scaled_dot') != 'scaled_dot':
@@ -160,6 +254,9 @@ class SpGraphTransAttentionLayer(nn.Module):
         materialised (dead for mix_features=False)."""
         g = self.graph_for(x, edge)
         norm_idx = int(self.opt['attention_norm_idx'])
+        if _needs_grad(x, self.Q.weight, self.Q.bias, self.K.weight, self.K.bias):
+            att = _EdgeAttention.apply(x, self.Q.weight, self.Q.bias, self.K.weight, self.K.bias, self, g, norm_idx)
+            return att, (None, None)
         ns, m, rl = self.scores_and_stats(g, x, norm_idx)
         return ops.edge_attention(g, ns, m, rl, norm_idx), (None, None)
 
@@ -198,9 +295,11 @@ class ODEFuncTransformerAtt(ODEFunc):
         if self.nfe > self.opt["max_nfe"]:
             raise MaxNFEException
         self.nfe += 1
-        _check_inference(self)
         g = self.graph_for(x)
         lay = self.multihead_att_layer
+        if stage is None and _needs_grad(x, self.alpha_train, self.beta_train, lay.Q.weight, lay.Q.bias,
+                                         lay.K.weight, lay.K.bias):
+            return self._rhs_autograd(g, x)
         norm_idx = int(self.opt['attention_norm_idx'])
         add_source = bool(self.opt.get('add_source', False))
         if add_source and self.x0 is None:
@@ -215,6 +314,23 @@ class ODEFuncTransformerAtt(ODEFunc):
         # source-grouped weights come straight from the scores (K2)
         m, rl = ops.softmax_stats(g, ns, 1) if norm_idx == 1 else (None, None)
         return ops.attn_rhs(g, ns, m, rl, norm_idx, x, **kw)
+
+    def _rhs_autograd(self, g, x):
+        """Training forward: attention [B,E,h] through _EdgeAttention, then the
+        Laplacian RHS autograd with those weights (head mean), so gradients
+        reach x (both paths), alpha, beta and the Q/K parameters."""
+        from .function_laplacian_diffusion import _LaplacianRHS
+        att, _ = self.multihead_att_layer(x, self.edge_index)
+        add_source = bool(self.opt.get('add_source', False))
+        if add_source and self.x0 is None:
+            raise RuntimeError("ODEFuncTransformerAtt: add_source needs x0 (ODEblock.set_x0)")
+        x0 = self.x0 if add_source else None
+        if x0 is not None and x0.dtype != torch.float32:
+            x0 = x0.float()
+        ad = att.detach()
+        return _LaplacianRHS.apply(x, self.alpha_train, self.beta_train, att, g, g.gather_weights(ad),
+                                   lambda: g.gather_weights(ad, transpose=True), x0,
+                                   not self.opt.get('no_alpha_sigmoid', False), add_source)
 
     def __repr__(self):
         return self.__class__.__name__ + ' (' + str(self.in_features) + ' -> ' + str(self.out_features) + ')'

@@ -607,6 +607,81 @@ def edge_attention(g, ns, m, rl, norm_idx):
     return att
 
 
+# --------------------------------------------------------------------------- backward passes
+def sddmm(g, gf, x, heads=1, alpha=None, alpha_sigmoid=False):
+    """d <gf, a (A(w) x)> / d w in COO order: [B,E] (heads=1) or [B,E,heads]
+    (w = the head mean of an [B,E,heads] attention): a <gf[src], x[dst]> / heads."""
+    gfr = _rows(gf, "gf")
+    xr = _rows(x, "x")
+    C = xr.shape[1]
+    dev = xr.device
+    a = _scalar(alpha, "alpha", dev)
+    shape = (g.B, g.E) if heads == 1 else (g.B, g.E, heads)
+    out = torch.empty(shape, dtype=torch.float32, device=dev)
+    _lib.call("gnpde_sddmm_f32", _ptr(g.csr.rowidx), _ptr(g.csr.col), _ptr(g.csr.perm), g.nnz, C, _ptr(gfr), C,
+              _ptr(xr), C, _ptr(a), int(alpha_sigmoid), int(heads), _ptr(out), _stream(dev))
+    return out
+
+
+def softmax_backward(grouped, att, g_att):
+    """Edge-softmax backward over the groups of ``grouped`` (COO [B,E,H] in and out)."""
+    _require_gpu(att, "attention", torch.float32)
+    _require_gpu(g_att, "attention grad", torch.float32)
+    att, g_att = att.contiguous(), g_att.contiguous()
+    H = att.shape[-1]
+    gs = torch.empty_like(att)
+    _lib.call("gnpde_softmax_backward_f32", _ptr(grouped.rowptr), _ptr(grouped.perm), grouped.R, grouped.nnz, H,
+              _ptr(att), _ptr(g_att), _ptr(gs), _stream(att.device))
+    return gs
+
+
+def segment_sum(grouped, vals):
+    """[R,H] fp64 sums of COO per-edge values [B,E,H] over the rows of ``grouped``."""
+    _require_gpu(vals, "values", torch.float32)
+    vals = vals.contiguous()
+    H = vals.shape[-1]
+    out = torch.empty(grouped.R, H, dtype=torch.float64, device=vals.device)
+    _lib.call("gnpde_segment_sum_f64", _ptr(grouped.rowptr), _ptr(grouped.perm), grouped.R, grouped.nnz, H,
+              _ptr(vals), _ptr(out), _stream(vals.device))
+    return out
+
+
+def wcolsum(x, B, N, w):
+    """y [B,H,C+1] fp64: y[b,h,:C] = sum_n w[b*N+n,h] x[b,n,:], y[b,h,C] = sum_n w[b*N+n,h]."""
+    xr = _rows(x, "x")
+    _require_gpu(w, "weights", torch.float64)
+    w = w.contiguous()
+    H = w.shape[-1]
+    C = xr.shape[1]
+    ws_bytes = _lib.fn("gnpde_wcolsum_workspace_bytes")(B, N, C, H)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=xr.device)
+    y = torch.empty(B, H, C + 1, dtype=torch.float64, device=xr.device)
+    _lib.call("gnpde_wcolsum_f64", _ptr(xr), B, N, C, C, _ptr(w), H, _ptr(y), _ptr(ws), ws_bytes,
+              _stream(xr.device))
+    return y
+
+
+def score_input_grad(gcs, U, deg, gxbar, B, N, C, out=None):
+    """gx [R,C] fp32 = gcs U_b^T + deg * gxbar_b  (reference-mode node-score backward)."""
+    H = gcs.shape[-1]
+    dev = gcs.device
+    gx = torch.empty(B * N, C, dtype=torch.float32, device=dev) if out is None else out
+    _lib.call("gnpde_score_input_grad_f32", _ptr(gcs.contiguous()), _ptr(U.contiguous()), _ptr(deg),
+              _ptr(gxbar.contiguous()), B, N, C, H, _ptr(gx), C, int(out is not None), _stream(dev))
+    return gx
+
+
+def gather_head(grouped, w, h, scale=1.0):
+    """scale * w[:, :, h] (COO [B,E,H]) in ``grouped`` order [nnz]."""
+    _require_gpu(w, "values", torch.float32)
+    w = w.contiguous()
+    H = w.shape[-1]
+    out = torch.empty(max(grouped.nnz, 1), dtype=torch.float32, device=w.device)
+    _lib.call("gnpde_gather_head_f32", _ptr(w), grouped.nnz, H, int(h), _ptr(grouped.perm), float(scale), _ptr(out),
+              _stream(w.device))
+    return out
+
+
 # --------------------------------------------------------------------------- solver glue
 def rk_combine(y0, ks, coefs, scale, out=None):
     """out = y0 + scale * sum_j coefs[j] * ks[j]  (one fused pass; y0=None means 0)."""

@@ -281,6 +281,46 @@ int gnpde_edge_attention_f32(const int32_t* rowidx, const int32_t* col, const in
 int gnpde_rk_combine_f32(int64_t n, const float* y0, int nk, const float* const* ks, const double* coef,
                          double scale, float* out, void* stream);
 
+/* ---------------------------------------------------------------- backward
+ * Gradients of the RHS f = a (A(w) x - x) [+ b x0] and of the attention that
+ * produces w; torch autograd of the reference (function_laplacian_diffusion.py:
+ * 39-77, function_transformer_attention.py:218-267, utils.py:116-127) restated
+ * as graph passes.  All sums in a fixed order (no float atomics).
+ *
+ * d f / d w: g_out[perm[p]*heads + h] = a * <gf[rowidx[p]], x[col[p]]> / heads
+ * for every head h < heads <= 64 (COO order; heads > 1: w is the head mean of [B,E,heads]).
+ * a = sigmoid(*alpha) / *alpha / 1 (alpha NULL), as the RHS epilogue.        */
+int gnpde_sddmm_f32(const int32_t* rowidx, const int32_t* col, const int32_t* perm, int64_t nnz, int64_t C,
+                    const float* gf, int64_t ldg, const float* x, int64_t ldx, const float* alpha, int alpha_sigmoid,
+                    int heads, float* g_out, void* stream);
+
+/* Edge-softmax backward per group of a grouped CSR (rowptr, perm -> COO ids):
+ * gs[i,h] = att[i,h] * (g[i,h] - sum_{j in grp(i)} att[j,h] g[j,h]), COO [nnz, heads]. */
+int gnpde_softmax_backward_f32(const int32_t* rowptr, const int32_t* perm, int64_t R, int64_t nnz, int heads,
+                               const float* att, const float* g, float* gs, void* stream);
+
+/* out[r,h] = sum_{p in row r} vals[perm[p]*heads + h]  (fp64 out, [R, heads]). */
+int gnpde_segment_sum_f64(const int32_t* rowptr, const int32_t* perm, int64_t R, int64_t nnz, int heads,
+                          const float* vals, double* out, void* stream);
+
+/* y[b][h][c] = sum_n w[b*N+n, h] x[b*N+n, c], y[b][h][C] = sum_n w[b*N+n, h]
+ * (fp64, y is [B][heads][C+1]); workspace gnpde_wcolsum_workspace_bytes.    */
+size_t gnpde_wcolsum_workspace_bytes(int64_t B, int64_t N, int64_t C, int heads);
+int gnpde_wcolsum_f64(const float* x, int64_t B, int64_t N, int64_t C, int64_t ldx, const double* w, int heads,
+                      double* y, void* workspace, size_t workspace_bytes, void* stream);
+
+/* Input gradient of the reference-mode node scores cs = x U_b + v_b and of the
+ * key sum xbar_b = sum_n deg[n] x_n:
+ *   gx[n,c] (+)= sum_h gcs[n,h] U[b][c][h] + deg[n] gxbar[b][c]   (b = n / N). */
+int gnpde_score_input_grad_f32(const double* gcs, const double* U, const int32_t* deg, const double* gxbar, int64_t B,
+                               int64_t N, int64_t C, int heads, float* gx, int64_t ldgx, int accumulate,
+                               void* stream);
+
+/* out[p] = scale * w[perm[p]*heads + h]: one head of COO per-edge values in a
+ * grouped CSR's order (per-head weights of the per-edge score backward).     */
+int gnpde_gather_head_f32(const float* w, int64_t nnz, int heads, int h, const int32_t* perm, float scale, float* out,
+                          void* stream);
+
 #ifdef __cplusplus
 }
 #endif

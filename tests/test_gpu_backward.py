@@ -1,0 +1,260 @@
+"""GPU gradients of the RHS and the attention against
+torch float64 autograd of a plain-torch restatement of the reference formulas
+(function_laplacian_diffusion.py:39-77, function_transformer_attention.py:
+218-267 incl. the fork's global-key-sum scaled_dot, utils.py:116-127).
+
+Tolerance: max|g - g_ref| / max|g_ref| <= 1e-4 per gradient (fp32 kernels with
+fp32/fp64 accumulation against fp64 autograd).
+"""
+import numpy as np
+import pytest
+import torch
+
+import gnpde
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+GTOL = 1e-4
+
+OPT = {'self_loop_weight': 1, 'leaky_relu_slope': 0.2, 'heads': 2, 'attention_norm_idx': 0, 'add_source': False,
+       'hidden_dim': 6, 'block': 'constant', 'function': 'laplacian', 'augment': False, 'adjoint': False,
+       'tol_scale': 1, 'time': 1, 'method': 'euler', 'no_alpha_sigmoid': False, 'reweight_attention': False,
+       'step_size': 1, 'beltrami': False, 'attention_type': 'scaled_dot', 'square_plus': False, 'max_nfe': 100000,
+       'data_norm': 'rw', 'max_iters': 1000, 'multi_modal': False, 'mix_features': False, 'attention_dim': 16}
+
+
+def relerr(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return float((a - b).abs().max() / max(float(b.abs().max()), 1e-30))
+
+
+# ---------------------------------------------------------------- torch fp64 restatement (test oracle)
+def t_aggregate(ei, w, x):
+    """sum_{e: src=i} w_e x[dst]  per batch element (function_laplacian_diffusion.py:39-58)."""
+    B, N, C = x.shape
+    out = []
+    for b in range(B):
+        src, dst = ei[b, 0], ei[b, 1]
+        out.append(torch.zeros(N, C, dtype=x.dtype, device=x.device).index_add(0, src, w[b][:, None] * x[b][dst]))
+    return torch.stack(out)
+
+
+def t_softmax(s, idx, N):
+    """utils.softmax (src/utils.py:116-127) for s [E,H] grouped by idx [E]."""
+    m = torch.full((N, s.shape[1]), -float('inf'), dtype=s.dtype, device=s.device)
+    m = m.index_reduce(0, idx, s.detach(), 'amax', include_self=True)
+    e = torch.exp(s - m[idx])
+    den = torch.zeros(N, s.shape[1], dtype=s.dtype, device=s.device).index_add(0, idx, e)
+    return e / (den[idx] + 1e-16)
+
+
+def t_attention(x, ei, Wq, bq, Wk, bk, H, norm_idx, mode):
+    """[B,E,H] attention: fork scaled_dot (mode 'reference': q_src . sum_e' k_dst(e') / sqrt dk)
+    or per-edge scaled_dot (q_src . k_dst / sqrt dk)."""
+    B, N, C = x.shape
+    att_dim = Wq.shape[0]
+    dk = att_dim // H
+    q = (x @ Wq.t() + bq).view(B, N, H, dk)
+    k = (x @ Wk.t() + bk).view(B, N, H, dk)
+    outs = []
+    for b in range(B):
+        src, dst = ei[b, 0], ei[b, 1]
+        if mode == 'reference':
+            S = k[b][dst].sum(0)                               # [H, dk]
+            s = (q[b][src] * S[None]).sum(-1) / dk ** 0.5      # [E, H]
+        else:
+            s = (q[b][src] * k[b][dst]).sum(-1) / dk ** 0.5
+        outs.append(t_softmax(s, ei[b, norm_idx], N))
+    return torch.stack(outs)
+
+
+def t_rhs(x, ei, w, alpha, beta=None, x0=None):
+    f = torch.sigmoid(alpha) * (t_aggregate(ei, w, x) - x)
+    return f if x0 is None else f + beta * x0
+
+
+def graph(seed, N, E, B=1, hub=True):
+    rng = np.random.default_rng(seed)
+    ei = rng.integers(0, N, size=(B, 2, E))
+    if hub:
+        ei[:, 0, :min(E // 5, 400)] = 3          # a hub source group
+        ei[:, 1, E // 5:E // 5 + min(E // 5, 400)] = 7  # a hub destination group
+    return torch.from_numpy(ei).to(DEV)
+
+
+def qk_params(seed, C, att, scale=0.2):
+    g = torch.Generator().manual_seed(seed)
+    return [(torch.randn(*sh, generator=g) * scale).to(DEV) for sh in ((att, C), (att,), (att, C), (att,))]
+
+
+# ---------------------------------------------------------------- Laplacian RHS: edge weights
+def test_laplacian_edge_weight_gradient_sddmm():
+    N, E, C = 900, 7000, 40
+    ei = graph(1, N, E)
+    torch.manual_seed(1)
+    x = torch.randn(1, N, C, device=DEV)
+    w = torch.rand(1, E, device=DEV)
+    R = torch.randn(1, N, C, device=DEV)
+    func = gnpde.LaplacianODEFunc(C, C, dict(OPT, hidden_dim=C), DEV).to(DEV)
+    with torch.no_grad():
+        func.alpha_train.fill_(0.4)
+    wt = w.clone().requires_grad_(True)
+    xt = x.clone().requires_grad_(True)
+    func.edge_index, func.edge_weight = ei, wt
+    (func(0, xt) * R).sum().backward()
+    w64 = w.double().requires_grad_(True)
+    x64 = x.double().requires_grad_(True)
+    a64 = torch.tensor(0.4, dtype=torch.float64, device=DEV, requires_grad=True)
+    (t_rhs(x64, ei, w64, a64) * R.double()).sum().backward()
+    assert relerr(wt.grad, w64.grad) <= GTOL
+    assert relerr(xt.grad, x64.grad) <= GTOL
+    assert relerr(func.alpha_train.grad, a64.grad) <= GTOL
+
+
+def test_laplacian_attention_mean_gradient():
+    """block='attention': w = attention_weights.mean(2); the SDDMM gradient lands on every head / H."""
+    N, E, C, H = 500, 4000, 16, 4
+    ei = graph(2, N, E, B=2)
+    torch.manual_seed(2)
+    x = torch.randn(2, N, C, device=DEV)
+    att = torch.rand(2, E, H, device=DEV)
+    R = torch.randn(2, N, C, device=DEV)
+    func = gnpde.LaplacianODEFunc(C, C, dict(OPT, hidden_dim=C, block='attention'), DEV).to(DEV)
+    at = att.clone().requires_grad_(True)
+    func.edge_index, func.attention_weights = ei, at
+    (func(0, x) * R).sum().backward()
+    a64 = att.double().requires_grad_(True)
+    (t_rhs(x.double(), ei, a64.mean(2), torch.tensor(0.0, dtype=torch.float64, device=DEV)) * R.double()).sum() \
+        .backward()
+    assert relerr(at.grad, a64.grad) <= GTOL
+
+
+# ---------------------------------------------------------------- transformer RHS: attention backward
+@pytest.mark.parametrize("mode,norm_idx", [("reference", 1), ("reference", 0), ("per_edge", 0), ("per_edge", 1)])
+@pytest.mark.parametrize("H,att", [(2, 16), (1, 8), (4, 32)])
+def test_transformer_rhs_gradients(mode, norm_idx, H, att):
+    N, E, C, B = 600, 5000, 24, 2
+    ei = graph(3 + H, N, E, B=B)
+    torch.manual_seed(3)
+    x = torch.randn(B, N, C, device=DEV)
+    x0 = torch.randn(B, N, C, device=DEV)
+    R = torch.randn(B, N, C, device=DEV)
+    Wq, bq, Wk, bk = qk_params(4, C, att, scale=0.3 if mode == 'per_edge' else 0.05)
+    opt = dict(OPT, hidden_dim=C, heads=H, attention_dim=att, function='transformer', attention_norm_idx=norm_idx,
+               attention_score_mode=mode, add_source=True)
+    func = gnpde.ODEFuncTransformerAtt(C, C, opt, DEV).to(DEV)
+    lay = func.multihead_att_layer
+    with torch.no_grad():
+        for p, v in ((lay.Q.weight, Wq), (lay.Q.bias, bq), (lay.K.weight, Wk), (lay.K.bias, bk)):
+            p.copy_(v)
+        func.alpha_train.fill_(0.3)
+        func.beta_train.fill_(0.6)
+    func.edge_index, func.x0 = ei, x0
+    xt = x.clone().requires_grad_(True)
+    (func(0, xt) * R).sum().backward()
+
+    p64 = [t.double().requires_grad_(True) for t in (x, Wq, bq, Wk, bk)]
+    a64 = torch.tensor(0.3, dtype=torch.float64, device=DEV, requires_grad=True)
+    attn = t_attention(p64[0], ei, *p64[1:], H, norm_idx, mode)
+    f64 = t_rhs(p64[0], ei, attn.mean(2), a64, 0.6, x0.double())
+    (f64 * R.double()).sum().backward()
+    got = [xt.grad, lay.Q.weight.grad, lay.Q.bias.grad, lay.K.weight.grad, lay.K.bias.grad, func.alpha_train.grad]
+    want = [p.grad for p in p64] + [a64.grad]
+    uniform = mode == 'reference' and norm_idx == 0
+    for name, gg, ww in zip(("x", "Wq", "bq", "Wk", "bk", "alpha"), got, want):
+        if uniform and name in ("Wq", "bq", "Wk", "bk"):
+            # fork scaled_dot under source-grouped softmax: the attention is 1/outdeg for any Q, K
+            assert float(ww.abs().max()) < 1e-9 and float(gg.abs().max()) == 0.0, name
+            continue
+        assert relerr(gg, ww) <= GTOL, (name, relerr(gg, ww))
+
+
+# ---------------------------------------------------------------- blocks: training through the integrator
+def test_attention_block_training_gradients():
+    """AttODEblock in training mode (euler, 3 steps): gradients of Q/K, alpha and the input."""
+    N, E, C, H, att = 400, 3000, 16, 2, 16
+    ei = graph(5, N, E, hub=False)
+    torch.manual_seed(5)
+    x = torch.randn(1, N, C, device=DEV)
+    R = torch.randn(1, N, C, device=DEV)
+    opt = dict(OPT, hidden_dim=C, heads=H, attention_dim=att, block='attention', attention_norm_idx=1,
+               method='euler', step_size=1.0 / 3.0)
+    blk = gnpde.AttODEblock(gnpde.LaplacianODEFunc, [], opt, DEV, t=torch.tensor([0, 1])).to(DEV).train()
+    Wq, bq, Wk, bk = qk_params(6, C, att, scale=0.1)
+    lay = blk.multihead_att_layer
+    with torch.no_grad():
+        for p, v in ((lay.Q.weight, Wq), (lay.Q.bias, bq), (lay.K.weight, Wk), (lay.K.bias, bk)):
+            p.copy_(v)
+        blk.odefunc.alpha_train.fill_(0.2)
+    data = gnpde.GraphData()
+    data.new_graph(ei, N)
+    xt = x.clone().requires_grad_(True)
+    (blk(xt, data) * R).sum().backward()
+
+    eo, wo = blk.odefunc.edge_index, blk.odefunc.edge_weight  # after self loops + rw normalisation
+    p64 = [t.double().requires_grad_(True) for t in (x, Wq, bq, Wk, bk)]
+    a64 = torch.tensor(0.2, dtype=torch.float64, device=DEV, requires_grad=True)
+    w = t_attention(p64[0], eo, *p64[1:], H, 1, 'reference').mean(2)
+    y = p64[0]
+    for _ in range(3):
+        y = y + (1.0 / 3.0) * t_rhs(y, eo, w, a64)
+    (y * R.double()).sum().backward()
+    got = [xt.grad, lay.Q.weight.grad, lay.Q.bias.grad, lay.K.weight.grad, lay.K.bias.grad,
+           blk.odefunc.alpha_train.grad]
+    want = [p.grad for p in p64] + [a64.grad]
+    for name, gg, ww in zip(("x", "Wq", "bq", "Wk", "bk", "alpha"), got, want):
+        assert relerr(gg, ww) <= GTOL, (name, relerr(gg, ww))
+
+
+def test_mixed_block_gamma_gradient():
+    N, E, C, H, att = 300, 2500, 12, 1, 8
+    ei = graph(7, N, E, hub=False)
+    torch.manual_seed(7)
+    x = torch.randn(1, N, C, device=DEV)
+    R = torch.randn(1, N, C, device=DEV)
+    opt = dict(OPT, hidden_dim=C, heads=H, attention_dim=att, block='mixed', attention_norm_idx=0,
+               attention_score_mode='per_edge', method='euler', step_size=0.5)
+    blk = gnpde.MixedODEblock(gnpde.LaplacianODEFunc, [], opt, DEV, t=torch.tensor([0, 1])).to(DEV).train()
+    Wq, bq, Wk, bk = qk_params(8, C, att, scale=0.3)
+    lay = blk.multihead_att_layer
+    with torch.no_grad():
+        for p, v in ((lay.Q.weight, Wq), (lay.Q.bias, bq), (lay.K.weight, Wk), (lay.K.bias, bk)):
+            p.copy_(v)
+        blk.gamma.fill_(0.3)
+    data = gnpde.GraphData()
+    data.new_graph(ei, N)
+    (blk(x, data) * R).sum().backward()
+
+    eo, wo = blk.odefunc.edge_index, blk.odefunc.edge_weight
+    p64 = [t.double().requires_grad_(True) for t in (Wq, bq, Wk, bk)]
+    g64 = torch.tensor([0.3], dtype=torch.float64, device=DEV, requires_grad=True)
+    s = torch.sigmoid(g64)
+    w = t_attention(x.double(), eo, *p64, H, 0, 'per_edge').mean(2) * (1 - s) + wo.double() * s
+    a = torch.tensor(0.0, dtype=torch.float64, device=DEV)
+    y = x.double()
+    for _ in range(2):
+        y = y + 0.5 * t_rhs(y, eo, w, a)
+    (y * R.double()).sum().backward()
+    assert relerr(blk.gamma.grad, g64.grad) <= GTOL
+    assert relerr(lay.Q.weight.grad, p64[0].grad) <= GTOL
+    assert relerr(lay.K.bias.grad, p64[3].grad) <= GTOL
+
+
+def test_backward_is_bit_reproducible():
+    N, E, C, H, att = 700, 6000, 32, 2, 16
+    ei = graph(9, N, E)
+    torch.manual_seed(9)
+    x = torch.randn(1, N, C, device=DEV)
+    R = torch.randn(1, N, C, device=DEV)
+    opt = dict(OPT, hidden_dim=C, heads=H, attention_dim=att, function='transformer', attention_norm_idx=1)
+    grads = []
+    for _ in range(2):
+        func = gnpde.ODEFuncTransformerAtt(C, C, opt, DEV).to(DEV)
+        torch.manual_seed(10)
+        for p in func.multihead_att_layer.parameters():
+            torch.nn.init.normal_(p, std=0.05)
+        func.edge_index = ei
+        xt = x.clone().requires_grad_(True)
+        (func(0, xt) * R).sum().backward()
+        grads.append((xt.grad.clone(), func.multihead_att_layer.Q.weight.grad.clone()))
+    assert torch.equal(grads[0][0], grads[1][0]) and torch.equal(grads[0][1], grads[1][1])
