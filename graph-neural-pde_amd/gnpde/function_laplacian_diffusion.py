@@ -32,6 +32,7 @@ class _LaplacianRHS(torch.autograd.Function):
         ctx.g, ctx.w_csr, ctx.w_csc_fn, ctx.x0 = g, w_csr, w_csc_fn, x0
         ctx.alpha_sigmoid, ctx.add_source = alpha_sigmoid, add_source
         ctx.w_heads = w_src.shape[2] if w_src.dim() == 3 else 1
+        ctx.w_shape = w_src.shape
         return f
 
     @staticmethod
@@ -61,7 +62,7 @@ class _LaplacianRHS(torch.autograd.Function):
         if ctx.needs_input_grad[3]:
             # d f[src] / d w_e = a x[dst]  ->  g_w[e] = a <gf[src], x[dst]> (/ heads for a head mean)
             gw = ops.sddmm(g, gf, x.detach(), heads=ctx.w_heads, alpha=alpha_train.detach(),
-                           alpha_sigmoid=ctx.alpha_sigmoid)
+                           alpha_sigmoid=ctx.alpha_sigmoid).view(ctx.w_shape)
         return gx, ga, gb, gw, None, None, None, None, None, None
 
 
