@@ -186,8 +186,18 @@ class ODEblock(nn.Module):
             raise NotImplementedError("gnpde: ODE regularisation terms are out of scope (SURVEY.md §2 row 12)")
         integrator = self.train_integrator if self.training else self.test_integrator
         t = self.t.type_as(x)
-        state_dt = integrator(self.odefunc, x, t, method=self.opt['method'], options=options, atol=self.atol,
-                              rtol=self.rtol)
+        if self.opt.get('adjoint', False) and self.training:
+            # block_constant.py:34-44: adjoint method / step size / tolerances of their own
+            a_opts = {'step_size': self.opt.get('adjoint_step_size', options.get('step_size'))}
+            if 'max_iters' in options:
+                a_opts['max_iters'] = options['max_iters']
+            state_dt = integrator(self.odefunc, x, t, method=self.opt['method'], options=options,
+                                  adjoint_method=self.opt.get('adjoint_method', self.opt['method']),
+                                  adjoint_options=a_opts, atol=self.atol, rtol=self.rtol,
+                                  adjoint_atol=self.atol_adjoint, adjoint_rtol=self.rtol_adjoint)
+        else:
+            state_dt = integrator(self.odefunc, x, t, method=self.opt['method'], options=options, atol=self.atol,
+                                  rtol=self.rtol)
         return state_dt[1]
 
     def __repr__(self):

@@ -314,8 +314,8 @@ class _Dopri5(object):
         return last_step * factor
 
     def _step(self, y0, f0, t0, dt):
-        dtf = float(dt)
-        t0f = float(t0)
+        dtf = float(dt.detach()) if isinstance(dt, torch.Tensor) else float(dt)
+        t0f = float(t0.detach()) if isinstance(t0, torch.Tensor) else float(t0)
         k = [f0]
         yi = y0
         for i, (a_i, beta_i) in enumerate(zip(_DP_ALPHA, _DP_BETA)):
@@ -329,7 +329,7 @@ class _Dopri5(object):
         return y1, f1, y1_error, k
 
     def _interp(self, y0, y1, k, dt, t0, t1, t):
-        dtf = float(dt)
+        dtf = float(dt.detach()) if isinstance(dt, torch.Tensor) else float(dt)
         y_mid = self.combine(y0, k, _DP_C_MID, dtf)
         f0, f1 = k[0], k[-1]
         a = 2 * dtf * (f1 - f0) - 8 * (y1 + y0) + 16 * y_mid
@@ -406,8 +406,103 @@ def odeint(func, y0, t, rtol=1e-7, atol=1e-9, method=None, options=None, combine
 odeint.last_n_steps = 0
 
 
-def odeint_adjoint(*args, **kwargs):
-    raise NotImplementedError("gnpde: adjoint integration needs the backward kernels (SURVEY §8(f) next-1)")
+# --------------------------------------------------------------------------- adjoint
+def _mixed_norm_fn(sizes):
+    """torchdiffeq's norm for tuple states (max over the components of their RMS
+    norms), applied to the flattened augmented state [y | adj_y | adj_params...]."""
+    bounds = []
+    o = 0
+    for n in sizes:
+        bounds.append((o, o + n))
+        o += n
+
+    def norm(z):
+        return torch.stack([_rms_norm(z[a:b]) for a, b in bounds if b > a]).max()
+    return norm
+
+
+class _OdeintAdjoint(torch.autograd.Function):
+    """torchdiffeq.odeint_adjoint (0.2.x OdeintAdjointMethod) restated: the
+    forward integrates without recording; the backward integrates the augmented
+    system (y, a_y, a_theta) from t[-1] back to t[0] with
+        dy/dt = f,  da_y/dt = -a_y^T df/dy,  da_theta/dt = -a_y^T df/dtheta
+    (vector-Jacobian products through the RHS autograd: K1 over the CSC, the
+    SDDMM and the attention backward), adding the output gradient at every
+    requested time.  Time runs backwards by integrating in s = -t."""
+
+    @staticmethod
+    def forward(ctx, y0, t, cfg, *params):
+        func, rtol, atol, method, options = cfg[:5]
+        with torch.no_grad():
+            ans = odeint(func, y0, t, rtol=rtol, atol=atol, method=method, options=options)
+        ctx.cfg = cfg
+        ctx.params = params  # the leaf parameters themselves: the VJPs are taken with respect to them
+        ctx.save_for_backward(t, ans)
+        return ans
+
+    @staticmethod
+    def backward(ctx, grad_y):
+        func, _rtol, _atol, _method, _options, a_rtol, a_atol, a_method, a_options = ctx.cfg
+        t, ans = ctx.saved_tensors
+        params = ctx.params
+        y_shape = ans.shape[1:]
+        ny = ans[0].numel()
+        sizes = [ny, ny] + [p.numel() for p in params]
+
+        def pack(y, ay, ap):
+            return torch.cat([y.reshape(-1).float(), ay.reshape(-1).float()] + [a.reshape(-1).float() for a in ap])
+
+        def aug(s, z):
+            y = z[:ny].view(y_shape)
+            ay = z[ny:2 * ny].view(y_shape)
+            with torch.enable_grad():
+                yv = y.detach().requires_grad_(True)
+                f = func(-s, yv)
+                grads = torch.autograd.grad(f, (yv,) + tuple(params), -ay, allow_unused=True)
+            vjp_y = grads[0] if grads[0] is not None else torch.zeros_like(y)
+            vjp_p = [torch.zeros_like(p) if g is None else g for g, p in zip(grads[1:], params)]
+            return -pack(f.detach(), vjp_y, vjp_p)  # d/ds = -d/dt
+
+        opts = dict(a_options or {})
+        if a_method == 'dopri5' and 'norm' not in opts:
+            opts['norm'] = _mixed_norm_fn(sizes)
+        ay = grad_y[-1]
+        ap = [torch.zeros_like(p) for p in params]
+        with torch.no_grad():
+            for i in range(len(t) - 1, 0, -1):
+                z0 = pack(ans[i], ay, ap)
+                s = torch.stack([-t[i], -t[i - 1]])
+                z1 = odeint(aug, z0, s, rtol=a_rtol, atol=a_atol, method=a_method, options=opts)[1]
+                ay = z1[ny:2 * ny].view(y_shape).to(grad_y.dtype) + grad_y[i - 1]
+                o = 2 * ny
+                ap = []
+                for p in params:
+                    ap.append(z1[o:o + p.numel()].view(p.shape).to(p.dtype))
+                    o += p.numel()
+        return (ay, None, None) + tuple(ap)
+
+
+def odeint_adjoint(func, y0, t, rtol=1e-7, atol=1e-9, method=None, options=None, adjoint_rtol=None,
+                   adjoint_atol=None, adjoint_method=None, adjoint_options=None, adjoint_params=None):
+    """torchdiffeq.odeint_adjoint(func, y0, t, ...) with its defaults: the adjoint
+    tolerances / method default to the forward ones, adjoint_options to the
+    forward options (without 'norm') when the methods match, adjoint_params to
+    func's parameters that require grad.  Gradients reach y0 and adjoint_params
+    (as in torchdiffeq, not other tensors the RHS closes over)."""
+    method = method or 'dopri5'
+    if adjoint_params is None:
+        adjoint_params = tuple(p for p in func.parameters() if p.requires_grad)
+    adjoint_params = tuple(adjoint_params)
+    adjoint_rtol = rtol if adjoint_rtol is None else adjoint_rtol
+    adjoint_atol = atol if adjoint_atol is None else adjoint_atol
+    adjoint_method = method if adjoint_method is None else adjoint_method
+    if adjoint_options is None:
+        adjoint_options = {k: v for k, v in (options or {}).items() if k != 'norm'} if adjoint_method == method \
+            else {}
+    if not isinstance(t, torch.Tensor):
+        t = torch.as_tensor(t)
+    cfg = (func, rtol, atol, method, options, adjoint_rtol, adjoint_atol, adjoint_method, adjoint_options)
+    return _OdeintAdjoint.apply(y0, t, cfg, *adjoint_params)
 
 
 __all__ = ['odeint', 'odeint_adjoint', 'fixed_grid', 'FIXED_METHODS', 'ADAPTIVE_METHODS', 'math']

@@ -266,3 +266,51 @@ def test_backward_is_bit_reproducible():
         (func(0, xt) * R).sum().backward()
         grads.append((xt.grad.clone(), func.multihead_att_layer.Q.weight.grad.clone()))
     assert torch.equal(grads[0][0], grads[1][0]) and torch.equal(grads[0][1], grads[1][1])
+
+
+# ---------------------------------------------------------------- adjoint integration
+@pytest.mark.parametrize("method,step", [("rk4", 0.05), ("dopri5", None)])
+def test_adjoint_matches_direct_backprop(method, step):
+    """odeint_adjoint (torchdiffeq semantics) against backprop through the solver:
+    gradients of y0 and of the RHS parameters (alpha_train, beta_train)."""
+    N, E, C = 500, 4000, 16
+    ei = graph(11, N, E)
+    torch.manual_seed(11)
+    x = torch.randn(1, N, C, device=DEV)
+    x0 = torch.randn(1, N, C, device=DEV)
+    w = torch.rand(1, E, device=DEV)
+    R = torch.randn(1, N, C, device=DEV)
+    t = torch.tensor([0.0, 0.5, 1.0], device=DEV)
+    opts = {} if step is None else {'step_size': step}
+    res = []
+    for integ in (gnpde.integrator.odeint, gnpde.integrator.odeint_adjoint):
+        func = gnpde.LaplacianODEFunc(C, C, dict(OPT, hidden_dim=C, add_source=True), DEV).to(DEV)
+        with torch.no_grad():
+            func.alpha_train.fill_(0.5)
+            func.beta_train.fill_(-0.3)
+        func.edge_index, func.edge_weight, func.x0 = ei, w, x0
+        xt = x.clone().requires_grad_(True)
+        z = integ(func, xt, t, rtol=1e-7, atol=1e-9, method=method, options=dict(opts))
+        (z[1:] * R).sum().backward()
+        res.append((xt.grad, func.alpha_train.grad, func.beta_train.grad))
+    for gd, ga in zip(*res):
+        assert relerr(ga, gd) <= 1e-3, relerr(ga, gd)
+
+
+def test_constant_block_adjoint_training():
+    """ConstantODEblock with opt['adjoint']: the block routes through odeint_adjoint with
+    adjoint_method / adjoint_step_size (block_constant.py:34-44) and trains alpha."""
+    N, E, C = 300, 2500, 8
+    ei = graph(12, N, E, hub=False)
+    torch.manual_seed(12)
+    x = torch.randn(1, N, C, device=DEV)
+    opt = dict(OPT, hidden_dim=C, adjoint=True, adjoint_method='rk4', adjoint_step_size=0.1, method='rk4',
+               step_size=0.1, tol_scale_adjoint=1.0)
+    blk = gnpde.ConstantODEblock(gnpde.LaplacianODEFunc, [], opt, DEV, t=torch.tensor([0, 1])).to(DEV).train()
+    assert blk.train_integrator is gnpde.integrator.odeint_adjoint
+    data = gnpde.GraphData()
+    data.new_graph(ei, N)
+    xt = x.clone().requires_grad_(True)
+    (blk(xt, data) ** 2).sum().backward()
+    assert xt.grad is not None and torch.isfinite(xt.grad).all()
+    assert blk.odefunc.alpha_train.grad is not None and float(blk.odefunc.alpha_train.grad) != 0.0
