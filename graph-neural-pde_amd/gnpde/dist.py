@@ -66,6 +66,8 @@ class RowShardedLaplacian(object):
     (global row order, padding at the end), aggregates the local rows of A and
     returns f_local [nb, C]; it drops into gnpde.odeint unchanged."""
 
+    graph_capturable = False  # an RCCL all-gather per RHS: the integrator runs it eagerly
+
     def __init__(self, edge_index, edge_weight, num_nodes, alpha, beta=None, x0_local=None, add_source=False,
                  alpha_sigmoid=True, group=None, local_rhs=None, chunk=ops.DEFAULT_CHUNK):
         self.group = group

@@ -233,7 +233,8 @@ def odeint_fixed(func, y0, t, method, step_size=None, combine=None, graph=None):
     t_h = [float(v) for v in t.tolist()]
     steps = list(zip(grid_h[:-1], grid_h[1:]))
     if graph is None:
-        graph = len(steps) >= GRAPH_MIN_STEPS
+        # a RHS with a collective inside (dist.RowShardedLaplacian) opts out of capture
+        graph = len(steps) >= GRAPH_MIN_STEPS and getattr(func, 'graph_capturable', True)
     graphs = None
     solution = [y0]
     j = 1
