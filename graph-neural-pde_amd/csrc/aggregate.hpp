@@ -4,6 +4,8 @@
 // fused, hub-row chunks summed in plan order by a fixup pass (deterministic, no
 // float atomics).
 #pragma once
+#include <algorithm>
+
 #include "common.hpp"
 
 namespace gnpde {
@@ -77,7 +79,7 @@ struct RefDstSoftmaxWeights {
 // (NCH column passes); U edges per group are in flight per iteration.  The
 // epilogue operands (x_r, x0_r, stage inputs) are loaded before the gathers
 // when NCH <= 2 (PRE) so their latency overlaps the aggregation.
-template <int VEC, int GL, int NCH, int U, int RPW, bool STG, class WP>
+template <int VEC, int GL, int NCH, int U, int RPW, bool STG, class WP, class T = float>
 __global__ __launch_bounds__(256) void agg_kernel(const int4* __restrict__ items, int n_items,
                                                    const int* __restrict__ col, WP wp, int C, Epi ep,
                                                    float* __restrict__ partials) {
@@ -101,7 +103,7 @@ __global__ __launch_bounds__(256) void agg_kernel(const int4* __restrict__ items
 #pragma unroll
       for (int ch = 0; ch < NCH; ++ch) {
         const int cc = (ch * GL + gl) * VEC;
-        if (cc < C) epi_prefetch<VEC, STG>(ep, row, cc, pre[ch]);
+        if (cc < C) epi_prefetch<VEC, STG, T>(ep, row, cc, pre[ch]);
       }
     }
   }
@@ -131,7 +133,7 @@ __global__ __launch_bounds__(256) void agg_kernel(const int4* __restrict__ items
         const int src = rs * SL + (jj < n ? jj : 0);
         srcl[u] = src;
         const int c = __shfl(mc, src);
-        const float* __restrict__ xr = ep.x + (int64_t)c * ep.ldx;
+        const T* __restrict__ xr = as_t<T>(ep.x) + (int64_t)c * ep.ldx;
 #pragma unroll
         for (int ch = 0; ch < NCH; ++ch) {
           const int cc = (ch * GL + gl) * VEC;
@@ -183,9 +185,9 @@ __global__ __launch_bounds__(256) void agg_kernel(const int4* __restrict__ items
     const int cc = (ch * GL + gl) * VEC;
     if (cc < C) {
       if constexpr (PRE)
-        epi_finish<VEC, STG>(ep, row, cc, acc[ch], a, b, pre[ch]);
+        epi_finish<VEC, STG, T>(ep, row, cc, acc[ch], a, b, pre[ch]);
       else
-        epilogue_store<VEC, STG>(ep, row, cc, acc[ch], a, b);
+        epilogue_store<VEC, STG, T>(ep, row, cc, acc[ch], a, b);
     }
   }
 }
@@ -193,7 +195,7 @@ __global__ __launch_bounds__(256) void agg_kernel(const int4* __restrict__ items
 // Hub rows: sum the chunk partials, then the epilogue.  GL lanes cover the
 // columns; the 64/GL lane groups take chunks g, g+G, ... and are combined by a
 // fixed xor tree (deterministic).
-template <int VEC, int GL, bool STG>
+template <int VEC, int GL, bool STG, class T = float>
 __global__ __launch_bounds__(256) void agg_fixup_kernel(const int4* __restrict__ heavy, int n_heavy, int C, Epi ep,
                                                          const float* __restrict__ partials) {
   constexpr int G = kWave / GL;
@@ -227,27 +229,29 @@ __global__ __launch_bounds__(256) void agg_fixup_kernel(const int4* __restrict__
     for (int o = GL; o < kWave; o <<= 1)
 #pragma unroll
       for (int t = 0; t < VEC; ++t) s[t] += __shfl_xor(s[t], o);
-    if (g == 0 && live) epilogue_store<VEC, STG>(ep, row, cc, s, a, b);
+    if (g == 0 && live) epilogue_store<VEC, STG, T>(ep, row, cc, s, a, b);
   }
 }
 
-template <int VEC, int GL, int NCH, int U, int RPW, class WP>
+template <int VEC, int GL, int NCH, int U, int RPW, class WP, class T = float>
 static int launch_agg_cfg(const int4* items, int64_t n_items, const int4* heavy, int64_t n_heavy, const int* col,
                           const WP& wp, int C, const Epi& ep, float* partials, hipStream_t s) {
   const unsigned grid = (unsigned)ceil_div(n_items, (int64_t)kWavesPerBlock * RPW);
   const unsigned gfix = (unsigned)ceil_div(n_heavy, kWavesPerBlock);
   if (n_items > 0) {
     if (ep.has_stage)
-      agg_kernel<VEC, GL, NCH, U, RPW, true, WP><<<grid, kBlock, 0, s>>>(items, (int)n_items, col, wp, C, ep, partials);
+      agg_kernel<VEC, GL, NCH, U, RPW, true, WP, T><<<grid, kBlock, 0, s>>>(items, (int)n_items, col, wp, C, ep,
+                                                                              partials);
     else
-      agg_kernel<VEC, GL, NCH, U, RPW, false, WP><<<grid, kBlock, 0, s>>>(items, (int)n_items, col, wp, C, ep, partials);
+      agg_kernel<VEC, GL, NCH, U, RPW, false, WP, T><<<grid, kBlock, 0, s>>>(items, (int)n_items, col, wp, C, ep,
+                                                                               partials);
     GNPDE_LAUNCH_CHECK();
   }
   if (n_heavy > 0) {
     if (ep.has_stage)
-      agg_fixup_kernel<VEC, GL, true><<<gfix, kBlock, 0, s>>>(heavy, (int)n_heavy, C, ep, partials);
+      agg_fixup_kernel<VEC, GL, true, T><<<gfix, kBlock, 0, s>>>(heavy, (int)n_heavy, C, ep, partials);
     else
-      agg_fixup_kernel<VEC, GL, false><<<gfix, kBlock, 0, s>>>(heavy, (int)n_heavy, C, ep, partials);
+      agg_fixup_kernel<VEC, GL, false, T><<<gfix, kBlock, 0, s>>>(heavy, (int)n_heavy, C, ep, partials);
     GNPDE_LAUNCH_CHECK();
   }
   return GNPDE_OK;
@@ -257,67 +261,72 @@ static int launch_agg_cfg(const int4* items, int64_t n_items, const int4* heavy,
 // alternative lane geometry for the dominant 32-lane (C = 128 fp32) case.
 int agg_variant();
 
-template <int VEC, class WP>
+template <int VEC, class WP, class T = float>
 static int launch_agg_vec(const int4* items, int64_t n_items, const int4* heavy, int64_t n_heavy, const int* col,
                           const WP& wp, int C, const Epi& ep, float* partials, hipStream_t s) {
   const int lanes = (int)ceil_div(C, VEC);
-  if (lanes <= 16) return launch_agg_cfg<VEC, 16, 1, 4, 1>(items, n_items, heavy, n_heavy, col, wp, C, ep, partials, s);
+#define GNPDE_AGG(GL, NCH, U, RPW) \
+  launch_agg_cfg<VEC, GL, NCH, U, RPW, WP, T>(items, n_items, heavy, n_heavy, col, wp, C, ep, partials, s)
+  if (lanes <= 16) return GNPDE_AGG(16, 1, 4, 1);
   if (lanes <= 32) {
-    switch (agg_variant()) {
-      case 1: return launch_agg_cfg<VEC, 32, 1, 4, 2>(items, n_items, heavy, n_heavy, col, wp, C, ep, partials, s);
-      case 2: return launch_agg_cfg<VEC, 32, 1, 2, 1>(items, n_items, heavy, n_heavy, col, wp, C, ep, partials, s);
-      default: return launch_agg_cfg<VEC, 32, 1, 4, 1>(items, n_items, heavy, n_heavy, col, wp, C, ep, partials, s);
+    if constexpr (sizeof(T) == 4) {
+      switch (agg_variant()) {
+        case 1: return GNPDE_AGG(32, 1, 4, 2);
+        case 2: return GNPDE_AGG(32, 1, 2, 1);
+        default: break;
+      }
     }
+    return GNPDE_AGG(32, 1, 4, 1);
   }
-  if (lanes <= 64) return launch_agg_cfg<VEC, 64, 1, 4, 1>(items, n_items, heavy, n_heavy, col, wp, C, ep, partials, s);
-  if (lanes <= 128) return launch_agg_cfg<VEC, 64, 2, 2, 1>(items, n_items, heavy, n_heavy, col, wp, C, ep, partials, s);
-  if (lanes <= 256) return launch_agg_cfg<VEC, 64, 4, 2, 1>(items, n_items, heavy, n_heavy, col, wp, C, ep, partials, s);
-  if (lanes <= 512) return launch_agg_cfg<VEC, 64, 8, 1, 1>(items, n_items, heavy, n_heavy, col, wp, C, ep, partials, s);
+  if (lanes <= 64) return GNPDE_AGG(64, 1, 4, 1);
+  if (lanes <= 128) return GNPDE_AGG(64, 2, 2, 1);
+  if (lanes <= 256) return GNPDE_AGG(64, 4, 2, 1);
+  if (lanes <= 512) return GNPDE_AGG(64, 8, 1, 1);
+#undef GNPDE_AGG
   set_error("aggregate: C=%d too wide (max %d)", C, 512 * VEC);
   return GNPDE_EUNSUPPORTED;
 }
 
-// Widest vector (4, 2 or 1 floats) every operand of the aggregation and its
-// epilogue allows: C, the leading dimensions and all pointers must agree.
+// Widest vector (elements per lane: 4, 2 or 1 floats; 8, 4, 2 or 1 bf16) every
+// operand of the aggregation and its epilogue allows: C, the leading dimensions
+// and all pointers must agree.
+template <class T = float>
 inline int epi_vec_width(const Epi& ep, int64_t C, const void* partials) {
-  const bool src_ok4 = !(ep.flags & GNPDE_ADD_SOURCE) || (ep.ldx0 % 4 == 0 && aligned16(ep.x0));
-  const bool src_ok2 = !(ep.flags & GNPDE_ADD_SOURCE) || (ep.ldx0 % 2 == 0 && aligned8(ep.x0));
-  bool st4 = true, st2 = true;
-  auto chk = [&](const void* p) {
-    if (p) {
-      st4 = st4 && aligned16(p);
-      st2 = st2 && aligned8(p);
+  constexpr int kMax = 16 / (int)sizeof(T);
+  for (int v = kMax; v > 1; v >>= 1) {
+    const size_t bytes = (size_t)v * sizeof(T);
+    auto al = [&](const void* p) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) % bytes) == 0; };
+    bool ok = C % v == 0 && ep.ldx % v == 0 && ep.ldf % v == 0 && al(ep.x);
+    if (ep.flags & GNPDE_ADD_SOURCE) ok = ok && ep.ldx0 % v == 0 && al(ep.x0);
+    if (ep.has_stage) {
+      ok = ok && al(ep.st.f_out);
+      for (int i = 0; i < ep.st.n_out; ++i) {
+        ok = ok && al(ep.st.o[i].out) && al(ep.st.o[i].base);
+        for (int j = 0; j < ep.st.o[i].nk; ++j) ok = ok && al(ep.st.o[i].k[j]);
+      }
+    } else {
+      ok = ok && al(ep.f);
     }
-  };
-  if (ep.has_stage) {
-    chk(ep.st.f_out);
-    for (int i = 0; i < ep.st.n_out; ++i) {
-      chk(ep.st.o[i].out);
-      chk(ep.st.o[i].base);
-      for (int j = 0; j < ep.st.o[i].nk; ++j) chk(ep.st.o[i].k[j]);
-    }
-  } else {
-    chk(ep.f);
+    // fp32 partials are written with the same lane slices: v floats per lane (16-B pieces at most)
+    ok = ok && (partials == nullptr || (reinterpret_cast<uintptr_t>(partials) % std::min<size_t>(16, 4 * v)) == 0);
+    if (ok) return v;
   }
-  if (C % 4 == 0 && ep.ldx % 4 == 0 && ep.ldf % 4 == 0 && aligned16(ep.x) && st4 && src_ok4 &&
-      (partials == nullptr || aligned16(partials)))
-    return 4;
-  if (C % 2 == 0 && ep.ldx % 2 == 0 && ep.ldf % 2 == 0 && aligned8(ep.x) && st2 && src_ok2 &&
-      (partials == nullptr || aligned8(partials)))
-    return 2;
   return 1;
 }
 
-template <class WP>
+template <class WP, class T = float>
 static int launch_agg(const int32_t* items, int64_t n_items, const int32_t* heavy, int64_t n_heavy,
                       const int32_t* col, const WP& wp, int64_t C, const Epi& ep, float* partials, hipStream_t s) {
   const int4* it = reinterpret_cast<const int4*>(items);
   const int4* hv = reinterpret_cast<const int4*>(heavy);
   const int c = (int)C;
-  switch (epi_vec_width(ep, C, partials)) {
-    case 4: return launch_agg_vec<4>(it, n_items, hv, n_heavy, col, wp, c, ep, partials, s);
-    case 2: return launch_agg_vec<2>(it, n_items, hv, n_heavy, col, wp, c, ep, partials, s);
-    default: return launch_agg_vec<1>(it, n_items, hv, n_heavy, col, wp, c, ep, partials, s);
+  switch (epi_vec_width<T>(ep, C, partials)) {
+    case 8:
+      if constexpr (sizeof(T) == 2) return launch_agg_vec<8, WP, T>(it, n_items, hv, n_heavy, col, wp, c, ep, partials, s);
+      [[fallthrough]];
+    case 4: return launch_agg_vec<4, WP, T>(it, n_items, hv, n_heavy, col, wp, c, ep, partials, s);
+    case 2: return launch_agg_vec<2, WP, T>(it, n_items, hv, n_heavy, col, wp, c, ep, partials, s);
+    default: return launch_agg_vec<1, WP, T>(it, n_items, hv, n_heavy, col, wp, c, ep, partials, s);
   }
 }
 

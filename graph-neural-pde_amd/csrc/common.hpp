@@ -46,7 +46,12 @@ constexpr float kSoftmaxEps = 1e-16f;  // utils.softmax denominator epsilon, src
 // ------------------------------------------------------------------ vector loads
 template <int VEC>
 __device__ __forceinline__ void load_vec(const float* __restrict__ p, float (&v)[VEC]) {
-  if constexpr (VEC == 4) {
+  if constexpr (VEC == 8) {
+    const float4 t = *reinterpret_cast<const float4*>(p);
+    const float4 u = *reinterpret_cast<const float4*>(p + 4);
+    v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+    v[4] = u.x; v[5] = u.y; v[6] = u.z; v[7] = u.w;
+  } else if constexpr (VEC == 4) {
     const float4 t = *reinterpret_cast<const float4*>(p);
     v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
   } else if constexpr (VEC == 2) {
@@ -59,12 +64,73 @@ __device__ __forceinline__ void load_vec(const float* __restrict__ p, float (&v)
 
 template <int VEC>
 __device__ __forceinline__ void store_vec(float* __restrict__ p, const float (&v)[VEC]) {
-  if constexpr (VEC == 4) {
+  if constexpr (VEC == 8) {
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+    *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+  } else if constexpr (VEC == 4) {
     *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
   } else if constexpr (VEC == 2) {
     *reinterpret_cast<float2*>(p) = make_float2(v[0], v[1]);
   } else {
     *p = v[0];
+  }
+}
+
+// bf16 storage (configs[3]): rows are stored as bfloat16, every sum and the
+// epilogue run in fp32; stores round to nearest even (as torch's .to(bfloat16)).
+struct bf16 {
+  uint16_t bits;
+};
+
+__device__ __forceinline__ float bf16_to_f32(uint32_t b) { return __uint_as_float(b << 16); }
+
+__device__ __forceinline__ uint32_t f32_to_bf16(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (u >> 16) | 0x40u;  // quiet NaN
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return u >> 16;
+}
+
+template <int VEC>
+__device__ __forceinline__ void load_vec(const bf16* __restrict__ p, float (&v)[VEC]) {
+  if constexpr (VEC == 8) {
+    const uint4 t = *reinterpret_cast<const uint4*>(p);
+    const uint32_t w[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[2 * i] = bf16_to_f32(w[i] & 0xffffu);
+      v[2 * i + 1] = bf16_to_f32(w[i] >> 16);
+    }
+  } else if constexpr (VEC == 4) {
+    const uint2 t = *reinterpret_cast<const uint2*>(p);
+    v[0] = bf16_to_f32(t.x & 0xffffu); v[1] = bf16_to_f32(t.x >> 16);
+    v[2] = bf16_to_f32(t.y & 0xffffu); v[3] = bf16_to_f32(t.y >> 16);
+  } else if constexpr (VEC == 2) {
+    const uint32_t t = *reinterpret_cast<const uint32_t*>(p);
+    v[0] = bf16_to_f32(t & 0xffffu); v[1] = bf16_to_f32(t >> 16);
+  } else {
+    v[0] = bf16_to_f32(p->bits);
+  }
+}
+
+template <int VEC>
+__device__ __forceinline__ void store_vec(bf16* __restrict__ p, const float (&v)[VEC]) {
+  if constexpr (VEC == 8) {
+    uint4 t;
+    t.x = f32_to_bf16(v[0]) | (f32_to_bf16(v[1]) << 16);
+    t.y = f32_to_bf16(v[2]) | (f32_to_bf16(v[3]) << 16);
+    t.z = f32_to_bf16(v[4]) | (f32_to_bf16(v[5]) << 16);
+    t.w = f32_to_bf16(v[6]) | (f32_to_bf16(v[7]) << 16);
+    *reinterpret_cast<uint4*>(p) = t;
+  } else if constexpr (VEC == 4) {
+    uint2 t;
+    t.x = f32_to_bf16(v[0]) | (f32_to_bf16(v[1]) << 16);
+    t.y = f32_to_bf16(v[2]) | (f32_to_bf16(v[3]) << 16);
+    *reinterpret_cast<uint2*>(p) = t;
+  } else if constexpr (VEC == 2) {
+    *reinterpret_cast<uint32_t*>(p) = f32_to_bf16(v[0]) | (f32_to_bf16(v[1]) << 16);
+  } else {
+    p->bits = (uint16_t)f32_to_bf16(v[0]);
   }
 }
 
@@ -122,28 +188,40 @@ struct EpiPre {
   float kv[GNPDE_STAGE_MAX_OUT][GNPDE_STAGE_MAX_K][VEC];
 };
 
-template <int VEC, bool STG>
+// The Epi / stage pointers are declared float*; for bf16 storage they address
+// bf16 arrays (gnpde_spmm_rhs_bf16) and are read through T.
+template <class T>
+__device__ __forceinline__ const T* as_t(const float* p) {
+  return reinterpret_cast<const T*>(p);
+}
+template <class T>
+__device__ __forceinline__ T* as_t(float* p) {
+  return reinterpret_cast<T*>(p);
+}
+
+template <int VEC, bool STG, class T = float>
 __device__ __forceinline__ void epi_prefetch(const Epi& e, int64_t row, int cc, EpiPre<VEC>& p) {
   const bool need_x = (e.flags & GNPDE_EPI_RHS) != 0;
-  if (need_x) load_vec<VEC>(e.x + row * e.ldx + cc, p.xr);
-  if (e.flags & GNPDE_ADD_SOURCE) load_vec<VEC>(e.x0 + row * e.ldx0 + cc, p.x0r);
+  if (need_x) load_vec<VEC>(as_t<T>(e.x) + row * e.ldx + cc, p.xr);
+  if (e.flags & GNPDE_ADD_SOURCE) load_vec<VEC>(as_t<T>(e.x0) + row * e.ldx0 + cc, p.x0r);
   if constexpr (!STG) return;
   const int64_t off = row * e.ldf + cc;
 #pragma unroll
   for (int i = 0; i < GNPDE_STAGE_MAX_OUT; ++i) {
     if (i < e.st.n_out) {
       const gnpde_stage_out_t& so = e.st.o[i];
-      if (so.base != nullptr && !(need_x && so.base == e.x && e.ldx == e.ldf)) load_vec<VEC>(so.base + off, p.base[i]);
+      if (so.base != nullptr && !(need_x && so.base == e.x && e.ldx == e.ldf))
+        load_vec<VEC>(as_t<T>(so.base) + off, p.base[i]);
 #pragma unroll
       for (int j = 0; j < GNPDE_STAGE_MAX_K; ++j)
-        if (j < so.nk) load_vec<VEC>(so.k[j] + off, p.kv[i][j]);
+        if (j < so.nk) load_vec<VEC>(as_t<T>(so.k[j]) + off, p.kv[i][j]);
     }
   }
 }
 
 // f = a*(ax - x) [+ b*x0]  (function_laplacian_diffusion.py:69-77) or f = ax,
 // then either store f or emit the fused Runge-Kutta stage outputs.
-template <int VEC, bool STG>
+template <int VEC, bool STG, class T = float>
 __device__ __forceinline__ void epi_finish(const Epi& e, int64_t row, int cc, const float (&ax)[VEC], float a,
                                            float b, const EpiPre<VEC>& p) {
   float o[VEC];
@@ -160,11 +238,11 @@ __device__ __forceinline__ void epi_finish(const Epi& e, int64_t row, int cc, co
     for (int t = 0; t < VEC; ++t) o[t] = ax[t];
   }
   if constexpr (!STG) {
-    store_vec<VEC>(e.f + row * e.ldf + cc, o);
+    store_vec<VEC>(as_t<T>(e.f) + row * e.ldf + cc, o);
     return;
   }
   const int64_t off = row * e.ldf + cc;
-  if (e.st.f_out) store_vec<VEC>(e.st.f_out + off, o);
+  if (e.st.f_out) store_vec<VEC>(as_t<T>(e.st.f_out) + off, o);
 #pragma unroll
   for (int i = 0; i < GNPDE_STAGE_MAX_OUT; ++i) {
     if (i >= e.st.n_out) break;
@@ -189,16 +267,16 @@ __device__ __forceinline__ void epi_finish(const Epi& e, int64_t row, int cc, co
     }
 #pragma unroll
     for (int t = 0; t < VEC; ++t) r[t] = fmaf(so.cf, o[t], r[t]);
-    store_vec<VEC>(so.out + off, r);
+    store_vec<VEC>(as_t<T>(so.out) + off, r);
   }
 }
 
-template <int VEC, bool STG>
+template <int VEC, bool STG, class T = float>
 __device__ __forceinline__ void epilogue_store(const Epi& e, int64_t row, int cc, const float (&ax)[VEC], float a,
                                                float b) {
   EpiPre<VEC> p;
-  epi_prefetch<VEC, STG>(e, row, cc, p);
-  epi_finish<VEC, STG>(e, row, cc, ax, a, b, p);
+  epi_prefetch<VEC, STG, T>(e, row, cc, p);
+  epi_finish<VEC, STG, T>(e, row, cc, ax, a, b, p);
 }
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }

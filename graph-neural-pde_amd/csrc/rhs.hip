@@ -680,6 +680,20 @@ int gnpde_spmm_rhs_f32(const int32_t* items, int64_t n_items, const int32_t* hea
   return launch_agg(items, n_items, heavy, n_heavy, col, wp, C, ep, partials, as_stream(stream));
 }
 
+int gnpde_spmm_rhs_bf16(const int32_t* items, int64_t n_items, const int32_t* heavy, int64_t n_heavy,
+                        const int32_t* col, const float* w, int64_t C, const uint16_t* x, int64_t ldx,
+                        const uint16_t* x0, int64_t ldx0, const float* alpha, const float* beta, int flags, uint16_t* f,
+                        int64_t ldf, float* partials, const gnpde_stage_epilogue_t* stage, void* stream) {
+  const Epi ep = make_epi(reinterpret_cast<const float*>(x), ldx, reinterpret_cast<const float*>(x0), ldx0, alpha,
+                          beta, flags, reinterpret_cast<float*>(f), ldf, stage);
+  int rc = check_epi(ep, C, n_heavy, partials);
+  if (rc) return rc;
+  GNPDE_REQUIRE(n_items >= 0 && n_items < INT32_MAX && n_heavy >= 0, GNPDE_EINVAL, "spmm_rhs_bf16: bad item counts");
+  GNPDE_REQUIRE(n_items == 0 || (items && col && w), GNPDE_EINVAL, "spmm_rhs_bf16: NULL plan/col/w");
+  PlainWeights wp{w};
+  return launch_agg<PlainWeights, bf16>(items, n_items, heavy, n_heavy, col, wp, C, ep, partials, as_stream(stream));
+}
+
 int gnpde_attn_ref_rhs_f32(const int32_t* items, int64_t n_items, const int32_t* heavy, int64_t n_heavy,
                            const int32_t* col, const double* cs, const double* m, const float* rl, int64_t heads,
                            int64_t C, const float* x, int64_t ldx, const float* x0, int64_t ldx0, const float* alpha,

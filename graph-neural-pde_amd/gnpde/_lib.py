@@ -54,6 +54,8 @@ SIGNATURES = {
                                 _size, _vp]),
     "gnpde_spmm_rhs_f32": (_int, [_vp, _i64, _vp, _i64, _vp, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _int, _vp,
                                   _i64, _vp, ctypes.POINTER(StageEpilogue), _vp]),
+    "gnpde_spmm_rhs_bf16": (_int, [_vp, _i64, _vp, _i64, _vp, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _int, _vp,
+                                   _i64, _vp, ctypes.POINTER(StageEpilogue), _vp]),
     "gnpde_attn_ref_rhs_f32": (_int, [_vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _i64, _i64, _vp, _i64, _vp, _i64,
                                       _vp, _vp, _int, _vp, _i64, _vp, ctypes.POINTER(StageEpilogue), _vp]),
     "gnpde_linear_f32": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _vp]),

@@ -110,6 +110,8 @@ class LaplacianODEFunc(ODEFunc):
         w, tag = self._weights_tensor()
         add_source = bool(self.opt.get('add_source', False))
         x0 = self.x0 if add_source else None
+        if x0 is not None and x0.dtype != x.dtype:
+            x0 = x0.to(x.dtype)
         ops.spmm_rhs(g, self.csr_weights(g, w, tag), x, x0=x0, alpha=self.alpha_train.detach(),
                      beta=self.beta_train.detach(), rhs=True, alpha_sigmoid=not self.opt.get('no_alpha_sigmoid', False),
                      add_source=add_source, stage=stage)
@@ -126,8 +128,14 @@ class LaplacianODEFunc(ODEFunc):
             raise RuntimeError("LaplacianODEFunc: add_source needs x0 (ODEblock.set_x0)")
         alpha_sigmoid = not self.opt.get('no_alpha_sigmoid', False)
         x0 = self.x0 if add_source else None
-        if x0 is not None and x0.dtype != torch.float32:
-            x0 = x0.float()
+        if x0 is not None and x0.dtype != x.dtype:
+            x0 = x0.to(x.dtype)
+        if x.dtype == torch.bfloat16:
+            # bf16 storage (configs[3]): inference only — the backward kernels are fp32
+            if torch.is_grad_enabled() and (x.requires_grad or self.alpha_train.requires_grad):
+                raise NotImplementedError("gnpde: bf16 state is inference-only; run under torch.no_grad()")
+            return ops.spmm_rhs(g, w_csr, x, x0=x0, alpha=self.alpha_train.detach(), beta=self.beta_train.detach(),
+                                rhs=True, alpha_sigmoid=alpha_sigmoid, add_source=add_source)
         return _LaplacianRHS.apply(x, self.alpha_train, self.beta_train, w, g, w_csr,
                                    lambda: self.csr_weights(g, w, tag, transpose=True), x0, alpha_sigmoid,
                                    add_source)

@@ -304,11 +304,19 @@ class ODEFuncTransformerAtt(ODEFunc):
         add_source = bool(self.opt.get('add_source', False))
         if add_source and self.x0 is None:
             raise RuntimeError("ODEFuncTransformerAtt: add_source needs x0 (ODEblock.set_x0)")
-        kw = dict(x0=self.x0 if add_source else None, alpha=self.alpha_train.detach(), beta=self.beta_train.detach(),
+        x0 = self.x0 if add_source else None
+        if x0 is not None and x0.dtype != x.dtype:
+            x0 = x0.to(x.dtype)
+        kw = dict(x0=x0, alpha=self.alpha_train.detach(), beta=self.beta_train.detach(),
                   rhs=True, alpha_sigmoid=not self.opt.get('no_alpha_sigmoid', False), add_source=add_source,
                   stage=stage)
         if lay.is_uniform(norm_idx):
             return ops.spmm_rhs(g, lay.uniform_weights(g), x, **kw)
+        if x.dtype == torch.bfloat16:
+            # bf16 storage: scores from an fp32 copy of the state, weights precomputed, bf16 aggregation
+            ns = lay.node_scores(g, x.float())
+            m, rl = ops.softmax_stats(g, ns, 1) if norm_idx == 1 else (None, None)
+            return ops.attn_rhs(g, ns, m, rl, norm_idx, x, fuse=False, **kw)
         ns = lay.node_scores(g, x)
         # destination-grouped softmax needs its statistics over the CSC first;
         # source-grouped weights come straight from the scores (K2)

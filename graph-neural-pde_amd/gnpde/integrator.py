@@ -62,6 +62,10 @@ class _Combine(object):
     def __call__(self, y0, ks, coefs, scale):
         if torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in [y0] + list(ks)):
             return _torch_combine(y0, ks, coefs, scale)
+        if ks[0].dtype == torch.bfloat16:
+            # bf16 state outside the fused fixed-grid path (dopri5): fp32 combination, one rounding
+            acc = _torch_combine(None if y0 is None else y0.float(), [k.float() for k in ks], coefs, scale)
+            return acc.to(torch.bfloat16)
         return ops.rk_combine(y0, ks, coefs, scale).view(ks[0].shape)
 
 
@@ -117,7 +121,7 @@ def _fixed_step(method, func, t0, dt, t1, y0, combine):
 def _fusable(func, y0, combine):
     """The RHS can emit the stage combinations itself (gnpde ODEFuncs, no autograd)."""
     return (isinstance(combine, _Combine) and hasattr(func, 'rhs_stage') and y0.is_cuda and
-            y0.dtype == torch.float32 and not torch.is_grad_enabled())
+            y0.dtype in ops.STATE_DTYPES and not torch.is_grad_enabled())
 
 
 RHS_PER_STEP = {'euler': 1, 'midpoint': 2, 'rk4': 4}

@@ -38,11 +38,14 @@ def _require_gpu(t, name, dtype=None):
         raise TypeError("gnpde: %s must be %s, got %s" % (name, dtype, t.dtype))
 
 
-def _rows(x, name):
-    """[B,N,C] or [R,C] fp32 -> contiguous [R,C] view."""
-    _require_gpu(x, name, torch.float32)
+def _rows(x, name, dtype=torch.float32):
+    """[B,N,C] or [R,C] -> contiguous [R,C] view (fp32 unless stated)."""
+    _require_gpu(x, name, dtype)
     x = x.contiguous()
     return x.reshape(-1, x.shape[-1])
+
+
+STATE_DTYPES = (torch.float32, torch.bfloat16)  # K1 storage types (fp32 math either way)
 
 
 # --------------------------------------------------------------------------- graph
@@ -348,14 +351,17 @@ class Stage(object):
 
 def spmm_rhs(g, w_csr, x, x0=None, alpha=None, beta=None, rhs=True, alpha_sigmoid=True, add_source=False,
              out=None, transpose=False, stage=None):
-    """K1: f = a*(A x - x) [+ b*x0] (or A x with rhs=False).  x [B,N,C] fp32.
+    """K1: f = a*(A x - x) [+ b*x0] (or A x with rhs=False).  x [B,N,C] fp32, or
+    bf16 storage (gnpde_spmm_rhs_bf16: x, x0, f and stage tensors bf16, sums in
+    fp32).
 
     transpose=True aggregates over the CSC instead (A^T x; ``w_csr`` must then
     be in CSC order) — the backward of the RHS with respect to x.
     stage: a ``Stage`` -> the fused Runge-Kutta outputs are written instead of f
     (returns None)."""
     shape = x.shape
-    xr = _rows(x, "x")
+    dt = x.dtype if isinstance(x, torch.Tensor) and x.dtype in STATE_DTYPES else torch.float32
+    xr = _rows(x, "x", dt)
     C = xr.shape[1]
     if xr.shape[0] != g.R:
         raise ValueError("x has %d rows, graph has %d" % (xr.shape[0], g.R))
@@ -364,11 +370,11 @@ def spmm_rhs(g, w_csr, x, x0=None, alpha=None, beta=None, rhs=True, alpha_sigmoi
     if rhs and a is None:
         raise ValueError("spmm_rhs: alpha required")
     b = _scalar(beta, "beta", dev) if add_source else None
-    x0r = _rows(x0, "x0") if add_source else None
+    x0r = _rows(x0, "x0", dt) if add_source else None
     st = None
     if stage is not None:
         for t in stage.tensors():
-            _require_gpu(t, "stage tensor", torch.float32)
+            _require_gpu(t, "stage tensor", dt)
             if not t.is_contiguous() or t.numel() != xr.numel():
                 raise ValueError("stage tensors must be contiguous and shaped like x")
         st = ctypes.byref(stage.struct(xr))
@@ -379,7 +385,12 @@ def spmm_rhs(g, w_csr, x, x0=None, alpha=None, beta=None, rhs=True, alpha_sigmoi
     partials = torch.empty(plan.n_slots * C, dtype=torch.float32, device=dev) if plan.n_slots else None
     epi = (C, _ptr(xr), C, _ptr(x0r), C, _ptr(a), _ptr(b), _flags(rhs, alpha_sigmoid, add_source), _ptr(out), C,
            _ptr(partials), st, _stream(dev))
-    if isinstance(w_csr, RefDstWeights):
+    if dt == torch.bfloat16:
+        if isinstance(w_csr, RefDstWeights):
+            raise ValueError("bf16 storage takes precomputed weights (attn_rhs(..., fuse=False))")
+        _lib.call("gnpde_spmm_rhs_bf16", _ptr(plan.items), plan.n_items, _ptr(plan.heavy), plan.n_heavy,
+                  _ptr(grouped.col), _ptr(w_csr), *epi)
+    elif isinstance(w_csr, RefDstWeights):
         if transpose:
             raise ValueError("on-the-fly attention weights aggregate over the CSR only")
         _lib.call("gnpde_attn_ref_rhs_f32", _ptr(plan.items), plan.n_items, _ptr(plan.heavy), plan.n_heavy,
@@ -586,7 +597,7 @@ def attn_rhs(g, ns, m, rl, norm_idx, x, x0=None, alpha=None, beta=None, rhs=True
     (m, rl: destination statistics for norm_idx 1, or None to compute them).
     Reference scores under norm_idx 1 (fuse=True): the weights are computed
     inside K1 from (cs, m, rl) — same bits as the separate weights pass."""
-    if fuse and norm_idx == 1 and ns.mode == _lib.SCORE_REFERENCE:
+    if fuse and norm_idx == 1 and ns.mode == _lib.SCORE_REFERENCE and x.dtype == torch.float32:
         if m is None:
             m, rl = softmax_stats(g, ns, 1, seg=seg)
         w = RefDstWeights(ns.cs, m, rl, ns.heads)

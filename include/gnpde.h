@@ -174,6 +174,16 @@ int gnpde_spmm_rhs_f32(const int32_t* items, int64_t n_items, const int32_t* hea
                        float* f, int64_t ldf, float* partials, const gnpde_stage_epilogue_t* stage,
                        void* stream);
 
+/* K1 on bfloat16 storage (configs[3], BLEND in bf16): x, x0, f and every
+ * stage pointer of `stage` address bf16 arrays (raw uint16 bits; the stage
+ * struct's float* fields are reinterpreted); weights, alpha, beta and the
+ * partials stay fp32, and every sum and the epilogue run in fp32 — only the
+ * stored rows are rounded (nearest even).  Otherwise as gnpde_spmm_rhs_f32.  */
+int gnpde_spmm_rhs_bf16(const int32_t* items, int64_t n_items, const int32_t* heavy, int64_t n_heavy,
+                        const int32_t* col, const float* w, int64_t C, const uint16_t* x, int64_t ldx,
+                        const uint16_t* x0, int64_t ldx0, const float* alpha, const float* beta, int flags, uint16_t* f,
+                        int64_t ldf, float* partials, const gnpde_stage_epilogue_t* stage, void* stream);
+
 /* K1 with the attention weights computed on the fly for the fork's scaled_dot
  * (reference score mode) under destination-grouped softmax (attention_norm_idx
  * 1): w_p = mean_h exp(cs[row,h] - m[col_p,h]) * rl[col_p,h], cs [R,H] fp64 node

@@ -831,3 +831,78 @@ def test_graph_replay_respects_max_nfe():
         gnpde.odeint(func, T(rng.standard_normal((1, N, C)).astype(np.float32)),
                      torch.tensor([0.0, 5.0], device=DEV), method='rk4', options={'step_size': 0.1})
     assert func.nfe == 38  # raised at the call after nfe passed max_nfe, as the eager reference does
+
+
+# ---------------------------------------------------------------- bf16 storage (configs[3])
+BF16_TOL = 2e-2   # bf16 against the fp32 oracle
+BF16_ROUND = 4e-3  # against the oracle on the same bf16-rounded inputs: output rounding only (2^-9 relative)
+
+
+def _bf16_round(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(torch.bfloat16).float().numpy()
+
+
+@pytest.mark.parametrize("C", [7, 16, 128, 162, 256])
+def test_spmm_rhs_bf16_vs_oracle(C):
+    N, E = 2000, 30000
+    ei = hub_graph(N, E, seed=70 + C)
+    rng = np.random.default_rng(71)
+    w = rng.uniform(0.1, 1, size=(1, E)).astype(np.float32)
+    x = rng.standard_normal((1, N, C)).astype(np.float32)
+    x0 = rng.standard_normal((1, N, C)).astype(np.float32)
+    g = ops.GraphCSR(T(ei), N)
+    wc = g.gather_weights(T(w))
+    xb, x0b = T(x).to(torch.bfloat16), T(x0).to(torch.bfloat16)
+    f = ops.spmm_rhs(g, wc, xb, x0=x0b, alpha=torch.tensor(0.3, device=DEV), beta=torch.tensor(0.7, device=DEV),
+                     add_source=True)
+    assert f.dtype == torch.bfloat16
+    want_rounded = O.laplacian_rhs(ei, _bf16_round(x), _bf16_round(x0), 0.3, 0.7, edge_weight=w, add_source=True)
+    want = O.laplacian_rhs(ei, x, x0, 0.3, 0.7, edge_weight=w, add_source=True)
+    assert rel(f.float(), want_rounded) <= BF16_ROUND
+    assert rel(f.float(), want) <= BF16_TOL
+    # the fp32 kernel on the rounded inputs, rounded once at the store: within one bf16 rounding
+    # (bf16 rows take 8 columns per lane, fp32 rows 4: the edge interleave, hence the fp32 sum order, differs)
+    f32 = ops.spmm_rhs(g, wc, xb.float(), x0=x0b.float(), alpha=torch.tensor(0.3, device=DEV),
+                       beta=torch.tensor(0.7, device=DEV), add_source=True)
+    assert bool(((f.float() - f32).abs() <= f32.abs() * 2.0 ** -8 + 1e-6).all())
+
+
+@pytest.mark.parametrize("method", ["euler", "rk4"])
+def test_blend_bf16_integration_vs_oracle(method):
+    """configs[3] shape in miniature: transformer function with the fork's scaled_dot
+    under source-grouped softmax (uniform 1/outdeg weights), C = 162, bf16 state,
+    fused fixed-grid steps (graph-replayed), against the fp32 oracle."""
+    N, E, C = 3000, 24000, 162
+    rng = np.random.default_rng(72)
+    ei = rng.integers(0, N, size=(1, 2, E))
+    x = rng.standard_normal((1, N, C)).astype(np.float32)
+    opt = dict(OPT, hidden_dim=C, heads=2, attention_dim=32, function='transformer', attention_norm_idx=0)
+    func = gnpde.ODEFuncTransformerAtt(C, C, opt, DEV).to(DEV)
+    func.edge_index = T(ei)
+    with torch.no_grad():
+        z = gnpde.odeint(func, T(x).to(torch.bfloat16), torch.tensor([0.0, 1.0], device=DEV), method=method,
+                         options={'step_size': 0.125})
+    assert z.dtype == torch.bfloat16
+    outdeg = np.bincount(ei[0, 0], minlength=N).astype(np.float64)
+    wu = 1.0 / (outdeg[ei[0, 0]] + 1e-16)
+    f = lambda t, y: O.laplacian_rhs(ei, y, None, 0.0, 0.0, edge_weight=wu[None])  # noqa: E731
+    want = O.odeint_fixed(f, x, 0.0, 1.0, method, 0.125)
+    assert rel(z[1].float(), want) <= BF16_TOL
+
+
+def test_bf16_attention_reference_norm1_rhs():
+    """Non-uniform scores in bf16: scores from an fp32 copy, precomputed weights, bf16 aggregation."""
+    N, E, C, h, att = 1500, 12000, 64, 2, 32
+    ei, x, _, Wq, bq, Wk, bk = _attn_case(N, E, C, h, att, seed=73, B=1, wscale=0.05)
+    opt = dict(OPT, hidden_dim=C, heads=h, attention_dim=att, function='transformer', attention_norm_idx=1)
+    func = gnpde.ODEFuncTransformerAtt(C, C, opt, DEV).to(DEV)
+    _set_qk(func.multihead_att_layer, np.random.default_rng(0), C, att)
+    with torch.no_grad():
+        lay = func.multihead_att_layer
+        Wq, bq, Wk, bk = [t.detach().cpu().numpy() for t in (lay.Q.weight, lay.Q.bias, lay.K.weight, lay.K.bias)]
+        func.alpha_train.fill_(0.2)
+    func.edge_index = T(ei)
+    with torch.no_grad():
+        f = func(0, T(x).to(torch.bfloat16))
+    want = O.transformer_rhs(ei, _bf16_round(x), None, Wq, bq, Wk, bk, h, 1, 0.2, 0.0)
+    assert f.dtype == torch.bfloat16 and rel(f.float(), want) <= BF16_ROUND
