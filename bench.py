@@ -235,6 +235,7 @@ def main():
 
     if not args.no_attention and rank == 0:
         result["attention"] = bench_attention(g, x, dev, ops)
+        result["blend_c162"] = bench_blend(g, dev)
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(ei, w, x, N, E, C, args.cpu_seconds)
@@ -338,6 +339,42 @@ def bench_attention(g, x, dev, ops, reps=20):
         gbs = nb / (ms * 1e-3) / 1e9
         out["%s_norm%d" % (mode, norm_idx)] = {"rhs_ms": round(ms, 4), "achieved_GBs": round(gbs, 1),
                                                "frac": round(gbs / HBM_PEAK_GBS, 4), "algorithmic_bytes": nb}
+    return out
+
+
+def bench_blend(g, dev, reps=50):
+    """configs[3] shape: the BLEND transformer RHS (fork scaled_dot under
+    source-grouped softmax -> cached 1/outdeg weights), C = 162 (64 features +
+    98 positional), one rk4 step per 4 RHS, fp32 and bf16 state storage."""
+    import gnpde
+    from gnpde import synthetic
+    C = 162
+    opt = {'hidden_dim': C, 'heads': 2, 'attention_dim': 32, 'attention_norm_idx': 0, 'attention_type': 'scaled_dot',
+           'function': 'transformer', 'add_source': False, 'no_alpha_sigmoid': False, 'max_nfe': 10 ** 9,
+           'multi_modal': False, 'mix_features': False, 'square_plus': False, 'beltrami': False}
+    out = {"config": "BLEND transformer RHS, fork scaled_dot norm_idx 0 (uniform weights), C=162, rk4 steps "
+                     "(configs[3] shape on the G-arxiv graph)"}
+    x32 = synthetic.features(1, g.N, C, seed=3, device=dev)
+    for name, dt in (("fp32", torch.float32), ("bf16", torch.bfloat16)):
+        func = gnpde.ODEFuncTransformerAtt(C, C, opt, dev).to(dev).eval()
+        func.edge_index = g.edge_index
+        x = x32.to(dt)
+        with torch.no_grad():
+            t = torch.tensor([0.0, 0.25 * reps], device=dev)
+            gnpde.odeint(func, x, t, method='rk4', options={'step_size': 0.25})  # warm-up: same call
+            torch.cuda.synchronize()
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            gnpde.odeint(func, x, t, method='rk4', options={'step_size': 0.25})
+            e.record()
+            torch.cuda.synchronize()
+        ms = s.elapsed_time(e) / reps
+        es = 2 if dt == torch.bfloat16 else 4
+        # per step: 4 x (gathers es*EC + CSR/weights 8E + 4(N+1) + own row es*NC) + 8 state passes es*NC
+        nb = 4 * (es * g.nnz * C + 8 * g.nnz + 4 * (g.N + 1) + es * g.N * C) + 8 * es * g.N * C
+        gbs = nb / (ms * 1e-3) / 1e9
+        out[name] = {"ms_per_step": round(ms, 4), "rhs_per_s": round(4e3 / ms, 1), "achieved_GBs": round(gbs, 1),
+                     "frac": round(gbs / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_step": nb}
     return out
 
 

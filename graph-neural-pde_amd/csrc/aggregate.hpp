@@ -97,7 +97,7 @@ __global__ __launch_bounds__(256) void agg_kernel(const int4* __restrict__ items
   const int row = it.x, beg = it.y, end = it.z, slot = it.w;
   const bool owner = live && slot < 0 && g == 0;
 
-  EpiPre<VEC> pre[PRE ? NCH : 1];
+  EpiPre<VEC, T> pre[PRE ? NCH : 1];
   if constexpr (PRE) {
     if (owner) {
 #pragma unroll
@@ -124,7 +124,7 @@ __global__ __launch_bounds__(256) void agg_kernel(const int4* __restrict__ items
     }
     float mw = 0.f;
     for (int j = 0; j < n; j += G * U) {
-      float v[U][NCH][VEC];
+      Packed<VEC, T> v[U][NCH];  // gathered row slices in storage form (bf16: half the registers)
       float ww[U];
       int srcl[U];
 #pragma unroll
@@ -138,10 +138,10 @@ __global__ __launch_bounds__(256) void agg_kernel(const int4* __restrict__ items
         for (int ch = 0; ch < NCH; ++ch) {
           const int cc = (ch * GL + gl) * VEC;
           if (jj < n && cc < C) {
-            load_vec<VEC>(xr + cc, v[u][ch]);
+            load_packed<VEC>(xr + cc, v[u][ch]);
           } else {
 #pragma unroll
-            for (int t = 0; t < VEC; ++t) v[u][ch][t] = 0.f;
+            for (int t = 0; t < Packed<VEC, T>::W; ++t) v[u][ch].d[t] = 0u;
           }
         }
       }
@@ -158,7 +158,7 @@ __global__ __launch_bounds__(256) void agg_kernel(const int4* __restrict__ items
 #pragma unroll
         for (int ch = 0; ch < NCH; ++ch)
 #pragma unroll
-          for (int t = 0; t < VEC; ++t) acc[ch][t] = fmaf(ww[u], v[u][ch][t], acc[ch][t]);
+          for (int t = 0; t < VEC; ++t) acc[ch][t] = fmaf(ww[u], unpack(v[u][ch], t), acc[ch][t]);
     }
   }
   // combine the G edge groups of each slot
@@ -269,16 +269,18 @@ static int launch_agg_vec(const int4* items, int64_t n_items, const int4* heavy,
   launch_agg_cfg<VEC, GL, NCH, U, RPW, WP, T>(items, n_items, heavy, n_heavy, col, wp, C, ep, partials, s)
   if (lanes <= 16) return GNPDE_AGG(16, 1, 4, 1);
   if (lanes <= 32) {
-    if constexpr (sizeof(T) == 4) {
-      switch (agg_variant()) {
-        case 1: return GNPDE_AGG(32, 1, 4, 2);
-        case 2: return GNPDE_AGG(32, 1, 2, 1);
-        default: break;
-      }
+    switch (agg_variant()) {
+      case 1: return GNPDE_AGG(32, 1, 4, 2);
+      case 2: return GNPDE_AGG(32, 1, 2, 1);
+      case 3: return GNPDE_AGG(32, 1, 8, 1);
+      default: break;
     }
     return GNPDE_AGG(32, 1, 4, 1);
   }
-  if (lanes <= 64) return GNPDE_AGG(64, 1, 4, 1);
+  if (lanes <= 64) {
+    if (agg_variant() == 3) return GNPDE_AGG(64, 1, 8, 1);
+    return GNPDE_AGG(64, 1, 4, 1);
+  }
   if (lanes <= 128) return GNPDE_AGG(64, 2, 2, 1);
   if (lanes <= 256) return GNPDE_AGG(64, 4, 2, 1);
   if (lanes <= 512) return GNPDE_AGG(64, 8, 1, 1);
@@ -290,9 +292,13 @@ static int launch_agg_vec(const int4* items, int64_t n_items, const int4* heavy,
 // Widest vector (elements per lane: 4, 2 or 1 floats; 8, 4, 2 or 1 bf16) every
 // operand of the aggregation and its epilogue allows: C, the leading dimensions
 // and all pointers must agree.
+// Experiment knob (not part of the ABI contract): GNPDE_BF16_VEC caps the
+// elements per lane of bf16 rows (default 4 = 8-byte gathers; 8 = 16-byte).
+int bf16_vec_cap();
+
 template <class T = float>
 inline int epi_vec_width(const Epi& ep, int64_t C, const void* partials) {
-  constexpr int kMax = 16 / (int)sizeof(T);
+  const int kMax = sizeof(T) == 2 ? bf16_vec_cap() : 16 / (int)sizeof(T);
   for (int v = kMax; v > 1; v >>= 1) {
     const size_t bytes = (size_t)v * sizeof(T);
     auto al = [&](const void* p) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) % bytes) == 0; };

@@ -180,12 +180,56 @@ __device__ __forceinline__ float epi_alpha(const Epi& e) {
 
 // Epilogue operands of one row slice, loaded ahead of the aggregation so their
 // latency overlaps the gathers (they depend only on the row).
+// A row slice kept in its storage form (VEC elements of T as raw dwords) until
+// it is used: bf16 operands held across the gather loop cost half the
+// registers of their fp32 conversion.
+template <int VEC, class T>
+struct Packed {
+  static constexpr int W = (VEC * (int)sizeof(T) + 3) / 4;
+  uint32_t d[W];
+};
+
 template <int VEC>
+__device__ __forceinline__ void load_packed(const float* __restrict__ p, Packed<VEC, float>& r) {
+  float v[VEC];
+  load_vec<VEC>(p, v);
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) r.d[i] = __float_as_uint(v[i]);
+}
+
+template <int VEC>
+__device__ __forceinline__ void load_packed(const bf16* __restrict__ p, Packed<VEC, bf16>& r) {
+  if constexpr (VEC == 8) {
+    const uint4 t = *reinterpret_cast<const uint4*>(p);
+    r.d[0] = t.x; r.d[1] = t.y; r.d[2] = t.z; r.d[3] = t.w;
+  } else if constexpr (VEC == 4) {
+    const uint2 t = *reinterpret_cast<const uint2*>(p);
+    r.d[0] = t.x; r.d[1] = t.y;
+  } else if constexpr (VEC == 2) {
+    r.d[0] = *reinterpret_cast<const uint32_t*>(p);
+  } else {
+    r.d[0] = p->bits;
+  }
+}
+
+template <int VEC>
+__device__ __forceinline__ float unpack(const Packed<VEC, float>& r, int t) {
+  return __uint_as_float(r.d[t]);
+}
+
+template <int VEC>
+__device__ __forceinline__ float unpack(const Packed<VEC, bf16>& r, int t) {
+  return bf16_to_f32((t & 1) ? (r.d[t >> 1] >> 16) : (r.d[t >> 1] & 0xffffu));
+}
+
+// Epilogue operands of one row slice, loaded ahead of the aggregation so their
+// latency overlaps the gathers (they depend only on the row).
+template <int VEC, class T = float>
 struct EpiPre {
-  float xr[VEC];
-  float x0r[VEC];
-  float base[GNPDE_STAGE_MAX_OUT][VEC];
-  float kv[GNPDE_STAGE_MAX_OUT][GNPDE_STAGE_MAX_K][VEC];
+  Packed<VEC, T> xr;
+  Packed<VEC, T> x0r;
+  Packed<VEC, T> base[GNPDE_STAGE_MAX_OUT];
+  Packed<VEC, T> kv[GNPDE_STAGE_MAX_OUT][GNPDE_STAGE_MAX_K];
 };
 
 // The Epi / stage pointers are declared float*; for bf16 storage they address
@@ -200,10 +244,10 @@ __device__ __forceinline__ T* as_t(float* p) {
 }
 
 template <int VEC, bool STG, class T = float>
-__device__ __forceinline__ void epi_prefetch(const Epi& e, int64_t row, int cc, EpiPre<VEC>& p) {
+__device__ __forceinline__ void epi_prefetch(const Epi& e, int64_t row, int cc, EpiPre<VEC, T>& p) {
   const bool need_x = (e.flags & GNPDE_EPI_RHS) != 0;
-  if (need_x) load_vec<VEC>(as_t<T>(e.x) + row * e.ldx + cc, p.xr);
-  if (e.flags & GNPDE_ADD_SOURCE) load_vec<VEC>(as_t<T>(e.x0) + row * e.ldx0 + cc, p.x0r);
+  if (need_x) load_packed<VEC>(as_t<T>(e.x) + row * e.ldx + cc, p.xr);
+  if (e.flags & GNPDE_ADD_SOURCE) load_packed<VEC>(as_t<T>(e.x0) + row * e.ldx0 + cc, p.x0r);
   if constexpr (!STG) return;
   const int64_t off = row * e.ldf + cc;
 #pragma unroll
@@ -211,10 +255,10 @@ __device__ __forceinline__ void epi_prefetch(const Epi& e, int64_t row, int cc, 
     if (i < e.st.n_out) {
       const gnpde_stage_out_t& so = e.st.o[i];
       if (so.base != nullptr && !(need_x && so.base == e.x && e.ldx == e.ldf))
-        load_vec<VEC>(as_t<T>(so.base) + off, p.base[i]);
+        load_packed<VEC>(as_t<T>(so.base) + off, p.base[i]);
 #pragma unroll
       for (int j = 0; j < GNPDE_STAGE_MAX_K; ++j)
-        if (j < so.nk) load_vec<VEC>(as_t<T>(so.k[j]) + off, p.kv[i][j]);
+        if (j < so.nk) load_packed<VEC>(as_t<T>(so.k[j]) + off, p.kv[i][j]);
     }
   }
 }
@@ -223,15 +267,15 @@ __device__ __forceinline__ void epi_prefetch(const Epi& e, int64_t row, int cc, 
 // then either store f or emit the fused Runge-Kutta stage outputs.
 template <int VEC, bool STG, class T = float>
 __device__ __forceinline__ void epi_finish(const Epi& e, int64_t row, int cc, const float (&ax)[VEC], float a,
-                                           float b, const EpiPre<VEC>& p) {
+                                           float b, const EpiPre<VEC, T>& p) {
   float o[VEC];
   const bool need_x = (e.flags & GNPDE_EPI_RHS) != 0;
   if (need_x) {
 #pragma unroll
-    for (int t = 0; t < VEC; ++t) o[t] = a * (ax[t] - p.xr[t]);
+    for (int t = 0; t < VEC; ++t) o[t] = a * (ax[t] - unpack(p.xr, t));
     if (e.flags & GNPDE_ADD_SOURCE) {
 #pragma unroll
-      for (int t = 0; t < VEC; ++t) o[t] = o[t] + b * p.x0r[t];
+      for (int t = 0; t < VEC; ++t) o[t] = o[t] + b * unpack(p.x0r, t);
     }
   } else {
 #pragma unroll
@@ -253,16 +297,16 @@ __device__ __forceinline__ void epi_finish(const Epi& e, int64_t row, int cc, co
       for (int t = 0; t < VEC; ++t) r[t] = 0.f;
     } else if (need_x && so.base == e.x && e.ldx == e.ldf) {
 #pragma unroll
-      for (int t = 0; t < VEC; ++t) r[t] = so.cb * p.xr[t];
+      for (int t = 0; t < VEC; ++t) r[t] = so.cb * unpack(p.xr, t);
     } else {
 #pragma unroll
-      for (int t = 0; t < VEC; ++t) r[t] = so.cb * p.base[i][t];
+      for (int t = 0; t < VEC; ++t) r[t] = so.cb * unpack(p.base[i], t);
     }
 #pragma unroll
     for (int j = 0; j < GNPDE_STAGE_MAX_K; ++j) {
       if (j < so.nk) {
 #pragma unroll
-        for (int t = 0; t < VEC; ++t) r[t] = fmaf(so.c[j], p.kv[i][j][t], r[t]);
+        for (int t = 0; t < VEC; ++t) r[t] = fmaf(so.c[j], unpack(p.kv[i][j], t), r[t]);
       }
     }
 #pragma unroll
@@ -274,7 +318,7 @@ __device__ __forceinline__ void epi_finish(const Epi& e, int64_t row, int cc, co
 template <int VEC, bool STG, class T = float>
 __device__ __forceinline__ void epilogue_store(const Epi& e, int64_t row, int cc, const float (&ax)[VEC], float a,
                                                float b) {
-  EpiPre<VEC> p;
+  EpiPre<VEC, T> p;
   epi_prefetch<VEC, STG, T>(e, row, cc, p);
   epi_finish<VEC, STG, T>(e, row, cc, ax, a, b, p);
 }

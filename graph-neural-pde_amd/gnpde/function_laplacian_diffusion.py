@@ -19,7 +19,7 @@ import torch
 from torch import nn
 
 from . import ops
-from .base_classes import ODEFunc
+from .base_classes import ODEFunc, _tensor_key
 from .utils import MaxNFEException
 
 
@@ -94,6 +94,25 @@ class LaplacianODEFunc(ODEFunc):
             raise RuntimeError("LaplacianODEFunc: %s weights are not set for block=%r" % (tag, blk))
         return w, tag
 
+    def supports_feature_padding(self):
+        """Columns are independent (A x per column, x0 per column): the fused
+        integrator may run on a zero-padded state (integrator._padded_width)."""
+        return True
+
+    def _x0_like(self, x):
+        """x0 in x's dtype and (padded) width."""
+        x0 = self.x0
+        if x0.dtype != x.dtype:
+            x0 = x0.to(x.dtype)
+        if x0.shape[-1] != x.shape[-1]:
+            key = (_tensor_key(self.x0), x.shape[-1], x.dtype)
+            if getattr(self, '_x0_pad', (None,))[0] != key:
+                xp = torch.zeros(*x0.shape[:-1], x.shape[-1], dtype=x.dtype, device=x.device)
+                xp[..., :x0.shape[-1]] = x0
+                self._x0_pad = (key, xp)
+            x0 = self._x0_pad[1]
+        return x0
+
     def sparse_multiply(self, x):
         """A x (src/function_laplacian_diffusion.py:39-58) — K1 without the epilogue."""
         g = self.graph_for(x)
@@ -109,9 +128,7 @@ class LaplacianODEFunc(ODEFunc):
         g = self.graph_for(x)
         w, tag = self._weights_tensor()
         add_source = bool(self.opt.get('add_source', False))
-        x0 = self.x0 if add_source else None
-        if x0 is not None and x0.dtype != x.dtype:
-            x0 = x0.to(x.dtype)
+        x0 = self._x0_like(x) if add_source else None
         ops.spmm_rhs(g, self.csr_weights(g, w, tag), x, x0=x0, alpha=self.alpha_train.detach(),
                      beta=self.beta_train.detach(), rhs=True, alpha_sigmoid=not self.opt.get('no_alpha_sigmoid', False),
                      add_source=add_source, stage=stage)
@@ -127,9 +144,7 @@ class LaplacianODEFunc(ODEFunc):
         if add_source and self.x0 is None:
             raise RuntimeError("LaplacianODEFunc: add_source needs x0 (ODEblock.set_x0)")
         alpha_sigmoid = not self.opt.get('no_alpha_sigmoid', False)
-        x0 = self.x0 if add_source else None
-        if x0 is not None and x0.dtype != x.dtype:
-            x0 = x0.to(x.dtype)
+        x0 = self._x0_like(x) if add_source else None
         if x.dtype == torch.bfloat16:
             # bf16 storage (configs[3]): inference only — the backward kernels are fp32
             if torch.is_grad_enabled() and (x.requires_grad or self.alpha_train.requires_grad):

@@ -288,6 +288,14 @@ class ODEFuncTransformerAtt(ODEFunc):
         aggregation epilogue (gnpde.integrator, no-grad fixed-grid solvers)."""
         self._rhs(x, stage)
 
+    def supports_feature_padding(self):
+        """With the fork's scaled_dot under source-grouped softmax the weights do
+        not depend on x (1/outdeg), so columns are independent and the fused
+        integrator may pad the state (integrator._padded_width); score modes
+        read Q/K over all C columns and may not."""
+        return self.multihead_att_layer.is_uniform(int(self.opt['attention_norm_idx'])) and \
+            not self.opt.get('add_source', False)
+
     def forward(self, t, x):  # t is needed when called by the integrator
         return self._rhs(x, None)
 

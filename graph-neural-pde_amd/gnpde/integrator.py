@@ -226,9 +226,33 @@ def _nfe_headroom(func, n):
     return func.nfe + n - 1 <= opt['max_nfe']
 
 
+def _padded_width(func, y0):
+    """Feature width the fused path pads the state to, or None.  Rows whose byte
+    length is not a multiple of 16 (C = 162 in fp32 or bf16, BLEND) cannot take
+    16-byte vector gathers; a RHS whose arithmetic is column-independent
+    (func.supports_feature_padding) integrates a zero-padded copy instead — the
+    padding columns stay exactly 0 (A 0 - 0 = 0) — and the result is cut back."""
+    per16 = 16 // y0.element_size()
+    C = y0.shape[-1]
+    if C % per16 == 0 or y0.dim() != 3:
+        return None
+    ok = getattr(func, 'supports_feature_padding', None)
+    if ok is None or not ok():
+        return None
+    return (C + per16 - 1) // per16 * per16
+
+
 def odeint_fixed(func, y0, t, method, step_size=None, combine=None, graph=None):
     combine = combine or _Combine()
     fused = _fusable(func, y0, combine)
+    if fused:
+        cp = _padded_width(func, y0)
+        if cp is not None:
+            C = y0.shape[-1]
+            yp = torch.zeros(*y0.shape[:-1], cp, dtype=y0.dtype, device=y0.device)
+            yp[..., :C] = y0
+            out = odeint_fixed(func, yp, t, method, step_size, combine, graph)
+            return out[..., :C].contiguous()
     ws = _Workspace()
     grid = t if step_size is None else fixed_grid(t, step_size)
     if not (bool(grid[0] == t[0]) and bool(grid[-1] == t[-1])):

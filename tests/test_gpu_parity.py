@@ -906,3 +906,30 @@ def test_bf16_attention_reference_norm1_rhs():
         f = func(0, T(x).to(torch.bfloat16))
     want = O.transformer_rhs(ei, _bf16_round(x), None, Wq, bq, Wk, bk, h, 1, 0.2, 0.0)
     assert f.dtype == torch.bfloat16 and rel(f.float(), want) <= BF16_ROUND
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, RTOL), (torch.bfloat16, BF16_TOL)])
+def test_padded_state_integration_c162(dtype, tol):
+    """C = 162 rows are not 16-byte multiples: the fused integrator runs on a
+    zero-padded copy (164 fp32 / 168 bf16 columns) with x0 padded alike, and
+    cuts the result back; against the oracle's integration of the unpadded state."""
+    N, E, C = 2500, 20000, 162
+    rng = np.random.default_rng(74)
+    ei = hub_graph(N, E, seed=74)
+    w = rng.uniform(0.1, 1, size=(1, E)).astype(np.float32)
+    x = rng.standard_normal((1, N, C)).astype(np.float32)
+    x0 = rng.standard_normal((1, N, C)).astype(np.float32)
+    func = gnpde.LaplacianODEFunc(C, C, dict(OPT, hidden_dim=C, add_source=True), DEV).to(DEV)
+    with torch.no_grad():
+        func.alpha_train.fill_(0.1)
+        func.beta_train.fill_(0.4)
+    func.edge_index, func.edge_weight, func.x0 = T(ei), T(w), T(x0).to(dtype)
+    assert gnpde.integrator._padded_width(func, T(x).to(dtype)) == (164 if dtype == torch.float32 else 168)
+    with torch.no_grad():
+        z = gnpde.odeint(func, T(x).to(dtype), torch.tensor([0.0, 0.5, 1.0], device=DEV), method='rk4',
+                         options={'step_size': 0.125})
+    assert z.shape == (3, 1, N, C) and z.dtype == dtype
+    f = lambda t, y: O.laplacian_rhs(ei, y, x0, 0.1, 0.4, edge_weight=w, add_source=True)  # noqa: E731
+    for i, tt in ((1, 0.5), (2, 1.0)):
+        want = O.odeint_fixed(f, x, 0.0, tt, 'rk4', 0.125)
+        assert rel(z[i].float(), want) <= tol
