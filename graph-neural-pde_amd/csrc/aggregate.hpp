@@ -89,7 +89,7 @@ __global__ __launch_bounds__(256) void agg_kernel(const int4* __restrict__ items
   const int lane = threadIdx.x & 63;
   const int rs = lane / SL, sl = lane % SL;
   const int g = sl / GL, gl = sl % GL;
-  const int wid = uniform(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
+  const int wid = uniform(xcd_block(ep.xcd_remap) * kWavesPerBlock + (threadIdx.x >> 6));
   const int item = wid * RPW + rs;
   if (wid * RPW >= n_items) return;
   const bool live = item < n_items;

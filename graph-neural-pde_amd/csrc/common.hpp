@@ -159,7 +159,21 @@ __device__ __forceinline__ double wave_sum(double v) {
 }
 
 // RHS epilogue scalars (device scalars: no host sync, graph-capturable)
+// Workgroups are dispatched round-robin over the 8 XCDs (workgroup b runs on
+// XCD b % 8).  With remap on, XCD x is handed one contiguous run of the grid's
+// work instead of every 8th workgroup, so rows handled together share an L2.
+constexpr int kNumXcd = 8;
+__device__ __forceinline__ int xcd_block(int remap) {
+  const int b = blockIdx.x;
+  if (!remap) return b;
+  const int nb = gridDim.x;
+  const int q = nb / kNumXcd, r = nb % kNumXcd;
+  const int x = b % kNumXcd, k = b / kNumXcd;
+  return x < r ? x * (q + 1) + k : r * (q + 1) + (x - r) * q + k;
+}
+
 struct Epi {
+  int xcd_remap;
   const float* x;
   int64_t ldx;
   const float* x0;

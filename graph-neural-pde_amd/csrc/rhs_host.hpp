@@ -36,9 +36,20 @@ inline ScoreArgs make_score_args(int mode, int64_t heads, int64_t dk, const doub
   return sa;
 }
 
+// Experiment knob (not part of the ABI contract): GNPDE_XCD_REMAP=1 maps
+// contiguous runs of K1 work items to one XCD (common.hpp xcd_block).
+inline int xcd_remap_enabled() {
+  static const int on = [] {
+    const char* e = std::getenv("GNPDE_XCD_REMAP");
+    return (e && e[0] == '1') ? 1 : 0;
+  }();
+  return on;
+}
+
 inline Epi make_epi(const float* x, int64_t ldx, const float* x0, int64_t ldx0, const float* alpha, const float* beta,
                     int flags, float* f, int64_t ldf, const gnpde_stage_epilogue_t* stage = nullptr) {
   Epi e;
+  e.xcd_remap = xcd_remap_enabled();
   e.has_stage = stage != nullptr;
   if (stage) e.st = *stage;
   e.x = x;
