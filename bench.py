@@ -172,10 +172,10 @@ def main():
     ms_per_step = elapsed * 1e3 / args.steps
     if args.rhs_only:
         nbytes = lap_bytes(N, E, C)
-        kname = "agg_kernel<4,32,1,4,1,false,PlainWeights> (+ agg_fixup_kernel<4,32,false>)"
+        kname = "agg_kernel<4,32,1,4,1,0,PlainWeights,float> (+ agg_fixup_kernel<4,32,0,float>)"
     else:
         nbytes = rk4_fused_step_bytes(N, E, C) / 4.0
-        kname = "agg_kernel<4,32,1,4,1,true,PlainWeights> (+ agg_fixup_kernel<4,32,true>): K1 with fused rk4 stage"
+        kname = "agg_kernel<4,32,1,4,1,1,PlainWeights,float> (+ agg_fixup_kernel<4,32,1,float>): K1 with fused rk4 stage"
     achieved = nbytes / (k1_ms * 1e-3) / 1e9
 
     # the plain RHS (no fused stage) on the same graph, for the per-RHS roofline
@@ -197,7 +197,7 @@ def main():
         pb = lap_bytes(N, E, C)
         plain = {"rhs_ms": round(pms, 4), "achieved": round(pb / (pms * 1e-3) / 1e9, 1),
                  "frac": round(pb / (pms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "algorithmic_bytes": pb,
-                 "kernel": "agg_kernel<4,32,1,4,1,false,PlainWeights> (+ fixup)"}
+                 "kernel": "agg_kernel<4,32,1,4,1,0,PlainWeights,float> (+ fixup)"}
 
     traffic = None
     tp = os.path.join(ROOT, "profiles", "k1_traffic.json")

@@ -79,7 +79,7 @@ struct RefDstSoftmaxWeights {
 // (NCH column passes); U edges per group are in flight per iteration.  The
 // epilogue operands (x_r, x0_r, stage inputs) are loaded before the gathers
 // when NCH <= 2 (PRE) so their latency overlaps the aggregation.
-template <int VEC, int GL, int NCH, int U, int RPW, bool STG, class WP, class T = float>
+template <int VEC, int GL, int NCH, int U, int RPW, int STG, class WP, class T = float>
 __global__ __launch_bounds__(256) void agg_kernel(const int4* __restrict__ items, int n_items,
                                                    const int* __restrict__ col, WP wp, int C, Epi ep,
                                                    float* __restrict__ partials) {
@@ -97,7 +97,7 @@ __global__ __launch_bounds__(256) void agg_kernel(const int4* __restrict__ items
   const int row = it.x, beg = it.y, end = it.z, slot = it.w;
   const bool owner = live && slot < 0 && g == 0;
 
-  EpiPre<VEC, T> pre[PRE ? NCH : 1];
+  EpiPre<VEC, T, stage_nout<STG>()> pre[PRE ? NCH : 1];
   if constexpr (PRE) {
     if (owner) {
 #pragma unroll
@@ -195,7 +195,7 @@ __global__ __launch_bounds__(256) void agg_kernel(const int4* __restrict__ items
 // Hub rows: sum the chunk partials, then the epilogue.  GL lanes cover the
 // columns; the 64/GL lane groups take chunks g, g+G, ... and are combined by a
 // fixed xor tree (deterministic).
-template <int VEC, int GL, bool STG, class T = float>
+template <int VEC, int GL, int STG, class T = float>
 __global__ __launch_bounds__(256) void agg_fixup_kernel(const int4* __restrict__ heavy, int n_heavy, int C, Epi ep,
                                                          const float* __restrict__ partials) {
   constexpr int G = kWave / GL;
@@ -238,20 +238,24 @@ static int launch_agg_cfg(const int4* items, int64_t n_items, const int4* heavy,
                           const WP& wp, int C, const Epi& ep, float* partials, hipStream_t s) {
   const unsigned grid = (unsigned)ceil_div(n_items, (int64_t)kWavesPerBlock * RPW);
   const unsigned gfix = (unsigned)ceil_div(n_heavy, kWavesPerBlock);
+  // single-output stages (every gnpde.integrator step) get the leaner instantiation
+  const int stg = ep.has_stage ? (ep.st.n_out <= 1 ? 1 : 2) : 0;
   if (n_items > 0) {
-    if (ep.has_stage)
-      agg_kernel<VEC, GL, NCH, U, RPW, true, WP, T><<<grid, kBlock, 0, s>>>(items, (int)n_items, col, wp, C, ep,
-                                                                              partials);
+    if (stg == 1)
+      agg_kernel<VEC, GL, NCH, U, RPW, 1, WP, T><<<grid, kBlock, 0, s>>>(items, (int)n_items, col, wp, C, ep, partials);
+    else if (stg == 2)
+      agg_kernel<VEC, GL, NCH, U, RPW, 2, WP, T><<<grid, kBlock, 0, s>>>(items, (int)n_items, col, wp, C, ep, partials);
     else
-      agg_kernel<VEC, GL, NCH, U, RPW, false, WP, T><<<grid, kBlock, 0, s>>>(items, (int)n_items, col, wp, C, ep,
-                                                                               partials);
+      agg_kernel<VEC, GL, NCH, U, RPW, 0, WP, T><<<grid, kBlock, 0, s>>>(items, (int)n_items, col, wp, C, ep, partials);
     GNPDE_LAUNCH_CHECK();
   }
   if (n_heavy > 0) {
-    if (ep.has_stage)
-      agg_fixup_kernel<VEC, GL, true, T><<<gfix, kBlock, 0, s>>>(heavy, (int)n_heavy, C, ep, partials);
+    if (stg == 1)
+      agg_fixup_kernel<VEC, GL, 1, T><<<gfix, kBlock, 0, s>>>(heavy, (int)n_heavy, C, ep, partials);
+    else if (stg == 2)
+      agg_fixup_kernel<VEC, GL, 2, T><<<gfix, kBlock, 0, s>>>(heavy, (int)n_heavy, C, ep, partials);
     else
-      agg_fixup_kernel<VEC, GL, false, T><<<gfix, kBlock, 0, s>>>(heavy, (int)n_heavy, C, ep, partials);
+      agg_fixup_kernel<VEC, GL, 0, T><<<gfix, kBlock, 0, s>>>(heavy, (int)n_heavy, C, ep, partials);
     GNPDE_LAUNCH_CHECK();
   }
   return GNPDE_OK;

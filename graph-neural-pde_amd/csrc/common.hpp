@@ -238,13 +238,21 @@ __device__ __forceinline__ float unpack(const Packed<VEC, bf16>& r, int t) {
 
 // Epilogue operands of one row slice, loaded ahead of the aggregation so their
 // latency overlaps the gathers (they depend only on the row).
-template <int VEC, class T = float>
+// STG = number of stage outputs the kernel is compiled for (0: store f; 1: the
+// single-output Runge-Kutta stages of gnpde.integrator; 2: the general
+// epilogue): an instantiation only holds registers for the outputs it can emit.
+template <int VEC, class T = float, int NOUT = GNPDE_STAGE_MAX_OUT>
 struct EpiPre {
   Packed<VEC, T> xr;
   Packed<VEC, T> x0r;
-  Packed<VEC, T> base[GNPDE_STAGE_MAX_OUT];
-  Packed<VEC, T> kv[GNPDE_STAGE_MAX_OUT][GNPDE_STAGE_MAX_K];
+  Packed<VEC, T> base[NOUT];
+  Packed<VEC, T> kv[NOUT][GNPDE_STAGE_MAX_K];
 };
+
+template <int STG>
+constexpr int stage_nout() {
+  return STG < 1 ? 1 : STG;
+}
 
 // The Epi / stage pointers are declared float*; for bf16 storage they address
 // bf16 arrays (gnpde_spmm_rhs_bf16) and are read through T.
@@ -257,15 +265,15 @@ __device__ __forceinline__ T* as_t(float* p) {
   return reinterpret_cast<T*>(p);
 }
 
-template <int VEC, bool STG, class T = float>
-__device__ __forceinline__ void epi_prefetch(const Epi& e, int64_t row, int cc, EpiPre<VEC, T>& p) {
+template <int VEC, int STG, class T = float>
+__device__ __forceinline__ void epi_prefetch(const Epi& e, int64_t row, int cc, EpiPre<VEC, T, stage_nout<STG>()>& p) {
   const bool need_x = (e.flags & GNPDE_EPI_RHS) != 0;
   if (need_x) load_packed<VEC>(as_t<T>(e.x) + row * e.ldx + cc, p.xr);
   if (e.flags & GNPDE_ADD_SOURCE) load_packed<VEC>(as_t<T>(e.x0) + row * e.ldx0 + cc, p.x0r);
   if constexpr (!STG) return;
   const int64_t off = row * e.ldf + cc;
 #pragma unroll
-  for (int i = 0; i < GNPDE_STAGE_MAX_OUT; ++i) {
+  for (int i = 0; i < stage_nout<STG>(); ++i) {
     if (i < e.st.n_out) {
       const gnpde_stage_out_t& so = e.st.o[i];
       if (so.base != nullptr && !(need_x && so.base == e.x && e.ldx == e.ldf))
@@ -279,9 +287,9 @@ __device__ __forceinline__ void epi_prefetch(const Epi& e, int64_t row, int cc, 
 
 // f = a*(ax - x) [+ b*x0]  (function_laplacian_diffusion.py:69-77) or f = ax,
 // then either store f or emit the fused Runge-Kutta stage outputs.
-template <int VEC, bool STG, class T = float>
+template <int VEC, int STG, class T = float>
 __device__ __forceinline__ void epi_finish(const Epi& e, int64_t row, int cc, const float (&ax)[VEC], float a,
-                                           float b, const EpiPre<VEC, T>& p) {
+                                           float b, const EpiPre<VEC, T, stage_nout<STG>()>& p) {
   float o[VEC];
   const bool need_x = (e.flags & GNPDE_EPI_RHS) != 0;
   if (need_x) {
@@ -302,7 +310,7 @@ __device__ __forceinline__ void epi_finish(const Epi& e, int64_t row, int cc, co
   const int64_t off = row * e.ldf + cc;
   if (e.st.f_out) store_vec<VEC>(as_t<T>(e.st.f_out) + off, o);
 #pragma unroll
-  for (int i = 0; i < GNPDE_STAGE_MAX_OUT; ++i) {
+  for (int i = 0; i < stage_nout<STG>(); ++i) {
     if (i >= e.st.n_out) break;
     const gnpde_stage_out_t& so = e.st.o[i];
     float r[VEC];
@@ -329,10 +337,10 @@ __device__ __forceinline__ void epi_finish(const Epi& e, int64_t row, int cc, co
   }
 }
 
-template <int VEC, bool STG, class T = float>
+template <int VEC, int STG, class T = float>
 __device__ __forceinline__ void epilogue_store(const Epi& e, int64_t row, int cc, const float (&ax)[VEC], float a,
                                                float b) {
-  EpiPre<VEC, T> p;
+  EpiPre<VEC, T, stage_nout<STG>()> p;
   epi_prefetch<VEC, STG, T>(e, row, cc, p);
   epi_finish<VEC, STG, T>(e, row, cc, ax, a, b, p);
 }

@@ -29,7 +29,7 @@ def main():
         if "agg_kernel" not in name:
             continue
         wv = write.get(name, [0.0])
-        tag = "fused_step_launch" if ", true," in name else "plain_launch"
+        tag = "fused_step_launch" if (", true," in name or ", 1, gnpde::PlainWeights" in name) else "plain_launch"
         f = sum(fv) / len(fv) * 1024
         w = sum(wv) / len(wv) * 1024
         out[tag] = {"kernel": name.split("(")[0], "fetch_bytes_raw": f, "write_bytes": w, "hbm_bytes": 2 * f + w,
