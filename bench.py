@@ -37,6 +37,14 @@ import torch.distributed as dist  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
+def graph_name(N, E):
+    if (N, E) == (169343, 1200000):
+        return "G-arxiv"
+    if (N, E) == (2000000, 20000000):
+        return "G-rmat (configs[4] graph)"
+    return "RMAT N=%d E=%d" % (N, E)
+
+
 def lap_bytes(N, E, C, add_source=False):
     """Algorithmic HBM bytes of one Laplacian RHS:
     gathered x rows 4EC + x_i read & f write 8NC + col/weight 8E + rowptr 4(N+1)."""
@@ -219,8 +227,9 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic (seeded RMAT G-arxiv graph per rank, N(0,1) features)",
-        "config": {"workload": "G-arxiv laplacian RHS, rk4 (configs[2])", "nodes": N, "edges": E, "dim": C,
+        "data": "synthetic (seeded RMAT graph per rank, N(0,1) features)",
+        "config": {"workload": "%s laplacian RHS, rk4%s" % (graph_name(N, E), " (configs[2])" if C == 128 else ""),
+                   "nodes": N, "edges": E, "dim": C,
                    "method": "rk4", "step_size": h, "rhs_per_step": rhs_per_step, "global_batch": world,
                    "parallelism": "replicas%d" % world, "chunk": g.chunk,
                    "hub_rows": g.csr.plan.n_heavy},
@@ -296,8 +305,9 @@ def bench_sharded(args, world, rank, dev):
             "value": round(value, 2), "unit": "RHS evals/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3 / args.steps, 4), "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": "f32",
-            "data": "synthetic (seeded RMAT G-arxiv graph, N(0,1) features)",
-            "config": {"workload": "G-arxiv laplacian RHS, rk4, one graph sharded (%s)" % args.mode, "nodes": N,
+            "data": "synthetic (seeded RMAT graph, N(0,1) features)",
+            "config": {"workload": "%s laplacian RHS, rk4, one graph sharded (%s)" % (graph_name(N, E), args.mode),
+                       "nodes": N,
                        "edges": E, "dim": C, "method": "rk4", "parallelism": "%s%d" % (args.mode, world)}}))
     dist.barrier()
     dist.destroy_process_group()
