@@ -337,15 +337,20 @@ int gnpde_seg_softmax_f32(const int32_t* items, int64_t n_items, const int32_t* 
   const bool ref = mode == GNPDE_SCORE_REFERENCE;
 #define GNPDE_SEG(R, O, ITEMS, N) \
   launch_seg<R, O>(ITEMS, N, rowptr, rowidx, gidx, group_is_dst, sa, tm, w, m, rl, partials, s)
+  // whole-group items and long-group chunks share one kernel (the slot field
+  // tells them apart): one launch when the caller stores them back to back
+  const bool adjacent = n_items > 0 && n_chunk_items > 0 && ch == it + n_items;
+  const int64_t n_first = adjacent ? n_items + n_chunk_items : n_items;
+  const int64_t n_second = adjacent ? 0 : n_chunk_items;
   if (out_kind == 0) {
-    rc = GNPDE_SEG(false, kSegWeights, it, n_items);
-    if (!rc) rc = GNPDE_SEG(false, kSegWeights, ch, n_chunk_items);
+    rc = GNPDE_SEG(false, kSegWeights, it, n_first);
+    if (!rc) rc = GNPDE_SEG(false, kSegWeights, ch, n_second);
   } else if (ref) {
-    rc = GNPDE_SEG(true, kSegStats, it, n_items);
-    if (!rc) rc = GNPDE_SEG(true, kSegStats, ch, n_chunk_items);
+    rc = GNPDE_SEG(true, kSegStats, it, n_first);
+    if (!rc) rc = GNPDE_SEG(true, kSegStats, ch, n_second);
   } else {
-    rc = GNPDE_SEG(false, kSegStats, it, n_items);
-    if (!rc) rc = GNPDE_SEG(false, kSegStats, ch, n_chunk_items);
+    rc = GNPDE_SEG(false, kSegStats, it, n_first);
+    if (!rc) rc = GNPDE_SEG(false, kSegStats, ch, n_second);
   }
   if (rc || n_chunk_items == 0) return rc;
   rc = launch_stats_fixup(hv, n_heavy, (int)heads, partials, m, rl, s);

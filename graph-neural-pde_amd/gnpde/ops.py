@@ -149,8 +149,11 @@ def build_seg_plan(rowptr, eb):
     def dev32(a, n):
         return torch.from_numpy(np.ascontiguousarray(a[:max(n, 1)]).reshape(-1)).to(dev)
 
-    return SegPlan(eb, dev32(items, ni.value), ni.value, dev32(chunks, nc.value), nc.value, dev32(heavy, nh.value),
-                   nh.value)
+    # items and chunk items back to back in one buffer: K2 then covers both in one launch
+    both = dev32(np.concatenate([items[:ni.value], chunks[:max(nc.value, 1)]], 0), ni.value + max(nc.value, 1))
+    it_view = both[:max(ni.value, 1) * 4] if ni.value else dev32(items, 0)
+    ch_view = both[ni.value * 4:]
+    return SegPlan(eb, it_view, ni.value, ch_view, nc.value, dev32(heavy, nh.value), nh.value)
 
 
 def build_grouped(edge_index, num_nodes, key_row, chunk=DEFAULT_CHUNK):

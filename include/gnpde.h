@@ -255,7 +255,8 @@ int gnpde_attn_weights_f32(const int32_t* rowidx, const int32_t* col, int64_t nn
  * those groups (partials: 2*heads doubles per slot; m/rl scratch).
  * gnpde_seg_plan_build builds them from a HOST copy of rowptr into HOST
  * arrays (plain C++, once per graph; capacities: items >= R, chunk_items >=
- * nnz/eb + R, heavy >= nnz/eb + 1).
+ * nnz/eb + R, heavy >= nnz/eb + 1).  When chunk_items == items + 4*n_items
+ * (stored back to back) both item kinds run in one launch.
  *   out_kind 0: w[p] = (1/H) sum_h softmax_p,h in grouped order (per-edge
  *               modes with norm_idx 0: the aggregation weights of K1);
  *   out_kind 1: m[g,h] = max (fp64), rl[g,h] = 1/(sum exp(s - m) + 1e-16).
