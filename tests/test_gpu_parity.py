@@ -933,3 +933,33 @@ def test_padded_state_integration_c162(dtype, tol):
     for i, tt in ((1, 0.5), (2, 1.0)):
         want = O.odeint_fixed(f, x, 0.0, tt, 'rk4', 0.125)
         assert rel(z[i].float(), want) <= tol
+
+
+# ---------------------------------------------------------------- attention properties (test_transformer_attention.py:166-205)
+@pytest.mark.parametrize("mode", ["reference", "per_edge"])
+@pytest.mark.parametrize("norm_idx", [0, 1])
+def test_layer_attention_properties(mode, norm_idx):
+    """SpGraphTransAttentionLayer.forward: attention [B,E,h]; every softmax group sums to 1;
+    0 < att <= 1 (the reference's own property tests, at B = 2 with hub groups)."""
+    N, E, C, h, att = 1500, 20000, 32, 4, 32
+    B = 2
+    ei = hub_graph(N, E, seed=80 + norm_idx, B=B)
+    rng = np.random.default_rng(81)
+    x = rng.standard_normal((B, N, C)).astype(np.float32)
+    opt = dict(OPT, hidden_dim=C, heads=h, attention_dim=att, attention_norm_idx=norm_idx,
+               attention_score_mode=mode)
+    lay = gnpde.SpGraphTransAttentionLayer(C, C, opt, DEV).to(DEV)
+    if mode == 'per_edge':
+        _set_qk(lay, rng, C, att, scale=0.3)
+    # reference mode keeps the layer's constant 1e-5 init (init_weights, :153-157): with random weights the
+    # fork's global key sum over 20k edges drives the softmax hard and exp underflows to 0 in fp32, as in the fork
+    with torch.no_grad():
+        a, _ = lay(T(x), T(ei))
+    assert tuple(a.shape) == (B, E, h)
+    an = a.double().cpu().numpy()
+    assert (an > 0).all() and (an <= 1 + 1e-7).all()
+    for b in range(B):
+        sums = np.zeros((N, h))
+        np.add.at(sums, ei[b, norm_idx], an[b])
+        live = np.unique(ei[b, norm_idx])
+        assert np.abs(sums[live] - 1).max() <= 1e-5
