@@ -568,6 +568,34 @@ def test_transformer_function_in_block_dopri5_runs():
     assert z.shape == x.shape and torch.isfinite(z).all()
 
 
+@pytest.mark.parametrize("method,tol_scale,step", [("dopri5", 0.01, None), ("rk4", 1.0, 0.02)])
+def test_c2_transformer_integration_vs_oracle(method, tol_scale, step):
+    """configs[1] (C2) shape: Cora-sized graph (N=2708), function=transformer with the fork's
+    scaled_dot, heads=8, attention_dim=128, norm_idx=1, through ConstantODEblock, against the
+    oracle's RHS integrated with rk4 steps of 0.02.  rk4 on the same grid agrees to ~6e-7.
+    dopri5 is run at tol_scale 0.01 (atol 1e-9, rtol 1e-11): at the reference's default
+    tol_scale 1 its own truncation error is 2e-5 of max|z| against the fine rk4 flow
+    (tools/c2diag.py), which is the solver, not the RHS."""
+    N, E, C, h, att = 2708, 10556, 80, 8, 128
+    rng = np.random.default_rng(90)
+    ei = rng.integers(0, N, size=(1, 2, E))
+    x = rng.standard_normal((1, N, C)).astype(np.float32)
+    opt = dict(OPT, hidden_dim=C, heads=h, attention_dim=att, function='transformer', attention_norm_idx=1,
+               method=method, tol_scale=tol_scale, step_size=step)
+    blk = gnpde.ConstantODEblock(gnpde.ODEFuncTransformerAtt, [], opt, DEV, t=torch.tensor([0, 1])).to(DEV).eval()
+    Wq, bq, Wk, bk = _set_qk(blk.odefunc.multihead_att_layer, rng, C, att, scale=0.03)
+    with torch.no_grad():
+        blk.odefunc.alpha_train.fill_(0.5)
+    data = gnpde.GraphData()
+    data.new_graph(T(ei), N)
+    with torch.no_grad():
+        z = blk(T(x), data)
+    eo, _ = _prep_oracle(ei, N)
+    f = lambda t, y: O.transformer_rhs(eo, y, None, Wq, bq, Wk, bk, h, 1, 0.5, 0.0)  # noqa: E731
+    want = O.odeint_fixed(f, x, 0.0, 1.0, 'rk4', 0.02)
+    assert rel(z, want) <= RTOL
+
+
 # ---------------------------------------------------------------- backward (x, alpha, beta)
 def test_laplacian_backward_vs_oracle():
     N, E, C = 1200, 15000, 24
