@@ -19,7 +19,10 @@ Stage combinations ``y0 + dt * sum_j b_j k_j`` are single fused HIP passes
 ODEFuncs run entirely in HIP).  Parity of integrated values is UNPINNED: the
 reference's tests only check shapes.
 """
+import itertools
 import math
+import os
+import weakref
 
 import torch
 
@@ -174,6 +177,9 @@ class _Workspace(dict):
 # Graph replay of fixed-grid steps (hipGraph through torch.cuda.CUDAGraph):
 # worth it once a few steps share one dt; capture itself costs host time.
 GRAPH_MIN_STEPS = 6
+# Steps per block graph (even; 0 disables), captured when a block of equal
+# steps remains after the first step.  GNPDE_GRAPH_BLOCK overrides.
+GRAPH_BLOCK = int(os.environ.get('GNPDE_GRAPH_BLOCK', '8'))
 # Set to a list to receive (start_event, end_event, n_rhs) per graph replay
 # (bench.py's per-launch roofline timing); None in normal use.
 replay_events = None
@@ -185,36 +191,97 @@ class _StepGraphs(object):
     and no copy of the state.  The RHS and its stage epilogues are the same
     launches as the eager fused step (same kernels, same arguments, same bits).
     Every per-graph structure (CSR, plans, cached weights) is built by the
-    eager step that precedes capture, so nothing synchronises inside it."""
+    eager step that precedes capture, so nothing synchronises inside it.
 
-    def __init__(self, method, func, dt, like, ws):
+    block >= 2 (even) also captures a block graph of ``block`` consecutive
+    steps bufs[0] -> bufs[1] -> ... -> bufs[0]: one launch per block instead of
+    one per step (each graph launch leaves the GPU idle for ≈20 µs between
+    replays; profiles/r01p trace)."""
+
+    def __init__(self, method, func, dt, like, ws, block=0):
         self.bufs = [torch.empty_like(like, memory_format=torch.contiguous_format) for _ in range(2)]
         self.graphs = []
         self.n_rhs = RHS_PER_STEP[method]
+        nfe = getattr(func, 'nfe', None)
         pool = None
         for i in range(2):
             g = torch.cuda.CUDAGraph()
-            nfe = getattr(func, 'nfe', None)
             with torch.cuda.graph(g, pool=pool):
                 _fused_step(method, func, 0.0, dt, dt, self.bufs[i], ws, out=self.bufs[1 - i])
-            if nfe is not None:
-                func.nfe = nfe  # capture records launches, it evaluates nothing
             pool = g.pool()
             self.graphs.append(g)
+        self.block, self.S = None, 0
+        if block >= 2 and block % 2 == 0:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=pool):
+                for k in range(block):
+                    _fused_step(method, func, 0.0, dt, dt, self.bufs[k % 2], ws, out=self.bufs[1 - k % 2])
+            self.block, self.S = g, block
+        if nfe is not None:
+            func.nfe = nfe  # capture records launches, it evaluates nothing
+
+    def _replay(self, g, n_rhs):
+        if replay_events is not None:
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            g.replay()
+            e.record()
+            replay_events.append((s, e, n_rhs))
+        else:
+            g.replay()
 
     def step(self, func, i):
         """Replay bufs[i] -> bufs[1-i]; counts the RHS evaluations like the eager calls."""
         if hasattr(func, 'nfe'):
             func.nfe += self.n_rhs
-        if replay_events is not None:
-            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            s.record()
-            self.graphs[i].replay()
-            e.record()
-            replay_events.append((s, e, self.n_rhs))
-        else:
-            self.graphs[i].replay()
+        self._replay(self.graphs[i], self.n_rhs)
         return self.bufs[1 - i]
+
+    def run_block(self, func):
+        """Replay S steps from bufs[0]; returns (state after the block, state
+        before its last step)."""
+        if hasattr(func, 'nfe'):
+            func.nfe += self.S * self.n_rhs
+        self._replay(self.block, self.S * self.n_rhs)
+        return self.bufs[0], self.bufs[1]
+
+
+# Captured step graphs kept per RHS module between odeint calls (one entry per
+# module, replaced when its key changes), so repeated solves — every forward
+# of a GRAND model in eval — replay without re-capturing.  A weak key: the
+# entry goes with the module.
+_GRAPH_CACHE = weakref.WeakKeyDictionary()
+
+
+def _graph_cache_key(func, method, y):
+    """Everything a captured step reads besides its own buffers: the module's
+    parameters and buffers, its graph / weight / x0 tensors (pointer, version,
+    shape, dtype; x0 only under add_source), its options, and the state's shape and layout.  A version
+    bump (in-place update) recaptures, so cached derived data (CSR-order
+    weights, padded x0) can never go stale under a replay."""
+    try:
+        tens = [_tkey(t) for t in itertools.chain(func.parameters(), func.buffers())]
+    except AttributeError:
+        return None
+    opt = getattr(func, 'opt', None)
+    names = ['edge_index', 'edge_weight', 'attention_weights']
+    if not isinstance(opt, dict) or opt.get('add_source', False):
+        names.append('x0')  # read only with add_source (GNN.forward resets it every call)
+    for name in names:
+        v = getattr(func, name, None)
+        if torch.is_tensor(v):
+            tens.append((name, _tkey(v)))
+    okey = repr(sorted(opt.items(), key=lambda kv: str(kv[0]))) if isinstance(opt, dict) else None
+    return (method, tuple(y.shape), tuple(y.stride()), y.dtype, str(y.device), okey, tuple(tens))
+
+
+def _tkey(t):
+    return (t.data_ptr(), t._version, tuple(t.shape), t.dtype, str(t.device))
+
+
+def _uniform_run(steps, n, k, dt):
+    """True when steps n .. n+k-1 exist and all have step dt."""
+    return k >= 2 and n + k <= len(steps) and all(steps[i][1] - steps[i][0] == dt for i in range(n, n + k))
 
 
 def _nfe_headroom(func, n):
@@ -254,37 +321,62 @@ def odeint_fixed(func, y0, t, method, step_size=None, combine=None, graph=None):
             out = odeint_fixed(func, yp, t, method, step_size, combine, graph)
             return out[..., :C].contiguous()
     ws = _Workspace()
-    grid = t if step_size is None else fixed_grid(t, step_size)
-    if not (bool(grid[0] == t[0]) and bool(grid[-1] == t[-1])):
-        raise AssertionError("time grid does not cover t")
-    grid_h = [float(v) for v in grid.tolist()]
+    # the grid lives on the host (the solver loop reads it there): one sync to
+    # read t, then torchdiffeq's grid built with the same torch ops on the CPU
+    # (IEEE fp32 there as on the device, so the same values)
     t_h = [float(v) for v in t.tolist()]
+    grid_h = t_h if step_size is None else \
+        [float(v) for v in fixed_grid(torch.tensor(t_h, dtype=t.dtype), step_size).tolist()]
+    if not (grid_h[0] == t_h[0] and grid_h[-1] == t_h[-1]):
+        raise AssertionError("time grid does not cover t")
     steps = list(zip(grid_h[:-1], grid_h[1:]))
     if graph is None:
         # a RHS with a collective inside (dist.RowShardedLaplacian) opts out of capture
         graph = len(steps) >= GRAPH_MIN_STEPS and getattr(func, 'graph_capturable', True)
     graphs = None
+    cache_key = _graph_cache_key(func, method, y0) if fused and graph else None
+    hit = _GRAPH_CACHE.get(func) if cache_key is not None else None
+    if hit is not None and hit[0] == cache_key and len(steps) >= 1 and steps[0][1] - steps[0][0] == hit[1][1]:
+        # same RHS state, shape and dt as a previous call: replay from the first step
+        _, graphs, ws = hit
+        graphs[0].bufs[0].copy_(y0)
+        gi = 0
     solution = [y0]
     j = 1
     yc = y0
-    for n, (ta, tb) in enumerate(steps):
+    n = 0
+    while n < len(steps):
+        ta, tb = steps[n]
         dt = tb - ta
         if fused and graph and n >= 1 and graphs is None and dt == steps[0][1] - steps[0][0] and \
                 len(steps) - n >= 2:
-            graphs = (_StepGraphs(method, func, dt, yc, ws), dt)
+            blk = GRAPH_BLOCK if _uniform_run(steps, n, GRAPH_BLOCK, dt) else 0
+            graphs = (_StepGraphs(method, func, dt, yc, ws, block=blk), dt)
             graphs[0].bufs[0].copy_(yc)
             gi = 0
-        if graphs is not None and dt == graphs[1] and _nfe_headroom(func, graphs[0].n_rhs):
-            y1 = graphs[0].step(func, gi)
-            gi = 1 - gi
-        elif fused:
-            y1 = _fused_step(method, func, ta, dt, tb, yc, ws)
+            if cache_key is not None:
+                _GRAPH_CACHE[func] = (cache_key, graphs, ws)
+        S = graphs[0].S if graphs is not None else 0
+        if S and gi == 0 and _uniform_run(steps, n, S, graphs[1]) and \
+                (j >= len(t_h) or t_h[j] > steps[n + S - 2][1]) and _nfe_headroom(func, S * graphs[0].n_rhs):
+            # no output time inside the block: only its end can be sampled
+            y1, yc = graphs[0].run_block(func)
+            ta, tb = steps[n + S - 1]
+            n += S
         else:
-            y1 = _fixed_step(method, func, ta, dt, tb, yc, combine)
+            if graphs is not None and dt == graphs[1] and _nfe_headroom(func, graphs[0].n_rhs):
+                y1 = graphs[0].step(func, gi)
+                gi = 1 - gi
+            elif fused:
+                y1 = _fused_step(method, func, ta, dt, tb, yc, ws)
+            else:
+                y1 = _fixed_step(method, func, ta, dt, tb, yc, combine)
+            n += 1
         while j < len(t_h) and tb >= t_h[j]:
             v = _linear_interp(ta, tb, yc, y1, t_h[j])
-            # graph buffers are overwritten by later replays
-            solution.append(v.clone() if graphs is not None and any(v is b for b in graphs[0].bufs) else v)
+            # graph buffers are overwritten by later replays (none after the last step)
+            solution.append(v.clone() if graphs is not None and n < len(steps) and
+                            any(v is b for b in graphs[0].bufs) else v)
             j += 1
         yc = y1
     return torch.stack(solution, 0)

@@ -828,6 +828,99 @@ def test_graph_replay_matches_eager_bitwise(method):
     assert torch.equal(z0, z1)
 
 
+@pytest.mark.parametrize("block", [2, 8])
+def test_block_graph_replay_matches_eager_bitwise(block, monkeypatch):
+    """Blocks of `block` captured steps (one graph launch per block) with output
+    times inside and at the end of blocks: same bits and nfe as the eager run,
+    and the block graph is actually replayed."""
+    import gnpde.integrator as integ
+    monkeypatch.setattr(integ, 'GRAPH_BLOCK', block)
+    N, E, C = 3000, 20000, 64
+    rng = np.random.default_rng(65)
+    ei = rng.integers(0, N, size=(1, 2, E))
+    ei[0, 0, :700] = 5
+    x = T(rng.standard_normal((1, N, C)).astype(np.float32))
+    opt = dict(OPT, hidden_dim=C, add_source=True, max_nfe=10 ** 6)
+    eo, wo = _prep_oracle(ei, N)
+    outs = []
+    for graph in (False, True):
+        func = gnpde.LaplacianODEFunc(C, C, opt, DEV).to(DEV)
+        func.edge_index, func.edge_weight, func.x0 = T(eo), T(wo).float(), x.clone()
+        ev = []
+        monkeypatch.setattr(integ, 'replay_events', ev)
+        with torch.no_grad():
+            func.alpha_train.fill_(0.3)
+            func.beta_train.fill_(-0.2)
+            t = torch.tensor([0.0, 0.5, 1.25, 2.5, 3.0], device=DEV)  # step 0.0625: 48 exact steps
+            z = gnpde.odeint(func, x, t, method='rk4', options={'step_size': 0.0625, 'gnpde_graph': graph})
+        torch.cuda.synchronize()
+        outs.append((z, func.nfe, [n for _, _, n in ev]))
+    (z0, n0, _), (z1, n1, ev1) = outs
+    assert n0 == n1 == 48 * 4
+    assert torch.equal(z0, z1)
+    assert ev1.count(4 * block) >= 2, ev1
+    assert sum(ev1) == 47 * 4  # every step after the first eager one is a replay
+
+
+def test_fixed_grid_host_equals_device():
+    """odeint_fixed builds torchdiffeq's grid with CPU torch ops; the device ops
+    give the same fp32 values (awkward step sizes included)."""
+    import gnpde.integrator as integ
+    for t0, t1 in [(0.0, 1.0), (0.0, 3.0), (0.3, 7.7), (1.0, 18.2948)]:
+        for h in (0.1, 0.25, 0.05, 1.0 / 3.0, 0.7, 0.0625):
+            td = torch.tensor([t0, t1], device=DEV)
+            gd = integ.fixed_grid(td, h).cpu()
+            gc = integ.fixed_grid(td.cpu(), h)
+            assert torch.equal(gd, gc), (t0, t1, h)
+
+
+def test_graph_cache_across_calls():
+    """A second odeint call with the same module replays the cached graphs (no
+    capture, no eager first step) and matches the eager result bitwise; an
+    in-place parameter update or a new x0 recaptures (never a stale replay)."""
+    import gnpde.integrator as integ
+    N, E, C = 3000, 20000, 64
+    rng = np.random.default_rng(66)
+    ei = rng.integers(0, N, size=(1, 2, E))
+    ei[0, 0, :700] = 5
+    x = T(rng.standard_normal((1, N, C)).astype(np.float32))
+    opt = dict(OPT, hidden_dim=C, add_source=True, max_nfe=10 ** 6)
+    eo, wo = _prep_oracle(ei, N)
+    t = torch.tensor([0.0, 1.0], device=DEV)
+    ref = gnpde.LaplacianODEFunc(C, C, opt, DEV).to(DEV)
+    func = gnpde.LaplacianODEFunc(C, C, opt, DEV).to(DEV)
+    for f in (ref, func):
+        f.edge_index, f.edge_weight, f.x0 = T(eo), T(wo).float(), x.clone()
+
+    def solve(f, graph, y):
+        with torch.no_grad():
+            z = gnpde.odeint(f, y, t, method='rk4', options={'step_size': 0.0625, 'gnpde_graph': graph})
+        torch.cuda.synchronize()
+        return z
+
+    with torch.no_grad():
+        for f in (ref, func):
+            f.alpha_train.fill_(0.3)
+            f.beta_train.fill_(-0.2)
+    solve(func, True, x)
+    entry = integ._GRAPH_CACHE[func]
+    y2 = x * 0.5
+    z_ref, z = solve(ref, False, y2), solve(func, True, y2)
+    assert integ._GRAPH_CACHE[func] is entry  # replayed, not recaptured
+    assert torch.equal(z_ref, z)
+    assert func.nfe == 2 * 16 * 4 and ref.nfe == 16 * 4
+    with torch.no_grad():
+        for f in (ref, func):
+            f.alpha_train.fill_(-0.4)
+    z_ref, z = solve(ref, False, x), solve(func, True, x)
+    assert integ._GRAPH_CACHE[func] is not entry
+    assert torch.equal(z_ref, z)
+    for f in (ref, func):
+        f.x0 = x.flip(1).contiguous()
+    z_ref, z = solve(ref, False, x), solve(func, True, x)
+    assert torch.equal(z_ref, z)
+
+
 def test_graph_replay_attention_rhs_matches_eager():
     """The transformer RHS (reference scores, norm_idx 1: key sum, node scores,
     CSC statistics, fused-weight K1) replayed from a graph equals the eager run."""
