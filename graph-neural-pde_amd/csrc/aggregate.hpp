@@ -1,8 +1,9 @@
 // aggregate.hpp — the gather-aggregate engine shared by the Laplacian RHS (K1)
 // and the attention RHS (K3): one wavefront per work item (a whole CSR row or a
 // chunk of a hub row), rows of x gathered with 16-byte loads, the RHS epilogue
-// fused, hub-row chunks summed in plan order by a fixup pass (deterministic, no
-// float atomics).
+// fused.  Hub rows are split into chunk items whose partial sums are combined
+// inside the same launch by the chunk that finishes last (arrival ticket on the
+// hub's plan entry; fixed summation order, so deterministic; no float atomics).
 #pragma once
 #include <algorithm>
 
@@ -72,16 +73,85 @@ struct RefDstSoftmaxWeights {
   }
 };
 
+// ------------------------------------------------------------------ hub rows
+// Sum the nch chunk partials of hub row `row` (slots first .. first+nch-1), then
+// run the epilogue.  GL lanes cover the columns; the 64/GL lane groups take
+// chunks g, g+G, ... and are combined by a fixed xor tree (deterministic).
+template <int VEC, int GL, int STG, class T>
+__device__ __forceinline__ void hub_combine(int row, int first, int nch, int C, const Epi& ep,
+                                            const float* __restrict__ partials) {
+  constexpr int G = kWave / GL;
+  const int lane = threadIdx.x & 63;
+  const int g = lane / GL, gl = lane % GL;
+  const float a = (ep.flags & GNPDE_EPI_RHS) ? epi_alpha(ep) : 1.f;
+  const float b = (ep.flags & GNPDE_ADD_SOURCE) ? *ep.beta : 0.f;
+  for (int c0 = 0; c0 < C; c0 += GL * VEC) {
+    const int cc = c0 + gl * VEC;
+    const bool live = cc < C;
+    float s[VEC];
+#pragma unroll
+    for (int t = 0; t < VEC; ++t) s[t] = 0.f;
+#pragma unroll 4
+    for (int c = g; c < nch; c += G) {
+      float v[VEC];
+      if (live) {
+        load_vec<VEC>(partials + (int64_t)(first + c) * C + cc, v);
+      } else {
+#pragma unroll
+        for (int t = 0; t < VEC; ++t) v[t] = 0.f;
+      }
+#pragma unroll
+      for (int t = 0; t < VEC; ++t) s[t] += v[t];
+    }
+#pragma unroll
+    for (int o = GL; o < kWave; o <<= 1)
+#pragma unroll
+      for (int t = 0; t < VEC; ++t) s[t] += __shfl_xor(s[t], o);
+    if (g == 0 && live) epilogue_store<VEC, STG, T>(ep, row, cc, s, a, b);
+  }
+}
+
+// A chunk wave whose write-through partial stores are issued: drain them, take
+// an arrival ticket on its hub's plan entry (heavy[h].w, an agent-scope atomic),
+// and if it arrived last, acquire and combine the hub row, then reset the
+// ticket to 0 for the next launch on this plan.  Hubs are found by a binary
+// search of the ascending first slots (log2(n_heavy) L2 reads, chunk waves only).
+template <int VEC, int GL, int STG, class T>
+__device__ __forceinline__ void hub_arrive(int4* heavy, int n_heavy, int slot, int C, const Epi& ep,
+                                           const float* partials) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  int lo = 0, hi = n_heavy - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (heavy[mid].y <= slot)
+      lo = mid;
+    else
+      hi = mid - 1;
+  }
+  const int row = heavy[lo].x, first = heavy[lo].y, nch = heavy[lo].z;
+  int* ticket_word = &heavy[lo].w;
+  int ticket = 0;
+  if ((threadIdx.x & 63) == 0)
+    ticket = __hip_atomic_fetch_add(ticket_word, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  ticket = __shfl(ticket, 0);
+  if (ticket != nch - 1) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  hub_combine<VEC, GL, STG, T>(row, first, nch, C, ep, partials);
+  if ((threadIdx.x & 63) == 0) __hip_atomic_store(ticket_word, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // ------------------------------------------------------------------ aggregation kernel
 // Lane layout: RPW row slots of SL = 64/RPW lanes per wavefront (one plan item
 // each); inside a slot lane = g*GL + gl: G = SL/GL edges are gathered side by
 // side, each by a group of GL lanes covering the C columns with VEC-wide loads
 // (NCH column passes); U edges per group are in flight per iteration.  The
 // epilogue operands (x_r, x0_r, stage inputs) are loaded before the gathers
-// when NCH <= 2 (PRE) so their latency overlaps the aggregation.
+// when NCH <= 2 (PRE) so their latency overlaps the aggregation.  RPW == 1:
+// hub rows are combined in-launch (hub_arrive); RPW > 1 leaves the partials
+// to agg_fixup_kernel.
 template <int VEC, int GL, int NCH, int U, int RPW, int STG, class WP, class T = float>
-__global__ __launch_bounds__(256) void agg_kernel(const int4* __restrict__ items, int n_items,
-                                                   const int* __restrict__ col, WP wp, int C, Epi ep,
+__global__ __launch_bounds__(256) void agg_kernel(const int4* __restrict__ items, int n_items, int4* heavy,
+                                                   int n_heavy, const int* __restrict__ col, WP wp, int C, Epi ep,
                                                    float* __restrict__ partials) {
   constexpr int SL = kWave / RPW;
   constexpr int G = SL / GL;
@@ -169,6 +239,20 @@ __global__ __launch_bounds__(256) void agg_kernel(const int4* __restrict__ items
 #pragma unroll
       for (int t = 0; t < VEC; ++t) acc[ch][t] += __shfl_xor(acc[ch][t], o);
 
+  if constexpr (RPW == 1) {
+    if (slot >= 0 && n_heavy > 0) {  // wave-uniform: a chunk of a hub row, combined in-launch
+      if (g == 0) {
+        const __amdgpu_buffer_rsrc_t rp = buf_rsrc(partials);
+#pragma unroll
+        for (int ch = 0; ch < NCH; ++ch) {
+          const int cc = (ch * GL + gl) * VEC;
+          buf_store_wt<VEC>(rp, cc < C ? (uint32_t)(((int64_t)slot * C + cc) * 4) : kBufNone, acc[ch]);
+        }
+      }
+      hub_arrive<VEC, GL, STG, T>(heavy, n_heavy, slot, C, ep, partials);
+      return;
+    }
+  }
   if (!live || g != 0) return;
   if (slot >= 0) {
 #pragma unroll
@@ -192,64 +276,43 @@ __global__ __launch_bounds__(256) void agg_kernel(const int4* __restrict__ items
   }
 }
 
-// Hub rows: sum the chunk partials, then the epilogue.  GL lanes cover the
-// columns; the 64/GL lane groups take chunks g, g+G, ... and are combined by a
-// fixed xor tree (deterministic).
+// Hub rows of the RPW > 1 geometries: one wavefront per hub, after the aggregation launch.
 template <int VEC, int GL, int STG, class T = float>
 __global__ __launch_bounds__(256) void agg_fixup_kernel(const int4* __restrict__ heavy, int n_heavy, int C, Epi ep,
                                                          const float* __restrict__ partials) {
-  constexpr int G = kWave / GL;
-  const int lane = threadIdx.x & 63;
   const int wid = uniform(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
   if (wid >= n_heavy) return;
   const int4 hv = heavy[wid];
-  const int row = uniform(hv.x), first = uniform(hv.y), nch = uniform(hv.z);
-  const int g = lane / GL, gl = lane % GL;
-  const float a = (ep.flags & GNPDE_EPI_RHS) ? epi_alpha(ep) : 1.f;
-  const float b = (ep.flags & GNPDE_ADD_SOURCE) ? *ep.beta : 0.f;
-  for (int c0 = 0; c0 < C; c0 += GL * VEC) {
-    const int cc = c0 + gl * VEC;
-    const bool live = cc < C;
-    float s[VEC];
-#pragma unroll
-    for (int t = 0; t < VEC; ++t) s[t] = 0.f;
-#pragma unroll 4
-    for (int c = g; c < nch; c += G) {
-      float v[VEC];
-      if (live) {
-        load_vec<VEC>(partials + (int64_t)(first + c) * C + cc, v);
-      } else {
-#pragma unroll
-        for (int t = 0; t < VEC; ++t) v[t] = 0.f;
-      }
-#pragma unroll
-      for (int t = 0; t < VEC; ++t) s[t] += v[t];
-    }
-#pragma unroll
-    for (int o = GL; o < kWave; o <<= 1)
-#pragma unroll
-      for (int t = 0; t < VEC; ++t) s[t] += __shfl_xor(s[t], o);
-    if (g == 0 && live) epilogue_store<VEC, STG, T>(ep, row, cc, s, a, b);
-  }
+  hub_combine<VEC, GL, STG, T>(uniform(hv.x), uniform(hv.y), uniform(hv.z), C, ep, partials);
 }
 
+// Experiment knob (not part of the ABI contract): GNPDE_HUB_FIXUP=1 combines hub
+// rows in a separate agg_fixup_kernel launch instead of inside the aggregation.
+bool hub_inlaunch();
+
 template <int VEC, int GL, int NCH, int U, int RPW, class WP, class T = float>
-static int launch_agg_cfg(const int4* items, int64_t n_items, const int4* heavy, int64_t n_heavy, const int* col,
+static int launch_agg_cfg(const int4* items, int64_t n_items, int4* heavy, int64_t n_heavy, const int* col,
                           const WP& wp, int C, const Epi& ep, float* partials, hipStream_t s) {
   const unsigned grid = (unsigned)ceil_div(n_items, (int64_t)kWavesPerBlock * RPW);
   const unsigned gfix = (unsigned)ceil_div(n_heavy, kWavesPerBlock);
+  // hub rows combined in the launch (RPW == 1) or by agg_fixup_kernel after it
+  const bool inlaunch = hub_inlaunch();
+  const int nh = inlaunch ? (int)n_heavy : 0;
   // single-output stages (every gnpde.integrator step) get the leaner instantiation
   const int stg = ep.has_stage ? (ep.st.n_out <= 1 ? 1 : 2) : 0;
   if (n_items > 0) {
     if (stg == 1)
-      agg_kernel<VEC, GL, NCH, U, RPW, 1, WP, T><<<grid, kBlock, 0, s>>>(items, (int)n_items, col, wp, C, ep, partials);
+      agg_kernel<VEC, GL, NCH, U, RPW, 1, WP, T><<<grid, kBlock, 0, s>>>(items, (int)n_items, heavy, nh, col, wp, C, ep,
+                                                                          partials);
     else if (stg == 2)
-      agg_kernel<VEC, GL, NCH, U, RPW, 2, WP, T><<<grid, kBlock, 0, s>>>(items, (int)n_items, col, wp, C, ep, partials);
+      agg_kernel<VEC, GL, NCH, U, RPW, 2, WP, T><<<grid, kBlock, 0, s>>>(items, (int)n_items, heavy, nh, col, wp, C, ep,
+                                                                          partials);
     else
-      agg_kernel<VEC, GL, NCH, U, RPW, 0, WP, T><<<grid, kBlock, 0, s>>>(items, (int)n_items, col, wp, C, ep, partials);
+      agg_kernel<VEC, GL, NCH, U, RPW, 0, WP, T><<<grid, kBlock, 0, s>>>(items, (int)n_items, heavy, nh, col, wp, C, ep,
+                                                                          partials);
     GNPDE_LAUNCH_CHECK();
   }
-  if (n_heavy > 0) {
+  if ((RPW > 1 || !inlaunch) && n_heavy > 0) {
     if (stg == 1)
       agg_fixup_kernel<VEC, GL, 1, T><<<gfix, kBlock, 0, s>>>(heavy, (int)n_heavy, C, ep, partials);
     else if (stg == 2)
@@ -266,7 +329,7 @@ static int launch_agg_cfg(const int4* items, int64_t n_items, const int4* heavy,
 int agg_variant();
 
 template <int VEC, class WP, class T = float>
-static int launch_agg_vec(const int4* items, int64_t n_items, const int4* heavy, int64_t n_heavy, const int* col,
+static int launch_agg_vec(const int4* items, int64_t n_items, int4* heavy, int64_t n_heavy, const int* col,
                           const WP& wp, int C, const Epi& ep, float* partials, hipStream_t s) {
   const int lanes = (int)ceil_div(C, VEC);
 #define GNPDE_AGG(GL, NCH, U, RPW) \
@@ -325,10 +388,10 @@ inline int epi_vec_width(const Epi& ep, int64_t C, const void* partials) {
 }
 
 template <class WP, class T = float>
-static int launch_agg(const int32_t* items, int64_t n_items, const int32_t* heavy, int64_t n_heavy,
+static int launch_agg(const int32_t* items, int64_t n_items, int32_t* heavy, int64_t n_heavy,
                       const int32_t* col, const WP& wp, int64_t C, const Epi& ep, float* partials, hipStream_t s) {
   const int4* it = reinterpret_cast<const int4*>(items);
-  const int4* hv = reinterpret_cast<const int4*>(heavy);
+  int4* hv = reinterpret_cast<int4*>(heavy);
   const int c = (int)C;
   switch (epi_vec_width<T>(ep, C, partials)) {
     case 8:

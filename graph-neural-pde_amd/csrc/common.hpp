@@ -370,4 +370,28 @@ __device__ __forceinline__ void buf_store_f64(__amdgpu_buffer_rsrc_t r, uint32_t
   __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, off, 0, 0);
 }
 
+// Write-through (sc1) stores of VEC floats at byte offset off: the bytes reach
+// the memory side before the storing wave's s_waitcnt vmcnt(0) returns, so a
+// workgroup on any XCD can read them after an agent-scope acquire (the in-launch
+// hand-off of cdna_hip_programming.md §6 Guideline 16, R1) with no release fence.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+constexpr int kAuxSc1 = 16;
+
+template <int VEC>
+__device__ __forceinline__ void buf_store_wt(__amdgpu_buffer_rsrc_t r, uint32_t off, const float (&v)[VEC]) {
+  if constexpr (VEC >= 4) {
+#pragma unroll
+    for (int q = 0; q < VEC / 4; ++q) {
+      const u32x4 d = {__builtin_bit_cast(uint32_t, v[4 * q]), __builtin_bit_cast(uint32_t, v[4 * q + 1]),
+                       __builtin_bit_cast(uint32_t, v[4 * q + 2]), __builtin_bit_cast(uint32_t, v[4 * q + 3])};
+      __builtin_amdgcn_raw_buffer_store_b128(d, r, off + 16 * q, 0, kAuxSc1);
+    }
+  } else if constexpr (VEC == 2) {
+    const u32x2 d = {__builtin_bit_cast(uint32_t, v[0]), __builtin_bit_cast(uint32_t, v[1])};
+    __builtin_amdgcn_raw_buffer_store_b64(d, r, off, 0, kAuxSc1);
+  } else {
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v[0]), r, off, 0, kAuxSc1);
+  }
+}
+
 }  // namespace gnpde

@@ -17,6 +17,14 @@ int bf16_vec_cap() {
   return v;
 }
 
+bool hub_inlaunch() {
+  static const bool v = [] {
+    const char* e = std::getenv("GNPDE_HUB_FIXUP");
+    return !(e && std::atoi(e) == 1);
+  }();
+  return v;
+}
+
 int agg_variant() {
   static const int v = [] {
     const char* e = std::getenv("GNPDE_AGG_VARIANT");
@@ -678,7 +686,7 @@ using namespace gnpde;
 
 extern "C" {
 
-int gnpde_spmm_rhs_f32(const int32_t* items, int64_t n_items, const int32_t* heavy, int64_t n_heavy,
+int gnpde_spmm_rhs_f32(const int32_t* items, int64_t n_items, int32_t* heavy, int64_t n_heavy,
                        const int32_t* col, const float* w, int64_t C, const float* x, int64_t ldx, const float* x0,
                        int64_t ldx0, const float* alpha, const float* beta, int flags, float* f, int64_t ldf,
                        float* partials, const gnpde_stage_epilogue_t* stage, void* stream) {
@@ -691,7 +699,7 @@ int gnpde_spmm_rhs_f32(const int32_t* items, int64_t n_items, const int32_t* hea
   return launch_agg(items, n_items, heavy, n_heavy, col, wp, C, ep, partials, as_stream(stream));
 }
 
-int gnpde_spmm_rhs_bf16(const int32_t* items, int64_t n_items, const int32_t* heavy, int64_t n_heavy,
+int gnpde_spmm_rhs_bf16(const int32_t* items, int64_t n_items, int32_t* heavy, int64_t n_heavy,
                         const int32_t* col, const float* w, int64_t C, const uint16_t* x, int64_t ldx,
                         const uint16_t* x0, int64_t ldx0, const float* alpha, const float* beta, int flags, uint16_t* f,
                         int64_t ldf, float* partials, const gnpde_stage_epilogue_t* stage, void* stream) {
@@ -705,7 +713,7 @@ int gnpde_spmm_rhs_bf16(const int32_t* items, int64_t n_items, const int32_t* he
   return launch_agg<PlainWeights, bf16>(items, n_items, heavy, n_heavy, col, wp, C, ep, partials, as_stream(stream));
 }
 
-int gnpde_attn_ref_rhs_f32(const int32_t* items, int64_t n_items, const int32_t* heavy, int64_t n_heavy,
+int gnpde_attn_ref_rhs_f32(const int32_t* items, int64_t n_items, int32_t* heavy, int64_t n_heavy,
                            const int32_t* col, const double* cs, const double* m, const float* rl, int64_t heads,
                            int64_t C, const float* x, int64_t ldx, const float* x0, int64_t ldx0, const float* alpha,
                            const float* beta, int flags, float* f, int64_t ldf, float* partials,

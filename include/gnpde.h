@@ -164,10 +164,15 @@ typedef struct {
  *         = a*(ax - x[r,:]) [+ b*x0[r,:]]        (GNPDE_EPI_RHS)
  * a = *alpha or sigmoid(*alpha), b = *beta: device scalars (no host sync).
  * partials: n_slots*C floats of scratch (NULL if n_slots == 0).
+ * heavy: the hub table of gnpde_plan_build.  The chunks of a hub row are
+ * combined inside the launch by the chunk that finishes last, which it learns
+ * from an arrival ticket kept in the 4th word of the row's heavy entry
+ * (plan_build writes 0; every launch leaves 0).  Launches that share one plan
+ * must therefore be ordered (one stream, or events) — never concurrent.
  * stage: NULL -> f[r,:] is stored to f; otherwise the stage epilogue above
  * decides what is stored (f is ignored).
  * Replaces function_laplacian_diffusion.py:39-77 per RHS evaluation.        */
-int gnpde_spmm_rhs_f32(const int32_t* items, int64_t n_items, const int32_t* heavy, int64_t n_heavy,
+int gnpde_spmm_rhs_f32(const int32_t* items, int64_t n_items, int32_t* heavy, int64_t n_heavy,
                        const int32_t* col, const float* w, int64_t C,
                        const float* x, int64_t ldx, const float* x0, int64_t ldx0,
                        const float* alpha, const float* beta, int flags,
@@ -179,7 +184,7 @@ int gnpde_spmm_rhs_f32(const int32_t* items, int64_t n_items, const int32_t* hea
  * struct's float* fields are reinterpreted); weights, alpha, beta and the
  * partials stay fp32, and every sum and the epilogue run in fp32 — only the
  * stored rows are rounded (nearest even).  Otherwise as gnpde_spmm_rhs_f32.  */
-int gnpde_spmm_rhs_bf16(const int32_t* items, int64_t n_items, const int32_t* heavy, int64_t n_heavy,
+int gnpde_spmm_rhs_bf16(const int32_t* items, int64_t n_items, int32_t* heavy, int64_t n_heavy,
                         const int32_t* col, const float* w, int64_t C, const uint16_t* x, int64_t ldx,
                         const uint16_t* x0, int64_t ldx0, const float* alpha, const float* beta, int flags, uint16_t* f,
                         int64_t ldf, float* partials, const gnpde_stage_epilogue_t* stage, void* stream);
@@ -192,7 +197,7 @@ int gnpde_spmm_rhs_bf16(const int32_t* items, int64_t n_items, const int32_t* he
  * gnpde_attn_weights_f32 + gnpde_spmm_rhs_f32 bit for bit, in one pass:
  * ODEFuncTransformerAtt.forward, function_transformer_attention.py:44-59.
  * Other arguments as gnpde_spmm_rhs_f32.                                     */
-int gnpde_attn_ref_rhs_f32(const int32_t* items, int64_t n_items, const int32_t* heavy, int64_t n_heavy,
+int gnpde_attn_ref_rhs_f32(const int32_t* items, int64_t n_items, int32_t* heavy, int64_t n_heavy,
                            const int32_t* col, const double* cs, const double* m, const float* rl, int64_t heads,
                            int64_t C, const float* x, int64_t ldx, const float* x0, int64_t ldx0, const float* alpha,
                            const float* beta, int flags, float* f, int64_t ldf, float* partials,

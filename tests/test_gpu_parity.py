@@ -277,6 +277,33 @@ def _check_seg_plan(grouped, eb):
     assert all(b in starts and e in starts for b, e in it[:, :2])
 
 
+@pytest.mark.parametrize("score_mode", ["reference", "per_edge"])
+def test_seg_stats_one_launch_equals_two_and_repeats(score_mode):
+    """Items and long groups' chunks stored back to back (one launch) give the
+    same statistics, bit for bit, as the two arrays in separate buffers (two
+    launches), on every one of several repeats."""
+    import copy
+    N, E = 1500, 24000
+    ei, x, x0, Wq, bq, Wk, bk = _attn_case(N, E, 128, 2, 32, seed=77)
+    g = ops.GraphCSR(T(ei), N)
+    ns = ops.node_scores(g, T(x), T(Wq), T(bq), T(Wk), T(bk), 2, 'scaled_dot', score_mode)
+    m1, rl1 = ops.softmax_stats(g, ns, 1)
+    eb = [k for k in g.csc._seg_plans][0]
+    plan = g.csc._seg_plans[eb]
+    assert plan.n_chunk > 0 and plan.n_items > 0
+    for _ in range(3):
+        m, rl = ops.softmax_stats(g, ns, 1)
+        assert torch.equal(m, m1) and torch.equal(rl, rl1)
+    p2 = copy.copy(plan)
+    p2.items, p2.chunk_items = plan.items.clone(), plan.chunk_items.clone()
+    g.csc._seg_plans[eb] = p2
+    m2, rl2 = ops.softmax_stats(g, ns, 1)
+    torch.cuda.synchronize()
+    assert torch.equal(m2, m1) and torch.equal(rl2, rl1)
+    assert int(plan.heavy.view(-1, 4)[:plan.n_heavy, 3].abs().sum()) == 0
+    assert int(p2.heavy.view(-1, 4)[:p2.n_heavy, 3].abs().sum()) == 0
+
+
 @pytest.mark.parametrize("C,h,att", [(128, 2, 32), (162, 2, 32), (80, 8, 128), (64, 4, 64), (256, 1, 16),
                                      (16, 16, 64)])
 @pytest.mark.parametrize("norm_idx", [0, 1])

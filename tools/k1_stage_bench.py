@@ -54,6 +54,7 @@ def main():
         def k1(xin, o=None, stage=None):
             return ops.spmm_rhs(g, wc, xin, alpha=a, out=None if o is None else o.view(-1, C), stage=stage)
 
+        r["hub_inlaunch"] = os.environ.get("GNPDE_HUB_FIXUP") != "1"
         r["plain_fixed"] = timeit(lambda i: k1(x, out), reps)
         r["plain_rotating"] = timeit(lambda i: k1(bufs[i % 5], bufs[(i + 1) % 5]), reps)
         r["stg_f_only"] = timeit(lambda i: k1(x, stage=ops.Stage(f_out=out)), reps)
