@@ -34,8 +34,10 @@ struct PlainWeights {
 // order, as attn_weights_kernel (rhs.hip), so fusing it into K1 changes no
 // bit; it saves the separate weights pass and its [nnz] round trip.
 // MAXH > 0: heads <= MAXH, the per-edge statistics are loaded up front;
-// MAXH == 0: any heads <= 16, loaded in finish().
-template <int MAXH>
+// MAXH == 0: any heads <= 16, loaded in finish().  EXACT (heads == MAXH == 2,
+// m 16-byte and rl 8-byte aligned): one 16-B load of m[c,:] and one 8-B load
+// of rl[c,:] per edge instead of four scalar gathers.
+template <int MAXH, bool EXACT = false>
 struct RefDstSoftmaxWeights {
   const double* __restrict__ cs;
   const double* __restrict__ m;
@@ -49,7 +51,15 @@ struct RefDstSoftmaxWeights {
   __device__ __forceinline__ Raw load(int /*row*/, int /*p*/, int c) const {
     Raw r;
     r.c = c;
-    if constexpr (MAXH > 0) {
+    if constexpr (EXACT) {
+      static_assert(MAXH == 2, "EXACT statistics loads are written for two heads");
+      const double2 mv = *reinterpret_cast<const double2*>(m + (int64_t)c * 2);
+      const float2 rv = *reinterpret_cast<const float2*>(rl + (int64_t)c * 2);
+      r.mm[0] = mv.x;
+      r.mm[1] = mv.y;
+      r.rr[0] = rv.x;
+      r.rr[1] = rv.y;
+    } else if constexpr (MAXH > 0) {
 #pragma unroll
       for (int h = 0; h < MAXH; ++h) {
         const int hh = h < H ? h : 0;

@@ -86,31 +86,16 @@ __global__ __launch_bounds__(256) void stats_kernel(const int4* __restrict__ ite
   }
 }
 
-// Hub groups: one wavefront per (group, head); lanes merge strided chunks, then a
-// fixed xor tree (deterministic).
+// Hub groups: one wavefront per (group, head) merging that group's chunk
+// statistics (stats_merge_store, scores.hpp).
 __global__ __launch_bounds__(256) void stats_fixup_kernel(const int4* __restrict__ heavy, int n_heavy, int H,
                                                            const double* __restrict__ partials,
                                                            double* __restrict__ m_out, float* __restrict__ rl_out) {
-  const int lane = threadIdx.x & 63;
   const int wid = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
   if (wid >= n_heavy * H) return;
   const int i = wid / H, h = wid - i * H;
   const int4 hv = heavy[i];
-  const int g = hv.x, first = hv.y, nch = hv.z;
-  double M = -INFINITY;
-  float L = 0.f;
-  for (int c = lane; c < nch; c += kWave)
-    online_merge(M, L, partials[(int64_t)(first + c) * 2 * H + h], (float)partials[(int64_t)(first + c) * 2 * H + H + h]);
-#pragma unroll
-  for (int o = 1; o < kWave; o <<= 1) {
-    const double M2 = __shfl_xor(M, o);
-    const float L2 = __shfl_xor(L, o);
-    online_merge(M, L, M2, L2);
-  }
-  if (lane == 0) {
-    m_out[(int64_t)g * H + h] = M;
-    rl_out[(int64_t)g * H + h] = 1.0f / (L + kSoftmaxEps);
-  }
+  stats_merge_store(hv.x, hv.y, hv.z, H, h, partials, m_out, rl_out);
 }
 
 int launch_stats_fixup(const int4* heavy, int64_t n_heavy, int H, const double* partials, double* m, float* rl,
@@ -284,7 +269,7 @@ __global__ __launch_bounds__(256) void attn_team_kernel(const int* __restrict__ 
 }
 
 // ------------------------------------------------------------------ reference-mode key sum
-// part[b][tile][c] = sum_{n in tile} indeg[b*N+n] * x[b*N+n][c]  (fp64), part[..][C] = sum indeg.
+// part[b][c][tile] = sum_{n in tile} indeg[b*N+n] * x[b*N+n][c]  (fp64), part[b][C][..] = sum indeg.
 // TPR threads per row, RPB = 256/TPR rows in flight per block iteration.
 template <int VEC>
 __global__ __launch_bounds__(256) void keysum_partial_kernel(const float* __restrict__ x, int64_t N, int C,
@@ -319,43 +304,30 @@ __global__ __launch_bounds__(256) void keysum_partial_kernel(const float* __rest
     red[rs * (C + 1) + C] = ds;
   }
   __syncthreads();
-  double* out = part + ((int64_t)b * ntiles + tile) * (C + 1);
+  double* out = part + (int64_t)b * (C + 1) * ntiles + tile;  // column-major: [b][c][tile]
   for (int c = threadIdx.x; c <= C; c += blockDim.x) {
     double s = 0.0;
     for (int r = 0; r < RPB; ++r) s += red[r * (C + 1) + c];
-    out[c] = s;
+    out[(int64_t)c * ntiles] = s;
   }
 }
 
-// xbar[b][c] = sum over tiles: kTileCols columns x kTileSubs interleaved tile
-// subsets per block (every subset's loads issued together), subsets combined
-// in a fixed order (deterministic).
-constexpr int kTileCols = 4;
-constexpr int kTileSubs = 64;
-
+// xbar[b][c] = sum over tiles: one wavefront per column, lane l sums tiles
+// l, l+64, ... (contiguous 512-B loads of the column-major partials), then a
+// fixed xor tree (deterministic).
 __global__ __launch_bounds__(256) void keysum_tiles_kernel(const double* __restrict__ part, int ntiles, int C,
                                                             double* __restrict__ xbar) {
-  __shared__ double red[kWavesPerBlock][kTileCols + 1];
   const int b = blockIdx.y;
-  const int cl = threadIdx.x % kTileCols, sub = threadIdx.x / kTileCols;
-  const int c = blockIdx.x * kTileCols + cl;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int c = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+  if (c > C) return;
+  const double* __restrict__ col = part + ((int64_t)b * (C + 1) + c) * ntiles;
   double s = 0.0;
-  if (c <= C) {
 #pragma unroll 16
-    for (int t = sub; t < ntiles; t += kTileSubs) s += part[((int64_t)b * ntiles + t) * (C + 1) + c];
-  }
-  // fixed tree: the 16 subsets of a wavefront by xor shuffles, then the 4 wavefronts
+  for (int t = lane; t < ntiles; t += kWave) s += col[t];
 #pragma unroll
-  for (int o = kTileCols; o < kWave; o <<= 1) s += __shfl_xor(s, o);
-  const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x >> 6;
-  if (lane < kTileCols) red[wv][lane] = s;
-  __syncthreads();
-  if (threadIdx.x < kTileCols && c <= C) {
-    double a = 0.0;
-#pragma unroll
-    for (int k = 0; k < kWavesPerBlock; ++k) a += red[k][cl];
-    xbar[(int64_t)b * (C + 1) + c] = a;
-  }
+  for (int o = 1; o < kWave; o <<= 1) s += __shfl_xor(s, o);
+  if (lane == 0) xbar[(int64_t)b * (C + 1) + c] = s;
 }
 
 // Per batch element b, from xbar = sum_n indeg(n) x_n (and xbar[C] = E):
@@ -491,32 +463,46 @@ __device__ __forceinline__ void ns_store(double (&acc)[MAXH], const double (&vb)
     buf_store_f64(rcs, (st && h < H) ? (uint32_t)((row * H + h) * 8) : kBufNone, acc[h] + vb[h]);
 }
 
+// One chunk per row: the wave's first two row groups are loaded BEFORE the key
+// projection (their HBM latency hides the LDS prologue), U[b] then sits in
+// registers and the loop keeps two row groups in flight ahead of the one being
+// reduced.  Prefetch addresses past the block's rows clamp to its last row (a
+// cache-line hit, no extra HBM traffic).
 template <int VEC, int GL, int MAXH, bool CLAMP>
-__device__ __forceinline__ void ns_rows_resident(const float* __restrict__ xb, const double* __restrict__ Ub,
-                                                 const double (&vb)[MAXH], __amdgpu_buffer_rsrc_t rcs, int64_t N,
-                                                 int64_t n0, int64_t n1, int C, int64_t ldx, int H, int g, int gl,
-                                                 int wv) {
+__device__ __forceinline__ void ns_block_resident(const KeyProj& kp, int64_t b, const float* __restrict__ xb,
+                                                  double* S, double* Ub, double* vl, __amdgpu_buffer_rsrc_t rcs,
+                                                  int64_t n0, int64_t n1, int C, int64_t ldx, int H, int Cp, int g,
+                                                  int gl, int wv) {
   constexpr int G = kWave / GL;
   constexpr int NP = node_scores_npv<MAXH>() / VEC;
   const int64_t step = (int64_t)kWavesPerBlock * G;
+  const int64_t last = n1 - 1;
+  int64_t nb = n0 + wv * G;
+  float xa[NP][VEC], xn[NP][VEC];
+  ns_load_x<VEC, NP, GL, CLAMP>(xb + min(nb + g, last) * ldx, 0, gl, C, xa);
+  ns_load_x<VEC, NP, GL, CLAMP>(xb + min(nb + g + step, last) * ldx, 0, gl, C, xn);
+  key_projection_lds(kp, b, C, H, Cp, MAXH, S, Ub, vl);
   double u[NP][VEC][MAXH];
   ns_load_u<VEC, NP, GL, MAXH>(Ub, 0, gl, u);
-  float xc[NP][VEC];
-  int64_t nb = n0 + wv * G;
-  ns_load_x<VEC, NP, GL, CLAMP>(xb + min(nb + g, N - 1) * ldx, 0, gl, C, xc);
+  double vb[MAXH];
+#pragma unroll
+  for (int h = 0; h < MAXH; ++h) vb[h] = vl[h];
   for (; nb < n1; nb += step) {
     const int64_t nr = nb + g;
-    float xn[NP][VEC];
-    ns_load_x<VEC, NP, GL, CLAMP>(xb + min(nr + step, N - 1) * ldx, 0, gl, C, xn);
+    float xf[NP][VEC];
+    ns_load_x<VEC, NP, GL, CLAMP>(xb + min(nr + 2 * step, last) * ldx, 0, gl, C, xf);
     double acc[MAXH];
 #pragma unroll
     for (int h = 0; h < MAXH; ++h) acc[h] = 0.0;
-    ns_dot<VEC, NP, MAXH>(xc, u, acc);
+    ns_dot<VEC, NP, MAXH>(xa, u, acc);
     ns_store<GL, MAXH>(acc, vb, gl, H, nr < n1, rcs, nr);
 #pragma unroll
     for (int p = 0; p < NP; ++p)
 #pragma unroll
-      for (int i = 0; i < VEC; ++i) xc[p][i] = xn[p][i];
+      for (int i = 0; i < VEC; ++i) {
+        xa[p][i] = xn[p][i];
+        xn[p][i] = xf[p][i];
+      }
   }
 }
 
@@ -542,18 +528,18 @@ __global__ __launch_bounds__(256) void node_scores_kernel(const float* __restric
   double* vl = Ub + Cp * MAXH;
   for (int64_t b = blockIdx.y; b < B; b += gridDim.y) {
     if (b != blockIdx.y) __syncthreads();  // the previous element's U is no longer read
-    key_projection_lds(kp, b, C, H, Cp, MAXH, S, Ub, vl);
     const float* __restrict__ xb = x + b * N * ldx;
     const __amdgpu_buffer_rsrc_t rcs = buf_rsrc(cs + b * N * H);
-    double vb[MAXH];
-#pragma unroll
-    for (int h = 0; h < MAXH; ++h) vb[h] = vl[h];
     if (nch == 1) {
       if (ragged)
-        ns_rows_resident<VEC, GL, MAXH, true>(xb, Ub, vb, rcs, N, n0, n1, C, ldx, H, g, gl, wv);
+        ns_block_resident<VEC, GL, MAXH, true>(kp, b, xb, S, Ub, vl, rcs, n0, n1, C, ldx, H, Cp, g, gl, wv);
       else
-        ns_rows_resident<VEC, GL, MAXH, false>(xb, Ub, vb, rcs, N, n0, n1, C, ldx, H, g, gl, wv);
+        ns_block_resident<VEC, GL, MAXH, false>(kp, b, xb, S, Ub, vl, rcs, n0, n1, C, ldx, H, Cp, g, gl, wv);
     } else {
+      key_projection_lds(kp, b, C, H, Cp, MAXH, S, Ub, vl);
+      double vb[MAXH];
+#pragma unroll
+      for (int h = 0; h < MAXH; ++h) vb[h] = vl[h];
       for (int64_t nb = n0 + wv * G; nb < n1; nb += step) {
         const int64_t nr = nb + g;
         const float* xrow = xb + min(nr, N - 1) * ldx;
@@ -641,12 +627,15 @@ static void launch_node_scores(dim3 grid, const NsGeom& ge, hipStream_t s, const
     node_scores_kernel<VEC, 64, MAXH><<<grid, kBlock, shm, s>>>(x, B, N, C, ldx, H, n, kp, cs, rpb);
 }
 
-// rows per block sized for ~4096 wavefronts over the whole launch (16 per CU)
+// rows per block sized for ~2048 wavefronts over the whole launch: the kernel
+// holds ~210 VGPRs (U[b] in registers + two row groups in flight), so 2 waves
+// per SIMD = 2 blocks per CU are resident and the whole grid runs in one round
+// (4096 waves left a 1.7-round tail: 26.9 us for an 87 MB pass)
 static void launch_node_scores_any(hipStream_t s, const NsGeom& ge, const float* x, int64_t B, int64_t N, int C,
                                    int64_t ldx, int H, const KeyProj& kp, double* cs) {
   const int G = kWave / ge.GL;
   const int64_t groups = ceil_div(N, (int64_t)G);
-  const int64_t waves_per_batch = std::max<int64_t>(1, 4096 / B);
+  const int64_t waves_per_batch = std::max<int64_t>(1, 2048 / B);
   const int64_t iters = std::max<int64_t>(1, ceil_div(groups, waves_per_batch));
   const int64_t rpb = (int64_t)kWavesPerBlock * G * iters;
   const dim3 grid((unsigned)ceil_div(N, rpb), (unsigned)std::min<int64_t>(B, 65535));
@@ -725,6 +714,10 @@ int gnpde_attn_ref_rhs_f32(const int32_t* items, int64_t n_items, int32_t* heavy
                 (long long)heads);
   GNPDE_REQUIRE(n_items >= 0 && n_items < INT32_MAX && n_heavy >= 0, GNPDE_EINVAL, "attn_ref_rhs: bad item counts");
   GNPDE_REQUIRE(n_items == 0 || (items && col && cs && m && rl), GNPDE_EINVAL, "attn_ref_rhs: NULL plan/col/cs/m/rl");
+  if (heads == 2 && aligned16(m) && aligned8(rl)) {
+    RefDstSoftmaxWeights<2, true> wp{cs, m, rl, 2};
+    return launch_agg(items, n_items, heavy, n_heavy, col, wp, C, ep, partials, as_stream(stream));
+  }
   if (heads <= 2) {
     RefDstSoftmaxWeights<2> wp{cs, m, rl, (int)heads};
     return launch_agg(items, n_items, heavy, n_heavy, col, wp, C, ep, partials, as_stream(stream));
@@ -853,7 +846,7 @@ int gnpde_ref_scores_f32(const float* x, int64_t B, int64_t N, int64_t C, int64_
   else
     keysum_partial_kernel<1><<<g1, kBlock, shm, s>>>(x, N, (int)C, ldx, indeg, rpt, tpr, ntiles, part);
   GNPDE_LAUNCH_CHECK();
-  keysum_tiles_kernel<<<dim3((unsigned)ceil_div(C + 1, kTileCols), (unsigned)B), kBlock, 0, s>>>(part, ntiles, (int)C,
+  keysum_tiles_kernel<<<dim3((unsigned)ceil_div(C + 1, kWavesPerBlock), (unsigned)B), kBlock, 0, s>>>(part, ntiles, (int)C,
                                                                                                  xbar);
   GNPDE_LAUNCH_CHECK();
   const KeyProj kp{xbar, Wq, bq, Wk, bk, (int)att};

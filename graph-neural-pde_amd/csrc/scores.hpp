@@ -104,6 +104,29 @@ __device__ __forceinline__ int wave_max_int(int v) {
 // Hub groups of the statistics kernels: merge the per-chunk (max, sum-exp)
 // partials [slot][2H] (max as fp64, then sum) into m[g,h], rl[g,h] = 1/(sum + 1e-16).
 // heavy: int4 {group, first_slot, n_chunks, 0}.  Defined in rhs.hip.
+// Merge of long group g's chunk statistics for head h (chunks first .. first+nch-1
+// of partials: [slot][M(H) | L(H)]): lanes take strided chunks, then a fixed xor
+// tree, so the result does not depend on which wave or launch runs it.
+__device__ __forceinline__ void stats_merge_store(int g, int first, int nch, int H, int h,
+                                                  const double* __restrict__ partials, double* __restrict__ m_out,
+                                                  float* __restrict__ rl_out) {
+  const int lane = threadIdx.x & 63;
+  double M = -INFINITY;
+  float L = 0.f;
+  for (int c = lane; c < nch; c += kWave)
+    online_merge(M, L, partials[(int64_t)(first + c) * 2 * H + h], (float)partials[(int64_t)(first + c) * 2 * H + H + h]);
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const double M2 = __shfl_xor(M, o);
+    const float L2 = __shfl_xor(L, o);
+    online_merge(M, L, M2, L2);
+  }
+  if (lane == 0) {
+    m_out[(int64_t)g * H + h] = M;
+    rl_out[(int64_t)g * H + h] = 1.0f / (L + kSoftmaxEps);
+  }
+}
+
 int launch_stats_fixup(const int4* heavy, int64_t n_heavy, int H, const double* partials, double* m, float* rl,
                        hipStream_t s);
 
