@@ -1,6 +1,7 @@
 #!/bin/bash
 # BLEND (configs[3] shape) fp32 vs bf16 rk4 step time under K1 lane-geometry knobs.
-for cfg in "8 0" "4 0" "8 1" "8 3" "4 3"; do set -- $cfg
+# BLEND_CFGS="vec:variant ..." (GNPDE_BF16_VEC : GNPDE_AGG_VARIANT)
+for cfg in ${BLEND_CFGS:-8:0 4:0 8:1 8:3 4:3}; do set -- ${cfg/:/ }
 GNPDE_BF16_VEC=$1 GNPDE_AGG_VARIANT=$2 timeout -k 10 200 python -c "
 import sys, torch, json; sys.path.insert(0,'graph-neural-pde_amd'); sys.path.insert(0,'.')
 import bench
