@@ -9,7 +9,7 @@ STEPS="${STEPS:-smoke tests bench}"
 for s in $STEPS; do
   case $s in
     smoke) timeout -k 10 400 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; rc=$? ;;
-    tests) timeout -k 10 1200 python -u -m pytest tests -m gpu -q -ra --timeout 120 --timeout-method thread ${PYTEST_ARGS:-} > gpurun_out/gpu_tests.log 2>&1; rc=$? ;;
+    tests) timeout -k 10 1200 python -u -m pytest tests -m gpu -q -ra --timeout 120 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > gpurun_out/gpu_tests.log 2>&1; rc=$? ;;
     bench) timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.log 2>&1; rc=$? ;;
     *) echo "unknown step $s"; rc=2 ;;
   esac
