@@ -16,7 +16,7 @@ import torch
 
 from . import _lib
 
-DEFAULT_CHUNK = 256  # hub-splitting threshold (edges per wavefront work item)
+DEFAULT_CHUNK = 128  # hub-splitting threshold (edges per wavefront work item; G-arxiv A/B: 64 137, 96 123, 128 121, 160 123, 256 128, 512 135 us per rk4 RHS)
 STATS_CHUNK = 64     # items of the softmax-statistics kernel (8 lanes per item)
 
 

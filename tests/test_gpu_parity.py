@@ -130,7 +130,7 @@ def test_kat_symmetric_attention_exactly_half():
 # ---------------------------------------------------------------- random graphs with hubs (plan split path)
 def hub_graph(N, E, seed, B=1, hub_frac=0.15):
     """Random graph where node 0 (and node 1 as destination) receive a large
-    share of the edges, so rows/columns exceed the 256-edge chunk."""
+    share of the edges, so rows/columns exceed the default chunk."""
     rng = np.random.default_rng(seed)
     ei = rng.integers(0, N, size=(B, 2, E))
     nh = int(hub_frac * E)

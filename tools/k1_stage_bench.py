@@ -39,9 +39,11 @@ def main():
     x = synthetic.features(1, N, C, device=dev)
     opt = {'hidden_dim': C, 'block': 'constant', 'add_source': False, 'no_alpha_sigmoid': False, 'max_nfe': 10 ** 9,
            'multi_modal': False}
+    if os.environ.get("K1_CHUNK"):
+        opt['gnpde_chunk'] = int(os.environ["K1_CHUNK"])  # hub-splitting threshold (default 256)
     func = gnpde.LaplacianODEFunc(C, C, opt, dev).to(dev)
     func.edge_index, func.edge_weight = ei, w
-    r = {"N": N, "E": E, "C": C}
+    r = {"N": N, "E": E, "C": C, "chunk": opt.get('gnpde_chunk', 256)}
     with torch.no_grad():
         g = func.graph_for(x)
         wc = func.csr_weights(g, w, 'w')
