@@ -10,6 +10,7 @@ Layout: node features [B,N,C] fp32 row-major, viewed as
 (rowptr[R+1], col[nnz] global node ids, perm[nnz] CSR pos -> COO edge id).
 """
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -18,6 +19,10 @@ from . import _lib
 
 DEFAULT_CHUNK = 128  # hub-splitting threshold (edges per wavefront work item; G-arxiv A/B: 64 137, 96 123, 128 121, 160 123, 256 128, 512 135 us per rk4 RHS)
 STATS_CHUNK = 64     # items of the softmax-statistics kernel (8 lanes per item)
+# K1 work items longest first ("lpt", stable; A/B on G-arxiv rk4: 8,130-8,205 against 7,917-7,932
+# RHS/s in row order; BLEND step 0.585 against 0.650 ms fp32, 0.434 against 0.565 ms bf16).
+# GNPDE_PLAN_ORDER=rows keeps the builder's row order.  Results do not depend on it.
+PLAN_ORDER = os.environ.get("GNPDE_PLAN_ORDER", "lpt")
 
 
 def _ptr(t):
@@ -114,6 +119,11 @@ def build_plan(rowptr, R, nnz, chunk=DEFAULT_CHUNK):
     n_it, n_hv, n_sl = ctypes.c_int64(0), ctypes.c_int64(0), ctypes.c_int64(0)
     _lib.call("gnpde_plan_build", _ptr(rowptr), R, chunk, _ptr(items), cap_items, _ptr(heavy), cap_heavy,
               ctypes.byref(n_it), ctypes.byref(n_hv), ctypes.byref(n_sl), _ptr(ws), ws_bytes, _stream(dev))
+    if PLAN_ORDER == "lpt" and n_it.value > 1:
+        # longest items first (stable): the wavefronts dispatched last are the short ones
+        it = items[:n_it.value * 4].view(-1, 4)
+        order = torch.argsort(it[:, 1] - it[:, 2], stable=True)
+        it.copy_(it[order])
     return Plan(items, heavy, n_it.value, n_hv.value, n_sl.value, chunk)
 
 

@@ -186,6 +186,8 @@ def test_csr_structures_exact():
         cover[b0:b1] += 1
     assert np.all(cover == 1)
     assert len(np.unique(items[:, 0])) == B * N  # every row has an item (empty rows too)
+    if ops.PLAN_ORDER == "lpt":  # longest items dispatched first
+        assert np.all(np.diff(items[:, 2] - items[:, 1]) <= 0)
     deg = g.indeg.cpu().numpy()
     assert np.array_equal(deg, np.bincount(dst, minlength=B * N))
 
