@@ -17,7 +17,10 @@ import torch
 
 from . import _lib
 
-DEFAULT_CHUNK = 128  # hub-splitting threshold (edges per wavefront work item; G-arxiv A/B: 64 137, 96 123, 128 121, 160 123, 256 128, 512 135 us per rk4 RHS)
+# hub-splitting threshold (edges per K1 work item).  With the longest-first item
+# order below, full-bench A/B on G-arxiv: 128 -> 8,048-8,200, 256 -> 8,485-8,496,
+# 384 -> 8,434-8,450 RHS/s (in row order 128 was best: 121 against 128 us per RHS)
+DEFAULT_CHUNK = int(os.environ.get("GNPDE_CHUNK", 256))
 STATS_CHUNK = 64     # items of the softmax-statistics kernel (8 lanes per item)
 # K1 work items longest first ("lpt", stable; A/B on G-arxiv rk4: 8,130-8,205 against 7,917-7,932
 # RHS/s in row order; BLEND step 0.585 against 0.650 ms fp32, 0.434 against 0.565 ms bf16).
