@@ -346,6 +346,10 @@ static int launch_agg_vec(const int4* items, int64_t n_items, int4* heavy, int64
   launch_agg_cfg<VEC, GL, NCH, U, RPW, WP, T>(items, n_items, heavy, n_heavy, col, wp, C, ep, partials, s)
   if (lanes <= 16) return GNPDE_AGG(16, 1, 4, 1);
   if (lanes <= 32) {
+    if constexpr (sizeof(T) == 2) {
+      // bf16 rows of 17-32 lanes: two rows per wavefront (epi_vec_width); variant 4 = one row
+      if (agg_variant() != 4 && lanes > 16) return GNPDE_AGG(32, 1, 4, 2);
+    }
     switch (agg_variant()) {
       case 1: return GNPDE_AGG(32, 1, 4, 2);
       case 2: return GNPDE_AGG(32, 1, 2, 1);
@@ -373,9 +377,14 @@ static int launch_agg_vec(const int4* items, int64_t n_items, int4* heavy, int64
 // elements per lane of bf16 rows (default 4 = 8-byte gathers; 8 = 16-byte).
 int bf16_vec_cap();
 
+// bf16 rows are sized to land in 17-32 lanes, the two-rows-per-wavefront
+// geometry (launch_agg_vec): 8-byte gathers up to 128 columns, 16-byte gathers
+// for 129-256 columns (G-arxiv, items longest first: C = 128 58 us against 77-96;
+// BLEND C = 168 77 us against 93-122, 0.353-0.361 ms per rk4 step against 0.402).
 template <class T = float>
 inline int epi_vec_width(const Epi& ep, int64_t C, const void* partials) {
-  const int kMax = sizeof(T) == 2 ? bf16_vec_cap() : 16 / (int)sizeof(T);
+  const int kMax = sizeof(T) == 2 ? ((C > 128 && C <= 256 && bf16_vec_cap() >= 4) ? 8 : bf16_vec_cap())
+                                  : 16 / (int)sizeof(T);
   for (int v = kMax; v > 1; v >>= 1) {
     const size_t bytes = (size_t)v * sizeof(T);
     auto al = [&](const void* p) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) % bytes) == 0; };

@@ -8,8 +8,8 @@ namespace gnpde {
 
 int bf16_vec_cap() {
   static const int v = [] {
-    // 4 (8-byte gathers) measured fastest on the BLEND rows (tools/blend_cmp.sh: 0.647 ms per rk4
-    // step against 0.766 ms with 16-byte gathers, whose wider lanes cost occupancy)
+    // cap of the elements per lane (default 4 = 8-byte gathers); rows of 129-256 columns take
+    // 16-byte gathers anyway (epi_vec_width) so that they fit the two-rows-per-wavefront geometry
     const char* e = std::getenv("GNPDE_BF16_VEC");
     const int c = e ? std::atoi(e) : 4;
     return (c == 1 || c == 2 || c == 8) ? c : 4;
