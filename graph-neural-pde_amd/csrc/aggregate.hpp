@@ -335,7 +335,8 @@ static int launch_agg_cfg(const int4* items, int64_t n_items, int4* heavy, int64
 }
 
 // Experiment knob (not part of the ABI contract): GNPDE_AGG_VARIANT selects an
-// alternative lane geometry for the dominant 32-lane (C = 128 fp32) case.
+// alternative lane geometry for the dominant 32-lane (C = 128 fp32) case
+// (2: U = 2, 3: U = 8, 4: one row per wavefront; default: two rows per wavefront).
 int agg_variant();
 
 template <int VEC, class WP, class T = float>
@@ -346,17 +347,16 @@ static int launch_agg_vec(const int4* items, int64_t n_items, int4* heavy, int64
   launch_agg_cfg<VEC, GL, NCH, U, RPW, WP, T>(items, n_items, heavy, n_heavy, col, wp, C, ep, partials, s)
   if (lanes <= 16) return GNPDE_AGG(16, 1, 4, 1);
   if (lanes <= 32) {
-    if constexpr (sizeof(T) == 2) {
-      // bf16 rows of 17-32 lanes: two rows per wavefront (epi_vec_width); variant 4 = one row
-      if (agg_variant() != 4 && lanes > 16) return GNPDE_AGG(32, 1, 4, 2);
-    }
+    // two rows per wavefront (fp32 C = 128 and bf16 rows of 17-32 lanes): with the
+    // plan's items longest first, G-arxiv rk4 bench 9,301 against 8,643 RHS/s with
+    // one row per wavefront (variant 4); hub rows then go to agg_fixup_kernel
     switch (agg_variant()) {
-      case 1: return GNPDE_AGG(32, 1, 4, 2);
       case 2: return GNPDE_AGG(32, 1, 2, 1);
       case 3: return GNPDE_AGG(32, 1, 8, 1);
+      case 4: return GNPDE_AGG(32, 1, 4, 1);
       default: break;
     }
-    return GNPDE_AGG(32, 1, 4, 1);
+    return GNPDE_AGG(32, 1, 4, 2);
   }
   if (lanes <= 64) {
     if (agg_variant() == 3) return GNPDE_AGG(64, 1, 8, 1);
