@@ -166,7 +166,7 @@ def main():
         integ.replay_events = None
     assert torch.isfinite(y).all()
     # per-RHS launch time: eager launches are bracketed one by one; a replayed
-    # step (4 K1 launches + their hub fixups, nothing else) is bracketed whole
+    # step (4 K1 launches, hub rows combined inside them, nothing else) is bracketed whole
     t_ev = sum(s.elapsed_time(e) for s, e in events) + sum(s.elapsed_time(e) for s, e, _ in replays)
     n_ev = len(events) + sum(n for _, _, n in replays)
     k1_ms = t_ev / max(n_ev, 1)
@@ -180,10 +180,10 @@ def main():
     ms_per_step = elapsed * 1e3 / args.steps
     if args.rhs_only:
         nbytes = lap_bytes(N, E, C)
-        kname = "agg_kernel<4,32,1,4,2,0,PlainWeights,float> + agg_fixup_kernel<4,32,0,float> (two rows per wavefront; hub rows in the fixup)"
+        kname = "agg_kernel<4,32,1,4,2,0,PlainWeights,float> (two rows per wavefront; hub rows combined in-launch)"
     else:
         nbytes = rk4_fused_step_bytes(N, E, C) / 4.0
-        kname = "agg_kernel<4,32,1,4,2,1,PlainWeights,float> + agg_fixup_kernel<4,32,1,float>: K1 with fused rk4 stage, two rows per wavefront (time per RHS includes the hub fixup)"
+        kname = "agg_kernel<4,32,1,4,2,1,PlainWeights,float>: K1 with fused rk4 stage, two rows per wavefront (hub rows combined in-launch)"
     achieved = nbytes / (k1_ms * 1e-3) / 1e9
 
     # the plain RHS (no fused stage) on the same graph, for the per-RHS roofline
@@ -205,7 +205,7 @@ def main():
         pb = lap_bytes(N, E, C)
         plain = {"rhs_ms": round(pms, 4), "achieved": round(pb / (pms * 1e-3) / 1e9, 1),
                  "frac": round(pb / (pms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "algorithmic_bytes": pb,
-                 "kernel": "agg_kernel<4,32,1,4,2,0,PlainWeights,float> + agg_fixup_kernel<4,32,0,float>"}
+                 "kernel": "agg_kernel<4,32,1,4,2,0,PlainWeights,float> (hub rows combined in-launch)"}
 
     traffic = None
     tp = os.path.join(ROOT, "profiles", "k1_traffic.json")

@@ -150,15 +150,52 @@ __device__ __forceinline__ void hub_arrive(int4* heavy, int n_heavy, int slot, i
   if ((threadIdx.x & 63) == 0) __hip_atomic_store(ticket_word, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// The RPW > 1 form of hub_arrive: each row slot of the wavefront that holds a
+// hub chunk takes its own ticket (its first lane); every slot whose chunk
+// arrived last is then combined by the WHOLE wavefront, one slot after the
+// other (hub_combine over 64 lanes: the same sums, in the same order, as
+// agg_fixup_kernel).  Called by all 64 lanes; `chunk` is per slot.
+template <int VEC, int GL, int SL, int RPW, int STG, class T>
+__device__ __forceinline__ void hub_arrive_slots(int4* heavy, int n_heavy, bool chunk, int slot, int C,
+                                                 const Epi& ep, const float* partials) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const int lane = threadIdx.x & 63;
+  int lo = 0, won = 0;
+  if (chunk) {
+    int hi = n_heavy - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (heavy[mid].y <= slot)
+        lo = mid;
+      else
+        hi = mid - 1;
+    }
+    if (lane % SL == 0) {
+      const int t = __hip_atomic_fetch_add(&heavy[lo].w, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      won = t == heavy[lo].z - 1;
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < RPW; ++s) {
+    if (__shfl(won, s * SL)) {  // wave-uniform
+      const int h = __shfl(lo, s * SL);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      const int4 hv = heavy[h];
+      hub_combine<VEC, GL, STG, T>(uniform(hv.x), uniform(hv.y), uniform(hv.z), C, ep, partials);
+      if (lane == 0) __hip_atomic_store(&heavy[h].w, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
 // ------------------------------------------------------------------ aggregation kernel
 // Lane layout: RPW row slots of SL = 64/RPW lanes per wavefront (one plan item
 // each); inside a slot lane = g*GL + gl: G = SL/GL edges are gathered side by
 // side, each by a group of GL lanes covering the C columns with VEC-wide loads
 // (NCH column passes); U edges per group are in flight per iteration.  The
 // epilogue operands (x_r, x0_r, stage inputs) are loaded before the gathers
-// when NCH <= 2 (PRE) so their latency overlaps the aggregation.  RPW == 1:
-// hub rows are combined in-launch (hub_arrive); RPW > 1 leaves the partials
-// to agg_fixup_kernel.
+// when NCH <= 2 (PRE) so their latency overlaps the aggregation.  Hub rows are
+// combined in-launch by the chunk that arrives last (hub_arrive for RPW == 1,
+// hub_arrive_slots for RPW > 1).
 template <int VEC, int GL, int NCH, int U, int RPW, int STG, class WP, class T = float>
 __global__ __launch_bounds__(256) void agg_kernel(const int4* __restrict__ items, int n_items, int4* heavy,
                                                    int n_heavy, const int* __restrict__ col, WP wp, int C, Epi ep,
@@ -262,6 +299,25 @@ __global__ __launch_bounds__(256) void agg_kernel(const int4* __restrict__ items
       hub_arrive<VEC, GL, STG, T>(heavy, n_heavy, slot, C, ep, partials);
       return;
     }
+  } else {
+    if (n_heavy > 0) {  // hub chunks of any slot combined in-launch (hub_arrive_slots)
+      const bool chunk = live && slot >= 0;
+      int anyc = 0;
+#pragma unroll
+      for (int s = 0; s < RPW; ++s) anyc |= __shfl((int)chunk, s * SL);
+      if (anyc) {  // wave-uniform
+        if (chunk && g == 0) {
+          const __amdgpu_buffer_rsrc_t rp = buf_rsrc(partials);
+#pragma unroll
+          for (int ch = 0; ch < NCH; ++ch) {
+            const int cc = (ch * GL + gl) * VEC;
+            buf_store_wt<VEC>(rp, cc < C ? (uint32_t)(((int64_t)slot * C + cc) * 4) : kBufNone, acc[ch]);
+          }
+        }
+        hub_arrive_slots<VEC, GL, SL, RPW, STG, T>(heavy, n_heavy, chunk, slot, C, ep, partials);
+        if (chunk) return;
+      }
+    }
   }
   if (!live || g != 0) return;
   if (slot >= 0) {
@@ -286,7 +342,7 @@ __global__ __launch_bounds__(256) void agg_kernel(const int4* __restrict__ items
   }
 }
 
-// Hub rows of the RPW > 1 geometries: one wavefront per hub, after the aggregation launch.
+// Hub rows combined after the aggregation launch (GNPDE_HUB_FIXUP=1): one wavefront per hub.
 template <int VEC, int GL, int STG, class T = float>
 __global__ __launch_bounds__(256) void agg_fixup_kernel(const int4* __restrict__ heavy, int n_heavy, int C, Epi ep,
                                                          const float* __restrict__ partials) {
@@ -305,8 +361,11 @@ static int launch_agg_cfg(const int4* items, int64_t n_items, int4* heavy, int64
                           const WP& wp, int C, const Epi& ep, float* partials, hipStream_t s) {
   const unsigned grid = (unsigned)ceil_div(n_items, (int64_t)kWavesPerBlock * RPW);
   const unsigned gfix = (unsigned)ceil_div(n_heavy, kWavesPerBlock);
-  // hub rows combined in the launch (RPW == 1) or by agg_fixup_kernel after it
-  const bool inlaunch = hub_inlaunch();
+  // hub rows combined in the launch (hub_arrive / hub_arrive_slots) or, with
+  // GNPDE_HUB_FIXUP=1, by agg_fixup_kernel after it
+  // (8-element lanes — bf16 rows of 129-256 columns — keep the separate pass: their in-launch
+  // combine fails the bf16 parity tests, cause not found yet)
+  const bool inlaunch = hub_inlaunch() && VEC <= 4;
   const int nh = inlaunch ? (int)n_heavy : 0;
   // single-output stages (every gnpde.integrator step) get the leaner instantiation
   const int stg = ep.has_stage ? (ep.st.n_out <= 1 ? 1 : 2) : 0;
@@ -322,7 +381,7 @@ static int launch_agg_cfg(const int4* items, int64_t n_items, int4* heavy, int64
                                                                           partials);
     GNPDE_LAUNCH_CHECK();
   }
-  if ((RPW > 1 || !inlaunch) && n_heavy > 0) {
+  if (!inlaunch && n_heavy > 0) {
     if (stg == 1)
       agg_fixup_kernel<VEC, GL, 1, T><<<gfix, kBlock, 0, s>>>(heavy, (int)n_heavy, C, ep, partials);
     else if (stg == 2)
