@@ -363,9 +363,7 @@ static int launch_agg_cfg(const int4* items, int64_t n_items, int4* heavy, int64
   const unsigned gfix = (unsigned)ceil_div(n_heavy, kWavesPerBlock);
   // hub rows combined in the launch (hub_arrive / hub_arrive_slots) or, with
   // GNPDE_HUB_FIXUP=1, by agg_fixup_kernel after it
-  // (8-element lanes — bf16 rows of 129-256 columns — keep the separate pass: their in-launch
-  // combine fails the bf16 parity tests, cause not found yet)
-  const bool inlaunch = hub_inlaunch() && VEC <= 4;
+  const bool inlaunch = hub_inlaunch();
   const int nh = inlaunch ? (int)n_heavy : 0;
   // single-output stages (every gnpde.integrator step) get the leaner instantiation
   const int stg = ep.has_stage ? (ep.st.n_out <= 1 ? 1 : 2) : 0;

@@ -384,7 +384,9 @@ __device__ __forceinline__ void buf_store_wt(__amdgpu_buffer_rsrc_t r, uint32_t 
     for (int q = 0; q < VEC / 4; ++q) {
       const u32x4 d = {__builtin_bit_cast(uint32_t, v[4 * q]), __builtin_bit_cast(uint32_t, v[4 * q + 1]),
                        __builtin_bit_cast(uint32_t, v[4 * q + 2]), __builtin_bit_cast(uint32_t, v[4 * q + 3])};
-      __builtin_amdgcn_raw_buffer_store_b128(d, r, off + 16 * q, 0, kAuxSc1);
+      // a dropped store (kBufNone) stays dropped: kBufNone + 16 would wrap to offset 0
+      const uint32_t o = off >= kBufRecords ? kBufNone : off + 16u * q;
+      __builtin_amdgcn_raw_buffer_store_b128(d, r, o, 0, kAuxSc1);
     }
   } else if constexpr (VEC == 2) {
     const u32x2 d = {__builtin_bit_cast(uint32_t, v[0]), __builtin_bit_cast(uint32_t, v[1])};
