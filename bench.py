@@ -239,6 +239,8 @@ def main():
                      # measured HBM bytes (PMC, profiles/k1_traffic.json) over the same launch time: the
                      # algorithmic rate passes the peak because x is re-read from the Infinity Cache
                      "traffic_GBs": round(traffic / (k1_ms * 1e-3) / 1e9, 1) if traffic else None,
+                     "note": "achieved charges every gathered row to HBM (SURVEY 8(d) bytes); x stays in the "
+                             "256 MB Infinity Cache between gathers, so the measured HBM traffic is lower",
                      "kernel": kname, "algorithmic_bytes_per_launch": int(nbytes),
                      "launch_ms": round(k1_ms, 4), "launches": n_ev,
                      "graph_replays": len(replays)},
