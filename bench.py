@@ -10,17 +10,30 @@ src/best_params.py:7 for ogbn-arxiv) and gnpde.odeint.  A "step" is one rk4
 step: 4 RHS evaluations (K1, gnpde_spmm_rhs_f32) whose epilogues also emit the
 Runge-Kutta stage combinations.
 
-value = RHS evaluations per second over the whole job (all ranks), inputs
-resident in HBM.  Multi-GPU: one process per GPU, each integrating its own
-G-arxiv graph (the reference's batch axis; independent objects, no data-path
-collective) -> "scaling": "weak"; the time is the max over ranks.
+value = RHS evaluations per second over the whole job, inputs resident in HBM.
+
+Multi-GPU (one process per GPU, RCCL): by default ONE shared graph, strong
+scaling.  The headline is G-arxiv in feature-column stripes
+(gnpde.dist.ColumnShardedLaplacian: replicated CSR, C/N columns per rank, no
+per-RHS collective); every line also carries the configs[4] graph (G-rmat:
+N = 2M, E = 20M, C = 256) in column stripes and in the north star's literal
+row partition (nnz-balanced blocks + an RCCL all-gather of the state before
+every RHS), each with the same graph timed unsharded on one GPU of the same
+job ("speedup_vs_1gpu").  --mode replicas keeps the old independent-graph
+weak-scaling layout.
 
 Extra objects on the JSON line:
-  roofline      K1 achieved GB/s (algorithmic bytes / mean per-launch time from
-                HIP events on the launch stream) vs the 8 TB/s HBM peak;
-  cpu_baseline  the CPU oracle (scipy CSR, fp32) on a bounded sample, rank 0, N=1;
+  roofline      K1: measured HBM bytes per launch (PMC 2*FETCH_SIZE + WRITE_SIZE,
+                profiles/k1_traffic.json) over the mean launch time from HIP
+                events on the launch stream, vs 8 TB/s; the SURVEY §8(d)
+                algorithmic byte count over the same time is kept as
+                algorithmic_achieved / algorithmic_frac;
+  cpu_baseline  torch sparse CSR A@x on the host cores (the reference's CPU
+                path restated with torch.sparse), bounded sample, rank 0, N=1;
   attention     the transformer RHS (config C4 shape: C=128, h=2, att=32) in
-                reference (fork scaled_dot) and per_edge modes.
+                reference (fork scaled_dot) and per_edge modes;
+  blend_c162    configs[3] shape (C = 162) rk4 steps, fp32 and bf16 state;
+  grmat         configs[4] graph (see above).
 """
 import argparse
 import json
@@ -84,12 +97,62 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU-baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-attention", action="store_true")
+    p.add_argument("--no-grmat", action="store_true", help="skip the configs[4] graph (G-rmat) measurements")
+    p.add_argument("--grmat-steps", type=int, default=10, help="timed rk4 steps on G-rmat")
     p.add_argument("--rhs-only", action="store_true", help="time K plain RHS calls instead of rk4 steps")
     p.add_argument("--rhs-plain-reps", type=int, default=20, help="plain-RHS launches timed after the steps")
-    p.add_argument("--mode", choices=("replicas", "rows", "cols"), default="replicas",
-                   help="multi-GPU layout: independent graph per rank (weak), or one graph row-partitioned with an "
-                        "all-gather per RHS / column-striped (strong)")
+    p.add_argument("--mode", choices=("auto", "replicas", "rows", "cols"), default="auto",
+                   help="multi-GPU layout of the headline: auto = cols for N > 1; cols / rows = one shared graph "
+                        "(column stripes / row partition + all-gather per RHS, strong scaling); replicas = an "
+                        "independent graph per rank (weak scaling)")
     return p.parse_args()
+
+
+LAP_OPT = {'block': 'constant', 'function': 'laplacian', 'add_source': False, 'no_alpha_sigmoid': False,
+           'max_nfe': 10 ** 9, 'multi_modal': False}
+
+
+def sync_all(world):
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+
+
+def max_over_ranks(v, world, dev):
+    if world > 1:
+        t = torch.tensor([v], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        v = float(t)
+    return v
+
+
+def rk4_solve(func, y0, n, h, dev):
+    """Exactly n rk4 steps through the drop-in integrator (stage combinations
+    fused into the RHS epilogues, steps replayed from captured hipGraphs)."""
+    import gnpde
+    t = torch.tensor([0.0, n * h], dtype=torch.float32, device=dev)
+    return gnpde.odeint(func, y0, t, method='rk4', options={'step_size': h})[1]
+
+
+def timed_solve(func, y0, steps, warmup, h, dev, world, sync_world=None):
+    """W warm-up steps, then the one-time capture of the step / block graphs the
+    timed call replays (a warm-up shorter than GRAPH_MIN_STEPS captures nothing),
+    then EXACTLY `steps` rk4 steps between barriers; max over ranks."""
+    import gnpde.integrator as integ
+    sw = world if sync_world is None else sync_world
+    with torch.no_grad():
+        if warmup > 0:
+            rk4_solve(func, y0, warmup, h, dev)
+        if getattr(func, 'graph_capturable', True):
+            rk4_solve(func, y0, max(integ.GRAPH_MIN_STEPS, 2 * integ.GRAPH_BLOCK), h, dev)
+        sync_all(sw)
+        t0 = time.perf_counter()
+        y = rk4_solve(func, y0, steps, h, dev)
+        sync_all(sw)
+        el = time.perf_counter() - t0
+    assert torch.isfinite(y).all()
+    return max_over_ranks(el, sw, dev), y
 
 
 def main():
@@ -102,18 +165,30 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    mode = args.mode if args.mode != "auto" else ("replicas" if world == 1 else "cols")
+    if mode == "replicas":
+        result = bench_single(args, world, rank, dev)
+    else:
+        result = bench_sharded(args, world, rank, dev, mode)
+    if not args.no_grmat:
+        result["grmat"] = bench_grmat(args, world, rank, dev)
+    if rank == 0:
+        print(json.dumps(result))
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
 
+
+def bench_single(args, world, rank, dev):
+    """The configs[2] headline: G-arxiv rk4 on one GPU (with N > 1 in replicas
+    mode: an independent graph per rank, weak scaling)."""
     import gnpde
     from gnpde import ops, synthetic
 
     N, E, C = args.nodes, args.edges, args.dim
-    if args.mode != "replicas":
-        return bench_sharded(args, world, rank, dev)
     ei, w = synthetic.rw_graph(N, E, seed=rank, device=dev)
     x = synthetic.features(1, N, C, seed=1 + rank, device=dev)
-    opt = {'hidden_dim': C, 'block': 'constant', 'function': 'laplacian', 'add_source': False,
-           'no_alpha_sigmoid': False, 'max_nfe': 10 ** 9, 'multi_modal': False}
-    func = gnpde.LaplacianODEFunc(C, C, opt, dev).to(dev)
+    func = gnpde.LaplacianODEFunc(C, C, dict(LAP_OPT, hidden_dim=C), dev).to(dev)
     func.edge_index, func.edge_weight = ei, w
     h = args.step_size
 
@@ -136,39 +211,27 @@ def main():
             for _ in range(n):
                 y = func(None, y)
             return y
-        # exactly n rk4 steps through the drop-in integrator (stage combinations
-        # fused into the RHS epilogues: gnpde.integrator._fused_step)
-        t = torch.tensor([0.0, n * h], dtype=torch.float32, device=dev)
-        return gnpde.odeint(func, y, t, method='rk4', options={'step_size': h})[1]
+        return rk4_solve(func, y, n, h, dev)
 
+    import gnpde.function_laplacian_diffusion as fld
+    import gnpde.integrator as integ
     with torch.no_grad():
         g = func.graph_for(x)  # once per graph: CSR + plan (outside the timed region)
-        y = run_steps(args.warmup, x) if args.warmup > 0 else x
+        if args.warmup > 0:
+            run_steps(args.warmup, x)
         if not args.rhs_only:
             # one-time setup outside the timed region whatever W is: capture the step and
-            # block hipGraphs the timed call replays from the integrator's cache (a warm-up
-            # shorter than gnpde.integrator.GRAPH_MIN_STEPS / GRAPH_BLOCK captures nothing)
-            import gnpde.integrator as integ
+            # block hipGraphs the timed call replays from the integrator's cache
             run_steps(max(integ.GRAPH_MIN_STEPS, 2 * integ.GRAPH_BLOCK), x)
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        ops.spmm_rhs = timed_spmm
-        import gnpde.function_laplacian_diffusion as fld
-        import gnpde.integrator as integ
-        fld.ops.spmm_rhs = timed_spmm
+        sync_all(world)
+        ops.spmm_rhs = fld.ops.spmm_rhs = timed_spmm
         replays = []
         integ.replay_events = replays  # hipGraph replays: events around each replayed rk4 step
         t0 = time.perf_counter()
         y = run_steps(args.steps, x)
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
+        sync_all(world)
         elapsed = time.perf_counter() - t0
-        ops.spmm_rhs = orig_spmm
-        fld.ops.spmm_rhs = orig_spmm
+        ops.spmm_rhs = fld.ops.spmm_rhs = orig_spmm
         integ.replay_events = None
     assert torch.isfinite(y).all()
     # per-RHS launch time: eager launches are bracketed one by one; a replayed
@@ -176,10 +239,7 @@ def main():
     t_ev = sum(s.elapsed_time(e) for s, e in events) + sum(s.elapsed_time(e) for s, e, _ in replays)
     n_ev = len(events) + sum(n for _, _, n in replays)
     k1_ms = t_ev / max(n_ev, 1)
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t)
+    elapsed = max_over_ranks(elapsed, world, dev)
     rhs_per_step = 1 if args.rhs_only else 4
     total_rhs = world * args.steps * rhs_per_step
     value = total_rhs / elapsed
@@ -189,8 +249,8 @@ def main():
         kname = "agg_kernel<4,32,1,4,2,0,PlainWeights,float> (two rows per wavefront; hub rows combined in-launch)"
     else:
         nbytes = rk4_fused_step_bytes(N, E, C) / 4.0
-        kname = "agg_kernel<4,32,1,4,2,1,PlainWeights,float>: K1 with fused rk4 stage, two rows per wavefront (hub rows combined in-launch)"
-    achieved = nbytes / (k1_ms * 1e-3) / 1e9
+        kname = "agg_kernel<4,32,1,4,2,1,PlainWeights,float>: K1 with fused rk4 stage, two rows per wavefront " \
+                "(hub rows combined in-launch)"
 
     # the plain RHS (no fused stage) on the same graph, for the per-RHS roofline
     plain = None
@@ -208,21 +268,15 @@ def main():
             e.record()
             torch.cuda.synchronize()
         pms = s.elapsed_time(e) / args.rhs_plain_reps
-        pb = lap_bytes(N, E, C)
-        plain = {"rhs_ms": round(pms, 4), "achieved": round(pb / (pms * 1e-3) / 1e9, 1),
-                 "frac": round(pb / (pms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "algorithmic_bytes": pb,
-                 "kernel": "agg_kernel<4,32,1,4,2,0,PlainWeights,float> (hub rows combined in-launch)"}
+        plain = roofline(pms, lap_bytes(N, E, C), traffic_bytes(N, E, C, "plain_launch"),
+                         "agg_kernel<4,32,1,4,2,0,PlainWeights,float> (hub rows combined in-launch)")
+        plain["rhs_ms"] = round(pms, 4)
 
-    traffic = None
-    tp = os.path.join(ROOT, "profiles", "k1_traffic.json")
-    if os.path.exists(tp):
-        with open(tp) as fh:
-            tj = json.load(fh)
-        if tj.get("nodes") == N and tj.get("edges") == E and tj.get("dim") == C:
-            traffic = tj.get("fused_step_launch" if not args.rhs_only else "plain_launch", {}).get("hbm_bytes")
-
+    rl = roofline(k1_ms, nbytes, traffic_bytes(N, E, C, "plain_launch" if args.rhs_only else "fused_step_launch"),
+                  kname)
+    rl.update({"launch_ms": round(k1_ms, 4), "launches": n_ev, "graph_replays": len(replays)})
     result = {
-        "metric": "ODE RHS evals/s (and ms/step) at |E|≈1.2M, d=128; achieved HBM GB/s vs roofline",
+        "metric": METRIC,
         "value": round(value, 2),
         "unit": "RHS evals/s",
         "n_gpus": world,
@@ -240,16 +294,7 @@ def main():
                    "parallelism": "replicas%d" % world, "chunk": g.chunk,
                    "hub_rows": g.csr.plan.n_heavy},
         "rhs_ms": round(k1_ms, 4),
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     # measured HBM bytes (PMC, profiles/k1_traffic.json) over the same launch time: the
-                     # algorithmic rate passes the peak because x is re-read from the Infinity Cache
-                     "traffic_GBs": round(traffic / (k1_ms * 1e-3) / 1e9, 1) if traffic else None,
-                     "note": "achieved charges every gathered row to HBM (SURVEY 8(d) bytes); x stays in the "
-                             "256 MB Infinity Cache between gathers, so the measured HBM traffic is lower",
-                     "kernel": kname, "algorithmic_bytes_per_launch": int(nbytes),
-                     "launch_ms": round(k1_ms, 4), "launches": n_ev,
-                     "graph_replays": len(replays)},
+        "roofline": rl,
         "rhs_plain": plain,
     }
 
@@ -259,69 +304,132 @@ def main():
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(ei, w, x, N, E, C, args.cpu_seconds)
-    if rank == 0:
-        print(json.dumps(result))
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
+    return result
 
 
-def bench_sharded(args, world, rank, dev):
-    """One graph shared by all ranks (strong scaling): 'rows' = north-star literal
-    row partition + RCCL all-gather of the state per RHS; 'cols' = feature-column
-    stripes (no per-RHS collective)."""
-    import gnpde
-    from gnpde import dist as gd, synthetic
+METRIC = "ODE RHS evals/s (and ms/step) at |E|≈1.2M, d=128; achieved HBM GB/s vs roofline"
+
+
+def traffic_bytes(N, E, C, which):
+    """Measured HBM bytes per K1 launch (PMC: 2*FETCH_SIZE + WRITE_SIZE with the
+    gfx950 corrections of MI355X_MICROARCH.md §HBM) from profiles/k1_traffic.json,
+    when that file was collected on this graph shape."""
+    tp = os.path.join(ROOT, "profiles", "k1_traffic.json")
+    if not os.path.exists(tp):
+        return None
+    with open(tp) as fh:
+        tj = json.load(fh)
+    if tj.get("nodes") == N and tj.get("edges") == E and tj.get("dim") == C:
+        return tj.get(which, {}).get("hbm_bytes")
+    return None
+
+
+def roofline(launch_ms, algorithmic, traffic, kernel):
+    """achieved = measured HBM bytes per launch / launch time (frac <= 1 is an HBM
+    fraction); the §8(d) algorithmic byte count over the same time is reported
+    beside it (it charges every gathered x row to HBM, but x is re-read from L2
+    and the Infinity Cache, so it can pass 8 TB/s)."""
+    t = launch_ms * 1e-3
+    alg = algorithmic / t / 1e9
+    out = {"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s", "kernel": kernel,
+           "algorithmic_bytes_per_launch": int(algorithmic), "algorithmic_achieved": round(alg, 1),
+           "algorithmic_frac": round(alg / HBM_PEAK_GBS, 4)}
+    if traffic:
+        ach = traffic / t / 1e9
+        out.update({"achieved": round(ach, 1), "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": int(traffic),
+                    "basis": "PMC bytes per launch (profiles/k1_traffic.json, 2*FETCH_SIZE+WRITE_SIZE) / HIP-event "
+                             "launch time"})
+    else:
+        out.update({"achieved": round(alg, 1), "frac": round(alg / HBM_PEAK_GBS, 4), "traffic": None,
+                    "basis": "algorithmic bytes / HIP-event launch time (no PMC traffic for this shape)"})
+    return out
+
+
+def bench_sharded(args, world, rank, dev, mode):
+    """The headline on ONE graph shared by all ranks (strong scaling): 'cols' =
+    feature-column stripes (no per-RHS collective), 'rows' = nnz-balanced row
+    partition + RCCL all-gather of the state per RHS.  Also times the same graph
+    unsharded on each rank's GPU first (speedup_vs_1gpu)."""
     N, E, C, h = args.nodes, args.edges, args.dim, args.step_size
     if not dist.is_initialized():  # single process: a world of one
         import random
         dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % random.randint(20000, 40000), rank=0,
                                 world_size=1, device_id=dev)
-    ei, w = synthetic.rw_graph(N, E, seed=0, device=dev)
-    x = synthetic.features(1, N, C, seed=1, device=dev)
+    r = sharded_point(N, E, C, h, args.steps, args.warmup, world, dev, mode)
+    return {
+        "metric": METRIC, "value": r["value"], "unit": "RHS evals/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": r["ms_per_step"], "higher_is_better": True, "scaling": "strong",
+        "vs_baseline": None, "dtype": "f32", "data": "synthetic (seeded RMAT graph, N(0,1) features)",
+        "config": {"workload": "%s laplacian RHS, rk4, one graph sharded over %d GPUs (%s)%s" % (
+            graph_name(N, E), world, mode, " (configs[2])" if C == 128 else ""),
+            "nodes": N, "edges": E, "dim": C, "method": "rk4", "step_size": h, "rhs_per_step": 4,
+            "global_batch": 1, "parallelism": "%s%d" % (mode, world)},
+        "speedup_vs_1gpu": r["speedup_vs_1gpu"], "one_gpu_value": r["one_gpu_value"],
+        "shard": r.get("shard"),
+    }
+
+
+def sharded_point(N, E, C, h, steps, warmup, world, dev, mode, seed=0):
+    """RHS evals/s of one graph in `mode` over the job's ranks, and the same graph
+    integrated unsharded on one GPU (every rank at once, max over ranks)."""
+    import gnpde
+    from gnpde import dist as gd, synthetic
+    ei, w = synthetic.rw_graph(N, E, seed=seed, device=dev)
+    x = synthetic.features(1, N, C, seed=1 + seed, device=dev)
+    # the 1-GPU point of the curve: the whole graph on this rank's GPU
+    func = gnpde.LaplacianODEFunc(C, C, dict(LAP_OPT, hidden_dim=C), dev).to(dev)
+    func.edge_index, func.edge_weight = ei, w
+    el1, _ = timed_solve(func, x, steps, warmup, h, dev, world)
+    del func
+    torch.cuda.empty_cache()
     alpha = torch.zeros((), device=dev)
-    if args.mode == "rows":
+    if mode == "rows":
         sh = gd.RowShardedLaplacian(ei, w, N, alpha)
         y0 = sh.scatter(x.view(-1, C))
+        info = {"blocks_nnz": None, "nbmax": sh.nb}
     else:
         sh = gd.ColumnShardedLaplacian(ei, w, N, C, alpha)
         y0 = sh.split(x)
+        info = {"columns_per_rank": sh.c1 - sh.c0}
+    el, y = timed_solve(sh, y0, steps, warmup, h, dev, world)
+    if mode == "rows":
+        rp = sh.g.csr.rowptr.cpu()
+        info["blocks_nnz"] = [int(rp[b] - rp[a]) for a, b in sh.blocks]
+    v1 = steps * 4 / el1
+    v = steps * 4 / el
+    out = {"value": round(v, 2), "ms_per_step": round(el * 1e3 / steps, 4), "one_gpu_value": round(v1, 2),
+           "one_gpu_ms_per_step": round(el1 * 1e3 / steps, 4), "speedup_vs_1gpu": round(v / v1, 3),
+           "shard": info}
+    del sh, y, y0, x, ei, w
+    torch.cuda.empty_cache()
+    return out
 
-    def run(n):
-        t = torch.tensor([0.0, n * h], dtype=torch.float32, device=dev)
-        return gnpde.odeint(sh, y0, t, method='rk4', options={'step_size': h})[1]
 
-    with torch.no_grad():
-        run(args.warmup)
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        y = run(args.steps)
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        elapsed = time.perf_counter() - t0
-    assert torch.isfinite(y).all()
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t)
-    value = args.steps * 4 / elapsed
-    if rank == 0:
-        print(json.dumps({
-            "metric": "ODE RHS evals/s (and ms/step) at |E|≈1.2M, d=128; achieved HBM GB/s vs roofline",
-            "value": round(value, 2), "unit": "RHS evals/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3 / args.steps, 4), "higher_is_better": True,
-            "scaling": "strong", "vs_baseline": None, "dtype": "f32",
-            "data": "synthetic (seeded RMAT graph, N(0,1) features)",
-            "config": {"workload": "%s laplacian RHS, rk4, one graph sharded (%s)" % (graph_name(N, E), args.mode),
-                       "nodes": N,
-                       "edges": E, "dim": C, "method": "rk4", "parallelism": "%s%d" % (args.mode, world)}}))
-    dist.barrier()
-    dist.destroy_process_group()
+def bench_grmat(args, world, rank, dev):
+    """configs[4]: G-rmat (N = 2M, E = 20M, C = 256) — one GPU at N = 1 (the first
+    point of the curve); at N > 1 column stripes and the row partition +
+    all-gather, each with its own unsharded 1-GPU time on the same job."""
+    N, E, C, h = 2_000_000, 20_000_000, 256, args.step_size
+    out = {"config": "configs[4] graph: RMAT N=%d E=%d C=%d, rk4 %d timed steps (step %.3g)" % (
+        N, E, C, args.grmat_steps, h)}
+    if world == 1:
+        import gnpde
+        from gnpde import synthetic
+        ei, w = synthetic.rw_graph(N, E, seed=0, device=dev)
+        x = synthetic.features(1, N, C, seed=1, device=dev)
+        func = gnpde.LaplacianODEFunc(C, C, dict(LAP_OPT, hidden_dim=C), dev).to(dev)
+        func.edge_index, func.edge_weight = ei, w
+        el, _ = timed_solve(func, x, args.grmat_steps, 1, h, dev, world)
+        nb = rk4_fused_step_bytes(N, E, C)
+        out["one_gpu"] = {"value": round(args.grmat_steps * 4 / el, 2), "unit": "RHS evals/s",
+                          "ms_per_step": round(el * 1e3 / args.grmat_steps, 4),
+                          "algorithmic_GBs": round(nb / (el / args.grmat_steps) / 1e9, 1)}
+        del func, x, ei, w
+        torch.cuda.empty_cache()
+        return out
+    for mode in ("cols", "rows"):
+        out[mode] = sharded_point(N, E, C, h, args.grmat_steps, 1, world, dev, mode)
+    return out
 
 
 def bench_attention(g, x, dev, ops, reps=20):
@@ -384,7 +492,10 @@ def bench_attention(g, x, dev, ops, reps=20):
 def bench_blend(g, dev, reps=50):
     """configs[3] shape: the BLEND transformer RHS (fork scaled_dot under
     source-grouped softmax -> cached 1/outdeg weights), C = 162 (64 features +
-    98 positional), one rk4 step per 4 RHS, fp32 and bf16 state storage."""
+    98 positional), one rk4 step per 4 RHS, fp32 and bf16 state storage.
+    Checked on the spot: the bf16 solve against the fp32 one (SURVEY §8(d) bf16
+    gate 2e-2), and the RHS of a constant state is 0 (the 1/outdeg weights are
+    row-stochastic: A 1 = 1); the fp64 oracle check is tests/test_gpu_blend.py."""
     import gnpde
     from gnpde import synthetic
     C = 162
@@ -394,6 +505,7 @@ def bench_blend(g, dev, reps=50):
     out = {"config": "BLEND transformer RHS, fork scaled_dot norm_idx 0 (uniform weights), C=162, rk4 steps "
                      "(configs[3] shape on the G-arxiv graph)"}
     x32 = synthetic.features(1, g.N, C, seed=3, device=dev)
+    res = {}
     for name, dt in (("fp32", torch.float32), ("bf16", torch.bfloat16)):
         func = gnpde.ODEFuncTransformerAtt(C, C, opt, dev).to(dev).eval()
         func.edge_index = g.edge_index
@@ -404,29 +516,45 @@ def bench_blend(g, dev, reps=50):
             torch.cuda.synchronize()
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record()
-            gnpde.odeint(func, x, t, method='rk4', options={'step_size': 0.25})
+            res[name] = gnpde.odeint(func, x, t, method='rk4', options={'step_size': 0.25})[1]
             e.record()
             torch.cuda.synchronize()
+            if name == "fp32":
+                f1 = func(None, torch.ones_like(x))
+                const_rhs = float(f1.abs().max())
         ms = s.elapsed_time(e) / reps
         es = 2 if dt == torch.bfloat16 else 4
         # per step: 4 x (gathers es*EC + CSR/weights 8E + 4(N+1) + own row es*NC) + 8 state passes es*NC
         nb = 4 * (es * g.nnz * C + 8 * g.nnz + 4 * (g.N + 1) + es * g.N * C) + 8 * es * g.N * C
         gbs = nb / (ms * 1e-3) / 1e9
-        out[name] = {"ms_per_step": round(ms, 4), "rhs_per_s": round(4e3 / ms, 1), "achieved_GBs": round(gbs, 1),
-                     "frac": round(gbs / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_step": nb}
+        out[name] = {"ms_per_step": round(ms, 4), "rhs_per_s": round(4e3 / ms, 1), "algorithmic_GBs": round(gbs, 1),
+                     "algorithmic_frac": round(gbs / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_step": nb}
+    a, b = res["fp32"].double(), res["bf16"].double()
+    rel = float((a - b).abs().max() / a.abs().max())
+    out["check"] = {"bf16_vs_fp32_rel": round(rel, 6), "constant_state_rhs_max": const_rhs,
+                    "ok": bool(rel <= 2e-2 and const_rhs <= 1e-5)}
     return out
 
 
 def cpu_baseline(ei, w, x, N, E, C, budget_s):
-    """The oracle's C restatement (oracle/c/rhs_oracle.c: fp32, CSR built once,
-    OpenMP over rows) timed on the host cores on a bounded sample of the same
-    workload: as many full G-arxiv RHS evaluations as fit in ~budget_s seconds.
-    The oracle's scipy path (single-threaded) is reported beside it."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    """The reference's CPU path restated with torch.sparse: f = sigma(a)(A x - x)
+    with A a torch CSR tensor (fp32), on the host cores of the GPU box, on a
+    bounded sample of the same workload (as many full G-arxiv RHS evaluations as
+    fit in ~budget_s seconds).  The literal reference densifies A ([N,N] = 114.7 GB
+    at G-arxiv) and cannot run at this size.  The oracle's OpenMP C
+    restatement is reported beside it (secondary)."""
     import numpy as np
-    import gnpde_oracle as O
-    ein, wn, xn = ei.cpu().numpy(), w.cpu().numpy(), x.cpu().numpy()
-    threads = int(os.environ.get("OMP_NUM_THREADS", min(16, os.cpu_count() or 1)))
+    cpus = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    threads = int(os.environ.get("OMP_NUM_THREADS", cpus))
+    model = "unknown CPU"
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
 
     def timed(fn, budget):
         fn()  # warm
@@ -438,25 +566,35 @@ def cpu_baseline(ei, w, x, N, E, C, budget_s):
             if (el > budget and n >= 3) or n >= 2000:
                 return n, el, y
 
-    out = {}
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
     try:
+        ec, wcpu = ei[0].cpu(), w[0].cpu()
+        A = torch.sparse_coo_tensor(ec, wcpu, (N, N)).coalesce().to_sparse_csr()
+        xc = x.view(N, C).cpu()
+        a = torch.sigmoid(torch.tensor(0.0))
+        n, el, y = timed(lambda: a * (A @ xc - xc), budget_s * 2 / 3)
+        assert torch.isfinite(y).all()
+    finally:
+        torch.set_num_threads(prev)
+    out = {"value": round(n / el, 3), "unit": "RHS evals/s", "cores": threads, "kind": "port",
+           "sample": "%d full G-arxiv Laplacian RHS evaluations (N=%d, E'=%d, C=%d) in %.1f s: torch sparse CSR "
+                     "A@x, fp32, torch %s, %d threads of %d visible host CPUs (%s)" % (
+                         n, N, E, C, el, torch.__version__, threads, cpus, model),
+           "cpu_model": model, "visible_cpus": cpus}
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    try:
+        import gnpde_oracle as O
+        ein, wn, xn = ei.cpu().numpy(), w.cpu().numpy(), x.cpu().numpy()
         co = O.COracle()
         csr = co.csr(ein, wn, N)
-        n, el, y = timed(lambda: co.laplacian_rhs(csr, xn, 0.0, nthreads=threads), budget_s * 2 / 3)
-        assert np.isfinite(y).all()
-        out = {"value": round(n / el, 3), "unit": "RHS evals/s", "cores": threads, "kind": "port",
-               "sample": "%d full G-arxiv Laplacian RHS evaluations (N=%d, E'=%d, C=%d) in %.1f s; oracle C "
-                         "restatement (fp32, CSR, OpenMP %d threads), %s" % (n, N, E, C, el, threads,
-                                                                            os.uname().machine)}
+        n2, el2, y2 = timed(lambda: co.laplacian_rhs(csr, xn, 0.0, nthreads=threads), budget_s / 3)
+        assert np.isfinite(y2).all()
+        out["oracle_c_openmp"] = {"value": round(n2 / el2, 3), "unit": "RHS evals/s", "cores": threads,
+                                  "sample": "%d RHS evaluations in %.1f s; oracle C restatement (fp32 CSR, OpenMP)" %
+                                            (n2, el2)}
     except OSError as exc:  # liboracle.so not built
-        out = {"error": "oracle/build/liboracle.so unavailable: %s" % exc}
-    lap = O.LaplacianCSR(ein, wn, N)
-    n, el, y = timed(lambda: lap.rhs(xn, 0.0), budget_s / 3)
-    alt = {"value": round(n / el, 3), "unit": "RHS evals/s", "cores": 1, "kind": "port",
-           "sample": "%d RHS evaluations in %.1f s; oracle LaplacianCSR (scipy CSR @ x, fp32)" % (n, el)}
-    if "value" not in out:
-        return dict(alt, note=out.get("error"))
-    out["scipy_single_thread"] = alt
+        out["oracle_c_openmp"] = {"error": "oracle/build/liboracle.so unavailable: %s" % exc}
     return out
 
 

@@ -393,7 +393,8 @@ static int launch_agg_cfg(const int4* items, int64_t n_items, int4* heavy, int64
 
 // Experiment knob (not part of the ABI contract): GNPDE_AGG_VARIANT selects an
 // alternative lane geometry for the dominant 32-lane (C = 128 fp32) case
-// (2: U = 2, 3: U = 8, 4: one row per wavefront; default: two rows per wavefront).
+// (2: U = 2, 3: U = 8, 4: one row per wavefront; default: two rows per wavefront)
+// and, with 5, the one-row geometry for rows of at most 16 lanes.
 int agg_variant();
 
 template <int VEC, class WP, class T = float>
@@ -402,6 +403,16 @@ static int launch_agg_vec(const int4* items, int64_t n_items, int4* heavy, int64
   const int lanes = (int)ceil_div(C, VEC);
 #define GNPDE_AGG(GL, NCH, U, RPW) \
   launch_agg_cfg<VEC, GL, NCH, U, RPW, WP, T>(items, n_items, heavy, n_heavy, col, wp, C, ep, partials, s)
+  // Narrow rows (the column stripes of gnpde.dist at 2-8 GPUs: G-arxiv C = 128 / 8 = 16
+  // floats = 4 lanes; G-rmat 256 / 8 = 32 floats = 8 lanes): several rows per
+  // wavefront, 2 edges side by side per row slot, 4 in flight per edge group, so a
+  // wavefront keeps 8 gathers in flight for each of its 2-8 rows instead of idling
+  // 3/4 of a 16-lane group (GNPDE_AGG_VARIANT=5: the previous one-row geometry).
+  if (agg_variant() != 5) {
+    if (lanes <= 4) return GNPDE_AGG(4, 1, 4, 8);
+    if (lanes <= 8) return GNPDE_AGG(8, 1, 4, 4);
+    if (lanes <= 16) return GNPDE_AGG(16, 1, 4, 2);
+  }
   if (lanes <= 16) return GNPDE_AGG(16, 1, 4, 1);
   if (lanes <= 32) {
     // two rows per wavefront (fp32 C = 128 and bf16 rows of 17-32 lanes): with the

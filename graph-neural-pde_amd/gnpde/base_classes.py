@@ -4,22 +4,31 @@ Same constructor signatures, attribute contract and state_dict keys as the
 reference, so ``GNN.__init__`` (src/GNN.py:12-15) and the torchdiffeq-style
 loop use them unchanged:
 
-* ``ODEFunc(opt, device)`` — src/base_classes.py:193-211: attributes
+* ``ODEFunc(opt, device)`` — src/base_classes.py:116-134: attributes
   ``edge_index``, ``edge_weight``, ``attention_weights``, ``x0``, ``nfe``,
   parameters ``alpha_train``, ``beta_train`` (0-d, init 0), ``alpha_sc``,
   ``beta_sc``.  Adds a per-graph CSR cache: the first RHS call after
   ``edge_index`` changes builds the device CSR + plan once; every later call
   reuses it.
 * ``ODEblock(odefunc, regularization_fns, opt, device, t)`` —
-  src/base_classes.py:110-175: ``odefunc``, ``reg_odefunc.odefunc``,
+  src/base_classes.py:33-98: ``odefunc``, ``reg_odefunc.odefunc``,
   ``train_integrator``/``test_integrator``, ``set_x0``, ``set_tol``,
-  ``reset_tol``, ``reset_graph_data``, ``set_time``.
-* ``GraphData`` — src/base_classes.py:177-190.
+  ``reset_tol``, ``reset_graph_data``, ``set_time``.  Module layout as the
+  reference: ``ODEblock.__init__`` builds an ODEFunc and wraps it in
+  ``reg_odefunc`` (:40, :43); every concrete block then builds a SECOND
+  ODEFunc as ``self.odefunc`` (src/block_constant.py:11,
+  src/block_transformer_attention.py:11, src/block_mixed.py:12,
+  src/block_transformer_hard_attention.py:11), which is the one the solver
+  integrates.  A reference ``state_dict`` therefore holds both
+  ``odefunc.*`` and ``reg_odefunc.odefunc.*`` and loads here unchanged, and
+  ``GNN.getNFE`` (src/base_classes.py:174-176) sums the two counters.
+* ``GraphData`` — src/base_classes.py:100-113.
 """
 import torch
 from torch import nn
 
 from . import ops
+from ._cache import _tensor_key  # noqa: F401  (re-exported for the function modules)
 from .integrator import odeint, odeint_adjoint
 from .utils import get_rw_adj, gcn_norm_fill_val
 
@@ -40,14 +49,10 @@ class GraphData(object):
         return self.__class__.__name__
 
 
-def _tensor_key(t):
-    if t is None:
-        return None
-    return (t.data_ptr(), t._version, tuple(t.shape), t.dtype, str(t.device))
 
 
 class ODEFunc(nn.Module):
-    """Base RHS module (src/base_classes.py:193-211)."""
+    """Base RHS module (src/base_classes.py:116-134)."""
 
     def __init__(self, opt, device):
         super(ODEFunc, self).__init__()
@@ -84,15 +89,53 @@ class ODEFunc(nn.Module):
 
     def csr_weights(self, g, w, tag, transpose=False):
         """COO-order weights (or [B,E,h] attention -> head mean) in CSR (or CSC) order,
-        cached per tensor version."""
+        cached per source tensor (identity and version).
+
+        Under no_grad a changed source (the attention blocks hand over a new
+        ``attention_weights`` tensor every forward) is gathered IN PLACE into the
+        buffer of the previous one when that buffer was made under no_grad and
+        never given to autograd: the integrator's captured step graphs read that
+        buffer, so they keep replaying with the new weights instead of being
+        re-captured every forward.  Buffers an autograd call has seen are never
+        overwritten (its backward may still read them)."""
         tag = (tag, transpose)
-        key = (tag, _tensor_key(w))
+        key = (tag, _tensor_key(w), id(g))
         hit = self._w_cache.get(tag)
+        grad = torch.is_grad_enabled()
         if hit is not None and hit[0] == key:
+            if grad and hit[2]:
+                self._w_cache[tag] = (hit[0], hit[1], False)
             return hit[1]
-        wc = g.gather_weights(w.detach().float() if w.dtype != torch.float32 else w.detach(), transpose=transpose)
-        self._w_cache[tag] = (key, wc)
+        src = w.detach().float() if w.dtype != torch.float32 else w.detach()
+        if hit is not None and hit[2] and not grad and hit[0][2] == id(g):
+            wc = g.gather_weights(src, transpose=transpose, out=hit[1])
+        else:
+            wc = g.gather_weights(src, transpose=transpose)
+        self._w_cache[tag] = (key, wc, not grad)
         return wc
+
+    def stable_x0(self, x):
+        """x0 in x's dtype and (zero-padded) width, in a buffer that stays the same
+        across set_x0 calls of the same shape (refreshed in place): what the fused
+        Runge-Kutta stages and their captured step graphs read.  ODEblock.set_x0
+        clones x0 every forward (src/base_classes.py:53-55), so reading self.x0
+        directly would pin a captured graph to a stale pointer."""
+        x0 = self.x0
+        if x0 is None:
+            raise RuntimeError("%s: add_source needs x0 (ODEblock.set_x0)" % self.__class__.__name__)
+        key = _tensor_key(x0)
+        shape = tuple(x0.shape[:-1]) + (x.shape[-1],)
+        hit = getattr(self, '_x0_buf', None)
+        if hit is not None and hit[0] == key and hit[1].shape == shape and hit[1].dtype == x.dtype and \
+                hit[1].device == x.device:
+            return hit[1]
+        if hit is not None and hit[1].shape == shape and hit[1].dtype == x.dtype and hit[1].device == x.device:
+            buf = hit[1]
+        else:
+            buf = torch.zeros(shape, dtype=x.dtype, device=x.device)
+        buf[..., :x0.shape[-1]].copy_(x0.detach())
+        self._x0_buf = (key, buf)
+        return buf
 
     def __repr__(self):
         return self.__class__.__name__
@@ -113,7 +156,7 @@ class RegularizedODEfunc(nn.Module):
 
 
 class ODEblock(nn.Module):
-    """src/base_classes.py:110-175."""
+    """src/base_classes.py:33-98."""
 
     def __init__(self, odefunc, regularization_fns, opt, device, t):
         super(ODEblock, self).__init__()
@@ -129,6 +172,13 @@ class ODEblock(nn.Module):
         self.set_tol()
         self._prep_key = None
         self._prep = None
+
+    def _new_odefunc(self, odefunc, opt, device):
+        """The block's own ODEFunc, built after ODEblock.__init__ exactly as the
+        reference blocks do (e.g. src/block_constant.py:10-11); ``reg_odefunc``
+        keeps the first copy."""
+        self.aug_dim = 2 if opt.get('augment', False) else 1
+        return odefunc(self.aug_dim * opt['hidden_dim'], self.aug_dim * opt['hidden_dim'], opt, device)
 
     def set_x0(self, x0):
         self.odefunc.x0 = x0.clone().detach()
@@ -148,23 +198,30 @@ class ODEblock(nn.Module):
         self.rtol_adjoint = 1e-9
 
     def reset_graph_data(self, data, dtype, y=None):
-        """src/base_classes.py:147-167 with the intended normalisation semantics
+        """src/base_classes.py:70-90 with the intended normalisation semantics
         (gnpde.utils): self-loops (weight self_loop_weight) + rw (norm_dim=1) or
         symmetric gcn normalisation.  The reference's second
-        add_remaining_self_loops (:160-162) is a no-op once every node has a
+        add_remaining_self_loops (:83-85) is a no-op once every node has a
         loop and is skipped.  Cached on (edge_index, edge_attr) identity, so a
-        model that passes the same graph every forward prepares it once."""
+        model that passes the same graph every forward prepares it once.
+
+        The weights are built in fp32 whatever the state dtype: the reference
+        passes ``dtype=x.dtype`` (:77, :82), which under a bf16 state would form
+        degree sums in bf16 (integers exact only to 256) and round every weight
+        to 8 bits before the fp32 aggregation reads it."""
         if data is not None:
+            dtype = torch.float32
             key = (_tensor_key(data.edge_index), _tensor_key(data.edge_attr), int(data.num_nodes),
-                   self.opt.get('data_norm', 'rw'), float(self.opt.get('self_loop_weight', 0)), dtype)
+                   self.opt.get('data_norm', 'rw'), float(self.opt.get('self_loop_weight', 0)))
             if key != self._prep_key:
                 self.num_nodes = data.num_nodes
+                ea = data.edge_attr.float() if data.edge_attr is not None else None
                 if self.opt.get('data_norm', 'rw') == 'rw':
-                    edge_index, edge_weight = get_rw_adj(data.edge_index, edge_weight=data.edge_attr, norm_dim=1,
+                    edge_index, edge_weight = get_rw_adj(data.edge_index, edge_weight=ea, norm_dim=1,
                                                          fill_value=self.opt['self_loop_weight'],
                                                          num_nodes=data.num_nodes, dtype=dtype)
                 else:
-                    edge_index, edge_weight = gcn_norm_fill_val(data.edge_index, edge_weight=data.edge_attr,
+                    edge_index, edge_weight = gcn_norm_fill_val(data.edge_index, edge_weight=ea,
                                                                 fill_value=self.opt['self_loop_weight'],
                                                                 num_nodes=data.num_nodes, dtype=dtype)
                 dev = self.device if self.device is not None else edge_index.device

@@ -13,6 +13,8 @@ from .integrator import odeint, odeint_adjoint
 class ConstantODEblock(ODEblock):
     def __init__(self, odefunc, regularization_fns, opt, device, t=torch.tensor([0, 1])):
         super(ConstantODEblock, self).__init__(odefunc, regularization_fns, opt, device, t)
+        self.device = device
+        self.odefunc = self._new_odefunc(odefunc, opt, device)  # the integrated copy (src/block_constant.py:11)
         self.train_integrator = odeint_adjoint if opt.get('adjoint', False) else odeint
         self.test_integrator = odeint
         self.set_tol()

@@ -51,6 +51,7 @@ class MixedODEblock(ODEblock):
     def __init__(self, odefunc, regularization_fns, opt, device, t=torch.tensor([0, 1]), gamma=0.):
         super(MixedODEblock, self).__init__(odefunc, regularization_fns, opt, device, t)
         self.device = device
+        self.odefunc = self._new_odefunc(odefunc, opt, device)  # the integrated copy (src/block_mixed.py:12)
         self.train_integrator = odeint_adjoint if opt.get('adjoint', False) else odeint
         self.test_integrator = odeint
         self.set_tol()

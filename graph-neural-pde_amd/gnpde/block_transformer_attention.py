@@ -14,6 +14,9 @@ from .integrator import odeint, odeint_adjoint
 class AttODEblock(ODEblock):
     def __init__(self, odefunc, regularization_fns, opt, device, t=torch.tensor([0, 1]), gamma=0.5):
         super(AttODEblock, self).__init__(odefunc, regularization_fns, opt, device, t)
+        self.device = device
+        # the integrated copy (src/block_transformer_attention.py:11)
+        self.odefunc = self._new_odefunc(odefunc, opt, device)
         self.train_integrator = odeint_adjoint if opt.get('adjoint', False) else odeint
         self.test_integrator = odeint
         self.set_tol()

@@ -32,8 +32,10 @@ from .integrator import odeint, odeint_adjoint
 class HardAttODEblock(ODEblock):
     def __init__(self, odefunc, regularization_fns, opt, device, t=torch.tensor([0, 1]), gamma=0.5):
         super(HardAttODEblock, self).__init__(odefunc, regularization_fns, opt, device, t)
-        assert opt['att_samp_pct'] > 0 and opt['att_samp_pct'] <= 1, "attention sampling threshold must be in (0,1]"
         self.device = device
+        # the integrated copy (src/block_transformer_hard_attention.py:11)
+        self.odefunc = self._new_odefunc(odefunc, opt, device)
+        assert opt['att_samp_pct'] > 0 and opt['att_samp_pct'] <= 1, "attention sampling threshold must be in (0,1]"
         self.train_integrator = odeint_adjoint if opt.get('adjoint', False) else odeint
         self.test_integrator = odeint
         self.set_tol()

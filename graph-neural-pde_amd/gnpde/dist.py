@@ -4,20 +4,22 @@ with the RCCL backend ("nccl" on ROCm) over xGMI.
 The reference has no multi-GPU hot path (only nn.DataParallel over the batch
 axis, src/ray_tune.py:58-59).  Three ways to shard it are provided:
 
-* ``shard_batch`` — independent objects: each rank integrates its slice of the
-  batch axis B (the reference's own parallel axis).  No data-path collective;
-  this is what ``bench.py --gpus N`` measures (weak scaling).
+* ``ColumnShardedLaplacian`` — feature-column stripes of ONE graph: rank p
+  owns columns [c0, c1) of every node and a replicated CSR.  A*x is
+  column-separable, so a fixed-grid integration needs no communication at
+  all; dopri5 needs one all-reduce of the squared error norm per step
+  (``global_rms_norm``); the columns are all-gathered once at the end.  This is
+  what ``bench.py --gpus N`` measures (strong scaling: one shared graph).
 * ``RowShardedLaplacian`` — the north star's literal design: a 1-D partition of
-  the graph rows (equal row blocks of the block-diagonal CSR); each RHS
-  evaluation computes its rows of f and the next evaluation needs every row of
-  the state, so the state is all-gathered (RCCL all_gather_into_tensor, half
-  the volume of the all-reduce the north star names) before each RHS.  Volume
-  per RHS = R*C*4 bytes in total.
-* ``ColumnShardedLaplacian`` — feature-column stripes: rank p owns columns
-  [c0, c1) of every node and a replicated CSR.  A*x is column-separable, so a
-  fixed-grid integration needs no communication at all; dopri5 needs one
-  all-reduce of the squared error norm per step (``global_rms_norm``); the
-  columns are all-gathered once at the end.
+  the graph rows into contiguous blocks balanced by nnz (``RowPartition``);
+  each RHS evaluation computes its rows of f and the next evaluation needs
+  every row of the state, so the state is all-gathered (RCCL
+  all_gather_into_tensor, half the volume of the all-reduce the north star
+  names) before each RHS.  Volume per RHS = world*nbmax*C*4 bytes.
+  ``bench.py --gpus N`` reports it beside the column layout.
+* ``shard_batch`` — independent objects: each rank integrates its slice of the
+  batch axis B (the reference's own parallel axis); no data-path collective
+  (``bench.py --mode replicas``, weak scaling).
 
 ``local_rhs`` lets tests substitute a CPU computation so the communication
 pattern is exercised with the gloo backend; the default is the HIP path.
@@ -34,6 +36,96 @@ def row_blocks(R, world):
     """Equal row blocks [(r0, r1)] of ceil(R/world) rows (last one shorter)."""
     nb = int(math.ceil(R / world))
     return [(min(R, p * nb), min(R, (p + 1) * nb)) for p in range(world)], nb
+
+
+def host_rowptr(edge_index, num_nodes):
+    """Row pointer [B*N+1] (numpy int64) of the block-diagonal aggregation CSR of
+    edge_index [B,2,E] (rows = sources), computed on the host."""
+    import numpy as np
+    ei = edge_index.detach().cpu().numpy() if isinstance(edge_index, torch.Tensor) else np.asarray(edge_index)
+    B = ei.shape[0]
+    rows = (ei[:, 0, :] + np.arange(B)[:, None] * int(num_nodes)).reshape(-1)
+    rp = np.zeros(B * int(num_nodes) + 1, np.int64)
+    rp[1:] = np.cumsum(np.bincount(rows, minlength=B * int(num_nodes)))
+    return rp
+
+
+def balanced_row_blocks(rowptr, world, row_weight=0.0):
+    """Contiguous row blocks balanced by work, not by row count (SURVEY §8(e):
+    "1-D partition ... balanced by nnz").  Block p ends at the row where the
+    cumulative cost nnz(0..r) + row_weight * r is nearest to (p+1)/world of
+    the total (rows are never split).  row_weight = 0: pure nnz balance (RMAT hub rows have low ids, so
+    equal row counts hand rank 0 most of the edges); a positive weight also
+    charges each row's share of the per-RHS state exchange.  ``rowptr``:
+    host int array [R+1].  Returns [(r0, r1)] covering [0, R)."""
+    import numpy as np
+    rp = np.asarray(rowptr, dtype=np.int64)
+    R = rp.shape[0] - 1
+    cost = rp.astype(np.float64) + float(row_weight) * np.arange(R + 1, dtype=np.float64)
+    total = cost[-1]
+    cuts = [0]
+    for p in range(1, world):
+        target = total * p / world
+        r = int(np.searchsorted(cost, target, side='left'))
+        if 0 < r <= R and target - cost[r - 1] < cost[r] - target:
+            r -= 1  # the nearer cut
+        cuts.append(min(max(r, cuts[-1]), R))
+    cuts.append(R)
+    return [(cuts[p], cuts[p + 1]) for p in range(world)]
+
+
+class RowPartition(object):
+    """One rank's share of a row-partitioned CSR, process-group free (so one
+    process can build and run every rank's part: tests/test_gpu_sharded.py).
+
+    The gathered state is laid out in padded blocks: rank p's rows [r0_p, r1_p)
+    sit at positions p*nbmax + (r - r0_p) of a [world*nbmax, C] buffer, which is
+    what ``all_gather_into_tensor`` of equal [nbmax, C] blocks produces.  The
+    column ids of the CSR are relabelled into those positions once per graph
+    (``col``); the local plan's item rows are positions too, and the outputs are
+    addressed through pointers shifted back by rank*nbmax rows."""
+
+    def __init__(self, g, world, rank, row_weight=0.0, chunk=ops.DEFAULT_CHUNK, blocks=None):
+        self.world, self.rank = int(world), int(rank)
+        rowptr = g.csr.rowptr
+        self.blocks = blocks if blocks is not None else balanced_row_blocks(rowptr.cpu().numpy(), world, row_weight)
+        self.nbmax = max(max(r1 - r0 for r0, r1 in self.blocks), 1)
+        self.r0, self.r1 = self.blocks[self.rank]
+        self.pos0 = self.rank * self.nbmax           # position of this rank's first row
+        dev = rowptr.device
+        starts = torch.tensor([b[0] for b in self.blocks], dtype=torch.int64, device=dev)
+        col = g.csr.col[:max(g.nnz, 1)].long()
+        if g.nnz:
+            blk = torch.searchsorted(starts, col, right=True) - 1
+            col = col - starts[blk] + blk * self.nbmax
+        self.col = col.to(torch.int32).contiguous()
+        self.plan = _local_plan(g.csr, self.r0, self.r1, chunk, self.pos0)
+
+    def pad_state(self, y):
+        """Full state [R, C] (global row order) -> the padded [world*nbmax, C] layout."""
+        out = torch.zeros((self.world * self.nbmax,) + tuple(y.shape[1:]), dtype=y.dtype, device=y.device)
+        for p, (a, b) in enumerate(self.blocks):
+            out[p * self.nbmax:p * self.nbmax + (b - a)] = y[a:b]
+        return out
+
+    def local_block(self, y):
+        """Full state [R, C] -> this rank's zero-padded [nbmax, C] block."""
+        out = torch.zeros((self.nbmax,) + tuple(y.shape[1:]), dtype=y.dtype, device=y.device)
+        out[:self.r1 - self.r0] = y[self.r0:self.r1]
+        return out
+
+    def unpad_state(self, y_full):
+        """Padded [world*nbmax, C] -> full [R, C] in global row order."""
+        return torch.cat([y_full[p * self.nbmax:p * self.nbmax + (b - a)] for p, (a, b) in enumerate(self.blocks)], 0)
+
+    def rhs(self, g, w, y_full, y_local, x0=None, alpha=None, beta=None, alpha_sigmoid=True, add_source=False,
+            stage=None):
+        """K1 over this rank's rows: gathers from the padded full state, the
+        epilogue's own rows from y_local (x0 and outputs local too)."""
+        if self.plan is None:
+            return None if stage is not None else torch.zeros_like(y_local)
+        return ops.spmm_rhs_rows(g, self.plan, w, y_full, y_local, self.pos0, x0=x0, alpha=alpha, beta=beta,
+                                 alpha_sigmoid=alpha_sigmoid, add_source=add_source, stage=stage, col=self.col)
 
 
 def col_blocks(C, world, align=4):
@@ -61,23 +153,23 @@ def shard_batch(edge_index, x, rank, world):
 class RowShardedLaplacian(object):
     """Row-partitioned Laplacian RHS with an all-gather of the state per RHS.
 
-    State per rank: y_local [nb, C] (its row block, zero padded).  Calling the
-    object with (t, y_local) all-gathers the blocks into y_full [world*nb, C]
-    (global row order, padding at the end), aggregates the local rows of A and
-    returns f_local [nb, C]; it drops into gnpde.odeint unchanged."""
+    Rows are split into contiguous blocks balanced by nnz (balanced_row_blocks;
+    ``row_weight`` > 0 also weighs the rows themselves).  State per rank:
+    y_local [nbmax, C] (its row block, zero padded to the largest block).
+    Calling the object with (t, y_local) all-gathers the blocks into the padded
+    [world*nbmax, C] layout of RowPartition, aggregates the local rows of A and
+    returns f_local [nbmax, C]; it drops into gnpde.odeint unchanged."""
 
     graph_capturable = False  # an RCCL all-gather per RHS: the integrator runs it eagerly
 
     def __init__(self, edge_index, edge_weight, num_nodes, alpha, beta=None, x0_local=None, add_source=False,
-                 alpha_sigmoid=True, group=None, local_rhs=None, chunk=ops.DEFAULT_CHUNK):
+                 alpha_sigmoid=True, group=None, local_rhs=None, chunk=ops.DEFAULT_CHUNK, row_weight=0.0):
         self.group = group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
         B, _, E = edge_index.shape
         self.N = int(num_nodes)
         self.R = B * self.N
-        self.blocks, self.nb = row_blocks(self.R, self.world)
-        self.r0, self.r1 = self.blocks[self.rank]
         self.alpha, self.beta = alpha, beta
         self.x0_local = x0_local
         self.add_source, self.alpha_sigmoid = add_source, alpha_sigmoid
@@ -86,7 +178,13 @@ class RowShardedLaplacian(object):
         if local_rhs is None:
             self.g = ops.GraphCSR(edge_index, self.N, chunk=chunk)
             self.w = self.g.gather_weights(edge_weight)
-            self.plan = _local_plan(self.g.csr, self.r0, self.r1, chunk)
+            self.part = RowPartition(self.g, self.world, self.rank, row_weight=row_weight, chunk=chunk)
+            self.blocks, self.nb = self.part.blocks, self.part.nbmax
+        else:  # injected arithmetic (tests): the same nnz-balanced blocks from a host CSR row pointer
+            self.part = None
+            self.blocks = balanced_row_blocks(host_rowptr(edge_index, self.N), self.world, row_weight)
+            self.nb = max(max(r1 - r0 for r0, r1 in self.blocks), 1)
+        self.r0, self.r1 = self.blocks[self.rank]
 
     def gather(self, y_local):
         """All-gather of the row blocks (RCCL over xGMI on ROCm)."""
@@ -100,15 +198,17 @@ class RowShardedLaplacian(object):
         self.nfe += 1
         y_full = self.gather(y_local)
         if self.local_rhs is not None:
-            return self.local_rhs(t, y_full, self.r0, self.r1, y_local)
-        return _rows_rhs(self, y_full, y_local, stage=None)
+            return self.local_rhs(t, self.unpad(y_full), self.r0, self.r1, y_local)
+        return self.part.rhs(self.g, self.w, y_full, y_local, x0=self.x0_local, alpha=self.alpha, beta=self.beta,
+                             alpha_sigmoid=self.alpha_sigmoid, add_source=self.add_source)
 
     def rhs_stage(self, t, y_local, stage):
         self.nfe += 1
         if self.local_rhs is not None:
             raise NotImplementedError
         y_full = self.gather(y_local)
-        _rows_rhs(self, y_full, y_local, stage=stage)
+        self.part.rhs(self.g, self.w, y_full, y_local, x0=self.x0_local, alpha=self.alpha, beta=self.beta,
+                      alpha_sigmoid=self.alpha_sigmoid, add_source=self.add_source, stage=stage)
 
     def scatter(self, y):
         """Full state [R, C] -> this rank's zero-padded block [nb, C]."""
@@ -117,32 +217,26 @@ class RowShardedLaplacian(object):
         return out
 
     def unpad(self, y_full):
-        return y_full[:self.R]
+        """Gathered padded blocks [world*nb, C] -> full state [R, C] in row order."""
+        return torch.cat([y_full[p * self.nb:p * self.nb + (b - a)] for p, (a, b) in enumerate(self.blocks)], 0)
 
 
-def _local_plan(csr, r0, r1, chunk):
+def _local_plan(csr, r0, r1, chunk, pos0=None):
     """Plan over rows [r0, r1) of a global CSR.  Items keep global edge offsets
-    and get global row ids (row + r0), so the epilogue reads its own row from
-    the gathered full state; outputs are addressed through pointers shifted by
-    -r0 rows (ops.spmm_rhs_rows)."""
+    and get row ids shifted to the rows' positions in the gathered state
+    (pos0 + row - r0; pos0 defaults to r0, i.e. global ids), so the epilogue
+    reads its own row from the gathered state; outputs are addressed through
+    pointers shifted back by pos0 rows (ops.spmm_rhs_rows)."""
     if r1 <= r0:
         return None
+    pos0 = r0 if pos0 is None else pos0
     rowptr = csr.rowptr[r0:r1 + 1].contiguous()
     plan = ops.build_plan(rowptr, r1 - r0, int(csr.nnz), chunk)
     if plan.n_items:
-        plan.items.view(-1, 4)[:plan.n_items, 0] += r0
+        plan.items.view(-1, 4)[:plan.n_items, 0] += pos0
     if plan.n_heavy:
-        plan.heavy.view(-1, 4)[:plan.n_heavy, 0] += r0
+        plan.heavy.view(-1, 4)[:plan.n_heavy, 0] += pos0
     return plan
-
-
-def _rows_rhs(sh, y_full, y_local, stage):
-    """K1 over the local rows: gathers from y_full (global row order), the
-    epilogue's own rows come from y_local (local row order)."""
-    if sh.plan is None:
-        return torch.zeros_like(y_local)
-    return ops.spmm_rhs_rows(sh.g, sh.plan, sh.w, y_full, y_local, sh.r0, x0=sh.x0_local, alpha=sh.alpha,
-                             beta=sh.beta, alpha_sigmoid=sh.alpha_sigmoid, add_source=sh.add_source, stage=stage)
 
 
 class ColumnShardedLaplacian(object):
@@ -165,6 +259,13 @@ class ColumnShardedLaplacian(object):
         if local_rhs is None:
             self.g = ops.GraphCSR(edge_index, self.N, chunk=chunk)
             self.w = self.g.gather_weights(edge_weight)
+
+    def graph_capture_state(self, x):
+        """What a captured fused step reads (gnpde.integrator._capture_state)."""
+        return (self.g, self.w) + ((self.x0_local,) if self.add_source else ())
+
+    def capture_key_tensors(self):
+        return tuple(t for t in (self.alpha, self.beta) if isinstance(t, torch.Tensor))
 
     def split(self, x):
         """[B,N,C] -> this rank's contiguous column stripe [B,N,c1-c0]."""

@@ -19,7 +19,7 @@ import torch
 from torch import nn
 
 from . import ops
-from .base_classes import ODEFunc, _tensor_key
+from .base_classes import ODEFunc
 from .utils import MaxNFEException
 
 
@@ -100,18 +100,24 @@ class LaplacianODEFunc(ODEFunc):
         return True
 
     def _x0_like(self, x):
-        """x0 in x's dtype and (padded) width."""
+        """x0 in x's dtype and (padded) width, for the eager autograd path."""
         x0 = self.x0
         if x0.dtype != x.dtype:
             x0 = x0.to(x.dtype)
         if x0.shape[-1] != x.shape[-1]:
-            key = (_tensor_key(self.x0), x.shape[-1], x.dtype)
-            if getattr(self, '_x0_pad', (None,))[0] != key:
-                xp = torch.zeros(*x0.shape[:-1], x.shape[-1], dtype=x.dtype, device=x.device)
-                xp[..., :x0.shape[-1]] = x0
-                self._x0_pad = (key, xp)
-            x0 = self._x0_pad[1]
+            x0 = self.stable_x0(x)
         return x0
+
+    def graph_capture_state(self, x):
+        """What a captured fused step reads (gnpde.integrator._capture_state):
+        the device CSR + plan, the CSR-order weights and, with add_source, the
+        stable x0 buffer — each refreshed in place from the current tensors."""
+        g = self.graph_for(x)
+        w, tag = self._weights_tensor()
+        st = [g, self.csr_weights(g, w, tag)]
+        if self.opt.get('add_source', False):
+            st.append(self.stable_x0(x))
+        return st
 
     def sparse_multiply(self, x):
         """A x (src/function_laplacian_diffusion.py:39-58) — K1 without the epilogue."""
@@ -128,7 +134,7 @@ class LaplacianODEFunc(ODEFunc):
         g = self.graph_for(x)
         w, tag = self._weights_tensor()
         add_source = bool(self.opt.get('add_source', False))
-        x0 = self._x0_like(x) if add_source else None
+        x0 = self.stable_x0(x) if add_source else None
         ops.spmm_rhs(g, self.csr_weights(g, w, tag), x, x0=x0, alpha=self.alpha_train.detach(),
                      beta=self.beta_train.detach(), rhs=True, alpha_sigmoid=not self.opt.get('no_alpha_sigmoid', False),
                      add_source=add_source, stage=stage)

@@ -235,15 +235,21 @@ class SpGraphTransAttentionLayer(nn.Module):
         self.scores_and_stats(g, None, 0)
         return self._uniform[4]
 
+    def uses_wcat(self):
+        """Per-edge score modes project Q|K with one fused MFMA GEMM over [Wq; Wk]."""
+        return self.score_mode != 'reference' or self.opt.get('attention_type', 'scaled_dot') != 'scaled_dot'
+
+    def wcat(self):
+        """([Wq; Wk], [bq; bk]) cached per parameter version."""
+        key = tuple(_tensor_key(t) for t in (self.Q.weight, self.Q.bias, self.K.weight, self.K.bias))
+        if self._wcat is None or self._wcat[0] != key:
+            self._wcat = (key, (torch.cat([self.Q.weight.detach(), self.K.weight.detach()], 0).contiguous(),
+                                torch.cat([self.Q.bias.detach(), self.K.bias.detach()], 0).contiguous()))
+        return self._wcat[1]
+
     def node_scores(self, g, x):
         p0, p1 = self._score_params()
-        wcat = None
-        if self.score_mode != 'reference' or self.opt.get('attention_type', 'scaled_dot') != 'scaled_dot':
-            key = tuple(_tensor_key(t) for t in (self.Q.weight, self.Q.bias, self.K.weight, self.K.bias))
-            if self._wcat is None or self._wcat[0] != key:  # [Wq; Wk] for the fused MFMA projection
-                self._wcat = (key, (torch.cat([self.Q.weight.detach(), self.K.weight.detach()], 0).contiguous(),
-                                    torch.cat([self.Q.bias.detach(), self.K.bias.detach()], 0).contiguous()))
-            wcat = self._wcat[1]
+        wcat = self.wcat() if self.uses_wcat() else None
         return ops.node_scores(g, x, self.Q.weight.detach(), self.Q.bias.detach(), self.K.weight.detach(),
                                self.K.bias.detach(), self.h, self.opt.get('attention_type', 'scaled_dot'),
                                self.score_mode, p0, p1, wcat=wcat)
@@ -288,6 +294,23 @@ class ODEFuncTransformerAtt(ODEFunc):
         aggregation epilogue (gnpde.integrator, no-grad fixed-grid solvers)."""
         self._rhs(x, stage)
 
+    def graph_capture_state(self, x):
+        """What a captured fused step reads (gnpde.integrator._capture_state):
+        the device CSR / CSC + plans, the layer's cached operands (the 1/outdeg
+        weights of the uniform case, or the concatenated [Wq; Wk] projection)
+        and, with add_source, the stable x0 buffer."""
+        g = self.graph_for(x)
+        lay = self.multihead_att_layer
+        st = [g]
+        if lay.is_uniform(int(self.opt['attention_norm_idx'])):
+            lay.uniform_weights(g)
+            st.append(lay._uniform)
+        elif lay.uses_wcat():
+            st.append(lay.wcat())
+        if self.opt.get('add_source', False):
+            st.append(self.stable_x0(x))
+        return st
+
     def supports_feature_padding(self):
         """With the fork's scaled_dot under source-grouped softmax the weights do
         not depend on x (1/outdeg), so columns are independent and the fused
@@ -312,7 +335,8 @@ class ODEFuncTransformerAtt(ODEFunc):
         add_source = bool(self.opt.get('add_source', False))
         if add_source and self.x0 is None:
             raise RuntimeError("ODEFuncTransformerAtt: add_source needs x0 (ODEblock.set_x0)")
-        x0 = self.x0 if add_source else None
+        # fused stages (and their captured graphs) read a stable x0 buffer (ODEFunc.stable_x0)
+        x0 = (self.stable_x0(x) if stage is not None else self.x0) if add_source else None
         if x0 is not None and x0.dtype != x.dtype:
             x0 = x0.to(x.dtype)
         kw = dict(x0=x0, alpha=self.alpha_train.detach(), beta=self.beta_train.detach(),

@@ -27,6 +27,7 @@ import weakref
 import torch
 
 from . import ops
+from ._cache import _tensor_key
 
 # Dormand-Prince-Shampine (torchdiffeq dopri5.py)
 _DP_ALPHA = [1 / 5, 3 / 10, 4 / 5, 8 / 9, 1., 1.]
@@ -253,30 +254,38 @@ class _StepGraphs(object):
 _GRAPH_CACHE = weakref.WeakKeyDictionary()
 
 
-def _graph_cache_key(func, method, y):
+def _capture_state(func, y):
+    """The derived device objects a captured step reads (device CSR and plans,
+    CSR-order weights, the stable x0 buffer, cached projection weights ...),
+    refreshed in place from the module's current tensors by
+    ``func.graph_capture_state(y)``; None when the module offers no such hook
+    (its graphs are then captured per call and never cached)."""
+    fn = getattr(func, 'graph_capture_state', None)
+    return None if fn is None else tuple(fn(y))
+
+
+def _graph_cache_key(func, method, y, state):
     """Everything a captured step reads besides its own buffers: the module's
-    parameters and buffers, its graph / weight / x0 tensors (pointer, version,
-    shape, dtype; x0 only under add_source), its options, and the state's shape and layout.  A version
-    bump (in-place update) recaptures, so cached derived data (CSR-order
-    weights, padded x0) can never go stale under a replay."""
-    try:
-        tens = [_tkey(t) for t in itertools.chain(func.parameters(), func.buffers())]
-    except AttributeError:
+    parameters and buffers (identity + version: in-place updates recapture,
+    host-read scalars such as exp_kernel's lengthscale are baked into the
+    launches), its options, the state's shape and layout, and the IDENTITY of
+    every derived object in ``state``.  The cache entry holds ``state``
+    itself, so the buffers a replay reads stay alive however the module
+    rebuilds its own caches (a solve on another graph replaces func._graph;
+    the replayed step then finds a different object and recaptures instead of
+    reading freed memory).  Source tensors (edge_index, edge_weight,
+    attention_weights, x0) are NOT in the key: what the launches read is the
+    derived buffers, refreshed in place when only the values change."""
+    if state is None:
         return None
+    if hasattr(func, 'parameters'):
+        tens = [_tensor_key(t) for t in itertools.chain(func.parameters(), func.buffers())]
+    else:  # a plain RHS object (gnpde.dist shards): the scalars it reads by pointer
+        tens = [_tensor_key(t) for t in getattr(func, 'capture_key_tensors', lambda: ())()]
     opt = getattr(func, 'opt', None)
-    names = ['edge_index', 'edge_weight', 'attention_weights']
-    if not isinstance(opt, dict) or opt.get('add_source', False):
-        names.append('x0')  # read only with add_source (GNN.forward resets it every call)
-    for name in names:
-        v = getattr(func, name, None)
-        if torch.is_tensor(v):
-            tens.append((name, _tkey(v)))
     okey = repr(sorted(opt.items(), key=lambda kv: str(kv[0]))) if isinstance(opt, dict) else None
-    return (method, tuple(y.shape), tuple(y.stride()), y.dtype, str(y.device), okey, tuple(tens))
-
-
-def _tkey(t):
-    return (t.data_ptr(), t._version, tuple(t.shape), t.dtype, str(t.device))
+    return (method, tuple(y.shape), tuple(y.stride()), y.dtype, str(y.device), okey, tuple(tens),
+            tuple(id(o) for o in state))
 
 
 def _uniform_run(steps, n, k, dt):
@@ -334,11 +343,12 @@ def odeint_fixed(func, y0, t, method, step_size=None, combine=None, graph=None):
         # a RHS with a collective inside (dist.RowShardedLaplacian) opts out of capture
         graph = len(steps) >= GRAPH_MIN_STEPS and getattr(func, 'graph_capturable', True)
     graphs = None
-    cache_key = _graph_cache_key(func, method, y0) if fused and graph else None
+    state = _capture_state(func, y0) if fused and graph else None
+    cache_key = _graph_cache_key(func, method, y0, state)
     hit = _GRAPH_CACHE.get(func) if cache_key is not None else None
     if hit is not None and hit[0] == cache_key and len(steps) >= 1 and steps[0][1] - steps[0][0] == hit[1][1]:
         # same RHS state, shape and dt as a previous call: replay from the first step
-        _, graphs, ws = hit
+        _, graphs, ws, _ = hit
         graphs[0].bufs[0].copy_(y0)
         gi = 0
     solution = [y0]
@@ -355,7 +365,9 @@ def odeint_fixed(func, y0, t, method, step_size=None, combine=None, graph=None):
             graphs[0].bufs[0].copy_(yc)
             gi = 0
             if cache_key is not None:
-                _GRAPH_CACHE[func] = (cache_key, graphs, ws)
+                # the eager first step may have rebuilt derived objects: key what the capture read
+                state = _capture_state(func, yc)
+                _GRAPH_CACHE[func] = (_graph_cache_key(func, method, y0, state), graphs, ws, state)
         S = graphs[0].S if graphs is not None else 0
         if S and gi == 0 and _uniform_run(steps, n, S, graphs[1]) and \
                 (j >= len(t_h) or t_h[j] > steps[n + S - 2][1]) and _nfe_headroom(func, S * graphs[0].n_rhs):

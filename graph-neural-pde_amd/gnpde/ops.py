@@ -219,9 +219,9 @@ class GraphCSR(object):
             self._indeg = deg
         return self._indeg
 
-    def gather_weights(self, w, transpose=False):
+    def gather_weights(self, w, transpose=False, out=None):
         """COO-order weights [B,E] or attention [B,E,h] -> CSR-order [nnz] (head mean);
-        transpose=True gives CSC order."""
+        transpose=True gives CSC order.  ``out``: an existing [nnz] fp32 buffer to fill."""
         _require_gpu(w, "edge weights", torch.float32)
         w = w.contiguous()
         if w.dim() == 2:
@@ -233,7 +233,12 @@ class GraphCSR(object):
         if w.shape[0] != self.B or w.shape[1] != self.E:
             raise ValueError("weights shape %s does not match edge_index [%d,2,%d]" % (tuple(w.shape), self.B,
                                                                                         self.E))
-        out = torch.empty(max(self.nnz, 1), dtype=torch.float32, device=w.device)
+        if out is None:
+            out = torch.empty(max(self.nnz, 1), dtype=torch.float32, device=w.device)
+        elif out.dtype != torch.float32 or out.numel() != max(self.nnz, 1) or not out.is_contiguous() or \
+                out.device != w.device:
+            raise ValueError("gather_weights: out must be a contiguous fp32 [%d] buffer on %s" % (max(self.nnz, 1),
+                                                                                              w.device))
         perm = self.csc.perm if transpose else self.csr.perm
         _lib.call("gnpde_gather_weights_f32", _ptr(w), self.nnz, H, _ptr(perm), _ptr(out),
                   _stream(w.device))
@@ -398,7 +403,7 @@ def spmm_rhs(g, w_csr, x, x0=None, alpha=None, beta=None, rhs=True, alpha_sigmoi
         out = torch.empty_like(xr)
     grouped = g.csc if transpose else g.csr
     plan = grouped.plan
-    partials = torch.empty(plan.n_slots * C, dtype=torch.float32, device=dev) if plan.n_slots else None
+    partials = _partials(plan, C, dev)
     epi = (C, _ptr(xr), C, _ptr(x0r), C, _ptr(a), _ptr(b), _flags(rhs, alpha_sigmoid, add_source), _ptr(out), C,
            _ptr(partials), st, _stream(dev))
     if dt == torch.bfloat16:
@@ -417,6 +422,20 @@ def spmm_rhs(g, w_csr, x, x0=None, alpha=None, beta=None, rhs=True, alpha_sigmoi
     return None if stage is not None else out.view(shape)
 
 
+# byte offsets of the hub partial stores are 32-bit (buffer addressing, csrc/common.hpp kBufRecords)
+_PARTIALS_MAX_BYTES = 0xffffff00
+
+
+def _partials(plan, C, dev):
+    """fp32 scratch of the hub chunk partial sums: n_slots * C floats."""
+    if not plan.n_slots:
+        return None
+    if plan.n_slots * C * 4 >= _PARTIALS_MAX_BYTES:
+        raise ValueError("gnpde: %d hub partial slots x %d columns exceed the 4 GiB of 32-bit buffer offsets the "
+                         "in-launch hub combine addresses; use a larger chunk (opt['gnpde_chunk'])" % (plan.n_slots, C))
+    return torch.empty(plan.n_slots * C, dtype=torch.float32, device=dev)
+
+
 class RefDstWeights(object):
     """Weights K1 computes on the fly (gnpde_attn_ref_rhs_f32): the fork's
     scaled_dot under destination-grouped softmax, head-mean per edge from the
@@ -427,12 +446,14 @@ class RefDstWeights(object):
 
 
 def spmm_rhs_rows(g, plan, w_csr, x_src, x_rows, row0, x0=None, alpha=None, beta=None, alpha_sigmoid=True,
-                  add_source=False, stage=None, out=None):
-    """K1 over a row block: ``plan`` covers rows [row0, row0 + n) with global row
-    ids; gathers read ``x_src`` (all rows, global order); the block's own state
-    ``x_rows`` [n, C], ``x0`` and the outputs are local buffers addressed through
-    pointers shifted back by row0 rows (never dereferenced outside the block).
-    The epilogue's x_r comes from x_src[row], which holds the same values."""
+                  add_source=False, stage=None, out=None, col=None):
+    """K1 over a row block: ``plan`` covers rows [row0, row0 + n) by their
+    positions in ``x_src`` (the gathered state); gathers read ``x_src`` through
+    ``col`` (default: the CSR's global ids; dist.RowPartition passes ids
+    relabelled into its padded layout); the block's own state ``x_rows`` [n, C],
+    ``x0`` and the outputs are local buffers addressed through pointers shifted
+    back by row0 rows (never dereferenced outside the block).  The epilogue's
+    x_r comes from x_src[row], which holds the same values."""
     xs = _rows(x_src, "x_src")
     xl = _rows(x_rows, "x_rows")
     C = xs.shape[1]
@@ -449,8 +470,9 @@ def spmm_rhs_rows(g, plan, w_csr, x_src, x_rows, row0, x0=None, alpha=None, beta
         st = ctypes.byref(stage.struct(xs, shift))
     elif out is None:
         out = torch.empty_like(xl)
-    partials = torch.empty(plan.n_slots * C, dtype=torch.float32, device=dev) if plan.n_slots else None
-    _lib.call("gnpde_spmm_rhs_f32", _ptr(plan.items), plan.n_items, _ptr(plan.heavy), plan.n_heavy, _ptr(g.csr.col),
+    partials = _partials(plan, C, dev)
+    _lib.call("gnpde_spmm_rhs_f32", _ptr(plan.items), plan.n_items, _ptr(plan.heavy), plan.n_heavy,
+              _ptr(g.csr.col if col is None else col),
               _ptr(w_csr), C, _ptr(xs), C, sp(x0r), C, _ptr(a), _ptr(b), _flags(True, alpha_sigmoid, add_source),
               sp(out) if out is not None else ctypes.c_void_p(0), C, _ptr(partials), st, _stream(dev))
     return None if stage is not None else out.view(x_rows.shape)

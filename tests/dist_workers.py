@@ -53,7 +53,7 @@ def rows_worker(rank, world, port, method, q):
 
         def local_rhs(t, y_full, r0, r1, y_local):
             f = torch.zeros_like(y_local)
-            f[:r1 - r0] = alpha * (At[r0:r1] @ y_full[:R] - y_full[r0:r1])
+            f[:r1 - r0] = alpha * (At[r0:r1] @ y_full - y_full[r0:r1])  # y_full: unpadded [R, C]
             return f
 
         sh = gd.RowShardedLaplacian(torch.from_numpy(ei), torch.from_numpy(w), x.shape[1], alpha, local_rhs=local_rhs)

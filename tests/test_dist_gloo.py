@@ -34,6 +34,28 @@ def test_row_blocks_and_col_blocks():
     assert cb[0][0] == 0 and cb[-1][1] == 10 and all(b > a for a, b in cb)
 
 
+def test_balanced_row_blocks():
+    """nnz-balanced contiguous row blocks: a power-law row pointer
+    whose first rows hold most edges gets short first blocks."""
+    import numpy as np
+    deg = np.array([500, 300, 100] + [2] * 997)
+    rp = np.concatenate([[0], np.cumsum(deg)])
+    b = gd.balanced_row_blocks(rp, 4)
+    assert b[0][0] == 0 and b[-1][1] == 1000 and all(b[i][1] == b[i + 1][0] for i in range(3))
+    work = [rp[r1] - rp[r0] for r0, r1 in b]
+    assert b[0] == (0, 2) and max(work) == 800  # rows are not split: the 500 + 300 head is the nearest cut
+    # row_weight: each row also costs row_weight edges
+    bw = gd.balanced_row_blocks(rp, 4, row_weight=10.0)
+    cost = [rp[r1] - rp[r0] + 10 * (r1 - r0) for r0, r1 in bw]
+    assert max(cost) - min(cost) <= 520
+    # more ranks than rows: empty blocks at the end, still a cover
+    assert gd.balanced_row_blocks(np.array([0, 3, 6]), 4)[-1] == (2, 2)
+    # host_rowptr over a batch (block-diagonal rows)
+    import torch
+    ei = torch.tensor([[[0, 0, 2], [1, 2, 0]], [[1, 1, 1], [0, 0, 2]]])
+    assert gd.host_rowptr(ei, 3).tolist() == [0, 2, 2, 3, 3, 6, 6]
+
+
 def test_shard_batch():
     import torch
     ei = torch.zeros(5, 2, 3, dtype=torch.int64)
@@ -46,10 +68,12 @@ def test_shard_batch():
 @pytest.mark.parametrize("method", ["euler", "rk4"])
 def test_row_sharded_integration_matches_single_process(method):
     res = _run(W.rows_worker, method)
+    ei = W.problem()[0]
+    want_blocks = [list(b) for b in gd.balanced_row_blocks(gd.host_rowptr(ei, 61), 2)]
     for rank, err, nfe, blocks in res:
         assert err < 1e-12
         assert nfe == (4 if method == "euler" else 16)
-        assert blocks == [[0, 31], [31, 61]]
+        assert blocks == want_blocks
 
 
 @pytest.mark.parametrize("method", ["rk4", "dopri5"])

@@ -229,3 +229,64 @@ def test_seg_plan_build_tiles_edges(eb):
         if a[1] == b[0]:
             first_len = rp[b[3] + 1] - b[0]
             assert a[1] - a[0] + first_len > eb
+
+
+# ---------------------------------------------------------------- ODE-block module layout (reference state_dict)
+@pytest.mark.parametrize("block,extra", [("constant", {}), ("attention", {}), ("mixed", dict(heads=1)),
+                                         ("hard_attention", dict(att_samp_pct=0.5))])
+def test_block_builds_two_odefuncs_like_reference(block, extra):
+    """src/base_classes.py:40,43 wraps a first ODEFunc in reg_odefunc; the block then
+    builds its own (src/block_constant.py:11, block_transformer_attention.py:11,
+    block_mixed.py:12, block_transformer_hard_attention.py:11).  A reference
+    state_dict whose two copies differ loads so that the integrated RHS is odefunc.*."""
+    opt = dict(OPT, block=block, **extra)
+    cls = gnpde.set_block(opt)
+    blk = cls(gnpde.LaplacianODEFunc, [], opt, None, t=torch.tensor([0, 1]))
+    assert blk.odefunc is not blk.reg_odefunc.odefunc
+    sd = blk.state_dict()
+    assert 'odefunc.alpha_train' in sd and 'reg_odefunc.odefunc.alpha_train' in sd
+    sd = {k: v.clone() for k, v in sd.items()}
+    sd['odefunc.alpha_train'].fill_(0.7)
+    sd['reg_odefunc.odefunc.alpha_train'].fill_(-3.0)
+    sd['odefunc.beta_train'].fill_(0.2)
+    blk.load_state_dict(sd)
+    assert blk.odefunc.alpha_train.item() == pytest.approx(0.7)
+    assert blk.reg_odefunc.odefunc.alpha_train.item() == pytest.approx(-3.0)
+    # the solver integrates self.odefunc (src/block_constant.py:31 in eval): spy integrator
+    seen = []
+
+    def spy(func, y, t, **kw):
+        seen.append(func)
+        return torch.stack([y, y], 0)
+
+    blk.eval()
+    blk.test_integrator = spy
+    blk.odefunc.attention_weights = torch.ones(1, 4)
+    blk._integrate(torch.ones(1, 3, 6), {'step_size': 1})
+    assert seen == [blk.odefunc]
+
+
+def test_reset_graph_data_sets_both_copies_and_fp32():
+    """reset_graph_data (src/base_classes.py:86-89) hands the same graph to both copies;
+    set_x0 (:53-55) both x0s; the weights are fp32 whatever the state dtype."""
+    blk = gnpde.ConstantODEblock(gnpde.LaplacianODEFunc, [], OPT, None, t=torch.tensor([0, 1]))
+    data = gnpde.GraphData()
+    data.new_graph(torch.tensor([[[0, 2, 2, 1], [1, 0, 1, 2]]]), 3)
+    blk.reset_graph_data(data, torch.bfloat16)
+    assert blk.odefunc.edge_weight.dtype == torch.float32
+    assert blk.reg_odefunc.odefunc.edge_index is blk.odefunc.edge_index
+    assert blk.reg_odefunc.odefunc.edge_weight is blk.odefunc.edge_weight
+    blk.set_x0(torch.ones(1, 3, 6))
+    assert blk.odefunc.x0 is not None and blk.reg_odefunc.odefunc.x0 is not None
+
+
+def test_tensor_key_is_identity_not_address():
+    """the derived-data caches must not confuse a freed tensor with a
+    new one allocated at the same address."""
+    from gnpde._cache import _tensor_key
+    a = torch.zeros(4)
+    ka = _tensor_key(a)
+    b = torch.zeros(4)
+    assert ka != _tensor_key(b) and ka == _tensor_key(a)
+    a.add_(1)
+    assert ka != _tensor_key(a)
