@@ -82,6 +82,12 @@ SIGNATURES = {
     "gnpde_score_input_grad_f32": (_int, [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _int, _vp, _i64, _int, _vp]),
     "gnpde_gather_head_f32": (_int, [_vp, _i64, _int, _int, _vp, _f32, _vp, _vp]),
     "gnpde_rk_combine_f32": (_int, [_i64, _vp, _int, ctypes.POINTER(_vp), ctypes.POINTER(_f64), _f64, _vp, _vp]),
+    "gnpde_self_loops_workspace_bytes": (_size, [_i64, _i64, _i64]),
+    "gnpde_self_loops_count": (_int, [_vp, _i64, _i64, c_i64p, _vp, _size, _vp]),
+    "gnpde_add_self_loops": (_int, [_vp, _vp, _i64, _i64, _i64, _f32, _i64, _vp, _vp, _vp, _size, _vp]),
+    "gnpde_norm_weights_f32": (_int, [_vp, _vp, _i64, _i64, _i64, _vp, _vp, _int, _vp, _vp, _vp]),
+    "gnpde_score_grad_f32": (_int, [_vp, _vp, _vp, _i64, _i64, _int, _int, _i64, _i64, _vp, _vp, _i64, _f32, _f32, _vp,
+                                    _vp, _i64, _vp, _vp]),
 }
 
 # constants mirrored from include/gnpde.h
@@ -100,6 +106,9 @@ SCORE_EXP_KERNEL = 2
 SCORE_COSINE = 3
 SCORE_PEARSON = 4
 SCORE_UNIFORM = 5
+NORM_RW_ROW = 0
+NORM_RW_COL = 1
+NORM_GCN = 2
 
 _lock = threading.Lock()
 _lib = None

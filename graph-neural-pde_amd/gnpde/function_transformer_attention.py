@@ -40,7 +40,11 @@ aggregations per head (q side over the CSR, k side over the CSC) and the
 projection backward (MFMA projection for d/dx, library GEMM for d/dW).  The
 transformer ODEFunc then composes it with the Laplacian RHS autograd
 (function_laplacian_diffusion._LaplacianRHS), whose weight gradient is an
-SDDMM.  exp_kernel / cosine_sim / pearson have no backward (raise).
+SDDMM.  exp_kernel / cosine_sim / pearson: one pass per side over the grouped
+CSR / CSC turns dL/ds into dL/dq and dL/dk (gnpde_score_grad_f32, exp_kernel
+also into dL/d output_var and dL/d lengthscale), then the same projection
+backward.  Every gradient is pinned by fixtures of the reference's own fp64
+autograd (tests/golden/grad_*.npz, tests/test_gpu_grad_golden.py).
 """
 import torch
 from torch import nn
@@ -70,14 +74,16 @@ def _needs_grad(*ts):
 
 class _EdgeAttention(torch.autograd.Function):
     """attention [B,E,h] (COO) = SpGraphTransAttentionLayer.forward's first
-    output as a function of (x, Wq, bq, Wk, bk); backward in graph passes."""
+    output as a function of (x, Wq, bq, Wk, bk[, output_var, lengthscale]);
+    backward in graph passes."""
 
     @staticmethod
-    def forward(ctx, x, Wq, bq, Wk, bk, layer, g, norm_idx):
+    def forward(ctx, x, Wq, bq, Wk, bk, ov, ls, layer, g, norm_idx):
         ns, m, rl = layer.scores_and_stats(g, x.detach(), norm_idx)
         att = ops.edge_attention(g, ns, m, rl, norm_idx)
         ctx.save_for_backward(x, Wq, bq, Wk, bk, att)
         ctx.layer, ctx.g, ctx.norm_idx, ctx.ns = layer, g, norm_idx, ns
+        ctx.p_shapes = (None if ov is None else (ov.shape, ov.dtype), None if ls is None else (ls.shape, ls.dtype))
         return att
 
     @staticmethod
@@ -86,19 +92,22 @@ class _EdgeAttention(torch.autograd.Function):
         g, ns, norm_idx = ctx.g, ctx.ns, ctx.norm_idx
         grouped = g.csr if norm_idx == 0 else g.csc
         gs = ops.softmax_backward(grouped, att, g_att.float())
+        g_ov = g_ls = None
         if ns.mode == ops._lib.SCORE_UNIFORM:
             # every score of a softmax group is the same node score: the attention does not move
-            return (torch.zeros_like(x), torch.zeros_like(Wq), torch.zeros_like(bq), torch.zeros_like(Wk),
-                    torch.zeros_like(bk), None, None, None)
-        if ns.mode == ops._lib.SCORE_REFERENCE:
+            grads = (torch.zeros_like(x), torch.zeros_like(Wq), torch.zeros_like(bq), torch.zeros_like(Wk),
+                     torch.zeros_like(bk))
+        elif ns.mode == ops._lib.SCORE_REFERENCE:
             grads = _reference_score_backward(g, ns, gs, x.detach(), Wq.detach(), bq.detach(), Wk.detach(),
                                               bk.detach())
         elif ns.mode == ops._lib.SCORE_DOT:
             grads = _dot_score_backward(g, ns, gs, x.detach(), Wq.detach(), Wk.detach())
         else:
-            raise NotImplementedError("gnpde: no backward for attention_type %r (scaled_dot only)" %
-                                      ctx.layer.opt.get('attention_type'))
-        return grads + (None, None, None)
+            grads, gp = _edge_score_backward(g, ns, gs, x.detach(), Wq.detach(), Wk.detach())
+            if gp is not None:
+                (so, do), (sl, dl) = ctx.p_shapes
+                g_ov, g_ls = gp[0].reshape(so).to(do), gp[1].reshape(sl).to(dl)
+        return grads + (g_ov, g_ls, None, None, None)
 
 
 def _reference_score_backward(g, ns, gs, x, Wq, bq, Wk, bk):
@@ -153,6 +162,29 @@ def _dot_score_backward(g, ns, gs, x, Wq, Wk):
     gb = gqk.sum(0)
     att_dim = H * dk
     return (gx.view(x.shape), gW[:att_dim], gb[:att_dim], gW[att_dim:], gb[att_dim:])
+
+
+def _edge_score_backward(g, ns, gs, x, Wq, Wk):
+    """exp_kernel / cosine_sim / pearson (function_transformer_attention.py:246-259):
+    dL/dq over the aggregation CSR (edges grouped by source) and dL/dk over the
+    CSC (grouped by destination) in one pass each (gnpde_score_grad_f32), then
+    the projection backward as for the per-edge scaled_dot.  exp_kernel also
+    returns dL/d(output_var), dL/d(lengthscale)."""
+    with_p = ns.mode == ops._lib.SCORE_EXP_KERNEL
+    if with_p:
+        gq, gov, gls = ops.score_grad(g.csr, 0, ns, gs, with_params=True)
+    else:
+        gq = ops.score_grad(g.csr, 0, ns, gs)
+    gk = ops.score_grad(g.csc, 1, ns, gs)
+    gqk = torch.cat([gq, gk], 1)
+    xr = x.reshape(g.R, -1)
+    W = torch.cat([Wq, Wk], 0)
+    gx, _ = ops.linear(gqk, W.t().contiguous())                # gx = [g_q | g_k] [Wq; Wk]
+    gW = gqk.t() @ xr
+    gb = gqk.sum(0)
+    att_dim = ns.heads * ns.dk
+    grads = (gx.view(x.shape), gW[:att_dim], gb[:att_dim], gW[att_dim:], gb[att_dim:])
+    return grads, ((gov, gls) if with_p else None)
 
 
 class SpGraphTransAttentionLayer(nn.Module):
@@ -260,8 +292,11 @@ class SpGraphTransAttentionLayer(nn.Module):
         materialised (dead for mix_features=False)."""
         g = self.graph_for(x, edge)
         norm_idx = int(self.opt['attention_norm_idx'])
-        if _needs_grad(x, self.Q.weight, self.Q.bias, self.K.weight, self.K.bias):
-            att = _EdgeAttention.apply(x, self.Q.weight, self.Q.bias, self.K.weight, self.K.bias, self, g, norm_idx)
+        ov = getattr(self, 'output_var', None)
+        ls = getattr(self, 'lengthscale', None)
+        if _needs_grad(x, self.Q.weight, self.Q.bias, self.K.weight, self.K.bias, ov, ls):
+            att = _EdgeAttention.apply(x, self.Q.weight, self.Q.bias, self.K.weight, self.K.bias, ov, ls, self, g,
+                                       norm_idx)
             return att, (None, None)
         ns, m, rl = self.scores_and_stats(g, x, norm_idx)
         return ops.edge_attention(g, ns, m, rl, norm_idx), (None, None)
@@ -329,7 +364,8 @@ class ODEFuncTransformerAtt(ODEFunc):
         g = self.graph_for(x)
         lay = self.multihead_att_layer
         if stage is None and _needs_grad(x, self.alpha_train, self.beta_train, lay.Q.weight, lay.Q.bias,
-                                         lay.K.weight, lay.K.bias):
+                                         lay.K.weight, lay.K.bias, getattr(lay, 'output_var', None),
+                                         getattr(lay, 'lengthscale', None)):
             return self._rhs_autograd(g, x)
         norm_idx = int(self.opt['attention_norm_idx'])
         add_source = bool(self.opt.get('add_source', False))

@@ -169,7 +169,7 @@ def build_seg_plan(rowptr, eb):
     return SegPlan(eb, it_view, ni.value, ch_view, nc.value, dev32(heavy, nh.value), nh.value)
 
 
-def build_grouped(edge_index, num_nodes, key_row, chunk=DEFAULT_CHUNK):
+def build_grouped(edge_index, num_nodes, key_row, chunk=DEFAULT_CHUNK, plan=True):
     """COO [B,2,E] -> block-diagonal CSR grouped by edge_index[:, key_row] (+ plan)."""
     B, _, E = edge_index.shape
     N = int(num_nodes)
@@ -183,8 +183,60 @@ def build_grouped(edge_index, num_nodes, key_row, chunk=DEFAULT_CHUNK):
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
     _lib.call("gnpde_csr_build", _ptr(ei), B, E, N, key_row, _ptr(rowptr), _ptr(col), _ptr(perm), _ptr(ws), ws_bytes,
               _stream(dev))
-    plan = build_plan(rowptr, R, nnz, chunk)
+    plan = build_plan(rowptr, R, nnz, chunk) if plan else None
     return GroupedCSR(rowptr, col, perm, R, nnz, key_row, plan)
+
+
+# --------------------------------------------------------------------------- graph normalisation
+def add_self_loops(edge_index, edge_weight, fill_value, num_nodes):
+    """gnpde_add_self_loops: non-loop edges in COO order, then one loop per node
+    with its last existing loop's weight or fill_value (intended semantics of
+    src/utils.py:16-42).  -> (edge_index [B,2,K+N] int64, weights [B,K+N] fp32)."""
+    _require_gpu(edge_index, "edge_index", torch.int64)
+    B, _, E = edge_index.shape
+    N = int(num_nodes)
+    ei = edge_index.contiguous()
+    dev = ei.device
+    w = None
+    if edge_weight is not None:
+        _require_gpu(edge_weight, "edge_weight", torch.float32)
+        w = edge_weight.contiguous()
+        if tuple(w.shape) != (B, E):
+            raise ValueError("edge_weight shape %s != [%d,%d]" % (tuple(w.shape), B, E))
+    ws_bytes = _lib.fn("gnpde_self_loops_workspace_bytes")(B, E, N)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    counts = (ctypes.c_int64 * B)()
+    _lib.call("gnpde_self_loops_count", _ptr(ei), B, E, counts, _ptr(ws), ws_bytes, _stream(dev))
+    ks = sorted(set(int(c) for c in counts))
+    if len(ks) != 1:
+        raise ValueError("batched edge lists have different lengths after self-loop insertion %s; the [B,2,E] "
+                         "format needs equal counts per batch element" % sorted(k + N for k in ks))
+    K = ks[0]
+    ei_out = torch.empty(B, 2, K + N, dtype=torch.int64, device=dev)
+    w_out = torch.empty(B, K + N, dtype=torch.float32, device=dev)
+    _lib.call("gnpde_add_self_loops", _ptr(ei), _ptr(w), B, E, N, float(fill_value), K, _ptr(ei_out), _ptr(w_out),
+              _ptr(ws), ws_bytes, _stream(dev))
+    return ei_out, w_out
+
+
+def norm_weights(edge_index, edge_weight, num_nodes, mode):
+    """gnpde_norm_weights_f32: rw (norm_dim 0 / 1) or symmetric gcn weights, degrees
+    summed in COO order over a grouped CSR (src/utils.py:177-194, :215-233)."""
+    _require_gpu(edge_index, "edge_index", torch.int64)
+    B, _, E = edge_index.shape
+    N = int(num_nodes)
+    ei = edge_index.contiguous()
+    w = None
+    if edge_weight is not None:
+        _require_gpu(edge_weight, "edge_weight", torch.float32)
+        w = edge_weight.contiguous()
+    key_row = 0 if mode == _lib.NORM_RW_ROW else 1
+    grouped = build_grouped(ei, N, key_row, plan=False)
+    fac = torch.empty(B * N, dtype=torch.float32, device=ei.device)
+    out = torch.empty(B, E, dtype=torch.float32, device=ei.device)
+    _lib.call("gnpde_norm_weights_f32", _ptr(ei), _ptr(w), B, E, N, _ptr(grouped.rowptr), _ptr(grouped.perm), int(mode),
+              _ptr(fac), _ptr(out), _stream(ei.device))
+    return out
 
 
 class GraphCSR(object):
@@ -718,6 +770,29 @@ def score_input_grad(gcs, U, deg, gxbar, B, N, C, out=None):
     _lib.call("gnpde_score_input_grad_f32", _ptr(gcs.contiguous()), _ptr(U.contiguous()), _ptr(deg),
               _ptr(gxbar.contiguous()), B, N, C, H, _ptr(gx), C, int(out is not None), _stream(dev))
     return gx
+
+
+def score_grad(grouped, side, ns, gs, with_params=False):
+    """gnpde_score_grad_f32: dL/d(q) (side 0, over the aggregation CSR) or dL/d(k)
+    (side 1, over the CSC) [R, att] from gs = dL/ds [B,E,H] (COO) for the per-edge
+    score modes; with_params (exp_kernel): also the per-edge terms of
+    dL/d(output_var), dL/d(lengthscale) summed in fp64 -> (out, g_p0, g_p1)."""
+    _require_gpu(gs, "score grad", torch.float32)
+    gs = gs.contiguous()
+    att = ns.heads * ns.dk
+    dev = gs.device
+    out = torch.empty(grouped.R, att, dtype=torch.float32, device=dev)
+    gp = torch.empty(max(grouped.nnz, 1), 2 * ns.heads, dtype=torch.float32, device=dev) if with_params else None
+    _lib.call("gnpde_score_grad_f32", _ptr(grouped.rowptr), _ptr(grouped.col), _ptr(grouped.perm), grouped.R,
+              grouped.nnz, int(side), ns.mode, ns.heads, ns.dk, _ptr(ns.q), _ptr(ns.k), ns.ldqk, ns.p0, ns.p1, _ptr(gs),
+              _ptr(out), att, _ptr(gp), _stream(dev))
+    if not with_params:
+        return out
+    if grouped.nnz == 0:
+        z = torch.zeros((), dtype=torch.float64, device=dev)
+        return out, z, z
+    gpd = gp[:grouped.nnz].double()
+    return out, gpd[:, :ns.heads].sum(), gpd[:, ns.heads:].sum()
 
 
 def gather_head(grouped, w, h, scale=1.0):

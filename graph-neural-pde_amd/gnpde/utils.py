@@ -9,7 +9,11 @@
   known-answer tests pin (test/test_utils.py:62-79: dense result ==
   sklearn.normalize(A + s*I, 'l1', axis = 0 if norm_dim == 1 else 1);
   test/test_function_laplacian_diffusion.py:56-86 for the symmetric form).
-  They run once per graph on the device with torch ops (not per RHS).
+  Device tensors go through the HIP kernels of csrc/prep.hip (once per graph,
+  deterministic: a node keeps its LAST existing loop's weight, degrees are
+  summed in COO order — the fp32 additions of torch's CPU scatter_add_); host
+  tensors (the reference tests' toy graphs) through the same semantics in
+  torch.
 * ``softmax`` — src/utils.py:116-127, for callers outside the fused RHS (the
   RHS itself never calls it; its edge softmax is fused into the HIP kernels).
 """
@@ -42,6 +46,9 @@ def add_remaining_self_loops(edge_index, edge_attr=None, fill_value=1.0, num_nod
     B, _, E = edge_index.shape
     n = maybe_num_nodes(edge_index, num_nodes)
     dev = edge_index.device
+    if edge_index.is_cuda:
+        from . import ops
+        return ops.add_self_loops(edge_index, None if edge_attr is None else edge_attr.float(), fill_value, n)
     if edge_attr is None:
         edge_attr = torch.ones(B, E, dtype=torch.float32, device=dev)
     out_e, out_w = [], []
@@ -53,7 +60,11 @@ def add_remaining_self_loops(edge_index, edge_attr=None, fill_value=1.0, num_nod
         loop_w = torch.full((n,), float(fill_value), dtype=w.dtype, device=dev)
         inv = ~mask
         if bool(inv.any()):
-            loop_w[row[inv]] = w[inv]
+            # the node's LAST existing loop in COO order (an integer max: no racing stores)
+            last = torch.full((n,), -1, dtype=torch.int64, device=dev)
+            last.scatter_reduce_(0, row[inv], torch.nonzero(inv).view(-1), 'amax')
+            has = last >= 0
+            loop_w[has] = w[last[has]]
         out_e.append(torch.cat([edge_index[b][:, mask], torch.stack([ar, ar])], 1))
         out_w.append(torch.cat([w[mask], loop_w]))
     return _per_batch_cat(out_e, out_w)
@@ -68,6 +79,10 @@ def get_rw_adj(edge_index, edge_weight=None, norm_dim=1, fill_value=0.0, num_nod
         edge_weight = torch.ones(B, E, dtype=dtype or torch.float32, device=edge_index.device)
     if fill_value != 0:
         edge_index, edge_weight = add_remaining_self_loops(edge_index, edge_weight, fill_value, n)
+    if edge_index.is_cuda:
+        from . import ops, _lib
+        mode = _lib.NORM_RW_ROW if norm_dim == 0 else _lib.NORM_RW_COL
+        return edge_index, ops.norm_weights(edge_index, edge_weight.float(), n, mode)
     idx = edge_index[:, 0] if norm_dim == 0 else edge_index[:, 1]
     deg = torch.zeros(edge_index.shape[0], n, dtype=edge_weight.dtype, device=edge_weight.device)
     deg.scatter_add_(1, idx, edge_weight)
@@ -83,6 +98,9 @@ def gcn_norm_fill_val(edge_index, edge_weight=None, fill_value=0.0, num_nodes=No
         edge_weight = torch.ones(B, E, dtype=dtype or torch.float32, device=edge_index.device)
     if int(fill_value) != 0:
         edge_index, edge_weight = add_remaining_self_loops(edge_index, edge_weight, fill_value, n)
+    if edge_index.is_cuda:
+        from . import ops, _lib
+        return edge_index, ops.norm_weights(edge_index, edge_weight.float(), n, _lib.NORM_GCN)
     row, col = edge_index[:, 0], edge_index[:, 1]
     deg = torch.zeros(edge_index.shape[0], n, dtype=edge_weight.dtype, device=edge_weight.device)
     deg.scatter_add_(1, col, edge_weight)

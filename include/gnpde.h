@@ -117,6 +117,38 @@ int gnpde_quantile_f32(const float* v, int64_t n, double q, float* out, void* wo
  * reference-mode key sum.                                                   */
 int gnpde_indegree_i32(const int32_t* idx, int64_t nnz, int64_t R, int32_t* deg, void* stream);
 
+/* ---------------------------------------------------------------- graph normalisation
+ * ODEblock.reset_graph_data (src/base_classes.py:70-90) with the intended
+ * semantics of add_remaining_self_loops / get_rw_adj / gcn_norm_fill_val
+ * (src/utils.py:16-42, :215-233, :177-194; pinned by test/test_utils.py:111-161
+ * and test/test_function_laplacian_diffusion.py:56-86), once per graph.
+ *
+ * gnpde_self_loops_count: nonloop[b] = #{e : edge_index[b,0,e] != edge_index[b,1,e]}
+ *   written to HOST memory (SYNCHRONOUS, like gnpde_plan_build).
+ * gnpde_add_self_loops: per batch element, the K non-loop edges in COO order,
+ *   then one loop (n, n) per node n < N whose weight is the weight of the node's
+ *   LAST existing loop in COO order, or `fill` (w NULL: every weight 1).  K must
+ *   be the same for every batch element (the [B,2,K+N] layout); outputs
+ *   ei_out [B,2,K+N] int64, w_out [B,K+N] fp32.
+ * gnpde_norm_weights_f32: fac[r] = deg(r)^-1 (RW_*) or deg^-1/2 with inf -> 0
+ *   (GCN), deg summed sequentially in COO order over the grouped CSR (rowptr,
+ *   perm) of gnpde_csr_build — grouped by source (key_row 0) for RW_ROW, by
+ *   destination (key_row 1) for RW_COL and GCN; then
+ *   RW_ROW: w_out = fac[row] * w,  RW_COL: w_out = w * fac[col],
+ *   GCN:    w_out = fac[row] * w * fac[col]  (fac [B*N] is caller scratch).  */
+#define GNPDE_NORM_RW_ROW 0  /* get_rw_adj(norm_dim=0)        */
+#define GNPDE_NORM_RW_COL 1  /* get_rw_adj(norm_dim=1)        */
+#define GNPDE_NORM_GCN 2     /* gcn_norm_fill_val             */
+size_t gnpde_self_loops_workspace_bytes(int64_t B, int64_t E, int64_t N);
+int gnpde_self_loops_count(const int64_t* edge_index, int64_t B, int64_t E, int64_t* nonloop, void* workspace,
+                           size_t workspace_bytes, void* stream);
+int gnpde_add_self_loops(const int64_t* edge_index, const float* w, int64_t B, int64_t E, int64_t N, float fill,
+                         int64_t K, int64_t* ei_out, float* w_out, void* workspace, size_t workspace_bytes,
+                         void* stream);
+int gnpde_norm_weights_f32(const int64_t* edge_index, const float* w, int64_t B, int64_t E, int64_t N,
+                           const int32_t* rowptr, const int32_t* perm, int mode, float* fac, float* w_out,
+                           void* stream);
+
 /* ---------------------------------------------------------------- work plan
  * Splits rows with more than `chunk` edges into balanced chunks so that one
  * power-law hub does not serialise a wavefront.  items[n_items] is int4
@@ -336,6 +368,22 @@ int gnpde_score_input_grad_f32(const double* gcs, const double* U, const int32_t
  * grouped CSR's order (per-head weights of the per-edge score backward).     */
 int gnpde_gather_head_f32(const float* w, int64_t nnz, int heads, int h, const int32_t* perm, float scale, float* out,
                           void* stream);
+
+/* Backward of the per-edge scores (SCORE_DOT / EXP_KERNEL / COSINE / PEARSON,
+ * function_transformer_attention.py:246-259) onto the projections: over a
+ * grouped CSR whose rows receive the gradient (side 0: the aggregation CSR,
+ * rows = sources, own operand q; side 1: the CSC, rows = destinations, own k;
+ * col = the other endpoint, perm -> COO ids), with gs [E, heads] = dL/ds in
+ * COO order:
+ *   out[r, h*dk + d] = sum_{e in row r} gs[e,h] * ds_e,h / d own[r, h*dk + d]
+ * (out [R, ldo], overwritten; fixed order, deterministic).  For EXP_KERNEL and
+ * gp != NULL also gp[e*2H + h] = gs * ds/d(output_var), gp[e*2H + H + h] =
+ * gs * ds/d(lengthscale) (COO order; the caller sums them).  attention_dim
+ * <= 1024.                                                                   */
+int gnpde_score_grad_f32(const int32_t* rowptr, const int32_t* col, const int32_t* perm, int64_t R, int64_t nnz,
+                         int side, int mode, int64_t heads, int64_t dk, const float* q, const float* k, int64_t ldqk,
+                         float score_p0, float score_p1, const float* gs, float* out, int64_t ldo, float* gp,
+                         void* stream);
 
 #ifdef __cplusplus
 }

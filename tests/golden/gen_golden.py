@@ -269,6 +269,125 @@ def main_blocks():
     print('wrote', len(made), 'fixtures to', OUT_DIR)
 
 
+# --------------------------------------------------------------------------- gradients (torch autograd, fp64)
+def _grads(loss_fn, named):
+    """fp64 autograd gradients of loss_fn() w.r.t. the named leaf tensors."""
+    loss = loss_fn()
+    gs = torch.autograd.grad(loss, [t for _, t in named], allow_unused=True)
+    return {'g_' + n: (np.zeros(tuple(t.shape)) if g is None else g.detach().numpy()) for (n, t), g in zip(named, gs)}
+
+
+def grad_laplacian(name, rng, B, N, E, C, block='constant', heads=4, add_source=False, no_alpha_sigmoid=False,
+                   alpha=0.3, beta=0.7, **gkw):
+    """Gradients of <gout, f> through the reference LaplacianODEFunc.forward
+    (src/function_laplacian_diffusion.py:39-77; the COO -> to_dense -> matmul
+    chain differentiates to the edge weights) w.r.t. x, alpha_train, beta_train
+    and the weights the block hands over (edge_weight [B,E] or attention [B,E,h])."""
+    opt = dict(BASE_OPT, hidden_dim=C, block=block, add_source=add_source, no_alpha_sigmoid=no_alpha_sigmoid,
+               heads=heads)
+    ei = random_graph(rng, B, N, E, **gkw)
+    x = f32(rng.standard_normal((B, N, C)))
+    x0 = f32(rng.standard_normal((B, N, C)))
+    w = f32(rng.uniform(0.05, 1.0, (B, E, heads) if block == 'attention' else (B, E)))
+    gout = f32(rng.standard_normal((B, N, C)))
+    alpha, beta = float(np.float32(alpha)), float(np.float32(beta))
+    func = ref_lap.LaplacianODEFunc(C, C, opt, 'cpu').double()
+    with torch.no_grad():
+        func.alpha_train.fill_(alpha)
+        func.beta_train.fill_(beta)
+    func.edge_index = torch.from_numpy(ei)
+    wt = torch.from_numpy(w).double().requires_grad_(True)
+    if block in ('attention', 'mixed', 'hard_attention'):
+        func.attention_weights = wt
+    else:
+        func.edge_weight = wt
+    func.x0 = torch.from_numpy(x0).double()
+    xt = torch.from_numpy(x).double().requires_grad_(True)
+    go = torch.from_numpy(gout).double()
+    g = _grads(lambda: (func(torch.tensor(0.0), xt) * go).sum(),
+               [('x', xt), ('alpha_train', func.alpha_train), ('beta_train', func.beta_train), ('weights', wt)])
+    meta = dict(kind='laplacian_grad', B=B, N=N, E=E, C=C, block=block, heads=heads, add_source=add_source,
+                no_alpha_sigmoid=no_alpha_sigmoid)
+    np.savez_compressed(os.path.join(OUT_DIR, name + '.npz'), meta=json.dumps(meta), edge_index=ei, x=x, x0=x0,
+                        weights=w, alpha_train=f32(alpha), beta_train=f32(beta), gout=gout, **g)
+    return name
+
+
+def grad_transformer(name, rng, B, N, E, C, heads, att_dim, norm_idx, attention_type='scaled_dot', add_source=False,
+                     no_alpha_sigmoid=False, alpha=0.2, beta=0.5, wstd=0.1, **gkw):
+    """Gradients of <gout, f> through the reference ODEFuncTransformerAtt.forward
+    (src/function_transformer_attention.py:44-59, 218-267: Q/K projections,
+    the score, utils.softmax, the head-mean aggregation) w.r.t. x, alpha_train,
+    beta_train, Q.weight, Q.bias, K.weight, K.bias (+ output_var, lengthscale
+    for exp_kernel)."""
+    opt = dict(BASE_OPT, hidden_dim=C, heads=heads, attention_dim=att_dim, attention_norm_idx=norm_idx,
+               attention_type=attention_type, add_source=add_source, no_alpha_sigmoid=no_alpha_sigmoid,
+               function='transformer')
+    ei = random_graph(rng, B, N, E, **gkw)
+    x = f32(rng.standard_normal((B, N, C)))
+    x0 = f32(rng.standard_normal((B, N, C)))
+    Wq = f32(rng.standard_normal((att_dim, C)) * wstd)
+    bq = f32(rng.standard_normal((att_dim,)) * wstd)
+    Wk = f32(rng.standard_normal((att_dim, C)) * wstd)
+    bk = f32(rng.standard_normal((att_dim,)) * wstd)
+    gout = f32(rng.standard_normal((B, N, C)))
+    alpha, beta = float(np.float32(alpha)), float(np.float32(beta))
+    func = ref_att.ODEFuncTransformerAtt(C, C, opt, 'cpu').double()
+    lay = func.multihead_att_layer
+    with torch.no_grad():
+        func.alpha_train.fill_(alpha)
+        func.beta_train.fill_(beta)
+        lay.Q.weight.copy_(torch.from_numpy(Wq))
+        lay.Q.bias.copy_(torch.from_numpy(bq))
+        lay.K.weight.copy_(torch.from_numpy(Wk))
+        lay.K.bias.copy_(torch.from_numpy(bk))
+        if attention_type == 'exp_kernel':
+            lay.output_var.fill_(float(np.float32(1.3)))
+            lay.lengthscale.fill_(float(np.float32(0.8)))
+    func.edge_index = torch.from_numpy(ei)
+    func.x0 = torch.from_numpy(x0).double()
+    func.y = None
+    xt = torch.from_numpy(x).double().requires_grad_(True)
+    go = torch.from_numpy(gout).double()
+    named = [('x', xt), ('alpha_train', func.alpha_train), ('beta_train', func.beta_train), ('Wq', lay.Q.weight),
+             ('bq', lay.Q.bias), ('Wk', lay.K.weight), ('bk', lay.K.bias)]
+    if attention_type == 'exp_kernel':
+        named += [('output_var', lay.output_var), ('lengthscale', lay.lengthscale)]
+    g = _grads(lambda: (func(torch.tensor(0.0), xt) * go).sum(), named)
+    meta = dict(kind='transformer_grad', B=B, N=N, E=E, C=C, heads=heads, attention_dim=att_dim,
+                attention_norm_idx=norm_idx, attention_type=attention_type, add_source=add_source,
+                no_alpha_sigmoid=no_alpha_sigmoid,
+                output_var=float(np.float32(1.3)) if attention_type == 'exp_kernel' else None,
+                lengthscale=float(np.float32(0.8)) if attention_type == 'exp_kernel' else None)
+    np.savez_compressed(os.path.join(OUT_DIR, name + '.npz'), meta=json.dumps(meta), edge_index=ei, x=x, x0=x0,
+                        Wq=Wq, bq=bq, Wk=Wk, bk=bk, alpha_train=f32(alpha), beta_train=f32(beta), gout=gout, **g)
+    return name
+
+
+def main_grads():
+    """Reference autograd gradient fixtures (separate seed: earlier fixtures untouched)."""
+    rng = np.random.default_rng(20250119)
+    made = [grad_laplacian('grad_lap_const_b1', rng, 1, 60, 300, 8),
+            grad_laplacian('grad_lap_const_b2_src', rng, 2, 40, 160, 6, add_source=True, no_alpha_sigmoid=True,
+                           alpha=-0.4, beta=0.9),
+            grad_laplacian('grad_lap_attn_mean_b2', rng, 2, 50, 260, 16, block='attention', heads=4),
+            grad_laplacian('grad_lap_mixed_b1', rng, 1, 80, 420, 12, block='mixed')]
+    made += [grad_transformer('grad_att_sd_n1_h2', rng, 1, 60, 320, 12, 2, 16, 1),
+             grad_transformer('grad_att_sd_n0_h2', rng, 1, 60, 320, 12, 2, 16, 0),
+             grad_transformer('grad_att_sd_n1_h8_b2', rng, 2, 40, 200, 16, 8, 32, 1, wstd=0.1),
+             grad_transformer('grad_att_sd_n1_src', rng, 1, 50, 260, 10, 2, 8, 1, add_source=True,
+                              no_alpha_sigmoid=True, alpha=0.8, beta=-0.3)]
+    for st in ('exp_kernel', 'cosine_sim', 'pearson'):
+        for ni in (0, 1):
+            made.append(grad_transformer('grad_att_%s_n%d' % (st, ni), rng, 2, 40, 200, 10, 2, 8, ni,
+                                         attention_type=st, wstd=0.3))
+    path = os.path.join(OUT_DIR, 'MANIFEST.json')
+    have = json.load(open(path))
+    with open(path, 'w') as fh:
+        json.dump(sorted(set(have) | set(made)), fh, indent=1)
+    print('wrote', len(made), 'fixtures to', OUT_DIR)
+
+
 def main():
     rng = np.random.default_rng(20250117)
     made = []
@@ -315,5 +434,7 @@ def main():
 if __name__ == '__main__':
     if len(sys.argv) > 1 and sys.argv[1] == 'blocks':
         main_blocks()
+    elif len(sys.argv) > 1 and sys.argv[1] == 'grads':
+        main_grads()
     else:
         main()

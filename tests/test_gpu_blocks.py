@@ -198,3 +198,33 @@ def test_add_source_new_x0_each_forward_replays_with_new_x0():
     xn, x0n = x.cpu().numpy(), x0b.cpu().numpy()
     f = lambda t, y: O.laplacian_rhs(eo, y, x0n, 0.0, 0.5, edge_weight=wo, add_source=True)  # noqa: E731
     assert rel(z, O.odeint_fixed(f, xn, 0.0, 1.0, 'rk4', 0.125)) <= RTOL
+
+
+@pytest.mark.parametrize("fn,kw", [("get_rw_adj", dict(norm_dim=1)), ("get_rw_adj", dict(norm_dim=0)),
+                                   ("gcn_norm_fill_val", {})])
+@pytest.mark.parametrize("weighted", [False, True])
+def test_graph_normalisation_kernels_bit_exact_vs_host(fn, kw, weighted):
+    """csrc/prep.hip (self loops + rw / gcn weights) equals the host restatement
+    in gnpde.utils bit for bit: same edge order, the node's last existing loop
+    weight, degrees added in COO order (= torch's CPU scatter_add_); and the
+    fp64 oracle within fp32 rounding.  Batched, duplicated edges, repeated
+    loops on one node, an isolated node."""
+    from gnpde import utils as gu
+    rng = np.random.default_rng(107)
+    B, N, E = 2, 500, 4000
+    ei = rng.integers(0, N - 1, size=(B, 2, E))  # node N-1 isolated
+    ei[:, 0, :30] = 4
+    ei[:, 1, :30] = 4  # 30 loops on node 4 with different weights: the last one wins
+    ei[:, :, 100:200] = ei[:, :, 200:300]  # duplicates
+    w = rng.uniform(0.1, 2.0, size=(B, E)).astype(np.float32) if weighted else None
+    args = dict(fill_value=1.5, num_nodes=N, **kw)
+    ge, gw = getattr(gu, fn)(T(ei), edge_weight=None if w is None else T(w), **args)
+    he, hw = getattr(gu, fn)(torch.from_numpy(ei), edge_weight=None if w is None else torch.from_numpy(w), **args)
+    assert torch.equal(ge.cpu(), he)
+    assert torch.equal(gw.cpu(), hw), float((gw.cpu() - hw).abs().max())
+    ge2, gw2 = getattr(gu, fn)(T(ei), edge_weight=None if w is None else T(w), **args)
+    assert torch.equal(gw2, gw)
+    oe, ow = getattr(O, fn)(ei, edge_weight=w, **args)
+    assert np.array_equal(ge.cpu().numpy(), np.stack(oe, 0))
+    ow = np.stack(ow, 0)
+    assert np.abs(gw.double().cpu().numpy() - ow).max() <= 1e-6 * np.abs(ow).max()

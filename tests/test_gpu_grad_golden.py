@@ -1,0 +1,107 @@
+"""GPU: gradients of the RHS through the HIP backward against the REFERENCE's
+own fp64 autograd (tests/golden/grad_*.npz, written by
+tests/golden/gen_golden.py grads from src/function_laplacian_diffusion.py and
+src/function_transformer_attention.py).
+
+d <gout, f> / d (x, alpha_train, beta_train, the block's edge weights or the
+attention's Q / K parameters [, output_var, lengthscale]), for the Laplacian
+RHS (constant / attention-mean / mixed weights, add_source, no_alpha_sigmoid)
+and the transformer RHS (the fork's scaled_dot under norm_idx 0 and 1,
+exp_kernel, cosine_sim, pearson).
+
+Tolerance: max |g - g_ref| <= 1e-4 * max |g_ref| per gradient (fp32 backward
+against fp64 autograd; the chains are 3-6 sums deep), with gradients the
+reference leaves at rounding level (the fork's scaled_dot under source-grouped
+softmax cannot move the attention) compared against 1e-6 of the
+x-gradient's scale instead."""
+import glob
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import gnpde
+from conftest import GOLDEN
+from test_gpu_parity import DEV, OPT, T
+
+pytestmark = pytest.mark.gpu
+GRAD_RTOL = 1e-4
+FIX = sorted(glob.glob(os.path.join(GOLDEN, "grad_*.npz")))
+
+
+def _load(path):
+    d = np.load(path, allow_pickle=False)
+    return d, json.loads(str(d["meta"]))
+
+
+def _check(name, got, want, scale):
+    got = np.zeros_like(want) if got is None else got.detach().double().cpu().numpy().reshape(want.shape)
+    err = np.abs(got - want).max() if want.size else 0.0
+    ref = max(np.abs(want).max() if want.size else 0.0, 1e-6 * scale)
+    assert err <= GRAD_RTOL * ref, "%s: max err %.3e vs max |g_ref| %.3e" % (name, err, ref)
+
+
+@pytest.mark.parametrize("path", [p for p in FIX if os.path.basename(p).startswith("grad_lap_")],
+                         ids=os.path.basename)
+def test_laplacian_grad_golden(path):
+    d, m = _load(path)
+    C = m["C"]
+    opt = dict(OPT, hidden_dim=C, block=m["block"], add_source=m["add_source"], no_alpha_sigmoid=m["no_alpha_sigmoid"],
+               heads=m["heads"])
+    func = gnpde.LaplacianODEFunc(C, C, opt, DEV).to(DEV)
+    with torch.no_grad():
+        func.alpha_train.fill_(float(d["alpha_train"]))
+        func.beta_train.fill_(float(d["beta_train"]))
+    func.edge_index = T(d["edge_index"])
+    w = T(d["weights"]).requires_grad_(True)
+    if m["block"] == "constant":
+        func.edge_weight = w
+    else:
+        func.attention_weights = w
+    func.x0 = T(d["x0"])
+    x = T(d["x"]).requires_grad_(True)
+    f = func(torch.tensor(0.0), x)
+    (f * T(d["gout"])).sum().backward()
+    scale = np.abs(d["g_x"]).max()
+    _check("x", x.grad, d["g_x"], scale)
+    _check("alpha_train", func.alpha_train.grad, d["g_alpha_train"], scale)
+    _check("beta_train", func.beta_train.grad, d["g_beta_train"], scale)
+    _check("weights", w.grad, d["g_weights"], scale)
+
+
+@pytest.mark.parametrize("path", [p for p in FIX if os.path.basename(p).startswith("grad_att_")],
+                         ids=os.path.basename)
+def test_transformer_grad_golden(path):
+    d, m = _load(path)
+    C = m["C"]
+    opt = dict(OPT, hidden_dim=C, heads=m["heads"], attention_dim=m["attention_dim"],
+               attention_norm_idx=m["attention_norm_idx"], attention_type=m["attention_type"],
+               add_source=m["add_source"], no_alpha_sigmoid=m["no_alpha_sigmoid"], function='transformer')
+    func = gnpde.ODEFuncTransformerAtt(C, C, opt, DEV).to(DEV)
+    lay = func.multihead_att_layer
+    with torch.no_grad():
+        func.alpha_train.fill_(float(d["alpha_train"]))
+        func.beta_train.fill_(float(d["beta_train"]))
+        lay.Q.weight.copy_(T(d["Wq"]))
+        lay.Q.bias.copy_(T(d["bq"]))
+        lay.K.weight.copy_(T(d["Wk"]))
+        lay.K.bias.copy_(T(d["bk"]))
+        if m["attention_type"] == "exp_kernel":
+            lay.output_var.fill_(m["output_var"])
+            lay.lengthscale.fill_(m["lengthscale"])
+    func.edge_index = T(d["edge_index"])
+    func.x0 = T(d["x0"])
+    x = T(d["x"]).requires_grad_(True)
+    f = func(torch.tensor(0.0), x)
+    (f * T(d["gout"])).sum().backward()
+    scale = np.abs(d["g_x"]).max()
+    _check("x", x.grad, d["g_x"], scale)
+    _check("alpha_train", func.alpha_train.grad, d["g_alpha_train"], scale)
+    _check("beta_train", func.beta_train.grad, d["g_beta_train"], scale)
+    for name, p in (("Wq", lay.Q.weight), ("bq", lay.Q.bias), ("Wk", lay.K.weight), ("bk", lay.K.bias)):
+        _check(name, p.grad, d["g_" + name], scale)
+    if m["attention_type"] == "exp_kernel":
+        _check("output_var", lay.output_var.grad, d["g_output_var"], scale)
+        _check("lengthscale", lay.lengthscale.grad, d["g_lengthscale"], scale)

