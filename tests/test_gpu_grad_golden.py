@@ -9,11 +9,14 @@ RHS (constant / attention-mean / mixed weights, add_source, no_alpha_sigmoid)
 and the transformer RHS (the fork's scaled_dot under norm_idx 0 and 1,
 exp_kernel, cosine_sim, pearson).
 
-Tolerance: max |g - g_ref| <= 1e-4 * max |g_ref| per gradient (fp32 backward
-against fp64 autograd; the chains are 3-6 sums deep), with gradients the
-reference leaves at rounding level (the fork's scaled_dot under source-grouped
-softmax cannot move the attention) compared against 1e-6 of the
-x-gradient's scale instead."""
+Tolerance: max |g - g_ref| <= max(1e-4 * max |g_ref|, 1e-6 * S) per gradient,
+S = the largest reference gradient of the case (fp32 backward against fp64
+autograd; the chains are 3-6 sums deep).  The second term covers gradients
+that vanish analytically and that the reference leaves at fp64 rounding
+level: the fork's scaled_dot under source-grouped softmax cannot move the
+attention, and under destination-grouped softmax d/d bq =
+S/sqrt(dk) * sum_e g_s[e], where every softmax group's g_s sums to
+(1 - sum att) * ... ~ 0 — fp32 gives the cancellation's rounding instead."""
 import glob
 import json
 import os
@@ -36,11 +39,15 @@ def _load(path):
     return d, json.loads(str(d["meta"]))
 
 
+def _case_scale(d):
+    return max(float(np.abs(d[k]).max()) for k in d.files if k.startswith("g_") and d[k].size)
+
+
 def _check(name, got, want, scale):
     got = np.zeros_like(want) if got is None else got.detach().double().cpu().numpy().reshape(want.shape)
     err = np.abs(got - want).max() if want.size else 0.0
-    ref = max(np.abs(want).max() if want.size else 0.0, 1e-6 * scale)
-    assert err <= GRAD_RTOL * ref, "%s: max err %.3e vs max |g_ref| %.3e" % (name, err, ref)
+    tol = max(GRAD_RTOL * (np.abs(want).max() if want.size else 0.0), 1e-6 * scale)
+    assert err <= tol, "%s: max err %.3e, tolerance %.3e" % (name, err, tol)
 
 
 @pytest.mark.parametrize("path", [p for p in FIX if os.path.basename(p).startswith("grad_lap_")],
@@ -64,7 +71,7 @@ def test_laplacian_grad_golden(path):
     x = T(d["x"]).requires_grad_(True)
     f = func(torch.tensor(0.0), x)
     (f * T(d["gout"])).sum().backward()
-    scale = np.abs(d["g_x"]).max()
+    scale = _case_scale(d)
     _check("x", x.grad, d["g_x"], scale)
     _check("alpha_train", func.alpha_train.grad, d["g_alpha_train"], scale)
     _check("beta_train", func.beta_train.grad, d["g_beta_train"], scale)
@@ -96,7 +103,7 @@ def test_transformer_grad_golden(path):
     x = T(d["x"]).requires_grad_(True)
     f = func(torch.tensor(0.0), x)
     (f * T(d["gout"])).sum().backward()
-    scale = np.abs(d["g_x"]).max()
+    scale = _case_scale(d)
     _check("x", x.grad, d["g_x"], scale)
     _check("alpha_train", func.alpha_train.grad, d["g_alpha_train"], scale)
     _check("beta_train", func.beta_train.grad, d["g_beta_train"], scale)
