@@ -22,3 +22,10 @@ __version__ = "0.1.0"
 
 def native_library_path():
     return _lib.LIB_PATH
+
+
+def build_info():
+    """Loaded library path, the source hash compiled into it and whether it
+    matches the sources of this tree."""
+    lib, src = _lib.build_id(), _lib.source_hash()
+    return {"library": _lib.LIB_PATH, "build_id": lib, "source_hash": src, "fresh": lib == src}

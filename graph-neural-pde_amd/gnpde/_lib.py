@@ -41,6 +41,7 @@ _size = ctypes.c_size_t
 SIGNATURES = {
     "gnpde_abi_version": (_int, []),
     "gnpde_last_error": (ctypes.c_char_p, []),
+    "gnpde_build_id": (ctypes.c_char_p, []),
     "gnpde_csr_workspace_bytes": (_size, [_i64, _i64, _i64]),
     "gnpde_csr_build": (_int, [_vp, _i64, _i64, _i64, _int, _vp, _vp, _vp, _vp, _size, _vp]),
     "gnpde_gather_weights_f32": (_int, [_vp, _i64, _int, _vp, _vp, _vp]),
@@ -116,6 +117,20 @@ _lib = None
 
 class GnpdeError(RuntimeError):
     pass
+
+
+def build_id():
+    """Source hash compiled into the loaded library (gnpde_build_id)."""
+    return load().gnpde_build_id().decode()
+
+
+def source_hash():
+    """Hash of the csrc/ sources and include/gnpde.h of this tree (srchash.py)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("gnpde_srchash", os.path.join(os.path.dirname(_HERE), "srchash.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod.source_hash()
 
 
 def load():

@@ -64,6 +64,24 @@ class Plan(object):
         self.items, self.heavy = items, heavy
         self.n_items, self.n_heavy, self.n_slots = n_items, n_heavy, n_slots
         self.chunk = chunk
+        self.last_stream = None
+
+    def order_launch(self, dev):
+        """K1 combines hub rows inside the launch through arrival tickets kept in
+        this plan (heavy[].w, include/gnpde.h), so two launches on one plan must
+        never overlap.  A launch on a different stream than the plan's previous
+        one first waits for everything already queued on that stream (an event;
+        free for the usual single-stream use).  During graph capture the capture
+        itself orders the launches."""
+        if self.n_heavy == 0:
+            return
+        s = torch.cuda.current_stream(dev)
+        last = self.last_stream
+        if last is not None and last != s and not torch.cuda.is_current_stream_capturing():
+            ev = torch.cuda.Event()
+            ev.record(last)
+            s.wait_event(ev)
+        self.last_stream = s
 
 
 class GroupedCSR(object):
@@ -456,6 +474,7 @@ def spmm_rhs(g, w_csr, x, x0=None, alpha=None, beta=None, rhs=True, alpha_sigmoi
     grouped = g.csc if transpose else g.csr
     plan = grouped.plan
     partials = _partials(plan, C, dev)
+    plan.order_launch(dev)
     epi = (C, _ptr(xr), C, _ptr(x0r), C, _ptr(a), _ptr(b), _flags(rhs, alpha_sigmoid, add_source), _ptr(out), C,
            _ptr(partials), st, _stream(dev))
     if dt == torch.bfloat16:
@@ -523,6 +542,7 @@ def spmm_rhs_rows(g, plan, w_csr, x_src, x_rows, row0, x0=None, alpha=None, beta
     elif out is None:
         out = torch.empty_like(xl)
     partials = _partials(plan, C, dev)
+    plan.order_launch(dev)
     _lib.call("gnpde_spmm_rhs_f32", _ptr(plan.items), plan.n_items, _ptr(plan.heavy), plan.n_heavy,
               _ptr(g.csr.col if col is None else col),
               _ptr(w_csr), C, _ptr(xs), C, sp(x0r), C, _ptr(a), _ptr(b), _flags(True, alpha_sigmoid, add_source),

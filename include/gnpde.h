@@ -69,6 +69,8 @@ extern "C" {
 
 int gnpde_abi_version(void);
 const char* gnpde_last_error(void);
+/* Hash of the sources the library was built from (graph-neural-pde_amd/srchash.py). */
+const char* gnpde_build_id(void);
 
 /* ---------------------------------------------------------------- graph build
  * COO edge_index [B,2,E] (int64, values in [0,N) — caller-validated) -> CSR

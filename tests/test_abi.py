@@ -38,6 +38,13 @@ def test_binding_covers_every_declared_symbol():
     assert sorted(_lib.SIGNATURES) == declared_symbols()
 
 
+def test_library_built_from_these_sources():
+    """The in-tree libgnpde.so carries the hash of the csrc/ sources it was built
+    from (gnpde_build_id); it must be this tree's."""
+    info = gnpde.build_info()
+    assert info["fresh"], info
+
+
 def test_abi_version():
     assert _lib.load().gnpde_abi_version() == _lib.ABI_VERSION == 1
 

@@ -230,3 +230,31 @@ def test_graph_normalisation_kernels_bit_exact_vs_host(fn, kw, weighted):
     assert np.array_equal(ge.cpu().numpy(), np.stack(oe, 0))
     ow = np.stack(ow, 0)
     assert np.abs(gw.double().cpu().numpy() - ow).max() <= 1e-6 * np.abs(ow).max()
+
+
+def test_k1_launches_on_two_streams_share_a_plan_safely():
+    """the hub arrival tickets live in the plan, so launches on one
+    plan must not overlap; ops orders a launch on another stream behind the
+    plan's previous stream.  Alternating streams, results stay bit-identical to
+    a single-stream run."""
+    from gnpde import ops
+    N, E, C = 4000, 60000, 128
+    ei, rng = _graph(N, E, 108)
+    ei[0, 0, :20000] = rng.integers(0, 12, 20000)  # many hub rows
+    g = ops.GraphCSR(T(ei), N)
+    assert g.csr.plan.n_heavy >= 10
+    w = g.gather_weights(T(rng.uniform(0.1, 1, size=(1, E)).astype(np.float32)))
+    xs = [torch.randn(N, C, device=DEV) for _ in range(6)]
+    alpha = torch.tensor(0.3, device=DEV)
+    want = [ops.spmm_rhs(g, w, x, alpha=alpha) for x in xs]
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    got = []
+    for rep in range(4):
+        for i, x in enumerate(xs):
+            with torch.cuda.stream(streams[i % 2]):
+                got.append((i, ops.spmm_rhs(g, w, x, alpha=alpha)))
+    torch.cuda.synchronize()
+    for i, f in got:
+        assert torch.equal(f, want[i])
+    assert int(g.csr.plan.heavy.view(-1, 4)[:g.csr.plan.n_heavy, 3].abs().sum()) == 0  # tickets back to 0
