@@ -1,0 +1,26 @@
+#!/bin/bash
+# Round-2 profile session: kernel trace + stats of the full bench, PMC passes
+# (FETCH_SIZE, WRITE_SIZE separately) over K1 and the attention kernels, and the
+# column-stripe per-rank widths (both narrow geometries).
+set -u
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+TAG=${TAG:-r02a}
+OUT=$R/gpurun_out
+mkdir -p $OUT
+cd /tmp && export TMPDIR=/tmp
+fatal() { case "$1" in 124|134|137|139) return 0;; *) return 1;; esac; }
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_${TAG}_trace -o run -- \
+  python3 $R/bench.py --no-cpu-baseline > $OUT/prof_${TAG}_trace.log 2>&1
+rc=$?; echo "trace rc=$rc"; tail -c 600 $OUT/prof_${TAG}_trace.log; echo; if fatal $rc; then exit $rc; fi
+KRE='agg_kernel|keysum|node_scores|seg_softmax|linear_mfma|stats_|attn_'
+for ctr in FETCH_SIZE WRITE_SIZE; do
+  timeout -k 10 300 rocprofv3 --pmc $ctr --kernel-include-regex "$KRE" --output-format csv \
+    -d $OUT/prof_${TAG}_pmc_$ctr -o run -- python3 $R/bench.py --no-cpu-baseline --no-grmat --steps 5 --warmup 2 \
+    --rhs-plain-reps 5 > $OUT/prof_${TAG}_pmc_$ctr.log 2>&1
+  rc=$?; echo "pmc $ctr rc=$rc"; if fatal $rc; then exit $rc; fi
+done
+cd $R
+for v in 0 5; do
+  GNPDE_AGG_VARIANT=$v timeout -k 10 300 python3 tools/stripe_bench.py > $OUT/stripe_v$v.log 2>&1
+  rc=$?; echo "stripe v$v rc=$rc"; cat $OUT/stripe_v$v.log | grep '^{'; if fatal $rc; then exit $rc; fi
+done
