@@ -405,13 +405,31 @@ static int launch_agg_vec(const int4* items, int64_t n_items, int4* heavy, int64
   launch_agg_cfg<VEC, GL, NCH, U, RPW, WP, T>(items, n_items, heavy, n_heavy, col, wp, C, ep, partials, s)
   // Narrow rows (the column stripes of gnpde.dist at 2-8 GPUs: G-arxiv C = 128 / 8 = 16
   // floats = 4 lanes; G-rmat 256 / 8 = 32 floats = 8 lanes): several rows per
-  // wavefront, 2 edges side by side per row slot, 4 in flight per edge group, so a
-  // wavefront keeps 8 gathers in flight for each of its 2-8 rows instead of idling
-  // 3/4 of a 16-lane group (GNPDE_AGG_VARIANT=5: the previous one-row geometry).
-  if (agg_variant() != 5) {
-    if (lanes <= 4) return GNPDE_AGG(4, 1, 4, 8);
-    if (lanes <= 8) return GNPDE_AGG(8, 1, 4, 4);
-    if (lanes <= 16) return GNPDE_AGG(16, 1, 4, 2);
+  // wavefront with 2-4 edges side by side per row slot, instead of one row per
+  // wavefront idling 3/4 of a 16-lane group (GNPDE_AGG_VARIANT=5).  G-arxiv rk4
+  // step at 16 / 32 / 64 columns: 0.133 / 0.152 / 0.243 ms against 0.266 / 0.270 /
+  // 0.296 with the one-row geometry (tools/stripe_sweep.sh).
+  switch (agg_variant()) {
+    case 5: break;  // the previous one-row geometry below
+    case 6:         // twice the gathers in flight per edge group
+      if (lanes <= 4) return GNPDE_AGG(4, 1, 8, 8);
+      if (lanes <= 8) return GNPDE_AGG(8, 1, 8, 4);
+      if (lanes <= 16) return GNPDE_AGG(16, 1, 8, 2);
+      break;
+    case 7:         // twice the rows per wavefront, one edge group per row
+      if (lanes <= 4) return GNPDE_AGG(4, 1, 4, 16);
+      if (lanes <= 8) return GNPDE_AGG(8, 1, 4, 8);
+      if (lanes <= 16) return GNPDE_AGG(16, 1, 4, 4);
+      break;
+    case 8:         // half the rows per wavefront, four edge groups per row
+      if (lanes <= 4) return GNPDE_AGG(4, 1, 4, 4);
+      if (lanes <= 8) return GNPDE_AGG(8, 1, 4, 2);
+      if (lanes <= 16) return GNPDE_AGG(16, 1, 4, 1);
+      break;
+    default:  // per width, the fastest of variants 0/6/7/8 (profiles/r02b_stripe_sweep.jsonl)
+      if (lanes <= 4) return GNPDE_AGG(4, 1, 4, 4);
+      if (lanes <= 8) return GNPDE_AGG(8, 1, 8, 4);
+      if (lanes <= 16) return GNPDE_AGG(16, 1, 4, 2);
   }
   if (lanes <= 16) return GNPDE_AGG(16, 1, 4, 1);
   if (lanes <= 32) {
