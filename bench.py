@@ -310,11 +310,11 @@ def bench_single(args, world, rank, dev):
 METRIC = "ODE RHS evals/s (and ms/step) at |E|≈1.2M, d=128; achieved HBM GB/s vs roofline"
 
 
-def traffic_bytes(N, E, C, which):
+def traffic_bytes(N, E, C, which, name="k1_traffic.json"):
     """Measured HBM bytes per K1 launch (PMC: 2*FETCH_SIZE + WRITE_SIZE with the
-    gfx950 corrections of MI355X_MICROARCH.md §HBM) from profiles/k1_traffic.json,
-    when that file was collected on this graph shape."""
-    tp = os.path.join(ROOT, "profiles", "k1_traffic.json")
+    gfx950 corrections of MI355X_MICROARCH.md §HBM) from profiles/<name>, when
+    that file was collected on this graph shape."""
+    tp = os.path.join(ROOT, "profiles", name)
     if not os.path.exists(tp):
         return None
     with open(tp) as fh:
@@ -420,10 +420,13 @@ def bench_grmat(args, world, rank, dev):
         func = gnpde.LaplacianODEFunc(C, C, dict(LAP_OPT, hidden_dim=C), dev).to(dev)
         func.edge_index, func.edge_weight = ei, w
         el, _ = timed_solve(func, x, args.grmat_steps, 1, h, dev, world)
-        nb = rk4_fused_step_bytes(N, E, C)
+        launch_ms = el * 1e3 / args.grmat_steps / 4  # a replayed step is its 4 K1 launches back to back
+        rl = roofline(launch_ms, rk4_fused_step_bytes(N, E, C) / 4.0, traffic_bytes(N, E, C, "fused_step_launch",
+                                                                                       "k1_traffic_grmat.json"),
+                      "agg_kernel<4,64,1,4,1,1,PlainWeights,float>: K1 with fused rk4 stage, one row per wavefront")
+        rl["launch_ms"] = round(launch_ms, 4)
         out["one_gpu"] = {"value": round(args.grmat_steps * 4 / el, 2), "unit": "RHS evals/s",
-                          "ms_per_step": round(el * 1e3 / args.grmat_steps, 4),
-                          "algorithmic_GBs": round(nb / (el / args.grmat_steps) / 1e9, 1)}
+                          "ms_per_step": round(el * 1e3 / args.grmat_steps, 4), "roofline": rl}
         del func, x, ei, w
         torch.cuda.empty_cache()
         return out

@@ -22,10 +22,14 @@ from . import _lib
 # 384 -> 8,434-8,450 RHS/s (in row order 128 was best: 121 against 128 us per RHS)
 DEFAULT_CHUNK = int(os.environ.get("GNPDE_CHUNK", 256))
 STATS_CHUNK = 64     # items of the softmax-statistics kernel (8 lanes per item)
-# K1 work items longest first ("lpt", stable; A/B on G-arxiv rk4: 8,130-8,205 against 7,917-7,932
-# RHS/s in row order; BLEND step 0.585 against 0.650 ms fp32, 0.434 against 0.565 ms bf16).
-# GNPDE_PLAN_ORDER=rows keeps the builder's row order.  Results do not depend on it.
-PLAN_ORDER = os.environ.get("GNPDE_PLAN_ORDER", "lpt")
+# K1 work items ordered by power-of-two length class, longest first, row order inside a class
+# ("classes", the default since round 2: tools/stripe_sweep2.sh, profiles/r02c_plan_order_sweep.jsonl —
+# rk4 step G-arxiv C = 128 / 16: 0.429 / 0.121 ms against 0.435 / 0.128 with a plain longest-first
+# sort ("lpt", round 1: 8,130-8,205 against 7,917-7,932 RHS/s in row order), G-rmat at 32 columns
+# 2.59 against 2.63 ms).
+# GNPDE_PLAN_ORDER=rows keeps the builder's row order; =classes sorts by power-of-two length class
+# only (row order inside a class); =hubs puts the hub chunks first.  Results do not depend on it.
+PLAN_ORDER = os.environ.get("GNPDE_PLAN_ORDER", "classes")
 
 
 def _ptr(t):
@@ -140,10 +144,18 @@ def build_plan(rowptr, R, nnz, chunk=DEFAULT_CHUNK):
     n_it, n_hv, n_sl = ctypes.c_int64(0), ctypes.c_int64(0), ctypes.c_int64(0)
     _lib.call("gnpde_plan_build", _ptr(rowptr), R, chunk, _ptr(items), cap_items, _ptr(heavy), cap_heavy,
               ctypes.byref(n_it), ctypes.byref(n_hv), ctypes.byref(n_sl), _ptr(ws), ws_bytes, _stream(dev))
-    if PLAN_ORDER == "lpt" and n_it.value > 1:
-        # longest items first (stable): the wavefronts dispatched last are the short ones
+    if PLAN_ORDER != "rows" and n_it.value > 1:
         it = items[:n_it.value * 4].view(-1, 4)
-        order = torch.argsort(it[:, 1] - it[:, 2], stable=True)
+        ln = (it[:, 2] - it[:, 1]).long()
+        if PLAN_ORDER == "classes":
+            # length classes (powers of two) longest first, row order inside a class: the
+            # wavefronts dispatched last are short, and neighbouring items touch neighbouring rows
+            key = -torch.floor(torch.log2(ln.clamp(min=1).double())).long()
+        elif PLAN_ORDER == "hubs":
+            key = (it[:, 3] < 0).long()  # hub chunks first, then every row in row order
+        else:
+            key = -ln  # longest items first (stable): the wavefronts dispatched last are the short ones
+        order = torch.argsort(key, stable=True)
         it.copy_(it[order])
     return Plan(items, heavy, n_it.value, n_hv.value, n_sl.value, chunk)
 
