@@ -84,6 +84,11 @@ struct RefDstSoftmaxWeights {
 };
 
 // ------------------------------------------------------------------ hub rows
+// Lane groups of the hub combine are powers of two (an xor tree joins them):
+// a geometry with GL = 21 lanes per row (three bf16 rows of 168 columns per
+// wavefront) combines its hub rows with 32-lane groups.
+constexpr int pow2_ceil(int v) { return v <= 1 ? 1 : 2 * pow2_ceil((v + 1) / 2); }
+
 // Sum the nch chunk partials of hub row `row` (slots first .. first+nch-1), then
 // run the epilogue.  GL lanes cover the columns; the 64/GL lane groups take
 // chunks g, g+G, ... and are combined by a fixed xor tree (deterministic).
@@ -146,7 +151,7 @@ __device__ __forceinline__ void hub_arrive(int4* heavy, int n_heavy, int slot, i
   ticket = __shfl(ticket, 0);
   if (ticket != nch - 1) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  hub_combine<VEC, GL, STG, T>(row, first, nch, C, ep, partials);
+  hub_combine<VEC, pow2_ceil(GL), STG, T>(row, first, nch, C, ep, partials);
   if ((threadIdx.x & 63) == 0) __hip_atomic_store(ticket_word, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -181,7 +186,7 @@ __device__ __forceinline__ void hub_arrive_slots(int4* heavy, int n_heavy, bool 
       const int h = __shfl(lo, s * SL);
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       const int4 hv = heavy[h];
-      hub_combine<VEC, GL, STG, T>(uniform(hv.x), uniform(hv.y), uniform(hv.z), C, ep, partials);
+      hub_combine<VEC, pow2_ceil(GL), STG, T>(uniform(hv.x), uniform(hv.y), uniform(hv.z), C, ep, partials);
       if (lane == 0) __hip_atomic_store(&heavy[h].w, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
@@ -202,6 +207,7 @@ __global__ __launch_bounds__(256) void agg_kernel(const int4* __restrict__ items
                                                    float* __restrict__ partials) {
   constexpr int SL = kWave / RPW;
   constexpr int G = SL / GL;
+  static_assert((SL & (SL - 1)) == 0 || G == 1, "non-power-of-two row slots hold one edge group");
   constexpr bool PRE = NCH <= 2;
   const int lane = threadIdx.x & 63;
   const int rs = lane / SL, sl = lane % SL;
@@ -209,7 +215,8 @@ __global__ __launch_bounds__(256) void agg_kernel(const int4* __restrict__ items
   const int wid = uniform(xcd_block(ep.xcd_remap) * kWavesPerBlock + (threadIdx.x >> 6));
   const int item = wid * RPW + rs;
   if (wid * RPW >= n_items) return;
-  const bool live = item < n_items;
+  // RPW = 3 (SL = 21): lane 63 is in no slot
+  const bool live = item < n_items && rs < RPW;
   const int4 it = live ? items[item] : make_int4(0, 0, 0, -1);
   const int row = it.x, beg = it.y, end = it.z, slot = it.w;
   const bool owner = live && slot < 0 && g == 0;
@@ -349,7 +356,7 @@ __global__ __launch_bounds__(256) void agg_fixup_kernel(const int4* __restrict__
   const int wid = uniform(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
   if (wid >= n_heavy) return;
   const int4 hv = heavy[wid];
-  hub_combine<VEC, GL, STG, T>(uniform(hv.x), uniform(hv.y), uniform(hv.z), C, ep, partials);
+  hub_combine<VEC, pow2_ceil(GL), STG, T>(uniform(hv.x), uniform(hv.y), uniform(hv.z), C, ep, partials);
 }
 
 // Experiment knob (not part of the ABI contract): GNPDE_HUB_FIXUP=1 combines hub
@@ -432,6 +439,11 @@ static int launch_agg_vec(const int4* items, int64_t n_items, int4* heavy, int64
       if (lanes <= 16) return GNPDE_AGG(16, 1, 4, 2);
   }
   if (lanes <= 16) return GNPDE_AGG(16, 1, 4, 1);
+  if constexpr (sizeof(T) == 2 && VEC == 8) {
+    // bf16 rows of 129-168 columns (BLEND: C = 162 padded to 168 = 21 lanes of 16 B):
+    // three rows per wavefront, 63 of 64 lanes busy (GNPDE_AGG_VARIANT=9: two rows, 21 of 32)
+    if (lanes > 16 && lanes <= 21 && agg_variant() != 9) return GNPDE_AGG(21, 1, 4, 3);
+  }
   if (lanes <= 32) {
     // two rows per wavefront (fp32 C = 128 and bf16 rows of 17-32 lanes): with the
     // plan's items longest first, G-arxiv rk4 bench 9,301 against 8,643 RHS/s with

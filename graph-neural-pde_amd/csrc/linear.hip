@@ -284,6 +284,16 @@ static int linear_variant() {
   return v;
 }
 
+// Experiment knob (not part of the ABI contract): GNPDE_LIN_WAVES = wavefronts of the
+// persistent projection grid (default 2048).
+static int64_t linear_waves() {
+  static const int64_t v = [] {
+    const char* e = std::getenv("GNPDE_LIN_WAVES");
+    return e ? std::max<int64_t>(4, std::atoll(e)) : (int64_t)2048;
+  }();
+  return v;
+}
+
 extern "C" int gnpde_linear_f32(const float* x, int64_t R, int64_t K, int64_t ldx, const float* W, const float* bias,
                                 int64_t Nout, int64_t split, float* out_a, int64_t lda, float* out_b, int64_t ldb,
                                 void* stream) {
@@ -306,7 +316,7 @@ extern "C" int gnpde_linear_f32(const float* x, int64_t R, int64_t K, int64_t ld
     // persistent tiles: about 2 workgroups per CU, tiles spread evenly over the wavefronts
     const int64_t ntiles = ceil_div(R, kLinRowsPerWave);
     const int64_t slices = ceil_div(Nout, kLinCols);
-    const int64_t max_waves = std::max<int64_t>(kWavesPerBlock, 2048 / slices);
+    const int64_t max_waves = std::max<int64_t>(kWavesPerBlock, linear_waves() / slices);
     const int64_t per_wave = ceil_div(ntiles, max_waves);
     const int64_t blocks = ceil_div(ceil_div(ntiles, per_wave), kWavesPerBlock);
     const dim3 gt((unsigned)blocks, (unsigned)slices);

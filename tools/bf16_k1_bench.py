@@ -34,9 +34,20 @@ def main():
             func(None, x)
         e.record()
         torch.cuda.synchronize()
+    rhs_us = s.elapsed_time(e) / reps * 1e3
+    # rk4 steps through the integrator (fused stages, graph replay), as bench.py's blend_c162
+    steps = 40
+    with torch.no_grad():
+        t = torch.tensor([0.0, 0.25 * steps], device=dev)
+        gnpde.odeint(func, x, t, method='rk4', options={'step_size': 0.25})
+        torch.cuda.synchronize()
+        s.record()
+        gnpde.odeint(func, x, t, method='rk4', options={'step_size': 0.25})
+        e.record()
+        torch.cuda.synchronize()
     print(json.dumps({"C": C, "dtype": "bf16", "vec": os.environ.get("GNPDE_BF16_VEC", "default"),
-                      "variant": os.environ.get("GNPDE_AGG_VARIANT", "0"),
-                      "rhs_us": round(s.elapsed_time(e) / reps * 1e3, 1)}))
+                      "variant": os.environ.get("GNPDE_AGG_VARIANT", "0"), "rhs_us": round(rhs_us, 1),
+                      "rk4_step_ms": round(s.elapsed_time(e) / steps, 4)}))
 
 
 if __name__ == "__main__":
