@@ -256,15 +256,18 @@ def bench_single(args, world, rank, dev):
     plain = None
     if args.rhs_plain_reps > 0:
         with torch.no_grad():
-            wc = func.csr_weights(g, w, 'w')
+            # on the numbering the solve ran in (the integrator's NodeLayout, when it used one)
+            lay = func.node_layout(x)
+            gp, xp = (lay.graph, lay.to_internal(x)) if lay is not None else (g, x)
+            wc = func.csr_weights(gp, w, 'w')
             out = torch.empty_like(x).view(-1, C)
             for _ in range(3):
-                orig_spmm(g, wc, x, alpha=func.alpha_train.detach(), out=out)
+                orig_spmm(gp, wc, xp, alpha=func.alpha_train.detach(), out=out)
             torch.cuda.synchronize()
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record()
             for _ in range(args.rhs_plain_reps):
-                orig_spmm(g, wc, x, alpha=func.alpha_train.detach(), out=out)
+                orig_spmm(gp, wc, xp, alpha=func.alpha_train.detach(), out=out)
             e.record()
             torch.cuda.synchronize()
         pms = s.elapsed_time(e) / args.rhs_plain_reps
@@ -292,6 +295,7 @@ def bench_single(args, world, rank, dev):
                    "nodes": N, "edges": E, "dim": C,
                    "method": "rk4", "step_size": h, "rhs_per_step": rhs_per_step, "global_batch": world,
                    "parallelism": "replicas%d" % world, "chunk": g.chunk,
+                   "node_order": "none" if args.rhs_only or func.node_layout(x) is None else ops.NODE_ORDER,
                    "hub_rows": g.csr.plan.n_heavy},
         "rhs_ms": round(k1_ms, 4),
         "roofline": rl,

@@ -1,9 +1,16 @@
 // linear.hip — the dense node projections of the attention RHS (Q and K of
 // SpGraphTransAttentionLayer, function_transformer_attention.py:224-225) on the
-// CDNA4 matrix cores: exact-f32 v_mfma_f32_32x32x2_f32 (one f32 fma chain per
-// output, same numerics as an fp32 GEMM with a different summation order).
+// CDNA4 matrix cores.
 //
-// Tile: one wavefront = 32 rows x 64 output columns (two 32x32 accumulators),
+// Default (K % 16 == 0, K <= 128): linear_split_kernel, the f32 product formed
+// from exact three-piece bf16 splits of both operands on
+// v_mfma_f32_32x32x16_bf16 (16x the f32 MFMA rate; f32-GEMM accuracy, see the
+// comment above it).  G-arxiv Q|K (R = 169,343, K = 128, Nout = 64): 32.8 us
+// against 42.2 us for the exact-f32 kernel below (profiles/r02b_*).
+//
+// Other shapes: exact-f32 v_mfma_f32_32x32x2_f32 (one f32 fma chain per output,
+// same numerics as an fp32 GEMM with a different summation order).  Tile: one
+// wavefront = 32 rows x 64 output columns (two 32x32 accumulators),
 // 4 wavefronts per workgroup = 128 rows; blockIdx.y walks 64-column slices of
 // the output.  The K (= C) reduction is split between the two lane halves of
 // the MFMA: half h covers k in [h*Kh, h*Kh + Kh), Kh = ceil(K/2), so each lane
@@ -270,12 +277,201 @@ __global__ __launch_bounds__(256, 2) void linear_mfma_tiles_kernel(const float* 
   }
 }
 
+// ------------------------------------------------------------------ split-bf16 projection
+// The same product on the bf16 matrix cores, which run 16x the f32 MFMA rate:
+// every f32 operand is split EXACTLY into three bf16 pieces, v = v0 + v1 + v2
+// (v0 = RNE(v), v1 = RNE(v - v0), v2 = v - v0 - v1: each residual keeps at most
+// 16, then 8 significant bits), and the six products whose magnitude is above
+// 2^-24 of the leading one (x0w0, x0w1, x1w0, x0w2, x1w1, x2w0) are summed by
+// v_mfma_f32_32x32x16_bf16 in f32.  The dropped ones (x1w2, x2w1, x2w2) are
+// below 2^-24 |x||w|: f32-GEMM accuracy at 6/16 of the f32 MFMA cost, so the
+// kernel is bound by its x stream instead of the matrix cores.
+//
+// Lane l = r + 32h of a wave owns row r of a 32-row tile and the K/2 contiguous
+// columns [h*K/2, (h+1)*K/2) of it (one 16-byte load stream per lane); MFMA
+// step s takes its 8 columns h*K/2 + 8s .. +7, i.e. the k index of the
+// operand layout (8h + j) is permuted, identically for A (x) and B (W).  The
+// B fragments of the 64-column slice — 2 tiles x 3 pieces x K/16 steps — are
+// split once per workgroup into LDS in lane order (ds_read_b128,
+// conflict-free).  Persistent waves walk tiles; as soon as step s has been
+// split, its registers are refilled with step s of the next tile.
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+
+// one v_cvt_pk_bf16_f32 (RNE) per pair; the pair's f32 values of the pieces
+// are the dword's halves moved to the high bits (shift / mask), the residuals
+// one packed subtraction
+__device__ __forceinline__ void split_pair(f32x2_t v, uint32_t& p0, uint32_t& p1, uint32_t& p2) {
+  auto widen = [](uint32_t p) {
+    const f32x2_t w = {__uint_as_float(p << 16), __uint_as_float(p & 0xffff0000u)};
+    return w;
+  };
+  p0 = __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_t));
+  const f32x2_t r1 = v - widen(p0);
+  p1 = __builtin_bit_cast(uint32_t, __builtin_convertvector(r1, bf16x2_t));
+  const f32x2_t r2 = r1 - widen(p1);
+  p2 = __builtin_bit_cast(uint32_t, __builtin_convertvector(r2, bf16x2_t));
+}
+
+__device__ __forceinline__ void split3(const float4& lo, const float4& hi, bf16x8_t& p0, bf16x8_t& p1,
+                                       bf16x8_t& p2) {
+  uint32_t a0, a1, a2, a3, b0, b1, b2, b3, c0, c1, c2, c3;
+  const f32x2_t v0 = {lo.x, lo.y}, v1 = {lo.z, lo.w}, v2 = {hi.x, hi.y}, v3 = {hi.z, hi.w};
+  split_pair(v0, a0, b0, c0);
+  split_pair(v1, a1, b1, c1);
+  split_pair(v2, a2, b2, c2);
+  split_pair(v3, a3, b3, c3);
+  const u32x4_t a = {a0, a1, a2, a3}, b = {b0, b1, b2, b3}, c = {c0, c1, c2, c3};
+  p0 = __builtin_bit_cast(bf16x8_t, a);
+  p1 = __builtin_bit_cast(bf16x8_t, b);
+  p2 = __builtin_bit_cast(bf16x8_t, c);
+}
+
+// The product is formed transposed, D = W x^T (W fragments as the A operand,
+// x as B), so that a lane ends with ITS row's outputs: 32 output columns of
+// tile t in 4 runs of 4 (rows (reg&3) + 8*(reg>>2) + 4h of the C layout), i.e.
+// four 16-byte stores per tile.  Stores are raw buffer stores with
+// out-of-range offsets dropped (no branch: every path has the same vmcnt
+// count, so the wait for a step's refill does not wait for the stores).
+// VST: float4 stores (split % 32 == 0 or no second output, Nout % 4 == 0,
+// 16-byte aligned outputs and strides); otherwise one store per element into
+// both outputs, the one that does not own the column dropped.
+template <int KS, bool VST>
+__global__ __launch_bounds__(256, 2) void linear_split_kernel(const float* __restrict__ x, int R, int64_t ldx,
+                                                               const float* __restrict__ W,
+                                                               const float* __restrict__ bias, int Nout, int split,
+                                                               float* __restrict__ out_a, int64_t lda,
+                                                               float* __restrict__ out_b, int64_t ldb) {
+  constexpr int K = 16 * KS, KH = 8 * KS;
+  extern __shared__ __attribute__((aligned(16))) bf16x8_t wfrag[];  // [tile 2][piece 3][step KS][lane 64] | bias[64]
+  float* __restrict__ bl = reinterpret_cast<float*>(wfrag + 2 * 3 * KS * kWave);
+  const int col0 = blockIdx.y * kLinCols;
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const int r32 = lane & 31, h = lane >> 5;
+  const int ntiles = (R + kLinRowsPerWave - 1) / kLinRowsPerWave;
+  const int step = gridDim.x * kWavesPerBlock;
+  int tile = blockIdx.x * kWavesPerBlock + wv;
+
+  // the wave's first tile goes out before the W staging
+  float4 xa[2 * KS];
+  {
+    const float* __restrict__ xr =
+        x + (int64_t)min(min(tile, ntiles - 1) * kLinRowsPerWave + r32, R - 1) * ldx + h * KH;
+#pragma unroll
+    for (int i = 0; i < 2 * KS; ++i) xa[i] = *reinterpret_cast<const float4*>(xr + 4 * i);
+  }
+  for (int e = threadIdx.x; e < 2 * KS * kWave; e += kBlock) {
+    const int t = e / (KS * kWave), s = (e / kWave) % KS, l = e % kWave;
+    const int n = col0 + 32 * t + (l & 31);
+    float4 lo = make_float4(0.f, 0.f, 0.f, 0.f), hi = lo;
+    if (n < Nout) {
+      const float* wr = W + (int64_t)n * K + (l >> 5) * KH + 8 * s;
+      lo = *reinterpret_cast<const float4*>(wr);
+      hi = *reinterpret_cast<const float4*>(wr + 4);
+    }
+    bf16x8_t p0, p1, p2;
+    split3(lo, hi, p0, p1, p2);
+    wfrag[((t * 3 + 0) * KS + s) * kWave + l] = p0;
+    wfrag[((t * 3 + 1) * KS + s) * kWave + l] = p1;
+    wfrag[((t * 3 + 2) * KS + s) * kWave + l] = p2;
+  }
+  if (threadIdx.x < kLinCols) {
+    const int n = col0 + threadIdx.x;
+    bl[threadIdx.x] = (bias && n < Nout) ? bias[n] : 0.f;
+  }
+  __syncthreads();
+  if (tile >= ntiles) return;
+
+  const __amdgpu_buffer_rsrc_t ra = buf_rsrc(out_a);
+  const __amdgpu_buffer_rsrc_t rb = buf_rsrc(out_b ? out_b : out_a);
+
+  for (; tile < ntiles; tile += step) {
+    const int nt = min(tile + step, ntiles - 1);  // clamped: the last pass re-reads a valid row
+    const float* __restrict__ xn = x + (int64_t)min(nt * kLinRowsPerWave + r32, R - 1) * ldx + h * KH;
+    f32x16 acc[2] = {{0}, {0}};
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      bf16x8_t a0, a1, a2;
+      split3(xa[2 * s], xa[2 * s + 1], a0, a1, a2);
+      // refill four steps at a time: the lane's 128-byte line of the next tile
+      // is then read by eight back-to-back loads (spread over four steps, its
+      // line left the 32 KB L1 between them and was fetched again from L2)
+      if (s % 4 == 3 || s == KS - 1) {
+#pragma unroll
+        for (int s2 = s - s % 4; s2 <= s; ++s2) {
+          xa[2 * s2] = *reinterpret_cast<const float4*>(xn + 8 * s2);
+          xa[2 * s2 + 1] = *reinterpret_cast<const float4*>(xn + 8 * s2 + 4);
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const bf16x8_t w0 = wfrag[((t * 3 + 0) * KS + s) * kWave + lane];
+        const bf16x8_t w1 = wfrag[((t * 3 + 1) * KS + s) * kWave + lane];
+        const bf16x8_t w2 = wfrag[((t * 3 + 2) * KS + s) * kWave + lane];
+        // smallest products first
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w0, a2, acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w1, a1, acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w2, a0, acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w0, a1, acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w1, a0, acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w0, a0, acc[t], 0, 0, 0);
+      }
+      // keep step s+1's refill behind step s+1's split: hoisted above it, the
+      // refill needs fresh registers and the loop head then copies them back
+      // after waiting for almost every load of the next tile
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // D = W x^T in the C layout: lane column = x row r32, register 4g + i = output
+    // column 8g + 4h + i of tile t
+    const int row = tile * kLinRowsPerWave + r32;
+    const bool row_ok = row < R;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int n0 = col0 + 32 * t;  // wave-uniform
+      if constexpr (VST) {
+        const bool to_a = n0 < split;
+        const int64_t ld = to_a ? lda : ldb;
+        const int nb = to_a ? n0 : n0 - split;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int c = 8 * g + 4 * h;
+          const float4 b4 = *reinterpret_cast<const float4*>(bl + 32 * t + c);
+          const u32x4_t d = {__float_as_uint(acc[t][4 * g] + b4.x), __float_as_uint(acc[t][4 * g + 1] + b4.y),
+                             __float_as_uint(acc[t][4 * g + 2] + b4.z), __float_as_uint(acc[t][4 * g + 3] + b4.w)};
+          const uint32_t off = (row_ok && n0 + c < Nout) ? (uint32_t)(((int64_t)row * ld + nb + c) * 4) : kBufNone;
+          __builtin_amdgcn_raw_buffer_store_b128(d, to_a ? ra : rb, off, 0, 0);
+        }
+      } else {
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+          const int n = n0 + 8 * (reg >> 2) + 4 * h + (reg & 3);
+          const float v = acc[t][reg] + bl[n - col0];
+          const bool ok = row_ok && n < Nout;
+          const uint32_t oa = (ok && n < split) ? (uint32_t)(((int64_t)row * lda + n) * 4) : kBufNone;
+          const uint32_t ob = (ok && n >= split) ? (uint32_t)(((int64_t)row * ldb + n - split) * 4) : kBufNone;
+          buf_store_f32(ra, oa, v);
+          buf_store_f32(rb, ob, v);
+        }
+      }
+    }
+  }
+}
+
+
 }  // namespace gnpde
 
 using namespace gnpde;
 
 // Experiment knob (not part of the ABI contract): GNPDE_LINEAR=1 forces the
-// per-tile (non-persistent) projection kernel.
+// per-tile (non-persistent) exact-f32 kernel, =2 the persistent exact-f32 one
+// (default: the split-bf16 kernel where K % 16 == 0 and K <= 128).  Measured
+// and dropped: 16-row tiles on 16x16x32 with a three-deep register ring of x
+// tiles (31.7-32.3 us), splitting the whole tile before refilling (1 wave per
+// SIMD, 32-38 us), refilling per step instead of per 128-byte line (32 us).
 static int linear_variant() {
   static const int v = [] {
     const char* e = std::getenv("GNPDE_LINEAR");
@@ -312,7 +508,42 @@ extern "C" int gnpde_linear_f32(const float* x, int64_t R, int64_t K, int64_t ld
   const bool vec4 = (K % 8 == 0) && (ldx % 4 == 0) && aligned16(x);
   hipStream_t s = as_stream(stream);
   const int nch = (int)(Khp / kLinChunk);
-  if (vec4 && nch <= 6 && linear_variant() == 0) {
+  if (vec4 && K % 16 == 0 && K <= 128 && aligned16(W) && linear_variant() == 0 &&
+      R * std::max(lda, split == Nout ? lda : ldb) * (int64_t)sizeof(float) < (int64_t)kBufRecords) {
+    // split-bf16 MFMA, persistent tiles (same wave budget as below)
+    const int64_t ntiles = ceil_div(R, kLinRowsPerWave);
+    const int64_t slices = ceil_div(Nout, kLinCols);
+    const int64_t max_waves = std::max<int64_t>(kWavesPerBlock, linear_waves() / slices);
+    const int64_t per_wave = ceil_div(ntiles, max_waves);
+    const int64_t blocks = ceil_div(ceil_div(ntiles, per_wave), kWavesPerBlock);
+    const dim3 gt((unsigned)blocks, (unsigned)slices);
+    const size_t lds = sizeof(bf16x8_t) * 2 * 3 * (size_t)(K / 16) * kWave + sizeof(float) * kLinCols;
+    const bool vst = (split % 32 == 0 || split == Nout) && Nout % 4 == 0 && lda % 4 == 0 && aligned16(out_a) &&
+                     (split == Nout || (ldb % 4 == 0 && aligned16(out_b)));
+#define GNPDE_LIN_S(KS)                                                                                         \
+  do {                                                                                                          \
+    if (vst)                                                                                                    \
+      linear_split_kernel<KS, true><<<gt, kBlock, lds, s>>>(x, (int)R, ldx, W, bias, (int)Nout, (int)split,     \
+                                                            out_a, lda, out_b, ldb);                            \
+    else                                                                                                        \
+      linear_split_kernel<KS, false><<<gt, kBlock, lds, s>>>(x, (int)R, ldx, W, bias, (int)Nout, (int)split,    \
+                                                             out_a, lda, out_b, ldb);                           \
+  } while (0)
+    switch (K / 16) {
+      case 1: GNPDE_LIN_S(1); break;
+      case 2: GNPDE_LIN_S(2); break;
+      case 3: GNPDE_LIN_S(3); break;
+      case 4: GNPDE_LIN_S(4); break;
+      case 5: GNPDE_LIN_S(5); break;
+      case 6: GNPDE_LIN_S(6); break;
+      case 7: GNPDE_LIN_S(7); break;
+      default: GNPDE_LIN_S(8); break;
+    }
+#undef GNPDE_LIN_S
+    GNPDE_LAUNCH_CHECK();
+    return GNPDE_OK;
+  }
+  if (vec4 && nch <= 6 && linear_variant() != 1) {
     // persistent tiles: about 2 workgroups per CU, tiles spread evenly over the wavefronts
     const int64_t ntiles = ceil_div(R, kLinRowsPerWave);
     const int64_t slices = ceil_div(Nout, kLinCols);

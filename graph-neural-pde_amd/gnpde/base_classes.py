@@ -70,6 +70,7 @@ class ODEFunc(nn.Module):
         self._graph = None
         self._graph_key = None
         self._w_cache = {}
+        self._layout = None  # the NodeLayout a fixed-grid solve runs in (gnpde.integrator), else None
 
     def graph_for(self, x):
         """Device CSR of ``self.edge_index`` for node count x.shape[1] (or x, an
@@ -85,7 +86,24 @@ class ODEFunc(nn.Module):
             self._graph = ops.GraphCSR(self.edge_index, n, chunk=chunk)
             self._graph_key = key
             self._w_cache = {}
+        if self._layout is not None:
+            return self._layout.graph
         return self._graph
+
+    def supports_node_layout(self):
+        """True when every operand of the RHS is per node or per edge in COO order,
+        so the integrator may run it on a renumbered state (ops.NodeLayout)."""
+        return False
+
+    def node_layout(self, x):
+        """The locality numbering the fixed-grid integrator keeps this solve's
+        state in (ops.NodeLayout, built once per graph), or None: not supported,
+        a layout already active, or a state too small to gain from it."""
+        if self._layout is not None or not self.supports_node_layout() or x.dim() != 3:
+            return None
+        if not ops.layout_worthwhile(x.shape[0] * x.shape[1], x.shape[-1], x.element_size()):
+            return None
+        return self.graph_for(x).node_layout
 
     def csr_weights(self, g, w, tag, transpose=False):
         """COO-order weights (or [B,E,h] attention -> head mean) in CSR (or CSC) order,
@@ -123,9 +141,11 @@ class ODEFunc(nn.Module):
         x0 = self.x0
         if x0 is None:
             raise RuntimeError("%s: add_source needs x0 (ODEblock.set_x0)" % self.__class__.__name__)
-        key = _tensor_key(x0)
+        lay = self._layout
+        key = (_tensor_key(x0), id(lay) if lay is not None else None)
+        slot = '_x0_buf' if lay is None else '_x0_buf_layout'  # one stable buffer per numbering
         shape = tuple(x0.shape[:-1]) + (x.shape[-1],)
-        hit = getattr(self, '_x0_buf', None)
+        hit = getattr(self, slot, None)
         if hit is not None and hit[0] == key and hit[1].shape == shape and hit[1].dtype == x.dtype and \
                 hit[1].device == x.device:
             return hit[1]
@@ -133,8 +153,9 @@ class ODEFunc(nn.Module):
             buf = hit[1]
         else:
             buf = torch.zeros(shape, dtype=x.dtype, device=x.device)
-        buf[..., :x0.shape[-1]].copy_(x0.detach())
-        self._x0_buf = (key, buf)
+        src = x0.detach()
+        buf[..., :x0.shape[-1]].copy_(src if lay is None else lay.to_internal(src))
+        setattr(self, slot, (key, buf))
         return buf
 
     def __repr__(self):

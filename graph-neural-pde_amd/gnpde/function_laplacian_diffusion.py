@@ -99,6 +99,11 @@ class LaplacianODEFunc(ODEFunc):
         integrator may run on a zero-padded state (integrator._padded_width)."""
         return True
 
+    def supports_node_layout(self):
+        """Weights are per edge in COO order, x0 per node: the fixed-grid
+        integrator may keep the state in the graph's locality numbering."""
+        return True
+
     def _x0_like(self, x):
         """x0 in x's dtype and (padded) width, for the eager autograd path."""
         x0 = self.x0

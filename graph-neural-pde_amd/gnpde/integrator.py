@@ -318,10 +318,26 @@ def _padded_width(func, y0):
     return (C + per16 - 1) // per16 * per16
 
 
+def _node_layout(func, y0):
+    """The locality numbering (ops.NodeLayout) the fused path keeps the state in, or None."""
+    fn = getattr(func, 'node_layout', None)
+    return fn(y0) if fn is not None else None
+
+
 def odeint_fixed(func, y0, t, method, step_size=None, combine=None, graph=None):
     combine = combine or _Combine()
     fused = _fusable(func, y0, combine)
     if fused:
+        lay = _node_layout(func, y0)
+        if lay is not None:
+            # the whole solve in the graph's locality numbering: one gather of the
+            # state in, one of the solution out (bit-identical results, ops.NodeLayout)
+            func._layout = lay
+            try:
+                out = odeint_fixed(func, lay.to_internal(y0), t, method, step_size, combine, graph)
+            finally:
+                func._layout = None
+            return lay.to_user(out)
         cp = _padded_width(func, y0)
         if cp is not None:
             C = y0.shape[-1]

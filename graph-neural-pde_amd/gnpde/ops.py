@@ -326,6 +326,67 @@ class GraphCSR(object):
                   _stream(w.device))
         return out
 
+    @property
+    def node_layout(self):
+        """The graph's locality numbering (NodeLayout), built once."""
+        if getattr(self, '_layout', None) is None:
+            self._layout = NodeLayout(self)
+        return self._layout
+
+
+# --------------------------------------------------------------------------- state layout
+# The fixed-grid integrator keeps the state of a large graph in a locality
+# numbering of its nodes for the whole solve (gnpde.integrator.odeint_fixed):
+# permuted once on entry, back once on exit.  "degree": nodes by in-degree,
+# descending (stable), per batch element — the rows the aggregation gathers most
+# sit together at the front of the state.  G-arxiv rk4 step (tools/reorder_bench.py,
+# profiles/r02b_reorder.jsonl): 420 -> 370 us; the same numbering applied to the
+# item ORDER only (rows of x where they were) gains nothing, so it is where the
+# gathered rows live, not when they are gathered.  "none" disables.
+NODE_ORDER = os.environ.get("GNPDE_NODE_ORDER", "degree")
+LAYOUT_MIN_ROWS = 32768          # below this the state sits in L2 / the Infinity Cache anyway
+LAYOUT_MIN_BYTES = 16 << 20      # and the two permutations would cost more than they save
+
+
+class NodeLayout(object):
+    """In-degree numbering of a GraphCSR's nodes and the same graph relabelled.
+
+    ``order[k]`` = user row held at internal row k, ``new_id[i]`` = internal row
+    of user row i (global rows, batch elements kept in their own row ranges).
+    ``graph`` is the GraphCSR of ``new_id[edge_index]``: the COO edge order is
+    unchanged (so COO-order weights apply as they are) and each row keeps its
+    edges in COO order, so every output row is summed over the same edges in the
+    same order — results are bit-identical to the user numbering."""
+
+    def __init__(self, g):
+        B, N, R = g.B, g.N, g.R
+        dev = g.edge_index.device
+        deg = g.indeg.view(B, N).long()
+        local_order = torch.argsort(-deg, dim=1, stable=True)  # old local id at each new position
+        base = (torch.arange(B, device=dev, dtype=torch.int64) * N).view(B, 1)
+        self.order = (local_order + base).reshape(R)
+        self.new_id = torch.empty_like(self.order)
+        self.new_id[self.order] = torch.arange(R, device=dev, dtype=torch.int64)
+        local_new = self.new_id.view(B, N) - base
+        ei = g.edge_index
+        eip = torch.gather(local_new, 1, ei.reshape(B, -1)).view(ei.shape)
+        self.graph = GraphCSR(eip, N, chunk=g.chunk, validate=False)
+        self.R = R
+
+    def to_internal(self, y):
+        """[B,N,C] (or [R,C]) in user order -> the same in internal order (new tensor)."""
+        C = y.shape[-1]
+        return y.reshape(-1, C).index_select(0, self.order).view(y.shape)
+
+    def to_user(self, y):
+        """[..., B, N, C] in internal order -> user order (new tensor)."""
+        C = y.shape[-1]
+        return y.reshape(-1, self.R, C).index_select(1, self.new_id).view(y.shape)
+
+
+def layout_worthwhile(R, C, elem_size):
+    return NODE_ORDER == "degree" and R >= LAYOUT_MIN_ROWS and R * C * elem_size >= LAYOUT_MIN_BYTES
+
 
 # --------------------------------------------------------------------------- block weight producers
 def mix_weights(att, edge_weight=None, gamma=None):

@@ -1,0 +1,97 @@
+"""GPU: the integrator's locality numbering of the state (ops.NodeLayout).
+
+A fixed-grid solve on a large graph runs in the graph's in-degree numbering
+(gathered rows together at the front of the state) and permutes back once at
+the end.  Every output row is summed over the same edges in the same order as
+in the user numbering, so the result must be BIT-identical to the solve with
+the layout disabled — checked here for euler / midpoint / rk4, add_source,
+a batch of two graphs, the zero-padded width (C = 162) and a bf16 state — and
+the layout must actually have been used (its graph built, its x0 buffer filled)."""
+import pytest
+import torch
+
+import gnpde
+from gnpde import ops, synthetic
+from test_gpu_parity import DEV, OPT
+
+pytestmark = pytest.mark.gpu
+
+
+def _func(N, E, C, B, add_source, seed=0):
+    eis, ws = [], []
+    for b in range(B):
+        ei, w = synthetic.rw_graph(N, E, seed=seed + b, device=DEV)
+        eis.append(ei)
+        ws.append(w)
+    ei, w = torch.cat(eis, 0), torch.cat(ws, 0)
+    opt = dict(OPT, hidden_dim=C, add_source=add_source)
+    func = gnpde.LaplacianODEFunc(C, C, opt, DEV).to(DEV)
+    with torch.no_grad():
+        func.alpha_train.fill_(0.3)
+        func.beta_train.fill_(0.7)
+    func.edge_index, func.edge_weight = ei, w
+    return func
+
+
+def _solve(func, x, method, steps, h, order):
+    saved = ops.NODE_ORDER
+    ops.NODE_ORDER = order
+    try:
+        with torch.no_grad():
+            t = torch.tensor([0.0, steps * h], device=DEV)
+            return gnpde.odeint(func, x, t, method=method, options={'step_size': h})
+    finally:
+        ops.NODE_ORDER = saved
+
+
+@pytest.mark.parametrize("method,steps", [("euler", 3), ("midpoint", 2), ("rk4", 9)])
+@pytest.mark.parametrize("add_source", [False, True])
+def test_layout_solve_bit_identical(method, steps, add_source):
+    N, E, C = 40000, 300000, 128
+    func = _func(N, E, C, 1, add_source)
+    x = synthetic.features(1, N, C, seed=3, device=DEV)
+    if add_source:
+        func.x0 = synthetic.features(1, N, C, seed=4, device=DEV)
+    ref = _solve(func, x, method, steps, 0.1, "none")
+    got = _solve(func, x, method, steps, 0.1, "degree")
+    assert func._layout is None  # released after the solve
+    assert getattr(func._graph, '_layout', None) is not None  # ... and it was used
+    if add_source:
+        assert getattr(func, '_x0_buf_layout', None) is not None
+    assert torch.equal(got, ref)
+    # a second solve replays the captured steps of the layout graph: same bits again
+    assert torch.equal(_solve(func, x, method, steps, 0.1, "degree"), ref)
+
+
+def test_layout_batched_padded_and_bf16():
+    N, E = 36000, 250000
+    for C, dtype in ((162, torch.float32), (128, torch.bfloat16)):
+        func = _func(N, E, C, 2, True, seed=11)
+        x = synthetic.features(2, N, C, seed=5, device=DEV).to(dtype)
+        func.x0 = synthetic.features(2, N, C, seed=6, device=DEV).to(dtype)
+        ref = _solve(func, x, "rk4", 7, 0.2, "none")
+        got = _solve(func, x, "rk4", 7, 0.2, "degree")
+        assert torch.equal(got, ref), (C, dtype)
+
+
+def test_node_layout_structure():
+    N, E = 40000, 300000
+    func = _func(N, E, 128, 2, False, seed=21)
+    x = synthetic.features(2, N, 128, seed=3, device=DEV)
+    g = func.graph_for(x)
+    lay = func.node_layout(x)
+    assert lay is g.node_layout
+    R = 2 * N
+    ar = torch.arange(R, device=DEV)
+    assert torch.equal(lay.new_id[lay.order], ar) and torch.equal(lay.order[lay.new_id], ar)
+    # batch elements keep their row ranges; in-degree non-increasing inside each
+    assert torch.equal(lay.order.view(2, N) // N, torch.arange(2, device=DEV).view(2, 1).expand(2, N))
+    deg = g.indeg.long()[lay.order].view(2, N)
+    assert bool((deg[:, 1:] <= deg[:, :-1]).all())
+    # the relabelled graph has the same in-degree multiset, renumbered
+    assert torch.equal(lay.graph.indeg.long(), g.indeg.long()[lay.order])
+    y = torch.randn(2, N, 128, device=DEV)
+    assert torch.equal(lay.to_user(lay.to_internal(y)), y)
+    # small states are not renumbered
+    small = _func(2000, 12000, 64, 1, False)
+    assert small.node_layout(torch.zeros(1, 2000, 64, device=DEV)) is None
