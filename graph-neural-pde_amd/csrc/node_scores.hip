@@ -1,0 +1,822 @@
+// node_scores.hip — the per-RHS score and softmax pieces of the attention RHS
+// around K1 (kept out of rhs.hip so that they rebuild without K1's
+// instantiations): softmax statistics over grouped CSRs and their hub fixup,
+// edge-parallel head-mean weights and per-edge attention, the team-mode
+// (per-edge q/k) kernels, and the reference-mode node scores (indegree-weighted
+// key sum + node scores, gnpde_ref_scores_f32).
+// Reference: SpGraphTransAttentionLayer.forward, src/function_transformer_attention.py:218-266;
+// utils.softmax, src/utils.py:116-127.
+#include "aggregate.hpp"
+#include "rhs_host.hpp"
+
+namespace gnpde {
+
+// ------------------------------------------------------------------ softmax statistics
+// GL lanes per plan item (64/GL items per wavefront).  Every lane keeps an
+// online (max, sum-exp) per head over its strided edges; the GL partial states
+// are merged by a fixed xor tree (deterministic).
+template <int MAXH, int GL>
+__global__ __launch_bounds__(256) void stats_kernel(const int4* __restrict__ items, int n_items,
+                                                     const int* __restrict__ gidx, int group_is_dst, ScoreArgs sa,
+                                                     double* __restrict__ m_out, float* __restrict__ rl_out,
+                                                     double* __restrict__ partials) {
+  constexpr int G = kWave / GL;
+  const int lane = threadIdx.x & 63;
+  const int g = lane / GL, gl = lane % GL;
+  const int item = (blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * G + g;
+  const bool live = item < n_items;
+  const int4 it = live ? items[item] : make_int4(0, 0, 0, -1);
+  const int grp = it.x, beg = it.y, end = it.z, slot = it.w;
+  const int H = sa.H;
+  double M[MAXH];
+  float L[MAXH];
+#pragma unroll
+  for (int h = 0; h < MAXH; ++h) {
+    M[h] = -INFINITY;
+    L[h] = 0.f;
+  }
+  for (int p = beg + gl; p < end; p += GL) {
+    const int o = gidx[p];
+    const int src = group_is_dst ? o : grp;
+    const int dst = group_is_dst ? grp : o;
+#pragma unroll
+    for (int h = 0; h < MAXH; ++h)
+      if (h < H) online_push(M[h], L[h], sa.score(src, dst, h));
+  }
+#pragma unroll
+  for (int o = 1; o < GL; o <<= 1) {
+#pragma unroll
+    for (int h = 0; h < MAXH; ++h) {
+      const double M2 = __shfl_xor(M[h], o);
+      const float L2 = __shfl_xor(L[h], o);
+      online_merge(M[h], L[h], M2, L2);
+    }
+  }
+  if (!live || gl != 0) return;
+  for (int h = 0; h < H && h < MAXH; ++h) {
+    if (slot >= 0) {
+      partials[(int64_t)slot * 2 * H + h] = M[h];
+      partials[(int64_t)slot * 2 * H + H + h] = (double)L[h];
+    } else {
+      m_out[(int64_t)grp * H + h] = M[h];
+      rl_out[(int64_t)grp * H + h] = 1.0f / (L[h] + kSoftmaxEps);
+    }
+  }
+}
+
+// Hub groups: one wavefront per (group, head) merging that group's chunk
+// statistics (stats_merge_store, scores.hpp).
+__global__ __launch_bounds__(256) void stats_fixup_kernel(const int4* __restrict__ heavy, int n_heavy, int H,
+                                                           const double* __restrict__ partials,
+                                                           double* __restrict__ m_out, float* __restrict__ rl_out) {
+  const int wid = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+  if (wid >= n_heavy * H) return;
+  const int i = wid / H, h = wid - i * H;
+  const int4 hv = heavy[i];
+  stats_merge_store(hv.x, hv.y, hv.z, H, h, partials, m_out, rl_out);
+}
+
+int launch_stats_fixup(const int4* heavy, int64_t n_heavy, int H, const double* partials, double* m, float* rl,
+                       hipStream_t s) {
+  if (n_heavy <= 0) return GNPDE_OK;
+  const unsigned g2 = (unsigned)ceil_div(n_heavy * H, kWavesPerBlock);
+  stats_fixup_kernel<<<g2, kBlock, 0, s>>>(heavy, (int)n_heavy, H, partials, m, rl);
+  GNPDE_LAUNCH_CHECK();
+  return GNPDE_OK;
+}
+
+// ------------------------------------------------------------------ edge-parallel weights
+// w[p] = (sum_h exp(s_p,h - m[g,h]) * rl[g,h]) / H   (softmax, then mean over heads)
+__global__ __launch_bounds__(256) void attn_weights_kernel(const int* __restrict__ rowidx, const int* __restrict__ col,
+                                                            int64_t nnz, int norm_idx, ScoreArgs sa,
+                                                            const double* __restrict__ m,
+                                                            const float* __restrict__ rl, float* __restrict__ w) {
+  const int H = sa.H;
+  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < nnz; p += (int64_t)gridDim.x * blockDim.x) {
+    const int r = rowidx[p], c = col[p];
+    const int64_t g = norm_idx == 0 ? r : c;
+    float acc = 0.f;
+    for (int h = 0; h < H; ++h) {
+      const double s = sa.score(r, c, h);
+      acc += expf((float)(s - m[g * H + h])) * rl[g * H + h];
+    }
+    w[p] = acc / (float)H;
+  }
+}
+
+// att[perm[p]*H + h] = exp(s_p,h - m[g,h]) * rl[g,h]   (COO order, per head)
+__global__ __launch_bounds__(256) void edge_attention_kernel(const int* __restrict__ rowidx,
+                                                              const int* __restrict__ col,
+                                                              const int* __restrict__ perm, int64_t nnz,
+                                                              int norm_idx, ScoreArgs sa,
+                                                              const double* __restrict__ m,
+                                                              const float* __restrict__ rl, float* __restrict__ att) {
+  const int H = sa.H;
+  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < nnz; p += (int64_t)gridDim.x * blockDim.x) {
+    const int r = rowidx[p], c = col[p];
+    const int64_t g = norm_idx == 0 ? r : c;
+    const int64_t e = perm[p];
+    for (int h = 0; h < H; ++h) {
+      const double s = sa.score(r, c, h);
+      att[e * H + h] = expf((float)(s - m[g * H + h])) * rl[g * H + h];
+    }
+  }
+}
+
+// ------------------------------------------------------------------ team-mode kernels (per-edge q/k scores)
+// Team-mode softmax statistics: one team of T lanes per work item.  The
+// item's own row (q of the source group, or k of the destination group) is
+// loaded once; the other endpoints' indices come in T at a time (one per
+// lane, then broadcast with shuffles) and kTeamEdges rows are in flight
+// together.  Edges are pushed in CSR order, as the lane-mode kernel does.
+// Loop trip counts are wave-uniform (maxima over the wave's teams), so every
+// shuffle runs with the whole wavefront active; a team past its own edges
+// computes throw-away scores and pushes nothing.
+constexpr int kTeamEdges = 4;
+
+template <int VEC>
+__global__ __launch_bounds__(256) void stats_team_kernel(const int4* __restrict__ items, int n_items,
+                                                          const int* __restrict__ gidx, int group_is_dst, ScoreArgs sa,
+                                                          Team tm, double* __restrict__ m_out,
+                                                          float* __restrict__ rl_out, double* __restrict__ partials) {
+  const int lane = threadIdx.x & 63;
+  const int T = tm.T, S = tm.S, tpw = kWave / T;
+  const int team = lane / T, t = lane % T, h = t / S;
+  const int item = (blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * tpw + team;
+  const bool live = item < n_items;
+  const int4 it = live ? items[item] : make_int4(0, 0, 0, -1);
+  const int grp = it.x, beg = it.y, end = it.z, slot = it.w;
+  float own[VEC];
+  team_row<VEC>(sa, group_is_dst ? sa.k : sa.q, grp, t, own);
+  const float* __restrict__ other_base = group_is_dst ? sa.q : sa.k;
+  double M = -INFINITY;
+  float L = 0.f;
+  const int rounds = wave_max_int((end - beg + T - 1) / T);
+  for (int r = 0; r < rounds; ++r) {
+    const int p0 = beg + r * T;
+    const int cnt = max(0, min(T, end - p0));
+    int mine = 0;
+    if (cnt > 0) mine = gidx[p0 + min(t, cnt - 1)];
+    const int jmax = wave_max_int(cnt);
+    for (int j = 0; j < jmax; j += kTeamEdges) {
+      float other[kTeamEdges][VEC];
+#pragma unroll
+      for (int u = 0; u < kTeamEdges; ++u) {
+        const int o = __shfl(mine, team * T + max(0, min(j + u, cnt - 1)));
+        team_row<VEC>(sa, other_base, o, t, other[u]);
+      }
+      float s[kTeamEdges];
+#pragma unroll
+      for (int u = 0; u < kTeamEdges; ++u)
+        s[u] = group_is_dst ? team_score_regs<VEC>(sa, other[u], own, S) : team_score_regs<VEC>(sa, own, other[u], S);
+#pragma unroll
+      for (int u = 0; u < kTeamEdges; ++u)
+        if (j + u < cnt) online_push(M, L, (double)s[u]);
+    }
+  }
+  if (!live || (t % S) != 0) return;
+  const int H = sa.H;
+  if (slot >= 0) {
+    partials[(int64_t)slot * 2 * H + h] = M;
+    partials[(int64_t)slot * 2 * H + H + h] = (double)L;
+  } else {
+    m_out[(int64_t)grp * H + h] = M;
+    rl_out[(int64_t)grp * H + h] = 1.0f / (L + kSoftmaxEps);
+  }
+}
+
+// Team-mode attention weights: a team takes T consecutive edges (indices
+// loaded one per lane, coalesced), then evaluates them kTeamEdges at a time
+// with the q/k rows and the group's softmax statistics all in flight.  Trip
+// counts are wave-uniform, as in stats_team_kernel.
+template <int VEC, bool COO>
+__global__ __launch_bounds__(256) void attn_team_kernel(const int* __restrict__ rowidx, const int* __restrict__ col,
+                                                         const int* __restrict__ perm, int64_t nnz, int norm_idx,
+                                                         ScoreArgs sa, Team tm, const double* __restrict__ m,
+                                                         const float* __restrict__ rl, float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int T = tm.T, S = tm.S, tpw = kWave / T;
+  const int team = lane / T, t = lane % T, h = t / S;
+  const int H = sa.H;
+  const bool leader = (t % S) == 0;
+  const __amdgpu_buffer_rsrc_t rout = buf_rsrc(out);
+  const int64_t wave_first = (int64_t)(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * tpw * T;
+  const int64_t sweep = (int64_t)gridDim.x * kWavesPerBlock * tpw * T;
+  for (int64_t w0 = wave_first; w0 < nnz; w0 += sweep) {
+    const int64_t p0 = w0 + (int64_t)team * T;
+    const int cnt = (int)max((int64_t)0, min((int64_t)T, nnz - p0));
+    int my_r = 0, my_c = 0, my_dst = 0;
+    if (cnt > 0) {
+      const int64_t pm = p0 + min(t, cnt - 1);
+      my_r = rowidx[pm];
+      my_c = col[pm];
+      if (COO) my_dst = perm[pm];
+    }
+    const int jmax = wave_max_int(cnt);
+    for (int j = 0; j < jmax; j += kTeamEdges) {
+      float qv[kTeamEdges][VEC], kv[kTeamEdges][VEC];
+      double mv[kTeamEdges];
+      float rv[kTeamEdges];
+      int dst[kTeamEdges];
+#pragma unroll
+      for (int u = 0; u < kTeamEdges; ++u) {
+        const int src = team * T + max(0, min(j + u, cnt - 1));
+        const int r = __shfl(my_r, src), c = __shfl(my_c, src);
+        dst[u] = COO ? __shfl(my_dst, src) : 0;
+        team_row<VEC>(sa, sa.q, r, t, qv[u]);
+        team_row<VEC>(sa, sa.k, c, t, kv[u]);
+        const int64_t g = norm_idx == 0 ? r : c;
+        mv[u] = m[g * H + h];
+        rv[u] = rl[g * H + h];
+      }
+#pragma unroll
+      for (int u = 0; u < kTeamEdges; ++u) {
+        const float s = team_score_regs<VEC>(sa, qv[u], kv[u], S);
+        float term = leader ? expf((float)((double)s - mv[u])) * rv[u] : 0.f;
+        if (COO) {
+          const bool st = leader && j + u < cnt;
+          buf_store_f32(rout, st ? (uint32_t)(((int64_t)dst[u] * H + h) * 4) : kBufNone, term);
+        } else {
+          for (int o = S; o < T; o <<= 1) term += __shfl_xor(term, o);
+          const bool st = t == 0 && j + u < cnt;
+          buf_store_f32(rout, st ? (uint32_t)((p0 + j + u) * 4) : kBufNone, term / (float)H);
+        }
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------ reference-mode key sum
+// part[b][c][tile] = sum_{n in tile} indeg[b*N+n] * x[b*N+n][c]  (fp64), part[b][C][..] = sum indeg.
+// TPR threads per row, RPB = 256/TPR rows in flight per block iteration.
+// Tiles come in groups of kKeysumGroup: the block whose tile of a group
+// finishes last (an agent-scope arrival ticket per group, the partials stored
+// write-through first: the in-launch hand-off of aggregate.hpp's hub rows)
+// sums the group's partials in tile order into gpart[b][c][group], and resets
+// the ticket to 0 for the next launch.  The node-score blocks sum the (at most
+// 1024 / kKeysumGroup) group partials themselves (key_projection_lds): no
+// launch between the two passes over x.
+constexpr int kKeysumGroup = 32;
+
+template <int VEC>
+__global__ __launch_bounds__(256) void keysum_partial_kernel(const float* __restrict__ x, int64_t N, int C,
+                                                              int64_t ldx, const int* __restrict__ indeg,
+                                                              int rows_per_tile, int TPR, int ntiles,
+                                                              double* __restrict__ part, double* __restrict__ gpart,
+                                                              int ngroups, int* __restrict__ tickets) {
+  extern __shared__ __attribute__((aligned(16))) double red[];  // [RPB][C+1]
+  const int tile = blockIdx.x, b = blockIdx.y;
+  const int RPB = blockDim.x / TPR;
+  const int rs = threadIdx.x / TPR, t = threadIdx.x % TPR;
+  const int64_t n0 = (int64_t)tile * rows_per_tile;
+  const int64_t n1 = min<int64_t>(N, n0 + rows_per_tile);
+  const int64_t base = (int64_t)b * N;
+  for (int c0 = t * VEC; c0 < C; c0 += TPR * VEC) {
+    double acc[VEC];
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) acc[i] = 0.0;
+#pragma unroll 8
+    for (int64_t n = n0 + rs; n < n1; n += RPB) {
+      const double d = (double)indeg[base + n];
+      float v[VEC];
+      load_vec<VEC>(x + (base + n) * ldx + c0, v);
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) acc[i] = fma(d, (double)v[i], acc[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) red[rs * (C + 1) + c0 + i] = acc[i];
+  }
+  if (t == 0) {
+    double ds = 0.0;
+    for (int64_t n = n0 + rs; n < n1; n += RPB) ds += (double)indeg[base + n];
+    red[rs * (C + 1) + C] = ds;
+  }
+  __syncthreads();
+  // column-major partials [b][c][tile], stored write-through (sc1)
+  const __amdgpu_buffer_rsrc_t rp = buf_rsrc(part + (int64_t)b * (C + 1) * ntiles);
+  for (int c = threadIdx.x; c <= C; c += blockDim.x) {
+    double sum = 0.0;
+    for (int r = 0; r < RPB; ++r) sum += red[r * (C + 1) + c];
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, sum), rp, (uint32_t)(((int64_t)c * ntiles + tile) * 8),
+                                          0, kAuxSc1);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();  // every partial of this block has reached the memory side
+  __shared__ int last;
+  const int grp = tile / kKeysumGroup;
+  const int t0 = grp * kKeysumGroup, t1 = min(ntiles, t0 + kKeysumGroup);
+  int* ticket = tickets + (int64_t)b * ngroups + grp;
+  if (threadIdx.x == 0) {
+    const int k = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = k == t1 - t0 - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  for (int c = threadIdx.x; c <= C; c += blockDim.x) {
+    const double* __restrict__ col = part + ((int64_t)b * (C + 1) + c) * ntiles;
+    double sum = 0.0;
+    for (int tt = t0; tt < t1; ++tt) sum += col[tt];  // tile order: deterministic
+    gpart[((int64_t)b * (C + 1) + c) * ngroups + grp] = sum;
+  }
+  if (threadIdx.x == 0) __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Per batch element b, from xbar = sum_n indeg(n) x_n (and xbar[C] = E):
+//   S[d]   = Wk[d,:] . xbar + E bk[d]                    (the fork's global key sum, :249)
+//   U[c,h] = sum_{d in head h} Wq[d,c] S[d] / sqrt(dk)   (padded [Cp][Hp], zeros past C, H)
+//   v[h]   = bq_h . S_h / sqrt(dk)
+// so that cs[n,h] = x_n . U[:,h] + v[h] = q_{n,h} . S_h / sqrt(dk).  Computed by
+// every node-score workgroup into its own LDS (a few KFLOP, operands from L2):
+// no single-workgroup launch between the key sum and the node scores.
+struct KeyProj {
+  const double* __restrict__ gpart;  // [B][C+1][ngroups] group partials of xbar
+  int ngroups;
+  const float* __restrict__ Wq;
+  const float* __restrict__ bq;
+  const float* __restrict__ Wk;
+  const float* __restrict__ bk;
+  int att;
+};
+
+constexpr int kFinishRows = 8;  // rows of Wk per wavefront pass (independent loads in flight)
+
+__device__ void key_projection_lds(const KeyProj& kp, int64_t b, int C, int H, int Cp, int Hp, double* S, double* U,
+                                   double* v, double* xb) {
+  // xbar[c] = sum of the group partials, in group order (deterministic)
+  for (int c = threadIdx.x; c <= C; c += blockDim.x) {
+    const double* __restrict__ gp = kp.gpart + (b * (C + 1) + c) * kp.ngroups;
+    double sum = 0.0;
+    for (int g = 0; g < kp.ngroups; ++g) sum += gp[g];
+    xb[c] = sum;
+  }
+  __syncthreads();
+  const int att = kp.att;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int d0 = wv * kFinishRows; d0 < att; d0 += kWavesPerBlock * kFinishRows) {
+    double sacc[kFinishRows];
+#pragma unroll
+    for (int j = 0; j < kFinishRows; ++j) sacc[j] = 0.0;
+    for (int c = lane; c < C; c += kWave) {
+      const double xv = xb[c];
+#pragma unroll
+      for (int j = 0; j < kFinishRows; ++j) {
+        const int d = min(d0 + j, att - 1);
+        sacc[j] = fma((double)kp.Wk[(int64_t)d * C + c], xv, sacc[j]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kFinishRows; ++j) {
+      const double t = wave_sum(sacc[j]);
+      if (lane == 0 && d0 + j < att) S[d0 + j] = t + xb[C] * (double)kp.bk[d0 + j];
+    }
+  }
+  __syncthreads();
+  const int dk = att / H;
+  const double inv = 1.0 / sqrt((double)dk);
+  // pair t -> (h = t / Cp, c = t % Cp): consecutive threads read consecutive Wq columns
+  for (int t = threadIdx.x; t < Cp * Hp; t += blockDim.x) {
+    const int h = t / Cp, c = t - h * Cp;
+    double a = 0.0;
+    if (c < C && h < H) {
+#pragma unroll 16
+      for (int d = h * dk; d < (h + 1) * dk; ++d) a = fma((double)kp.Wq[(int64_t)d * C + c], S[d], a);
+    }
+    U[c * Hp + h] = a * inv;
+  }
+  if (threadIdx.x < Hp) {
+    const int h = threadIdx.x;
+    double a = 0.0;
+    if (h < H)
+      for (int d = h * dk; d < (h + 1) * dk; ++d) a = fma((double)kp.bq[d], S[d], a);
+    v[h] = a * inv;
+  }
+  __syncthreads();
+}
+
+// cs[b*N+n, h] = x_{b,n} . U[b,:,h] + v[b,h]  (fp64 accumulation).
+// GL lanes per row, G = 64/GL rows per wavefront step; each lane owns NPV
+// columns of a chunk of CW = GL*NPV columns.  When the row fits one chunk (the
+// usual case) the lane's slice of U[b] stays in registers for every row the
+// wave visits and the next row's x slice is prefetched while the current one
+// is reduced.  U is padded ([Cp][Hp], Cp = nch*CW, Hp = MAXH), so its loads
+// take compile-time offsets from one lane base; x loads past C (ragged last
+// chunk only) are clamped and zeroed.  No load sits behind a branch.
+constexpr int kNodeScoreURegs = 32;  // doubles of U held per lane
+
+template <int MAXH>
+constexpr int node_scores_npv() { return kNodeScoreURegs / MAXH; }
+
+template <int VEC, int NP, int GL, bool CLAMP>
+__device__ __forceinline__ void ns_load_x(const float* __restrict__ xrow, int cbase, int gl, int C,
+                                          float (&xv)[NP][VEC]) {
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    const int c0 = cbase + (p * GL + gl) * VEC;
+    if constexpr (CLAMP) {
+      const bool ok = c0 < C;  // C % VEC == 0 (host)
+      float t[VEC];
+      load_vec<VEC>(xrow + (ok ? c0 : 0), t);
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) xv[p][i] = ok ? t[i] : 0.f;
+    } else {
+      load_vec<VEC>(xrow + c0, xv[p]);
+    }
+  }
+}
+
+template <int VEC, int NP, int GL, int MAXH>
+__device__ __forceinline__ void ns_load_u(const double* __restrict__ Ub, int cbase, int gl,
+                                          double (&u)[NP][VEC][MAXH]) {
+  const double* __restrict__ base = Ub + (int64_t)(cbase + gl * VEC) * MAXH;
+#pragma unroll
+  for (int p = 0; p < NP; ++p)
+#pragma unroll
+    for (int i = 0; i < VEC; ++i)
+#pragma unroll
+      for (int h = 0; h < MAXH; ++h) u[p][i][h] = base[(p * GL * VEC + i) * MAXH + h];
+}
+
+template <int VEC, int NP, int MAXH>
+__device__ __forceinline__ void ns_dot(const float (&xv)[NP][VEC], const double (&u)[NP][VEC][MAXH],
+                                       double (&acc)[MAXH]) {
+#pragma unroll
+  for (int p = 0; p < NP; ++p)
+#pragma unroll
+    for (int i = 0; i < VEC; ++i)
+#pragma unroll
+      for (int h = 0; h < MAXH; ++h) acc[h] = fma((double)xv[p][i], u[p][i][h], acc[h]);
+}
+
+// reduce over the GL lanes of a row and store cs[row, :H] from lane gl == 0
+// (branch-free buffer stores; other lanes and heads past H pass kBufNone)
+template <int GL, int MAXH>
+__device__ __forceinline__ void ns_store(double (&acc)[MAXH], const double (&vb)[MAXH], int gl, int H, bool live,
+                                         __amdgpu_buffer_rsrc_t rcs, int64_t row) {
+#pragma unroll
+  for (int o = 1; o < GL; o <<= 1)
+#pragma unroll
+    for (int h = 0; h < MAXH; ++h) acc[h] += __shfl_xor(acc[h], o);
+  const bool st = gl == 0 && live;
+#pragma unroll
+  for (int h = 0; h < MAXH; ++h)
+    buf_store_f64(rcs, (st && h < H) ? (uint32_t)((row * H + h) * 8) : kBufNone, acc[h] + vb[h]);
+}
+
+// One chunk per row: the wave's first two row groups are loaded BEFORE the key
+// projection (their HBM latency hides the LDS prologue), U[b] then sits in
+// registers and the loop keeps two row groups in flight ahead of the one being
+// reduced.  Prefetch addresses past the block's rows clamp to its last row (a
+// cache-line hit, no extra HBM traffic).
+template <int VEC, int GL, int MAXH, bool CLAMP>
+__device__ __forceinline__ void ns_block_resident(const KeyProj& kp, int64_t b, const float* __restrict__ xb,
+                                                  double* S, double* Ub, double* vl, double* xbl, __amdgpu_buffer_rsrc_t rcs,
+                                                  int64_t n0, int64_t n1, int C, int64_t ldx, int H, int Cp, int g,
+                                                  int gl, int wv) {
+  constexpr int G = kWave / GL;
+  constexpr int NP = node_scores_npv<MAXH>() / VEC;
+  const int64_t step = (int64_t)kWavesPerBlock * G;
+  const int64_t last = n1 - 1;
+  int64_t nb = n0 + wv * G;
+  float xa[NP][VEC], xn[NP][VEC];
+  ns_load_x<VEC, NP, GL, CLAMP>(xb + min(nb + g, last) * ldx, 0, gl, C, xa);
+  ns_load_x<VEC, NP, GL, CLAMP>(xb + min(nb + g + step, last) * ldx, 0, gl, C, xn);
+  key_projection_lds(kp, b, C, H, Cp, MAXH, S, Ub, vl, xbl);
+  double u[NP][VEC][MAXH];
+  ns_load_u<VEC, NP, GL, MAXH>(Ub, 0, gl, u);
+  double vb[MAXH];
+#pragma unroll
+  for (int h = 0; h < MAXH; ++h) vb[h] = vl[h];
+  for (; nb < n1; nb += step) {
+    const int64_t nr = nb + g;
+    float xf[NP][VEC];
+    ns_load_x<VEC, NP, GL, CLAMP>(xb + min(nr + 2 * step, last) * ldx, 0, gl, C, xf);
+    double acc[MAXH];
+#pragma unroll
+    for (int h = 0; h < MAXH; ++h) acc[h] = 0.0;
+    ns_dot<VEC, NP, MAXH>(xa, u, acc);
+    ns_store<GL, MAXH>(acc, vb, gl, H, nr < n1, rcs, nr);
+#pragma unroll
+    for (int p = 0; p < NP; ++p)
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) {
+        xa[p][i] = xn[p][i];
+        xn[p][i] = xf[p][i];
+      }
+  }
+}
+
+template <int VEC, int GL, int MAXH>
+__global__ __launch_bounds__(256) void node_scores_kernel(const float* __restrict__ x, int64_t B, int64_t N, int C,
+                                                           int64_t ldx, int H, int nch, KeyProj kp,
+                                                           double* __restrict__ cs, int64_t rows_per_block) {
+  extern __shared__ __attribute__((aligned(16))) double ns_lds[];  // S[att_pad] | U[Cp][MAXH] | v[MAXH] | xbar[Cp+1]
+  constexpr int G = kWave / GL;
+  constexpr int NPV = node_scores_npv<MAXH>();
+  constexpr int NP = NPV / VEC;
+  constexpr int CW = GL * NPV;
+  static_assert(NP >= 1, "node_scores: VEC wider than the per-lane column budget");
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int g = lane / GL, gl = lane % GL;
+  const int64_t n0 = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t n1 = min(N, n0 + rows_per_block);
+  const int64_t step = (int64_t)kWavesPerBlock * G;
+  const bool ragged = C != nch * CW;
+  const int Cp = nch * CW;
+  double* S = ns_lds;
+  double* Ub = ns_lds + ((kp.att + 1) & ~1);
+  double* vl = Ub + Cp * MAXH;
+  double* xbl = vl + MAXH;
+  for (int64_t b = blockIdx.y; b < B; b += gridDim.y) {
+    if (b != blockIdx.y) __syncthreads();  // the previous element's U is no longer read
+    const float* __restrict__ xb = x + b * N * ldx;
+    const __amdgpu_buffer_rsrc_t rcs = buf_rsrc(cs + b * N * H);
+    if (nch == 1) {
+      if (ragged)
+        ns_block_resident<VEC, GL, MAXH, true>(kp, b, xb, S, Ub, vl, xbl, rcs, n0, n1, C, ldx, H, Cp, g, gl, wv);
+      else
+        ns_block_resident<VEC, GL, MAXH, false>(kp, b, xb, S, Ub, vl, xbl, rcs, n0, n1, C, ldx, H, Cp, g, gl, wv);
+    } else {
+      key_projection_lds(kp, b, C, H, Cp, MAXH, S, Ub, vl, xbl);
+      double vb[MAXH];
+#pragma unroll
+      for (int h = 0; h < MAXH; ++h) vb[h] = vl[h];
+      for (int64_t nb = n0 + wv * G; nb < n1; nb += step) {
+        const int64_t nr = nb + g;
+        const float* xrow = xb + min(nr, N - 1) * ldx;
+        double acc[MAXH];
+#pragma unroll
+        for (int h = 0; h < MAXH; ++h) acc[h] = 0.0;
+        for (int ch = 0; ch < nch; ++ch) {
+          double u[NP][VEC][MAXH];
+          float xc[NP][VEC];
+          ns_load_x<VEC, NP, GL, true>(xrow, ch * CW, gl, C, xc);
+          ns_load_u<VEC, NP, GL, MAXH>(Ub, ch * CW, gl, u);
+          ns_dot<VEC, NP, MAXH>(xc, u, acc);
+        }
+        ns_store<GL, MAXH>(acc, vb, gl, H, nr < n1, rcs, nr);
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------ host helpers
+static int pow2_at_least(int v, int cap) {
+  int p = 1;
+  while (p < v && p < cap) p <<= 1;
+  return p;
+}
+
+constexpr int kKeysumTilesTarget = 1024;
+
+static int keysum_vec(int64_t C, const float* x, int64_t ldx) {
+  if (C % 4 == 0 && ldx % 4 == 0 && aligned16(x)) return 4;
+  if (C % 2 == 0 && ldx % 2 == 0 && aligned8(x)) return 2;
+  return 1;
+}
+
+// tiles of rows for the partial column sums (independent of the vector width)
+static void keysum_tiles(int64_t B, int64_t N, int* rows_per_tile, int* ntiles) {
+  const int64_t per_batch = std::max<int64_t>(1, kKeysumTilesTarget / B);
+  const int64_t rpt = std::max<int64_t>(ceil_div(N, per_batch), 1);
+  *rows_per_tile = (int)rpt;
+  *ntiles = (int)ceil_div(N, rpt);
+}
+
+template <int MAXH>
+static void launch_stats(unsigned grid, int GL, hipStream_t s, const int4* it, int n, const int* gidx, int gid,
+                         const ScoreArgs& sa, double* m, float* rl, double* partials) {
+  if (GL == 8)
+    stats_kernel<MAXH, 8><<<grid, kBlock, 0, s>>>(it, n, gidx, gid, sa, m, rl, partials);
+  else
+    stats_kernel<MAXH, 64><<<grid, kBlock, 0, s>>>(it, n, gidx, gid, sa, m, rl, partials);
+}
+
+// node_scores geometry: VEC, MAXH (= Hp), lanes per row GL (8..64) so one
+// chunk of CW = GL*NPV columns covers the row when it can, nch chunks.
+struct NsGeom {
+  int vec, maxh, GL, CW, nch;
+};
+
+static NsGeom ns_geometry(int vec, int64_t C, int64_t H) {
+  NsGeom g;
+  g.maxh = H <= 1 ? 1 : H <= 2 ? 2 : H <= 4 ? 4 : H <= 8 ? 8 : 16;
+  const int npv = kNodeScoreURegs / g.maxh;
+  g.vec = (vec == 4 && npv >= 4) ? 4 : 1;
+  g.GL = std::max(8, pow2_at_least((int)ceil_div(C, npv), 64));
+  g.CW = g.GL * npv;
+  g.nch = (int)ceil_div(C, g.CW);
+  return g;
+}
+
+static size_t ns_lds_bytes(const NsGeom& ge, int att) {
+  const int64_t cp = (int64_t)ge.nch * ge.CW;  // >= C
+  return sizeof(double) * (size_t)(((att + 1) & ~1) + cp * ge.maxh + ge.maxh + cp + 1);
+}
+
+template <int VEC, int MAXH>
+static void launch_node_scores(dim3 grid, const NsGeom& ge, hipStream_t s, const float* x, int64_t B, int64_t N, int C,
+                               int64_t ldx, int H, const KeyProj& kp, double* cs, int64_t rpb) {
+  const int n = ge.nch;
+  const size_t shm = ns_lds_bytes(ge, kp.att);
+  if (ge.GL <= 8)
+    node_scores_kernel<VEC, 8, MAXH><<<grid, kBlock, shm, s>>>(x, B, N, C, ldx, H, n, kp, cs, rpb);
+  else if (ge.GL <= 16)
+    node_scores_kernel<VEC, 16, MAXH><<<grid, kBlock, shm, s>>>(x, B, N, C, ldx, H, n, kp, cs, rpb);
+  else if (ge.GL <= 32)
+    node_scores_kernel<VEC, 32, MAXH><<<grid, kBlock, shm, s>>>(x, B, N, C, ldx, H, n, kp, cs, rpb);
+  else
+    node_scores_kernel<VEC, 64, MAXH><<<grid, kBlock, shm, s>>>(x, B, N, C, ldx, H, n, kp, cs, rpb);
+}
+
+// rows per block sized for ~2048 wavefronts over the whole launch: the kernel
+// holds ~210 VGPRs (U[b] in registers + two row groups in flight), so 2 waves
+// per SIMD = 2 blocks per CU are resident and the whole grid runs in one round
+// (4096 waves left a 1.7-round tail: 26.9 us for an 87 MB pass)
+static void launch_node_scores_any(hipStream_t s, const NsGeom& ge, const float* x, int64_t B, int64_t N, int C,
+                                   int64_t ldx, int H, const KeyProj& kp, double* cs) {
+  const int G = kWave / ge.GL;
+  const int64_t groups = ceil_div(N, (int64_t)G);
+  const int64_t waves_per_batch = std::max<int64_t>(1, 2048 / B);
+  const int64_t iters = std::max<int64_t>(1, ceil_div(groups, waves_per_batch));
+  const int64_t rpb = (int64_t)kWavesPerBlock * G * iters;
+  const dim3 grid((unsigned)ceil_div(N, rpb), (unsigned)std::min<int64_t>(B, 65535));
+#define GNPDE_NS(V, M) launch_node_scores<V, M>(grid, ge, s, x, B, N, C, ldx, H, kp, cs, rpb)
+  if (ge.vec == 4) {
+    switch (ge.maxh) {
+      case 1: GNPDE_NS(4, 1); break;
+      case 2: GNPDE_NS(4, 2); break;
+      case 4: GNPDE_NS(4, 4); break;
+      default: GNPDE_NS(4, 8); break;
+    }
+  } else {
+    switch (ge.maxh) {
+      case 1: GNPDE_NS(1, 1); break;
+      case 2: GNPDE_NS(1, 2); break;
+      case 4: GNPDE_NS(1, 4); break;
+      case 8: GNPDE_NS(1, 8); break;
+      default: GNPDE_NS(1, 16); break;
+    }
+  }
+#undef GNPDE_NS
+}
+
+static unsigned edge_grid(int64_t nnz) {
+  return (unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(nnz, kBlock), 16384));
+}
+
+// a block takes kWavesPerBlock * 64 consecutive edges per pass (T per team)
+static unsigned team_grid(int64_t nnz, const Team& tm) {
+  const int64_t per_block = (int64_t)kWavesPerBlock * (kWave / tm.T) * tm.T;
+  return (unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(nnz, per_block), 32768));
+}
+
+}  // namespace gnpde
+
+using namespace gnpde;
+
+extern "C" {
+
+int gnpde_softmax_stats_f32(const int32_t* items, int64_t n_items, const int32_t* heavy, int64_t n_heavy,
+                            const int32_t* gidx, int group_is_dst, int mode, int64_t heads, int64_t dk,
+                            const double* cs, const float* q, const float* k, int64_t ldqk, float score_p0,
+                            float score_p1, double* m, float* rl, double* partials, void* stream) {
+  int rc = check_score_args(mode, heads, dk, cs, q, k);
+  if (rc) return rc;
+  GNPDE_REQUIRE(m && rl, GNPDE_EINVAL, "softmax_stats: NULL m/rl");
+  GNPDE_REQUIRE(n_heavy == 0 || partials, GNPDE_EINVAL, "softmax_stats: hub groups need partials");
+  if (n_items == 0) return GNPDE_OK;
+  GNPDE_REQUIRE(items && gidx, GNPDE_EINVAL, "softmax_stats: NULL items/gidx");
+  const ScoreArgs sa = make_score_args(mode, heads, dk, cs, q, k, ldqk, score_p0, score_p1);
+  hipStream_t s = as_stream(stream);
+  const int4* it = reinterpret_cast<const int4*>(items);
+  const Team tm = team_geometry(sa);
+  if (tm.T > 0) {
+    const unsigned grid = (unsigned)ceil_div(n_items, (int64_t)kWavesPerBlock * (kWave / tm.T));
+    stats_team_kernel<4><<<grid, kBlock, 0, s>>>(it, (int)n_items, gidx, group_is_dst, sa, tm, m, rl, partials);
+    GNPDE_LAUNCH_CHECK();
+  } else {
+  const int GL = 8;  // lanes per item
+  const unsigned grid = (unsigned)ceil_div(n_items, (int64_t)kWavesPerBlock * (kWave / GL));
+  if (heads <= 1)
+    launch_stats<1>(grid, GL, s, it, (int)n_items, gidx, group_is_dst, sa, m, rl, partials);
+  else if (heads <= 2)
+    launch_stats<2>(grid, GL, s, it, (int)n_items, gidx, group_is_dst, sa, m, rl, partials);
+  else if (heads <= 4)
+    launch_stats<4>(grid, GL, s, it, (int)n_items, gidx, group_is_dst, sa, m, rl, partials);
+  else if (heads <= 8)
+    launch_stats<8>(grid, GL, s, it, (int)n_items, gidx, group_is_dst, sa, m, rl, partials);
+  else
+    launch_stats<16>(grid, GL, s, it, (int)n_items, gidx, group_is_dst, sa, m, rl, partials);
+  GNPDE_LAUNCH_CHECK();
+  }
+  return launch_stats_fixup(reinterpret_cast<const int4*>(heavy), n_heavy, (int)heads, partials, m, rl, s);
+}
+
+int gnpde_attn_weights_f32(const int32_t* rowidx, const int32_t* col, int64_t nnz, int norm_idx, int mode,
+                           int64_t heads, int64_t dk, const double* cs, const float* q, const float* k, int64_t ldqk,
+                           float score_p0, float score_p1, const double* m, const float* rl, float* w_out,
+                           void* stream) {
+  int rc = check_score_args(mode, heads, dk, cs, q, k);
+  if (rc) return rc;
+  GNPDE_REQUIRE(norm_idx == 0 || norm_idx == 1, GNPDE_EINVAL, "attn_weights: norm_idx must be 0 or 1");
+  if (nnz == 0) return GNPDE_OK;
+  GNPDE_REQUIRE(rowidx && col && m && rl && w_out, GNPDE_EINVAL, "attn_weights: NULL pointer");
+  const ScoreArgs sa = make_score_args(mode, heads, dk, cs, q, k, ldqk, score_p0, score_p1);
+  Team tm = team_geometry(sa);
+  if ((uint64_t)nnz * 4 >= kBufRecords) tm.T = 0;  // buffer-store offsets are 32-bit
+  if (tm.T > 0)
+    attn_team_kernel<4, false><<<team_grid(nnz, tm), kBlock, 0, as_stream(stream)>>>(rowidx, col, nullptr, nnz, norm_idx,
+                                                                                    sa, tm, m, rl, w_out);
+  else
+    attn_weights_kernel<<<edge_grid(nnz), kBlock, 0, as_stream(stream)>>>(rowidx, col, nnz, norm_idx, sa, m, rl,
+                                                                          w_out);
+  GNPDE_LAUNCH_CHECK();
+  return GNPDE_OK;
+}
+
+int gnpde_edge_attention_f32(const int32_t* rowidx, const int32_t* col, const int32_t* perm, int64_t nnz,
+                             int norm_idx, int mode, int64_t heads, int64_t dk, const double* cs, const float* q,
+                             const float* k, int64_t ldqk, float score_p0, float score_p1, const double* m,
+                             const float* rl, float* att, void* stream) {
+  int rc = check_score_args(mode, heads, dk, cs, q, k);
+  if (rc) return rc;
+  GNPDE_REQUIRE(norm_idx == 0 || norm_idx == 1, GNPDE_EINVAL, "edge_attention: norm_idx must be 0 or 1");
+  if (nnz == 0) return GNPDE_OK;
+  GNPDE_REQUIRE(rowidx && col && perm && m && rl && att, GNPDE_EINVAL, "edge_attention: NULL pointer");
+  const ScoreArgs sa = make_score_args(mode, heads, dk, cs, q, k, ldqk, score_p0, score_p1);
+  Team tm = team_geometry(sa);
+  if ((uint64_t)nnz * heads * 4 >= kBufRecords) tm.T = 0;  // buffer-store offsets are 32-bit
+  if (tm.T > 0)
+    attn_team_kernel<4, true><<<team_grid(nnz, tm), kBlock, 0, as_stream(stream)>>>(rowidx, col, perm, nnz, norm_idx, sa,
+                                                                                   tm, m, rl, att);
+  else
+    edge_attention_kernel<<<edge_grid(nnz), kBlock, 0, as_stream(stream)>>>(rowidx, col, perm, nnz, norm_idx, sa, m,
+                                                                            rl, att);
+  GNPDE_LAUNCH_CHECK();
+  return GNPDE_OK;
+}
+
+size_t gnpde_keysum_workspace_bytes(int64_t B, int64_t N, int64_t C, int64_t att) {
+  (void)att;
+  int rpt, ntiles;
+  keysum_tiles(B, N, &rpt, &ntiles);
+  const int64_t ngroups = ceil_div(ntiles, kKeysumGroup);
+  // tickets (B * ngroups ints, 256-B aligned) | tile partials | group partials
+  const size_t tick = (size_t)ceil_div(B * ngroups * (int64_t)sizeof(int), 256) * 256;
+  return tick + sizeof(double) * (size_t)(B * (ntiles + ngroups) * (C + 1));
+}
+
+size_t gnpde_keysum_ticket_bytes(int64_t B, int64_t N) {
+  int rpt, ntiles;
+  keysum_tiles(B, N, &rpt, &ntiles);
+  return (size_t)ceil_div(B * ceil_div(ntiles, kKeysumGroup) * (int64_t)sizeof(int), 256) * 256;
+}
+
+int gnpde_ref_scores_f32(const float* x, int64_t B, int64_t N, int64_t C, int64_t ldx, const int32_t* indeg,
+                         const float* Wq, const float* bq, const float* Wk, const float* bk, int64_t att,
+                         int64_t heads, double* cs, void* workspace, size_t workspace_bytes, void* stream) {
+  GNPDE_REQUIRE(x && indeg && Wq && bq && Wk && bk && cs && workspace, GNPDE_EINVAL, "ref_scores: NULL pointer");
+  GNPDE_REQUIRE(B >= 1 && N >= 1 && C >= 1 && ldx >= C, GNPDE_EINVAL, "ref_scores: bad sizes");
+  GNPDE_REQUIRE(heads >= 1 && heads <= 16 && att % heads == 0, GNPDE_EUNSUPPORTED,
+                "ref_scores: heads must divide attention_dim and be <= 16");
+  GNPDE_REQUIRE(workspace_bytes >= gnpde_keysum_workspace_bytes(B, N, C, att), GNPDE_EINVAL,
+                "ref_scores: workspace too small");
+  GNPDE_REQUIRE(att <= 4096, GNPDE_EUNSUPPORTED, "ref_scores: attention_dim too large");
+  GNPDE_REQUIRE((uint64_t)N * heads * 8 < kBufRecords, GNPDE_EUNSUPPORTED, "ref_scores: N*heads too large");
+  hipStream_t s = as_stream(stream);
+  const int vec = keysum_vec(C, x, ldx);
+  const int tpr = pow2_at_least((int)ceil_div(C, vec), 256);
+  int rpt, ntiles;
+  keysum_tiles(B, N, &rpt, &ntiles);
+  const int ngroups = (int)ceil_div(ntiles, kKeysumGroup);
+  int* tickets = static_cast<int*>(workspace);
+  double* part = reinterpret_cast<double*>(static_cast<char*>(workspace) + gnpde_keysum_ticket_bytes(B, N));
+  double* gpart = part + B * ntiles * (C + 1);
+  const NsGeom ge = ns_geometry(vec, C, heads);
+  GNPDE_REQUIRE(ns_lds_bytes(ge, (int)att) <= 64 * 1024, GNPDE_EUNSUPPORTED,
+                "ref_scores: key projection (attention_dim %lld, C %lld) does not fit the LDS", (long long)att,
+                (long long)C);
+  const int rpb = kBlock / tpr;
+  const size_t shm = sizeof(double) * (size_t)rpb * (C + 1);
+  GNPDE_REQUIRE(shm <= 64 * 1024, GNPDE_EUNSUPPORTED, "ref_scores: C too large");
+  GNPDE_REQUIRE((uint64_t)B * (C + 1) * ntiles * 8 < kBufRecords, GNPDE_EUNSUPPORTED, "ref_scores: partials too large");
+  const dim3 g1((unsigned)ntiles, (unsigned)B);
+#define GNPDE_KS(V)                                                                                              \
+  keysum_partial_kernel<V><<<g1, kBlock, shm, s>>>(x, N, (int)C, ldx, indeg, rpt, tpr, ntiles, part, gpart, ngroups, \
+                                                   tickets)
+  if (vec == 4)
+    GNPDE_KS(4);
+  else if (vec == 2)
+    GNPDE_KS(2);
+  else
+    GNPDE_KS(1);
+#undef GNPDE_KS
+  GNPDE_LAUNCH_CHECK();
+  const KeyProj kp{gpart, ngroups, Wq, bq, Wk, bk, (int)att};
+  launch_node_scores_any(s, ge, x, B, N, (int)C, ldx, (int)heads, kp, cs);
+  GNPDE_LAUNCH_CHECK();
+  return GNPDE_OK;
+}
+
+}  // extern "C"

@@ -61,6 +61,7 @@ SIGNATURES = {
                                       _vp, _vp, _int, _vp, _i64, _vp, ctypes.POINTER(StageEpilogue), _vp]),
     "gnpde_linear_f32": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _vp]),
     "gnpde_keysum_workspace_bytes": (_size, [_i64, _i64, _i64, _i64]),
+    "gnpde_keysum_ticket_bytes": (_size, [_i64, _i64]),
     "gnpde_ref_scores_f32": (_int, [_vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _vp, _vp,
                                     _size, _vp]),
     "gnpde_softmax_stats_f32": (_int, [_vp, _i64, _vp, _i64, _vp, _int, _int, _i64, _i64, _vp, _vp, _vp, _i64, _f32,

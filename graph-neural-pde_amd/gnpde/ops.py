@@ -666,6 +666,21 @@ class NodeScores(object):
         self.ldqk = q.shape[1] if q is not None else 1
 
 
+_KEYSUM_WS = {}
+
+
+def _keysum_workspace(dev, nbytes):
+    """Key-sum workspace of gnpde_ref_scores_f32: its arrival tickets must be zero
+    on entry and every call leaves them zero, so one zeroed buffer per device,
+    stream and size is kept and reused (also by captured step graphs)."""
+    key = (str(dev), torch.cuda.current_stream(dev).cuda_stream, int(nbytes))
+    ws = _KEYSUM_WS.get(key)
+    if ws is None:
+        ws = torch.zeros(int(nbytes), dtype=torch.uint8, device=dev)
+        _KEYSUM_WS[key] = ws
+    return ws
+
+
 def node_scores(g, x, Wq, bq, Wk, bk, heads, attention_type='scaled_dot', score_mode='reference',
                 output_var=1.0, lengthscale=1.0, wcat=None):
     """Q/K-side work of SpGraphTransAttentionLayer.forward (function_transformer_attention.py:224-259)."""
@@ -679,7 +694,7 @@ def node_scores(g, x, Wq, bq, Wk, bk, heads, attention_type='scaled_dot', score_
         B, N, C = g.B, g.N, xr.shape[1]
         cs = torch.empty(g.R, heads, dtype=torch.float64, device=xr.device)
         ws_bytes = _lib.fn("gnpde_keysum_workspace_bytes")(B, N, C, att)
-        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=xr.device)
+        ws = _keysum_workspace(xr.device, ws_bytes)
         for name, t in (("Wq", Wq), ("bq", bq), ("Wk", Wk), ("bk", bk)):
             _require_gpu(t, name, torch.float32)
         _lib.call("gnpde_ref_scores_f32", _ptr(xr), B, N, C, C, _ptr(g.indeg), _ptr(Wq.contiguous()),

@@ -238,7 +238,9 @@ int gnpde_attn_ref_rhs_f32(const int32_t* items, int64_t n_items, int32_t* heavy
                            const gnpde_stage_epilogue_t* stage, void* stream);
 
 /* ---------------------------------------------------------------- attention
- * Node-level projection (MFMA, v_mfma_f32_32x32x2_f32):
+ * Node-level projection on the matrix cores (K % 16 == 0, K <= 128: exact
+ * three-piece bf16 splits of both operands on v_mfma_f32_32x32x16_bf16, f32-GEMM
+ * accuracy; other shapes: v_mfma_f32_32x32x2_f32):
  *   out[r, j] = sum_k x[r,k] * W[j,k] + bias[j], j < Nout; columns [0, split)
  *   go to out_a (ld lda), [split, Nout) to out_b (ld ldb).
  * Replaces the nn.Linear Q/K of function_transformer_attention.py:224-225.  */
@@ -250,9 +252,14 @@ int gnpde_linear_f32(const float* x, int64_t R, int64_t K, int64_t ldx, const fl
  *   S_b = Wk * (sum_n indeg(n) x_n) + (sum_n indeg(n)) bk    (fp64)
  *   cs[r,h] = (q_r,h . S_b,h) / sqrt(dk),  q = Wq x + bq      (fp64 out)
  * indeg: in-degree per global node (int32, R); ws: gnpde_keysum_workspace_bytes.
- * Three launches: indegree-weighted column sums (fp64 row tiles), the fixed-order
- * tile reduction, then the node scores, whose workgroups each form S_b and
- * U = Wq^T S / sqrt(dk) in LDS.  attention_dim <= 4096.                      */
+ * Two launches: indegree-weighted column sums (fp64 row tiles; the last tile of
+ * each group of 32 to finish sums the group, through an arrival ticket), then
+ * the node scores, whose workgroups each sum the group partials and form S_b
+ * and U = Wq^T S / sqrt(dk) in LDS.  attention_dim <= 4096.
+ * Workspace contract: its first gnpde_keysum_ticket_bytes(B, N) bytes are the
+ * arrival tickets — zero before the first call, left zero by every call — so
+ * keep one workspace per stream (calls on one workspace must not overlap).  */
+size_t gnpde_keysum_ticket_bytes(int64_t B, int64_t N);
 size_t gnpde_keysum_workspace_bytes(int64_t B, int64_t N, int64_t C, int64_t att);
 int gnpde_ref_scores_f32(const float* x, int64_t B, int64_t N, int64_t C, int64_t ldx, const int32_t* indeg,
                          const float* Wq, const float* bq, const float* Wk, const float* bk,
