@@ -131,6 +131,16 @@ __device__ __forceinline__ void hub_combine(int row, int first, int nch, int C, 
 // and if it arrived last, acquire and combine the hub row, then reset the
 // ticket to 0 for the next launch on this plan.  Hubs are found by a binary
 // search of the ascending first slots (log2(n_heavy) L2 reads, chunk waves only).
+// Memory order of the arrival ticket.  The partials are stored write-through and
+// drained (s_waitcnt vmcnt(0)) before the ticket, which is what an agent-scope
+// release orders at the ISA level; GNPDE_HUB_RELEASE=1 builds the ticket as a
+// formal C++ release as well (it adds buffer_wbl2 sc1: a write-back of every
+// dirty line of the XCD's L2 before each chunk's ticket).
+#ifndef GNPDE_HUB_RELEASE
+#define GNPDE_HUB_RELEASE 0
+#endif
+constexpr int kHubTicketOrder = GNPDE_HUB_RELEASE ? __ATOMIC_RELEASE : __ATOMIC_RELAXED;
+
 template <int VEC, int GL, int STG, class T>
 __device__ __forceinline__ void hub_arrive(int4* heavy, int n_heavy, int slot, int C, const Epi& ep,
                                            const float* partials) {
@@ -147,7 +157,7 @@ __device__ __forceinline__ void hub_arrive(int4* heavy, int n_heavy, int slot, i
   int* ticket_word = &heavy[lo].w;
   int ticket = 0;
   if ((threadIdx.x & 63) == 0)
-    ticket = __hip_atomic_fetch_add(ticket_word, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    ticket = __hip_atomic_fetch_add(ticket_word, 1, kHubTicketOrder, __HIP_MEMORY_SCOPE_AGENT);
   ticket = __shfl(ticket, 0);
   if (ticket != nch - 1) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -176,7 +186,7 @@ __device__ __forceinline__ void hub_arrive_slots(int4* heavy, int n_heavy, bool 
         hi = mid - 1;
     }
     if (lane % SL == 0) {
-      const int t = __hip_atomic_fetch_add(&heavy[lo].w, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int t = __hip_atomic_fetch_add(&heavy[lo].w, 1, kHubTicketOrder, __HIP_MEMORY_SCOPE_AGENT);
       won = t == heavy[lo].z - 1;
     }
   }

@@ -256,13 +256,39 @@ class ColumnShardedLaplacian(object):
         self.add_source, self.alpha_sigmoid = add_source, alpha_sigmoid
         self.nfe = 0
         self.local_rhs = local_rhs
+        self._layout = None   # the NodeLayout a fixed-grid solve runs in (gnpde.integrator), else None
+        self._lay_ops = None  # (layout, its CSR-order weights, its x0 stripe)
         if local_rhs is None:
+            self.edge_weight = edge_weight
             self.g = ops.GraphCSR(edge_index, self.N, chunk=chunk)
             self.w = self.g.gather_weights(edge_weight)
 
+    def node_layout(self, x_local):
+        """The graph's locality numbering for a fixed-grid solve of the stripes
+        (ops.NodeLayout), decided on the FULL state's size so that every rank of
+        a job — and the unsharded run it is compared with — runs the same
+        numbering.  Bit-identical results (the stripe's rows are permuted, each
+        row keeps its edges and their order)."""
+        if self._layout is not None or self.local_rhs is not None or x_local.dim() != 3:
+            return None
+        if not ops.layout_worthwhile(x_local.shape[0] * x_local.shape[1], self.C, x_local.element_size()):
+            return None
+        return self.g.node_layout
+
+    def _operands(self):
+        """(graph, CSR-order weights, x0 stripe) in the numbering of the running solve."""
+        lay = self._layout
+        if lay is None:
+            return self.g, self.w, self.x0_local
+        if self._lay_ops is None or self._lay_ops[0] is not lay:
+            x0 = lay.to_internal(self.x0_local) if (self.add_source and self.x0_local is not None) else None
+            self._lay_ops = (lay, lay.graph.gather_weights(self.edge_weight), x0)
+        return lay.graph, self._lay_ops[1], self._lay_ops[2]
+
     def graph_capture_state(self, x):
         """What a captured fused step reads (gnpde.integrator._capture_state)."""
-        return (self.g, self.w) + ((self.x0_local,) if self.add_source else ())
+        g, w, x0 = self._operands()
+        return (g, w) + ((x0,) if self.add_source else ())
 
     def capture_key_tensors(self):
         return tuple(t for t in (self.alpha, self.beta) if isinstance(t, torch.Tensor))
@@ -282,7 +308,8 @@ class ColumnShardedLaplacian(object):
         self.nfe += 1
         if self.local_rhs is not None:
             raise NotImplementedError
-        ops.spmm_rhs(self.g, self.w, x_local, x0=self.x0_local, alpha=self.alpha, beta=self.beta,
+        g, w, x0 = self._operands()
+        ops.spmm_rhs(g, w, x_local, x0=x0, alpha=self.alpha, beta=self.beta,
                      alpha_sigmoid=self.alpha_sigmoid, add_source=self.add_source, stage=stage)
 
     def global_rms_norm(self, t):

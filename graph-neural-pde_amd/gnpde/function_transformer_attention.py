@@ -346,6 +346,16 @@ class ODEFuncTransformerAtt(ODEFunc):
             st.append(self.stable_x0(x))
         return st
 
+    def supports_node_layout(self):
+        """The graph's locality numbering (ops.NodeLayout) is offered when the
+        attention weights are the graph-only 1/outdeg (BLEND: the fork's
+        scaled_dot under source-grouped softmax): every operand is then per node
+        or per edge and the renumbered solve is bit-identical.  Score modes are
+        not renumbered: the reference scores sum a key over all nodes (fp64, in
+        row-tile order) and the per-edge softmax scans depend on where a group
+        sits in its packed edge block — both would round differently."""
+        return self.multihead_att_layer.is_uniform(int(self.opt['attention_norm_idx']))
+
     def supports_feature_padding(self):
         """With the fork's scaled_dot under source-grouped softmax the weights do
         not depend on x (1/outdeg), so columns are independent and the fused

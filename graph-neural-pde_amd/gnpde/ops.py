@@ -345,7 +345,8 @@ class GraphCSR(object):
 # gathered rows live, not when they are gathered.  "none" disables.
 NODE_ORDER = os.environ.get("GNPDE_NODE_ORDER", "degree")
 LAYOUT_MIN_ROWS = 32768          # below this the state sits in L2 / the Infinity Cache anyway
-LAYOUT_MIN_BYTES = 16 << 20      # and the two permutations would cost more than they save
+# and the two permutations would cost more than they save (GNPDE_LAYOUT_MIN_MB overrides)
+LAYOUT_MIN_BYTES = int(float(os.environ.get("GNPDE_LAYOUT_MIN_MB", 16)) * (1 << 20))
 
 
 class NodeLayout(object):

@@ -74,6 +74,29 @@ def test_layout_batched_padded_and_bf16():
         assert torch.equal(got, ref), (C, dtype)
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_layout_blend_transformer_bit_identical(dtype):
+    """configs[3] shape: the transformer RHS with the fork's scaled_dot under
+    source-grouped softmax (1/outdeg weights), C = 162 (zero-padded width)."""
+    N, E, C = 60000, 450000, 162  # >= 16 MB in bf16 too (ops.LAYOUT_MIN_BYTES)
+    ei, _ = synthetic.rw_graph(N, E, seed=31, device=DEV)
+    opt = dict(OPT, hidden_dim=C, heads=2, attention_dim=32, attention_norm_idx=0, attention_type='scaled_dot',
+               function='transformer', mix_features=False, square_plus=False, beltrami=False)
+    func = gnpde.ODEFuncTransformerAtt(C, C, opt, DEV).to(DEV).eval()
+    func.edge_index = ei
+    x = synthetic.features(1, N, C, seed=8, device=DEV).to(dtype)
+    lay = func.node_layout(x)
+    assert lay is not None
+    ref = _solve(func, x, "rk4", 7, 0.25, "none")
+    got = _solve(func, x, "rk4", 7, 0.25, "degree")
+    assert torch.equal(got, ref)
+    # score modes keep the user numbering
+    opt2 = dict(opt, attention_norm_idx=1)
+    f2 = gnpde.ODEFuncTransformerAtt(C, C, opt2, DEV).to(DEV).eval()
+    f2.edge_index = ei
+    assert f2.node_layout(x) is None
+
+
 def test_node_layout_structure():
     N, E = 40000, 300000
     func = _func(N, E, 128, 2, False, seed=21)
@@ -95,3 +118,33 @@ def test_node_layout_structure():
     # small states are not renumbered
     small = _func(2000, 12000, 64, 1, False)
     assert small.node_layout(torch.zeros(1, 2000, 64, device=DEV)) is None
+
+
+def test_layout_column_stripes_bit_identical():
+    """gnpde.dist.ColumnShardedLaplacian (the multi-GPU headline layout) solves its
+    stripe in the same numbering as the unsharded run: a world of one (gloo
+    group, no collective on the fixed-grid path), layout on vs off vs the
+    unsharded LaplacianODEFunc — all bit-identical."""
+    import random
+    import torch.distributed as dist
+    from gnpde import dist as gd
+    N, E, C = 40000, 300000, 128
+    ei, w = synthetic.rw_graph(N, E, seed=41, device=DEV)
+    x = synthetic.features(1, N, C, seed=9, device=DEV)
+    own = not dist.is_initialized()
+    if own:
+        dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % random.randint(20000, 40000), rank=0,
+                                world_size=1)
+    try:
+        alpha = torch.tensor(0.3, device=DEV)
+        sh = gd.ColumnShardedLaplacian(ei, w, N, C, alpha)
+        assert sh.node_layout(sh.split(x)) is not None
+        ref = _solve(sh, sh.split(x), "rk4", 9, 0.1, "none")
+        got = _solve(sh, sh.split(x), "rk4", 9, 0.1, "degree")
+        assert sh._layout is None and sh._lay_ops is not None
+        assert torch.equal(got, ref)
+        func = _func(N, E, C, 1, False, seed=41)
+        assert torch.equal(_solve(func, x, "rk4", 9, 0.1, "degree"), ref)
+    finally:
+        if own:
+            dist.destroy_process_group()
