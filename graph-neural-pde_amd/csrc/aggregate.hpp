@@ -452,6 +452,8 @@ static int launch_agg_vec(const int4* items, int64_t n_items, int4* heavy, int64
   if constexpr (sizeof(T) == 2 && VEC == 8) {
     // bf16 rows of 129-168 columns (BLEND: C = 162 padded to 168 = 21 lanes of 16 B):
     // three rows per wavefront, 63 of 64 lanes busy (GNPDE_AGG_VARIANT=9: two rows, 21 of 32)
+    if (lanes > 16 && lanes <= 21 && agg_variant() == 10) return GNPDE_AGG(21, 1, 8, 3);  // 8 edges in flight
+    if (lanes > 16 && lanes <= 21 && agg_variant() == 11) return GNPDE_AGG(21, 1, 2, 3);  // 2 edges in flight
     if (lanes > 16 && lanes <= 21 && agg_variant() != 9) return GNPDE_AGG(21, 1, 4, 3);
   }
   if (lanes <= 32) {
