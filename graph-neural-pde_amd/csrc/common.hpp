@@ -167,8 +167,18 @@ __device__ __forceinline__ int xcd_block(int remap) {
   const int b = blockIdx.x;
   if (!remap) return b;
   const int nb = gridDim.x;
-  const int q = nb / kNumXcd, r = nb % kNumXcd;
   const int x = b % kNumXcd, k = b / kNumXcd;
+  if (remap >= 2) {
+    // chunks of `remap` consecutive blocks, chunk i on XCD i % 8: each XCD walks
+    // runs of neighbouring items (L2 locality) while every XCD still samples
+    // every part of the item list (load balance).  Blocks past the last whole
+    // round of chunks keep the hardware's order.
+    const int K = remap, round = K * kNumXcd;
+    const int whole = nb / round * round;
+    if (b >= whole) return b;
+    return ((k / K) * kNumXcd + x) * K + (k % K);
+  }
+  const int q = nb / kNumXcd, r = nb % kNumXcd;
   return x < r ? x * (q + 1) + k : r * (q + 1) + (x - r) * q + k;
 }
 

@@ -37,11 +37,12 @@ inline ScoreArgs make_score_args(int mode, int64_t heads, int64_t dk, const doub
 }
 
 // Experiment knob (not part of the ABI contract): GNPDE_XCD_REMAP=1 maps
-// contiguous runs of K1 work items to one XCD (common.hpp xcd_block).
+// contiguous eighths of the K1 work items to one XCD each; =K (>= 2) deals
+// chunks of K consecutive blocks to the XCDs in turn (common.hpp xcd_block).
 inline int xcd_remap_enabled() {
   static const int on = [] {
     const char* e = std::getenv("GNPDE_XCD_REMAP");
-    return (e && e[0] == '1') ? 1 : 0;
+    return e ? std::max(0, std::atoi(e)) : 0;
   }();
   return on;
 }
