@@ -97,6 +97,7 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU-baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-attention", action="store_true")
+    p.add_argument("--no-train", action="store_true", help="skip the training-step (forward + backward) measurement")
     p.add_argument("--no-grmat", action="store_true", help="skip the configs[4] graph (G-rmat) measurements")
     p.add_argument("--grmat-steps", type=int, default=10, help="timed rk4 steps on G-rmat")
     p.add_argument("--rhs-only", action="store_true", help="time K plain RHS calls instead of rk4 steps")
@@ -160,12 +161,14 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    mode = args.mode if args.mode != "auto" else ("replicas" if world == 1 else "cols")
+    if world > 1 or (mode != "replicas" and "MASTER_ADDR" in os.environ):
+        # one process per GPU under torch.distributed.run: RCCL through env:// (a
+        # world of one too, so a one-GPU rehearsal takes the N > 1 code path)
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
-    mode = args.mode if args.mode != "auto" else ("replicas" if world == 1 else "cols")
     if mode == "replicas":
         result = bench_single(args, world, rank, dev)
     else:
@@ -174,7 +177,7 @@ def main():
         result["grmat"] = bench_grmat(args, world, rank, dev)
     if rank == 0:
         print(json.dumps(result))
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
 
@@ -302,9 +305,14 @@ def bench_single(args, world, rank, dev):
         "rhs_plain": plain,
     }
 
+    progress("headline: %.1f RHS evals/s" % value)
     if not args.no_attention and rank == 0:
         result["attention"] = bench_attention(g, x, dev, ops)
+        progress("attention done")
         result["blend_c162"] = bench_blend(g, dev)
+        progress("blend done")
+    if not args.no_train and rank == 0 and world == 1:
+        result["train_rk4"] = bench_train(ei, w, x, h, dev)
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(ei, w, x, N, E, C, args.cpu_seconds)
@@ -373,17 +381,27 @@ def bench_sharded(args, world, rank, dev, mode):
     }
 
 
+def progress(*a):
+    """One line to stderr per bench phase (long sharded / G-rmat phases stay visibly alive)."""
+    print("[bench %.1fs]" % (time.perf_counter() - T_START), *a, file=sys.stderr, flush=True)
+
+
+T_START = time.perf_counter()
+
+
 def sharded_point(N, E, C, h, steps, warmup, world, dev, mode, seed=0):
     """RHS evals/s of one graph in `mode` over the job's ranks, and the same graph
     integrated unsharded on one GPU (every rank at once, max over ranks)."""
     import gnpde
     from gnpde import dist as gd, synthetic
+    progress("sharded point: N=%d E=%d C=%d mode=%s world=%d" % (N, E, C, mode, world))
     ei, w = synthetic.rw_graph(N, E, seed=seed, device=dev)
     x = synthetic.features(1, N, C, seed=1 + seed, device=dev)
     # the 1-GPU point of the curve: the whole graph on this rank's GPU
     func = gnpde.LaplacianODEFunc(C, C, dict(LAP_OPT, hidden_dim=C), dev).to(dev)
     func.edge_index, func.edge_weight = ei, w
     el1, _ = timed_solve(func, x, steps, warmup, h, dev, world)
+    progress("unsharded 1-GPU point: %.3f ms per step" % (el1 * 1e3 / steps))
     del func
     torch.cuda.empty_cache()
     alpha = torch.zeros((), device=dev)
@@ -396,6 +414,7 @@ def sharded_point(N, E, C, h, steps, warmup, world, dev, mode, seed=0):
         y0 = sh.split(x)
         info = {"columns_per_rank": sh.c1 - sh.c0}
     el, y = timed_solve(sh, y0, steps, warmup, h, dev, world)
+    progress("%s: %.3f ms per step" % (mode, el * 1e3 / steps))
     if mode == "rows":
         rp = sh.g.csr.rowptr.cpu()
         info["blocks_nnz"] = [int(rp[b] - rp[a]) for a, b in sh.blocks]
@@ -416,6 +435,7 @@ def bench_grmat(args, world, rank, dev):
     N, E, C, h = 2_000_000, 20_000_000, 256, args.step_size
     out = {"config": "configs[4] graph: RMAT N=%d E=%d C=%d, rk4 %d timed steps (step %.3g)" % (
         N, E, C, args.grmat_steps, h)}
+    progress("configs[4] graph (G-rmat)")
     if world == 1:
         import gnpde
         from gnpde import synthetic
@@ -543,6 +563,44 @@ def bench_blend(g, dev, reps=50):
     out["check"] = {"bf16_vs_fp32_rel": round(rel, 6), "constant_state_rhs_max": const_rhs,
                     "ok": bool(rel <= 2e-2 and const_rhs <= 1e-5)}
     return out
+
+
+def bench_train(ei, w, x, h, dev, steps=4, reps=5):
+    """one training step of the drop-in path on G-arxiv —
+    `steps` rk4 steps with autograd through every RHS (the eager path: K1
+    forward, K1 over the CSC for d/dx, the alpha reduction), a linear loss, and
+    backward to x and alpha_train.  Timed with events around the whole step."""
+    import gnpde
+    C = x.shape[-1]
+    func = gnpde.LaplacianODEFunc(C, C, dict(LAP_OPT, hidden_dim=C), dev).to(dev)
+    func.edge_index, func.edge_weight = ei, w
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(7)
+    gout = torch.randn(x.shape, generator=gen, device=dev)
+    t = torch.tensor([0.0, steps * h], dtype=torch.float32, device=dev)
+
+    def one():
+        xi = x.detach().clone().requires_grad_(True)
+        func.alpha_train.grad = None
+        y = gnpde.odeint(func, xi, t, method='rk4', options={'step_size': h})[1]
+        (y * gout).sum().backward()
+        return xi.grad
+
+    for _ in range(2):
+        one()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        gx = one()
+    e.record()
+    torch.cuda.synchronize()
+    ms = s.elapsed_time(e) / reps
+    assert torch.isfinite(gx).all() and func.alpha_train.grad is not None
+    return {"config": "G-arxiv laplacian, %d rk4 steps forward with autograd + backward to x and alpha_train "
+                      "(eager drop-in path)" % steps,
+            "ms_per_train_step": round(ms, 4), "ms_per_rk4_step_fwd_bwd": round(ms / steps, 4),
+            "forward_rhs": 4 * steps}
 
 
 def cpu_baseline(ei, w, x, N, E, C, budget_s):

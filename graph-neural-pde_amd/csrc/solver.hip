@@ -1,6 +1,8 @@
 // solver.hip — fused Runge-Kutta stage combination: one streaming pass for
 // y0 + dt * sum_j b_j k_j (torchdiffeq's rk4_alt_step_func / _runge_kutta_step
-// do it with several elementwise torch kernels per stage).
+// do it with several elementwise torch kernels per stage); and the fp64 dot
+// product of two fp32 tensors the parameter gradients of the RHS need
+// (d alpha_train = sigma'(alpha) <gf, A x - x>, d beta_train = <gf, x0>).
 #include "common.hpp"
 
 namespace gnpde {
@@ -39,9 +41,79 @@ __global__ __launch_bounds__(256) void rk_combine_kernel(int64_t n, const float*
   }
 }
 
+// <a, b> in fp64: a fixed grid of kDotBlocks blocks, each thread summing a fixed
+// set of elements in order, a fixed tree per block, then one block summing the
+// block partials in order — the same bits on every run (no float atomics).
+constexpr int kDotBlocks = 1024;
+
+__device__ __forceinline__ double block_sum_f64(double v, double* red) {
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) v += __shfl_xor(v, o);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (lane == 0) red[wv] = v;
+  __syncthreads();
+  double t = 0.0;
+  if (threadIdx.x == 0)
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += red[w];
+  return t;  // thread 0 only
+}
+
+template <bool VEC4>
+__global__ __launch_bounds__(256) void dot_partial_kernel(int64_t n, const float* __restrict__ a,
+                                                           const float* __restrict__ b, double* __restrict__ part) {
+  __shared__ double red[kBlock / kWave];
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  double acc = 0.0;
+  if constexpr (VEC4) {
+    const float4* a4 = reinterpret_cast<const float4*>(a);
+    const float4* b4 = reinterpret_cast<const float4*>(b);
+#pragma unroll 4
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < (n >> 2); i += stride) {
+      const float4 u = a4[i], v = b4[i];
+      acc = fma((double)u.x, (double)v.x, acc);
+      acc = fma((double)u.y, (double)v.y, acc);
+      acc = fma((double)u.z, (double)v.z, acc);
+      acc = fma((double)u.w, (double)v.w, acc);
+    }
+  } else {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride)
+      acc = fma((double)a[i], (double)b[i], acc);
+  }
+  const double t = block_sum_f64(acc, red);
+  if (threadIdx.x == 0) part[blockIdx.x] = t;
+}
+
+__global__ __launch_bounds__(256) void dot_final_kernel(const double* __restrict__ part, int nb,
+                                                         double* __restrict__ out) {
+  __shared__ double red[kBlock / kWave];
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < nb; i += blockDim.x) acc += part[i];
+  const double t = block_sum_f64(acc, red);
+  if (threadIdx.x == 0) *out = t;
+}
+
 }  // namespace gnpde
 
 using namespace gnpde;
+
+extern "C" size_t gnpde_dot_workspace_bytes(void) { return sizeof(double) * kDotBlocks; }
+
+extern "C" int gnpde_dot_f64(int64_t n, const float* a, const float* b, double* out, void* workspace,
+                             size_t workspace_bytes, void* stream) {
+  GNPDE_REQUIRE(n >= 0 && a && b && out && workspace, GNPDE_EINVAL, "dot: NULL pointer or bad n");
+  GNPDE_REQUIRE(workspace_bytes >= gnpde_dot_workspace_bytes(), GNPDE_EINVAL, "dot: workspace too small");
+  hipStream_t s = as_stream(stream);
+  double* part = static_cast<double*>(workspace);
+  const bool vec4 = n % 4 == 0 && aligned16(a) && aligned16(b);
+  if (vec4)
+    dot_partial_kernel<true><<<kDotBlocks, kBlock, 0, s>>>(n, a, b, part);
+  else
+    dot_partial_kernel<false><<<kDotBlocks, kBlock, 0, s>>>(n, a, b, part);
+  GNPDE_LAUNCH_CHECK();
+  dot_final_kernel<<<1, kBlock, 0, s>>>(part, kDotBlocks, out);
+  GNPDE_LAUNCH_CHECK();
+  return GNPDE_OK;
+}
 
 extern "C" int gnpde_rk_combine_f32(int64_t n, const float* y0, int nk, const float* const* ks, const double* coef,
                                     double scale, float* out, void* stream) {

@@ -84,6 +84,8 @@ SIGNATURES = {
     "gnpde_score_input_grad_f32": (_int, [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _int, _vp, _i64, _int, _vp]),
     "gnpde_gather_head_f32": (_int, [_vp, _i64, _int, _int, _vp, _f32, _vp, _vp]),
     "gnpde_rk_combine_f32": (_int, [_i64, _vp, _int, ctypes.POINTER(_vp), ctypes.POINTER(_f64), _f64, _vp, _vp]),
+    "gnpde_dot_workspace_bytes": (_size, []),
+    "gnpde_dot_f64": (_int, [_i64, _vp, _vp, _vp, _vp, _size, _vp]),
     "gnpde_self_loops_workspace_bytes": (_size, [_i64, _i64, _i64]),
     "gnpde_self_loops_count": (_int, [_vp, _i64, _i64, c_i64p, _vp, _size, _vp]),
     "gnpde_add_self_loops": (_int, [_vp, _vp, _i64, _i64, _i64, _f32, _i64, _vp, _vp, _vp, _size, _vp]),

@@ -48,14 +48,14 @@ class _LaplacianRHS(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             one = torch.ones((), dtype=torch.float32, device=x.device)
             d = ops.spmm_rhs(g, ctx.w_csr, x.detach(), alpha=one, rhs=True, alpha_sigmoid=False)  # A x - x
-            s = (gf.double() * d.double()).sum().to(alpha_train.dtype)
+            s = ops.dot(gf, d).to(alpha_train.dtype)  # fp64 accumulation, fixed order
             if ctx.alpha_sigmoid:
                 sg = torch.sigmoid(alpha_train.detach())
                 s = s * sg * (1 - sg)
             ga = s.reshape(alpha_train.shape)
         if ctx.needs_input_grad[2]:
             if ctx.add_source:
-                gb = (gf.double() * ctx.x0.double()).sum().to(beta_train.dtype).reshape(beta_train.shape)
+                gb = ops.dot(gf, ctx.x0.float()).to(beta_train.dtype).reshape(beta_train.shape)
             else:
                 gb = torch.zeros_like(beta_train)
         gw = None

@@ -58,13 +58,33 @@ FIXED_METHODS = ('euler', 'midpoint', 'rk4')
 ADAPTIVE_METHODS = ('dopri5',)
 
 
+class _CombineFn(torch.autograd.Function):
+    """The fused HIP stage combination under autograd: forward one streaming pass
+    (gnpde_rk_combine_f32) instead of a clone plus a multiply and an add per
+    term; backward d/dy0 = g, d/dk_j = scale * c_j * g."""
+
+    @staticmethod
+    def forward(ctx, y0, scale, coefs, *ks):
+        ctx.scale, ctx.coefs, ctx.has_y0 = scale, coefs, y0 is not None
+        return ops.rk_combine(y0, list(ks), list(coefs), scale).view(ks[0].shape)
+
+    @staticmethod
+    def backward(ctx, g):
+        g = g.contiguous()
+        gk = [g * float(ctx.scale * c) for c in ctx.coefs]
+        return (g if ctx.has_y0 else None, None, None) + tuple(gk)
+
+
 class _Combine(object):
     """y0 + scale * sum_j c_j k_j on the device (fused HIP pass).  When autograd
     has to see the combination (grad enabled and an operand requires grad) it
-    is written with torch ops so gradients flow through the solver."""
+    runs through _CombineFn so gradients flow through the solver (torch ops for
+    CPU tensors: the host-logic tests' injected RHS)."""
 
     def __call__(self, y0, ks, coefs, scale):
         if torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in [y0] + list(ks)):
+            if ks[0].is_cuda and ks[0].dtype == torch.float32:
+                return _CombineFn.apply(y0, float(scale), tuple(float(c) for c in coefs), *ks)
             return _torch_combine(y0, ks, coefs, scale)
         if ks[0].dtype == torch.bfloat16:
             # bf16 state outside the fused fixed-grid path (dopri5): fp32 combination, one rounding

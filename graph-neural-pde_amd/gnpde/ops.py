@@ -856,6 +856,21 @@ def segment_sum(grouped, vals):
     return out
 
 
+def dot(a, b):
+    """<a, b> of two fp32 device tensors of the same size, accumulated in fp64
+    (gnpde_dot_f64, fixed order): 0-d float64 tensor on the device."""
+    _require_gpu(a, "a", torch.float32)
+    _require_gpu(b, "b", torch.float32)
+    if a.numel() != b.numel():
+        raise ValueError("dot: sizes differ (%d, %d)" % (a.numel(), b.numel()))
+    a, b = a.contiguous(), b.contiguous()
+    out = torch.empty((), dtype=torch.float64, device=a.device)
+    nbytes = _lib.fn("gnpde_dot_workspace_bytes")()
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=a.device)
+    _lib.call("gnpde_dot_f64", a.numel(), _ptr(a), _ptr(b), _ptr(out), _ptr(ws), nbytes, _stream(a.device))
+    return out
+
+
 def wcolsum(x, B, N, w):
     """y [B,H,C+1] fp64: y[b,h,:C] = sum_n w[b*N+n,h] x[b,n,:], y[b,h,C] = sum_n w[b*N+n,h]."""
     xr = _rows(x, "x")

@@ -338,6 +338,15 @@ int gnpde_edge_attention_f32(const int32_t* rowidx, const int32_t* col, const in
 int gnpde_rk_combine_f32(int64_t n, const float* y0, int nk, const float* const* ks, const double* coef,
                          double scale, float* out, void* stream);
 
+/* <a, b> of two fp32 arrays in fp64 (n elements), written to *out on the device:
+ * the parameter gradients of the RHS backward, d alpha_train = sigma'(alpha)
+ * <gf, A x - x> and d beta_train = <gf, x0> (torch autograd of
+ * function_laplacian_diffusion.py:69-76).  Fixed reduction order (deterministic);
+ * two launches; workspace: gnpde_dot_workspace_bytes().                      */
+size_t gnpde_dot_workspace_bytes(void);
+int gnpde_dot_f64(int64_t n, const float* a, const float* b, double* out, void* workspace, size_t workspace_bytes,
+                  void* stream);
+
 /* ---------------------------------------------------------------- backward
  * Gradients of the RHS f = a (A(w) x - x) [+ b x0] and of the attention that
  * produces w; torch autograd of the reference (function_laplacian_diffusion.py:

@@ -11,6 +11,7 @@ import pytest
 import torch
 
 import gnpde
+from gnpde import ops
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -314,3 +315,19 @@ def test_constant_block_adjoint_training():
     (blk(xt, data) ** 2).sum().backward()
     assert xt.grad is not None and torch.isfinite(xt.grad).all()
     assert blk.odefunc.alpha_train.grad is not None and float(blk.odefunc.alpha_train.grad) != 0.0
+
+
+@pytest.mark.parametrize("n", [1, 7, 4096, 1000003, 21675904])
+def test_dot_f64_vs_torch_and_deterministic(n):
+    """gnpde_dot_f64 (the alpha / beta gradient reductions): fp64 accumulation
+    of fp32 products, fixed order — equal to torch's fp64 sum to 1e-12 relative
+    and bit-identical run to run (also on an unaligned view: scalar path)."""
+    gen = torch.Generator(device=DEV)
+    gen.manual_seed(n)
+    a = torch.randn(n + 1, generator=gen, device=DEV)
+    b = torch.randn(n + 1, generator=gen, device=DEV)
+    for x, y in ((a[:n], b[:n]), (a[1:], b[1:])):
+        got = ops.dot(x, y)
+        want = (x.double() * y.double()).sum()
+        assert abs(float(got - want)) <= 1e-12 * max(1.0, float((x.double() * y.double()).abs().sum()))
+        assert torch.equal(ops.dot(x, y), got)
