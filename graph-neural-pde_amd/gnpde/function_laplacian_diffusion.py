@@ -99,6 +99,14 @@ class LaplacianODEFunc(ODEFunc):
         integrator may run on a zero-padded state (integrator._padded_width)."""
         return True
 
+    def fixed_grid_backward_ok(self):
+        """The fused discrete adjoint of a fixed-grid solve (integrator.
+        _LaplacianFixedGridFn) covers gradients to the state, alpha_train and
+        beta_train; a weight tensor that needs its own gradient (attention
+        blocks training through the weights) keeps the per-RHS autograd path."""
+        w, _ = self._weights_tensor()
+        return not w.requires_grad
+
     def supports_node_layout(self):
         """Weights are per edge in COO order, x0 per node: the fixed-grid
         integrator may keep the state in the graph's locality numbering."""

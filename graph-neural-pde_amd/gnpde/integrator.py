@@ -346,6 +346,153 @@ def _padded_width(func, y0):
     return (C + align - 1) // align * align
 
 
+# --------------------------------------------------------------------------- training path
+# Fixed-grid solves of the (linear) Laplacian RHS under autograd: the discrete
+# adjoint of the whole solve as ONE autograd node.  GNPDE_FUSED_BACKWARD=0 falls
+# back to autograd through every RHS and stage combination.
+FUSED_BACKWARD = os.environ.get('GNPDE_FUSED_BACKWARD', '1') != '0'
+
+
+def _fused_backward_ok(func, y0, combine, grid_h, t_h):
+    if not (FUSED_BACKWARD and torch.is_grad_enabled() and isinstance(combine, _Combine) and y0.is_cuda and
+            y0.dtype == torch.float32 and y0.dim() == 3):
+        return False
+    fn = getattr(func, 'fixed_grid_backward_ok', None)
+    if fn is None or not fn():
+        return False
+    params = [y0, func.alpha_train, func.beta_train]
+    if not any(p.requires_grad for p in params):
+        return False
+    gs = set(grid_h)
+    return all(v in gs for v in t_h)  # every output time is a grid point (no interpolation)
+
+
+class _LaplacianFixedGridFn(torch.autograd.Function):
+    """The discrete adjoint of a fixed-grid solve (euler, midpoint, rk4 3/8) of
+    f(x) = a (A x - x) [+ b x0], a = sigma(alpha_train) (or alpha_train),
+    b = beta_train: exactly the gradient of the stepped computation, like
+    backprop through every RHS call, but formed with the fused kernels.
+
+    Forward: the fused steps (stage combinations in the K1 epilogues), the state
+    at every step start and the stage inputs kept (3 states per rk4 step).
+    Backward, step by step from the last, for rk4
+        gk4 = dt/8 g              u4 = (A^T - I) gk4
+        gk3 = 3dt/8 g + dt a u4   u3 = (A^T - I) gk3
+        gk2 = 3dt/8 g - dt a u4 + dt a u3                       ...
+        gk1 = dt/8 g + dt a u4 - dt/3 a u3 + dt/3 a u2
+        g  <- g + a (u4 + u3 + u2 + u1)
+        d alpha += a'(alpha) sum_i <u_i, x_i>,  d beta += sum_i <gk_i, x0>
+    (K1 over the CSC for (A^T - I), each gk line and the running sum formed in
+    the epilogue of the launch before it (gnpde_stage_epilogue_t), fp64 dot
+    products): four transpose launches per rk4 step instead of autograd's ~40
+    elementwise kernels and a second K1 per RHS for d alpha."""
+
+    @staticmethod
+    def forward(ctx, y0, alpha_train, beta_train, func, method, steps, t_h):
+        starts, stage_inputs = [], []
+        y = y0.detach().contiguous()
+        sol = [y]
+        j = 1
+        for ta, tb in steps:
+            starts.append(y)
+            ws = _Workspace()  # a fresh one per step: its stage inputs are kept for the backward
+            y = _fused_step(method, func, ta, tb - ta, tb, y, ws)
+            stage_inputs.append([ws[k] for k in ('a', 'b', 'c') if k in ws])
+            while j < len(t_h) and tb >= t_h[j]:
+                sol.append(y)
+                j += 1
+        ctx.func, ctx.method, ctx.steps, ctx.t_h = func, method, steps, t_h
+        ctx.starts, ctx.stage_inputs = starts, stage_inputs
+        return torch.stack(sol, 0)
+
+    @staticmethod
+    def backward(ctx, g_sol):
+        func, method, steps, t_h = ctx.func, ctx.method, ctx.steps, ctx.t_h
+        g_sol = g_sol.contiguous()
+        with torch.no_grad():
+            gr = func.graph_for(ctx.starts[0])
+            w, tag = func._weights_tensor()
+            w_csc = func.csr_weights(gr, w, tag, transpose=True)
+            one = torch.ones((), dtype=torch.float32, device=g_sol.device)
+            alpha = func.alpha_train.detach()
+            sig = not func.opt.get('no_alpha_sigmoid', False)
+            a_dev = torch.sigmoid(alpha) if sig else alpha
+            a = float(a_dev)  # one host read per backward: the combination coefficients
+            add_source = bool(func.opt.get('add_source', False))
+            x0 = func.stable_x0(ctx.starts[0]) if add_source else None
+
+            def u_of(v):  # (A^T - I) v
+                return ops.spmm_rhs(gr, w_csc, v, alpha=one, rhs=True, alpha_sigmoid=False, transpose=True)
+
+            comb = ops.rk_combine
+            ga = torch.zeros((), dtype=torch.float64, device=g_sol.device)
+            gb = torch.zeros((), dtype=torch.float64, device=g_sol.device)
+            # the output-time gradients join the running gradient at their grid points
+            out_at = {}
+            j = 1
+            for n, (ta, tb) in enumerate(steps):
+                while j < len(t_h) and tb >= t_h[j]:
+                    out_at.setdefault(n, []).append(j)
+                    j += 1
+            g = torch.zeros_like(ctx.starts[0])
+            nfe = getattr(func, 'nfe', None)
+            for n in range(len(steps) - 1, -1, -1):
+                for jj in out_at.get(n, []):
+                    g = g + g_sol[jj]
+                ta, tb = steps[n]
+                dt = tb - ta
+                y = ctx.starts[n]
+                if method == 'rk4':
+                    # the adjoint stage combinations ride in the transpose launches' epilogues
+                    # (v = (A^T - I) g, so u4 = dt/8 v by linearity)
+                    x2, x3, x4 = ctx.stage_inputs[n]
+                    e = lambda: torch.empty_like(g)  # noqa: E731
+                    v, gk3, u3, gk2, u2, gk1, acc, u1, g_new = (e() for _ in range(9))
+                    c8, ad = dt / 8.0, dt * a
+                    T = dict(alpha=one, rhs=True, alpha_sigmoid=False, transpose=True)
+                    ops.spmm_rhs(gr, w_csc, g, stage=ops.Stage(f_out=v, outs=[(gk3, g, 3 * c8, ad * c8, [])]), **T)
+                    ops.spmm_rhs(gr, w_csc, gk3, stage=ops.Stage(f_out=u3, outs=[(gk2, g, 3 * c8, ad,
+                                                                                  [(v, -ad * c8)])]), **T)
+                    ops.spmm_rhs(gr, w_csc, gk2, stage=ops.Stage(f_out=u2, outs=[
+                        (gk1, g, c8, ad / 3.0, [(v, ad * c8), (u3, -ad / 3.0)]),
+                        (acc, u3, a, a, [(v, a * c8)])]), **T)
+                    ops.spmm_rhs(gr, w_csc, gk1, stage=ops.Stage(f_out=u1, outs=[(g_new, g, 1.0, a, [(acc, 1.0)])]),
+                                 **T)
+                    ga = ga + c8 * ops.dot(v, x4) + ops.dot(u3, x3) + ops.dot(u2, x2) + ops.dot(u1, y)
+                    if add_source:
+                        gb = gb + c8 * ops.dot(g, x0) + ops.dot(gk3, x0) + ops.dot(gk2, x0) + ops.dot(gk1, x0)
+                    g = g_new
+                    continue
+                if method == 'euler':
+                    gk = [comb(None, [g], [dt], 1.0)]
+                    xs = [y]
+                    us = [u_of(gk[0])]
+                else:  # midpoint
+                    ym = ctx.stage_inputs[n][0]
+                    gk2 = comb(None, [g], [dt], 1.0)
+                    u2 = u_of(gk2)
+                    gk1 = comb(None, [u2], [0.5 * dt * a], 1.0)
+                    u1 = u_of(gk1)
+                    gk, xs, us = [gk2, gk1], [ym, y], [u2, u1]
+                for u, xv in zip(us, xs):
+                    ga = ga + ops.dot(u, xv)
+                if add_source:
+                    for gkv in gk:
+                        gb = gb + ops.dot(gkv, x0)
+                g = comb(g, us, [a] * len(us), 1.0).view(g.shape)
+            if nfe is not None:
+                func.nfe = nfe  # the recomputed stages are not new RHS evaluations
+            for jj in out_at.get(-1, []):
+                g = g + g_sol[jj]
+            g = g + g_sol[0]
+            if sig:
+                ga = ga * (a_dev * (1 - a_dev)).double()
+        gy = g if ctx.needs_input_grad[0] else None
+        galpha = ga.to(func.alpha_train.dtype).reshape(func.alpha_train.shape) if ctx.needs_input_grad[1] else None
+        gbeta = gb.to(func.beta_train.dtype).reshape(func.beta_train.shape) if ctx.needs_input_grad[2] else None
+        return gy, galpha, gbeta, None, None, None, None
+
+
 def _node_layout(func, y0):
     """The locality numbering (ops.NodeLayout) the fused path keeps the state in, or None."""
     fn = getattr(func, 'node_layout', None)
@@ -383,6 +530,8 @@ def odeint_fixed(func, y0, t, method, step_size=None, combine=None, graph=None):
     if not (grid_h[0] == t_h[0] and grid_h[-1] == t_h[-1]):
         raise AssertionError("time grid does not cover t")
     steps = list(zip(grid_h[:-1], grid_h[1:]))
+    if _fused_backward_ok(func, y0, combine, grid_h, t_h) and _nfe_headroom(func, len(steps) * RHS_PER_STEP[method]):
+        return _LaplacianFixedGridFn.apply(y0, func.alpha_train, func.beta_train, func, method, steps, t_h)
     if graph is None:
         # a RHS with a collective inside (dist.RowShardedLaplacian) opts out of capture
         graph = len(steps) >= GRAPH_MIN_STEPS and getattr(func, 'graph_capturable', True)

@@ -331,3 +331,49 @@ def test_dot_f64_vs_torch_and_deterministic(n):
         want = (x.double() * y.double()).sum()
         assert abs(float(got - want)) <= 1e-12 * max(1.0, float((x.double() * y.double()).abs().sum()))
         assert torch.equal(ops.dot(x, y), got)
+
+
+@pytest.mark.parametrize("method", ["euler", "midpoint", "rk4"])
+@pytest.mark.parametrize("add_source,no_sig", [(False, False), (True, False), (True, True)])
+def test_fused_fixed_grid_backward_matches_autograd(method, add_source, no_sig):
+    """integrator._LaplacianFixedGridFn (the discrete adjoint of a fixed-grid
+    Laplacian solve as one autograd node) against autograd through every RHS
+    and stage combination (GNPDE_FUSED_BACKWARD=0): gradients to the state,
+    alpha_train and beta_train, with output times inside the grid."""
+    import gnpde.integrator as integ
+    from gnpde import synthetic
+    N, E, C = 3000, 24000, 64
+    ei, w = synthetic.rw_graph(N, E, seed=5, device=DEV)
+    opt = {'hidden_dim': C, 'block': 'constant', 'add_source': add_source, 'no_alpha_sigmoid': no_sig,
+           'max_nfe': 10 ** 6, 'multi_modal': False}
+    func = gnpde.LaplacianODEFunc(C, C, opt, DEV).to(DEV)
+    with torch.no_grad():
+        func.alpha_train.fill_(0.4)
+        func.beta_train.fill_(0.3)
+    func.edge_index, func.edge_weight = ei, w
+    gen = torch.Generator(device=DEV)
+    gen.manual_seed(3)
+    x = torch.randn(1, N, C, generator=gen, device=DEV)
+    func.x0 = torch.randn(1, N, C, generator=gen, device=DEV)
+    g1, g2 = torch.randn(2, 1, N, C, generator=gen, device=DEV)
+    t = torch.tensor([0.0, 0.5, 1.0], device=DEV)
+    res = []
+    for fused in (True, False):
+        integ.FUSED_BACKWARD = fused
+        try:
+            xi = x.clone().requires_grad_(True)
+            func.alpha_train.grad = func.beta_train.grad = None
+            func.nfe = 0
+            y = gnpde.odeint(func, xi, t, method=method, options={'step_size': 0.25})
+            ((y[1] * g1).sum() + (y[2] * g2).sum()).backward()
+            res.append((y.detach(), xi.grad, func.alpha_train.grad.clone(), None if func.beta_train.grad is None
+                        else func.beta_train.grad.clone(), func.nfe))
+        finally:
+            integ.FUSED_BACKWARD = True
+    (yf, gxf, gaf, gbf, nf), (ye, gxe, gae, gbe, ne) = res
+    assert nf == ne  # the backward's recomputed stages are not counted as RHS evaluations
+    assert (yf - ye).abs().max() / ye.abs().max() < 1e-5
+    assert (gxf - gxe).abs().max() / gxe.abs().max() < 1e-5
+    assert abs(float(gaf - gae)) <= 1e-5 * max(1.0, abs(float(gae)))
+    if add_source:
+        assert abs(float(gbf - gbe)) <= 1e-5 * max(1.0, abs(float(gbe)))
