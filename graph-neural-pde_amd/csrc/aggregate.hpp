@@ -444,6 +444,16 @@ static int launch_agg_vec(const int4* items, int64_t n_items, int4* heavy, int64
       if (lanes <= 16) return GNPDE_AGG(16, 1, 4, 1);
       break;
     default:  // per width, the fastest of variants 0/6/7/8 (profiles/r02b_stripe_sweep.jsonl)
+      // A state far beyond the Infinity Cache (G-rmat stripes: 2M rows x 32-64 columns) is
+      // gathered from HBM, where more independent rows per wavefront win (variant 7: G-rmat
+      // rk4 step at 32 / 64 columns 2.06 / 3.67 ms against 2.56 / 4.52); a cache-resident one
+      // (G-arxiv stripes) prefers several edge groups per row (0.149 / 0.124 ms at 32 / 16
+      // columns against 0.283 / 0.318; profiles/r02b_layout_ab.jsonl).
+      if (n_items * (int64_t)C * (int64_t)sizeof(T) > (int64_t)(96 << 20)) {
+        if (lanes <= 4) return GNPDE_AGG(4, 1, 4, 16);
+        if (lanes <= 8) return GNPDE_AGG(8, 1, 4, 8);
+        if (lanes <= 16) return GNPDE_AGG(16, 1, 4, 4);
+      }
       if (lanes <= 4) return GNPDE_AGG(4, 1, 4, 4);
       if (lanes <= 8) return GNPDE_AGG(8, 1, 8, 4);
       if (lanes <= 16) return GNPDE_AGG(16, 1, 4, 2);
