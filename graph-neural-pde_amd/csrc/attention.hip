@@ -184,6 +184,8 @@ __global__ __launch_bounds__(256) void seg_softmax_kernel(const int4* __restrict
   const int round_of_lane = lane / ER, team_src = (lane % ER) * T;
 
   const int H = sa.H;
+  // (Gathering every head's cs[src] before the head loop measured slower:
+  // 16.5 against 15.3 us for the G-arxiv CSC statistics.)
   float wsum = 0.f;
   for (int h = 0; h < H; ++h) {
     S_t v;
