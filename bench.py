@@ -312,7 +312,9 @@ def bench_single(args, world, rank, dev):
         result["blend_c162"] = bench_blend(g, dev)
         progress("blend done")
     if not args.no_train and rank == 0 and world == 1:
+        result["block_forward"] = bench_block(ei, x, h, dev)
         result["train_rk4"] = bench_train(ei, w, x, h, dev)
+        progress("block / train done")
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(ei, w, x, N, E, C, args.cpu_seconds)
@@ -563,6 +565,43 @@ def bench_blend(g, dev, reps=50):
     out["check"] = {"bf16_vs_fp32_rel": round(rel, 6), "constant_state_rhs_max": const_rhs,
                     "ok": bool(rel <= 2e-2 and const_rhs <= 1e-5)}
     return out
+
+
+def bench_block(ei, x, h, dev, T=4.0, reps=5):
+    """The drop-in block as GRAND's forward calls it (src/GNN.py:17 ->
+    ConstantODEblock.forward, src/block_constant.py:22-59): reset_graph_data
+    (self loops + rw normalisation, cached per graph), set_x0, rk4 over [0, T]
+    through gnpde.odeint (in-degree numbering, captured steps), eval mode.  The
+    raw RMAT edge list goes in (the block adds its own self loops)."""
+    import gnpde
+    C = x.shape[-1]
+    N = x.shape[1]
+    opt = dict(LAP_OPT, hidden_dim=C, method='rk4', step_size=h, self_loop_weight=1.0, data_norm='rw',
+               tol_scale=1.0, adjoint=False, augment=False)
+    blk = gnpde.ConstantODEblock(gnpde.LaplacianODEFunc, [], opt, dev,
+                                 t=torch.tensor([0.0, T], device=dev)).to(dev).eval()
+    data = gnpde.GraphData()
+    raw = ei[:, :, :ei.shape[2] - N]  # synthetic.rw_graph appended N self loops; the block adds its own
+    data.new_graph(raw, N)
+    with torch.no_grad():
+        for _ in range(2):
+            blk.set_x0(x)
+            blk(x, data)
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(reps):
+            blk.set_x0(x)
+            z = blk(x, data)
+        e.record()
+        torch.cuda.synchronize()
+    ms = s.elapsed_time(e) / reps
+    steps = int(round(T / h))
+    assert torch.isfinite(z).all()
+    return {"config": "ConstantODEblock.forward (eval), G-arxiv raw edges + block self loops, rk4 over [0, %g], "
+                      "step %g" % (T, h),
+            "ms_per_forward": round(ms, 4), "rk4_steps": steps, "rhs_evals_per_s": round(4 * steps / ms * 1e3, 1),
+            "nfe": blk.odefunc.nfe}
 
 
 def bench_train(ei, w, x, h, dev, steps=4, reps=5):

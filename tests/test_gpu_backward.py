@@ -377,3 +377,34 @@ def test_fused_fixed_grid_backward_matches_autograd(method, add_source, no_sig):
     assert abs(float(gaf - gae)) <= 1e-5 * max(1.0, abs(float(gae)))
     if add_source:
         assert abs(float(gbf - gbe)) <= 1e-5 * max(1.0, abs(float(gbe)))
+
+
+def test_fused_fixed_grid_backward_full_size_garxiv():
+    """The discrete-adjoint node on the full G-arxiv graph (hub rows split into
+    chunk items over the CSC): two rk4 steps, gradients to x and alpha_train
+    against autograd through every RHS call."""
+    import gnpde.integrator as integ
+    from gnpde import synthetic
+    N, E, C = synthetic.ARXIV_N, synthetic.ARXIV_E, 64
+    ei, w = synthetic.rw_graph(N, E, seed=0, device=DEV)
+    opt = {'hidden_dim': C, 'block': 'constant', 'add_source': False, 'no_alpha_sigmoid': False,
+           'max_nfe': 10 ** 6, 'multi_modal': False}
+    func = gnpde.LaplacianODEFunc(C, C, opt, DEV).to(DEV)
+    func.edge_index, func.edge_weight = ei, w
+    x = synthetic.features(1, N, C, seed=1, device=DEV)
+    gout = synthetic.features(1, N, C, seed=2, device=DEV)
+    t = torch.tensor([0.0, 0.5], device=DEV)
+    res = []
+    for fused in (True, False):
+        integ.FUSED_BACKWARD = fused
+        try:
+            xi = x.clone().requires_grad_(True)
+            func.alpha_train.grad = None
+            y = gnpde.odeint(func, xi, t, method='rk4', options={'step_size': 0.25})[1]
+            (y * gout).sum().backward()
+            res.append((xi.grad, func.alpha_train.grad.clone()))
+        finally:
+            integ.FUSED_BACKWARD = True
+    (gxf, gaf), (gxe, gae) = res
+    assert (gxf - gxe).abs().max() / gxe.abs().max() < 1e-5
+    assert abs(float(gaf - gae)) <= 1e-5 * max(1.0, abs(float(gae)))
