@@ -9,10 +9,12 @@ is restated here from its published algorithm (torchdiffeq 0.2.x):
   ``_grid_constructor_from_step_size`` (niters = ceil((t1-t0)/h + 1), the last
   grid point snapped to t1) and linear interpolation onto the requested times;
   rk4 is ``rk4_alt_step_func`` (the 3/8 rule);
-* ``dopri5``: ``RKAdaptiveStepsizeODESolver`` with the Dormand-Prince-Shampine
-  tableau, ``_select_initial_step``, the RMS error norm, the
-  safety 0.9 / ifactor 10 / dfactor 0.2 controller and 4th-order dense output
-  (``_interp_fit`` with the DPS mid-point coefficients) at the requested times.
+* ``dopri5``, ``bosh3``, ``fehlberg2``, ``adaptive_heun``:
+  ``RKAdaptiveStepsizeODESolver`` with the solver's embedded tableau,
+  ``_select_initial_step``, the RMS error norm, the safety 0.9 / ifactor 10 /
+  dfactor 0.2 controller and 4th-order dense output (``_interp_fit`` with the
+  solver's mid-point coefficients) at the requested times.  adaptive_heun is the
+  reference's default ``adjoint_method`` (src/run_GNN.py:334).
 
 Stage combinations ``y0 + dt * sum_j b_j k_j`` are single fused HIP passes
 (gnpde_rk_combine_f32).  The RHS calls are whatever ``func`` is (the gnpde
@@ -54,8 +56,38 @@ _DP_C_MID = [
     187940372067 / 1594534317056 / 2, -1776094331 / 19743644256 / 2, 11237099 / 235043384 / 2,
 ]
 
+# Bogacki-Shampine 3(2) (torchdiffeq bosh3.py)
+_BS_ALPHA = [1 / 2, 3 / 4, 1.]
+_BS_BETA = [[1 / 2], [0., 3 / 4], [2 / 9, 1 / 3, 4 / 9]]
+_BS_C_SOL = [2 / 9, 1 / 3, 4 / 9, 0.]
+_BS_C_ERROR = [2 / 9 - 7 / 24, 1 / 3 - 1 / 4, 4 / 9 - 1 / 3, -1 / 8]
+_BS_C_MID = [0., 0.5, 0., 0.]
+
+# Heun-Euler 2(1) (torchdiffeq adaptive_heun.py; the reference's default adjoint_method,
+# src/run_GNN.py:334, src/best_params.py)
+_AH_ALPHA = [1.]
+_AH_BETA = [[1.]]
+_AH_C_SOL = [0.5, 0.5]
+_AH_C_ERROR = [0.5, -0.5]
+_AH_C_MID = [0.5, 0.]
+
+# Runge-Kutta-Fehlberg 2(1) (torchdiffeq fehlberg2.py)
+_FE_ALPHA = [1 / 2, 1.]
+_FE_BETA = [[1 / 2], [1 / 256, 255 / 256]]
+_FE_C_SOL = [1 / 512, 255 / 256, 1 / 512]
+_FE_C_ERROR = [-1 / 512, 0., 1 / 512]
+_FE_C_MID = [0., 0.5, 0.]
+
+# name -> (order, alpha, beta, c_sol, c_error, c_mid)
+_TABLEAUS = {
+    'dopri5': (5, _DP_ALPHA, _DP_BETA, _DP_C_SOL, _DP_C_ERROR, _DP_C_MID),
+    'bosh3': (3, _BS_ALPHA, _BS_BETA, _BS_C_SOL, _BS_C_ERROR, _BS_C_MID),
+    'fehlberg2': (2, _FE_ALPHA, _FE_BETA, _FE_C_SOL, _FE_C_ERROR, _FE_C_MID),
+    'adaptive_heun': (2, _AH_ALPHA, _AH_BETA, _AH_C_SOL, _AH_C_ERROR, _AH_C_MID),
+}
+
 FIXED_METHODS = ('euler', 'midpoint', 'rk4')
-ADAPTIVE_METHODS = ('dopri5',)
+ADAPTIVE_METHODS = ('dopri5', 'bosh3', 'fehlberg2', 'adaptive_heun')
 
 
 class _CombineFn(torch.autograd.Function):
@@ -587,12 +619,15 @@ def odeint_fixed(func, y0, t, method, step_size=None, combine=None, graph=None):
     return torch.stack(solution, 0)
 
 
-class _Dopri5(object):
-    """torchdiffeq RKAdaptiveStepsizeODESolver restated for dopri5."""
-    order = 5
+class _RKAdaptive(object):
+    """torchdiffeq RKAdaptiveStepsizeODESolver (0.2.x rk_common.py) restated for an
+    explicit embedded tableau (dopri5, bosh3, fehlberg2, adaptive_heun)."""
 
-    def __init__(self, func, y0, rtol, atol, combine, first_step=None, safety=0.9, ifactor=10.0, dfactor=0.2,
-                 max_num_steps=2 ** 31 - 1, norm=_rms_norm):
+    def __init__(self, func, y0, rtol, atol, combine, method='dopri5', first_step=None, safety=0.9, ifactor=10.0,
+                 dfactor=0.2, max_num_steps=2 ** 31 - 1, norm=_rms_norm):
+        (self.order, self.alpha, self.beta, self.c_sol, self.c_error, self.c_mid) = _TABLEAUS[method]
+        # FSAL tableaus (dopri5, bosh3): c_sol == beta[-1] and c_sol[-1] == 0, so y1 is the last stage input
+        self.fsal = self.c_sol[-1] == 0 and list(self.c_sol[:-1]) == list(self.beta[-1])
         dtype = torch.promote_types(torch.float64, y0.dtype)
         dev = y0.device
         self.func, self.y0, self.combine, self.norm = func, y0, combine, norm
@@ -644,26 +679,28 @@ class _Dopri5(object):
         t0f = float(t0.detach()) if isinstance(t0, torch.Tensor) else float(t0)
         k = [f0]
         yi = y0
-        for i, (a_i, beta_i) in enumerate(zip(_DP_ALPHA, _DP_BETA)):
+        for i, (a_i, beta_i) in enumerate(zip(self.alpha, self.beta)):
             ti = t0f + dtf if a_i == 1. else t0f + a_i * dtf
             yi = self.combine(y0, k, beta_i, dtf)
             k.append(self.func(ti, yi))
-        # c_sol == beta[-1] and c_sol[-1] == 0 for dopri5: y1 is the last stage input
-        y1 = yi
+        # non-FSAL tableaus (adaptive_heun, fehlberg2): y1 from c_sol, while the next
+        # step's f0 is still the last stage k[-1], exactly as torchdiffeq does
+        y1 = yi if self.fsal else self.combine(y0, k, self.c_sol, dtf)
         f1 = k[-1]
-        y1_error = self.combine(None, k, _DP_C_ERROR, dtf)
+        y1_error = self.combine(None, k, self.c_error, dtf)
         return y1, f1, y1_error, k
 
     def _interp(self, y0, y1, k, dt, t0, t1, t):
         dtf = float(dt.detach()) if isinstance(dt, torch.Tensor) else float(dt)
-        y_mid = self.combine(y0, k, _DP_C_MID, dtf)
+        y_mid = self.combine(y0, k, self.c_mid, dtf)
         f0, f1 = k[0], k[-1]
         a = 2 * dtf * (f1 - f0) - 8 * (y1 + y0) + 16 * y_mid
         b = dtf * (5 * f0 - 3 * f1) + 18 * y0 + 14 * y1 - 32 * y_mid
         c = dtf * (f1 - 4 * f0) - 11 * y0 - 5 * y1 + 16 * y_mid
         d = dtf * f0
         e = y0
-        x = float((t - t0) / (t1 - t0))
+        x = (t - t0) / (t1 - t0)
+        x = float(x.detach()) if isinstance(x, torch.Tensor) else float(x)
         total = e + x * d
         xp = x
         for coeff in (c, b, a):
@@ -719,7 +756,7 @@ def odeint(func, y0, t, rtol=1e-7, atol=1e-9, method=None, options=None, combine
     if method in FIXED_METHODS:
         return odeint_fixed(func, y0, t, method, options.get('step_size'), combine, graph=options.get('gnpde_graph'))
     if method in ADAPTIVE_METHODS:
-        solver = _Dopri5(func, y0, rtol, atol, combine, first_step=options.get('first_step'),
+        solver = _RKAdaptive(func, y0, rtol, atol, combine, method=method, first_step=options.get('first_step'),
                          max_num_steps=options.get('max_num_steps', 2 ** 31 - 1),
                          norm=options.get('norm', _rms_norm))
         out = solver.integrate(t)
@@ -790,7 +827,7 @@ class _OdeintAdjoint(torch.autograd.Function):
             return -pack(f.detach(), vjp_y, vjp_p)  # d/ds = -d/dt
 
         opts = dict(a_options or {})
-        if a_method == 'dopri5' and 'norm' not in opts:
+        if a_method in ADAPTIVE_METHODS and 'norm' not in opts:
             opts['norm'] = _mixed_norm_fn(sizes)
         ay = grad_y[-1]
         ap = [torch.zeros_like(p) for p in params]

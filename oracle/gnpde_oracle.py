@@ -382,6 +382,81 @@ def odeint_fixed(func, y0, t0, t1, method, step_size):
     return y
 
 
+# Embedded explicit RK pairs of torchdiffeq 0.2.x (dopri5.py, bosh3.py, fehlberg2.py,
+# adaptive_heun.py): (order, A rows, b of the propagated solution, b - b_hat, dense-output mid).
+_DPS = (5, [[1 / 5], [3 / 40, 9 / 40], [44 / 45, -56 / 15, 32 / 9],
+            [19372 / 6561, -25360 / 2187, 64448 / 6561, -212 / 729],
+            [9017 / 3168, -355 / 33, 46732 / 5247, 49 / 176, -5103 / 18656],
+            [35 / 384, 0, 500 / 1113, 125 / 192, -2187 / 6784, 11 / 84]],
+        [35 / 384, 0, 500 / 1113, 125 / 192, -2187 / 6784, 11 / 84, 0],
+        [35 / 384 - 1951 / 21600, 0, 500 / 1113 - 22642 / 50085, 125 / 192 - 451 / 720,
+         -2187 / 6784 + 12231 / 42400, 11 / 84 - 649 / 6300, -1 / 60],
+        [v / 2 for v in (6025192743 / 30085553152, 0, 51252292925 / 65400821598, -2691868925 / 45128329728,
+                         187940372067 / 1594534317056, -1776094331 / 19743644256, 11237099 / 235043384)])
+ADAPTIVE_TABLEAUS = {
+    'dopri5': _DPS,
+    'bosh3': (3, [[1 / 2], [0, 3 / 4], [2 / 9, 1 / 3, 4 / 9]], [2 / 9, 1 / 3, 4 / 9, 0],
+              [2 / 9 - 7 / 24, 1 / 3 - 1 / 4, 4 / 9 - 1 / 3, -1 / 8], [0, 1 / 2, 0, 0]),
+    'fehlberg2': (2, [[1 / 2], [1 / 256, 255 / 256]], [1 / 512, 255 / 256, 1 / 512],
+                  [-1 / 512, 0, 1 / 512], [0, 1 / 2, 0]),
+    'adaptive_heun': (2, [[1.0]], [1 / 2, 1 / 2], [1 / 2, -1 / 2], [1 / 2, 0]),
+}
+
+
+def odeint_adaptive(func, y0, ts, method, rtol, atol):
+    """torchdiffeq 0.2.x ``RKAdaptiveStepsizeODESolver`` in float64 numpy: initial
+    step from ``_select_initial_step`` (Hairer's d0/d1/d2 rule), RMS error ratio
+    over ``atol + rtol*max(|y0|,|y1|)``, step factor ``min(10, max(0.9 r^(-1/order),
+    0.2 if rejected else 1))``, the next step's f0 = the last stage (as torchdiffeq,
+    also for the non-FSAL pairs) and the quartic ``_interp_fit`` dense output at
+    every requested time.  Returns (solution [len(ts), ...], n_steps).  Parity
+    unpinned (torchdiffeq absent): checked against exact flows."""
+    order, A, b, e, mid = ADAPTIVE_TABLEAUS[method]
+    fsal = b[-1] == 0 and list(b[:-1]) == list(A[-1])
+    rms = lambda v: float(np.sqrt(np.mean(np.square(v))))  # noqa: E731
+    y = _as64(y0)
+    ts = [float(v) for v in ts]
+    f = func(ts[0], y)
+    sc = atol + np.abs(y) * rtol
+    d0, d1 = rms(y / sc), rms(f / sc)
+    h0 = 1e-6 if (d0 < 1e-5 or d1 < 1e-5) else 0.01 * d0 / d1
+    f_probe = func(ts[0] + h0, y + h0 * f)
+    d2 = rms((f_probe - f) / sc) / h0
+    h1 = max(1e-6, h0 * 1e-3) if (d1 <= 1e-15 and d2 <= 1e-15) else (0.01 / max(d1, d2)) ** (1.0 / order)
+    h = min(100 * h0, h1)
+    t = ts[0]
+    out = [y]
+    seg = None  # (t_a, t_b, y_a, y_b, f_a, f_b, y_mid) of the last accepted step
+    n = 0
+    for target in ts[1:]:
+        while target > t:
+            ks = [f]
+            for row in A:
+                ks.append(func(t + h * sum(row), y + h * sum(c * k for c, k in zip(row, ks))))
+            y_new = y + h * sum(c * k for c, k in zip(A[-1], ks)) if fsal else \
+                y + h * sum(c * k for c, k in zip(b, ks))
+            err = h * sum(c * k for c, k in zip(e, ks))
+            ratio = rms(err / (atol + rtol * np.maximum(np.abs(y), np.abs(y_new))))
+            if ratio <= 1:
+                seg = (t, t + h, y, y_new, ks[0], ks[-1], y + h * sum(c * k for c, k in zip(mid, ks)), h)
+                t, y, f = t + h, y_new, ks[-1]
+            if ratio == 0:
+                h = h * 10.0
+            else:
+                h = h * min(10.0, max(0.9 * ratio ** (-1.0 / order), 0.2 if ratio >= 1 else 1.0))
+            n += 1
+        if seg is None or target == t:
+            out.append(y)
+        else:
+            ta, tb, ya, yb, fa, fb, ym, hs = seg
+            p4 = 2 * hs * (fb - fa) - 8 * (yb + ya) + 16 * ym
+            p3 = hs * (5 * fa - 3 * fb) + 18 * ya + 14 * yb - 32 * ym
+            p2 = hs * (fb - 4 * fa) - 11 * ya - 5 * yb + 16 * ym
+            x = (target - ta) / (tb - ta)
+            out.append(ya + x * (hs * fa) + x ** 2 * p2 + x ** 3 * p3 + x ** 4 * p4)
+    return np.stack(out, 0), n
+
+
 # --------------------------------------------------------------------------- prepared CSR (timed CPU baseline)
 class LaplacianCSR(object):
     """The Laplacian RHS with the COO -> CSR conversion done once (scipy), so the

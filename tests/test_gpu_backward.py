@@ -270,8 +270,9 @@ def test_backward_is_bit_reproducible():
 
 
 # ---------------------------------------------------------------- adjoint integration
-@pytest.mark.parametrize("method,step", [("rk4", 0.05), ("dopri5", None)])
-def test_adjoint_matches_direct_backprop(method, step):
+@pytest.mark.parametrize("method,step,tol", [("rk4", 0.05, 1e-7), ("dopri5", None, 1e-7),
+                                             ("adaptive_heun", None, 1e-5)])
+def test_adjoint_matches_direct_backprop(method, step, tol):
     """odeint_adjoint (torchdiffeq semantics) against backprop through the solver:
     gradients of y0 and of the RHS parameters (alpha_train, beta_train)."""
     N, E, C = 500, 4000, 16
@@ -291,22 +292,24 @@ def test_adjoint_matches_direct_backprop(method, step):
             func.beta_train.fill_(-0.3)
         func.edge_index, func.edge_weight, func.x0 = ei, w, x0
         xt = x.clone().requires_grad_(True)
-        z = integ(func, xt, t, rtol=1e-7, atol=1e-9, method=method, options=dict(opts))
+        z = integ(func, xt, t, rtol=tol, atol=tol * 1e-2, method=method, options=dict(opts))
         (z[1:] * R).sum().backward()
         res.append((xt.grad, func.alpha_train.grad, func.beta_train.grad))
     for gd, ga in zip(*res):
         assert relerr(ga, gd) <= 1e-3, relerr(ga, gd)
 
 
-def test_constant_block_adjoint_training():
+@pytest.mark.parametrize("adjoint_method", ["rk4", "adaptive_heun"])
+def test_constant_block_adjoint_training(adjoint_method):
     """ConstantODEblock with opt['adjoint']: the block routes through odeint_adjoint with
-    adjoint_method / adjoint_step_size (block_constant.py:34-44) and trains alpha."""
+    adjoint_method / adjoint_step_size (block_constant.py:34-44) and trains alpha;
+    adaptive_heun is the reference's default adjoint_method (run_GNN.py:334)."""
     N, E, C = 300, 2500, 8
     ei = graph(12, N, E, hub=False)
     torch.manual_seed(12)
     x = torch.randn(1, N, C, device=DEV)
-    opt = dict(OPT, hidden_dim=C, adjoint=True, adjoint_method='rk4', adjoint_step_size=0.1, method='rk4',
-               step_size=0.1, tol_scale_adjoint=1.0)
+    opt = dict(OPT, hidden_dim=C, adjoint=True, adjoint_method=adjoint_method, adjoint_step_size=0.1, method='rk4',
+               step_size=0.1, tol_scale_adjoint=1000.0)
     blk = gnpde.ConstantODEblock(gnpde.LaplacianODEFunc, [], opt, DEV, t=torch.tensor([0, 1])).to(DEV).train()
     assert blk.train_integrator is gnpde.integrator.odeint_adjoint
     data = gnpde.GraphData()

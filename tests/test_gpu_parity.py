@@ -536,15 +536,17 @@ def test_constant_block_integration_vs_oracle(method, step):
     assert blk.odefunc.nfe == (10 if method == "euler" else 16)
 
 
-def test_constant_block_dopri5_vs_exact():
-    """dopri5 on the linear diffusion ODE vs expm (integrated-value parity is unpinned
-    against the reference; this checks the solver converges to the exact flow)."""
+@pytest.mark.parametrize("method,bound", [("dopri5", 1e-4), ("bosh3", 1e-3), ("fehlberg2", 3e-3),
+                                          ("adaptive_heun", 1e-3)])
+def test_constant_block_adaptive_vs_exact(method, bound):
+    """Adaptive solvers on the linear diffusion ODE vs expm (integrated-value parity is
+    unpinned against the reference; this checks the solver converges to the exact flow)."""
     import scipy.linalg
     N, E, C = 300, 1500, 8
     rng = np.random.default_rng(8)
     ei = rng.integers(0, N, size=(1, 2, E))
     x = rng.standard_normal((1, N, C)).astype(np.float32)
-    opt = dict(OPT, hidden_dim=C, method='dopri5', tol_scale=100.0)
+    opt = dict(OPT, hidden_dim=C, method=method, tol_scale=100.0)
     blk = gnpde.ConstantODEblock(gnpde.LaplacianODEFunc, [], opt, DEV, t=torch.tensor([0, 1])).to(DEV).eval()
     data = gnpde.GraphData()
     data.new_graph(T(ei), N)
@@ -554,7 +556,30 @@ def test_constant_block_dopri5_vs_exact():
     A = O.to_dense(eo[0], wo[0], N)
     M = 0.5 * (A - np.eye(N))
     want = scipy.linalg.expm(M) @ x[0].astype(np.float64)
-    assert rel(z[0], want) <= 1e-4
+    assert rel(z[0], want) <= bound
+
+
+@pytest.mark.parametrize("method", ["bosh3", "adaptive_heun"])
+def test_adaptive_integrator_vs_oracle_steps(method):
+    """gnpde.odeint (HIP RHS + HIP stage combinations) against the oracle's float64
+    restatement of torchdiffeq's adaptive loop on the same RHS: same accepted/rejected
+    step sequence (step count) and values within fp32 rounding."""
+    N, E, C = 400, 2400, 8
+    rng = np.random.default_rng(21)
+    ei = rng.integers(0, N, size=(1, 2, E))
+    x = rng.standard_normal((1, N, C)).astype(np.float32)
+    func = gnpde.LaplacianODEFunc(C, C, dict(OPT, hidden_dim=C), DEV).to(DEV)
+    eo, wo = _prep_oracle(ei, N)
+    func.edge_index, func.edge_weight = T(eo), T(wo.astype(np.float32))
+    with torch.no_grad():
+        func.alpha_train.fill_(0.0)
+        got = gnpde.integrator.odeint(func, T(x), torch.tensor([0.0, 0.5, 1.0], dtype=torch.float64, device=DEV),
+                                      rtol=1e-3, atol=1e-4, method=method)
+    n_got = gnpde.integrator.odeint.last_n_steps
+    f = lambda t, y: O.laplacian_rhs(eo, y, None, 0.0, 0.0, edge_weight=wo)  # noqa: E731
+    want, n_want = O.odeint_adaptive(f, x, [0.0, 0.5, 1.0], method, 1e-3, 1e-4)
+    assert n_got == n_want
+    assert rel(got, want) <= 1e-5
 
 
 def test_attention_block_vs_oracle():
