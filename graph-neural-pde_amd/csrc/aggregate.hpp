@@ -37,7 +37,12 @@ struct PlainWeights {
 // MAXH == 0: any heads <= 16, loaded in finish().  EXACT (heads == MAXH == 2,
 // m 16-byte and rl 8-byte aligned): one 16-B load of m[c,:] and one 8-B load
 // of rl[c,:] per edge instead of four scalar gathers.
-template <int MAXH, bool EXACT = false>
+// REC (with EXACT): m and rl come from the packed statistics records of the
+// destinations (m = the record base, stats_record_doubles(2) = 4 doubles:
+// m[0..1], then rl[0..1] as floats; rl unused): one 32-byte-aligned record per
+// edge, one cache line instead of the two of the separate arrays; same values
+// and the same finish(), so the same bits.
+template <int MAXH, bool EXACT = false, bool REC = false>
 struct RefDstSoftmaxWeights {
   const double* __restrict__ cs;
   const double* __restrict__ m;
@@ -53,8 +58,11 @@ struct RefDstSoftmaxWeights {
     r.c = c;
     if constexpr (EXACT) {
       static_assert(MAXH == 2, "EXACT statistics loads are written for two heads");
-      const double2 mv = *reinterpret_cast<const double2*>(m + (int64_t)c * 2);
-      const float2 rv = *reinterpret_cast<const float2*>(rl + (int64_t)c * 2);
+      static_assert(!REC || stats_record_doubles(2) == 4, "two-head records are 32 bytes");
+      const double* mp = REC ? m + (int64_t)c * 4 : m + (int64_t)c * 2;
+      const float* rp = REC ? reinterpret_cast<const float*>(mp + 2) : rl + (int64_t)c * 2;
+      const double2 mv = *reinterpret_cast<const double2*>(mp);
+      const float2 rv = *reinterpret_cast<const float2*>(rp);
       r.mm[0] = mv.x;
       r.mm[1] = mv.y;
       r.rr[0] = rv.x;

@@ -139,7 +139,7 @@ __global__ __launch_bounds__(256) void seg_softmax_kernel(const int4* __restrict
                                                            const int* __restrict__ gidx, int group_is_dst,
                                                            ScoreArgs sa, Team tm, float* __restrict__ w,
                                                            double* __restrict__ m, float* __restrict__ rl,
-                                                           double* __restrict__ partials) {
+                                                           double* __restrict__ mr, double* __restrict__ partials) {
   using S_t = typename std::conditional<REF, double, float>::type;
   const int lane = threadIdx.x & 63;
   const int item = uniform(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
@@ -217,10 +217,7 @@ __global__ __launch_bounds__(256) void seg_softmax_kernel(const int4* __restrict
       } else if constexpr (OUT == kSegWeights) {
         wsum += e / (Ls + kSoftmaxEps);
       } else {
-        if (live && lane == seg_end) {
-          m[(int64_t)grp * H + h] = (double)M;
-          rl[(int64_t)grp * H + h] = 1.0f / (Ls + kSoftmaxEps);
-        }
+        if (live && lane == seg_end) store_stats(m, rl, mr, grp, H, h, (double)M, 1.0f / (Ls + kSoftmaxEps));
       }
     }
   }
@@ -231,11 +228,11 @@ __global__ __launch_bounds__(256) void seg_softmax_kernel(const int4* __restrict
 
 template <bool REF, int OUT>
 static int launch_seg(const int4* items, int64_t n, const int* rowptr, const int* rowidx, const int* gidx, int gid,
-                      const ScoreArgs& sa, const Team& tm, float* w, double* m, float* rl, double* partials,
-                      hipStream_t s) {
+                      const ScoreArgs& sa, const Team& tm, float* w, double* m, float* rl, double* mr,
+                      double* partials, hipStream_t s) {
   if (n <= 0) return GNPDE_OK;
   seg_softmax_kernel<REF, OUT><<<(unsigned)ceil_div(n, kWavesPerBlock), kBlock, 0, s>>>(
-      items, (int)n, rowptr, rowidx, gidx, gid, sa, tm, w, m, rl, partials);
+      items, (int)n, rowptr, rowidx, gidx, gid, sa, tm, w, m, rl, mr, partials);
   GNPDE_LAUNCH_CHECK();
   return GNPDE_OK;
 }
@@ -308,7 +305,8 @@ int gnpde_seg_softmax_f32(const int32_t* items, int64_t n_items, const int32_t* 
                           const int32_t* heavy, int64_t n_heavy, const int32_t* rowptr, const int32_t* rowidx,
                           const int32_t* gidx, int group_is_dst, int out_kind, int mode, int64_t heads, int64_t dk,
                           const double* cs, const float* q, const float* k, int64_t ldqk, float score_p0,
-                          float score_p1, float* w, double* m, float* rl, double* partials, void* stream) {
+                          float score_p1, float* w, double* m, float* rl, double* mr, double* partials,
+                          void* stream) {
   int rc = check_score_args(mode, heads, dk, cs, q, k);
   if (rc) return rc;
   GNPDE_REQUIRE(out_kind == 0 || out_kind == 1, GNPDE_EINVAL, "seg_softmax: out_kind must be 0 (weights) or 1 (stats)");
@@ -322,10 +320,11 @@ int gnpde_seg_softmax_f32(const int32_t* items, int64_t n_items, const int32_t* 
   if (n_items + n_chunk_items == 0) return GNPDE_OK;
   GNPDE_REQUIRE(rowptr && rowidx && gidx, GNPDE_EINVAL, "seg_softmax: NULL graph arrays");
   GNPDE_REQUIRE(n_items == 0 || items, GNPDE_EINVAL, "seg_softmax: NULL items");
-  GNPDE_REQUIRE(n_chunk_items == 0 || (chunk_items && heavy && n_heavy > 0 && partials && m && rl), GNPDE_EINVAL,
-                "seg_softmax: chunk items need heavy, partials and m/rl scratch");
+  GNPDE_REQUIRE(n_chunk_items == 0 || (chunk_items && heavy && n_heavy > 0 && partials &&
+                                      ((m && rl) || (out_kind == 1 && mr))),
+                GNPDE_EINVAL, "seg_softmax: chunk items need heavy, partials and m/rl scratch");
   if (out_kind == 0) GNPDE_REQUIRE(w != nullptr, GNPDE_EINVAL, "seg_softmax: NULL w");
-  if (out_kind == 1) GNPDE_REQUIRE(m && rl, GNPDE_EINVAL, "seg_softmax: NULL m/rl");
+  if (out_kind == 1) GNPDE_REQUIRE((m && rl) || mr, GNPDE_EINVAL, "seg_softmax: no output (m/rl or the packed records)");
   const ScoreArgs sa = make_score_args(mode, heads, dk, cs, q, k, ldqk, score_p0, score_p1);
   Team tm{1, 1};
   if (mode != GNPDE_SCORE_REFERENCE) {
@@ -338,7 +337,8 @@ int gnpde_seg_softmax_f32(const int32_t* items, int64_t n_items, const int32_t* 
   const int4* hv = reinterpret_cast<const int4*>(heavy);
   const bool ref = mode == GNPDE_SCORE_REFERENCE;
 #define GNPDE_SEG(R, O, ITEMS, N) \
-  launch_seg<R, O>(ITEMS, N, rowptr, rowidx, gidx, group_is_dst, sa, tm, w, m, rl, partials, s)
+  launch_seg<R, O>(ITEMS, N, rowptr, rowidx, gidx, group_is_dst, sa, tm, w, m, rl, (O) == kSegStats ? mr : nullptr, \
+                   partials, s)
   // whole-group items and long-group chunks share one kernel (the slot field
   // tells them apart): one launch when the caller stores them back to back
   const bool adjacent = n_items > 0 && n_chunk_items > 0 && ch == it + n_items;
@@ -355,7 +355,7 @@ int gnpde_seg_softmax_f32(const int32_t* items, int64_t n_items, const int32_t* 
     if (!rc) rc = GNPDE_SEG(false, kSegStats, ch, n_second);
   }
   if (rc || n_chunk_items == 0) return rc;
-  rc = launch_stats_fixup(hv, n_heavy, (int)heads, partials, m, rl, s);
+  rc = launch_stats_fixup(hv, n_heavy, (int)heads, partials, m, rl, out_kind == 1 ? mr : nullptr, s);
   if (rc || out_kind == 1) return rc;
   return GNPDE_SEG(false, kSegChunkWeights, ch, n_chunk_items);
 #undef GNPDE_SEG

@@ -42,6 +42,10 @@ constexpr int kWave = 64;          // CDNA wavefront width
 constexpr int kBlock = 256;        // 4 waves per workgroup
 constexpr int kWavesPerBlock = kBlock / kWave;
 constexpr float kSoftmaxEps = 1e-16f;  // utils.softmax denominator epsilon, src/utils.py:124-125
+// Packed statistics record of one softmax group (optional output of the
+// statistics kernels, read by the fused-weight K1 in one cache line per edge):
+// H doubles m[h], then H floats rl[h], padded to 16 bytes.
+__host__ __device__ constexpr int stats_record_doubles(int H) { return ((H + (H + 1) / 2) + 1) & ~1; }
 
 // ------------------------------------------------------------------ vector loads
 template <int VEC>

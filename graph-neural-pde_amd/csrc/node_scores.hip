@@ -19,7 +19,7 @@ template <int MAXH, int GL>
 __global__ __launch_bounds__(256) void stats_kernel(const int4* __restrict__ items, int n_items,
                                                      const int* __restrict__ gidx, int group_is_dst, ScoreArgs sa,
                                                      double* __restrict__ m_out, float* __restrict__ rl_out,
-                                                     double* __restrict__ partials) {
+                                                     double* __restrict__ mr_out, double* __restrict__ partials) {
   constexpr int G = kWave / GL;
   const int lane = threadIdx.x & 63;
   const int g = lane / GL, gl = lane % GL;
@@ -58,8 +58,7 @@ __global__ __launch_bounds__(256) void stats_kernel(const int4* __restrict__ ite
       partials[(int64_t)slot * 2 * H + h] = M[h];
       partials[(int64_t)slot * 2 * H + H + h] = (double)L[h];
     } else {
-      m_out[(int64_t)grp * H + h] = M[h];
-      rl_out[(int64_t)grp * H + h] = 1.0f / (L[h] + kSoftmaxEps);
+      store_stats(m_out, rl_out, mr_out, grp, H, h, M[h], 1.0f / (L[h] + kSoftmaxEps));
     }
   }
 }
@@ -68,19 +67,20 @@ __global__ __launch_bounds__(256) void stats_kernel(const int4* __restrict__ ite
 // statistics (stats_merge_store, scores.hpp).
 __global__ __launch_bounds__(256) void stats_fixup_kernel(const int4* __restrict__ heavy, int n_heavy, int H,
                                                            const double* __restrict__ partials,
-                                                           double* __restrict__ m_out, float* __restrict__ rl_out) {
+                                                           double* __restrict__ m_out, float* __restrict__ rl_out,
+                                                           double* __restrict__ mr_out) {
   const int wid = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
   if (wid >= n_heavy * H) return;
   const int i = wid / H, h = wid - i * H;
   const int4 hv = heavy[i];
-  stats_merge_store(hv.x, hv.y, hv.z, H, h, partials, m_out, rl_out);
+  stats_merge_store(hv.x, hv.y, hv.z, H, h, partials, m_out, rl_out, mr_out);
 }
 
 int launch_stats_fixup(const int4* heavy, int64_t n_heavy, int H, const double* partials, double* m, float* rl,
-                       hipStream_t s) {
+                       double* mr, hipStream_t s) {
   if (n_heavy <= 0) return GNPDE_OK;
   const unsigned g2 = (unsigned)ceil_div(n_heavy * H, kWavesPerBlock);
-  stats_fixup_kernel<<<g2, kBlock, 0, s>>>(heavy, (int)n_heavy, H, partials, m, rl);
+  stats_fixup_kernel<<<g2, kBlock, 0, s>>>(heavy, (int)n_heavy, H, partials, m, rl, mr);
   GNPDE_LAUNCH_CHECK();
   return GNPDE_OK;
 }
@@ -138,7 +138,8 @@ template <int VEC>
 __global__ __launch_bounds__(256) void stats_team_kernel(const int4* __restrict__ items, int n_items,
                                                           const int* __restrict__ gidx, int group_is_dst, ScoreArgs sa,
                                                           Team tm, double* __restrict__ m_out,
-                                                          float* __restrict__ rl_out, double* __restrict__ partials) {
+                                                          float* __restrict__ rl_out, double* __restrict__ mr_out,
+                                                          double* __restrict__ partials) {
   const int lane = threadIdx.x & 63;
   const int T = tm.T, S = tm.S, tpw = kWave / T;
   const int team = lane / T, t = lane % T, h = t / S;
@@ -180,8 +181,7 @@ __global__ __launch_bounds__(256) void stats_team_kernel(const int4* __restrict_
     partials[(int64_t)slot * 2 * H + h] = M;
     partials[(int64_t)slot * 2 * H + H + h] = (double)L;
   } else {
-    m_out[(int64_t)grp * H + h] = M;
-    rl_out[(int64_t)grp * H + h] = 1.0f / (L + kSoftmaxEps);
+    store_stats(m_out, rl_out, mr_out, grp, H, h, M, 1.0f / (L + kSoftmaxEps));
   }
 }
 
@@ -247,24 +247,30 @@ __global__ __launch_bounds__(256) void attn_team_kernel(const int* __restrict__ 
 }
 
 // ------------------------------------------------------------------ reference-mode key sum
-// part[b][c][tile] = sum_{n in tile} indeg[b*N+n] * x[b*N+n][c]  (fp64), part[b][C][..] = sum indeg.
-// TPR threads per row, RPB = 256/TPR rows in flight per block iteration.
-// Tiles come in groups of kKeysumGroup: the block whose tile of a group
-// finishes last (an agent-scope arrival ticket per group, the partials stored
-// write-through first: the in-launch hand-off of aggregate.hpp's hub rows)
-// sums the group's partials in tile order into gpart[b][c][group], and resets
-// the ticket to 0 for the next launch.  The node-score blocks sum the (at most
-// 1024 / kKeysumGroup) group partials themselves (key_projection_lds): no
-// launch between the two passes over x.
-constexpr int kKeysumGroup = 32;
+// The fork's global key sum S = sum_e k_dst(e) = Wk xbar + E bk with
+// xbar = sum_n indeg(n) x_n is linear in the rows, so every row tile carries
+// its own share of S.  Three launches, no tickets:
+//   keysum_partial: per tile, xt = sum_{n in tile} indeg(n) x[b,n,:] (fp64,
+//                   xt[C] = sum indeg), then St = Wk xt + xt[C] bk  -> part[b][tile][att]
+//                   (about 256 tiles per launch);
+//   key_projection: one 1024-thread workgroup per batch element sums the tile
+//                   shares of S (fixed order), forms U = Wq^T S / sqrt(dk) and v;
+//   node_scores:    cs = x . U + v with U[b] loaded from the workspace.
+// KS_BLOCK threads per tile, TPR threads per row, RPB = KS_BLOCK/TPR rows in
+// flight per iteration (16-byte loads, 8 rows unrolled per thread).
+constexpr int kKeysumBlock = 1024;
+constexpr int kKeysumTilesTarget = 256;  // tiles per launch: the projection block reads them all
+constexpr int kProjLanes = 32;           // lanes per row of Wk (S phase)
+constexpr int kProjLoads = 16;           // tile shares in flight per thread (key_projection)
 
 template <int VEC>
-__global__ __launch_bounds__(256) void keysum_partial_kernel(const float* __restrict__ x, int64_t N, int C,
-                                                              int64_t ldx, const int* __restrict__ indeg,
-                                                              int rows_per_tile, int TPR, int ntiles,
-                                                              double* __restrict__ part, double* __restrict__ gpart,
-                                                              int ngroups, int* __restrict__ tickets) {
-  extern __shared__ __attribute__((aligned(16))) double red[];  // [RPB][C+1]
+__global__ __launch_bounds__(kKeysumBlock) void keysum_partial_kernel(const float* __restrict__ x, int64_t N, int C,
+                                                                       int64_t ldx, const int* __restrict__ indeg,
+                                                                       const float* __restrict__ Wk,
+                                                                       const float* __restrict__ bk, int att,
+                                                                       int rows_per_tile, int TPR, int ntiles,
+                                                                       double* __restrict__ part) {
+  extern __shared__ __attribute__((aligned(16))) double red[];  // [RPB][C+1] | xt[C+1]
   const int tile = blockIdx.x, b = blockIdx.y;
   const int RPB = blockDim.x / TPR;
   const int rs = threadIdx.x / TPR, t = threadIdx.x % TPR;
@@ -292,106 +298,122 @@ __global__ __launch_bounds__(256) void keysum_partial_kernel(const float* __rest
     red[rs * (C + 1) + C] = ds;
   }
   __syncthreads();
-  // column-major partials [b][c][tile], stored write-through (sc1)
-  const __amdgpu_buffer_rsrc_t rp = buf_rsrc(part + (int64_t)b * (C + 1) * ntiles);
+  double* xt = red + RPB * (C + 1);
   for (int c = threadIdx.x; c <= C; c += blockDim.x) {
     double sum = 0.0;
-    for (int r = 0; r < RPB; ++r) sum += red[r * (C + 1) + c];
-    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, sum), rp, (uint32_t)(((int64_t)c * ntiles + tile) * 8),
-                                          0, kAuxSc1);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();  // every partial of this block has reached the memory side
-  __shared__ int last;
-  const int grp = tile / kKeysumGroup;
-  const int t0 = grp * kKeysumGroup, t1 = min(ntiles, t0 + kKeysumGroup);
-  int* ticket = tickets + (int64_t)b * ngroups + grp;
-  if (threadIdx.x == 0) {
-    const int k = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = k == t1 - t0 - 1;
+    for (int r = 0; r < RPB; ++r) sum += red[r * (C + 1) + c];  // row-slot order: deterministic
+    xt[c] = sum;
   }
   __syncthreads();
-  if (!last) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  for (int c = threadIdx.x; c <= C; c += blockDim.x) {
-    const double* __restrict__ col = part + ((int64_t)b * (C + 1) + c) * ntiles;
-    double sum = 0.0;
-    for (int tt = t0; tt < t1; ++tt) sum += col[tt];  // tile order: deterministic
-    gpart[((int64_t)b * (C + 1) + c) * ngroups + grp] = sum;
+  // this tile's share of S: kProjLanes lanes per row of Wk, xor tree over them
+  const int l = threadIdx.x % kProjLanes;
+  double* __restrict__ pb = part + ((int64_t)b * ntiles + tile) * att;
+  for (int d0 = 0; d0 < att; d0 += kKeysumBlock / kProjLanes) {
+    const int d = d0 + threadIdx.x / kProjLanes;
+    const int dd = min(d, att - 1);
+    double acc = 0.0;
+#pragma unroll 4
+    for (int c = l; c < C; c += kProjLanes) acc = fma((double)Wk[(int64_t)dd * C + c], xt[c], acc);
+#pragma unroll
+    for (int o = kProjLanes / 2; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+    if (l == 0 && d < att) pb[d] = acc + xt[C] * (double)bk[d];
   }
-  if (threadIdx.x == 0) __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Per batch element b, from xbar = sum_n indeg(n) x_n (and xbar[C] = E):
-//   S[d]   = Wk[d,:] . xbar + E bk[d]                    (the fork's global key sum, :249)
+// Per batch element b (one workgroup of kKeysumBlock threads), from the tile
+// shares:  S = sum_tiles St  (the fork's global key sum, :249),
 //   U[c,h] = sum_{d in head h} Wq[d,c] S[d] / sqrt(dk)   (padded [Cp][Hp], zeros past C, H)
-//   v[h]   = bq_h . S_h / sqrt(dk)
-// so that cs[n,h] = x_n . U[:,h] + v[h] = q_{n,h} . S_h / sqrt(dk).  Computed by
-// every node-score workgroup into its own LDS (a few KFLOP, operands from L2):
-// no single-workgroup launch between the key sum and the node scores.
-struct KeyProj {
-  const double* __restrict__ gpart;  // [B][C+1][ngroups] group partials of xbar
-  int ngroups;
-  const float* __restrict__ Wq;
-  const float* __restrict__ bq;
-  const float* __restrict__ Wk;
-  const float* __restrict__ bk;
-  int att;
-};
+//   v[h]   = bq_h . S_h / sqrt(dk)                       (stored as row c = Cp of U)
+// so that cs[n,h] = x_n . U[:,h] + v[h] = q_{n,h} . S_h / sqrt(dk).  U, v go to
+// the workspace (uv[b] = U[Cp*Hp] | v[Hp]).  The launch is latency-bound, so
+// every global load is issued at the start: the tile shares (kProjLoads per
+// thread) and the thread's slice of Wq / bq (kProjW values: thread (j, h, c)
+// takes rows d = h*dk + j, + J, ... of its head, J splits per output).  Sums run
+// in a fixed order (tiles, then tile groups; rows, then splits).
+constexpr int kProjW = 8;  // Wq values prefetched per thread
 
-constexpr int kFinishRows = 8;  // rows of Wk per wavefront pass (independent loads in flight)
-
-__device__ void key_projection_lds(const KeyProj& kp, int64_t b, int C, int H, int Cp, int Hp, double* S, double* U,
-                                   double* v, double* xb) {
-  // xbar[c] = sum of the group partials, in group order (deterministic)
-  for (int c = threadIdx.x; c <= C; c += blockDim.x) {
-    const double* __restrict__ gp = kp.gpart + (b * (C + 1) + c) * kp.ngroups;
-    double sum = 0.0;
-    for (int g = 0; g < kp.ngroups; ++g) sum += gp[g];
-    xb[c] = sum;
-  }
-  __syncthreads();
-  const int att = kp.att;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  for (int d0 = wv * kFinishRows; d0 < att; d0 += kWavesPerBlock * kFinishRows) {
-    double sacc[kFinishRows];
-#pragma unroll
-    for (int j = 0; j < kFinishRows; ++j) sacc[j] = 0.0;
-    for (int c = lane; c < C; c += kWave) {
-      const double xv = xb[c];
-#pragma unroll
-      for (int j = 0; j < kFinishRows; ++j) {
-        const int d = min(d0 + j, att - 1);
-        sacc[j] = fma((double)kp.Wk[(int64_t)d * C + c], xv, sacc[j]);
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < kFinishRows; ++j) {
-      const double t = wave_sum(sacc[j]);
-      if (lane == 0 && d0 + j < att) S[d0 + j] = t + xb[C] * (double)kp.bk[d0 + j];
-    }
-  }
-  __syncthreads();
+__global__ __launch_bounds__(kKeysumBlock) void key_projection_kernel(const double* __restrict__ part, int ntiles,
+                                                                       int C, const float* __restrict__ Wq,
+                                                                       const float* __restrict__ bq, int att, int H,
+                                                                       int Cp, int Hp, double* __restrict__ uv) {
+  extern __shared__ __attribute__((aligned(16))) double kp_lds[];  // S[att] | red[kKeysumBlock]
+  double* S = kp_lds;
+  double* red = S + att;
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x;
   const int dk = att / H;
   const double inv = 1.0 / sqrt((double)dk);
-  // pair t -> (h = t / Cp, c = t % Cp): consecutive threads read consecutive Wq columns
-  for (int t = threadIdx.x; t < Cp * Hp; t += blockDim.x) {
-    const int h = t / Cp, c = t - h * Cp;
+  double* __restrict__ U = uv + (int64_t)b * (Cp * Hp + Hp);
+  // output pairs (h, c), c = Cp being v; J splits of the head's rows per pair
+  const int P = (Cp + 1) * Hp;
+  const int J = P <= kKeysumBlock ? max(1, min(kKeysumBlock / P, dk)) : 1;
+  const bool pre = P <= kKeysumBlock && (dk + J - 1) / J <= kProjW;
+  const int pj = tid / P, pq = tid - pj * P;
+  const int ph = pq / (Cp + 1), pc = pq - ph * (Cp + 1);
+  float wq[kProjW];
+  if (pre) {
+#pragma unroll
+    for (int i = 0; i < kProjW; ++i) {
+      const int dd = pj + J * i;
+      const bool ok = pj < J && ph < H && dd < dk && (pc < C || pc == Cp);
+      const int d = ph * dk + (ok ? dd : 0);
+      wq[i] = ok ? (pc == Cp ? bq[d] : Wq[(int64_t)d * C + pc]) : 0.f;
+    }
+  }
+  const double* __restrict__ pb = part + (int64_t)b * ntiles * att;
+  // S: rows of att in chunks of DW, TG tile groups per chunk; thread (tg, d) sums
+  // tiles tg, tg + TG, ... in tile order, then the TG group sums in group order
+  const int DW = min(att, kKeysumBlock), TG = kKeysumBlock / DW;
+  const int tg = tid / DW, dl = tid - tg * DW;
+  for (int d0 = 0; d0 < att; d0 += DW) {
+    const int d = d0 + dl;
+    double acc = 0.0;
+    if (tg < TG && d < att) {
+      for (int t0 = tg; t0 < ntiles; t0 += kProjLoads * TG) {
+        double v[kProjLoads];
+#pragma unroll
+        for (int k = 0; k < kProjLoads; ++k) v[k] = pb[(int64_t)min(t0 + k * TG, ntiles - 1) * att + d];
+#pragma unroll
+        for (int k = 0; k < kProjLoads; ++k)
+          if (t0 + k * TG < ntiles) acc += v[k];
+      }
+    }
+    red[tid] = acc;
+    __syncthreads();
+    if (tid < DW && d0 + tid < att) {
+      double sum = 0.0;
+      for (int g = 0; g < TG; ++g) sum += red[g * DW + tid];
+      S[d0 + tid] = sum;
+    }
+    __syncthreads();
+  }
+  if (pre) {
     double a = 0.0;
-    if (c < C && h < H) {
+#pragma unroll
+    for (int i = 0; i < kProjW; ++i) {
+      const int dd = pj + J * i;
+      if (pj < J && ph < H && dd < dk) a = fma((double)wq[i], S[ph * dk + dd], a);
+    }
+    red[tid] = a;
+    __syncthreads();
+    if (tid < P) {
+      double sum = 0.0;
+      for (int j = 0; j < J; ++j) sum += red[j * P + tid];
+      U[pc * Hp + ph] = sum * inv;
+    }
+    return;
+  }
+  // general shapes: one thread per output, Wq / bq loaded in the loop
+  for (int t = tid; t < P; t += blockDim.x) {
+    const int h = t / (Cp + 1), c = t - h * (Cp + 1);
+    double a = 0.0;
+    if (h < H && (c < C || c == Cp)) {
 #pragma unroll 16
-      for (int d = h * dk; d < (h + 1) * dk; ++d) a = fma((double)kp.Wq[(int64_t)d * C + c], S[d], a);
+      for (int d = h * dk; d < (h + 1) * dk; ++d)
+        a = fma((double)(c == Cp ? bq[d] : Wq[(int64_t)d * C + c]), S[d], a);
     }
     U[c * Hp + h] = a * inv;
   }
-  if (threadIdx.x < Hp) {
-    const int h = threadIdx.x;
-    double a = 0.0;
-    if (h < H)
-      for (int d = h * dk; d < (h + 1) * dk; ++d) a = fma((double)kp.bq[d], S[d], a);
-    v[h] = a * inv;
-  }
-  __syncthreads();
 }
 
 // cs[b*N+n, h] = x_{b,n} . U[b,:,h] + v[b,h]  (fp64 accumulation).
@@ -463,16 +485,13 @@ __device__ __forceinline__ void ns_store(double (&acc)[MAXH], const double (&vb)
     buf_store_f64(rcs, (st && h < H) ? (uint32_t)((row * H + h) * 8) : kBufNone, acc[h] + vb[h]);
 }
 
-// One chunk per row: the wave's first two row groups are loaded BEFORE the key
-// projection (their HBM latency hides the LDS prologue), U[b] then sits in
-// registers and the loop keeps two row groups in flight ahead of the one being
-// reduced.  Prefetch addresses past the block's rows clamp to its last row (a
-// cache-line hit, no extra HBM traffic).
+// One chunk per row: U[b] sits in registers and the loop keeps two row groups
+// in flight ahead of the one being reduced.  Prefetch addresses past the
+// block's rows clamp to its last row (a cache-line hit, no extra HBM traffic).
 template <int VEC, int GL, int MAXH, bool CLAMP>
-__device__ __forceinline__ void ns_block_resident(const KeyProj& kp, int64_t b, const float* __restrict__ xb,
-                                                  double* S, double* Ub, double* vl, double* xbl, __amdgpu_buffer_rsrc_t rcs,
-                                                  int64_t n0, int64_t n1, int C, int64_t ldx, int H, int Cp, int g,
-                                                  int gl, int wv) {
+__device__ __forceinline__ void ns_block_resident(const double* __restrict__ Ub, const float* __restrict__ xb,
+                                                  __amdgpu_buffer_rsrc_t rcs, int64_t n0, int64_t n1, int C,
+                                                  int64_t ldx, int H, int Cp, int g, int gl, int wv) {
   constexpr int G = kWave / GL;
   constexpr int NP = node_scores_npv<MAXH>() / VEC;
   const int64_t step = (int64_t)kWavesPerBlock * G;
@@ -481,12 +500,11 @@ __device__ __forceinline__ void ns_block_resident(const KeyProj& kp, int64_t b, 
   float xa[NP][VEC], xn[NP][VEC];
   ns_load_x<VEC, NP, GL, CLAMP>(xb + min(nb + g, last) * ldx, 0, gl, C, xa);
   ns_load_x<VEC, NP, GL, CLAMP>(xb + min(nb + g + step, last) * ldx, 0, gl, C, xn);
-  key_projection_lds(kp, b, C, H, Cp, MAXH, S, Ub, vl, xbl);
   double u[NP][VEC][MAXH];
   ns_load_u<VEC, NP, GL, MAXH>(Ub, 0, gl, u);
   double vb[MAXH];
 #pragma unroll
-  for (int h = 0; h < MAXH; ++h) vb[h] = vl[h];
+  for (int h = 0; h < MAXH; ++h) vb[h] = Ub[Cp * MAXH + h];
   for (; nb < n1; nb += step) {
     const int64_t nr = nb + g;
     float xf[NP][VEC];
@@ -506,11 +524,11 @@ __device__ __forceinline__ void ns_block_resident(const KeyProj& kp, int64_t b, 
   }
 }
 
+// uv: per batch element U[Cp][MAXH] | v[MAXH] (key_projection_kernel)
 template <int VEC, int GL, int MAXH>
 __global__ __launch_bounds__(256) void node_scores_kernel(const float* __restrict__ x, int64_t B, int64_t N, int C,
-                                                           int64_t ldx, int H, int nch, KeyProj kp,
+                                                           int64_t ldx, int H, int nch, const double* __restrict__ uv,
                                                            double* __restrict__ cs, int64_t rows_per_block) {
-  extern __shared__ __attribute__((aligned(16))) double ns_lds[];  // S[att_pad] | U[Cp][MAXH] | v[MAXH] | xbar[Cp+1]
   constexpr int G = kWave / GL;
   constexpr int NPV = node_scores_npv<MAXH>();
   constexpr int NP = NPV / VEC;
@@ -523,24 +541,19 @@ __global__ __launch_bounds__(256) void node_scores_kernel(const float* __restric
   const int64_t step = (int64_t)kWavesPerBlock * G;
   const bool ragged = C != nch * CW;
   const int Cp = nch * CW;
-  double* S = ns_lds;
-  double* Ub = ns_lds + ((kp.att + 1) & ~1);
-  double* vl = Ub + Cp * MAXH;
-  double* xbl = vl + MAXH;
   for (int64_t b = blockIdx.y; b < B; b += gridDim.y) {
-    if (b != blockIdx.y) __syncthreads();  // the previous element's U is no longer read
     const float* __restrict__ xb = x + b * N * ldx;
+    const double* __restrict__ Ub = uv + b * ((int64_t)Cp * MAXH + MAXH);
     const __amdgpu_buffer_rsrc_t rcs = buf_rsrc(cs + b * N * H);
     if (nch == 1) {
       if (ragged)
-        ns_block_resident<VEC, GL, MAXH, true>(kp, b, xb, S, Ub, vl, xbl, rcs, n0, n1, C, ldx, H, Cp, g, gl, wv);
+        ns_block_resident<VEC, GL, MAXH, true>(Ub, xb, rcs, n0, n1, C, ldx, H, Cp, g, gl, wv);
       else
-        ns_block_resident<VEC, GL, MAXH, false>(kp, b, xb, S, Ub, vl, xbl, rcs, n0, n1, C, ldx, H, Cp, g, gl, wv);
+        ns_block_resident<VEC, GL, MAXH, false>(Ub, xb, rcs, n0, n1, C, ldx, H, Cp, g, gl, wv);
     } else {
-      key_projection_lds(kp, b, C, H, Cp, MAXH, S, Ub, vl, xbl);
       double vb[MAXH];
 #pragma unroll
-      for (int h = 0; h < MAXH; ++h) vb[h] = vl[h];
+      for (int h = 0; h < MAXH; ++h) vb[h] = Ub[Cp * MAXH + h];
       for (int64_t nb = n0 + wv * G; nb < n1; nb += step) {
         const int64_t nr = nb + g;
         const float* xrow = xb + min(nr, N - 1) * ldx;
@@ -567,29 +580,43 @@ static int pow2_at_least(int v, int cap) {
   return p;
 }
 
-constexpr int kKeysumTilesTarget = 1024;
-
 static int keysum_vec(int64_t C, const float* x, int64_t ldx) {
   if (C % 4 == 0 && ldx % 4 == 0 && aligned16(x)) return 4;
   if (C % 2 == 0 && ldx % 2 == 0 && aligned8(x)) return 2;
   return 1;
 }
 
-// tiles of rows for the partial column sums (independent of the vector width)
-static void keysum_tiles(int64_t B, int64_t N, int* rows_per_tile, int* ntiles) {
-  const int64_t per_batch = std::max<int64_t>(1, kKeysumTilesTarget / B);
-  const int64_t rpt = std::max<int64_t>(ceil_div(N, per_batch), 1);
+// tiles of rows for the partial column sums (independent of the vector width):
+// about kKeysumTilesTarget over the launch, at least one row per row slot
+static int keysum_tiles_target() {
+  static const int t = [] {
+    const char* e = std::getenv("GNPDE_KEYSUM_TILES");  // tuning knob (measurement only)
+    const int v = e ? std::atoi(e) : 0;
+    return v >= 8 && v <= 4096 ? v : kKeysumTilesTarget;
+  }();
+  return t;
+}
+
+static void keysum_tiles(int64_t B, int64_t N, int rpb, int* rows_per_tile, int* ntiles) {
+  const int64_t per_batch = std::max<int64_t>(1, keysum_tiles_target() / B);
+  const int64_t rpt = std::max<int64_t>(ceil_div(N, per_batch), rpb);
   *rows_per_tile = (int)rpt;
   *ntiles = (int)ceil_div(N, rpt);
 }
 
+// keysum geometry: 16-byte (or narrower) loads, TPR threads per row
+static void keysum_geometry(int64_t C, const float* x, int64_t ldx, int* vec, int* tpr) {
+  *vec = keysum_vec(C, x, ldx);
+  *tpr = pow2_at_least((int)ceil_div(C, *vec), kKeysumBlock);
+}
+
 template <int MAXH>
 static void launch_stats(unsigned grid, int GL, hipStream_t s, const int4* it, int n, const int* gidx, int gid,
-                         const ScoreArgs& sa, double* m, float* rl, double* partials) {
+                         const ScoreArgs& sa, double* m, float* rl, double* mr, double* partials) {
   if (GL == 8)
-    stats_kernel<MAXH, 8><<<grid, kBlock, 0, s>>>(it, n, gidx, gid, sa, m, rl, partials);
+    stats_kernel<MAXH, 8><<<grid, kBlock, 0, s>>>(it, n, gidx, gid, sa, m, rl, mr, partials);
   else
-    stats_kernel<MAXH, 64><<<grid, kBlock, 0, s>>>(it, n, gidx, gid, sa, m, rl, partials);
+    stats_kernel<MAXH, 64><<<grid, kBlock, 0, s>>>(it, n, gidx, gid, sa, m, rl, mr, partials);
 }
 
 // node_scores geometry: VEC, MAXH (= Hp), lanes per row GL (8..64) so one
@@ -609,24 +636,21 @@ static NsGeom ns_geometry(int vec, int64_t C, int64_t H) {
   return g;
 }
 
-static size_t ns_lds_bytes(const NsGeom& ge, int att) {
-  const int64_t cp = (int64_t)ge.nch * ge.CW;  // >= C
-  return sizeof(double) * (size_t)(((att + 1) & ~1) + cp * ge.maxh + ge.maxh + cp + 1);
-}
+// doubles of U[Cp][MAXH] | v[MAXH] per batch element
+static int64_t ns_uv_doubles(const NsGeom& ge) { return (int64_t)ge.nch * ge.CW * ge.maxh + ge.maxh; }
 
 template <int VEC, int MAXH>
 static void launch_node_scores(dim3 grid, const NsGeom& ge, hipStream_t s, const float* x, int64_t B, int64_t N, int C,
-                               int64_t ldx, int H, const KeyProj& kp, double* cs, int64_t rpb) {
+                               int64_t ldx, int H, const double* uv, double* cs, int64_t rpb) {
   const int n = ge.nch;
-  const size_t shm = ns_lds_bytes(ge, kp.att);
   if (ge.GL <= 8)
-    node_scores_kernel<VEC, 8, MAXH><<<grid, kBlock, shm, s>>>(x, B, N, C, ldx, H, n, kp, cs, rpb);
+    node_scores_kernel<VEC, 8, MAXH><<<grid, kBlock, 0, s>>>(x, B, N, C, ldx, H, n, uv, cs, rpb);
   else if (ge.GL <= 16)
-    node_scores_kernel<VEC, 16, MAXH><<<grid, kBlock, shm, s>>>(x, B, N, C, ldx, H, n, kp, cs, rpb);
+    node_scores_kernel<VEC, 16, MAXH><<<grid, kBlock, 0, s>>>(x, B, N, C, ldx, H, n, uv, cs, rpb);
   else if (ge.GL <= 32)
-    node_scores_kernel<VEC, 32, MAXH><<<grid, kBlock, shm, s>>>(x, B, N, C, ldx, H, n, kp, cs, rpb);
+    node_scores_kernel<VEC, 32, MAXH><<<grid, kBlock, 0, s>>>(x, B, N, C, ldx, H, n, uv, cs, rpb);
   else
-    node_scores_kernel<VEC, 64, MAXH><<<grid, kBlock, shm, s>>>(x, B, N, C, ldx, H, n, kp, cs, rpb);
+    node_scores_kernel<VEC, 64, MAXH><<<grid, kBlock, 0, s>>>(x, B, N, C, ldx, H, n, uv, cs, rpb);
 }
 
 // rows per block sized for ~2048 wavefronts over the whole launch: the kernel
@@ -634,14 +658,14 @@ static void launch_node_scores(dim3 grid, const NsGeom& ge, hipStream_t s, const
 // per SIMD = 2 blocks per CU are resident and the whole grid runs in one round
 // (4096 waves left a 1.7-round tail: 26.9 us for an 87 MB pass)
 static void launch_node_scores_any(hipStream_t s, const NsGeom& ge, const float* x, int64_t B, int64_t N, int C,
-                                   int64_t ldx, int H, const KeyProj& kp, double* cs) {
+                                   int64_t ldx, int H, const double* uv, double* cs) {
   const int G = kWave / ge.GL;
   const int64_t groups = ceil_div(N, (int64_t)G);
   const int64_t waves_per_batch = std::max<int64_t>(1, 2048 / B);
   const int64_t iters = std::max<int64_t>(1, ceil_div(groups, waves_per_batch));
   const int64_t rpb = (int64_t)kWavesPerBlock * G * iters;
   const dim3 grid((unsigned)ceil_div(N, rpb), (unsigned)std::min<int64_t>(B, 65535));
-#define GNPDE_NS(V, M) launch_node_scores<V, M>(grid, ge, s, x, B, N, C, ldx, H, kp, cs, rpb)
+#define GNPDE_NS(V, M) launch_node_scores<V, M>(grid, ge, s, x, B, N, C, ldx, H, uv, cs, rpb)
   if (ge.vec == 4) {
     switch (ge.maxh) {
       case 1: GNPDE_NS(4, 1); break;
@@ -680,10 +704,11 @@ extern "C" {
 int gnpde_softmax_stats_f32(const int32_t* items, int64_t n_items, const int32_t* heavy, int64_t n_heavy,
                             const int32_t* gidx, int group_is_dst, int mode, int64_t heads, int64_t dk,
                             const double* cs, const float* q, const float* k, int64_t ldqk, float score_p0,
-                            float score_p1, double* m, float* rl, double* partials, void* stream) {
+                            float score_p1, double* m, float* rl, double* mr, double* partials,
+                            void* stream) {
   int rc = check_score_args(mode, heads, dk, cs, q, k);
   if (rc) return rc;
-  GNPDE_REQUIRE(m && rl, GNPDE_EINVAL, "softmax_stats: NULL m/rl");
+  GNPDE_REQUIRE((m && rl) || mr, GNPDE_EINVAL, "softmax_stats: no output (m/rl or the packed records)");
   GNPDE_REQUIRE(n_heavy == 0 || partials, GNPDE_EINVAL, "softmax_stats: hub groups need partials");
   if (n_items == 0) return GNPDE_OK;
   GNPDE_REQUIRE(items && gidx, GNPDE_EINVAL, "softmax_stats: NULL items/gidx");
@@ -693,24 +718,24 @@ int gnpde_softmax_stats_f32(const int32_t* items, int64_t n_items, const int32_t
   const Team tm = team_geometry(sa);
   if (tm.T > 0) {
     const unsigned grid = (unsigned)ceil_div(n_items, (int64_t)kWavesPerBlock * (kWave / tm.T));
-    stats_team_kernel<4><<<grid, kBlock, 0, s>>>(it, (int)n_items, gidx, group_is_dst, sa, tm, m, rl, partials);
+    stats_team_kernel<4><<<grid, kBlock, 0, s>>>(it, (int)n_items, gidx, group_is_dst, sa, tm, m, rl, mr, partials);
     GNPDE_LAUNCH_CHECK();
   } else {
   const int GL = 8;  // lanes per item
   const unsigned grid = (unsigned)ceil_div(n_items, (int64_t)kWavesPerBlock * (kWave / GL));
   if (heads <= 1)
-    launch_stats<1>(grid, GL, s, it, (int)n_items, gidx, group_is_dst, sa, m, rl, partials);
+    launch_stats<1>(grid, GL, s, it, (int)n_items, gidx, group_is_dst, sa, m, rl, mr, partials);
   else if (heads <= 2)
-    launch_stats<2>(grid, GL, s, it, (int)n_items, gidx, group_is_dst, sa, m, rl, partials);
+    launch_stats<2>(grid, GL, s, it, (int)n_items, gidx, group_is_dst, sa, m, rl, mr, partials);
   else if (heads <= 4)
-    launch_stats<4>(grid, GL, s, it, (int)n_items, gidx, group_is_dst, sa, m, rl, partials);
+    launch_stats<4>(grid, GL, s, it, (int)n_items, gidx, group_is_dst, sa, m, rl, mr, partials);
   else if (heads <= 8)
-    launch_stats<8>(grid, GL, s, it, (int)n_items, gidx, group_is_dst, sa, m, rl, partials);
+    launch_stats<8>(grid, GL, s, it, (int)n_items, gidx, group_is_dst, sa, m, rl, mr, partials);
   else
-    launch_stats<16>(grid, GL, s, it, (int)n_items, gidx, group_is_dst, sa, m, rl, partials);
+    launch_stats<16>(grid, GL, s, it, (int)n_items, gidx, group_is_dst, sa, m, rl, mr, partials);
   GNPDE_LAUNCH_CHECK();
   }
-  return launch_stats_fixup(reinterpret_cast<const int4*>(heavy), n_heavy, (int)heads, partials, m, rl, s);
+  return launch_stats_fixup(reinterpret_cast<const int4*>(heavy), n_heavy, (int)heads, partials, m, rl, mr, s);
 }
 
 int gnpde_attn_weights_f32(const int32_t* rowidx, const int32_t* col, int64_t nnz, int norm_idx, int mode,
@@ -758,19 +783,11 @@ int gnpde_edge_attention_f32(const int32_t* rowidx, const int32_t* col, const in
 }
 
 size_t gnpde_keysum_workspace_bytes(int64_t B, int64_t N, int64_t C, int64_t att) {
-  (void)att;
+  // most tiles: 4-byte loads (fewest rows per slot), whatever x's alignment
   int rpt, ntiles;
-  keysum_tiles(B, N, &rpt, &ntiles);
-  const int64_t ngroups = ceil_div(ntiles, kKeysumGroup);
-  // tickets (B * ngroups ints, 256-B aligned) | tile partials | group partials
-  const size_t tick = (size_t)ceil_div(B * ngroups * (int64_t)sizeof(int), 256) * 256;
-  return tick + sizeof(double) * (size_t)(B * (ntiles + ngroups) * (C + 1));
-}
-
-size_t gnpde_keysum_ticket_bytes(int64_t B, int64_t N) {
-  int rpt, ntiles;
-  keysum_tiles(B, N, &rpt, &ntiles);
-  return (size_t)ceil_div(B * ceil_div(ntiles, kKeysumGroup) * (int64_t)sizeof(int), 256) * 256;
+  keysum_tiles(B, N, kKeysumBlock / pow2_at_least((int)C, kKeysumBlock), &rpt, &ntiles);
+  // tile shares of S [B][ntiles][att] | U, v per batch element: Cp*Hp = nch*GL*32 < 16*C + 2048, Hp <= 16
+  return sizeof(double) * (size_t)(B * ntiles * att + B * (16 * C + 2048 + 16));
 }
 
 int gnpde_ref_scores_f32(const float* x, int64_t B, int64_t N, int64_t C, int64_t ldx, const int32_t* indeg,
@@ -783,28 +800,23 @@ int gnpde_ref_scores_f32(const float* x, int64_t B, int64_t N, int64_t C, int64_
   GNPDE_REQUIRE(workspace_bytes >= gnpde_keysum_workspace_bytes(B, N, C, att), GNPDE_EINVAL,
                 "ref_scores: workspace too small");
   GNPDE_REQUIRE(att <= 4096, GNPDE_EUNSUPPORTED, "ref_scores: attention_dim too large");
+  GNPDE_REQUIRE(B <= 65535, GNPDE_EUNSUPPORTED, "ref_scores: batch too large");
   GNPDE_REQUIRE((uint64_t)N * heads * 8 < kBufRecords, GNPDE_EUNSUPPORTED, "ref_scores: N*heads too large");
   hipStream_t s = as_stream(stream);
-  const int vec = keysum_vec(C, x, ldx);
-  const int tpr = pow2_at_least((int)ceil_div(C, vec), 256);
-  int rpt, ntiles;
-  keysum_tiles(B, N, &rpt, &ntiles);
-  const int ngroups = (int)ceil_div(ntiles, kKeysumGroup);
-  int* tickets = static_cast<int*>(workspace);
-  double* part = reinterpret_cast<double*>(static_cast<char*>(workspace) + gnpde_keysum_ticket_bytes(B, N));
-  double* gpart = part + B * ntiles * (C + 1);
+  int vec, tpr, rpt, ntiles;
+  keysum_geometry(C, x, ldx, &vec, &tpr);
+  const int rpb = kKeysumBlock / tpr;
+  keysum_tiles(B, N, rpb, &rpt, &ntiles);
   const NsGeom ge = ns_geometry(vec, C, heads);
-  GNPDE_REQUIRE(ns_lds_bytes(ge, (int)att) <= 64 * 1024, GNPDE_EUNSUPPORTED,
-                "ref_scores: key projection (attention_dim %lld, C %lld) does not fit the LDS", (long long)att,
-                (long long)C);
-  const int rpb = kBlock / tpr;
-  const size_t shm = sizeof(double) * (size_t)rpb * (C + 1);
+  const int64_t cp = (int64_t)ge.nch * ge.CW;
+  GNPDE_REQUIRE(ns_uv_doubles(ge) <= 16 * C + 2048 + 16, GNPDE_EUNSUPPORTED, "ref_scores: node-score geometry");
+  double* part = static_cast<double*>(workspace);
+  double* uv = part + B * ntiles * att;
+  const size_t shm = sizeof(double) * (size_t)(rpb + 1) * (C + 1);
   GNPDE_REQUIRE(shm <= 64 * 1024, GNPDE_EUNSUPPORTED, "ref_scores: C too large");
-  GNPDE_REQUIRE((uint64_t)B * (C + 1) * ntiles * 8 < kBufRecords, GNPDE_EUNSUPPORTED, "ref_scores: partials too large");
   const dim3 g1((unsigned)ntiles, (unsigned)B);
-#define GNPDE_KS(V)                                                                                              \
-  keysum_partial_kernel<V><<<g1, kBlock, shm, s>>>(x, N, (int)C, ldx, indeg, rpt, tpr, ntiles, part, gpart, ngroups, \
-                                                   tickets)
+#define GNPDE_KS(V) keysum_partial_kernel<V><<<g1, kKeysumBlock, shm, s>>>(x, N, (int)C, ldx, indeg, Wk, bk, (int)att, rpt, tpr, \
+                                                         ntiles, part)
   if (vec == 4)
     GNPDE_KS(4);
   else if (vec == 2)
@@ -813,8 +825,11 @@ int gnpde_ref_scores_f32(const float* x, int64_t B, int64_t N, int64_t C, int64_
     GNPDE_KS(1);
 #undef GNPDE_KS
   GNPDE_LAUNCH_CHECK();
-  const KeyProj kp{gpart, ngroups, Wq, bq, Wk, bk, (int)att};
-  launch_node_scores_any(s, ge, x, B, N, (int)C, ldx, (int)heads, kp, cs);
+  const size_t shm2 = sizeof(double) * (size_t)(att + kKeysumBlock);
+  key_projection_kernel<<<(unsigned)B, kKeysumBlock, shm2, s>>>(part, ntiles, (int)C, Wq, bq, (int)att, (int)heads,
+                                                                 (int)cp, ge.maxh, uv);
+  GNPDE_LAUNCH_CHECK();
+  launch_node_scores_any(s, ge, x, B, N, (int)C, ldx, (int)heads, uv, cs);
   GNPDE_LAUNCH_CHECK();
   return GNPDE_OK;
 }

@@ -67,7 +67,8 @@ int gnpde_spmm_rhs_bf16(const int32_t* items, int64_t n_items, int32_t* heavy, i
 }
 
 int gnpde_attn_ref_rhs_f32(const int32_t* items, int64_t n_items, int32_t* heavy, int64_t n_heavy,
-                           const int32_t* col, const double* cs, const double* m, const float* rl, int64_t heads,
+                           const int32_t* col, const double* cs, const double* m, const float* rl, const double* mr,
+                           int64_t heads,
                            int64_t C, const float* x, int64_t ldx, const float* x0, int64_t ldx0, const float* alpha,
                            const float* beta, int flags, float* f, int64_t ldf, float* partials,
                            const gnpde_stage_epilogue_t* stage, void* stream) {
@@ -77,7 +78,14 @@ int gnpde_attn_ref_rhs_f32(const int32_t* items, int64_t n_items, int32_t* heavy
   GNPDE_REQUIRE(heads >= 1 && heads <= 16, GNPDE_EUNSUPPORTED, "attn_ref_rhs: heads=%lld not in [1,16]",
                 (long long)heads);
   GNPDE_REQUIRE(n_items >= 0 && n_items < INT32_MAX && n_heavy >= 0, GNPDE_EINVAL, "attn_ref_rhs: bad item counts");
-  GNPDE_REQUIRE(n_items == 0 || (items && col && cs && m && rl), GNPDE_EINVAL, "attn_ref_rhs: NULL plan/col/cs/m/rl");
+  GNPDE_REQUIRE(n_items == 0 || (items && col && cs && ((m && rl) || mr)), GNPDE_EINVAL,
+                "attn_ref_rhs: NULL plan/col/cs/statistics");
+  if (mr) {
+    GNPDE_REQUIRE(heads == 2 && aligned16(mr), GNPDE_EUNSUPPORTED,
+                  "attn_ref_rhs: packed statistics records are read for two heads, 16-byte aligned");
+    RefDstSoftmaxWeights<2, true, true> wp{cs, mr, nullptr, 2};
+    return launch_agg(items, n_items, heavy, n_heavy, col, wp, C, ep, partials, as_stream(stream));
+  }
   if (heads == 2 && aligned16(m) && aligned8(rl)) {
     RefDstSoftmaxWeights<2, true> wp{cs, m, rl, 2};
     return launch_agg(items, n_items, heavy, n_heavy, col, wp, C, ep, partials, as_stream(stream));

@@ -57,15 +57,14 @@ SIGNATURES = {
                                   _i64, _vp, ctypes.POINTER(StageEpilogue), _vp]),
     "gnpde_spmm_rhs_bf16": (_int, [_vp, _i64, _vp, _i64, _vp, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _int, _vp,
                                    _i64, _vp, ctypes.POINTER(StageEpilogue), _vp]),
-    "gnpde_attn_ref_rhs_f32": (_int, [_vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _i64, _i64, _vp, _i64, _vp, _i64,
+    "gnpde_attn_ref_rhs_f32": (_int, [_vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _vp, _i64, _vp, _i64,
                                       _vp, _vp, _int, _vp, _i64, _vp, ctypes.POINTER(StageEpilogue), _vp]),
     "gnpde_linear_f32": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _vp]),
     "gnpde_keysum_workspace_bytes": (_size, [_i64, _i64, _i64, _i64]),
-    "gnpde_keysum_ticket_bytes": (_size, [_i64, _i64]),
     "gnpde_ref_scores_f32": (_int, [_vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _vp, _vp,
                                     _size, _vp]),
     "gnpde_softmax_stats_f32": (_int, [_vp, _i64, _vp, _i64, _vp, _int, _int, _i64, _i64, _vp, _vp, _vp, _i64, _f32,
-                                       _f32, _vp, _vp, _vp, _vp]),
+                                       _f32, _vp, _vp, _vp, _vp, _vp]),
     "gnpde_attn_weights_f32": (_int, [_vp, _vp, _i64, _int, _int, _i64, _i64, _vp, _vp, _vp, _i64, _f32, _f32, _vp,
                                       _vp, _vp, _vp]),
     "gnpde_edge_attention_f32": (_int, [_vp, _vp, _vp, _i64, _int, _int, _i64, _i64, _vp, _vp, _vp, _i64, _f32, _f32,
@@ -74,7 +73,7 @@ SIGNATURES = {
     "gnpde_seg_plan_build": (_int, [_vp, _i64, ctypes.c_int32, _vp, _i64, _vp, _i64, _vp, _i64, c_i64p, c_i64p,
                                     c_i64p]),
     "gnpde_seg_softmax_f32": (_int, [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _int, _int, _int, _i64, _i64,
-                                     _vp, _vp, _vp, _i64, _f32, _f32, _vp, _vp, _vp, _vp, _vp]),
+                                     _vp, _vp, _vp, _i64, _f32, _f32, _vp, _vp, _vp, _vp, _vp, _vp]),
     "gnpde_csr_rowidx": (_int, [_vp, _i64, _i64, _vp, _vp]),
     "gnpde_sddmm_f32": (_int, [_vp, _vp, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _vp, _int, _int, _vp, _vp]),
     "gnpde_softmax_backward_f32": (_int, [_vp, _vp, _i64, _i64, _int, _vp, _vp, _vp, _vp]),

@@ -396,10 +396,10 @@ class ODEFuncTransformerAtt(ODEFunc):
             m, rl = ops.softmax_stats(g, ns, 1) if norm_idx == 1 else (None, None)
             return ops.attn_rhs(g, ns, m, rl, norm_idx, x, fuse=False, **kw)
         ns = lay.node_scores(g, x)
-        # destination-grouped softmax needs its statistics over the CSC first;
-        # source-grouped weights come straight from the scores (K2)
-        m, rl = ops.softmax_stats(g, ns, 1) if norm_idx == 1 else (None, None)
-        return ops.attn_rhs(g, ns, m, rl, norm_idx, x, **kw)
+        # destination-grouped softmax needs its statistics over the CSC first
+        # (attn_rhs computes them: packed records for the fork's two-head
+        # scores); source-grouped weights come straight from the scores (K2)
+        return ops.attn_rhs(g, ns, None, None, norm_idx, x, **kw)
 
     def _rhs_autograd(self, g, x):
         """Training forward: attention [B,E,h] through _EdgeAttention, then the

@@ -560,7 +560,8 @@ def spmm_rhs(g, w_csr, x, x0=None, alpha=None, beta=None, rhs=True, alpha_sigmoi
         if transpose:
             raise ValueError("on-the-fly attention weights aggregate over the CSR only")
         _lib.call("gnpde_attn_ref_rhs_f32", _ptr(plan.items), plan.n_items, _ptr(plan.heavy), plan.n_heavy,
-                  _ptr(grouped.col), _ptr(w_csr.cs), _ptr(w_csr.m), _ptr(w_csr.rl), w_csr.heads, *epi)
+                  _ptr(grouped.col), _ptr(w_csr.cs), _ptr(w_csr.m), _ptr(w_csr.rl), _ptr(w_csr.mr), w_csr.heads,
+                  *epi)
     else:
         _lib.call("gnpde_spmm_rhs_f32", _ptr(plan.items), plan.n_items, _ptr(plan.heavy), plan.n_heavy,
                   _ptr(grouped.col), _ptr(w_csr), *epi)
@@ -584,10 +585,11 @@ def _partials(plan, C, dev):
 class RefDstWeights(object):
     """Weights K1 computes on the fly (gnpde_attn_ref_rhs_f32): the fork's
     scaled_dot under destination-grouped softmax, head-mean per edge from the
-    node scores cs [R,h] and the CSC statistics m [R,h], rl [R,h]."""
+    node scores cs [R,h] and the CSC statistics m [R,h], rl [R,h] or their
+    packed records mr [R, stats_record_doubles(h)] (two heads)."""
 
-    def __init__(self, cs, m, rl, heads):
-        self.cs, self.m, self.rl, self.heads = cs, m, rl, int(heads)
+    def __init__(self, cs, m, rl, heads, mr=None):
+        self.cs, self.m, self.rl, self.heads, self.mr = cs, m, rl, int(heads), mr
 
 
 def spmm_rhs_rows(g, plan, w_csr, x_src, x_rows, row0, x0=None, alpha=None, beta=None, alpha_sigmoid=True,
@@ -671,13 +673,13 @@ _KEYSUM_WS = {}
 
 
 def _keysum_workspace(dev, nbytes):
-    """Key-sum workspace of gnpde_ref_scores_f32: its arrival tickets must be zero
-    on entry and every call leaves them zero, so one zeroed buffer per device,
-    stream and size is kept and reused (also by captured step graphs)."""
+    """Scratch of gnpde_ref_scores_f32 (tile partials, U and v), kept per
+    device, stream and size so that captured step graphs keep reading the
+    buffer they were captured with."""
     key = (str(dev), torch.cuda.current_stream(dev).cuda_stream, int(nbytes))
     ws = _KEYSUM_WS.get(key)
     if ws is None:
-        ws = torch.zeros(int(nbytes), dtype=torch.uint8, device=dev)
+        ws = torch.empty(int(nbytes), dtype=torch.uint8, device=dev)
         _KEYSUM_WS[key] = ws
     return ws
 
@@ -719,10 +721,16 @@ def uniform_scores(heads):
     return NodeScores(_lib.SCORE_UNIFORM, heads, 1)
 
 
-def _seg_call(g, ns, norm_idx, out_kind):
+def stats_record_doubles(heads):
+    """Doubles per packed statistics record (include/gnpde.h GNPDE_STATS_RECORD_DOUBLES)."""
+    return ((heads + (heads + 1) // 2) + 1) & ~1
+
+
+def _seg_call(g, ns, norm_idx, out_kind, packed=False):
     """K2 (gnpde_seg_softmax_f32) over the grouped CSR of the softmax groups:
     out_kind 0 -> head-mean weights in aggregation-CSR order (norm_idx 0 only);
-    1 -> (m, rl).  NotImplemented when the shape is outside the kernel."""
+    1 -> (m, rl), or with packed=True (None, None, mr): the packed statistics
+    records only.  NotImplemented when the shape is outside the kernel."""
     if ns.mode == _lib.SCORE_UNIFORM or (ns.mode == _lib.SCORE_REFERENCE and out_kind == 0):
         return NotImplemented
     eb = _lib.fn("gnpde_seg_block_edges")(ns.mode, ns.heads, ns.dk)
@@ -734,41 +742,48 @@ def _seg_call(g, ns, norm_idx, out_kind):
     plan = grouped.seg_plan(eb)
     dev = grouped.col.device
     H = ns.heads
-    need_stats = out_kind == 1 or plan.n_chunk > 0
+    packed = packed and out_kind == 1
+    need_stats = not packed and (out_kind == 1 or plan.n_chunk > 0)
     m = torch.empty(g.R, H, dtype=torch.float64, device=dev) if need_stats else None
     rl = torch.empty(g.R, H, dtype=torch.float32, device=dev) if need_stats else None
+    mr = torch.empty(g.R, stats_record_doubles(H), dtype=torch.float64, device=dev) if packed else None
     partials = torch.empty(plan.n_slots * 2 * H, dtype=torch.float64, device=dev) if plan.n_slots else None
     w = torch.empty(max(g.nnz, 1), dtype=torch.float32, device=dev) if out_kind == 0 else None
     rc = _lib.call_rc("gnpde_seg_softmax_f32", _ptr(plan.items), plan.n_items, _ptr(plan.chunk_items), plan.n_chunk,
                       _ptr(plan.heavy), plan.n_heavy, _ptr(grouped.rowptr), _ptr(grouped.rowidx), _ptr(grouped.col),
                       int(norm_idx == 1), out_kind, ns.mode, H, ns.dk, _ptr(ns.cs), _ptr(ns.q), _ptr(ns.k), ns.ldqk,
-                      ns.p0, ns.p1, _ptr(w), _ptr(m), _ptr(rl), _ptr(partials), _stream(dev))
+                      ns.p0, ns.p1, _ptr(w), _ptr(m), _ptr(rl), _ptr(mr), _ptr(partials), _stream(dev))
     if rc == _lib.EUNSUPPORTED:
         return NotImplemented
     _lib.check(rc, "gnpde_seg_softmax_f32")
-    return w if out_kind == 0 else (m, rl)
+    if out_kind == 0:
+        return w
+    return (None, None, mr) if packed else (m, rl)
 
 
-def softmax_stats(g, ns, norm_idx, seg=True):
+def softmax_stats(g, ns, norm_idx, seg=True, packed=False):
     """m [R,h] fp64, rl [R,h]: per-group max and 1/(sum-exp + 1e-16)
     (utils.softmax, src/utils.py:116-127).  seg=True: the edge-block kernel K2;
     shapes outside it (and seg=False) use the per-group kernels
-    (gnpde_softmax_stats_f32)."""
+    (gnpde_softmax_stats_f32).  packed=True returns (None, None, mr): the same
+    statistics as packed records [R, stats_record_doubles(h)] only (the form
+    the fused-weight K1 reads in one cache line per edge)."""
     if seg:
-        r = _seg_call(g, ns, norm_idx, 1)
+        r = _seg_call(g, ns, norm_idx, 1, packed=packed)
         if r is not NotImplemented:
             return r
     grouped = g.csr if norm_idx == 0 else g.csc
     plan = grouped.stats_plan
     dev = grouped.col.device
     H = ns.heads
-    m = torch.empty(g.R, H, dtype=torch.float64, device=dev)
-    rl = torch.empty(g.R, H, dtype=torch.float32, device=dev)
+    m = None if packed else torch.empty(g.R, H, dtype=torch.float64, device=dev)
+    rl = None if packed else torch.empty(g.R, H, dtype=torch.float32, device=dev)
+    mr = torch.empty(g.R, stats_record_doubles(H), dtype=torch.float64, device=dev) if packed else None
     partials = torch.empty(plan.n_slots * 2 * H, dtype=torch.float64, device=dev) if plan.n_slots else None
     _lib.call("gnpde_softmax_stats_f32", _ptr(plan.items), plan.n_items, _ptr(plan.heavy), plan.n_heavy,
               _ptr(grouped.col), int(norm_idx == 1), ns.mode, H, ns.dk, _ptr(ns.cs), _ptr(ns.q), _ptr(ns.k), ns.ldqk,
-              ns.p0, ns.p1, _ptr(m), _ptr(rl), _ptr(partials), _stream(dev))
-    return m, rl
+              ns.p0, ns.p1, _ptr(m), _ptr(rl), _ptr(mr), _ptr(partials), _stream(dev))
+    return (None, None, mr) if packed else (m, rl)
 
 
 def attn_weights(g, ns, m, rl, norm_idx, seg=True):
@@ -791,15 +806,20 @@ def attn_weights(g, ns, m, rl, norm_idx, seg=True):
 
 
 def attn_rhs(g, ns, m, rl, norm_idx, x, x0=None, alpha=None, beta=None, rhs=True, alpha_sigmoid=True,
-             add_source=False, out=None, stage=None, seg=True, fuse=True):
+             add_source=False, out=None, stage=None, seg=True, fuse=True, mr=None):
     """K2 + K1: f = a*(A_att x - x) [+ b x0], A_att = head-mean softmax weights
-    (m, rl: destination statistics for norm_idx 1, or None to compute them).
+    (m, rl: destination statistics for norm_idx 1, or None to compute them;
+    mr: the same statistics as packed records, softmax_stats(packed=True)).
     Reference scores under norm_idx 1 (fuse=True): the weights are computed
-    inside K1 from (cs, m, rl) — same bits as the separate weights pass."""
+    inside K1 from (cs, m, rl) or (cs, mr) — same bits as the separate weights
+    pass.  Two heads with no statistics given: the packed records."""
     if fuse and norm_idx == 1 and ns.mode == _lib.SCORE_REFERENCE and x.dtype == torch.float32:
-        if m is None:
-            m, rl = softmax_stats(g, ns, 1, seg=seg)
-        w = RefDstWeights(ns.cs, m, rl, ns.heads)
+        if m is None and mr is None:
+            if ns.heads == 2:
+                _, _, mr = softmax_stats(g, ns, 1, seg=seg, packed=True)
+            else:
+                m, rl = softmax_stats(g, ns, 1, seg=seg)
+        w = RefDstWeights(ns.cs, m, rl, ns.heads, mr=mr)
         return spmm_rhs(g, w, x, x0=x0, alpha=alpha, beta=beta, rhs=rhs, alpha_sigmoid=alpha_sigmoid,
                         add_source=add_source, out=out, stage=stage)
     w = attn_weights(g, ns, m, rl, norm_idx, seg=seg)

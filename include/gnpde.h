@@ -227,12 +227,17 @@ int gnpde_spmm_rhs_bf16(const int32_t* items, int64_t n_items, int32_t* heavy, i
  * (reference score mode) under destination-grouped softmax (attention_norm_idx
  * 1): w_p = mean_h exp(cs[row,h] - m[col_p,h]) * rl[col_p,h], cs [R,H] fp64 node
  * scores (gnpde_ref_scores_f32), m [R,H] fp64 / rl [R,H] group statistics
- * (gnpde_softmax_stats_f32 / gnpde_seg_softmax_f32 over the CSC).  Equals
- * gnpde_attn_weights_f32 + gnpde_spmm_rhs_f32 bit for bit, in one pass:
+ * (gnpde_softmax_stats_f32 / gnpde_seg_softmax_f32 over the CSC), or, when
+ * mr is given (heads == 2, 16-byte aligned), the packed statistics records
+ * those kernels write into mr (GNPDE_STATS_RECORD_DOUBLES(heads) doubles per
+ * group: m[0..h-1], then rl[0..h-1] as floats): one cache line per edge.
+ * Equals gnpde_attn_weights_f32 + gnpde_spmm_rhs_f32 bit for bit, in one pass:
  * ODEFuncTransformerAtt.forward, function_transformer_attention.py:44-59.
  * Other arguments as gnpde_spmm_rhs_f32.                                     */
+#define GNPDE_STATS_RECORD_DOUBLES(h) ((((h) + ((h) + 1) / 2) + 1) & ~1)
 int gnpde_attn_ref_rhs_f32(const int32_t* items, int64_t n_items, int32_t* heavy, int64_t n_heavy,
-                           const int32_t* col, const double* cs, const double* m, const float* rl, int64_t heads,
+                           const int32_t* col, const double* cs, const double* m, const float* rl, const double* mr,
+                           int64_t heads,
                            int64_t C, const float* x, int64_t ldx, const float* x0, int64_t ldx0, const float* alpha,
                            const float* beta, int flags, float* f, int64_t ldf, float* partials,
                            const gnpde_stage_epilogue_t* stage, void* stream);
@@ -251,15 +256,11 @@ int gnpde_linear_f32(const float* x, int64_t R, int64_t K, int64_t ldx, const fl
 /* Reference-mode node scores (fork scaled_dot, function_transformer_attention.py:249):
  *   S_b = Wk * (sum_n indeg(n) x_n) + (sum_n indeg(n)) bk    (fp64)
  *   cs[r,h] = (q_r,h . S_b,h) / sqrt(dk),  q = Wq x + bq      (fp64 out)
- * indeg: in-degree per global node (int32, R); ws: gnpde_keysum_workspace_bytes.
- * Two launches: indegree-weighted column sums (fp64 row tiles; the last tile of
- * each group of 32 to finish sums the group, through an arrival ticket), then
- * the node scores, whose workgroups each sum the group partials and form S_b
- * and U = Wq^T S / sqrt(dk) in LDS.  attention_dim <= 4096.
- * Workspace contract: its first gnpde_keysum_ticket_bytes(B, N) bytes are the
- * arrival tickets — zero before the first call, left zero by every call — so
- * keep one workspace per stream (calls on one workspace must not overlap).  */
-size_t gnpde_keysum_ticket_bytes(int64_t B, int64_t N);
+ * indeg: in-degree per global node (int32, R); ws: gnpde_keysum_workspace_bytes
+ * (scratch, no state between calls).  Three launches: indegree-weighted column
+ * sums over ~256 fp64 row tiles; one workgroup per batch element summing the
+ * tiles in fixed order and forming S_b, U = Wq^T S / sqrt(dk) and v; the node
+ * scores cs = x U + v.  attention_dim <= 4096.                               */
 size_t gnpde_keysum_workspace_bytes(int64_t B, int64_t N, int64_t C, int64_t att);
 int gnpde_ref_scores_f32(const float* x, int64_t B, int64_t N, int64_t C, int64_t ldx, const int32_t* indeg,
                          const float* Wq, const float* bq, const float* Wk, const float* bk,
@@ -273,12 +274,14 @@ int gnpde_ref_scores_f32(const float* x, int64_t B, int64_t N, int64_t C, int64_
  * partials: 2*heads doubles per plan slot.
  * Edge scores by `mode` from cs (REFERENCE) or q/k (per-edge modes).
  * Groups of 8 lanes per item: plan it with a small chunk (e.g. 64).
+ * m, rl and mr (packed records, see gnpde_attn_ref_rhs_f32) are each optional;
+ * m and rl come as a pair, and at least one of the two forms is written.
  * Restates utils.softmax, src/utils.py:116-127.                              */
 int gnpde_softmax_stats_f32(const int32_t* items, int64_t n_items, const int32_t* heavy, int64_t n_heavy,
                             const int32_t* gidx, int group_is_dst, int mode, int64_t heads, int64_t dk,
                             const double* cs, const float* q, const float* k, int64_t ldqk,
                             float score_p0, float score_p1,
-                            double* m, float* rl, double* partials, void* stream);
+                            double* m, float* rl, double* mr, double* partials, void* stream);
 
 /* Head-mean attention weights in aggregation-CSR order (edge-parallel):
  *   w[p] = (1/h) sum_h exp(s_p,h - m[g,h]) * rl[g,h],  g = src (norm_idx 0) or dst (1)
@@ -305,7 +308,8 @@ int gnpde_attn_weights_f32(const int32_t* rowidx, const int32_t* col, int64_t nn
  * (stored back to back) both item kinds run in one launch.
  *   out_kind 0: w[p] = (1/H) sum_h softmax_p,h in grouped order (per-edge
  *               modes with norm_idx 0: the aggregation weights of K1);
- *   out_kind 1: m[g,h] = max (fp64), rl[g,h] = 1/(sum exp(s - m) + 1e-16).
+ *   out_kind 1: m[g,h] = max (fp64), rl[g,h] = 1/(sum exp(s - m) + 1e-16),
+ *               into m/rl and/or the packed records mr (gnpde_attn_ref_rhs_f32).
  * Per-group max and sum come from segmented scans across the lanes (fixed
  * order, deterministic).  Restates utils.softmax, src/utils.py:116-127, with
  * the scores of function_transformer_attention.py:246-259 and the head mean of
@@ -319,8 +323,8 @@ int gnpde_seg_softmax_f32(const int32_t* items, int64_t n_items, const int32_t* 
                           const int32_t* heavy, int64_t n_heavy, const int32_t* rowptr, const int32_t* rowidx,
                           const int32_t* gidx, int group_is_dst, int out_kind, int mode, int64_t heads, int64_t dk,
                           const double* cs, const float* q, const float* k, int64_t ldqk,
-                          float score_p0, float score_p1, float* w, double* m, float* rl, double* partials,
-                          void* stream);
+                          float score_p0, float score_p1, float* w, double* m, float* rl, double* mr,
+                          double* partials, void* stream);
 
 /* Per-edge, per-head attention in COO order (the [B,E,h] `attention` that
  * SpGraphTransAttentionLayer.forward returns, function_transformer_attention.py:265-267):

@@ -81,7 +81,7 @@ def test_errors_are_reported_not_raised():
     rc = lib.gnpde_csr_build(vp(0), 1, 10, 5, 2, vp(0), vp(0), vp(0), vp(0), 0, vp(0))
     assert rc == -1 and b"key_row" in lib.gnpde_last_error()
     rc = lib.gnpde_softmax_stats_f32(vp(0), 0, vp(0), 0, vp(0), 0, 0, 17, 1, vp(0), vp(0), vp(0), 1,
-                                     ctypes.c_float(1), ctypes.c_float(1), vp(0), vp(0), vp(0), vp(0))
+                                     ctypes.c_float(1), ctypes.c_float(1), vp(0), vp(0), vp(0), vp(0), vp(0))
     assert rc == -3 and b"heads" in lib.gnpde_last_error()
     rc = lib.gnpde_rk_combine_f32(16, vp(0), 9, None, None, ctypes.c_double(1.0), vp(1), vp(0))
     assert rc == -3

@@ -354,6 +354,18 @@ def test_seg_softmax_reference_norm1(heads, att):
     # weights computed inside K1 (gnpde_attn_ref_rhs_f32) == separate weights pass + K1, bit for bit
     f_unfused = ops.attn_rhs(g, ns, m, rl, 1, T(x), alpha=torch.tensor(0.25, device=DEV), fuse=False)
     assert torch.equal(f, f_unfused)
+    # packed statistics records (m then rl in one record per group): the same values, and for two
+    # heads the K1 that reads them gives the same bits
+    for seg in (True, False):
+        _, _, mr = ops.softmax_stats(g, ns, 1, seg=seg, packed=True)
+        mm, rr = (m, rl) if seg else (m2, rl2)
+        assert mr.shape == (g.R, ops.stats_record_doubles(heads))
+        assert torch.equal(mr[nz, :heads], mm[nz])
+        assert torch.equal(mr[:, heads:].contiguous().view(torch.float32)[nz, :heads], rr[nz])
+        if heads == 2:
+            f_rec = ops.attn_rhs(g, ns, None, None, 1, T(x), alpha=torch.tensor(0.25, device=DEV), mr=mr)
+            f_ref = f if seg else ops.attn_rhs(g, ns, m2, rl2, 1, T(x), alpha=torch.tensor(0.25, device=DEV))
+            assert torch.equal(f_rec, f_ref)
 
 
 @pytest.mark.parametrize("attention_type", ["exp_kernel", "cosine_sim", "pearson"])
