@@ -132,6 +132,115 @@ __device__ __forceinline__ float seg_team_score(const ScoreArgs& sa, const float
   return team_score_regs<4>(sa, q, k, S);
 }
 
+// ------------------------------------------------------------------ long groups (reference statistics)
+// Reference-score statistics take groups longer than a wavefront's EB edges as
+// LONG items, lanes striding over the edges (kSegLongU per lane per pass, each
+// lane an online (max, sum-exp) per head, a fixed xor tree across lanes):
+//   slot field -2:        a whole group of at most kSegLongMax edges -> m, rl / mr;
+//   slot field -3 - slot: a kSegLongMax-edge chunk of a longer group -> its partial
+//                         statistics (write-through); the chunk that arrives last
+//                         (agent-scope ticket in heavy[].w, as K1's hub rows)
+//                         merges the group's chunks in chunk order, reading them
+//                         with sc1 loads, and resets the ticket.
+// With 256-edge chunks G-arxiv's CSC has 239 chunked groups (at most 29 chunks
+// each) instead of 3,707 groups of 64-edge chunks and a fixup launch.
+constexpr int kSegLongU = 4;                   // edges per lane per pass
+constexpr int kSegLongMax = kWave * kSegLongU;  // 256: one pass
+
+__device__ __forceinline__ double load_sc1_f64(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, kAuxSc1));
+}
+
+__device__ __forceinline__ void seg_long_stats(int e0, int e1, int grp, int slot, const int* __restrict__ gidx,
+                                               int group_is_dst, const ScoreArgs& sa, double* m, float* rl,
+                                               double* mr, double* partials, int4* heavy, int n_heavy) {
+  const int lane = threadIdx.x & 63;
+  const int H = sa.H;
+  const __amdgpu_buffer_rsrc_t rp = buf_rsrc(partials);
+  for (int h0 = 0; h0 < H; h0 += 2) {
+    const bool two = h0 + 1 < H;
+    double M0 = -INFINITY, M1 = -INFINITY;
+    float L0 = 0.f, L1 = 0.f;
+    for (int pb = e0; pb < e1; pb += kSegLongMax) {
+      int src[kSegLongU];
+#pragma unroll
+      for (int u = 0; u < kSegLongU; ++u) {
+        const int p = pb + lane + kWave * u;
+        src[u] = p < e1 ? (group_is_dst ? gidx[p] : grp) : -1;
+      }
+      double a[kSegLongU], b[kSegLongU];
+#pragma unroll
+      for (int u = 0; u < kSegLongU; ++u) {
+        const int64_t o = (int64_t)max(src[u], 0) * H + h0;
+        a[u] = sa.cs[o];
+        b[u] = two ? sa.cs[o + 1] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < kSegLongU; ++u) {
+        if (src[u] >= 0) {
+          online_push(M0, L0, a[u]);
+          if (two) online_push(M1, L1, b[u]);
+        }
+      }
+    }
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+      const double Ma = __shfl_xor(M0, o), Mb = __shfl_xor(M1, o);
+      const float La = __shfl_xor(L0, o), Lb = __shfl_xor(L1, o);
+      online_merge(M0, L0, Ma, La);
+      online_merge(M1, L1, Mb, Lb);
+    }
+    if (slot < 0) {
+      if (lane == 0) {
+        store_stats(m, rl, mr, grp, H, h0, M0, 1.0f / (L0 + kSoftmaxEps));
+        if (two) store_stats(m, rl, mr, grp, H, h0 + 1, M1, 1.0f / (L1 + kSoftmaxEps));
+      }
+    } else {  // partials [slot][2H]: max then sum-exp, write-through
+      const uint32_t o = (uint32_t)(((int64_t)slot * 2 * H + h0) * 8);
+      const bool w0 = lane == 0, w1 = lane == 0 && two;
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, M0), rp, w0 ? o : kBufNone, 0, kAuxSc1);
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, (double)L0), rp, w0 ? o + 8u * H : kBufNone, 0,
+                                            kAuxSc1);
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, M1), rp, w1 ? o + 8u : kBufNone, 0, kAuxSc1);
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, (double)L1), rp, w1 ? o + 8u * H + 8u : kBufNone,
+                                            0, kAuxSc1);
+    }
+  }
+  if (slot < 0) return;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this chunk's partials have reached the memory side
+  int lo = 0, hi = n_heavy - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (heavy[mid].y <= slot)
+      lo = mid;
+    else
+      hi = mid - 1;
+  }
+  int ticket = 0;
+  if (lane == 0) ticket = __hip_atomic_fetch_add(&heavy[lo].w, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  ticket = __shfl(ticket, 0);
+  const int4 hv = heavy[lo];
+  const int g = uniform(hv.x), first = uniform(hv.y), nch = uniform(hv.z);
+  if (ticket != nch - 1) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the sc1 loads below the ticket
+  for (int h = 0; h < H; ++h) {
+    double M = -INFINITY;
+    float L = 0.f;
+    for (int c = lane; c < nch; c += kWave) {
+      const uint32_t o = (uint32_t)(((int64_t)(first + c) * 2 * H + h) * 8);
+      online_merge(M, L, load_sc1_f64(rp, o), (float)load_sc1_f64(rp, o + 8u * H));
+    }
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+      const double M2 = __shfl_xor(M, o);
+      const float L2 = __shfl_xor(L, o);
+      online_merge(M, L, M2, L2);
+    }
+    if (lane == 0) store_stats(m, rl, mr, g, H, h, M, 1.0f / (L + kSoftmaxEps));
+  }
+  if (lane == 0) __hip_atomic_store(&heavy[lo].w, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <bool REF, int OUT>
 __global__ __launch_bounds__(256) void seg_softmax_kernel(const int4* __restrict__ items, int n_items,
                                                            const int* __restrict__ rowptr,
@@ -139,7 +248,8 @@ __global__ __launch_bounds__(256) void seg_softmax_kernel(const int4* __restrict
                                                            const int* __restrict__ gidx, int group_is_dst,
                                                            ScoreArgs sa, Team tm, float* __restrict__ w,
                                                            double* __restrict__ m, float* __restrict__ rl,
-                                                           double* __restrict__ mr, double* __restrict__ partials) {
+                                                           double* __restrict__ mr, double* __restrict__ partials,
+                                                           int4* heavy, int n_heavy) {
   using S_t = typename std::conditional<REF, double, float>::type;
   const int lane = threadIdx.x & 63;
   const int item = uniform(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
@@ -148,6 +258,12 @@ __global__ __launch_bounds__(256) void seg_softmax_kernel(const int4* __restrict
   const int e0 = uniform(it.x), e1 = uniform(it.y), slot = uniform(it.z);
   const int n = e1 - e0;
   if (n <= 0) return;
+  if (slot <= -2) {  // long item (reference statistics only; other kinds are rejected by the host)
+    if constexpr (REF && OUT == kSegStats)
+      seg_long_stats(e0, e1, uniform(it.w), slot == -2 ? -1 : -3 - slot, gidx, group_is_dst, sa, m, rl, mr, partials,
+                     heavy, n_heavy);
+    return;
+  }
   const bool live = lane < n;
   const int p = e0 + min(lane, n - 1);
   const int grp = rowidx[p];
@@ -229,10 +345,10 @@ __global__ __launch_bounds__(256) void seg_softmax_kernel(const int4* __restrict
 template <bool REF, int OUT>
 static int launch_seg(const int4* items, int64_t n, const int* rowptr, const int* rowidx, const int* gidx, int gid,
                       const ScoreArgs& sa, const Team& tm, float* w, double* m, float* rl, double* mr,
-                      double* partials, hipStream_t s) {
+                      double* partials, int4* heavy, int n_heavy, hipStream_t s) {
   if (n <= 0) return GNPDE_OK;
   seg_softmax_kernel<REF, OUT><<<(unsigned)ceil_div(n, kWavesPerBlock), kBlock, 0, s>>>(
-      items, (int)n, rowptr, rowidx, gidx, gid, sa, tm, w, m, rl, mr, partials);
+      items, (int)n, rowptr, rowidx, gidx, gid, sa, tm, w, m, rl, mr, partials, heavy, n_heavy);
   GNPDE_LAUNCH_CHECK();
   return GNPDE_OK;
 }
@@ -302,7 +418,7 @@ int gnpde_seg_plan_build(const int32_t* rowptr, int64_t R, int32_t eb, int32_t* 
 }
 
 int gnpde_seg_softmax_f32(const int32_t* items, int64_t n_items, const int32_t* chunk_items, int64_t n_chunk_items,
-                          const int32_t* heavy, int64_t n_heavy, const int32_t* rowptr, const int32_t* rowidx,
+                          int32_t* heavy, int64_t n_heavy, const int32_t* rowptr, const int32_t* rowidx,
                           const int32_t* gidx, int group_is_dst, int out_kind, int mode, int64_t heads, int64_t dk,
                           const double* cs, const float* q, const float* k, int64_t ldqk, float score_p0,
                           float score_p1, float* w, double* m, float* rl, double* mr, double* partials,
@@ -334,11 +450,13 @@ int gnpde_seg_softmax_f32(const int32_t* items, int64_t n_items, const int32_t* 
   hipStream_t s = as_stream(stream);
   const int4* it = reinterpret_cast<const int4*>(items);
   const int4* ch = reinterpret_cast<const int4*>(chunk_items);
-  const int4* hv = reinterpret_cast<const int4*>(heavy);
+  int4* hv = reinterpret_cast<int4*>(heavy);
   const bool ref = mode == GNPDE_SCORE_REFERENCE;
-#define GNPDE_SEG(R, O, ITEMS, N) \
+  GNPDE_REQUIRE((uint64_t)(n_items + n_chunk_items) * 2 * heads * 8 < kBufRecords && n_heavy < INT32_MAX,
+                GNPDE_EUNSUPPORTED, "seg_softmax: partials too large");
+#define GNPDE_SEG(R, O, ITEMS, N)                                                                                  \
   launch_seg<R, O>(ITEMS, N, rowptr, rowidx, gidx, group_is_dst, sa, tm, w, m, rl, (O) == kSegStats ? mr : nullptr, \
-                   partials, s)
+                   partials, hv, (int)n_heavy, s)
   // whole-group items and long-group chunks share one kernel (the slot field
   // tells them apart): one launch when the caller stores them back to back
   const bool adjacent = n_items > 0 && n_chunk_items > 0 && ch == it + n_items;

@@ -108,12 +108,15 @@ class GroupedCSR(object):
             self._rowidx = ri
         return self._rowidx
 
-    def seg_plan(self, eb):
+    def seg_plan(self, eb, long_items=False):
         """Edge-block plan of the segmented-softmax kernel (K2) for blocks of at
-        most ``eb`` edges (SegPlan), built once per grouped CSR and block size."""
-        if eb not in self._seg_plans:
-            self._seg_plans[eb] = build_seg_plan(self.rowptr, eb)
-        return self._seg_plans[eb]
+        most ``eb`` edges (SegPlan), built once per grouped CSR and block size.
+        long_items=True (reference-score statistics): groups longer than eb
+        as long items instead of eb-edge chunks + a fixup launch."""
+        key = (eb, bool(long_items))
+        if key not in self._seg_plans:
+            self._seg_plans[key] = build_seg_plan(self.rowptr, eb, long_items)
+        return self._seg_plans[key]
 
     @property
     def stats_plan(self):
@@ -175,8 +178,15 @@ class SegPlan(object):
         self.n_slots = n_chunk
 
 
-def build_seg_plan(rowptr, eb):
-    """gnpde_seg_plan_build on a host copy of rowptr (once per graph and block size)."""
+SEG_LONG_MAX = 256  # edges of a long item (csrc/attention.hip kSegLongMax)
+
+
+def build_seg_plan(rowptr, eb, long_items=False):
+    """gnpde_seg_plan_build on a host copy of rowptr (once per graph and block size).
+    long_items=True: every group longer than eb becomes one item {e_begin,
+    e_end, -2, group} when it has at most SEG_LONG_MAX edges, else SEG_LONG_MAX-
+    edge chunk items {.., -3 - slot, group} merged inside the launch (heavy
+    {group, first_slot, n_chunks, 0}); long items come first, longest first."""
     rp = np.ascontiguousarray(rowptr.cpu().numpy().astype(np.int32))
     R = rp.shape[0] - 1
     nnz = int(rp[-1])
@@ -191,6 +201,29 @@ def build_seg_plan(rowptr, eb):
 
     def dev32(a, n):
         return torch.from_numpy(np.ascontiguousarray(a[:max(n, 1)]).reshape(-1)).to(dev)
+
+    if long_items:
+        rows = heavy[:nh.value, 0].astype(np.int64)
+        s0, s1 = rp[rows].astype(np.int64), rp[rows + 1].astype(np.int64)
+        order = np.argsort(-(s1 - s0), kind="stable")
+        out, hv, slot = [], [], 0
+        for i in order:
+            r, a, b = int(rows[i]), int(s0[i]), int(s1[i])
+            if b - a <= SEG_LONG_MAX:
+                out.append((a, b, -2, r))
+                continue
+            nch = (b - a + SEG_LONG_MAX - 1) // SEG_LONG_MAX
+            hv.append((r, slot, nch, 0))
+            for c in range(nch):
+                out.append((a + c * SEG_LONG_MAX, min(b, a + (c + 1) * SEG_LONG_MAX), -3 - slot, r))
+                slot += 1
+        long_arr = np.asarray(out, np.int32).reshape(-1, 4)
+        all_items = np.concatenate([long_arr, items[:ni.value]], 0)
+        hv_arr = np.asarray(hv, np.int32).reshape(-1, 4) if hv else np.zeros((1, 4), np.int32)
+        plan = SegPlan(eb, dev32(all_items, all_items.shape[0]), all_items.shape[0], dev32(np.zeros((1, 4), np.int32), 0),
+                       0, dev32(hv_arr, len(hv)), len(hv))
+        plan.n_slots = slot
+        return plan
 
     # items and chunk items back to back in one buffer: K2 then covers both in one launch
     both = dev32(np.concatenate([items[:ni.value], chunks[:max(nc.value, 1)]], 0), ni.value + max(nc.value, 1))
@@ -739,7 +772,7 @@ def _seg_call(g, ns, norm_idx, out_kind, packed=False):
     if ns.q is not None and (ns.ldqk % 4 or ns.q.data_ptr() % 16 or ns.k.data_ptr() % 16):
         return NotImplemented
     grouped = g.csr if norm_idx == 0 else g.csc
-    plan = grouped.seg_plan(eb)
+    plan = grouped.seg_plan(eb, long_items=ns.mode == _lib.SCORE_REFERENCE and out_kind == 1)
     dev = grouped.col.device
     H = ns.heads
     packed = packed and out_kind == 1

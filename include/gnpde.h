@@ -302,6 +302,12 @@ int gnpde_attn_weights_f32(const int32_t* rowidx, const int32_t* col, int64_t nn
  * (packed greedily up to EB edges); chunk_items {e_begin, e_end, slot, group}
  * split groups of degree > EB, heavy {group, first_slot, n_chunks, 0} lists
  * those groups (partials: 2*heads doubles per slot; m/rl scratch).
+ * Reference scores with out_kind 1 also take LONG items inside `items`:
+ * {e_begin, e_end, -2, group} = a whole group of at most 256 edges, and
+ * {e_begin, e_end, -3 - slot, group} = a 256-edge chunk of a longer group whose
+ * partials the last-arriving chunk merges inside the launch (agent-scope ticket
+ * in heavy[].w: zero on entry, left zero; launches on one heavy array must not
+ * overlap); heavy then lists those groups, and no fixup runs.
  * gnpde_seg_plan_build builds them from a HOST copy of rowptr into HOST
  * arrays (plain C++, once per graph; capacities: items >= R, chunk_items >=
  * nnz/eb + R, heavy >= nnz/eb + 1).  When chunk_items == items + 4*n_items
@@ -320,7 +326,7 @@ int gnpde_seg_plan_build(const int32_t* rowptr, int64_t R, int32_t eb, int32_t* 
                          int32_t* chunk_items, int64_t chunks_capacity, int32_t* heavy, int64_t heavy_capacity,
                          int64_t* n_items, int64_t* n_chunks, int64_t* n_heavy);
 int gnpde_seg_softmax_f32(const int32_t* items, int64_t n_items, const int32_t* chunk_items, int64_t n_chunk_items,
-                          const int32_t* heavy, int64_t n_heavy, const int32_t* rowptr, const int32_t* rowidx,
+                          int32_t* heavy, int64_t n_heavy, const int32_t* rowptr, const int32_t* rowidx,
                           const int32_t* gidx, int group_is_dst, int out_kind, int mode, int64_t heads, int64_t dk,
                           const double* cs, const float* q, const float* k, int64_t ldqk,
                           float score_p0, float score_p1, float* w, double* m, float* rl, double* mr,

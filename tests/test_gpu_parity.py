@@ -279,8 +279,7 @@ def _check_seg_plan(grouped, eb):
     assert all(b in starts and e in starts for b, e in it[:, :2])
 
 
-@pytest.mark.parametrize("score_mode", ["reference", "per_edge"])
-def test_seg_stats_one_launch_equals_two_and_repeats(score_mode):
+def test_seg_stats_one_launch_equals_two_and_repeats():
     """Items and long groups' chunks stored back to back (one launch) give the
     same statistics, bit for bit, as the two arrays in separate buffers (two
     launches), on every one of several repeats."""
@@ -288,22 +287,65 @@ def test_seg_stats_one_launch_equals_two_and_repeats(score_mode):
     N, E = 1500, 24000
     ei, x, x0, Wq, bq, Wk, bk = _attn_case(N, E, 128, 2, 32, seed=77)
     g = ops.GraphCSR(T(ei), N)
-    ns = ops.node_scores(g, T(x), T(Wq), T(bq), T(Wk), T(bk), 2, 'scaled_dot', score_mode)
+    ns = ops.node_scores(g, T(x), T(Wq), T(bq), T(Wk), T(bk), 2, 'scaled_dot', 'per_edge')
     m1, rl1 = ops.softmax_stats(g, ns, 1)
-    eb = [k for k in g.csc._seg_plans][0]
-    plan = g.csc._seg_plans[eb]
+    key = [k for k in g.csc._seg_plans][0]
+    plan = g.csc._seg_plans[key]
     assert plan.n_chunk > 0 and plan.n_items > 0
     for _ in range(3):
         m, rl = ops.softmax_stats(g, ns, 1)
         assert torch.equal(m, m1) and torch.equal(rl, rl1)
     p2 = copy.copy(plan)
     p2.items, p2.chunk_items = plan.items.clone(), plan.chunk_items.clone()
-    g.csc._seg_plans[eb] = p2
+    g.csc._seg_plans[key] = p2
     m2, rl2 = ops.softmax_stats(g, ns, 1)
     torch.cuda.synchronize()
     assert torch.equal(m2, m1) and torch.equal(rl2, rl1)
+
+
+@pytest.mark.parametrize("norm_idx", [0, 1])
+@pytest.mark.parametrize("heads,att", [(2, 32), (3, 24)])
+def test_seg_stats_long_items(norm_idx, heads, att):
+    """Reference-score statistics take groups longer than a wavefront's block
+    as long items (whole groups up to 256 edges; 256-edge chunks merged inside
+    the launch by the last-arriving chunk): the plan tiles every edge once, long
+    items come first, repeats are bit-identical (tickets back to 0), and the
+    statistics match the 64-edge-chunk plan + fixup (max exactly, 1/sum to fp32
+    rounding of the other summation order) and the oracle RHS."""
+    N, E = 1500, 40000
+    ei, x, x0, Wq, bq, Wk, bk = _attn_case(N, E, 128, heads, att, seed=78)
+    ei[:, norm_idx, :3000] = 7   # one group of several 256-edge chunks
+    ei[:, norm_idx, 3000:3200] = 9  # and one whole long group
+    g = ops.GraphCSR(T(ei), N)
+    ns = ops.node_scores(g, T(x), T(Wq), T(bq), T(Wk), T(bk), heads, 'scaled_dot', 'reference')
+    grouped = g.csc if norm_idx == 1 else g.csr
+    m1, rl1 = ops.softmax_stats(g, ns, norm_idx)
+    plan = grouped.seg_plan(64, long_items=True)
+    rp = grouped.rowptr.cpu().numpy()
+    it = plan.items.cpu().numpy().reshape(-1, 4)[:plan.n_items]
+    lng = it[it[:, 2] <= -2]
+    assert plan.n_chunk == 0 and plan.n_heavy >= 1 and (it[:len(lng), 2] <= -2).all()
+    assert (lng[:, 1] - lng[:, 0] <= ops.SEG_LONG_MAX).all()
+    assert (it[len(lng):, 2] == -1).all() and (it[len(lng):, 1] - it[len(lng):, 0] <= 64).all()
+    spans = it[:, :2][np.argsort(it[:, 0])]
+    assert spans[0, 0] == 0 and spans[-1, 1] == rp[-1] and (spans[1:, 0] == spans[:-1, 1]).all()
+    hv = plan.heavy.view(-1, 4)[:plan.n_heavy].cpu().numpy()
+    assert 7 in hv[:, 0]
+    for _ in range(3):
+        m, rl = ops.softmax_stats(g, ns, norm_idx)
+        assert torch.equal(m, m1) and torch.equal(rl, rl1)
     assert int(plan.heavy.view(-1, 4)[:plan.n_heavy, 3].abs().sum()) == 0
-    assert int(p2.heavy.view(-1, 4)[:p2.n_heavy, 3].abs().sum()) == 0
+    g2 = ops.GraphCSR(T(ei), N)
+    gr2 = g2.csc if norm_idx == 1 else g2.csr
+    gr2._seg_plans[(64, True)] = gr2.seg_plan(64)  # the chunked plan + fixup
+    m2, rl2 = ops.softmax_stats(g2, ns, norm_idx)
+    nz = torch.from_numpy(np.diff(rp) > 0).to(DEV)
+    assert torch.equal(m1[nz], m2[nz])
+    assert torch.allclose(rl1[nz], rl2[nz], rtol=2e-6, atol=0)
+    if norm_idx == 1:
+        f = ops.attn_rhs(g, ns, None, None, 1, T(x), alpha=torch.tensor(0.25, device=DEV))
+        want = O.transformer_rhs(ei, x, None, Wq, bq, Wk, bk, heads, 1, 0.25, 0.0)
+        assert rel(f, want) <= RTOL
 
 
 @pytest.mark.parametrize("C,h,att", [(128, 2, 32), (162, 2, 32), (80, 8, 128), (64, 4, 64), (256, 1, 16),
