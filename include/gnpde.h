@@ -197,7 +197,10 @@ typedef struct {
  * f[r,:]  = ax                                  (flags & 1 == 0)
  *         = a*(ax - x[r,:]) [+ b*x0[r,:]]        (GNPDE_EPI_RHS)
  * a = *alpha or sigmoid(*alpha), b = *beta: device scalars (no host sync).
- * partials: n_slots*C floats of scratch (NULL if n_slots == 0).
+ * partials: n_slots*C floats of scratch (NULL if n_slots == 0); n_slots*C*4
+ * must stay below 0xffffff00 bytes (the hub partials are addressed with 32-bit
+ * buffer offsets; the library cannot see n_slots, so the caller checks it —
+ * gnpde.ops._partials raises past it: use a larger plan chunk).
  * heavy: the hub table of gnpde_plan_build.  The chunks of a hub row are
  * combined inside the launch by the chunk that finishes last, which it learns
  * from an arrival ticket kept in the 4th word of the row's heavy entry

@@ -12,11 +12,12 @@ if [ "${TESTS:-1}" = 1 ]; then
 fi
 for kv in ${AB:-base}; do
   if [ "$kv" = base ]; then envs=(); else envs=(env "$kv"); fi
-  "${envs[@]}" timeout -k 10 200 python -u tools/attn_ref_bench.py > $OUT/ab_attn_$kv.jsonl 2>&1; rc=$?
-  echo "attn[$kv] rc=$rc $(tail -1 $OUT/ab_attn_$kv.jsonl)"; if fatal $rc; then exit $rc; fi
+  tag=${kv//\//_}
+  "${envs[@]}" timeout -k 10 200 python -u tools/attn_ref_bench.py > $OUT/ab_attn_$tag.jsonl 2>&1; rc=$?
+  echo "attn[$kv] rc=$rc $(tail -1 $OUT/ab_attn_$tag.jsonl)"; if fatal $rc; then exit $rc; fi
   if [ "${HEADLINE:-1}" = 1 ]; then
-    "${envs[@]}" timeout -k 10 300 python bench.py --no-cpu-baseline --no-grmat --no-train --no-attention > $OUT/ab_bench_$kv.log 2>&1; rc=$?
-    echo "bench[$kv] rc=$rc $(tail -1 $OUT/ab_bench_$kv.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["roofline"]["launch_ms"], d.get("rhs_plain",{}).get("rhs_ms"))' 2>&1)"
+    "${envs[@]}" timeout -k 10 300 python bench.py --no-cpu-baseline --no-grmat --no-train --no-attention > $OUT/ab_bench_$tag.log 2>&1; rc=$?
+    echo "bench[$kv] rc=$rc $(tail -1 $OUT/ab_bench_$tag.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["roofline"]["launch_ms"], d.get("rhs_plain",{}).get("rhs_ms"))' 2>&1)"
     if fatal $rc; then exit $rc; fi
   fi
 done
