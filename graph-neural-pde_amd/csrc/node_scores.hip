@@ -653,15 +653,16 @@ static void launch_node_scores(dim3 grid, const NsGeom& ge, hipStream_t s, const
     node_scores_kernel<VEC, 64, MAXH><<<grid, kBlock, 0, s>>>(x, B, N, C, ldx, H, n, uv, cs, rpb);
 }
 
-// rows per block sized for ~2048 wavefronts over the whole launch: the kernel
-// holds ~210 VGPRs (U[b] in registers + two row groups in flight), so 2 waves
-// per SIMD = 2 blocks per CU are resident and the whole grid runs in one round
-// (4096 waves left a 1.7-round tail: 26.9 us for an 87 MB pass)
+// rows per block sized for ~1024 wavefronts over the whole launch (one block per
+// CU, one wave per SIMD streaming its rows with two row groups in flight): the
+// kernel holds U[b] in registers, and the whole grid runs in one round (G-arxiv,
+// 87 MB: 15.4-15.5 us against 16.0-16.1 with 2048 wavefronts, three A/B pairs;
+// 4096 waves left a 1.7-round tail: 26.9 us)
 static void launch_node_scores_any(hipStream_t s, const NsGeom& ge, const float* x, int64_t B, int64_t N, int C,
                                    int64_t ldx, int H, const double* uv, double* cs) {
   const int G = kWave / ge.GL;
   const int64_t groups = ceil_div(N, (int64_t)G);
-  const int64_t waves_per_batch = std::max<int64_t>(1, 2048 / B);
+  const int64_t waves_per_batch = std::max<int64_t>(1, 1024 / B);
   const int64_t iters = std::max<int64_t>(1, ceil_div(groups, waves_per_batch));
   const int64_t rpb = (int64_t)kWavesPerBlock * G * iters;
   const dim3 grid((unsigned)ceil_div(N, rpb), (unsigned)std::min<int64_t>(B, 65535));
