@@ -281,7 +281,7 @@ __global__ __launch_bounds__(kKeysumBlock) void keysum_partial_kernel(const floa
     double acc[VEC];
 #pragma unroll
     for (int i = 0; i < VEC; ++i) acc[i] = 0.0;
-#pragma unroll 8
+#pragma unroll 4
     for (int64_t n = n0 + rs; n < n1; n += RPB) {
       const double d = (double)indeg[base + n];
       float v[VEC];
