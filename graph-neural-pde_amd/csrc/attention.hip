@@ -359,6 +359,8 @@ using namespace gnpde;
 
 extern "C" {
 
+int gnpde_seg_long_edges(void) { return kSegLongMax; }
+
 int gnpde_seg_block_edges(int mode, int64_t heads, int64_t dk) {
   if (mode == GNPDE_SCORE_REFERENCE || mode == GNPDE_SCORE_UNIFORM) return kWave;
   if (heads < 1 || dk < 4 || dk % 4 != 0) return 0;

@@ -178,14 +178,16 @@ class SegPlan(object):
         self.n_slots = n_chunk
 
 
-SEG_LONG_MAX = 256  # edges of a long item (csrc/attention.hip kSegLongMax)
+def seg_long_max():
+    """Edges of a long statistics item (gnpde_seg_long_edges, csrc/attention.hip kSegLongMax)."""
+    return int(_lib.fn("gnpde_seg_long_edges")())
 
 
 def build_seg_plan(rowptr, eb, long_items=False):
     """gnpde_seg_plan_build on a host copy of rowptr (once per graph and block size).
     long_items=True: every group longer than eb becomes one item {e_begin,
-    e_end, -2, group} when it has at most SEG_LONG_MAX edges, else SEG_LONG_MAX-
-    edge chunk items {.., -3 - slot, group} merged inside the launch (heavy
+    e_end, -2, group} when it has at most seg_long_max() edges, else chunk items
+    of that many edges {.., -3 - slot, group} merged inside the launch (heavy
     {group, first_slot, n_chunks, 0}); long items come first, longest first."""
     rp = np.ascontiguousarray(rowptr.cpu().numpy().astype(np.int32))
     R = rp.shape[0] - 1
@@ -203,19 +205,20 @@ def build_seg_plan(rowptr, eb, long_items=False):
         return torch.from_numpy(np.ascontiguousarray(a[:max(n, 1)]).reshape(-1)).to(dev)
 
     if long_items:
+        long_max = seg_long_max()
         rows = heavy[:nh.value, 0].astype(np.int64)
         s0, s1 = rp[rows].astype(np.int64), rp[rows + 1].astype(np.int64)
         order = np.argsort(-(s1 - s0), kind="stable")
         out, hv, slot = [], [], 0
         for i in order:
             r, a, b = int(rows[i]), int(s0[i]), int(s1[i])
-            if b - a <= SEG_LONG_MAX:
+            if b - a <= long_max:
                 out.append((a, b, -2, r))
                 continue
-            nch = (b - a + SEG_LONG_MAX - 1) // SEG_LONG_MAX
+            nch = (b - a + long_max - 1) // long_max
             hv.append((r, slot, nch, 0))
             for c in range(nch):
-                out.append((a + c * SEG_LONG_MAX, min(b, a + (c + 1) * SEG_LONG_MAX), -3 - slot, r))
+                out.append((a + c * long_max, min(b, a + (c + 1) * long_max), -3 - slot, r))
                 slot += 1
         long_arr = np.asarray(out, np.int32).reshape(-1, 4)
         all_items = np.concatenate([long_arr, items[:ni.value]], 0)

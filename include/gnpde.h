@@ -306,8 +306,9 @@ int gnpde_attn_weights_f32(const int32_t* rowidx, const int32_t* col, int64_t nn
  * split groups of degree > EB, heavy {group, first_slot, n_chunks, 0} lists
  * those groups (partials: 2*heads doubles per slot; m/rl scratch).
  * Reference scores with out_kind 1 also take LONG items inside `items`:
- * {e_begin, e_end, -2, group} = a whole group of at most 256 edges, and
- * {e_begin, e_end, -3 - slot, group} = a 256-edge chunk of a longer group whose
+ * {e_begin, e_end, -2, group} = a whole group of at most gnpde_seg_long_edges()
+ * edges, and {e_begin, e_end, -3 - slot, group} = a chunk of that many edges of a
+ * longer group whose
  * partials the last-arriving chunk merges inside the launch (agent-scope ticket
  * in heavy[].w: zero on entry, left zero; launches on one heavy array must not
  * overlap); heavy then lists those groups, and no fixup runs.
@@ -325,6 +326,9 @@ int gnpde_attn_weights_f32(const int32_t* rowidx, const int32_t* col, int64_t nn
  * :34.  Returns GNPDE_EUNSUPPORTED for shapes outside the kernel (dk % 4 != 0,
  * non-power-of-two teams, uniform scores, reference scores with out_kind 0).  */
 int gnpde_seg_block_edges(int mode, int64_t heads, int64_t dk);
+/* Edges of one long item of the reference statistics (whole groups up to it,
+ * chunks of it beyond): the plan builder's unit. */
+int gnpde_seg_long_edges(void);
 int gnpde_seg_plan_build(const int32_t* rowptr, int64_t R, int32_t eb, int32_t* items, int64_t items_capacity,
                          int32_t* chunk_items, int64_t chunks_capacity, int32_t* heavy, int64_t heavy_capacity,
                          int64_t* n_items, int64_t* n_chunks, int64_t* n_heavy);

@@ -325,7 +325,7 @@ def test_seg_stats_long_items(norm_idx, heads, att):
     it = plan.items.cpu().numpy().reshape(-1, 4)[:plan.n_items]
     lng = it[it[:, 2] <= -2]
     assert plan.n_chunk == 0 and plan.n_heavy >= 1 and (it[:len(lng), 2] <= -2).all()
-    assert (lng[:, 1] - lng[:, 0] <= ops.SEG_LONG_MAX).all()
+    assert (lng[:, 1] - lng[:, 0] <= ops.seg_long_max()).all()
     assert (it[len(lng):, 2] == -1).all() and (it[len(lng):, 1] - it[len(lng):, 0] <= 64).all()
     spans = it[:, :2][np.argsort(it[:, 0])]
     assert spans[0, 0] == 0 and spans[-1, 1] == rp[-1] and (spans[1:, 0] == spans[:-1, 1]).all()
