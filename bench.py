@@ -145,8 +145,12 @@ def timed_solve(func, y0, steps, warmup, h, dev, world, sync_world=None):
     with torch.no_grad():
         if warmup > 0:
             rk4_solve(func, y0, warmup, h, dev)
-        if getattr(func, 'graph_capturable', True):
-            rk4_solve(func, y0, max(integ.GRAPH_MIN_STEPS, 2 * integ.GRAPH_BLOCK), h, dev)
+        if getattr(func, 'graph_capturable', True) and steps >= integ.GRAPH_MIN_STEPS:
+            # one-time setup: capture the block graphs a solve of `steps` steps replays
+            # (the first solve of a module runs its first step eagerly, the second
+            # captures the block sizes of the whole run)
+            for _ in range(2):
+                rk4_solve(func, y0, steps, h, dev)
         sync_all(sw)
         t0 = time.perf_counter()
         y = rk4_solve(func, y0, steps, h, dev)
@@ -222,10 +226,11 @@ def bench_single(args, world, rank, dev):
         g = func.graph_for(x)  # once per graph: CSR + plan (outside the timed region)
         if args.warmup > 0:
             run_steps(args.warmup, x)
-        if not args.rhs_only:
-            # one-time setup outside the timed region whatever W is: capture the step and
-            # block hipGraphs the timed call replays from the integrator's cache
-            run_steps(max(integ.GRAPH_MIN_STEPS, 2 * integ.GRAPH_BLOCK), x)
+        if not args.rhs_only and args.steps >= integ.GRAPH_MIN_STEPS:
+            # one-time setup outside the timed region whatever W is: capture the block
+            # hipGraphs a solve of --steps steps replays from the integrator's cache
+            for _ in range(2):
+                run_steps(args.steps, x)
         sync_all(world)
         ops.spmm_rhs = fld.ops.spmm_rhs = timed_spmm
         replays = []
@@ -274,12 +279,14 @@ def bench_single(args, world, rank, dev):
             e.record()
             torch.cuda.synchronize()
         pms = s.elapsed_time(e) / args.rhs_plain_reps
-        plain = roofline(pms, lap_bytes(N, E, C), traffic_bytes(N, E, C, "plain_launch"),
-                         "agg_kernel<4,32,1,4,2,0,PlainWeights,float> (hub rows combined in-launch)")
+        plain = roofline(pms, lap_bytes(N, E, C), kernel_traffic("lap", PLAIN_K1),
+                         "agg_kernel<4,32,1,4,2,0,PlainWeights,float> (hub rows combined in-launch)",
+                         lap_compulsory(N, E, C, 1))
         plain["rhs_ms"] = round(pms, 4)
 
-    rl = roofline(k1_ms, nbytes, traffic_bytes(N, E, C, "plain_launch" if args.rhs_only else "fused_step_launch"),
-                  kname)
+    rl = roofline(k1_ms, nbytes, kernel_traffic("lap", PLAIN_K1 if args.rhs_only else FUSED_K1) if
+                  (N, E, C) == (169343, 1200000, 128) else None, kname,
+                  lap_compulsory(N, E, C, 1 if args.rhs_only else 2))
     rl.update({"launch_ms": round(k1_ms, 4), "launches": n_ev, "graph_replays": len(replays)})
     result = {
         "metric": METRIC,
@@ -303,6 +310,8 @@ def bench_single(args, world, rank, dev):
         "rhs_ms": round(k1_ms, 4),
         "roofline": rl,
         "rhs_plain": plain,
+        "solve_overhead_ms": round(elapsed * 1e3 - args.steps * rhs_per_step * k1_ms, 4),
+        "traffic_source": traffic_source(),
     }
 
     progress("headline: %.1f RHS evals/s" % value)
@@ -322,41 +331,97 @@ def bench_single(args, world, rank, dev):
 
 
 METRIC = "ODE RHS evals/s (and ms/step) at |E|≈1.2M, d=128; achieved HBM GB/s vs roofline"
+FUSED_K1 = "agg_kernel<4, 32, 1, 4, 2, 1, PlainWeights, float>"
+PLAIN_K1 = "agg_kernel<4, 32, 1, 4, 2, 0, PlainWeights, float>"
+GRMAT_K1 = "agg_kernel<4, 64, 1, 4, 1, 1, PlainWeights, float>"
 
 
-def traffic_bytes(N, E, C, which, name="k1_traffic.json"):
-    """Measured HBM bytes per K1 launch (PMC: 2*FETCH_SIZE + WRITE_SIZE with the
-    gfx950 corrections of MI355X_MICROARCH.md §HBM) from profiles/<name>, when
-    that file was collected on this graph shape."""
-    tp = os.path.join(ROOT, "profiles", name)
-    if not os.path.exists(tp):
+TRAFFIC_FILE = os.path.join("profiles", "traffic.json")
+_TRAFFIC = None
+
+
+def traffic():
+    """profiles/traffic.json (tools/prof_r03.sh -> tools/pmc_reduce.py): PMC bytes
+    (2*FETCH_SIZE + WRITE_SIZE, the gfx950 corrections of MI355X_MICROARCH.md
+    §HBM) per dispatch of every kernel of each bench workload, measured in
+    separate rocprofv3 --pmc passes of tools/pmc_run.py."""
+    global _TRAFFIC
+    if _TRAFFIC is None:
+        _TRAFFIC = {}
+        path = os.path.join(ROOT, TRAFFIC_FILE)
+        if os.path.exists(path):
+            with open(path) as fh:
+                _TRAFFIC = json.load(fh)
+    return _TRAFFIC
+
+
+def traffic_source():
+    """Where the counter bytes come from, and whether they were measured on the
+    library that is running (build id = hash of csrc/)."""
+    tj = traffic()
+    src = {"file": TRAFFIC_FILE, "tag": tj.get("tag"), "build_id": tj.get("build_id")}
+    try:
+        from gnpde import _lib
+        src["fresh"] = tj.get("build_id") == _lib.build_id()
+    except Exception:  # noqa: BLE001
+        src["fresh"] = None
+    return src
+
+
+def kernel_traffic(workload, kernel_prefix):
+    """Mean PMC bytes per dispatch of the kernel whose name starts with
+    kernel_prefix in `workload`, or None."""
+    w = traffic().get("workloads", {}).get(workload)
+    if not w:
         return None
-    with open(tp) as fh:
-        tj = json.load(fh)
-    if tj.get("nodes") == N and tj.get("edges") == E and tj.get("dim") == C:
-        return tj.get(which, {}).get("hbm_bytes")
-    return None
+    best = None
+    for k in w["kernels"]:
+        if k["kernel"].startswith(kernel_prefix) and (best is None or k["count"] > best["count"]):
+            best = k
+    return best["bytes"] if best else None
 
 
-def roofline(launch_ms, algorithmic, traffic, kernel):
-    """achieved = measured HBM bytes per launch / launch time (frac <= 1 is an HBM
-    fraction); the §8(d) algorithmic byte count over the same time is reported
-    beside it (it charges every gathered x row to HBM, but x is re-read from L2
-    and the Infinity Cache, so it can pass 8 TB/s)."""
+def rhs_traffic(workload):
+    """PMC bytes of one RHS evaluation of an attention workload (every kernel it dispatches)."""
+    w = traffic().get("workloads", {}).get(workload)
+    return w.get("per_rhs_bytes") if w else None
+
+
+def roofline(launch_ms, algorithmic, traffic_b, kernel, compulsory=None):
+    """frac = PMC bytes per launch / launch time / 8 TB/s: the HBM (fabric)
+    fraction — FETCH_SIZE counts Infinity-Cache hits too, so it bounds HBM
+    traffic from above.  Beside it: the §8(d) algorithmic bytes (every gathered
+    x row charged; x is re-read from L2 and the Infinity Cache, so that rate can
+    pass 8 TB/s: not a roofline fraction) and the compulsory bytes (x read once,
+    the CSR, the launch's state passes): traffic / compulsory is the re-fetch
+    ratio."""
     t = launch_ms * 1e-3
     alg = algorithmic / t / 1e9
     out = {"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s", "kernel": kernel,
            "algorithmic_bytes_per_launch": int(algorithmic), "algorithmic_achieved": round(alg, 1),
            "algorithmic_frac": round(alg / HBM_PEAK_GBS, 4)}
-    if traffic:
-        ach = traffic / t / 1e9
-        out.update({"achieved": round(ach, 1), "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": int(traffic),
-                    "basis": "PMC bytes per launch (profiles/k1_traffic.json, 2*FETCH_SIZE+WRITE_SIZE) / HIP-event "
-                             "launch time"})
+    if compulsory:
+        out.update({"compulsory_bytes": int(compulsory),
+                    "compulsory_frac": round(compulsory / t / 1e9 / HBM_PEAK_GBS, 4)})
+    if traffic_b:
+        ach = traffic_b / t / 1e9
+        out.update({"achieved": round(ach, 1), "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": int(traffic_b),
+                    "basis": "PMC bytes per launch (%s, 2*FETCH_SIZE+WRITE_SIZE) / HIP-event launch time" %
+                             TRAFFIC_FILE})
+        if compulsory:
+            out["refetch_ratio"] = round(traffic_b / compulsory, 3)
     else:
-        out.update({"achieved": round(alg, 1), "frac": round(alg / HBM_PEAK_GBS, 4), "traffic": None,
-                    "basis": "algorithmic bytes / HIP-event launch time (no PMC traffic for this shape)"})
+        out.update({"achieved": None, "frac": None, "traffic": None,
+                    "basis": "no PMC traffic for this shape in %s" % TRAFFIC_FILE})
     return out
+
+
+def lap_compulsory(N, E, C, state_passes):
+    """Compulsory bytes of one K1 launch: x read once (its own rows and every
+    gathered row), the CSR (col + weight 8E, rowptr), and `state_passes` more
+    full passes over [N, C] (f written: 1; a fused rk4 stage: 2 on average —
+    its stage output plus the average 1 extra stage operand)."""
+    return 4 * N * C * (1 + state_passes) + 8 * E + 4 * (N + 1)
 
 
 def bench_sharded(args, world, rank, dev, mode):
@@ -447,9 +512,9 @@ def bench_grmat(args, world, rank, dev):
         func.edge_index, func.edge_weight = ei, w
         el, _ = timed_solve(func, x, args.grmat_steps, 1, h, dev, world)
         launch_ms = el * 1e3 / args.grmat_steps / 4  # a replayed step is its 4 K1 launches back to back
-        rl = roofline(launch_ms, rk4_fused_step_bytes(N, E, C) / 4.0, traffic_bytes(N, E, C, "fused_step_launch",
-                                                                                       "k1_traffic_grmat.json"),
-                      "agg_kernel<4,64,1,4,1,1,PlainWeights,float>: K1 with fused rk4 stage, one row per wavefront")
+        rl = roofline(launch_ms, rk4_fused_step_bytes(N, E, C) / 4.0, kernel_traffic("grmat", GRMAT_K1),
+                      "agg_kernel<4,64,1,4,1,1,PlainWeights,float>: K1 with fused rk4 stage, one row per wavefront "
+                      "(launch time = the replayed solve's time / its launches)", lap_compulsory(N, E, C, 2))
         rl["launch_ms"] = round(launch_ms, 4)
         out["one_gpu"] = {"value": round(args.grmat_steps * 4 / el, 2), "unit": "RHS evals/s",
                           "ms_per_step": round(el * 1e3 / args.grmat_steps, 4), "roofline": rl}
@@ -461,25 +526,51 @@ def bench_grmat(args, world, rank, dev):
     return out
 
 
+ATTN_HEADS, ATTN_DIM = 2, 32
+ATTN_MODES = (("reference", 1), ("reference", 0), ("per_edge", 0), ("per_edge", 1))
+
+
+def attention_func(mode, norm_idx, C, dev):
+    """The drop-in ODEFuncTransformerAtt of the attention lines (configs[3] shape
+    h = 2, att = 32), Q/K weights N(0, 0.1^2) drawn from one seed per mode."""
+    import gnpde
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(2 + 10 * ATTN_MODES.index((mode, norm_idx)))
+    opt = {'hidden_dim': C, 'heads': ATTN_HEADS, 'attention_dim': ATTN_DIM, 'attention_norm_idx': norm_idx,
+           'attention_type': 'scaled_dot', 'attention_score_mode': mode, 'function': 'transformer',
+           'add_source': False, 'no_alpha_sigmoid': False, 'max_nfe': 10 ** 9, 'multi_modal': False,
+           'mix_features': False, 'square_plus': False, 'beltrami': False}
+    func = gnpde.ODEFuncTransformerAtt(C, C, opt, dev).to(dev).eval()
+    with torch.no_grad():
+        for lin in (func.multihead_att_layer.Q, func.multihead_att_layer.K):
+            lin.weight.copy_(torch.randn(ATTN_DIM, C, generator=gen, device=dev) * 0.1)
+            lin.bias.copy_(torch.randn(ATTN_DIM, generator=gen, device=dev) * 0.1)
+    return func
+
+
+def blend_func(dev):
+    """configs[3] shape: the BLEND transformer RHS (fork scaled_dot, norm_idx 0), C = 162."""
+    import gnpde
+    C = BLEND_C
+    opt = {'hidden_dim': C, 'heads': 2, 'attention_dim': 32, 'attention_norm_idx': 0, 'attention_type': 'scaled_dot',
+           'function': 'transformer', 'add_source': False, 'no_alpha_sigmoid': False, 'max_nfe': 10 ** 9,
+           'multi_modal': False, 'mix_features': False, 'square_plus': False, 'beltrami': False}
+    return gnpde.ODEFuncTransformerAtt(C, C, opt, dev).to(dev).eval()
+
+
+BLEND_C = 162
+BLEND_K1 = {"fp32": "agg_kernel<4, 64, 1, 4, 1, 1, PlainWeights, float>",
+            "bf16": "agg_kernel<8, 21, 1, 4, 3, 1, PlainWeights, bf16>"}
+
+
 def bench_attention(g, x, dev, ops, reps=20):
     """The transformer RHS through the drop-in ODEFuncTransformerAtt (config C4 shape)."""
-    import gnpde
     C = x.shape[-1]
-    heads, att = 2, 32
-    gen = torch.Generator(device=dev)
-    gen.manual_seed(2)
+    heads, att = ATTN_HEADS, ATTN_DIM
     out = {"config": "ODEFuncTransformerAtt, C=%d heads=%d attention_dim=%d (configs[3] shape, fp32)" % (C, heads,
                                                                                                           att)}
-    for mode, norm_idx in (("reference", 1), ("reference", 0), ("per_edge", 0), ("per_edge", 1)):
-        opt = {'hidden_dim': C, 'heads': heads, 'attention_dim': att, 'attention_norm_idx': norm_idx,
-               'attention_type': 'scaled_dot', 'attention_score_mode': mode, 'function': 'transformer',
-               'add_source': False, 'no_alpha_sigmoid': False, 'max_nfe': 10 ** 9, 'multi_modal': False,
-               'mix_features': False, 'square_plus': False, 'beltrami': False}
-        func = gnpde.ODEFuncTransformerAtt(C, C, opt, dev).to(dev).eval()
-        with torch.no_grad():
-            for lin in (func.multihead_att_layer.Q, func.multihead_att_layer.K):
-                lin.weight.copy_(torch.randn(att, C, generator=gen, device=dev) * 0.1)
-                lin.bias.copy_(torch.randn(att, generator=gen, device=dev) * 0.1)
+    for mode, norm_idx in ATTN_MODES:
+        func = attention_func(mode, norm_idx, C, dev)
         func.edge_index = g.edge_index
         func.graph_for(x)  # builds this function's CSR/CSC + plans once (outside the timed loop)
         with torch.no_grad():
@@ -510,12 +601,36 @@ def bench_attention(g, x, dev, ops, reps=20):
             torch.cuda.synchronize()
         ms = s.elapsed_time(e) / reps
         del cg
-        nb = attn_bytes(g.N, g.nnz, C, att, "uniform" if (mode, norm_idx) == ("reference", 0) else mode)
-        gbs = nb / (ms * 1e-3) / 1e9
-        out["%s_norm%d" % (mode, norm_idx)] = {"rhs_ms": round(ms, 4), "achieved_GBs": round(gbs, 1),
-                                               "frac": round(gbs / HBM_PEAK_GBS, 4), "algorithmic_bytes": nb,
-                                               "rhs_ms_eager": round(ms_eager, 4)}
+        kind = "uniform" if (mode, norm_idx) == ("reference", 0) else mode
+        nb = attn_bytes(g.N, g.nnz, C, att, kind)
+        cb = attn_compulsory(g.N, g.nnz, C, att, kind)
+        tb = rhs_traffic("attn:%s_norm%d" % (mode, norm_idx))
+        t = ms * 1e-3
+        ent = {"rhs_ms": round(ms, 4), "rhs_ms_eager": round(ms_eager, 4),
+               "algorithmic_bytes": nb, "algorithmic_frac": round(nb / t / 1e9 / HBM_PEAK_GBS, 4),
+               "compulsory_bytes": cb, "compulsory_frac": round(cb / t / 1e9 / HBM_PEAK_GBS, 4)}
+        if tb:
+            ent.update({"traffic": int(tb), "achieved_GBs": round(tb / t / 1e9, 1),
+                        "frac": round(tb / t / 1e9 / HBM_PEAK_GBS, 4),
+                        "basis": "PMC bytes of every kernel of one RHS (%s workload attn:%s_norm%d) / replayed "
+                                 "RHS time" % (TRAFFIC_FILE, mode, norm_idx)})
+        else:
+            ent.update({"traffic": None, "frac": None, "basis": "no PMC traffic in %s" % TRAFFIC_FILE})
+        out["%s_norm%d" % (mode, norm_idx)] = ent
     return out
+
+
+def attn_compulsory(N, E, C, att, mode):
+    """Compulsory bytes of one attention RHS: x read once and f written (8NC), the
+    aggregation CSR (col 4E, rowptr 4(N+1)); the softmax groups' CSC (4E +
+    4(N+1)) when the weights depend on x (not 'uniform', whose 1/outdeg weights
+    are cached: + 4E); per_edge: + q, k written and read once (4 * 2N*att * 2)."""
+    base = 8 * N * C + 4 * E + 4 * (N + 1)
+    if mode == "uniform":
+        return base + 4 * E
+    if mode == "per_edge":
+        return base + 4 * E + 4 * (N + 1) + 16 * N * att
+    return base + 4 * E + 4 * (N + 1)
 
 
 def bench_blend(g, dev, reps=50):
@@ -528,16 +643,13 @@ def bench_blend(g, dev, reps=50):
     size is tests/test_gpu_blend.py."""
     import gnpde
     from gnpde import synthetic
-    C = 162
-    opt = {'hidden_dim': C, 'heads': 2, 'attention_dim': 32, 'attention_norm_idx': 0, 'attention_type': 'scaled_dot',
-           'function': 'transformer', 'add_source': False, 'no_alpha_sigmoid': False, 'max_nfe': 10 ** 9,
-           'multi_modal': False, 'mix_features': False, 'square_plus': False, 'beltrami': False}
+    C = BLEND_C
     out = {"config": "BLEND transformer RHS, fork scaled_dot norm_idx 0 (uniform weights), C=162, rk4 steps "
                      "(configs[3] shape on the G-arxiv graph)"}
     x32 = synthetic.features(1, g.N, C, seed=3, device=dev)
     res = {}
     for name, dt in (("fp32", torch.float32), ("bf16", torch.bfloat16)):
-        func = gnpde.ODEFuncTransformerAtt(C, C, opt, dev).to(dev).eval()
+        func = blend_func(dev)
         func.edge_index = g.edge_index
         x = x32.to(dt)
         with torch.no_grad():
@@ -555,11 +667,20 @@ def bench_blend(g, dev, reps=50):
                 const_rhs = float(func(None, torch.ones_like(x)).abs().max())
         ms = s.elapsed_time(e) / reps
         es = 2 if dt == torch.bfloat16 else 4
+        Cp = 168 if dt == torch.bfloat16 else 164  # the zero-padded width the fused integrator runs
         # per step: 4 x (gathers es*EC + CSR/weights 8E + 4(N+1) + own row es*NC) + 8 state passes es*NC
-        nb = 4 * (es * g.nnz * C + 8 * g.nnz + 4 * (g.N + 1) + es * g.N * C) + 8 * es * g.N * C
+        nb = 4 * (es * g.nnz * Cp + 8 * g.nnz + 4 * (g.N + 1) + es * g.N * Cp) + 8 * es * g.N * Cp
         gbs = nb / (ms * 1e-3) / 1e9
-        out[name] = {"ms_per_step": round(ms, 4), "rhs_per_s": round(4e3 / ms, 1), "algorithmic_GBs": round(gbs, 1),
-                     "algorithmic_frac": round(gbs / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_step": nb}
+        ent = {"ms_per_step": round(ms, 4), "rhs_per_s": round(4e3 / ms, 1), "algorithmic_GBs": round(gbs, 1),
+               "algorithmic_frac": round(gbs / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_step": nb}
+        kb = kernel_traffic("blend_%s" % name, BLEND_K1[name])
+        if kb:
+            # K1 launches at ~the step's time / 4: the counter bytes of the four over the step time
+            ent.update({"k1": BLEND_K1[name], "traffic_per_step": int(4 * kb),
+                        "frac": round(4 * kb / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                        "basis": "PMC bytes of the 4 K1 launches of a step (%s workload blend_%s) / step time" %
+                                 (TRAFFIC_FILE, name)})
+        out[name] = ent
     a, b = res["fp32"].double(), res["bf16"].double()
     rel = float((a - b).abs().max() / a.abs().max())
     out["check"] = {"bf16_vs_fp32_rel": round(rel, 6), "constant_state_rhs_max": const_rhs,
@@ -651,7 +772,10 @@ def cpu_baseline(ei, w, x, N, E, C, budget_s):
     restatement is reported beside it (secondary)."""
     import numpy as np
     cpus = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
-    threads = int(os.environ.get("OMP_NUM_THREADS", cpus))
+    quota = cgroup_cpus()
+    # the job's CPU share: the cgroup quota when one is set (the GPU box gives each GPU's job
+    # 16 CPUs of a 256-CPU host and exports OMP_NUM_THREADS=16 to match), else every visible CPU
+    threads = int(os.environ.get("OMP_NUM_THREADS", quota or cpus))
     model = "unknown CPU"
     try:
         with open("/proc/cpuinfo") as fh:
@@ -679,7 +803,7 @@ def cpu_baseline(ei, w, x, N, E, C, budget_s):
         A = torch.sparse_coo_tensor(ec, wcpu, (N, N)).coalesce().to_sparse_csr()
         xc = x.view(N, C).cpu()
         a = torch.sigmoid(torch.tensor(0.0))
-        n, el, y = timed(lambda: a * (A @ xc - xc), budget_s * 2 / 3)
+        n, el, y = timed(lambda: a * (A @ xc - xc), budget_s / 2)
         assert torch.isfinite(y).all()
     finally:
         torch.set_num_threads(prev)
@@ -687,20 +811,84 @@ def cpu_baseline(ei, w, x, N, E, C, budget_s):
            "sample": "%d full G-arxiv Laplacian RHS evaluations (N=%d, E'=%d, C=%d) in %.1f s: torch sparse CSR "
                      "A@x, fp32, torch %s, %d threads of %d visible host CPUs (%s)" % (
                          n, N, E, C, el, torch.__version__, threads, cpus, model),
-           "cpu_model": model, "visible_cpus": cpus}
+           "cpu_model": model, "visible_cpus": cpus, "cgroup_cpu_quota": quota}
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        out["attention"] = cpu_attention_baseline(ei, x, N, C, budget_s / 3, threads, timed)
+    finally:
+        torch.set_num_threads(prev)
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     try:
         import gnpde_oracle as O
         ein, wn, xn = ei.cpu().numpy(), w.cpu().numpy(), x.cpu().numpy()
         co = O.COracle()
         csr = co.csr(ein, wn, N)
-        n2, el2, y2 = timed(lambda: co.laplacian_rhs(csr, xn, 0.0, nthreads=threads), budget_s / 3)
+        n2, el2, y2 = timed(lambda: co.laplacian_rhs(csr, xn, 0.0, nthreads=threads), budget_s / 6)
         assert np.isfinite(y2).all()
         out["oracle_c_openmp"] = {"value": round(n2 / el2, 3), "unit": "RHS evals/s", "cores": threads,
                                   "sample": "%d RHS evaluations in %.1f s; oracle C restatement (fp32 CSR, OpenMP)" %
                                             (n2, el2)}
     except OSError as exc:  # liboracle.so not built
         out["oracle_c_openmp"] = {"error": "oracle/build/liboracle.so unavailable: %s" % exc}
+    return out
+
+
+def cgroup_cpus():
+    """CPUs the job's cgroup may use (cpu.max quota / period), or None."""
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            with open(path) as fh:
+                q, p = fh.read().split()[:2]
+            if q != "max":
+                return max(1, int(round(int(q) / int(p))))
+        except (OSError, ValueError):
+            pass
+    return None
+
+
+def cpu_attention_baseline(ei, x, N, C, budget, threads, timed):
+    """The attention RHS of the bench's reference_norm1 line (fork scaled_dot,
+    destination-grouped softmax, head mean, aggregation; src/function_transformer_
+    attention.py:218-267, src/utils.py:116-127) restated with torch CPU ops in
+    fp32 at O(E*d) — the fork's literal [h, E, E] score matmul is 2.9 TB at
+    G-arxiv and cannot run.  Same weights as the GPU line (bench.attention_func)."""
+    gen = torch.Generator(device=x.device)
+    gen.manual_seed(2)  # attention_func's seed for ("reference", 1)
+    Wq = (torch.randn(ATTN_DIM, C, generator=gen, device=x.device) * 0.1).cpu()
+    bq = (torch.randn(ATTN_DIM, generator=gen, device=x.device) * 0.1).cpu()
+    Wk = (torch.randn(ATTN_DIM, C, generator=gen, device=x.device) * 0.1).cpu()
+    bk = (torch.randn(ATTN_DIM, generator=gen, device=x.device) * 0.1).cpu()
+    src, dst = ei[0, 0].cpu(), ei[0, 1].cpu()
+    xc = x.view(N, C).cpu()
+    H, dk = ATTN_HEADS, ATTN_DIM // ATTN_HEADS
+    a = torch.sigmoid(torch.tensor(0.0))
+
+    def rhs():
+        q = xc @ Wq.t() + bq
+        k = xc @ Wk.t() + bk
+        S = k.index_select(0, dst).sum(0)                            # the fork's sum over edges of k_dst
+        cs = (q.view(N, H, dk) * S.view(1, H, dk)).sum(-1) / dk ** 0.5  # [N, H]
+        s = cs.index_select(0, src)                                   # [E, H]
+        m = torch.full((N, H), -float("inf")).index_reduce_(0, dst, s, "amax")
+        e = torch.exp(s - m.index_select(0, dst))
+        den = torch.zeros(N, H).index_add_(0, dst, e)
+        att = e / (den.index_select(0, dst) + 1e-16)
+        wm = att.mean(1)
+        ax = torch.zeros(N, C).index_add_(0, src, wm[:, None] * xc.index_select(0, dst))
+        return a * (ax - xc)
+
+    n, el, y = timed(rhs, budget)
+    assert torch.isfinite(y).all()
+    out = {"value": round(n / el, 3), "unit": "RHS evals/s", "cores": threads, "kind": "port",
+           "sample": "%d attention RHS evaluations (reference scaled_dot, norm_idx 1, h=%d, att=%d, G-arxiv) in "
+                     "%.1f s: torch CPU fp32 index ops" % (n, H, ATTN_DIM, el)}
+    if x.is_cuda:  # the restatement computes what the GPU line computes
+        func = attention_func("reference", 1, C, x.device)
+        func.edge_index = ei
+        with torch.no_grad():
+            fg = func(None, x).view(N, C).cpu()
+        out["vs_gpu_rel"] = float((fg - y).abs().max() / y.abs().max())
     return out
 
 

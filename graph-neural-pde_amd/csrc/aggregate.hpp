@@ -377,18 +377,21 @@ __global__ __launch_bounds__(256) void agg_fixup_kernel(const int4* __restrict__
   hub_combine<VEC, pow2_ceil(GL), STG, T>(uniform(hv.x), uniform(hv.y), uniform(hv.z), C, ep, partials);
 }
 
-// Experiment knob (not part of the ABI contract): GNPDE_HUB_FIXUP=1 combines hub
-// rows in a separate agg_fixup_kernel launch instead of inside the aggregation.
+// Experiment builds only (make EXPERIMENTS=1 defines GNPDE_EXPERIMENTS=1; the
+// product library has none of this): GNPDE_HUB_FIXUP=1 combines hub rows in a
+// separate agg_fixup_kernel launch instead of inside the aggregation, and
+// GNPDE_AGG_VARIANT selects alternative lane geometries (the round-2 A/B sweeps
+// recorded in DESIGN.md §6-§7).
 bool hub_inlaunch();
+int agg_variant();
 
 template <int VEC, int GL, int NCH, int U, int RPW, class WP, class T = float>
 static int launch_agg_cfg(const int4* items, int64_t n_items, int4* heavy, int64_t n_heavy, const int* col,
                           const WP& wp, int C, const Epi& ep, float* partials, hipStream_t s) {
   const unsigned grid = (unsigned)ceil_div(n_items, (int64_t)kWavesPerBlock * RPW);
-  const unsigned gfix = (unsigned)ceil_div(n_heavy, kWavesPerBlock);
-  // hub rows combined in the launch (hub_arrive / hub_arrive_slots) or, with
-  // GNPDE_HUB_FIXUP=1, by agg_fixup_kernel after it
-  const bool inlaunch = hub_inlaunch();
+  // hub rows are combined in the launch (hub_arrive / hub_arrive_slots)
+  bool inlaunch = true;
+  if constexpr (GNPDE_EXPERIMENTS) inlaunch = hub_inlaunch();
   const int nh = inlaunch ? (int)n_heavy : 0;
   // single-output stages (every gnpde.integrator step) get the leaner instantiation
   const int stg = ep.has_stage ? (ep.st.n_out <= 1 ? 1 : 2) : 0;
@@ -404,92 +407,82 @@ static int launch_agg_cfg(const int4* items, int64_t n_items, int4* heavy, int64
                                                                           partials);
     GNPDE_LAUNCH_CHECK();
   }
-  if (!inlaunch && n_heavy > 0) {
-    if (stg == 1)
-      agg_fixup_kernel<VEC, GL, 1, T><<<gfix, kBlock, 0, s>>>(heavy, (int)n_heavy, C, ep, partials);
-    else if (stg == 2)
-      agg_fixup_kernel<VEC, GL, 2, T><<<gfix, kBlock, 0, s>>>(heavy, (int)n_heavy, C, ep, partials);
-    else
-      agg_fixup_kernel<VEC, GL, 0, T><<<gfix, kBlock, 0, s>>>(heavy, (int)n_heavy, C, ep, partials);
-    GNPDE_LAUNCH_CHECK();
+  if constexpr (GNPDE_EXPERIMENTS) {
+    const unsigned gfix = (unsigned)ceil_div(n_heavy, kWavesPerBlock);
+    if (!inlaunch && n_heavy > 0) {
+      if (stg == 1)
+        agg_fixup_kernel<VEC, GL, 1, T><<<gfix, kBlock, 0, s>>>(heavy, (int)n_heavy, C, ep, partials);
+      else if (stg == 2)
+        agg_fixup_kernel<VEC, GL, 2, T><<<gfix, kBlock, 0, s>>>(heavy, (int)n_heavy, C, ep, partials);
+      else
+        agg_fixup_kernel<VEC, GL, 0, T><<<gfix, kBlock, 0, s>>>(heavy, (int)n_heavy, C, ep, partials);
+      GNPDE_LAUNCH_CHECK();
+    }
   }
   return GNPDE_OK;
 }
 
-// Experiment knob (not part of the ABI contract): GNPDE_AGG_VARIANT selects an
-// alternative lane geometry for the dominant 32-lane (C = 128 fp32) case
-// (2: U = 2, 3: U = 8, 4: one row per wavefront; default: two rows per wavefront)
-// and, with 5, the one-row geometry for rows of at most 16 lanes.
-int agg_variant();
-
+// The lane geometry of a row width (lanes = ceil(C / VEC)), measured per width in
+// round 1-2 (profiles/r02b_stripe_sweep.jsonl, r02b_layout_ab.jsonl).
 template <int VEC, class WP, class T = float>
 static int launch_agg_vec(const int4* items, int64_t n_items, int4* heavy, int64_t n_heavy, const int* col,
                           const WP& wp, int C, const Epi& ep, float* partials, hipStream_t s) {
   const int lanes = (int)ceil_div(C, VEC);
 #define GNPDE_AGG(GL, NCH, U, RPW) \
   launch_agg_cfg<VEC, GL, NCH, U, RPW, WP, T>(items, n_items, heavy, n_heavy, col, wp, C, ep, partials, s)
+  const int var = GNPDE_EXPERIMENTS ? agg_variant() : 0;
+  if constexpr (GNPDE_EXPERIMENTS) {
+    switch (var) {
+      case 6:  // twice the gathers in flight per edge group
+        if (lanes <= 4) return GNPDE_AGG(4, 1, 8, 8);
+        if (lanes <= 8) return GNPDE_AGG(8, 1, 8, 4);
+        if (lanes <= 16) return GNPDE_AGG(16, 1, 8, 2);
+        break;
+      case 8:  // half the rows per wavefront, four edge groups per row
+        if (lanes <= 4) return GNPDE_AGG(4, 1, 4, 4);
+        if (lanes <= 8) return GNPDE_AGG(8, 1, 4, 2);
+        if (lanes <= 16) return GNPDE_AGG(16, 1, 4, 1);
+        break;
+      case 2: if (lanes > 16 && lanes <= 32) return GNPDE_AGG(32, 1, 2, 1); break;
+      case 3:
+        if (lanes > 16 && lanes <= 32) return GNPDE_AGG(32, 1, 8, 1);
+        if (lanes > 32 && lanes <= 64) return GNPDE_AGG(64, 1, 8, 1);
+        break;
+      case 4: if (lanes > 16 && lanes <= 32) return GNPDE_AGG(32, 1, 4, 1); break;
+      default: break;
+    }
+  }
   // Narrow rows (the column stripes of gnpde.dist at 2-8 GPUs: G-arxiv C = 128 / 8 = 16
   // floats = 4 lanes; G-rmat 256 / 8 = 32 floats = 8 lanes): several rows per
   // wavefront with 2-4 edges side by side per row slot, instead of one row per
-  // wavefront idling 3/4 of a 16-lane group (GNPDE_AGG_VARIANT=5).  G-arxiv rk4
-  // step at 16 / 32 / 64 columns: 0.133 / 0.152 / 0.243 ms against 0.266 / 0.270 /
-  // 0.296 with the one-row geometry (tools/stripe_sweep.sh).
-  switch (agg_variant()) {
-    case 5: break;  // the previous one-row geometry below
-    case 6:         // twice the gathers in flight per edge group
-      if (lanes <= 4) return GNPDE_AGG(4, 1, 8, 8);
-      if (lanes <= 8) return GNPDE_AGG(8, 1, 8, 4);
-      if (lanes <= 16) return GNPDE_AGG(16, 1, 8, 2);
-      break;
-    case 7:         // twice the rows per wavefront, one edge group per row
+  // wavefront idling 3/4 of a 16-lane group (G-arxiv rk4 step at 16 / 32 / 64 columns:
+  // 0.133 / 0.152 / 0.243 ms against 0.266 / 0.270 / 0.296 with one row per wavefront).
+  // A state far beyond the Infinity Cache (G-rmat stripes: 2M rows x 32-64 columns) is
+  // gathered from HBM, where more independent rows per wavefront win (G-rmat rk4 step at
+  // 32 / 64 columns 2.06 / 3.67 ms against 2.56 / 4.52); a cache-resident one (G-arxiv
+  // stripes) prefers several edge groups per row (0.149 / 0.124 ms at 32 / 16 columns
+  // against 0.283 / 0.318).
+  if (var != 5) {
+    if (n_items * (int64_t)C * (int64_t)sizeof(T) > (int64_t)(96 << 20)) {
       if (lanes <= 4) return GNPDE_AGG(4, 1, 4, 16);
       if (lanes <= 8) return GNPDE_AGG(8, 1, 4, 8);
       if (lanes <= 16) return GNPDE_AGG(16, 1, 4, 4);
-      break;
-    case 8:         // half the rows per wavefront, four edge groups per row
-      if (lanes <= 4) return GNPDE_AGG(4, 1, 4, 4);
-      if (lanes <= 8) return GNPDE_AGG(8, 1, 4, 2);
-      if (lanes <= 16) return GNPDE_AGG(16, 1, 4, 1);
-      break;
-    default:  // per width, the fastest of variants 0/6/7/8 (profiles/r02b_stripe_sweep.jsonl)
-      // A state far beyond the Infinity Cache (G-rmat stripes: 2M rows x 32-64 columns) is
-      // gathered from HBM, where more independent rows per wavefront win (variant 7: G-rmat
-      // rk4 step at 32 / 64 columns 2.06 / 3.67 ms against 2.56 / 4.52); a cache-resident one
-      // (G-arxiv stripes) prefers several edge groups per row (0.149 / 0.124 ms at 32 / 16
-      // columns against 0.283 / 0.318; profiles/r02b_layout_ab.jsonl).
-      if (n_items * (int64_t)C * (int64_t)sizeof(T) > (int64_t)(96 << 20)) {
-        if (lanes <= 4) return GNPDE_AGG(4, 1, 4, 16);
-        if (lanes <= 8) return GNPDE_AGG(8, 1, 4, 8);
-        if (lanes <= 16) return GNPDE_AGG(16, 1, 4, 4);
-      }
-      if (lanes <= 4) return GNPDE_AGG(4, 1, 4, 4);
-      if (lanes <= 8) return GNPDE_AGG(8, 1, 8, 4);
-      if (lanes <= 16) return GNPDE_AGG(16, 1, 4, 2);
+    }
+    if (lanes <= 4) return GNPDE_AGG(4, 1, 4, 4);
+    if (lanes <= 8) return GNPDE_AGG(8, 1, 8, 4);
+    if (lanes <= 16) return GNPDE_AGG(16, 1, 4, 2);
   }
   if (lanes <= 16) return GNPDE_AGG(16, 1, 4, 1);
   if constexpr (sizeof(T) == 2 && VEC == 8) {
     // bf16 rows of 129-168 columns (BLEND: C = 162 padded to 168 = 21 lanes of 16 B):
-    // three rows per wavefront, 63 of 64 lanes busy (GNPDE_AGG_VARIANT=9: two rows, 21 of 32)
-    if (lanes > 16 && lanes <= 21 && agg_variant() == 10) return GNPDE_AGG(21, 1, 8, 3);  // 8 edges in flight
-    if (lanes > 16 && lanes <= 21 && agg_variant() == 11) return GNPDE_AGG(21, 1, 2, 3);  // 2 edges in flight
-    if (lanes > 16 && lanes <= 21 && agg_variant() != 9) return GNPDE_AGG(21, 1, 4, 3);
+    // three rows per wavefront, 63 of 64 lanes busy
+    if (lanes > 16 && lanes <= 21) return GNPDE_AGG(21, 1, 4, 3);
   }
-  if (lanes <= 32) {
-    // two rows per wavefront (fp32 C = 128 and bf16 rows of 17-32 lanes): with the
-    // plan's items longest first, G-arxiv rk4 bench 9,301 against 8,643 RHS/s with
-    // one row per wavefront (variant 4); hub rows then go to agg_fixup_kernel
-    switch (agg_variant()) {
-      case 2: return GNPDE_AGG(32, 1, 2, 1);
-      case 3: return GNPDE_AGG(32, 1, 8, 1);
-      case 4: return GNPDE_AGG(32, 1, 4, 1);
-      default: break;
-    }
-    return GNPDE_AGG(32, 1, 4, 2);
-  }
-  if (lanes <= 64) {
-    if (agg_variant() == 3) return GNPDE_AGG(64, 1, 8, 1);
-    return GNPDE_AGG(64, 1, 4, 1);
-  }
+  // two rows per wavefront (fp32 C = 128 and bf16 rows of 17-32 lanes): with the
+  // plan's items longest first, G-arxiv rk4 bench 9,301 against 8,643 RHS/s with
+  // one row per wavefront
+  if (lanes <= 32) return GNPDE_AGG(32, 1, 4, 2);
+  if (lanes <= 64) return GNPDE_AGG(64, 1, 4, 1);
   if (lanes <= 128) return GNPDE_AGG(64, 2, 2, 1);
   if (lanes <= 256) return GNPDE_AGG(64, 4, 2, 1);
   if (lanes <= 512) return GNPDE_AGG(64, 8, 1, 1);

@@ -342,6 +342,101 @@ __global__ __launch_bounds__(256) void seg_softmax_kernel(const int4* __restrict
   }
 }
 
+// ------------------------------------------------------------------ reference statistics, short items
+// The reference scores' destination statistics (norm_idx 1) over the short items
+// (whole groups packed up to 64 edges): NI items per wavefront with every load
+// of all NI items issued before any arithmetic (item -> {group id, source id} ->
+// the sources' node scores is a chain of three dependent loads, and the kernel
+// is latency-bound: two items per wave halve the waves and overlap the chains).
+// A lane's segment end comes from a ballot of group changes (no rowptr gather).
+// Long items (slot <= -2, the first n_long items of the plan) keep one
+// wavefront each (seg_long_stats).  Same arithmetic as seg_softmax_kernel<true,
+// kSegStats>: segmented max, exp(v - M), segmented sum, in the same lane order.
+constexpr int kRefStatsNI = 2;
+
+template <int NI, int MAXH>
+__global__ __launch_bounds__(256) void ref_stats_kernel(const int4* __restrict__ items, int n_items, int n_long,
+                                                         const int* __restrict__ rowidx, const int* __restrict__ gidx,
+                                                         ScoreArgs sa, double* __restrict__ m,
+                                                         float* __restrict__ rl, double* __restrict__ mr,
+                                                         double* __restrict__ partials, int4* heavy, int n_heavy) {
+  const int lane = threadIdx.x & 63;
+  const int wid = uniform(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
+  if (wid < n_long) {
+    const int4 it = items[wid];
+    const int e0 = uniform(it.x), e1 = uniform(it.y), slot = uniform(it.z);
+    if (e1 > e0)
+      seg_long_stats(e0, e1, uniform(it.w), slot == -2 ? -1 : -3 - slot, gidx, 1, sa, m, rl, mr, partials, heavy,
+                     n_heavy);
+    return;
+  }
+  const int base = n_long + (wid - n_long) * NI;
+  if (base >= n_items) return;
+  const int H = sa.H;
+  int e0[NI], n[NI], grp[NI], src[NI];
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int4 it = base + i < n_items ? items[base + i] : make_int4(0, 0, -1, 0);
+    e0[i] = uniform(it.x);
+    n[i] = uniform(it.y) - e0[i];
+  }
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int p = e0[i] + min(lane, max(n[i] - 1, 0));
+    grp[i] = n[i] > 0 ? rowidx[p] : 0;
+    src[i] = n[i] > 0 ? gidx[p] : 0;
+  }
+  double v[NI][MAXH];
+#pragma unroll
+  for (int i = 0; i < NI; ++i)
+#pragma unroll
+    for (int h = 0; h < MAXH; ++h) v[i][h] = (h < H && n[i] > 0) ? sa.cs[(int64_t)src[i] * H + h] : 0.0;
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    if (n[i] > 0) {  // wave-uniform
+      const bool live = lane < n[i];
+      const int nxt = __shfl(grp[i], min(lane + 1, 63));
+      const unsigned long long ends = __ballot(live && (lane == n[i] - 1 || nxt != grp[i]));
+      const int seg_end = lane + (int)__builtin_ctzll(ends >> lane | (1ull << 63 >> lane));
+      const unsigned same = seg_flags(grp[i]) & (live ? 0x3fu : 0u);
+#pragma unroll
+      for (int h = 0; h < MAXH; ++h) {
+        if (h < H) {
+          const double x = live ? v[i][h] : -INFINITY;
+          const double M = __shfl(seg_scan<true>(x, same), seg_end);
+          const float e = live ? expf((float)(x - M)) : 0.f;
+          const float Ls = __shfl(seg_scan<false>(e, same), seg_end);
+          if (live && lane == seg_end) store_stats(m, rl, mr, grp[i], H, h, M, 1.0f / (Ls + kSoftmaxEps));
+        }
+      }
+    }
+  }
+}
+
+template <int NI>
+static int launch_ref_stats(const int4* items, int64_t n_items, int64_t n_long, const int* rowidx, const int* gidx,
+                            const ScoreArgs& sa, double* m, float* rl, double* mr, double* partials, int4* heavy,
+                            int n_heavy, hipStream_t s) {
+  const int64_t waves = n_long + ceil_div(n_items - n_long, (int64_t)NI);
+  const unsigned grid = (unsigned)ceil_div(waves, kWavesPerBlock);
+#define GNPDE_RS(M)                                                                                              \
+  ref_stats_kernel<NI, M><<<grid, kBlock, 0, s>>>(items, (int)n_items, (int)n_long, rowidx, gidx, sa, m, rl, mr, \
+                                                   partials, heavy, n_heavy)
+  if (sa.H <= 1)
+    GNPDE_RS(1);
+  else if (sa.H <= 2)
+    GNPDE_RS(2);
+  else if (sa.H <= 4)
+    GNPDE_RS(4);
+  else if (sa.H <= 8)
+    GNPDE_RS(8);
+  else
+    GNPDE_RS(16);
+#undef GNPDE_RS
+  GNPDE_LAUNCH_CHECK();
+  return GNPDE_OK;
+}
+
 template <bool REF, int OUT>
 static int launch_seg(const int4* items, int64_t n, const int* rowptr, const int* rowidx, const int* gidx, int gid,
                       const ScoreArgs& sa, const Team& tm, float* w, double* m, float* rl, double* mr,
@@ -419,8 +514,9 @@ int gnpde_seg_plan_build(const int32_t* rowptr, int64_t R, int32_t eb, int32_t* 
   return GNPDE_OK;
 }
 
-int gnpde_seg_softmax_f32(const int32_t* items, int64_t n_items, const int32_t* chunk_items, int64_t n_chunk_items,
-                          int32_t* heavy, int64_t n_heavy, const int32_t* rowptr, const int32_t* rowidx,
+int gnpde_seg_softmax_f32(const int32_t* items, int64_t n_items, int64_t n_long_items, const int32_t* chunk_items,
+                          int64_t n_chunk_items, int32_t* heavy, int64_t n_heavy, const int32_t* rowptr,
+                          const int32_t* rowidx,
                           const int32_t* gidx, int group_is_dst, int out_kind, int mode, int64_t heads, int64_t dk,
                           const double* cs, const float* q, const float* k, int64_t ldqk, float score_p0,
                           float score_p1, float* w, double* m, float* rl, double* mr, double* partials,
@@ -431,8 +527,11 @@ int gnpde_seg_softmax_f32(const int32_t* items, int64_t n_items, const int32_t* 
   GNPDE_REQUIRE(mode != GNPDE_SCORE_UNIFORM, GNPDE_EUNSUPPORTED, "seg_softmax: uniform scores need no softmax pass");
   GNPDE_REQUIRE(!(mode == GNPDE_SCORE_REFERENCE && out_kind == 0), GNPDE_EUNSUPPORTED,
                 "seg_softmax: reference scores grouped by source are uniform");
-  GNPDE_REQUIRE(n_items >= 0 && n_chunk_items >= 0 && n_heavy >= 0 && n_items + n_chunk_items < INT32_MAX,
+  GNPDE_REQUIRE(n_items >= 0 && n_chunk_items >= 0 && n_heavy >= 0 && n_items + n_chunk_items < INT32_MAX &&
+                    n_long_items >= 0 && n_long_items <= n_items,
                 GNPDE_EINVAL, "seg_softmax: bad item counts");
+  GNPDE_REQUIRE(n_long_items == 0 || (mode == GNPDE_SCORE_REFERENCE && out_kind == 1), GNPDE_EINVAL,
+                "seg_softmax: long items are for the reference statistics only");
   GNPDE_REQUIRE(gnpde_seg_block_edges(mode, heads, dk) > 0, GNPDE_EUNSUPPORTED,
                 "seg_softmax: per-edge scores need dk %% 4 == 0 and power-of-two dk/4, heads*dk/4 <= 64");
   if (n_items + n_chunk_items == 0) return GNPDE_OK;
@@ -464,6 +563,11 @@ int gnpde_seg_softmax_f32(const int32_t* items, int64_t n_items, const int32_t* 
   const bool adjacent = n_items > 0 && n_chunk_items > 0 && ch == it + n_items;
   const int64_t n_first = adjacent ? n_items + n_chunk_items : n_items;
   const int64_t n_second = adjacent ? 0 : n_chunk_items;
+  if (ref && out_kind == 1 && n_chunk_items == 0 && group_is_dst) {
+    // the reference statistics of the attention RHS: long items, then short items NI per wave
+    return launch_ref_stats<kRefStatsNI>(it, n_items, n_long_items, rowidx, gidx, sa, m, rl, mr, partials, hv,
+                                         (int)n_heavy, s);
+  }
   if (out_kind == 0) {
     rc = GNPDE_SEG(false, kSegWeights, it, n_first);
     if (!rc) rc = GNPDE_SEG(false, kSegWeights, ch, n_second);

@@ -8,6 +8,13 @@
 
 #include "../../include/gnpde.h"
 
+// Experiment builds (make EXPERIMENTS=1): the A/B knobs of the round-1/2 sweeps
+// (environment-selected K1 geometries, the separate hub fixup launch, the
+// XCD remap, the bf16 vector cap).  The product library is built without them.
+#ifndef GNPDE_EXPERIMENTS
+#define GNPDE_EXPERIMENTS 0
+#endif
+
 namespace gnpde {
 
 // ------------------------------------------------------------------ error plumbing
@@ -323,6 +330,8 @@ __device__ __forceinline__ void epi_finish(const Epi& e, int64_t row, int cc, co
   }
   const int64_t off = row * e.ldf + cc;
   if (e.st.f_out) store_vec<VEC>(as_t<T>(e.st.f_out) + off, o);
+  // the stage outputs' row (out_rows: the last step of a renumbered solve writes the caller's numbering)
+  const int64_t oo = e.st.out_rows ? (int64_t)e.st.out_rows[row] * e.ldf + cc : off;
 #pragma unroll
   for (int i = 0; i < stage_nout<STG>(); ++i) {
     if (i >= e.st.n_out) break;
@@ -347,7 +356,7 @@ __device__ __forceinline__ void epi_finish(const Epi& e, int64_t row, int cc, co
     }
 #pragma unroll
     for (int t = 0; t < VEC; ++t) r[t] = fmaf(so.cf, o[t], r[t]);
-    store_vec<VEC>(as_t<T>(so.out) + off, r);
+    store_vec<VEC>(as_t<T>(so.out) + oo, r);
   }
 }
 

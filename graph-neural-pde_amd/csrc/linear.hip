@@ -466,13 +466,14 @@ __global__ __launch_bounds__(256, 2) void linear_split_kernel(const float* __res
 
 using namespace gnpde;
 
-// Experiment knob (not part of the ABI contract): GNPDE_LINEAR=1 forces the
+// Experiment builds only (GNPDE_EXPERIMENTS): GNPDE_LINEAR=1 forces the
 // per-tile (non-persistent) exact-f32 kernel, =2 the persistent exact-f32 one
 // (default: the split-bf16 kernel where K % 16 == 0 and K <= 128).  Measured
 // and dropped: 16-row tiles on 16x16x32 with a three-deep register ring of x
 // tiles (31.7-32.3 us), splitting the whole tile before refilling (1 wave per
 // SIMD, 32-38 us), refilling per step instead of per 128-byte line (32 us).
 static int linear_variant() {
+  if constexpr (!GNPDE_EXPERIMENTS) return 0;
   static const int v = [] {
     const char* e = std::getenv("GNPDE_LINEAR");
     return e ? std::atoi(e) : 0;
@@ -480,9 +481,10 @@ static int linear_variant() {
   return v;
 }
 
-// Experiment knob (not part of the ABI contract): GNPDE_LIN_WAVES = wavefronts of the
+// Experiment builds only: GNPDE_LIN_WAVES = wavefronts of the
 // persistent projection grid (default 2048).
 static int64_t linear_waves() {
+  if constexpr (!GNPDE_EXPERIMENTS) return 2048;
   static const int64_t v = [] {
     const char* e = std::getenv("GNPDE_LIN_WAVES");
     return e ? std::max<int64_t>(4, std::atoll(e)) : (int64_t)2048;

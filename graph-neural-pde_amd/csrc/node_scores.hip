@@ -488,18 +488,33 @@ __device__ __forceinline__ void ns_store(double (&acc)[MAXH], const double (&vb)
 // One chunk per row: U[b] sits in registers and the loop keeps two row groups
 // in flight ahead of the one being reduced.  Prefetch addresses past the
 // block's rows clamp to its last row (a cache-line hit, no extra HBM traffic).
+// The first two row groups of a wave (ns_block_resident's prefetch), issued
+// before U exists when the block forms U itself (node_scores_fused_kernel).
 template <int VEC, int GL, int MAXH, bool CLAMP>
+__device__ __forceinline__ void ns_first_rows(const float* __restrict__ xb, int64_t n0, int64_t n1, int C,
+                                              int64_t ldx, int g, int gl, int wv,
+                                              float (&xa)[node_scores_npv<MAXH>() / VEC][VEC],
+                                              float (&xn)[node_scores_npv<MAXH>() / VEC][VEC]) {
+  constexpr int G = kWave / GL;
+  constexpr int NP = node_scores_npv<MAXH>() / VEC;
+  const int64_t step = (int64_t)kWavesPerBlock * G;
+  const int64_t last = n1 - 1, nb = n0 + wv * G;
+  ns_load_x<VEC, NP, GL, CLAMP>(xb + min(nb + g, last) * ldx, 0, gl, C, xa);
+  ns_load_x<VEC, NP, GL, CLAMP>(xb + min(nb + g + step, last) * ldx, 0, gl, C, xn);
+}
+
+template <int VEC, int GL, int MAXH, bool CLAMP, bool PRELOADED = false>
 __device__ __forceinline__ void ns_block_resident(const double* __restrict__ Ub, const float* __restrict__ xb,
                                                   __amdgpu_buffer_rsrc_t rcs, int64_t n0, int64_t n1, int C,
-                                                  int64_t ldx, int H, int Cp, int g, int gl, int wv) {
+                                                  int64_t ldx, int H, int Cp, int g, int gl, int wv,
+                                                  float (&xa)[node_scores_npv<MAXH>() / VEC][VEC],
+                                                  float (&xn)[node_scores_npv<MAXH>() / VEC][VEC]) {
   constexpr int G = kWave / GL;
   constexpr int NP = node_scores_npv<MAXH>() / VEC;
   const int64_t step = (int64_t)kWavesPerBlock * G;
   const int64_t last = n1 - 1;
   int64_t nb = n0 + wv * G;
-  float xa[NP][VEC], xn[NP][VEC];
-  ns_load_x<VEC, NP, GL, CLAMP>(xb + min(nb + g, last) * ldx, 0, gl, C, xa);
-  ns_load_x<VEC, NP, GL, CLAMP>(xb + min(nb + g + step, last) * ldx, 0, gl, C, xn);
+  if constexpr (!PRELOADED) ns_first_rows<VEC, GL, MAXH, CLAMP>(xb, n0, n1, C, ldx, g, gl, wv, xa, xn);
   double u[NP][VEC][MAXH];
   ns_load_u<VEC, NP, GL, MAXH>(Ub, 0, gl, u);
   double vb[MAXH];
@@ -546,10 +561,11 @@ __global__ __launch_bounds__(256) void node_scores_kernel(const float* __restric
     const double* __restrict__ Ub = uv + b * ((int64_t)Cp * MAXH + MAXH);
     const __amdgpu_buffer_rsrc_t rcs = buf_rsrc(cs + b * N * H);
     if (nch == 1) {
+      float xa[NP][VEC], xn[NP][VEC];
       if (ragged)
-        ns_block_resident<VEC, GL, MAXH, true>(Ub, xb, rcs, n0, n1, C, ldx, H, Cp, g, gl, wv);
+        ns_block_resident<VEC, GL, MAXH, true>(Ub, xb, rcs, n0, n1, C, ldx, H, Cp, g, gl, wv, xa, xn);
       else
-        ns_block_resident<VEC, GL, MAXH, false>(Ub, xb, rcs, n0, n1, C, ldx, H, Cp, g, gl, wv);
+        ns_block_resident<VEC, GL, MAXH, false>(Ub, xb, rcs, n0, n1, C, ldx, H, Cp, g, gl, wv, xa, xn);
     } else {
       double vb[MAXH];
 #pragma unroll
@@ -573,6 +589,82 @@ __global__ __launch_bounds__(256) void node_scores_kernel(const float* __restric
   }
 }
 
+// Node scores with the key projection formed by every workgroup itself (no
+// separate key_projection launch: it was one latency-bound workgroup, 6.4 us on
+// G-arxiv, between two bandwidth-bound launches).  Each block issues its first
+// two row groups of x, then sums the keysum tile shares of S (thread (tg, d):
+// tiles tg, tg + TG, ... in order, then the TG group sums in order — the same
+// fixed order in every block, so every block forms the same U bit for bit),
+// forms U = Wq^T S / sqrt(dk) and v = bq . S / sqrt(dk) into LDS and streams its
+// rows with U[b] in registers.  One chunk per row (nch == 1), one batch element
+// per grid row (gridDim.y == B).
+template <int VEC, int GL, int MAXH, bool CLAMP>
+__global__ __launch_bounds__(256) void node_scores_fused_kernel(const float* __restrict__ x, int64_t N, int C,
+                                                                 int64_t ldx, int H, const double* __restrict__ part,
+                                                                 int ntiles, const float* __restrict__ Wq,
+                                                                 const float* __restrict__ bq, int att,
+                                                                 double* __restrict__ cs, int64_t rows_per_block) {
+  constexpr int NPV = node_scores_npv<MAXH>();
+  constexpr int NP = NPV / VEC;
+  constexpr int Cp = GL * NPV;
+  extern __shared__ __attribute__((aligned(16))) double nsf_lds[];  // S[att] | red[256] | U[Cp*MAXH] | v[MAXH]
+  double* S = nsf_lds;
+  double* red = S + att;
+  double* U = red + kBlock;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wv = tid >> 6;
+  const int g = lane / GL, gl = lane % GL;
+  const int64_t b = blockIdx.y;
+  const int64_t n0 = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t n1 = min(N, n0 + rows_per_block);
+  const float* __restrict__ xb = x + b * N * ldx;
+  float xa[NP][VEC], xn[NP][VEC];
+  ns_first_rows<VEC, GL, MAXH, CLAMP>(xb, n0, n1, C, ldx, g, gl, wv, xa, xn);
+  // S = sum over the tile shares
+  const double* __restrict__ pb = part + b * (int64_t)ntiles * att;
+  const int DW = min(att, kBlock), TG = kBlock / DW;
+  const int tg = tid / DW, dl = tid - tg * DW;
+  for (int d0 = 0; d0 < att; d0 += DW) {
+    const int d = d0 + dl;
+    double acc = 0.0;
+    if (tg < TG && d < att) {
+      for (int t0 = tg; t0 < ntiles; t0 += kProjLoads * TG) {
+        double v[kProjLoads];
+#pragma unroll
+        for (int k = 0; k < kProjLoads; ++k) v[k] = pb[(int64_t)min(t0 + k * TG, ntiles - 1) * att + d];
+#pragma unroll
+        for (int k = 0; k < kProjLoads; ++k)
+          if (t0 + k * TG < ntiles) acc += v[k];
+      }
+    }
+    red[tid] = acc;
+    __syncthreads();
+    if (tid < DW && d0 + tid < att) {
+      double sum = 0.0;
+      for (int q = 0; q < TG; ++q) sum += red[q * DW + tid];
+      S[d0 + tid] = sum;
+    }
+    __syncthreads();
+  }
+  // U[c][h] (c < Cp; zero past C and H) and v[h] (row c = Cp)
+  const int dk = att / H;
+  const double inv = 1.0 / sqrt((double)dk);
+  for (int t = tid; t < (Cp + 1) * MAXH; t += kBlock) {
+    const int c = t / MAXH, h = t - c * MAXH;
+    double a = 0.0;
+    if (h < H && (c < C || c == Cp)) {
+      const int d0 = h * dk;
+#pragma unroll 8
+      for (int d = 0; d < dk; ++d)
+        a = fma((double)(c == Cp ? bq[d0 + d] : Wq[(int64_t)(d0 + d) * C + c]), S[d0 + d], a);
+    }
+    U[t] = a * inv;
+  }
+  __syncthreads();
+  const __amdgpu_buffer_rsrc_t rcs = buf_rsrc(cs + b * N * H);
+  ns_block_resident<VEC, GL, MAXH, CLAMP, true>(U, xb, rcs, n0, n1, C, ldx, H, Cp, g, gl, wv, xa, xn);
+}
+
 // ------------------------------------------------------------------ host helpers
 static int pow2_at_least(int v, int cap) {
   int p = 1;
@@ -589,8 +681,9 @@ static int keysum_vec(int64_t C, const float* x, int64_t ldx) {
 // tiles of rows for the partial column sums (independent of the vector width):
 // about kKeysumTilesTarget over the launch, at least one row per row slot
 static int keysum_tiles_target() {
+  if constexpr (!GNPDE_EXPERIMENTS) return kKeysumTilesTarget;
   static const int t = [] {
-    const char* e = std::getenv("GNPDE_KEYSUM_TILES");  // tuning knob (measurement only)
+    const char* e = std::getenv("GNPDE_KEYSUM_TILES");  // tuning knob (experiment builds)
     const int v = e ? std::atoi(e) : 0;
     return v >= 8 && v <= 4096 ? v : kKeysumTilesTarget;
   }();
@@ -684,6 +777,69 @@ static void launch_node_scores_any(hipStream_t s, const NsGeom& ge, const float*
     }
   }
 #undef GNPDE_NS
+}
+
+// Experiment builds: GNPDE_NS_FUSED=0 keeps the separate key_projection launch.
+static bool ns_fused_enabled() {
+  if constexpr (!GNPDE_EXPERIMENTS) return true;
+  static const bool v = [] {
+    const char* e = std::getenv("GNPDE_NS_FUSED");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
+template <int VEC, int GL, int MAXH>
+static void launch_nsf(dim3 grid, size_t lds, bool ragged, hipStream_t s, const float* x, int64_t N, int C,
+                       int64_t ldx, int H, const double* part, int ntiles, const float* Wq, const float* bq, int att,
+                       double* cs, int64_t rpb) {
+  if (ragged)
+    node_scores_fused_kernel<VEC, GL, MAXH, true><<<grid, kBlock, lds, s>>>(x, N, C, ldx, H, part, ntiles, Wq, bq, att,
+                                                                          cs, rpb);
+  else
+    node_scores_fused_kernel<VEC, GL, MAXH, false><<<grid, kBlock, lds, s>>>(x, N, C, ldx, H, part, ntiles, Wq, bq,
+                                                                           att, cs, rpb);
+}
+
+// the same grid as launch_node_scores_any (~1024 wavefronts), one grid row per batch element
+static void launch_node_scores_fused(hipStream_t s, const NsGeom& ge, const float* x, int64_t B, int64_t N, int C,
+                                     int64_t ldx, int H, const double* part, int ntiles, const float* Wq,
+                                     const float* bq, int att, double* cs) {
+  const int G = kWave / ge.GL;
+  const int64_t groups = ceil_div(N, (int64_t)G);
+  const int64_t waves_per_batch = std::max<int64_t>(1, 1024 / B);
+  const int64_t iters = std::max<int64_t>(1, ceil_div(groups, waves_per_batch));
+  const int64_t rpb = (int64_t)kWavesPerBlock * G * iters;
+  const dim3 grid((unsigned)ceil_div(N, rpb), (unsigned)B);
+  const size_t lds = sizeof(double) * (size_t)(att + kBlock + (ge.CW + 1) * ge.maxh);
+  const bool ragged = C != ge.CW;
+#define GNPDE_NSF(V, GLV, M) \
+  launch_nsf<V, GLV, M>(grid, lds, ragged, s, x, N, C, ldx, H, part, ntiles, Wq, bq, att, cs, rpb)
+#define GNPDE_NSF_GL(V, M)                    \
+  do {                                        \
+    if (ge.GL <= 8) GNPDE_NSF(V, 8, M);       \
+    else if (ge.GL <= 16) GNPDE_NSF(V, 16, M); \
+    else if (ge.GL <= 32) GNPDE_NSF(V, 32, M); \
+    else GNPDE_NSF(V, 64, M);                 \
+  } while (0)
+  if (ge.vec == 4) {
+    switch (ge.maxh) {
+      case 1: GNPDE_NSF_GL(4, 1); break;
+      case 2: GNPDE_NSF_GL(4, 2); break;
+      case 4: GNPDE_NSF_GL(4, 4); break;
+      default: GNPDE_NSF_GL(4, 8); break;
+    }
+  } else {
+    switch (ge.maxh) {
+      case 1: GNPDE_NSF_GL(1, 1); break;
+      case 2: GNPDE_NSF_GL(1, 2); break;
+      case 4: GNPDE_NSF_GL(1, 4); break;
+      case 8: GNPDE_NSF_GL(1, 8); break;
+      default: GNPDE_NSF_GL(1, 16); break;
+    }
+  }
+#undef GNPDE_NSF_GL
+#undef GNPDE_NSF
 }
 
 static unsigned edge_grid(int64_t nnz) {
@@ -826,6 +982,12 @@ int gnpde_ref_scores_f32(const float* x, int64_t B, int64_t N, int64_t C, int64_
     GNPDE_KS(1);
 #undef GNPDE_KS
   GNPDE_LAUNCH_CHECK();
+  if (ge.nch == 1 && att <= 1024 && B <= 65535 && ns_fused_enabled()) {
+    // every node-score workgroup forms U itself (node_scores_fused_kernel): two launches
+    launch_node_scores_fused(s, ge, x, B, N, (int)C, ldx, (int)heads, part, ntiles, Wq, bq, (int)att, cs);
+    GNPDE_LAUNCH_CHECK();
+    return GNPDE_OK;
+  }
   const size_t shm2 = sizeof(double) * (size_t)(att + kKeysumBlock);
   key_projection_kernel<<<(unsigned)B, kKeysumBlock, shm2, s>>>(part, ntiles, (int)C, Wq, bq, (int)att, (int)heads,
                                                                  (int)cp, ge.maxh, uv);

@@ -7,6 +7,7 @@
 namespace gnpde {
 
 int bf16_vec_cap() {
+  if constexpr (!GNPDE_EXPERIMENTS) return 4;
   static const int v = [] {
     // cap of the elements per lane (default 4 = 8-byte gathers); rows of 129-256 columns take
     // 16-byte gathers anyway (epi_vec_width) so that they fit the two-rows-per-wavefront geometry
@@ -18,6 +19,7 @@ int bf16_vec_cap() {
 }
 
 bool hub_inlaunch() {
+  if constexpr (!GNPDE_EXPERIMENTS) return true;
   static const bool v = [] {
     const char* e = std::getenv("GNPDE_HUB_FIXUP");
     return !(e && std::atoi(e) == 1);
@@ -26,6 +28,7 @@ bool hub_inlaunch() {
 }
 
 int agg_variant() {
+  if constexpr (!GNPDE_EXPERIMENTS) return 0;
   static const int v = [] {
     const char* e = std::getenv("GNPDE_AGG_VARIANT");
     return e ? std::atoi(e) : 0;
@@ -42,9 +45,9 @@ extern "C" {
 int gnpde_spmm_rhs_f32(const int32_t* items, int64_t n_items, int32_t* heavy, int64_t n_heavy,
                        const int32_t* col, const float* w, int64_t C, const float* x, int64_t ldx, const float* x0,
                        int64_t ldx0, const float* alpha, const float* beta, int flags, float* f, int64_t ldf,
-                       float* partials, const gnpde_stage_epilogue_t* stage, void* stream) {
+                       float* partials, int64_t n_slots, const gnpde_stage_epilogue_t* stage, void* stream) {
   const Epi ep = make_epi(x, ldx, x0, ldx0, alpha, beta, flags, f, ldf, stage);
-  int rc = check_epi(ep, C, n_heavy, partials);
+  int rc = check_epi(ep, C, n_heavy, partials, n_slots);
   if (rc) return rc;
   GNPDE_REQUIRE(n_items >= 0 && n_items < INT32_MAX && n_heavy >= 0, GNPDE_EINVAL, "spmm_rhs: bad item counts");
   GNPDE_REQUIRE(n_items == 0 || (items && col && w), GNPDE_EINVAL, "spmm_rhs: NULL plan/col/w");
@@ -55,10 +58,11 @@ int gnpde_spmm_rhs_f32(const int32_t* items, int64_t n_items, int32_t* heavy, in
 int gnpde_spmm_rhs_bf16(const int32_t* items, int64_t n_items, int32_t* heavy, int64_t n_heavy,
                         const int32_t* col, const float* w, int64_t C, const uint16_t* x, int64_t ldx,
                         const uint16_t* x0, int64_t ldx0, const float* alpha, const float* beta, int flags, uint16_t* f,
-                        int64_t ldf, float* partials, const gnpde_stage_epilogue_t* stage, void* stream) {
+                        int64_t ldf, float* partials, int64_t n_slots, const gnpde_stage_epilogue_t* stage,
+                        void* stream) {
   const Epi ep = make_epi(reinterpret_cast<const float*>(x), ldx, reinterpret_cast<const float*>(x0), ldx0, alpha,
                           beta, flags, reinterpret_cast<float*>(f), ldf, stage);
-  int rc = check_epi(ep, C, n_heavy, partials);
+  int rc = check_epi(ep, C, n_heavy, partials, n_slots);
   if (rc) return rc;
   GNPDE_REQUIRE(n_items >= 0 && n_items < INT32_MAX && n_heavy >= 0, GNPDE_EINVAL, "spmm_rhs_bf16: bad item counts");
   GNPDE_REQUIRE(n_items == 0 || (items && col && w), GNPDE_EINVAL, "spmm_rhs_bf16: NULL plan/col/w");
@@ -70,10 +74,10 @@ int gnpde_attn_ref_rhs_f32(const int32_t* items, int64_t n_items, int32_t* heavy
                            const int32_t* col, const double* cs, const double* m, const float* rl, const double* mr,
                            int64_t heads,
                            int64_t C, const float* x, int64_t ldx, const float* x0, int64_t ldx0, const float* alpha,
-                           const float* beta, int flags, float* f, int64_t ldf, float* partials,
+                           const float* beta, int flags, float* f, int64_t ldf, float* partials, int64_t n_slots,
                            const gnpde_stage_epilogue_t* stage, void* stream) {
   const Epi ep = make_epi(x, ldx, x0, ldx0, alpha, beta, flags, f, ldf, stage);
-  int rc = check_epi(ep, C, n_heavy, partials);
+  int rc = check_epi(ep, C, n_heavy, partials, n_slots);
   if (rc) return rc;
   GNPDE_REQUIRE(heads >= 1 && heads <= 16, GNPDE_EUNSUPPORTED, "attn_ref_rhs: heads=%lld not in [1,16]",
                 (long long)heads);

@@ -40,6 +40,7 @@ inline ScoreArgs make_score_args(int mode, int64_t heads, int64_t dk, const doub
 // contiguous eighths of the K1 work items to one XCD each; =K (>= 2) deals
 // chunks of K consecutive blocks to the XCDs in turn (common.hpp xcd_block).
 inline int xcd_remap_enabled() {
+  if constexpr (!GNPDE_EXPERIMENTS) return 0;
   static const int on = [] {
     const char* e = std::getenv("GNPDE_XCD_REMAP");
     return e ? std::max(0, std::atoi(e)) : 0;
@@ -49,7 +50,7 @@ inline int xcd_remap_enabled() {
 
 inline Epi make_epi(const float* x, int64_t ldx, const float* x0, int64_t ldx0, const float* alpha, const float* beta,
                     int flags, float* f, int64_t ldf, const gnpde_stage_epilogue_t* stage = nullptr) {
-  Epi e;
+  Epi e{};
   e.xcd_remap = xcd_remap_enabled();
   e.has_stage = stage != nullptr;
   if (stage) e.st = *stage;
@@ -65,7 +66,7 @@ inline Epi make_epi(const float* x, int64_t ldx, const float* x0, int64_t ldx0, 
   return e;
 }
 
-inline int check_epi(const Epi& e, int64_t C, int64_t n_heavy, const void* partials) {
+inline int check_epi(const Epi& e, int64_t C, int64_t n_heavy, const void* partials, int64_t n_slots) {
   GNPDE_REQUIRE(C >= 1, GNPDE_EINVAL, "rhs: C must be >= 1");
   GNPDE_REQUIRE(e.x && (e.f || e.has_stage), GNPDE_EINVAL, "rhs: NULL x or f");
   if (e.has_stage) {
@@ -84,7 +85,12 @@ inline int check_epi(const Epi& e, int64_t C, int64_t n_heavy, const void* parti
     GNPDE_REQUIRE(e.flags & GNPDE_EPI_RHS, GNPDE_EINVAL, "rhs: ADD_SOURCE needs EPI_RHS");
     GNPDE_REQUIRE(e.x0 && e.beta && e.ldx0 >= C, GNPDE_EINVAL, "rhs: ADD_SOURCE needs x0, beta, ldx0 >= C");
   }
-  GNPDE_REQUIRE(n_heavy == 0 || partials != nullptr, GNPDE_EINVAL, "rhs: hub rows need a partials buffer");
+  GNPDE_REQUIRE(n_heavy == 0 || (partials != nullptr && n_slots > 0), GNPDE_EINVAL,
+                "rhs: hub rows need a partials buffer and its slot count");
+  // hub partials are addressed with 32-bit buffer offsets (aggregate.hpp, buf_store_wt)
+  GNPDE_REQUIRE(n_slots >= 0 && (n_heavy == 0 || n_slots * C * 4 < (int64_t)kBufRecords), GNPDE_EUNSUPPORTED,
+                "rhs: %lld hub partial slots x %lld columns exceed the 4 GiB of 32-bit buffer offsets; plan the "
+                "graph with a larger chunk", (long long)n_slots, (long long)C);
   return GNPDE_OK;
 }
 

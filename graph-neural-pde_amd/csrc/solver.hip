@@ -92,9 +92,52 @@ __global__ __launch_bounds__(256) void dot_final_kernel(const double* __restrict
   if (threadIdx.x == 0) *out = t;
 }
 
+// Entry of a solve: dst[k] = src[order[k]] (and dst_copy[order[k]] = the same row)
+// in 16-byte pieces, one thread per piece, consecutive threads along a row.
+template <bool ORDER, bool COPY>
+__global__ __launch_bounds__(256) void rows_copy_kernel(const uint4* __restrict__ src, int64_t rows, int64_t v4,
+                                                         const int64_t* __restrict__ order, uint4* __restrict__ dst,
+                                                         uint4* __restrict__ dst_copy) {
+  const int64_t n = rows * v4;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride) {
+    const int64_t k = i / v4, j = i - k * v4;
+    const int64_t r = ORDER ? order[k] : k;
+    const uint4 v = src[r * v4 + j];
+    dst[i] = v;
+    if constexpr (COPY) dst_copy[r * v4 + j] = v;
+  }
+}
+
 }  // namespace gnpde
 
 using namespace gnpde;
+
+extern "C" int gnpde_rows_copy(const void* src, int64_t rows, int64_t row_bytes, const int64_t* order, void* dst,
+                               void* dst_copy, void* stream) {
+  GNPDE_REQUIRE(rows >= 0 && row_bytes >= 0 && src && dst, GNPDE_EINVAL, "rows_copy: bad arguments");
+  GNPDE_REQUIRE(row_bytes % 16 == 0 && aligned16(src) && aligned16(dst) && (!dst_copy || aligned16(dst_copy)),
+                GNPDE_EUNSUPPORTED, "rows_copy: rows of %lld bytes / pointers not 16-byte aligned",
+                (long long)row_bytes);
+  GNPDE_REQUIRE(src != dst && src != dst_copy, GNPDE_EINVAL, "rows_copy: src aliases an output");
+  const int64_t v4 = row_bytes / 16;
+  if (rows == 0 || v4 == 0) return GNPDE_OK;
+  const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(rows * v4, kBlock), 16384));
+  hipStream_t s = as_stream(stream);
+  const uint4* sp = reinterpret_cast<const uint4*>(src);
+  uint4* dp = reinterpret_cast<uint4*>(dst);
+  uint4* cp = reinterpret_cast<uint4*>(dst_copy);
+  if (order && cp)
+    rows_copy_kernel<true, true><<<grid, kBlock, 0, s>>>(sp, rows, v4, order, dp, cp);
+  else if (order)
+    rows_copy_kernel<true, false><<<grid, kBlock, 0, s>>>(sp, rows, v4, order, dp, cp);
+  else if (cp)
+    rows_copy_kernel<false, true><<<grid, kBlock, 0, s>>>(sp, rows, v4, order, dp, cp);
+  else
+    rows_copy_kernel<false, false><<<grid, kBlock, 0, s>>>(sp, rows, v4, order, dp, cp);
+  GNPDE_LAUNCH_CHECK();
+  return GNPDE_OK;
+}
 
 extern "C" size_t gnpde_dot_workspace_bytes(void) { return sizeof(double) * kDotBlocks; }
 

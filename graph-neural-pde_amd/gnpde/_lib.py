@@ -25,7 +25,8 @@ class StageOut(ctypes.Structure):
 
 class StageEpilogue(ctypes.Structure):
     """gnpde_stage_epilogue_t (include/gnpde.h)."""
-    _fields_ = [("f_out", ctypes.c_void_p), ("n_out", ctypes.c_int), ("o", StageOut * STAGE_MAX_OUT)]
+    _fields_ = [("f_out", ctypes.c_void_p), ("n_out", ctypes.c_int), ("o", StageOut * STAGE_MAX_OUT),
+                ("out_rows", ctypes.c_void_p)]
 
 
 c_i32p = ctypes.POINTER(ctypes.c_int32)
@@ -54,11 +55,12 @@ SIGNATURES = {
     "gnpde_plan_build": (_int, [_vp, _i64, ctypes.c_int32, _vp, _i64, _vp, _i64, c_i64p, c_i64p, c_i64p, _vp,
                                 _size, _vp]),
     "gnpde_spmm_rhs_f32": (_int, [_vp, _i64, _vp, _i64, _vp, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _int, _vp,
-                                  _i64, _vp, ctypes.POINTER(StageEpilogue), _vp]),
+                                  _i64, _vp, _i64, ctypes.POINTER(StageEpilogue), _vp]),
     "gnpde_spmm_rhs_bf16": (_int, [_vp, _i64, _vp, _i64, _vp, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _int, _vp,
-                                   _i64, _vp, ctypes.POINTER(StageEpilogue), _vp]),
+                                   _i64, _vp, _i64, ctypes.POINTER(StageEpilogue), _vp]),
     "gnpde_attn_ref_rhs_f32": (_int, [_vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _vp, _i64, _vp, _i64,
-                                      _vp, _vp, _int, _vp, _i64, _vp, ctypes.POINTER(StageEpilogue), _vp]),
+                                      _vp, _vp, _int, _vp, _i64, _vp, _i64, ctypes.POINTER(StageEpilogue), _vp]),
+    "gnpde_rows_copy": (_int, [_vp, _i64, _i64, _vp, _vp, _vp, _vp]),
     "gnpde_seg_long_edges": (_int, []),
     "gnpde_linear_f32": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _vp]),
     "gnpde_keysum_workspace_bytes": (_size, [_i64, _i64, _i64, _i64]),
@@ -73,7 +75,7 @@ SIGNATURES = {
     "gnpde_seg_block_edges": (_int, [_int, _i64, _i64]),
     "gnpde_seg_plan_build": (_int, [_vp, _i64, ctypes.c_int32, _vp, _i64, _vp, _i64, _vp, _i64, c_i64p, c_i64p,
                                     c_i64p]),
-    "gnpde_seg_softmax_f32": (_int, [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _int, _int, _int, _i64, _i64,
+    "gnpde_seg_softmax_f32": (_int, [_vp, _i64, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _int, _int, _int, _i64, _i64,
                                      _vp, _vp, _vp, _i64, _f32, _f32, _vp, _vp, _vp, _vp, _vp, _vp]),
     "gnpde_csr_rowidx": (_int, [_vp, _i64, _i64, _vp, _vp]),
     "gnpde_sddmm_f32": (_int, [_vp, _vp, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _vp, _int, _int, _vp, _vp]),
@@ -95,7 +97,7 @@ SIGNATURES = {
 }
 
 # constants mirrored from include/gnpde.h
-ABI_VERSION = 1
+ABI_VERSION = 2
 OK = 0
 EINVAL = -1
 EHIP = -2
@@ -156,8 +158,30 @@ def load():
         ver = lib.gnpde_abi_version()
         if ver != ABI_VERSION:
             raise GnpdeError("libgnpde ABI version %d != expected %d" % (ver, ABI_VERSION))
+        _check_fresh(lib)
         _lib = lib
         return lib
+
+
+def _check_fresh(lib):
+    """An in-tree library built from other sources than this tree's csrc/ (a
+    stale build with another argument list would shift every argument) is
+    refused; GNPDE_ALLOW_STALE=1 downgrades it to a warning."""
+    if "GNPDE_LIB" in os.environ:
+        return  # an explicitly chosen library: the caller vouches for it
+    try:
+        src = source_hash()
+    except OSError:
+        return  # no sources next to the library (an installed copy): nothing to compare
+    built = lib.gnpde_build_id().decode()
+    if built != src:
+        msg = ("libgnpde.so at %s was built from sources %s, this tree's csrc/ hash to %s: rebuild it "
+               "(make -C graph-neural-pde_amd)" % (LIB_PATH, built, src))
+        if os.environ.get("GNPDE_ALLOW_STALE") == "1":
+            import warnings
+            warnings.warn(msg)
+        else:
+            raise GnpdeError(msg)
 
 
 def call(name, *args):

@@ -21,8 +21,9 @@ axis, src/ray_tune.py:58-59).  Three ways to shard it are provided:
   batch axis B (the reference's own parallel axis); no data-path collective
   (``bench.py --mode replicas``, weak scaling).
 
-``local_rhs`` lets tests substitute a CPU computation so the communication
-pattern is exercised with the gloo backend; the default is the HIP path.
+``local_rhs`` / ``local_stage`` let tests substitute a CPU computation so the
+communication pattern — including the fused-stage path the integrator runs
+(``rhs_stage``) — is exercised with the gloo backend; the default is the HIP path.
 """
 import math
 
@@ -163,7 +164,8 @@ class RowShardedLaplacian(object):
     graph_capturable = False  # an RCCL all-gather per RHS: the integrator runs it eagerly
 
     def __init__(self, edge_index, edge_weight, num_nodes, alpha, beta=None, x0_local=None, add_source=False,
-                 alpha_sigmoid=True, group=None, local_rhs=None, chunk=ops.DEFAULT_CHUNK, row_weight=0.0):
+                 alpha_sigmoid=True, group=None, local_rhs=None, chunk=ops.DEFAULT_CHUNK, row_weight=0.0,
+                 local_stage=None):
         self.group = group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
@@ -175,7 +177,11 @@ class RowShardedLaplacian(object):
         self.add_source, self.alpha_sigmoid = add_source, alpha_sigmoid
         self.nfe = 0
         self.local_rhs = local_rhs
-        if local_rhs is None:
+        # local_stage(t, y_full, r0, r1, y_local, stage): an injected (test) RHS that also
+        # writes the fused stage outputs; host_stages lets the integrator's fused path run it
+        self.local_stage = local_stage
+        self.host_stages = local_stage is not None
+        if local_rhs is None and local_stage is None:
             self.g = ops.GraphCSR(edge_index, self.N, chunk=chunk)
             self.w = self.g.gather_weights(edge_weight)
             self.part = RowPartition(self.g, self.world, self.rank, row_weight=row_weight, chunk=chunk)
@@ -203,10 +209,16 @@ class RowShardedLaplacian(object):
                              alpha_sigmoid=self.alpha_sigmoid, add_source=self.add_source)
 
     def rhs_stage(self, t, y_local, stage):
+        """One RHS with the solver's stage combination in the epilogue (the path
+        gnpde.integrator's fused fixed-grid solve takes): all-gather, then K1
+        over this rank's rows writing the stage outputs."""
         self.nfe += 1
-        if self.local_rhs is not None:
-            raise NotImplementedError
         y_full = self.gather(y_local)
+        if self.local_stage is not None:
+            self.local_stage(t, self.unpad(y_full), self.r0, self.r1, y_local, stage)
+            return
+        if self.local_rhs is not None:
+            raise NotImplementedError("rhs_stage needs local_stage (or the HIP path)")
         self.part.rhs(self.g, self.w, y_full, y_local, x0=self.x0_local, alpha=self.alpha, beta=self.beta,
                       alpha_sigmoid=self.alpha_sigmoid, add_source=self.add_source, stage=stage)
 

@@ -175,29 +175,34 @@ def _fixed_step(method, func, t0, dt, t1, y0, combine):
 
 
 def _fusable(func, y0, combine):
-    """The RHS can emit the stage combinations itself (gnpde ODEFuncs, no autograd)."""
-    return (isinstance(combine, _Combine) and hasattr(func, 'rhs_stage') and y0.is_cuda and
-            y0.dtype in ops.STATE_DTYPES and not torch.is_grad_enabled())
+    """The RHS can emit the stage combinations itself (gnpde ODEFuncs, no autograd).
+    A host-side RHS object with ``host_stages`` (tests/dist_workers.py: the gloo
+    tests of gnpde.dist) takes the same path on CPU tensors."""
+    if not (isinstance(combine, _Combine) and hasattr(func, 'rhs_stage')) or torch.is_grad_enabled():
+        return False
+    return y0.dtype in ops.STATE_DTYPES if y0.is_cuda else bool(getattr(func, 'host_stages', False))
 
 
 RHS_PER_STEP = {'euler': 1, 'midpoint': 2, 'rk4': 4}
 
 
-def _fused_step(method, func, t0, dt, t1, y0, ws, out=None):
+def _fused_step(method, func, t0, dt, t1, y0, ws, out=None, out_rows=None):
     """One grid step with the stage combinations fused into the RHS epilogues
     (gnpde_stage_epilogue_t): same arithmetic as _fixed_step, ~7 fewer passes
     over the state per rk4 step and no separate combine launches.  ``out``:
-    the buffer that receives y1 (default: a new tensor)."""
+    the buffer that receives y1 (default: a new tensor); ``out_rows`` (int32
+    [R]): y1's row r is stored at row out_rows[r] of ``out`` (the last step of
+    a solve run in a node renumbering writes the caller's numbering)."""
     y0 = y0.contiguous()
     if method == 'euler':
         y1 = torch.empty_like(y0) if out is None else out
-        func.rhs_stage(t0, y0, ops.Stage(outs=[(y1, y0, 1.0, dt, [])]))
+        func.rhs_stage(t0, y0, ops.Stage(outs=[(y1, y0, 1.0, dt, [])], out_rows=out_rows))
         return y1
     if method == 'midpoint':
         ym = ws.get('a', y0)
         y1 = torch.empty_like(y0) if out is None else out
         func.rhs_stage(t0, y0, ops.Stage(outs=[(ym, y0, 1.0, 0.5 * dt, [])]))
-        func.rhs_stage(t0 + 0.5 * dt, ym, ops.Stage(outs=[(y1, y0, 1.0, dt, [])]))
+        func.rhs_stage(t0 + 0.5 * dt, ym, ops.Stage(outs=[(y1, y0, 1.0, dt, [])], out_rows=out_rows))
         return y1
     if method == 'rk4':
         # rk4_alt_step_func (3/8 rule).  With x2 = y + dt k1/3 the stage inputs
@@ -213,7 +218,8 @@ def _fused_step(method, func, t0, dt, t1, y0, ws, out=None):
         func.rhs_stage(t0, y0, ops.Stage(outs=[(x2, y0, 1.0, dt / 3.0, [])]))
         func.rhs_stage(t0 + dt / 3.0, x2, ops.Stage(outs=[(x3, x2, -1.0, dt, [(y0, 2.0)])]))
         func.rhs_stage(t0 + dt * 2.0 / 3.0, x3, ops.Stage(outs=[(x4, x3, -1.0, dt, [(x2, 2.0)])]))
-        func.rhs_stage(t1, x4, ops.Stage(outs=[(y1, x4, 0.375, dt * 0.125, [(x3, 0.75), (y0, -0.125)])]))
+        func.rhs_stage(t1, x4, ops.Stage(outs=[(y1, x4, 0.375, dt * 0.125, [(x3, 0.75), (y0, -0.125)])],
+                                         out_rows=out_rows))
         return y1
     raise ValueError(method)
 
@@ -227,76 +233,111 @@ class _Workspace(dict):
         return t
 
 
-# Graph replay of fixed-grid steps (hipGraph through torch.cuda.CUDAGraph):
-# worth it once a few steps share one dt; capture itself costs host time.
+# Graph replay of fixed-grid steps (hipGraph through torch.cuda.CUDAGraph): a run
+# of k equal steps is replayed as the binary decomposition of k into captured
+# blocks of 2^i steps (at most GRAPH_BLOCK each), so a solve costs a handful of
+# graph launches whatever its length (each launch leaves the GPU idle ~18 us
+# between replays: profiles/r03a trace).  Capture itself costs host time, so a
+# solve shorter than GRAPH_MIN_STEPS runs eagerly.
 GRAPH_MIN_STEPS = 6
-# Steps per block graph (even; 0 disables), captured when a block of equal
-# steps remains after the first step.  GNPDE_GRAPH_BLOCK overrides.
-GRAPH_BLOCK = int(os.environ.get('GNPDE_GRAPH_BLOCK', '8'))
+# Largest block graph, in steps (a power of two; GNPDE_GRAPH_BLOCK overrides).
+GRAPH_BLOCK = int(os.environ.get('GNPDE_GRAPH_BLOCK', '64'))
 # Set to a list to receive (start_event, end_event, n_rhs) per graph replay
 # (bench.py's per-launch roofline timing); None in normal use.
 replay_events = None
 
 
-class _StepGraphs(object):
-    """Two captured grid steps with a fixed dt, ping-ponging between two state
-    buffers (bufs[0] -> bufs[1] and back), so a step costs one hipGraphLaunch
-    and no copy of the state.  The RHS and its stage epilogues are the same
-    launches as the eager fused step (same kernels, same arguments, same bits).
-    Every per-graph structure (CSR, plans, cached weights) is built by the
-    eager step that precedes capture, so nothing synchronises inside it.
+def _pow2_blocks(k, cap):
+    """k as a sum of powers of two <= cap, largest first (odd sizes last)."""
+    out = []
+    b = 1
+    while b * 2 <= max(cap, 1):
+        b *= 2
+    while k > 0:
+        while b > k:
+            b //= 2
+        out.append(b)
+        k -= b
+    return out
 
-    block >= 2 (even) also captures a block graph of ``block`` consecutive
-    steps bufs[0] -> bufs[1] -> ... -> bufs[0]: one launch per block instead of
-    one per step (each graph launch leaves the GPU idle for ≈20 µs between
-    replays; profiles/r01p trace)."""
 
-    def __init__(self, method, func, dt, like, ws, block=0):
+class _StatePool(object):
+    """The two ping-pong state buffers and the stage-input workspace of a
+    module's fused fixed-grid solves of one state shape (kept across calls, so
+    the captured graphs that read them stay valid and a solve needs no
+    allocation)."""
+
+    def __init__(self, like):
         self.bufs = [torch.empty_like(like, memory_format=torch.contiguous_format) for _ in range(2)]
-        self.graphs = []
-        self.n_rhs = RHS_PER_STEP[method]
-        nfe = getattr(func, 'nfe', None)
-        pool = None
-        for i in range(2):
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=pool):
-                _fused_step(method, func, 0.0, dt, dt, self.bufs[i], ws, out=self.bufs[1 - i])
-            pool = g.pool()
-            self.graphs.append(g)
-        self.block, self.S = None, 0
-        if block >= 2 and block % 2 == 0:
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=pool):
-                for k in range(block):
-                    _fused_step(method, func, 0.0, dt, dt, self.bufs[k % 2], ws, out=self.bufs[1 - k % 2])
-            self.block, self.S = g, block
-        if nfe is not None:
-            func.nfe = nfe  # capture records launches, it evaluates nothing
+        self.ws = _Workspace()
 
-    def _replay(self, g, n_rhs):
+
+_POOLS = weakref.WeakKeyDictionary()  # module -> {(shape, dtype, device): _StatePool}
+
+
+def _state_pool(func, y):
+    key = (tuple(y.shape), y.dtype, str(y.device))
+    d = _POOLS.get(func)
+    if d is None:
+        d = {}
+        _POOLS[func] = d
+    pool = d.get(key)
+    if pool is None:
+        if len(d) >= 4:
+            d.clear()
+        pool = _StatePool(y)
+        d[key] = pool
+    return pool
+
+
+class _StepGraphs(object):
+    """Captured blocks of fixed-dt grid steps over a _StatePool: graph (s, p)
+    runs s steps starting from bufs[p] (ping-ponging, so it ends in bufs[p ^ (s & 1)]);
+    captured on first use.  The launches are those of the eager fused step (same
+    kernels, same arguments, same bits).  ``warm`` is False until one eager step
+    of this entry has run: every per-graph structure (CSR, plans, cached weights,
+    scratch) is built by an eager call before anything is captured, so nothing
+    synchronises inside a capture."""
+
+    def __init__(self, method, func, dt, pool):
+        self.method, self.dt, self.pool = method, dt, pool
+        self.n_rhs = RHS_PER_STEP[method]
+        self.graphs = {}
+        self.mempool = None
+        self.warm = False
+
+    def graph(self, func, s, p):
+        g = self.graphs.get((s, p))
+        if g is None:
+            nfe = getattr(func, 'nfe', None)
+            bufs, ws = self.pool.bufs, self.pool.ws
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=self.mempool):
+                for k in range(s):
+                    i = p ^ (k & 1)
+                    _fused_step(self.method, func, 0.0, self.dt, self.dt, bufs[i], ws, out=bufs[1 - i])
+            if self.mempool is None:
+                self.mempool = g.pool()
+            if nfe is not None:
+                func.nfe = nfe  # capture records launches, it evaluates nothing
+            self.graphs[(s, p)] = g
+        return g
+
+    def replay(self, func, s, p):
+        """Replay s steps from bufs[p]; counts the RHS evaluations like the eager
+        calls; returns the parity the state ends in."""
+        g = self.graph(func, s, p)
+        if hasattr(func, 'nfe'):
+            func.nfe += s * self.n_rhs
         if replay_events is not None:
-            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            s.record()
+            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            ev0.record()
             g.replay()
-            e.record()
-            replay_events.append((s, e, n_rhs))
+            ev1.record()
+            replay_events.append((ev0, ev1, s * self.n_rhs))
         else:
             g.replay()
-
-    def step(self, func, i):
-        """Replay bufs[i] -> bufs[1-i]; counts the RHS evaluations like the eager calls."""
-        if hasattr(func, 'nfe'):
-            func.nfe += self.n_rhs
-        self._replay(self.graphs[i], self.n_rhs)
-        return self.bufs[1 - i]
-
-    def run_block(self, func):
-        """Replay S steps from bufs[0]; returns (state after the block, state
-        before its last step)."""
-        if hasattr(func, 'nfe'):
-            func.nfe += self.S * self.n_rhs
-        self._replay(self.block, self.S * self.n_rhs)
-        return self.bufs[0], self.bufs[1]
+        return p ^ (s & 1)
 
 
 # Captured step graphs kept per RHS module between odeint calls (one entry per
@@ -338,11 +379,6 @@ def _graph_cache_key(func, method, y, state):
     okey = repr(sorted(opt.items(), key=lambda kv: str(kv[0]))) if isinstance(opt, dict) else None
     return (method, tuple(y.shape), tuple(y.stride()), y.dtype, str(y.device), okey, tuple(tens),
             tuple(id(o) for o in state))
-
-
-def _uniform_run(steps, n, k, dt):
-    """True when steps n .. n+k-1 exist and all have step dt."""
-    return k >= 2 and n + k <= len(steps) and all(steps[i][1] - steps[i][0] == dt for i in range(n, n + k))
 
 
 def _nfe_headroom(func, n):
@@ -421,6 +457,16 @@ class _LaplacianFixedGridFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, y0, alpha_train, beta_train, func, method, steps, t_h):
+        # everything the backward reads is taken NOW: a second forward with
+        # another graph, x0 or alpha before this backward must not change its gradient
+        gr = func.graph_for(y0)
+        w, tag = func._weights_tensor()
+        ctx.w_csc = func.csr_weights(gr, w, tag, transpose=True)  # seen by autograd: never refreshed in place
+        ctx.gr = gr
+        ctx.sig = not func.opt.get('no_alpha_sigmoid', False)
+        ctx.alpha = func.alpha_train.detach().clone()
+        ctx.add_source = bool(func.opt.get('add_source', False))
+        ctx.x0 = func.stable_x0(y0).clone() if ctx.add_source else None
         starts, stage_inputs = [], []
         y = y0.detach().contiguous()
         sol = [y]
@@ -442,16 +488,14 @@ class _LaplacianFixedGridFn(torch.autograd.Function):
         func, method, steps, t_h = ctx.func, ctx.method, ctx.steps, ctx.t_h
         g_sol = g_sol.contiguous()
         with torch.no_grad():
-            gr = func.graph_for(ctx.starts[0])
-            w, tag = func._weights_tensor()
-            w_csc = func.csr_weights(gr, w, tag, transpose=True)
+            gr, w_csc = ctx.gr, ctx.w_csc
             one = torch.ones((), dtype=torch.float32, device=g_sol.device)
-            alpha = func.alpha_train.detach()
-            sig = not func.opt.get('no_alpha_sigmoid', False)
+            alpha = ctx.alpha
+            sig = ctx.sig
             a_dev = torch.sigmoid(alpha) if sig else alpha
             a = float(a_dev)  # one host read per backward: the combination coefficients
-            add_source = bool(func.opt.get('add_source', False))
-            x0 = func.stable_x0(ctx.starts[0]) if add_source else None
+            add_source = ctx.add_source
+            x0 = ctx.x0
 
             def u_of(v):  # (A^T - I) v
                 return ops.spmm_rhs(gr, w_csc, v, alpha=one, rhs=True, alpha_sigmoid=False, transpose=True)
@@ -531,92 +575,195 @@ def _node_layout(func, y0):
     return fn(y0) if fn is not None else None
 
 
+# Host copies of time grids.  A solve needs t on the host (the loop is there); a
+# device t costs a device->host copy, i.e. a wait for everything queued before it.
+# The values of a device t are kept per tensor object (and version), so a model
+# that integrates over the same ``self.t`` every forward (ODEblock) reads it once.
+_T_HOST = {}
+_GRIDS = {}
+
+
+def _host_times(t):
+    if not t.is_cuda:
+        return [float(v) for v in t.tolist()]
+    hit = _T_HOST.get(id(t))
+    if hit is not None and hit[0]() is t and hit[1] == t._version and hit[2] == t.data_ptr():
+        return hit[3]
+    vals = [float(v) for v in t.tolist()]
+    if len(_T_HOST) >= 64:
+        _T_HOST.clear()
+    _T_HOST[id(t)] = (weakref.ref(t), t._version, t.data_ptr(), vals)
+    return vals
+
+
+def _host_grid(t_h, dtype, step_size):
+    """torchdiffeq's grid for the host times t_h (built with CPU torch ops in t's
+    dtype: IEEE on the host as on the device, the same values), cached."""
+    if step_size is None:
+        return list(t_h)
+    key = (tuple(t_h), dtype, float(step_size))
+    g = _GRIDS.get(key)
+    if g is None:
+        g = [float(v) for v in fixed_grid(torch.tensor(t_h, dtype=dtype), step_size).tolist()]
+        if len(_GRIDS) >= 256:
+            _GRIDS.clear()
+        _GRIDS[key] = g
+    return g
+
+
 def odeint_fixed(func, y0, t, method, step_size=None, combine=None, graph=None):
     combine = combine or _Combine()
-    fused = _fusable(func, y0, combine)
-    if fused:
-        lay = _node_layout(func, y0)
-        if lay is not None:
-            # the whole solve in the graph's locality numbering: one gather of the
-            # state in, one of the solution out (bit-identical results, ops.NodeLayout)
-            func._layout = lay
-            try:
-                out = odeint_fixed(func, lay.to_internal(y0), t, method, step_size, combine, graph)
-            finally:
-                func._layout = None
-            return lay.to_user(out)
+    t_h = _host_times(t)
+    grid_h = _host_grid(t_h, t.dtype, step_size)
+    if not (grid_h[0] == t_h[0] and grid_h[-1] == t_h[-1]):
+        raise AssertionError("time grid does not cover t")
+    steps = list(zip(grid_h[:-1], grid_h[1:]))
+    if _fusable(func, y0, combine):
         cp = _padded_width(func, y0)
         if cp is not None:
             C = y0.shape[-1]
             yp = torch.zeros(*y0.shape[:-1], cp, dtype=y0.dtype, device=y0.device)
             yp[..., :C] = y0
-            out = odeint_fixed(func, yp, t, method, step_size, combine, graph)
+            out = _solve_fused(func, yp, t_h, steps, method, graph)
             return out[..., :C].contiguous()
-    ws = _Workspace()
-    # the grid lives on the host (the solver loop reads it there): one sync to
-    # read t, then torchdiffeq's grid built with the same torch ops on the CPU
-    # (IEEE fp32 there as on the device, so the same values)
-    t_h = [float(v) for v in t.tolist()]
-    grid_h = t_h if step_size is None else \
-        [float(v) for v in fixed_grid(torch.tensor(t_h, dtype=t.dtype), step_size).tolist()]
-    if not (grid_h[0] == t_h[0] and grid_h[-1] == t_h[-1]):
-        raise AssertionError("time grid does not cover t")
-    steps = list(zip(grid_h[:-1], grid_h[1:]))
+        return _solve_fused(func, y0, t_h, steps, method, graph)
     if _fused_backward_ok(func, y0, combine, grid_h, t_h) and _nfe_headroom(func, len(steps) * RHS_PER_STEP[method]):
         return _LaplacianFixedGridFn.apply(y0, func.alpha_train, func.beta_train, func, method, steps, t_h)
-    if graph is None:
-        # a RHS with a collective inside (dist.RowShardedLaplacian) opts out of capture
-        graph = len(steps) >= GRAPH_MIN_STEPS and getattr(func, 'graph_capturable', True)
-    graphs = None
-    state = _capture_state(func, y0) if fused and graph else None
-    cache_key = _graph_cache_key(func, method, y0, state)
-    hit = _GRAPH_CACHE.get(func) if cache_key is not None else None
-    if hit is not None and hit[0] == cache_key and len(steps) >= 1 and steps[0][1] - steps[0][0] == hit[1][1]:
-        # same RHS state, shape and dt as a previous call: replay from the first step
-        _, graphs, ws, _ = hit
-        graphs[0].bufs[0].copy_(y0)
-        gi = 0
     solution = [y0]
     j = 1
     yc = y0
-    n = 0
-    while n < len(steps):
-        ta, tb = steps[n]
-        dt = tb - ta
-        if fused and graph and n >= 1 and graphs is None and dt == steps[0][1] - steps[0][0] and \
-                len(steps) - n >= 2:
-            blk = GRAPH_BLOCK if _uniform_run(steps, n, GRAPH_BLOCK, dt) else 0
-            graphs = (_StepGraphs(method, func, dt, yc, ws, block=blk), dt)
-            graphs[0].bufs[0].copy_(yc)
-            gi = 0
-            if cache_key is not None:
-                # the eager first step may have rebuilt derived objects: key what the capture read
-                state = _capture_state(func, yc)
-                _GRAPH_CACHE[func] = (_graph_cache_key(func, method, y0, state), graphs, ws, state)
-        S = graphs[0].S if graphs is not None else 0
-        if S and gi == 0 and _uniform_run(steps, n, S, graphs[1]) and \
-                (j >= len(t_h) or t_h[j] > steps[n + S - 2][1]) and _nfe_headroom(func, S * graphs[0].n_rhs):
-            # no output time inside the block: only its end can be sampled
-            y1, yc = graphs[0].run_block(func)
-            ta, tb = steps[n + S - 1]
-            n += S
-        else:
-            if graphs is not None and dt == graphs[1] and _nfe_headroom(func, graphs[0].n_rhs):
-                y1 = graphs[0].step(func, gi)
-                gi = 1 - gi
-            elif fused:
-                y1 = _fused_step(method, func, ta, dt, tb, yc, ws)
-            else:
-                y1 = _fixed_step(method, func, ta, dt, tb, yc, combine)
-            n += 1
+    for ta, tb in steps:
+        y1 = _fixed_step(method, func, ta, tb - ta, tb, yc, combine)
         while j < len(t_h) and tb >= t_h[j]:
-            v = _linear_interp(ta, tb, yc, y1, t_h[j])
-            # graph buffers are overwritten by later replays (none after the last step)
-            solution.append(v.clone() if graphs is not None and n < len(steps) and
-                            any(v is b for b in graphs[0].bufs) else v)
+            solution.append(_linear_interp(ta, tb, yc, y1, t_h[j]))
             j += 1
         yc = y1
+    while j < len(t_h):  # a degenerate grid (t0 == t1): the state itself
+        solution.append(yc)
+        j += 1
     return torch.stack(solution, 0)
+
+
+def _entry_copy(y0, buf, sol0, order):
+    """buf = y0 in the solve's numbering (order: internal row k holds user row
+    order[k]), sol0 = y0: one pass (gnpde_rows_copy) when rows are 16-byte
+    multiples, torch copies otherwise."""
+    if y0.is_cuda and (y0.shape[-1] * y0.element_size()) % 16 == 0 and y0.is_contiguous():
+        ops.rows_copy(y0, buf, order=order, dst_copy=sol0)
+        return
+    sol0.copy_(y0)
+    if order is None:
+        buf.copy_(y0)
+    else:
+        C = y0.shape[-1]
+        torch.index_select(y0.reshape(-1, C), 0, order, out=buf.view(-1, C))
+
+
+def _to_user(src, dst, lay):
+    """dst = src in the caller's numbering (a fresh solution slice)."""
+    if lay is None:
+        dst.copy_(src)
+    elif src.is_cuda and (src.shape[-1] * src.element_size()) % 16 == 0:
+        ops.rows_copy(src, dst, order=lay.new_id)
+    else:
+        C = src.shape[-1]
+        torch.index_select(src.reshape(-1, C), 0, lay.new_id, out=dst.view(-1, C))
+
+
+def _solve_fused(func, y0, t_h, steps, method, graph):
+    """A fixed-grid solve whose RHS emits the stage combinations itself (gnpde
+    ODEFuncs, no autograd), in the graph's node numbering when the module offers
+    one (ops.NodeLayout: bit-identical results).
+
+    The solution tensor is allocated once; the entry pass writes its t0 slice
+    and the working state (renumbered) in one read of y0; runs of equal steps
+    replay captured block graphs over two ping-pong buffers; when the last
+    requested time is the last grid point, the last step's epilogue writes the
+    result straight into the solution in the caller's numbering (out_rows), so
+    there is no exit pass.  Other output times are copied out (or linearly
+    interpolated, as torchdiffeq) when their step has run."""
+    lay = _node_layout(func, y0)
+    n = len(steps)
+    if graph is None:
+        # a RHS with a collective inside (dist.RowShardedLaplacian) opts out of capture
+        graph = n >= GRAPH_MIN_STEPS and getattr(func, 'graph_capturable', True)
+    sol = torch.empty((len(t_h),) + tuple(y0.shape), dtype=y0.dtype, device=y0.device)
+    pool = _state_pool(func, y0)
+    bufs, ws = pool.bufs, pool.ws
+    _entry_copy(y0.contiguous(), bufs[0], sol[0], lay.order if lay is not None else None)
+    if lay is not None:
+        func._layout = lay
+    try:
+        sg = None
+        if graph and n >= 2:
+            # the first step's dt; the captured graphs replay only runs of exactly this dt
+            state = _capture_state(func, bufs[0])
+            key = _graph_cache_key(func, method, bufs[0], state)
+            dt0 = steps[0][1] - steps[0][0]
+            hit = _GRAPH_CACHE.get(func) if key is not None else None
+            if hit is not None and hit[0] == key and hit[1].dt == dt0 and hit[1].pool is pool:
+                sg = hit[1]
+            else:
+                sg = _StepGraphs(method, func, dt0, pool)
+                if key is not None:
+                    _GRAPH_CACHE[func] = (key, sg, state)
+        p = 0      # the state is in bufs[p]
+        i = 0      # next step to run
+        j = 1      # next output time
+        while j < len(t_h):
+            if i >= n:  # a degenerate grid (t0 == t1): the state itself
+                _to_user(bufs[p], sol[j], lay)
+                j += 1
+                continue
+            m = i
+            while m < n - 1 and steps[m][1] < t_h[j]:
+                m += 1
+            p = _advance(func, method, steps, i, m, p, pool, sg)
+            ta, tb = steps[m]
+            if m == n - 1 and j == len(t_h) - 1 and t_h[j] == tb:
+                # the last step writes the result in the caller's numbering
+                _fused_step(method, func, ta, tb - ta, tb, bufs[p], ws, out=sol[j],
+                            out_rows=lay.order32 if lay is not None else None)
+                j += 1
+                break
+            p = _advance(func, method, steps, m, m + 1, p, pool, sg)
+            ya, yb = bufs[1 - p], bufs[p]
+            while j < len(t_h) and tb >= t_h[j]:
+                if t_h[j] == tb:
+                    _to_user(yb, sol[j], lay)
+                else:
+                    _to_user(_linear_interp(ta, tb, ya, yb, t_h[j]), sol[j], lay)
+                j += 1
+            i = m + 1
+    finally:
+        func._layout = None
+    return sol
+
+
+def _advance(func, method, steps, i, m, p, pool, sg):
+    """Run steps i .. m-1 from bufs[p]; returns the parity the state ends in.
+    Steps of the captured dt go through block graphs (binary decomposition),
+    others — and every step while the module is not warm or too close to its
+    max_nfe — run eagerly (a MaxNFEException is then raised at the exact call)."""
+    bufs, ws = pool.bufs, pool.ws
+    while i < m:
+        ta, tb = steps[i]
+        dt = tb - ta
+        if sg is not None and sg.warm and dt == sg.dt:
+            k = 1
+            while i + k < m and steps[i + k][1] - steps[i + k][0] == dt:
+                k += 1
+            if _nfe_headroom(func, k * sg.n_rhs):
+                for s in _pow2_blocks(k, GRAPH_BLOCK):
+                    p = sg.replay(func, s, p)
+                i += k
+                continue
+        _fused_step(method, func, ta, dt, tb, bufs[p], ws, out=bufs[1 - p])
+        if sg is not None and dt == sg.dt:
+            sg.warm = True
+        p = 1 - p
+        i += 1
+    return p
 
 
 class _RKAdaptive(object):

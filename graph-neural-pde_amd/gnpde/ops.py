@@ -61,22 +61,17 @@ STATE_DTYPES = (torch.float32, torch.bfloat16)  # K1 storage types (fp32 math ei
 
 
 # --------------------------------------------------------------------------- graph
-class Plan(object):
-    """Wavefront work items over a grouped CSR (gnpde_plan_build)."""
-
-    def __init__(self, items, heavy, n_items, n_heavy, n_slots, chunk):
-        self.items, self.heavy = items, heavy
-        self.n_items, self.n_heavy, self.n_slots = n_items, n_heavy, n_slots
-        self.chunk = chunk
-        self.last_stream = None
+class _TicketOrder(object):
+    """Launch ordering of a plan whose kernels keep arrival tickets in it (K1's
+    hub rows, the statistics kernel's long groups: heavy[].w, include/gnpde.h):
+    two launches on one plan must never overlap.  A launch on a different stream
+    than the plan's previous one first waits for everything already queued on
+    that stream (an event; free for the usual single-stream use).  During graph
+    capture the capture itself orders the launches."""
+    last_stream = None
+    n_heavy = 0
 
     def order_launch(self, dev):
-        """K1 combines hub rows inside the launch through arrival tickets kept in
-        this plan (heavy[].w, include/gnpde.h), so two launches on one plan must
-        never overlap.  A launch on a different stream than the plan's previous
-        one first waits for everything already queued on that stream (an event;
-        free for the usual single-stream use).  During graph capture the capture
-        itself orders the launches."""
         if self.n_heavy == 0:
             return
         s = torch.cuda.current_stream(dev)
@@ -86,6 +81,16 @@ class Plan(object):
             ev.record(last)
             s.wait_event(ev)
         self.last_stream = s
+
+
+class Plan(_TicketOrder):
+    """Wavefront work items over a grouped CSR (gnpde_plan_build)."""
+
+    def __init__(self, items, heavy, n_items, n_heavy, n_slots, chunk):
+        self.items, self.heavy = items, heavy
+        self.n_items, self.n_heavy, self.n_slots = n_items, n_heavy, n_slots
+        self.chunk = chunk
+        self.last_stream = None
 
 
 class GroupedCSR(object):
@@ -163,19 +168,21 @@ def build_plan(rowptr, R, nnz, chunk=DEFAULT_CHUNK):
     return Plan(items, heavy, n_it.value, n_hv.value, n_sl.value, chunk)
 
 
-class SegPlan(object):
+class SegPlan(_TicketOrder):
     """Work items of gnpde_seg_softmax_f32 (include/gnpde.h): ``items`` int4
     {e_begin, e_end, -1, first_group} — consecutive whole groups packed greedily
     up to ``eb`` edges — and ``chunk_items`` {e_begin, e_end, slot, group}
     covering groups of more than eb edges in eb-edge chunks, ``heavy`` {group,
     first_slot, n_chunks, 0} per long group."""
 
-    def __init__(self, eb, items, n_items, chunk_items, n_chunk, heavy, n_heavy):
+    def __init__(self, eb, items, n_items, chunk_items, n_chunk, heavy, n_heavy, n_long=0):
         self.eb = eb
         self.items, self.n_items = items, n_items
+        self.n_long = n_long  # long items at the front of ``items`` (reference statistics)
         self.chunk_items, self.n_chunk = chunk_items, n_chunk
         self.heavy, self.n_heavy = heavy, n_heavy
         self.n_slots = n_chunk
+        self.last_stream = None
 
 
 def seg_long_max():
@@ -224,7 +231,7 @@ def build_seg_plan(rowptr, eb, long_items=False):
         all_items = np.concatenate([long_arr, items[:ni.value]], 0)
         hv_arr = np.asarray(hv, np.int32).reshape(-1, 4) if hv else np.zeros((1, 4), np.int32)
         plan = SegPlan(eb, dev32(all_items, all_items.shape[0]), all_items.shape[0], dev32(np.zeros((1, 4), np.int32), 0),
-                       0, dev32(hv_arr, len(hv)), len(hv))
+                       0, dev32(hv_arr, len(hv)), len(hv), n_long=long_arr.shape[0])
         plan.n_slots = slot
         return plan
 
@@ -258,7 +265,7 @@ def add_self_loops(edge_index, edge_weight, fill_value, num_nodes):
     """gnpde_add_self_loops: non-loop edges in COO order, then one loop per node
     with its last existing loop's weight or fill_value (intended semantics of
     src/utils.py:16-42).  -> (edge_index [B,2,K+N] int64, weights [B,K+N] fp32)."""
-    _require_gpu(edge_index, "edge_index", torch.int64)
+    validate_edge_index(edge_index, num_nodes)  # the kernels index per-node arrays with these ids
     B, _, E = edge_index.shape
     N = int(num_nodes)
     ei = edge_index.contiguous()
@@ -288,7 +295,7 @@ def add_self_loops(edge_index, edge_weight, fill_value, num_nodes):
 def norm_weights(edge_index, edge_weight, num_nodes, mode):
     """gnpde_norm_weights_f32: rw (norm_dim 0 / 1) or symmetric gcn weights, degrees
     summed in COO order over a grouped CSR (src/utils.py:177-194, :215-233)."""
-    _require_gpu(edge_index, "edge_index", torch.int64)
+    validate_edge_index(edge_index, num_nodes)  # the kernels index per-node arrays with these ids
     B, _, E = edge_index.shape
     N = int(num_nodes)
     ei = edge_index.contiguous()
@@ -402,6 +409,7 @@ class NodeLayout(object):
         local_order = torch.argsort(-deg, dim=1, stable=True)  # old local id at each new position
         base = (torch.arange(B, device=dev, dtype=torch.int64) * N).view(B, 1)
         self.order = (local_order + base).reshape(R)
+        self.order32 = self.order.to(torch.int32)  # the stage epilogue's out_rows (last step of a solve)
         self.new_id = torch.empty_like(self.order)
         self.new_id[self.order] = torch.arange(R, device=dev, dtype=torch.int64)
         local_new = self.new_id.view(B, N) - base
@@ -512,9 +520,10 @@ class Stage(object):
     ``base`` may be None, the RHS input x, or ``out`` itself (in place).  No
     output may alias the RHS input."""
 
-    def __init__(self, f_out=None, outs=()):
+    def __init__(self, f_out=None, outs=(), out_rows=None):
         self.f_out = f_out
         self.outs = list(outs)
+        self.out_rows = out_rows  # int32 [R] or None: row r's ``outs`` stores go to row out_rows[r]
 
     def tensors(self):
         ts = [self.f_out] if self.f_out is not None else []
@@ -533,6 +542,13 @@ class Stage(object):
         st = _lib.StageEpilogue()
         st.f_out = self.f_out.data_ptr() - shift if self.f_out is not None else None
         st.n_out = len(self.outs)
+        if self.out_rows is not None:
+            if shift:
+                raise ValueError("out_rows cannot be combined with shifted row-block buffers")
+            _require_gpu(self.out_rows, "out_rows", torch.int32)
+            if self.out_rows.numel() * x_input.shape[-1] != x_input.numel():
+                raise ValueError("out_rows must hold one row index per RHS row")
+            st.out_rows = self.out_rows.data_ptr()
         for i, (out, base, cb, cf, ks) in enumerate(self.outs):
             if len(ks) > _lib.STAGE_MAX_K:
                 raise ValueError("at most %d k terms per stage output" % _lib.STAGE_MAX_K)
@@ -586,7 +602,7 @@ def spmm_rhs(g, w_csr, x, x0=None, alpha=None, beta=None, rhs=True, alpha_sigmoi
     partials = _partials(plan, C, dev)
     plan.order_launch(dev)
     epi = (C, _ptr(xr), C, _ptr(x0r), C, _ptr(a), _ptr(b), _flags(rhs, alpha_sigmoid, add_source), _ptr(out), C,
-           _ptr(partials), st, _stream(dev))
+           _ptr(partials), plan.n_slots, st, _stream(dev))
     if dt == torch.bfloat16:
         if isinstance(w_csr, RefDstWeights):
             raise ValueError("bf16 storage takes precomputed weights (attn_rhs(..., fuse=False))")
@@ -658,7 +674,7 @@ def spmm_rhs_rows(g, plan, w_csr, x_src, x_rows, row0, x0=None, alpha=None, beta
     _lib.call("gnpde_spmm_rhs_f32", _ptr(plan.items), plan.n_items, _ptr(plan.heavy), plan.n_heavy,
               _ptr(g.csr.col if col is None else col),
               _ptr(w_csr), C, _ptr(xs), C, sp(x0r), C, _ptr(a), _ptr(b), _flags(True, alpha_sigmoid, add_source),
-              sp(out) if out is not None else ctypes.c_void_p(0), C, _ptr(partials), st, _stream(dev))
+              sp(out) if out is not None else ctypes.c_void_p(0), C, _ptr(partials), plan.n_slots, st, _stream(dev))
     return None if stage is not None else out.view(x_rows.shape)
 
 
@@ -705,18 +721,16 @@ class NodeScores(object):
         self.ldqk = q.shape[1] if q is not None else 1
 
 
-_KEYSUM_WS = {}
-
-
-def _keysum_workspace(dev, nbytes):
-    """Scratch of gnpde_ref_scores_f32 (tile partials, U and v), kept per
-    device, stream and size so that captured step graphs keep reading the
-    buffer they were captured with."""
-    key = (str(dev), torch.cuda.current_stream(dev).cuda_stream, int(nbytes))
-    ws = _KEYSUM_WS.get(key)
+def _keysum_workspace(g, dev, nbytes):
+    """Scratch of gnpde_ref_scores_f32 (tile partials, U and v), held by the graph
+    (freed with it) per stream and size, so that captured step graphs
+    keep reading the buffer they were captured with and two streams never share one."""
+    d = g.__dict__.setdefault('_keysum_ws', {})
+    key = (torch.cuda.current_stream(dev).cuda_stream, int(nbytes))
+    ws = d.get(key)
     if ws is None:
         ws = torch.empty(int(nbytes), dtype=torch.uint8, device=dev)
-        _KEYSUM_WS[key] = ws
+        d[key] = ws
     return ws
 
 
@@ -733,7 +747,7 @@ def node_scores(g, x, Wq, bq, Wk, bk, heads, attention_type='scaled_dot', score_
         B, N, C = g.B, g.N, xr.shape[1]
         cs = torch.empty(g.R, heads, dtype=torch.float64, device=xr.device)
         ws_bytes = _lib.fn("gnpde_keysum_workspace_bytes")(B, N, C, att)
-        ws = _keysum_workspace(xr.device, ws_bytes)
+        ws = _keysum_workspace(g, xr.device, ws_bytes)
         for name, t in (("Wq", Wq), ("bq", bq), ("Wk", Wk), ("bk", bk)):
             _require_gpu(t, name, torch.float32)
         _lib.call("gnpde_ref_scores_f32", _ptr(xr), B, N, C, C, _ptr(g.indeg), _ptr(Wq.contiguous()),
@@ -785,7 +799,9 @@ def _seg_call(g, ns, norm_idx, out_kind, packed=False):
     mr = torch.empty(g.R, stats_record_doubles(H), dtype=torch.float64, device=dev) if packed else None
     partials = torch.empty(plan.n_slots * 2 * H, dtype=torch.float64, device=dev) if plan.n_slots else None
     w = torch.empty(max(g.nnz, 1), dtype=torch.float32, device=dev) if out_kind == 0 else None
-    rc = _lib.call_rc("gnpde_seg_softmax_f32", _ptr(plan.items), plan.n_items, _ptr(plan.chunk_items), plan.n_chunk,
+    plan.order_launch(dev)  # long groups merged in-launch keep arrival tickets in plan.heavy
+    rc = _lib.call_rc("gnpde_seg_softmax_f32", _ptr(plan.items), plan.n_items, plan.n_long, _ptr(plan.chunk_items),
+                      plan.n_chunk,
                       _ptr(plan.heavy), plan.n_heavy, _ptr(grouped.rowptr), _ptr(grouped.rowidx), _ptr(grouped.col),
                       int(norm_idx == 1), out_kind, ns.mode, H, ns.dk, _ptr(ns.cs), _ptr(ns.q), _ptr(ns.k), ns.ldqk,
                       ns.p0, ns.p1, _ptr(w), _ptr(m), _ptr(rl), _ptr(mr), _ptr(partials), _stream(dev))
@@ -987,6 +1003,26 @@ def gather_head(grouped, w, h, scale=1.0):
 
 
 # --------------------------------------------------------------------------- solver glue
+def rows_copy(src, dst, order=None, dst_copy=None):
+    """gnpde_rows_copy: dst[k] = src[order[k]] (rows = the leading dims flattened,
+    order int64 or None = identity) and, when given, dst_copy[order[k]] = the same
+    row (a plain copy of src) from the same read."""
+    _require_gpu(src, "src")
+    src = src.contiguous()
+    C = src.shape[-1]
+    rows = src.numel() // max(C, 1)
+    for t, nm in ((dst, "dst"), (dst_copy, "dst_copy")):
+        if t is not None:
+            _require_gpu(t, nm, src.dtype)
+            if not t.is_contiguous() or t.numel() != src.numel():
+                raise ValueError("rows_copy: %s must be contiguous and sized like src" % nm)
+    if order is not None:
+        _require_gpu(order, "order", torch.int64)
+        if order.numel() != rows:
+            raise ValueError("rows_copy: %d order entries for %d rows" % (order.numel(), rows))
+    _lib.call("gnpde_rows_copy", _ptr(src), rows, C * src.element_size(), _ptr(order), _ptr(dst), _ptr(dst_copy),
+              _stream(src.device))
+    return dst
 def rk_combine(y0, ks, coefs, scale, out=None):
     """out = y0 + scale * sum_j coefs[j] * ks[j]  (one fused pass; y0=None means 0)."""
     ref = y0 if y0 is not None else ks[0]

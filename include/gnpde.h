@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define GNPDE_ABI_VERSION 1
+#define GNPDE_ABI_VERSION 2
 
 #define GNPDE_OK 0
 #define GNPDE_EINVAL (-1)
@@ -173,7 +173,11 @@ size_t gnpde_plan_workspace_bytes(int64_t R);
  * base may be NULL (0), equal to the RHS input x (the row already read by the
  * epilogue is reused) or equal to o[i].out (in-place accumulation).  Every
  * array has the leading dimension ldf of the RHS output.  No output may alias
- * the RHS input x (other rows of x are still being gathered).                */
+ * the RHS input x (other rows of x are still being gathered).
+ * out_rows (NULL = identity): the o[i].out stores of row r go to row
+ * out_rows[r] instead (base, k and f_out stay at row r) — the last step of a
+ * solve run in a renumbered node order writes its result straight into the
+ * caller's numbering (gnpde.integrator); it must be a permutation of [0, R).  */
 #define GNPDE_STAGE_MAX_OUT 2
 #define GNPDE_STAGE_MAX_K 2
 typedef struct {
@@ -190,6 +194,7 @@ typedef struct {
   float* f_out;
   int n_out;
   gnpde_stage_out_t o[GNPDE_STAGE_MAX_OUT];
+  const int32_t* out_rows;
 } gnpde_stage_epilogue_t;
 
 /* ---------------------------------------------------------------- K1: SpMM RHS
@@ -197,10 +202,10 @@ typedef struct {
  * f[r,:]  = ax                                  (flags & 1 == 0)
  *         = a*(ax - x[r,:]) [+ b*x0[r,:]]        (GNPDE_EPI_RHS)
  * a = *alpha or sigmoid(*alpha), b = *beta: device scalars (no host sync).
- * partials: n_slots*C floats of scratch (NULL if n_slots == 0); n_slots*C*4
- * must stay below 0xffffff00 bytes (the hub partials are addressed with 32-bit
- * buffer offsets; the library cannot see n_slots, so the caller checks it —
- * gnpde.ops._partials raises past it: use a larger plan chunk).
+ * partials: n_slots*C floats of scratch (NULL if n_slots == 0; n_slots from
+ * gnpde_plan_build); n_slots*C*4 must stay below 0xffffff00 bytes (the hub
+ * partials are addressed with 32-bit buffer offsets): GNPDE_EUNSUPPORTED past
+ * it — plan the graph with a larger chunk.
  * heavy: the hub table of gnpde_plan_build.  The chunks of a hub row are
  * combined inside the launch by the chunk that finishes last, which it learns
  * from an arrival ticket kept in the 4th word of the row's heavy entry
@@ -213,8 +218,8 @@ int gnpde_spmm_rhs_f32(const int32_t* items, int64_t n_items, int32_t* heavy, in
                        const int32_t* col, const float* w, int64_t C,
                        const float* x, int64_t ldx, const float* x0, int64_t ldx0,
                        const float* alpha, const float* beta, int flags,
-                       float* f, int64_t ldf, float* partials, const gnpde_stage_epilogue_t* stage,
-                       void* stream);
+                       float* f, int64_t ldf, float* partials, int64_t n_slots,
+                       const gnpde_stage_epilogue_t* stage, void* stream);
 
 /* K1 on bfloat16 storage (configs[3], BLEND in bf16): x, x0, f and every
  * stage pointer of `stage` address bf16 arrays (raw uint16 bits; the stage
@@ -224,7 +229,8 @@ int gnpde_spmm_rhs_f32(const int32_t* items, int64_t n_items, int32_t* heavy, in
 int gnpde_spmm_rhs_bf16(const int32_t* items, int64_t n_items, int32_t* heavy, int64_t n_heavy,
                         const int32_t* col, const float* w, int64_t C, const uint16_t* x, int64_t ldx,
                         const uint16_t* x0, int64_t ldx0, const float* alpha, const float* beta, int flags, uint16_t* f,
-                        int64_t ldf, float* partials, const gnpde_stage_epilogue_t* stage, void* stream);
+                        int64_t ldf, float* partials, int64_t n_slots, const gnpde_stage_epilogue_t* stage,
+                        void* stream);
 
 /* K1 with the attention weights computed on the fly for the fork's scaled_dot
  * (reference score mode) under destination-grouped softmax (attention_norm_idx
@@ -242,7 +248,7 @@ int gnpde_attn_ref_rhs_f32(const int32_t* items, int64_t n_items, int32_t* heavy
                            const int32_t* col, const double* cs, const double* m, const float* rl, const double* mr,
                            int64_t heads,
                            int64_t C, const float* x, int64_t ldx, const float* x0, int64_t ldx0, const float* alpha,
-                           const float* beta, int flags, float* f, int64_t ldf, float* partials,
+                           const float* beta, int flags, float* f, int64_t ldf, float* partials, int64_t n_slots,
                            const gnpde_stage_epilogue_t* stage, void* stream);
 
 /* ---------------------------------------------------------------- attention
@@ -311,7 +317,9 @@ int gnpde_attn_weights_f32(const int32_t* rowidx, const int32_t* col, int64_t nn
  * longer group whose
  * partials the last-arriving chunk merges inside the launch (agent-scope ticket
  * in heavy[].w: zero on entry, left zero; launches on one heavy array must not
- * overlap); heavy then lists those groups, and no fixup runs.
+ * overlap); heavy then lists those groups, and no fixup runs.  The long items
+ * come first in `items`: n_long_items of them (0 for other plans); the rest are
+ * whole-group items, taken two per wavefront when grouped by destination.
  * gnpde_seg_plan_build builds them from a HOST copy of rowptr into HOST
  * arrays (plain C++, once per graph; capacities: items >= R, chunk_items >=
  * nnz/eb + R, heavy >= nnz/eb + 1).  When chunk_items == items + 4*n_items
@@ -332,8 +340,9 @@ int gnpde_seg_long_edges(void);
 int gnpde_seg_plan_build(const int32_t* rowptr, int64_t R, int32_t eb, int32_t* items, int64_t items_capacity,
                          int32_t* chunk_items, int64_t chunks_capacity, int32_t* heavy, int64_t heavy_capacity,
                          int64_t* n_items, int64_t* n_chunks, int64_t* n_heavy);
-int gnpde_seg_softmax_f32(const int32_t* items, int64_t n_items, const int32_t* chunk_items, int64_t n_chunk_items,
-                          int32_t* heavy, int64_t n_heavy, const int32_t* rowptr, const int32_t* rowidx,
+int gnpde_seg_softmax_f32(const int32_t* items, int64_t n_items, int64_t n_long_items, const int32_t* chunk_items,
+                          int64_t n_chunk_items, int32_t* heavy, int64_t n_heavy, const int32_t* rowptr,
+                          const int32_t* rowidx,
                           const int32_t* gidx, int group_is_dst, int out_kind, int mode, int64_t heads, int64_t dk,
                           const double* cs, const float* q, const float* k, int64_t ldqk,
                           float score_p0, float score_p1, float* w, double* m, float* rl, double* mr,
@@ -354,6 +363,14 @@ int gnpde_edge_attention_f32(const int32_t* rowidx, const int32_t* col, const in
  * rk4_alt_step_func / _runge_kutta_step combinations).                      */
 int gnpde_rk_combine_f32(int64_t n, const float* y0, int nk, const float* const* ks, const double* coef,
                          double scale, float* out, void* stream);
+
+/* Entry of a solve (gnpde.integrator): dst[k] = src[order[k]] for k < rows
+ * (order NULL: identity), rows of row_bytes bytes (a multiple of 16, 16-byte
+ * aligned pointers); dst_copy (may be NULL) receives src unchanged,
+ * dst_copy[order[k]] = src[order[k]], from the same read — the solution's
+ * t0 slice and the renumbered working state in one pass.  No aliasing.      */
+int gnpde_rows_copy(const void* src, int64_t rows, int64_t row_bytes, const int64_t* order, void* dst,
+                    void* dst_copy, void* stream);
 
 /* <a, b> of two fp32 arrays in fp64 (n elements), written to *out on the device:
  * the parameter gradients of the RHS backward, d alpha_train = sigma'(alpha)

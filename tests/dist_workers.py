@@ -89,3 +89,53 @@ def cols_worker(rank, world, port, method, q):
         q.put((rank, float(np.abs(full - want).max()), steps, want_steps if method == "dopri5" else steps))
     finally:
         dist.destroy_process_group()
+
+
+def host_stage(f, stage):
+    """The fused stage epilogue (include/gnpde.h gnpde_stage_epilogue_t) restated in
+    torch on the host: out = cb*base + cf*f + sum_j c_j k_j for every output."""
+    if stage.f_out is not None:
+        stage.f_out.copy_(f)
+    for out, base, cb, cf, ks in stage.outs:
+        acc = cf * f
+        if base is not None:
+            acc = acc + cb * base
+        for k, c in ks:
+            acc = acc + c * k
+        if stage.out_rows is not None:
+            out.view(-1, out.shape[-1])[stage.out_rows.long()] = acc.view(-1, acc.shape[-1])
+        else:
+            out.copy_(acc)
+
+
+def rows_stage_worker(rank, world, port, method, q):
+    """the fused-stage path of the row partition (rhs_stage: the
+    all-gather, then the stage outputs written by the local RHS) driven by the
+    integrator's fused fixed-grid solve, with the arithmetic injected on the host."""
+    _init(rank, world, port)
+    try:
+        from gnpde import dist as gd, integrator as gi
+        ei, w, x, A = problem(seed=2)
+        alpha = 0.55
+        R, C = A.shape[0], x.shape[-1]
+        At = torch.from_numpy(A)
+
+        def local_stage(t, y_full, r0, r1, y_local, stage):
+            f = torch.zeros_like(y_local)
+            f[:r1 - r0] = alpha * (At[r0:r1] @ y_full - y_full[r0:r1])
+            host_stage(f, stage)
+
+        sh = gd.RowShardedLaplacian(torch.from_numpy(ei), torch.from_numpy(w), x.shape[1], alpha,
+                                    local_stage=local_stage)
+        y0 = sh.scatter(torch.from_numpy(x.reshape(R, C)))
+        calls = []
+        orig = sh.rhs_stage
+        sh.rhs_stage = lambda t, y, st: (calls.append(1), orig(t, y, st))[1]
+        with torch.no_grad():
+            y = gi.odeint(sh, y0, torch.tensor([0.0, 1.0], dtype=torch.float64), method=method,
+                          options=dict(step_size=0.25), combine=gi._Combine())[1]
+        full = sh.unpad(sh.gather(y)).numpy()
+        want, _ = reference(A, x, alpha, method, 1.0, 0.25)
+        q.put((rank, float(np.abs(full - want).max()), sh.nfe, len(calls)))
+    finally:
+        dist.destroy_process_group()

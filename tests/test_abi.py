@@ -46,7 +46,7 @@ def test_library_built_from_these_sources():
 
 
 def test_abi_version():
-    assert _lib.load().gnpde_abi_version() == _lib.ABI_VERSION == 1
+    assert _lib.load().gnpde_abi_version() == _lib.ABI_VERSION == 2
 
 
 def test_library_is_gfx950_code_object():
@@ -59,14 +59,31 @@ def test_errors_are_reported_not_raised():
     vp = ctypes.c_void_p
     # C = 0 -> EINVAL before any launch
     rc = lib.gnpde_spmm_rhs_f32(vp(0), 0, vp(0), 0, vp(0), vp(0), 0, vp(0), 0, vp(0), 0, vp(0), vp(0), 0, vp(0), 0,
-                                vp(0), None, vp(0))
+                                vp(0), 0, None, vp(0))
     assert rc == -1
     assert b"C must be" in lib.gnpde_last_error()
     st = _lib.StageEpilogue()
     st.n_out = 3
     rc = lib.gnpde_spmm_rhs_f32(vp(0), 0, vp(0), 0, vp(0), vp(0), 4, vp(16), 4, vp(0), 0, vp(0), vp(0), 0, vp(0), 4,
-                                vp(0), ctypes.byref(st), vp(0))
+                                vp(0), 0, ctypes.byref(st), vp(0))
     assert rc == -1 and b"n_out" in lib.gnpde_last_error()
+    # the hub partials' 32-bit offsets are checked at the ABI (n_slots is an argument):
+    # 2^22 slots x 256 columns x 4 B = 4 GiB -> unsupported; a partials buffer without its slot count -> invalid
+    rc = lib.gnpde_spmm_rhs_f32(vp(0), 0, vp(0), 1, vp(0), vp(0), 256, vp(16), 256, vp(0), 0, vp(0), vp(0), 0, vp(64),
+                                256, vp(4096), 1 << 22, None, vp(0))
+    assert rc == -3 and b"32-bit buffer offsets" in lib.gnpde_last_error()
+    rc = lib.gnpde_spmm_rhs_f32(vp(0), 0, vp(0), 1, vp(0), vp(0), 256, vp(16), 256, vp(0), 0, vp(0), vp(0), 0, vp(64),
+                                256, vp(4096), 0, None, vp(0))
+    assert rc == -1 and b"slot count" in lib.gnpde_last_error()
+    rc = lib.gnpde_attn_ref_rhs_f32(vp(0), 0, vp(0), 1, vp(0), vp(0), vp(0), vp(0), vp(0), 2, 256, vp(16), 256, vp(0),
+                                    0, vp(0), vp(0), 0, vp(64), 256, vp(4096), 1 << 22, None, vp(0))
+    assert rc == -3 and b"32-bit buffer offsets" in lib.gnpde_last_error()
+    # the solve entry copy: 16-byte rows only, no aliasing
+    rc = lib.gnpde_rows_copy(vp(16), 4, 20, vp(0), vp(64), vp(0), vp(0))
+    assert rc == -3 and b"16-byte" in lib.gnpde_last_error()
+    rc = lib.gnpde_rows_copy(vp(16), 4, 32, vp(0), vp(16), vp(0), vp(0))
+    assert rc == -1 and b"alias" in lib.gnpde_last_error()
+    assert lib.gnpde_rows_copy(vp(16), 0, 32, vp(0), vp(64), vp(128), vp(0)) == 0
     # a well-formed stage struct passes validation (no items -> nothing launched):
     # catches a library built against a stale header layout
     st = _lib.StageEpilogue()
@@ -74,7 +91,7 @@ def test_errors_are_reported_not_raised():
     st.o[0].out, st.o[0].cb, st.o[0].cf, st.o[0].nk = 4096, 1.0, 0.5, 1
     st.o[0].k[0], st.o[0].c[0] = 8192, 2.0
     rc = lib.gnpde_spmm_rhs_f32(vp(0), 0, vp(0), 0, vp(0), vp(0), 4, vp(16), 4, vp(0), 0, vp(32), vp(0), 1, vp(0), 4,
-                                vp(0), ctypes.byref(st), vp(0))
+                                vp(0), 0, ctypes.byref(st), vp(0))
     assert rc == 0, lib.gnpde_last_error()
     rc = lib.gnpde_linear_f32(vp(0), 10, 4, 4, vp(0), vp(0), 8, 8, vp(0), 8, vp(0), 0, vp(0))
     assert rc == -1 and b"NULL" in lib.gnpde_last_error()
@@ -97,7 +114,9 @@ def test_stage_struct_layout_matches_header():
     # gnpde_stage_out_t: out, base (8 B each), cb, cf, nk (4 B each), k[2] (8 B, aligned), c[2]
     assert ctypes.sizeof(_lib.StageOut) == 8 + 8 + 4 + 4 + 4 + 4 + 16 + 8
     assert _lib.StageOut.k.offset == 32
-    assert ctypes.sizeof(_lib.StageEpilogue) == 8 + 8 + 2 * ctypes.sizeof(_lib.StageOut)
+    # gnpde_stage_epilogue_t: f_out, n_out (padded to 8), o[2], out_rows
+    assert ctypes.sizeof(_lib.StageEpilogue) == 8 + 8 + 2 * ctypes.sizeof(_lib.StageOut) + 8
+    assert _lib.StageEpilogue.out_rows.offset == 16 + 2 * ctypes.sizeof(_lib.StageOut)
 
 
 def test_workspace_size_queries():
@@ -119,10 +138,26 @@ def test_c_header_struct_layout_with_gcc(tmp_path):
         pytest.skip("gcc not available")
     src = tmp_path / "layout.c"
     src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "gnpde.h"\nint main(void){'
-                   'printf("%zu %zu %zu %zu\\n", sizeof(gnpde_stage_out_t), offsetof(gnpde_stage_out_t, k),'
-                   'offsetof(gnpde_stage_out_t, c), sizeof(gnpde_stage_epilogue_t));return 0;}\n')
+                   'printf("%zu %zu %zu %zu %zu\\n", sizeof(gnpde_stage_out_t), offsetof(gnpde_stage_out_t, k),'
+                   'offsetof(gnpde_stage_out_t, c), sizeof(gnpde_stage_epilogue_t),'
+                   'offsetof(gnpde_stage_epilogue_t, out_rows));return 0;}\n')
     exe = tmp_path / "layout"
     subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
     got = [int(v) for v in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()]
     assert got == [ctypes.sizeof(_lib.StageOut), _lib.StageOut.k.offset, _lib.StageOut.c.offset,
-                   ctypes.sizeof(_lib.StageEpilogue)]
+                   ctypes.sizeof(_lib.StageEpilogue), _lib.StageEpilogue.out_rows.offset]
+
+
+def test_stale_library_is_refused(monkeypatch):
+    """a library built from other sources than this tree (another
+    argument list would shift every argument) is refused at load time, not
+    only reported by smoke()."""
+    lib = _lib.load()
+    monkeypatch.setattr(_lib, "source_hash", lambda: "0000000000000000")
+    monkeypatch.delenv("GNPDE_LIB", raising=False)
+    monkeypatch.delenv("GNPDE_ALLOW_STALE", raising=False)
+    with pytest.raises(_lib.GnpdeError, match="rebuild"):
+        _lib._check_fresh(lib)
+    monkeypatch.setenv("GNPDE_ALLOW_STALE", "1")
+    with pytest.warns(UserWarning):
+        _lib._check_fresh(lib)

@@ -82,3 +82,16 @@ def test_column_sharded_integration_matches_single_process(method):
     for rank, err, steps, want_steps in res:
         assert err < 1e-9
         assert steps == want_steps  # same accept/reject sequence: the error norm is global
+
+
+@pytest.mark.parametrize("method", ["euler", "midpoint", "rk4"])
+def test_row_sharded_fused_stage_path(method):
+    """The row partition's rhs_stage (all-gather + stage outputs in the epilogue)
+    through the integrator's fused fixed-grid solve, on gloo with the arithmetic
+    injected: every RHS call is a stage call and the result matches the
+    single-process integration."""
+    res = _run(W.rows_stage_worker, method)
+    n = {"euler": 4, "midpoint": 8, "rk4": 16}[method]
+    for rank, err, nfe, calls in res:
+        assert err < 1e-12
+        assert nfe == calls == n

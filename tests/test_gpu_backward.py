@@ -411,3 +411,46 @@ def test_fused_fixed_grid_backward_full_size_garxiv():
     (gxf, gaf), (gxe, gae) = res
     assert (gxf - gxe).abs().max() / gxe.abs().max() < 1e-5
     assert abs(float(gaf - gae)) <= 1e-5 * max(1.0, abs(float(gae)))
+
+
+def test_fused_backward_reads_its_forward_state():
+    """two forwards with different x0 (and alpha, and graph
+    weights) before ONE backward — each backward uses the operands of its own
+    forward, so the summed gradient equals the gradients taken one at a time."""
+    from gnpde import synthetic
+    N, E, C = 2000, 16000, 32
+    ei, w = synthetic.rw_graph(N, E, seed=8, device=DEV)
+    opt = {'hidden_dim': C, 'block': 'constant', 'add_source': True, 'no_alpha_sigmoid': False,
+           'max_nfe': 10 ** 6, 'multi_modal': False}
+    func = gnpde.LaplacianODEFunc(C, C, opt, DEV).to(DEV)
+    func.edge_index, func.edge_weight = ei, w
+    gen = torch.Generator(device=DEV)
+    gen.manual_seed(9)
+    xs = [torch.randn(1, N, C, generator=gen, device=DEV) for _ in range(2)]
+    x0s = [torch.randn(1, N, C, generator=gen, device=DEV) for _ in range(2)]
+    gs = [torch.randn(1, N, C, generator=gen, device=DEV) for _ in range(2)]
+    alphas = [0.4, -0.3]
+    t = torch.tensor([0.0, 0.5], device=DEV)
+
+    def fwd(k):
+        with torch.no_grad():
+            func.alpha_train.fill_(alphas[k])
+        func.x0 = x0s[k]
+        xi = xs[k].clone().requires_grad_(True)
+        return xi, gnpde.odeint(func, xi, t, method='rk4', options={'step_size': 0.125})[1]
+
+    one_at_a_time = []
+    for k in range(2):
+        func.alpha_train.grad = func.beta_train.grad = None
+        xi, y = fwd(k)
+        (y * gs[k]).sum().backward()
+        one_at_a_time.append((xi.grad.clone(), func.alpha_train.grad.clone(), func.beta_train.grad.clone()))
+    func.alpha_train.grad = func.beta_train.grad = None
+    (xa, ya), (xb, yb) = fwd(0), fwd(1)  # the second forward changes x0 and alpha before any backward
+    ((ya * gs[0]).sum() + (yb * gs[1]).sum()).backward()
+    assert torch.equal(xa.grad, one_at_a_time[0][0])
+    assert torch.equal(xb.grad, one_at_a_time[1][0])
+    ga = one_at_a_time[0][1] + one_at_a_time[1][1]
+    gb = one_at_a_time[0][2] + one_at_a_time[1][2]
+    assert abs(float(func.alpha_train.grad - ga)) <= 1e-6 * max(1.0, abs(float(ga)))
+    assert abs(float(func.beta_train.grad - gb)) <= 1e-6 * max(1.0, abs(float(gb)))

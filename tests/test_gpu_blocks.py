@@ -258,3 +258,54 @@ def test_k1_launches_on_two_streams_share_a_plan_safely():
     for i, f in got:
         assert torch.equal(f, want[i])
     assert int(g.csr.plan.heavy.view(-1, 4)[:g.csr.plan.n_heavy, 3].abs().sum()) == 0  # tickets back to 0
+
+
+def test_reference_statistics_on_two_streams_share_a_plan_safely():
+    """the long-group statistics items of the reference-score
+    attention keep arrival tickets in their SegPlan; launches on another stream
+    are ordered behind the plan's previous stream.  The attention RHS (norm_idx 1,
+    a destination group far longer than one long item) alternating between two
+    streams stays bit-identical to a single-stream run, and the tickets return to 0."""
+    from gnpde import ops
+    N, E, C, H, att = 4000, 60000, 64, 2, 32
+    ei, rng = _graph(N, E, 109)
+    ei[0, 1, :9000] = 7  # destination hub: statistics chunks merged in-launch
+    g = ops.GraphCSR(T(ei), N)
+    Wq, Wk = [T((rng.standard_normal((att, C)) * 0.1).astype(np.float32)) for _ in range(2)]
+    bq, bk = [T((rng.standard_normal(att) * 0.1).astype(np.float32)) for _ in range(2)]
+    xs = [torch.randn(N, C, device=DEV).view(1, N, C) for _ in range(4)]
+    alpha = torch.tensor(0.3, device=DEV)
+
+    def rhs(x):
+        ns = ops.node_scores(g, x, Wq, bq, Wk, bk, H, 'scaled_dot', 'reference')
+        return ops.attn_rhs(g, ns, None, None, 1, x, alpha=alpha)
+
+    want = [rhs(x) for x in xs]
+    torch.cuda.synchronize()
+    sp = g.csc.seg_plan(ops._lib.fn("gnpde_seg_block_edges")(ops._lib.SCORE_REFERENCE, H, att // H), True)
+    assert sp.n_heavy >= 1
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    got = []
+    for rep in range(3):
+        for i, x in enumerate(xs):
+            with torch.cuda.stream(streams[i % 2]):
+                got.append((i, rhs(x)))
+    torch.cuda.synchronize()
+    for i, f in got:
+        assert torch.equal(f, want[i])
+    assert int(sp.heavy.view(-1, 4)[:sp.n_heavy, 3].abs().sum()) == 0
+
+
+def test_rows_copy_entry_pass():
+    """gnpde_rows_copy (the solve entry): dst = src[order], dst_copy = src, one read."""
+    from gnpde import ops
+    for dt, C in ((torch.float32, 128), (torch.float32, 12), (torch.bfloat16, 168)):
+        src = torch.randn(3, 1001, C, device=DEV).to(dt)
+        order = torch.randperm(3 * 1001, device=DEV)
+        dst, cpy = torch.empty_like(src), torch.empty_like(src)
+        ops.rows_copy(src, dst, order=order, dst_copy=cpy)
+        assert torch.equal(dst.view(-1, C), src.view(-1, C)[order])
+        assert torch.equal(cpy, src)
+        dst2 = torch.empty_like(src)
+        ops.rows_copy(src, dst2)
+        assert torch.equal(dst2, src)

@@ -777,6 +777,39 @@ def test_arxiv_scale_attention_vs_oracle():
         assert rel(f, want) <= RTOL, mode
 
 
+@pytest.mark.parametrize("mode,norm_idx", [("reference", 1), ("per_edge", 0), ("per_edge", 1)])
+def test_arxiv_scale_dropin_attention_default_path(mode, norm_idx):
+    """ODEFuncTransformerAtt.forward at G-arxiv size on the path
+    the bench times — no statistics passed in, so the reference scores under
+    norm_idx 1 go through the packed {m, rl} records with the long destination
+    groups merged inside the statistics launch, and the per-edge modes through
+    their default kernels — against the fp64 oracle (1e-5), plus the same RHS
+    replayed from a captured graph (same bits)."""
+    import bench
+    N, E, C = synthetic.ARXIV_N, synthetic.ARXIV_E, 128
+    ei, _ = synthetic.rw_graph(N, E, seed=0, device=DEV)
+    x = synthetic.features(1, N, C, seed=1, device=DEV)
+    func = bench.attention_func(mode, norm_idx, C, DEV)
+    func.edge_index = ei
+    with torch.no_grad():
+        func.alpha_train.fill_(0.25)
+        f = func(None, x)
+        cg = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(cg):
+            fg = func(None, x)
+        cg.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(f, fg)
+    if mode == "reference":
+        sp = func.graph_for(x).csc.seg_plan(ops._lib.fn("gnpde_seg_block_edges")(ops._lib.SCORE_REFERENCE, 2, 16),
+                                            True)
+        assert sp.n_heavy > 0  # destination groups longer than one long item: merged in-launch
+    lay = func.multihead_att_layer
+    npw = [t.detach().cpu().numpy() for t in (lay.Q.weight, lay.Q.bias, lay.K.weight, lay.K.bias)]
+    want = O.transformer_rhs(ei.cpu().numpy(), x.cpu().numpy(), None, *npw, 2, norm_idx, 0.25, 0.0, score_mode=mode)
+    assert rel(f, want) <= RTOL, rel(f, want)
+
+
 # ---------------------------------------------------------------- mixed / hard-attention weight producers
 @pytest.mark.parametrize("path", [p for p in FIXTURES if os.path.basename(p).startswith("mixed_")],
                          ids=os.path.basename)

@@ -1,13 +1,19 @@
 #!/bin/bash
-# GPU test session: the listed test files (default: all -m gpu), then optionally the bench.
-# Usage: FILES="tests/a.py tests/b.py" PYTEST_K="bf16 or blend" BENCH=1 tools/gpu_tests.sh
+# GPU test session: the -m gpu suite (one process, per-test time limits), smoke(),
+# then a short bench line.  Stops at the first failing step.
 set -u
-mkdir -p gpurun_out
-fatal() { case "$1" in 124|134|137|139) return 0;; *) return 1;; esac; }
-if [ -n "${PYTEST_K:-}" ]; then KARG=(-k "$PYTEST_K"); else KARG=(); fi
-timeout -k 10 1100 python -u -m pytest ${FILES:-tests} -m gpu -q -ra --timeout 300 --timeout-method thread "${KARG[@]}" > gpurun_out/gpu_tests.log 2>&1; rc=$?
-echo "gpu tests rc=$rc"; tail -25 gpurun_out/gpu_tests.log; if fatal $rc; then exit $rc; fi
-if [ "${BENCH:-0}" = 1 ]; then
-  timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.log 2>&1; rc=$?
-  echo "bench rc=$rc"; tail -c 2500 gpurun_out/bench.log
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out/${TAG:-tests}
+mkdir -p $OUT
+cd $R
+timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} \
+  > $OUT/pytest.log 2>&1; rc=$?
+echo "pytest rc=$rc"; tail -15 $OUT/pytest.log
+[ $rc = 0 ] || exit $rc
+timeout -k 10 300 python3 -c 'import __graft_entry__ as g; g.smoke()' > $OUT/smoke.log 2>&1; rc=$?
+echo "smoke rc=$rc"; tail -3 $OUT/smoke.log
+[ $rc = 0 ] || exit $rc
+if [ "${BENCH:-1}" = 1 ]; then
+  timeout -k 10 400 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $OUT/bench.log 2>&1; rc=$?
+  echo "bench rc=$rc"; tail -c 1500 $OUT/bench.log
 fi
