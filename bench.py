@@ -128,12 +128,19 @@ def max_over_ranks(v, world, dev):
     return v
 
 
+_T = {}
+
+
 def rk4_solve(func, y0, n, h, dev):
     """Exactly n rk4 steps through the drop-in integrator (stage combinations
-    fused into the RHS epilogues, steps replayed from captured hipGraphs)."""
+    fused into the RHS epilogues, steps replayed from captured hipGraphs).  The
+    time tensor is made once per (n, h) and reused, as ODEblock keeps its
+    ``self.t`` (src/base_classes.py): the integrator then reads its values once."""
     import gnpde
-    t = torch.tensor([0.0, n * h], dtype=torch.float32, device=dev)
-    return gnpde.odeint(func, y0, t, method='rk4', options={'step_size': h})[1]
+    key = (n, h, str(dev))
+    if key not in _T:
+        _T[key] = torch.tensor([0.0, n * h], dtype=torch.float32, device=dev)
+    return gnpde.odeint(func, y0, _T[key], method='rk4', options={'step_size': h})[1]
 
 
 def timed_solve(func, y0, steps, warmup, h, dev, world, sync_world=None):

@@ -38,16 +38,17 @@ struct PlainWeights {
 // m 16-byte and rl 8-byte aligned): one 16-B load of m[c,:] and one 8-B load
 // of rl[c,:] per edge instead of four scalar gathers.
 // REC (with EXACT): m and rl come from the packed statistics records of the
-// destinations (m = the record base, stats_record_doubles(2) = 4 doubles:
-// m[0..1], then rl[0..1] as floats; rl unused): one 32-byte-aligned record per
-// edge, one cache line instead of the two of the separate arrays; same values
-// and the same finish(), so the same bits.
+// destinations (rec, stats_record_floats(2) = 4 floats: m[0..1], rl[0..1]):
+// one 16-byte load per edge, a quarter of a cache line, instead of two lines of
+// the separate arrays; the same values (the stored max is fp32-exact in both
+// forms) and the same finish(), so the same bits.
 template <int MAXH, bool EXACT = false, bool REC = false>
 struct RefDstSoftmaxWeights {
   const double* __restrict__ cs;
   const double* __restrict__ m;
   const float* __restrict__ rl;
   int H;
+  const float* __restrict__ rec;
   struct Raw {
     double mm[MAXH > 0 ? MAXH : 1];
     float rr[MAXH > 0 ? MAXH : 1];
@@ -56,13 +57,17 @@ struct RefDstSoftmaxWeights {
   __device__ __forceinline__ Raw load(int /*row*/, int /*p*/, int c) const {
     Raw r;
     r.c = c;
-    if constexpr (EXACT) {
+    if constexpr (EXACT && REC) {
+      static_assert(MAXH == 2 && stats_record_floats(2) == 4, "two-head records are 16 bytes");
+      const float4 v = *reinterpret_cast<const float4*>(rec + (int64_t)c * 4);
+      r.mm[0] = (double)v.x;
+      r.mm[1] = (double)v.y;
+      r.rr[0] = v.z;
+      r.rr[1] = v.w;
+    } else if constexpr (EXACT) {
       static_assert(MAXH == 2, "EXACT statistics loads are written for two heads");
-      static_assert(!REC || stats_record_doubles(2) == 4, "two-head records are 32 bytes");
-      const double* mp = REC ? m + (int64_t)c * 4 : m + (int64_t)c * 2;
-      const float* rp = REC ? reinterpret_cast<const float*>(mp + 2) : rl + (int64_t)c * 2;
-      const double2 mv = *reinterpret_cast<const double2*>(mp);
-      const float2 rv = *reinterpret_cast<const float2*>(rp);
+      const double2 mv = *reinterpret_cast<const double2*>(m + (int64_t)c * 2);
+      const float2 rv = *reinterpret_cast<const float2*>(rl + (int64_t)c * 2);
       r.mm[0] = mv.x;
       r.mm[1] = mv.y;
       r.rr[0] = rv.x;
@@ -108,6 +113,7 @@ __device__ __forceinline__ void hub_combine(int row, int first, int nch, int C, 
   const int g = lane / GL, gl = lane % GL;
   const float a = (ep.flags & GNPDE_EPI_RHS) ? epi_alpha(ep) : 1.f;
   const float b = (ep.flags & GNPDE_ADD_SOURCE) ? *ep.beta : 0.f;
+  double dpart = 0.0;
   for (int c0 = 0; c0 < C; c0 += GL * VEC) {
     const int cc = c0 + gl * VEC;
     const bool live = cc < C;
@@ -130,8 +136,10 @@ __device__ __forceinline__ void hub_combine(int row, int first, int nch, int C, 
     for (int o = GL; o < kWave; o <<= 1)
 #pragma unroll
       for (int t = 0; t < VEC; ++t) s[t] += __shfl_xor(s[t], o);
-    if (g == 0 && live) epilogue_store<VEC, STG, T>(ep, row, cc, s, a, b);
+    if (g == 0 && live) epilogue_store<VEC, STG, T>(ep, row, cc, s, a, b, &dpart);
   }
+  if constexpr (STG > 0 && sizeof(T) == 4)
+    if (ep.st.dot_rows) epi_dot_store<GL>(ep, row, dpart, lane == 0);  // wave-uniform
 }
 
 // A chunk wave whose write-through partial stores are issued: drain them, take
@@ -355,16 +363,20 @@ __global__ __launch_bounds__(256) void agg_kernel(const int4* __restrict__ items
   }
   const float a = (ep.flags & GNPDE_EPI_RHS) ? epi_alpha(ep) : 1.f;
   const float b = (ep.flags & GNPDE_ADD_SOURCE) ? *ep.beta : 0.f;
+  double dpart = 0.0;
 #pragma unroll
   for (int ch = 0; ch < NCH; ++ch) {
     const int cc = (ch * GL + gl) * VEC;
     if (cc < C) {
       if constexpr (PRE)
-        epi_finish<VEC, STG, T>(ep, row, cc, acc[ch], a, b, pre[ch]);
+        epi_finish<VEC, STG, T>(ep, row, cc, acc[ch], a, b, pre[ch], &dpart);
       else
-        epilogue_store<VEC, STG, T>(ep, row, cc, acc[ch], a, b);
+        epilogue_store<VEC, STG, T>(ep, row, cc, acc[ch], a, b, &dpart);
     }
   }
+  // the row's owner lanes (g == 0: lanes [rs*SL, rs*SL + GL)) are all here
+  if constexpr (STG > 0 && sizeof(T) == 4 && (GL & (GL - 1)) == 0)
+    if (ep.st.dot_rows) epi_dot_store<GL>(ep, row, dpart, gl == 0);
 }
 
 // Hub rows combined after the aggregation launch (GNPDE_HUB_FIXUP=1): one wavefront per hub.

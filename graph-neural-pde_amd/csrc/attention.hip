@@ -133,112 +133,105 @@ __device__ __forceinline__ float seg_team_score(const ScoreArgs& sa, const float
 }
 
 // ------------------------------------------------------------------ long groups (reference statistics)
-// Reference-score statistics take groups longer than a wavefront's EB edges as
-// LONG items, lanes striding over the edges (kSegLongU per lane per pass, each
-// lane an online (max, sum-exp) per head, a fixed xor tree across lanes):
-//   slot field -2:        a whole group of at most kSegLongMax edges -> m, rl / mr;
-//   slot field -3 - slot: a kSegLongMax-edge chunk of a longer group -> its partial
-//                         statistics (write-through); the chunk that arrives last
-//                         (agent-scope ticket in heavy[].w, as K1's hub rows)
-//                         merges the group's chunks in chunk order, reading them
-//                         with sc1 loads, and resets the ticket.
-// With 256-edge chunks G-arxiv's CSC has 239 chunked groups (at most 29 chunks
-// each) instead of 3,707 groups of 64-edge chunks and a fixup launch.
+// Reference-score statistics of destination groups longer than a wavefront's
+// 64-edge block (ref_stats_kernel):
+//   * LONG items (slot field -2): a whole group of at most kSegLongMax edges, one
+//     wavefront, lanes striding (kSegLongU edges per lane, one pass), each lane an
+//     online (max, sum-exp) per head, a fixed xor tree across the lanes;
+//   * HUB items (slot field -4): a longer group, one whole 1024-thread workgroup:
+//     every thread pushes up to kHubU edges per pass, the 16 wavefronts reduce by
+//     xor trees, then in wavefront order through LDS — fixed order, no chunk
+//     partials, no arrival tickets, no second launch.  G-arxiv's CSC has 239 such
+//     groups (up to 7,444 edges): one pass of 8 edges per thread covers 8,192.
 constexpr int kSegLongU = 4;                   // edges per lane per pass
 constexpr int kSegLongMax = kWave * kSegLongU;  // 256: one pass
+constexpr int kRefBlock = 1024;                 // ref_stats_kernel workgroup (hub items: all of it)
+constexpr int kRefWaves = kRefBlock / kWave;
+constexpr int kHubU = 8;                        // edges per thread per pass of a hub group
 
-__device__ __forceinline__ double load_sc1_f64(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, kAuxSc1));
+template <int U, int MAXH>
+__device__ __forceinline__ void push_edges(int pb, int stride, int e1, const int* __restrict__ gidx,
+                                           const ScoreArgs& sa, double (&M)[MAXH], float (&L)[MAXH]) {
+  const int H = sa.H;
+  int src[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int p = pb + stride * u;
+    src[u] = p < e1 ? gidx[p] : -1;
+  }
+  double v[U][MAXH];
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int h = 0; h < MAXH; ++h) v[u][h] = h < H ? sa.cs[(int64_t)max(src[u], 0) * H + h] : 0.0;
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int h = 0; h < MAXH; ++h)
+      if (src[u] >= 0 && h < H) online_push(M[h], L[h], v[u][h]);
 }
 
-__device__ __forceinline__ void seg_long_stats(int e0, int e1, int grp, int slot, const int* __restrict__ gidx,
-                                               int group_is_dst, const ScoreArgs& sa, double* m, float* rl,
-                                               double* mr, double* partials, int4* heavy, int n_heavy) {
+template <int MAXH>
+__device__ __forceinline__ void wave_merge(double (&M)[MAXH], float (&L)[MAXH]) {
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1)
+#pragma unroll
+    for (int h = 0; h < MAXH; ++h) {
+      const double M2 = __shfl_xor(M[h], o);
+      const float L2 = __shfl_xor(L[h], o);
+      online_merge(M[h], L[h], M2, L2);
+    }
+}
+
+// a whole group of at most kSegLongMax edges by one wavefront
+template <int MAXH>
+__device__ __forceinline__ void long_group_stats(int e0, int e1, int grp, const int* __restrict__ gidx,
+                                                 const ScoreArgs& sa, double* m, float* rl, float* mr) {
   const int lane = threadIdx.x & 63;
-  const int H = sa.H;
-  const __amdgpu_buffer_rsrc_t rp = buf_rsrc(partials);
-  for (int h0 = 0; h0 < H; h0 += 2) {
-    const bool two = h0 + 1 < H;
-    double M0 = -INFINITY, M1 = -INFINITY;
-    float L0 = 0.f, L1 = 0.f;
-    for (int pb = e0; pb < e1; pb += kSegLongMax) {
-      int src[kSegLongU];
+  double M[MAXH];
+  float L[MAXH];
 #pragma unroll
-      for (int u = 0; u < kSegLongU; ++u) {
-        const int p = pb + lane + kWave * u;
-        src[u] = p < e1 ? (group_is_dst ? gidx[p] : grp) : -1;
-      }
-      double a[kSegLongU], b[kSegLongU];
-#pragma unroll
-      for (int u = 0; u < kSegLongU; ++u) {
-        const int64_t o = (int64_t)max(src[u], 0) * H + h0;
-        a[u] = sa.cs[o];
-        b[u] = two ? sa.cs[o + 1] : 0.0;
-      }
-#pragma unroll
-      for (int u = 0; u < kSegLongU; ++u) {
-        if (src[u] >= 0) {
-          online_push(M0, L0, a[u]);
-          if (two) online_push(M1, L1, b[u]);
-        }
-      }
-    }
-#pragma unroll
-    for (int o = 1; o < kWave; o <<= 1) {
-      const double Ma = __shfl_xor(M0, o), Mb = __shfl_xor(M1, o);
-      const float La = __shfl_xor(L0, o), Lb = __shfl_xor(L1, o);
-      online_merge(M0, L0, Ma, La);
-      online_merge(M1, L1, Mb, Lb);
-    }
-    if (slot < 0) {
-      if (lane == 0) {
-        store_stats(m, rl, mr, grp, H, h0, M0, 1.0f / (L0 + kSoftmaxEps));
-        if (two) store_stats(m, rl, mr, grp, H, h0 + 1, M1, 1.0f / (L1 + kSoftmaxEps));
-      }
-    } else {  // partials [slot][2H]: max then sum-exp, write-through
-      const uint32_t o = (uint32_t)(((int64_t)slot * 2 * H + h0) * 8);
-      const bool w0 = lane == 0, w1 = lane == 0 && two;
-      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, M0), rp, w0 ? o : kBufNone, 0, kAuxSc1);
-      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, (double)L0), rp, w0 ? o + 8u * H : kBufNone, 0,
-                                            kAuxSc1);
-      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, M1), rp, w1 ? o + 8u : kBufNone, 0, kAuxSc1);
-      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, (double)L1), rp, w1 ? o + 8u * H + 8u : kBufNone,
-                                            0, kAuxSc1);
-    }
+  for (int h = 0; h < MAXH; ++h) {
+    M[h] = -INFINITY;
+    L[h] = 0.f;
   }
-  if (slot < 0) return;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this chunk's partials have reached the memory side
-  int lo = 0, hi = n_heavy - 1;
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (heavy[mid].y <= slot)
-      lo = mid;
-    else
-      hi = mid - 1;
-  }
-  int ticket = 0;
-  if (lane == 0) ticket = __hip_atomic_fetch_add(&heavy[lo].w, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  ticket = __shfl(ticket, 0);
-  const int4 hv = heavy[lo];
-  const int g = uniform(hv.x), first = uniform(hv.y), nch = uniform(hv.z);
-  if (ticket != nch - 1) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the sc1 loads below the ticket
-  for (int h = 0; h < H; ++h) {
-    double M = -INFINITY;
-    float L = 0.f;
-    for (int c = lane; c < nch; c += kWave) {
-      const uint32_t o = (uint32_t)(((int64_t)(first + c) * 2 * H + h) * 8);
-      online_merge(M, L, load_sc1_f64(rp, o), (float)load_sc1_f64(rp, o + 8u * H));
-    }
+  for (int pb = e0 + lane; pb < e1; pb += kSegLongMax) push_edges<kSegLongU, MAXH>(pb, kWave, e1, gidx, sa, M, L);
+  wave_merge<MAXH>(M, L);
+  if (lane == 0)
 #pragma unroll
-    for (int o = 1; o < kWave; o <<= 1) {
-      const double M2 = __shfl_xor(M, o);
-      const float L2 = __shfl_xor(L, o);
-      online_merge(M, L, M2, L2);
-    }
-    if (lane == 0) store_stats(m, rl, mr, g, H, h, M, 1.0f / (L + kSoftmaxEps));
+    for (int h = 0; h < MAXH; ++h)
+      if (h < sa.H) store_stats(m, rl, mr, grp, sa.H, h, M[h], L[h]);
+}
+
+// a hub group by the whole 1024-thread workgroup (block-uniform call)
+template <int MAXH>
+__device__ __forceinline__ void hub_group_stats(int e0, int e1, int grp, const int* __restrict__ gidx,
+                                                const ScoreArgs& sa, double* m, float* rl, float* mr) {
+  __shared__ double sM[kRefWaves][MAXH];
+  __shared__ float sL[kRefWaves][MAXH];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  double M[MAXH];
+  float L[MAXH];
+#pragma unroll
+  for (int h = 0; h < MAXH; ++h) {
+    M[h] = -INFINITY;
+    L[h] = 0.f;
   }
-  if (lane == 0) __hip_atomic_store(&heavy[lo].w, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (int pb = e0 + tid; pb < e1; pb += kRefBlock * kHubU) push_edges<kHubU, MAXH>(pb, kRefBlock, e1, gidx, sa, M, L);
+  wave_merge<MAXH>(M, L);
+  if (lane == 0)
+#pragma unroll
+    for (int h = 0; h < MAXH; ++h) {
+      sM[wv][h] = M[h];
+      sL[wv][h] = L[h];
+    }
+  __syncthreads();
+  if (tid < MAXH && tid < sa.H) {
+    double Mh = -INFINITY;
+    float Lh = 0.f;
+    for (int w = 0; w < kRefWaves; ++w) online_merge(Mh, Lh, sM[w][tid], sL[w][tid]);
+    store_stats(m, rl, mr, grp, sa.H, tid, Mh, Lh);
+  }
 }
 
 template <bool REF, int OUT>
@@ -248,7 +241,7 @@ __global__ __launch_bounds__(256) void seg_softmax_kernel(const int4* __restrict
                                                            const int* __restrict__ gidx, int group_is_dst,
                                                            ScoreArgs sa, Team tm, float* __restrict__ w,
                                                            double* __restrict__ m, float* __restrict__ rl,
-                                                           double* __restrict__ mr, double* __restrict__ partials,
+                                                           float* __restrict__ mr, double* __restrict__ partials,
                                                            int4* heavy, int n_heavy) {
   using S_t = typename std::conditional<REF, double, float>::type;
   const int lane = threadIdx.x & 63;
@@ -258,12 +251,6 @@ __global__ __launch_bounds__(256) void seg_softmax_kernel(const int4* __restrict
   const int e0 = uniform(it.x), e1 = uniform(it.y), slot = uniform(it.z);
   const int n = e1 - e0;
   if (n <= 0) return;
-  if (slot <= -2) {  // long item (reference statistics only; other kinds are rejected by the host)
-    if constexpr (REF && OUT == kSegStats)
-      seg_long_stats(e0, e1, uniform(it.w), slot == -2 ? -1 : -3 - slot, gidx, group_is_dst, sa, m, rl, mr, partials,
-                     heavy, n_heavy);
-    return;
-  }
   const bool live = lane < n;
   const int p = e0 + min(lane, n - 1);
   const int grp = rowidx[p];
@@ -333,7 +320,7 @@ __global__ __launch_bounds__(256) void seg_softmax_kernel(const int4* __restrict
       } else if constexpr (OUT == kSegWeights) {
         wsum += e / (Ls + kSoftmaxEps);
       } else {
-        if (live && lane == seg_end) store_stats(m, rl, mr, grp, H, h, (double)M, 1.0f / (Ls + kSoftmaxEps));
+        if (live && lane == seg_end) store_stats(m, rl, mr, grp, H, h, (double)M, Ls);
       }
     }
   }
@@ -342,35 +329,37 @@ __global__ __launch_bounds__(256) void seg_softmax_kernel(const int4* __restrict
   }
 }
 
-// ------------------------------------------------------------------ reference statistics, short items
-// The reference scores' destination statistics (norm_idx 1) over the short items
-// (whole groups packed up to 64 edges): NI items per wavefront with every load
-// of all NI items issued before any arithmetic (item -> {group id, source id} ->
-// the sources' node scores is a chain of three dependent loads, and the kernel
-// is latency-bound: two items per wave halve the waves and overlap the chains).
+// ------------------------------------------------------------------ reference statistics
+// The reference scores' destination statistics (norm_idx 1) in one launch of
+// 1024-thread workgroups over a plan of HUB items (one workgroup each), then
+// LONG items (one wavefront each), then SHORT items (whole groups packed up to 64
+// edges, NI per wavefront with every load of all NI items issued before any
+// arithmetic: item -> {group id, source id} -> the sources' node scores is a
+// chain of three dependent loads, so two items per wave overlap their chains).
 // A lane's segment end comes from a ballot of group changes (no rowptr gather).
-// Long items (slot <= -2, the first n_long items of the plan) keep one
-// wavefront each (seg_long_stats).  Same arithmetic as seg_softmax_kernel<true,
-// kSegStats>: segmented max, exp(v - M), segmented sum, in the same lane order.
+// Same arithmetic as seg_softmax_kernel<true, kSegStats>: segmented max,
+// exp(v - M), segmented sum, in the same lane order.
 constexpr int kRefStatsNI = 2;
 
 template <int NI, int MAXH>
-__global__ __launch_bounds__(256) void ref_stats_kernel(const int4* __restrict__ items, int n_items, int n_long,
-                                                         const int* __restrict__ rowidx, const int* __restrict__ gidx,
-                                                         ScoreArgs sa, double* __restrict__ m,
-                                                         float* __restrict__ rl, double* __restrict__ mr,
-                                                         double* __restrict__ partials, int4* heavy, int n_heavy) {
+__global__ __launch_bounds__(kRefBlock) void ref_stats_kernel(const int4* __restrict__ items, int n_items, int n_hub,
+                                                               int n_long, const int* __restrict__ rowidx,
+                                                               const int* __restrict__ gidx, ScoreArgs sa,
+                                                               double* __restrict__ m, float* __restrict__ rl,
+                                                               float* __restrict__ mr) {
   const int lane = threadIdx.x & 63;
-  const int wid = uniform(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
-  if (wid < n_long) {
-    const int4 it = items[wid];
-    const int e0 = uniform(it.x), e1 = uniform(it.y), slot = uniform(it.z);
-    if (e1 > e0)
-      seg_long_stats(e0, e1, uniform(it.w), slot == -2 ? -1 : -3 - slot, gidx, 1, sa, m, rl, mr, partials, heavy,
-                     n_heavy);
+  if ((int)blockIdx.x < n_hub) {
+    const int4 it = items[blockIdx.x];
+    hub_group_stats<MAXH>(it.x, it.y, it.w, gidx, sa, m, rl, mr);
     return;
   }
-  const int base = n_long + (wid - n_long) * NI;
+  const int wid = uniform(((int)blockIdx.x - n_hub) * kRefWaves + (int)(threadIdx.x >> 6));
+  if (wid < n_long) {
+    const int4 it = items[n_hub + wid];
+    long_group_stats<MAXH>(uniform(it.x), uniform(it.y), uniform(it.w), gidx, sa, m, rl, mr);
+    return;
+  }
+  const int base = n_hub + n_long + (wid - n_long) * NI;
   if (base >= n_items) return;
   const int H = sa.H;
   int e0[NI], n[NI], grp[NI], src[NI];
@@ -406,7 +395,7 @@ __global__ __launch_bounds__(256) void ref_stats_kernel(const int4* __restrict__
           const double M = __shfl(seg_scan<true>(x, same), seg_end);
           const float e = live ? expf((float)(x - M)) : 0.f;
           const float Ls = __shfl(seg_scan<false>(e, same), seg_end);
-          if (live && lane == seg_end) store_stats(m, rl, mr, grp[i], H, h, M, 1.0f / (Ls + kSoftmaxEps));
+          if (live && lane == seg_end) store_stats(m, rl, mr, grp[i], H, h, M, Ls);
         }
       }
     }
@@ -414,14 +403,13 @@ __global__ __launch_bounds__(256) void ref_stats_kernel(const int4* __restrict__
 }
 
 template <int NI>
-static int launch_ref_stats(const int4* items, int64_t n_items, int64_t n_long, const int* rowidx, const int* gidx,
-                            const ScoreArgs& sa, double* m, float* rl, double* mr, double* partials, int4* heavy,
-                            int n_heavy, hipStream_t s) {
-  const int64_t waves = n_long + ceil_div(n_items - n_long, (int64_t)NI);
-  const unsigned grid = (unsigned)ceil_div(waves, kWavesPerBlock);
-#define GNPDE_RS(M)                                                                                              \
-  ref_stats_kernel<NI, M><<<grid, kBlock, 0, s>>>(items, (int)n_items, (int)n_long, rowidx, gidx, sa, m, rl, mr, \
-                                                   partials, heavy, n_heavy)
+static int launch_ref_stats(const int4* items, int64_t n_items, int64_t n_hub, int64_t n_long, const int* rowidx,
+                            const int* gidx, const ScoreArgs& sa, double* m, float* rl, float* mr, hipStream_t s) {
+  const int64_t waves = n_long + ceil_div(n_items - n_hub - n_long, (int64_t)NI);
+  const unsigned grid = (unsigned)(n_hub + ceil_div(waves, kRefWaves));
+#define GNPDE_RS(M)                                                                                             \
+  ref_stats_kernel<NI, M><<<grid, kRefBlock, 0, s>>>(items, (int)n_items, (int)n_hub, (int)n_long, rowidx, gidx, sa, \
+                                                      m, rl, mr)
   if (sa.H <= 1)
     GNPDE_RS(1);
   else if (sa.H <= 2)
@@ -439,7 +427,7 @@ static int launch_ref_stats(const int4* items, int64_t n_items, int64_t n_long, 
 
 template <bool REF, int OUT>
 static int launch_seg(const int4* items, int64_t n, const int* rowptr, const int* rowidx, const int* gidx, int gid,
-                      const ScoreArgs& sa, const Team& tm, float* w, double* m, float* rl, double* mr,
+                      const ScoreArgs& sa, const Team& tm, float* w, double* m, float* rl, float* mr,
                       double* partials, int4* heavy, int n_heavy, hipStream_t s) {
   if (n <= 0) return GNPDE_OK;
   seg_softmax_kernel<REF, OUT><<<(unsigned)ceil_div(n, kWavesPerBlock), kBlock, 0, s>>>(
@@ -514,12 +502,13 @@ int gnpde_seg_plan_build(const int32_t* rowptr, int64_t R, int32_t eb, int32_t* 
   return GNPDE_OK;
 }
 
-int gnpde_seg_softmax_f32(const int32_t* items, int64_t n_items, int64_t n_long_items, const int32_t* chunk_items,
+int gnpde_seg_softmax_f32(const int32_t* items, int64_t n_items, int64_t n_hub_items, int64_t n_long_items,
+                          const int32_t* chunk_items,
                           int64_t n_chunk_items, int32_t* heavy, int64_t n_heavy, const int32_t* rowptr,
                           const int32_t* rowidx,
                           const int32_t* gidx, int group_is_dst, int out_kind, int mode, int64_t heads, int64_t dk,
                           const double* cs, const float* q, const float* k, int64_t ldqk, float score_p0,
-                          float score_p1, float* w, double* m, float* rl, double* mr, double* partials,
+                          float score_p1, float* w, double* m, float* rl, float* mr, double* partials,
                           void* stream) {
   int rc = check_score_args(mode, heads, dk, cs, q, k);
   if (rc) return rc;
@@ -528,10 +517,11 @@ int gnpde_seg_softmax_f32(const int32_t* items, int64_t n_items, int64_t n_long_
   GNPDE_REQUIRE(!(mode == GNPDE_SCORE_REFERENCE && out_kind == 0), GNPDE_EUNSUPPORTED,
                 "seg_softmax: reference scores grouped by source are uniform");
   GNPDE_REQUIRE(n_items >= 0 && n_chunk_items >= 0 && n_heavy >= 0 && n_items + n_chunk_items < INT32_MAX &&
-                    n_long_items >= 0 && n_long_items <= n_items,
+                    n_hub_items >= 0 && n_long_items >= 0 && n_hub_items + n_long_items <= n_items,
                 GNPDE_EINVAL, "seg_softmax: bad item counts");
-  GNPDE_REQUIRE(n_long_items == 0 || (mode == GNPDE_SCORE_REFERENCE && out_kind == 1), GNPDE_EINVAL,
-                "seg_softmax: long items are for the reference statistics only");
+  GNPDE_REQUIRE(n_hub_items + n_long_items == 0 || (mode == GNPDE_SCORE_REFERENCE && out_kind == 1 && group_is_dst &&
+                                                    n_chunk_items == 0),
+                GNPDE_EINVAL, "seg_softmax: hub / long items are for the reference statistics (norm_idx 1) only");
   GNPDE_REQUIRE(gnpde_seg_block_edges(mode, heads, dk) > 0, GNPDE_EUNSUPPORTED,
                 "seg_softmax: per-edge scores need dk %% 4 == 0 and power-of-two dk/4, heads*dk/4 <= 64");
   if (n_items + n_chunk_items == 0) return GNPDE_OK;
@@ -564,9 +554,9 @@ int gnpde_seg_softmax_f32(const int32_t* items, int64_t n_items, int64_t n_long_
   const int64_t n_first = adjacent ? n_items + n_chunk_items : n_items;
   const int64_t n_second = adjacent ? 0 : n_chunk_items;
   if (ref && out_kind == 1 && n_chunk_items == 0 && group_is_dst) {
-    // the reference statistics of the attention RHS: long items, then short items NI per wave
-    return launch_ref_stats<kRefStatsNI>(it, n_items, n_long_items, rowidx, gidx, sa, m, rl, mr, partials, hv,
-                                         (int)n_heavy, s);
+    // the reference statistics of the attention RHS: hub groups, long groups, then short items
+    GNPDE_REQUIRE((uint64_t)n_items < (uint64_t)INT32_MAX / kRefWaves, GNPDE_EUNSUPPORTED, "seg_softmax: too many items");
+    return launch_ref_stats<kRefStatsNI>(it, n_items, n_hub_items, n_long_items, rowidx, gidx, sa, m, rl, mr, s);
   }
   if (out_kind == 0) {
     rc = GNPDE_SEG(false, kSegWeights, it, n_first);

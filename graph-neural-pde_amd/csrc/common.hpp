@@ -50,9 +50,10 @@ constexpr int kBlock = 256;        // 4 waves per workgroup
 constexpr int kWavesPerBlock = kBlock / kWave;
 constexpr float kSoftmaxEps = 1e-16f;  // utils.softmax denominator epsilon, src/utils.py:124-125
 // Packed statistics record of one softmax group (optional output of the
-// statistics kernels, read by the fused-weight K1 in one cache line per edge):
-// H doubles m[h], then H floats rl[h], padded to 16 bytes.
-__host__ __device__ constexpr int stats_record_doubles(int H) { return ((H + (H + 1) / 2) + 1) & ~1; }
+// statistics kernels, read by the fused-weight K1 with one load per edge):
+// H floats m[h] (the group max rounded to fp32; the sum is taken relative to
+// it), then H floats rl[h], padded to 16 bytes — 16 B for two heads.
+__host__ __device__ constexpr int stats_record_floats(int H) { return (2 * H + 3) & ~3; }
 
 // ------------------------------------------------------------------ vector loads
 template <int VEC>
@@ -268,6 +269,7 @@ struct EpiPre {
   Packed<VEC, T> x0r;
   Packed<VEC, T> base[NOUT];
   Packed<VEC, T> kv[NOUT][GNPDE_STAGE_MAX_K];
+  Packed<VEC, T> dw;  // the stage's dot operand (dot_rows)
 };
 
 template <int STG>
@@ -304,13 +306,15 @@ __device__ __forceinline__ void epi_prefetch(const Epi& e, int64_t row, int cc, 
         if (j < so.nk) load_packed<VEC>(as_t<T>(so.k[j]) + off, p.kv[i][j]);
     }
   }
+  if (e.st.dot_rows) load_packed<VEC>(as_t<T>(e.st.dot_with) + off, p.dw);
 }
 
 // f = a*(ax - x) [+ b*x0]  (function_laplacian_diffusion.py:69-77) or f = ax,
 // then either store f or emit the fused Runge-Kutta stage outputs.
 template <int VEC, int STG, class T = float>
 __device__ __forceinline__ void epi_finish(const Epi& e, int64_t row, int cc, const float (&ax)[VEC], float a,
-                                           float b, const EpiPre<VEC, T, stage_nout<STG>()>& p) {
+                                           float b, const EpiPre<VEC, T, stage_nout<STG>()>& p,
+                                           double* dpart = nullptr) {
   float o[VEC];
   const bool need_x = (e.flags & GNPDE_EPI_RHS) != 0;
   if (need_x) {
@@ -330,6 +334,10 @@ __device__ __forceinline__ void epi_finish(const Epi& e, int64_t row, int cc, co
   }
   const int64_t off = row * e.ldf + cc;
   if (e.st.f_out) store_vec<VEC>(as_t<T>(e.st.f_out) + off, o);
+  if (e.st.dot_rows && dpart) {
+#pragma unroll
+    for (int t = 0; t < VEC; ++t) *dpart = fma((double)o[t], (double)unpack(p.dw, t), *dpart);
+  }
   // the stage outputs' row (out_rows: the last step of a renumbered solve writes the caller's numbering)
   const int64_t oo = e.st.out_rows ? (int64_t)e.st.out_rows[row] * e.ldf + cc : off;
 #pragma unroll
@@ -362,10 +370,25 @@ __device__ __forceinline__ void epi_finish(const Epi& e, int64_t row, int cc, co
 
 template <int VEC, int STG, class T = float>
 __device__ __forceinline__ void epilogue_store(const Epi& e, int64_t row, int cc, const float (&ax)[VEC], float a,
-                                               float b) {
+                                               float b, double* dpart = nullptr) {
   EpiPre<VEC, T, stage_nout<STG>()> p;
   epi_prefetch<VEC, STG, T>(e, row, cc, p);
-  epi_finish<VEC, STG, T>(e, row, cc, ax, a, b, p);
+  epi_finish<VEC, STG, T>(e, row, cc, ax, a, b, p, dpart);
+}
+
+// The row's dot_rows term: the owner lanes' partials (lanes [base, base + GL) of
+// the wavefront, GL a power of two) summed by a fixed xor tree, stored by the
+// first of them.  Called by every lane of the wavefront (convergent).
+template <int GL>
+__device__ __forceinline__ void epi_dot_store(const Epi& e, int64_t row, double dpart, bool store) {
+  static_assert((GL & (GL - 1)) == 0, "dot_rows needs power-of-two row lanes");
+#pragma unroll
+  for (int o = 1; o < GL; o <<= 1) dpart += __shfl_xor(dpart, o);
+  if (store) {
+    double* d = e.st.dot_rows + row;
+    const double v = e.st.dot_coef * dpart;
+    *d = e.st.dot_accumulate ? *d + v : v;
+  }
 }
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }

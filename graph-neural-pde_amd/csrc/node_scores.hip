@@ -19,7 +19,7 @@ template <int MAXH, int GL>
 __global__ __launch_bounds__(256) void stats_kernel(const int4* __restrict__ items, int n_items,
                                                      const int* __restrict__ gidx, int group_is_dst, ScoreArgs sa,
                                                      double* __restrict__ m_out, float* __restrict__ rl_out,
-                                                     double* __restrict__ mr_out, double* __restrict__ partials) {
+                                                     float* __restrict__ mr_out, double* __restrict__ partials) {
   constexpr int G = kWave / GL;
   const int lane = threadIdx.x & 63;
   const int g = lane / GL, gl = lane % GL;
@@ -58,7 +58,7 @@ __global__ __launch_bounds__(256) void stats_kernel(const int4* __restrict__ ite
       partials[(int64_t)slot * 2 * H + h] = M[h];
       partials[(int64_t)slot * 2 * H + H + h] = (double)L[h];
     } else {
-      store_stats(m_out, rl_out, mr_out, grp, H, h, M[h], 1.0f / (L[h] + kSoftmaxEps));
+      store_stats(m_out, rl_out, mr_out, grp, H, h, M[h], L[h]);
     }
   }
 }
@@ -68,7 +68,7 @@ __global__ __launch_bounds__(256) void stats_kernel(const int4* __restrict__ ite
 __global__ __launch_bounds__(256) void stats_fixup_kernel(const int4* __restrict__ heavy, int n_heavy, int H,
                                                            const double* __restrict__ partials,
                                                            double* __restrict__ m_out, float* __restrict__ rl_out,
-                                                           double* __restrict__ mr_out) {
+                                                           float* __restrict__ mr_out) {
   const int wid = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
   if (wid >= n_heavy * H) return;
   const int i = wid / H, h = wid - i * H;
@@ -77,7 +77,7 @@ __global__ __launch_bounds__(256) void stats_fixup_kernel(const int4* __restrict
 }
 
 int launch_stats_fixup(const int4* heavy, int64_t n_heavy, int H, const double* partials, double* m, float* rl,
-                       double* mr, hipStream_t s) {
+                       float* mr, hipStream_t s) {
   if (n_heavy <= 0) return GNPDE_OK;
   const unsigned g2 = (unsigned)ceil_div(n_heavy * H, kWavesPerBlock);
   stats_fixup_kernel<<<g2, kBlock, 0, s>>>(heavy, (int)n_heavy, H, partials, m, rl, mr);
@@ -138,7 +138,7 @@ template <int VEC>
 __global__ __launch_bounds__(256) void stats_team_kernel(const int4* __restrict__ items, int n_items,
                                                           const int* __restrict__ gidx, int group_is_dst, ScoreArgs sa,
                                                           Team tm, double* __restrict__ m_out,
-                                                          float* __restrict__ rl_out, double* __restrict__ mr_out,
+                                                          float* __restrict__ rl_out, float* __restrict__ mr_out,
                                                           double* __restrict__ partials) {
   const int lane = threadIdx.x & 63;
   const int T = tm.T, S = tm.S, tpw = kWave / T;
@@ -181,7 +181,7 @@ __global__ __launch_bounds__(256) void stats_team_kernel(const int4* __restrict_
     partials[(int64_t)slot * 2 * H + h] = M;
     partials[(int64_t)slot * 2 * H + H + h] = (double)L;
   } else {
-    store_stats(m_out, rl_out, mr_out, grp, H, h, M, 1.0f / (L + kSoftmaxEps));
+    store_stats(m_out, rl_out, mr_out, grp, H, h, M, L);
   }
 }
 
@@ -598,6 +598,9 @@ __global__ __launch_bounds__(256) void node_scores_kernel(const float* __restric
 // forms U = Wq^T S / sqrt(dk) and v = bq . S / sqrt(dk) into LDS and streams its
 // rows with U[b] in registers.  One chunk per row (nch == 1), one batch element
 // per grid row (gridDim.y == B).
+constexpr int kNsfPre = 16;    // Wq values per U output held in registers (dk <= 16)
+constexpr int kNsfLoads = 32;  // tile shares in flight per thread
+
 template <int VEC, int GL, int MAXH, bool CLAMP>
 __global__ __launch_bounds__(256) void node_scores_fused_kernel(const float* __restrict__ x, int64_t N, int C,
                                                                  int64_t ldx, int H, const double* __restrict__ part,
@@ -620,7 +623,23 @@ __global__ __launch_bounds__(256) void node_scores_fused_kernel(const float* __r
   const float* __restrict__ xb = x + b * N * ldx;
   float xa[NP][VEC], xn[NP][VEC];
   ns_first_rows<VEC, GL, MAXH, CLAMP>(xb, n0, n1, C, ldx, g, gl, wv, xa, xn);
-  // S = sum over the tile shares
+  // this thread's operands of U (output (c, h) = (tid / MAXH, tid % MAXH); the v
+  // outputs c = Cp go to the first threads' second slot), loaded before S is known
+  const int dk = att / H;
+  const bool pre = dk <= kNsfPre && Cp * MAXH == kBlock;  // one U output per thread (+ v on the first MAXH)
+  float wq[2][kNsfPre];
+#pragma unroll
+  for (int o = 0; o < 2; ++o) {
+    const int t = o == 0 ? tid : Cp * MAXH + tid;
+    const int c = t / MAXH, h = t - c * MAXH;
+    const bool ok = pre && (o == 0 || tid < MAXH) && h < H && (c < C || c == Cp);
+#pragma unroll
+    for (int d = 0; d < kNsfPre; ++d) {
+      const int dd = h * dk + min(d, dk - 1);
+      wq[o][d] = (ok && d < dk) ? (c == Cp ? bq[dd] : Wq[(int64_t)dd * C + c]) : 0.f;
+    }
+  }
+  // S = sum over the tile shares: every share of the thread in flight at once
   const double* __restrict__ pb = part + b * (int64_t)ntiles * att;
   const int DW = min(att, kBlock), TG = kBlock / DW;
   const int tg = tid / DW, dl = tid - tg * DW;
@@ -628,12 +647,12 @@ __global__ __launch_bounds__(256) void node_scores_fused_kernel(const float* __r
     const int d = d0 + dl;
     double acc = 0.0;
     if (tg < TG && d < att) {
-      for (int t0 = tg; t0 < ntiles; t0 += kProjLoads * TG) {
-        double v[kProjLoads];
+      for (int t0 = tg; t0 < ntiles; t0 += kNsfLoads * TG) {
+        double v[kNsfLoads];
 #pragma unroll
-        for (int k = 0; k < kProjLoads; ++k) v[k] = pb[(int64_t)min(t0 + k * TG, ntiles - 1) * att + d];
+        for (int k = 0; k < kNsfLoads; ++k) v[k] = pb[(int64_t)min(t0 + k * TG, ntiles - 1) * att + d];
 #pragma unroll
-        for (int k = 0; k < kProjLoads; ++k)
+        for (int k = 0; k < kNsfLoads; ++k)
           if (t0 + k * TG < ntiles) acc += v[k];
       }
     }
@@ -647,18 +666,32 @@ __global__ __launch_bounds__(256) void node_scores_fused_kernel(const float* __r
     __syncthreads();
   }
   // U[c][h] (c < Cp; zero past C and H) and v[h] (row c = Cp)
-  const int dk = att / H;
   const double inv = 1.0 / sqrt((double)dk);
-  for (int t = tid; t < (Cp + 1) * MAXH; t += kBlock) {
-    const int c = t / MAXH, h = t - c * MAXH;
-    double a = 0.0;
-    if (h < H && (c < C || c == Cp)) {
-      const int d0 = h * dk;
-#pragma unroll 8
-      for (int d = 0; d < dk; ++d)
-        a = fma((double)(c == Cp ? bq[d0 + d] : Wq[(int64_t)(d0 + d) * C + c]), S[d0 + d], a);
+  if (pre) {
+#pragma unroll
+    for (int o = 0; o < 2; ++o) {
+      const int t = o == 0 ? tid : Cp * MAXH + tid;
+      if (t < (Cp + 1) * MAXH && (o == 0 || tid < MAXH)) {
+        const int c = t / MAXH, h = t - c * MAXH;
+        double a = 0.0;
+#pragma unroll
+        for (int d = 0; d < kNsfPre; ++d)
+          if (d < dk && h < H) a = fma((double)wq[o][d], S[h * dk + d], a);
+        U[t] = a * inv;
+      }
     }
-    U[t] = a * inv;
+  } else {
+    for (int t = tid; t < (Cp + 1) * MAXH; t += kBlock) {
+      const int c = t / MAXH, h = t - c * MAXH;
+      double a = 0.0;
+      if (h < H && (c < C || c == Cp)) {
+        const int d0 = h * dk;
+#pragma unroll 8
+        for (int d = 0; d < dk; ++d)
+          a = fma((double)(c == Cp ? bq[d0 + d] : Wq[(int64_t)(d0 + d) * C + c]), S[d0 + d], a);
+      }
+      U[t] = a * inv;
+    }
   }
   __syncthreads();
   const __amdgpu_buffer_rsrc_t rcs = buf_rsrc(cs + b * N * H);
@@ -705,7 +738,7 @@ static void keysum_geometry(int64_t C, const float* x, int64_t ldx, int* vec, in
 
 template <int MAXH>
 static void launch_stats(unsigned grid, int GL, hipStream_t s, const int4* it, int n, const int* gidx, int gid,
-                         const ScoreArgs& sa, double* m, float* rl, double* mr, double* partials) {
+                         const ScoreArgs& sa, double* m, float* rl, float* mr, double* partials) {
   if (GL == 8)
     stats_kernel<MAXH, 8><<<grid, kBlock, 0, s>>>(it, n, gidx, gid, sa, m, rl, mr, partials);
   else
@@ -861,7 +894,7 @@ extern "C" {
 int gnpde_softmax_stats_f32(const int32_t* items, int64_t n_items, const int32_t* heavy, int64_t n_heavy,
                             const int32_t* gidx, int group_is_dst, int mode, int64_t heads, int64_t dk,
                             const double* cs, const float* q, const float* k, int64_t ldqk, float score_p0,
-                            float score_p1, double* m, float* rl, double* mr, double* partials,
+                            float score_p1, double* m, float* rl, float* mr, double* partials,
                             void* stream) {
   int rc = check_score_args(mode, heads, dk, cs, q, k);
   if (rc) return rc;

@@ -60,6 +60,7 @@ int gnpde_spmm_rhs_bf16(const int32_t* items, int64_t n_items, int32_t* heavy, i
                         const uint16_t* x0, int64_t ldx0, const float* alpha, const float* beta, int flags, uint16_t* f,
                         int64_t ldf, float* partials, int64_t n_slots, const gnpde_stage_epilogue_t* stage,
                         void* stream) {
+  GNPDE_REQUIRE(!stage || !stage->dot_rows, GNPDE_EUNSUPPORTED, "spmm_rhs_bf16: stage dot terms are fp32 only");
   const Epi ep = make_epi(reinterpret_cast<const float*>(x), ldx, reinterpret_cast<const float*>(x0), ldx0, alpha,
                           beta, flags, reinterpret_cast<float*>(f), ldf, stage);
   int rc = check_epi(ep, C, n_heavy, partials, n_slots);
@@ -71,7 +72,7 @@ int gnpde_spmm_rhs_bf16(const int32_t* items, int64_t n_items, int32_t* heavy, i
 }
 
 int gnpde_attn_ref_rhs_f32(const int32_t* items, int64_t n_items, int32_t* heavy, int64_t n_heavy,
-                           const int32_t* col, const double* cs, const double* m, const float* rl, const double* mr,
+                           const int32_t* col, const double* cs, const double* m, const float* rl, const float* mr,
                            int64_t heads,
                            int64_t C, const float* x, int64_t ldx, const float* x0, int64_t ldx0, const float* alpha,
                            const float* beta, int flags, float* f, int64_t ldf, float* partials, int64_t n_slots,
@@ -87,18 +88,18 @@ int gnpde_attn_ref_rhs_f32(const int32_t* items, int64_t n_items, int32_t* heavy
   if (mr) {
     GNPDE_REQUIRE(heads == 2 && aligned16(mr), GNPDE_EUNSUPPORTED,
                   "attn_ref_rhs: packed statistics records are read for two heads, 16-byte aligned");
-    RefDstSoftmaxWeights<2, true, true> wp{cs, mr, nullptr, 2};
+    RefDstSoftmaxWeights<2, true, true> wp{cs, nullptr, nullptr, 2, mr};
     return launch_agg(items, n_items, heavy, n_heavy, col, wp, C, ep, partials, as_stream(stream));
   }
   if (heads == 2 && aligned16(m) && aligned8(rl)) {
-    RefDstSoftmaxWeights<2, true> wp{cs, m, rl, 2};
+    RefDstSoftmaxWeights<2, true> wp{cs, m, rl, 2, nullptr};
     return launch_agg(items, n_items, heavy, n_heavy, col, wp, C, ep, partials, as_stream(stream));
   }
   if (heads <= 2) {
-    RefDstSoftmaxWeights<2> wp{cs, m, rl, (int)heads};
+    RefDstSoftmaxWeights<2> wp{cs, m, rl, (int)heads, nullptr};
     return launch_agg(items, n_items, heavy, n_heavy, col, wp, C, ep, partials, as_stream(stream));
   }
-  RefDstSoftmaxWeights<0> wp{cs, m, rl, (int)heads};
+  RefDstSoftmaxWeights<0> wp{cs, m, rl, (int)heads, nullptr};
   return launch_agg(items, n_items, heavy, n_heavy, col, wp, C, ep, partials, as_stream(stream));
 }
 

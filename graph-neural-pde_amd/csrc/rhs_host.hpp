@@ -78,6 +78,7 @@ inline int check_epi(const Epi& e, int64_t C, int64_t n_heavy, const void* parti
       for (int j = 0; j < e.st.o[i].nk; ++j)
         GNPDE_REQUIRE(e.st.o[i].k[j] != nullptr, GNPDE_EINVAL, "rhs: stage output %d k[%d] is NULL", i, j);
     }
+    GNPDE_REQUIRE(!e.st.dot_rows || e.st.dot_with, GNPDE_EINVAL, "rhs: stage dot_rows without dot_with");
   }
   GNPDE_REQUIRE(e.ldx >= C && e.ldf >= C, GNPDE_EINVAL, "rhs: leading dimension < C");
   if (e.flags & GNPDE_EPI_RHS) GNPDE_REQUIRE(e.alpha != nullptr, GNPDE_EINVAL, "rhs: NULL alpha");

@@ -107,20 +107,29 @@ __device__ __forceinline__ int wave_max_int(int v) {
 // Merge of long group g's chunk statistics for head h (chunks first .. first+nch-1
 // of partials: [slot][M(H) | L(H)]): lanes take strided chunks, then a fixed xor
 // tree, so the result does not depend on which wave or launch runs it.
-__device__ __forceinline__ void store_stats(double* __restrict__ m, float* __restrict__ rl, double* __restrict__ mr,
-                                            int64_t g, int H, int h, double M, float r) {
-  if (m) m[g * H + h] = M;
+// The stored max is M rounded to fp32 (exact in the fp64 m array and in the
+// float records alike) and rl = 1/(sum exp(s - m) + 1e-16) is taken relative to
+// that rounded max: L (the sum relative to M) times exp(M - m).  Any shift gives
+// the same softmax; this one makes the 16-byte two-head record hold exactly the
+// values of the separate arrays.
+__device__ __forceinline__ void store_stats(double* __restrict__ m, float* __restrict__ rl, float* __restrict__ mr,
+                                            int64_t g, int H, int h, double M, float L) {
+  const float m32 = (float)M;
+  const double d = M - (double)m32;
+  const float Lr = (d == 0.0 || !isfinite(d)) ? L : L * expf((float)d);
+  const float r = 1.0f / (Lr + kSoftmaxEps);
+  if (m) m[g * H + h] = (double)m32;
   if (rl) rl[g * H + h] = r;
   if (mr) {
-    double* rec = mr + g * stats_record_doubles(H);
-    rec[h] = M;
-    reinterpret_cast<float*>(rec + H)[h] = r;
+    float* rec = mr + g * stats_record_floats(H);
+    rec[h] = m32;
+    rec[H + h] = r;
   }
 }
 
 __device__ __forceinline__ void stats_merge_store(int g, int first, int nch, int H, int h,
                                                   const double* __restrict__ partials, double* __restrict__ m_out,
-                                                  float* __restrict__ rl_out, double* __restrict__ mr_out) {
+                                                  float* __restrict__ rl_out, float* __restrict__ mr_out) {
   const int lane = threadIdx.x & 63;
   double M = -INFINITY;
   float L = 0.f;
@@ -132,11 +141,11 @@ __device__ __forceinline__ void stats_merge_store(int g, int first, int nch, int
     const float L2 = __shfl_xor(L, o);
     online_merge(M, L, M2, L2);
   }
-  if (lane == 0) store_stats(m_out, rl_out, mr_out, g, H, h, M, 1.0f / (L + kSoftmaxEps));
+  if (lane == 0) store_stats(m_out, rl_out, mr_out, g, H, h, M, L);
 }
 
 int launch_stats_fixup(const int4* heavy, int64_t n_heavy, int H, const double* partials, double* m, float* rl,
-                       double* mr, hipStream_t s);
+                       float* mr, hipStream_t s);
 
 struct ScoreArgs {
   int mode;

@@ -92,6 +92,26 @@ __global__ __launch_bounds__(256) void dot_final_kernel(const double* __restrict
   if (threadIdx.x == 0) *out = t;
 }
 
+// sum of n doubles: the same fixed grid and per-block tree as dot_partial_kernel
+__global__ __launch_bounds__(256) void sum_partial_kernel(int64_t n, const double* __restrict__ v,
+                                                           double* __restrict__ part) {
+  __shared__ double red[kBlock / kWave];
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  double acc = 0.0;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride) acc += v[i];
+  const double t = block_sum_f64(acc, red);
+  if (threadIdx.x == 0) part[blockIdx.x] = t;
+}
+
+__global__ __launch_bounds__(256) void sum_final_kernel(const double* __restrict__ part, int nb, double* out,
+                                                         int accumulate) {
+  __shared__ double red[kBlock / kWave];
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < nb; i += blockDim.x) acc += part[i];
+  const double t = block_sum_f64(acc, red);
+  if (threadIdx.x == 0) *out = accumulate ? *out + t : t;
+}
+
 // Entry of a solve: dst[k] = src[order[k]] (and dst_copy[order[k]] = the same row)
 // in 16-byte pieces, one thread per piece, consecutive threads along a row.
 template <bool ORDER, bool COPY>
@@ -140,6 +160,19 @@ extern "C" int gnpde_rows_copy(const void* src, int64_t rows, int64_t row_bytes,
 }
 
 extern "C" size_t gnpde_dot_workspace_bytes(void) { return sizeof(double) * kDotBlocks; }
+
+extern "C" int gnpde_sum_f64(int64_t n, const double* v, double* out, int accumulate, void* workspace,
+                             size_t workspace_bytes, void* stream) {
+  GNPDE_REQUIRE(n >= 0 && (v || n == 0) && out && workspace, GNPDE_EINVAL, "sum_f64: NULL pointer or bad n");
+  GNPDE_REQUIRE(workspace_bytes >= gnpde_dot_workspace_bytes(), GNPDE_EINVAL, "sum_f64: workspace too small");
+  hipStream_t s = as_stream(stream);
+  double* part = static_cast<double*>(workspace);
+  sum_partial_kernel<<<kDotBlocks, kBlock, 0, s>>>(n, v, part);
+  GNPDE_LAUNCH_CHECK();
+  sum_final_kernel<<<1, kBlock, 0, s>>>(part, kDotBlocks, out, accumulate);
+  GNPDE_LAUNCH_CHECK();
+  return GNPDE_OK;
+}
 
 extern "C" int gnpde_dot_f64(int64_t n, const float* a, const float* b, double* out, void* workspace,
                              size_t workspace_bytes, void* stream) {

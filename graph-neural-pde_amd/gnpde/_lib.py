@@ -26,7 +26,8 @@ class StageOut(ctypes.Structure):
 class StageEpilogue(ctypes.Structure):
     """gnpde_stage_epilogue_t (include/gnpde.h)."""
     _fields_ = [("f_out", ctypes.c_void_p), ("n_out", ctypes.c_int), ("o", StageOut * STAGE_MAX_OUT),
-                ("out_rows", ctypes.c_void_p)]
+                ("out_rows", ctypes.c_void_p), ("dot_with", ctypes.c_void_p), ("dot_rows", ctypes.c_void_p),
+                ("dot_coef", ctypes.c_double), ("dot_accumulate", ctypes.c_int)]
 
 
 c_i32p = ctypes.POINTER(ctypes.c_int32)
@@ -75,7 +76,8 @@ SIGNATURES = {
     "gnpde_seg_block_edges": (_int, [_int, _i64, _i64]),
     "gnpde_seg_plan_build": (_int, [_vp, _i64, ctypes.c_int32, _vp, _i64, _vp, _i64, _vp, _i64, c_i64p, c_i64p,
                                     c_i64p]),
-    "gnpde_seg_softmax_f32": (_int, [_vp, _i64, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _int, _int, _int, _i64, _i64,
+    "gnpde_seg_softmax_f32": (_int, [_vp, _i64, _i64, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _int, _int, _int, _i64,
+                                     _i64,
                                      _vp, _vp, _vp, _i64, _f32, _f32, _vp, _vp, _vp, _vp, _vp, _vp]),
     "gnpde_csr_rowidx": (_int, [_vp, _i64, _i64, _vp, _vp]),
     "gnpde_sddmm_f32": (_int, [_vp, _vp, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _vp, _int, _int, _vp, _vp]),
@@ -88,6 +90,7 @@ SIGNATURES = {
     "gnpde_rk_combine_f32": (_int, [_i64, _vp, _int, ctypes.POINTER(_vp), ctypes.POINTER(_f64), _f64, _vp, _vp]),
     "gnpde_dot_workspace_bytes": (_size, []),
     "gnpde_dot_f64": (_int, [_i64, _vp, _vp, _vp, _vp, _size, _vp]),
+    "gnpde_sum_f64": (_int, [_i64, _vp, _vp, _int, _vp, _size, _vp]),
     "gnpde_self_loops_workspace_bytes": (_size, [_i64, _i64, _i64]),
     "gnpde_self_loops_count": (_int, [_vp, _i64, _i64, c_i64p, _vp, _size, _vp]),
     "gnpde_add_self_loops": (_int, [_vp, _vp, _i64, _i64, _i64, _f32, _i64, _vp, _vp, _vp, _size, _vp]),

@@ -175,10 +175,12 @@ class SegPlan(_TicketOrder):
     covering groups of more than eb edges in eb-edge chunks, ``heavy`` {group,
     first_slot, n_chunks, 0} per long group."""
 
-    def __init__(self, eb, items, n_items, chunk_items, n_chunk, heavy, n_heavy, n_long=0):
+    def __init__(self, eb, items, n_items, chunk_items, n_chunk, heavy, n_heavy, n_hub=0, n_long=0):
         self.eb = eb
         self.items, self.n_items = items, n_items
-        self.n_long = n_long  # long items at the front of ``items`` (reference statistics)
+        # reference statistics: hub items (one workgroup each), then long items (one
+        # wavefront each) at the front of ``items``
+        self.n_hub, self.n_long = n_hub, n_long
         self.chunk_items, self.n_chunk = chunk_items, n_chunk
         self.heavy, self.n_heavy = heavy, n_heavy
         self.n_slots = n_chunk
@@ -192,10 +194,11 @@ def seg_long_max():
 
 def build_seg_plan(rowptr, eb, long_items=False):
     """gnpde_seg_plan_build on a host copy of rowptr (once per graph and block size).
-    long_items=True: every group longer than eb becomes one item {e_begin,
-    e_end, -2, group} when it has at most seg_long_max() edges, else chunk items
-    of that many edges {.., -3 - slot, group} merged inside the launch (heavy
-    {group, first_slot, n_chunks, 0}); long items come first, longest first."""
+    long_items=True (the reference statistics over the CSC): every group longer
+    than eb becomes one item — {e_begin, e_end, -4, group} (a HUB, one workgroup)
+    when it has more than seg_long_max() edges, else {e_begin, e_end, -2, group}
+    (LONG, one wavefront); hubs first, then long items, each longest first, then
+    the packed short items.  No chunks, no heavy table."""
     rp = np.ascontiguousarray(rowptr.cpu().numpy().astype(np.int32))
     R = rp.shape[0] - 1
     nnz = int(rp[-1])
@@ -216,24 +219,13 @@ def build_seg_plan(rowptr, eb, long_items=False):
         rows = heavy[:nh.value, 0].astype(np.int64)
         s0, s1 = rp[rows].astype(np.int64), rp[rows + 1].astype(np.int64)
         order = np.argsort(-(s1 - s0), kind="stable")
-        out, hv, slot = [], [], 0
-        for i in order:
-            r, a, b = int(rows[i]), int(s0[i]), int(s1[i])
-            if b - a <= long_max:
-                out.append((a, b, -2, r))
-                continue
-            nch = (b - a + long_max - 1) // long_max
-            hv.append((r, slot, nch, 0))
-            for c in range(nch):
-                out.append((a + c * long_max, min(b, a + (c + 1) * long_max), -3 - slot, r))
-                slot += 1
-        long_arr = np.asarray(out, np.int32).reshape(-1, 4)
-        all_items = np.concatenate([long_arr, items[:ni.value]], 0)
-        hv_arr = np.asarray(hv, np.int32).reshape(-1, 4) if hv else np.zeros((1, 4), np.int32)
-        plan = SegPlan(eb, dev32(all_items, all_items.shape[0]), all_items.shape[0], dev32(np.zeros((1, 4), np.int32), 0),
-                       0, dev32(hv_arr, len(hv)), len(hv), n_long=long_arr.shape[0])
-        plan.n_slots = slot
-        return plan
+        hubs = [(int(s0[i]), int(s1[i]), -4, int(rows[i])) for i in order if s1[i] - s0[i] > long_max]
+        longs = [(int(s0[i]), int(s1[i]), -2, int(rows[i])) for i in order if s1[i] - s0[i] <= long_max]
+        front = np.asarray(hubs + longs, np.int32).reshape(-1, 4)
+        all_items = np.concatenate([front, items[:ni.value]], 0)
+        return SegPlan(eb, dev32(all_items, all_items.shape[0]), all_items.shape[0],
+                       dev32(np.zeros((1, 4), np.int32), 0), 0, dev32(np.zeros((1, 4), np.int32), 0), 0,
+                       n_hub=len(hubs), n_long=len(longs))
 
     # items and chunk items back to back in one buffer: K2 then covers both in one launch
     both = dev32(np.concatenate([items[:ni.value], chunks[:max(nc.value, 1)]], 0), ni.value + max(nc.value, 1))
@@ -520,13 +512,17 @@ class Stage(object):
     ``base`` may be None, the RHS input x, or ``out`` itself (in place).  No
     output may alias the RHS input."""
 
-    def __init__(self, f_out=None, outs=(), out_rows=None):
+    def __init__(self, f_out=None, outs=(), out_rows=None, dot=None):
         self.f_out = f_out
         self.outs = list(outs)
         self.out_rows = out_rows  # int32 [R] or None: row r's ``outs`` stores go to row out_rows[r]
+        # (y, rows, coef, accumulate) or None: rows[r] (+)= coef * <f[r], y[r]> in fp64 (fp32 state)
+        self.dot = dot
 
     def tensors(self):
         ts = [self.f_out] if self.f_out is not None else []
+        if self.dot is not None:
+            ts.append(self.dot[0])
         for out, base, _cb, _cf, ks in self.outs:
             ts.append(out)
             if base is not None:
@@ -549,6 +545,13 @@ class Stage(object):
             if self.out_rows.numel() * x_input.shape[-1] != x_input.numel():
                 raise ValueError("out_rows must hold one row index per RHS row")
             st.out_rows = self.out_rows.data_ptr()
+        if self.dot is not None:
+            y, rows, coef, accumulate = self.dot
+            _require_gpu(rows, "dot rows", torch.float64)
+            if rows.numel() * x_input.shape[-1] != x_input.numel() or shift:
+                raise ValueError("dot rows must hold one fp64 per RHS row")
+            st.dot_with, st.dot_rows = y.data_ptr(), rows.data_ptr()
+            st.dot_coef, st.dot_accumulate = float(coef), int(bool(accumulate))
         for i, (out, base, cb, cf, ks) in enumerate(self.outs):
             if len(ks) > _lib.STAGE_MAX_K:
                 raise ValueError("at most %d k terms per stage output" % _lib.STAGE_MAX_K)
@@ -638,7 +641,7 @@ class RefDstWeights(object):
     """Weights K1 computes on the fly (gnpde_attn_ref_rhs_f32): the fork's
     scaled_dot under destination-grouped softmax, head-mean per edge from the
     node scores cs [R,h] and the CSC statistics m [R,h], rl [R,h] or their
-    packed records mr [R, stats_record_doubles(h)] (two heads)."""
+    packed records mr [R, stats_record_floats(h)] fp32 (two heads)."""
 
     def __init__(self, cs, m, rl, heads, mr=None):
         self.cs, self.m, self.rl, self.heads, self.mr = cs, m, rl, int(heads), mr
@@ -771,9 +774,9 @@ def uniform_scores(heads):
     return NodeScores(_lib.SCORE_UNIFORM, heads, 1)
 
 
-def stats_record_doubles(heads):
-    """Doubles per packed statistics record (include/gnpde.h GNPDE_STATS_RECORD_DOUBLES)."""
-    return ((heads + (heads + 1) // 2) + 1) & ~1
+def stats_record_floats(heads):
+    """Floats per packed statistics record (include/gnpde.h GNPDE_STATS_RECORD_FLOATS)."""
+    return (2 * heads + 3) & ~3
 
 
 def _seg_call(g, ns, norm_idx, out_kind, packed=False):
@@ -789,19 +792,19 @@ def _seg_call(g, ns, norm_idx, out_kind, packed=False):
     if ns.q is not None and (ns.ldqk % 4 or ns.q.data_ptr() % 16 or ns.k.data_ptr() % 16):
         return NotImplemented
     grouped = g.csr if norm_idx == 0 else g.csc
-    plan = grouped.seg_plan(eb, long_items=ns.mode == _lib.SCORE_REFERENCE and out_kind == 1)
+    plan = grouped.seg_plan(eb, long_items=ns.mode == _lib.SCORE_REFERENCE and out_kind == 1 and norm_idx == 1)
     dev = grouped.col.device
     H = ns.heads
     packed = packed and out_kind == 1
     need_stats = not packed and (out_kind == 1 or plan.n_chunk > 0)
     m = torch.empty(g.R, H, dtype=torch.float64, device=dev) if need_stats else None
     rl = torch.empty(g.R, H, dtype=torch.float32, device=dev) if need_stats else None
-    mr = torch.empty(g.R, stats_record_doubles(H), dtype=torch.float64, device=dev) if packed else None
+    mr = torch.empty(g.R, stats_record_floats(H), dtype=torch.float32, device=dev) if packed else None
     partials = torch.empty(plan.n_slots * 2 * H, dtype=torch.float64, device=dev) if plan.n_slots else None
     w = torch.empty(max(g.nnz, 1), dtype=torch.float32, device=dev) if out_kind == 0 else None
-    plan.order_launch(dev)  # long groups merged in-launch keep arrival tickets in plan.heavy
-    rc = _lib.call_rc("gnpde_seg_softmax_f32", _ptr(plan.items), plan.n_items, plan.n_long, _ptr(plan.chunk_items),
-                      plan.n_chunk,
+    plan.order_launch(dev)  # chunked plans' statistics fixups read partials written by this launch
+    rc = _lib.call_rc("gnpde_seg_softmax_f32", _ptr(plan.items), plan.n_items, plan.n_hub, plan.n_long,
+                      _ptr(plan.chunk_items), plan.n_chunk,
                       _ptr(plan.heavy), plan.n_heavy, _ptr(grouped.rowptr), _ptr(grouped.rowidx), _ptr(grouped.col),
                       int(norm_idx == 1), out_kind, ns.mode, H, ns.dk, _ptr(ns.cs), _ptr(ns.q), _ptr(ns.k), ns.ldqk,
                       ns.p0, ns.p1, _ptr(w), _ptr(m), _ptr(rl), _ptr(mr), _ptr(partials), _stream(dev))
@@ -818,7 +821,7 @@ def softmax_stats(g, ns, norm_idx, seg=True, packed=False):
     (utils.softmax, src/utils.py:116-127).  seg=True: the edge-block kernel K2;
     shapes outside it (and seg=False) use the per-group kernels
     (gnpde_softmax_stats_f32).  packed=True returns (None, None, mr): the same
-    statistics as packed records [R, stats_record_doubles(h)] only (the form
+    statistics as packed records [R, stats_record_floats(h)] fp32 only (the form
     the fused-weight K1 reads in one cache line per edge)."""
     if seg:
         r = _seg_call(g, ns, norm_idx, 1, packed=packed)
@@ -830,7 +833,7 @@ def softmax_stats(g, ns, norm_idx, seg=True, packed=False):
     H = ns.heads
     m = None if packed else torch.empty(g.R, H, dtype=torch.float64, device=dev)
     rl = None if packed else torch.empty(g.R, H, dtype=torch.float32, device=dev)
-    mr = torch.empty(g.R, stats_record_doubles(H), dtype=torch.float64, device=dev) if packed else None
+    mr = torch.empty(g.R, stats_record_floats(H), dtype=torch.float32, device=dev) if packed else None
     partials = torch.empty(plan.n_slots * 2 * H, dtype=torch.float64, device=dev) if plan.n_slots else None
     _lib.call("gnpde_softmax_stats_f32", _ptr(plan.items), plan.n_items, _ptr(plan.heavy), plan.n_heavy,
               _ptr(grouped.col), int(norm_idx == 1), ns.mode, H, ns.dk, _ptr(ns.cs), _ptr(ns.q), _ptr(ns.k), ns.ldqk,
@@ -940,6 +943,20 @@ def dot(a, b):
     nbytes = _lib.fn("gnpde_dot_workspace_bytes")()
     ws = torch.empty(nbytes, dtype=torch.uint8, device=a.device)
     _lib.call("gnpde_dot_f64", a.numel(), _ptr(a), _ptr(b), _ptr(out), _ptr(ws), nbytes, _stream(a.device))
+    return out
+
+
+def sum_f64(v, out=None, accumulate=False):
+    """sum of an fp64 device vector (gnpde_sum_f64, fixed order) into a 0-d fp64
+    tensor (added to ``out`` with accumulate=True)."""
+    _require_gpu(v, "v", torch.float64)
+    v = v.contiguous()
+    if out is None:
+        out = torch.zeros((), dtype=torch.float64, device=v.device)
+    nbytes = _lib.fn("gnpde_dot_workspace_bytes")()
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=v.device)
+    _lib.call("gnpde_sum_f64", v.numel(), _ptr(v), _ptr(out), int(bool(accumulate)), _ptr(ws), nbytes,
+              _stream(v.device))
     return out
 
 

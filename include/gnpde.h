@@ -177,7 +177,12 @@ size_t gnpde_plan_workspace_bytes(int64_t R);
  * out_rows (NULL = identity): the o[i].out stores of row r go to row
  * out_rows[r] instead (base, k and f_out stay at row r) — the last step of a
  * solve run in a renumbered node order writes its result straight into the
- * caller's numbering (gnpde.integrator); it must be a permutation of [0, R).  */
+ * caller's numbering (gnpde.integrator); it must be a permutation of [0, R).
+ * dot_rows (NULL = none; fp32 state, power-of-two lanes per row): per row,
+ *   dot_rows[r] (+)= dot_coef * sum_c f[r,c] * dot_with[r,c]   (fp64; "+=" when
+ * dot_accumulate), summed over the row's lanes in a fixed order — the per-row
+ * terms of a parameter gradient <f, y> that the caller reduces once
+ * (gnpde_sum_f64), instead of a separate pass re-reading f.                    */
 #define GNPDE_STAGE_MAX_OUT 2
 #define GNPDE_STAGE_MAX_K 2
 typedef struct {
@@ -195,6 +200,10 @@ typedef struct {
   int n_out;
   gnpde_stage_out_t o[GNPDE_STAGE_MAX_OUT];
   const int32_t* out_rows;
+  const float* dot_with;
+  double* dot_rows;
+  double dot_coef;
+  int dot_accumulate;
 } gnpde_stage_epilogue_t;
 
 /* ---------------------------------------------------------------- K1: SpMM RHS
@@ -238,14 +247,16 @@ int gnpde_spmm_rhs_bf16(const int32_t* items, int64_t n_items, int32_t* heavy, i
  * scores (gnpde_ref_scores_f32), m [R,H] fp64 / rl [R,H] group statistics
  * (gnpde_softmax_stats_f32 / gnpde_seg_softmax_f32 over the CSC), or, when
  * mr is given (heads == 2, 16-byte aligned), the packed statistics records
- * those kernels write into mr (GNPDE_STATS_RECORD_DOUBLES(heads) doubles per
- * group: m[0..h-1], then rl[0..h-1] as floats): one cache line per edge.
+ * those kernels write into mr (GNPDE_STATS_RECORD_FLOATS(heads) floats per
+ * group: m[0..h-1], then rl[0..h-1]): one 16-byte load per edge.  Every
+ * statistics kernel stores the group max rounded to fp32 (exact in both forms)
+ * and the sum relative to it, so both forms hold the same values.
  * Equals gnpde_attn_weights_f32 + gnpde_spmm_rhs_f32 bit for bit, in one pass:
  * ODEFuncTransformerAtt.forward, function_transformer_attention.py:44-59.
  * Other arguments as gnpde_spmm_rhs_f32.                                     */
-#define GNPDE_STATS_RECORD_DOUBLES(h) ((((h) + ((h) + 1) / 2) + 1) & ~1)
+#define GNPDE_STATS_RECORD_FLOATS(h) ((2 * (h) + 3) & ~3)
 int gnpde_attn_ref_rhs_f32(const int32_t* items, int64_t n_items, int32_t* heavy, int64_t n_heavy,
-                           const int32_t* col, const double* cs, const double* m, const float* rl, const double* mr,
+                           const int32_t* col, const double* cs, const double* m, const float* rl, const float* mr,
                            int64_t heads,
                            int64_t C, const float* x, int64_t ldx, const float* x0, int64_t ldx0, const float* alpha,
                            const float* beta, int flags, float* f, int64_t ldf, float* partials, int64_t n_slots,
@@ -279,7 +290,7 @@ int gnpde_ref_scores_f32(const float* x, int64_t B, int64_t N, int64_t C, int64_
 /* Destination- or source-grouped softmax statistics over a grouped CSR
  * (items from gnpde_plan_build over the CSC for norm_idx=1, the CSR for
  * norm_idx=0; gidx = the OTHER endpoint of each edge):
- * m[g,h] = max_e s_e,h (fp64), rl[g,h] = 1/(sum_e exp(s_e,h - m) + 1e-16).
+ * m[g,h] = max_e s_e,h rounded to fp32 (stored as fp64), rl[g,h] = 1/(sum_e exp(s_e,h - m) + 1e-16).
  * partials: 2*heads doubles per plan slot.
  * Edge scores by `mode` from cs (REFERENCE) or q/k (per-edge modes).
  * Groups of 8 lanes per item: plan it with a small chunk (e.g. 64).
@@ -290,7 +301,7 @@ int gnpde_softmax_stats_f32(const int32_t* items, int64_t n_items, const int32_t
                             const int32_t* gidx, int group_is_dst, int mode, int64_t heads, int64_t dk,
                             const double* cs, const float* q, const float* k, int64_t ldqk,
                             float score_p0, float score_p1,
-                            double* m, float* rl, double* mr, double* partials, void* stream);
+                            double* m, float* rl, float* mr, double* partials, void* stream);
 
 /* Head-mean attention weights in aggregation-CSR order (edge-parallel):
  *   w[p] = (1/h) sum_h exp(s_p,h - m[g,h]) * rl[g,h],  g = src (norm_idx 0) or dst (1)
@@ -311,15 +322,13 @@ int gnpde_attn_weights_f32(const int32_t* rowidx, const int32_t* col, int64_t nn
  * (packed greedily up to EB edges); chunk_items {e_begin, e_end, slot, group}
  * split groups of degree > EB, heavy {group, first_slot, n_chunks, 0} lists
  * those groups (partials: 2*heads doubles per slot; m/rl scratch).
- * Reference scores with out_kind 1 also take LONG items inside `items`:
- * {e_begin, e_end, -2, group} = a whole group of at most gnpde_seg_long_edges()
- * edges, and {e_begin, e_end, -3 - slot, group} = a chunk of that many edges of a
- * longer group whose
- * partials the last-arriving chunk merges inside the launch (agent-scope ticket
- * in heavy[].w: zero on entry, left zero; launches on one heavy array must not
- * overlap); heavy then lists those groups, and no fixup runs.  The long items
- * come first in `items`: n_long_items of them (0 for other plans); the rest are
- * whole-group items, taken two per wavefront when grouped by destination.
+ * Reference scores with out_kind 1 over the CSC (norm_idx 1) also take, at the
+ * front of `items`, n_hub_items HUB items {e_begin, e_end, -4, group} (a group of
+ * more than gnpde_seg_long_edges() edges, one 1024-thread workgroup each) and
+ * then n_long_items LONG items {e_begin, e_end, -2, group} (a whole group of at
+ * most gnpde_seg_long_edges() edges, one wavefront each); the rest are
+ * whole-group items, taken two per wavefront.  No chunks, no partials, no
+ * tickets: launches may overlap.  (n_hub_items = n_long_items = 0 for other plans.)
  * gnpde_seg_plan_build builds them from a HOST copy of rowptr into HOST
  * arrays (plain C++, once per graph; capacities: items >= R, chunk_items >=
  * nnz/eb + R, heavy >= nnz/eb + 1).  When chunk_items == items + 4*n_items
@@ -340,12 +349,13 @@ int gnpde_seg_long_edges(void);
 int gnpde_seg_plan_build(const int32_t* rowptr, int64_t R, int32_t eb, int32_t* items, int64_t items_capacity,
                          int32_t* chunk_items, int64_t chunks_capacity, int32_t* heavy, int64_t heavy_capacity,
                          int64_t* n_items, int64_t* n_chunks, int64_t* n_heavy);
-int gnpde_seg_softmax_f32(const int32_t* items, int64_t n_items, int64_t n_long_items, const int32_t* chunk_items,
+int gnpde_seg_softmax_f32(const int32_t* items, int64_t n_items, int64_t n_hub_items, int64_t n_long_items,
+                          const int32_t* chunk_items,
                           int64_t n_chunk_items, int32_t* heavy, int64_t n_heavy, const int32_t* rowptr,
                           const int32_t* rowidx,
                           const int32_t* gidx, int group_is_dst, int out_kind, int mode, int64_t heads, int64_t dk,
                           const double* cs, const float* q, const float* k, int64_t ldqk,
-                          float score_p0, float score_p1, float* w, double* m, float* rl, double* mr,
+                          float score_p0, float score_p1, float* w, double* m, float* rl, float* mr,
                           double* partials, void* stream);
 
 /* Per-edge, per-head attention in COO order (the [B,E,h] `attention` that
@@ -378,6 +388,11 @@ int gnpde_rows_copy(const void* src, int64_t rows, int64_t row_bytes, const int6
  * function_laplacian_diffusion.py:69-76).  Fixed reduction order (deterministic);
  * two launches; workspace: gnpde_dot_workspace_bytes().                      */
 size_t gnpde_dot_workspace_bytes(void);
+/* *out (+)= sum_i v[i] for n fp64 values (the per-row terms of the stage
+ * epilogue's dot_rows), fixed order; accumulate: add to *out instead of storing.
+ * Workspace gnpde_dot_workspace_bytes().                                      */
+int gnpde_sum_f64(int64_t n, const double* v, double* out, int accumulate, void* workspace, size_t workspace_bytes,
+                  void* stream);
 int gnpde_dot_f64(int64_t n, const float* a, const float* b, double* out, void* workspace, size_t workspace_bytes,
                   void* stream);
 

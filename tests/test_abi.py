@@ -114,9 +114,12 @@ def test_stage_struct_layout_matches_header():
     # gnpde_stage_out_t: out, base (8 B each), cb, cf, nk (4 B each), k[2] (8 B, aligned), c[2]
     assert ctypes.sizeof(_lib.StageOut) == 8 + 8 + 4 + 4 + 4 + 4 + 16 + 8
     assert _lib.StageOut.k.offset == 32
-    # gnpde_stage_epilogue_t: f_out, n_out (padded to 8), o[2], out_rows
-    assert ctypes.sizeof(_lib.StageEpilogue) == 8 + 8 + 2 * ctypes.sizeof(_lib.StageOut) + 8
-    assert _lib.StageEpilogue.out_rows.offset == 16 + 2 * ctypes.sizeof(_lib.StageOut)
+    # gnpde_stage_epilogue_t: f_out, n_out (padded to 8), o[2], out_rows, dot_with, dot_rows, dot_coef,
+    # dot_accumulate (padded to 8)
+    so = ctypes.sizeof(_lib.StageOut)
+    assert ctypes.sizeof(_lib.StageEpilogue) == 8 + 8 + 2 * so + 8 + 8 + 8 + 8 + 8
+    assert _lib.StageEpilogue.out_rows.offset == 16 + 2 * so
+    assert _lib.StageEpilogue.dot_coef.offset == 16 + 2 * so + 24
 
 
 def test_workspace_size_queries():
@@ -138,14 +141,16 @@ def test_c_header_struct_layout_with_gcc(tmp_path):
         pytest.skip("gcc not available")
     src = tmp_path / "layout.c"
     src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "gnpde.h"\nint main(void){'
-                   'printf("%zu %zu %zu %zu %zu\\n", sizeof(gnpde_stage_out_t), offsetof(gnpde_stage_out_t, k),'
+                   'printf("%zu %zu %zu %zu %zu %zu %zu\\n", sizeof(gnpde_stage_out_t), offsetof(gnpde_stage_out_t, k),'
                    'offsetof(gnpde_stage_out_t, c), sizeof(gnpde_stage_epilogue_t),'
-                   'offsetof(gnpde_stage_epilogue_t, out_rows));return 0;}\n')
+                   'offsetof(gnpde_stage_epilogue_t, out_rows), offsetof(gnpde_stage_epilogue_t, dot_coef),'
+                   'offsetof(gnpde_stage_epilogue_t, dot_accumulate));return 0;}\n')
     exe = tmp_path / "layout"
     subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
     got = [int(v) for v in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()]
     assert got == [ctypes.sizeof(_lib.StageOut), _lib.StageOut.k.offset, _lib.StageOut.c.offset,
-                   ctypes.sizeof(_lib.StageEpilogue), _lib.StageEpilogue.out_rows.offset]
+                   ctypes.sizeof(_lib.StageEpilogue), _lib.StageEpilogue.out_rows.offset,
+                   _lib.StageEpilogue.dot_coef.offset, _lib.StageEpilogue.dot_accumulate.offset]
 
 
 def test_stale_library_is_refused(monkeypatch):
