@@ -138,7 +138,7 @@ __device__ __forceinline__ void hub_combine(int row, int first, int nch, int C, 
       for (int t = 0; t < VEC; ++t) s[t] += __shfl_xor(s[t], o);
     if (g == 0 && live) epilogue_store<VEC, STG, T>(ep, row, cc, s, a, b, &dpart);
   }
-  if constexpr (STG > 0 && sizeof(T) == 4)
+  if constexpr (STG >= 2 && sizeof(T) == 4)
     if (ep.st.dot_rows) epi_dot_store<GL>(ep, row, dpart, lane == 0);  // wave-uniform
 }
 
@@ -375,7 +375,7 @@ __global__ __launch_bounds__(256) void agg_kernel(const int4* __restrict__ items
     }
   }
   // the row's owner lanes (g == 0: lanes [rs*SL, rs*SL + GL)) are all here
-  if constexpr (STG > 0 && sizeof(T) == 4 && (GL & (GL - 1)) == 0)
+  if constexpr (STG >= 2 && sizeof(T) == 4 && (GL & (GL - 1)) == 0)
     if (ep.st.dot_rows) epi_dot_store<GL>(ep, row, dpart, gl == 0);
 }
 
@@ -405,8 +405,10 @@ static int launch_agg_cfg(const int4* items, int64_t n_items, int4* heavy, int64
   bool inlaunch = true;
   if constexpr (GNPDE_EXPERIMENTS) inlaunch = hub_inlaunch();
   const int nh = inlaunch ? (int)n_heavy : 0;
-  // single-output stages (every gnpde.integrator step) get the leaner instantiation
-  const int stg = ep.has_stage ? (ep.st.n_out <= 1 ? 1 : 2) : 0;
+  // single-output stages without dot terms (every forward gnpde.integrator step) get the
+  // leaner instantiation: 56-60 VGPRs, 8 waves per SIMD; the dot terms of the adjoint
+  // stages alone cost the general one 40+ VGPRs (fused rk4 K1 92.9 -> 107 us at 4 waves)
+  const int stg = epi_stage_kind(ep);
   if (n_items > 0) {
     if (stg == 1)
       agg_kernel<VEC, GL, NCH, U, RPW, 1, WP, T><<<grid, kBlock, 0, s>>>(items, (int)n_items, heavy, nh, col, wp, C, ep,

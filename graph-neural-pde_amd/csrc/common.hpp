@@ -306,7 +306,8 @@ __device__ __forceinline__ void epi_prefetch(const Epi& e, int64_t row, int cc, 
         if (j < so.nk) load_packed<VEC>(as_t<T>(so.k[j]) + off, p.kv[i][j]);
     }
   }
-  if (e.st.dot_rows) load_packed<VEC>(as_t<T>(e.st.dot_with) + off, p.dw);
+  if constexpr (STG >= 2)  // dot terms (the adjoint stages) only in the general instantiation
+    if (e.st.dot_rows) load_packed<VEC>(as_t<T>(e.st.dot_with) + off, p.dw);
 }
 
 // f = a*(ax - x) [+ b*x0]  (function_laplacian_diffusion.py:69-77) or f = ax,
@@ -334,9 +335,11 @@ __device__ __forceinline__ void epi_finish(const Epi& e, int64_t row, int cc, co
   }
   const int64_t off = row * e.ldf + cc;
   if (e.st.f_out) store_vec<VEC>(as_t<T>(e.st.f_out) + off, o);
-  if (e.st.dot_rows && dpart) {
+  if constexpr (STG >= 2) {
+    if (e.st.dot_rows && dpart) {
 #pragma unroll
-    for (int t = 0; t < VEC; ++t) *dpart = fma((double)o[t], (double)unpack(p.dw, t), *dpart);
+      for (int t = 0; t < VEC; ++t) *dpart = fma((double)o[t], (double)unpack(p.dw, t), *dpart);
+    }
   }
   // the stage outputs' row (out_rows: the last step of a renumbered solve writes the caller's numbering)
   const int64_t oo = e.st.out_rows ? (int64_t)e.st.out_rows[row] * e.ldf + cc : off;
@@ -392,6 +395,13 @@ __device__ __forceinline__ void epi_dot_store(const Epi& e, int64_t row, double 
 }
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// The STG instantiation an epilogue needs: 0 = store f, 1 = one stage output
+// and no dot term (the forward Runge-Kutta steps), 2 = the general epilogue.
+inline int epi_stage_kind(const Epi& e) {
+  if (!e.has_stage) return 0;
+  return (e.st.n_out <= 1 && !e.st.dot_rows) ? 1 : 2;
+}
 
 // ------------------------------------------------------------------ buffer memory ops
 // Raw buffer loads/stores take a 32-bit byte offset from a wave-uniform base,

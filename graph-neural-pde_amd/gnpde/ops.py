@@ -877,9 +877,64 @@ def attn_rhs(g, ns, m, rl, norm_idx, x, x0=None, alpha=None, beta=None, rhs=True
         w = RefDstWeights(ns.cs, m, rl, ns.heads, mr=mr)
         return spmm_rhs(g, w, x, x0=x0, alpha=alpha, beta=beta, rhs=rhs, alpha_sigmoid=alpha_sigmoid,
                         add_source=add_source, out=out, stage=stage)
+    if fuse and norm_idx == 0 and ns.mode == _lib.SCORE_DOT and x.dtype == torch.float32:
+        r = attn_dot_rhs(g, ns, x, x0=x0, alpha=alpha, beta=beta, rhs=rhs, alpha_sigmoid=alpha_sigmoid,
+                         add_source=add_source, out=out, stage=stage)
+        if r is not NotImplemented:
+            return r
     w = attn_weights(g, ns, m, rl, norm_idx, seg=seg)
     return spmm_rhs(g, w, x, x0=x0, alpha=alpha, beta=beta, rhs=rhs, alpha_sigmoid=alpha_sigmoid,
                     add_source=add_source, out=out, stage=stage)
+
+
+def attn_dot_rhs(g, ns, x, x0=None, alpha=None, beta=None, rhs=True, alpha_sigmoid=True, add_source=False,
+                 out=None, stage=None):
+    """The per-edge scaled_dot RHS under source-grouped softmax (norm_idx 0) in
+    one online-softmax aggregation pass (gnpde_attn_dot_rhs_f32, csrc/flash.hip):
+    no [nnz] weights, no separate softmax launch.  NotImplemented for shapes
+    outside the fused kernel (gnpde_attn_dot_supported)."""
+    xr = _rows(x, "x")
+    C = xr.shape[1]
+    H, dk = ns.heads, ns.dk
+    if not _lib.fn("gnpde_attn_dot_supported")(H, dk, C):
+        return NotImplemented
+    if ns.ldqk % 4 or ns.q.data_ptr() % 16 or ns.k.data_ptr() % 16 or xr.data_ptr() % 16:
+        return NotImplemented
+    if xr.shape[0] != g.R:
+        raise ValueError("x has %d rows, graph has %d" % (xr.shape[0], g.R))
+    dev = xr.device
+    a = _scalar(alpha, "alpha", dev) if rhs else None
+    if rhs and a is None:
+        raise ValueError("attn_dot_rhs: alpha required")
+    b = _scalar(beta, "beta", dev) if add_source else None
+    x0r = _rows(x0, "x0") if add_source else None
+    if x0r is not None and x0r.data_ptr() % 16:
+        return NotImplemented
+    st = None
+    if stage is not None:
+        for t in stage.tensors():
+            _require_gpu(t, "stage tensor", torch.float32)
+            if not t.is_contiguous() or t.numel() != xr.numel():
+                raise ValueError("stage tensors must be contiguous and shaped like x")
+        st = ctypes.byref(stage.struct(xr))
+    elif out is None:
+        out = torch.empty_like(xr)
+    plan = g.csr.plan
+    ps = int(_lib.fn("gnpde_attn_dot_partial_floats")(H, C))
+    partials = None
+    if plan.n_slots:
+        if plan.n_slots * ps * 4 >= _PARTIALS_MAX_BYTES:
+            return NotImplemented
+        partials = torch.empty(plan.n_slots * ps, dtype=torch.float32, device=dev)
+    plan.order_launch(dev)
+    rc = _lib.call_rc("gnpde_attn_dot_rhs_f32", _ptr(plan.items), plan.n_items, _ptr(plan.heavy), plan.n_heavy,
+                      _ptr(g.csr.col), _ptr(ns.q), _ptr(ns.k), ns.ldqk, H, dk, C, _ptr(xr), C, _ptr(x0r), C, _ptr(a),
+                      _ptr(b), _flags(rhs, alpha_sigmoid, add_source), _ptr(out), C, _ptr(partials), plan.n_slots, st,
+                      _stream(dev))
+    if rc == _lib.EUNSUPPORTED:
+        return NotImplemented
+    _lib.check(rc, "gnpde_attn_dot_rhs_f32")
+    return None if stage is not None else out.view(x.shape)
 
 
 def edge_attention(g, ns, m, rl, norm_idx):
