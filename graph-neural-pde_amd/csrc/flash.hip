@@ -1,38 +1,44 @@
 // flash.hip — the per-edge scaled_dot attention RHS under source-grouped
 // softmax (attention_norm_idx 0, upstream GRAND's default transformer RHS) as
-// ONE aggregation pass: the softmax group of an edge is its source, which is
-// the row the aggregation sums into, so each wavefront row slot scores the
-// edges it gathers and keeps an online (running max, rescaled sum) softmax per
-// head while it accumulates (the flash-attention recurrence on a graph row).
-// No [nnz] weight array, no separate softmax launch.  Reference:
+// ONE aggregation pass over the CSR plan: the softmax group of an edge is its
+// source, i.e. the row the aggregation sums into, so each row slot scores the
+// edges it is about to gather, forms the group statistics itself and then runs
+// K1's gather loop with the finished weights.  No [nnz] weight array, no
+// separate softmax launch over the edges.  Reference:
 //   SpGraphTransAttentionLayer.forward  src/function_transformer_attention.py:218-266
-//     (q = Q x, k = K x, prods = q_src . k_dst / sqrt(dk) — upstream's per-edge score)
+//     (q = Q x, k = K x, prods = q_src . k_dst / sqrt(dk) — upstream GRAND's per-edge score)
 //   utils.softmax (groups = edge_index[0])  src/utils.py:116-127
 //   multiply_attention (head mean, A x)     src/function_transformer_attention.py:33-41
 //   ODEFuncTransformerAtt.forward            :44-59 (f = a (A x - x) [+ b x0])
 //
-// Per row r with edges e -> c_e, head h:
+// Per row r with edges e -> c_e, head h (scores in log2 units, s * log2(e)):
 //   s_e,h = q_r,h . k_c,h / sqrt(dk)
-//   M_h = max_e s_e,h,  L_h = sum_e exp(s_e,h - M_h),  acc_h = sum_e exp(s_e,h - M_h) x_c
-//   ax_r = (1/H) sum_h acc_h / (L_h + 1e-16)
-// which is sum_e w_e x_c with the reference's w_e = mean_h softmax_e,h.  The
-// running (M, L, acc) of a row slot are rescaled by exp(M_old - M_new) once per
-// batch of U edges.  Scores and exponentials use base 2 (s * log2(e) and
-// v_exp_f32), 1-2 ulp from expf.
+//   M_h = max_e s_e,h,  L_h = sum_e exp(s_e,h - M_h)
+//   w_e = (1/H) sum_h exp(s_e,h - M_h) / (L_h + 1e-16)        (utils.softmax + head mean)
+//   ax_r = sum_e w_e x_c
 //
-// Lane layout (row slots of GL = 16 / 32 / 64 lanes, C <= 4 GL, 4 floats per lane
-// as in K1): the q . k product of an edge is formed in every 16-lane DPP row of
-// the slot — lane l of a row holds q / k elements [4 (l mod att/4), +4) — and
-// reduced over the dk/4 lanes of a head by quad permutes and row mirrors; each
-// head's score then reaches the whole row by a row_newbcast.  The k slice of an
-// edge is loaded with the same column index as its x row, so both gathers are in
-// flight together (one memory round trip per batch, as K1).
+// Work item = K1's plan item (a row of at most `chunk` edges, or a chunk of a
+// hub row), RPW rows per wavefront, SL = 64/RPW lanes per row; the item's
+// edges go in batches of SL, lane l of the slot owning edge e0 + l:
+//   pass 1: the lane scores its own edge — the k row of its destination (att
+//           floats, 16-byte loads) against the row's q (staged once per slot in
+//           LDS, read back as broadcasts) — and the slot folds the batch into a
+//           running (M_h, L_h) by xor trees (fixed order);
+//   pass 2: each lane turns its edge's scores into the weight w_e (kept in
+//           registers for an item of one batch, recomputed from k otherwise)
+//           and K1's gather loop aggregates x with it (U edges in flight), the
+//           RHS / Runge-Kutta epilogue fused as in K1.
+// A lane scoring a whole edge costs att FMAs per edge against ~10 VALU per edge
+// and head for a slot-cooperative score (the first version of this kernel,
+// 158 us on G-arxiv against 86 us for K1, was VALU-bound that way).
 //
-// Hub rows (more than `chunk` edges) are split into chunk items as in K1; a
-// chunk stores its running state (acc_h, M_h, L_h) write-through to its slot
-// and takes an arrival ticket on the hub's plan entry; the last chunk merges
-// the slots in fixed order (deterministic, no float atomics) and runs the
-// epilogue.
+// Hub rows (more than `chunk` edges, split into chunk items, as in K1): a chunk
+// forms its own statistics and per-head unnormalised sums, which the last chunk
+// of the row to arrive merges with the rescaling of the online softmax
+// (dot_hub_combine; arrival tickets on the plan's heavy entries, fixed merge
+// order).  A wavefront holding a chunk accumulates per head for all its rows.
+// (A one-workgroup-per-hub statistics pre-pass launched first, so that chunks
+// weight with final statistics and merge like K1's, measured 17 us on G-arxiv.)
 #include "aggregate.hpp"
 #include "rhs_host.hpp"
 
@@ -40,102 +46,183 @@ namespace gnpde {
 
 constexpr float kLog2e = 1.4426950408889634f;
 
-template <int CTRL>
-__device__ __forceinline__ float dpp_mov(float v) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xf, 0xf, false));
-}
-
-// sum over the S = dk/4 lanes of a head (S in {1, 2, 4, 8, 16}, aligned inside a 16-lane row)
-__device__ __forceinline__ float head_reduce(float v, int S) {
-  if (S >= 2) v += dpp_mov<0xB1>(v);   // quad_perm [1,0,3,2]
-  if (S >= 4) v += dpp_mov<0x4E>(v);   // quad_perm [2,3,0,1]
-  if (S >= 8) v += dpp_mov<0x141>(v);  // row_half_mirror
-  if (S >= 16) v += dpp_mov<0x140>(v); // row_mirror
-  return v;
-}
-
-// lane l of a 16-lane row: score of head h (lanes [h S, (h+1) S) of the row) to every lane of the row
-template <int MAXH>
-__device__ __forceinline__ void heads_bcast(float v, int S, float (&s)[MAXH]) {
-#define GNPDE_NB(H)                                                  \
-  if constexpr (MAXH > H) {                                          \
-    if (S == 1) s[H] = dpp_mov<0x150 + H>(v);                        \
-    else if (S == 2) s[H] = dpp_mov<0x150 + ((2 * H) & 15)>(v);      \
-    else if (S == 4) s[H] = dpp_mov<0x150 + ((4 * H) & 15)>(v);      \
-    else if (S == 8) s[H] = dpp_mov<0x150 + ((8 * H) & 15)>(v);      \
-    else s[H] = v;                                                   \
-  }
-  GNPDE_NB(0)
-  GNPDE_NB(1)
-  GNPDE_NB(2)
-  GNPDE_NB(3)
-#undef GNPDE_NB
-}
+// A/B knobs of variant builds (make variant VFLAGS=...; the product build uses the defaults)
+#ifndef GNPDE_FL_PREFETCH
+#define GNPDE_FL_PREFETCH 0  // batch 0's first U gathers issued before pass 1 (195 against 176 us: registers)
+#endif
+#ifndef GNPDE_FL_TILEU
+#define GNPDE_FL_TILEU 4     // score-tile load instructions in flight
+#endif
+#ifndef GNPDE_FL_U
+#define GNPDE_FL_U 4         // edges in flight per row in the gather loop
+#endif
+#ifndef GNPDE_FL_DIAG
+#define GNPDE_FL_DIAG 0      // diagnostics only (wrong results): 1 no pass 1, 2 no pass-2 rescoring, 3 no slot reductions
+#endif
+#ifndef GNPDE_FL_DPPRED
+#define GNPDE_FL_DPPRED 1    // slot max / sum by DPP inside 16-lane rows (+ one swizzle per further row)
+#endif
+#ifndef GNPDE_FL_WAVES
+#define GNPDE_FL_WAVES 0     // amdgpu_waves_per_eu floor of the aggregation kernel (0: none)
+#endif
 
 struct DotArgs {
   const float* __restrict__ q;  // [R, ldqk]: q_r at q + r*ldqk, att = H*dk floats
   const float* __restrict__ k;
   int64_t ldqk;
-  int H, S;       // heads, lanes per head (dk / 4)
-  int qlanes;     // att / 4: lanes of a row holding distinct slices
-  float scale;    // log2(e) / sqrt(dk)
-  int ps;         // floats per partial slot: H*C acc, then M[H], L[H] (rounded up to 4)
+  float scale;                  // log2(e) / sqrt(dk)
 };
 
-__device__ __forceinline__ int64_t slice_off(const DotArgs& da, int lane) {
-  return (int64_t)((lane & 15) % da.qlanes) * 4;
+// sum over the S = dk/4 lanes of a head (S in {1, 2, 4, 8, 16}, aligned inside a 16-lane row)
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xf, 0xf, false));
+}
+template <int S>
+__device__ __forceinline__ float head_reduce(float v) {
+  if constexpr (S >= 2) v += dpp_mov<0xB1>(v);   // quad_perm [1,0,3,2]
+  if constexpr (S >= 4) v += dpp_mov<0x4E>(v);   // quad_perm [2,3,0,1]
+  if constexpr (S >= 8) v += dpp_mov<0x141>(v);  // row_half_mirror
+  if constexpr (S >= 16) v += dpp_mov<0x140>(v); // row_mirror
+  return v;
 }
 
-// Merge the chunk slots of hub row `row` (first .. first+nch-1) and run the
-// epilogue: per head M = max of the chunk maxima, then acc and L scaled by
-// exp(M_c - M), summed in chunk order.  Lanes cover the columns (C <= 256).
-template <int MAXH, int STG>
-__device__ __forceinline__ void flash_hub_combine(int row, int first, int nch, int C, const DotArgs& da,
-                                                  const Epi& ep, const float* __restrict__ partials) {
+// Scores of n <= SL edges (destinations mc of lanes [base, base + n)) against
+// one row's q, in score tiles: NA = att/4 lanes per edge, each holding one
+// 16-byte slice of q (qv) and loading the same slice of its edge's k row, so one
+// load instruction covers SL/NA whole k rows (whole cache lines, no lane
+// re-reading a line another load already touched); the dk/4 lanes of a head
+// sum by DPP, and the head's first lane writes the score to the slot's LDS
+// scores sc[e][h].  kTileU instructions' loads are in flight together.
+constexpr int kTileU = GNPDE_FL_TILEU;
+
+template <int SL, int NA, int S, int H>
+__device__ __forceinline__ void tile_scores(const float (&qv)[4], int mc, int n, int base, int sl, const DotArgs& da,
+                                            float* __restrict__ sc) {
+  constexpr int EPI = SL / NA;  // edges per load instruction
+  const int sub = sl % NA, eo = sl / NA;
+  for (int i0 = 0; i0 < n; i0 += EPI * kTileU) {
+    float4 kv[kTileU];
+#pragma unroll
+    for (int u = 0; u < kTileU; ++u) {
+      const int e = i0 + u * EPI + eo;
+      const int c = __shfl(mc, base + (e < SL ? e : 0));
+      kv[u] = e < n ? *reinterpret_cast<const float4*>(da.k + (int64_t)c * da.ldqk + 4 * sub)
+                    : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < kTileU; ++u) {
+      const int e = i0 + u * EPI + eo;
+      float d = qv[0] * kv[u].x;
+      d = fmaf(qv[1], kv[u].y, d);
+      d = fmaf(qv[2], kv[u].z, d);
+      d = fmaf(qv[3], kv[u].w, d);
+      d = head_reduce<S>(d) * da.scale;  // DPP inside the NA-lane group
+      if (e < n && sub % S == 0) sc[e * H + sub / S] = d;
+    }
+  }
+}
+
+// the lane's own edge's scores back from the slot's LDS tile (-inf past n)
+template <int H>
+__device__ __forceinline__ void own_scores(const float* __restrict__ sc, int sl, int n, float (&s)[H]) {
+#pragma unroll
+  for (int h = 0; h < H; ++h) s[h] = sl < n ? sc[sl * H + h] : -INFINITY;
+}
+
+// xor trees over the SL lanes of a row slot (SL a power of two, slots aligned)
+template <int SL>
+__device__ __forceinline__ float slot_max(float v) {
+  if constexpr (GNPDE_FL_DPPRED) {
+    v = fmaxf(v, dpp_mov<0xB1>(v));
+    v = fmaxf(v, dpp_mov<0x4E>(v));
+    v = fmaxf(v, dpp_mov<0x141>(v));
+    v = fmaxf(v, dpp_mov<0x140>(v));
+#pragma unroll
+    for (int o = 16; o < SL; o <<= 1) v = fmaxf(v, __shfl_xor(v, o));
+    return v;
+  }
+#pragma unroll
+  for (int o = 1; o < SL; o <<= 1) v = fmaxf(v, __shfl_xor(v, o));
+  return v;
+}
+template <int SL>
+__device__ __forceinline__ float slot_sum(float v) {
+  if constexpr (GNPDE_FL_DPPRED) {
+    v += dpp_mov<0xB1>(v);
+    v += dpp_mov<0x4E>(v);
+    v += dpp_mov<0x141>(v);
+    v += dpp_mov<0x140>(v);
+#pragma unroll
+    for (int o = 16; o < SL; o <<= 1) v += __shfl_xor(v, o);
+    return v;
+  }
+#pragma unroll
+  for (int o = 1; o < SL; o <<= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// the edge weight from its scores and the group statistics (M, Rl = 1/(L + eps))
+template <int H>
+__device__ __forceinline__ float edge_weight(const float (&s)[H], const float (&M)[H], const float (&Rl)[H]) {
+  float w = 0.f;
+#pragma unroll
+  for (int h = 0; h < H; ++h) w = fmaf(__builtin_amdgcn_exp2f(s[h] - M[h]), Rl[h], w);
+  constexpr float inv_h = 1.0f / (float)H;
+  return w * inv_h;
+}
+
+// ------------------------------------------------------------------ hub rows
+// A chunk of a hub row keeps its own statistics: per head the chunk max M_c,
+// sum L_c and the unnormalised sum acc_c = sum_e exp(s_e - M_c) x_e, stored
+// write-through in its partial slot ([H][C] acc, then M[H], L[H]; ps floats).
+// The last chunk to arrive merges the slots in chunk order:
+//   M = max_c M_c,  L = sum_c L_c 2^(M_c - M),  acc = sum_c acc_c 2^(M_c - M)
+// and runs the epilogue with ax = (1/H) sum_h acc_h / (L_h + 1e-16).  Lanes cover
+// the columns (C <= 256: 4 per lane).
+__host__ __device__ constexpr int64_t dot_partial_floats(int64_t H, int64_t C) { return (H * C + 2 * H + 3) & ~3; }
+
+template <int H, int STG>
+__device__ __forceinline__ void dot_hub_combine(int row, int first, int nch, int C, int ps, const Epi& ep,
+                                                const float* __restrict__ partials) {
   const int lane = threadIdx.x & 63;
   const int cc = lane * 4;
   const bool live = cc < C;
-  const int H = da.H;
-  float M[MAXH], L[MAXH], acc[MAXH][4];
+  float M[H], L[H], acc[H][4];
 #pragma unroll
-  for (int h = 0; h < MAXH; ++h) {
+  for (int h = 0; h < H; ++h) {
     M[h] = -INFINITY;
     L[h] = 0.f;
 #pragma unroll
     for (int t = 0; t < 4; ++t) acc[h][t] = 0.f;
   }
   for (int c = 0; c < nch; ++c) {
-    const float* p = partials + (int64_t)(first + c) * da.ps;
+    const float* p = partials + (int64_t)(first + c) * ps;
 #pragma unroll
-    for (int h = 0; h < MAXH; ++h)
-      if (h < H) M[h] = fmaxf(M[h], p[H * C + h]);
+    for (int h = 0; h < H; ++h) M[h] = fmaxf(M[h], p[H * C + h]);
   }
   for (int c = 0; c < nch; ++c) {
-    const float* p = partials + (int64_t)(first + c) * da.ps;
+    const float* p = partials + (int64_t)(first + c) * ps;
 #pragma unroll
-    for (int h = 0; h < MAXH; ++h) {
-      if (h < H) {
-        const float f = __builtin_amdgcn_exp2f(p[H * C + h] - M[h]);
-        L[h] = fmaf(p[H * C + H + h], f, L[h]);
-        if (live) {
-          float v[4];
-          load_vec<4>(p + h * C + cc, v);
+    for (int h = 0; h < H; ++h) {
+      const float f = __builtin_amdgcn_exp2f(p[H * C + h] - M[h]);
+      L[h] = fmaf(p[H * C + H + h], f, L[h]);
+      if (live) {
+        float v[4];
+        load_vec<4>(p + h * C + cc, v);
 #pragma unroll
-          for (int t = 0; t < 4; ++t) acc[h][t] = fmaf(v[t], f, acc[h][t]);
-        }
+        for (int t = 0; t < 4; ++t) acc[h][t] = fmaf(v[t], f, acc[h][t]);
       }
     }
   }
   float ax[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int h = 0; h < MAXH; ++h) {
-    if (h < H) {
-      const float r = 1.0f / (L[h] + kSoftmaxEps);
+  for (int h = 0; h < H; ++h) {
+    const float r = 1.0f / (L[h] + kSoftmaxEps);
 #pragma unroll
-      for (int t = 0; t < 4; ++t) ax[t] = fmaf(acc[h][t], r, ax[t]);
-    }
+    for (int t = 0; t < 4; ++t) ax[t] = fmaf(acc[h][t], r, ax[t]);
   }
-  const float inv_h = 1.0f / (float)H;
+  constexpr float inv_h = 1.0f / (float)H;
 #pragma unroll
   for (int t = 0; t < 4; ++t) ax[t] *= inv_h;
   const float a = (ep.flags & GNPDE_EPI_RHS) ? epi_alpha(ep) : 1.f;
@@ -146,215 +233,260 @@ __device__ __forceinline__ void flash_hub_combine(int row, int first, int nch, i
     if (ep.st.dot_rows) epi_dot_store<64>(ep, row, dpart, lane == 0);  // every lane of the wave (convergent)
 }
 
-template <int GL, int U, int MAXH, int STG>
-__global__ __launch_bounds__(256) void flash_agg_kernel(const int4* __restrict__ items, int n_items, int4* heavy,
-                                                         int n_heavy, const int* __restrict__ col, DotArgs da, int C,
-                                                         Epi ep, float* __restrict__ partials) {
+// ------------------------------------------------------------------ the fused attention RHS
+template <int GL, int U, int NA, int S, int H, int STG>
+__global__ __launch_bounds__(256)
+#if GNPDE_FL_WAVES
+__attribute__((amdgpu_waves_per_eu(GNPDE_FL_WAVES)))
+#endif
+void dot_agg_kernel(const int4* __restrict__ items, int n_items, int4* heavy, int n_heavy,
+                    const int* __restrict__ col, DotArgs da, int C, Epi ep, float* __restrict__ partials) {
   constexpr int RPW = kWave / GL;
   constexpr int SL = GL;
-  const int lane = threadIdx.x & 63;
-  const int rs = lane / SL, gl = lane % SL;
-  const int wid = uniform(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
+  __shared__ float scs[kWavesPerBlock][RPW][SL * H];  // each slot's batch scores
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int rs = lane / SL, sl = lane % SL;
+  const int wid = uniform(blockIdx.x * kWavesPerBlock + wv);
   const int item = wid * RPW + rs;
   if (wid * RPW >= n_items) return;
   const bool live = item < n_items;
   const int4 it = live ? items[item] : make_int4(0, 0, 0, -1);
   const int row = it.x, beg = it.y, end = it.z, slot = it.w;
-  const int cc = gl * 4;
-  const bool colv = cc < C;
-  const int H = da.H;
+  const int cc = sl * 4;
+  const bool owner = live && slot < 0 && cc < C;
+  const bool chunk = live && slot >= 0;
+  const int base = rs * SL;
+  float* sc = scs[wv][rs];
+  // a wavefront holding a hub chunk accumulates per head (its statistics are the chunk's own)
+  int wchunk = 0;
+  if (n_heavy > 0) {
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) wchunk |= __shfl((int)chunk, r * SL);
+  }
+  wchunk = uniform(wchunk);
 
   EpiPre<4, float, stage_nout<STG>()> pre;
-  if (live && slot < 0 && colv) epi_prefetch<4, STG, float>(ep, row, cc, pre);
-  const int64_t ko = slice_off(da, lane);
-  float qv[4];
-  load_vec<4>(da.q + (int64_t)row * da.ldqk + ko, qv);
+  if (owner) epi_prefetch<4, STG, float>(ep, row, cc, pre);
+  float qv[4];  // this lane's slice of the row's q (score tiles)
+  load_vec<4>(da.q + (int64_t)row * da.ldqk + 4 * (sl % NA), qv);
 
-  float M[MAXH], L[MAXH], acc[MAXH][4];
+  const int len = end - beg;
+  const int mc0 = sl < len ? col[beg + sl] : 0;
+  // batch 0's first U gathers issued before pass 1 (A/B knob; off: the registers cost more)
+  float xv0[U][4];
 #pragma unroll
-  for (int h = 0; h < MAXH; ++h) {
+  for (int u = 0; u < (GNPDE_FL_PREFETCH ? U : 0); ++u) {
+    const int c = __shfl(mc0, base + (u < len ? u : 0));
+    if (u < len && cc < C) {
+      load_vec<4>(ep.x + (int64_t)c * ep.ldx + cc, xv0[u]);
+    } else {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) xv0[u][t] = 0.f;
+    }
+  }
+  float M[H], L[H], Rl[H];
+  float s1[H];  // the lane's scores of batch 0 (kept for pass 2)
+#pragma unroll
+  for (int h = 0; h < H; ++h) {
     M[h] = -INFINITY;
     L[h] = 0.f;
-#pragma unroll
-    for (int t = 0; t < 4; ++t) acc[h][t] = 0.f;
   }
+  // pass 1: the statistics of the item's edges, batch by batch
+  for (int e0 = 0; e0 < (GNPDE_FL_DIAG == 1 ? 0 : len); e0 += SL) {
+    const int n = min(SL, len - e0);
+    const int mc = e0 == 0 ? mc0 : (sl < n ? col[beg + e0 + sl] : 0);
+    tile_scores<SL, NA, S, H>(qv, mc, n, base, sl, da, sc);
+    float s[H];
+    own_scores<H>(sc, sl, n, s);
+    if (e0 == 0) {
+#pragma unroll
+      for (int h = 0; h < H; ++h) s1[h] = s[h];
+    }
+    if (GNPDE_FL_DIAG == 3) break;
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+      const float mb = slot_max<SL>(s[h]);  // inside the slot (slot-uniform control flow)
+      const float mn = fmaxf(M[h], mb);
+      const float lb = slot_sum<SL>(__builtin_amdgcn_exp2f(s[h] - mn));  // s = -inf -> 0
+      L[h] = fmaf(L[h], __builtin_amdgcn_exp2f(M[h] - mn), lb);
+      M[h] = mn;
+    }
+  }
+#pragma unroll
+  for (int h = 0; h < H; ++h) Rl[h] = 1.0f / (L[h] + kSoftmaxEps);
 
-  // every lane runs the loop the same number of times (the DPP steps need the
-  // whole row): the slot with the longest item sets the trip count
-  int len = end - beg;
-  int nmax = len;
+  // pass 2: K1's gather loop; one finished weight per edge, or (a wavefront with a
+  // hub chunk) one unnormalised weight per edge and head
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  float acch[H][4];
 #pragma unroll
-  for (int o = SL; o < kWave; o <<= 1) nmax = max(nmax, __shfl_xor(nmax, o));
-  for (int e0 = 0; e0 < nmax; e0 += SL) {
-    const int n = min(SL, len - e0);  // may be <= 0 for a short slot
-    int mc = 0;
-    if (gl < n) mc = col[beg + e0 + gl];
-    const int nn = min(SL, nmax - e0);
-    for (int j = 0; j < nn; j += U) {
-      float xv[U][4], kv[U][4];
+  for (int h = 0; h < H; ++h)
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int jj = j + u;
-        const bool ok = jj < n;
-        const int c = __shfl(mc, rs * SL + (jj < SL ? jj : 0));
-        if (ok && colv) {
-          load_vec<4>(ep.x + (int64_t)c * ep.ldx + cc, xv[u]);
-        } else {
+    for (int t = 0; t < 4; ++t) acch[h][t] = 0.f;
+  for (int e0 = 0; e0 < len; e0 += SL) {
+    const int n = min(SL, len - e0);
+    int mc;
+    float s[H];
+    if (e0 == 0 || GNPDE_FL_DIAG) {
+      mc = e0 == 0 ? mc0 : (sl < n ? col[beg + e0 + sl] : 0);
 #pragma unroll
-          for (int t = 0; t < 4; ++t) xv[u][t] = 0.f;
-        }
-        if (ok) {
-          load_vec<4>(da.k + (int64_t)c * da.ldqk + ko, kv[u]);
-        } else {
+      for (int h = 0; h < H; ++h) s[h] = GNPDE_FL_DIAG == 1 ? 0.f : s1[h];
+    } else {  // a later batch of a long row: its scores again
+      mc = sl < n ? col[beg + e0 + sl] : 0;
+      tile_scores<SL, NA, S, H>(qv, mc, n, base, sl, da, sc);
+      own_scores<H>(sc, sl, n, s);
+    }
+    if (!wchunk) {
+      const float mw = sl < n ? edge_weight<H>(s, M, Rl) : 0.f;
+      for (int j = 0; j < n; j += U) {
+        float v[U][4];
+        float ww[U];
 #pragma unroll
-          for (int t = 0; t < 4; ++t) kv[u][t] = 0.f;
-        }
-      }
-      float s[U][MAXH];
+        for (int u = 0; u < U; ++u) {
+          const int jj = j + u;
+          const int src = base + (jj < n ? jj : 0);
+          const int c = __shfl(mc, src);
+          ww[u] = jj < n ? __shfl(mw, src) : 0.f;
+          if (GNPDE_FL_PREFETCH && e0 == 0 && j == 0) {  // gathered before pass 1
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        float d = 0.f;
+            for (int t = 0; t < 4; ++t) v[u][t] = xv0[u][t];
+          } else if (jj < n && cc < C) {
+            load_vec<4>(ep.x + (int64_t)c * ep.ldx + cc, v[u]);
+          } else {
 #pragma unroll
-        for (int t = 0; t < 4; ++t) d = fmaf(qv[t], kv[u][t], d);
-        d = head_reduce(d, da.S) * da.scale;  // full-wave DPP
-        heads_bcast<MAXH>(d, da.S, s[u]);
-        if (j + u >= n) {
-#pragma unroll
-          for (int h = 0; h < MAXH; ++h) s[u][h] = -INFINITY;
-        }
-      }
-#pragma unroll
-      for (int h = 0; h < MAXH; ++h) {
-        if (h < H) {
-          float mb = M[h];
-#pragma unroll
-          for (int u = 0; u < U; ++u) mb = fmaxf(mb, s[u][h]);
-          if (mb != -INFINITY) {  // some edge of the batch is live for this slot
-            const float corr = __builtin_amdgcn_exp2f(M[h] - mb);  // exp2(-inf) = 0 on the first batch
-            float p[U];
-            float ls = 0.f;
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-              p[u] = __builtin_amdgcn_exp2f(s[u][h] - mb);
-              ls += p[u];
-            }
-            L[h] = fmaf(L[h], corr, ls);
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-              float a = acc[h][t] * corr;
-#pragma unroll
-              for (int u = 0; u < U; ++u) a = fmaf(p[u], xv[u][t], a);
-              acc[h][t] = a;
-            }
-            M[h] = mb;
+            for (int t = 0; t < 4; ++t) v[u][t] = 0.f;
           }
         }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+          for (int t = 0; t < 4; ++t) acc[t] = fmaf(ww[u], v[u][t], acc[t]);
+      }
+    } else {
+      float ph[H];
+#pragma unroll
+      for (int h = 0; h < H; ++h) ph[h] = sl < n ? __builtin_amdgcn_exp2f(s[h] - M[h]) : 0.f;
+      for (int j = 0; j < n; j += U) {
+        float v[U][4];
+        float ww[U][H];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int jj = j + u;
+          const int src = base + (jj < n ? jj : 0);
+          const int c = __shfl(mc, src);
+#pragma unroll
+          for (int h = 0; h < H; ++h) ww[u][h] = jj < n ? __shfl(ph[h], src) : 0.f;
+          if (GNPDE_FL_PREFETCH && e0 == 0 && j == 0) {
+#pragma unroll
+            for (int t = 0; t < 4; ++t) v[u][t] = xv0[u][t];
+          } else if (jj < n && cc < C) {
+            load_vec<4>(ep.x + (int64_t)c * ep.ldx + cc, v[u]);
+          } else {
+#pragma unroll
+            for (int t = 0; t < 4; ++t) v[u][t] = 0.f;
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+          for (int h = 0; h < H; ++h)
+#pragma unroll
+            for (int t = 0; t < 4; ++t) acch[h][t] = fmaf(ww[u][h], v[u][t], acch[h][t]);
       }
     }
   }
 
-  // a chunk of a hub row: store the running state, merge in-launch (last arrival)
-  const bool chunk = live && slot >= 0;
-  if (n_heavy > 0) {
-    int anyc = 0;
+  if (wchunk) {
+    // hub chunks: (acc_h, M_h, L_h) written through to the slot, merged in-launch by
+    // the last arrival (arrival tickets on the plan's heavy entries, as K1)
+    const int ps = (int)dot_partial_floats(H, C);
+    const __amdgpu_buffer_rsrc_t rp = buf_rsrc(partials);
+    const int64_t pb = (int64_t)(chunk ? slot : 0) * ps;
 #pragma unroll
-    for (int s = 0; s < RPW; ++s) anyc |= __shfl((int)chunk, s * SL);
-    if (anyc) {  // wave-uniform
-      const __amdgpu_buffer_rsrc_t rp = buf_rsrc(partials);
-      const int64_t base = (int64_t)(chunk ? slot : 0) * da.ps;
-#pragma unroll
-      for (int h = 0; h < MAXH; ++h) {
-        if (h < H) {
-          buf_store_wt<4>(rp, (chunk && colv) ? (uint32_t)((base + h * C + cc) * 4) : kBufNone, acc[h]);
-          float ml[1] = {M[h]};
-          buf_store_wt<1>(rp, (chunk && gl == 0) ? (uint32_t)((base + H * C + h) * 4) : kBufNone, ml);
-          ml[0] = L[h];
-          buf_store_wt<1>(rp, (chunk && gl == 0) ? (uint32_t)((base + H * C + H + h) * 4) : kBufNone, ml);
-        }
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      int lo = 0, won = 0;
-      if (chunk) {
-        int hi = n_heavy - 1;
-        while (lo < hi) {
-          const int mid = (lo + hi + 1) >> 1;
-          if (heavy[mid].y <= slot)
-            lo = mid;
-          else
-            hi = mid - 1;
-        }
-        if (gl == 0) {
-          const int t = __hip_atomic_fetch_add(&heavy[lo].w, 1, kHubTicketOrder, __HIP_MEMORY_SCOPE_AGENT);
-          won = t == heavy[lo].z - 1;
-        }
-      }
-#pragma unroll
-      for (int s = 0; s < RPW; ++s) {
-        if (__shfl(won, s * SL)) {  // wave-uniform
-          const int hh = __shfl(lo, s * SL);
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-          const int4 hv = heavy[hh];
-          flash_hub_combine<MAXH, STG>(uniform(hv.x), uniform(hv.y), uniform(hv.z), C, da, ep, partials);
-          if (lane == 0) __hip_atomic_store(&heavy[hh].w, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-      }
-      if (chunk) return;
+    for (int h = 0; h < H; ++h) {
+      buf_store_wt<4>(rp, (chunk && cc < C) ? (uint32_t)((pb + h * C + cc) * 4) : kBufNone, acch[h]);
+      float ml[1] = {M[h]};
+      buf_store_wt<1>(rp, (chunk && sl == 0) ? (uint32_t)((pb + H * C + h) * 4) : kBufNone, ml);
+      ml[0] = L[h];
+      buf_store_wt<1>(rp, (chunk && sl == 0) ? (uint32_t)((pb + H * C + H + h) * 4) : kBufNone, ml);
     }
-  }
-  if (!live || slot >= 0) return;
-  float ax[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int h = 0; h < MAXH; ++h) {
-    if (h < H) {
-      const float r = 1.0f / (L[h] + kSoftmaxEps);
-#pragma unroll
-      for (int t = 0; t < 4; ++t) ax[t] = fmaf(acc[h][t], r, ax[t]);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int lo = 0, won = 0;
+    if (chunk) {
+      int hi = n_heavy - 1;
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (heavy[mid].y <= slot)
+          lo = mid;
+        else
+          hi = mid - 1;
+      }
+      if (sl == 0) {
+        const int t = __hip_atomic_fetch_add(&heavy[lo].w, 1, kHubTicketOrder, __HIP_MEMORY_SCOPE_AGENT);
+        won = t == heavy[lo].z - 1;
+      }
     }
-  }
-  const float inv_h = 1.0f / (float)H;
 #pragma unroll
-  for (int t = 0; t < 4; ++t) ax[t] *= inv_h;
+    for (int r = 0; r < RPW; ++r) {
+      if (__shfl(won, r * SL)) {  // wave-uniform
+        const int hh = __shfl(lo, r * SL);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        const int4 hv = heavy[hh];
+        dot_hub_combine<H, STG>(uniform(hv.x), uniform(hv.y), uniform(hv.z), C, ps, ep, partials);
+        if (lane == 0) __hip_atomic_store(&heavy[hh].w, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    if (chunk) return;
+    // the whole rows of this wavefront: normalise the per-head sums
+#pragma unroll
+    for (int h = 0; h < H; ++h)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[t] = fmaf(acch[h][t], Rl[h], acc[t]);
+    constexpr float inv_h = 1.0f / (float)H;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[t] *= inv_h;
+  }
+  if (!live) return;
   const float a = (ep.flags & GNPDE_EPI_RHS) ? epi_alpha(ep) : 1.f;
   const float b = (ep.flags & GNPDE_ADD_SOURCE) ? *ep.beta : 0.f;
   double dpart = 0.0;
-  if (colv) epi_finish<4, STG, float>(ep, row, cc, ax, a, b, pre, &dpart);
+  if (owner) epi_finish<4, STG, float>(ep, row, cc, acc, a, b, pre, &dpart);
   if constexpr (STG >= 2)
-    if (ep.st.dot_rows) {
-      // the slot's lanes hold the row's partial dot terms: a fixed xor tree over the slot
-#pragma unroll
-      for (int o = 1; o < SL; o <<= 1) dpart += __shfl_xor(dpart, o);
-      if (gl == 0) {
-        double* d = ep.st.dot_rows + row;
-        const double v = ep.st.dot_coef * dpart;
-        *d = ep.st.dot_accumulate ? *d + v : v;
-      }
-    }
+    if (ep.st.dot_rows) epi_dot_store<GL>(ep, row, dpart, sl == 0);
 }
 
-template <int GL, int MAXH>
-static int launch_flash_h(const int4* items, int64_t n_items, int4* heavy, int64_t n_heavy, const int* col,
-                          const DotArgs& da, int C, const Epi& ep, float* partials, hipStream_t s) {
+template <int GL, int NA, int S, int H>
+static int launch_dot_nh(const int4* items, int64_t n_items, int4* heavy, int64_t n_heavy, const int* col,
+                         const DotArgs& da, int C, const Epi& ep, float* partials, hipStream_t s) {
   constexpr int RPW = kWave / GL;
-  constexpr int U = 4;
+  constexpr int U = GNPDE_FL_U;
   const unsigned grid = (unsigned)ceil_div(n_items, (int64_t)kWavesPerBlock * RPW);
   const int stg = epi_stage_kind(ep);
   const int nh = (int)n_heavy;
   if (stg == 1)
-    flash_agg_kernel<GL, U, MAXH, 1><<<grid, kBlock, 0, s>>>(items, (int)n_items, heavy, nh, col, da, C, ep, partials);
+    dot_agg_kernel<GL, U, NA, S, H, 1><<<grid, kBlock, 0, s>>>(items, (int)n_items, heavy, nh, col, da, C, ep, partials);
   else if (stg == 2)
-    flash_agg_kernel<GL, U, MAXH, 2><<<grid, kBlock, 0, s>>>(items, (int)n_items, heavy, nh, col, da, C, ep, partials);
+    dot_agg_kernel<GL, U, NA, S, H, 2><<<grid, kBlock, 0, s>>>(items, (int)n_items, heavy, nh, col, da, C, ep, partials);
   else
-    flash_agg_kernel<GL, U, MAXH, 0><<<grid, kBlock, 0, s>>>(items, (int)n_items, heavy, nh, col, da, C, ep, partials);
+    dot_agg_kernel<GL, U, NA, S, H, 0><<<grid, kBlock, 0, s>>>(items, (int)n_items, heavy, nh, col, da, C, ep, partials);
   GNPDE_LAUNCH_CHECK();
   return GNPDE_OK;
 }
 
+// (att/4, heads) pairs: att in {8, 16, 32, 64}, heads in {1, 2, 4} dividing att/4
 template <int GL>
-static int launch_flash(const int4* items, int64_t n_items, int4* heavy, int64_t n_heavy, const int* col,
-                        const DotArgs& da, int C, const Epi& ep, float* partials, hipStream_t s) {
-  if (da.H <= 1) return launch_flash_h<GL, 1>(items, n_items, heavy, n_heavy, col, da, C, ep, partials, s);
-  if (da.H <= 2) return launch_flash_h<GL, 2>(items, n_items, heavy, n_heavy, col, da, C, ep, partials, s);
-  return launch_flash_h<GL, 4>(items, n_items, heavy, n_heavy, col, da, C, ep, partials, s);
+static int launch_dot(int NA, int H, const int4* items, int64_t n_items, int4* heavy, int64_t n_heavy, const int* col,
+                      const DotArgs& da, int C, const Epi& ep, float* partials, hipStream_t s) {
+#define GNPDE_DOT(A, HH) \
+  if (NA == A && H == HH) \
+    return launch_dot_nh<GL, A, (A / HH), HH>(items, n_items, heavy, n_heavy, col, da, C, ep, partials, s)
+  GNPDE_DOT(2, 1); GNPDE_DOT(2, 2);
+  GNPDE_DOT(4, 1); GNPDE_DOT(4, 2); GNPDE_DOT(4, 4);
+  GNPDE_DOT(8, 1); GNPDE_DOT(8, 2); GNPDE_DOT(8, 4);
+  GNPDE_DOT(16, 1); GNPDE_DOT(16, 2); GNPDE_DOT(16, 4);
+#undef GNPDE_DOT
+  set_error("attn_dot_rhs: att=%d heads=%d not instantiated", 4 * NA, H);
+  return GNPDE_EUNSUPPORTED;
 }
 
 }  // namespace gnpde
@@ -363,44 +495,40 @@ using namespace gnpde;
 
 extern "C" {
 
-int64_t gnpde_attn_dot_partial_floats(int64_t heads, int64_t C) { return (heads * C + 2 * heads + 3) & ~(int64_t)3; }
-
 int gnpde_attn_dot_supported(int64_t heads, int64_t dk, int64_t C) {
   const int64_t att = heads * dk;
-  if (heads < 1 || heads > 4 || dk < 4 || dk % 4 || C < 1 || C > 256 || C % 4) return 0;
-  const int64_t S = dk / 4;
-  if (S & (S - 1)) return 0;
-  // a 16-lane row holds att/4 distinct slices; att/4 must divide 16
-  if (att > 64 || 16 % (att / 4)) return 0;
-  return 1;
+  if (!(heads == 1 || heads == 2 || heads == 4) || dk < 4 || dk % 4) return 0;
+  if (!(att == 8 || att == 16 || att == 32 || att == 64)) return 0;
+  return C >= 1 && C <= 256 && C % 4 == 0;
+}
+
+int64_t gnpde_attn_dot_workspace_floats(int64_t heads, int64_t C, int64_t n_slots) {
+  return n_slots * dot_partial_floats(heads, C);
 }
 
 int gnpde_attn_dot_rhs_f32(const int32_t* items, int64_t n_items, int32_t* heavy, int64_t n_heavy,
-                           const int32_t* col, const float* q, const float* k, int64_t ldqk, int64_t heads, int64_t dk,
-                           int64_t C, const float* x, int64_t ldx, const float* x0, int64_t ldx0, const float* alpha,
-                           const float* beta, int flags, float* f, int64_t ldf, float* partials, int64_t n_slots,
-                           const gnpde_stage_epilogue_t* stage, void* stream) {
+                           const int32_t* col, const float* q, const float* k, int64_t ldqk,
+                           int64_t heads, int64_t dk, int64_t C, const float* x, int64_t ldx, const float* x0,
+                           int64_t ldx0, const float* alpha, const float* beta, int flags, float* f, int64_t ldf,
+                           float* workspace, int64_t n_slots, const gnpde_stage_epilogue_t* stage, void* stream) {
   GNPDE_REQUIRE(gnpde_attn_dot_supported(heads, dk, C), GNPDE_EUNSUPPORTED,
-                "attn_dot_rhs: heads=%lld dk=%lld C=%lld outside the fused kernel (heads <= 4, dk %% 4 == 0 with "
-                "dk/4 a power of two, heads*dk <= 64 dividing 64, C %% 4 == 0, C <= 256)",
+                "attn_dot_rhs: heads=%lld dk=%lld C=%lld outside the fused kernel (heads in {1, 2, 4}, dk %% 4 == 0, "
+                "heads*dk in {8, 16, 32, 64}, C %% 4 == 0, C <= 256)",
                 (long long)heads, (long long)dk, (long long)C);
   const Epi ep = make_epi(x, ldx, x0, ldx0, alpha, beta, flags, f, ldf, stage);
-  // the partial slots hold ps floats each (gnpde_attn_dot_partial_floats): check_epi
-  // bounds n_slots * C, the wider slots are bounded here
-  int rc = check_epi(ep, C, 0, partials, n_slots);
+  int rc = check_epi(ep, C, n_heavy, workspace, n_slots);
   if (rc) return rc;
-  const int64_t ps = gnpde_attn_dot_partial_floats(heads, C);
-  GNPDE_REQUIRE(n_heavy == 0 || (partials != nullptr && n_slots > 0), GNPDE_EINVAL,
-                "attn_dot_rhs: hub rows need a partials buffer and its slot count");
-  GNPDE_REQUIRE(n_slots >= 0 && n_slots * ps * 4 < (int64_t)kBufRecords, GNPDE_EUNSUPPORTED,
-                "attn_dot_rhs: %lld partial slots x %lld floats exceed the 4 GiB of 32-bit buffer offsets",
-                (long long)n_slots, (long long)ps);
-  GNPDE_REQUIRE(n_items >= 0 && n_items < INT32_MAX && n_heavy >= 0, GNPDE_EINVAL, "attn_dot_rhs: bad item counts");
+  GNPDE_REQUIRE(n_items >= 0 && n_items < INT32_MAX && n_heavy >= 0 && n_heavy < INT32_MAX, GNPDE_EINVAL,
+                "attn_dot_rhs: bad item counts");
   GNPDE_REQUIRE(n_items == 0 || (items && col && q && k), GNPDE_EINVAL, "attn_dot_rhs: NULL plan/col/q/k");
+  GNPDE_REQUIRE(n_heavy == 0 || (heavy && workspace && n_slots > 0), GNPDE_EINVAL,
+                "attn_dot_rhs: hub rows need heavy and the workspace");
+  GNPDE_REQUIRE(n_slots * dot_partial_floats(heads, C) * 4 < (int64_t)kBufRecords, GNPDE_EUNSUPPORTED,
+                "attn_dot_rhs: %lld partial slots exceed the 4 GiB of 32-bit buffer offsets", (long long)n_slots);
   GNPDE_REQUIRE(ldqk >= heads * dk && ldqk % 4 == 0 && aligned16(q) && aligned16(k), GNPDE_EUNSUPPORTED,
                 "attn_dot_rhs: q/k rows must be 16-byte aligned (ldqk %% 4 == 0)");
-  GNPDE_REQUIRE(ldx % 4 == 0 && ldf % 4 == 0 && aligned16(x) && (!f || aligned16(f)) && aligned16(partials),
-                GNPDE_EUNSUPPORTED, "attn_dot_rhs: x / f rows must be 16-byte aligned");
+  GNPDE_REQUIRE(ldx % 4 == 0 && ldf % 4 == 0 && aligned16(x) && (!f || aligned16(f)) && aligned16(workspace),
+                GNPDE_EUNSUPPORTED, "attn_dot_rhs: x / f rows and the workspace must be 16-byte aligned");
   if (flags & GNPDE_ADD_SOURCE)
     GNPDE_REQUIRE(ldx0 % 4 == 0 && aligned16(x0), GNPDE_EUNSUPPORTED, "attn_dot_rhs: x0 rows must be 16-byte aligned");
   if (stage) {
@@ -417,18 +545,15 @@ int gnpde_attn_dot_rhs_f32(const int32_t* items, int64_t n_items, int32_t* heavy
   da.q = q;
   da.k = k;
   da.ldqk = ldqk;
-  da.H = (int)heads;
-  da.S = (int)(dk / 4);
-  da.qlanes = (int)(heads * dk / 4);
   da.scale = kLog2e / sqrtf((float)dk);
-  da.ps = (int)ps;
   const int4* it = reinterpret_cast<const int4*>(items);
   int4* hv = reinterpret_cast<int4*>(heavy);
   const int lanes = (int)(C / 4);
+  const int NA = (int)(heads * dk / 4), H = (int)heads;
   hipStream_t s = as_stream(stream);
-  if (lanes <= 16) return launch_flash<16>(it, n_items, hv, n_heavy, col, da, (int)C, ep, partials, s);
-  if (lanes <= 32) return launch_flash<32>(it, n_items, hv, n_heavy, col, da, (int)C, ep, partials, s);
-  return launch_flash<64>(it, n_items, hv, n_heavy, col, da, (int)C, ep, partials, s);
+  if (lanes <= 16) return launch_dot<16>(NA, H, it, n_items, hv, n_heavy, col, da, (int)C, ep, workspace, s);
+  if (lanes <= 32) return launch_dot<32>(NA, H, it, n_items, hv, n_heavy, col, da, (int)C, ep, workspace, s);
+  return launch_dot<64>(NA, H, it, n_items, hv, n_heavy, col, da, (int)C, ep, workspace, s);
 }
 
 }  // extern "C"

@@ -920,17 +920,17 @@ def attn_dot_rhs(g, ns, x, x0=None, alpha=None, beta=None, rhs=True, alpha_sigmo
     elif out is None:
         out = torch.empty_like(xr)
     plan = g.csr.plan
-    ps = int(_lib.fn("gnpde_attn_dot_partial_floats")(H, C))
-    partials = None
-    if plan.n_slots:
-        if plan.n_slots * ps * 4 >= _PARTIALS_MAX_BYTES:
+    nws = int(_lib.fn("gnpde_attn_dot_workspace_floats")(H, C, plan.n_slots))
+    ws = None
+    if nws:
+        if nws * 4 >= _PARTIALS_MAX_BYTES:
             return NotImplemented
-        partials = torch.empty(plan.n_slots * ps, dtype=torch.float32, device=dev)
+        ws = torch.empty(nws, dtype=torch.float32, device=dev)
     plan.order_launch(dev)
     rc = _lib.call_rc("gnpde_attn_dot_rhs_f32", _ptr(plan.items), plan.n_items, _ptr(plan.heavy), plan.n_heavy,
-                      _ptr(g.csr.col), _ptr(ns.q), _ptr(ns.k), ns.ldqk, H, dk, C, _ptr(xr), C, _ptr(x0r), C, _ptr(a),
-                      _ptr(b), _flags(rhs, alpha_sigmoid, add_source), _ptr(out), C, _ptr(partials), plan.n_slots, st,
-                      _stream(dev))
+                      _ptr(g.csr.col), _ptr(ns.q), _ptr(ns.k), ns.ldqk, H, dk, C, _ptr(xr), C,
+                      _ptr(x0r), C, _ptr(a), _ptr(b), _flags(rhs, alpha_sigmoid, add_source), _ptr(out), C, _ptr(ws),
+                      plan.n_slots, st, _stream(dev))
     if rc == _lib.EUNSUPPORTED:
         return NotImplemented
     _lib.check(rc, "gnpde_attn_dot_rhs_f32")

@@ -265,28 +265,29 @@ int gnpde_attn_ref_rhs_f32(const int32_t* items, int64_t n_items, int32_t* heavy
 /* The per-edge scaled_dot attention RHS under source-grouped softmax
  * (attention_norm_idx 0; upstream GRAND's transformer RHS) in ONE aggregation
  * pass over the CSR plan (csrc/flash.hip): every row slot scores the edges it
- * gathers, s_e,h = q[row,h] . k[col_e,h] / sqrt(dk), and keeps a running max /
- * rescaled sum per head while it accumulates (online softmax), so
- *   ax_r = (1/H) sum_h (sum_e exp(s_e,h - M_h) x_c) / (sum_e exp(s_e,h - M_h) + 1e-16)
- * = multiply_attention with the head-mean of utils.softmax over edge_index[0]
+ * gathers, s_e,h = q[row,h] . k[col_e,h] / sqrt(dk), forms its group's
+ * statistics (max M_h, sum L_h of exp(s - M_h)) and aggregates with
+ *   w_e = (1/H) sum_h exp(s_e,h - M_h) / (L_h + 1e-16)
+ * = multiply_attention with the head mean of utils.softmax over edge_index[0]
  * (function_transformer_attention.py:33-41, 246-266; src/utils.py:116-127),
  * then the RHS / stage epilogue as gnpde_spmm_rhs_f32.  Replaces
  * gnpde_seg_softmax_f32(out_kind 0) + gnpde_spmm_rhs_f32 (no [nnz] weights).
- * q, k: [R, ldqk] fp32 (gnpde_linear_f32), 16-byte aligned rows.  Hub chunks
- * keep (acc[h][C], M[h], L[h]) in partial slots of
- * gnpde_attn_dot_partial_floats(heads, C) floats (n_slots of them) and are
- * merged in-launch by the last-arriving chunk (heavy[].w tickets, as K1).
- * Shapes: gnpde_attn_dot_supported(heads, dk, C) != 0 (heads <= 4, dk % 4 == 0
- * with dk/4 a power of two, heads*dk in {4, 8, 16, 32, 64}, C % 4 == 0,
- * C <= 256); otherwise GNPDE_EUNSUPPORTED.  Exponentials in base 2
- * (1-2 ulp from expf).                                                       */
+ * q, k: [R, ldqk] fp32 (gnpde_linear_f32), 16-byte aligned rows.  Hub rows
+ * (heavy entries of the plan): each chunk keeps its own statistics and
+ * per-head sums in a partial slot, merged in-launch by the last chunk to
+ * arrive (heavy[].w tickets, as K1).  workspace:
+ * gnpde_attn_dot_workspace_floats(heads, C, n_slots) floats, 16-byte aligned.
+ * Shapes:
+ * gnpde_attn_dot_supported(heads, dk, C) != 0 (heads in {1, 2, 4}, dk % 4 ==
+ * 0, heads*dk in {8, 16, 32, 64}, C % 4 == 0, C <= 256); otherwise
+ * GNPDE_EUNSUPPORTED.  Exponentials in base 2 (1-2 ulp from expf).         */
 int gnpde_attn_dot_supported(int64_t heads, int64_t dk, int64_t C);
-int64_t gnpde_attn_dot_partial_floats(int64_t heads, int64_t C);
+int64_t gnpde_attn_dot_workspace_floats(int64_t heads, int64_t C, int64_t n_slots);
 int gnpde_attn_dot_rhs_f32(const int32_t* items, int64_t n_items, int32_t* heavy, int64_t n_heavy,
-                           const int32_t* col, const float* q, const float* k, int64_t ldqk, int64_t heads, int64_t dk,
-                           int64_t C, const float* x, int64_t ldx, const float* x0, int64_t ldx0, const float* alpha,
-                           const float* beta, int flags, float* f, int64_t ldf, float* partials, int64_t n_slots,
-                           const gnpde_stage_epilogue_t* stage, void* stream);
+                           const int32_t* col, const float* q, const float* k, int64_t ldqk,
+                           int64_t heads, int64_t dk, int64_t C, const float* x, int64_t ldx, const float* x0,
+                           int64_t ldx0, const float* alpha, const float* beta, int flags, float* f, int64_t ldf,
+                           float* workspace, int64_t n_slots, const gnpde_stage_epilogue_t* stage, void* stream);
 
 /* ---------------------------------------------------------------- attention
  * Node-level projection on the matrix cores (K % 16 == 0, K <= 128: exact
