@@ -6,6 +6,7 @@
 // hub's plan entry; fixed summation order, so deterministic; no float atomics).
 #pragma once
 #include <algorithm>
+#include <type_traits>
 
 #include "common.hpp"
 
@@ -96,6 +97,12 @@ struct RefDstSoftmaxWeights {
   }
 };
 
+template <class WP>
+__host__ __device__ inline PlainWeights as_plain(const WP& wp) {
+  if constexpr (std::is_same<WP, PlainWeights>::value) return wp;
+  else return PlainWeights{nullptr};  // never launched (launch_agg_cfg)
+}
+
 // ------------------------------------------------------------------ hub rows
 // Lane groups of the hub combine are powers of two (an xor tree joins them):
 // a geometry with GL = 21 lanes per row (three bf16 rows of 168 columns per
@@ -138,7 +145,7 @@ __device__ __forceinline__ void hub_combine(int row, int first, int nch, int C, 
       for (int t = 0; t < VEC; ++t) s[t] += __shfl_xor(s[t], o);
     if (g == 0 && live) epilogue_store<VEC, STG, T>(ep, row, cc, s, a, b, &dpart);
   }
-  if constexpr (STG >= 2 && sizeof(T) == 4)
+  if constexpr (stage_dot<STG>() && sizeof(T) == 4)
     if (ep.st.dot_rows) epi_dot_store<GL>(ep, row, dpart, lane == 0);  // wave-uniform
 }
 
@@ -375,7 +382,7 @@ __global__ __launch_bounds__(256) void agg_kernel(const int4* __restrict__ items
     }
   }
   // the row's owner lanes (g == 0: lanes [rs*SL, rs*SL + GL)) are all here
-  if constexpr (STG >= 2 && sizeof(T) == 4 && (GL & (GL - 1)) == 0)
+  if constexpr (stage_dot<STG>() && sizeof(T) == 4 && (GL & (GL - 1)) == 0)
     if (ep.st.dot_rows) epi_dot_store<GL>(ep, row, dpart, gl == 0);
 }
 
@@ -408,9 +415,14 @@ static int launch_agg_cfg(const int4* items, int64_t n_items, int4* heavy, int64
   // single-output stages without dot terms (every forward gnpde.integrator step) get the
   // leaner instantiation: 56-60 VGPRs, 8 waves per SIMD; the dot terms of the adjoint
   // stages alone cost the general one 40+ VGPRs (fused rk4 K1 92.9 -> 107 us at 4 waves)
-  const int stg = epi_stage_kind(ep);
+  int stg = epi_stage_kind(ep);
   if (n_items > 0) {
-    if (stg == 1)
+    // the one-output adjoint stages: fp32 plain weights only (the transposed aggregation)
+    if (stg == 3 && !(std::is_same<WP, PlainWeights>::value && sizeof(T) == 4)) stg = 2;
+    if (stg == 3)
+      agg_kernel<VEC, GL, NCH, U, RPW, 3, PlainWeights, float><<<grid, kBlock, 0, s>>>(
+          items, (int)n_items, heavy, nh, col, as_plain(wp), C, ep, partials);
+    else if (stg == 1)
       agg_kernel<VEC, GL, NCH, U, RPW, 1, WP, T><<<grid, kBlock, 0, s>>>(items, (int)n_items, heavy, nh, col, wp, C, ep,
                                                                           partials);
     else if (stg == 2)
@@ -424,6 +436,7 @@ static int launch_agg_cfg(const int4* items, int64_t n_items, int4* heavy, int64
   if constexpr (GNPDE_EXPERIMENTS) {
     const unsigned gfix = (unsigned)ceil_div(n_heavy, kWavesPerBlock);
     if (!inlaunch && n_heavy > 0) {
+      if (stg == 3) stg = 2;
       if (stg == 1)
         agg_fixup_kernel<VEC, GL, 1, T><<<gfix, kBlock, 0, s>>>(heavy, (int)n_heavy, C, ep, partials);
       else if (stg == 2)
@@ -476,15 +489,19 @@ static int launch_agg_vec(const int4* items, int64_t n_items, int4* heavy, int64
   // 32 / 64 columns 2.06 / 3.67 ms against 2.56 / 4.52); a cache-resident one (G-arxiv
   // stripes) prefers several edge groups per row (0.149 / 0.124 ms at 32 / 16 columns
   // against 0.283 / 0.318).
-  if (var != 5) {
-    if (n_items * (int64_t)C * (int64_t)sizeof(T) > (int64_t)(96 << 20)) {
-      if (lanes <= 4) return GNPDE_AGG(4, 1, 4, 16);
-      if (lanes <= 8) return GNPDE_AGG(8, 1, 4, 8);
-      if (lanes <= 16) return GNPDE_AGG(16, 1, 4, 4);
+  // (plain weights only: the attention-weight policies take the 16-lane geometry for
+  // narrow rows, which keeps the library's instantiation count down)
+  if constexpr (std::is_same<WP, PlainWeights>::value) {
+    if (var != 5) {
+      if (n_items * (int64_t)C * (int64_t)sizeof(T) > (int64_t)(96 << 20)) {
+        if (lanes <= 4) return GNPDE_AGG(4, 1, 4, 16);
+        if (lanes <= 8) return GNPDE_AGG(8, 1, 4, 8);
+        if (lanes <= 16) return GNPDE_AGG(16, 1, 4, 4);
+      }
+      if (lanes <= 4) return GNPDE_AGG(4, 1, 4, 4);
+      if (lanes <= 8) return GNPDE_AGG(8, 1, 8, 4);
+      if (lanes <= 16) return GNPDE_AGG(16, 1, 4, 2);
     }
-    if (lanes <= 4) return GNPDE_AGG(4, 1, 4, 4);
-    if (lanes <= 8) return GNPDE_AGG(8, 1, 8, 4);
-    if (lanes <= 16) return GNPDE_AGG(16, 1, 4, 2);
   }
   if (lanes <= 16) return GNPDE_AGG(16, 1, 4, 1);
   if constexpr (sizeof(T) == 2 && VEC == 8) {

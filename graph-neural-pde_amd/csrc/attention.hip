@@ -149,6 +149,31 @@ constexpr int kRefBlock = 1024;                 // ref_stats_kernel workgroup (h
 constexpr int kRefWaves = kRefBlock / kWave;
 constexpr int kHubU = 8;                        // edges per thread per pass of a hub group
 
+// node scores cs[src[u], 0..MAXH) of U sources (src < 0: row 0, unused): two
+// heads as one 16-byte load — one gather instruction instead of two (random
+// 8-byte gathers are bound by the address unit, one cache line per lane): G-arxiv
+// CSC statistics 21.0 -> 19.3 us, hub groups alone 15.2 -> 13.7 us.  (Two-phase
+// max-then-sum reductions instead of merging online pairs: hub / long groups 10.6 /
+// 6.9 us, but the scores kept in registers between the phases cost the short
+// items their occupancy, 22.7 us in all; reloading them, 20.2 us.)
+template <int U, int MAXH>
+__device__ __forceinline__ void load_cs_rows(const ScoreArgs& sa, const int (&src)[U], double (&v)[U][MAXH]) {
+  const int H = sa.H;
+  if constexpr (MAXH == 2) {  // launch_ref_stats: MAXH == 2 means H == 2 and 16-byte aligned rows
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const double2 t = *reinterpret_cast<const double2*>(sa.cs + (int64_t)max(src[u], 0) * 2);
+      v[u][0] = t.x;
+      v[u][1] = t.y;
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int h = 0; h < MAXH; ++h) v[u][h] = h < H ? sa.cs[(int64_t)max(src[u], 0) * H + h] : 0.0;
+  }
+}
+
 template <int U, int MAXH>
 __device__ __forceinline__ void push_edges(int pb, int stride, int e1, const int* __restrict__ gidx,
                                            const ScoreArgs& sa, double (&M)[MAXH], float (&L)[MAXH]) {
@@ -160,10 +185,7 @@ __device__ __forceinline__ void push_edges(int pb, int stride, int e1, const int
     src[u] = p < e1 ? gidx[p] : -1;
   }
   double v[U][MAXH];
-#pragma unroll
-  for (int u = 0; u < U; ++u)
-#pragma unroll
-    for (int h = 0; h < MAXH; ++h) v[u][h] = h < H ? sa.cs[(int64_t)max(src[u], 0) * H + h] : 0.0;
+  load_cs_rows<U, MAXH>(sa, src, v);
 #pragma unroll
   for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -339,7 +361,7 @@ __global__ __launch_bounds__(256) void seg_softmax_kernel(const int4* __restrict
 // A lane's segment end comes from a ballot of group changes (no rowptr gather).
 // Same arithmetic as seg_softmax_kernel<true, kSegStats>: segmented max,
 // exp(v - M), segmented sum, in the same lane order.
-constexpr int kRefStatsNI = 2;
+constexpr int kRefStatsNI = 2;  // 1 / 4 items per wavefront: 20.9 / 23.1 us against 21.0
 
 template <int NI, int MAXH>
 __global__ __launch_bounds__(kRefBlock) void ref_stats_kernel(const int4* __restrict__ items, int n_items, int n_hub,
@@ -376,10 +398,7 @@ __global__ __launch_bounds__(kRefBlock) void ref_stats_kernel(const int4* __rest
     src[i] = n[i] > 0 ? gidx[p] : 0;
   }
   double v[NI][MAXH];
-#pragma unroll
-  for (int i = 0; i < NI; ++i)
-#pragma unroll
-    for (int h = 0; h < MAXH; ++h) v[i][h] = (h < H && n[i] > 0) ? sa.cs[(int64_t)src[i] * H + h] : 0.0;
+  load_cs_rows<NI, MAXH>(sa, src, v);
 #pragma unroll
   for (int i = 0; i < NI; ++i) {
     if (n[i] > 0) {  // wave-uniform
@@ -412,7 +431,7 @@ static int launch_ref_stats(const int4* items, int64_t n_items, int64_t n_hub, i
                                                       m, rl, mr)
   if (sa.H <= 1)
     GNPDE_RS(1);
-  else if (sa.H <= 2)
+  else if (sa.H <= 2 && aligned16(sa.cs))  // MAXH 2: two heads, 16-byte node-score rows
     GNPDE_RS(2);
   else if (sa.H <= 4)
     GNPDE_RS(4);

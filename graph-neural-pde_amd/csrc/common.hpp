@@ -272,9 +272,15 @@ struct EpiPre {
   Packed<VEC, T> dw;  // the stage's dot operand (dot_rows)
 };
 
+// STG = 3: one stage output plus the dot term (the adjoint stages of the
+// discrete-adjoint backward that emit one combination)
 template <int STG>
 constexpr int stage_nout() {
-  return STG < 1 ? 1 : STG;
+  return STG == 2 ? 2 : 1;
+}
+template <int STG>
+constexpr bool stage_dot() {
+  return STG >= 2;
 }
 
 // The Epi / stage pointers are declared float*; for bf16 storage they address
@@ -306,7 +312,7 @@ __device__ __forceinline__ void epi_prefetch(const Epi& e, int64_t row, int cc, 
         if (j < so.nk) load_packed<VEC>(as_t<T>(so.k[j]) + off, p.kv[i][j]);
     }
   }
-  if constexpr (STG >= 2)  // dot terms (the adjoint stages) only in the general instantiation
+  if constexpr (STG == 2)  // STG 3 loads its dot operand in the epilogue (registers: occupancy)
     if (e.st.dot_rows) load_packed<VEC>(as_t<T>(e.st.dot_with) + off, p.dw);
 }
 
@@ -335,10 +341,15 @@ __device__ __forceinline__ void epi_finish(const Epi& e, int64_t row, int cc, co
   }
   const int64_t off = row * e.ldf + cc;
   if (e.st.f_out) store_vec<VEC>(as_t<T>(e.st.f_out) + off, o);
-  if constexpr (STG >= 2) {
+  if constexpr (stage_dot<STG>()) {
     if (e.st.dot_rows && dpart) {
+      Packed<VEC, T> dw;
+      if constexpr (STG == 2)
+        dw = p.dw;
+      else
+        load_packed<VEC>(as_t<T>(e.st.dot_with) + off, dw);
 #pragma unroll
-      for (int t = 0; t < VEC; ++t) *dpart = fma((double)o[t], (double)unpack(p.dw, t), *dpart);
+      for (int t = 0; t < VEC; ++t) *dpart = fma((double)o[t], (double)unpack(dw, t), *dpart);
     }
   }
   // the stage outputs' row (out_rows: the last step of a renumbered solve writes the caller's numbering)
@@ -397,10 +408,13 @@ __device__ __forceinline__ void epi_dot_store(const Epi& e, int64_t row, double 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 // The STG instantiation an epilogue needs: 0 = store f, 1 = one stage output
-// and no dot term (the forward Runge-Kutta steps), 2 = the general epilogue.
+// and no dot term (the forward Runge-Kutta steps), 3 = one stage output and the
+// dot term (three of the four adjoint launches of an rk4 step), 2 = the general
+// epilogue.
 inline int epi_stage_kind(const Epi& e) {
   if (!e.has_stage) return 0;
-  return (e.st.n_out <= 1 && !e.st.dot_rows) ? 1 : 2;
+  if (e.st.n_out <= 1) return e.st.dot_rows ? 3 : 1;
+  return 2;
 }
 
 // ------------------------------------------------------------------ buffer memory ops

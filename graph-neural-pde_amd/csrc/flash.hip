@@ -229,8 +229,7 @@ __device__ __forceinline__ void dot_hub_combine(int row, int first, int nch, int
   const float b = (ep.flags & GNPDE_ADD_SOURCE) ? *ep.beta : 0.f;
   double dpart = 0.0;
   if (live) epilogue_store<4, STG, float>(ep, row, cc, ax, a, b, &dpart);
-  if constexpr (STG >= 2)
-    if (ep.st.dot_rows) epi_dot_store<64>(ep, row, dpart, lane == 0);  // every lane of the wave (convergent)
+  static_assert(!stage_dot<STG>(), "dot-term epilogues are not fused here");
 }
 
 // ------------------------------------------------------------------ the fused attention RHS
@@ -451,8 +450,7 @@ void dot_agg_kernel(const int4* __restrict__ items, int n_items, int4* heavy, in
   const float b = (ep.flags & GNPDE_ADD_SOURCE) ? *ep.beta : 0.f;
   double dpart = 0.0;
   if (owner) epi_finish<4, STG, float>(ep, row, cc, acc, a, b, pre, &dpart);
-  if constexpr (STG >= 2)
-    if (ep.st.dot_rows) epi_dot_store<GL>(ep, row, dpart, sl == 0);
+  (void)dpart;
 }
 
 template <int GL, int NA, int S, int H>
@@ -465,9 +463,12 @@ static int launch_dot_nh(const int4* items, int64_t n_items, int4* heavy, int64_
   const int nh = (int)n_heavy;
   if (stg == 1)
     dot_agg_kernel<GL, U, NA, S, H, 1><<<grid, kBlock, 0, s>>>(items, (int)n_items, heavy, nh, col, da, C, ep, partials);
-  else if (stg == 2)
-    dot_agg_kernel<GL, U, NA, S, H, 2><<<grid, kBlock, 0, s>>>(items, (int)n_items, heavy, nh, col, da, C, ep, partials);
-  else
+  else if (stg >= 2) {
+    // two-output / dot-term stage epilogues (not used by the forward integrator): the caller
+    // takes the unfused path (gnpde_seg_softmax_f32 + gnpde_spmm_rhs_f32)
+    set_error("attn_dot_rhs: only the plain RHS and single-output stage epilogues are fused");
+    return GNPDE_EUNSUPPORTED;
+  } else
     dot_agg_kernel<GL, U, NA, S, H, 0><<<grid, kBlock, 0, s>>>(items, (int)n_items, heavy, nh, col, da, C, ep, partials);
   GNPDE_LAUNCH_CHECK();
   return GNPDE_OK;

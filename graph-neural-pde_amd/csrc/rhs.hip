@@ -91,11 +91,7 @@ int gnpde_attn_ref_rhs_f32(const int32_t* items, int64_t n_items, int32_t* heavy
     RefDstSoftmaxWeights<2, true, true> wp{cs, nullptr, nullptr, 2, mr};
     return launch_agg(items, n_items, heavy, n_heavy, col, wp, C, ep, partials, as_stream(stream));
   }
-  if (heads == 2 && aligned16(m) && aligned8(rl)) {
-    RefDstSoftmaxWeights<2, true> wp{cs, m, rl, 2, nullptr};
-    return launch_agg(items, n_items, heavy, n_heavy, col, wp, C, ep, partials, as_stream(stream));
-  }
-  if (heads <= 2) {
+  if (heads <= 2) {  // separate m / rl arrays (the packed records above are the fast path)
     RefDstSoftmaxWeights<2> wp{cs, m, rl, (int)heads, nullptr};
     return launch_agg(items, n_items, heavy, n_heavy, col, wp, C, ep, partials, as_stream(stream));
   }

@@ -270,7 +270,9 @@ int gnpde_attn_ref_rhs_f32(const int32_t* items, int64_t n_items, int32_t* heavy
  *   w_e = (1/H) sum_h exp(s_e,h - M_h) / (L_h + 1e-16)
  * = multiply_attention with the head mean of utils.softmax over edge_index[0]
  * (function_transformer_attention.py:33-41, 246-266; src/utils.py:116-127),
- * then the RHS / stage epilogue as gnpde_spmm_rhs_f32.  Replaces
+ * then the RHS epilogue, or a single-output stage epilogue without a dot
+ * term (the forward integrator's; others: GNPDE_EUNSUPPORTED), as
+ * gnpde_spmm_rhs_f32.  Replaces
  * gnpde_seg_softmax_f32(out_kind 0) + gnpde_spmm_rhs_f32 (no [nnz] weights).
  * q, k: [R, ldqk] fp32 (gnpde_linear_f32), 16-byte aligned rows.  Hub rows
  * (heavy entries of the plan): each chunk keeps its own statistics and
