@@ -38,7 +38,7 @@ def counters(path):
     last dot kernel, tools/pmc_run.py)."""
     rows = list(csv.DictReader(open(path)))
     rows.sort(key=lambda r: int(r["Dispatch_Id"]))
-    marks = [i for i, r in enumerate(rows) if "dot_" in r["Kernel_Name"]]
+    marks = [i for i, r in enumerate(rows) if "dot_final_kernel" in r["Kernel_Name"]]
     start = marks[-1] + 1 if marks else 0
     acc = collections.defaultdict(list)
     for r in rows[start:]:

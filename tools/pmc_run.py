@@ -40,7 +40,7 @@ def main():
     mk = torch.ones(64, device=dev)
 
     def marker():
-        # the measured region starts after the last dot kernel (gnpde_dot_f64 runs in no workload)
+        # the measured region starts after the last dot_final_kernel (gnpde_dot_f64 runs in no workload)
         torch.cuda.synchronize()
         ops.dot(mk, mk)
         torch.cuda.synchronize()
