@@ -466,6 +466,11 @@ __global__ __launch_bounds__(256, 2) void linear_split_kernel(const float* __res
 
 using namespace gnpde;
 
+// Measured and dropped (round 3): x tiles moved by the DMA path into LDS
+// (global_load_lds_dwordx4, two 16-KB buffers per wave, rows rotated by one 16-B
+// slot per row against bank conflicts, 3 waves per CU to fit 48 KB of W fragments +
+// 96 KB of tiles): 39.7 us against 33 us — one wave per SIMD at most cannot hide
+// the next tile's latency behind one tile of matrix work.
 // Experiment builds only (GNPDE_EXPERIMENTS): GNPDE_LINEAR=1 forces the
 // per-tile (non-persistent) exact-f32 kernel, =2 the persistent exact-f32 one
 // (default: the split-bf16 kernel where K % 16 == 0 and K <= 128).  Measured
