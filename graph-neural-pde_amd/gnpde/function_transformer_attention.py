@@ -37,7 +37,7 @@ passes (backward.hip): edge-softmax backward per group, then for the fork's
 scaled_dot the node-score / key-sum chain rule (segment sums, fp64 weighted
 column sums, a few [att, C] products) and for the per-edge scaled_dot two K1
 aggregations per head (q side over the CSR, k side over the CSC) and the
-projection backward (MFMA projection for d/dx, library GEMM for d/dW).  The
+projection backward (MFMA projections for d/dx and d/dW, gnpde_linear_wgrad_f32).  The
 transformer ODEFunc then composes it with the Laplacian RHS autograd
 (function_laplacian_diffusion._LaplacianRHS), whose weight gradient is an
 SDDMM.  exp_kernel / cosine_sim / pearson: one pass per side over the grouped
@@ -158,7 +158,7 @@ def _dot_score_backward(g, ns, gs, x, Wq, Wk):
                                                                      rhs=False, transpose=True)
     W = torch.cat([Wq, Wk], 0)                                 # [2att, C]
     gx, _ = ops.linear(gqk, W.t().contiguous())                # gx = [g_q | g_k] [Wq; Wk]
-    gW = gqk.t() @ xr                                          # [2att, C] (library GEMM)
+    gW = ops.linear_wgrad(gqk, xr)                             # [2att, C] = gqk^T x on the matrix cores
     gb = gqk.sum(0)
     att_dim = H * dk
     return (gx.view(x.shape), gW[:att_dim], gb[:att_dim], gW[att_dim:], gb[att_dim:])
@@ -180,7 +180,7 @@ def _edge_score_backward(g, ns, gs, x, Wq, Wk):
     xr = x.reshape(g.R, -1)
     W = torch.cat([Wq, Wk], 0)
     gx, _ = ops.linear(gqk, W.t().contiguous())                # gx = [g_q | g_k] [Wq; Wk]
-    gW = gqk.t() @ xr
+    gW = ops.linear_wgrad(gqk, xr)
     gb = gqk.sum(0)
     att_dim = ns.heads * ns.dk
     grads = (gx.view(x.shape), gW[:att_dim], gb[:att_dim], gW[att_dim:], gb[att_dim:])

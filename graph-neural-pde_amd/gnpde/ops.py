@@ -714,6 +714,24 @@ def linear(x, W, bias=None, split=None):
     return out_a, out_b
 
 
+def linear_wgrad(gy, x):
+    """gW = gy^T x [M, K] on the fp32 matrix cores (gnpde_linear_wgrad_f32): the
+    weight gradient of the Q / K projections (the backward of nn.Linear,
+    function_transformer_attention.py:224-225), rows reduced in a fixed order."""
+    gyr = _rows(gy, "gy")
+    xr = _rows(x, "x")
+    if gyr.shape[0] != xr.shape[0]:
+        raise ValueError("linear_wgrad: gy has %d rows, x has %d" % (gyr.shape[0], xr.shape[0]))
+    R, M = gyr.shape
+    K = xr.shape[1]
+    out = torch.empty(M, K, dtype=torch.float32, device=xr.device)
+    nb = _lib.fn("gnpde_linear_wgrad_workspace_bytes")(M, K)
+    ws = torch.empty(nb, dtype=torch.uint8, device=xr.device)
+    _lib.call("gnpde_linear_wgrad_f32", _ptr(gyr), R, M, M, _ptr(xr), K, K, _ptr(out), K, _ptr(ws), nb,
+              _stream(xr.device))
+    return out
+
+
 class NodeScores(object):
     """Per-RHS node-level operands of the attention scores."""
 

@@ -302,6 +302,17 @@ int gnpde_linear_f32(const float* x, int64_t R, int64_t K, int64_t ldx, const fl
                      int64_t Nout, int64_t split, float* out_a, int64_t lda, float* out_b, int64_t ldb,
                      void* stream);
 
+/* Weight gradient of the projection: gW[m, k] = sum_r gy[r, m] * x[r, k]
+ * (gy [R, M] ld ldg = dL/d[q | k], x [R, K] ld ldx; gW [M, K] ld ldw), the
+ * backward of nn.Linear's weight for the Q / K of
+ * function_transformer_attention.py:224-225.  fp32 matrix cores
+ * (v_mfma_f32_32x32x2_f32), the rows split over 512 wavefronts whose partial
+ * tiles are summed in wave order (deterministic).  workspace:
+ * gnpde_linear_wgrad_workspace_bytes(M, K) bytes.                            */
+size_t gnpde_linear_wgrad_workspace_bytes(int64_t M, int64_t K);
+int gnpde_linear_wgrad_f32(const float* gy, int64_t R, int64_t M, int64_t ldg, const float* x, int64_t K, int64_t ldx,
+                           float* gW, int64_t ldw, void* workspace, size_t workspace_bytes, void* stream);
+
 /* Reference-mode node scores (fork scaled_dot, function_transformer_attention.py:249):
  *   S_b = Wk * (sum_n indeg(n) x_n) + (sum_n indeg(n)) bk    (fp64)
  *   cs[r,h] = (q_r,h . S_b,h) / sqrt(dk),  q = Wq x + bq      (fp64 out)

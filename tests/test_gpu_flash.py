@@ -147,3 +147,41 @@ def test_flash_unsupported_shapes_fall_back():
     f = ops.attn_rhs(g, ns, None, None, 0, T(x), alpha=torch.tensor(0.1, device=DEV))
     want = O.transformer_rhs(ei, x, None, Wq, bq, Wk, bk, h, 0, 0.1, 0.0, score_mode='per_edge')
     assert rel(f, want) <= RTOL
+
+
+@pytest.mark.parametrize("R,M,K", [(169343, 64, 128), (1001, 48, 40), (3, 64, 128), (0, 32, 32), (777, 8, 300)])
+def test_linear_wgrad_vs_fp64(R, M, K):
+    """gnpde_linear_wgrad_f32 (the Q / K weight gradient on fp32 matrix cores) against
+    an fp64 gy^T x; repeated calls bit-identical (fixed reduction order)."""
+    g = torch.Generator(device=DEV)
+    g.manual_seed(R + M + K)
+    gy = torch.randn(R, M, generator=g, device=DEV)
+    x = torch.randn(R, K, generator=g, device=DEV)
+    w = ops.linear_wgrad(gy, x)
+    ref = gy.double().t() @ x.double()
+    den = max(float(ref.abs().max()), 1e-30)
+    assert float((w.double() - ref).abs().max()) / den <= 1e-5
+    assert torch.equal(w, ops.linear_wgrad(gy, x))
+
+
+def test_flash_two_streams_share_the_plan():
+    """The fused kernel's hub tickets live in the plan's heavy entries, as K1's:
+    launches of it and of K1 on two streams sharing one graph stay ordered
+    (Plan.order_launch) and give the same bits as on one stream."""
+    N, E, C, h, att = 3000, 50000, 128, 2, 32
+    ei, x, x0, Wq, bq, Wk, bk = case(N, E, C, att, seed=11)
+    g = ops.GraphCSR(T(ei), N)
+    ns = ops.node_scores(g, T(x), T(Wq), T(bq), T(Wk), T(bk), h, 'scaled_dot', 'per_edge')
+    a = torch.tensor(0.3, device=DEV)
+    ref = ops.attn_dot_rhs(g, ns, T(x), alpha=a)
+    wref = g.gather_weights(torch.rand(1, E, device=DEV))
+    kref = ops.spmm_rhs(g, wref, T(x), alpha=a)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    outs = []
+    torch.cuda.synchronize()
+    for i in range(6):
+        with torch.cuda.stream(s1 if i % 2 == 0 else s2):
+            outs.append((ops.attn_dot_rhs(g, ns, T(x), alpha=a), ops.spmm_rhs(g, wref, T(x), alpha=a)))
+    torch.cuda.synchronize()
+    for f, k in outs:
+        assert torch.equal(f, ref) and torch.equal(k, kref)
