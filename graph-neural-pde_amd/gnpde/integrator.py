@@ -460,35 +460,47 @@ class _LaplacianFixedGridFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, y0, alpha_train, beta_train, func, method, steps, t_h):
         # everything the backward reads is taken NOW: a second forward with
-        # another graph, x0 or alpha before this backward must not change its gradient
-        gr = func.graph_for(y0)
-        w, tag = func._weights_tensor()
-        ctx.w_csc = func.csr_weights(gr, w, tag, transpose=True)  # seen by autograd: never refreshed in place
-        ctx.gr = gr
-        ctx.sig = not func.opt.get('no_alpha_sigmoid', False)
-        ctx.alpha = func.alpha_train.detach().clone()
-        ctx.add_source = bool(func.opt.get('add_source', False))
-        ctx.x0 = func.stable_x0(y0).clone() if ctx.add_source else None
-        starts, stage_inputs = [], []
-        y = y0.detach().contiguous()
-        sol = [y]
-        j = 1
-        for ta, tb in steps:
-            starts.append(y)
-            ws = _Workspace()  # a fresh one per step: its stage inputs are kept for the backward
-            y = _fused_step(method, func, ta, tb - ta, tb, y, ws)
-            stage_inputs.append([ws[k] for k in ('a', 'b', 'c') if k in ws])
-            while j < len(t_h) and tb >= t_h[j]:
-                sol.append(y)
-                j += 1
-        ctx.func, ctx.method, ctx.steps, ctx.t_h = func, method, steps, t_h
+        # another graph, x0 or alpha before this backward must not change its gradient.
+        # The solve and its adjoint run in the graph's in-degree numbering when the module
+        # offers one (as the no-grad solves, ops.NodeLayout); the solution and the input
+        # gradient are in the caller's numbering.
+        lay = _node_layout(func, y0)
+        y0d = y0.detach().contiguous()
+        sol = torch.empty((len(t_h),) + tuple(y0.shape), dtype=y0.dtype, device=y0.device)
+        sol[0].copy_(y0d)
+        y = lay.to_internal(y0d) if lay is not None else y0d
+        if lay is not None:
+            func._layout = lay
+        try:
+            gr = func.graph_for(y0)
+            w, tag = func._weights_tensor()
+            ctx.w_csc = func.csr_weights(gr, w, tag, transpose=True)  # seen by autograd: never refreshed in place
+            ctx.gr = gr
+            ctx.sig = not func.opt.get('no_alpha_sigmoid', False)
+            ctx.alpha = func.alpha_train.detach().clone()
+            ctx.add_source = bool(func.opt.get('add_source', False))
+            ctx.x0 = func.stable_x0(y0).clone() if ctx.add_source else None
+            starts, stage_inputs = [], []
+            j = 1
+            for ta, tb in steps:
+                starts.append(y)
+                ws = _Workspace()  # a fresh one per step: its stage inputs are kept for the backward
+                y = _fused_step(method, func, ta, tb - ta, tb, y, ws)
+                stage_inputs.append([ws[k] for k in ('a', 'b', 'c') if k in ws])
+                while j < len(t_h) and tb >= t_h[j]:
+                    _to_user(y, sol[j], lay)
+                    j += 1
+        finally:
+            func._layout = None
+        ctx.func, ctx.method, ctx.steps, ctx.t_h, ctx.lay = func, method, steps, t_h, lay
         ctx.starts, ctx.stage_inputs = starts, stage_inputs
-        return torch.stack(sol, 0)
+        return sol
 
     @staticmethod
     def backward(ctx, g_sol):
         func, method, steps, t_h = ctx.func, ctx.method, ctx.steps, ctx.t_h
         g_sol = g_sol.contiguous()
+        lay = ctx.lay
         with torch.no_grad():
             gr, w_csc = ctx.gr, ctx.w_csc
             one = torch.ones((), dtype=torch.float32, device=g_sol.device)
@@ -518,9 +530,12 @@ class _LaplacianFixedGridFn(torch.autograd.Function):
             # launches' epilogues (gnpde_stage_epilogue_t dot_rows), summed once at the end
             drow = torch.zeros(g.numel() // g.shape[-1], dtype=torch.float64, device=g.device) \
                 if method == 'rk4' else None
+            def g_at(jj):  # an output time's gradient in the solve's numbering
+                return lay.to_internal(g_sol[jj]) if lay is not None else g_sol[jj]
+
             for n in range(len(steps) - 1, -1, -1):
                 for jj in out_at.get(n, []):
-                    g = g + g_sol[jj]
+                    g = g + g_at(jj)
                 ta, tb = steps[n]
                 dt = tb - ta
                 y = ctx.starts[n]
@@ -570,7 +585,9 @@ class _LaplacianFixedGridFn(torch.autograd.Function):
             if drow is not None:
                 ga = ops.sum_f64(drow, out=ga, accumulate=True)
             for jj in out_at.get(-1, []):
-                g = g + g_sol[jj]
+                g = g + g_at(jj)
+            if lay is not None:
+                g = lay.to_user(g)
             g = g + g_sol[0]
             if sig:
                 ga = ga * (a_dev * (1 - a_dev)).double()
