@@ -453,14 +453,130 @@ void dot_agg_kernel(const int4* __restrict__ items, int n_items, int4* heavy, in
   (void)dpart;
 }
 
+// ------------------------------------------------------------------ per-edge scores, destination-grouped softmax
+// attention_norm_idx 1: the softmax group of an edge is its destination, so its
+// statistics come from the CSC statistics kernel (gnpde_seg_softmax_f32 -> the
+// packed records {m[h], rl[h]} of every destination) and this pass only scores
+// the edges it gathers (score tiles, as above) and weights them:
+//   w_e = (1/H) sum_h exp(s_e,h - m[c,h]) * rl[c,h]
+// — the weights pass (gnpde_attn_weights_f32) and its [nnz] round trip fused into
+// K1; hub chunks merge exactly like K1's (the weights are final).
+template <int GL, int U, int NA, int S, int H, int STG>
+__global__ __launch_bounds__(256) void dot_dst_agg_kernel(const int4* __restrict__ items, int n_items, int4* heavy,
+                                                           int n_heavy, const int* __restrict__ col, DotArgs da,
+                                                           const float* __restrict__ rec, int C, Epi ep,
+                                                           float* __restrict__ partials) {
+  constexpr int RPW = kWave / GL;
+  constexpr int SL = GL;
+  constexpr int RF = stats_record_floats(H);
+  __shared__ float scs[kWavesPerBlock][RPW][SL * H];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int rs = lane / SL, sl = lane % SL;
+  const int wid = uniform(blockIdx.x * kWavesPerBlock + wv);
+  const int item = wid * RPW + rs;
+  if (wid * RPW >= n_items) return;
+  const bool live = item < n_items;
+  const int4 it = live ? items[item] : make_int4(0, 0, 0, -1);
+  const int row = it.x, beg = it.y, end = it.z, slot = it.w;
+  const int cc = sl * 4;
+  const bool owner = live && slot < 0 && cc < C;
+  const int base = rs * SL;
+  float* sc = scs[wv][rs];
+
+  EpiPre<4, float, stage_nout<STG>()> pre;
+  if (owner) epi_prefetch<4, STG, float>(ep, row, cc, pre);
+  float qv[4];
+  load_vec<4>(da.q + (int64_t)row * da.ldqk + 4 * (sl % NA), qv);
+  const int len = end - beg;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int e0 = 0; e0 < len; e0 += SL) {
+    const int n = min(SL, len - e0);
+    const int mc = sl < n ? col[beg + e0 + sl] : 0;
+    // the destination's record, issued with the score tile's loads
+    float rm[H], rr[H];
+    if constexpr (RF == 4 && H == 2) {
+      const float4 v = *reinterpret_cast<const float4*>(rec + (int64_t)mc * 4);
+      rm[0] = v.x; rm[1] = v.y; rr[0] = v.z; rr[1] = v.w;
+    } else {
+#pragma unroll
+      for (int h = 0; h < H; ++h) {
+        rm[h] = rec[(int64_t)mc * RF + h];
+        rr[h] = rec[(int64_t)mc * RF + H + h];
+      }
+    }
+    tile_scores<SL, NA, S, H>(qv, mc, n, base, sl, da, sc);
+    float s[H];
+    own_scores<H>(sc, sl, n, s);
+    float mw = 0.f;
+    if (sl < n) {
+#pragma unroll
+      for (int h = 0; h < H; ++h) mw = fmaf(__builtin_amdgcn_exp2f(s[h] - rm[h] * kLog2e), rr[h], mw);
+      constexpr float inv_h = 1.0f / (float)H;
+      mw *= inv_h;
+    }
+    for (int j = 0; j < n; j += U) {
+      float v[U][4];
+      float ww[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int jj = j + u;
+        const int src = base + (jj < n ? jj : 0);
+        const int c = __shfl(mc, src);
+        ww[u] = jj < n ? __shfl(mw, src) : 0.f;
+        if (jj < n && cc < C) {
+          load_vec<4>(ep.x + (int64_t)c * ep.ldx + cc, v[u]);
+        } else {
+#pragma unroll
+          for (int t = 0; t < 4; ++t) v[u][t] = 0.f;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc[t] = fmaf(ww[u], v[u][t], acc[t]);
+    }
+  }
+  if (n_heavy > 0) {  // hub chunks: write-through partials, merged in-launch by the last arrival (K1's)
+    const bool chunk = live && slot >= 0;
+    int anyc = 0;
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) anyc |= __shfl((int)chunk, r * SL);
+    if (anyc) {  // wave-uniform
+      const __amdgpu_buffer_rsrc_t rp = buf_rsrc(partials);
+      buf_store_wt<4>(rp, (chunk && cc < C) ? (uint32_t)(((int64_t)slot * C + cc) * 4) : kBufNone, acc);
+      hub_arrive_slots<4, GL, SL, RPW, STG, float>(heavy, n_heavy, chunk, slot, C, ep, partials);
+      if (chunk) return;
+    }
+  }
+  if (!live || slot >= 0) return;
+  const float a = (ep.flags & GNPDE_EPI_RHS) ? epi_alpha(ep) : 1.f;
+  const float b = (ep.flags & GNPDE_ADD_SOURCE) ? *ep.beta : 0.f;
+  double dpart = 0.0;
+  if (owner) epi_finish<4, STG, float>(ep, row, cc, acc, a, b, pre, &dpart);
+  (void)dpart;
+}
+
 template <int GL, int NA, int S, int H>
 static int launch_dot_nh(const int4* items, int64_t n_items, int4* heavy, int64_t n_heavy, const int* col,
-                         const DotArgs& da, int C, const Epi& ep, float* partials, hipStream_t s) {
+                         const DotArgs& da, const float* rec, int C, const Epi& ep, float* partials, hipStream_t s) {
   constexpr int RPW = kWave / GL;
   constexpr int U = GNPDE_FL_U;
   const unsigned grid = (unsigned)ceil_div(n_items, (int64_t)kWavesPerBlock * RPW);
   const int stg = epi_stage_kind(ep);
   const int nh = (int)n_heavy;
+  if (rec != nullptr) {  // destination-grouped softmax (norm_idx 1): statistics records given
+    if (stg == 1)
+      dot_dst_agg_kernel<GL, U, NA, S, H, 1><<<grid, kBlock, 0, s>>>(items, (int)n_items, heavy, nh, col, da, rec, C,
+                                                                      ep, partials);
+    else if (stg >= 2) {
+      set_error("attn_dot_rhs: only the plain RHS and single-output stage epilogues are fused");
+      return GNPDE_EUNSUPPORTED;
+    } else
+      dot_dst_agg_kernel<GL, U, NA, S, H, 0><<<grid, kBlock, 0, s>>>(items, (int)n_items, heavy, nh, col, da, rec, C,
+                                                                      ep, partials);
+    GNPDE_LAUNCH_CHECK();
+    return GNPDE_OK;
+  }
   if (stg == 1)
     dot_agg_kernel<GL, U, NA, S, H, 1><<<grid, kBlock, 0, s>>>(items, (int)n_items, heavy, nh, col, da, C, ep, partials);
   else if (stg >= 2) {
@@ -477,10 +593,10 @@ static int launch_dot_nh(const int4* items, int64_t n_items, int4* heavy, int64_
 // (att/4, heads) pairs: att in {8, 16, 32, 64}, heads in {1, 2, 4} dividing att/4
 template <int GL>
 static int launch_dot(int NA, int H, const int4* items, int64_t n_items, int4* heavy, int64_t n_heavy, const int* col,
-                      const DotArgs& da, int C, const Epi& ep, float* partials, hipStream_t s) {
+                      const DotArgs& da, const float* rec, int C, const Epi& ep, float* partials, hipStream_t s) {
 #define GNPDE_DOT(A, HH) \
   if (NA == A && H == HH) \
-    return launch_dot_nh<GL, A, (A / HH), HH>(items, n_items, heavy, n_heavy, col, da, C, ep, partials, s)
+    return launch_dot_nh<GL, A, (A / HH), HH>(items, n_items, heavy, n_heavy, col, da, rec, C, ep, partials, s)
   GNPDE_DOT(2, 1); GNPDE_DOT(2, 2);
   GNPDE_DOT(4, 1); GNPDE_DOT(4, 2); GNPDE_DOT(4, 4);
   GNPDE_DOT(8, 1); GNPDE_DOT(8, 2); GNPDE_DOT(8, 4);
@@ -508,8 +624,8 @@ int64_t gnpde_attn_dot_workspace_floats(int64_t heads, int64_t C, int64_t n_slot
 }
 
 int gnpde_attn_dot_rhs_f32(const int32_t* items, int64_t n_items, int32_t* heavy, int64_t n_heavy,
-                           const int32_t* col, const float* q, const float* k, int64_t ldqk,
-                           int64_t heads, int64_t dk, int64_t C, const float* x, int64_t ldx, const float* x0,
+                           const int32_t* col, const float* q, const float* k, int64_t ldqk, int64_t heads, int64_t dk,
+                           const float* dst_stats, int64_t C, const float* x, int64_t ldx, const float* x0,
                            int64_t ldx0, const float* alpha, const float* beta, int flags, float* f, int64_t ldf,
                            float* workspace, int64_t n_slots, const gnpde_stage_epilogue_t* stage, void* stream) {
   GNPDE_REQUIRE(gnpde_attn_dot_supported(heads, dk, C), GNPDE_EUNSUPPORTED,
@@ -526,6 +642,8 @@ int gnpde_attn_dot_rhs_f32(const int32_t* items, int64_t n_items, int32_t* heavy
                 "attn_dot_rhs: hub rows need heavy and the workspace");
   GNPDE_REQUIRE(n_slots * dot_partial_floats(heads, C) * 4 < (int64_t)kBufRecords, GNPDE_EUNSUPPORTED,
                 "attn_dot_rhs: %lld partial slots exceed the 4 GiB of 32-bit buffer offsets", (long long)n_slots);
+  GNPDE_REQUIRE(!dst_stats || aligned16(dst_stats), GNPDE_EUNSUPPORTED,
+                "attn_dot_rhs: the statistics records must be 16-byte aligned");
   GNPDE_REQUIRE(ldqk >= heads * dk && ldqk % 4 == 0 && aligned16(q) && aligned16(k), GNPDE_EUNSUPPORTED,
                 "attn_dot_rhs: q/k rows must be 16-byte aligned (ldqk %% 4 == 0)");
   GNPDE_REQUIRE(ldx % 4 == 0 && ldf % 4 == 0 && aligned16(x) && (!f || aligned16(f)) && aligned16(workspace),
@@ -552,9 +670,9 @@ int gnpde_attn_dot_rhs_f32(const int32_t* items, int64_t n_items, int32_t* heavy
   const int lanes = (int)(C / 4);
   const int NA = (int)(heads * dk / 4), H = (int)heads;
   hipStream_t s = as_stream(stream);
-  if (lanes <= 16) return launch_dot<16>(NA, H, it, n_items, hv, n_heavy, col, da, (int)C, ep, workspace, s);
-  if (lanes <= 32) return launch_dot<32>(NA, H, it, n_items, hv, n_heavy, col, da, (int)C, ep, workspace, s);
-  return launch_dot<64>(NA, H, it, n_items, hv, n_heavy, col, da, (int)C, ep, workspace, s);
+  if (lanes <= 16) return launch_dot<16>(NA, H, it, n_items, hv, n_heavy, col, da, dst_stats, (int)C, ep, workspace, s);
+  if (lanes <= 32) return launch_dot<32>(NA, H, it, n_items, hv, n_heavy, col, da, dst_stats, (int)C, ep, workspace, s);
+  return launch_dot<64>(NA, H, it, n_items, hv, n_heavy, col, da, dst_stats, (int)C, ep, workspace, s);
 }
 
 }  // extern "C"

@@ -63,7 +63,7 @@ SIGNATURES = {
                                       _vp, _vp, _int, _vp, _i64, _vp, _i64, ctypes.POINTER(StageEpilogue), _vp]),
     "gnpde_attn_dot_supported": (_int, [_i64, _i64, _i64]),
     "gnpde_attn_dot_workspace_floats": (_i64, [_i64, _i64, _i64]),
-    "gnpde_attn_dot_rhs_f32": (_int, [_vp, _i64, _vp, _i64, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _vp, _i64, _vp,
+    "gnpde_attn_dot_rhs_f32": (_int, [_vp, _i64, _vp, _i64, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _i64, _vp, _i64, _vp,
                                       _i64, _vp, _vp, _int, _vp, _i64, _vp, _i64, ctypes.POINTER(StageEpilogue), _vp]),
     "gnpde_rows_copy": (_int, [_vp, _i64, _i64, _vp, _vp, _vp, _vp]),
     "gnpde_seg_long_edges": (_int, []),

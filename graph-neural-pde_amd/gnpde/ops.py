@@ -885,7 +885,9 @@ def attn_rhs(g, ns, m, rl, norm_idx, x, x0=None, alpha=None, beta=None, rhs=True
     mr: the same statistics as packed records, softmax_stats(packed=True)).
     Reference scores under norm_idx 1 (fuse=True): the weights are computed
     inside K1 from (cs, m, rl) or (cs, mr) — same bits as the separate weights
-    pass.  Two heads with no statistics given: the packed records."""
+    pass.  Two heads with no statistics given: the packed records.  Per-edge
+    scaled_dot (fuse=True, shapes of gnpde_attn_dot_supported): one fused pass
+    (attn_dot_rhs) for either grouping."""
     if fuse and norm_idx == 1 and ns.mode == _lib.SCORE_REFERENCE and x.dtype == torch.float32:
         if m is None and mr is None:
             if ns.heads == 2:
@@ -895,9 +897,12 @@ def attn_rhs(g, ns, m, rl, norm_idx, x, x0=None, alpha=None, beta=None, rhs=True
         w = RefDstWeights(ns.cs, m, rl, ns.heads, mr=mr)
         return spmm_rhs(g, w, x, x0=x0, alpha=alpha, beta=beta, rhs=rhs, alpha_sigmoid=alpha_sigmoid,
                         add_source=add_source, out=out, stage=stage)
-    if fuse and norm_idx == 0 and ns.mode == _lib.SCORE_DOT and x.dtype == torch.float32:
+    if fuse and ns.mode == _lib.SCORE_DOT and x.dtype == torch.float32 and \
+            _lib.fn("gnpde_attn_dot_supported")(ns.heads, ns.dk, x.shape[-1]):
+        if norm_idx == 1 and mr is None:
+            _, _, mr = softmax_stats(g, ns, 1, seg=seg, packed=True)
         r = attn_dot_rhs(g, ns, x, x0=x0, alpha=alpha, beta=beta, rhs=rhs, alpha_sigmoid=alpha_sigmoid,
-                         add_source=add_source, out=out, stage=stage)
+                         add_source=add_source, out=out, stage=stage, mr=mr if norm_idx == 1 else None)
         if r is not NotImplemented:
             return r
     w = attn_weights(g, ns, m, rl, norm_idx, seg=seg)
@@ -906,11 +911,14 @@ def attn_rhs(g, ns, m, rl, norm_idx, x, x0=None, alpha=None, beta=None, rhs=True
 
 
 def attn_dot_rhs(g, ns, x, x0=None, alpha=None, beta=None, rhs=True, alpha_sigmoid=True, add_source=False,
-                 out=None, stage=None):
-    """The per-edge scaled_dot RHS under source-grouped softmax (norm_idx 0) in
-    one online-softmax aggregation pass (gnpde_attn_dot_rhs_f32, csrc/flash.hip):
-    no [nnz] weights, no separate softmax launch.  NotImplemented for shapes
-    outside the fused kernel (gnpde_attn_dot_supported)."""
+                 out=None, stage=None, mr=None):
+    """The per-edge scaled_dot RHS in one aggregation pass (gnpde_attn_dot_rhs_f32,
+    csrc/flash.hip): under source-grouped softmax (norm_idx 0; mr None) the pass
+    forms each row's softmax statistics itself; under destination-grouped softmax
+    (norm_idx 1) ``mr`` holds the destinations' packed statistics records
+    (softmax_stats(..., packed=True)) and the pass weights every scored edge with
+    them.  No [nnz] weights.  NotImplemented for shapes outside the fused kernel
+    (gnpde_attn_dot_supported)."""
     xr = _rows(x, "x")
     C = xr.shape[1]
     H, dk = ns.heads, ns.dk
@@ -946,7 +954,7 @@ def attn_dot_rhs(g, ns, x, x0=None, alpha=None, beta=None, rhs=True, alpha_sigmo
         ws = torch.empty(nws, dtype=torch.float32, device=dev)
     plan.order_launch(dev)
     rc = _lib.call_rc("gnpde_attn_dot_rhs_f32", _ptr(plan.items), plan.n_items, _ptr(plan.heavy), plan.n_heavy,
-                      _ptr(g.csr.col), _ptr(ns.q), _ptr(ns.k), ns.ldqk, H, dk, C, _ptr(xr), C,
+                      _ptr(g.csr.col), _ptr(ns.q), _ptr(ns.k), ns.ldqk, H, dk, _ptr(mr), C, _ptr(xr), C,
                       _ptr(x0r), C, _ptr(a), _ptr(b), _flags(rhs, alpha_sigmoid, add_source), _ptr(out), C, _ptr(ws),
                       plan.n_slots, st, _stream(dev))
     if rc == _lib.EUNSUPPORTED:

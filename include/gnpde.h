@@ -282,14 +282,20 @@ int gnpde_attn_ref_rhs_f32(const int32_t* items, int64_t n_items, int32_t* heavy
  * Shapes:
  * gnpde_attn_dot_supported(heads, dk, C) != 0 (heads in {1, 2, 4}, dk % 4 ==
  * 0, heads*dk in {8, 16, 32, 64}, C % 4 == 0, C <= 256); otherwise
- * GNPDE_EUNSUPPORTED.  Exponentials in base 2 (1-2 ulp from expf).         */
+ * GNPDE_EUNSUPPORTED.  Exponentials in base 2 (1-2 ulp from expf).
+ * dst_stats != NULL: destination-grouped softmax (attention_norm_idx 1)
+ * instead — the packed statistics records of every destination
+ * (GNPDE_STATS_RECORD_FLOATS(heads) floats: m[h] then rl[h], from
+ * gnpde_seg_softmax_f32 over the CSC, 16-byte aligned) weight each scored
+ * edge, w_e = (1/H) sum_h exp(s_e,h - m[c,h]) rl[c,h]: replaces
+ * gnpde_attn_weights_f32 + gnpde_spmm_rhs_f32.                              */
 int gnpde_attn_dot_supported(int64_t heads, int64_t dk, int64_t C);
 int64_t gnpde_attn_dot_workspace_floats(int64_t heads, int64_t C, int64_t n_slots);
 int gnpde_attn_dot_rhs_f32(const int32_t* items, int64_t n_items, int32_t* heavy, int64_t n_heavy,
-                           const int32_t* col, const float* q, const float* k, int64_t ldqk,
-                           int64_t heads, int64_t dk, int64_t C, const float* x, int64_t ldx, const float* x0,
-                           int64_t ldx0, const float* alpha, const float* beta, int flags, float* f, int64_t ldf,
-                           float* workspace, int64_t n_slots, const gnpde_stage_epilogue_t* stage, void* stream);
+                           const int32_t* col, const float* q, const float* k, int64_t ldqk, int64_t heads, int64_t dk,
+                           const float* dst_stats, int64_t C, const float* x, int64_t ldx, const float* x0, int64_t ldx0,
+                           const float* alpha, const float* beta, int flags, float* f, int64_t ldf, float* workspace,
+                           int64_t n_slots, const gnpde_stage_epilogue_t* stage, void* stream);
 
 /* ---------------------------------------------------------------- attention
  * Node-level projection on the matrix cores (K % 16 == 0, K <= 128: exact

@@ -185,3 +185,25 @@ def test_flash_two_streams_share_the_plan():
     torch.cuda.synchronize()
     for f, k in outs:
         assert torch.equal(f, ref) and torch.equal(k, kref)
+
+
+@pytest.mark.parametrize("C,h,att", [(16, 1, 8), (64, 2, 16), (128, 2, 32), (160, 4, 32), (256, 2, 64), (100, 4, 64)])
+@pytest.mark.parametrize("B", [1, 2])
+def test_flash_dst_rhs_vs_oracle(C, h, att, B):
+    """Destination-grouped softmax (norm_idx 1): the CSC statistics records weight
+    every edge the fused pass scores (the weights pass and K1 in one launch),
+    against the oracle and the unfused path (CSR hub chunks merged as K1's)."""
+    N, E = 1500, 24000
+    ei, x, x0, Wq, bq, Wk, bk = case(N, E, C, att, seed=3 * C + h + B, B=B)
+    g = ops.GraphCSR(T(ei), N)
+    assert g.csr.plan.n_heavy >= 1
+    ns = ops.node_scores(g, T(x), T(Wq), T(bq), T(Wk), T(bk), h, 'scaled_dot', 'per_edge')
+    _, _, mr = ops.softmax_stats(g, ns, 1, packed=True)
+    a, b = torch.tensor(-0.4, device=DEV), torch.tensor(0.7, device=DEV)
+    f = ops.attn_dot_rhs(g, ns, T(x), T(x0), a, b, add_source=True, mr=mr)
+    assert f is not NotImplemented
+    want = O.transformer_rhs(ei, x, x0, Wq, bq, Wk, bk, h, 1, -0.4, 0.7, score_mode='per_edge', add_source=True)
+    assert rel(f, want) <= RTOL
+    fu = ops.attn_rhs(g, ns, None, None, 1, T(x), T(x0), a, b, add_source=True, fuse=False)
+    assert rel(f, fu.double().cpu().numpy()) <= RTOL
+    assert torch.equal(f, ops.attn_rhs(g, ns, None, None, 1, T(x), T(x0), a, b, add_source=True))
