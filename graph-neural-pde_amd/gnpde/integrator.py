@@ -467,17 +467,25 @@ class _LaplacianFixedGridFn(torch.autograd.Function):
         lay = _node_layout(func, y0)
         y0d = y0.detach().contiguous()
         sol = torch.empty((len(t_h),) + tuple(y0.shape), dtype=y0.dtype, device=y0.device)
-        sol[0].copy_(y0d)
-        y = lay.to_internal(y0d) if lay is not None else y0d
-        if lay is not None:
+        if lay is not None:  # sol[0] = y0 and the solve's copy in one pass
+            y = torch.empty_like(y0d)
+            _entry_copy(y0d, y, sol[0], lay.order)
             func._layout = lay
+        else:
+            sol[0].copy_(y0d)
+            y = y0d
+        # the backward's combination coefficients need a = sigma(alpha) on the host: copied
+        # now, behind an event, so the backward does not drain the queue to read it
+        sig = not func.opt.get('no_alpha_sigmoid', False)
+        ctx.alpha = func.alpha_train.detach().clone()
+        ctx.a_dev = torch.sigmoid(ctx.alpha) if sig else ctx.alpha
+        ctx.a_host = _host_scalar(ctx.a_dev)
         try:
             gr = func.graph_for(y0)
             w, tag = func._weights_tensor()
             ctx.w_csc = func.csr_weights(gr, w, tag, transpose=True)  # seen by autograd: never refreshed in place
             ctx.gr = gr
-            ctx.sig = not func.opt.get('no_alpha_sigmoid', False)
-            ctx.alpha = func.alpha_train.detach().clone()
+            ctx.sig = sig
             ctx.add_source = bool(func.opt.get('add_source', False))
             ctx.x0 = func.stable_x0(y0).clone() if ctx.add_source else None
             starts, stage_inputs = [], []
@@ -504,10 +512,9 @@ class _LaplacianFixedGridFn(torch.autograd.Function):
         with torch.no_grad():
             gr, w_csc = ctx.gr, ctx.w_csc
             one = torch.ones((), dtype=torch.float32, device=g_sol.device)
-            alpha = ctx.alpha
             sig = ctx.sig
-            a_dev = torch.sigmoid(alpha) if sig else alpha
-            a = float(a_dev)  # one host read per backward: the combination coefficients
+            a_dev = ctx.a_dev
+            a = ctx.a_host()  # the combination coefficients (copied to the host in the forward)
             add_source = ctx.add_source
             x0 = ctx.x0
 
@@ -524,18 +531,21 @@ class _LaplacianFixedGridFn(torch.autograd.Function):
                 while j < len(t_h) and tb >= t_h[j]:
                     out_at.setdefault(n, []).append(j)
                     j += 1
-            g = torch.zeros_like(ctx.starts[0])
+            s0 = ctx.starts[0]
+            g = None  # the running gradient (None: still zero)
             nfe = getattr(func, 'nfe', None)
             # rk4: the alpha gradient's per-row terms <u_i, x_i> accumulate in the transpose
             # launches' epilogues (gnpde_stage_epilogue_t dot_rows), summed once at the end
-            drow = torch.zeros(g.numel() // g.shape[-1], dtype=torch.float64, device=g.device) \
+            drow = torch.zeros(s0.numel() // s0.shape[-1], dtype=torch.float64, device=s0.device) \
                 if method == 'rk4' else None
             def g_at(jj):  # an output time's gradient in the solve's numbering
                 return lay.to_internal(g_sol[jj]) if lay is not None else g_sol[jj]
 
             for n in range(len(steps) - 1, -1, -1):
                 for jj in out_at.get(n, []):
-                    g = g + g_at(jj)
+                    g = g_at(jj) if g is None else g + g_at(jj)
+                if g is None:
+                    g = torch.zeros_like(s0)
                 ta, tb = steps[n]
                 dt = tb - ta
                 y = ctx.starts[n]
@@ -584,6 +594,8 @@ class _LaplacianFixedGridFn(torch.autograd.Function):
                 func.nfe = nfe  # the recomputed stages are not new RHS evaluations
             if drow is not None:
                 ga = ops.sum_f64(drow, out=ga, accumulate=True)
+            if g is None:
+                g = torch.zeros_like(s0)
             for jj in out_at.get(-1, []):
                 g = g + g_at(jj)
             if lay is not None:
@@ -595,6 +607,24 @@ class _LaplacianFixedGridFn(torch.autograd.Function):
         galpha = ga.to(func.alpha_train.dtype).reshape(func.alpha_train.shape) if ctx.needs_input_grad[1] else None
         gbeta = gb.to(func.beta_train.dtype).reshape(func.beta_train.shape) if ctx.needs_input_grad[2] else None
         return gy, galpha, gbeta, None, None, None, None
+
+
+def _host_scalar(v):
+    """A device scalar's value for the host later: an asynchronous copy into pinned
+    memory behind an event; the returned callable waits for that event only (not
+    for the work queued after it) and returns the float."""
+    if not v.is_cuda:
+        val = float(v)
+        return lambda: val
+    h = torch.empty(v.shape, dtype=v.dtype, pin_memory=True)
+    h.copy_(v, non_blocking=True)
+    ev = torch.cuda.Event()
+    ev.record()
+
+    def get():
+        ev.synchronize()
+        return float(h)
+    return get
 
 
 def _node_layout(func, y0):
