@@ -17,7 +17,19 @@
 namespace gnpde {
 
 typedef float f32x16w __attribute__((ext_vector_type(16)));
-constexpr int kWgWaves = 512;  // row ranges (wavefronts) per tile group
+constexpr int kWgWaves = 512;  // most row ranges (wavefronts) per tile group
+constexpr int64_t kWgRowsMin = 128;                 // fewest rows a range is given
+constexpr int64_t kWgWorkspaceMax = 64ll << 20;     // partials budget (bytes) when M x K is large
+
+// Row ranges for R rows and an M x K result: enough wavefronts to fill the chip on a
+// large R, no more than R / kWgRowsMin, and no more partial tiles than kWgWorkspaceMax
+// holds (a fixed 512 cost 128 MiB of scratch and traffic at M = K = 256);
+// a multiple of the waves per workgroup.
+static int64_t wgrad_waves(int64_t R, int64_t M, int64_t K) {
+  int64_t nw = std::min<int64_t>(kWgWaves, std::max<int64_t>(1, ceil_div(R, kWgRowsMin)));
+  nw = std::min<int64_t>(nw, std::max<int64_t>(1, kWgWorkspaceMax / (M * K * (int64_t)sizeof(float))));
+  return ceil_div(nw, kWavesPerBlock) * kWavesPerBlock;
+}
 
 template <int TM, int TK>
 __global__ __launch_bounds__(256) void wgrad_kernel(const float* __restrict__ gy, int64_t R, int M, int64_t ldg,
@@ -89,14 +101,17 @@ using namespace gnpde;
 
 extern "C" {
 
-size_t gnpde_linear_wgrad_workspace_bytes(int64_t M, int64_t K) { return (size_t)kWgWaves * M * K * sizeof(float); }
+size_t gnpde_linear_wgrad_workspace_bytes(int64_t R, int64_t M, int64_t K) {
+  if (R < 0 || M < 1 || K < 1) return 0;
+  return (size_t)wgrad_waves(R, M, K) * M * K * sizeof(float);
+}
 
 int gnpde_linear_wgrad_f32(const float* gy, int64_t R, int64_t M, int64_t ldg, const float* x, int64_t K, int64_t ldx,
                            float* gW, int64_t ldw, void* workspace, size_t workspace_bytes, void* stream) {
   GNPDE_REQUIRE(gW && (R == 0 || (gy && x)), GNPDE_EINVAL, "linear_wgrad: NULL pointer");
   GNPDE_REQUIRE(R >= 0 && M >= 1 && K >= 1 && ldg >= M && ldx >= K && ldw >= K && M <= 65536 && K <= 65536,
                 GNPDE_EINVAL, "linear_wgrad: bad sizes");
-  GNPDE_REQUIRE(workspace && workspace_bytes >= gnpde_linear_wgrad_workspace_bytes(M, K), GNPDE_EINVAL,
+  GNPDE_REQUIRE(workspace && workspace_bytes >= gnpde_linear_wgrad_workspace_bytes(R, M, K), GNPDE_EINVAL,
                 "linear_wgrad: workspace smaller than gnpde_linear_wgrad_workspace_bytes");
   hipStream_t s = as_stream(stream);
   float* part = static_cast<float*>(workspace);
@@ -105,9 +120,10 @@ int gnpde_linear_wgrad_f32(const float* gy, int64_t R, int64_t M, int64_t ldg, c
   const int TK = KT >= 4 ? 4 : (KT >= 2 ? 2 : 1);
   const int tgm = (int)ceil_div(MT, TM), tgk = (int)ceil_div(KT, TK);
   // row pairs spread evenly over the wavefronts (an even count per wave keeps the pairs aligned)
-  int64_t rpw = ceil_div(R, (int64_t)kWgWaves);
+  const int64_t nw = wgrad_waves(R, M, K);
+  int64_t rpw = ceil_div(R, nw);
   rpw += rpw & 1;
-  const dim3 grid((unsigned)(kWgWaves / kWavesPerBlock), (unsigned)(tgm * tgk));
+  const dim3 grid((unsigned)(nw / kWavesPerBlock), (unsigned)(tgm * tgk));
 #define GNPDE_WG(A, B)                                                                                         \
   wgrad_kernel<A, B><<<grid, kBlock, 0, s>>>(gy, R, (int)M, ldg, x, (int)K, ldx, part, std::max<int64_t>(rpw, 2), \
                                              tgk)
@@ -120,7 +136,7 @@ int gnpde_linear_wgrad_f32(const float* gy, int64_t R, int64_t M, int64_t ldg, c
 #undef GNPDE_WG
   GNPDE_LAUNCH_CHECK();
   const int64_t MK = M * K;
-  wgrad_reduce_kernel<<<(unsigned)ceil_div(MK, (int64_t)kBlock), kBlock, 0, s>>>(part, kWgWaves, MK, (int)K, gW, ldw);
+  wgrad_reduce_kernel<<<(unsigned)ceil_div(MK, (int64_t)kBlock), kBlock, 0, s>>>(part, (int)nw, MK, (int)K, gW, ldw);
   GNPDE_LAUNCH_CHECK();
   return GNPDE_OK;
 }

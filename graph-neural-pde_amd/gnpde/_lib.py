@@ -68,7 +68,7 @@ SIGNATURES = {
     "gnpde_rows_copy": (_int, [_vp, _i64, _i64, _vp, _vp, _vp, _vp]),
     "gnpde_seg_long_edges": (_int, []),
     "gnpde_linear_f32": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _vp]),
-    "gnpde_linear_wgrad_workspace_bytes": (_size, [_i64, _i64]),
+    "gnpde_linear_wgrad_workspace_bytes": (_size, [_i64, _i64, _i64]),
     "gnpde_linear_wgrad_f32": (_int, [_vp, _i64, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _vp, _size, _vp]),
     "gnpde_keysum_workspace_bytes": (_size, [_i64, _i64, _i64, _i64]),
     "gnpde_ref_scores_f32": (_int, [_vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _vp, _vp,

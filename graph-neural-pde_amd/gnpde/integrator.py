@@ -483,7 +483,11 @@ class _LaplacianFixedGridFn(torch.autograd.Function):
         try:
             gr = func.graph_for(y0)
             w, tag = func._weights_tensor()
-            ctx.w_csc = func.csr_weights(gr, w, tag, transpose=True)  # seen by autograd: never refreshed in place
+            # a private CSC-order copy: grad mode is off inside a Function's forward,
+            # so the module's cached buffer counts as no_grad-made and a later no_grad call with
+            # new weights would refresh it in place under this node's pending backward
+            src = w.detach().float() if w.dtype != torch.float32 else w.detach()
+            ctx.w_csc = gr.gather_weights(src, transpose=True)
             ctx.gr = gr
             ctx.sig = sig
             ctx.add_source = bool(func.opt.get('add_source', False))

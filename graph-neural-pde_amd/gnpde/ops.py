@@ -725,7 +725,7 @@ def linear_wgrad(gy, x):
     R, M = gyr.shape
     K = xr.shape[1]
     out = torch.empty(M, K, dtype=torch.float32, device=xr.device)
-    nb = _lib.fn("gnpde_linear_wgrad_workspace_bytes")(M, K)
+    nb = _lib.fn("gnpde_linear_wgrad_workspace_bytes")(R, M, K)
     ws = torch.empty(nb, dtype=torch.uint8, device=xr.device)
     _lib.call("gnpde_linear_wgrad_f32", _ptr(gyr), R, M, M, _ptr(xr), K, K, _ptr(out), K, _ptr(ws), nb,
               _stream(xr.device))

@@ -312,10 +312,11 @@ int gnpde_linear_f32(const float* x, int64_t R, int64_t K, int64_t ldx, const fl
  * (gy [R, M] ld ldg = dL/d[q | k], x [R, K] ld ldx; gW [M, K] ld ldw), the
  * backward of nn.Linear's weight for the Q / K of
  * function_transformer_attention.py:224-225.  fp32 matrix cores
- * (v_mfma_f32_32x32x2_f32), the rows split over 512 wavefronts whose partial
- * tiles are summed in wave order (deterministic).  workspace:
- * gnpde_linear_wgrad_workspace_bytes(M, K) bytes.                            */
-size_t gnpde_linear_wgrad_workspace_bytes(int64_t M, int64_t K);
+ * (v_mfma_f32_32x32x2_f32), the rows split over up to 512 wavefronts (at least
+ * 128 rows each, and no more partial tiles than 64 MiB hold) whose partial tiles
+ * are summed in wave order (deterministic).  workspace:
+ * gnpde_linear_wgrad_workspace_bytes(R, M, K) bytes.                         */
+size_t gnpde_linear_wgrad_workspace_bytes(int64_t R, int64_t M, int64_t K);
 int gnpde_linear_wgrad_f32(const float* gy, int64_t R, int64_t M, int64_t ldg, const float* x, int64_t K, int64_t ldx,
                            float* gW, int64_t ldw, void* workspace, size_t workspace_bytes, void* stream);
 

@@ -264,6 +264,53 @@ def transformer_rhs(edge_index, x, x0, Wq, bq, Wk, bk, heads, norm_idx, alpha_tr
     return rhs_epilogue(ax, x, x0, alpha_train, beta_train, add_source, no_alpha_sigmoid)
 
 
+def transformer_rhs_f32(edge_index, x, Wq, bq, Wk, bk, heads, norm_idx, alpha_train, score_mode='per_edge'):
+    """The transformer RHS in FLOAT32 arithmetic, in the reference's operation
+    order — the precision the reference itself runs in (the torch fp32 CPU path):
+    nn.Linear Q/K (function_transformer_attention.py:224-225, x W^T + b in fp32),
+    the gathers (:240-244), ``(src * dst_k).sum(dk) / sqrt(dk)`` per edge and head
+    (upstream GRAND's scaled_dot; the fork's global key sum with
+    score_mode='reference', :249), utils.softmax in fp32 (src/utils.py:116-127:
+    group max, exp(s - max), group sum, / (sum + 1e-16)), the head mean (:34) and
+    the aggregation + epilogue (:33-41, :52-59), every array float32.
+
+    Not a parity target: the yardstick of how far an fp32 evaluation of the
+    reference's own formula sits from the float64 restatement above on the same
+    inputs.  At score ranges in the hundreds the fp32 score alone carries a
+    relative error of ~1e-5 in the output (tests/test_gpu_flash.py)."""
+    f32 = np.float32
+    edge_index = np.asarray(edge_index)
+    x = np.asarray(x, f32)
+    B, N, C = x.shape
+    q = x @ np.asarray(Wq, f32).T + np.asarray(bq, f32)
+    k = x @ np.asarray(Wk, f32).T + np.asarray(bk, f32)
+    A = q.shape[-1]
+    dk = A // heads
+    inv = f32(1.0 / np.sqrt(dk))
+    a = f32(alpha_value(alpha_train, False))
+    out = np.empty_like(x)
+    for b in range(B):
+        src, dst = edge_index[b, 0], edge_index[b, 1]
+        qs = q[b][src].reshape(-1, heads, dk)
+        kd = k[b][dst].reshape(-1, heads, dk)
+        if score_mode == 'reference':
+            s = (qs * kd.sum(axis=0, dtype=f32)[None]).sum(axis=2, dtype=f32) * inv
+        else:
+            s = (qs * kd).sum(axis=2, dtype=f32) * inv
+        g = edge_index[b, norm_idx]
+        mx = np.full((N, heads), -np.inf, f32)
+        np.maximum.at(mx, g, s)
+        ex = np.exp(s - mx[g]).astype(f32)
+        sm = np.zeros((N, heads), f32)
+        np.add.at(sm, g, ex)
+        att = ex / (sm[g] + f32(1e-16))
+        w = att.mean(axis=1, dtype=f32)
+        ax = np.zeros((N, C), f32)
+        np.add.at(ax, src, w[:, None] * x[b][dst])
+        out[b] = a * (ax - x[b])
+    return out
+
+
 # --------------------------------------------------------------------------- graph preparation
 def add_remaining_self_loops(edge_index, edge_weight, fill_value, num_nodes):
     """Intended semantics of src/utils.py:16-42 (the fork's batched rewrite

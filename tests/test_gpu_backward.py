@@ -414,9 +414,10 @@ def test_fused_fixed_grid_backward_full_size_garxiv():
 
 
 def test_fused_backward_reads_its_forward_state():
-    """two forwards with different x0 (and alpha, and graph
-    weights) before ONE backward — each backward uses the operands of its own
-    forward, so the summed gradient equals the gradients taken one at a time."""
+    """two forwards with different x0, alpha AND graph
+    weights (a new edge_weight tensor on the same edge_index) before ONE
+    backward — each backward uses the operands of its own forward, so the summed
+    gradient equals the gradients taken one at a time."""
     from gnpde import synthetic
     N, E, C = 2000, 16000, 32
     ei, w = synthetic.rw_graph(N, E, seed=8, device=DEV)
@@ -430,12 +431,14 @@ def test_fused_backward_reads_its_forward_state():
     x0s = [torch.randn(1, N, C, generator=gen, device=DEV) for _ in range(2)]
     gs = [torch.randn(1, N, C, generator=gen, device=DEV) for _ in range(2)]
     alphas = [0.4, -0.3]
+    wts = [w, w * (0.5 + torch.rand(w.shape, generator=gen, device=DEV))]
     t = torch.tensor([0.0, 0.5], device=DEV)
 
     def fwd(k):
         with torch.no_grad():
             func.alpha_train.fill_(alphas[k])
         func.x0 = x0s[k]
+        func.edge_weight = wts[k]
         xi = xs[k].clone().requires_grad_(True)
         return xi, gnpde.odeint(func, xi, t, method='rk4', options={'step_size': 0.125})[1]
 

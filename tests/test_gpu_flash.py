@@ -71,24 +71,44 @@ def test_flash_rhs_vs_oracle(C, h, att, B):
     assert rel(ax, 2.0 * wa + x) <= RTOL
 
 
-def test_flash_large_scores_and_repeats():
-    """Wide score ranges (the running max moves within a row and across a hub's
-    chunks: rescaling by exp2(M_old - M_new) underflows to 0 for far-away
-    edges) stay within tolerance; two launches give the same bits.  (wscale 0.35
-    gives scores of tens; at wscale 1 they reach hundreds and the fp32 score
-    itself — fused or not — carries ~1e-5 of relative weight error.)"""
+@pytest.mark.parametrize("norm_idx", [0, 1])
+def test_flash_large_scores_and_repeats(norm_idx):
+    """Wide score ranges (wscale 1: scores reach ~650; the running max moves within
+    a row and across a hub's chunks, rescaling by exp2(M_old - M_new) underflows
+    to 0 for far-away edges) — re-pinned at the full range.
+
+    At scores in the hundreds an fp32 evaluation of q_src . k_dst / sqrt(dk)
+    carries ~eps * |s| ~ 4e-5 of absolute score error, i.e. that much relative
+    error on a weight, whoever computes it: the reference's own formula run in
+    float32 as the reference runs it (O.transformer_rhs_f32: nn.Linear, the
+    per-edge sum, utils.softmax, all fp32) sits 1.19e-5 (seed 7; 1.37-1.39e-5 on
+    seeds 1-3) from the float64 restatement on this case.  Tolerance: the
+    reference's own fp32 distance, measured here on the same inputs (floored at
+    RTOL); the fused kernel (measured 1.03e-5 in round 3) and the unfused K2 + K1
+    path must each sit no farther from fp64 than the reference's fp32 run does.
+    Two launches give the same bits."""
     N, E, C, h, att = 3000, 50000, 128, 2, 32
-    ei, x, x0, Wq, bq, Wk, bk = case(N, E, C, att, seed=7, wscale=0.35)
+    ei, x, x0, Wq, bq, Wk, bk = case(N, E, C, att, seed=7, wscale=1.0)
+    s = O.attention_scores(x, ei, Wq, bq, Wk, bk, h, score_mode='per_edge')
+    assert np.abs(s).max() > 300.0  # the case does exercise near-hard softmax groups
+    want = O.transformer_rhs(ei, x, None, Wq, bq, Wk, bk, h, norm_idx, 0.8, 0.0, score_mode='per_edge')
+    d_ref32 = rel(O.transformer_rhs_f32(ei, x, Wq, bq, Wk, bk, h, norm_idx, 0.8), want)
+    tol = max(RTOL, d_ref32)
     g = ops.GraphCSR(T(ei), N)
     ns = ops.node_scores(g, T(x), T(Wq), T(bq), T(Wk), T(bk), h, 'scaled_dot', 'per_edge')
     a = torch.tensor(0.8, device=DEV)
-    f1 = ops.attn_dot_rhs(g, ns, T(x), alpha=a)
-    f2 = ops.attn_dot_rhs(g, ns, T(x), alpha=a)
+    mr = ops.softmax_stats(g, ns, 1, packed=True)[2] if norm_idx == 1 else None
+    f1 = ops.attn_dot_rhs(g, ns, T(x), alpha=a, mr=mr)
+    f2 = ops.attn_dot_rhs(g, ns, T(x), alpha=a, mr=mr)
+    assert f1 is not NotImplemented
     assert torch.equal(f1, f2)
-    want = O.transformer_rhs(ei, x, None, Wq, bq, Wk, bk, h, 0, 0.8, 0.0, score_mode='per_edge')
-    assert rel(f1, want) <= RTOL
-    s = O.attention_scores(x, ei, Wq, bq, Wk, bk, h, score_mode='per_edge')
-    assert np.abs(s).max() > 10.0  # the case does exercise sharp softmax groups
+    d_fused = rel(f1, want)
+    fu = ops.attn_rhs(g, ns, None, None, norm_idx, T(x), alpha=a, fuse=False)
+    d_unfused = rel(fu, want)
+    print("per-edge norm_idx %d, max|s| %.0f: fp32 reference %.3e, fused %.3e, unfused %.3e from fp64"
+          % (norm_idx, np.abs(s).max(), d_ref32, d_fused, d_unfused))
+    assert d_fused <= tol, (d_fused, d_ref32)
+    assert d_unfused <= tol, (d_unfused, d_ref32)
 
 
 def test_flash_default_dropin_path_and_stage():
