@@ -145,8 +145,8 @@ __device__ __forceinline__ void hub_combine(int row, int first, int nch, int C, 
       for (int t = 0; t < VEC; ++t) s[t] += __shfl_xor(s[t], o);
     if (g == 0 && live) epilogue_store<VEC, STG, T>(ep, row, cc, s, a, b, &dpart);
   }
-  if constexpr (stage_dot<STG>() && sizeof(T) == 4)
-    if (ep.st.dot_rows) epi_dot_store<GL>(ep, row, dpart, lane == 0);  // wave-uniform
+  if constexpr (stage_rowsum<STG, T>())
+    if (ep.st.dot_rows || ep.st.err_rows) epi_rowsum_store<GL>(ep, row, dpart, lane == 0);  // wave-uniform
 }
 
 // A chunk wave whose write-through partial stores are issued: drain them, take
@@ -254,7 +254,7 @@ __global__ __launch_bounds__(256) void agg_kernel(const int4* __restrict__ items
   const int row = it.x, beg = it.y, end = it.z, slot = it.w;
   const bool owner = live && slot < 0 && g == 0;
 
-  EpiPre<VEC, T, stage_nout<STG>()> pre[PRE ? NCH : 1];
+  EpiPre<VEC, T, STG> pre[PRE ? NCH : 1];
   if constexpr (PRE) {
     if (owner) {
 #pragma unroll
@@ -382,8 +382,8 @@ __global__ __launch_bounds__(256) void agg_kernel(const int4* __restrict__ items
     }
   }
   // the row's owner lanes (g == 0: lanes [rs*SL, rs*SL + GL)) are all here
-  if constexpr (stage_dot<STG>() && sizeof(T) == 4 && (GL & (GL - 1)) == 0)
-    if (ep.st.dot_rows) epi_dot_store<GL>(ep, row, dpart, gl == 0);
+  if constexpr (stage_rowsum<STG, T>())
+    if (ep.st.dot_rows || ep.st.err_rows) epi_rowsum_store_any<GL>(ep, row, dpart, rs * SL, gl == 0);
 }
 
 // Hub rows combined after the aggregation launch (GNPDE_HUB_FIXUP=1): one wavefront per hub.
@@ -419,7 +419,18 @@ static int launch_agg_cfg(const int4* items, int64_t n_items, int4* heavy, int64
   if (n_items > 0) {
     // the one-output adjoint stages: fp32 plain weights only (the transposed aggregation)
     if (stg == 3 && !(std::is_same<WP, PlainWeights>::value && sizeof(T) == 4)) stg = 2;
-    if (stg == 3)
+    if (stg == 4) {
+      // the adaptive solvers' wide epilogue: plain weights only (the Laplacian RHS and
+      // precomputed attention weights); the callers apply it after the other policies
+      if constexpr (std::is_same<WP, PlainWeights>::value) {
+        agg_kernel<VEC, GL, NCH, U, RPW, 4, PlainWeights, T><<<grid, kBlock, 0, s>>>(
+            items, (int)n_items, heavy, nh, col, as_plain(wp), C, ep, partials);
+      } else {
+        set_error("rhs: the wide (adaptive-solver) stage epilogue is fused with plain weights only; "
+                  "apply it with gnpde_stage_apply_*");
+        return GNPDE_EUNSUPPORTED;
+      }
+    } else if (stg == 3)
       agg_kernel<VEC, GL, NCH, U, RPW, 3, PlainWeights, float><<<grid, kBlock, 0, s>>>(
           items, (int)n_items, heavy, nh, col, as_plain(wp), C, ep, partials);
     else if (stg == 1)
@@ -436,7 +447,7 @@ static int launch_agg_cfg(const int4* items, int64_t n_items, int4* heavy, int64
   if constexpr (GNPDE_EXPERIMENTS) {
     const unsigned gfix = (unsigned)ceil_div(n_heavy, kWavesPerBlock);
     if (!inlaunch && n_heavy > 0) {
-      if (stg == 3) stg = 2;
+      if (stg == 3 || stg == 4) stg = 2;
       if (stg == 1)
         agg_fixup_kernel<VEC, GL, 1, T><<<gfix, kBlock, 0, s>>>(heavy, (int)n_heavy, C, ep, partials);
       else if (stg == 2)
@@ -546,8 +557,9 @@ inline int epi_vec_width(const Epi& ep, int64_t C, const void* partials) {
       ok = ok && al(ep.st.f_out);
       for (int i = 0; i < ep.st.n_out; ++i) {
         ok = ok && al(ep.st.o[i].out) && al(ep.st.o[i].base);
-        for (int j = 0; j < ep.st.o[i].nk; ++j) ok = ok && al(ep.st.o[i].k[j]);
       }
+      for (int j = 0; j < ep.st.nk; ++j) ok = ok && al(ep.st.k[j]);
+      if (ep.st.err_rows) ok = ok && al(ep.st.err.base) && al(ep.st.err_y0);
     } else {
       ok = ok && al(ep.f);
     }

@@ -260,28 +260,43 @@ __device__ __forceinline__ float unpack(const Packed<VEC, bf16>& r, int t) {
 
 // Epilogue operands of one row slice, loaded ahead of the aggregation so their
 // latency overlaps the gathers (they depend only on the row).
-// STG = number of stage outputs the kernel is compiled for (0: store f; 1: the
-// single-output Runge-Kutta stages of gnpde.integrator; 2: the general
-// epilogue): an instantiation only holds registers for the outputs it can emit.
-template <int VEC, class T = float, int NOUT = GNPDE_STAGE_MAX_OUT>
-struct EpiPre {
-  Packed<VEC, T> xr;
-  Packed<VEC, T> x0r;
-  Packed<VEC, T> base[NOUT];
-  Packed<VEC, T> kv[NOUT][GNPDE_STAGE_MAX_K];
-  Packed<VEC, T> dw;  // the stage's dot operand (dot_rows)
-};
-
-// STG = 3: one stage output plus the dot term (the adjoint stages of the
-// discrete-adjoint backward that emit one combination)
+// STG = the stage epilogue an instantiation is compiled for:
+//   0: store f;
+//   1: one stage output, at most kStagePre shared operands, no dot / error term
+//      (every fixed-grid step of gnpde.integrator);
+//   3: one output plus the dot term (its operand loaded in the epilogue: the
+//      adjoint stages that emit one combination);
+//   2: the general fixed-grid epilogue (two outputs, dot term);
+//   4: the wide epilogue of the adaptive solvers: two outputs, up to
+//      GNPDE_STAGE_MAX_K operands and the embedded pair's error rows, every stage
+//      operand loaded after the aggregation (nothing held across the gathers).
+// An instantiation only holds registers for what it can emit.
+constexpr int kStagePre = 2;
 template <int STG>
 constexpr int stage_nout() {
-  return STG == 2 ? 2 : 1;
+  return (STG == 2 || STG == 4) ? 2 : 1;
+}
+template <int STG>
+constexpr int stage_kpre() {  // operands prefetched before the gathers
+  return (STG == 0 || STG == 4) ? 0 : kStagePre;
 }
 template <int STG>
 constexpr bool stage_dot() {
-  return STG >= 2;
+  return STG == 2 || STG == 3;
 }
+template <int STG>
+constexpr bool stage_err() {
+  return STG == 4;
+}
+
+template <int VEC, class T, int STG>
+struct EpiPre {
+  Packed<VEC, T> xr;
+  Packed<VEC, T> x0r;
+  Packed<VEC, T> base[(STG == 0 || STG == 4) ? 1 : stage_nout<STG>()];
+  Packed<VEC, T> kv[stage_kpre<STG>() > 0 ? stage_kpre<STG>() : 1];
+  Packed<VEC, T> dw;  // the stage's dot operand (dot_rows, STG 2)
+};
 
 // The Epi / stage pointers are declared float*; for bf16 storage they address
 // bf16 arrays (gnpde_spmm_rhs_bf16) and are read through T.
@@ -295,11 +310,11 @@ __device__ __forceinline__ T* as_t(float* p) {
 }
 
 template <int VEC, int STG, class T = float>
-__device__ __forceinline__ void epi_prefetch(const Epi& e, int64_t row, int cc, EpiPre<VEC, T, stage_nout<STG>()>& p) {
+__device__ __forceinline__ void epi_prefetch(const Epi& e, int64_t row, int cc, EpiPre<VEC, T, STG>& p) {
   const bool need_x = (e.flags & GNPDE_EPI_RHS) != 0;
   if (need_x) load_packed<VEC>(as_t<T>(e.x) + row * e.ldx + cc, p.xr);
   if (e.flags & GNPDE_ADD_SOURCE) load_packed<VEC>(as_t<T>(e.x0) + row * e.ldx0 + cc, p.x0r);
-  if constexpr (!STG) return;
+  if constexpr (STG == 0 || STG == 4) return;
   const int64_t off = row * e.ldf + cc;
 #pragma unroll
   for (int i = 0; i < stage_nout<STG>(); ++i) {
@@ -307,21 +322,54 @@ __device__ __forceinline__ void epi_prefetch(const Epi& e, int64_t row, int cc, 
       const gnpde_stage_out_t& so = e.st.o[i];
       if (so.base != nullptr && !(need_x && so.base == e.x && e.ldx == e.ldf))
         load_packed<VEC>(as_t<T>(so.base) + off, p.base[i]);
-#pragma unroll
-      for (int j = 0; j < GNPDE_STAGE_MAX_K; ++j)
-        if (j < so.nk) load_packed<VEC>(as_t<T>(so.k[j]) + off, p.kv[i][j]);
     }
   }
+#pragma unroll
+  for (int j = 0; j < stage_kpre<STG>(); ++j)
+    if (j < e.st.nk) load_packed<VEC>(as_t<T>(e.st.k[j]) + off, p.kv[j]);
   if constexpr (STG == 2)  // STG 3 loads its dot operand in the epilogue (registers: occupancy)
     if (e.st.dot_rows) load_packed<VEC>(as_t<T>(e.st.dot_with) + off, p.dw);
 }
 
+// One stage combination cb*base + cf*f + sum_j c[j]*k[j] of a row slice.  The base
+// is x (already in registers), a prefetched row (pre != nullptr) or loaded here.
+template <int VEC, int NK, class T, class KV>
+__device__ __forceinline__ void stage_combine(const Epi& e, const gnpde_stage_out_t& so, int64_t off,
+                                              const float (&o)[VEC], const Packed<VEC, T>& xr,
+                                              const Packed<VEC, T>* pre, const KV& kval, float (&r)[VEC]) {
+  const bool need_x = (e.flags & GNPDE_EPI_RHS) != 0;
+  if (so.base == nullptr) {
+#pragma unroll
+    for (int t = 0; t < VEC; ++t) r[t] = 0.f;
+  } else if (need_x && so.base == e.x && e.ldx == e.ldf) {
+#pragma unroll
+    for (int t = 0; t < VEC; ++t) r[t] = so.cb * unpack(xr, t);
+  } else {
+    Packed<VEC, T> bv;
+    if (pre)
+      bv = *pre;
+    else
+      load_packed<VEC>(as_t<T>(so.base) + off, bv);
+#pragma unroll
+    for (int t = 0; t < VEC; ++t) r[t] = so.cb * unpack(bv, t);
+  }
+#pragma unroll
+  for (int j = 0; j < NK; ++j) {
+    if (j < e.st.nk) {
+#pragma unroll
+      for (int t = 0; t < VEC; ++t) r[t] = fmaf(so.c[j], kval(j, t), r[t]);
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < VEC; ++t) r[t] = fmaf(so.cf, o[t], r[t]);
+}
+
 // f = a*(ax - x) [+ b*x0]  (function_laplacian_diffusion.py:69-77) or f = ax,
-// then either store f or emit the fused Runge-Kutta stage outputs.
+// then either store f or emit the fused Runge-Kutta stage outputs.  dpart
+// accumulates the row's dot term (STG 2, 3) or error term (STG 4) of this slice.
 template <int VEC, int STG, class T = float>
 __device__ __forceinline__ void epi_finish(const Epi& e, int64_t row, int cc, const float (&ax)[VEC], float a,
-                                           float b, const EpiPre<VEC, T, stage_nout<STG>()>& p,
-                                           double* dpart = nullptr) {
+                                           float b, const EpiPre<VEC, T, STG>& p, double* dpart = nullptr) {
   float o[VEC];
   const bool need_x = (e.flags & GNPDE_EPI_RHS) != 0;
   if (need_x) {
@@ -352,56 +400,103 @@ __device__ __forceinline__ void epi_finish(const Epi& e, int64_t row, int cc, co
       for (int t = 0; t < VEC; ++t) *dpart = fma((double)o[t], (double)unpack(dw, t), *dpart);
     }
   }
+  // the shared stage operands: prefetched (STG 1-3) or loaded now (STG 4), each once
+  constexpr int NK = STG == 4 ? GNPDE_STAGE_MAX_K : stage_kpre<STG>();
+  Packed<VEC, T> kw[STG == 4 ? GNPDE_STAGE_MAX_K : 1];
+  if constexpr (STG == 4) {
+#pragma unroll
+    for (int j = 0; j < GNPDE_STAGE_MAX_K; ++j)
+      if (j < e.st.nk) load_packed<VEC>(as_t<T>(e.st.k[j]) + off, kw[j]);
+  }
+  auto kval = [&](int j, int t) -> float {
+    if constexpr (STG == 4)
+      return unpack(kw[j], t);
+    else
+      return unpack(p.kv[j], t);
+  };
   // the stage outputs' row (out_rows: the last step of a renumbered solve writes the caller's numbering)
   const int64_t oo = e.st.out_rows ? (int64_t)e.st.out_rows[row] * e.ldf + cc : off;
+  float y1[VEC];  // STG 4: the output the error tolerance reads (err_y1 >= 0)
 #pragma unroll
   for (int i = 0; i < stage_nout<STG>(); ++i) {
     if (i >= e.st.n_out) break;
-    const gnpde_stage_out_t& so = e.st.o[i];
     float r[VEC];
-    if (so.base == nullptr) {
+    const Packed<VEC, T>* pre = nullptr;
+    if constexpr (STG != 4) pre = &p.base[i];
+    stage_combine<VEC, NK, T>(e, e.st.o[i], off, o, p.xr, pre, kval, r);
+    store_vec<VEC>(as_t<T>(e.st.o[i].out) + oo, r);
+    if constexpr (STG == 4) {
+      if (i == e.st.err_y1) {
 #pragma unroll
-      for (int t = 0; t < VEC; ++t) r[t] = 0.f;
-    } else if (need_x && so.base == e.x && e.ldx == e.ldf) {
-#pragma unroll
-      for (int t = 0; t < VEC; ++t) r[t] = so.cb * unpack(p.xr, t);
-    } else {
-#pragma unroll
-      for (int t = 0; t < VEC; ++t) r[t] = so.cb * unpack(p.base[i], t);
-    }
-#pragma unroll
-    for (int j = 0; j < GNPDE_STAGE_MAX_K; ++j) {
-      if (j < so.nk) {
-#pragma unroll
-        for (int t = 0; t < VEC; ++t) r[t] = fmaf(so.c[j], unpack(p.kv[i][j], t), r[t]);
+        for (int t = 0; t < VEC; ++t) y1[t] = r[t];
       }
     }
+  }
+  if constexpr (STG == 4) {
+    if (e.st.err_rows && dpart) {
+      float ev[VEC];
+      stage_combine<VEC, NK, T>(e, e.st.err, off, o, p.xr, nullptr, kval, ev);
+      Packed<VEC, T> y0v;
+      load_packed<VEC>(as_t<T>(e.st.err_y0) + off, y0v);
 #pragma unroll
-    for (int t = 0; t < VEC; ++t) r[t] = fmaf(so.cf, o[t], r[t]);
-    store_vec<VEC>(as_t<T>(so.out) + oo, r);
+      for (int t = 0; t < VEC; ++t) {
+        const float yb = e.st.err_y1 < 0 ? unpack(p.xr, t) : y1[t];
+        const double tol = e.st.atol + e.st.rtol * (double)fmaxf(fabsf(unpack(y0v, t)), fabsf(yb));
+        const double q = (double)ev[t] / tol;
+        *dpart = fma(q, q, *dpart);
+      }
+    }
   }
 }
 
 template <int VEC, int STG, class T = float>
 __device__ __forceinline__ void epilogue_store(const Epi& e, int64_t row, int cc, const float (&ax)[VEC], float a,
                                                float b, double* dpart = nullptr) {
-  EpiPre<VEC, T, stage_nout<STG>()> p;
+  EpiPre<VEC, T, STG> p;
   epi_prefetch<VEC, STG, T>(e, row, cc, p);
   epi_finish<VEC, STG, T>(e, row, cc, ax, a, b, p, dpart);
 }
 
-// The row's dot_rows term: the owner lanes' partials (lanes [base, base + GL) of
-// the wavefront, GL a power of two) summed by a fixed xor tree, stored by the
-// first of them.  Called by every lane of the wavefront (convergent).
+// Whether an instantiation has a per-row fp64 term to reduce and store (the dot
+// term of the adjoint stages on fp32 rows, the error rows of the wide epilogue).
+template <int STG, class T>
+constexpr bool stage_rowsum() {
+  return (stage_dot<STG>() && sizeof(T) == 4) || stage_err<STG>();
+}
+
+__device__ __forceinline__ void epi_rowsum_write(const Epi& e, int64_t row, double v) {
+  if (e.st.err_rows) {
+    e.st.err_rows[row] = v;
+  } else if (e.st.dot_rows) {
+    double* d = e.st.dot_rows + row;
+    const double w = e.st.dot_coef * v;
+    *d = e.st.dot_accumulate ? *d + w : w;
+  }
+}
+
+// The row's dot / error term: the owner lanes' partials (lanes [base, base + GL)
+// of the wavefront, GL a power of two, base a multiple of GL) summed by a fixed
+// xor tree, stored by the first of them.  Called by every lane of the row's slot
+// (convergent).
 template <int GL>
-__device__ __forceinline__ void epi_dot_store(const Epi& e, int64_t row, double dpart, bool store) {
-  static_assert((GL & (GL - 1)) == 0, "dot_rows needs power-of-two row lanes");
+__device__ __forceinline__ void epi_rowsum_store(const Epi& e, int64_t row, double dpart, bool store) {
+  static_assert((GL & (GL - 1)) == 0, "the xor tree needs power-of-two row lanes");
 #pragma unroll
   for (int o = 1; o < GL; o <<= 1) dpart += __shfl_xor(dpart, o);
-  if (store) {
-    double* d = e.st.dot_rows + row;
-    const double v = e.st.dot_coef * dpart;
-    *d = e.st.dot_accumulate ? *d + v : v;
+  if (store) epi_rowsum_write(e, row, dpart);
+}
+
+// The same for any GL (e.g. 21 lanes: three bf16 rows of 168 columns per wavefront):
+// the first owner lane sums the slot's lanes base .. base + GL - 1 in order.
+template <int GL>
+__device__ __forceinline__ void epi_rowsum_store_any(const Epi& e, int64_t row, double dpart, int base, bool store) {
+  if constexpr ((GL & (GL - 1)) == 0) {
+    epi_rowsum_store<GL>(e, row, dpart, store);
+  } else {
+    double tot = 0.0;
+#pragma unroll
+    for (int j = 0; j < GL; ++j) tot += __shfl(dpart, base + j);
+    if (store) epi_rowsum_write(e, row, tot);
   }
 }
 
@@ -410,9 +505,11 @@ inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 // The STG instantiation an epilogue needs: 0 = store f, 1 = one stage output
 // and no dot term (the forward Runge-Kutta steps), 3 = one stage output and the
 // dot term (three of the four adjoint launches of an rk4 step), 2 = the general
-// epilogue.
+// epilogue, 4 = the wide epilogue (error rows or more than kStagePre operands:
+// the adaptive solvers).
 inline int epi_stage_kind(const Epi& e) {
   if (!e.has_stage) return 0;
+  if (e.st.err_rows || e.st.nk > kStagePre) return 4;
   if (e.st.n_out <= 1) return e.st.dot_rows ? 3 : 1;
   return 2;
 }

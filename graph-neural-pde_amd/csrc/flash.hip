@@ -264,7 +264,7 @@ void dot_agg_kernel(const int4* __restrict__ items, int n_items, int4* heavy, in
   }
   wchunk = uniform(wchunk);
 
-  EpiPre<4, float, stage_nout<STG>()> pre;
+  EpiPre<4, float, STG> pre;
   if (owner) epi_prefetch<4, STG, float>(ep, row, cc, pre);
   float qv[4];  // this lane's slice of the row's q (score tiles)
   load_vec<4>(da.q + (int64_t)row * da.ldqk + 4 * (sl % NA), qv);
@@ -483,7 +483,7 @@ __global__ __launch_bounds__(256) void dot_dst_agg_kernel(const int4* __restrict
   const int base = rs * SL;
   float* sc = scs[wv][rs];
 
-  EpiPre<4, float, stage_nout<STG>()> pre;
+  EpiPre<4, float, STG> pre;
   if (owner) epi_prefetch<4, STG, float>(ep, row, cc, pre);
   float qv[4];
   load_vec<4>(da.q + (int64_t)row * da.ldqk + 4 * (sl % NA), qv);
@@ -654,8 +654,8 @@ int gnpde_attn_dot_rhs_f32(const int32_t* items, int64_t n_items, int32_t* heavy
     bool ok = !stage->f_out || aligned16(stage->f_out);
     for (int i = 0; i < stage->n_out; ++i) {
       ok = ok && aligned16(stage->o[i].out) && (!stage->o[i].base || aligned16(stage->o[i].base));
-      for (int j = 0; j < stage->o[i].nk; ++j) ok = ok && aligned16(stage->o[i].k[j]);
     }
+    for (int j = 0; j < stage->nk; ++j) ok = ok && aligned16(stage->k[j]);
     GNPDE_REQUIRE(ok && (!stage->dot_rows || aligned16(stage->dot_with)), GNPDE_EUNSUPPORTED,
                   "attn_dot_rhs: stage rows must be 16-byte aligned");
   }

@@ -48,6 +48,27 @@ inline int xcd_remap_enabled() {
   return on;
 }
 
+// The stage struct's own consistency (include/gnpde.h, fused solver epilogue).
+inline int check_stage(const gnpde_stage_epilogue_t& st) {
+  GNPDE_REQUIRE(st.n_out >= 0 && st.n_out <= GNPDE_STAGE_MAX_OUT, GNPDE_EINVAL, "stage: n_out out of range");
+  GNPDE_REQUIRE(st.nk >= 0 && st.nk <= GNPDE_STAGE_MAX_K, GNPDE_EINVAL, "stage: nk=%d out of [0, %d]", st.nk,
+                GNPDE_STAGE_MAX_K);
+  for (int j = 0; j < st.nk; ++j) GNPDE_REQUIRE(st.k[j] != nullptr, GNPDE_EINVAL, "stage: k[%d] is NULL", j);
+  for (int i = 0; i < st.n_out; ++i) GNPDE_REQUIRE(st.o[i].out, GNPDE_EINVAL, "stage: output %d is NULL", i);
+  GNPDE_REQUIRE(st.f_out || st.n_out > 0 || st.err_rows, GNPDE_EINVAL, "stage: the epilogue stores nothing");
+  GNPDE_REQUIRE(!st.dot_rows || st.dot_with, GNPDE_EINVAL, "stage: dot_rows without dot_with");
+  GNPDE_REQUIRE(!(st.dot_rows && st.err_rows), GNPDE_EINVAL, "stage: dot_rows and err_rows together");
+  GNPDE_REQUIRE(!st.dot_rows || st.nk <= 2, GNPDE_EUNSUPPORTED, "stage: dot_rows with more than 2 operands");
+  if (st.err_rows) {
+    GNPDE_REQUIRE(st.err_y0 != nullptr, GNPDE_EINVAL, "stage: err_rows without err_y0");
+    GNPDE_REQUIRE(st.err_y1 >= -1 && st.err_y1 < st.n_out, GNPDE_EINVAL, "stage: err_y1=%d names no output",
+                  st.err_y1);
+    GNPDE_REQUIRE(st.atol >= 0.0 && st.rtol >= 0.0 && (st.atol > 0.0 || st.rtol > 0.0), GNPDE_EINVAL,
+                  "stage: tolerances must be >= 0 and not both 0");
+  }
+  return GNPDE_OK;
+}
+
 inline Epi make_epi(const float* x, int64_t ldx, const float* x0, int64_t ldx0, const float* alpha, const float* beta,
                     int flags, float* f, int64_t ldf, const gnpde_stage_epilogue_t* stage = nullptr) {
   Epi e{};
@@ -70,15 +91,8 @@ inline int check_epi(const Epi& e, int64_t C, int64_t n_heavy, const void* parti
   GNPDE_REQUIRE(C >= 1, GNPDE_EINVAL, "rhs: C must be >= 1");
   GNPDE_REQUIRE(e.x && (e.f || e.has_stage), GNPDE_EINVAL, "rhs: NULL x or f");
   if (e.has_stage) {
-    GNPDE_REQUIRE(e.st.n_out >= 0 && e.st.n_out <= GNPDE_STAGE_MAX_OUT, GNPDE_EINVAL, "rhs: stage n_out out of range");
-    GNPDE_REQUIRE(e.st.f_out || e.st.n_out > 0, GNPDE_EINVAL, "rhs: stage epilogue stores nothing");
-    for (int i = 0; i < e.st.n_out; ++i) {
-      GNPDE_REQUIRE(e.st.o[i].out && e.st.o[i].nk >= 0 && e.st.o[i].nk <= GNPDE_STAGE_MAX_K, GNPDE_EINVAL,
-                    "rhs: bad stage output %d", i);
-      for (int j = 0; j < e.st.o[i].nk; ++j)
-        GNPDE_REQUIRE(e.st.o[i].k[j] != nullptr, GNPDE_EINVAL, "rhs: stage output %d k[%d] is NULL", i, j);
-    }
-    GNPDE_REQUIRE(!e.st.dot_rows || e.st.dot_with, GNPDE_EINVAL, "rhs: stage dot_rows without dot_with");
+    int rc = check_stage(e.st);
+    if (rc) return rc;
   }
   GNPDE_REQUIRE(e.ldx >= C && e.ldf >= C, GNPDE_EINVAL, "rhs: leading dimension < C");
   if (e.flags & GNPDE_EPI_RHS) GNPDE_REQUIRE(e.alpha != nullptr, GNPDE_EINVAL, "rhs: NULL alpha");

@@ -3,7 +3,7 @@
 // do it with several elementwise torch kernels per stage); and the fp64 dot
 // product of two fp32 tensors the parameter gradients of the RHS need
 // (d alpha_train = sigma'(alpha) <gf, A x - x>, d beta_train = <gf, x0>).
-#include "common.hpp"
+#include "rhs_host.hpp"
 
 namespace gnpde {
 
@@ -129,9 +129,170 @@ __global__ __launch_bounds__(256) void rows_copy_kernel(const uint4* __restrict_
   }
 }
 
+// The stage epilogue as a pass of its own (gnpde_stage_apply_*): GL lanes per row
+// (RPW = 64 / GL rows per wavefront), VEC elements per lane, column passes of
+// GL*VEC.  Per element the same arithmetic, in the same order, as epi_finish
+// (cb*base, the operands by fmaf in index order, then cf*f), so the pass and the
+// fused epilogue give the same bits from the same f; the error rows summed over
+// the row's lanes by the same xor tree.
+template <int VEC, int GL, class T>
+__global__ __launch_bounds__(256) void stage_apply_kernel(int64_t R, int C, int64_t ld, const T* __restrict__ f,
+                                                           const T* __restrict__ x, gnpde_stage_epilogue_t st) {
+  constexpr int RPW = kWave / GL;
+  const int lane = threadIdx.x & 63;
+  const int rs = lane / GL, gl = lane % GL;
+  const int64_t row = ((int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * RPW + rs;
+  const bool live = row < R;
+  double dpart = 0.0;
+  for (int c0 = 0; c0 < C; c0 += GL * VEC) {
+    const int cc = c0 + gl * VEC;
+    if (!live || cc >= C) continue;
+    const int64_t off = row * ld + cc;
+    float fv[VEC], xv[VEC], kv[GNPDE_STAGE_MAX_K][VEC];
+    if (f) {
+      load_vec<VEC>(f + off, fv);
+    } else {
+#pragma unroll
+      for (int t = 0; t < VEC; ++t) fv[t] = 0.f;
+    }
+    if (x) {
+      load_vec<VEC>(x + off, xv);
+    } else {
+#pragma unroll
+      for (int t = 0; t < VEC; ++t) xv[t] = 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < GNPDE_STAGE_MAX_K; ++j)
+      if (j < st.nk) load_vec<VEC>(as_t<T>(st.k[j]) + off, kv[j]);
+    auto comb = [&](const gnpde_stage_out_t& so, float (&r)[VEC]) {
+      if (so.base == nullptr) {
+#pragma unroll
+        for (int t = 0; t < VEC; ++t) r[t] = 0.f;
+      } else if (x && so.base == reinterpret_cast<const float*>(x)) {
+#pragma unroll
+        for (int t = 0; t < VEC; ++t) r[t] = so.cb * xv[t];
+      } else {
+        float bv[VEC];
+        load_vec<VEC>(as_t<T>(so.base) + off, bv);
+#pragma unroll
+        for (int t = 0; t < VEC; ++t) r[t] = so.cb * bv[t];
+      }
+#pragma unroll
+      for (int j = 0; j < GNPDE_STAGE_MAX_K; ++j) {
+        if (j < st.nk) {
+#pragma unroll
+          for (int t = 0; t < VEC; ++t) r[t] = fmaf(so.c[j], kv[j][t], r[t]);
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < VEC; ++t) r[t] = fmaf(so.cf, fv[t], r[t]);
+    };
+    if (st.f_out) store_vec<VEC>(as_t<T>(st.f_out) + off, fv);
+    const int64_t oo = st.out_rows ? (int64_t)st.out_rows[row] * ld + cc : off;
+    float y1[VEC];
+#pragma unroll
+    for (int t = 0; t < VEC; ++t) y1[t] = xv[t];
+#pragma unroll
+    for (int i = 0; i < GNPDE_STAGE_MAX_OUT; ++i) {
+      if (i >= st.n_out) break;
+      float r[VEC];
+      comb(st.o[i], r);
+      store_vec<VEC>(as_t<T>(st.o[i].out) + oo, r);
+      if (i == st.err_y1) {
+#pragma unroll
+        for (int t = 0; t < VEC; ++t) y1[t] = r[t];
+      }
+    }
+    if (st.err_rows) {
+      float ev[VEC], y0v[VEC];
+      comb(st.err, ev);
+      load_vec<VEC>(as_t<T>(st.err_y0) + off, y0v);
+#pragma unroll
+      for (int t = 0; t < VEC; ++t) {
+        const double tol = st.atol + st.rtol * (double)fmaxf(fabsf(y0v[t]), fabsf(y1[t]));
+        const double q = (double)ev[t] / tol;
+        dpart = fma(q, q, dpart);
+      }
+    }
+  }
+  if (st.err_rows) {  // kernel-uniform
+#pragma unroll
+    for (int o = 1; o < GL; o <<= 1) dpart += __shfl_xor(dpart, o);
+    if (live && gl == 0) st.err_rows[row] = dpart;
+  }
+}
+
+template <int VEC, class T>
+static int launch_stage_apply(int64_t R, int C, int64_t ld, const T* f, const T* x,
+                              const gnpde_stage_epilogue_t& st, hipStream_t s) {
+  const int lanes = (int)ceil_div(C, VEC);
+  const int64_t waves = [&](int rpw) { return ceil_div(R, (int64_t)rpw); }(lanes <= 16 ? 4 : (lanes <= 32 ? 2 : 1));
+  const unsigned grid = (unsigned)std::max<int64_t>(1, ceil_div(waves, kWavesPerBlock));
+  if (lanes <= 16)
+    stage_apply_kernel<VEC, 16, T><<<grid, kBlock, 0, s>>>(R, C, ld, f, x, st);
+  else if (lanes <= 32)
+    stage_apply_kernel<VEC, 32, T><<<grid, kBlock, 0, s>>>(R, C, ld, f, x, st);
+  else
+    stage_apply_kernel<VEC, 64, T><<<grid, kBlock, 0, s>>>(R, C, ld, f, x, st);
+  GNPDE_LAUNCH_CHECK();
+  return GNPDE_OK;
+}
+
+template <class T>
+static int stage_apply(int64_t R, int64_t C, int64_t ld, const T* f, const T* x, const gnpde_stage_epilogue_t* stage,
+                       void* stream) {
+  GNPDE_REQUIRE(stage != nullptr && R >= 0 && C >= 1 && ld >= C && C < INT32_MAX, GNPDE_EINVAL,
+                "stage_apply: bad arguments");
+  int rc = check_stage(*stage);
+  if (rc) return rc;
+  const gnpde_stage_epilogue_t& st = *stage;
+  GNPDE_REQUIRE(!st.dot_rows, GNPDE_EUNSUPPORTED, "stage_apply: dot_rows are fused into the RHS kernels only");
+  bool needs_x = st.err_rows && st.err_y1 < 0;
+  for (int i = 0; i < st.n_out; ++i)
+    GNPDE_REQUIRE(st.o[i].out != reinterpret_cast<const float*>(x), GNPDE_EINVAL, "stage_apply: output %d aliases x",
+                  i);
+  GNPDE_REQUIRE(!needs_x || x, GNPDE_EINVAL, "stage_apply: the error tolerance reads y1 = x, which is NULL");
+  if (R == 0) return GNPDE_OK;
+  // widest vector every row array allows
+  const int kMax = 16 / (int)sizeof(T);
+  int vec = 1;
+  for (int v = kMax; v > 1; v >>= 1) {
+    const size_t bytes = (size_t)v * sizeof(T);
+    auto al = [&](const void* p) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) % bytes) == 0; };
+    bool ok = C % v == 0 && ld % v == 0 && al(f) && al(x) && al(st.f_out) && al(st.err.base) && al(st.err_y0);
+    for (int i = 0; i < st.n_out; ++i) ok = ok && al(st.o[i].out) && al(st.o[i].base);
+    for (int j = 0; j < st.nk; ++j) ok = ok && al(st.k[j]);
+    if (ok) {
+      vec = v;
+      break;
+    }
+  }
+  hipStream_t s = as_stream(stream);
+  const int c = (int)C;
+  switch (vec) {
+    case 8:
+      if constexpr (sizeof(T) == 2) return launch_stage_apply<8, T>(R, c, ld, f, x, st, s);
+      [[fallthrough]];
+    case 4: return launch_stage_apply<4, T>(R, c, ld, f, x, st, s);
+    case 2: return launch_stage_apply<2, T>(R, c, ld, f, x, st, s);
+    default: return launch_stage_apply<1, T>(R, c, ld, f, x, st, s);
+  }
+}
+
 }  // namespace gnpde
 
 using namespace gnpde;
+
+extern "C" int gnpde_stage_apply_f32(int64_t R, int64_t C, int64_t ld, const float* f, const float* x,
+                                     const gnpde_stage_epilogue_t* stage, void* stream) {
+  return stage_apply<float>(R, C, ld, f, x, stage, stream);
+}
+
+extern "C" int gnpde_stage_apply_bf16(int64_t R, int64_t C, int64_t ld, const uint16_t* f, const uint16_t* x,
+                                      const gnpde_stage_epilogue_t* stage, void* stream) {
+  return stage_apply<bf16>(R, C, ld, reinterpret_cast<const bf16*>(f), reinterpret_cast<const bf16*>(x), stage,
+                           stream);
+}
 
 extern "C" int gnpde_rows_copy(const void* src, int64_t rows, int64_t row_bytes, const int64_t* order, void* dst,
                                void* dst_copy, void* stream) {

@@ -14,20 +14,24 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GNPDE_LIB", os.path.join(_HERE, "libgnpde.so"))
 
 STAGE_MAX_OUT = 2
-STAGE_MAX_K = 2
+STAGE_MAX_K = 6
+STAGE_PRE_K = 2  # operands the fixed-grid epilogues prefetch (csrc/common.hpp kStagePre)
 
 
 class StageOut(ctypes.Structure):
-    """gnpde_stage_out_t: out = cb*base + cf*f + sum_j c[j]*k[j]."""
+    """gnpde_stage_out_t: out = cb*base + cf*f + sum_j c[j]*k[j] (k: the stage's shared operands)."""
     _fields_ = [("out", ctypes.c_void_p), ("base", ctypes.c_void_p), ("cb", ctypes.c_float), ("cf", ctypes.c_float),
-                ("nk", ctypes.c_int), ("k", ctypes.c_void_p * STAGE_MAX_K), ("c", ctypes.c_float * STAGE_MAX_K)]
+                ("c", ctypes.c_float * STAGE_MAX_K)]
 
 
 class StageEpilogue(ctypes.Structure):
     """gnpde_stage_epilogue_t (include/gnpde.h)."""
     _fields_ = [("f_out", ctypes.c_void_p), ("n_out", ctypes.c_int), ("o", StageOut * STAGE_MAX_OUT),
+                ("nk", ctypes.c_int), ("k", ctypes.c_void_p * STAGE_MAX_K),
                 ("out_rows", ctypes.c_void_p), ("dot_with", ctypes.c_void_p), ("dot_rows", ctypes.c_void_p),
-                ("dot_coef", ctypes.c_double), ("dot_accumulate", ctypes.c_int)]
+                ("dot_coef", ctypes.c_double), ("dot_accumulate", ctypes.c_int),
+                ("err_rows", ctypes.c_void_p), ("err", StageOut), ("err_y0", ctypes.c_void_p), ("err_y1", ctypes.c_int),
+                ("atol", ctypes.c_double), ("rtol", ctypes.c_double)]
 
 
 c_i32p = ctypes.POINTER(ctypes.c_int32)
@@ -66,6 +70,8 @@ SIGNATURES = {
     "gnpde_attn_dot_rhs_f32": (_int, [_vp, _i64, _vp, _i64, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _i64, _vp, _i64, _vp,
                                       _i64, _vp, _vp, _int, _vp, _i64, _vp, _i64, ctypes.POINTER(StageEpilogue), _vp]),
     "gnpde_rows_copy": (_int, [_vp, _i64, _i64, _vp, _vp, _vp, _vp]),
+    "gnpde_stage_apply_f32": (_int, [_i64, _i64, _i64, _vp, _vp, ctypes.POINTER(StageEpilogue), _vp]),
+    "gnpde_stage_apply_bf16": (_int, [_i64, _i64, _i64, _vp, _vp, ctypes.POINTER(StageEpilogue), _vp]),
     "gnpde_seg_long_edges": (_int, []),
     "gnpde_linear_f32": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _vp]),
     "gnpde_linear_wgrad_workspace_bytes": (_size, [_i64, _i64, _i64]),
@@ -106,7 +112,7 @@ SIGNATURES = {
 }
 
 # constants mirrored from include/gnpde.h
-ABI_VERSION = 2
+ABI_VERSION = 3
 OK = 0
 EINVAL = -1
 EHIP = -2

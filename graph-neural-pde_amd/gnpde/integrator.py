@@ -276,7 +276,10 @@ _POOLS = weakref.WeakKeyDictionary()  # module -> {(shape, dtype, device): _Stat
 
 
 def _state_pool(func, y):
-    key = (tuple(y.shape), y.dtype, str(y.device))
+    # keyed by stream too: two concurrent solves of one module on two streams
+    # must not share ping-pong buffers or stage workspaces
+    sid = torch.cuda.current_stream(y.device).cuda_stream if y.is_cuda else None
+    key = (tuple(y.shape), y.dtype, str(y.device), sid)
     d = _POOLS.get(func)
     if d is None:
         d = {}
@@ -962,6 +965,291 @@ class _RKAdaptive(object):
         return torch.stack(solution, 0)
 
 
+# --------------------------------------------------------------------------- fused adaptive steps
+# An embedded Runge-Kutta step of torchdiffeq's adaptive solver (dopri5 — the method
+# of every src/best_params.py entry — bosh3, fehlberg2, adaptive_heun) with every
+# stage combination and the error estimate in the RHS epilogues (gnpde_stage_
+# epilogue_t, the wide epilogue): launch i evaluates k_{i+1} = f(X_i) and writes the
+# next stage input X_{i+1} from the rows it holds; the last launch forms the rows of
+# the squared error norm.  One host read per step (the norm); no separate
+# combination passes besides the step's first stage input.  The plan below derives
+# every launch's operands from the tableau, choosing per combination the form that
+# reads fewest state arrays:
+#   from the launch's own input:  X_{i+1} = X_i + dt sum_j (b_{i+1,j} - b_{i,j}) k_j + dt b_{i+1,i+1} f
+#   from the step start:          X_{i+1} = y0  + dt sum_j b_{i+1,j} k_j + dt b_{i+1,i+1} f
+# (same values up to rounding: a combination of the k's scaled by dt, never a
+# difference of states, so the error estimate keeps its precision).
+
+def _nz(c):
+    return c != 0.0
+
+
+class _AdaptivePlan(object):
+    """Per-launch operands of one step of an embedded tableau.
+
+    Symbols: 'Y' the step start y0, 'X' the launch's own input, 'E' the error
+    partial, 'K<j>' stage derivative j (K0 = f0 from the previous step).  Each
+    combination is (base symbol or None, [(K<j>, coefficient / dt)...], f
+    coefficient / dt); dt multiplies every k and f coefficient at run time."""
+
+    def __init__(self, method):
+        order, alpha, beta, c_sol, c_err, c_mid = _TABLEAUS[method]
+        self.method, self.order, self.alpha, self.beta = method, order, alpha, beta
+        self.c_sol, self.c_err, self.c_mid = c_sol, c_err, c_mid
+        ns = len(alpha)
+        self.ns = ns
+        self.fsal = c_sol[-1] == 0 and list(c_sol[:-1]) == list(beta[-1])
+        self.launches = []
+        reads = []  # K indices each launch reads
+        for i in range(ns):
+            L = {'next': None, 'y1': None, 'epart': None, 'err': None}
+            rd = set()
+            if i < ns - 1:
+                d = [(j, beta[i + 1][j] - beta[i][j]) for j in range(i + 1)]
+                d = [(j, c) for j, c in d if _nz(c)]
+                yv = [(j, beta[i + 1][j]) for j in range(i + 1) if _nz(beta[i + 1][j])]
+                if len(d) <= len(yv) + 1:
+                    L['next'] = ('X', [('K%d' % j, c) for j, c in d], beta[i + 1][i + 1])
+                    rd |= {j for j, _ in d}
+                else:
+                    L['next'] = ('Y', [('K%d' % j, c) for j, c in yv], beta[i + 1][i + 1])
+                    rd |= {j for j, _ in yv}
+            else:
+                if not self.fsal:
+                    yv = [(j, c_sol[j]) for j in range(ns) if _nz(c_sol[j])]
+                    L['y1'] = ('Y', [('K%d' % j, c) for j, c in yv], c_sol[ns])
+                    rd |= {j for j, _ in yv}
+            reads.append(rd)
+            self.launches.append(L)
+        # the error combination e = dt sum_j c_err[j] k_j (k_ns = the last launch's f): all in
+        # the last launch, or its first ns terms precomputed by the launch before (a second
+        # output 'E') when that launch already reads most of their operands
+        last = ns - 1
+        ev = [(j, c_err[j]) for j in range(ns) if _nz(c_err[j])]
+        direct = {j for j, _ in ev if j < ns} - reads[last]
+        pre_ok = ns >= 2
+        if pre_ok:
+            held = reads[last - 1] | {last}  # launch ns-2 reads its operands and holds k_{ns-1} = its own f
+            pre_cost = 2 + len({j for j, _ in ev} - held)
+            pre_ok = pre_cost < len(direct) + (0 if last in reads[last] else 0)
+        if pre_ok:
+            self.launches[last - 1]['epart'] = (None, [('K%d' % j, c) for j, c in ev if j < last], c_err[last])
+            self.launches[last]['err'] = ('E', [], c_err[ns])
+            reads[last - 1] |= {j for j, _ in ev if j < last}
+        else:
+            self.launches[last]['err'] = (None, [('K%d' % j, c) for j, c in ev], c_err[ns])
+            reads[last] |= {j for j, _ in ev}
+        self.reads = reads
+        # k_j stored when a later launch reads it (k_ns: always, the next step's f0)
+        self.store = set()
+        for i in range(ns):
+            for j in reads[i]:
+                if j >= 1:
+                    self.store.add(j)
+        self.store.add(ns)
+        # dense output (a step that may cross an output time): every k with a c_mid term
+        self.store_mid = {j for j in range(1, ns + 1) if _nz(c_mid[j])} - self.store
+
+    def state_passes(self):
+        """Full-state reads / writes per step beyond each launch's own gathers,
+        input row and one output (the bench's overhead check)."""
+        r = 2  # the step's first stage input: y0 and k0
+        w = 1
+        for i, L in enumerate(self.launches):
+            outs = [c for c in (L['next'], L['y1'], L['epart']) if c is not None]
+            r += len(self.reads[i]) + sum(1 for c in outs if c[0] in ('Y', 'E'))
+            if L['err'] is not None:
+                r += 1 + (1 if L['err'][0] == 'E' else 0)  # y0 for the tolerance, E
+            stored = (i + 1) in self.store
+            w += len(outs) + (1 if stored else 0) - 1
+        return r, w
+
+
+_PLANS = {}
+
+
+def _adaptive_plan(method):
+    p = _PLANS.get(method)
+    if p is None:
+        p = _PLANS[method] = _AdaptivePlan(method)
+    return p
+
+
+def _fused_adaptive_ok(func, y0, combine, options):
+    """The fused adaptive step applies: a gnpde RHS (rhs_stage) without autograd, a
+    device state (or a host-stage test RHS on CPU), torchdiffeq's RMS norm (or a
+    sharded RHS's global one, reduced through func.reduce_error_sq)."""
+    if not (isinstance(combine, _Combine) and hasattr(func, 'rhs_stage')) or torch.is_grad_enabled():
+        return False
+    if os.environ.get('GNPDE_FUSED_ADAPTIVE', '1') == '0':
+        return False
+    norm = options.get('norm')
+    if norm is not None and not (getattr(norm, '__self__', None) is func and hasattr(func, 'reduce_error_sq')):
+        return False
+    if y0.is_cuda:
+        return y0.dtype in ops.STATE_DTYPES
+    return bool(getattr(func, 'host_stages', False)) and hasattr(func, 'host_stage_apply')
+
+
+class _RKAdaptiveFused(_RKAdaptive):
+    """_RKAdaptive with the step formed by the RHS epilogues (_AdaptivePlan): the same
+    controller (torchdiffeq's, in host float64 arithmetic), the same accepted /
+    rejected sequence, dense output from the stored stage derivatives.  Per step:
+    one stage-input pass, len(alpha) RHS launches carrying the combinations and the
+    error rows, one fixed-order fp64 reduction and one host read of it."""
+
+    def __init__(self, func, y0, rtol, atol, combine, method='dopri5', options=None, **kw):
+        super(_RKAdaptiveFused, self).__init__(func, y0, rtol, atol, combine, method=method, **kw)
+        self.options = dict(options or {})
+        self.plan = _adaptive_plan(method)
+        self.host = not y0.is_cuda
+        self.rtol_f, self.atol_f = float(rtol), float(atol)
+
+    # ---- device primitives (host-stage RHS objects supply CPU versions: tests only)
+    def _apply(self, stage, f, x, like):
+        if self.host:
+            self.func.host_stage_apply(stage, f, x, like)
+        else:
+            ops.stage_apply(stage, f, x, like)
+
+    def _err_sum(self, rows):
+        v = rows.sum() if self.host else ops.sum_f64(rows)
+        red = getattr(self.func, 'reduce_error_sq', None)
+        if red is not None and 'norm' in self.options:
+            pair = torch.stack([v.reshape(()), torch.tensor(float(rows.numel() * self.C), dtype=torch.float64,
+                                                            device=rows.device)])
+            red(pair)
+            return float(pair[0]), float(pair[1])
+        return float(v), float(rows.numel() * self.C)
+
+    def _combo(self, spec, bufs, dt, x):
+        """(base tensor, cb, cf, [(k tensor, c)]) of a plan combination at step size dt."""
+        base, terms, cfc = spec
+        bt = {'Y': bufs['Y'], 'X': x, 'E': bufs.get('E'), None: None}[base]
+        return bt, (1.0 if bt is not None else 0.0), dt * cfc, [(bufs[k], dt * c) for k, c in terms]
+
+    def _launch(self, i, bufs, x, t, dt, rows, mid):
+        P = self.plan
+        L = P.launches[i]
+        outs = []
+        if L['next'] is not None:
+            b, cb, cf, ks = self._combo(L['next'], bufs, dt, x)
+            outs.append((bufs['X%d' % (i + 1)], b, cb, cf, ks))
+        if L['y1'] is not None:
+            b, cb, cf, ks = self._combo(L['y1'], bufs, dt, x)
+            outs.append((bufs['Y1'], b, cb, cf, ks))
+        if L['epart'] is not None:
+            b, cb, cf, ks = self._combo(L['epart'], bufs, dt, x)
+            outs.append((bufs['E'], b, cb, cf, ks))
+        err = None
+        if L['err'] is not None:
+            b, cb, cf, ks = self._combo(L['err'], bufs, dt, x)
+            err = (rows, (b, cb, cf, ks), bufs['Y'], 0 if L['y1'] is not None else -1, self.atol_f, self.rtol_f)
+        j = i + 1
+        f_out = bufs['K%d' % j] if (j in P.store or (mid and j in P.store_mid)) else None
+        stage = ops.Stage(f_out=f_out, outs=outs, err=err)
+        self.func.rhs_stage(t, x, stage)
+
+    def integrate(self, t):
+        P = self.plan
+        th = [float(v) for v in t.detach().to(torch.float64).cpu().tolist()]
+        y0 = self.y0.contiguous()
+        self.C = y0.shape[-1]
+        R = y0.numel() // self.C
+        dev = y0.device
+        sol = torch.empty((len(th),) + tuple(y0.shape), dtype=y0.dtype, device=dev)
+        sol[0].copy_(y0)
+        new = lambda: torch.empty_like(y0, memory_format=torch.contiguous_format)  # noqa: E731
+        bufs = {'Y': new(), 'Y1': new(), 'K0': None}
+        bufs['Y'].copy_(y0)
+        for j in sorted(P.store | P.store_mid):
+            bufs['K%d' % j] = new()
+        xa, xb = new(), new()
+        for i in range(P.ns):
+            if P.fsal and i == P.ns - 1:
+                bufs['X%d' % i] = bufs['Y1']
+            else:
+                bufs['X%d' % i] = xa if i % 2 == 0 else xb
+        if any(L['epart'] is not None for L in P.launches):
+            bufs['E'] = new()
+        rows = torch.empty(R, dtype=torch.float64, device=dev)
+        t0 = torch.tensor(th[0], dtype=torch.float64)
+        f0 = self.func(t0, bufs['Y'])
+        bufs['K0'] = f0.contiguous() if f0.dtype == y0.dtype else f0.to(y0.dtype).contiguous()
+        if self.first_step is None:
+            dt = float(self._select_initial_step(t0.to(dev) if not self.host else t0, bufs['K0']))
+        else:
+            dt = float(self.first_step)
+        t_cur = th[0]
+        last = None  # (t_prev, dt of the accepted step, needs a dense output)
+        order = float(P.order)
+        safety, ifactor, dfactor = float(self.safety), float(self.ifactor), float(self.dfactor)
+        for i_out in range(1, len(th)):
+            next_t = th[i_out]
+            while next_t > t_cur:
+                if not (t_cur + dt > t_cur):
+                    raise AssertionError('underflow in dt {}'.format(dt))
+                if self.n_steps >= self.max_num_steps:
+                    raise AssertionError('max_num_steps exceeded ({}>={})'.format(self.n_steps, self.max_num_steps))
+                mid = t_cur + dt >= next_t  # an accepted step would cross an output time: keep the dense-output k's
+                # the step's first stage input X0 = y0 + dt b00 k0
+                self._apply(ops.Stage(outs=[(bufs['X0'], bufs['Y'], 1.0, 0.0, [(bufs['K0'], dt * P.beta[0][0])])]),
+                            None, None, bufs['Y'])
+                for i in range(P.ns):
+                    ti = t_cur + dt if P.alpha[i] == 1. else t_cur + P.alpha[i] * dt
+                    self._launch(i, bufs, bufs['X%d' % i], ti, dt, rows, mid)
+                s, n = self._err_sum(rows)
+                ratio = math.sqrt(s / n) if n > 0 else 0.0
+                accept = ratio <= 1
+                if accept:
+                    t_prev, t_cur = t_cur, t_cur + dt
+                    kn = 'K%d' % P.ns
+                    last = (t_prev, dt)
+                    # a step that crossed an output time keeps its operands for the dense output (the
+                    # references as they are now; the buffers are only rewritten by the next step)
+                    self._dense = dict(bufs) if mid else None
+                    bufs['Y'], bufs['Y1'] = bufs['Y1'], bufs['Y']
+                    bufs['K0'], bufs[kn] = bufs[kn], bufs['K0']
+                    if P.fsal:
+                        bufs['X%d' % (P.ns - 1)] = bufs['Y1']
+                if ratio == 0:
+                    dt = dt * ifactor
+                else:
+                    df = 1.0 if ratio < 1 else dfactor
+                    dt = dt * min(ifactor, max(safety / ratio ** (1.0 / order), df))
+                self.n_steps += 1
+            if next_t == t_cur or last is None:
+                sol[i_out].copy_(bufs['Y'])
+            else:
+                self._interp_into(sol[i_out], last, next_t, t_cur)
+        return sol
+
+    def _interp_into(self, out, last, t, t1):
+        """torchdiffeq's 4th-order dense output (_interp_fit / _interp_evaluate, with the
+        tableau's mid-point coefficients) of the last accepted step at time t, as two
+        stage passes: y_mid = y0 + dt sum_j c_mid[j] k_j, then the polynomial, a
+        combination of y0, y1, y_mid, f0 and f1."""
+        P = self.plan
+        t0, dt = last
+        d = self._dense
+        if d is None:
+            raise RuntimeError("gnpde: dense output of a step whose stage derivatives were not kept")
+        y_prev, y_cur = d['Y'], d['Y1']
+        f0, f1 = d['K0'], d['K%d' % P.ns]
+        ymid = torch.empty_like(out)
+        terms = [(d['K%d' % j], dt * P.c_mid[j]) for j in range(P.ns + 1) if _nz(P.c_mid[j])]
+        self._apply(ops.Stage(outs=[(ymid, y_prev, 1.0, 0.0, terms)]), None, None, y_prev)
+        x = (t - t0) / (t1 - t0)
+        x2, x3, x4 = x * x, x * x * x, x * x * x * x
+        cy0 = 1.0 - 11.0 * x2 + 18.0 * x3 - 8.0 * x4
+        cy1 = -5.0 * x2 + 14.0 * x3 - 8.0 * x4
+        cym = 16.0 * x2 - 32.0 * x3 + 16.0 * x4
+        cf0 = dt * (x - 4.0 * x2 + 5.0 * x3 - 2.0 * x4)
+        cf1 = dt * (x2 - 3.0 * x3 + 2.0 * x4)
+        self._apply(ops.Stage(outs=[(out, y_prev, cy0, 0.0, [(y_cur, cy1), (ymid, cym), (f0, cf0), (f1, cf1)])]),
+                    None, None, y_prev)
+
+
 def odeint(func, y0, t, rtol=1e-7, atol=1e-9, method=None, options=None, combine=None):
     """torchdiffeq.odeint(func, y0, t, rtol, atol, method, options) -> [len(t), *y0.shape]."""
     method = method or 'dopri5'
@@ -977,9 +1265,12 @@ def odeint(func, y0, t, rtol=1e-7, atol=1e-9, method=None, options=None, combine
     if method in FIXED_METHODS:
         return odeint_fixed(func, y0, t, method, options.get('step_size'), combine, graph=options.get('gnpde_graph'))
     if method in ADAPTIVE_METHODS:
-        solver = _RKAdaptive(func, y0, rtol, atol, combine, method=method, first_step=options.get('first_step'),
-                         max_num_steps=options.get('max_num_steps', 2 ** 31 - 1),
-                         norm=options.get('norm', _rms_norm))
+        kw = dict(method=method, first_step=options.get('first_step'),
+                  max_num_steps=options.get('max_num_steps', 2 ** 31 - 1), norm=options.get('norm', _rms_norm))
+        if _fused_adaptive_ok(func, y0, combine, options):
+            solver = _RKAdaptiveFused(func, y0, rtol, atol, combine, options=options, **kw)
+        else:
+            solver = _RKAdaptive(func, y0, rtol, atol, combine, **kw)
         out = solver.integrate(t)
         odeint.last_n_steps = solver.n_steps
         return out

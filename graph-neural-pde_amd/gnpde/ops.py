@@ -510,63 +510,130 @@ class Stage(object):
     ``f_out`` receives f (optional); each entry of ``outs`` is
     (out, base, cb, cf, [(k_j, c_j), ...]) meaning out = cb*base + cf*f + sum_j c_j*k_j.
     ``base`` may be None, the RHS input x, or ``out`` itself (in place).  No
-    output may alias the RHS input."""
+    output may alias the RHS input.  The k operands of all outputs (and of the
+    error term) are collected into the stage's shared operand table, each
+    distinct tensor once (read once per row by the kernel).
 
-    def __init__(self, f_out=None, outs=(), out_rows=None, dot=None):
+    ``err`` (the adaptive solvers' embedded-pair error rows): (rows, (base, cb,
+    cf, [(k_j, c_j)...]), y0, y1_out, atol, rtol) -> rows[r] = sum_c (e / tol)^2
+    in fp64 with e the combination, tol = atol + rtol * max(|y0|, |y1|), y1 = the
+    RHS input (y1_out = -1) or output ``y1_out``."""
+
+    def __init__(self, f_out=None, outs=(), out_rows=None, dot=None, err=None):
         self.f_out = f_out
         self.outs = list(outs)
         self.out_rows = out_rows  # int32 [R] or None: row r's ``outs`` stores go to row out_rows[r]
         # (y, rows, coef, accumulate) or None: rows[r] (+)= coef * <f[r], y[r]> in fp64 (fp32 state)
         self.dot = dot
+        self.err = err
+
+    def _operands(self):
+        """The distinct k tensors of every combination, in first-use order."""
+        ks, seen = [], set()
+        combos = [o[4] for o in self.outs] + ([self.err[1][3]] if self.err is not None else [])
+        for terms in combos:
+            for k, _ in terms:
+                if k.data_ptr() not in seen:
+                    seen.add(k.data_ptr())
+                    ks.append(k)
+        return ks
+
+    @property
+    def wide(self):
+        """True when the stage needs the adaptive solvers' wide epilogue (error rows,
+        or more operands than the fixed-grid epilogues prefetch)."""
+        return self.err is not None or len(self._operands()) > _lib.STAGE_PRE_K
 
     def tensors(self):
         ts = [self.f_out] if self.f_out is not None else []
         if self.dot is not None:
             ts.append(self.dot[0])
-        for out, base, _cb, _cf, ks in self.outs:
+        for out, base, _cb, _cf, _ks in self.outs:
             ts.append(out)
             if base is not None:
                 ts.append(base)
-            ts.extend(k for k, _ in ks)
+        if self.err is not None:
+            if self.err[1][0] is not None:
+                ts.append(self.err[1][0])
+            ts.append(self.err[2])
+        ts.extend(self._operands())
         return ts
 
-    def struct(self, x_input, shift=0):
+    def struct(self, x_input, shift=0, like=None):
         """ctypes struct; every pointer is moved back by ``shift`` bytes (row-block
-        buffers addressed with global row ids, dist.RowShardedLaplacian)."""
+        buffers addressed with global row ids, dist.RowShardedLaplacian).
+        ``x_input`` = the RHS input (None for a stage applied without one: ``like``
+        then gives the row shape)."""
+        ref = x_input if x_input is not None else like
         if len(self.outs) > _lib.STAGE_MAX_OUT:
             raise ValueError("at most %d stage outputs" % _lib.STAGE_MAX_OUT)
+        ks = self._operands()
+        if len(ks) > _lib.STAGE_MAX_K:
+            raise ValueError("at most %d distinct k operands per stage" % _lib.STAGE_MAX_K)
+        slot = {k.data_ptr(): j for j, k in enumerate(ks)}
         st = _lib.StageEpilogue()
         st.f_out = self.f_out.data_ptr() - shift if self.f_out is not None else None
         st.n_out = len(self.outs)
+        st.nk = len(ks)
+        for j, k in enumerate(ks):
+            st.k[j] = k.data_ptr() - shift
         if self.out_rows is not None:
             if shift:
                 raise ValueError("out_rows cannot be combined with shifted row-block buffers")
             _require_gpu(self.out_rows, "out_rows", torch.int32)
-            if self.out_rows.numel() * x_input.shape[-1] != x_input.numel():
+            if self.out_rows.numel() * ref.shape[-1] != ref.numel():
                 raise ValueError("out_rows must hold one row index per RHS row")
             st.out_rows = self.out_rows.data_ptr()
         if self.dot is not None:
             y, rows, coef, accumulate = self.dot
             _require_gpu(rows, "dot rows", torch.float64)
-            if rows.numel() * x_input.shape[-1] != x_input.numel() or shift:
+            if rows.numel() * ref.shape[-1] != ref.numel() or shift:
                 raise ValueError("dot rows must hold one fp64 per RHS row")
             st.dot_with, st.dot_rows = y.data_ptr(), rows.data_ptr()
             st.dot_coef, st.dot_accumulate = float(coef), int(bool(accumulate))
-        for i, (out, base, cb, cf, ks) in enumerate(self.outs):
-            if len(ks) > _lib.STAGE_MAX_K:
-                raise ValueError("at most %d k terms per stage output" % _lib.STAGE_MAX_K)
-            if out.data_ptr() == x_input.data_ptr():
-                raise ValueError("a stage output may not alias the RHS input")
-            o = st.o[i]
-            o.out = out.data_ptr() - shift
+
+        def fill(o, out, base, cb, cf, terms):
+            o.out = out.data_ptr() - shift if out is not None else None
             o.base = base.data_ptr() - shift if base is not None else None
             o.cb = float(cb)
             o.cf = float(cf)
-            o.nk = len(ks)
-            for j, (k, c) in enumerate(ks):
-                o.k[j] = k.data_ptr() - shift
-                o.c[j] = float(c)
+            for k, c in terms:
+                o.c[slot[k.data_ptr()]] += float(c)
+
+        for i, (out, base, cb, cf, terms) in enumerate(self.outs):
+            if x_input is not None and out.data_ptr() == x_input.data_ptr():
+                raise ValueError("a stage output may not alias the RHS input")
+            fill(st.o[i], out, base, cb, cf, terms)
+        if self.err is not None:
+            rows, (base, cb, cf, terms), y0, y1_out, atol, rtol = self.err
+            _require_gpu(rows, "error rows", torch.float64)
+            if rows.numel() * ref.shape[-1] != ref.numel() or shift:
+                raise ValueError("error rows must hold one fp64 per RHS row")
+            st.err_rows = rows.data_ptr()
+            fill(st.err, None, base, cb, cf, terms)
+            st.err_y0 = y0.data_ptr()
+            st.err_y1 = int(y1_out)
+            st.atol, st.rtol = float(atol), float(rtol)
         return st
+
+
+def stage_apply(stage, f, x, like):
+    """The stage epilogue as a pass of its own (gnpde_stage_apply_f32 / _bf16):
+    ``f`` the RHS value (None: a plain combination), ``x`` the RHS input (None
+    unless a base or the error tolerance reads it), ``like`` any row array of the
+    stage (fixes the row count, width and storage type)."""
+    dt = like.dtype
+    if dt not in STATE_DTYPES:
+        raise TypeError("stage_apply: state dtype %s" % dt)
+    lr = _rows(like, "stage rows", dt)
+    R, C = lr.shape
+    for t in stage.tensors() + [v for v in (f, x) if v is not None]:
+        _require_gpu(t, "stage tensor", dt)
+        if not t.is_contiguous() or t.numel() != lr.numel():
+            raise ValueError("stage tensors must be contiguous and shaped alike")
+    st = stage.struct(x, like=lr)
+    name = "gnpde_stage_apply_bf16" if dt == torch.bfloat16 else "gnpde_stage_apply_f32"
+    _lib.call(name, R, C, C, _ptr(f), _ptr(x), ctypes.byref(st), _stream(lr.device))
 
 
 def spmm_rhs(g, w_csr, x, x0=None, alpha=None, beta=None, rhs=True, alpha_sigmoid=True, add_source=False,
@@ -578,7 +645,14 @@ def spmm_rhs(g, w_csr, x, x0=None, alpha=None, beta=None, rhs=True, alpha_sigmoi
     transpose=True aggregates over the CSC instead (A^T x; ``w_csr`` must then
     be in CSC order) — the backward of the RHS with respect to x.
     stage: a ``Stage`` -> the fused Runge-Kutta outputs are written instead of f
-    (returns None)."""
+    (returns None).  The adaptive solvers' wide stages (Stage.wide) are fused
+    with plain weights; with weights computed on the fly (RefDstWeights) f is
+    formed first and the stage applied in a second pass (stage_apply)."""
+    if stage is not None and stage.wide and isinstance(w_csr, RefDstWeights):
+        f = spmm_rhs(g, w_csr, x, x0=x0, alpha=alpha, beta=beta, rhs=rhs, alpha_sigmoid=alpha_sigmoid,
+                     add_source=add_source, transpose=transpose)
+        stage_apply(stage, f, x, x)
+        return None
     shape = x.shape
     dt = x.dtype if isinstance(x, torch.Tensor) and x.dtype in STATE_DTYPES else torch.float32
     xr = _rows(x, "x", dt)
@@ -924,6 +998,8 @@ def attn_dot_rhs(g, ns, x, x0=None, alpha=None, beta=None, rhs=True, alpha_sigmo
     H, dk = ns.heads, ns.dk
     if not _lib.fn("gnpde_attn_dot_supported")(H, dk, C):
         return NotImplemented
+    if stage is not None and (stage.wide or len(stage.outs) > 1 or stage.dot is not None):
+        return NotImplemented  # fused here: single-output fixed-grid stages (the caller takes K2 + K1)
     if ns.ldqk % 4 or ns.q.data_ptr() % 16 or ns.k.data_ptr() % 16 or xr.data_ptr() % 16:
         return NotImplemented
     if xr.shape[0] != g.R:

@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define GNPDE_ABI_VERSION 2
+#define GNPDE_ABI_VERSION 3
 
 #define GNPDE_OK 0
 #define GNPDE_EINVAL (-1)
@@ -167,9 +167,11 @@ size_t gnpde_plan_workspace_bytes(int64_t R);
 /* ---------------------------------------------------------------- fused solver epilogue
  * Optional stage outputs of the RHS kernels, so a Runge-Kutta stage combination
  * y0 + dt*sum_j b_j k_j is produced by the same pass that computes k_i (no
- * separate read of k_i, no extra launch).  With f = the RHS value of row r:
- *   f_out[r]    = f                                       (f_out may be NULL)
- *   o[i].out[r] = cb*base[r] + cf*f + sum_{j<nk} c[j]*k[j][r]   for i < n_out
+ * separate read of k_i, no extra launch).  A stage has nk shared operand
+ * arrays k[0..nk-1] (each read once per row however many outputs use it); with
+ * f = the RHS value of row r:
+ *   f_out[r]    = f                                            (f_out may be NULL)
+ *   o[i].out[r] = cb*base[r] + cf*f + sum_{j<nk} o[i].c[j]*k[j][r]   for i < n_out
  * base may be NULL (0), equal to the RHS input x (the row already read by the
  * epilogue is reused) or equal to o[i].out (in-place accumulation).  Every
  * array has the leading dimension ldf of the RHS output.  No output may alias
@@ -182,16 +184,25 @@ size_t gnpde_plan_workspace_bytes(int64_t R);
  *   dot_rows[r] (+)= dot_coef * sum_c f[r,c] * dot_with[r,c]   (fp64; "+=" when
  * dot_accumulate), summed over the row's lanes in a fixed order — the per-row
  * terms of a parameter gradient <f, y> that the caller reduces once
- * (gnpde_sum_f64), instead of a separate pass re-reading f.                    */
+ * (gnpde_sum_f64), instead of a separate pass re-reading f.
+ * err_rows (NULL = none): the error estimate of an embedded Runge-Kutta pair
+ * (torchdiffeq's RKAdaptiveStepsizeODESolver: error_ratio = RMS(e / tol)):
+ *   e      = err.cb*err.base + err.cf*f + sum_{j<nk} err.c[j]*k[j]   (err.out unused)
+ *   y1     = the RHS input x (err_y1 = -1) or the value of output err_y1
+ *   tol    = atol + rtol * max(|err_y0|, |y1|)
+ *   err_rows[r] = sum_c (e / tol)^2     (fp64, the row's lanes in a fixed order)
+ * which the caller sums (gnpde_sum_f64) into the squared norm of one step.
+ * At most 2 k operands with dot_rows; err_rows and 3..6 operands take the wide
+ * epilogue (operands loaded after the aggregation), fused into the plain-weight
+ * K1 (gnpde_spmm_rhs_f32 / _bf16); the attention kernels return
+ * GNPDE_EUNSUPPORTED for it (the caller applies it with gnpde_stage_apply_*).  */
 #define GNPDE_STAGE_MAX_OUT 2
-#define GNPDE_STAGE_MAX_K 2
+#define GNPDE_STAGE_MAX_K 6
 typedef struct {
   float* out;
   const float* base;
   float cb;
   float cf;
-  int nk;
-  const float* k[GNPDE_STAGE_MAX_K];
   float c[GNPDE_STAGE_MAX_K];
 } gnpde_stage_out_t;
 
@@ -199,12 +210,34 @@ typedef struct {
   float* f_out;
   int n_out;
   gnpde_stage_out_t o[GNPDE_STAGE_MAX_OUT];
+  int nk;
+  const float* k[GNPDE_STAGE_MAX_K];
   const int32_t* out_rows;
   const float* dot_with;
   double* dot_rows;
   double dot_coef;
   int dot_accumulate;
+  double* err_rows;
+  gnpde_stage_out_t err;
+  const float* err_y0;
+  int err_y1;
+  double atol;
+  double rtol;
 } gnpde_stage_epilogue_t;
+
+/* The stage epilogue as a pass of its own, over rows [0, R) of C columns
+ * (leading dimension ld, every array of the stage included): f [R, ld] is the
+ * RHS value (NULL: every cf term is 0 — a plain combination such as a stage
+ * input y0 + dt*b0*k0 or dense output), x the RHS input (needed when a base is
+ * x or err_y1 = -1; may be NULL otherwise).  Same arithmetic, per element, as
+ * the fused epilogue (fp32; err_rows in fp64).  bf16: every row array is bf16
+ * (the struct's float* reinterpreted), the arithmetic fp32.  Used by the
+ * adaptive solvers for the attention RHS kernels that fuse only the fixed-grid
+ * stages, and for the pre-step and dense-output combinations.               */
+int gnpde_stage_apply_f32(int64_t R, int64_t C, int64_t ld, const float* f, const float* x,
+                          const gnpde_stage_epilogue_t* stage, void* stream);
+int gnpde_stage_apply_bf16(int64_t R, int64_t C, int64_t ld, const uint16_t* f, const uint16_t* x,
+                           const gnpde_stage_epilogue_t* stage, void* stream);
 
 /* ---------------------------------------------------------------- K1: SpMM RHS
  * ax[r,:] = sum_{p in row r} w[p] * x[col[p],:]

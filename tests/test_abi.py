@@ -46,7 +46,7 @@ def test_library_built_from_these_sources():
 
 
 def test_abi_version():
-    assert _lib.load().gnpde_abi_version() == _lib.ABI_VERSION == 2
+    assert _lib.load().gnpde_abi_version() == _lib.ABI_VERSION == 3
 
 
 def test_library_is_gfx950_code_object():
@@ -88,11 +88,25 @@ def test_errors_are_reported_not_raised():
     # catches a library built against a stale header layout
     st = _lib.StageEpilogue()
     st.n_out = 1
-    st.o[0].out, st.o[0].cb, st.o[0].cf, st.o[0].nk = 4096, 1.0, 0.5, 1
-    st.o[0].k[0], st.o[0].c[0] = 8192, 2.0
+    st.o[0].out, st.o[0].cb, st.o[0].cf = 4096, 1.0, 0.5
+    st.nk, st.k[0], st.o[0].c[0] = 1, 8192, 2.0
     rc = lib.gnpde_spmm_rhs_f32(vp(0), 0, vp(0), 0, vp(0), vp(0), 4, vp(16), 4, vp(0), 0, vp(32), vp(0), 1, vp(0), 4,
                                 vp(0), 0, ctypes.byref(st), vp(0))
     assert rc == 0, lib.gnpde_last_error()
+    # the wide (adaptive) epilogue: error rows need err_y0 and an output or x for y1
+    st.err_rows, st.err_y1, st.atol, st.rtol = 16384, -1, 1e-7, 1e-9
+    rc = lib.gnpde_spmm_rhs_f32(vp(0), 0, vp(0), 0, vp(0), vp(0), 4, vp(16), 4, vp(0), 0, vp(32), vp(0), 1, vp(0), 4,
+                                vp(0), 0, ctypes.byref(st), vp(0))
+    assert rc == -1 and b"err_y0" in lib.gnpde_last_error()
+    st.err_y0 = 32768
+    st.err_y1 = 1
+    rc = lib.gnpde_stage_apply_f32(0, 4, 4, vp(0), vp(0), ctypes.byref(st), vp(0))
+    assert rc == -1 and b"err_y1" in lib.gnpde_last_error()
+    st.err_y1 = 0
+    assert lib.gnpde_stage_apply_f32(0, 4, 4, vp(0), vp(0), ctypes.byref(st), vp(0)) == 0
+    st.nk = 7
+    rc = lib.gnpde_stage_apply_bf16(0, 4, 4, vp(0), vp(0), ctypes.byref(st), vp(0))
+    assert rc == -1 and b"nk=7" in lib.gnpde_last_error()
     rc = lib.gnpde_linear_f32(vp(0), 10, 4, 4, vp(0), vp(0), 8, 8, vp(0), 8, vp(0), 0, vp(0))
     assert rc == -1 and b"NULL" in lib.gnpde_last_error()
     rc = lib.gnpde_csr_build(vp(0), 1, 10, 5, 2, vp(0), vp(0), vp(0), vp(0), 0, vp(0))
@@ -111,15 +125,17 @@ def test_python_wrapper_raises_with_message():
 
 
 def test_stage_struct_layout_matches_header():
-    # gnpde_stage_out_t: out, base (8 B each), cb, cf, nk (4 B each), k[2] (8 B, aligned), c[2]
-    assert ctypes.sizeof(_lib.StageOut) == 8 + 8 + 4 + 4 + 4 + 4 + 16 + 8
-    assert _lib.StageOut.k.offset == 32
-    # gnpde_stage_epilogue_t: f_out, n_out (padded to 8), o[2], out_rows, dot_with, dot_rows, dot_coef,
-    # dot_accumulate (padded to 8)
+    # gnpde_stage_out_t (ABI 3): out, base (8 B each), cb, cf (4 B each), c[6] -> 48 B
+    assert ctypes.sizeof(_lib.StageOut) == 8 + 8 + 4 + 4 + 4 * 6
+    assert _lib.StageOut.c.offset == 24
+    # gnpde_stage_epilogue_t: f_out, n_out (padded to 8), o[2], nk (padded to 8), k[6], out_rows, dot_with,
+    # dot_rows, dot_coef, dot_accumulate (padded to 8), err_rows, err, err_y0, err_y1 (padded), atol, rtol
     so = ctypes.sizeof(_lib.StageOut)
-    assert ctypes.sizeof(_lib.StageEpilogue) == 8 + 8 + 2 * so + 8 + 8 + 8 + 8 + 8
-    assert _lib.StageEpilogue.out_rows.offset == 16 + 2 * so
-    assert _lib.StageEpilogue.dot_coef.offset == 16 + 2 * so + 24
+    assert _lib.StageEpilogue.nk.offset == 16 + 2 * so
+    assert _lib.StageEpilogue.out_rows.offset == 16 + 2 * so + 8 + 48
+    assert _lib.StageEpilogue.dot_coef.offset == _lib.StageEpilogue.out_rows.offset + 24
+    assert _lib.StageEpilogue.err.offset == _lib.StageEpilogue.dot_coef.offset + 24
+    assert ctypes.sizeof(_lib.StageEpilogue) == _lib.StageEpilogue.err.offset + so + 8 + 8 + 8 + 8
 
 
 def test_workspace_size_queries():
@@ -141,16 +157,19 @@ def test_c_header_struct_layout_with_gcc(tmp_path):
         pytest.skip("gcc not available")
     src = tmp_path / "layout.c"
     src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "gnpde.h"\nint main(void){'
-                   'printf("%zu %zu %zu %zu %zu %zu %zu\\n", sizeof(gnpde_stage_out_t), offsetof(gnpde_stage_out_t, k),'
-                   'offsetof(gnpde_stage_out_t, c), sizeof(gnpde_stage_epilogue_t),'
-                   'offsetof(gnpde_stage_epilogue_t, out_rows), offsetof(gnpde_stage_epilogue_t, dot_coef),'
-                   'offsetof(gnpde_stage_epilogue_t, dot_accumulate));return 0;}\n')
+                   'printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\\n", sizeof(gnpde_stage_out_t),'
+                   'offsetof(gnpde_stage_out_t, c), sizeof(gnpde_stage_epilogue_t), offsetof(gnpde_stage_epilogue_t, nk),'
+                   'offsetof(gnpde_stage_epilogue_t, k), offsetof(gnpde_stage_epilogue_t, out_rows),'
+                   'offsetof(gnpde_stage_epilogue_t, dot_coef), offsetof(gnpde_stage_epilogue_t, dot_accumulate),'
+                   'offsetof(gnpde_stage_epilogue_t, err), offsetof(gnpde_stage_epilogue_t, err_y1),'
+                   'offsetof(gnpde_stage_epilogue_t, rtol));return 0;}\n')
     exe = tmp_path / "layout"
     subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
     got = [int(v) for v in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()]
-    assert got == [ctypes.sizeof(_lib.StageOut), _lib.StageOut.k.offset, _lib.StageOut.c.offset,
-                   ctypes.sizeof(_lib.StageEpilogue), _lib.StageEpilogue.out_rows.offset,
-                   _lib.StageEpilogue.dot_coef.offset, _lib.StageEpilogue.dot_accumulate.offset]
+    E = _lib.StageEpilogue
+    assert got == [ctypes.sizeof(_lib.StageOut), _lib.StageOut.c.offset, ctypes.sizeof(E), E.nk.offset, E.k.offset,
+                   E.out_rows.offset, E.dot_coef.offset, E.dot_accumulate.offset, E.err.offset, E.err_y1.offset,
+                   E.rtol.offset]
 
 
 def test_stale_library_is_refused(monkeypatch):

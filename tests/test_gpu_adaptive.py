@@ -1,0 +1,259 @@
+"""GPU parity of the fused adaptive solvers (gnpde.integrator._RKAdaptiveFused:
+dopri5 — the method of every src/best_params.py entry — bosh3, fehlberg2 and
+adaptive_heun with every stage combination and the error rows in the RHS
+epilogues, include/gnpde.h gnpde_stage_epilogue_t):
+
+* against the oracle's float64 restatement of torchdiffeq's adaptive loop
+  (O.odeint_adaptive) on the oracle RHS: the same accepted / rejected step
+  sequence, values within 1e-5 (torchdiffeq is absent: integrated-value parity
+  is unpinned against the reference, whose tests check shapes only);
+* against the unfused tableau loop (GNPDE_FUSED_ADAPTIVE=0) on the same HIP RHS;
+* the stage pass (gnpde_stage_apply_*) against torch on random operands, and
+  against the fused epilogue bit for bit from the same f;
+* bf16 state: no torch stage combination anywhere (the fp32 testing aid
+  _torch_combine is never called), within bf16 rounding of the fp32 solve."""
+import numpy as np
+import pytest
+import torch
+
+import gnpde
+import gnpde_oracle as O
+from gnpde import integrator as gi, ops
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+RTOL = 1e-5
+
+OPT = {'self_loop_weight': 1, 'leaky_relu_slope': 0.2, 'heads': 2, 'attention_norm_idx': 0, 'add_source': False,
+       'hidden_dim': 6, 'block': 'constant', 'function': 'laplacian', 'augment': False, 'adjoint': False,
+       'tol_scale': 1, 'time': 1, 'method': 'dopri5', 'no_alpha_sigmoid': False, 'reweight_attention': False,
+       'step_size': 1, 'beltrami': False, 'attention_type': 'scaled_dot', 'square_plus': False, 'max_nfe': 10 ** 7,
+       'data_norm': 'rw', 'max_iters': 1000, 'multi_modal': False, 'mix_features': False, 'attention_dim': 16}
+
+
+def rel(a, b):
+    a = a.detach().double().cpu().numpy() if isinstance(a, torch.Tensor) else np.asarray(a, np.float64)
+    b = b.detach().double().cpu().numpy() if isinstance(b, torch.Tensor) else np.asarray(b, np.float64)
+    return np.abs(a - b).max() / max(np.abs(b).max(), 1e-30)
+
+
+def T(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+
+
+def _graph(N, E, seed):
+    rng = np.random.default_rng(seed)
+    ei = rng.integers(0, N, size=(1, 2, E))
+    ei[:, 0, :E // 8] = 0  # a hub row: split plan, in-launch combine in the wide epilogue too
+    eis, ws = O.get_rw_adj(ei, norm_dim=1, fill_value=1.0, num_nodes=N)
+    return np.stack(eis, 0), np.stack(ws, 0), rng
+
+
+def _laplacian(C, eo, wo, alpha=0.3, add_source=False, x0=None):
+    func = gnpde.LaplacianODEFunc(C, C, dict(OPT, hidden_dim=C, add_source=add_source), DEV).to(DEV)
+    func.edge_index, func.edge_weight = T(eo), T(wo.astype(np.float32))
+    if x0 is not None:
+        func.x0 = x0
+    with torch.no_grad():
+        func.alpha_train.fill_(alpha)
+        func.beta_train.fill_(0.4)
+    return func
+
+
+@pytest.mark.parametrize("method", ["dopri5", "bosh3", "fehlberg2", "adaptive_heun"])
+def test_fused_adaptive_vs_oracle_steps(method):
+    N, E, C = 3000, 24000, 32
+    eo, wo, rng = _graph(N, E, 31)
+    x = rng.standard_normal((1, N, C)).astype(np.float32)
+    func = _laplacian(C, eo, wo, alpha=0.0)
+    ts = [0.0, 0.05, 0.5, 1.0]
+    with torch.no_grad():
+        got = gi.odeint(func, T(x), torch.tensor(ts, dtype=torch.float64, device=DEV), rtol=1e-3, atol=1e-4,
+                        method=method)
+    n_got = gi.odeint.last_n_steps
+    f = lambda t, y: O.laplacian_rhs(eo, y, None, 0.0, 0.0, edge_weight=wo)  # noqa: E731
+    want, n_want = O.odeint_adaptive(f, x, ts, method, 1e-3, 1e-4)
+    assert n_got == n_want
+    assert rel(got, want) <= RTOL
+
+
+@pytest.mark.parametrize("method", ["dopri5", "bosh3", "fehlberg2", "adaptive_heun"])
+def test_fused_adaptive_vs_unfused_loop(method, monkeypatch):
+    """Same HIP RHS, fused step against the tableau loop (separate combination and
+    norm passes): same step count, values within fp32 rounding; the fused solve
+    runs every RHS through rhs_stage."""
+    N, E, C = 5000, 60000, 64
+    eo, wo, rng = _graph(N, E, 32)
+    x = T(rng.standard_normal((1, N, C)).astype(np.float32))
+    x0 = T(rng.standard_normal((1, N, C)).astype(np.float32))
+    func = _laplacian(C, eo, wo, add_source=True, x0=x0)
+    t = torch.tensor([0.0, 0.7, 1.5], dtype=torch.float64, device=DEV)
+    calls = {'stage': 0}
+    orig = func.rhs_stage
+
+    def spy(*a, **k):
+        calls['stage'] += 1
+        return orig(*a, **k)
+
+    with torch.no_grad():
+        func.rhs_stage = spy
+        fused = gi.odeint(func, x, t, rtol=1e-5, atol=1e-6, method=method)
+        n_fused = gi.odeint.last_n_steps
+        del func.rhs_stage
+        monkeypatch.setenv("GNPDE_FUSED_ADAPTIVE", "0")
+        loop = gi.odeint(func, x, t, rtol=1e-5, atol=1e-6, method=method)
+        n_loop = gi.odeint.last_n_steps
+    assert n_fused == n_loop
+    assert calls['stage'] == gi._adaptive_plan(method).ns * n_fused
+    assert rel(fused, loop) <= 2e-6
+
+
+def _random_stage(rows, C, dtype, gen, n_out=2, nk=5, err_y1=-1):
+    mk = lambda: torch.randn(rows, C, generator=gen, device=DEV).to(dtype)  # noqa: E731
+    ks = [mk() for _ in range(nk)]
+    x, y0 = mk(), mk()
+    outs = []
+    for i in range(n_out):
+        base = x if i == 0 else y0
+        outs.append((torch.empty_like(x), base, 0.7 + i, -0.3, [(k, 0.1 * (j + 1) - 0.25 * i) for j, k in enumerate(ks)]))
+    e_rows = torch.empty(rows, dtype=torch.float64, device=DEV)
+    err = (e_rows, (None, 0.0, 1e-3, [(k, 1e-3 * (j - 2)) for j, k in enumerate(ks)]), y0, err_y1, 1e-4, 1e-3)
+    return ops.Stage(f_out=torch.empty_like(x), outs=outs, err=err), ks, x, y0
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("C", [32, 80, 128, 168, 256])
+def test_stage_apply_vs_torch(dtype, C):
+    gen = torch.Generator(device=DEV)
+    gen.manual_seed(C)
+    R = 1000
+    st, ks, x, y0 = _random_stage(R, C, dtype, gen, err_y1=1)
+    f = torch.randn(R, C, generator=gen, device=DEV).to(dtype)
+    ops.stage_apply(st, f, x, x)
+    F, X, Y0 = f.float(), x.float(), y0.float()
+    Ks = [k.float() for k in ks]
+    vals = []
+    for out, base, cb, cf, terms in st.outs:
+        want = cb * base.float() + sum(c * k.float() for k, c in terms) + cf * F
+        vals.append(want)
+        tol = 1e-6 if dtype == torch.float32 else 2 ** -7
+        assert rel(out.float(), want) <= tol
+    assert torch.equal(st.f_out, f)
+    e = sum(c * k for k, c in zip(Ks, [1e-3 * (j - 2) for j in range(len(Ks))])) + 1e-3 * F
+    # err_y1 = 1: the tolerance reads output 1 as computed (fp32, before the bf16 rounding of its store)
+    tol = 1e-4 + 1e-3 * torch.maximum(Y0.abs(), vals[1].abs())
+    want_rows = ((e.double() / tol.double()) ** 2).sum(-1)
+    assert rel(st.err[0], want_rows) <= 1e-5
+    assert X.shape == F.shape
+
+
+def test_wide_epilogue_bit_equal_to_stage_pass():
+    """The fused wide epilogue (K1, STG 4) and the stage pass applied to K1's f give
+    the same bits (same per-element arithmetic in the same order), error rows
+    included (same lane partials, same xor tree)."""
+    N, E, C = 4000, 50000, 128
+    eo, wo, rng = _graph(N, E, 33)
+    x = T(rng.standard_normal((1, N, C)).astype(np.float32))
+    g = ops.GraphCSR(T(eo), N)
+    w = g.gather_weights(T(wo.astype(np.float32)))
+    a = torch.tensor(0.2, device=DEV)
+    gen = torch.Generator(device=DEV)
+    gen.manual_seed(5)
+    st1, ks, _, y0 = _random_stage(N, C, torch.float32, gen, err_y1=0)
+    st1.outs[0] = (st1.outs[0][0], x.view(N, C), *st1.outs[0][2:])  # base = the RHS input
+    ops.spmm_rhs(g, w, x, alpha=a, stage=st1)
+    f = ops.spmm_rhs(g, w, x, alpha=a)
+    outs2 = [(torch.empty_like(o[0]),) + tuple(o[1:]) for o in st1.outs]
+    rows2 = torch.empty_like(st1.err[0])
+    st2 = ops.Stage(f_out=torch.empty_like(st1.f_out), outs=outs2, err=(rows2,) + tuple(st1.err[1:]))
+    ops.stage_apply(st2, f.view(N, C), x.view(N, C), x.view(N, C))
+    assert torch.equal(st1.f_out, st2.f_out)
+    for o1, o2 in zip(st1.outs, st2.outs):
+        assert torch.equal(o1[0], o2[0])
+    # error rows: the same per-element terms; the row sums differ only by the lane tree
+    # of the two geometries (K1's 32-lane rows vs the pass's) -> within fp64 rounding
+    assert rel(st1.err[0], rows2) <= 1e-12
+
+
+def test_bf16_dopri5_without_torch_combinations(monkeypatch):
+    """bf16 state (configs[3]'s storage) under dopri5: every stage combination in
+    HIP (the wide bf16 epilogue and the bf16 stage pass), never _torch_combine;
+    within bf16 rounding of the fp32 solve."""
+    N, E, C = 4000, 40000, 168
+    eo, wo, rng = _graph(N, E, 34)
+    x = T(rng.standard_normal((1, N, C)).astype(np.float32))
+    func = _laplacian(C, eo, wo)
+    t = torch.tensor([0.0, 1.0], dtype=torch.float64, device=DEV)
+
+    def boom(*a, **k):
+        raise AssertionError("_torch_combine on the product path")
+
+    monkeypatch.setattr(gi, "_torch_combine", boom)
+    with torch.no_grad():
+        z32 = gi.odeint(func, x, t, rtol=1e-3, atol=1e-4, method='dopri5')[1]
+        zb = gi.odeint(func, x.to(torch.bfloat16), t, rtol=1e-3, atol=1e-4, method='dopri5')[1]
+    assert zb.dtype == torch.bfloat16
+    assert rel(zb.float(), z32) <= 2e-2
+
+
+def test_attention_rhs_dopri5_fused_vs_unfused(monkeypatch):
+    """The transformer RHS (fork scaled_dot, norm_idx 1: weights formed inside K1 from
+    the statistics records, a policy the wide epilogue is not fused with) under
+    dopri5: f then the stage pass; same steps and values as the tableau loop."""
+    N, E, C, h, att = 2708, 10556, 80, 8, 128
+    rng = np.random.default_rng(41)
+    ei = rng.integers(0, N, size=(1, 2, E))
+    eo, _ = (np.stack(a, 0) for a in O.get_rw_adj(ei, norm_dim=1, fill_value=1.0, num_nodes=N))
+    opt = dict(OPT, hidden_dim=C, heads=h, attention_dim=att, function='transformer', attention_norm_idx=1)
+    func = gnpde.ODEFuncTransformerAtt(C, C, opt, DEV).to(DEV).eval()
+    lay = func.multihead_att_layer
+    with torch.no_grad():
+        for lin in (lay.Q, lay.K):
+            lin.weight.copy_(T((rng.standard_normal((att, C)) * 0.03).astype(np.float32)))
+            lin.bias.copy_(T((rng.standard_normal(att) * 0.03).astype(np.float32)))
+        func.alpha_train.fill_(0.5)
+    func.edge_index = T(eo)
+    x = T(rng.standard_normal((1, N, C)).astype(np.float32))
+    t = torch.tensor([0.0, 1.0], dtype=torch.float64, device=DEV)
+    with torch.no_grad():
+        fused = gi.odeint(func, x, t, rtol=1e-7, atol=1e-9, method='dopri5')
+        n_fused = gi.odeint.last_n_steps
+        monkeypatch.setenv("GNPDE_FUSED_ADAPTIVE", "0")
+        loop = gi.odeint(func, x, t, rtol=1e-7, atol=1e-9, method='dopri5')
+    assert gi.odeint.last_n_steps == n_fused
+    assert rel(fused, loop) <= 2e-6
+
+
+def test_c2_dopri5_default_tolerances_vs_oracle_steps():
+    """configs[1] (C2): Cora-sized graph, function=transformer with the fork's
+    scaled_dot, heads 8, attention_dim 128, norm_idx 1, dopri5 at the reference's
+    default tolerances (tol_scale 1: atol 1e-7, rtol 1e-9, src/base_classes.py:
+    set_tol), through ConstantODEblock, against the oracle's float64 restatement of
+    the same adaptive loop on the oracle RHS: same step sequence, values within 1e-5."""
+    N, E, C, h, att = 2708, 10556, 80, 8, 128
+    rng = np.random.default_rng(90)
+    ei = rng.integers(0, N, size=(1, 2, E))
+    x = rng.standard_normal((1, N, C)).astype(np.float32)
+    opt = dict(OPT, hidden_dim=C, heads=h, attention_dim=att, function='transformer', attention_norm_idx=1,
+               method='dopri5', tol_scale=1.0)
+    blk = gnpde.ConstantODEblock(gnpde.ODEFuncTransformerAtt, [], opt, DEV, t=torch.tensor([0, 1])).to(DEV).eval()
+    lay = blk.odefunc.multihead_att_layer
+    Wq, Wk = [(rng.standard_normal((att, C)) * 0.03).astype(np.float32) for _ in range(2)]
+    bq, bk = [(rng.standard_normal(att) * 0.03).astype(np.float32) for _ in range(2)]
+    with torch.no_grad():
+        lay.Q.weight.copy_(T(Wq))
+        lay.Q.bias.copy_(T(bq))
+        lay.K.weight.copy_(T(Wk))
+        lay.K.bias.copy_(T(bk))
+        blk.odefunc.alpha_train.fill_(0.5)
+    data = gnpde.GraphData()
+    data.new_graph(T(ei), N)
+    with torch.no_grad():
+        z = blk(T(x), data)
+    n_got = gi.odeint.last_n_steps
+    eo, _ = (np.stack(a, 0) for a in O.get_rw_adj(ei, norm_dim=1, fill_value=1.0, num_nodes=N))
+    f = lambda t, y: O.transformer_rhs(eo, y, None, Wq, bq, Wk, bk, h, 1, 0.5, 0.0)  # noqa: E731
+    want, n_want = O.odeint_adaptive(f, x, [0.0, 1.0], 'dopri5', 1e-9, 1e-7)
+    print("C2 dopri5 steps: gnpde %d, oracle %d" % (n_got, n_want))
+    assert n_got == n_want
+    assert rel(z, want[-1]) <= RTOL

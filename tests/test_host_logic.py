@@ -312,3 +312,43 @@ def test_tensor_key_is_identity_not_address():
     assert ka != _tensor_key(b) and ka == _tensor_key(a)
     a.add_(1)
     assert ka != _tensor_key(a)
+
+
+@pytest.mark.parametrize("method", list(gode.ADAPTIVE_METHODS))
+@pytest.mark.parametrize("tol", [1e-3, 1e-7])
+def test_fused_adaptive_plan_matches_the_tableau_loop(method, tol):
+    """The fused adaptive step (integrator._AdaptivePlan: each stage input, y1 and the
+    error estimate formed in the RHS epilogues from the operands the plan picks, the
+    error norm from per-row terms, dense output as two stage passes) against the
+    tableau loop (_RKAdaptive) in float64 on CPU: the same step sequence and the same
+    values to rounding, several output times inside one step included."""
+    from host_stage import HostLinearRHS
+    rng = np.random.default_rng(7)
+    C = 6
+    A = torch.from_numpy(rng.standard_normal((C, C)) * 0.7)
+    y0 = torch.from_numpy(rng.standard_normal((1, 40, C)))
+    ts = torch.tensor([0.0, 0.01, 0.02, 0.3, 1.0, 2.5], dtype=torch.float64)
+    want = gode.odeint(lambda t, y: y @ A.T, y0, ts, method=method, rtol=tol, atol=tol * 0.1,
+                       combine=gode._torch_combine)
+    n_want = gode.odeint.last_n_steps
+    f = HostLinearRHS(A)
+    with torch.no_grad():  # the fused paths are the no-grad ones
+        got = gode.odeint(f, y0, ts, method=method, rtol=tol, atol=tol * 0.1, combine=gode._Combine())
+    assert gode.odeint.last_n_steps == n_want
+    assert float((got - want).abs().max()) <= 1e-11 * max(1.0, float(want.abs().max()))
+    P = gode._adaptive_plan(method)
+    assert f.nfe == 2 + P.ns * n_want  # f0, the initial-step probe, then len(alpha) per step
+    assert f.n_stage == P.ns * n_want  # every stage through the fused epilogue
+
+
+def test_fused_adaptive_plan_dopri5_operands():
+    """dopri5's plan: every stage input from the launch's own input (no y0 read), the
+    error's first six terms precomputed by the launch that forms y1 (a second
+    output), so the FSAL launch reads only that partial and y0; k5 is stored only on
+    steps that may cross an output time (dense output)."""
+    P = gode._adaptive_plan('dopri5')
+    assert P.fsal and P.ns == 6
+    assert all(L['next'][0] == 'X' for L in P.launches[:5])
+    assert P.launches[4]['epart'] is not None and P.launches[5]['err'][0] == 'E'
+    assert P.reads[5] == set()
+    assert P.store == {1, 2, 3, 4, 6} and P.store_mid == {5}
