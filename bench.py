@@ -327,6 +327,8 @@ def bench_single(args, world, rank, dev):
         progress("attention done")
         result["blend_c162"] = bench_blend(g, dev)
         progress("blend done")
+    if not args.no_attention and rank == 0:
+        result["dopri5"] = bench_dopri5(ei, w, x, dev, k1_ms, plain["rhs_ms"] if plain else None)
     if not args.no_train and rank == 0 and world == 1:
         result["block_forward"] = bench_block(ei, x, h, dev)
         result["train_rk4"] = bench_train(ei, w, x, h, dev)
@@ -692,6 +694,91 @@ def bench_blend(g, dev, reps=50):
     rel = float((a - b).abs().max() / a.abs().max())
     out["check"] = {"bf16_vs_fp32_rel": round(rel, 6), "constant_state_rhs_max": const_rhs,
                     "ok": bool(rel <= 2e-2 and const_rhs <= 1e-5)}
+    return out
+
+
+# src/best_params.py: every dataset integrates with dopri5; ogbn-arxiv (:7) over T = 3.676 at
+# tol_scale 11353.6, Cora (:1, configs[1]) over T = 18.29 at tol_scale 822.0 (atol = 1e-7 tol_scale,
+# rtol = 1e-9 tol_scale, src/base_classes.py set_tol)
+ARXIV_DOPRI5 = (3.6760155951687636, 11353.558848254957)
+CORA_DOPRI5 = (18.294754260552843, 821.9773048827274)
+
+
+def _timed_dopri5(func, x, T, tol_scale, dev, reps):
+    """One warm-up solve, then `reps` solves of dopri5 over [0, T] timed between
+    device syncs (the step's one host read is inside)."""
+    import gnpde
+    import gnpde.integrator as integ
+    t = torch.tensor([0.0, T], dtype=torch.float32, device=dev)
+    kw = dict(method='dopri5', rtol=1e-9 * tol_scale, atol=1e-7 * tol_scale)
+    with torch.no_grad():
+        z = gnpde.odeint(func, x, t, **kw)[1]
+        torch.cuda.synchronize()
+        nfe0 = func.nfe
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            z = gnpde.odeint(func, x, t, **kw)[1]
+        torch.cuda.synchronize()
+        el = (time.perf_counter() - t0) / reps
+    assert torch.isfinite(z).all()
+    steps = integ.odeint.last_n_steps
+    nfe = (func.nfe - nfe0) // reps
+    return el, steps, nfe
+
+
+def bench_dopri5(ei, w, x, dev, k1_stage_ms, k1_plain_ms, reps=3):
+    """dopri5 as the reference runs it (src/best_params.py): the fused adaptive step
+    (gnpde.integrator._RKAdaptiveFused: stage combinations and error rows in the RHS
+    epilogues, one fixed-order norm reduction and one host read per step).
+    G-arxiv Laplacian at ogbn-arxiv's T / tol_scale, and configs[1]'s shape (a
+    Cora-sized graph, transformer RHS: fork scaled_dot, heads 8, attention_dim 128,
+    norm_idx 1, C = 80) at Cora's."""
+    import gnpde
+    import gnpde.integrator as integ
+    from gnpde import synthetic
+    out = {}
+    C = x.shape[-1]
+    func = gnpde.LaplacianODEFunc(C, C, dict(LAP_OPT, hidden_dim=C), dev).to(dev)
+    func.edge_index, func.edge_weight = ei, w
+    T, ts = ARXIV_DOPRI5
+    el, steps, nfe = _timed_dopri5(func, x, T, ts, dev, reps)
+    plan = integ._adaptive_plan('dopri5')
+    ms_step = el * 1e3 / max(steps, 1)
+    r, wr = plan.state_passes()
+    out["garxiv_laplacian"] = {
+        "config": "G-arxiv laplacian (C=128), dopri5 over [0, %.3f], tol_scale %.1f (ogbn-arxiv best_params)" % (T, ts),
+        "ms_per_solve": round(el * 1e3, 4), "steps": steps, "rhs_evals": nfe, "ms_per_step": round(ms_step, 4),
+        "rhs_evals_per_s": round(nfe / el, 1),
+        "ms_per_step_over_6_rhs_stage": round(ms_step / (6 * k1_stage_ms), 4),
+        "ms_per_step_over_6_rhs_plain": round(ms_step / (6 * k1_plain_ms), 4) if k1_plain_ms else None,
+        "state_passes_per_step": {"reads": r, "writes": wr},
+        "basis": "6 RHS launches per step carrying the stage combinations and the error rows + 1 stage-input pass + "
+                 "the norm reduction and one host read; rhs_stage_ms = the rk4 fused-stage K1 launch time"}
+    progress("dopri5 G-arxiv: %.3f ms/step, %d steps" % (ms_step, steps))
+    # configs[1] shape
+    N, E, Cc, h, att = 2708, 13264, 80, 8, 128  # Cora: 10,556 edges + 2,708 self loops (SURVEY §8(a) C2)
+    gei, _ = synthetic.rw_graph(N, E, seed=5, device=dev)
+    xc = synthetic.features(1, N, Cc, seed=6, device=dev)
+    opt = {'hidden_dim': Cc, 'heads': h, 'attention_dim': att, 'attention_norm_idx': 1, 'attention_type': 'scaled_dot',
+           'function': 'transformer', 'add_source': False, 'no_alpha_sigmoid': False, 'max_nfe': 10 ** 9,
+           'multi_modal': False, 'mix_features': False, 'square_plus': False, 'beltrami': False}
+    tf = gnpde.ODEFuncTransformerAtt(Cc, Cc, opt, dev).to(dev).eval()
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(11)
+    with torch.no_grad():
+        for lin in (tf.multihead_att_layer.Q, tf.multihead_att_layer.K):
+            lin.weight.copy_(torch.randn(att, Cc, generator=gen, device=dev) * 0.03)
+            lin.bias.copy_(torch.randn(att, generator=gen, device=dev) * 0.03)
+    tf.edge_index = gei
+    T, ts = CORA_DOPRI5
+    el, steps, nfe = _timed_dopri5(tf, xc, T, ts, dev, reps)
+    out["c2_transformer"] = {
+        "config": "configs[1] shape: N=2708 E'=%d (RMAT + self loops), transformer RHS (fork scaled_dot, heads 8, "
+                  "attention_dim 128, norm_idx 1), C=80, dopri5 over [0, %.2f], tol_scale %.1f (Cora best_params)"
+                  % (E, T, ts),
+        "ms_per_solve": round(el * 1e3, 4), "steps": steps, "rhs_evals": nfe,
+        "ms_per_step": round(el * 1e3 / max(steps, 1), 4), "rhs_evals_per_s": round(nfe / el, 1)}
+    progress("dopri5 C2: %.3f ms/step, %d steps" % (el * 1e3 / max(steps, 1), steps))
     return out
 
 

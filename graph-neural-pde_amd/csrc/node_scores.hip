@@ -698,6 +698,20 @@ __global__ __launch_bounds__(256) void node_scores_fused_kernel(const float* __r
   ns_block_resident<VEC, GL, MAXH, CLAMP, true>(U, xb, rcs, n0, n1, C, ldx, H, Cp, g, gl, wv, xa, xn);
 }
 
+// S[b][d] = sum of the tile shares part[b][tile][d] in tile order (one thread per
+// (b, d)): the key sum of gnpde_ref_keysum_f32, handed to the caller (a sharded
+// solve all-reduces it over the column stripes before the node scores).
+__global__ __launch_bounds__(256) void keysum_reduce_kernel(const double* __restrict__ part, int ntiles, int att,
+                                                             int64_t B, double* __restrict__ S) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * att) return;
+  const int64_t b = i / att, d = i - b * att;
+  const double* __restrict__ pb = part + b * (int64_t)ntiles * att + d;
+  double acc = 0.0;
+  for (int t = 0; t < ntiles; ++t) acc += pb[(int64_t)t * att];
+  S[i] = acc;
+}
+
 // ------------------------------------------------------------------ host helpers
 static int pow2_at_least(int v, int cap) {
   int p = 1;
@@ -980,28 +994,14 @@ size_t gnpde_keysum_workspace_bytes(int64_t B, int64_t N, int64_t C, int64_t att
   return sizeof(double) * (size_t)(B * ntiles * att + B * (16 * C + 2048 + 16));
 }
 
-int gnpde_ref_scores_f32(const float* x, int64_t B, int64_t N, int64_t C, int64_t ldx, const int32_t* indeg,
-                         const float* Wq, const float* bq, const float* Wk, const float* bk, int64_t att,
-                         int64_t heads, double* cs, void* workspace, size_t workspace_bytes, void* stream) {
-  GNPDE_REQUIRE(x && indeg && Wq && bq && Wk && bk && cs && workspace, GNPDE_EINVAL, "ref_scores: NULL pointer");
-  GNPDE_REQUIRE(B >= 1 && N >= 1 && C >= 1 && ldx >= C, GNPDE_EINVAL, "ref_scores: bad sizes");
-  GNPDE_REQUIRE(heads >= 1 && heads <= 16 && att % heads == 0, GNPDE_EUNSUPPORTED,
-                "ref_scores: heads must divide attention_dim and be <= 16");
-  GNPDE_REQUIRE(workspace_bytes >= gnpde_keysum_workspace_bytes(B, N, C, att), GNPDE_EINVAL,
-                "ref_scores: workspace too small");
-  GNPDE_REQUIRE(att <= 4096, GNPDE_EUNSUPPORTED, "ref_scores: attention_dim too large");
-  GNPDE_REQUIRE(B <= 65535, GNPDE_EUNSUPPORTED, "ref_scores: batch too large");
-  GNPDE_REQUIRE((uint64_t)N * heads * 8 < kBufRecords, GNPDE_EUNSUPPORTED, "ref_scores: N*heads too large");
-  hipStream_t s = as_stream(stream);
+// The key-sum launch of the reference scores: part[b][tile][att] tile shares of
+// S = Wk xbar + E bk (keysum_partial_kernel).  Returns the tile count.
+static int ref_keysum_launch(const float* x, int64_t B, int64_t N, int64_t C, int64_t ldx, const int32_t* indeg,
+                             const float* Wk, const float* bk, int64_t att, double* part, hipStream_t s, int* ntiles_out) {
   int vec, tpr, rpt, ntiles;
   keysum_geometry(C, x, ldx, &vec, &tpr);
   const int rpb = kKeysumBlock / tpr;
   keysum_tiles(B, N, rpb, &rpt, &ntiles);
-  const NsGeom ge = ns_geometry(vec, C, heads);
-  const int64_t cp = (int64_t)ge.nch * ge.CW;
-  GNPDE_REQUIRE(ns_uv_doubles(ge) <= 16 * C + 2048 + 16, GNPDE_EUNSUPPORTED, "ref_scores: node-score geometry");
-  double* part = static_cast<double*>(workspace);
-  double* uv = part + B * ntiles * att;
   const size_t shm = sizeof(double) * (size_t)(rpb + 1) * (C + 1);
   GNPDE_REQUIRE(shm <= 64 * 1024, GNPDE_EUNSUPPORTED, "ref_scores: C too large");
   const dim3 g1((unsigned)ntiles, (unsigned)B);
@@ -1015,6 +1015,20 @@ int gnpde_ref_scores_f32(const float* x, int64_t B, int64_t N, int64_t C, int64_
     GNPDE_KS(1);
 #undef GNPDE_KS
   GNPDE_LAUNCH_CHECK();
+  *ntiles_out = ntiles;
+  return GNPDE_OK;
+}
+
+// The node-score launches from the tile shares `part` (ntiles of them per batch
+// element; ntiles = 1: S itself): U = Wq^T S / sqrt(dk), v, cs = x U + v.
+static int ref_node_scores_launch(const float* x, int64_t B, int64_t N, int64_t C, int64_t ldx, const float* Wq,
+                                  const float* bq, int64_t att, int64_t heads, const double* part, int ntiles,
+                                  double* cs, double* uv, hipStream_t s) {
+  int vec, tpr;
+  keysum_geometry(C, x, ldx, &vec, &tpr);
+  const NsGeom ge = ns_geometry(vec, C, heads);
+  const int64_t cp = (int64_t)ge.nch * ge.CW;
+  GNPDE_REQUIRE(ns_uv_doubles(ge) <= 16 * C + 2048 + 16, GNPDE_EUNSUPPORTED, "ref_scores: node-score geometry");
   if (ge.nch == 1 && att <= 1024 && B <= 65535 && ns_fused_enabled()) {
     // every node-score workgroup forms U itself (node_scores_fused_kernel): two launches
     launch_node_scores_fused(s, ge, x, B, N, (int)C, ldx, (int)heads, part, ntiles, Wq, bq, (int)att, cs);
@@ -1028,6 +1042,59 @@ int gnpde_ref_scores_f32(const float* x, int64_t B, int64_t N, int64_t C, int64_
   launch_node_scores_any(s, ge, x, B, N, (int)C, ldx, (int)heads, uv, cs);
   GNPDE_LAUNCH_CHECK();
   return GNPDE_OK;
+}
+
+static int ref_scores_check(const float* x, int64_t B, int64_t N, int64_t C, int64_t ldx, int64_t att, int64_t heads,
+                            size_t workspace_bytes) {
+  GNPDE_REQUIRE(B >= 1 && N >= 1 && C >= 1 && ldx >= C, GNPDE_EINVAL, "ref_scores: bad sizes");
+  GNPDE_REQUIRE(heads >= 1 && heads <= 16 && att % heads == 0, GNPDE_EUNSUPPORTED,
+                "ref_scores: heads must divide attention_dim and be <= 16");
+  GNPDE_REQUIRE(workspace_bytes >= gnpde_keysum_workspace_bytes(B, N, C, att), GNPDE_EINVAL,
+                "ref_scores: workspace too small");
+  GNPDE_REQUIRE(att <= 4096, GNPDE_EUNSUPPORTED, "ref_scores: attention_dim too large");
+  GNPDE_REQUIRE(B <= 65535, GNPDE_EUNSUPPORTED, "ref_scores: batch too large");
+  GNPDE_REQUIRE((uint64_t)N * heads * 8 < kBufRecords, GNPDE_EUNSUPPORTED, "ref_scores: N*heads too large");
+  return GNPDE_OK;
+}
+
+int gnpde_ref_scores_f32(const float* x, int64_t B, int64_t N, int64_t C, int64_t ldx, const int32_t* indeg,
+                         const float* Wq, const float* bq, const float* Wk, const float* bk, int64_t att,
+                         int64_t heads, double* cs, void* workspace, size_t workspace_bytes, void* stream) {
+  GNPDE_REQUIRE(x && indeg && Wq && bq && Wk && bk && cs && workspace, GNPDE_EINVAL, "ref_scores: NULL pointer");
+  int rc = ref_scores_check(x, B, N, C, ldx, att, heads, workspace_bytes);
+  if (rc) return rc;
+  hipStream_t s = as_stream(stream);
+  double* part = static_cast<double*>(workspace);
+  int ntiles = 0;
+  rc = ref_keysum_launch(x, B, N, C, ldx, indeg, Wk, bk, att, part, s, &ntiles);
+  if (rc) return rc;
+  return ref_node_scores_launch(x, B, N, C, ldx, Wq, bq, att, heads, part, ntiles, cs, part + B * ntiles * att, s);
+}
+
+int gnpde_ref_keysum_f32(const float* x, int64_t B, int64_t N, int64_t C, int64_t ldx, const int32_t* indeg,
+                         const float* Wk, const float* bk, int64_t att, double* S, void* workspace,
+                         size_t workspace_bytes, void* stream) {
+  GNPDE_REQUIRE(x && indeg && Wk && bk && S && workspace, GNPDE_EINVAL, "ref_keysum: NULL pointer");
+  int rc = ref_scores_check(x, B, N, C, ldx, att, 1, workspace_bytes);
+  if (rc) return rc;
+  hipStream_t s = as_stream(stream);
+  double* part = static_cast<double*>(workspace);
+  int ntiles = 0;
+  rc = ref_keysum_launch(x, B, N, C, ldx, indeg, Wk, bk, att, part, s, &ntiles);
+  if (rc) return rc;
+  keysum_reduce_kernel<<<(unsigned)ceil_div(B * att, (int64_t)kBlock), kBlock, 0, s>>>(part, ntiles, (int)att, B, S);
+  GNPDE_LAUNCH_CHECK();
+  return GNPDE_OK;
+}
+
+int gnpde_ref_scores_from_keysum_f32(const float* x, int64_t B, int64_t N, int64_t C, int64_t ldx, const double* S,
+                                     const float* Wq, const float* bq, int64_t att, int64_t heads, double* cs,
+                                     void* workspace, size_t workspace_bytes, void* stream) {
+  GNPDE_REQUIRE(x && S && Wq && bq && cs && workspace, GNPDE_EINVAL, "ref_scores_from_keysum: NULL pointer");
+  int rc = ref_scores_check(x, B, N, C, ldx, att, heads, workspace_bytes);
+  if (rc) return rc;
+  return ref_node_scores_launch(x, B, N, C, ldx, Wq, bq, att, heads, S, 1, cs, static_cast<double*>(workspace),
+                                as_stream(stream));
 }
 
 }  // extern "C"

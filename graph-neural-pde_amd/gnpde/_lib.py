@@ -79,6 +79,9 @@ SIGNATURES = {
     "gnpde_keysum_workspace_bytes": (_size, [_i64, _i64, _i64, _i64]),
     "gnpde_ref_scores_f32": (_int, [_vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _vp, _vp,
                                     _size, _vp]),
+    "gnpde_ref_keysum_f32": (_int, [_vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _i64, _vp, _vp, _size, _vp]),
+    "gnpde_ref_scores_from_keysum_f32": (_int, [_vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _i64, _i64, _vp, _vp,
+                                                _size, _vp]),
     "gnpde_softmax_stats_f32": (_int, [_vp, _i64, _vp, _i64, _vp, _int, _int, _i64, _i64, _vp, _vp, _vp, _i64, _f32,
                                        _f32, _vp, _vp, _vp, _vp, _vp]),
     "gnpde_attn_weights_f32": (_int, [_vp, _vp, _i64, _int, _int, _i64, _i64, _vp, _vp, _vp, _i64, _f32, _f32, _vp,

@@ -162,6 +162,7 @@ class RowShardedLaplacian(object):
     returns f_local [nbmax, C]; it drops into gnpde.odeint unchanged."""
 
     graph_capturable = False  # an RCCL all-gather per RHS: the integrator runs it eagerly
+    fused_adaptive = False    # the adaptive solvers' wide stages run in column stripes or unsharded
 
     def __init__(self, edge_index, edge_weight, num_nodes, alpha, beta=None, x0_local=None, add_source=False,
                  alpha_sigmoid=True, group=None, local_rhs=None, chunk=ops.DEFAULT_CHUNK, row_weight=0.0,
@@ -331,15 +332,312 @@ class ColumnShardedLaplacian(object):
         dist.all_reduce(v, group=self.group)
         return (v[0] / v[1]).sqrt().to(t.dtype)
 
+    def reduce_error_sq(self, pair):
+        """dopri5's squared error sum and element count over all stripes (in place;
+        the fused adaptive step, gnpde.integrator._RKAdaptiveFused)."""
+        dist.all_reduce(pair, group=self.group)
+
     def gather(self, x_local):
         """All stripes -> full [B,N,C] (once, at the end of an integration)."""
-        widths = [c1 - c0 for c0, c1 in self.cols]
-        wmax = max(widths)
-        shp = tuple(x_local.shape[:-1])
-        pad = torch.zeros(shp + (wmax,), dtype=x_local.dtype, device=x_local.device)
-        pad[..., :x_local.shape[-1]] = x_local
-        pad = pad.reshape((-1, wmax))
-        out = torch.empty((self.world * pad.shape[0], wmax), dtype=x_local.dtype, device=x_local.device)
-        dist.all_gather_into_tensor(out, pad, group=self.group)
-        out = out.view((self.world,) + shp + (wmax,))
-        return torch.cat([out[p][..., :widths[p]] for p in range(self.world)], dim=-1)
+        return _gather_cols(x_local, self.cols, self.world, self.group)
+
+
+# --------------------------------------------------------------------------- transformer attention RHS
+class _Comm(object):
+    """The collectives of the sharded transformer RHS: torch.distributed on the
+    job's group (RCCL over xGMI for device tensors).  Tests substitute an object
+    with the same two methods (e.g. staging device tensors through gloo)."""
+
+    def __init__(self, group=None):
+        self.group = group
+
+    def all_reduce(self, t):
+        dist.all_reduce(t, group=self.group)
+
+    def all_gather_into_tensor(self, out, t):
+        dist.all_gather_into_tensor(out, t, group=self.group)
+
+
+class _HipAttentionLocal(object):
+    """A rank's arithmetic of the sharded transformer RHS on the HIP path (tests
+    inject a CPU object with the same methods to run the collectives under gloo)."""
+
+    def __init__(self, g):
+        self.g = g
+        self._uni = None
+
+    def keysum(self, x, Wk, bk):
+        return ops.ref_keysum(self.g, x, Wk, bk)
+
+    def node_scores(self, x, S, Wq, bq, heads):
+        return ops.ref_scores_from_keysum(self.g, x, S, Wq, bq, heads)
+
+    def project(self, x, W, b):
+        return ops.linear(x, W, b)[0]
+
+    def uniform_weights(self, heads):
+        if self._uni is None:
+            ns = ops.uniform_scores(heads)
+            m, rl = ops.softmax_stats(self.g, ns, 0)
+            self._uni = ops.attn_weights(self.g, ns, m, rl, 0)
+        return self._uni
+
+    def aggregate(self, ns, norm_idx, x, stage=None, **kw):
+        if ns is None:  # uniform weights (fork scaled_dot, norm_idx 0): graph-only
+            return ops.spmm_rhs(self.g, self.uniform_weights(kw.pop('heads')), x, stage=stage, **kw)
+        kw.pop('heads', None)
+        return ops.attn_rhs(self.g, ns, None, None, norm_idx, x, stage=stage, **kw)
+
+
+def _qk_scores(qk, heads, att):
+    """NodeScores of the per-edge scaled_dot over a [R, 2 att] q | k buffer (rows of
+    ld 2 att: q and k are column views of it)."""
+    ns = ops.NodeScores(ops._lib.SCORE_DOT, heads, att // heads, q=qk[:, :att], k=qk[:, att:])
+    ns.ldqk = qk.shape[1]
+    return ns
+
+
+class ColumnShardedTransformer(object):
+    """Column-striped transformer attention RHS (ODEFuncTransformerAtt,
+    src/function_transformer_attention.py:44-59, 218-267):
+    rank p holds columns [c0, c1) of every node and the replicated CSR / CSC.
+    The scores read all C columns, but both score forms are LINEAR in the
+    columns, so each rank forms its stripe's share and one all-reduce completes
+    it; the aggregation is then column-local:
+
+    * fork scaled_dot (score_mode 'reference'): the key sum S [B, att] (fp64, the
+      stripe's columns of Wk) all-reduced, then the node scores cs [R, heads]
+      (fp64, the stripe's columns of Wq) all-reduced — 2 R heads 8 bytes per RHS;
+      under source-grouped softmax (norm_idx 0) the weights are 1/outdeg: no
+      communication at all;
+    * per-edge scaled_dot: the projection q | k [R, 2 att] (fp32, the stripe's
+      columns of [Wq; Wk]) all-reduced — R 2 att 4 bytes per RHS.
+
+    The biases enter on rank 0 only.  Every rank then runs the same softmax
+    statistics (replicated, they are graph- and score-sized) and aggregates its
+    own columns with the fused kernels.  Drops into gnpde.odeint: __call__ /
+    rhs_stage (fixed-grid fused stages, the adaptive solvers' wide stages),
+    global_rms_norm / reduce_error_sq (dopri5's error norm over all stripes)."""
+
+    graph_capturable = False  # collectives per RHS
+
+    def __init__(self, edge_index, num_nodes, C, Wq, bq, Wk, bk, heads, norm_idx, alpha, score_mode='reference',
+                 beta=None, x0_local=None, add_source=False, alpha_sigmoid=True, group=None, local=None,
+                 chunk=ops.DEFAULT_CHUNK, comm=None):
+        self.group = group
+        self.comm = comm if comm is not None else _Comm(group)
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self.C = int(C)
+        self.cols = col_blocks(self.C, self.world)
+        self.c0, self.c1 = self.cols[self.rank]
+        self.N = int(num_nodes)
+        self.heads, self.norm_idx = int(heads), int(norm_idx)
+        self.score_mode = score_mode
+        self.att = int(Wq.shape[0])
+        self.alpha, self.beta = alpha, beta
+        self.x0_local = x0_local
+        self.add_source, self.alpha_sigmoid = add_source, alpha_sigmoid
+        self.nfe = 0
+        first = self.rank == 0
+        sl = slice(self.c0, self.c1)
+        self.Wq, self.Wk = Wq[:, sl].contiguous(), Wk[:, sl].contiguous()
+        self.bq = bq.clone() if first else torch.zeros_like(bq)
+        self.bk = bk.clone() if first else torch.zeros_like(bk)
+        self.Wcat = torch.cat([self.Wq, self.Wk], 0).contiguous()
+        self.bcat = torch.cat([self.bq, self.bk], 0).contiguous()
+        self.uniform = score_mode == 'reference' and self.norm_idx == 0
+        self.local = local if local is not None else _HipAttentionLocal(ops.GraphCSR(edge_index, self.N, chunk=chunk))
+        self.bytes_per_rhs = 0  # collective payload of the last RHS (bench.py)
+
+    def split(self, x):
+        """[B,N,C] -> this rank's contiguous column stripe."""
+        return x[..., self.c0:self.c1].contiguous()
+
+    def _kw(self):
+        return dict(x0=self.x0_local, alpha=self.alpha, beta=self.beta, rhs=True, alpha_sigmoid=self.alpha_sigmoid,
+                    add_source=self.add_source, heads=self.heads)
+
+    def scores(self, x_local):
+        """The full node-level operands of the scores (None for uniform weights)."""
+        if self.uniform:
+            self.bytes_per_rhs = 0
+            return None
+        if self.score_mode == 'reference':
+            S = self.local.keysum(x_local, self.Wk, self.bk)
+            self.comm.all_reduce(S)
+            cs = self.local.node_scores(x_local, S, self.Wq, self.bq, self.heads)
+            self.comm.all_reduce(cs)
+            self.bytes_per_rhs = S.numel() * 8 + cs.numel() * 8
+            return ops.NodeScores(ops._lib.SCORE_REFERENCE, self.heads, self.att // self.heads, cs=cs)
+        qk = self.local.project(x_local, self.Wcat, self.bcat)
+        self.comm.all_reduce(qk)
+        self.bytes_per_rhs = qk.numel() * 4
+        return _qk_scores(qk, self.heads, self.att)
+
+    def __call__(self, t, x_local):
+        self.nfe += 1
+        return self.local.aggregate(self.scores(x_local), self.norm_idx, x_local, **self._kw())
+
+    def rhs_stage(self, t, x_local, stage):
+        self.nfe += 1
+        self.local.aggregate(self.scores(x_local), self.norm_idx, x_local, stage=stage, **self._kw())
+
+    def global_rms_norm(self, t):
+        v = torch.stack([t.double().pow(2).sum(), torch.tensor(float(t.numel()), dtype=torch.float64,
+                                                                device=t.device)])
+        self.comm.all_reduce(v)
+        return (v[0] / v[1]).sqrt().to(t.dtype)
+
+    def reduce_error_sq(self, pair):
+        """dopri5's squared error sum and element count over all stripes (in place)."""
+        self.comm.all_reduce(pair)
+
+    def gather(self, x_local):
+        """All stripes -> full [B,N,C] (once, at the end of an integration)."""
+        return _gather_cols(x_local, self.cols, self.world, self.group)
+
+
+def _gather_cols(x_local, cols, world, group):
+    widths = [c1 - c0 for c0, c1 in cols]
+    wmax = max(widths)
+    shp = tuple(x_local.shape[:-1])
+    pad = torch.zeros(shp + (wmax,), dtype=x_local.dtype, device=x_local.device)
+    pad[..., :x_local.shape[-1]] = x_local
+    pad = pad.reshape((-1, wmax))
+    out = torch.empty((world * pad.shape[0], wmax), dtype=x_local.dtype, device=x_local.device)
+    dist.all_gather_into_tensor(out, pad, group=group)
+    out = out.view((world,) + shp + (wmax,))
+    return torch.cat([out[p][..., :widths[p]] for p in range(world)], dim=-1)
+
+
+class _RowView(object):
+    """The B = 1 row range [r0, r1) of a GraphCSR as the node-score kernels see a
+    graph (B, N, R, indeg): the key sum and node scores of one rank's rows."""
+
+    def __init__(self, g, r0, r1):
+        self.B, self.N, self.R = 1, r1 - r0, r1 - r0
+        self.indeg = g.indeg[r0:r1]
+        self._owner = g
+
+
+class RowShardedTransformer(object):
+    """Row-partitioned transformer attention RHS (the north star's literal 1-D
+    partition): contiguous row blocks balanced by nnz
+    (balanced_row_blocks), rank p owns rows [r0, r1) — its rows' state, scores
+    and RHS.  Per RHS:
+
+    * the state is all-gathered (RCCL all_gather_into_tensor of the padded blocks,
+      unpadded into global row order): the aggregation gathers any row;
+    * fork scaled_dot: each rank's share of the key sum S over its own rows (fp64)
+      is all-reduced, its rows' node scores cs are all-gathered; per-edge
+      scaled_dot: each rank projects its own rows and q | k [n, 2 att] is
+      all-gathered (4x less than the state at att = C/4);
+    * the destination-grouped softmax statistics (norm_idx 1) are formed by every
+      rank over the whole CSC (score-sized, replicated);
+    * the rank's rows are aggregated by the fused kernels over a local plan
+      (ops.spmm_rhs_rows), written through pointers shifted to its block.
+
+    B = 1 (one graph; batches shard as replicas, shard_batch)."""
+
+    graph_capturable = False  # collectives per RHS
+    fused_adaptive = False    # the adaptive solvers' wide stages run in column stripes or unsharded
+
+    def __init__(self, edge_index, num_nodes, C, Wq, bq, Wk, bk, heads, norm_idx, alpha, score_mode='reference',
+                 beta=None, x0_local=None, add_source=False, alpha_sigmoid=True, group=None,
+                 chunk=ops.DEFAULT_CHUNK, row_weight=0.0, comm=None):
+        if edge_index.shape[0] != 1:
+            raise NotImplementedError("RowShardedTransformer: one graph (B = 1); shard batches with shard_batch")
+        self.group = group
+        self.comm = comm if comm is not None else _Comm(group)
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self.N = self.R = int(num_nodes)
+        self.C = int(C)
+        self.heads, self.norm_idx, self.score_mode = int(heads), int(norm_idx), score_mode
+        self.att = int(Wq.shape[0])
+        self.Wq, self.bq, self.Wk, self.bk = Wq.contiguous(), bq.contiguous(), Wk.contiguous(), bk.contiguous()
+        self.Wcat = torch.cat([self.Wq, self.Wk], 0).contiguous()
+        self.bcat = torch.cat([self.bq, self.bk], 0).contiguous()
+        self.alpha, self.beta = alpha, beta
+        self.x0_local = x0_local
+        self.add_source, self.alpha_sigmoid = add_source, alpha_sigmoid
+        self.nfe = 0
+        self.g = ops.GraphCSR(edge_index, self.N, chunk=chunk)
+        self.blocks = balanced_row_blocks(self.g.csr.rowptr.cpu().numpy(), self.world, row_weight)
+        self.nb = max(max(r1 - r0 for r0, r1 in self.blocks), 1)
+        self.r0, self.r1 = self.blocks[self.rank]
+        self.plan = _local_plan(self.g.csr, self.r0, self.r1, chunk)  # item rows = global row ids
+        self.view = _RowView(self.g, self.r0, self.r1)
+        self.uniform = score_mode == 'reference' and self.norm_idx == 0
+        self._uni = None
+        self.bytes_per_rhs = 0
+
+    def scatter(self, y):
+        """Full state [1, N, C] or [N, C] -> this rank's zero-padded block [nb, C]."""
+        y = y.reshape(-1, y.shape[-1])
+        out = torch.zeros((self.nb, y.shape[-1]), dtype=y.dtype, device=y.device)
+        out[:self.r1 - self.r0] = y[self.r0:self.r1]
+        return out
+
+    def _gather_rows(self, v_local):
+        """Padded blocks [nb, K] of every rank -> [R, K] in global row order."""
+        v_local = v_local.contiguous()
+        pad = torch.empty((self.world * self.nb,) + tuple(v_local.shape[1:]), dtype=v_local.dtype,
+                          device=v_local.device)
+        self.comm.all_gather_into_tensor(pad, v_local)
+        return torch.cat([pad[p * self.nb:p * self.nb + (b - a)] for p, (a, b) in enumerate(self.blocks)], 0)
+
+    def gather(self, y_local):
+        """All blocks -> the full state [N, C] (global row order)."""
+        return self._gather_rows(y_local)
+
+    def _blockify(self, v_own):
+        out = torch.zeros((self.nb,) + tuple(v_own.shape[1:]), dtype=v_own.dtype, device=v_own.device)
+        out[:v_own.shape[0]] = v_own
+        return out
+
+    def _rhs(self, y_local, stage):
+        self.nfe += 1
+        x_full = self._gather_rows(y_local)                     # [N, C]
+        nbytes = x_full.numel() * 4
+        own = x_full[self.r0:self.r1]
+        kw = dict(x0=self.x0_local, alpha=self.alpha, beta=self.beta, alpha_sigmoid=self.alpha_sigmoid,
+                  add_source=self.add_source, stage=stage)
+        if self.plan is None:
+            self.bytes_per_rhs = nbytes
+            return None if stage is not None else torch.zeros_like(y_local)
+        if self.uniform:
+            if self._uni is None:
+                ns = ops.uniform_scores(self.heads)
+                m, rl = ops.softmax_stats(self.g, ns, 0)
+                self._uni = ops.attn_weights(self.g, ns, m, rl, 0)
+            self.bytes_per_rhs = nbytes
+            return ops.spmm_rhs_rows(self.g, self.plan, self._uni, x_full, y_local, self.r0, **kw)
+        if self.score_mode == 'reference':
+            S = ops.ref_keysum(self.view, own, self.Wk, self.bk)
+            self.comm.all_reduce(S)
+            cs = self._gather_rows(self._blockify(ops.ref_scores_from_keysum(self.view, own, S, self.Wq, self.bq,
+                                                                             self.heads)))
+            self.bytes_per_rhs = nbytes + S.numel() * 8 + cs.numel() * 8
+            ns = ops.NodeScores(ops._lib.SCORE_REFERENCE, self.heads, self.att // self.heads, cs=cs)
+            if self.norm_idx != 1:
+                raise NotImplementedError("reference scores under source-grouped softmax are uniform")
+            if self.heads == 2:
+                _, _, mr = ops.softmax_stats(self.g, ns, 1, packed=True)
+                w = ops.RefDstWeights(cs, None, None, 2, mr=mr)
+            else:
+                m, rl = ops.softmax_stats(self.g, ns, 1)
+                w = ops.RefDstWeights(cs, m, rl, self.heads)
+            return ops.spmm_rhs_rows(self.g, self.plan, w, x_full, y_local, self.r0, **kw)
+        qk = self._gather_rows(self._blockify(ops.linear(own, self.Wcat, self.bcat)[0]))  # [N, 2 att]
+        self.bytes_per_rhs = nbytes + qk.numel() * 4
+        ns = _qk_scores(qk, self.heads, self.att)
+        mr = ops.softmax_stats(self.g, ns, 1, packed=True)[2] if self.norm_idx == 1 else None
+        return ops.spmm_rhs_rows(self.g, self.plan, None, x_full, y_local, self.r0, ns=ns, mr=mr, **kw)
+
+    def __call__(self, t, y_local):
+        return self._rhs(y_local, None)
+
+    def rhs_stage(self, t, y_local, stage):
+        self._rhs(y_local, stage)

@@ -1081,7 +1081,7 @@ def _fused_adaptive_ok(func, y0, combine, options):
     sharded RHS's global one, reduced through func.reduce_error_sq)."""
     if not (isinstance(combine, _Combine) and hasattr(func, 'rhs_stage')) or torch.is_grad_enabled():
         return False
-    if os.environ.get('GNPDE_FUSED_ADAPTIVE', '1') == '0':
+    if not getattr(func, 'fused_adaptive', True) or os.environ.get('GNPDE_FUSED_ADAPTIVE', '1') == '0':
         return False
     norm = options.get('norm')
     if norm is not None and not (getattr(norm, '__self__', None) is func and hasattr(func, 'reduce_error_sq')):

@@ -722,14 +722,21 @@ class RefDstWeights(object):
 
 
 def spmm_rhs_rows(g, plan, w_csr, x_src, x_rows, row0, x0=None, alpha=None, beta=None, alpha_sigmoid=True,
-                  add_source=False, stage=None, out=None, col=None):
+                  add_source=False, stage=None, out=None, col=None, ns=None, mr=None):
     """K1 over a row block: ``plan`` covers rows [row0, row0 + n) by their
     positions in ``x_src`` (the gathered state); gathers read ``x_src`` through
     ``col`` (default: the CSR's global ids; dist.RowPartition passes ids
     relabelled into its padded layout); the block's own state ``x_rows`` [n, C],
     ``x0`` and the outputs are local buffers addressed through pointers shifted
     back by row0 rows (never dereferenced outside the block).  The epilogue's
-    x_r comes from x_src[row], which holds the same values."""
+    x_r comes from x_src[row], which holds the same values.
+
+    Weights: ``w_csr`` in CSR order (plain), a RefDstWeights (the fork's scaled_dot
+    under destination-grouped softmax, formed in the gather loop:
+    gnpde_attn_ref_rhs_f32), or ``ns`` = per-edge scaled_dot NodeScores over the
+    whole state (q, k rows at the positions of x_src; ``mr``: destination
+    statistics records for norm_idx 1, None for source-grouped softmax: the fused
+    gnpde_attn_dot_rhs_f32)."""
     xs = _rows(x_src, "x_src")
     xl = _rows(x_rows, "x_rows")
     C = xs.shape[1]
@@ -743,15 +750,33 @@ def spmm_rhs_rows(g, plan, w_csr, x_src, x_rows, row0, x0=None, alpha=None, beta
     if stage is not None:
         for t in stage.tensors():
             _require_gpu(t, "stage tensor", torch.float32)
+        if stage.wide:
+            raise ValueError("spmm_rhs_rows: the adaptive solvers' wide stages run unsharded or in column stripes")
         st = ctypes.byref(stage.struct(xs, shift))
     elif out is None:
         out = torch.empty_like(xl)
-    partials = _partials(plan, C, dev)
+    cp = _ptr(g.csr.col if col is None else col)
+    epi = (C, _ptr(xs), C, sp(x0r), C, _ptr(a), _ptr(b), _flags(True, alpha_sigmoid, add_source),
+           sp(out) if out is not None else ctypes.c_void_p(0), C)
     plan.order_launch(dev)
-    _lib.call("gnpde_spmm_rhs_f32", _ptr(plan.items), plan.n_items, _ptr(plan.heavy), plan.n_heavy,
-              _ptr(g.csr.col if col is None else col),
-              _ptr(w_csr), C, _ptr(xs), C, sp(x0r), C, _ptr(a), _ptr(b), _flags(True, alpha_sigmoid, add_source),
-              sp(out) if out is not None else ctypes.c_void_p(0), C, _ptr(partials), plan.n_slots, st, _stream(dev))
+    if ns is not None:
+        H, dk = ns.heads, ns.dk
+        if not _lib.fn("gnpde_attn_dot_supported")(H, dk, C):
+            raise ValueError("spmm_rhs_rows: per-edge scores of heads=%d dk=%d C=%d outside the fused kernel" %
+                             (H, dk, C))
+        nws = int(_lib.fn("gnpde_attn_dot_workspace_floats")(H, C, plan.n_slots))
+        ws = torch.empty(max(nws, 4), dtype=torch.float32, device=dev)
+        _lib.call("gnpde_attn_dot_rhs_f32", _ptr(plan.items), plan.n_items, _ptr(plan.heavy), plan.n_heavy, cp,
+                  _ptr(ns.q), _ptr(ns.k), ns.ldqk, H, dk, _ptr(mr), *epi, _ptr(ws), plan.n_slots, st, _stream(dev))
+    elif isinstance(w_csr, RefDstWeights):
+        partials = _partials(plan, C, dev)
+        _lib.call("gnpde_attn_ref_rhs_f32", _ptr(plan.items), plan.n_items, _ptr(plan.heavy), plan.n_heavy, cp,
+                  _ptr(w_csr.cs), _ptr(w_csr.m), _ptr(w_csr.rl), _ptr(w_csr.mr), w_csr.heads, *epi, _ptr(partials),
+                  plan.n_slots, st, _stream(dev))
+    else:
+        partials = _partials(plan, C, dev)
+        _lib.call("gnpde_spmm_rhs_f32", _ptr(plan.items), plan.n_items, _ptr(plan.heavy), plan.n_heavy, cp,
+                  _ptr(w_csr), *epi, _ptr(partials), plan.n_slots, st, _stream(dev))
     return None if stage is not None else out.view(x_rows.shape)
 
 
@@ -856,6 +881,43 @@ def node_scores(g, x, Wq, bq, Wk, bk, heads, attention_type='scaled_dot', score_
         b = torch.cat([bq, bk], 0) if bq is not None else None
     q, k = linear(xr, W, b, split=att)
     return NodeScores(mode, heads, dk, q=q, k=k, p0=output_var, p1=lengthscale)
+
+
+def ref_keysum(g, x, Wk, bk):
+    """The fork's global key sum S [B, att] fp64 of a (column stripe of the) state:
+    S_b = Wk xbar_b + (sum indeg) bk with xbar_b = sum_n indeg(n) x_n
+    (gnpde_ref_keysum_f32; function_transformer_attention.py:249's
+    sum over e' of k_dst(e')).  Linear in x's columns: the shares of the stripes of
+    a state sum to the key sum of the whole (bk on one stripe only)."""
+    xr = _rows(x, "x")
+    C = xr.shape[1]
+    att = Wk.shape[0]
+    for name, t in (("Wk", Wk), ("bk", bk)):
+        _require_gpu(t, name, torch.float32)
+    S = torch.empty(g.B, att, dtype=torch.float64, device=xr.device)
+    nb = _lib.fn("gnpde_keysum_workspace_bytes")(g.B, g.N, C, att)
+    ws = _keysum_workspace(g, xr.device, nb)
+    _lib.call("gnpde_ref_keysum_f32", _ptr(xr), g.B, g.N, C, C, _ptr(g.indeg), _ptr(Wk.contiguous()),
+              _ptr(bk.contiguous()), att, _ptr(S), _ptr(ws), nb, _stream(xr.device))
+    return S
+
+
+def ref_scores_from_keysum(g, x, S, Wq, bq, heads):
+    """Node scores cs [R, heads] fp64 = q . S / sqrt(dk) of a (column stripe of the)
+    state from a given key sum S (gnpde_ref_scores_from_keysum_f32): the stripe's
+    share of cs (bq on one stripe only)."""
+    xr = _rows(x, "x")
+    C = xr.shape[1]
+    att = Wq.shape[0]
+    _require_gpu(S, "S", torch.float64)
+    for name, t in (("Wq", Wq), ("bq", bq)):
+        _require_gpu(t, name, torch.float32)
+    cs = torch.empty(g.R, heads, dtype=torch.float64, device=xr.device)
+    nb = _lib.fn("gnpde_keysum_workspace_bytes")(g.B, g.N, C, att)
+    ws = _keysum_workspace(g, xr.device, nb)
+    _lib.call("gnpde_ref_scores_from_keysum_f32", _ptr(xr), g.B, g.N, C, C, _ptr(S.contiguous()),
+              _ptr(Wq.contiguous()), _ptr(bq.contiguous()), att, heads, _ptr(cs), _ptr(ws), nb, _stream(xr.device))
+    return cs
 
 
 def uniform_scores(heads):

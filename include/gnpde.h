@@ -367,6 +367,23 @@ int gnpde_ref_scores_f32(const float* x, int64_t B, int64_t N, int64_t C, int64_
                          int64_t att, int64_t heads, double* cs, void* workspace, size_t workspace_bytes,
                          void* stream);
 
+/* The same in two phases, for a state split into column stripes (gnpde.dist):
+ * S and cs are linear in the columns, so each stripe forms its share and the
+ * caller sums the shares over the stripes between the phases (one all-reduce of
+ * S [B, att] fp64, one of cs [R, heads] fp64):
+ *   gnpde_ref_keysum_f32:             S[b] = Wk xbar_b + (sum_n indeg(n)) bk   (fp64 [B][att];
+ *                                     the stripe's columns of Wk, bk on one stripe only)
+ *   gnpde_ref_scores_from_keysum_f32: cs[r,h] = q_r,h . S_b,h / sqrt(dk) from a given S
+ *                                     (the stripe's columns of Wq, bq on one stripe only).
+ * x, Wk, Wq: the stripe's columns (C of them, contiguous [att, C] weights);
+ * workspace as gnpde_ref_scores_f32.                                          */
+int gnpde_ref_keysum_f32(const float* x, int64_t B, int64_t N, int64_t C, int64_t ldx, const int32_t* indeg,
+                         const float* Wk, const float* bk, int64_t att, double* S, void* workspace,
+                         size_t workspace_bytes, void* stream);
+int gnpde_ref_scores_from_keysum_f32(const float* x, int64_t B, int64_t N, int64_t C, int64_t ldx, const double* S,
+                                     const float* Wq, const float* bq, int64_t att, int64_t heads, double* cs,
+                                     void* workspace, size_t workspace_bytes, void* stream);
+
 /* Destination- or source-grouped softmax statistics over a grouped CSR
  * (items from gnpde_plan_build over the CSC for norm_idx=1, the CSR for
  * norm_idx=0; gidx = the OTHER endpoint of each edge):

@@ -139,3 +139,99 @@ def rows_stage_worker(rank, world, port, method, q):
         q.put((rank, float(np.abs(full - want).max()), sh.nfe, len(calls)))
     finally:
         dist.destroy_process_group()
+
+
+class CpuAttentionLocal(object):
+    """The per-rank arithmetic of gnpde.dist.ColumnShardedTransformer restated on
+    the host in float64 (test infrastructure), over the FULL graph and a column
+    stripe of the state: key-sum share, node-score share, projection share, and
+    the softmax + aggregation of the stripe (src/function_transformer_attention.py:
+    218-267, src/utils.py:116-127) — so the gloo test checks the partitioning and
+    the collectives."""
+
+    def __init__(self, ei, N):
+        self.ei = np.asarray(ei)
+        self.N = N
+        self.indeg = np.bincount(self.ei[0, 1], minlength=N).astype(np.float64)
+
+    def keysum(self, x, Wk, bk):
+        xb = (self.indeg[:, None] * x[0].numpy()).sum(0)
+        S = Wk.numpy() @ xb + self.indeg.sum() * bk.numpy()
+        return torch.from_numpy(S[None].copy())
+
+    def node_scores(self, x, S, Wq, bq, heads):
+        q = x[0].numpy() @ Wq.numpy().T + bq.numpy()
+        att = q.shape[1]
+        dk = att // heads
+        Sv = S[0].numpy()
+        cs = np.stack([(q[:, h * dk:(h + 1) * dk] * Sv[h * dk:(h + 1) * dk]).sum(1) / np.sqrt(dk)
+                       for h in range(heads)], 1)
+        return torch.from_numpy(cs.copy())
+
+    def project(self, x, W, b):
+        return torch.from_numpy(x[0].numpy() @ W.numpy().T + b.numpy())
+
+    def aggregate(self, ns, norm_idx, x, stage=None, **kw):
+        import gnpde_oracle as O
+        heads = kw['heads']
+        src, dst = self.ei[0, 0], self.ei[0, 1]
+        if ns is None:  # uniform
+            s = np.zeros((len(src), heads))
+        elif ns.cs is not None:
+            s = ns.cs.numpy()[src]
+        else:
+            q, k = ns.q.numpy(), ns.k.numpy()
+            dk = ns.dk
+            s = np.stack([(q[src, h * dk:(h + 1) * dk] * k[dst, h * dk:(h + 1) * dk]).sum(1) / np.sqrt(dk)
+                          for h in range(heads)], 1)
+        att = O.edge_softmax(s[None], self.ei[:, norm_idx], self.N)
+        f = O.rhs_epilogue(O.aggregate(self.ei, att.mean(axis=2), x.numpy()), x.numpy(), None, kw['alpha'], 0.0,
+                           False, False)
+        f = torch.from_numpy(f)
+        if stage is not None:
+            from host_stage import apply_stage
+            apply_stage(stage, f, x)
+            return None
+        return f
+
+
+def attn_cols_worker(rank, world, port, score_mode, norm_idx, method, q):
+    """gnpde.dist.ColumnShardedTransformer under gloo with CPU arithmetic: the
+    stripes' key-sum / node-score / projection shares all-reduced, the stripes
+    aggregated, integrated with gnpde.odeint (fused fixed-grid stages), against
+    the oracle RHS on the whole state integrated in one process."""
+    _init(rank, world, port)
+    try:
+        import gnpde_oracle as O
+        from gnpde import dist as gd, integrator as gi
+        N, E, C, h, att = 41, 300, 12, 2, 8
+        rng = np.random.default_rng(17)
+        ei = rng.integers(0, N, size=(1, 2, E))
+        x = rng.standard_normal((1, N, C))
+        Wq, Wk = [rng.standard_normal((att, C)) * 0.3 for _ in range(2)]
+        bq, bk = [rng.standard_normal(att) * 0.3 for _ in range(2)]
+        alpha = 0.35
+        T = lambda a: torch.from_numpy(np.ascontiguousarray(a))  # noqa: E731
+        sh = gd.ColumnShardedTransformer(T(ei), N, C, T(Wq), T(bq), T(Wk), T(bk), h, norm_idx, alpha,
+                                         score_mode=score_mode, local=CpuAttentionLocal(ei, N))
+        # the injected aggregation writes the fused stage outputs on the host (fixed-grid and
+        # adaptive stages; the adaptive step's own passes through host_stage_apply)
+        from host_stage import apply_stage
+        sh.host_stages = True
+        sh.host_stage_apply = lambda stage, f, xx, like: apply_stage(stage, f, xx)
+        xl = sh.split(T(x))
+        opts = dict(step_size=0.125) if method != 'dopri5' else dict(norm=sh.global_rms_norm)
+        with torch.no_grad():
+            f = sh(None, xl)
+            y = gi.odeint(sh, xl, torch.tensor([0.0, 0.5], dtype=torch.float64), method=method, options=opts,
+                          combine=gi._Combine(), rtol=1e-8, atol=1e-10)[1]
+        f_full = sh.gather(f).numpy()
+        y_full = sh.gather(y).numpy()
+        rhs = lambda t, v: O.transformer_rhs(ei, v, None, Wq, bq, Wk, bk, h, norm_idx, alpha, 0.0,  # noqa: E731
+                                             score_mode=score_mode)
+        err_f = float(np.abs(f_full - rhs(0, x)).max())
+        want = O.odeint_fixed(rhs, x, 0.0, 0.5, method, 0.125) if method != 'dopri5' else \
+            O.odeint_adaptive(rhs, x, [0.0, 0.5], method, 1e-8, 1e-10)[0][-1]
+        q.put((rank, err_f, float(np.abs(y_full - want).max()), sh.nfe, sh.bytes_per_rhs))
+    finally:
+        dist.destroy_process_group()

@@ -95,3 +95,24 @@ def test_row_sharded_fused_stage_path(method):
     for rank, err, nfe, calls in res:
         assert err < 1e-12
         assert nfe == calls == n
+
+
+@pytest.mark.parametrize("score_mode,norm_idx", [("reference", 1), ("reference", 0), ("per_edge", 0),
+                                                 ("per_edge", 1)])
+@pytest.mark.parametrize("method", ["rk4", "dopri5"])
+def test_column_sharded_transformer_matches_single_process(score_mode, norm_idx, method):
+    """the transformer RHS in column stripes — the
+    key-sum and node-score shares (fork scaled_dot) or the q | k projection shares
+    (per-edge) all-reduced, the stripes aggregated — equals the oracle RHS of the
+    whole state; integrated (rk4 through the fused stages, dopri5 through the
+    global error norm) it matches the single-process integration."""
+    res = _run(W.attn_cols_worker, score_mode, norm_idx, method)
+    for rank, err_f, err_y, nfe, nbytes in res:
+        assert err_f < 1e-12
+        assert err_y < 1e-9
+        if score_mode == "reference" and norm_idx == 0:
+            assert nbytes == 0  # uniform 1/outdeg weights: no collective at all
+        elif score_mode == "reference":
+            assert nbytes == (8 + 41 * 2) * 8  # S [1, att] + cs [N, heads], fp64
+        else:
+            assert nbytes == 41 * 16 * 4  # q | k [N, 2 att], fp32

@@ -1,0 +1,195 @@
+"""GPU: the transformer attention RHS sharded (gnpde.dist, SURVEY.md §8(e),
+VERDICT r3 item 3) on the G-arxiv graph (N = 169,343, E' = 1.2M, C = 128, heads 2,
+attention_dim 32 — configs[3]'s attention shape), every rank's share run in ONE
+process through the HIP path (the multi-GPU runs are the driver's):
+
+* column stripes: the key-sum and node-score shares of the stripes (fork
+  scaled_dot) or their q | k projection shares (per-edge scaled_dot), summed as the
+  all-reduce sums them, equal the unsharded scores (fp64: 1e-12; the fp32
+  projection: 1e-6), and the stripes aggregated with them equal the unsharded
+  RHS within 1e-6;
+* row partition: each rank's key-sum share over its rows, its rows' node scores
+  (or q | k), all-gathered, then its rows aggregated over a local plan: equal to
+  the unsharded RHS within 1e-6 (bit-equal rows where the scores are);
+* the sharded classes themselves in two processes on one GPU, their collectives
+  staged through gloo: the same RHS as one process."""
+import multiprocessing
+import os
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from gnpde import dist as gd
+from gnpde import ops, synthetic
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+N, E, C, H, ATT = 169_343, 1_200_000, 128, 2, 32
+
+
+def rel(a, b):
+    return float((a.double() - b.double()).abs().max() / b.double().abs().max())
+
+
+@pytest.fixture(scope="module")
+def arxiv():
+    ei, _ = synthetic.rw_graph(N, E, seed=0, device=DEV)
+    g = ops.GraphCSR(ei, N)
+    x = synthetic.features(1, N, C, seed=1, device=DEV)
+    gen = torch.Generator(device=DEV)
+    gen.manual_seed(2)
+    Wq, Wk = [torch.randn(ATT, C, generator=gen, device=DEV) * 0.1 for _ in range(2)]
+    bq, bk = [torch.randn(ATT, generator=gen, device=DEV) * 0.1 for _ in range(2)]
+    yield ei, g, x, Wq, bq, Wk, bk
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_column_stripe_shares_reference(arxiv, world):
+    ei, g, x, Wq, bq, Wk, bk = arxiv
+    a = torch.tensor(0.3, device=DEV)
+    ns_full = ops.node_scores(g, x, Wq, bq, Wk, bk, H, 'scaled_dot', 'reference')
+    f_full = ops.attn_rhs(g, ns_full, None, None, 1, x, alpha=a)
+    cols = gd.col_blocks(C, world)
+    S = sum(ops.ref_keysum(g, x[..., c0:c1].contiguous(), Wk[:, c0:c1].contiguous(),
+                           bk if p == 0 else torch.zeros_like(bk)) for p, (c0, c1) in enumerate(cols))
+    cs = sum(ops.ref_scores_from_keysum(g, x[..., c0:c1].contiguous(), S, Wq[:, c0:c1].contiguous(),
+                                        bq if p == 0 else torch.zeros_like(bq), H) for p, (c0, c1) in enumerate(cols))
+    assert rel(cs, ns_full.cs) <= 1e-12
+    ns = ops.NodeScores(ops._lib.SCORE_REFERENCE, H, ATT // H, cs=cs)
+    f = torch.cat([ops.attn_rhs(g, ns, None, None, 1, x[..., c0:c1].contiguous(), alpha=a) for c0, c1 in cols], -1)
+    assert rel(f, f_full) <= 1e-6
+
+
+@pytest.mark.parametrize("world,norm_idx", [(2, 0), (4, 1), (8, 0)])
+def test_column_stripe_shares_per_edge(arxiv, world, norm_idx):
+    ei, g, x, Wq, bq, Wk, bk = arxiv
+    a = torch.tensor(0.3, device=DEV)
+    W, b = torch.cat([Wq, Wk], 0), torch.cat([bq, bk], 0)
+    ns_full = ops.node_scores(g, x, Wq, bq, Wk, bk, H, 'scaled_dot', 'per_edge', wcat=(W, b))
+    f_full = ops.attn_rhs(g, ns_full, None, None, norm_idx, x, alpha=a)
+    cols = gd.col_blocks(C, world)
+    qk = sum(ops.linear(x[..., c0:c1].contiguous(), W[:, c0:c1].contiguous(),
+                        b if p == 0 else torch.zeros_like(b))[0] for p, (c0, c1) in enumerate(cols))
+    ref = torch.cat([ns_full.q, ns_full.k], 1)
+    assert rel(qk, ref) <= 1e-6
+    ns = gd._qk_scores(qk, H, ATT)
+    f = torch.cat([ops.attn_rhs(g, ns, None, None, norm_idx, x[..., c0:c1].contiguous(), alpha=a)
+                   for c0, c1 in cols], -1)
+    assert rel(f, f_full) <= 1e-6
+
+
+@pytest.mark.parametrize("world,mode,norm_idx", [(2, 'reference', 1), (8, 'reference', 1), (4, 'per_edge', 0),
+                                                 (2, 'per_edge', 1), (4, 'reference', 0)])
+def test_row_partition_shares(arxiv, world, mode, norm_idx):
+    """Every rank's rows through ops.spmm_rhs_rows with the scores assembled as the
+    row-partitioned class assembles them (key-sum shares over its rows all-reduced,
+    node scores / q | k of its rows all-gathered)."""
+    ei, g, x, Wq, bq, Wk, bk = arxiv
+    a = torch.tensor(0.3, device=DEV)
+    xr = x.view(N, C)
+    W, b = torch.cat([Wq, Wk], 0), torch.cat([bq, bk], 0)
+    if mode == 'reference' and norm_idx == 0:
+        ns_full = ops.uniform_scores(H)
+        m, rl = ops.softmax_stats(g, ns_full, 0)
+        w_uni = ops.attn_weights(g, ns_full, m, rl, 0)
+        f_full = ops.spmm_rhs(g, w_uni, xr, alpha=a)
+    elif mode == 'reference':
+        ns_full = ops.node_scores(g, x, Wq, bq, Wk, bk, H, 'scaled_dot', 'reference')
+        f_full = ops.attn_rhs(g, ns_full, None, None, 1, x, alpha=a).view(N, C)
+    else:
+        ns_full = ops.node_scores(g, x, Wq, bq, Wk, bk, H, 'scaled_dot', 'per_edge', wcat=(W, b))
+        f_full = ops.attn_rhs(g, ns_full, None, None, norm_idx, x, alpha=a).view(N, C)
+    blocks = gd.balanced_row_blocks(g.csr.rowptr.cpu().numpy(), world)
+    if mode == 'reference' and norm_idx == 1:
+        views = [gd._RowView(g, r0, r1) for r0, r1 in blocks]
+        S = sum(ops.ref_keysum(v, xr[r0:r1], Wk, bk) for v, (r0, r1) in zip(views, blocks))
+        cs = torch.cat([ops.ref_scores_from_keysum(v, xr[r0:r1], S, Wq, bq, H) for v, (r0, r1) in zip(views, blocks)])
+        assert rel(cs, ns_full.cs) <= 1e-12
+        ns = ops.NodeScores(ops._lib.SCORE_REFERENCE, H, ATT // H, cs=cs)
+        _, _, mr = ops.softmax_stats(g, ns, 1, packed=True)
+        wts, nsd, mrd = ops.RefDstWeights(cs, None, None, H, mr=mr), None, None
+    elif mode == 'reference':
+        wts, nsd, mrd = w_uni, None, None
+    else:
+        qk = torch.cat([ops.linear(xr[r0:r1], W, b)[0] for r0, r1 in blocks])
+        nsd = gd._qk_scores(qk, H, ATT)
+        mrd = ops.softmax_stats(g, nsd, 1, packed=True)[2] if norm_idx == 1 else None
+        wts = None
+    for r0, r1 in blocks:
+        plan = gd._local_plan(g.csr, r0, r1, ops.DEFAULT_CHUNK)
+        yl = xr[r0:r1].contiguous()
+        loc = ops.spmm_rhs_rows(g, plan, wts, xr, yl, r0, alpha=a, ns=nsd, mr=mrd)
+        assert rel(loc, f_full[r0:r1]) <= 1e-6, (world, r0)
+
+
+def _two_rank_worker(rank, world, port, cls, mode, norm_idx, q):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.join(os.path.dirname(here), "graph-neural-pde_amd"))
+    import torch.distributed as dist
+    from gnpde import dist as gdd, ops as o, synthetic as syn
+
+    class StagedComm(object):
+        """The class's collectives through gloo on host copies (two ranks share one GPU here)."""
+
+        def all_reduce(self, t):
+            h = t.cpu()
+            dist.all_reduce(h)
+            t.copy_(h)
+
+        def all_gather_into_tensor(self, out, t):
+            h = torch.empty(out.shape, dtype=out.dtype)
+            dist.all_gather_into_tensor(h, t.cpu().contiguous())
+            out.copy_(h)
+
+    os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        n, e, c = 20000, 200000, 64
+        ei, _ = syn.rw_graph(n, e, seed=3, device="cuda")
+        x = syn.features(1, n, c, seed=4, device="cuda")
+        gen = torch.Generator(device="cuda")
+        gen.manual_seed(5)
+        Wq, Wk = [torch.randn(ATT, c, generator=gen, device="cuda") * 0.1 for _ in range(2)]
+        bq, bk = [torch.randn(ATT, generator=gen, device="cuda") * 0.1 for _ in range(2)]
+        a = torch.tensor(0.4, device="cuda")
+        g = o.GraphCSR(ei, n)
+        if mode == 'reference' and norm_idx == 0:
+            ns = o.uniform_scores(H)
+            m, rl = o.softmax_stats(g, ns, 0)
+            want = o.spmm_rhs(g, o.attn_weights(g, ns, m, rl, 0), x, alpha=a)
+        else:
+            kw = dict(wcat=(torch.cat([Wq, Wk]), torch.cat([bq, bk]))) if mode == 'per_edge' else {}
+            ns = o.node_scores(g, x, Wq, bq, Wk, bk, H, 'scaled_dot', mode, **kw)
+            want = o.attn_rhs(g, ns, None, None, norm_idx, x, alpha=a)
+        if cls == 'cols':
+            sh = gdd.ColumnShardedTransformer(ei, n, c, Wq, bq, Wk, bk, H, norm_idx, a, score_mode=mode,
+                                              comm=StagedComm())
+            f = sh.gather(sh(None, sh.split(x)))
+        else:
+            sh = gdd.RowShardedTransformer(ei, n, c, Wq, bq, Wk, bk, H, norm_idx, a, score_mode=mode,
+                                           comm=StagedComm())
+            f = sh.gather(sh(None, sh.scatter(x)))
+        torch.cuda.synchronize()
+        q.put((rank, rel(f.view(want.shape), want)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("cls,mode,norm_idx", [("cols", "reference", 1), ("cols", "per_edge", 0),
+                                               ("rows", "reference", 1), ("rows", "per_edge", 1),
+                                               ("rows", "reference", 0)])
+def test_sharded_classes_two_ranks_one_gpu(cls, mode, norm_idx):
+    import torch.multiprocessing as mp
+    ctx = multiprocessing.get_context("spawn")
+    q = ctx.Queue()
+    port = random.randint(20000, 40000)
+    mp.start_processes(_two_rank_worker, args=(2, port, cls, mode, norm_idx, q), nprocs=2, join=True,
+                       start_method="spawn")
+    res = sorted(q.get(timeout=120) for _ in range(2))
+    for rank, err in res:
+        assert err <= 1e-6, (rank, err)
