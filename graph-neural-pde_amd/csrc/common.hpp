@@ -331,12 +331,13 @@ __device__ __forceinline__ void epi_prefetch(const Epi& e, int64_t row, int cc, 
     if (e.st.dot_rows) load_packed<VEC>(as_t<T>(e.st.dot_with) + off, p.dw);
 }
 
-// One stage combination cb*base + cf*f + sum_j c[j]*k[j] of a row slice.  The base
-// is x (already in registers), a prefetched row (pre != nullptr) or loaded here.
+// One stage combination cb*base + sc*cf*f + sum_j sc*c[j]*k[j] of a row slice
+// (sc = *coef_scale or 1; multiplying by 1.0f changes no bit).  The base is x
+// (already in registers), a prefetched row (pre != nullptr) or loaded here.
 template <int VEC, int NK, class T, class KV>
 __device__ __forceinline__ void stage_combine(const Epi& e, const gnpde_stage_out_t& so, int64_t off,
                                               const float (&o)[VEC], const Packed<VEC, T>& xr,
-                                              const Packed<VEC, T>* pre, const KV& kval, float (&r)[VEC]) {
+                                              const Packed<VEC, T>* pre, const KV& kval, float sc, float (&r)[VEC]) {
   const bool need_x = (e.flags & GNPDE_EPI_RHS) != 0;
   if (so.base == nullptr) {
 #pragma unroll
@@ -356,12 +357,100 @@ __device__ __forceinline__ void stage_combine(const Epi& e, const gnpde_stage_ou
 #pragma unroll
   for (int j = 0; j < NK; ++j) {
     if (j < e.st.nk) {
+      const float c = so.c[j] * sc;
 #pragma unroll
-      for (int t = 0; t < VEC; ++t) r[t] = fmaf(so.c[j], kval(j, t), r[t]);
+      for (int t = 0; t < VEC; ++t) r[t] = fmaf(c, kval(j, t), r[t]);
+    }
+  }
+  const float cf = so.cf * sc;
+#pragma unroll
+  for (int t = 0; t < VEC; ++t) r[t] = fmaf(cf, o[t], r[t]);
+}
+
+__device__ __forceinline__ float stage_scale(const gnpde_stage_epilogue_t& st) {
+  return st.coef_scale ? *st.coef_scale : 1.f;
+}
+
+// The wide stage epilogue of one row slice (STG 4; also gnpde_stage_apply_*),
+// streamed over the shared operands so that one operand row is live at a time:
+// every output and the error combination start from cb*base (x when the base is
+// the RHS input xid, with values xv), take sc*c[j]*k[j] for j ascending, then
+// sc*cf*f — per output the same order as stage_combine, so the same bits.
+// Returns the error combination in ev (when err_rows) and output values in r.
+template <int VEC, class T>
+__device__ __forceinline__ void wide_combine(const gnpde_stage_epilogue_t& st, int64_t off, const float (&o)[VEC],
+                                             const float* xid, const float (&xv)[VEC], float (&r)[2][VEC],
+                                             float (&ev)[VEC]) {
+  const float sc = stage_scale(st);
+  auto base_term = [&](const gnpde_stage_out_t& so, float (&acc)[VEC]) {
+    if (so.base == nullptr) {
+#pragma unroll
+      for (int t = 0; t < VEC; ++t) acc[t] = 0.f;
+    } else if (xid != nullptr && so.base == xid) {
+#pragma unroll
+      for (int t = 0; t < VEC; ++t) acc[t] = so.cb * xv[t];
+    } else {
+      Packed<VEC, T> bv;
+      load_packed<VEC>(as_t<T>(so.base) + off, bv);
+#pragma unroll
+      for (int t = 0; t < VEC; ++t) acc[t] = so.cb * unpack(bv, t);
+    }
+  };
+  const bool has_err = st.err_rows != nullptr;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+    if (i < st.n_out) base_term(st.o[i], r[i]);
+  if (has_err) base_term(st.err, ev);
+#pragma unroll
+  for (int j = 0; j < GNPDE_STAGE_MAX_K; ++j) {
+    if (j < st.nk) {
+      Packed<VEC, T> kv;
+      load_packed<VEC>(as_t<T>(st.k[j]) + off, kv);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        if (i < st.n_out) {
+          const float c = st.o[i].c[j] * sc;
+#pragma unroll
+          for (int t = 0; t < VEC; ++t) r[i][t] = fmaf(c, unpack(kv, t), r[i][t]);
+        }
+      }
+      if (has_err) {
+        const float c = st.err.c[j] * sc;
+#pragma unroll
+        for (int t = 0; t < VEC; ++t) ev[t] = fmaf(c, unpack(kv, t), ev[t]);
+      }
     }
   }
 #pragma unroll
-  for (int t = 0; t < VEC; ++t) r[t] = fmaf(so.cf, o[t], r[t]);
+  for (int i = 0; i < 2; ++i) {
+    if (i < st.n_out) {
+      const float cf = st.o[i].cf * sc;
+#pragma unroll
+      for (int t = 0; t < VEC; ++t) r[i][t] = fmaf(cf, o[t], r[i][t]);
+    }
+  }
+  if (has_err) {
+    const float cf = st.err.cf * sc;
+#pragma unroll
+    for (int t = 0; t < VEC; ++t) ev[t] = fmaf(cf, o[t], ev[t]);
+  }
+}
+
+// sum_t (e_t / tol_t)^2 in fp64 with tol = atol + rtol * max(|y0|, |y1|): the
+// slice's share of the embedded pair's squared error norm.
+template <int VEC, class T>
+__device__ __forceinline__ double err_terms(const gnpde_stage_epilogue_t& st, int64_t off, const float (&ev)[VEC],
+                                            const float (&y1)[VEC]) {
+  Packed<VEC, T> y0v;
+  load_packed<VEC>(as_t<T>(st.err_y0) + off, y0v);
+  double d = 0.0;
+#pragma unroll
+  for (int t = 0; t < VEC; ++t) {
+    const double tol = st.atol + st.rtol * (double)fmaxf(fabsf(unpack(y0v, t)), fabsf(y1[t]));
+    const double q = (double)ev[t] / tol;
+    d = fma(q, q, d);
+  }
+  return d;
 }
 
 // f = a*(ax - x) [+ b*x0]  (function_laplacian_diffusion.py:69-77) or f = ax,
@@ -389,62 +478,45 @@ __device__ __forceinline__ void epi_finish(const Epi& e, int64_t row, int cc, co
   }
   const int64_t off = row * e.ldf + cc;
   if (e.st.f_out) store_vec<VEC>(as_t<T>(e.st.f_out) + off, o);
-  if constexpr (stage_dot<STG>()) {
-    if (e.st.dot_rows && dpart) {
-      Packed<VEC, T> dw;
-      if constexpr (STG == 2)
-        dw = p.dw;
-      else
-        load_packed<VEC>(as_t<T>(e.st.dot_with) + off, dw);
-#pragma unroll
-      for (int t = 0; t < VEC; ++t) *dpart = fma((double)o[t], (double)unpack(dw, t), *dpart);
-    }
-  }
-  // the shared stage operands: prefetched (STG 1-3) or loaded now (STG 4), each once
-  constexpr int NK = STG == 4 ? GNPDE_STAGE_MAX_K : stage_kpre<STG>();
-  Packed<VEC, T> kw[STG == 4 ? GNPDE_STAGE_MAX_K : 1];
-  if constexpr (STG == 4) {
-#pragma unroll
-    for (int j = 0; j < GNPDE_STAGE_MAX_K; ++j)
-      if (j < e.st.nk) load_packed<VEC>(as_t<T>(e.st.k[j]) + off, kw[j]);
-  }
-  auto kval = [&](int j, int t) -> float {
-    if constexpr (STG == 4)
-      return unpack(kw[j], t);
-    else
-      return unpack(p.kv[j], t);
-  };
   // the stage outputs' row (out_rows: the last step of a renumbered solve writes the caller's numbering)
   const int64_t oo = e.st.out_rows ? (int64_t)e.st.out_rows[row] * e.ldf + cc : off;
-  float y1[VEC];  // STG 4: the output the error tolerance reads (err_y1 >= 0)
+  if constexpr (STG == 4) {
+    float xv[VEC], r[2][VEC], ev[VEC];
 #pragma unroll
-  for (int i = 0; i < stage_nout<STG>(); ++i) {
-    if (i >= e.st.n_out) break;
-    float r[VEC];
-    const Packed<VEC, T>* pre = nullptr;
-    if constexpr (STG != 4) pre = &p.base[i];
-    stage_combine<VEC, NK, T>(e, e.st.o[i], off, o, p.xr, pre, kval, r);
-    store_vec<VEC>(as_t<T>(e.st.o[i].out) + oo, r);
-    if constexpr (STG == 4) {
-      if (i == e.st.err_y1) {
+    for (int t = 0; t < VEC; ++t) xv[t] = need_x ? unpack(p.xr, t) : 0.f;
+    wide_combine<VEC, T>(e.st, off, o, (need_x && e.ldx == e.ldf) ? e.x : nullptr, xv, r, ev);
 #pragma unroll
-        for (int t = 0; t < VEC; ++t) y1[t] = r[t];
+    for (int i = 0; i < 2; ++i)
+      if (i < e.st.n_out) store_vec<VEC>(as_t<T>(e.st.o[i].out) + oo, r[i]);
+    if (e.st.err_rows && dpart) {
+      float y1[VEC];
+#pragma unroll
+      for (int t = 0; t < VEC; ++t) y1[t] = e.st.err_y1 == 1 ? r[1][t] : (e.st.err_y1 == 0 ? r[0][t] : xv[t]);
+      *dpart += err_terms<VEC, T>(e.st, off, ev, y1);
+    }
+    return;
+  } else {
+    if constexpr (stage_dot<STG>()) {
+      if (e.st.dot_rows && dpart) {
+        Packed<VEC, T> dw;
+        if constexpr (STG == 2)
+          dw = p.dw;
+        else
+          load_packed<VEC>(as_t<T>(e.st.dot_with) + off, dw);
+#pragma unroll
+        for (int t = 0; t < VEC; ++t) *dpart = fma((double)o[t], (double)unpack(dw, t), *dpart);
       }
     }
-  }
-  if constexpr (STG == 4) {
-    if (e.st.err_rows && dpart) {
-      float ev[VEC];
-      stage_combine<VEC, NK, T>(e, e.st.err, off, o, p.xr, nullptr, kval, ev);
-      Packed<VEC, T> y0v;
-      load_packed<VEC>(as_t<T>(e.st.err_y0) + off, y0v);
+    // the shared stage operands, prefetched before the gathers
+    constexpr int NK = stage_kpre<STG>();
+    auto kval = [&](int j, int t) -> float { return unpack(p.kv[j], t); };
+    const float sc = stage_scale(e.st);
 #pragma unroll
-      for (int t = 0; t < VEC; ++t) {
-        const float yb = e.st.err_y1 < 0 ? unpack(p.xr, t) : y1[t];
-        const double tol = e.st.atol + e.st.rtol * (double)fmaxf(fabsf(unpack(y0v, t)), fabsf(yb));
-        const double q = (double)ev[t] / tol;
-        *dpart = fma(q, q, *dpart);
-      }
+    for (int i = 0; i < stage_nout<STG>(); ++i) {
+      if (i >= e.st.n_out) break;
+      float r[VEC];
+      stage_combine<VEC, NK, T>(e, e.st.o[i], off, o, p.xr, &p.base[i], kval, sc, r);
+      store_vec<VEC>(as_t<T>(e.st.o[i].out) + oo, r);
     }
   }
 }

@@ -148,7 +148,7 @@ __global__ __launch_bounds__(256) void stage_apply_kernel(int64_t R, int C, int6
     const int cc = c0 + gl * VEC;
     if (!live || cc >= C) continue;
     const int64_t off = row * ld + cc;
-    float fv[VEC], xv[VEC], kv[GNPDE_STAGE_MAX_K][VEC];
+    float fv[VEC], xv[VEC];
     if (f) {
       load_vec<VEC>(f + off, fv);
     } else {
@@ -161,58 +161,18 @@ __global__ __launch_bounds__(256) void stage_apply_kernel(int64_t R, int C, int6
 #pragma unroll
       for (int t = 0; t < VEC; ++t) xv[t] = 0.f;
     }
-#pragma unroll
-    for (int j = 0; j < GNPDE_STAGE_MAX_K; ++j)
-      if (j < st.nk) load_vec<VEC>(as_t<T>(st.k[j]) + off, kv[j]);
-    auto comb = [&](const gnpde_stage_out_t& so, float (&r)[VEC]) {
-      if (so.base == nullptr) {
-#pragma unroll
-        for (int t = 0; t < VEC; ++t) r[t] = 0.f;
-      } else if (x && so.base == reinterpret_cast<const float*>(x)) {
-#pragma unroll
-        for (int t = 0; t < VEC; ++t) r[t] = so.cb * xv[t];
-      } else {
-        float bv[VEC];
-        load_vec<VEC>(as_t<T>(so.base) + off, bv);
-#pragma unroll
-        for (int t = 0; t < VEC; ++t) r[t] = so.cb * bv[t];
-      }
-#pragma unroll
-      for (int j = 0; j < GNPDE_STAGE_MAX_K; ++j) {
-        if (j < st.nk) {
-#pragma unroll
-          for (int t = 0; t < VEC; ++t) r[t] = fmaf(so.c[j], kv[j][t], r[t]);
-        }
-      }
-#pragma unroll
-      for (int t = 0; t < VEC; ++t) r[t] = fmaf(so.cf, fv[t], r[t]);
-    };
     if (st.f_out) store_vec<VEC>(as_t<T>(st.f_out) + off, fv);
+    float r[2][VEC], ev[VEC];
+    wide_combine<VEC, T>(st, off, fv, x ? reinterpret_cast<const float*>(x) : nullptr, xv, r, ev);
     const int64_t oo = st.out_rows ? (int64_t)st.out_rows[row] * ld + cc : off;
-    float y1[VEC];
 #pragma unroll
-    for (int t = 0; t < VEC; ++t) y1[t] = xv[t];
-#pragma unroll
-    for (int i = 0; i < GNPDE_STAGE_MAX_OUT; ++i) {
-      if (i >= st.n_out) break;
-      float r[VEC];
-      comb(st.o[i], r);
-      store_vec<VEC>(as_t<T>(st.o[i].out) + oo, r);
-      if (i == st.err_y1) {
-#pragma unroll
-        for (int t = 0; t < VEC; ++t) y1[t] = r[t];
-      }
-    }
+    for (int i = 0; i < 2; ++i)
+      if (i < st.n_out) store_vec<VEC>(as_t<T>(st.o[i].out) + oo, r[i]);
     if (st.err_rows) {
-      float ev[VEC], y0v[VEC];
-      comb(st.err, ev);
-      load_vec<VEC>(as_t<T>(st.err_y0) + off, y0v);
+      float y1[VEC];
 #pragma unroll
-      for (int t = 0; t < VEC; ++t) {
-        const double tol = st.atol + st.rtol * (double)fmaxf(fabsf(y0v[t]), fabsf(y1[t]));
-        const double q = (double)ev[t] / tol;
-        dpart = fma(q, q, dpart);
-      }
+      for (int t = 0; t < VEC; ++t) y1[t] = st.err_y1 == 1 ? r[1][t] : (st.err_y1 == 0 ? r[0][t] : xv[t]);
+      dpart += err_terms<VEC, T>(st, off, ev, y1);
     }
   }
   if (st.err_rows) {  // kernel-uniform

@@ -31,7 +31,7 @@ class StageEpilogue(ctypes.Structure):
                 ("out_rows", ctypes.c_void_p), ("dot_with", ctypes.c_void_p), ("dot_rows", ctypes.c_void_p),
                 ("dot_coef", ctypes.c_double), ("dot_accumulate", ctypes.c_int),
                 ("err_rows", ctypes.c_void_p), ("err", StageOut), ("err_y0", ctypes.c_void_p), ("err_y1", ctypes.c_int),
-                ("atol", ctypes.c_double), ("rtol", ctypes.c_double)]
+                ("atol", ctypes.c_double), ("rtol", ctypes.c_double), ("coef_scale", ctypes.c_void_p)]
 
 
 c_i32p = ctypes.POINTER(ctypes.c_int32)

@@ -1091,12 +1091,46 @@ def _fused_adaptive_ok(func, y0, combine, options):
     return bool(getattr(func, 'host_stages', False)) and hasattr(func, 'host_stage_apply')
 
 
+# Captured adaptive steps (hipGraph): one graph per (buffer binding, dense-output
+# variant) replays a whole step — the stage-input pass, the RHS launches and the
+# error reduction — whatever dt (the coefficients scale by a device scalar), so a
+# step costs one graph launch and one host read.  GNPDE_ADAPTIVE_GRAPH=0 runs
+# every step eagerly.
+ADAPTIVE_GRAPH = os.environ.get('GNPDE_ADAPTIVE_GRAPH', '1') != '0'
+_ADAPTIVE_CACHE = weakref.WeakKeyDictionary()  # module -> (key, _AdaptiveState)
+
+
+class _AdaptiveState(object):
+    """Buffers and captured step graphs of one module's fused adaptive solves of one
+    state shape and tolerance (kept across odeint calls, like _StatePool)."""
+
+    def __init__(self, plan, y0, host):
+        new = lambda: torch.empty_like(y0, memory_format=torch.contiguous_format)  # noqa: E731
+        b = {'Y': new(), 'Y1': new(), 'K0': new()}
+        for j in sorted(plan.store | plan.store_mid):
+            b['K%d' % j] = new()
+        xa, xb = new(), new()
+        for i in range(plan.ns):
+            b['X%d' % i] = b['Y1'] if (plan.fsal and i == plan.ns - 1) else (xa if i % 2 == 0 else xb)
+        if any(L['epart'] is not None for L in plan.launches):
+            b['E'] = new()
+        self.bufs = b
+        self.rows = torch.empty(y0.numel() // y0.shape[-1], dtype=torch.float64, device=y0.device)
+        # the step size the stage coefficients are scaled by (device fp32 scalar; the host-stage
+        # test RHS objects apply it in their own precision)
+        self.scale = torch.zeros((), dtype=torch.float32 if not host else torch.float64, device=y0.device)
+        self.graphs = {}   # (id Y, id K0, mid) -> (graph, error-sum tensor)
+        self.mempool = None
+        self.warm = False
+
+
 class _RKAdaptiveFused(_RKAdaptive):
     """_RKAdaptive with the step formed by the RHS epilogues (_AdaptivePlan): the same
     controller (torchdiffeq's, in host float64 arithmetic), the same accepted /
     rejected sequence, dense output from the stored stage derivatives.  Per step:
     one stage-input pass, len(alpha) RHS launches carrying the combinations and the
-    error rows, one fixed-order fp64 reduction and one host read of it."""
+    error rows, one fixed-order fp64 reduction and one host read of it; the step
+    replayed from a captured hipGraph once the module's structures are built."""
 
     def __init__(self, func, y0, rtol, atol, combine, method='dopri5', options=None, **kw):
         super(_RKAdaptiveFused, self).__init__(func, y0, rtol, atol, combine, method=method, **kw)
@@ -1113,77 +1147,121 @@ class _RKAdaptiveFused(_RKAdaptive):
             ops.stage_apply(stage, f, x, like)
 
     def _err_sum(self, rows):
+        """The step's squared error sum (0-d fp64 tensor) and its element count."""
         v = rows.sum() if self.host else ops.sum_f64(rows)
+        n = float(rows.numel() * self.C)
         red = getattr(self.func, 'reduce_error_sq', None)
         if red is not None and 'norm' in self.options:
-            pair = torch.stack([v.reshape(()), torch.tensor(float(rows.numel() * self.C), dtype=torch.float64,
-                                                            device=rows.device)])
+            pair = torch.stack([v.reshape(()), torch.tensor(n, dtype=torch.float64, device=rows.device)])
             red(pair)
-            return float(pair[0]), float(pair[1])
-        return float(v), float(rows.numel() * self.C)
+            return pair
+        return v
 
-    def _combo(self, spec, bufs, dt, x):
-        """(base tensor, cb, cf, [(k tensor, c)]) of a plan combination at step size dt."""
+    def _combo(self, spec, bufs, x):
+        """(base tensor, cb, cf, [(k tensor, c)]) of a plan combination; the k and f
+        coefficients are the tableau's, scaled by dt on the device (Stage.scale)."""
         base, terms, cfc = spec
         bt = {'Y': bufs['Y'], 'X': x, 'E': bufs.get('E'), None: None}[base]
-        return bt, (1.0 if bt is not None else 0.0), dt * cfc, [(bufs[k], dt * c) for k, c in terms]
+        return bt, (1.0 if bt is not None else 0.0), cfc, [(bufs[k], c) for k, c in terms]
 
-    def _launch(self, i, bufs, x, t, dt, rows, mid):
+    def _launch(self, i, st, x, t, mid):
         P = self.plan
+        bufs = st.bufs
         L = P.launches[i]
         outs = []
-        if L['next'] is not None:
-            b, cb, cf, ks = self._combo(L['next'], bufs, dt, x)
-            outs.append((bufs['X%d' % (i + 1)], b, cb, cf, ks))
-        if L['y1'] is not None:
-            b, cb, cf, ks = self._combo(L['y1'], bufs, dt, x)
-            outs.append((bufs['Y1'], b, cb, cf, ks))
-        if L['epart'] is not None:
-            b, cb, cf, ks = self._combo(L['epart'], bufs, dt, x)
-            outs.append((bufs['E'], b, cb, cf, ks))
+        for key, dst in (('next', 'X%d' % (i + 1)), ('y1', 'Y1'), ('epart', 'E')):
+            if L[key] is not None:
+                b, cb, cf, ks = self._combo(L[key], bufs, x)
+                outs.append((bufs[dst], b, cb, cf, ks))
         err = None
         if L['err'] is not None:
-            b, cb, cf, ks = self._combo(L['err'], bufs, dt, x)
-            err = (rows, (b, cb, cf, ks), bufs['Y'], 0 if L['y1'] is not None else -1, self.atol_f, self.rtol_f)
+            b, cb, cf, ks = self._combo(L['err'], bufs, x)
+            err = (st.rows, (b, cb, cf, ks), bufs['Y'], 0 if L['y1'] is not None else -1, self.atol_f, self.rtol_f)
         j = i + 1
         f_out = bufs['K%d' % j] if (j in P.store or (mid and j in P.store_mid)) else None
-        stage = ops.Stage(f_out=f_out, outs=outs, err=err)
-        self.func.rhs_stage(t, x, stage)
+        self.func.rhs_stage(t, x, ops.Stage(f_out=f_out, outs=outs, err=err, scale=st.scale))
+
+    def _step(self, st, t_cur, dt, mid):
+        """Enqueue one step (stage-input pass, RHS launches, error reduction); returns
+        the device error sum."""
+        P = self.plan
+        bufs = st.bufs
+        self._apply(ops.Stage(outs=[(bufs['X0'], bufs['Y'], 1.0, 0.0, [(bufs['K0'], P.beta[0][0])])],
+                              scale=st.scale), None, None, bufs['Y'])
+        for i in range(P.ns):
+            ti = t_cur + dt if P.alpha[i] == 1. else t_cur + P.alpha[i] * dt
+            self._launch(i, st, bufs['X%d' % i], ti, mid)
+        return self._err_sum(st.rows)
+
+    def _state(self, y0):
+        """The module's cached buffers / graphs for this shape, tolerance and graph
+        state (a new entry when any of them changed)."""
+        P = self.plan
+        if self.host or not ADAPTIVE_GRAPH or not getattr(self.func, 'graph_capturable', True):
+            return _AdaptiveState(P, y0, self.host), False
+        state = _capture_state(self.func, y0)
+        key = _graph_cache_key(self.func, 'adaptive:' + P.method, y0, state)
+        if key is None:
+            return _AdaptiveState(P, y0, self.host), False
+        key = key + (self.atol_f, self.rtol_f, torch.cuda.current_stream(y0.device).cuda_stream,
+                     'norm' in self.options)
+        hit = _ADAPTIVE_CACHE.get(self.func)
+        if hit is not None and hit[0] == key:
+            return hit[1], True
+        ast = _AdaptiveState(P, y0, self.host)
+        _ADAPTIVE_CACHE[self.func] = (key, ast, state)
+        return ast, True
+
+    def _run_step(self, st, graphs_ok, t_cur, dt, mid):
+        """One step: replayed from its graph when the binding's graph exists (captured
+        on first use once the module is warm), eagerly otherwise."""
+        P = self.plan
+        if graphs_ok and st.warm and _nfe_headroom(self.func, P.ns):
+            gk = (id(st.bufs['Y']), id(st.bufs['K0']), bool(mid))
+            ent = st.graphs.get(gk)
+            if ent is None:
+                nfe = getattr(self.func, 'nfe', None)
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=st.mempool):
+                    err = self._step(st, t_cur, dt, mid)
+                if st.mempool is None:
+                    st.mempool = g.pool()
+                if nfe is not None:
+                    self.func.nfe = nfe  # capture records launches, it evaluates nothing
+                ent = (g, err)
+                st.graphs[gk] = ent
+            ent[0].replay()
+            if hasattr(self.func, 'nfe'):
+                self.func.nfe += P.ns
+            return ent[1]
+        err = self._step(st, t_cur, dt, mid)
+        st.warm = True
+        return err
 
     def integrate(self, t):
         P = self.plan
         th = [float(v) for v in t.detach().to(torch.float64).cpu().tolist()]
         y0 = self.y0.contiguous()
         self.C = y0.shape[-1]
-        R = y0.numel() // self.C
         dev = y0.device
         sol = torch.empty((len(th),) + tuple(y0.shape), dtype=y0.dtype, device=dev)
         sol[0].copy_(y0)
-        new = lambda: torch.empty_like(y0, memory_format=torch.contiguous_format)  # noqa: E731
-        bufs = {'Y': new(), 'Y1': new(), 'K0': None}
+        st, graphs_ok = self._state(y0)
+        bufs = st.bufs
         bufs['Y'].copy_(y0)
-        for j in sorted(P.store | P.store_mid):
-            bufs['K%d' % j] = new()
-        xa, xb = new(), new()
-        for i in range(P.ns):
-            if P.fsal and i == P.ns - 1:
-                bufs['X%d' % i] = bufs['Y1']
-            else:
-                bufs['X%d' % i] = xa if i % 2 == 0 else xb
-        if any(L['epart'] is not None for L in P.launches):
-            bufs['E'] = new()
-        rows = torch.empty(R, dtype=torch.float64, device=dev)
         t0 = torch.tensor(th[0], dtype=torch.float64)
         f0 = self.func(t0, bufs['Y'])
-        bufs['K0'] = f0.contiguous() if f0.dtype == y0.dtype else f0.to(y0.dtype).contiguous()
+        bufs['K0'].copy_(f0)
         if self.first_step is None:
             dt = float(self._select_initial_step(t0.to(dev) if not self.host else t0, bufs['K0']))
         else:
             dt = float(self.first_step)
         t_cur = th[0]
-        last = None  # (t_prev, dt of the accepted step, needs a dense output)
+        last = None  # (t_prev, dt) of the last accepted step
+        self._dense = None
         order = float(P.order)
         safety, ifactor, dfactor = float(self.safety), float(self.ifactor), float(self.dfactor)
+        kn = 'K%d' % P.ns
         for i_out in range(1, len(th)):
             next_t = th[i_out]
             while next_t > t_cur:
@@ -1192,22 +1270,19 @@ class _RKAdaptiveFused(_RKAdaptive):
                 if self.n_steps >= self.max_num_steps:
                     raise AssertionError('max_num_steps exceeded ({}>={})'.format(self.n_steps, self.max_num_steps))
                 mid = t_cur + dt >= next_t  # an accepted step would cross an output time: keep the dense-output k's
-                # the step's first stage input X0 = y0 + dt b00 k0
-                self._apply(ops.Stage(outs=[(bufs['X0'], bufs['Y'], 1.0, 0.0, [(bufs['K0'], dt * P.beta[0][0])])]),
-                            None, None, bufs['Y'])
-                for i in range(P.ns):
-                    ti = t_cur + dt if P.alpha[i] == 1. else t_cur + P.alpha[i] * dt
-                    self._launch(i, bufs, bufs['X%d' % i], ti, dt, rows, mid)
-                s, n = self._err_sum(rows)
-                ratio = math.sqrt(s / n) if n > 0 else 0.0
-                accept = ratio <= 1
-                if accept:
+                st.scale.fill_(dt)
+                err = self._run_step(st, graphs_ok, t_cur, dt, mid)
+                if err.dim() == 0:
+                    ratio = math.sqrt(float(err) / (y0.numel()))  # the one host read of the step
+                else:
+                    e2, n = (float(v) for v in err.tolist())
+                    ratio = math.sqrt(e2 / n) if n > 0 else 0.0
+                if ratio <= 1:
                     t_prev, t_cur = t_cur, t_cur + dt
-                    kn = 'K%d' % P.ns
                     last = (t_prev, dt)
                     # a step that crossed an output time keeps its operands for the dense output (the
                     # references as they are now; the buffers are only rewritten by the next step)
-                    self._dense = dict(bufs) if mid else None
+                    self._dense = dict(bufs, scale=dt) if mid else None
                     bufs['Y'], bufs['Y1'] = bufs['Y1'], bufs['Y']
                     bufs['K0'], bufs[kn] = bufs[kn], bufs['K0']
                     if P.fsal:

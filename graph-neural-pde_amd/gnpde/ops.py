@@ -519,8 +519,10 @@ class Stage(object):
     in fp64 with e the combination, tol = atol + rtol * max(|y0|, |y1|), y1 = the
     RHS input (y1_out = -1) or output ``y1_out``."""
 
-    def __init__(self, f_out=None, outs=(), out_rows=None, dot=None, err=None):
+    def __init__(self, f_out=None, outs=(), out_rows=None, dot=None, err=None, scale=None):
         self.f_out = f_out
+        # a device fp32 0-d tensor multiplying every cf and c_j (not cb): the adaptive step size
+        self.scale = scale
         self.outs = list(outs)
         self.out_rows = out_rows  # int32 [R] or None: row r's ``outs`` stores go to row out_rows[r]
         # (y, rows, coef, accumulate) or None: rows[r] (+)= coef * <f[r], y[r]> in fp64 (fp32 state)
@@ -614,6 +616,9 @@ class Stage(object):
             st.err_y0 = y0.data_ptr()
             st.err_y1 = int(y1_out)
             st.atol, st.rtol = float(atol), float(rtol)
+        if self.scale is not None:
+            _require_gpu(self.scale, "coefficient scale", torch.float32)
+            st.coef_scale = self.scale.data_ptr()
         return st
 
 

@@ -192,6 +192,10 @@ size_t gnpde_plan_workspace_bytes(int64_t R);
  *   tol    = atol + rtol * max(|err_y0|, |y1|)
  *   err_rows[r] = sum_c (e / tol)^2     (fp64, the row's lanes in a fixed order)
  * which the caller sums (gnpde_sum_f64) into the squared norm of one step.
+ * coef_scale (NULL = 1): a device fp32 scalar multiplying every cf and c[j] of the
+ * outputs and of err (not cb): the step size of an adaptive solve, so the
+ * launches of a step do not change with it (hipGraph-replayable, one graph per
+ * step whatever dt).
  * At most 2 k operands with dot_rows; err_rows and 3..6 operands take the wide
  * epilogue (operands loaded after the aggregation), fused into the plain-weight
  * K1 (gnpde_spmm_rhs_f32 / _bf16); the attention kernels return
@@ -223,6 +227,7 @@ typedef struct {
   int err_y1;
   double atol;
   double rtol;
+  const float* coef_scale;
 } gnpde_stage_epilogue_t;
 
 /* The stage epilogue as a pass of its own, over rows [0, R) of C columns

@@ -6,11 +6,11 @@ stages only in HIP."""
 import torch
 
 
-def _combo(base, cb, cf, terms, f):
+def _combo(base, cb, cf, terms, f, sc=1.0):
     r = torch.zeros_like(f) if base is None else cb * base
     for k, c in terms:
-        r = r + c * k
-    return r + cf * f
+        r = r + (c * sc) * k
+    return r + (cf * sc) * f
 
 
 def apply_stage(stage, f, x):
@@ -20,14 +20,15 @@ def apply_stage(stage, f, x):
         f = torch.zeros_like(like)
     if stage.f_out is not None:
         stage.f_out.copy_(f)
+    sc = float(stage.scale) if stage.scale is not None else 1.0
     vals = []
     for out, base, cb, cf, terms in stage.outs:
-        v = _combo(base, cb, cf, terms, f)
+        v = _combo(base, cb, cf, terms, f, sc)
         vals.append(v)
         out.copy_(v)
     if stage.err is not None:
         rows, (base, cb, cf, terms), y0, y1_out, atol, rtol = stage.err
-        e = _combo(base, cb, cf, terms, f).double()
+        e = _combo(base, cb, cf, terms, f, sc).double()
         y1 = x if y1_out < 0 else vals[y1_out]
         tol = atol + rtol * torch.maximum(y0.abs(), y1.abs()).double()
         C = f.shape[-1]
