@@ -572,16 +572,19 @@ BLEND_K1 = {"fp32": "agg_kernel<4, 64, 1, 4, 1, 1, PlainWeights, float>",
             "bf16": "agg_kernel<8, 21, 1, 4, 3, 1, PlainWeights, bf16>"}
 
 
-def bench_attention(g, x, dev, ops, reps=20):
-    """The transformer RHS through the drop-in ODEFuncTransformerAtt (config C4 shape)."""
-    C = x.shape[-1]
-    heads, att = ATTN_HEADS, ATTN_DIM
-    out = {"config": "ODEFuncTransformerAtt, C=%d heads=%d attention_dim=%d (configs[3] shape, fp32)" % (C, heads,
-                                                                                                          att)}
-    for mode, norm_idx in ATTN_MODES:
-        func = attention_func(mode, norm_idx, C, dev)
-        func.edge_index = g.edge_index
-        func.graph_for(x)  # builds this function's CSR/CSC + plans once (outside the timed loop)
+def solve_numbering(func, x):
+    """(state, layout): the numbering a fixed-grid solve of ``func`` runs in
+    (gnpde.ops.NodeLayout, the graph's in-degree order) and x in it; (x, None)
+    when the module keeps the user numbering."""
+    lay = func.node_layout(x)
+    return (x, None) if lay is None else (lay.to_internal(x), lay)
+
+
+def _time_rhs(func, x, lay, reps):
+    """(eager ms, graph-replayed ms) of one RHS evaluation of ``func`` at x in the
+    numbering ``lay`` (None: the user numbering)."""
+    func._layout = lay
+    try:
         with torch.no_grad():
             for _ in range(3):
                 func(None, x)
@@ -592,11 +595,10 @@ def bench_attention(g, x, dev, ops, reps=20):
                 func(None, x)
             e.record()
             torch.cuda.synchronize()
-        ms_eager = s.elapsed_time(e) / reps
-        # the same RHS replayed from a captured hipGraph, as the fixed-grid
-        # integrator runs it (gnpde.integrator._StepGraphs): device time without
-        # the eager path's per-launch host cost
-        with torch.no_grad():
+            ms_eager = s.elapsed_time(e) / reps
+            # the same RHS replayed from a captured hipGraph, as the fixed-grid integrator
+            # runs it (gnpde.integrator._StepGraphs): device time without the eager path's
+            # per-launch host cost
             cg = torch.cuda.CUDAGraph()
             with torch.cuda.graph(cg):
                 func(None, x)
@@ -608,21 +610,42 @@ def bench_attention(g, x, dev, ops, reps=20):
                 cg.replay()
             e.record()
             torch.cuda.synchronize()
-        ms = s.elapsed_time(e) / reps
-        del cg
+            ms = s.elapsed_time(e) / reps
+            del cg
+    finally:
+        func._layout = None
+    return ms_eager, ms
+
+
+def bench_attention(g, x, dev, ops, reps=20):
+    """The transformer RHS through the drop-in ODEFuncTransformerAtt (config C4 shape),
+    in the node numbering a fixed-grid solve runs it in (the graph's in-degree order,
+    gnpde.ops.NodeLayout: VERDICT r3 item 4); the user-numbering time beside it."""
+    C = x.shape[-1]
+    heads, att = ATTN_HEADS, ATTN_DIM
+    out = {"config": "ODEFuncTransformerAtt, C=%d heads=%d attention_dim=%d (configs[3] shape, fp32), one RHS in "
+                     "the solve's node numbering" % (C, heads, att)}
+    for mode, norm_idx in ATTN_MODES:
+        func = attention_func(mode, norm_idx, C, dev)
+        func.edge_index = g.edge_index
+        func.graph_for(x)  # builds this function's CSR/CSC + plans once (outside the timed loop)
+        xs, lay = solve_numbering(func, x)
+        ms_eager, ms = _time_rhs(func, xs, lay, reps)
+        ms_user = _time_rhs(func, x, None, reps)[1] if lay is not None else ms
         kind = "uniform" if (mode, norm_idx) == ("reference", 0) else mode
         nb = attn_bytes(g.N, g.nnz, C, att, kind)
         cb = attn_compulsory(g.N, g.nnz, C, att, kind)
         tb = rhs_traffic("attn:%s_norm%d" % (mode, norm_idx))
         t = ms * 1e-3
-        ent = {"rhs_ms": round(ms, 4), "rhs_ms_eager": round(ms_eager, 4),
+        ent = {"rhs_ms": round(ms, 4), "rhs_ms_eager": round(ms_eager, 4), "rhs_ms_user_numbering": round(ms_user, 4),
+               "node_order": "degree" if lay is not None else "none",
                "algorithmic_bytes": nb, "algorithmic_frac": round(nb / t / 1e9 / HBM_PEAK_GBS, 4),
                "compulsory_bytes": cb, "compulsory_frac": round(cb / t / 1e9 / HBM_PEAK_GBS, 4)}
         if tb:
             ent.update({"traffic": int(tb), "achieved_GBs": round(tb / t / 1e9, 1),
                         "frac": round(tb / t / 1e9 / HBM_PEAK_GBS, 4),
-                        "basis": "PMC bytes of every kernel of one RHS (%s workload attn:%s_norm%d) / replayed "
-                                 "RHS time" % (TRAFFIC_FILE, mode, norm_idx)})
+                        "basis": "PMC bytes of every kernel of one RHS (%s workload attn:%s_norm%d, same numbering) / "
+                                 "replayed RHS time" % (TRAFFIC_FILE, mode, norm_idx)})
         else:
             ent.update({"traffic": None, "frac": None, "basis": "no PMC traffic in %s" % TRAFFIC_FILE})
         out["%s_norm%d" % (mode, norm_idx)] = ent

@@ -377,7 +377,7 @@ __device__ __forceinline__ float stage_scale(const gnpde_stage_epilogue_t& st) {
 // the RHS input xid, with values xv), take sc*c[j]*k[j] for j ascending, then
 // sc*cf*f — per output the same order as stage_combine, so the same bits.
 // Returns the error combination in ev (when err_rows) and output values in r.
-template <int VEC, class T>
+template <int VEC, class T, int NKMAX = GNPDE_STAGE_MAX_K, int NOUT = 2, bool ERR = true>
 __device__ __forceinline__ void wide_combine(const gnpde_stage_epilogue_t& st, int64_t off, const float (&o)[VEC],
                                              const float* xid, const float (&xv)[VEC], float (&r)[2][VEC],
                                              float (&ev)[VEC]) {
@@ -396,18 +396,18 @@ __device__ __forceinline__ void wide_combine(const gnpde_stage_epilogue_t& st, i
       for (int t = 0; t < VEC; ++t) acc[t] = so.cb * unpack(bv, t);
     }
   };
-  const bool has_err = st.err_rows != nullptr;
+  const bool has_err = ERR && st.err_rows != nullptr;
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < NOUT; ++i)
     if (i < st.n_out) base_term(st.o[i], r[i]);
   if (has_err) base_term(st.err, ev);
 #pragma unroll
-  for (int j = 0; j < GNPDE_STAGE_MAX_K; ++j) {
+  for (int j = 0; j < NKMAX; ++j) {
     if (j < st.nk) {
       Packed<VEC, T> kv;
       load_packed<VEC>(as_t<T>(st.k[j]) + off, kv);
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
+      for (int i = 0; i < NOUT; ++i) {
         if (i < st.n_out) {
           const float c = st.o[i].c[j] * sc;
 #pragma unroll
@@ -422,7 +422,7 @@ __device__ __forceinline__ void wide_combine(const gnpde_stage_epilogue_t& st, i
     }
   }
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < NOUT; ++i) {
     if (i < st.n_out) {
       const float cf = st.o[i].cf * sc;
 #pragma unroll

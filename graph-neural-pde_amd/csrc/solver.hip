@@ -135,7 +135,10 @@ __global__ __launch_bounds__(256) void rows_copy_kernel(const uint4* __restrict_
 // (cb*base, the operands by fmaf in index order, then cf*f), so the pass and the
 // fused epilogue give the same bits from the same f; the error rows summed over
 // the row's lanes by the same xor tree.
-template <int VEC, int GL, class T>
+// NKMAX / NOUT / ERR: the operands, outputs and error term an instantiation holds
+// registers for (the plain combinations of the adaptive step — its first stage input,
+// the dense output — take the light one: more waves, more bytes in flight).
+template <int VEC, int GL, class T, int NKMAX, int NOUT, bool ERR>
 __global__ __launch_bounds__(256) void stage_apply_kernel(int64_t R, int C, int64_t ld, const T* __restrict__ f,
                                                            const T* __restrict__ x, gnpde_stage_epilogue_t st) {
   constexpr int RPW = kWave / GL;
@@ -163,19 +166,19 @@ __global__ __launch_bounds__(256) void stage_apply_kernel(int64_t R, int C, int6
     }
     if (st.f_out) store_vec<VEC>(as_t<T>(st.f_out) + off, fv);
     float r[2][VEC], ev[VEC];
-    wide_combine<VEC, T>(st, off, fv, x ? reinterpret_cast<const float*>(x) : nullptr, xv, r, ev);
+    wide_combine<VEC, T, NKMAX, NOUT, ERR>(st, off, fv, x ? reinterpret_cast<const float*>(x) : nullptr, xv, r, ev);
     const int64_t oo = st.out_rows ? (int64_t)st.out_rows[row] * ld + cc : off;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < NOUT; ++i)
       if (i < st.n_out) store_vec<VEC>(as_t<T>(st.o[i].out) + oo, r[i]);
-    if (st.err_rows) {
+    if (ERR && st.err_rows) {
       float y1[VEC];
 #pragma unroll
       for (int t = 0; t < VEC; ++t) y1[t] = st.err_y1 == 1 ? r[1][t] : (st.err_y1 == 0 ? r[0][t] : xv[t]);
       dpart += err_terms<VEC, T>(st, off, ev, y1);
     }
   }
-  if (st.err_rows) {  // kernel-uniform
+  if (ERR && st.err_rows) {  // kernel-uniform
 #pragma unroll
     for (int o = 1; o < GL; o <<= 1) dpart += __shfl_xor(dpart, o);
     if (live && gl == 0) st.err_rows[row] = dpart;
@@ -188,12 +191,20 @@ static int launch_stage_apply(int64_t R, int C, int64_t ld, const T* f, const T*
   const int lanes = (int)ceil_div(C, VEC);
   const int64_t waves = [&](int rpw) { return ceil_div(R, (int64_t)rpw); }(lanes <= 16 ? 4 : (lanes <= 32 ? 2 : 1));
   const unsigned grid = (unsigned)std::max<int64_t>(1, ceil_div(waves, kWavesPerBlock));
-  if (lanes <= 16)
-    stage_apply_kernel<VEC, 16, T><<<grid, kBlock, 0, s>>>(R, C, ld, f, x, st);
-  else if (lanes <= 32)
-    stage_apply_kernel<VEC, 32, T><<<grid, kBlock, 0, s>>>(R, C, ld, f, x, st);
-  else
-    stage_apply_kernel<VEC, 64, T><<<grid, kBlock, 0, s>>>(R, C, ld, f, x, st);
+  const bool light = !st.err_rows && st.n_out <= 1 && st.nk <= 2;
+#define GNPDE_SA(GL)                                                                                  \
+  if (light)                                                                                          \
+    stage_apply_kernel<VEC, GL, T, 2, 1, false><<<grid, kBlock, 0, s>>>(R, C, ld, f, x, st);          \
+  else                                                                                                \
+    stage_apply_kernel<VEC, GL, T, GNPDE_STAGE_MAX_K, 2, true><<<grid, kBlock, 0, s>>>(R, C, ld, f, x, st)
+  if (lanes <= 16) {
+    GNPDE_SA(16);
+  } else if (lanes <= 32) {
+    GNPDE_SA(32);
+  } else {
+    GNPDE_SA(64);
+  }
+#undef GNPDE_SA
   GNPDE_LAUNCH_CHECK();
   return GNPDE_OK;
 }

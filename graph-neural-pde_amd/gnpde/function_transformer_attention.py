@@ -347,14 +347,20 @@ class ODEFuncTransformerAtt(ODEFunc):
         return st
 
     def supports_node_layout(self):
-        """The graph's locality numbering (ops.NodeLayout) is offered when the
-        attention weights are the graph-only 1/outdeg (BLEND: the fork's
-        scaled_dot under source-grouped softmax): every operand is then per node
-        or per edge and the renumbered solve is bit-identical.  Score modes are
-        not renumbered: the reference scores sum a key over all nodes (fp64, in
-        row-tile order) and the per-edge softmax scans depend on where a group
-        sits in its packed edge block — both would round differently."""
-        return self.multihead_att_layer.is_uniform(int(self.opt['attention_norm_idx']))
+        """The graph's locality numbering (ops.NodeLayout) for fixed-grid solves: every
+        operand of the scaled_dot RHS is per node (x, q, k, node scores) or per edge
+        in COO order, and a renumbering relabels them consistently, so the scores,
+        the softmax groups and the aggregation are the same.  Bit-identical for the
+        weights that are row-local in the fused kernels (the fork's 1/outdeg weights
+        under source-grouped softmax — BLEND — and the per-edge scores under
+        source-grouped softmax: each row scores and sums its own edges in COO
+        order); the key sum of the fork's scores (fp64, row-tile order) and the
+        destination statistics (packed CSC edge blocks) are summed in another order,
+        within fp64 / fp32 rounding (tests/test_gpu_layout.py).  Other attention
+        types keep the user numbering."""
+        lay = self.multihead_att_layer
+        return lay.is_uniform(int(self.opt['attention_norm_idx'])) or \
+            self.opt.get('attention_type', 'scaled_dot') == 'scaled_dot'
 
     def supports_feature_padding(self):
         """With the fork's scaled_dot under source-grouped softmax the weights do

@@ -90,11 +90,44 @@ def test_layout_blend_transformer_bit_identical(dtype):
     ref = _solve(func, x, "rk4", 7, 0.25, "none")
     got = _solve(func, x, "rk4", 7, 0.25, "degree")
     assert torch.equal(got, ref)
-    # score modes keep the user numbering
-    opt2 = dict(opt, attention_norm_idx=1)
+    # other attention types keep the user numbering
+    opt2 = dict(opt, attention_norm_idx=1, attention_type='cosine_sim')
     f2 = gnpde.ODEFuncTransformerAtt(C, C, opt2, DEV).to(DEV).eval()
     f2.edge_index = ei
     assert f2.node_layout(x) is None
+
+
+@pytest.mark.parametrize("mode,norm_idx,exact", [("per_edge", 0, True), ("per_edge", 1, False),
+                                                 ("reference", 1, False)])
+def test_layout_attention_scores(mode, norm_idx, exact):
+    """the scaled_dot score modes run fixed-grid solves in the
+    in-degree numbering too.  Per-edge scores under source-grouped softmax (the fused
+    kernel: each row scores and sums its own edges in COO order) are bit-identical;
+    the fork's key sum (fp64 row tiles) and the destination statistics (packed CSC
+    blocks) sum in another order: within 1e-6."""
+    N, E, C, h, att = 60000, 450000, 128, 2, 32
+    ei, _ = synthetic.rw_graph(N, E, seed=32, device=DEV)
+    opt = dict(OPT, hidden_dim=C, heads=h, attention_dim=att, attention_norm_idx=norm_idx,
+               attention_type='scaled_dot', attention_score_mode=mode, function='transformer', mix_features=False,
+               square_plus=False, beltrami=False)
+    func = gnpde.ODEFuncTransformerAtt(C, C, opt, DEV).to(DEV).eval()
+    gen = torch.Generator(device=DEV)
+    gen.manual_seed(9)
+    with torch.no_grad():
+        for lin in (func.multihead_att_layer.Q, func.multihead_att_layer.K):
+            lin.weight.copy_(torch.randn(att, C, generator=gen, device=DEV) * 0.1)
+            lin.bias.copy_(torch.randn(att, generator=gen, device=DEV) * 0.1)
+        func.alpha_train.fill_(0.3)
+    func.edge_index = ei
+    x = synthetic.features(1, N, C, seed=8, device=DEV)
+    assert func.node_layout(x) is not None
+    ref = _solve(func, x, "rk4", 7, 0.25, "none")
+    got = _solve(func, x, "rk4", 7, 0.25, "degree")
+    assert getattr(func._graph, '_layout', None) is not None
+    if exact:
+        assert torch.equal(got, ref)
+    else:
+        assert float((got - ref).abs().max() / ref.abs().max()) <= 1e-6
 
 
 def test_node_layout_structure():
