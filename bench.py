@@ -454,6 +454,7 @@ def bench_sharded(args, world, rank, dev, mode):
             "global_batch": 1, "parallelism": "%s%d" % (mode, world)},
         "speedup_vs_1gpu": r["speedup_vs_1gpu"], "one_gpu_value": r["one_gpu_value"],
         "shard": r.get("shard"),
+        "attention_sharded": None if args.no_attention else bench_attention_sharded(args, world, dev, mode),
     }
 
 
@@ -501,6 +502,44 @@ def sharded_point(N, E, C, h, steps, warmup, world, dev, mode, seed=0):
            "shard": info}
     del sh, y, y0, x, ei, w
     torch.cuda.empty_cache()
+    return out
+
+
+def bench_attention_sharded(args, world, dev, mode, steps=8):
+    """The transformer RHS on G-arxiv (configs[3]'s attention shape: heads 2,
+    attention_dim 32, C = 128) sharded in `mode` (gnpde.dist.ColumnShardedTransformer
+    / RowShardedTransformer) for the fork's scaled_dot (norm_idx 1)
+    and upstream GRAND's per-edge scaled_dot (norm_idx 0): rk4 steps through the
+    fused stages, against the unsharded ODEFuncTransformerAtt on each rank's GPU."""
+    import gnpde
+    from gnpde import dist as gd, synthetic
+    N, E, C, h = args.nodes, args.edges, args.dim, args.step_size
+    ei, _ = synthetic.rw_graph(N, E, seed=0, device=dev)
+    x = synthetic.features(1, N, C, seed=1, device=dev)
+    out = {"config": "ODEFuncTransformerAtt on %s (heads %d, attention_dim %d, C=%d), rk4 %d steps, %s over %d GPUs"
+                     % (graph_name(N, E), ATTN_HEADS, ATTN_DIM, C, steps, mode, world)}
+    for smode, norm_idx in (("reference", 1), ("per_edge", 0)):
+        func = attention_func(smode, norm_idx, C, dev)
+        func.edge_index = ei
+        el1, _ = timed_solve(func, x, steps, 2, h, dev, world)
+        lay = func.multihead_att_layer
+        a = torch.full((), 0.0, device=dev)
+        args_ = (ei, N, C, lay.Q.weight.detach(), lay.Q.bias.detach(), lay.K.weight.detach(), lay.K.bias.detach(),
+                 ATTN_HEADS, norm_idx, a)
+        if mode == "rows":
+            sh = gd.RowShardedTransformer(*args_, score_mode=smode)
+            y0 = sh.scatter(x)
+        else:
+            sh = gd.ColumnShardedTransformer(*args_, score_mode=smode)
+            y0 = sh.split(x)
+        el, _ = timed_solve(sh, y0, steps, 2, h, dev, world)
+        out["%s_norm%d" % (smode, norm_idx)] = {
+            "ms_per_step": round(el * 1e3 / steps, 4), "rhs_evals_per_s": round(4 * steps / el, 1),
+            "one_gpu_ms_per_step": round(el1 * 1e3 / steps, 4), "speedup_vs_1gpu": round(el1 / el, 3),
+            "collective_bytes_per_rhs": sh.bytes_per_rhs}
+        progress("attention %s %s_norm%d: %.3f ms per step" % (mode, smode, norm_idx, el * 1e3 / steps))
+        del sh, y0, func
+        torch.cuda.empty_cache()
     return out
 
 
