@@ -97,14 +97,14 @@ def test_layout_blend_transformer_bit_identical(dtype):
     assert f2.node_layout(x) is None
 
 
-@pytest.mark.parametrize("mode,norm_idx,exact", [("per_edge", 0, True), ("per_edge", 1, False),
-                                                 ("reference", 1, False)])
-def test_layout_attention_scores(mode, norm_idx, exact):
+@pytest.mark.parametrize("mode,norm_idx", [("per_edge", 0), ("per_edge", 1), ("reference", 1)])
+def test_layout_attention_scores(mode, norm_idx):
     """the scaled_dot score modes run fixed-grid solves in the
-    in-degree numbering too.  Per-edge scores under source-grouped softmax (the fused
-    kernel: each row scores and sums its own edges in COO order) are bit-identical;
-    the fork's key sum (fp64 row tiles) and the destination statistics (packed CSC
-    blocks) sum in another order: within 1e-6."""
+    in-degree numbering too, within 1e-6 of the user numbering: the fork's key sum
+    (fp64 row tiles) and the destination statistics (packed CSC blocks) sum in
+    another order, and in the fused per-edge kernel a row that shares its wavefront
+    with a hub chunk accumulates per head (the items pair up differently in the
+    other numbering's plan)."""
     N, E, C, h, att = 60000, 450000, 128, 2, 32
     ei, _ = synthetic.rw_graph(N, E, seed=32, device=DEV)
     opt = dict(OPT, hidden_dim=C, heads=h, attention_dim=att, attention_norm_idx=norm_idx,
@@ -124,10 +124,7 @@ def test_layout_attention_scores(mode, norm_idx, exact):
     ref = _solve(func, x, "rk4", 7, 0.25, "none")
     got = _solve(func, x, "rk4", 7, 0.25, "degree")
     assert getattr(func._graph, '_layout', None) is not None
-    if exact:
-        assert torch.equal(got, ref)
-    else:
-        assert float((got - ref).abs().max() / ref.abs().max()) <= 1e-6
+    assert float((got - ref).abs().max() / ref.abs().max()) <= 1e-6
 
 
 def test_node_layout_structure():
