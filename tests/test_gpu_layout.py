@@ -100,7 +100,9 @@ def test_layout_blend_transformer_bit_identical(dtype):
 @pytest.mark.parametrize("mode,norm_idx", [("per_edge", 0), ("per_edge", 1), ("reference", 1)])
 def test_layout_attention_scores(mode, norm_idx):
     """the scaled_dot score modes run fixed-grid solves in the
-    in-degree numbering too, within 1e-6 of the user numbering: the fork's key sum
+    in-degree numbering too, within the suite's 1e-5 of the user numbering (7e-6
+    measured for per-edge norm_idx 1 over 7 rk4 steps: the softmax of scores in the
+    tens amplifies last-bit differences; 1e-6 for one RHS): the fork's key sum
     (fp64 row tiles) and the destination statistics (packed CSC blocks) sum in
     another order, and in the fused per-edge kernel a row that shares its wavefront
     with a hub chunk accumulates per head (the items pair up differently in the
@@ -124,7 +126,18 @@ def test_layout_attention_scores(mode, norm_idx):
     ref = _solve(func, x, "rk4", 7, 0.25, "none")
     got = _solve(func, x, "rk4", 7, 0.25, "degree")
     assert getattr(func._graph, '_layout', None) is not None
-    assert float((got - ref).abs().max() / ref.abs().max()) <= 1e-6
+    assert float((got - ref).abs().max() / ref.abs().max()) <= 1e-5
+    # one RHS in either numbering
+    x_int, lay = func.node_layout(x).to_internal(x), func.node_layout(x)
+    with torch.no_grad():
+        f_user = func(None, x)
+        func._layout = lay
+        try:
+            f_int = func(None, x_int)
+        finally:
+            func._layout = None
+    f_back = lay.to_user(f_int)
+    assert float((f_back - f_user).abs().max() / f_user.abs().max()) <= 1e-6
 
 
 def test_node_layout_structure():
