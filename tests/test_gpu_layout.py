@@ -106,8 +106,13 @@ def test_layout_attention_scores(mode, norm_idx):
     (fp64 row tiles) and the destination statistics (packed CSC blocks) sum in
     another order, and in the fused per-edge kernel a row that shares its wavefront
     with a hub chunk accumulates per head (the items pair up differently in the
-    other numbering's plan)."""
+    other numbering's plan).  The fork's scores sum the keys of all E edges (q . S with
+    S ~ E |k|): at the per-edge cases' weight scale they reach ~1e4 and the softmax is
+    a hard arg-max whose choice a last-bit difference flips, so a solve is chaotic in
+    either numbering (its single RHS is still bit-equal: tools/layout_diag.py); its
+    weights are scaled so the scores stay O(1)."""
     N, E, C, h, att = 60000, 450000, 128, 2, 32
+    wscale = 1e-3 if mode == "reference" else 0.1
     ei, _ = synthetic.rw_graph(N, E, seed=32, device=DEV)
     opt = dict(OPT, hidden_dim=C, heads=h, attention_dim=att, attention_norm_idx=norm_idx,
                attention_type='scaled_dot', attention_score_mode=mode, function='transformer', mix_features=False,
@@ -117,8 +122,8 @@ def test_layout_attention_scores(mode, norm_idx):
     gen.manual_seed(9)
     with torch.no_grad():
         for lin in (func.multihead_att_layer.Q, func.multihead_att_layer.K):
-            lin.weight.copy_(torch.randn(att, C, generator=gen, device=DEV) * 0.1)
-            lin.bias.copy_(torch.randn(att, generator=gen, device=DEV) * 0.1)
+            lin.weight.copy_(torch.randn(att, C, generator=gen, device=DEV) * wscale)
+            lin.bias.copy_(torch.randn(att, generator=gen, device=DEV) * wscale)
         func.alpha_train.fill_(0.3)
     func.edge_index = ei
     x = synthetic.features(1, N, C, seed=8, device=DEV)
