@@ -192,12 +192,33 @@ class RowShardedLaplacian(object):
             self.blocks = balanced_row_blocks(host_rowptr(edge_index, self.N), self.world, row_weight)
             self.nb = max(max(r1 - r0 for r0, r1 in self.blocks), 1)
         self.r0, self.r1 = self.blocks[self.rank]
+        self._full = {}    # data_ptr of a state block -> its gathered buffer (alloc_state)
+        self._gbuf = None  # the gathered buffer of other states
+
+    def alloc_state(self, like):
+        """A state block [nb, C] that is rank p's row block of a gathered buffer
+        [world*nb, C] (gnpde.integrator places its stage inputs here): the all-gather
+        before each RHS then runs in place — no send copy, and at world 1 no copy at
+        all."""
+        full = torch.empty((self.world * self.nb,) + tuple(like.shape[1:]), dtype=like.dtype, device=like.device)
+        blk = full[self.rank * self.nb:(self.rank + 1) * self.nb]
+        self._full[blk.data_ptr()] = full
+        return blk
 
     def gather(self, y_local):
-        """All-gather of the row blocks (RCCL over xGMI on ROCm)."""
+        """All-gather of the row blocks (RCCL over xGMI on ROCm): in place when
+        y_local is a block of one of this object's gathered buffers (alloc_state),
+        else into a persistent buffer."""
         y_local = y_local.contiguous()
-        out = torch.empty((self.world * self.nb,) + tuple(y_local.shape[1:]), dtype=y_local.dtype,
-                          device=y_local.device)
+        full = self._full.get(y_local.data_ptr())
+        if full is not None and full.dtype == y_local.dtype and full.shape[1:] == y_local.shape[1:]:
+            if self.world > 1:
+                dist.all_gather_into_tensor(full, y_local, group=self.group)
+            return full
+        shape = (self.world * self.nb,) + tuple(y_local.shape[1:])
+        out = self._gbuf
+        if out is None or tuple(out.shape) != shape or out.dtype != y_local.dtype or out.device != y_local.device:
+            out = self._gbuf = torch.empty(shape, dtype=y_local.dtype, device=y_local.device)
         dist.all_gather_into_tensor(out, y_local, group=self.group)
         return out
 

@@ -225,12 +225,24 @@ def _fused_step(method, func, t0, dt, t1, y0, ws, out=None, out_rows=None):
 
 
 class _Workspace(dict):
+    """Stage-input buffers of the fused steps.  A RHS object may place the state
+    itself (``alloc_state(like)``: dist.RowShardedLaplacian hands out row blocks of
+    its gathered buffers, so the all-gather before each RHS is in place)."""
+
+    def __init__(self, alloc=None):
+        dict.__init__(self)
+        self.alloc = alloc
+
     def get(self, name, like):
         t = dict.get(self, name)
         if t is None or t.shape != like.shape or t.device != like.device:
-            t = torch.empty_like(like, memory_format=torch.contiguous_format)
+            t = _new_state(like, self.alloc)
             self[name] = t
         return t
+
+
+def _new_state(like, alloc=None):
+    return alloc(like) if alloc is not None else torch.empty_like(like, memory_format=torch.contiguous_format)
 
 
 # Graph replay of fixed-grid steps (hipGraph through torch.cuda.CUDAGraph): a run
@@ -267,9 +279,9 @@ class _StatePool(object):
     the captured graphs that read them stay valid and a solve needs no
     allocation)."""
 
-    def __init__(self, like):
-        self.bufs = [torch.empty_like(like, memory_format=torch.contiguous_format) for _ in range(2)]
-        self.ws = _Workspace()
+    def __init__(self, like, alloc=None):
+        self.bufs = [_new_state(like, alloc) for _ in range(2)]
+        self.ws = _Workspace(alloc)
 
 
 _POOLS = weakref.WeakKeyDictionary()  # module -> {(shape, dtype, device): _StatePool}
@@ -288,7 +300,7 @@ def _state_pool(func, y):
     if pool is None:
         if len(d) >= 4:
             d.clear()
-        pool = _StatePool(y)
+        pool = _StatePool(y, getattr(func, 'alloc_state', None))
         d[key] = pool
     return pool
 
