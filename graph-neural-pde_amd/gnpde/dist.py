@@ -159,14 +159,19 @@ class RowShardedLaplacian(object):
     y_local [nbmax, C] (its row block, zero padded to the largest block).
     Calling the object with (t, y_local) all-gathers the blocks into the padded
     [world*nbmax, C] layout of RowPartition, aggregates the local rows of A and
-    returns f_local [nbmax, C]; it drops into gnpde.odeint unchanged."""
+    returns f_local [nbmax, C]; it drops into gnpde.odeint unchanged.
+
+    On a large graph (ops.LAYOUT_MIN_ROWS, ops.NODE_ORDER 'degree') the rows are
+    those of the graph's in-degree numbering (ops.NodeLayout, as the unsharded and
+    column-striped solves): scatter() / unpad() map from / to the caller's numbering,
+    and x0_local must come from scatter(x0)."""
 
     graph_capturable = False  # an RCCL all-gather per RHS: the integrator runs it eagerly
     fused_adaptive = False    # the adaptive solvers' wide stages run in column stripes or unsharded
 
     def __init__(self, edge_index, edge_weight, num_nodes, alpha, beta=None, x0_local=None, add_source=False,
                  alpha_sigmoid=True, group=None, local_rhs=None, chunk=ops.DEFAULT_CHUNK, row_weight=0.0,
-                 local_stage=None):
+                 local_stage=None, node_order=None):
         self.group = group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
@@ -182,8 +187,15 @@ class RowShardedLaplacian(object):
         # writes the fused stage outputs; host_stages lets the integrator's fused path run it
         self.local_stage = local_stage
         self.host_stages = local_stage is not None
+        self.lay = None
         if local_rhs is None and local_stage is None:
             self.g = ops.GraphCSR(edge_index, self.N, chunk=chunk)
+            order = ops.NODE_ORDER if node_order is None else node_order
+            if order == "degree" and self.R >= ops.LAYOUT_MIN_ROWS:
+                # the rows of the in-degree numbering: hot gathered rows together (G-rmat rk4
+                # 232 -> 281 RHS/s unsharded); COO-order weights apply unchanged
+                self.lay = self.g.node_layout
+                self.g = self.lay.graph
             self.w = self.g.gather_weights(edge_weight)
             self.part = RowPartition(self.g, self.world, self.rank, row_weight=row_weight, chunk=chunk)
             self.blocks, self.nb = self.part.blocks, self.part.nbmax
@@ -245,14 +257,17 @@ class RowShardedLaplacian(object):
                       alpha_sigmoid=self.alpha_sigmoid, add_source=self.add_source, stage=stage)
 
     def scatter(self, y):
-        """Full state [R, C] -> this rank's zero-padded block [nb, C]."""
+        """Full state [R, C] (the caller's numbering) -> this rank's zero-padded block [nb, C]."""
+        if self.lay is not None:
+            y = self.lay.to_internal(y.reshape(-1, y.shape[-1]))
         out = torch.zeros((self.nb,) + tuple(y.shape[1:]), dtype=y.dtype, device=y.device)
         out[:self.r1 - self.r0] = y[self.r0:self.r1]
         return out
 
     def unpad(self, y_full):
-        """Gathered padded blocks [world*nb, C] -> full state [R, C] in row order."""
-        return torch.cat([y_full[p * self.nb:p * self.nb + (b - a)] for p, (a, b) in enumerate(self.blocks)], 0)
+        """Gathered padded blocks [world*nb, C] -> full state [R, C] in the caller's numbering."""
+        y = torch.cat([y_full[p * self.nb:p * self.nb + (b - a)] for p, (a, b) in enumerate(self.blocks)], 0)
+        return self.lay.to_user(y) if self.lay is not None else y
 
 
 def _local_plan(csr, r0, r1, chunk, pos0=None):

@@ -1209,7 +1209,8 @@ class _RKAdaptiveFused(_RKAdaptive):
         """The module's cached buffers / graphs for this shape, tolerance and graph
         state (a new entry when any of them changed)."""
         P = self.plan
-        if self.host or not ADAPTIVE_GRAPH or not getattr(self.func, 'graph_capturable', True):
+        if self.host or not ADAPTIVE_GRAPH or not getattr(self.func, 'graph_capturable', True) or \
+                'norm' in self.options:  # a sharded RHS's global norm: a collective inside the step
             return _AdaptiveState(P, y0, self.host), False
         state = _capture_state(self.func, y0)
         key = _graph_cache_key(self.func, 'adaptive:' + P.method, y0, state)

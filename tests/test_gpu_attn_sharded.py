@@ -193,3 +193,36 @@ def test_sharded_classes_two_ranks_one_gpu(cls, mode, norm_idx):
     res = sorted(q.get(timeout=120) for _ in range(2))
     for rank, err in res:
         assert err <= 1e-6, (rank, err)
+
+
+def test_row_sharded_laplacian_world_one_in_degree_numbering(tmp_path):
+    """The row partition in the graph's in-degree numbering at a
+    world of one (gloo, in-process): the integrator's state blocks are the gathered
+    buffers themselves (in-place all-gather), the solve equals the unsharded one."""
+    import torch.distributed as dist
+    import gnpde
+    init = not dist.is_initialized()
+    if init:
+        dist.init_process_group("gloo", init_method="file://%s" % (tmp_path / "pg"), rank=0, world_size=1)
+    try:
+        n, e, c = 40000, 300000, 64
+        ei, w = synthetic.rw_graph(n, e, seed=12, device=DEV)
+        x = synthetic.features(1, n, c, seed=13, device=DEV)
+        a = torch.tensor(0.3, device=DEV)
+        opt = {'block': 'constant', 'function': 'laplacian', 'add_source': False, 'no_alpha_sigmoid': False,
+               'max_nfe': 10 ** 9, 'multi_modal': False, 'hidden_dim': c}
+        func = gnpde.LaplacianODEFunc(c, c, opt, DEV).to(DEV)
+        func.edge_index, func.edge_weight = ei, w
+        with torch.no_grad():
+            func.alpha_train.fill_(0.3)
+            t = torch.tensor([0.0, 1.0], device=DEV)
+            want = gnpde.odeint(func, x, t, method='rk4', options={'step_size': 0.25})[1]
+            sh = gd.RowShardedLaplacian(ei, w, n, a)
+            assert sh.lay is not None  # the in-degree numbering
+            y = gnpde.odeint(sh, sh.scatter(x), t, method='rk4', options={'step_size': 0.25})[1]
+            got = sh.unpad(sh.gather(y)).view(want.shape)
+        assert len(sh._full) >= 2  # the solve's states were gathered in place
+        assert rel(got, want) <= 1e-6
+    finally:
+        if init:
+            dist.destroy_process_group()
