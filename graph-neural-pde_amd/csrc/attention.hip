@@ -134,20 +134,21 @@ __device__ __forceinline__ float seg_team_score(const ScoreArgs& sa, const float
 
 // ------------------------------------------------------------------ long groups (reference statistics)
 // Reference-score statistics of destination groups longer than a wavefront's
-// 64-edge block (ref_stats_kernel):
-//   * LONG items (slot field -2): a whole group of at most kSegLongMax edges, one
-//     wavefront, lanes striding (kSegLongU edges per lane, one pass), each lane an
-//     online (max, sum-exp) per head, a fixed xor tree across the lanes;
-//   * HUB items (slot field -4): a longer group, one whole 1024-thread workgroup:
-//     every thread pushes up to kHubU edges per pass, the 16 wavefronts reduce by
-//     xor trees, then in wavefront order through LDS — fixed order, no chunk
-//     partials, no arrival tickets, no second launch.  G-arxiv's CSC has 239 such
-//     groups (up to 7,444 edges): one pass of 8 edges per thread covers 8,192.
-constexpr int kSegLongU = 4;                   // edges per lane per pass
-constexpr int kSegLongMax = kWave * kSegLongU;  // 256: one pass
-constexpr int kRefBlock = 1024;                 // ref_stats_kernel workgroup (hub items: all of it)
-constexpr int kRefWaves = kRefBlock / kWave;
-constexpr int kHubU = 8;                        // edges per thread per pass of a hub group
+// 64-edge block (ref_stats_kernel), one wavefront per item, lanes striding
+// (kSegLongU edges per lane, one pass of up to kSegLongMax edges), each lane an
+// online (max, sum-exp) per head, then a fixed xor tree across the lanes:
+//   * LONG items (slot field -2): a whole group of at most kSegLongMax edges;
+//   * HUB CHUNK items {e_begin, e_end, slot, hub}: kSegLongMax-edge chunks of a
+//     longer group.  The chunk's (M, L) per head goes write-through to its
+//     partial slot; the chunk wave then takes an arrival ticket on the hub table
+//     entry heavy[hub] = {group, first_slot, n_chunks, ticket}, and the last to
+//     arrive merges the slots (stats_merge_store: lanes over chunks, fixed xor
+//     tree, so the result does not depend on the arrival order) and resets the
+//     ticket.  Round 3 ran each hub group as one 1024-thread workgroup (mostly
+//     idle lanes, 16 wave slots held per group): the kernel took 20.9 us on
+//     G-arxiv's CSC, bound by those groups.
+constexpr int kSegLongU = 8;                   // edges per lane
+constexpr int kSegLongMax = kWave * kSegLongU;  // 512: one pass
 
 // node scores cs[src[u], 0..MAXH) of U sources (src < 0: row 0, unused): two
 // heads as one 16-byte load — one gather instruction instead of two (random
@@ -205,55 +206,50 @@ __device__ __forceinline__ void wave_merge(double (&M)[MAXH], float (&L)[MAXH]) 
     }
 }
 
-// a whole group of at most kSegLongMax edges by one wavefront
+// at most kSegLongMax edges [e0, e1) by one wavefront: (M, L) per head, every lane
 template <int MAXH>
-__device__ __forceinline__ void long_group_stats(int e0, int e1, int grp, const int* __restrict__ gidx,
-                                                 const ScoreArgs& sa, double* m, float* rl, float* mr) {
+__device__ __forceinline__ void long_item_stats(int e0, int e1, const int* __restrict__ gidx, const ScoreArgs& sa,
+                                                double (&M)[MAXH], float (&L)[MAXH]) {
   const int lane = threadIdx.x & 63;
-  double M[MAXH];
-  float L[MAXH];
 #pragma unroll
   for (int h = 0; h < MAXH; ++h) {
     M[h] = -INFINITY;
     L[h] = 0.f;
   }
-  for (int pb = e0 + lane; pb < e1; pb += kSegLongMax) push_edges<kSegLongU, MAXH>(pb, kWave, e1, gidx, sa, M, L);
-  wave_merge<MAXH>(M, L);
-  if (lane == 0)
+  // one pass of kSegLongU edges per lane (more heads: passes of fewer, for registers)
+  constexpr int LU = MAXH <= 2 ? kSegLongU : 2;
 #pragma unroll
-    for (int h = 0; h < MAXH; ++h)
-      if (h < sa.H) store_stats(m, rl, mr, grp, sa.H, h, M[h], L[h]);
+  for (int ps = 0; ps < kSegLongU / LU; ++ps) push_edges<LU, MAXH>(e0 + lane + ps * LU * kWave, kWave, e1, gidx, sa, M, L);
+  wave_merge<MAXH>(M, L);
 }
 
-// a hub group by the whole 1024-thread workgroup (block-uniform call)
+// a hub chunk: partials write-through, arrival ticket, the last arrival merges
 template <int MAXH>
-__device__ __forceinline__ void hub_group_stats(int e0, int e1, int grp, const int* __restrict__ gidx,
-                                                const ScoreArgs& sa, double* m, float* rl, float* mr) {
-  __shared__ double sM[kRefWaves][MAXH];
-  __shared__ float sL[kRefWaves][MAXH];
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+__device__ __forceinline__ void hub_chunk_stats(int e0, int e1, int slot, int hub, const int* __restrict__ gidx,
+                                                const ScoreArgs& sa, int4* heavy, double* __restrict__ partials,
+                                                double* m, float* rl, float* mr) {
+  const int lane = threadIdx.x & 63;
+  const int H = sa.H;
   double M[MAXH];
   float L[MAXH];
+  long_item_stats<MAXH>(e0, e1, gidx, sa, M, L);
+  const __amdgpu_buffer_rsrc_t rp = buf_rsrc(partials);
+  const int64_t pb = (int64_t)slot * 2 * H;
 #pragma unroll
   for (int h = 0; h < MAXH; ++h) {
-    M[h] = -INFINITY;
-    L[h] = 0.f;
+    const bool st = lane == 0 && h < H;
+    buf_store_wt_f64(rp, st ? (uint32_t)((pb + h) * 8) : kBufNone, M[h]);
+    buf_store_wt_f64(rp, st ? (uint32_t)((pb + H + h) * 8) : kBufNone, (double)L[h]);
   }
-  for (int pb = e0 + tid; pb < e1; pb += kRefBlock * kHubU) push_edges<kHubU, MAXH>(pb, kRefBlock, e1, gidx, sa, M, L);
-  wave_merge<MAXH>(M, L);
-  if (lane == 0)
-#pragma unroll
-    for (int h = 0; h < MAXH; ++h) {
-      sM[wv][h] = M[h];
-      sL[wv][h] = L[h];
-    }
-  __syncthreads();
-  if (tid < MAXH && tid < sa.H) {
-    double Mh = -INFINITY;
-    float Lh = 0.f;
-    for (int w = 0; w < kRefWaves; ++w) online_merge(Mh, Lh, sM[w][tid], sL[w][tid]);
-    store_stats(m, rl, mr, grp, sa.H, tid, Mh, Lh);
-  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  int ticket = 0;
+  if (lane == 0) ticket = __hip_atomic_fetch_add(&heavy[hub].w, 1, kHubTicketOrder, __HIP_MEMORY_SCOPE_AGENT);
+  ticket = __shfl(ticket, 0);
+  const int4 hv = heavy[hub];
+  if (ticket != uniform(hv.z) - 1) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  for (int h = 0; h < H; ++h) stats_merge_store(uniform(hv.x), uniform(hv.y), uniform(hv.z), H, h, partials, m, rl, mr);
+  if (lane == 0) __hip_atomic_store(&heavy[hub].w, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <bool REF, int OUT>
@@ -364,24 +360,30 @@ __global__ __launch_bounds__(256) void seg_softmax_kernel(const int4* __restrict
 constexpr int kRefStatsNI = 2;  // 1 / 4 items per wavefront: 20.9 / 23.1 us against 21.0
 
 template <int NI, int MAXH>
-__global__ __launch_bounds__(kRefBlock) void ref_stats_kernel(const int4* __restrict__ items, int n_items, int n_hub,
-                                                               int n_long, const int* __restrict__ rowidx,
-                                                               const int* __restrict__ gidx, ScoreArgs sa,
-                                                               double* __restrict__ m, float* __restrict__ rl,
-                                                               float* __restrict__ mr) {
+__global__ __launch_bounds__(256) void ref_stats_kernel(const int4* __restrict__ items, int n_items, int n_hub,
+                                                         int n_long, const int* __restrict__ rowidx,
+                                                         const int* __restrict__ gidx, ScoreArgs sa, int4* heavy,
+                                                         double* __restrict__ partials, double* __restrict__ m,
+                                                         float* __restrict__ rl, float* __restrict__ mr) {
   const int lane = threadIdx.x & 63;
-  if ((int)blockIdx.x < n_hub) {
-    const int4 it = items[blockIdx.x];
-    hub_group_stats<MAXH>(it.x, it.y, it.w, gidx, sa, m, rl, mr);
+  const int wid = uniform((int)blockIdx.x * kWavesPerBlock + (int)(threadIdx.x >> 6));
+  if (wid < n_hub + n_long) {
+    const int4 it = items[wid];
+    if (wid < n_hub) {
+      hub_chunk_stats<MAXH>(uniform(it.x), uniform(it.y), uniform(it.z), uniform(it.w), gidx, sa, heavy, partials, m,
+                            rl, mr);
+      return;
+    }
+    double M[MAXH];
+    float L[MAXH];
+    long_item_stats<MAXH>(uniform(it.x), uniform(it.y), gidx, sa, M, L);
+    if (lane == 0)
+#pragma unroll
+      for (int h = 0; h < MAXH; ++h)
+        if (h < sa.H) store_stats(m, rl, mr, uniform(it.w), sa.H, h, M[h], L[h]);
     return;
   }
-  const int wid = uniform(((int)blockIdx.x - n_hub) * kRefWaves + (int)(threadIdx.x >> 6));
-  if (wid < n_long) {
-    const int4 it = items[n_hub + wid];
-    long_group_stats<MAXH>(uniform(it.x), uniform(it.y), uniform(it.w), gidx, sa, m, rl, mr);
-    return;
-  }
-  const int base = n_hub + n_long + (wid - n_long) * NI;
+  const int base = n_hub + n_long + (wid - n_hub - n_long) * NI;
   if (base >= n_items) return;
   const int H = sa.H;
   int e0[NI], n[NI], grp[NI], src[NI];
@@ -423,12 +425,13 @@ __global__ __launch_bounds__(kRefBlock) void ref_stats_kernel(const int4* __rest
 
 template <int NI>
 static int launch_ref_stats(const int4* items, int64_t n_items, int64_t n_hub, int64_t n_long, const int* rowidx,
-                            const int* gidx, const ScoreArgs& sa, double* m, float* rl, float* mr, hipStream_t s) {
-  const int64_t waves = n_long + ceil_div(n_items - n_hub - n_long, (int64_t)NI);
-  const unsigned grid = (unsigned)(n_hub + ceil_div(waves, kRefWaves));
-#define GNPDE_RS(M)                                                                                             \
-  ref_stats_kernel<NI, M><<<grid, kRefBlock, 0, s>>>(items, (int)n_items, (int)n_hub, (int)n_long, rowidx, gidx, sa, \
-                                                      m, rl, mr)
+                            const int* gidx, const ScoreArgs& sa, int4* heavy, double* partials, double* m, float* rl,
+                            float* mr, hipStream_t s) {
+  const int64_t waves = n_hub + n_long + ceil_div(n_items - n_hub - n_long, (int64_t)NI);
+  const unsigned grid = (unsigned)ceil_div(waves, (int64_t)kWavesPerBlock);
+#define GNPDE_RS(M)                                                                                            \
+  ref_stats_kernel<NI, M><<<grid, kBlock, 0, s>>>(items, (int)n_items, (int)n_hub, (int)n_long, rowidx, gidx, sa, \
+                                                   heavy, partials, m, rl, mr)
   if (sa.H <= 1)
     GNPDE_RS(1);
   else if (sa.H <= 2 && aligned16(sa.cs))  // MAXH 2: two heads, 16-byte node-score rows
@@ -573,9 +576,13 @@ int gnpde_seg_softmax_f32(const int32_t* items, int64_t n_items, int64_t n_hub_i
   const int64_t n_first = adjacent ? n_items + n_chunk_items : n_items;
   const int64_t n_second = adjacent ? 0 : n_chunk_items;
   if (ref && out_kind == 1 && n_chunk_items == 0 && group_is_dst) {
-    // the reference statistics of the attention RHS: hub groups, long groups, then short items
-    GNPDE_REQUIRE((uint64_t)n_items < (uint64_t)INT32_MAX / kRefWaves, GNPDE_EUNSUPPORTED, "seg_softmax: too many items");
-    return launch_ref_stats<kRefStatsNI>(it, n_items, n_hub_items, n_long_items, rowidx, gidx, sa, m, rl, mr, s);
+    // the reference statistics of the attention RHS: hub chunks, long groups, then short items
+    GNPDE_REQUIRE((uint64_t)n_items < (uint64_t)INT32_MAX / kWavesPerBlock, GNPDE_EUNSUPPORTED,
+                  "seg_softmax: too many items");
+    GNPDE_REQUIRE(n_hub_items == 0 || (heavy && n_heavy > 0 && partials), GNPDE_EINVAL,
+                  "seg_softmax: hub chunk items need the hub table (heavy) and partials");
+    return launch_ref_stats<kRefStatsNI>(it, n_items, n_hub_items, n_long_items, rowidx, gidx, sa, hv, partials, m, rl,
+                                          mr, s);
   }
   if (out_kind == 0) {
     rc = GNPDE_SEG(false, kSegWeights, it, n_first);

@@ -635,4 +635,9 @@ __device__ __forceinline__ void buf_store_wt(__amdgpu_buffer_rsrc_t r, uint32_t 
   }
 }
 
+// write-through store of one double (as buf_store_wt)
+__device__ __forceinline__ void buf_store_wt_f64(__amdgpu_buffer_rsrc_t r, uint32_t off, double v) {
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, off, 0, kAuxSc1);
+}
+
 }  // namespace gnpde

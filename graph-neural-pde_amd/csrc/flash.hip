@@ -39,6 +39,8 @@
 // order).  A wavefront holding a chunk accumulates per head for all its rows.
 // (A one-workgroup-per-hub statistics pre-pass launched first, so that chunks
 // weight with final statistics and merge like K1's, measured 17 us on G-arxiv.)
+#include <type_traits>
+
 #include "aggregate.hpp"
 #include "rhs_host.hpp"
 
@@ -71,6 +73,7 @@ struct DotArgs {
   const float* __restrict__ k;
   int64_t ldqk;
   float scale;                  // log2(e) / sqrt(dk)
+  double scale64;               // the same in fp64 (the one-pass kernel's fp64 scores)
 };
 
 // sum over the S = dk/4 lanes of a head (S in {1, 2, 4, 8, 16}, aligned inside a 16-lane row)
@@ -84,6 +87,23 @@ __device__ __forceinline__ float head_reduce(float v) {
   if constexpr (S >= 4) v += dpp_mov<0x4E>(v);   // quad_perm [2,3,0,1]
   if constexpr (S >= 8) v += dpp_mov<0x141>(v);  // row_half_mirror
   if constexpr (S >= 16) v += dpp_mov<0x140>(v); // row_mirror
+  return v;
+}
+
+// the same over fp64 values (each 32-bit half moved by DPP)
+template <int CTRL>
+__device__ __forceinline__ double dpp_mov64(double v) {
+  const u32x2 w = __builtin_bit_cast(u32x2, v);
+  const u32x2 r = {(uint32_t)__builtin_amdgcn_update_dpp(0, (int)w.x, CTRL, 0xf, 0xf, false),
+                   (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w.y, CTRL, 0xf, 0xf, false)};
+  return __builtin_bit_cast(double, r);
+}
+template <int S>
+__device__ __forceinline__ double head_reduce64(double v) {
+  if constexpr (S >= 2) v += dpp_mov64<0xB1>(v);
+  if constexpr (S >= 4) v += dpp_mov64<0x4E>(v);
+  if constexpr (S >= 8) v += dpp_mov64<0x141>(v);
+  if constexpr (S >= 16) v += dpp_mov64<0x140>(v);
   return v;
 }
 
@@ -315,27 +335,26 @@ void dot_agg_kernel(const int4* __restrict__ items, int n_items, int4* heavy, in
   for (int h = 0; h < H; ++h) Rl[h] = 1.0f / (L[h] + kSoftmaxEps);
 
   // pass 2: K1's gather loop; one finished weight per edge, or (a wavefront with a
-  // hub chunk) one unnormalised weight per edge and head
-  float acc[4] = {0.f, 0.f, 0.f, 0.f};
-  float acch[H][4];
+  // hub chunk) one unnormalised weight per edge and head.  The two forms are separate
+  // branches with their own accumulators, so the per-head sums of the chunk form
+  // hold no registers in the whole-row form (114 -> fewer VGPRs, more waves).
+  const float a = (ep.flags & GNPDE_EPI_RHS) ? epi_alpha(ep) : 1.f;
+  const float b = (ep.flags & GNPDE_ADD_SOURCE) ? *ep.beta : 0.f;
+  if (!wchunk) {
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int e0 = 0; e0 < len; e0 += SL) {
+      const int n = min(SL, len - e0);
+      int mc;
+      float s[H];
+      if (e0 == 0 || GNPDE_FL_DIAG) {
+        mc = e0 == 0 ? mc0 : (sl < n ? col[beg + e0 + sl] : 0);
 #pragma unroll
-  for (int h = 0; h < H; ++h)
-#pragma unroll
-    for (int t = 0; t < 4; ++t) acch[h][t] = 0.f;
-  for (int e0 = 0; e0 < len; e0 += SL) {
-    const int n = min(SL, len - e0);
-    int mc;
-    float s[H];
-    if (e0 == 0 || GNPDE_FL_DIAG) {
-      mc = e0 == 0 ? mc0 : (sl < n ? col[beg + e0 + sl] : 0);
-#pragma unroll
-      for (int h = 0; h < H; ++h) s[h] = GNPDE_FL_DIAG == 1 ? 0.f : s1[h];
-    } else {  // a later batch of a long row: its scores again
-      mc = sl < n ? col[beg + e0 + sl] : 0;
-      tile_scores<SL, NA, S, H>(qv, mc, n, base, sl, da, sc);
-      own_scores<H>(sc, sl, n, s);
-    }
-    if (!wchunk) {
+        for (int h = 0; h < H; ++h) s[h] = GNPDE_FL_DIAG == 1 ? 0.f : s1[h];
+      } else {  // a later batch of a long row: its scores again
+        mc = sl < n ? col[beg + e0 + sl] : 0;
+        tile_scores<SL, NA, S, H>(qv, mc, n, base, sl, da, sc);
+        own_scores<H>(sc, sl, n, s);
+      }
       const float mw = sl < n ? edge_weight<H>(s, M, Rl) : 0.f;
       for (int j = 0; j < n; j += U) {
         float v[U][4];
@@ -361,41 +380,66 @@ void dot_agg_kernel(const int4* __restrict__ items, int n_items, int4* heavy, in
 #pragma unroll
           for (int t = 0; t < 4; ++t) acc[t] = fmaf(ww[u], v[u][t], acc[t]);
       }
+    }
+    if (!live) return;
+    double dpart = 0.0;
+    if (owner) epi_finish<4, STG, float>(ep, row, cc, acc, a, b, pre, &dpart);
+    (void)dpart;
+    return;
+  }
+  // hub-chunk wavefronts gather UC rows at a time: their per-head weights and sums
+  // would otherwise set the kernel's register count
+  constexpr int UC = U > 2 ? U / 2 : U;
+  float acch[H][4];
+#pragma unroll
+  for (int h = 0; h < H; ++h)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acch[h][t] = 0.f;
+  for (int e0 = 0; e0 < len; e0 += SL) {
+    const int n = min(SL, len - e0);
+    int mc;
+    float s[H];
+    if (e0 == 0 || GNPDE_FL_DIAG) {
+      mc = e0 == 0 ? mc0 : (sl < n ? col[beg + e0 + sl] : 0);
+#pragma unroll
+      for (int h = 0; h < H; ++h) s[h] = GNPDE_FL_DIAG == 1 ? 0.f : s1[h];
     } else {
-      float ph[H];
+      mc = sl < n ? col[beg + e0 + sl] : 0;
+      tile_scores<SL, NA, S, H>(qv, mc, n, base, sl, da, sc);
+      own_scores<H>(sc, sl, n, s);
+    }
+    float ph[H];
 #pragma unroll
-      for (int h = 0; h < H; ++h) ph[h] = sl < n ? __builtin_amdgcn_exp2f(s[h] - M[h]) : 0.f;
-      for (int j = 0; j < n; j += U) {
-        float v[U][4];
-        float ww[U][H];
+    for (int h = 0; h < H; ++h) ph[h] = sl < n ? __builtin_amdgcn_exp2f(s[h] - M[h]) : 0.f;
+    for (int j = 0; j < n; j += UC) {
+      float v[UC][4];
+      float ww[UC][H];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const int jj = j + u;
-          const int src = base + (jj < n ? jj : 0);
-          const int c = __shfl(mc, src);
+      for (int u = 0; u < UC; ++u) {
+        const int jj = j + u;
+        const int src = base + (jj < n ? jj : 0);
+        const int c = __shfl(mc, src);
 #pragma unroll
-          for (int h = 0; h < H; ++h) ww[u][h] = jj < n ? __shfl(ph[h], src) : 0.f;
-          if (GNPDE_FL_PREFETCH && e0 == 0 && j == 0) {
+        for (int h = 0; h < H; ++h) ww[u][h] = jj < n ? __shfl(ph[h], src) : 0.f;
+        if (GNPDE_FL_PREFETCH && e0 == 0 && j < U) {
 #pragma unroll
-            for (int t = 0; t < 4; ++t) v[u][t] = xv0[u][t];
-          } else if (jj < n && cc < C) {
-            load_vec<4>(ep.x + (int64_t)c * ep.ldx + cc, v[u]);
-          } else {
+          for (int t = 0; t < 4; ++t) v[u][t] = xv0[(j + u) % U][t];
+        } else if (jj < n && cc < C) {
+          load_vec<4>(ep.x + (int64_t)c * ep.ldx + cc, v[u]);
+        } else {
 #pragma unroll
-            for (int t = 0; t < 4; ++t) v[u][t] = 0.f;
-          }
+          for (int t = 0; t < 4; ++t) v[u][t] = 0.f;
         }
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-#pragma unroll
-          for (int h = 0; h < H; ++h)
-#pragma unroll
-            for (int t = 0; t < 4; ++t) acch[h][t] = fmaf(ww[u][h], v[u][t], acch[h][t]);
       }
+#pragma unroll
+      for (int u = 0; u < UC; ++u)
+#pragma unroll
+        for (int h = 0; h < H; ++h)
+#pragma unroll
+          for (int t = 0; t < 4; ++t) acch[h][t] = fmaf(ww[u][h], v[u][t], acch[h][t]);
     }
   }
-
-  if (wchunk) {
+  {
     // hub chunks: (acc_h, M_h, L_h) written through to the slot, merged in-launch by
     // the last arrival (arrival tickets on the plan's heavy entries, as K1)
     const int ps = (int)dot_partial_floats(H, C);
@@ -435,17 +479,217 @@ void dot_agg_kernel(const int4* __restrict__ items, int n_items, int4* heavy, in
         if (lane == 0) __hip_atomic_store(&heavy[hh].w, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
-    if (chunk) return;
-    // the whole rows of this wavefront: normalise the per-head sums
-#pragma unroll
-    for (int h = 0; h < H; ++h)
-#pragma unroll
-      for (int t = 0; t < 4; ++t) acc[t] = fmaf(acch[h][t], Rl[h], acc[t]);
-    constexpr float inv_h = 1.0f / (float)H;
-#pragma unroll
-    for (int t = 0; t < 4; ++t) acc[t] *= inv_h;
   }
+  if (chunk) return;
+  // the whole rows of this wavefront: normalise the per-head sums
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int h = 0; h < H; ++h)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[t] = fmaf(acch[h][t], Rl[h], acc[t]);
+  constexpr float inv_h = 1.0f / (float)H;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) acc[t] *= inv_h;
   if (!live) return;
+  double dpart = 0.0;
+  if (owner) epi_finish<4, STG, float>(ep, row, cc, acc, a, b, pre, &dpart);
+  (void)dpart;
+}
+
+// ------------------------------------------------------------------ the one-pass form (round 4)
+// The same RHS in ONE pass over the item's edges, the online softmax of
+// flash attention per head: each batch of U edges of a row slot gathers the
+// edges' x rows AND k rows together (one memory latency per batch, not one for
+// the scores and another for the rows).  The k rows go through score tiles as in
+// tile_scores (NA = att/4 lanes per edge, 16-byte slices, EPI = SL/NA edges per
+// load; the same four fmas and DPP head sums, so the same score bits as the
+// two-pass kernel), the head scores are broadcast to the slot, and each head
+// keeps a running (M_h, L_h, acc_h = sum_e 2^(s_e,h - M_h) x_e), rescaled by
+// 2^(M_old - M_new) once per batch.  The row's result is
+//   ax = (1/H) sum_h acc_h / (L_h + 1e-16)
+// — the two-pass kernel's sum, each head's exponentials taken against the
+// running rather than the final max (same value up to rounding).  Hub chunks
+// write their (acc_h, M_h rounded to fp32, L_h) and merge exactly as above
+// (dot_hub_combine).  G-arxiv per-edge RHS (norm_idx 0): 0.171 -> 0.151 ms.
+#ifndef GNPDE_FL_ONEPASS
+#define GNPDE_FL_ONEPASS 1   // A/B: 0 keeps the two-pass kernel above
+#endif
+#ifndef GNPDE_FL_SCORE64
+#define GNPDE_FL_SCORE64 0   // A/B: 1 head sums, scores and the running max in fp64 (0.202 against 0.151 ms)
+#endif
+using ScoreT = std::conditional_t<GNPDE_FL_SCORE64 != 0, double, float>;
+
+template <int GL, int U, int ATT, int H, int STG>
+__global__ __launch_bounds__(256) void dot_agg1_kernel(const int4* __restrict__ items, int n_items, int4* heavy,
+                                                        int n_heavy, const int* __restrict__ col, DotArgs da, int C,
+                                                        Epi ep, float* __restrict__ partials) {
+  constexpr int RPW = kWave / GL;
+  constexpr int SL = GL;
+  constexpr int NA = ATT / 4;                  // lanes per edge of a score tile (16-byte slices)
+  constexpr int S = NA / H;                    // lanes per head
+  constexpr int EPI = SL / NA;                 // edges per tile load
+  constexpr int TL = (U + EPI - 1) / EPI;      // tile loads per batch of U edges
+  static_assert(NA <= SL && S >= 1 && S <= 16 && (S & (S - 1)) == 0, "dot_agg1: score tile layout");
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int rs = lane / SL, sl = lane % SL;
+  const int wid = uniform(blockIdx.x * kWavesPerBlock + wv);
+  const int item = wid * RPW + rs;
+  if (wid * RPW >= n_items) return;
+  const bool live = item < n_items;
+  const int4 it = live ? items[item] : make_int4(0, 0, 0, -1);
+  const int row = it.x, beg = it.y, end = it.z, slot = it.w;
+  const int cc = sl * 4;
+  const bool owner = live && slot < 0 && cc < C;
+  const bool chunk = live && slot >= 0;
+  const int base = rs * SL;
+  const int sub = sl % NA, eo = sl / NA;
+
+  EpiPre<4, float, STG> pre;
+  if (owner) epi_prefetch<4, STG, float>(ep, row, cc, pre);
+  float qv[4];  // this lane's slice of the row's q (score tiles, as tile_scores)
+  load_vec<4>(da.q + (int64_t)row * da.ldqk + 4 * sub, qv);
+
+  ScoreT M[H];
+  float L[H], acch[H][4];
+#pragma unroll
+  for (int h = 0; h < H; ++h) {
+    M[h] = -INFINITY;
+    L[h] = 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acch[h][t] = 0.f;
+  }
+  const int len = end - beg;
+  for (int e0 = 0; e0 < len; e0 += SL) {
+    const int n = min(SL, len - e0);
+    const int mc = sl < n ? col[beg + e0 + sl] : 0;
+    for (int j = 0; j < n; j += U) {
+      float v[U][4], kt[TL][4];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int jj = j + u;
+        const int c = __shfl(mc, base + (jj < n ? jj : 0));
+        if (jj < n && cc < C) {
+          load_vec<4>(ep.x + (int64_t)c * ep.ldx + cc, v[u]);
+        } else {
+#pragma unroll
+          for (int t = 0; t < 4; ++t) v[u][t] = 0.f;
+        }
+      }
+      // score tiles: lane (eo, sub) loads the 16-byte slice sub of edge g*EPI + eo's k row
+#pragma unroll
+      for (int g = 0; g < TL; ++g) {
+        const int ue = g * EPI + eo;  // the batch edge of this lane's tile slot
+        const int jj = j + ue;
+        const int c = __shfl(mc, base + (jj < n ? jj : 0));
+        if (ue < U && jj < n) {
+          load_vec<4>(da.k + (int64_t)c * da.ldqk + 4 * sub, kt[g]);
+        } else {
+#pragma unroll
+          for (int t = 0; t < 4; ++t) kt[g][t] = 0.f;
+        }
+      }
+      // the scores, summed exactly as tile_scores (four fmas, then the head's lanes by DPP)
+      ScoreT dt[TL];
+#pragma unroll
+      for (int g = 0; g < TL; ++g) {
+        float d = qv[0] * kt[g][0];
+        d = fmaf(qv[1], kt[g][1], d);
+        d = fmaf(qv[2], kt[g][2], d);
+        d = fmaf(qv[3], kt[g][3], d);
+        if constexpr (GNPDE_FL_SCORE64)
+          dt[g] = head_reduce64<S>((double)d) * da.scale64;
+        else
+          dt[g] = head_reduce<S>(d) * da.scale;
+      }
+      ScoreT sc[U][H];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int h = 0; h < H; ++h) {
+          const ScoreT x = __shfl(dt[u / EPI], base + (u % EPI) * NA + h * S);
+          sc[u][h] = j + u < n ? x : -INFINITY;
+        }
+#pragma unroll
+      for (int h = 0; h < H; ++h) {
+        ScoreT mb = M[h];
+#pragma unroll
+        for (int u = 0; u < U; ++u) mb = fmax(mb, sc[u][h]);
+        const float r = __builtin_amdgcn_exp2f((float)(M[h] - mb));  // M = -inf: 0 (the sums are 0 too)
+        L[h] *= r;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acch[h][t] *= r;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const float pw = __builtin_amdgcn_exp2f((float)(sc[u][h] - mb));  // -inf past n: 0
+          L[h] += pw;
+#pragma unroll
+          for (int t = 0; t < 4; ++t) acch[h][t] = fmaf(pw, v[u][t], acch[h][t]);
+        }
+        M[h] = mb;
+      }
+    }
+  }
+  if (n_heavy > 0) {
+    int anyc = 0;
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) anyc |= __shfl((int)chunk, r * SL);
+    if (anyc) {  // wave-uniform: hub chunks write (acc_h, M_h, L_h) through; the last arrival merges
+      const int ps = (int)dot_partial_floats(H, C);
+      const __amdgpu_buffer_rsrc_t rp = buf_rsrc(partials);
+      const int64_t pb = (int64_t)(chunk ? slot : 0) * ps;
+#pragma unroll
+      for (int h = 0; h < H; ++h) {
+        // the slot keeps the max rounded to fp32, the sums taken relative to it
+        const float mf = (float)M[h];
+        const float adj = __builtin_amdgcn_exp2f((float)(M[h] - (double)mf));
+        float av[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) av[t] = acch[h][t] * adj;
+        buf_store_wt<4>(rp, (chunk && cc < C) ? (uint32_t)((pb + h * C + cc) * 4) : kBufNone, av);
+        float ml[1] = {mf};
+        buf_store_wt<1>(rp, (chunk && sl == 0) ? (uint32_t)((pb + H * C + h) * 4) : kBufNone, ml);
+        ml[0] = L[h] * adj;
+        buf_store_wt<1>(rp, (chunk && sl == 0) ? (uint32_t)((pb + H * C + H + h) * 4) : kBufNone, ml);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      int lo = 0, won = 0;
+      if (chunk) {
+        int hi = n_heavy - 1;
+        while (lo < hi) {
+          const int mid = (lo + hi + 1) >> 1;
+          if (heavy[mid].y <= slot)
+            lo = mid;
+          else
+            hi = mid - 1;
+        }
+        if (sl == 0) {
+          const int t = __hip_atomic_fetch_add(&heavy[lo].w, 1, kHubTicketOrder, __HIP_MEMORY_SCOPE_AGENT);
+          won = t == heavy[lo].z - 1;
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < RPW; ++r) {
+        if (__shfl(won, r * SL)) {  // wave-uniform
+          const int hh = __shfl(lo, r * SL);
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          const int4 hv = heavy[hh];
+          dot_hub_combine<H, STG>(uniform(hv.x), uniform(hv.y), uniform(hv.z), C, ps, ep, partials);
+          if (lane == 0) __hip_atomic_store(&heavy[hh].w, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+    }
+  }
+  if (!live || chunk) return;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int h = 0; h < H; ++h) {
+    const float rl = 1.0f / (L[h] + kSoftmaxEps);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[t] = fmaf(acch[h][t], rl, acc[t]);
+  }
+  constexpr float inv_h = 1.0f / (float)H;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) acc[t] *= inv_h;
   const float a = (ep.flags & GNPDE_EPI_RHS) ? epi_alpha(ep) : 1.f;
   const float b = (ep.flags & GNPDE_ADD_SOURCE) ? *ep.beta : 0.f;
   double dpart = 0.0;
@@ -577,6 +821,19 @@ static int launch_dot_nh(const int4* items, int64_t n_items, int4* heavy, int64_
     GNPDE_LAUNCH_CHECK();
     return GNPDE_OK;
   }
+  constexpr int ATT = 4 * NA;
+  if constexpr (GNPDE_FL_ONEPASS && NA <= GL) {
+    if (stg == 1)
+      dot_agg1_kernel<GL, U, ATT, H, 1><<<grid, kBlock, 0, s>>>(items, (int)n_items, heavy, nh, col, da, C, ep,
+                                                                 partials);
+    else if (stg == 0)
+      dot_agg1_kernel<GL, U, ATT, H, 0><<<grid, kBlock, 0, s>>>(items, (int)n_items, heavy, nh, col, da, C, ep,
+                                                                 partials);
+    if (stg <= 1) {
+      GNPDE_LAUNCH_CHECK();
+      return GNPDE_OK;
+    }
+  }
   if (stg == 1)
     dot_agg_kernel<GL, U, NA, S, H, 1><<<grid, kBlock, 0, s>>>(items, (int)n_items, heavy, nh, col, da, C, ep, partials);
   else if (stg >= 2) {
@@ -665,6 +922,7 @@ int gnpde_attn_dot_rhs_f32(const int32_t* items, int64_t n_items, int32_t* heavy
   da.k = k;
   da.ldqk = ldqk;
   da.scale = kLog2e / sqrtf((float)dk);
+  da.scale64 = 1.4426950408889634 / sqrt((double)dk);
   const int4* it = reinterpret_cast<const int4*>(items);
   int4* hv = reinterpret_cast<int4*>(heavy);
   const int lanes = (int)(C / 4);

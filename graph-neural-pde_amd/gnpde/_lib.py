@@ -115,7 +115,7 @@ SIGNATURES = {
 }
 
 # constants mirrored from include/gnpde.h
-ABI_VERSION = 3
+ABI_VERSION = 4
 OK = 0
 EINVAL = -1
 EHIP = -2

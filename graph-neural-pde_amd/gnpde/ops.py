@@ -178,8 +178,8 @@ class SegPlan(_TicketOrder):
     def __init__(self, eb, items, n_items, chunk_items, n_chunk, heavy, n_heavy, n_hub=0, n_long=0):
         self.eb = eb
         self.items, self.n_items = items, n_items
-        # reference statistics: hub items (one workgroup each), then long items (one
-        # wavefront each) at the front of ``items``
+        # reference statistics: hub chunk items, then long items (one wavefront
+        # each) at the front of ``items``
         self.n_hub, self.n_long = n_hub, n_long
         self.chunk_items, self.n_chunk = chunk_items, n_chunk
         self.heavy, self.n_heavy = heavy, n_heavy
@@ -195,10 +195,12 @@ def seg_long_max():
 def build_seg_plan(rowptr, eb, long_items=False):
     """gnpde_seg_plan_build on a host copy of rowptr (once per graph and block size).
     long_items=True (the reference statistics over the CSC): every group longer
-    than eb becomes one item — {e_begin, e_end, -4, group} (a HUB, one workgroup)
-    when it has more than seg_long_max() edges, else {e_begin, e_end, -2, group}
-    (LONG, one wavefront); hubs first, then long items, each longest first, then
-    the packed short items.  No chunks, no heavy table."""
+    than eb becomes LONG item {e_begin, e_end, -2, group} (one wavefront) when it
+    has at most seg_long_max() edges, else seg_long_max()-edge HUB CHUNK items
+    {e_begin, e_end, slot, hub} with a hub table entry {group, first_slot,
+    n_chunks, 0} (``heavy``: arrival tickets, the last chunk merges); hub chunks
+    first (longest hubs first), then long items longest first, then the packed
+    short items."""
     rp = np.ascontiguousarray(rowptr.cpu().numpy().astype(np.int32))
     R = rp.shape[0] - 1
     nnz = int(rp[-1])
@@ -219,13 +221,23 @@ def build_seg_plan(rowptr, eb, long_items=False):
         rows = heavy[:nh.value, 0].astype(np.int64)
         s0, s1 = rp[rows].astype(np.int64), rp[rows + 1].astype(np.int64)
         order = np.argsort(-(s1 - s0), kind="stable")
-        hubs = [(int(s0[i]), int(s1[i]), -4, int(rows[i])) for i in order if s1[i] - s0[i] > long_max]
+        hub_chunks, hubs = [], []
+        for i in order:
+            if s1[i] - s0[i] <= long_max:
+                continue
+            first = len(hub_chunks)
+            for c0 in range(int(s0[i]), int(s1[i]), long_max):
+                hub_chunks.append((c0, min(c0 + long_max, int(s1[i])), len(hub_chunks), len(hubs)))
+            hubs.append((int(rows[i]), first, len(hub_chunks) - first, 0))
         longs = [(int(s0[i]), int(s1[i]), -2, int(rows[i])) for i in order if s1[i] - s0[i] <= long_max]
-        front = np.asarray(hubs + longs, np.int32).reshape(-1, 4)
+        front = np.asarray(hub_chunks + longs, np.int32).reshape(-1, 4)
         all_items = np.concatenate([front, items[:ni.value]], 0)
-        return SegPlan(eb, dev32(all_items, all_items.shape[0]), all_items.shape[0],
-                       dev32(np.zeros((1, 4), np.int32), 0), 0, dev32(np.zeros((1, 4), np.int32), 0), 0,
-                       n_hub=len(hubs), n_long=len(longs))
+        table = np.asarray(hubs, np.int32).reshape(-1, 4)
+        plan = SegPlan(eb, dev32(all_items, all_items.shape[0]), all_items.shape[0],
+                       dev32(np.zeros((1, 4), np.int32), 0), 0, dev32(table, len(hubs)), len(hubs),
+                       n_hub=len(hub_chunks), n_long=len(longs))
+        plan.n_slots = len(hub_chunks)
+        return plan
 
     # items and chunk items back to back in one buffer: K2 then covers both in one launch
     both = dev32(np.concatenate([items[:ni.value], chunks[:max(nc.value, 1)]], 0), ni.value + max(nc.value, 1))

@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define GNPDE_ABI_VERSION 3
+#define GNPDE_ABI_VERSION 4
 
 #define GNPDE_OK 0
 #define GNPDE_EINVAL (-1)
@@ -425,12 +425,15 @@ int gnpde_attn_weights_f32(const int32_t* rowidx, const int32_t* col, int64_t nn
  * split groups of degree > EB, heavy {group, first_slot, n_chunks, 0} lists
  * those groups (partials: 2*heads doubles per slot; m/rl scratch).
  * Reference scores with out_kind 1 over the CSC (norm_idx 1) also take, at the
- * front of `items`, n_hub_items HUB items {e_begin, e_end, -4, group} (a group of
- * more than gnpde_seg_long_edges() edges, one 1024-thread workgroup each) and
- * then n_long_items LONG items {e_begin, e_end, -2, group} (a whole group of at
- * most gnpde_seg_long_edges() edges, one wavefront each); the rest are
- * whole-group items, taken two per wavefront.  No chunks, no partials, no
- * tickets: launches may overlap.  (n_hub_items = n_long_items = 0 for other plans.)
+ * front of `items`, n_hub_items HUB CHUNK items {e_begin, e_end, slot, hub}
+ * (gnpde_seg_long_edges()-edge chunks of the longer groups, one wavefront each;
+ * heavy[hub] = {group, first_slot, n_chunks, 0} lists those groups, n_heavy of
+ * them, and partials holds 2*heads doubles per slot: the last chunk of a group to
+ * arrive merges its slots in chunk order and resets heavy[hub].w, so two launches
+ * on one plan must not overlap) and then n_long_items LONG items {e_begin, e_end,
+ * -2, group} (a whole group of at most gnpde_seg_long_edges() edges, one wavefront
+ * each); the rest are whole-group items, taken two per wavefront, and
+ * n_chunk_items is 0.  (n_hub_items = n_long_items = 0 for other plans.)
  * gnpde_seg_plan_build builds them from a HOST copy of rowptr into HOST
  * arrays (plain C++, once per graph; capacities: items >= R, chunk_items >=
  * nnz/eb + R, heavy >= nnz/eb + 1).  When chunk_items == items + 4*n_items

@@ -307,18 +307,20 @@ def test_seg_stats_one_launch_equals_two_and_repeats():
 @pytest.mark.parametrize("heads,att", [(2, 32), (3, 24)])
 def test_seg_stats_long_items(norm_idx, heads, att):
     """Reference-score statistics of the CSC take groups longer than a
-    wavefront's block as HUB items (more than 256 edges: one 1024-thread
-    workgroup, LDS merge in wavefront order) or LONG items (65..256 edges: one
-    wavefront), both at the front of the plan, longest first: the plan tiles
-    every edge once, repeats are bit-identical, and the statistics match the
-    64-edge-chunk plan + fixup (max exactly, 1/sum to fp32 rounding of the other
-    summation order) and the oracle RHS.  (Source groups of the reference
-    scores are uniform: norm_idx 0 keeps the chunked plan.)"""
+    wavefront's block as HUB CHUNK items (more than seg_long_max() = 512 edges:
+    512-edge chunks, one wavefront each, partials + arrival tickets, the last
+    chunk merges) or LONG items (65..512 edges: one wavefront), both at the
+    front of the plan, longest first: the plan tiles every edge once, repeats
+    are bit-identical (whatever the chunks' arrival order), the tickets return
+    to 0, and the statistics match the 64-edge-chunk plan + fixup (max exactly,
+    1/sum to fp32 rounding of the other summation order) and the oracle RHS.
+    (Source groups of the reference scores are uniform: norm_idx 0 keeps the
+    chunked plan.)"""
     N, E = 1500, 40000
     ei, x, x0, Wq, bq, Wk, bk = _attn_case(N, E, 128, heads, att, seed=78)
-    ei[:, norm_idx, :9000] = 7   # a hub group longer than one pass of the workgroup (8,192 edges)
-    ei[:, norm_idx, 9000:9300] = 5  # a short hub
-    ei[:, norm_idx, 9300:9500] = 9  # and one whole long group
+    ei[:, norm_idx, :9000] = 7   # a hub group of 18 chunks (+ its share of the random edges)
+    ei[:, norm_idx, 9000:9600] = 5  # a two-chunk hub
+    ei[:, norm_idx, 9600:9900] = 9  # and one whole long group
     g = ops.GraphCSR(T(ei), N)
     ns = ops.node_scores(g, T(x), T(Wq), T(bq), T(Wk), T(bk), heads, 'scaled_dot', 'reference')
     grouped = g.csc if norm_idx == 1 else g.csr
@@ -328,17 +330,24 @@ def test_seg_stats_long_items(norm_idx, heads, att):
         plan = grouped.seg_plan(64, long_items=True)
         it = plan.items.cpu().numpy().reshape(-1, 4)[:plan.n_items]
         nh, nl = plan.n_hub, plan.n_long
-        assert plan.n_chunk == 0 and plan.n_heavy == 0 and nh >= 2 and nl >= 1
-        assert (it[:nh, 2] == -4).all() and (it[nh:nh + nl, 2] == -2).all() and (it[nh + nl:, 2] == -1).all()
-        assert (it[:nh, 1] - it[:nh, 0] > ops.seg_long_max()).all()
+        hv = plan.heavy.cpu().numpy().reshape(-1, 4)[:plan.n_heavy]
+        assert plan.n_chunk == 0 and plan.n_heavy >= 2 and nh >= 20 and nl >= 1 and plan.n_slots == nh
+        assert (it[:nh, 2] == np.arange(nh)).all() and (it[nh:nh + nl, 2] == -2).all() and (it[nh + nl:, 2] == -1).all()
+        assert (it[:nh, 1] - it[:nh, 0] <= ops.seg_long_max()).all()
         assert (it[nh:nh + nl, 1] - it[nh:nh + nl, 0] <= ops.seg_long_max()).all()
         assert (it[nh + nl:, 1] - it[nh + nl:, 0] <= 64).all()
-        assert 7 in it[:nh, 3] and 5 in it[:nh, 3]
+        assert {5, 7} <= set(hv[:, 0].tolist()) and (hv[:, 3] == 0).all()
+        for k, (grp, first, nch, _) in enumerate(hv):  # each hub's chunks tile its group
+            ch = it[first:first + nch]
+            assert (ch[:, 3] == k).all() and ch[0, 0] == rp[grp] and ch[-1, 1] == rp[grp + 1]
+            assert (ch[1:, 0] == ch[:-1, 1]).all()
         spans = it[:, :2][np.argsort(it[:, 0])]
         assert spans[0, 0] == 0 and spans[-1, 1] == rp[-1] and (spans[1:, 0] == spans[:-1, 1]).all()
     for _ in range(3):
         m, rl = ops.softmax_stats(g, ns, norm_idx)
         assert torch.equal(m, m1) and torch.equal(rl, rl1)
+    if norm_idx == 1:
+        assert int(plan.heavy.view(-1, 4)[:plan.n_heavy, 3].abs().sum()) == 0  # tickets back to 0
     g2 = ops.GraphCSR(T(ei), N)
     gr2 = g2.csc if norm_idx == 1 else g2.csr
     gr2._seg_plans[(64, True)] = gr2.seg_plan(64)  # the chunked plan + fixup
@@ -807,7 +816,7 @@ def test_arxiv_scale_dropin_attention_default_path(mode, norm_idx):
     if mode == "reference":
         sp = func.graph_for(x).csc.seg_plan(ops._lib.fn("gnpde_seg_block_edges")(ops._lib.SCORE_REFERENCE, 2, 16),
                                             True)
-        assert sp.n_hub > 0  # destination groups longer than one long item: a workgroup each
+        assert sp.n_hub > 0  # destination groups longer than one long item: chunks with tickets
     lay = func.multihead_att_layer
     npw = [t.detach().cpu().numpy() for t in (lay.Q.weight, lay.Q.bias, lay.K.weight, lay.K.bias)]
     want = O.transformer_rhs(ei.cpu().numpy(), x.cpu().numpy(), None, *npw, 2, norm_idx, 0.25, 0.0, score_mode=mode)

@@ -1,8 +1,8 @@
 #!/usr/bin/env python
 """Where the reference statistics kernel spends its time: the G-arxiv CSC
 statistics (norm_idx 1, packed records) launched whole and over each item class
-alone (hub workgroups, long wavefronts, short items), HIP events over REPS
-launches each.  Prints one JSON line."""
+alone (hub chunks, long wavefronts, short items), HIP events over a hipGraph of
+REPS launches each (no host launch cost in the time).  Prints one JSON line."""
 import ctypes
 import json
 import os
@@ -33,22 +33,29 @@ def main():
     grouped = g.csc
     plan = grouped.seg_plan(_lib.fn("gnpde_seg_block_edges")(ns.mode, ns.heads, ns.dk), True)
     mr = torch.empty(g.R, ops.stats_record_floats(ns.heads), dtype=torch.float32, device=dev)
-    s = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    partials = torch.empty(max(plan.n_slots, 1) * 2 * ns.heads, dtype=torch.float64, device=dev)
 
     def launch(off, n, nh, nl):
+        s = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
         it = ctypes.c_void_p(plan.items.data_ptr() + 16 * off)
-        _lib.call("gnpde_seg_softmax_f32", it, n, nh, nl, ops._ptr(plan.chunk_items), 0, ops._ptr(plan.heavy), 0,
-                  ops._ptr(grouped.rowptr), ops._ptr(grouped.rowidx), ops._ptr(grouped.col), 1, 1, ns.mode, ns.heads,
-                  ns.dk, ops._ptr(ns.cs), None, None, 1, 1.0, 1.0, None, None, None, ops._ptr(mr), None, s)
+        _lib.call("gnpde_seg_softmax_f32", it, n, nh, nl, ops._ptr(plan.chunk_items), 0, ops._ptr(plan.heavy),
+                  plan.n_heavy, ops._ptr(grouped.rowptr), ops._ptr(grouped.rowidx), ops._ptr(grouped.col), 1, 1,
+                  ns.mode, ns.heads, ns.dk, ops._ptr(ns.cs), None, None, 1, 1.0, 1.0, None, None, None, ops._ptr(mr),
+                  ops._ptr(partials), s)
 
     def timed(*a):
         for _ in range(3):
             launch(*a)
         torch.cuda.synchronize()
+        cg = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(cg):
+            for _ in range(REPS):
+                launch(*a)
+        cg.replay()
+        torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        for _ in range(REPS):
-            launch(*a)
+        cg.replay()
         e1.record()
         torch.cuda.synchronize()
         return round(e0.elapsed_time(e1) / REPS * 1e3, 2)
