@@ -4,6 +4,8 @@ line per (mode, norm) with the graph-replayed RHS time in the solve's numbering
 and in the user numbering.  Run once per library (GNPDE_LIB=... for a variant):
 
   tools/attn_ab.py [--tag NAME] [--modes reference:1,per_edge:0,per_edge:1] [--reps 50]
+
+(--modes defaults to $ATT_MODES when set: tools/variants_ab.sh, tools/lin_check.sh.)
 """
 import argparse
 import json
@@ -22,7 +24,7 @@ import bench  # noqa: E402
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--tag", default=os.environ.get("GNPDE_LIB", "product"))
-    p.add_argument("--modes", default="reference:1,per_edge:0,per_edge:1")
+    p.add_argument("--modes", default=os.environ.get("ATT_MODES", "reference:1,per_edge:0,per_edge:1"))
     p.add_argument("--reps", type=int, default=50)
     a = p.parse_args()
     from gnpde import synthetic
