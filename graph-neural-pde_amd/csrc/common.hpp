@@ -272,13 +272,32 @@ __device__ __forceinline__ float unpack(const Packed<VEC, bf16>& r, int t) {
 //      operand loaded after the aggregation (nothing held across the gathers).
 // An instantiation only holds registers for what it can emit.
 constexpr int kStagePre = 2;
+// A/B knobs: whether the STG 1 / 2 / 3 instantiations prefetch their stage
+// operands before the gathers (1) or stream them after the aggregation (0, as STG 4)
+#ifndef GNPDE_STG1_PRE
+#define GNPDE_STG1_PRE 1
+#endif
+#ifndef GNPDE_STG2_PRE
+#define GNPDE_STG2_PRE 0  // 111 -> 69 VGPRs (4 -> 7 waves per SIMD)
+#endif
+#ifndef GNPDE_STG3_PRE
+#define GNPDE_STG3_PRE 1
+#endif
 template <int STG>
 constexpr int stage_nout() {
   return (STG == 2 || STG == 4) ? 2 : 1;
 }
 template <int STG>
+constexpr bool stage_prefetch() {
+  return (STG == 1 && GNPDE_STG1_PRE) || (STG == 2 && GNPDE_STG2_PRE) || (STG == 3 && GNPDE_STG3_PRE);
+}
+template <int STG>
 constexpr int stage_kpre() {  // operands prefetched before the gathers
-  return (STG == 0 || STG == 4) ? 0 : kStagePre;
+  return stage_prefetch<STG>() ? kStagePre : 0;
+}
+template <int STG>
+constexpr int stage_bpre() {  // stage-output bases prefetched before the gathers
+  return stage_prefetch<STG>() ? stage_nout<STG>() : 0;
 }
 template <int STG>
 constexpr bool stage_dot() {
@@ -293,9 +312,9 @@ template <int VEC, class T, int STG>
 struct EpiPre {
   Packed<VEC, T> xr;
   Packed<VEC, T> x0r;
-  Packed<VEC, T> base[(STG == 0 || STG == 4) ? 1 : stage_nout<STG>()];
+  Packed<VEC, T> base[stage_bpre<STG>() > 0 ? stage_bpre<STG>() : 1];
   Packed<VEC, T> kv[stage_kpre<STG>() > 0 ? stage_kpre<STG>() : 1];
-  Packed<VEC, T> dw;  // the stage's dot operand (dot_rows, STG 2)
+  Packed<VEC, T> dw;  // the stage's dot operand (dot_rows, STG 2 with GNPDE_STG2_PRE)
 };
 
 // The Epi / stage pointers are declared float*; for bf16 storage they address
@@ -317,7 +336,7 @@ __device__ __forceinline__ void epi_prefetch(const Epi& e, int64_t row, int cc, 
   if constexpr (STG == 0 || STG == 4) return;
   const int64_t off = row * e.ldf + cc;
 #pragma unroll
-  for (int i = 0; i < stage_nout<STG>(); ++i) {
+  for (int i = 0; i < stage_bpre<STG>(); ++i) {
     if (i < e.st.n_out) {
       const gnpde_stage_out_t& so = e.st.o[i];
       if (so.base != nullptr && !(need_x && so.base == e.x && e.ldx == e.ldf))
@@ -327,7 +346,8 @@ __device__ __forceinline__ void epi_prefetch(const Epi& e, int64_t row, int cc, 
 #pragma unroll
   for (int j = 0; j < stage_kpre<STG>(); ++j)
     if (j < e.st.nk) load_packed<VEC>(as_t<T>(e.st.k[j]) + off, p.kv[j]);
-  if constexpr (STG == 2)  // STG 3 loads its dot operand in the epilogue (registers: occupancy)
+  // STG 3 (and STG 2 unless prefetching) load the dot operand in the epilogue (registers: occupancy)
+  if constexpr (STG == 2 && stage_prefetch<STG>())
     if (e.st.dot_rows) load_packed<VEC>(as_t<T>(e.st.dot_with) + off, p.dw);
 }
 
@@ -499,7 +519,7 @@ __device__ __forceinline__ void epi_finish(const Epi& e, int64_t row, int cc, co
     if constexpr (stage_dot<STG>()) {
       if (e.st.dot_rows && dpart) {
         Packed<VEC, T> dw;
-        if constexpr (STG == 2)
+        if constexpr (STG == 2 && stage_prefetch<STG>())
           dw = p.dw;
         else
           load_packed<VEC>(as_t<T>(e.st.dot_with) + off, dw);
@@ -507,16 +527,30 @@ __device__ __forceinline__ void epi_finish(const Epi& e, int64_t row, int cc, co
         for (int t = 0; t < VEC; ++t) *dpart = fma((double)o[t], (double)unpack(dw, t), *dpart);
       }
     }
-    // the shared stage operands, prefetched before the gathers
-    constexpr int NK = stage_kpre<STG>();
-    auto kval = [&](int j, int t) -> float { return unpack(p.kv[j], t); };
     const float sc = stage_scale(e.st);
+    if constexpr (!stage_prefetch<STG>()) {
+      // no prefetch: the stage operands streamed after the gathers (wide_combine, the
+      // same per-output order as stage_combine: same bits)
+      constexpr int NO = stage_nout<STG>();
+      float xv[VEC], r[2][VEC], ev[VEC];
 #pragma unroll
-    for (int i = 0; i < stage_nout<STG>(); ++i) {
-      if (i >= e.st.n_out) break;
-      float r[VEC];
-      stage_combine<VEC, NK, T>(e, e.st.o[i], off, o, p.xr, &p.base[i], kval, sc, r);
-      store_vec<VEC>(as_t<T>(e.st.o[i].out) + oo, r);
+      for (int t = 0; t < VEC; ++t) xv[t] = need_x ? unpack(p.xr, t) : 0.f;
+      wide_combine<VEC, T, kStagePre, NO, false>(e.st, off, o, (need_x && e.ldx == e.ldf) ? e.x : nullptr, xv, r,
+                                                 ev);
+#pragma unroll
+      for (int i = 0; i < NO; ++i)
+        if (i < e.st.n_out) store_vec<VEC>(as_t<T>(e.st.o[i].out) + oo, r[i]);
+    } else {
+      // the shared stage operands, prefetched before the gathers
+      constexpr int NK = stage_kpre<STG>();
+      auto kval = [&](int j, int t) -> float { return unpack(p.kv[j], t); };
+#pragma unroll
+      for (int i = 0; i < stage_nout<STG>(); ++i) {
+        if (i >= e.st.n_out) break;
+        float r[VEC];
+        stage_combine<VEC, NK, T>(e, e.st.o[i], off, o, p.xr, &p.base[i], kval, sc, r);
+        store_vec<VEC>(as_t<T>(e.st.o[i].out) + oo, r);
+      }
     }
   }
 }

@@ -259,6 +259,10 @@ __global__ __launch_bounds__(256) void attn_team_kernel(const int* __restrict__ 
 // KS_BLOCK threads per tile, TPR threads per row, RPB = KS_BLOCK/TPR rows in
 // flight per iteration (16-byte loads, 8 rows unrolled per thread).
 constexpr int kKeysumBlock = 1024;
+#ifndef GNPDE_KS_ROWS
+#define GNPDE_KS_ROWS 4  // 4 / 8 / 12: 0.1423 / 0.1429 / 0.1437 ms per reference RHS (with ring depth 2 / 4 / 6)
+#endif
+constexpr int kKeysumRows = GNPDE_KS_ROWS;  // rows per thread in flight (keysum_partial)
 constexpr int kKeysumTilesTarget = 256;  // tiles per launch: the projection block reads them all
 constexpr int kProjLanes = 32;           // lanes per row of Wk (S phase)
 constexpr int kProjLoads = 16;           // tile shares in flight per thread (key_projection)
@@ -281,13 +285,26 @@ __global__ __launch_bounds__(kKeysumBlock) void keysum_partial_kernel(const floa
     double acc[VEC];
 #pragma unroll
     for (int i = 0; i < VEC; ++i) acc[i] = 0.0;
-#pragma unroll 4
-    for (int64_t n = n0 + rs; n < n1; n += RPB) {
-      const double d = (double)indeg[base + n];
-      float v[VEC];
-      load_vec<VEC>(x + (base + n) * ldx + c0, v);
+    // KSB rows per thread in flight: every load of a batch issued before its sums (the
+    // loop was one memory latency per 4 rows, ~5 in a row per thread: 18.4 us on G-arxiv)
+    for (int64_t nb = n0 + rs; nb < n1; nb += (int64_t)RPB * kKeysumRows) {
+      float v[kKeysumRows][VEC];
+      int dg[kKeysumRows];
 #pragma unroll
-      for (int i = 0; i < VEC; ++i) acc[i] = fma(d, (double)v[i], acc[i]);
+      for (int k = 0; k < kKeysumRows; ++k) {
+        const int64_t n = nb + (int64_t)k * RPB;
+        const int64_t nn = n < n1 ? n : n0;  // past the tile: a row of it again, weighted 0
+        load_vec<VEC>(x + (base + nn) * ldx + c0, v[k]);
+        dg[k] = n < n1 ? indeg[base + nn] : 0;
+      }
+#pragma unroll
+      for (int k = 0; k < kKeysumRows; ++k) {
+        if (nb + (int64_t)k * RPB < n1) {  // same sums, same order as one row at a time
+          const double d = (double)dg[k];
+#pragma unroll
+          for (int i = 0; i < VEC; ++i) acc[i] = fma(d, (double)v[k][i], acc[i]);
+        }
+      }
     }
 #pragma unroll
     for (int i = 0; i < VEC; ++i) red[rs * (C + 1) + c0 + i] = acc[i];
@@ -485,57 +502,68 @@ __device__ __forceinline__ void ns_store(double (&acc)[MAXH], const double (&vb)
     buf_store_f64(rcs, (st && h < H) ? (uint32_t)((row * H + h) * 8) : kBufNone, acc[h] + vb[h]);
 }
 
-// One chunk per row: U[b] sits in registers and the loop keeps two row groups
-// in flight ahead of the one being reduced.  Prefetch addresses past the
-// block's rows clamp to its last row (a cache-line hit, no extra HBM traffic).
-// The first two row groups of a wave (ns_block_resident's prefetch), issued
+// One chunk per row: U[b] sits in registers and each wave keeps kNsDepth row
+// groups in flight (a ring of kNsDepth register buffers, the loop unrolled by
+// it so every index is static): a group is reduced, then its buffer refilled
+// with the group kNsDepth steps ahead.  Depth 2 / 4 / 6 (with 4 / 8 / 12 key-sum
+// rows in flight): reference attention RHS 0.1423 / 0.1429 / 0.1437 ms — the
+// ~20 us of the launch is not the prefetch depth.
+// Prefetch addresses past the block's rows clamp to its last row (a cache-line
+// hit, no extra HBM traffic).  ns_first_rows issues the first kNsDepth groups,
 // before U exists when the block forms U itself (node_scores_fused_kernel).
+#ifndef GNPDE_NS_DEPTH
+#define GNPDE_NS_DEPTH 2  // deeper rings measured no faster (above)
+#endif
+// depth per head count: GNPDE_NS_DEPTH groups of NPV floats, capped at 64 floats of ring
+template <int MAXH>
+constexpr int ns_depth() {
+  constexpr int d = 64 / node_scores_npv<MAXH>();
+  return d < 2 ? 2 : (d > GNPDE_NS_DEPTH ? GNPDE_NS_DEPTH : d);
+}
+
+template <int VEC, int GL, int MAXH>
+using NsRing = float[ns_depth<MAXH>()][node_scores_npv<MAXH>() / VEC][VEC];
+
 template <int VEC, int GL, int MAXH, bool CLAMP>
 __device__ __forceinline__ void ns_first_rows(const float* __restrict__ xb, int64_t n0, int64_t n1, int C,
-                                              int64_t ldx, int g, int gl, int wv,
-                                              float (&xa)[node_scores_npv<MAXH>() / VEC][VEC],
-                                              float (&xn)[node_scores_npv<MAXH>() / VEC][VEC]) {
+                                              int64_t ldx, int g, int gl, int wv, NsRing<VEC, GL, MAXH>& xr) {
   constexpr int G = kWave / GL;
   constexpr int NP = node_scores_npv<MAXH>() / VEC;
   const int64_t step = (int64_t)kWavesPerBlock * G;
   const int64_t last = n1 - 1, nb = n0 + wv * G;
-  ns_load_x<VEC, NP, GL, CLAMP>(xb + min(nb + g, last) * ldx, 0, gl, C, xa);
-  ns_load_x<VEC, NP, GL, CLAMP>(xb + min(nb + g + step, last) * ldx, 0, gl, C, xn);
+  constexpr int kNsDepth = ns_depth<MAXH>();
+#pragma unroll
+  for (int d = 0; d < kNsDepth; ++d)
+    ns_load_x<VEC, NP, GL, CLAMP>(xb + min(nb + g + d * step, last) * ldx, 0, gl, C, xr[d]);
 }
 
 template <int VEC, int GL, int MAXH, bool CLAMP, bool PRELOADED = false>
 __device__ __forceinline__ void ns_block_resident(const double* __restrict__ Ub, const float* __restrict__ xb,
                                                   __amdgpu_buffer_rsrc_t rcs, int64_t n0, int64_t n1, int C,
                                                   int64_t ldx, int H, int Cp, int g, int gl, int wv,
-                                                  float (&xa)[node_scores_npv<MAXH>() / VEC][VEC],
-                                                  float (&xn)[node_scores_npv<MAXH>() / VEC][VEC]) {
+                                                  NsRing<VEC, GL, MAXH>& xr) {
   constexpr int G = kWave / GL;
   constexpr int NP = node_scores_npv<MAXH>() / VEC;
   const int64_t step = (int64_t)kWavesPerBlock * G;
   const int64_t last = n1 - 1;
-  int64_t nb = n0 + wv * G;
-  if constexpr (!PRELOADED) ns_first_rows<VEC, GL, MAXH, CLAMP>(xb, n0, n1, C, ldx, g, gl, wv, xa, xn);
+  constexpr int kNsDepth = ns_depth<MAXH>();
+  if constexpr (!PRELOADED) ns_first_rows<VEC, GL, MAXH, CLAMP>(xb, n0, n1, C, ldx, g, gl, wv, xr);
   double u[NP][VEC][MAXH];
   ns_load_u<VEC, NP, GL, MAXH>(Ub, 0, gl, u);
   double vb[MAXH];
 #pragma unroll
   for (int h = 0; h < MAXH; ++h) vb[h] = Ub[Cp * MAXH + h];
-  for (; nb < n1; nb += step) {
-    const int64_t nr = nb + g;
-    float xf[NP][VEC];
-    ns_load_x<VEC, NP, GL, CLAMP>(xb + min(nr + 2 * step, last) * ldx, 0, gl, C, xf);
-    double acc[MAXH];
+  for (int64_t nb = n0 + wv * G; nb < n1; nb += kNsDepth * step) {
 #pragma unroll
-    for (int h = 0; h < MAXH; ++h) acc[h] = 0.0;
-    ns_dot<VEC, NP, MAXH>(xa, u, acc);
-    ns_store<GL, MAXH>(acc, vb, gl, H, nr < n1, rcs, nr);
+    for (int d = 0; d < kNsDepth; ++d) {
+      const int64_t nr = nb + d * step + g;
+      double acc[MAXH];
 #pragma unroll
-    for (int p = 0; p < NP; ++p)
-#pragma unroll
-      for (int i = 0; i < VEC; ++i) {
-        xa[p][i] = xn[p][i];
-        xn[p][i] = xf[p][i];
-      }
+      for (int h = 0; h < MAXH; ++h) acc[h] = 0.0;
+      ns_dot<VEC, NP, MAXH>(xr[d], u, acc);
+      ns_store<GL, MAXH>(acc, vb, gl, H, nr < n1, rcs, nr);
+      ns_load_x<VEC, NP, GL, CLAMP>(xb + min(nr + kNsDepth * step, last) * ldx, 0, gl, C, xr[d]);
+    }
   }
 }
 
@@ -561,11 +589,11 @@ __global__ __launch_bounds__(256) void node_scores_kernel(const float* __restric
     const double* __restrict__ Ub = uv + b * ((int64_t)Cp * MAXH + MAXH);
     const __amdgpu_buffer_rsrc_t rcs = buf_rsrc(cs + b * N * H);
     if (nch == 1) {
-      float xa[NP][VEC], xn[NP][VEC];
+      NsRing<VEC, GL, MAXH> xr;
       if (ragged)
-        ns_block_resident<VEC, GL, MAXH, true>(Ub, xb, rcs, n0, n1, C, ldx, H, Cp, g, gl, wv, xa, xn);
+        ns_block_resident<VEC, GL, MAXH, true>(Ub, xb, rcs, n0, n1, C, ldx, H, Cp, g, gl, wv, xr);
       else
-        ns_block_resident<VEC, GL, MAXH, false>(Ub, xb, rcs, n0, n1, C, ldx, H, Cp, g, gl, wv, xa, xn);
+        ns_block_resident<VEC, GL, MAXH, false>(Ub, xb, rcs, n0, n1, C, ldx, H, Cp, g, gl, wv, xr);
     } else {
       double vb[MAXH];
 #pragma unroll
@@ -608,7 +636,6 @@ __global__ __launch_bounds__(256) void node_scores_fused_kernel(const float* __r
                                                                  const float* __restrict__ bq, int att,
                                                                  double* __restrict__ cs, int64_t rows_per_block) {
   constexpr int NPV = node_scores_npv<MAXH>();
-  constexpr int NP = NPV / VEC;
   constexpr int Cp = GL * NPV;
   extern __shared__ __attribute__((aligned(16))) double nsf_lds[];  // S[att] | red[256] | U[Cp*MAXH] | v[MAXH]
   double* S = nsf_lds;
@@ -621,8 +648,8 @@ __global__ __launch_bounds__(256) void node_scores_fused_kernel(const float* __r
   const int64_t n0 = (int64_t)blockIdx.x * rows_per_block;
   const int64_t n1 = min(N, n0 + rows_per_block);
   const float* __restrict__ xb = x + b * N * ldx;
-  float xa[NP][VEC], xn[NP][VEC];
-  ns_first_rows<VEC, GL, MAXH, CLAMP>(xb, n0, n1, C, ldx, g, gl, wv, xa, xn);
+  NsRing<VEC, GL, MAXH> xr;
+  ns_first_rows<VEC, GL, MAXH, CLAMP>(xb, n0, n1, C, ldx, g, gl, wv, xr);
   // this thread's operands of U (output (c, h) = (tid / MAXH, tid % MAXH); the v
   // outputs c = Cp go to the first threads' second slot), loaded before S is known
   const int dk = att / H;
@@ -695,7 +722,7 @@ __global__ __launch_bounds__(256) void node_scores_fused_kernel(const float* __r
   }
   __syncthreads();
   const __amdgpu_buffer_rsrc_t rcs = buf_rsrc(cs + b * N * H);
-  ns_block_resident<VEC, GL, MAXH, CLAMP, true>(U, xb, rcs, n0, n1, C, ldx, H, Cp, g, gl, wv, xa, xn);
+  ns_block_resident<VEC, GL, MAXH, CLAMP, true>(U, xb, rcs, n0, n1, C, ldx, H, Cp, g, gl, wv, xr);
 }
 
 // S[b][d] = sum of the tile shares part[b][tile][d] in tile order (one thread per

@@ -15,4 +15,5 @@ from gnpde import synthetic  # noqa: E402
 dev = torch.device("cuda", 0)
 ei, w = synthetic.rw_graph(synthetic.ARXIV_N, synthetic.ARXIV_E, seed=0, device=dev)
 x = synthetic.features(1, synthetic.ARXIV_N, 128, seed=1, device=dev)
-print(json.dumps(bench.bench_train(ei, w, x, 0.25, dev)))
+print(json.dumps(dict(lib=os.path.basename(os.environ.get("GNPDE_LIB", "libgnpde.so")),
+                      **bench.bench_train(ei, w, x, 0.25, dev))))

@@ -7,7 +7,7 @@ OUT=$R/gpurun_out/${TAG:-ab}
 mkdir -p $OUT
 cd $R
 for r in $(seq 1 ${ROUNDS:-2}); do
-  for lib in variants/libgnpde_*.so; do
+  for lib in ${VDIR:-variants}/libgnpde_*.so; do
     if [ "${PROF:-0}" = 1 ] && [ $r = 1 ]; then
       n=$(basename $lib .so)
       (cd /tmp && export TMPDIR=/tmp && GNPDE_LIB=$R/$lib timeout -k 10 240 rocprofv3 --kernel-trace --stats \
