@@ -382,8 +382,13 @@ __global__ __launch_bounds__(256) void agg_kernel(const int4* __restrict__ items
     }
   }
   // the row's owner lanes (g == 0: lanes [rs*SL, rs*SL + GL)) are all here
-  if constexpr (stage_rowsum<STG, T>())
-    if (ep.st.dot_rows || ep.st.err_rows) epi_rowsum_store_any<GL>(ep, row, dpart, rs * SL, gl == 0);
+  if constexpr (stage_rowsum<STG, T>()) {
+    if (ep.st.dot_rows || ep.st.err_rows) {
+      const double* prev = nullptr;
+      if constexpr (PRE && stage_dot<STG>() && GNPDE_DOT_PRE) prev = &pre[0].dprev;
+      epi_rowsum_store_any<GL>(ep, row, dpart, rs * SL, gl == 0, prev);
+    }
+  }
 }
 
 // Hub rows combined after the aggregation launch (GNPDE_HUB_FIXUP=1): one wavefront per hub.

@@ -281,7 +281,13 @@ constexpr int kStagePre = 2;
 #define GNPDE_STG2_PRE 0  // 111 -> 69 VGPRs (4 -> 7 waves per SIMD)
 #endif
 #ifndef GNPDE_STG3_PRE
-#define GNPDE_STG3_PRE 1
+#define GNPDE_STG3_PRE 0  // G-arxiv adjoint launch (CSC): 134 with, 117 us without (105 -> fewer VGPRs)
+#endif
+#ifndef GNPDE_DOT_PRE
+#define GNPDE_DOT_PRE 1   // the dot operand and the row's running dot read before the gathers: 128 -> 117 us
+#endif
+#ifndef GNPDE_STG2_DW
+#define GNPDE_STG2_DW 1   // STG 2 prefetches its dot operand too (with GNPDE_DOT_PRE)
 #endif
 template <int STG>
 constexpr int stage_nout() {
@@ -304,6 +310,10 @@ constexpr bool stage_dot() {
   return STG == 2 || STG == 3;
 }
 template <int STG>
+constexpr bool stage_dw_pre() {  // the dot operand read before the gathers
+  return (STG == 2 && (stage_prefetch<STG>() || (GNPDE_DOT_PRE && GNPDE_STG2_DW))) || (STG == 3 && GNPDE_DOT_PRE);
+}
+template <int STG>
 constexpr bool stage_err() {
   return STG == 4;
 }
@@ -314,7 +324,8 @@ struct EpiPre {
   Packed<VEC, T> x0r;
   Packed<VEC, T> base[stage_bpre<STG>() > 0 ? stage_bpre<STG>() : 1];
   Packed<VEC, T> kv[stage_kpre<STG>() > 0 ? stage_kpre<STG>() : 1];
-  Packed<VEC, T> dw;  // the stage's dot operand (dot_rows, STG 2 with GNPDE_STG2_PRE)
+  Packed<VEC, T> dw;  // the stage's dot operand (dot_rows; STG 2 with GNPDE_STG2_PRE, STG 3 with GNPDE_DOT_PRE)
+  double dprev;       // the row's running dot (dot_accumulate), read before the gathers
 };
 
 // The Epi / stage pointers are declared float*; for bf16 storage they address
@@ -333,6 +344,8 @@ __device__ __forceinline__ void epi_prefetch(const Epi& e, int64_t row, int cc, 
   const bool need_x = (e.flags & GNPDE_EPI_RHS) != 0;
   if (need_x) load_packed<VEC>(as_t<T>(e.x) + row * e.ldx + cc, p.xr);
   if (e.flags & GNPDE_ADD_SOURCE) load_packed<VEC>(as_t<T>(e.x0) + row * e.ldx0 + cc, p.x0r);
+  if constexpr (stage_dot<STG>() && GNPDE_DOT_PRE)  // the running dot: its read is off the epilogue's chain
+    p.dprev = (e.st.dot_rows && e.st.dot_accumulate) ? e.st.dot_rows[row] : 0.0;
   if constexpr (STG == 0 || STG == 4) return;
   const int64_t off = row * e.ldf + cc;
 #pragma unroll
@@ -346,8 +359,8 @@ __device__ __forceinline__ void epi_prefetch(const Epi& e, int64_t row, int cc, 
 #pragma unroll
   for (int j = 0; j < stage_kpre<STG>(); ++j)
     if (j < e.st.nk) load_packed<VEC>(as_t<T>(e.st.k[j]) + off, p.kv[j]);
-  // STG 3 (and STG 2 unless prefetching) load the dot operand in the epilogue (registers: occupancy)
-  if constexpr (STG == 2 && stage_prefetch<STG>())
+  // the dot operand: STG 2 when prefetching, STG 2 / 3 under GNPDE_DOT_PRE (else in the epilogue)
+  if constexpr (stage_dw_pre<STG>())
     if (e.st.dot_rows) load_packed<VEC>(as_t<T>(e.st.dot_with) + off, p.dw);
 }
 
@@ -519,7 +532,7 @@ __device__ __forceinline__ void epi_finish(const Epi& e, int64_t row, int cc, co
     if constexpr (stage_dot<STG>()) {
       if (e.st.dot_rows && dpart) {
         Packed<VEC, T> dw;
-        if constexpr (STG == 2 && stage_prefetch<STG>())
+        if constexpr (stage_dw_pre<STG>())
           dw = p.dw;
         else
           load_packed<VEC>(as_t<T>(e.st.dot_with) + off, dw);
@@ -570,13 +583,14 @@ constexpr bool stage_rowsum() {
   return (stage_dot<STG>() && sizeof(T) == 4) || stage_err<STG>();
 }
 
-__device__ __forceinline__ void epi_rowsum_write(const Epi& e, int64_t row, double v) {
+// prev: the row's running dot read before the gathers (GNPDE_DOT_PRE), or nullptr
+__device__ __forceinline__ void epi_rowsum_write(const Epi& e, int64_t row, double v, const double* prev = nullptr) {
   if (e.st.err_rows) {
     e.st.err_rows[row] = v;
   } else if (e.st.dot_rows) {
     double* d = e.st.dot_rows + row;
     const double w = e.st.dot_coef * v;
-    *d = e.st.dot_accumulate ? *d + w : w;
+    *d = e.st.dot_accumulate ? (prev ? *prev : *d) + w : w;
   }
 }
 
@@ -585,24 +599,26 @@ __device__ __forceinline__ void epi_rowsum_write(const Epi& e, int64_t row, doub
 // xor tree, stored by the first of them.  Called by every lane of the row's slot
 // (convergent).
 template <int GL>
-__device__ __forceinline__ void epi_rowsum_store(const Epi& e, int64_t row, double dpart, bool store) {
+__device__ __forceinline__ void epi_rowsum_store(const Epi& e, int64_t row, double dpart, bool store,
+                                                 const double* prev = nullptr) {
   static_assert((GL & (GL - 1)) == 0, "the xor tree needs power-of-two row lanes");
 #pragma unroll
   for (int o = 1; o < GL; o <<= 1) dpart += __shfl_xor(dpart, o);
-  if (store) epi_rowsum_write(e, row, dpart);
+  if (store) epi_rowsum_write(e, row, dpart, prev);
 }
 
 // The same for any GL (e.g. 21 lanes: three bf16 rows of 168 columns per wavefront):
 // the first owner lane sums the slot's lanes base .. base + GL - 1 in order.
 template <int GL>
-__device__ __forceinline__ void epi_rowsum_store_any(const Epi& e, int64_t row, double dpart, int base, bool store) {
+__device__ __forceinline__ void epi_rowsum_store_any(const Epi& e, int64_t row, double dpart, int base, bool store,
+                                                     const double* prev = nullptr) {
   if constexpr ((GL & (GL - 1)) == 0) {
-    epi_rowsum_store<GL>(e, row, dpart, store);
+    epi_rowsum_store<GL>(e, row, dpart, store, prev);
   } else {
     double tot = 0.0;
 #pragma unroll
     for (int j = 0; j < GL; ++j) tot += __shfl(dpart, base + j);
-    if (store) epi_rowsum_write(e, row, tot);
+    if (store) epi_rowsum_write(e, row, tot, prev);
   }
 }
 

@@ -464,6 +464,8 @@ class _LaplacianFixedGridFn(torch.autograd.Function):
         gk2 = 3dt/8 g - dt a u4 + dt a u3                       ...
         gk1 = dt/8 g + dt a u4 - dt/3 a u3 + dt/3 a u2
         g  <- g + a (u4 + u3 + u2 + u1)
+    (formed as gk2 = gk3 + dt a u3 - 2 dt a u4, gk1 = gk2/3 + dt a (u2 + 4 u4 - 2 u3)/3
+    and a running sum that carries g, so that each launch reads as few rows as it can)
         d alpha += a'(alpha) sum_i <u_i, x_i>,  d beta += sum_i <gk_i, x0>
     (K1 over the CSC for (A^T - I), each gk line and the running sum formed in
     the epilogue of the launch before it (gnpde_stage_epilogue_t), and the
@@ -557,8 +559,10 @@ class _LaplacianFixedGridFn(torch.autograd.Function):
             # launches' epilogues (gnpde_stage_epilogue_t dot_rows), summed once at the end
             drow = torch.zeros(s0.numel() // s0.shape[-1], dtype=torch.float64, device=s0.device) \
                 if method == 'rk4' else None
-            def g_at(jj):  # an output time's gradient in the solve's numbering
-                return lay.to_internal(g_sol[jj]) if lay is not None else g_sol[jj]
+            def g_at(jj):  # an output time's gradient in the solve's numbering (one gnpde_rows_copy pass)
+                if lay is None:
+                    return g_sol[jj]
+                return _to_internal(g_sol[jj], lay)
 
             for n in range(len(steps) - 1, -1, -1):
                 for jj in out_at.get(n, []):
@@ -578,15 +582,19 @@ class _LaplacianFixedGridFn(torch.autograd.Function):
                     T = dict(alpha=one, rhs=True, alpha_sigmoid=False, transpose=True)
                     # d alpha += a'(alpha) (dt/8 <v, x4> + <u3, x3> + <u2, x2> + <u1, y>): the epilogue of
                     # each launch adds its row terms; u2 and u1 are used only inside their own launch
+                    # Each gk line is written against the launch's own input where it can (that row is
+                    # in registers already): gk2 = gk3 + ad u3 - 2 ad c8 v, gk1 = gk2/3 + ad/3 u2 +
+                    # 4/3 ad c8 v - 2/3 ad u3, and the running sum carries g (acc = g + a(c8 v + u3 + u2)),
+                    # so g is read by the third launch only: 20 state passes per step, not 23
                     ops.spmm_rhs(gr, w_csc, g, stage=ops.Stage(f_out=v, outs=[(gk3, g, 3 * c8, ad * c8, [])],
                                                                dot=(x4, drow, c8, True)), **T)
-                    ops.spmm_rhs(gr, w_csc, gk3, stage=ops.Stage(f_out=u3, outs=[(gk2, g, 3 * c8, ad,
-                                                                                  [(v, -ad * c8)])],
+                    ops.spmm_rhs(gr, w_csc, gk3, stage=ops.Stage(f_out=u3, outs=[(gk2, gk3, 1.0, ad,
+                                                                                  [(v, -2.0 * ad * c8)])],
                                                                  dot=(x3, drow, 1.0, True)), **T)
                     ops.spmm_rhs(gr, w_csc, gk2, stage=ops.Stage(outs=[
-                        (gk1, g, c8, ad / 3.0, [(v, ad * c8), (u3, -ad / 3.0)]),
-                        (acc, u3, a, a, [(v, a * c8)])], dot=(x2, drow, 1.0, True)), **T)
-                    ops.spmm_rhs(gr, w_csc, gk1, stage=ops.Stage(outs=[(g_new, g, 1.0, a, [(acc, 1.0)])],
+                        (gk1, gk2, 1.0 / 3.0, ad / 3.0, [(v, 4.0 * ad * c8 / 3.0), (u3, -2.0 * ad / 3.0)]),
+                        (acc, g, 1.0, a, [(v, a * c8), (u3, a)])], dot=(x2, drow, 1.0, True)), **T)
+                    ops.spmm_rhs(gr, w_csc, gk1, stage=ops.Stage(outs=[(g_new, acc, 1.0, a, [])],
                                                                  dot=(y, drow, 1.0, True)), **T)
                     if add_source:
                         gb = gb + c8 * ops.dot(g, x0) + ops.dot(gk3, x0) + ops.dot(gk2, x0) + ops.dot(gk1, x0)
@@ -618,7 +626,9 @@ class _LaplacianFixedGridFn(torch.autograd.Function):
             for jj in out_at.get(-1, []):
                 g = g + g_at(jj)
             if lay is not None:
-                g = lay.to_user(g)
+                gu = torch.empty_like(g)
+                _to_user(g, gu, lay)
+                g = gu
             g = g + g_sol[0]
             if sig:
                 ga = ga * (a_dev * (1 - a_dev)).double()
@@ -734,6 +744,15 @@ def _entry_copy(y0, buf, sol0, order):
     else:
         C = y0.shape[-1]
         torch.index_select(y0.reshape(-1, C), 0, order, out=buf.view(-1, C))
+
+
+def _to_internal(src, lay):
+    """src (caller's numbering) gathered into the solve's numbering: a fresh tensor."""
+    if src.is_cuda and (src.shape[-1] * src.element_size()) % 16 == 0 and src.is_contiguous():
+        dst = torch.empty_like(src)
+        ops.rows_copy(src, dst, order=lay.order)
+        return dst
+    return lay.to_internal(src)
 
 
 def _to_user(src, dst, lay):
