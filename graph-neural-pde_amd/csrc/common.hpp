@@ -286,6 +286,9 @@ constexpr int kStagePre = 2;
 #ifndef GNPDE_DOT_PRE
 #define GNPDE_DOT_PRE 1   // the dot operand and the row's running dot read before the gathers: 128 -> 117 us
 #endif
+#ifndef GNPDE_DOT_DIAG
+#define GNPDE_DOT_DIAG 0  // diagnostics only (wrong results): 1 no dot arithmetic, 2 no row reduction / store
+#endif
 #ifndef GNPDE_STG2_DW
 #define GNPDE_STG2_DW 1   // STG 2 prefetches its dot operand too (with GNPDE_DOT_PRE)
 #endif
@@ -536,8 +539,12 @@ __device__ __forceinline__ void epi_finish(const Epi& e, int64_t row, int cc, co
           dw = p.dw;
         else
           load_packed<VEC>(as_t<T>(e.st.dot_with) + off, dw);
+        if constexpr (GNPDE_DOT_DIAG == 1) {
+          *dpart += (double)unpack(dw, 0);
+        } else {
 #pragma unroll
-        for (int t = 0; t < VEC; ++t) *dpart = fma((double)o[t], (double)unpack(dw, t), *dpart);
+          for (int t = 0; t < VEC; ++t) *dpart = fma((double)o[t], (double)unpack(dw, t), *dpart);
+        }
       }
     }
     const float sc = stage_scale(e.st);
@@ -583,6 +590,34 @@ constexpr bool stage_rowsum() {
   return (stage_dot<STG>() && sizeof(T) == 4) || stage_err<STG>();
 }
 
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+// an fp64 value moved by DPP (each 32-bit half), bound controls as in flash.hip's dpp_mov
+template <int CTRL>
+__device__ __forceinline__ double dpp_mov64(double v) {
+  const u32x2 w = __builtin_bit_cast(u32x2, v);
+  const u32x2 r = {(uint32_t)__builtin_amdgcn_update_dpp(0, (int)w.x, CTRL, 0xf, 0xf, false),
+                   (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w.y, CTRL, 0xf, 0xf, false)};
+  return __builtin_bit_cast(double, r);
+}
+
+// Sum over aligned groups of GL lanes (GL a power of two), every lane of a group
+// ending with the group's sum: DPP inside 16-lane rows (xor 1, xor 2, then the
+// half-row and row mirrors, which pair lanes holding equal partial sums), a
+// cross-lane shuffle per further doubling.  A fixed order: deterministic.
+// (An xor tree of 64-bit shuffles costs two LDS-unit permutes per step; the
+// adjoint launch's row dot term measured 27 us of a 117-us launch that way.)
+template <int GL>
+__device__ __forceinline__ double group_sum64(double v) {
+  if constexpr (GL >= 2) v += dpp_mov64<0xB1>(v);   // quad_perm [1,0,3,2]
+  if constexpr (GL >= 4) v += dpp_mov64<0x4E>(v);   // quad_perm [2,3,0,1]
+  if constexpr (GL >= 8) v += dpp_mov64<0x141>(v);  // row_half_mirror
+  if constexpr (GL >= 16) v += dpp_mov64<0x140>(v); // row_mirror
+#pragma unroll
+  for (int o = 16; o < GL; o <<= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
 // prev: the row's running dot read before the gathers (GNPDE_DOT_PRE), or nullptr
 __device__ __forceinline__ void epi_rowsum_write(const Epi& e, int64_t row, double v, const double* prev = nullptr) {
   if (e.st.err_rows) {
@@ -602,8 +637,8 @@ template <int GL>
 __device__ __forceinline__ void epi_rowsum_store(const Epi& e, int64_t row, double dpart, bool store,
                                                  const double* prev = nullptr) {
   static_assert((GL & (GL - 1)) == 0, "the xor tree needs power-of-two row lanes");
-#pragma unroll
-  for (int o = 1; o < GL; o <<= 1) dpart += __shfl_xor(dpart, o);
+  if constexpr (GNPDE_DOT_DIAG == 2) return;
+  dpart = group_sum64<GL>(dpart);
   if (store) epi_rowsum_write(e, row, dpart, prev);
 }
 
@@ -647,7 +682,6 @@ inline int epi_stage_kind(const Epi& e) {
 constexpr uint32_t kBufRecords = 0xffffff00u;
 constexpr uint32_t kBufNone = 0xfffffff0u;
 constexpr int kWaitVm0 = 0x0f70;  // s_waitcnt vmcnt(0) (expcnt, lgkmcnt at max)
-typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* p) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)kBufRecords, 0x00020000);

@@ -90,14 +90,7 @@ __device__ __forceinline__ float head_reduce(float v) {
   return v;
 }
 
-// the same over fp64 values (each 32-bit half moved by DPP)
-template <int CTRL>
-__device__ __forceinline__ double dpp_mov64(double v) {
-  const u32x2 w = __builtin_bit_cast(u32x2, v);
-  const u32x2 r = {(uint32_t)__builtin_amdgcn_update_dpp(0, (int)w.x, CTRL, 0xf, 0xf, false),
-                   (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w.y, CTRL, 0xf, 0xf, false)};
-  return __builtin_bit_cast(double, r);
-}
+// the same over fp64 values (dpp_mov64: common.hpp)
 template <int S>
 __device__ __forceinline__ double head_reduce64(double v) {
   if constexpr (S >= 2) v += dpp_mov64<0xB1>(v);

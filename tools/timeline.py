@@ -1,6 +1,7 @@
 #!/usr/bin/env python
-"""Kernel timeline of a rocprofv3 kernel trace: the last `--span` ms before the
-final kernel, kernels in start order with the idle gap before each.
+"""Kernel timeline of a rocprofv3 kernel trace: the window between the last two
+marker kernels (dot_final_kernel) when there are two, else the last `span` ms
+before the final kernel; kernels in start order with the idle gap before each.
 python tools/timeline.py <run_kernel_trace.csv> [span_ms]"""
 import csv
 import sys
@@ -8,8 +9,13 @@ import sys
 rows = list(csv.DictReader(open(sys.argv[1])))
 span = float(sys.argv[2]) if len(sys.argv) > 2 else 5.0
 ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in rows)
-t_end = ev[-1][1]
-ev = [e for e in ev if e[0] >= t_end - span * 1e6]
+# a marker pair (dot_final_kernel, tools/train_trace.py): the window between the last two
+mk = [i for i, e in enumerate(ev) if "dot_final_kernel" in e[2]]
+if len(mk) >= 2:
+    ev = ev[mk[-2]:mk[-1] + 1]
+else:
+    t_end = ev[-1][1]
+    ev = [e for e in ev if e[0] >= t_end - span * 1e6]
 prev = ev[0][0]
 busy = 0
 for s, e, n in ev:
