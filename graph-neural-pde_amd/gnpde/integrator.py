@@ -491,12 +491,14 @@ class _LaplacianFixedGridFn(torch.autograd.Function):
         else:
             sol[0].copy_(y0d)
             y = y0d
-        # the backward's combination coefficients need a = sigma(alpha) on the host: copied
-        # now, behind an event, so the backward does not drain the queue to read it
         sig = not func.opt.get('no_alpha_sigmoid', False)
         ctx.alpha = func.alpha_train.detach().clone()
         ctx.a_dev = torch.sigmoid(ctx.alpha) if sig else ctx.alpha
-        ctx.a_host = _host_scalar(ctx.a_dev)
+        # rk4's adjoint scales its a-dependent coefficients by a on the device (the stage
+        # epilogue's coef_scale); the other methods' combinations need a on the host: copied
+        # now, behind an event, so the backward does not drain the queue to read it
+        ctx.a_scale = ctx.a_dev.reshape(()).float().contiguous()
+        ctx.a_host = _host_scalar(ctx.a_dev) if method != 'rk4' else None
         try:
             gr = func.graph_for(y0)
             w, tag = func._weights_tensor()
@@ -511,9 +513,17 @@ class _LaplacianFixedGridFn(torch.autograd.Function):
             ctx.x0 = func.stable_x0(y0).clone() if ctx.add_source else None
             starts, stage_inputs = [], []
             j = 1
-            for ta, tb in steps:
+            for n_step, (ta, tb) in enumerate(steps):
                 starts.append(y)
                 ws = _Workspace()  # a fresh one per step: its stage inputs are kept for the backward
+                if n_step == len(steps) - 1 and j == len(t_h) - 1 and t_h[j] == tb:
+                    # the last step writes the result in the caller's numbering (no exit pass;
+                    # the backward never reads the last step's output)
+                    _fused_step(method, func, ta, tb - ta, tb, y, ws, out=sol[j],
+                                out_rows=lay.order32 if lay is not None else None)
+                    stage_inputs.append([ws[k] for k in ('a', 'b', 'c') if k in ws])
+                    j += 1
+                    break
                 y = _fused_step(method, func, ta, tb - ta, tb, y, ws)
                 stage_inputs.append([ws[k] for k in ('a', 'b', 'c') if k in ws])
                 while j < len(t_h) and tb >= t_h[j]:
@@ -535,7 +545,8 @@ class _LaplacianFixedGridFn(torch.autograd.Function):
             one = torch.ones((), dtype=torch.float32, device=g_sol.device)
             sig = ctx.sig
             a_dev = ctx.a_dev
-            a = ctx.a_host()  # the combination coefficients (copied to the host in the forward)
+            a = ctx.a_host() if ctx.a_host is not None else None  # euler / midpoint combinations
+            asc = ctx.a_scale  # rk4: coef_scale of every adjoint launch (cb unscaled, cf and c_j times a)
             add_source = ctx.add_source
             x0 = ctx.x0
 
@@ -578,7 +589,7 @@ class _LaplacianFixedGridFn(torch.autograd.Function):
                     x2, x3, x4 = ctx.stage_inputs[n]
                     e = lambda: torch.empty_like(g)  # noqa: E731
                     v, gk3, u3, gk2, gk1, acc, g_new = (e() for _ in range(7))
-                    c8, ad = dt / 8.0, dt * a
+                    c8 = dt / 8.0
                     T = dict(alpha=one, rhs=True, alpha_sigmoid=False, transpose=True)
                     # d alpha += a'(alpha) (dt/8 <v, x4> + <u3, x3> + <u2, x2> + <u1, y>): the epilogue of
                     # each launch adds its row terms; u2 and u1 are used only inside their own launch
@@ -586,16 +597,17 @@ class _LaplacianFixedGridFn(torch.autograd.Function):
                     # in registers already): gk2 = gk3 + ad u3 - 2 ad c8 v, gk1 = gk2/3 + ad/3 u2 +
                     # 4/3 ad c8 v - 2/3 ad u3, and the running sum carries g (acc = g + a(c8 v + u3 + u2)),
                     # so g is read by the third launch only: 20 state passes per step, not 23
-                    ops.spmm_rhs(gr, w_csc, g, stage=ops.Stage(f_out=v, outs=[(gk3, g, 3 * c8, ad * c8, [])],
-                                                               dot=(x4, drow, c8, True)), **T)
-                    ops.spmm_rhs(gr, w_csc, gk3, stage=ops.Stage(f_out=u3, outs=[(gk2, gk3, 1.0, ad,
-                                                                                  [(v, -2.0 * ad * c8)])],
-                                                                 dot=(x3, drow, 1.0, True)), **T)
+                    # (coefficients written without a: the epilogue multiplies cf and every c_j by *asc)
+                    ops.spmm_rhs(gr, w_csc, g, stage=ops.Stage(f_out=v, outs=[(gk3, g, 3 * c8, dt * c8, [])],
+                                                               dot=(x4, drow, c8, True), scale=asc), **T)
+                    ops.spmm_rhs(gr, w_csc, gk3, stage=ops.Stage(f_out=u3, outs=[(gk2, gk3, 1.0, dt,
+                                                                                  [(v, -2.0 * dt * c8)])],
+                                                                 dot=(x3, drow, 1.0, True), scale=asc), **T)
                     ops.spmm_rhs(gr, w_csc, gk2, stage=ops.Stage(outs=[
-                        (gk1, gk2, 1.0 / 3.0, ad / 3.0, [(v, 4.0 * ad * c8 / 3.0), (u3, -2.0 * ad / 3.0)]),
-                        (acc, g, 1.0, a, [(v, a * c8), (u3, a)])], dot=(x2, drow, 1.0, True)), **T)
-                    ops.spmm_rhs(gr, w_csc, gk1, stage=ops.Stage(outs=[(g_new, acc, 1.0, a, [])],
-                                                                 dot=(y, drow, 1.0, True)), **T)
+                        (gk1, gk2, 1.0 / 3.0, dt / 3.0, [(v, 4.0 * dt * c8 / 3.0), (u3, -2.0 * dt / 3.0)]),
+                        (acc, g, 1.0, 1.0, [(v, c8), (u3, 1.0)])], dot=(x2, drow, 1.0, True), scale=asc), **T)
+                    ops.spmm_rhs(gr, w_csc, gk1, stage=ops.Stage(outs=[(g_new, acc, 1.0, 1.0, [])],
+                                                                 dot=(y, drow, 1.0, True), scale=asc), **T)
                     if add_source:
                         gb = gb + c8 * ops.dot(g, x0) + ops.dot(gk3, x0) + ops.dot(gk2, x0) + ops.dot(gk1, x0)
                     g = g_new
