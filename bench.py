@@ -415,7 +415,8 @@ def roofline(launch_ms, algorithmic, traffic_b, kernel, compulsory=None):
     if traffic_b:
         ach = traffic_b / t / 1e9
         out.update({"achieved": round(ach, 1), "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": int(traffic_b),
-                    "basis": "PMC bytes per launch (%s, 2*FETCH_SIZE+WRITE_SIZE) / HIP-event launch time" %
+                    "basis": "PMC bytes per launch (%s, 2*FETCH_SIZE+WRITE_SIZE; the counters include Infinity-Cache "
+                             "hits, so frac bounds HBM traffic from above) / HIP-event launch time" %
                              TRAFFIC_FILE})
         if compulsory:
             out["refetch_ratio"] = round(traffic_b / compulsory, 3)
@@ -683,7 +684,8 @@ def bench_attention(g, x, dev, ops, reps=20):
         if tb:
             ent.update({"traffic": int(tb), "achieved_GBs": round(tb / t / 1e9, 1),
                         "frac": round(tb / t / 1e9 / HBM_PEAK_GBS, 4),
-                        "basis": "PMC bytes of every kernel of one RHS (%s workload attn:%s_norm%d, same numbering) / "
+                        "basis": "PMC bytes of every kernel of one RHS (%s workload attn:%s_norm%d, same numbering; "
+                                 "counters include Infinity-Cache hits: an upper bound of HBM bytes) / "
                                  "replayed RHS time" % (TRAFFIC_FILE, mode, norm_idx)})
         else:
             ent.update({"traffic": None, "frac": None, "basis": "no PMC traffic in %s" % TRAFFIC_FILE})
@@ -749,7 +751,8 @@ def bench_blend(g, dev, reps=50):
             # K1 launches at ~the step's time / 4: the counter bytes of the four over the step time
             ent.update({"k1": BLEND_K1[name], "traffic_per_step": int(4 * kb),
                         "frac": round(4 * kb / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                        "basis": "PMC bytes of the 4 K1 launches of a step (%s workload blend_%s) / step time" %
+                        "basis": "PMC bytes of the 4 K1 launches of a step (%s workload blend_%s; counters include "
+                                 "Infinity-Cache hits: an upper bound of HBM bytes) / step time" %
                                  (TRAFFIC_FILE, name)})
         out[name] = ent
     a, b = res["fp32"].double(), res["bf16"].double()
