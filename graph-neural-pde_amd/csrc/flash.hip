@@ -793,6 +793,131 @@ __global__ __launch_bounds__(256) void dot_dst_agg_kernel(const int4* __restrict
   (void)dpart;
 }
 
+// The one-pass form of the destination-grouped kernel (round 4, A/B knob
+// GNPDE_FL_DST1, off): each batch of U edges gathers the edges' x rows, their
+// k-row score tiles and their statistics records together, then weights and
+// accumulates (as dot_agg1_kernel; the score bits are those of tile_scores).
+// Measured: per-edge norm_idx 1 RHS 0.1706 against 0.1731 ms in the solve's
+// numbering, 0.1938 against 0.1851 in the user numbering (the per-batch record
+// loads) — not taken.
+#ifndef GNPDE_FL_DST1
+#define GNPDE_FL_DST1 0
+#endif
+template <int GL, int U, int ATT, int H, int STG>
+__global__ __launch_bounds__(256) void dot_dst_agg1_kernel(const int4* __restrict__ items, int n_items, int4* heavy,
+                                                            int n_heavy, const int* __restrict__ col, DotArgs da,
+                                                            const float* __restrict__ rec, int C, Epi ep,
+                                                            float* __restrict__ partials) {
+  constexpr int RPW = kWave / GL;
+  constexpr int SL = GL;
+  constexpr int RF = stats_record_floats(H);
+  constexpr int NA = ATT / 4;
+  constexpr int S = NA / H;
+  constexpr int EPI = SL / NA;
+  constexpr int TL = (U + EPI - 1) / EPI;
+  static_assert(NA <= SL && S >= 1 && S <= 16 && (S & (S - 1)) == 0, "dot_dst_agg1: score tile layout");
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int rs = lane / SL, sl = lane % SL;
+  const int wid = uniform(blockIdx.x * kWavesPerBlock + wv);
+  const int item = wid * RPW + rs;
+  if (wid * RPW >= n_items) return;
+  const bool live = item < n_items;
+  const int4 it = live ? items[item] : make_int4(0, 0, 0, -1);
+  const int row = it.x, beg = it.y, end = it.z, slot = it.w;
+  const int cc = sl * 4;
+  const bool owner = live && slot < 0 && cc < C;
+  const int base = rs * SL;
+  const int sub = sl % NA, eo = sl / NA;
+
+  EpiPre<4, float, STG> pre;
+  if (owner) epi_prefetch<4, STG, float>(ep, row, cc, pre);
+  float qv[4];
+  load_vec<4>(da.q + (int64_t)row * da.ldqk + 4 * sub, qv);
+  const int len = end - beg;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int e0 = 0; e0 < len; e0 += SL) {
+    const int n = min(SL, len - e0);
+    const int mc = sl < n ? col[beg + e0 + sl] : 0;
+    for (int j = 0; j < n; j += U) {
+      float v[U][4], kt[TL][4], rm[U][H], rr[U][H];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int jj = j + u;
+        const int c = __shfl(mc, base + (jj < n ? jj : 0));
+        if (jj < n && cc < C) {
+          load_vec<4>(ep.x + (int64_t)c * ep.ldx + cc, v[u]);
+        } else {
+#pragma unroll
+          for (int t = 0; t < 4; ++t) v[u][t] = 0.f;
+        }
+        // the destination's statistics record (one line; the same address across the slot)
+        if constexpr (RF == 4 && H == 2) {
+          const float4 r4 = *reinterpret_cast<const float4*>(rec + (int64_t)c * 4);
+          rm[u][0] = r4.x; rm[u][1] = r4.y; rr[u][0] = r4.z; rr[u][1] = r4.w;
+        } else {
+#pragma unroll
+          for (int h = 0; h < H; ++h) {
+            rm[u][h] = rec[(int64_t)c * RF + h];
+            rr[u][h] = rec[(int64_t)c * RF + H + h];
+          }
+        }
+      }
+#pragma unroll
+      for (int g = 0; g < TL; ++g) {
+        const int ue = g * EPI + eo;
+        const int jj = j + ue;
+        const int c = __shfl(mc, base + (jj < n ? jj : 0));
+        if (ue < U && jj < n) {
+          load_vec<4>(da.k + (int64_t)c * da.ldqk + 4 * sub, kt[g]);
+        } else {
+#pragma unroll
+          for (int t = 0; t < 4; ++t) kt[g][t] = 0.f;
+        }
+      }
+      float dt[TL];
+#pragma unroll
+      for (int g = 0; g < TL; ++g) {
+        float d = qv[0] * kt[g][0];
+        d = fmaf(qv[1], kt[g][1], d);
+        d = fmaf(qv[2], kt[g][2], d);
+        d = fmaf(qv[3], kt[g][3], d);
+        dt[g] = head_reduce<S>(d) * da.scale;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        float w = 0.f;
+#pragma unroll
+        for (int h = 0; h < H; ++h) {
+          const float sh = __shfl(dt[u / EPI], base + (u % EPI) * NA + h * S);
+          w = fmaf(__builtin_amdgcn_exp2f(sh - rm[u][h] * kLog2e), rr[u][h], w);
+        }
+        constexpr float inv_h = 1.0f / (float)H;
+        w = j + u < n ? w * inv_h : 0.f;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc[t] = fmaf(w, v[u][t], acc[t]);
+      }
+    }
+  }
+  if (n_heavy > 0) {  // hub chunks: write-through partials, merged in-launch by the last arrival (K1's)
+    const bool chunk = live && slot >= 0;
+    int anyc = 0;
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) anyc |= __shfl((int)chunk, r * SL);
+    if (anyc) {  // wave-uniform
+      const __amdgpu_buffer_rsrc_t rp = buf_rsrc(partials);
+      buf_store_wt<4>(rp, (chunk && cc < C) ? (uint32_t)(((int64_t)slot * C + cc) * 4) : kBufNone, acc);
+      hub_arrive_slots<4, GL, SL, RPW, STG, float>(heavy, n_heavy, chunk, slot, C, ep, partials);
+      if (chunk) return;
+    }
+  }
+  if (!live || slot >= 0) return;
+  const float a = (ep.flags & GNPDE_EPI_RHS) ? epi_alpha(ep) : 1.f;
+  const float b = (ep.flags & GNPDE_ADD_SOURCE) ? *ep.beta : 0.f;
+  double dpart = 0.0;
+  if (owner) epi_finish<4, STG, float>(ep, row, cc, acc, a, b, pre, &dpart);
+  (void)dpart;
+}
+
 template <int GL, int NA, int S, int H>
 static int launch_dot_nh(const int4* items, int64_t n_items, int4* heavy, int64_t n_heavy, const int* col,
                          const DotArgs& da, const float* rec, int C, const Epi& ep, float* partials, hipStream_t s) {
@@ -802,6 +927,18 @@ static int launch_dot_nh(const int4* items, int64_t n_items, int4* heavy, int64_
   const int stg = epi_stage_kind(ep);
   const int nh = (int)n_heavy;
   if (rec != nullptr) {  // destination-grouped softmax (norm_idx 1): statistics records given
+    if constexpr (GNPDE_FL_DST1 && 4 * NA <= 4 * GL) {
+      if (stg <= 1) {
+        if (stg == 1)
+          dot_dst_agg1_kernel<GL, U, 4 * NA, H, 1><<<grid, kBlock, 0, s>>>(items, (int)n_items, heavy, nh, col, da,
+                                                                            rec, C, ep, partials);
+        else
+          dot_dst_agg1_kernel<GL, U, 4 * NA, H, 0><<<grid, kBlock, 0, s>>>(items, (int)n_items, heavy, nh, col, da,
+                                                                            rec, C, ep, partials);
+        GNPDE_LAUNCH_CHECK();
+        return GNPDE_OK;
+      }
+    }
     if (stg == 1)
       dot_dst_agg_kernel<GL, U, NA, S, H, 1><<<grid, kBlock, 0, s>>>(items, (int)n_items, heavy, nh, col, da, rec, C,
                                                                       ep, partials);
