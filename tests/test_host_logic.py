@@ -253,6 +253,71 @@ def test_seg_plan_build_tiles_edges(eb):
             assert a[1] - a[0] + first_len > eb
 
 
+def test_reference_statistics_plan_hub_chunks():
+    """gnpde.ops.build_seg_plan(long_items=True) (host only; the plan of the
+    reference statistics, ABI 4): groups over seg_long_max() edges become
+    seg_long_max()-edge HUB CHUNK items {e_begin, e_end, slot, hub} at the front
+    (longest hub first, chunks of a hub consecutive and tiling it), the hub table
+    {group, first_slot, n_chunks, 0} indexes them, groups of eb+1..seg_long_max()
+    edges are LONG items {.., -2, group} longest first, the rest whole-group items;
+    every edge is covered once."""
+    from gnpde import ops
+    L = ops.seg_long_max()
+    eb = 64
+    rng = np.random.default_rng(5)
+    deg = rng.integers(0, 20, size=4000)
+    deg[[7, 100, 2500]] = [3 * L + 17, L + 1, 5 * L]  # hubs
+    deg[[11, 12]] = [L, eb + 1]                      # long items at both ends of the range
+    rp = np.zeros(len(deg) + 1, np.int32)
+    rp[1:] = np.cumsum(deg)
+    plan = ops.build_seg_plan(torch.from_numpy(rp), eb, long_items=True)
+    it = plan.items.numpy().reshape(-1, 4)[:plan.n_items]
+    hv = plan.heavy.numpy().reshape(-1, 4)[:plan.n_heavy]
+    nh, nl = plan.n_hub, plan.n_long
+    assert plan.n_chunk == 0 and plan.n_slots == nh
+    assert hv[:, 0].tolist() == [2500, 7, 100]  # longest hub first
+    assert (hv[:, 3] == 0).all() and hv[:, 2].tolist() == [5, 4, 2]
+    for k, (grp, first, nch, _) in enumerate(hv):
+        ch = it[first:first + nch]
+        assert (ch[:, 2] == np.arange(first, first + nch)).all() and (ch[:, 3] == k).all()
+        assert ch[0, 0] == rp[grp] and ch[-1, 1] == rp[grp + 1] and (ch[1:, 0] == ch[:-1, 1]).all()
+        assert ((ch[:, 1] - ch[:, 0]) <= L).all()
+    assert hv[0, 1] == 0 and (hv[1:, 1] == hv[:-1, 1] + hv[:-1, 2]).all() and hv[-1, 1] + hv[-1, 2] == nh
+    lg = it[nh:nh + nl]
+    ln = lg[:, 1] - lg[:, 0]
+    assert (lg[:, 2] == -2).all() and (ln > eb).all() and (ln <= L).all() and (np.diff(ln) <= 0).all()
+    assert {11, 12} <= set(lg[:, 3].tolist())
+    sh = it[nh + nl:]
+    assert (sh[:, 2] == -1).all() and ((sh[:, 1] - sh[:, 0]) <= eb).all()
+    spans = it[:, :2][np.argsort(it[:, 0], kind="stable")]
+    assert spans[0, 0] == 0 and spans[-1, 1] == rp[-1] and (spans[1:, 0] == spans[:-1, 1]).all()
+
+
+def test_rk4_adjoint_reformulation_is_the_same_algebra():
+    """The rk4 adjoint launches (integrator._LaplacianFixedGridFn.backward) form
+    gk2 from gk3, gk1 from gk2 and carry g in the running sum, so that each launch
+    reads few rows; restated with the (A^T - I) applications as free vectors, the
+    combinations equal the textbook adjoint of the 3/8 rule (float64)."""
+    rng = np.random.default_rng(3)
+    g, v, u3, u2, u1 = (rng.standard_normal(50) for _ in range(5))
+    a, dt = 0.37, 0.25
+    c8, ad = dt / 8.0, dt * a
+    u4 = c8 * v
+    # textbook
+    gk3 = 3 * c8 * g + ad * u4
+    gk2 = 3 * c8 * g - ad * u4 + ad * u3
+    gk1 = c8 * g + ad * u4 - ad / 3 * u3 + ad / 3 * u2
+    g_new = g + a * (u4 + u3 + u2 + u1)
+    # as launched (coefficients without a, times the device scale a)
+    gk3_l = 3 * c8 * g + a * (dt * c8) * v
+    gk2_l = gk3_l + a * dt * u3 + a * (-2.0 * dt * c8) * v
+    gk1_l = gk2_l / 3.0 + a * (dt / 3.0) * u2 + a * (4.0 * dt * c8 / 3.0) * v + a * (-2.0 * dt / 3.0) * u3
+    acc = g + a * u2 + a * c8 * v + a * u3
+    g_new_l = acc + a * u1
+    for x, y in ((gk3, gk3_l), (gk2, gk2_l), (gk1, gk1_l), (g_new, g_new_l)):
+        assert np.allclose(x, y, rtol=1e-13, atol=1e-13)
+
+
 # ---------------------------------------------------------------- ODE-block module layout (reference state_dict)
 @pytest.mark.parametrize("block,extra", [("constant", {}), ("attention", {}), ("mixed", dict(heads=1)),
                                          ("hard_attention", dict(att_samp_pct=0.5))])
