@@ -492,25 +492,8 @@ class _LaplacianFixedGridFn(torch.autograd.Function):
             sol[0].copy_(y0d)
             y = y0d
         sig = not func.opt.get('no_alpha_sigmoid', False)
-        ctx.alpha = func.alpha_train.detach().clone()
-        ctx.a_dev = torch.sigmoid(ctx.alpha) if sig else ctx.alpha
-        # rk4's adjoint scales its a-dependent coefficients by a on the device (the stage
-        # epilogue's coef_scale); the other methods' combinations need a on the host: copied
-        # now, behind an event, so the backward does not drain the queue to read it
-        ctx.a_scale = ctx.a_dev.reshape(()).float().contiguous()
-        ctx.a_host = _host_scalar(ctx.a_dev) if method != 'rk4' else None
         try:
             gr = func.graph_for(y0)
-            w, tag = func._weights_tensor()
-            # a private CSC-order copy: grad mode is off inside a Function's forward,
-            # so the module's cached buffer counts as no_grad-made and a later no_grad call with
-            # new weights would refresh it in place under this node's pending backward
-            src = w.detach().float() if w.dtype != torch.float32 else w.detach()
-            ctx.w_csc = gr.gather_weights(src, transpose=True)
-            ctx.gr = gr
-            ctx.sig = sig
-            ctx.add_source = bool(func.opt.get('add_source', False))
-            ctx.x0 = func.stable_x0(y0).clone() if ctx.add_source else None
             starts, stage_inputs = [], []
             j = 1
             for n_step, (ta, tb) in enumerate(steps):
@@ -529,6 +512,26 @@ class _LaplacianFixedGridFn(torch.autograd.Function):
                 while j < len(t_h) and tb >= t_h[j]:
                     _to_user(y, sol[j], lay)
                     j += 1
+            # The backward's own copies, taken after the forward launches are queued (the GPU
+            # starts on the solve while the host does this; still before this call returns):
+            # alpha (rk4's adjoint scales its a-dependent coefficients by a on the device, the
+            # stage epilogue's coef_scale; the other methods' combinations need a on the host,
+            # copied behind an event so the backward does not drain the queue to read it), and a
+            # private CSC-order copy of the weights (grad mode is off inside a
+            # Function's forward, so the module's cached buffer counts as no_grad-made and a
+            # later no_grad call with new weights would refresh it in place under this node's
+            # pending backward).
+            ctx.alpha = func.alpha_train.detach().clone()
+            ctx.a_dev = torch.sigmoid(ctx.alpha) if sig else ctx.alpha
+            ctx.a_scale = ctx.a_dev.reshape(()).float().contiguous()
+            ctx.a_host = _host_scalar(ctx.a_dev) if method != 'rk4' else None
+            w, tag = func._weights_tensor()
+            src = w.detach().float() if w.dtype != torch.float32 else w.detach()
+            ctx.w_csc = gr.gather_weights(src, transpose=True)
+            ctx.gr = gr
+            ctx.sig = sig
+            ctx.add_source = bool(func.opt.get('add_source', False))
+            ctx.x0 = func.stable_x0(y0).clone() if ctx.add_source else None
         finally:
             func._layout = None
         ctx.func, ctx.method, ctx.steps, ctx.t_h, ctx.lay = func, method, steps, t_h, lay
