@@ -201,6 +201,37 @@ def test_bf16_dopri5_without_torch_combinations(monkeypatch):
     assert rel(zb.float(), z32) <= 2e-2
 
 
+def test_bf16_unfused_adaptive_loop_combines_in_hip(monkeypatch):
+    """The unfused adaptive loop (GNPDE_FUSED_ADAPTIVE=0) on a bf16 state combines
+    its stages with the bf16 stage pass (gnpde_stage_apply_bf16), not torch ops;
+    the combination is the fp32 one rounded once, and the solve stays within bf16
+    rounding of the fp32 solve."""
+    N, E, C = 3000, 30000, 168
+    eo, wo, rng = _graph(N, E, 35)
+    x = T(rng.standard_normal((1, N, C)).astype(np.float32))
+    func = _laplacian(C, eo, wo)
+    t = torch.tensor([0.0, 1.0], dtype=torch.float64, device=DEV)
+    ks = [T(rng.standard_normal((1, N, C)).astype(np.float32)).to(torch.bfloat16) for _ in range(6)]
+    y0 = x.to(torch.bfloat16)
+    coefs = [0.1, -0.2, 0.3, 0.05, -0.7, 0.25]
+    with torch.no_grad():
+        got = gi._Combine()(y0, ks, coefs, 0.5)
+    want = y0.float() + sum(0.5 * c * k.float() for c, k in zip(coefs, ks))
+    assert got.dtype == torch.bfloat16
+    assert (got.float() - want).abs().max().item() <= 2.0 ** -7 * want.abs().max().item()
+
+    def boom(*a, **k):
+        raise AssertionError("_torch_combine on the product path")
+
+    monkeypatch.setattr(gi, "_torch_combine", boom)
+    monkeypatch.setenv("GNPDE_FUSED_ADAPTIVE", "0")
+    with torch.no_grad():
+        z32 = gi.odeint(func, x, t, rtol=1e-3, atol=1e-4, method='dopri5')[1]
+        zb = gi.odeint(func, y0, t, rtol=1e-3, atol=1e-4, method='dopri5')[1]
+    assert zb.dtype == torch.bfloat16
+    assert rel(zb.float(), z32) <= 2e-2
+
+
 def test_attention_rhs_dopri5_fused_vs_unfused(monkeypatch):
     """The transformer RHS (fork scaled_dot, norm_idx 1: weights formed inside K1 from
     the statistics records, a policy the wide epilogue is not fused with) under
