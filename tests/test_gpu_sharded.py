@@ -36,9 +36,27 @@ def grmat():
     alpha = torch.tensor(0.3, device=DEV)
     full = ops.spmm_rhs(g, wc, x, alpha=alpha)
     torch.cuda.synchronize()
+    g.coo = (ei, w)  # the COO the CSR was built from (test_grmat_csr_matches_coo_restatement)
     yield g, wc, x, alpha, full
     del g, wc, x, full
     torch.cuda.empty_cache()
+
+
+def test_grmat_csr_matches_coo_restatement(grmat):
+    """at configs[4] size the CSR itself (rowptr, col, perm) and the
+    CSR-order weights equal a restatement from the COO edge list with torch ops (a
+    stable sort by source: in-row order = COO order), so the sampled oracle check
+    below is anchored on the edge list, not on the product's own structure."""
+    g, wc, x, alpha, full = grmat
+    ei, w = g.coo
+    src, dst = ei[0, 0].long(), ei[0, 1].long()
+    order = torch.argsort(src, stable=True)
+    assert torch.equal(g.csr.perm.long(), order)
+    assert torch.equal(g.csr.col.long(), dst[order])
+    rp = torch.zeros(N + 1, dtype=torch.int64, device=DEV)
+    rp[1:] = torch.cumsum(torch.bincount(src, minlength=N), 0)
+    assert torch.equal(g.csr.rowptr.long(), rp)
+    assert torch.equal(wc.view(-1), w.view(-1)[order])
 
 
 @pytest.mark.parametrize("world", [2, 8])
