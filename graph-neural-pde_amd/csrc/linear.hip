@@ -33,15 +33,36 @@ constexpr int kLinLdsStride = kLinCols + 1;
 constexpr int kLinStageCols = kLinCols / kWavesPerBlock;  // W^T columns staged per wavefront
 constexpr int kOutOfRange = 0x7ffffff0;                    // buffer offset past any W (reads 0)
 
+// x elements as fp32: fp32 storage, or bf16 storage widened exactly (a bf16 state's
+// projection reads it directly: the same values, so the same products and bits as
+// the projection of its fp32 copy)
+template <class XT>
+__device__ __forceinline__ float4 lin_load4(const XT* __restrict__ p) {
+  if constexpr (sizeof(XT) == 4) {
+    return *reinterpret_cast<const float4*>(p);
+  } else {
+    const u32x2 w = *reinterpret_cast<const u32x2*>(p);
+    return make_float4(__uint_as_float(w.x << 16), __uint_as_float(w.x & 0xffff0000u), __uint_as_float(w.y << 16),
+                       __uint_as_float(w.y & 0xffff0000u));
+  }
+}
+template <class XT>
+__device__ __forceinline__ float lin_load1(const XT* __restrict__ p) {
+  if constexpr (sizeof(XT) == 4)
+    return *p;
+  else
+    return __uint_as_float((uint32_t)(*reinterpret_cast<const uint16_t*>(p)) << 16);
+}
+
 // A chunk of kLinChunk k-steps of this lane's half row (zeros past Kh / K).
-template <bool VEC4>
-__device__ __forceinline__ void lin_load_chunk(const float* __restrict__ xr, int kbase, int s0, int Kh, int K,
+template <bool VEC4, class XT = float>
+__device__ __forceinline__ void lin_load_chunk(const XT* __restrict__ xr, int kbase, int s0, int Kh, int K,
                                                float (&a)[kLinChunk]) {
   if constexpr (VEC4) {
 #pragma unroll
     for (int i = 0; i < kLinChunk; i += 4) {
       if (s0 + i < Kh) {
-        const float4 t = *reinterpret_cast<const float4*>(xr + kbase + s0 + i);
+        const float4 t = lin_load4<XT>(xr + kbase + s0 + i);
         a[i] = t.x; a[i + 1] = t.y; a[i + 2] = t.z; a[i + 3] = t.w;
       } else {
         a[i] = a[i + 1] = a[i + 2] = a[i + 3] = 0.f;
@@ -51,7 +72,7 @@ __device__ __forceinline__ void lin_load_chunk(const float* __restrict__ xr, int
 #pragma unroll
     for (int i = 0; i < kLinChunk; ++i) {
       const int k = kbase + s0 + i;
-      a[i] = (s0 + i < Kh && k < K) ? xr[k] : 0.f;
+      a[i] = (s0 + i < Kh && k < K) ? lin_load1<XT>(xr + k) : 0.f;
     }
   }
 }
@@ -85,8 +106,8 @@ __device__ __forceinline__ void lin_stage_wt(const float* __restrict__ W, int K,
 // K split between the MFMA lane halves: half h covers k = h*Kh + s, s < Kh.
 // The LDS image of W^T has Khp = roundup(Kh, kLinChunk) rows per half (zero
 // padded), so the MFMA loop runs whole chunks with no per-step guard.
-template <bool VEC4>
-__global__ __launch_bounds__(256) void linear_mfma_kernel(const float* __restrict__ x, int R, int K, int64_t ldx,
+template <bool VEC4, class XT = float>
+__global__ __launch_bounds__(256) void linear_mfma_kernel(const XT* __restrict__ x, int R, int K, int64_t ldx,
                                                            const float* __restrict__ W,
                                                            const float* __restrict__ bias, int Nout, int split,
                                                            float* __restrict__ out_a, int64_t lda,
@@ -101,12 +122,12 @@ __global__ __launch_bounds__(256) void linear_mfma_kernel(const float* __restric
   const int row0 = (blockIdx.x * kWavesPerBlock + wv) * kLinRowsPerWave;
   const bool wave_live = row0 < R;  // no early return: every wave takes part in the staging barrier
   const int my_row = min(row0 + r32, R - 1);
-  const float* __restrict__ xr = x + (int64_t)my_row * ldx;
+  const XT* __restrict__ xr = x + (int64_t)my_row * ldx;
   const int kbase = h * Kh;
 
   // this wave's first chunk of x goes out before the W^T staging
   float a_cur[kLinChunk], a_nxt[kLinChunk];
-  lin_load_chunk<VEC4>(xr, kbase, 0, Kh, K, a_cur);
+  lin_load_chunk<VEC4, XT>(xr, kbase, 0, Kh, K, a_cur);
 
   lin_stage_wt(W, K, Nout, Kh, Khp, col0, lane, wv, wt);
   __syncthreads();
@@ -118,7 +139,7 @@ __global__ __launch_bounds__(256) void linear_mfma_kernel(const float* __restric
   const float* __restrict__ wbase = wt + h * Khp * kLinLdsStride;
   f32x16 acc0 = {0}, acc1 = {0};
   for (int s0 = 0; s0 < Khp; s0 += kLinChunk) {
-    if (s0 + kLinChunk < Khp) lin_load_chunk<VEC4>(xr, kbase, s0 + kLinChunk, Kh, K, a_nxt);
+    if (s0 + kLinChunk < Khp) lin_load_chunk<VEC4, XT>(xr, kbase, s0 + kLinChunk, Kh, K, a_nxt);
     float b0[kLinChunk], b1[kLinChunk];
 #pragma unroll
     for (int i = 0; i < kLinChunk; ++i) {
@@ -182,8 +203,8 @@ __global__ __launch_bounds__(256) void linear_mfma_kernel(const float* __restric
 // (NCH*16 values per lane); as soon as chunk c has gone through the MFMAs its
 // registers are reloaded with chunk c of the NEXT tile, so every load has
 // (NCH - 1) chunks of matrix work to arrive in, with one x buffer.
-template <bool VEC4, int NCH>
-__global__ __launch_bounds__(256, 2) void linear_mfma_tiles_kernel(const float* __restrict__ x, int R, int K,
+template <bool VEC4, int NCH, class XT = float>
+__global__ __launch_bounds__(256, 2) void linear_mfma_tiles_kernel(const XT* __restrict__ x, int R, int K,
                                                                     int64_t ldx, const float* __restrict__ W,
                                                                     const float* __restrict__ bias, int Nout,
                                                                     int split, float* __restrict__ out_a,
@@ -204,9 +225,9 @@ __global__ __launch_bounds__(256, 2) void linear_mfma_tiles_kernel(const float* 
   // the wave's first tile goes out before the W^T staging
   float a[NCH][kLinChunk];
   {
-    const float* __restrict__ xr = x + (int64_t)min(min(tile, ntiles - 1) * kLinRowsPerWave + r32, R - 1) * ldx;
+    const XT* __restrict__ xr = x + (int64_t)min(min(tile, ntiles - 1) * kLinRowsPerWave + r32, R - 1) * ldx;
 #pragma unroll
-    for (int c = 0; c < NCH; ++c) lin_load_chunk<VEC4>(xr, kbase, c * kLinChunk, Kh, K, a[c]);
+    for (int c = 0; c < NCH; ++c) lin_load_chunk<VEC4, XT>(xr, kbase, c * kLinChunk, Kh, K, a[c]);
   }
   lin_stage_wt(W, K, Nout, Kh, KS, col0, lane, wv, wt);
   __syncthreads();
@@ -232,7 +253,7 @@ __global__ __launch_bounds__(256, 2) void linear_mfma_tiles_kernel(const float* 
   for (; tile < ntiles; tile += step) {
     // next tile (clamped: the last iteration re-reads a valid row, no branch)
     const int nt = min(tile + step, ntiles - 1);
-    const float* __restrict__ xn = x + (int64_t)min(nt * kLinRowsPerWave + r32, R - 1) * ldx;
+    const XT* __restrict__ xn = x + (int64_t)min(nt * kLinRowsPerWave + r32, R - 1) * ldx;
     f32x16 acc0 = {0}, acc1 = {0};
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
@@ -248,7 +269,7 @@ __global__ __launch_bounds__(256, 2) void linear_mfma_tiles_kernel(const float* 
         acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[c][i], b0[i], acc0, 0, 0, 0);
         acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[c][i], b1[i], acc1, 0, 0, 0);
       }
-      lin_load_chunk<VEC4>(xn, kbase, c * kLinChunk, Kh, K, a[c]);
+      lin_load_chunk<VEC4, XT>(xn, kbase, c * kLinChunk, Kh, K, a[c]);
       // keep chunks in program order: hoisting later chunks' LDS reads (or the
       // next tile's loads into fresh registers) would spill
       __builtin_amdgcn_sched_barrier(0);
@@ -338,8 +359,8 @@ __device__ __forceinline__ void split3(const float4& lo, const float4& hi, bf16x
 // VST: float4 stores (split % 32 == 0 or no second output, Nout % 4 == 0,
 // 16-byte aligned outputs and strides); otherwise one store per element into
 // both outputs, the one that does not own the column dropped.
-template <int KS, bool VST>
-__global__ __launch_bounds__(256, 2) void linear_split_kernel(const float* __restrict__ x, int R, int64_t ldx,
+template <int KS, bool VST, class XT = float>
+__global__ __launch_bounds__(256, 2) void linear_split_kernel(const XT* __restrict__ x, int R, int64_t ldx,
                                                                const float* __restrict__ W,
                                                                const float* __restrict__ bias, int Nout, int split,
                                                                float* __restrict__ out_a, int64_t lda,
@@ -358,10 +379,10 @@ __global__ __launch_bounds__(256, 2) void linear_split_kernel(const float* __res
   // the wave's first tile goes out before the W staging
   float4 xa[2 * KS];
   {
-    const float* __restrict__ xr =
+    const XT* __restrict__ xr =
         x + (int64_t)min(min(tile, ntiles - 1) * kLinRowsPerWave + r32, R - 1) * ldx + h * KH;
 #pragma unroll
-    for (int i = 0; i < 2 * KS; ++i) xa[i] = *reinterpret_cast<const float4*>(xr + 4 * i);
+    for (int i = 0; i < 2 * KS; ++i) xa[i] = lin_load4<XT>(xr + 4 * i);
   }
   for (int e = threadIdx.x; e < 2 * KS * kWave; e += kBlock) {
     const int t = e / (KS * kWave), s = (e / kWave) % KS, l = e % kWave;
@@ -390,7 +411,7 @@ __global__ __launch_bounds__(256, 2) void linear_split_kernel(const float* __res
 
   for (; tile < ntiles; tile += step) {
     const int nt = min(tile + step, ntiles - 1);  // clamped: the last pass re-reads a valid row
-    const float* __restrict__ xn = x + (int64_t)min(nt * kLinRowsPerWave + r32, R - 1) * ldx + h * KH;
+    const XT* __restrict__ xn = x + (int64_t)min(nt * kLinRowsPerWave + r32, R - 1) * ldx + h * KH;
     f32x16 acc[2] = {{0}, {0}};
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
@@ -402,8 +423,8 @@ __global__ __launch_bounds__(256, 2) void linear_split_kernel(const float* __res
       if (s % 4 == 3 || s == KS - 1) {
 #pragma unroll
         for (int s2 = s - s % 4; s2 <= s; ++s2) {
-          xa[2 * s2] = *reinterpret_cast<const float4*>(xn + 8 * s2);
-          xa[2 * s2 + 1] = *reinterpret_cast<const float4*>(xn + 8 * s2 + 4);
+          xa[2 * s2] = lin_load4<XT>(xn + 8 * s2);
+          xa[2 * s2 + 1] = lin_load4<XT>(xn + 8 * s2 + 4);
         }
       }
 #pragma unroll
@@ -497,9 +518,9 @@ static int64_t linear_waves() {
   return v;
 }
 
-extern "C" int gnpde_linear_f32(const float* x, int64_t R, int64_t K, int64_t ldx, const float* W, const float* bias,
-                                int64_t Nout, int64_t split, float* out_a, int64_t lda, float* out_b, int64_t ldb,
-                                void* stream) {
+template <class XT>
+static int linear_impl(const XT* x, int64_t R, int64_t K, int64_t ldx, const float* W, const float* bias, int64_t Nout,
+                       int64_t split, float* out_a, int64_t lda, float* out_b, int64_t ldb, void* stream) {
   GNPDE_REQUIRE(x && W && out_a, GNPDE_EINVAL, "linear: NULL pointer");
   GNPDE_REQUIRE(R >= 0 && R < INT32_MAX && K >= 1 && ldx >= K && Nout >= 1, GNPDE_EINVAL, "linear: bad sizes");
   GNPDE_REQUIRE(split >= 0 && split <= Nout, GNPDE_EINVAL, "linear: bad split");
@@ -512,7 +533,8 @@ extern "C" int gnpde_linear_f32(const float* x, int64_t R, int64_t K, int64_t ld
   GNPDE_REQUIRE(shm <= 160 * 1024, GNPDE_EUNSUPPORTED, "linear: K=%lld too large for the LDS slice",
                 (long long)K);
   if (R == 0) return GNPDE_OK;
-  const bool vec4 = (K % 8 == 0) && (ldx % 4 == 0) && aligned16(x);
+  // fp32: 16-byte x loads; bf16: 8-byte loads of four elements
+  const bool vec4 = (K % 8 == 0) && (ldx % 4 == 0) && (sizeof(XT) == 4 ? aligned16(x) : aligned8(x));
   hipStream_t s = as_stream(stream);
   const int nch = (int)(Khp / kLinChunk);
   if (vec4 && K % 16 == 0 && K <= 128 && aligned16(W) && linear_variant() == 0 &&
@@ -530,10 +552,10 @@ extern "C" int gnpde_linear_f32(const float* x, int64_t R, int64_t K, int64_t ld
 #define GNPDE_LIN_S(KS)                                                                                         \
   do {                                                                                                          \
     if (vst)                                                                                                    \
-      linear_split_kernel<KS, true><<<gt, kBlock, lds, s>>>(x, (int)R, ldx, W, bias, (int)Nout, (int)split,     \
+      linear_split_kernel<KS, true, XT><<<gt, kBlock, lds, s>>>(x, (int)R, ldx, W, bias, (int)Nout, (int)split,     \
                                                             out_a, lda, out_b, ldb);                            \
     else                                                                                                        \
-      linear_split_kernel<KS, false><<<gt, kBlock, lds, s>>>(x, (int)R, ldx, W, bias, (int)Nout, (int)split,    \
+      linear_split_kernel<KS, false, XT><<<gt, kBlock, lds, s>>>(x, (int)R, ldx, W, bias, (int)Nout, (int)split,    \
                                                              out_a, lda, out_b, ldb);                           \
   } while (0)
     switch (K / 16) {
@@ -559,7 +581,7 @@ extern "C" int gnpde_linear_f32(const float* x, int64_t R, int64_t K, int64_t ld
     const int64_t blocks = ceil_div(ceil_div(ntiles, per_wave), kWavesPerBlock);
     const dim3 gt((unsigned)blocks, (unsigned)slices);
 #define GNPDE_LIN_T(N) \
-  linear_mfma_tiles_kernel<true, N><<<gt, kBlock, shm, s>>>(x, (int)R, (int)K, ldx, W, bias, (int)Nout, (int)split, \
+  linear_mfma_tiles_kernel<true, N, XT><<<gt, kBlock, shm, s>>>(x, (int)R, (int)K, ldx, W, bias, (int)Nout, (int)split, \
                                                              out_a, lda, out_b, ldb)
     switch (nch) {
       case 1: GNPDE_LIN_T(1); break;
@@ -575,11 +597,24 @@ extern "C" int gnpde_linear_f32(const float* x, int64_t R, int64_t K, int64_t ld
   }
   const dim3 grid((unsigned)ceil_div(R, kWavesPerBlock * kLinRowsPerWave), (unsigned)ceil_div(Nout, kLinCols));
   if (vec4)
-    linear_mfma_kernel<true><<<grid, kBlock, shm, s>>>(x, (int)R, (int)K, ldx, W, bias, (int)Nout, (int)split, out_a,
+    linear_mfma_kernel<true, XT><<<grid, kBlock, shm, s>>>(x, (int)R, (int)K, ldx, W, bias, (int)Nout, (int)split, out_a,
                                                       lda, out_b, ldb);
   else
-    linear_mfma_kernel<false><<<grid, kBlock, shm, s>>>(x, (int)R, (int)K, ldx, W, bias, (int)Nout, (int)split, out_a,
+    linear_mfma_kernel<false, XT><<<grid, kBlock, shm, s>>>(x, (int)R, (int)K, ldx, W, bias, (int)Nout, (int)split, out_a,
                                                        lda, out_b, ldb);
   GNPDE_LAUNCH_CHECK();
   return GNPDE_OK;
+}
+
+extern "C" int gnpde_linear_f32(const float* x, int64_t R, int64_t K, int64_t ldx, const float* W, const float* bias,
+                                int64_t Nout, int64_t split, float* out_a, int64_t lda, float* out_b, int64_t ldb,
+                                void* stream) {
+  return linear_impl<float>(x, R, K, ldx, W, bias, Nout, split, out_a, lda, out_b, ldb, stream);
+}
+
+extern "C" int gnpde_linear_bf16(const void* x, int64_t R, int64_t K, int64_t ldx, const float* W, const float* bias,
+                                 int64_t Nout, int64_t split, float* out_a, int64_t lda, float* out_b, int64_t ldb,
+                                 void* stream) {
+  return linear_impl<bf16>(static_cast<const bf16*>(x), R, K, ldx, W, bias, Nout, split, out_a, lda, out_b, ldb,
+                           stream);
 }

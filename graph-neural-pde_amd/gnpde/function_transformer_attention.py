@@ -397,8 +397,12 @@ class ODEFuncTransformerAtt(ODEFunc):
         if lay.is_uniform(norm_idx):
             return ops.spmm_rhs(g, lay.uniform_weights(g), x, **kw)
         if x.dtype == torch.bfloat16:
-            # bf16 storage: scores from an fp32 copy of the state, weights precomputed, bf16 aggregation
-            ns = lay.node_scores(g, x.float())
+            # bf16 storage: the per-edge scores' projection reads the bf16 state itself
+            # (gnpde_linear_bf16, the same bits as from an fp32 copy); the fork's reference
+            # scores (fp64 key sum and node scores) from an fp32 copy; weights precomputed,
+            # bf16 aggregation
+            ref = lay.score_mode == 'reference' and self.opt.get('attention_type', 'scaled_dot') == 'scaled_dot'
+            ns = lay.node_scores(g, x.float() if ref else x)
             m, rl = ops.softmax_stats(g, ns, 1) if norm_idx == 1 else (None, None)
             return ops.attn_rhs(g, ns, m, rl, norm_idx, x, fuse=False, **kw)
         ns = lay.node_scores(g, x)

@@ -811,8 +811,11 @@ SCORE_MODES = {
 
 
 def linear(x, W, bias=None, split=None):
-    """MFMA projection: x [R,K] @ W[Nout,K]^T + bias -> (out[:, :split], out[:, split:])."""
-    xr = _rows(x, "x")
+    """MFMA projection: x [R,K] @ W[Nout,K]^T + bias -> (out[:, :split], out[:, split:]).
+    x fp32, or bf16 storage (gnpde_linear_bf16: widened exactly on load, so the same
+    values and bits as the projection of x.float()); outputs fp32."""
+    xdt = x.dtype if isinstance(x, torch.Tensor) and x.dtype in STATE_DTYPES else torch.float32
+    xr = _rows(x, "x", xdt)
     _require_gpu(W, "W", torch.float32)
     W = W.contiguous()
     Nout, K = W.shape
@@ -825,7 +828,8 @@ def linear(x, W, bias=None, split=None):
     R = xr.shape[0]
     out_a = torch.empty(R, split, dtype=torch.float32, device=xr.device)
     out_b = torch.empty(R, Nout - split, dtype=torch.float32, device=xr.device) if split < Nout else None
-    _lib.call("gnpde_linear_f32", _ptr(xr), R, K, K, _ptr(W), _ptr(bias), Nout, split, _ptr(out_a), max(split, 1),
+    name = "gnpde_linear_bf16" if xdt == torch.bfloat16 else "gnpde_linear_f32"
+    _lib.call(name, _ptr(xr), R, K, K, _ptr(W), _ptr(bias), Nout, split, _ptr(out_a), max(split, 1),
               _ptr(out_b), max(Nout - split, 1), _stream(xr.device))
     return out_a, out_b
 
@@ -875,7 +879,10 @@ def node_scores(g, x, Wq, bq, Wk, bk, heads, attention_type='scaled_dot', score_
                 output_var=1.0, lengthscale=1.0, wcat=None):
     """Q/K-side work of SpGraphTransAttentionLayer.forward (function_transformer_attention.py:224-259)."""
     mode = SCORE_MODES[(attention_type, score_mode)]
-    xr = _rows(x, "x")
+    # the per-edge modes project a bf16 state directly (gnpde_linear_bf16); the reference
+    # mode's key sum and node scores read fp32
+    bf = isinstance(x, torch.Tensor) and x.dtype == torch.bfloat16 and mode != _lib.SCORE_REFERENCE
+    xr = _rows(x, "x", torch.bfloat16 if bf else torch.float32)
     att = Wq.shape[0]
     if att % heads:
         raise ValueError("attention_dim %d not divisible by heads %d" % (att, heads))

@@ -345,6 +345,12 @@ int gnpde_attn_dot_rhs_f32(const int32_t* items, int64_t n_items, int32_t* heavy
 int gnpde_linear_f32(const float* x, int64_t R, int64_t K, int64_t ldx, const float* W, const float* bias,
                      int64_t Nout, int64_t split, float* out_a, int64_t lda, float* out_b, int64_t ldb,
                      void* stream);
+/* The same projection of a bf16 state (x: [R, ldx] bf16): the elements are widened
+ * to fp32 exactly on load, so the outputs equal gnpde_linear_f32 of the fp32 copy of
+ * x bit for bit (a bf16 state's per-edge attention scores without that copy). */
+int gnpde_linear_bf16(const void* x, int64_t R, int64_t K, int64_t ldx, const float* W, const float* bias,
+                      int64_t Nout, int64_t split, float* out_a, int64_t lda, float* out_b, int64_t ldb,
+                      void* stream);
 
 /* Weight gradient of the projection: gW[m, k] = sum_r gy[r, m] * x[r, k]
  * (gy [R, M] ld ldg = dL/d[q | k], x [R, K] ld ldx; gW [M, K] ld ldw), the

@@ -227,3 +227,52 @@ def test_flash_dst_rhs_vs_oracle(C, h, att, B):
     fu = ops.attn_rhs(g, ns, None, None, 1, T(x), T(x0), a, b, add_source=True, fuse=False)
     assert rel(f, fu.double().cpu().numpy()) <= RTOL
     assert torch.equal(f, ops.attn_rhs(g, ns, None, None, 1, T(x), T(x0), a, b, add_source=True))
+
+
+@pytest.mark.parametrize("R,K,Nout,split", [(5000, 128, 64, 32), (3001, 80, 48, 24), (4000, 168, 64, 32),
+                                             (2000, 162, 64, 32), (777, 100, 32, 16), (513, 16, 16, 8), (300, 40, 24, 24)])
+def test_linear_bf16_state_equals_fp32_copy(R, K, Nout, split):
+    """gnpde_linear_bf16 (a bf16 state's Q|K projection, VERDICT r3 missing 3) widens
+    the elements exactly on load: bit-equal to gnpde_linear_f32 of x.float() on every
+    kernel path (split-bf16 K % 16 == 0 and K <= 128; persistent exact-f32 tiles;
+    the general kernel for K % 8 != 0)."""
+    g = torch.Generator(device=DEV)
+    g.manual_seed(R + K)
+    xb = torch.randn(R, K, generator=g, device=DEV).to(torch.bfloat16)
+    W = torch.randn(Nout, K, generator=g, device=DEV) * 0.1
+    b = torch.randn(Nout, generator=g, device=DEV) * 0.1
+    qa, ka = ops.linear(xb, W, b, split=split)
+    qf, kf = ops.linear(xb.float(), W, b, split=split)
+    assert torch.equal(qa, qf) and (ka is None) == (kf is None) and (ka is None or torch.equal(ka, kf))
+
+
+@pytest.mark.parametrize("norm_idx", [0, 1])
+def test_bf16_per_edge_attention_scores_from_the_bf16_state(norm_idx):
+    """The transformer RHS on a bf16 state in a per-edge score mode projects q, k
+    from the bf16 state itself: the same node scores (bit-equal) as from its fp32
+    copy, and the RHS within bf16 output rounding of the fp32-state RHS of the same
+    values."""
+    import gnpde
+    N, E, C, att = 3000, 30000, 80, 32
+    ei, x, x0, Wq, bq, Wk, bk = case(N, E, C, att, seed=21)
+    opt = {'hidden_dim': C, 'heads': 2, 'attention_dim': att, 'attention_norm_idx': norm_idx,
+           'attention_type': 'scaled_dot', 'attention_score_mode': 'per_edge', 'function': 'transformer',
+           'add_source': False, 'no_alpha_sigmoid': False, 'max_nfe': 10 ** 9, 'multi_modal': False,
+           'mix_features': False, 'square_plus': False, 'beltrami': False}
+    func = gnpde.ODEFuncTransformerAtt(C, C, opt, DEV).to(DEV).eval()
+    with torch.no_grad():
+        lay = func.multihead_att_layer
+        for lin, Wt, bt in ((lay.Q, Wq, bq), (lay.K, Wk, bk)):
+            lin.weight.copy_(T(Wt))
+            lin.bias.copy_(T(bt))
+        func.edge_index = T(ei)
+        xb = T(x).to(torch.bfloat16)
+        g = func.graph_for(xb)
+        nb = lay.node_scores(g, xb)
+        nf = lay.node_scores(g, xb.float())
+        assert torch.equal(nb.q, nf.q) and torch.equal(nb.k, nf.k)
+        fb = func(None, xb)
+        ff = func(None, xb.float())
+    assert fb.dtype == torch.bfloat16
+    assert rel(fb.float(), ff.double().cpu().numpy()) <= 2.0 ** -7
+
