@@ -195,7 +195,7 @@ __device__ __forceinline__ float edge_weight(const float (&s)[H], const float (&
 // the columns (C <= 256: 4 per lane).
 __host__ __device__ constexpr int64_t dot_partial_floats(int64_t H, int64_t C) { return (H * C + 2 * H + 3) & ~3; }
 
-template <int H, int STG>
+template <int H, int STG, class T = float>
 __device__ __forceinline__ void dot_hub_combine(int row, int first, int nch, int C, int ps, const Epi& ep,
                                                 const float* __restrict__ partials) {
   const int lane = threadIdx.x & 63;
@@ -241,7 +241,7 @@ __device__ __forceinline__ void dot_hub_combine(int row, int first, int nch, int
   const float a = (ep.flags & GNPDE_EPI_RHS) ? epi_alpha(ep) : 1.f;
   const float b = (ep.flags & GNPDE_ADD_SOURCE) ? *ep.beta : 0.f;
   double dpart = 0.0;
-  if (live) epilogue_store<4, STG, float>(ep, row, cc, ax, a, b, &dpart);
+  if (live) epilogue_store<4, STG, T>(ep, row, cc, ax, a, b, &dpart);
   static_assert(!stage_dot<STG>(), "dot-term epilogues are not fused here");
 }
 
@@ -512,7 +512,7 @@ void dot_agg_kernel(const int4* __restrict__ items, int n_items, int4* heavy, in
 #endif
 using ScoreT = std::conditional_t<GNPDE_FL_SCORE64 != 0, double, float>;
 
-template <int GL, int U, int ATT, int H, int STG>
+template <int GL, int U, int ATT, int H, int STG, class T = float>
 __global__ __launch_bounds__(256) void dot_agg1_kernel(const int4* __restrict__ items, int n_items, int4* heavy,
                                                         int n_heavy, const int* __restrict__ col, DotArgs da, int C,
                                                         Epi ep, float* __restrict__ partials) {
@@ -537,8 +537,8 @@ __global__ __launch_bounds__(256) void dot_agg1_kernel(const int4* __restrict__ 
   const int base = rs * SL;
   const int sub = sl % NA, eo = sl / NA;
 
-  EpiPre<4, float, STG> pre;
-  if (owner) epi_prefetch<4, STG, float>(ep, row, cc, pre);
+  EpiPre<4, T, STG> pre;
+  if (owner) epi_prefetch<4, STG, T>(ep, row, cc, pre);
   float qv[4];  // this lane's slice of the row's q (score tiles, as tile_scores)
   load_vec<4>(da.q + (int64_t)row * da.ldqk + 4 * sub, qv);
 
@@ -562,7 +562,14 @@ __global__ __launch_bounds__(256) void dot_agg1_kernel(const int4* __restrict__ 
         const int jj = j + u;
         const int c = __shfl(mc, base + (jj < n ? jj : 0));
         if (jj < n && cc < C) {
-          load_vec<4>(ep.x + (int64_t)c * ep.ldx + cc, v[u]);
+          if constexpr (sizeof(T) == 4) {
+            load_vec<4>(ep.x + (int64_t)c * ep.ldx + cc, v[u]);
+          } else {  // bf16 state: 8-byte row slices, widened in registers
+            Packed<4, T> pk;
+            load_packed<4>(as_t<T>(ep.x) + (int64_t)c * ep.ldx + cc, pk);
+#pragma unroll
+            for (int t = 0; t < 4; ++t) v[u][t] = unpack(pk, t);
+          }
         } else {
 #pragma unroll
           for (int t = 0; t < 4; ++t) v[u][t] = 0.f;
@@ -666,7 +673,7 @@ __global__ __launch_bounds__(256) void dot_agg1_kernel(const int4* __restrict__ 
           const int hh = __shfl(lo, r * SL);
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
           const int4 hv = heavy[hh];
-          dot_hub_combine<H, STG>(uniform(hv.x), uniform(hv.y), uniform(hv.z), C, ps, ep, partials);
+          dot_hub_combine<H, STG, T>(uniform(hv.x), uniform(hv.y), uniform(hv.z), C, ps, ep, partials);
           if (lane == 0) __hip_atomic_store(&heavy[hh].w, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
       }
@@ -686,7 +693,7 @@ __global__ __launch_bounds__(256) void dot_agg1_kernel(const int4* __restrict__ 
   const float a = (ep.flags & GNPDE_EPI_RHS) ? epi_alpha(ep) : 1.f;
   const float b = (ep.flags & GNPDE_ADD_SOURCE) ? *ep.beta : 0.f;
   double dpart = 0.0;
-  if (owner) epi_finish<4, STG, float>(ep, row, cc, acc, a, b, pre, &dpart);
+  if (owner) epi_finish<4, STG, T>(ep, row, cc, acc, a, b, pre, &dpart);
   (void)dpart;
 }
 
@@ -918,7 +925,7 @@ __global__ __launch_bounds__(256) void dot_dst_agg1_kernel(const int4* __restric
   (void)dpart;
 }
 
-template <int GL, int NA, int S, int H>
+template <int GL, int NA, int S, int H, class T = float>
 static int launch_dot_nh(const int4* items, int64_t n_items, int4* heavy, int64_t n_heavy, const int* col,
                          const DotArgs& da, const float* rec, int C, const Epi& ep, float* partials, hipStream_t s) {
   constexpr int RPW = kWave / GL;
@@ -926,6 +933,21 @@ static int launch_dot_nh(const int4* items, int64_t n_items, int4* heavy, int64_
   const unsigned grid = (unsigned)ceil_div(n_items, (int64_t)kWavesPerBlock * RPW);
   const int stg = epi_stage_kind(ep);
   const int nh = (int)n_heavy;
+  if constexpr (sizeof(T) != 4) {
+    // a bf16 state: the one-pass source-grouped kernel only (the caller takes K2 + the bf16 K1 otherwise)
+    if (rec != nullptr || stg >= 2 || !(GNPDE_FL_ONEPASS && NA <= GL)) {
+      set_error("attn_dot_rhs_bf16: only the source-grouped plain RHS and single-output stages are fused");
+      return GNPDE_EUNSUPPORTED;
+    }
+    if (stg == 1)
+      dot_agg1_kernel<GL, U, 4 * NA, H, 1, T><<<grid, kBlock, 0, s>>>(items, (int)n_items, heavy, nh, col, da, C, ep,
+                                                                      partials);
+    else
+      dot_agg1_kernel<GL, U, 4 * NA, H, 0, T><<<grid, kBlock, 0, s>>>(items, (int)n_items, heavy, nh, col, da, C, ep,
+                                                                      partials);
+    GNPDE_LAUNCH_CHECK();
+    return GNPDE_OK;
+  }
   if (rec != nullptr) {  // destination-grouped softmax (norm_idx 1): statistics records given
     if constexpr (GNPDE_FL_DST1 && 4 * NA <= 4 * GL) {
       if (stg <= 1) {
@@ -978,12 +1000,12 @@ static int launch_dot_nh(const int4* items, int64_t n_items, int4* heavy, int64_
 }
 
 // (att/4, heads) pairs: att in {8, 16, 32, 64}, heads in {1, 2, 4} dividing att/4
-template <int GL>
+template <int GL, class T = float>
 static int launch_dot(int NA, int H, const int4* items, int64_t n_items, int4* heavy, int64_t n_heavy, const int* col,
                       const DotArgs& da, const float* rec, int C, const Epi& ep, float* partials, hipStream_t s) {
 #define GNPDE_DOT(A, HH) \
   if (NA == A && H == HH) \
-    return launch_dot_nh<GL, A, (A / HH), HH>(items, n_items, heavy, n_heavy, col, da, rec, C, ep, partials, s)
+    return launch_dot_nh<GL, A, (A / HH), HH, T>(items, n_items, heavy, n_heavy, col, da, rec, C, ep, partials, s)
   GNPDE_DOT(2, 1); GNPDE_DOT(2, 2);
   GNPDE_DOT(4, 1); GNPDE_DOT(4, 2); GNPDE_DOT(4, 4);
   GNPDE_DOT(8, 1); GNPDE_DOT(8, 2); GNPDE_DOT(8, 4);
@@ -1010,11 +1032,18 @@ int64_t gnpde_attn_dot_workspace_floats(int64_t heads, int64_t C, int64_t n_slot
   return n_slots * dot_partial_floats(heads, C);
 }
 
-int gnpde_attn_dot_rhs_f32(const int32_t* items, int64_t n_items, int32_t* heavy, int64_t n_heavy,
-                           const int32_t* col, const float* q, const float* k, int64_t ldqk, int64_t heads, int64_t dk,
-                           const float* dst_stats, int64_t C, const float* x, int64_t ldx, const float* x0,
-                           int64_t ldx0, const float* alpha, const float* beta, int flags, float* f, int64_t ldf,
-                           float* workspace, int64_t n_slots, const gnpde_stage_epilogue_t* stage, void* stream) {
+}  // extern "C"
+
+// the fp32 entry and its bf16-state twin (x, x0, f and the stage rows bf16; q, k, the
+// statistics and the partials fp32): 16-byte rows of fp32, 8-byte slices of bf16
+template <class T>
+static int attn_dot_rhs_impl(const int32_t* items, int64_t n_items, int32_t* heavy, int64_t n_heavy,
+                             const int32_t* col, const float* q, const float* k, int64_t ldqk, int64_t heads,
+                             int64_t dk, const float* dst_stats, int64_t C, const float* x, int64_t ldx,
+                             const float* x0, int64_t ldx0, const float* alpha, const float* beta, int flags, float* f,
+                             int64_t ldf, float* workspace, int64_t n_slots, const gnpde_stage_epilogue_t* stage,
+                             void* stream) {
+  auto rows_ok = [](const void* p) { return sizeof(T) == 4 ? aligned16(p) : aligned8(p); };
   GNPDE_REQUIRE(gnpde_attn_dot_supported(heads, dk, C), GNPDE_EUNSUPPORTED,
                 "attn_dot_rhs: heads=%lld dk=%lld C=%lld outside the fused kernel (heads in {1, 2, 4}, dk %% 4 == 0, "
                 "heads*dk in {8, 16, 32, 64}, C %% 4 == 0, C <= 256)",
@@ -1033,16 +1062,17 @@ int gnpde_attn_dot_rhs_f32(const int32_t* items, int64_t n_items, int32_t* heavy
                 "attn_dot_rhs: the statistics records must be 16-byte aligned");
   GNPDE_REQUIRE(ldqk >= heads * dk && ldqk % 4 == 0 && aligned16(q) && aligned16(k), GNPDE_EUNSUPPORTED,
                 "attn_dot_rhs: q/k rows must be 16-byte aligned (ldqk %% 4 == 0)");
-  GNPDE_REQUIRE(ldx % 4 == 0 && ldf % 4 == 0 && aligned16(x) && (!f || aligned16(f)) && aligned16(workspace),
-                GNPDE_EUNSUPPORTED, "attn_dot_rhs: x / f rows and the workspace must be 16-byte aligned");
+  GNPDE_REQUIRE(ldx % 4 == 0 && ldf % 4 == 0 && rows_ok(x) && (!f || rows_ok(f)) && aligned16(workspace),
+                GNPDE_EUNSUPPORTED, "attn_dot_rhs: x / f rows (16 bytes fp32, 8 bytes bf16) and the workspace "
+                "must be aligned");
   if (flags & GNPDE_ADD_SOURCE)
-    GNPDE_REQUIRE(ldx0 % 4 == 0 && aligned16(x0), GNPDE_EUNSUPPORTED, "attn_dot_rhs: x0 rows must be 16-byte aligned");
+    GNPDE_REQUIRE(ldx0 % 4 == 0 && rows_ok(x0), GNPDE_EUNSUPPORTED, "attn_dot_rhs: x0 rows must be aligned");
   if (stage) {
-    bool ok = !stage->f_out || aligned16(stage->f_out);
+    bool ok = !stage->f_out || rows_ok(stage->f_out);
     for (int i = 0; i < stage->n_out; ++i) {
-      ok = ok && aligned16(stage->o[i].out) && (!stage->o[i].base || aligned16(stage->o[i].base));
+      ok = ok && rows_ok(stage->o[i].out) && (!stage->o[i].base || rows_ok(stage->o[i].base));
     }
-    for (int j = 0; j < stage->nk; ++j) ok = ok && aligned16(stage->k[j]);
+    for (int j = 0; j < stage->nk; ++j) ok = ok && rows_ok(stage->k[j]);
     GNPDE_REQUIRE(ok && (!stage->dot_rows || aligned16(stage->dot_with)), GNPDE_EUNSUPPORTED,
                   "attn_dot_rhs: stage rows must be 16-byte aligned");
   }
@@ -1058,9 +1088,33 @@ int gnpde_attn_dot_rhs_f32(const int32_t* items, int64_t n_items, int32_t* heavy
   const int lanes = (int)(C / 4);
   const int NA = (int)(heads * dk / 4), H = (int)heads;
   hipStream_t s = as_stream(stream);
-  if (lanes <= 16) return launch_dot<16>(NA, H, it, n_items, hv, n_heavy, col, da, dst_stats, (int)C, ep, workspace, s);
-  if (lanes <= 32) return launch_dot<32>(NA, H, it, n_items, hv, n_heavy, col, da, dst_stats, (int)C, ep, workspace, s);
-  return launch_dot<64>(NA, H, it, n_items, hv, n_heavy, col, da, dst_stats, (int)C, ep, workspace, s);
+  if (lanes <= 16)
+    return launch_dot<16, T>(NA, H, it, n_items, hv, n_heavy, col, da, dst_stats, (int)C, ep, workspace, s);
+  if (lanes <= 32)
+    return launch_dot<32, T>(NA, H, it, n_items, hv, n_heavy, col, da, dst_stats, (int)C, ep, workspace, s);
+  return launch_dot<64, T>(NA, H, it, n_items, hv, n_heavy, col, da, dst_stats, (int)C, ep, workspace, s);
 }
+
+extern "C" {
+
+int gnpde_attn_dot_rhs_f32(const int32_t* items, int64_t n_items, int32_t* heavy, int64_t n_heavy,
+                           const int32_t* col, const float* q, const float* k, int64_t ldqk, int64_t heads, int64_t dk,
+                           const float* dst_stats, int64_t C, const float* x, int64_t ldx, const float* x0,
+                           int64_t ldx0, const float* alpha, const float* beta, int flags, float* f, int64_t ldf,
+                           float* workspace, int64_t n_slots, const gnpde_stage_epilogue_t* stage, void* stream) {
+  return attn_dot_rhs_impl<float>(items, n_items, heavy, n_heavy, col, q, k, ldqk, heads, dk, dst_stats, C, x, ldx,
+                                  x0, ldx0, alpha, beta, flags, f, ldf, workspace, n_slots, stage, stream);
+}
+
+int gnpde_attn_dot_rhs_bf16(const int32_t* items, int64_t n_items, int32_t* heavy, int64_t n_heavy,
+                            const int32_t* col, const float* q, const float* k, int64_t ldqk, int64_t heads,
+                            int64_t dk, const float* dst_stats, int64_t C, const void* x, int64_t ldx, const void* x0,
+                            int64_t ldx0, const float* alpha, const float* beta, int flags, void* f, int64_t ldf,
+                            float* workspace, int64_t n_slots, const gnpde_stage_epilogue_t* stage, void* stream) {
+  return attn_dot_rhs_impl<bf16>(items, n_items, heavy, n_heavy, col, q, k, ldqk, heads, dk, dst_stats, C,
+                                 static_cast<const float*>(x), ldx, static_cast<const float*>(x0), ldx0, alpha, beta,
+                                 flags, static_cast<float*>(f), ldf, workspace, n_slots, stage, stream);
+}
+
 
 }  // extern "C"

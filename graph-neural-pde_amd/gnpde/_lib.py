@@ -69,6 +69,8 @@ SIGNATURES = {
     "gnpde_attn_dot_workspace_floats": (_i64, [_i64, _i64, _i64]),
     "gnpde_attn_dot_rhs_f32": (_int, [_vp, _i64, _vp, _i64, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _i64, _vp, _i64, _vp,
                                       _i64, _vp, _vp, _int, _vp, _i64, _vp, _i64, ctypes.POINTER(StageEpilogue), _vp]),
+    "gnpde_attn_dot_rhs_bf16": (_int, [_vp, _i64, _vp, _i64, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _i64, _vp, _i64, _vp,
+                                      _i64, _vp, _vp, _int, _vp, _i64, _vp, _i64, ctypes.POINTER(StageEpilogue), _vp]),
     "gnpde_rows_copy": (_int, [_vp, _i64, _i64, _vp, _vp, _vp, _vp]),
     "gnpde_stage_apply_f32": (_int, [_i64, _i64, _i64, _vp, _vp, ctypes.POINTER(StageEpilogue), _vp]),
     "gnpde_stage_apply_bf16": (_int, [_i64, _i64, _i64, _vp, _vp, ctypes.POINTER(StageEpilogue), _vp]),

@@ -404,7 +404,9 @@ class ODEFuncTransformerAtt(ODEFunc):
             ref = lay.score_mode == 'reference' and self.opt.get('attention_type', 'scaled_dot') == 'scaled_dot'
             ns = lay.node_scores(g, x.float() if ref else x)
             m, rl = ops.softmax_stats(g, ns, 1) if norm_idx == 1 else (None, None)
-            return ops.attn_rhs(g, ns, m, rl, norm_idx, x, fuse=False, **kw)
+            # per-edge scaled_dot under source-grouped softmax: the fused pass over the bf16
+            # state (gnpde_attn_dot_rhs_bf16); otherwise K2 weights + the bf16 K1
+            return ops.attn_rhs(g, ns, m, rl, norm_idx, x, fuse=not ref and norm_idx == 0, **kw)
         ns = lay.node_scores(g, x)
         # destination-grouped softmax needs its statistics over the CSC first
         # (attn_rhs computes them: packed records for the fork's two-head

@@ -1057,7 +1057,8 @@ def attn_rhs(g, ns, m, rl, norm_idx, x, x0=None, alpha=None, beta=None, rhs=True
         w = RefDstWeights(ns.cs, m, rl, ns.heads, mr=mr)
         return spmm_rhs(g, w, x, x0=x0, alpha=alpha, beta=beta, rhs=rhs, alpha_sigmoid=alpha_sigmoid,
                         add_source=add_source, out=out, stage=stage)
-    if fuse and ns.mode == _lib.SCORE_DOT and x.dtype == torch.float32 and \
+    if fuse and ns.mode == _lib.SCORE_DOT and (x.dtype == torch.float32 or (x.dtype == torch.bfloat16 and
+                                                                              norm_idx == 0)) and \
             _lib.fn("gnpde_attn_dot_supported")(ns.heads, ns.dk, x.shape[-1]):
         if norm_idx == 1 and mr is None:
             _, _, mr = softmax_stats(g, ns, 1, seg=seg, packed=True)
@@ -1079,14 +1080,19 @@ def attn_dot_rhs(g, ns, x, x0=None, alpha=None, beta=None, rhs=True, alpha_sigmo
     (softmax_stats(..., packed=True)) and the pass weights every scored edge with
     them.  No [nnz] weights.  NotImplemented for shapes outside the fused kernel
     (gnpde_attn_dot_supported)."""
-    xr = _rows(x, "x")
+    dt = x.dtype if isinstance(x, torch.Tensor) and x.dtype in STATE_DTYPES else torch.float32
+    bf = dt == torch.bfloat16
+    xr = _rows(x, "x", dt)
     C = xr.shape[1]
     H, dk = ns.heads, ns.dk
     if not _lib.fn("gnpde_attn_dot_supported")(H, dk, C):
         return NotImplemented
     if stage is not None and (stage.wide or len(stage.outs) > 1 or stage.dot is not None):
         return NotImplemented  # fused here: single-output fixed-grid stages (the caller takes K2 + K1)
-    if ns.ldqk % 4 or ns.q.data_ptr() % 16 or ns.k.data_ptr() % 16 or xr.data_ptr() % 16:
+    if bf and mr is not None:
+        return NotImplemented  # a bf16 state: source-grouped softmax only (K2 + the bf16 K1 otherwise)
+    row_align = 8 if bf else 16
+    if ns.ldqk % 4 or ns.q.data_ptr() % 16 or ns.k.data_ptr() % 16 or xr.data_ptr() % row_align:
         return NotImplemented
     if xr.shape[0] != g.R:
         raise ValueError("x has %d rows, graph has %d" % (xr.shape[0], g.R))
@@ -1095,13 +1101,13 @@ def attn_dot_rhs(g, ns, x, x0=None, alpha=None, beta=None, rhs=True, alpha_sigmo
     if rhs and a is None:
         raise ValueError("attn_dot_rhs: alpha required")
     b = _scalar(beta, "beta", dev) if add_source else None
-    x0r = _rows(x0, "x0") if add_source else None
-    if x0r is not None and x0r.data_ptr() % 16:
+    x0r = _rows(x0, "x0", dt) if add_source else None
+    if x0r is not None and x0r.data_ptr() % row_align:
         return NotImplemented
     st = None
     if stage is not None:
         for t in stage.tensors():
-            _require_gpu(t, "stage tensor", torch.float32)
+            _require_gpu(t, "stage tensor", dt)
             if not t.is_contiguous() or t.numel() != xr.numel():
                 raise ValueError("stage tensors must be contiguous and shaped like x")
         st = ctypes.byref(stage.struct(xr))
@@ -1115,7 +1121,8 @@ def attn_dot_rhs(g, ns, x, x0=None, alpha=None, beta=None, rhs=True, alpha_sigmo
             return NotImplemented
         ws = torch.empty(nws, dtype=torch.float32, device=dev)
     plan.order_launch(dev)
-    rc = _lib.call_rc("gnpde_attn_dot_rhs_f32", _ptr(plan.items), plan.n_items, _ptr(plan.heavy), plan.n_heavy,
+    rc = _lib.call_rc("gnpde_attn_dot_rhs_bf16" if bf else "gnpde_attn_dot_rhs_f32", _ptr(plan.items), plan.n_items,
+                      _ptr(plan.heavy), plan.n_heavy,
                       _ptr(g.csr.col), _ptr(ns.q), _ptr(ns.k), ns.ldqk, H, dk, _ptr(mr), C, _ptr(xr), C,
                       _ptr(x0r), C, _ptr(a), _ptr(b), _flags(rhs, alpha_sigmoid, add_source), _ptr(out), C, _ptr(ws),
                       plan.n_slots, st, _stream(dev))

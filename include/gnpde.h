@@ -334,6 +334,15 @@ int gnpde_attn_dot_rhs_f32(const int32_t* items, int64_t n_items, int32_t* heavy
                            const float* dst_stats, int64_t C, const float* x, int64_t ldx, const float* x0, int64_t ldx0,
                            const float* alpha, const float* beta, int flags, float* f, int64_t ldf, float* workspace,
                            int64_t n_slots, const gnpde_stage_epilogue_t* stage, void* stream);
+/* The same over a bf16 state (x, x0, f and the stage rows bf16, 8-byte aligned
+ * 4-element slices; q, k, dst_stats and the workspace fp32): source-grouped
+ * softmax (dst_stats NULL) with the plain RHS or a single-output stage only,
+ * GNPDE_EUNSUPPORTED otherwise (the binding then takes K2 + gnpde_spmm_rhs_bf16). */
+int gnpde_attn_dot_rhs_bf16(const int32_t* items, int64_t n_items, int32_t* heavy, int64_t n_heavy,
+                            const int32_t* col, const float* q, const float* k, int64_t ldqk, int64_t heads,
+                            int64_t dk, const float* dst_stats, int64_t C, const void* x, int64_t ldx, const void* x0,
+                            int64_t ldx0, const float* alpha, const float* beta, int flags, void* f, int64_t ldf,
+                            float* workspace, int64_t n_slots, const gnpde_stage_epilogue_t* stage, void* stream);
 
 /* ---------------------------------------------------------------- attention
  * Node-level projection on the matrix cores (K % 16 == 0, K <= 128: exact

@@ -276,3 +276,33 @@ def test_bf16_per_edge_attention_scores_from_the_bf16_state(norm_idx):
     assert fb.dtype == torch.bfloat16
     assert rel(fb.float(), ff.double().cpu().numpy()) <= 2.0 ** -7
 
+
+@pytest.mark.parametrize("C,h,att", [(128, 2, 32), (64, 2, 16), (160, 4, 32), (256, 2, 64), (36, 2, 8)])
+def test_flash_bf16_state_vs_unfused_and_oracle(C, h, att):
+    """gnpde_attn_dot_rhs_bf16: the one-pass per-edge RHS (norm_idx 0) over a bf16
+    state (bf16 row gathers and epilogue, fp32 scores and sums) against the unfused
+    K2 + bf16 K1 path on the same state, and against the fp64 oracle of the state's
+    values, within bf16 output rounding; hub chunks included; a fused rk4 stage
+    within the same bound of its unfused twin."""
+    N, E = 1500, 24000
+    ei, x, x0, Wq, bq, Wk, bk = case(N, E, C, att, seed=C + h + 7)
+    g = ops.GraphCSR(T(ei), N)
+    assert g.csr.plan.n_heavy >= 1
+    xb = T(x).to(torch.bfloat16)
+    ns = ops.node_scores(g, xb, T(Wq), T(bq), T(Wk), T(bk), h, 'scaled_dot', 'per_edge')
+    a = torch.tensor(0.3, device=DEV)
+    f = ops.attn_dot_rhs(g, ns, xb, alpha=a)
+    assert f is not NotImplemented and f.dtype == torch.bfloat16
+    fu = ops.attn_rhs(g, ns, None, None, 0, xb, alpha=a, fuse=False)
+    assert fu.dtype == torch.bfloat16
+    assert rel(f.float(), fu.double().cpu().numpy()) <= 2.0 ** -7
+    want = O.transformer_rhs(ei, xb.float().cpu().numpy(), None, Wq, bq, Wk, bk, h, 0, 0.3, 0.0,
+                             score_mode='per_edge')
+    assert rel(f.float(), want) <= 2.0 ** -7
+    # a fused single-output stage: y = x + 0.25 f
+    y = torch.empty_like(xb)
+    r = ops.attn_dot_rhs(g, ns, xb, alpha=a, stage=ops.Stage(outs=[(y, xb, 1.0, 0.25, [])]))
+    assert r is None
+    want_y = xb.float() + 0.25 * fu.float()
+    assert rel(y.float(), want_y.double().cpu().numpy()) <= 2.0 ** -7
+
