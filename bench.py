@@ -621,8 +621,9 @@ def solve_numbering(func, x):
 
 
 def _time_rhs(func, x, lay, reps):
-    """(eager ms, graph-replayed ms) of one RHS evaluation of ``func`` at x in the
-    numbering ``lay`` (None: the user numbering)."""
+    """(eager ms, graph-replayed ms: the median of three windows of ``reps``
+    replays) of one RHS evaluation of ``func`` at x in the numbering ``lay``
+    (None: the user numbering)."""
     func._layout = lay
     try:
         with torch.no_grad():
@@ -645,19 +646,22 @@ def _time_rhs(func, x, lay, reps):
             for _ in range(3):
                 cg.replay()
             torch.cuda.synchronize()
-            s.record()
-            for _ in range(reps):
-                cg.replay()
-            e.record()
-            torch.cuda.synchronize()
-            ms = s.elapsed_time(e) / reps
+            wins = []
+            for _ in range(3):  # the median of three windows of `reps` replays
+                s.record()
+                for _ in range(reps):
+                    cg.replay()
+                e.record()
+                torch.cuda.synchronize()
+                wins.append(s.elapsed_time(e) / reps)
+            ms = sorted(wins)[1]
             del cg
     finally:
         func._layout = None
     return ms_eager, ms
 
 
-def bench_attention(g, x, dev, ops, reps=20):
+def bench_attention(g, x, dev, ops, reps=50):
     """The transformer RHS through the drop-in ODEFuncTransformerAtt (config C4 shape),
     in the node numbering a fixed-grid solve runs it in (the graph's in-degree order,
     gnpde.ops.NodeLayout: VERDICT r3 item 4); the user-numbering time beside it."""
