@@ -357,7 +357,12 @@ __global__ __launch_bounds__(256) void seg_softmax_kernel(const int4* __restrict
 // A lane's segment end comes from a ballot of group changes (no rowptr gather).
 // Same arithmetic as seg_softmax_kernel<true, kSegStats>: segmented max,
 // exp(v - M), segmented sum, in the same lane order.
-constexpr int kRefStatsNI = 2;  // 1 / 4 items per wavefront: 20.9 / 23.1 us against 21.0
+#ifndef GNPDE_RS_NI
+#define GNPDE_RS_NI 1
+#endif
+// short items per wavefront: round 3 (1024-thread workgroups) 1 / 2 / 4 = 20.9 / 21.0 / 23.1 us;
+// round 4 (256-thread workgroups, hub chunks) 16.25 / 16.9 / 19.1 us (tools/ab_stats.sh)
+constexpr int kRefStatsNI = GNPDE_RS_NI;
 
 template <int NI, int MAXH>
 __global__ __launch_bounds__(256) void ref_stats_kernel(const int4* __restrict__ items, int n_items, int n_hub,
