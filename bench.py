@@ -903,7 +903,7 @@ def bench_train(ei, w, x, h, dev, steps=4, reps=5):
     t = torch.tensor([0.0, steps * h], dtype=torch.float32, device=dev)
 
     def one():
-        xi = x.detach().clone().requires_grad_(True)
+        xi = x.detach().requires_grad_(True)  # a fresh leaf on x's storage (no copy: not the step's work)
         func.alpha_train.grad = None
         y = gnpde.odeint(func, xi, t, method='rk4', options={'step_size': h})[1]
         (y * gout).sum().backward()

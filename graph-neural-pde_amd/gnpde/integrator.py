@@ -555,7 +555,7 @@ class _LaplacianFixedGridFn(torch.autograd.Function):
         lay = ctx.lay
         with torch.no_grad():
             gr, w_csc = ctx.gr, ctx.w_csc
-            one = torch.ones((), dtype=torch.float32, device=g_sol.device)
+            one = _device_one(g_sol.device)
             sig = ctx.sig
             a_dev = ctx.a_dev
             a = ctx.a_host() if ctx.a_host is not None else None  # euler / midpoint combinations
@@ -567,8 +567,6 @@ class _LaplacianFixedGridFn(torch.autograd.Function):
                 return ops.spmm_rhs(gr, w_csc, v, alpha=one, rhs=True, alpha_sigmoid=False, transpose=True)
 
             comb = ops.rk_combine
-            ga = torch.zeros((), dtype=torch.float64, device=g_sol.device)
-            gb = torch.zeros((), dtype=torch.float64, device=g_sol.device)
             # the output-time gradients join the running gradient at their grid points
             out_at = {}
             j = 1
@@ -579,10 +577,17 @@ class _LaplacianFixedGridFn(torch.autograd.Function):
             s0 = ctx.starts[0]
             g = None  # the running gradient (None: still zero)
             nfe = getattr(func, 'nfe', None)
-            # rk4: the alpha gradient's per-row terms <u_i, x_i> accumulate in the transpose
-            # launches' epilogues (gnpde_stage_epilogue_t dot_rows), summed once at the end
-            drow = torch.zeros(s0.numel() // s0.shape[-1], dtype=torch.float64, device=s0.device) \
-                if method == 'rk4' else None
+            # d alpha, d beta and (rk4) the alpha gradient's per-row terms <u_i, x_i>, which
+            # accumulate in the transpose launches' epilogues (gnpde_stage_epilogue_t dot_rows)
+            # and are summed once at the end: one zero-filled fp64 buffer for the three
+            n_drow = s0.numel() // s0.shape[-1] if method == 'rk4' else 0
+            acc64 = torch.zeros(2 + n_drow, dtype=torch.float64, device=s0.device)
+            ga, gb = acc64[0], acc64[1]
+            drow = acc64[2:] if method == 'rk4' else None
+            # rk4 in a renumbered solve: the first step's last launch stores the input gradient
+            # straight into the caller's numbering (its out_rows), as the forward's last step
+            # stores the solution — no exit pass
+            user_rows = lay.order32 if (lay is not None and method == 'rk4' and not out_at.get(-1)) else None
             def g_at(jj):  # an output time's gradient in the solve's numbering (one gnpde_rows_copy pass)
                 if lay is None:
                     return g_sol[jj]
@@ -619,11 +624,15 @@ class _LaplacianFixedGridFn(torch.autograd.Function):
                     ops.spmm_rhs(gr, w_csc, gk2, stage=ops.Stage(outs=[
                         (gk1, gk2, 1.0 / 3.0, dt / 3.0, [(v, 4.0 * dt * c8 / 3.0), (u3, -2.0 * dt / 3.0)]),
                         (acc, g, 1.0, 1.0, [(v, c8), (u3, 1.0)])], dot=(x2, drow, 1.0, True), scale=asc), **T)
+                    last = n == 0 and user_rows is not None
                     ops.spmm_rhs(gr, w_csc, gk1, stage=ops.Stage(outs=[(g_new, acc, 1.0, 1.0, [])],
+                                                                 out_rows=user_rows if last else None,
                                                                  dot=(y, drow, 1.0, True), scale=asc), **T)
                     if add_source:
                         gb = gb + c8 * ops.dot(g, x0) + ops.dot(gk3, x0) + ops.dot(gk2, x0) + ops.dot(gk1, x0)
                     g = g_new
+                    if last:
+                        lay = None  # g is in the caller's numbering now
                     continue
                 if method == 'euler':
                     gk = [comb(None, [g], [dt], 1.0)]
@@ -654,12 +663,15 @@ class _LaplacianFixedGridFn(torch.autograd.Function):
                 gu = torch.empty_like(g)
                 _to_user(g, gu, lay)
                 g = gu
-            g = g + g_sol[0]
+            g = g + g_sol[0] if g._base is g_sol else g.add_(g_sol[0])  # (never g_sol itself in place)
             if sig:
                 ga = ga * (a_dev * (1 - a_dev)).double()
         gy = g if ctx.needs_input_grad[0] else None
         galpha = ga.to(func.alpha_train.dtype).reshape(func.alpha_train.shape) if ctx.needs_input_grad[1] else None
-        gbeta = gb.to(func.beta_train.dtype).reshape(func.beta_train.shape) if ctx.needs_input_grad[2] else None
+        # without add_source beta_train is not on the path: no gradient, as autograd through
+        # the reference's RHS leaves it (src/function_laplacian_diffusion.py:74-77)
+        gbeta = gb.to(func.beta_train.dtype).reshape(func.beta_train.shape) \
+            if ctx.needs_input_grad[2] and add_source else None
         return gy, galpha, gbeta, None, None, None, None
 
 
@@ -679,6 +691,18 @@ def _host_scalar(v):
         ev.synchronize()
         return float(h)
     return get
+
+
+_ONES = {}
+
+
+def _device_one(device):
+    """A read-only fp32 1.0 on `device` (the adjoint launches' alpha operand), made once
+    per device rather than filled per backward."""
+    one = _ONES.get(device)
+    if one is None:
+        one = _ONES[device] = torch.ones((), dtype=torch.float32, device=device)
+    return one
 
 
 def _node_layout(func, y0):

@@ -457,3 +457,45 @@ def test_fused_backward_reads_its_forward_state():
     gb = one_at_a_time[0][2] + one_at_a_time[1][2]
     assert abs(float(func.alpha_train.grad - ga)) <= 1e-6 * max(1.0, abs(float(ga)))
     assert abs(float(func.beta_train.grad - gb)) <= 1e-6 * max(1.0, abs(float(gb)))
+
+
+@pytest.mark.parametrize("add_source", [False, True])
+def test_fused_backward_in_node_layout_equals_user_numbering(monkeypatch, add_source):
+    """A training solve large enough for the in-degree numbering (ops.NodeLayout):
+    the adjoint's last launch stores the input gradient straight into the caller's
+    numbering (the stage's out_rows) and the x0 gradient joins in place.  Against
+    the same solve with the numbering switched off: x gradients bit-identical
+    (every row keeps its edges and their order), alpha within fp64 summation order,
+    beta's gradient None without add_source (it is not on the path)."""
+    from gnpde import synthetic
+    N, E, C = 40000, 320000, 128
+    ei, w = synthetic.rw_graph(N, E, seed=11, device=DEV)
+    gen = torch.Generator(device=DEV)
+    gen.manual_seed(12)
+    x = torch.randn(1, N, C, generator=gen, device=DEV)
+    gout = torch.randn(2, 1, N, C, generator=gen, device=DEV)
+    t = torch.tensor([0.0, 0.5], device=DEV)
+    res = []
+    for on in (True, False):
+        monkeypatch.setattr(ops, "LAYOUT_MIN_ROWS", 32768 if on else 1 << 40)
+        monkeypatch.setattr(ops, "LAYOUT_MIN_BYTES", 1 << 20)
+        opt = dict(OPT, hidden_dim=C, add_source=add_source)
+        func = gnpde.LaplacianODEFunc(C, C, opt, DEV).to(DEV)
+        func.edge_index, func.edge_weight = ei, w
+        with torch.no_grad():
+            func.alpha_train.fill_(0.3)
+            func.beta_train.fill_(0.2)
+        func.x0 = x * 0.5
+        assert (func.node_layout(x) is not None) == on
+        xi = x.clone().requires_grad_(True)
+        sol = gnpde.odeint(func, xi, t, method='rk4', options={'step_size': 0.125})
+        (sol * gout).sum().backward()  # both output times: sol[0]'s gradient joins x's
+        res.append((sol.detach(), xi.grad, func.alpha_train.grad, func.beta_train.grad))
+    (s1, gx1, ga1, gb1), (s0, gx0, ga0, gb0) = res
+    assert torch.equal(s1, s0)
+    assert torch.equal(gx1, gx0)
+    assert abs(float(ga1 - ga0)) <= 1e-6 * max(1.0, abs(float(ga0)))
+    if add_source:
+        assert abs(float(gb1 - gb0)) <= 1e-6 * max(1.0, abs(float(gb0)))
+    else:
+        assert gb1 is None and gb0 is None

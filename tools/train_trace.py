@@ -32,7 +32,7 @@ def main():
     mk = torch.ones(64, device=dev)
 
     def one():
-        xi = x.detach().clone().requires_grad_(True)
+        xi = x.detach().requires_grad_(True)
         func.alpha_train.grad = None
         y = gnpde.odeint(func, xi, t, method='rk4', options={'step_size': 0.25})[1]
         (y * gout).sum().backward()
