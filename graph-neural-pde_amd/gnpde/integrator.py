@@ -701,7 +701,9 @@ def _device_one(device):
     per device rather than filled per backward."""
     one = _ONES.get(device)
     if one is None:
-        one = _ONES[device] = torch.ones((), dtype=torch.float32, device=device)
+        one = torch.ones((), dtype=torch.float32, device=device)
+        if not torch.cuda.is_current_stream_capturing():  # a captured fill runs only on replay
+            _ONES[device] = one
     return one
 
 
