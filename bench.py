@@ -390,6 +390,12 @@ def kernel_traffic(workload, kernel_prefix):
     return best["bytes"] if best else None
 
 
+def step_traffic(workload):
+    """PMC bytes of one replayed adaptive step of a workload (tools/pmc_run.py dopri5)."""
+    w = traffic().get("workloads", {}).get(workload)
+    return w.get("per_step_bytes") if w else None
+
+
 def rhs_traffic(workload):
     """PMC bytes of one RHS evaluation of an attention workload (every kernel it dispatches)."""
     w = traffic().get("workloads", {}).get(workload)
@@ -814,15 +820,57 @@ def bench_dopri5(ei, w, x, dev, k1_stage_ms, k1_plain_ms, reps=3):
     plan = integ._adaptive_plan('dopri5')
     ms_step = el * 1e3 / max(steps, 1)
     r, wr = plan.state_passes()
+    affine = bool(getattr(func, 'affine', False)) and integ.AFFINE_STAGE
+    if affine:  # no first stage-input pass (y0 and k0 read, X0 written): launch 0 reads k0 as its input
+        r, wr = r - 2, wr - 1
+    # device time of one step: a captured step (6 RHS launches, the error reduction and the device
+    # controller) replayed back to back between HIP events on the launch stream
+    dev_ms = None
+    g = integ.adaptive_step_graph(func)
+    if g is not None:
+        for _ in range(3):
+            g.replay()
+        torch.cuda.synchronize()
+        s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s0.record()
+        for _ in range(20):
+            g.replay()
+        s1.record()
+        torch.cuda.synchronize()
+        dev_ms = s0.elapsed_time(s1) / 20
+    N, E = x.shape[1], ei.shape[2]
+    # algorithmic bytes of one step: 6 x (gathers 4EC + CSR 8E + rowptr 4(N+1) + own row 4NC) + the plan's
+    # further state passes (reads + writes of 4NC each)
+    alg = 6 * (4 * E * C + 8 * E + 4 * (N + 1) + 4 * N * C) + (r + wr) * 4 * N * C
+    tb = step_traffic("dopri5")
+    rl = None
+    if dev_ms:
+        t = dev_ms * 1e-3
+        rl = {"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s", "kernel": "one replayed dopri5 step (2 STG1 + 4 "
+              "STG4 agg_kernel launches, sum_partial_kernel, adaptive_control_kernel)", "step_ms": round(dev_ms, 4),
+              "algorithmic_bytes_per_step": int(alg), "algorithmic_frac": round(alg / t / 1e9 / HBM_PEAK_GBS, 4)}
+        if tb:
+            rl.update({"traffic": int(tb), "achieved": round(tb / t / 1e9, 1),
+                       "frac": round(tb / t / 1e9 / HBM_PEAK_GBS, 4),
+                       "basis": "PMC bytes of one replayed step (%s workload dopri5; counters include Infinity-Cache "
+                                "hits) / HIP-event step time" % TRAFFIC_FILE})
+        else:
+            rl.update({"traffic": None, "achieved": None, "frac": None,
+                       "basis": "no PMC traffic for workload dopri5 in %s" % TRAFFIC_FILE})
     out["garxiv_laplacian"] = {
         "config": "G-arxiv laplacian (C=128), dopri5 over [0, %.3f], tol_scale %.1f (ogbn-arxiv best_params)" % (T, ts),
         "ms_per_solve": round(el * 1e3, 4), "steps": steps, "rhs_evals": nfe, "ms_per_step": round(ms_step, 4),
         "rhs_evals_per_s": round(nfe / el, 1),
         "ms_per_step_over_6_rhs_stage": round(ms_step / (6 * k1_stage_ms), 4),
         "ms_per_step_over_6_rhs_plain": round(ms_step / (6 * k1_plain_ms), 4) if k1_plain_ms else None,
+        "step_ms_device": round(dev_ms, 4) if dev_ms else None,
         "state_passes_per_step": {"reads": r, "writes": wr},
-        "basis": "6 RHS launches per step carrying the stage combinations and the error rows + 1 stage-input pass + "
-                 "the norm reduction and one host read; rhs_stage_ms = the rk4 fused-stage K1 launch time"}
+        "affine_first_stage": affine,
+        "roofline": rl,
+        "basis": "ms_per_step = whole solve (entry copy, initial-step selection, steps, dense output) / steps; "
+                 "per step: 6 RHS launches carrying the stage combinations and the error rows (the first stage's "
+                 "input never formed: f affine) + the error reduction with the device step-size controller, one "
+                 "host read; rhs_stage_ms = the rk4 fused-stage K1 launch time"}
     progress("dopri5 G-arxiv: %.3f ms/step, %d steps" % (ms_step, steps))
     # configs[1] shape
     N, E, Cc, h, att = 2708, 13264, 80, 8, 128  # Cora: 10,556 edges + 2,708 self loops

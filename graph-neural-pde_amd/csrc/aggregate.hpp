@@ -149,11 +149,44 @@ __device__ __forceinline__ void hub_combine(int row, int first, int nch, int C, 
     if (ep.st.dot_rows || ep.st.err_rows) epi_rowsum_store<GL>(ep, row, dpart, lane == 0);  // wave-uniform
 }
 
-// A chunk wave whose write-through partial stores are issued: drain them, take
-// an arrival ticket on its hub's plan entry (heavy[h].w, an agent-scope atomic),
-// and if it arrived last, acquire and combine the hub row, then reset the
-// ticket to 0 for the next launch on this plan.  Hubs are found by a binary
-// search of the ascending first slots (log2(n_heavy) L2 reads, chunk waves only).
+// The sum of the nch chunk partials of a hub row (slots first .. first+nch-1),
+// computed by all 64 lanes: lane groups of GLp = pow2_ceil(GL) lanes take chunks
+// g, g+G, ... (4 loads in flight), joined by a fixed xor tree — the order of
+// hub_combine, so the same bits.  Every lane ends with the sums of the columns
+// (ch*GLp + lane % GLp)*VEC.
+template <int VEC, int GL, int NCH>
+__device__ __forceinline__ void hub_sum(int first, int nch, int C, const float* __restrict__ partials,
+                                        float (&hs)[NCH][VEC]) {
+  constexpr int GLp = pow2_ceil(GL);
+  constexpr int G = kWave / GLp;
+  static_assert(NCH == 1 || GLp == GL, "several column passes need power-of-two row lanes");
+  const int lane = threadIdx.x & 63;
+  const int g = lane / GLp, gl = lane % GLp;
+#pragma unroll
+  for (int ch = 0; ch < NCH; ++ch) {
+    const int cc = (ch * GLp + gl) * VEC;
+    const bool live = cc < C;
+#pragma unroll
+    for (int t = 0; t < VEC; ++t) hs[ch][t] = 0.f;
+#pragma unroll 4
+    for (int c = g; c < nch; c += G) {
+      float v[VEC];
+      if (live) {
+        load_vec<VEC>(partials + (int64_t)(first + c) * C + cc, v);
+      } else {
+#pragma unroll
+        for (int t = 0; t < VEC; ++t) v[t] = 0.f;
+      }
+#pragma unroll
+      for (int t = 0; t < VEC; ++t) hs[ch][t] += v[t];
+    }
+#pragma unroll
+    for (int o = GLp; o < kWave; o <<= 1)
+#pragma unroll
+      for (int t = 0; t < VEC; ++t) hs[ch][t] += __shfl_xor(hs[ch][t], o);
+  }
+}
+
 // Memory order of the arrival ticket.  The partials are stored write-through and
 // drained (s_waitcnt vmcnt(0)) before the ticket, which is what an agent-scope
 // release orders at the ISA level; GNPDE_HUB_RELEASE=1 builds the ticket as a
@@ -164,31 +197,64 @@ __device__ __forceinline__ void hub_combine(int row, int first, int nch, int C, 
 #endif
 constexpr int kHubTicketOrder = GNPDE_HUB_RELEASE ? __ATOMIC_RELEASE : __ATOMIC_RELAXED;
 
-template <int VEC, int GL, int STG, class T>
-__device__ __forceinline__ void hub_arrive(int4* heavy, int n_heavy, int slot, int C, const Epi& ep,
-                                           const float* partials) {
+// Chunk waves whose write-through partial stores are issued: drain them; each
+// row slot holding a hub chunk takes an arrival ticket on its hub's plan entry
+// (heavy[h].w, an agent-scope atomic; hubs found by a binary search of the
+// ascending first slots); every slot whose chunk arrived last then has its hub
+// row summed by the whole wavefront (hub_sum, after an acquire; the ticket is
+// reset to 0 for the next launch on this plan), and the slot's owner lanes take
+// the row (erow) and its sums (acc) for the kernel's one epilogue.  Called by
+// all 64 lanes; `chunk`, `slot` are per slot.  Returns whether this lane now
+// owns a hub row.
+template <int VEC, int GL, int SL, int RPW, int NCH>
+__device__ __forceinline__ bool hub_claim(int4* heavy, int n_heavy, bool chunk, int slot, int C,
+                                          const float* partials, int rs, int g, int gl, int& erow,
+                                          float (&acc)[NCH][VEC]) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  int lo = 0, hi = n_heavy - 1;
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (heavy[mid].y <= slot)
-      lo = mid;
-    else
-      hi = mid - 1;
+  const int lane = threadIdx.x & 63;
+  int lo = 0, won = 0;
+  if (chunk) {
+    int hi = n_heavy - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (heavy[mid].y <= slot)
+        lo = mid;
+      else
+        hi = mid - 1;
+    }
+    if (lane % SL == 0) {
+      const int t = __hip_atomic_fetch_add(&heavy[lo].w, 1, kHubTicketOrder, __HIP_MEMORY_SCOPE_AGENT);
+      won = t == heavy[lo].z - 1;
+    }
   }
-  const int row = heavy[lo].x, first = heavy[lo].y, nch = heavy[lo].z;
-  int* ticket_word = &heavy[lo].w;
-  int ticket = 0;
-  if ((threadIdx.x & 63) == 0)
-    ticket = __hip_atomic_fetch_add(ticket_word, 1, kHubTicketOrder, __HIP_MEMORY_SCOPE_AGENT);
-  ticket = __shfl(ticket, 0);
-  if (ticket != nch - 1) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  hub_combine<VEC, pow2_ceil(GL), STG, T>(row, first, nch, C, ep, partials);
-  if ((threadIdx.x & 63) == 0) __hip_atomic_store(ticket_word, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  bool mine = false;
+  for (int s = 0; s < RPW; ++s) {
+    if (__shfl(won, s * SL)) {  // wave-uniform
+      const int h = __shfl(lo, s * SL);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      const int4 hv = heavy[h];
+      float hs[NCH][VEC];
+      hub_sum<VEC, GL, NCH>(uniform(hv.y), uniform(hv.z), C, partials, hs);
+      // the slot's lane gl takes the sums of its columns from lane gl (group 0 holds every column)
+      const bool take = rs == s && g == 0;
+#pragma unroll
+      for (int ch = 0; ch < NCH; ++ch)
+#pragma unroll
+        for (int t = 0; t < VEC; ++t) {
+          const float v = (GL == kWave) ? hs[ch][t] : __shfl(hs[ch][t], gl);
+          acc[ch][t] = take ? v : acc[ch][t];
+        }
+      if (take) {
+        erow = uniform(hv.x);
+        mine = true;
+      }
+      if (lane == 0) __hip_atomic_store(&heavy[h].w, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  return mine;
 }
 
-// The RPW > 1 form of hub_arrive: each row slot of the wavefront that holds a
+// The hub combine of the flash kernels (flash.hip; agg_kernel uses hub_claim): each row slot of the wavefront that holds a
 // hub chunk takes its own ticket (its first lane); every slot whose chunk
 // arrived last is then combined by the WHOLE wavefront, one slot after the
 // other (hub_combine over 64 lanes: the same sums, in the same order, as
@@ -232,8 +298,8 @@ __device__ __forceinline__ void hub_arrive_slots(int4* heavy, int n_heavy, bool 
 // (NCH column passes); U edges per group are in flight per iteration.  The
 // epilogue operands (x_r, x0_r, stage inputs) are loaded before the gathers
 // when NCH <= 2 (PRE) so their latency overlaps the aggregation.  Hub rows are
-// combined in-launch by the chunk that arrives last (hub_arrive for RPW == 1,
-// hub_arrive_slots for RPW > 1).
+// combined in-launch by the chunk that arrives last (hub_claim), and run
+// through the same epilogue as whole rows.
 template <int VEC, int GL, int NCH, int U, int RPW, int STG, class WP, class T = float>
 __global__ __launch_bounds__(256) void agg_kernel(const int4* __restrict__ items, int n_items, int4* heavy,
                                                    int n_heavy, const int* __restrict__ col, WP wp, int C, Epi ep,
@@ -326,9 +392,20 @@ __global__ __launch_bounds__(256) void agg_kernel(const int4* __restrict__ items
 #pragma unroll
       for (int t = 0; t < VEC; ++t) acc[ch][t] += __shfl_xor(acc[ch][t], o);
 
-  if constexpr (RPW == 1) {
-    if (slot >= 0 && n_heavy > 0) {  // wave-uniform: a chunk of a hub row, combined in-launch
-      if (g == 0) {
+  // The row whose epilogue this lane runs: its own (an owner lane of a whole
+  // row), or a hub row whose chunk arrived last in this wavefront (hub_claim);
+  // ONE epilogue below serves both, so the hub combine adds no second copy of
+  // the (wide) epilogue to the kernel's register allocation.
+  int erow = row;
+  bool fin = live && slot < 0 && g == 0;
+  bool hub = false;
+  if (n_heavy > 0) {  // hub chunks of any slot combined in-launch
+    const bool chunk = live && slot >= 0;
+    int anyc = 0;
+#pragma unroll
+    for (int s = 0; s < RPW; ++s) anyc |= __shfl((int)chunk, s * SL);
+    if (anyc) {  // wave-uniform
+      if (chunk && g == 0) {
         const __amdgpu_buffer_rsrc_t rp = buf_rsrc(partials);
 #pragma unroll
         for (int ch = 0; ch < NCH; ++ch) {
@@ -336,37 +413,26 @@ __global__ __launch_bounds__(256) void agg_kernel(const int4* __restrict__ items
           buf_store_wt<VEC>(rp, cc < C ? (uint32_t)(((int64_t)slot * C + cc) * 4) : kBufNone, acc[ch]);
         }
       }
-      hub_arrive<VEC, GL, STG, T>(heavy, n_heavy, slot, C, ep, partials);
-      return;
+      hub = hub_claim<VEC, GL, SL, RPW, NCH>(heavy, n_heavy, chunk, slot, C, partials, rs, g, gl, erow, acc);
+      fin = fin || hub;
     }
-  } else {
-    if (n_heavy > 0) {  // hub chunks of any slot combined in-launch (hub_arrive_slots)
-      const bool chunk = live && slot >= 0;
-      int anyc = 0;
-#pragma unroll
-      for (int s = 0; s < RPW; ++s) anyc |= __shfl((int)chunk, s * SL);
-      if (anyc) {  // wave-uniform
-        if (chunk && g == 0) {
-          const __amdgpu_buffer_rsrc_t rp = buf_rsrc(partials);
-#pragma unroll
-          for (int ch = 0; ch < NCH; ++ch) {
-            const int cc = (ch * GL + gl) * VEC;
-            buf_store_wt<VEC>(rp, cc < C ? (uint32_t)(((int64_t)slot * C + cc) * 4) : kBufNone, acc[ch]);
-          }
-        }
-        hub_arrive_slots<VEC, GL, SL, RPW, STG, T>(heavy, n_heavy, chunk, slot, C, ep, partials);
-        if (chunk) return;
-      }
-    }
-  }
-  if (!live || g != 0) return;
-  if (slot >= 0) {
+  } else if (live && slot >= 0 && g == 0) {  // chunk partials of a later agg_fixup_kernel
 #pragma unroll
     for (int ch = 0; ch < NCH; ++ch) {
       const int cc = (ch * GL + gl) * VEC;
       if (cc < C) store_vec<VEC>(partials + (int64_t)slot * C + cc, acc[ch]);
     }
     return;
+  }
+  if (!fin) return;
+  if constexpr (PRE) {  // a hub row's epilogue operands were not prefetched
+    if (hub) {
+#pragma unroll
+      for (int ch = 0; ch < NCH; ++ch) {
+        const int cc = (ch * GL + gl) * VEC;
+        if (cc < C) epi_prefetch<VEC, STG, T>(ep, erow, cc, pre[ch]);
+      }
+    }
   }
   const float a = (ep.flags & GNPDE_EPI_RHS) ? epi_alpha(ep) : 1.f;
   const float b = (ep.flags & GNPDE_ADD_SOURCE) ? *ep.beta : 0.f;
@@ -376,9 +442,9 @@ __global__ __launch_bounds__(256) void agg_kernel(const int4* __restrict__ items
     const int cc = (ch * GL + gl) * VEC;
     if (cc < C) {
       if constexpr (PRE)
-        epi_finish<VEC, STG, T>(ep, row, cc, acc[ch], a, b, pre[ch], &dpart);
+        epi_finish<VEC, STG, T>(ep, erow, cc, acc[ch], a, b, pre[ch], &dpart);
       else
-        epilogue_store<VEC, STG, T>(ep, row, cc, acc[ch], a, b, &dpart);
+        epilogue_store<VEC, STG, T>(ep, erow, cc, acc[ch], a, b, &dpart);
     }
   }
   // the row's owner lanes (g == 0: lanes [rs*SL, rs*SL + GL)) are all here
@@ -386,7 +452,7 @@ __global__ __launch_bounds__(256) void agg_kernel(const int4* __restrict__ items
     if (ep.st.dot_rows || ep.st.err_rows) {
       const double* prev = nullptr;
       if constexpr (PRE && stage_dot<STG>() && GNPDE_DOT_PRE) prev = &pre[0].dprev;
-      epi_rowsum_store_any<GL>(ep, row, dpart, rs * SL, gl == 0, prev);
+      epi_rowsum_store_any<GL>(ep, erow, dpart, rs * SL, gl == 0, prev);
     }
   }
 }
@@ -413,7 +479,7 @@ template <int VEC, int GL, int NCH, int U, int RPW, class WP, class T = float>
 static int launch_agg_cfg(const int4* items, int64_t n_items, int4* heavy, int64_t n_heavy, const int* col,
                           const WP& wp, int C, const Epi& ep, float* partials, hipStream_t s) {
   const unsigned grid = (unsigned)ceil_div(n_items, (int64_t)kWavesPerBlock * RPW);
-  // hub rows are combined in the launch (hub_arrive / hub_arrive_slots)
+  // hub rows are combined in the launch (hub_claim)
   bool inlaunch = true;
   if constexpr (GNPDE_EXPERIMENTS) inlaunch = hub_inlaunch();
   const int nh = inlaunch ? (int)n_heavy : 0;

@@ -148,6 +148,32 @@ __device__ __forceinline__ void store_vec(bf16* __restrict__ p, const float (&v)
 
 __device__ __forceinline__ int uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// ------------------------------------------------------------------ buffer memory ops
+// Raw buffer loads/stores take a 32-bit byte offset from a wave-uniform base,
+// and the hardware drops an access at or past num_records: a lane with nothing
+// to load or store passes kBufNone, so predicated accesses need no branch.
+// That matters on gfx9, where stores count in vmcnt: a store under a branch
+// makes the compiler's later waits conservative (vmcnt(0)), which serialises
+// every following store and load behind it.  Byte offsets must stay below
+// kBufRecords (callers check their buffer sizes).
+constexpr uint32_t kBufRecords = 0xffffff00u;
+constexpr uint32_t kBufNone = 0xfffffff0u;
+constexpr int kWaitVm0 = 0x0f70;  // s_waitcnt vmcnt(0) (expcnt, lgkmcnt at max)
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)kBufRecords, 0x00020000);
+}
+__device__ __forceinline__ void buf_store_f32(__amdgpu_buffer_rsrc_t r, uint32_t off, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, off, 0, 0);
+}
+__device__ __forceinline__ void buf_store_f64(__amdgpu_buffer_rsrc_t r, uint32_t off, double v) {
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, off, 0, 0);
+}
+
+
 // butterfly reductions over the 64 lanes of a wavefront
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
@@ -258,6 +284,22 @@ __device__ __forceinline__ float unpack(const Packed<VEC, bf16>& r, int t) {
   return bf16_to_f32((t & 1) ? (r.d[t >> 1] >> 16) : (r.d[t >> 1] & 0xffffu));
 }
 
+// fp32 values -> a row slice in storage form (bf16: round to nearest even); for an
+// operand that equals the RHS input, whose values are already fp32-exact in T
+template <int VEC, class T>
+__device__ __forceinline__ void pack_into(const float (&v)[VEC], Packed<VEC, T>& r) {
+  if constexpr (sizeof(T) == 4) {
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) r.d[i] = __float_as_uint(v[i]);
+  } else {
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) {
+      const uint32_t b = f32_to_bf16(v[i]);
+      r.d[i >> 1] = (i & 1) ? (r.d[i >> 1] | (b << 16)) : b;
+    }
+  }
+}
+
 // Epilogue operands of one row slice, loaded ahead of the aggregation so their
 // latency overlaps the gathers (they depend only on the row).
 // STG = the stage epilogue an instantiation is compiled for:
@@ -361,7 +403,7 @@ __device__ __forceinline__ void epi_prefetch(const Epi& e, int64_t row, int cc, 
   }
 #pragma unroll
   for (int j = 0; j < stage_kpre<STG>(); ++j)
-    if (j < e.st.nk) load_packed<VEC>(as_t<T>(e.st.k[j]) + off, p.kv[j]);
+    if (j < e.st.nk && !(need_x && e.st.k[j] == e.x && e.ldx == e.ldf)) load_packed<VEC>(as_t<T>(e.st.k[j]) + off, p.kv[j]);
   // the dot operand: STG 2 when prefetching, STG 2 / 3 under GNPDE_DOT_PRE (else in the epilogue)
   if constexpr (stage_dw_pre<STG>())
     if (e.st.dot_rows) load_packed<VEC>(as_t<T>(e.st.dot_with) + off, p.dw);
@@ -407,17 +449,163 @@ __device__ __forceinline__ float stage_scale(const gnpde_stage_epilogue_t& st) {
   return st.coef_scale ? *st.coef_scale : 1.f;
 }
 
-// The wide stage epilogue of one row slice (STG 4; also gnpde_stage_apply_*),
-// streamed over the shared operands so that one operand row is live at a time:
+// ------------------------------------------------------------------ streamed stage operands
+// The operand rows of the streamed stage epilogues (STG 4, the non-prefetching
+// STG 1-3, gnpde_stage_apply_*) are ISSUED TOGETHER, before any of them is used:
+// one memory round trip per epilogue.  Written as "if (j < nk) { load k[j];
+// fma }" the compiler waits for each load before the next (one round trip per
+// operand: the G-arxiv dopri5 launches with 3-6 operands ran at 172 us against
+// 92 us for the rk4 stage, round 4).  The loads are raw buffer loads whose absent
+// operands take the out-of-range offset kBufNone (no memory access, value 0),
+// so nothing in the load sequence branches.  Buffer byte offsets are 32-bit: a
+// wavefront any of whose rows lies past 4 GiB of the state takes the per-operand
+// form.
+// GNPDE_WIDE_BATCH=0 builds the per-operand form (A/B only).
+#ifndef GNPDE_WIDE_BATCH
+#define GNPDE_WIDE_BATCH 1
+#endif
+#ifndef GNPDE_WIDE_NOFB
+#define GNPDE_WIDE_NOFB 0
+#endif
+#ifndef GNPDE_WIDE_DEPTH
+#define GNPDE_WIDE_DEPTH 0
+#endif
+
+template <int VEC, class T>
+__device__ __forceinline__ void buf_load_packed(const void* p, uint32_t boff, Packed<VEC, T>& r) {
+  const __amdgpu_buffer_rsrc_t rs = buf_rsrc(p);
+  constexpr int B = VEC * (int)sizeof(T);
+  if constexpr (B == 32) {
+    // a dropped load (kBufNone) stays dropped: kBufNone + 16 would wrap to offset 0
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, boff, 0, 0);
+    const u32x4 u = __builtin_amdgcn_raw_buffer_load_b128(rs, boff >= kBufRecords ? kBufNone : boff + 16u, 0, 0);
+    r.d[0] = v.x;
+    r.d[1] = v.y;
+    r.d[2] = v.z;
+    r.d[3] = v.w;
+    r.d[4] = u.x;
+    r.d[5] = u.y;
+    r.d[6] = u.z;
+    r.d[7] = u.w;
+  } else if constexpr (B == 16) {
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, boff, 0, 0);
+    r.d[0] = v.x;
+    r.d[1] = v.y;
+    r.d[2] = v.z;
+    r.d[3] = v.w;
+  } else if constexpr (B == 8) {
+    const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(rs, boff, 0, 0);
+    r.d[0] = v.x;
+    r.d[1] = v.y;
+  } else if constexpr (B == 4) {
+    r.d[0] = __builtin_amdgcn_raw_buffer_load_b32(rs, boff, 0, 0);
+  } else {
+    static_assert(B == 2, "row slices are 2-16 bytes");
+    r.d[0] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(rs, boff, 0, 0);
+  }
+}
+
+// Whether every row of the wavefront addresses the state with 32-bit buffer offsets
+template <int VEC, class T>
+__device__ __forceinline__ bool rows_fit_buffer(int64_t off) {
+  return __all((off + VEC) * (int64_t)sizeof(T) < (int64_t)kBufRecords);
+}
+
+// The wide stage epilogue of one row slice (STG 4; also gnpde_stage_apply_*):
 // every output and the error combination start from cb*base (x when the base is
 // the RHS input xid, with values xv), take sc*c[j]*k[j] for j ascending, then
 // sc*cf*f — per output the same order as stage_combine, so the same bits.
-// Returns the error combination in ev (when err_rows) and output values in r.
+// Returns the error combination in ev (when err_rows), output values in r and,
+// when y0v is given and err_rows is set, the tolerance's y0 row slice.
 template <int VEC, class T, int NKMAX = GNPDE_STAGE_MAX_K, int NOUT = 2, bool ERR = true>
 __device__ __forceinline__ void wide_combine(const gnpde_stage_epilogue_t& st, int64_t off, const float (&o)[VEC],
                                              const float* xid, const float (&xv)[VEC], float (&r)[2][VEC],
-                                             float (&ev)[VEC]) {
+                                             float (&ev)[VEC], Packed<VEC, T>* y0v = nullptr) {
   const float sc = stage_scale(st);
+  if (GNPDE_WIDE_BATCH && (GNPDE_WIDE_NOFB || rows_fit_buffer<VEC, T>(off))) {
+    const bool has_err = ERR && st.err_rows != nullptr;
+    // operand table: NOUT output bases, the error base, NKMAX k rows, the tolerance's y0
+    constexpr int NE = ERR ? 2 : 0;
+    constexpr int N = NOUT + NKMAX + NE;
+    const float* p[N];
+    float cb[NOUT + 1];
+#pragma unroll
+    for (int i = 0; i <= NOUT; ++i) {
+      const bool on = i < NOUT ? i < st.n_out : has_err;
+      const gnpde_stage_out_t& so = i < NOUT ? st.o[i] : st.err;
+      const float* b = (on && (i < NOUT || ERR)) ? so.base : nullptr;
+      cb[i] = b ? so.cb : 0.f;
+      if (i < NOUT) p[i] = (b && b != xid) ? b : nullptr;
+      else if constexpr (ERR) p[NOUT + NKMAX] = (b && b != xid) ? b : nullptr;
+    }
+#pragma unroll
+    for (int j = 0; j < NKMAX; ++j) p[NOUT + j] = (j < st.nk && st.k[j] != xid) ? st.k[j] : nullptr;
+    if constexpr (ERR) p[N - 1] = has_err ? st.err_y0 : nullptr;
+    // slots: output bases [0, NOUT), the error base NOUT + NKMAX, k rows NOUT + j, y0 last;
+    // consumed in the order bases, error base, k0..k_{NKMAX-1} with at most D loads in
+    // flight (GNPDE_WIDE_DEPTH; 0 = all N issued at once)
+    constexpr int D = (GNPDE_WIDE_DEPTH > 0 && GNPDE_WIDE_DEPTH < N) ? GNPDE_WIDE_DEPTH : N;
+    int order[N];
+#pragma unroll
+    for (int i = 0; i < NOUT; ++i) order[i] = i;
+    if constexpr (ERR) order[NOUT] = NOUT + NKMAX;
+#pragma unroll
+    for (int j = 0; j < NKMAX; ++j) order[NOUT + (ERR ? 1 : 0) + j] = NOUT + j;
+    if constexpr (ERR) order[N - 1] = N - 1;
+    const uint32_t bo = (uint32_t)(off * (int64_t)sizeof(T));
+    Packed<VEC, T> ring[D];
+#pragma unroll
+    for (int q = 0; q < D; ++q) buf_load_packed<VEC, T>(p[order[q]], p[order[q]] ? bo : kBufNone, ring[q]);
+#pragma unroll
+    for (int q = 0; q < N; ++q) {
+      const int slot = order[q];
+      const Packed<VEC, T> v = ring[q % D];
+      if (q + D < N) buf_load_packed<VEC, T>(p[order[q + D]], p[order[q + D]] ? bo : kBufNone, ring[q % D]);
+      if (slot < NOUT) {
+        const bool isx = xid != nullptr && slot < st.n_out && st.o[slot].base == xid;
+#pragma unroll
+        for (int t = 0; t < VEC; ++t) r[slot][t] = cb[slot] * (isx ? xv[t] : unpack(v, t));
+      } else if (slot < NOUT + NKMAX) {
+        const int j = slot - NOUT;
+        const bool on = j < st.nk;
+        const bool kx = on && xid != nullptr && st.k[j] == xid;  // the RHS input row, already held
+        float kv[VEC];
+#pragma unroll
+        for (int t = 0; t < VEC; ++t) kv[t] = kx ? xv[t] : unpack(v, t);
+#pragma unroll
+        for (int i = 0; i < NOUT; ++i) {
+          const float c = (on && i < st.n_out) ? st.o[i].c[j] * sc : 0.f;
+#pragma unroll
+          for (int t = 0; t < VEC; ++t) r[i][t] = fmaf(c, kv[t], r[i][t]);
+        }
+        if constexpr (ERR) {
+          const float c = (on && has_err) ? st.err.c[j] * sc : 0.f;
+#pragma unroll
+          for (int t = 0; t < VEC; ++t) ev[t] = fmaf(c, kv[t], ev[t]);
+        }
+      } else if (slot == NOUT + NKMAX) {
+        if constexpr (ERR) {
+          const bool isx = xid != nullptr && has_err && st.err.base == xid;
+#pragma unroll
+          for (int t = 0; t < VEC; ++t) ev[t] = cb[NOUT] * (isx ? xv[t] : unpack(v, t));
+        }
+      } else if (y0v) {
+        *y0v = v;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NOUT; ++i) {
+      const float cf = i < st.n_out ? st.o[i].cf * sc : 0.f;
+#pragma unroll
+      for (int t = 0; t < VEC; ++t) r[i][t] = fmaf(cf, o[t], r[i][t]);
+    }
+    if constexpr (ERR) {
+      const float cf = has_err ? st.err.cf * sc : 0.f;
+#pragma unroll
+      for (int t = 0; t < VEC; ++t) ev[t] = fmaf(cf, o[t], ev[t]);
+    }
+    return;
+  }
   auto base_term = [&](const gnpde_stage_out_t& so, float (&acc)[VEC]) {
     if (so.base == nullptr) {
 #pragma unroll
@@ -441,7 +629,13 @@ __device__ __forceinline__ void wide_combine(const gnpde_stage_epilogue_t& st, i
   for (int j = 0; j < NKMAX; ++j) {
     if (j < st.nk) {
       Packed<VEC, T> kv;
-      load_packed<VEC>(as_t<T>(st.k[j]) + off, kv);
+      if (xid != nullptr && st.k[j] == xid) {
+#pragma unroll
+        for (int t = 0; t < Packed<VEC, T>::W; ++t) kv.d[t] = 0u;
+        pack_into<VEC, T>(xv, kv);
+      } else {
+        load_packed<VEC>(as_t<T>(st.k[j]) + off, kv);
+      }
 #pragma unroll
       for (int i = 0; i < NOUT; ++i) {
         if (i < st.n_out) {
@@ -476,9 +670,12 @@ __device__ __forceinline__ void wide_combine(const gnpde_stage_epilogue_t& st, i
 // slice's share of the embedded pair's squared error norm.
 template <int VEC, class T>
 __device__ __forceinline__ double err_terms(const gnpde_stage_epilogue_t& st, int64_t off, const float (&ev)[VEC],
-                                            const float (&y1)[VEC]) {
+                                            const float (&y1)[VEC], const Packed<VEC, T>* y0pre = nullptr) {
   Packed<VEC, T> y0v;
-  load_packed<VEC>(as_t<T>(st.err_y0) + off, y0v);
+  if (GNPDE_WIDE_BATCH && y0pre)  // loaded with the operands (wide_combine)
+    y0v = *y0pre;
+  else
+    load_packed<VEC>(as_t<T>(st.err_y0) + off, y0v);
   double d = 0.0;
 #pragma unroll
   for (int t = 0; t < VEC; ++t) {
@@ -512,15 +709,21 @@ __device__ __forceinline__ void epi_finish(const Epi& e, int64_t row, int cc, co
     store_vec<VEC>(as_t<T>(e.f) + row * e.ldf + cc, o);
     return;
   }
+  if (e.st.f_lin != 0.f && need_x) {  // f = x + sc*f_lin*f: the affine stage derivative (ABI 5)
+    const float cl = stage_scale(e.st) * e.st.f_lin;
+#pragma unroll
+    for (int t = 0; t < VEC; ++t) o[t] = fmaf(cl, o[t], unpack(p.xr, t));
+  }
   const int64_t off = row * e.ldf + cc;
   if (e.st.f_out) store_vec<VEC>(as_t<T>(e.st.f_out) + off, o);
   // the stage outputs' row (out_rows: the last step of a renumbered solve writes the caller's numbering)
   const int64_t oo = e.st.out_rows ? (int64_t)e.st.out_rows[row] * e.ldf + cc : off;
   if constexpr (STG == 4) {
     float xv[VEC], r[2][VEC], ev[VEC];
+    Packed<VEC, T> y0v;
 #pragma unroll
     for (int t = 0; t < VEC; ++t) xv[t] = need_x ? unpack(p.xr, t) : 0.f;
-    wide_combine<VEC, T>(e.st, off, o, (need_x && e.ldx == e.ldf) ? e.x : nullptr, xv, r, ev);
+    wide_combine<VEC, T>(e.st, off, o, (need_x && e.ldx == e.ldf) ? e.x : nullptr, xv, r, ev, &y0v);
 #pragma unroll
     for (int i = 0; i < 2; ++i)
       if (i < e.st.n_out) store_vec<VEC>(as_t<T>(e.st.o[i].out) + oo, r[i]);
@@ -528,7 +731,7 @@ __device__ __forceinline__ void epi_finish(const Epi& e, int64_t row, int cc, co
       float y1[VEC];
 #pragma unroll
       for (int t = 0; t < VEC; ++t) y1[t] = e.st.err_y1 == 1 ? r[1][t] : (e.st.err_y1 == 0 ? r[0][t] : xv[t]);
-      *dpart += err_terms<VEC, T>(e.st, off, ev, y1);
+      *dpart += err_terms<VEC, T>(e.st, off, ev, y1, &y0v);
     }
     return;
   } else {
@@ -563,7 +766,9 @@ __device__ __forceinline__ void epi_finish(const Epi& e, int64_t row, int cc, co
     } else {
       // the shared stage operands, prefetched before the gathers
       constexpr int NK = stage_kpre<STG>();
-      auto kval = [&](int j, int t) -> float { return unpack(p.kv[j], t); };
+      auto kval = [&](int j, int t) -> float {
+        return (need_x && e.st.k[j] == e.x && e.ldx == e.ldf) ? unpack(p.xr, t) : unpack(p.kv[j], t);
+      };
 #pragma unroll
       for (int i = 0; i < stage_nout<STG>(); ++i) {
         if (i >= e.st.n_out) break;
@@ -590,7 +795,6 @@ constexpr bool stage_rowsum() {
   return (stage_dot<STG>() && sizeof(T) == 4) || stage_err<STG>();
 }
 
-typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
 // an fp64 value moved by DPP (each 32-bit half), bound controls as in flash.hip's dpp_mov
 template <int CTRL>
@@ -671,33 +875,10 @@ inline int epi_stage_kind(const Epi& e) {
   return 2;
 }
 
-// ------------------------------------------------------------------ buffer memory ops
-// Raw buffer loads/stores take a 32-bit byte offset from a wave-uniform base,
-// and the hardware drops an access at or past num_records: a lane with nothing
-// to load or store passes kBufNone, so predicated accesses need no branch.
-// That matters on gfx9, where stores count in vmcnt: a store under a branch
-// makes the compiler's later waits conservative (vmcnt(0)), which serialises
-// every following store and load behind it.  Byte offsets must stay below
-// kBufRecords (callers check their buffer sizes).
-constexpr uint32_t kBufRecords = 0xffffff00u;
-constexpr uint32_t kBufNone = 0xfffffff0u;
-constexpr int kWaitVm0 = 0x0f70;  // s_waitcnt vmcnt(0) (expcnt, lgkmcnt at max)
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* p) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)kBufRecords, 0x00020000);
-}
-__device__ __forceinline__ void buf_store_f32(__amdgpu_buffer_rsrc_t r, uint32_t off, float v) {
-  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, off, 0, 0);
-}
-__device__ __forceinline__ void buf_store_f64(__amdgpu_buffer_rsrc_t r, uint32_t off, double v) {
-  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, off, 0, 0);
-}
-
 // Write-through (sc1) stores of VEC floats at byte offset off: the bytes reach
 // the memory side before the storing wave's s_waitcnt vmcnt(0) returns, so a
 // workgroup on any XCD can read them after an agent-scope acquire (the in-launch
 // hand-off of cdna_hip_programming.md §6 Guideline 16, R1) with no release fence.
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 constexpr int kAuxSc1 = 16;
 
 template <int VEC>

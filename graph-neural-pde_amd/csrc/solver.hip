@@ -164,9 +164,16 @@ __global__ __launch_bounds__(256) void stage_apply_kernel(int64_t R, int C, int6
 #pragma unroll
       for (int t = 0; t < VEC; ++t) xv[t] = 0.f;
     }
+    if (st.f_lin != 0.f && x) {  // f = x + sc*f_lin*f, as the fused epilogue (ABI 5)
+      const float cl = stage_scale(st) * st.f_lin;
+#pragma unroll
+      for (int t = 0; t < VEC; ++t) fv[t] = fmaf(cl, fv[t], xv[t]);
+    }
     if (st.f_out) store_vec<VEC>(as_t<T>(st.f_out) + off, fv);
     float r[2][VEC], ev[VEC];
-    wide_combine<VEC, T, NKMAX, NOUT, ERR>(st, off, fv, x ? reinterpret_cast<const float*>(x) : nullptr, xv, r, ev);
+    Packed<VEC, T> y0v;
+    wide_combine<VEC, T, NKMAX, NOUT, ERR>(st, off, fv, x ? reinterpret_cast<const float*>(x) : nullptr, xv, r, ev,
+                                           &y0v);
     const int64_t oo = st.out_rows ? (int64_t)st.out_rows[row] * ld + cc : off;
 #pragma unroll
     for (int i = 0; i < NOUT; ++i)
@@ -175,7 +182,7 @@ __global__ __launch_bounds__(256) void stage_apply_kernel(int64_t R, int C, int6
       float y1[VEC];
 #pragma unroll
       for (int t = 0; t < VEC; ++t) y1[t] = st.err_y1 == 1 ? r[1][t] : (st.err_y1 == 0 ? r[0][t] : xv[t]);
-      dpart += err_terms<VEC, T>(st, off, ev, y1);
+      dpart += err_terms<VEC, T>(st, off, ev, y1, &y0v);
     }
   }
   if (ERR && st.err_rows) {  // kernel-uniform
@@ -183,6 +190,113 @@ __global__ __launch_bounds__(256) void stage_apply_kernel(int64_t R, int C, int6
     for (int o = 1; o < GL; o <<= 1) dpart += __shfl_xor(dpart, o);
     if (live && gl == 0) st.err_rows[row] = dpart;
   }
+}
+
+// ------------------------------------------------------------------ initial step
+// torchdiffeq's _select_initial_step (misc.py, called by RKAdaptiveStepsizeODESolver
+// ._before_integrate with order - 1; integrator._RKAdaptive._select_initial_step):
+//   scale = atol + |y0| rtol,  d0 = rms(y0/scale),  d1 = rms(f0/scale)
+//   h0 = 1e-6 if d0 < 1e-5 or d1 < 1e-5 else 0.01 d0/d1;  f1 = f(t0 + h0, y0 + h0 f0)
+//   d2 = rms((f1 - f0)/scale)/h0
+//   h1 = max(1e-6, 1e-3 h0) if d1 <= 1e-15 and d2 <= 1e-15 else (0.01/max(d1, d2))^(1/order)
+//   first step = min(100 h0, h1)
+// as two fixed-order reductions (no float atomics: the same bits every run) whose
+// last block applies the scalar rules on the device, so the host reads the step
+// once.  Elementwise arithmetic in fp32 as torch runs it on an fp32 state (the
+// 0-d fp64 atol / rtol tensors do not promote it), squares summed in fp64.
+template <class T, int VEC, int PHASE>
+__global__ __launch_bounds__(256) void init_step_partial_kernel(int64_t n, const T* __restrict__ y0,
+                                                                 const T* __restrict__ f0, const T* __restrict__ f1,
+                                                                 float atol, float rtol, double* __restrict__ part) {
+  __shared__ double red[kBlock / kWave];
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  double a0 = 0.0, a1 = 0.0;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n / VEC; i += stride) {
+    float y[VEC], f[VEC], g[VEC];
+    load_vec<VEC>(y0 + i * VEC, y);
+    load_vec<VEC>(f0 + i * VEC, f);
+    if constexpr (PHASE == 1) load_vec<VEC>(f1 + i * VEC, g);
+#pragma unroll
+    for (int t = 0; t < VEC; ++t) {
+      const float sc = __fadd_rn(atol, __fmul_rn(fabsf(y[t]), rtol));  // no fma: torch rounds twice
+      if constexpr (PHASE == 0) {
+        const double q0 = (double)(y[t] / sc), q1 = (double)(f[t] / sc);
+        a0 = fma(q0, q0, a0);
+        a1 = fma(q1, q1, a1);
+      } else {
+        const double q = (double)((g[t] - f[t]) / sc);
+        a0 = fma(q, q, a0);
+      }
+    }
+  }
+  const double t0 = block_sum_f64(a0, red);
+  __syncthreads();
+  const double t1 = PHASE == 0 ? block_sum_f64(a1, red) : 0.0;
+  if (threadIdx.x == 0) {
+    part[2 * blockIdx.x] = t0;
+    part[2 * blockIdx.x + 1] = t1;
+  }
+}
+
+// h[0] = h0, h[1] = d1 (phase 0; hf = (float)h0, the probe's coefficient scale);
+// h[2] = the first step (phase 1)
+template <int PHASE>
+__global__ __launch_bounds__(256) void init_step_final_kernel(const double* __restrict__ part, int nb, double n,
+                                                               double order, double* h, float* hf) {
+  __shared__ double red[kBlock / kWave];
+  double a0 = 0.0, a1 = 0.0;
+  for (int i = threadIdx.x; i < nb; i += blockDim.x) {
+    a0 += part[2 * i];
+    a1 += part[2 * i + 1];
+  }
+  const double s0 = block_sum_f64(a0, red);
+  __syncthreads();
+  const double s1 = block_sum_f64(a1, red);
+  if (threadIdx.x != 0) return;
+  if constexpr (PHASE == 0) {
+    const double d0 = sqrt(s0 / n), d1 = sqrt(s1 / n);
+    const double h0 = (d0 < 1e-5 || d1 < 1e-5) ? 1e-6 : 0.01 * d0 / d1;
+    h[0] = h0;
+    h[1] = d1;
+    *hf = (float)h0;
+  } else {
+    const double h0 = h[0], d1 = h[1];
+    const double d2 = sqrt(s0 / n) / h0;
+    const double h1 = (d1 <= 1e-15 && d2 <= 1e-15) ? fmax(1e-6, h0 * 1e-3) : pow(0.01 / fmax(d1, d2), 1.0 / order);
+    h[2] = fmin(100.0 * h0, h1);
+    if (hf) *hf = (float)h[2];  // the first step's coefficient scale, in place for its launches
+  }
+}
+
+template <class T>
+static int initial_step(int64_t n, const T* y0, const T* f0, const T* f1, double atol, double rtol, double order,
+                        double* h, float* hf, void* workspace, size_t ws_bytes, void* stream) {
+  GNPDE_REQUIRE(n >= 1 && y0 && f0 && h && (f1 || hf) && workspace && order > 0.0, GNPDE_EINVAL,
+                "initial_step: bad arguments");
+  GNPDE_REQUIRE(ws_bytes >= 2 * sizeof(double) * kDotBlocks, GNPDE_EINVAL, "initial_step: workspace too small");
+  hipStream_t s = as_stream(stream);
+  double* part = static_cast<double*>(workspace);
+  const float a = (float)atol, r = (float)rtol;
+  const size_t vb = 4 * sizeof(T);
+  auto al = [&](const void* p) { return p == nullptr || reinterpret_cast<uintptr_t>(p) % vb == 0; };
+  const bool v4 = n % 4 == 0 && al(y0) && al(f0) && al(f1);
+  if (f1 == nullptr) {
+    if (v4)
+      init_step_partial_kernel<T, 4, 0><<<kDotBlocks, kBlock, 0, s>>>(n, y0, f0, f1, a, r, part);
+    else
+      init_step_partial_kernel<T, 1, 0><<<kDotBlocks, kBlock, 0, s>>>(n, y0, f0, f1, a, r, part);
+    GNPDE_LAUNCH_CHECK();
+    init_step_final_kernel<0><<<1, kBlock, 0, s>>>(part, kDotBlocks, (double)n, order, h, hf);
+  } else {
+    if (v4)
+      init_step_partial_kernel<T, 4, 1><<<kDotBlocks, kBlock, 0, s>>>(n, y0, f0, f1, a, r, part);
+    else
+      init_step_partial_kernel<T, 1, 1><<<kDotBlocks, kBlock, 0, s>>>(n, y0, f0, f1, a, r, part);
+    GNPDE_LAUNCH_CHECK();
+    init_step_final_kernel<1><<<1, kBlock, 0, s>>>(part, kDotBlocks, (double)n, order, h, hf);
+  }
+  GNPDE_LAUNCH_CHECK();
+  return GNPDE_OK;
 }
 
 template <int VEC, class T>
@@ -223,6 +337,7 @@ static int stage_apply(int64_t R, int64_t C, int64_t ld, const T* f, const T* x,
     GNPDE_REQUIRE(st.o[i].out != reinterpret_cast<const float*>(x), GNPDE_EINVAL, "stage_apply: output %d aliases x",
                   i);
   GNPDE_REQUIRE(!needs_x || x, GNPDE_EINVAL, "stage_apply: the error tolerance reads y1 = x, which is NULL");
+  GNPDE_REQUIRE(st.f_lin == 0.f || (x && f), GNPDE_EINVAL, "stage_apply: f_lin needs f and the input x");
   if (R == 0) return GNPDE_OK;
   // widest vector every row array allows
   const int kMax = 16 / (int)sizeof(T);
@@ -347,6 +462,68 @@ extern "C" int gnpde_rk_combine_f32(int64_t n, const float* y0, int nk, const fl
     rk_combine_kernel<true><<<grid, kBlock, 0, s>>>(n, y0, a, out);
   else
     rk_combine_kernel<false><<<grid, kBlock, 0, s>>>(n, y0, a, out);
+  GNPDE_LAUNCH_CHECK();
+  return GNPDE_OK;
+}
+
+extern "C" size_t gnpde_initial_step_workspace_bytes(void) { return 2 * sizeof(double) * kDotBlocks; }
+
+extern "C" int gnpde_initial_step_f32(int64_t n, const float* y0, const float* f0, const float* f1, double atol,
+                                      double rtol, double order, double* h, float* hf, void* workspace,
+                                      size_t workspace_bytes, void* stream) {
+  return initial_step<float>(n, y0, f0, f1, atol, rtol, order, h, hf, workspace, workspace_bytes, stream);
+}
+
+extern "C" int gnpde_initial_step_bf16(int64_t n, const uint16_t* y0, const uint16_t* f0, const uint16_t* f1,
+                                       double atol, double rtol, double order, double* h, float* hf, void* workspace,
+                                       size_t workspace_bytes, void* stream) {
+  return initial_step<bf16>(n, reinterpret_cast<const bf16*>(y0), reinterpret_cast<const bf16*>(f0),
+                            reinterpret_cast<const bf16*>(f1), atol, rtol, order, h, hf, workspace, workspace_bytes,
+                            stream);
+}
+
+// torchdiffeq's step-size controller (rk_common.py _optimal_step_size, the adaptive
+// loop's accept test) on the device, fused with the last level of the step's error
+// reduction (the same fixed order as gnpde_sum_f64): the host reads rec = {error
+// ratio, dt of the step, dt of the next step, squared error sum} once, and the next
+// step's coefficient scale is already in place (no host fill between two replayed
+// steps, no separate sum launch).
+__global__ __launch_bounds__(256) void adaptive_control_kernel(const double* __restrict__ part, int nb, double n,
+                                                                double order, double safety, double ifactor,
+                                                                double dfactor, double* dt, float* scale, double* rec) {
+  __shared__ double red[kBlock / kWave];
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < nb; i += blockDim.x) acc += part[i];
+  const double e2 = block_sum_f64(acc, red);
+  if (threadIdx.x != 0) return;
+  const double h = *dt;
+  const double ratio = n > 0.0 ? sqrt(e2 / n) : 0.0;
+  double next;
+  if (ratio == 0.0) {
+    next = h * ifactor;
+  } else {
+    const double df = ratio < 1.0 ? 1.0 : dfactor;
+    next = h * fmin(ifactor, fmax(safety / pow(ratio, 1.0 / order), df));
+  }
+  rec[0] = ratio;
+  rec[1] = h;
+  rec[2] = next;
+  rec[3] = e2;
+  *dt = next;
+  *scale = (float)next;
+}
+
+extern "C" int gnpde_adaptive_control(int64_t nrows, const double* err_rows, double n, double order, double safety,
+                                      double ifactor, double dfactor, double* dt, float* scale, double* rec,
+                                      void* workspace, size_t workspace_bytes, void* stream) {
+  GNPDE_REQUIRE(nrows >= 0 && (err_rows || nrows == 0) && dt && scale && rec && workspace && order > 0.0,
+                GNPDE_EINVAL, "adaptive_control: bad arguments");
+  GNPDE_REQUIRE(workspace_bytes >= sizeof(double) * kDotBlocks, GNPDE_EINVAL, "adaptive_control: workspace too small");
+  hipStream_t s = as_stream(stream);
+  double* part = static_cast<double*>(workspace);
+  sum_partial_kernel<<<kDotBlocks, kBlock, 0, s>>>(nrows, err_rows, part);
+  GNPDE_LAUNCH_CHECK();
+  adaptive_control_kernel<<<1, kBlock, 0, s>>>(part, kDotBlocks, n, order, safety, ifactor, dfactor, dt, scale, rec);
   GNPDE_LAUNCH_CHECK();
   return GNPDE_OK;
 }

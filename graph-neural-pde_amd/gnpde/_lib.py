@@ -31,7 +31,8 @@ class StageEpilogue(ctypes.Structure):
                 ("out_rows", ctypes.c_void_p), ("dot_with", ctypes.c_void_p), ("dot_rows", ctypes.c_void_p),
                 ("dot_coef", ctypes.c_double), ("dot_accumulate", ctypes.c_int),
                 ("err_rows", ctypes.c_void_p), ("err", StageOut), ("err_y0", ctypes.c_void_p), ("err_y1", ctypes.c_int),
-                ("atol", ctypes.c_double), ("rtol", ctypes.c_double), ("coef_scale", ctypes.c_void_p)]
+                ("atol", ctypes.c_double), ("rtol", ctypes.c_double), ("coef_scale", ctypes.c_void_p),
+                ("f_lin", ctypes.c_float)]
 
 
 c_i32p = ctypes.POINTER(ctypes.c_int32)
@@ -72,6 +73,10 @@ SIGNATURES = {
     "gnpde_attn_dot_rhs_bf16": (_int, [_vp, _i64, _vp, _i64, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _i64, _vp, _i64, _vp,
                                       _i64, _vp, _vp, _int, _vp, _i64, _vp, _i64, ctypes.POINTER(StageEpilogue), _vp]),
     "gnpde_rows_copy": (_int, [_vp, _i64, _i64, _vp, _vp, _vp, _vp]),
+    "gnpde_initial_step_workspace_bytes": (_size, []),
+    "gnpde_adaptive_control": (_int, [_i64, _vp, _f64, _f64, _f64, _f64, _f64, _vp, _vp, _vp, _vp, _size, _vp]),
+    "gnpde_initial_step_f32": (_int, [_i64, _vp, _vp, _vp, _f64, _f64, _f64, _vp, _vp, _vp, _size, _vp]),
+    "gnpde_initial_step_bf16": (_int, [_i64, _vp, _vp, _vp, _f64, _f64, _f64, _vp, _vp, _vp, _size, _vp]),
     "gnpde_stage_apply_f32": (_int, [_i64, _i64, _i64, _vp, _vp, ctypes.POINTER(StageEpilogue), _vp]),
     "gnpde_stage_apply_bf16": (_int, [_i64, _i64, _i64, _vp, _vp, ctypes.POINTER(StageEpilogue), _vp]),
     "gnpde_seg_long_edges": (_int, []),
@@ -118,7 +123,7 @@ SIGNATURES = {
 }
 
 # constants mirrored from include/gnpde.h
-ABI_VERSION = 4
+ABI_VERSION = 5
 OK = 0
 EINVAL = -1
 EHIP = -2

@@ -54,6 +54,11 @@ class GraphData(object):
 class ODEFunc(nn.Module):
     """Base RHS module (src/base_classes.py:116-134)."""
 
+    # f(t, x) does not read t (every RHS of the path: src/function_laplacian_diffusion.py:60-77,
+    # src/function_transformer_attention.py:44-59): the integrator may replay captured steps whose
+    # recorded stage times are stale, and evaluate the initial-step probe without reading h0 back
+    autonomous = True
+
     def __init__(self, opt, device):
         super(ODEFunc, self).__init__()
         self.opt = opt

@@ -166,6 +166,8 @@ class RowShardedLaplacian(object):
     column-striped solves): scatter() / unpad() map from / to the caller's numbering,
     and x0_local must come from scatter(x0)."""
 
+    autonomous = True  # the RHS does not read t (gnpde.base_classes.ODEFunc.autonomous)
+
     graph_capturable = False  # an RCCL all-gather per RHS: the integrator runs it eagerly
     fused_adaptive = False    # the adaptive solvers' wide stages run in column stripes or unsharded
 
@@ -290,6 +292,8 @@ def _local_plan(csr, r0, r1, chunk, pos0=None):
 
 class ColumnShardedLaplacian(object):
     """Column-striped Laplacian RHS: no communication per RHS."""
+
+    autonomous = True  # the RHS does not read t (gnpde.base_classes.ODEFunc.autonomous)
 
     def __init__(self, edge_index, edge_weight, num_nodes, C, alpha, beta=None, x0_local=None, add_source=False,
                  alpha_sigmoid=True, group=None, local_rhs=None, chunk=ops.DEFAULT_CHUNK):
@@ -455,6 +459,8 @@ class ColumnShardedTransformer(object):
     rhs_stage (fixed-grid fused stages, the adaptive solvers' wide stages),
     global_rms_norm / reduce_error_sq (dopri5's error norm over all stripes)."""
 
+    autonomous = True  # the RHS does not read t (gnpde.base_classes.ODEFunc.autonomous)
+
     graph_capturable = False  # collectives per RHS
 
     def __init__(self, edge_index, num_nodes, C, Wq, bq, Wk, bk, heads, norm_idx, alpha, score_mode='reference',
@@ -575,6 +581,8 @@ class RowShardedTransformer(object):
       (ops.spmm_rhs_rows), written through pointers shifted to its block.
 
     B = 1 (one graph; batches shard as replicas, shard_batch)."""
+
+    autonomous = True  # the RHS does not read t (gnpde.base_classes.ODEFunc.autonomous)
 
     graph_capturable = False  # collectives per RHS
     fused_adaptive = False    # the adaptive solvers' wide stages run in column stripes or unsharded

@@ -138,15 +138,21 @@ class LaplacianODEFunc(ODEFunc):
         w, tag = self._weights_tensor()
         return ops.spmm_rhs(g, self.csr_weights(g, w, tag), x, rhs=False)
 
-    def rhs_stage(self, t, x, stage):
+    # f(x) = sigma(alpha)(A - I) x [+ beta x0] is affine in x with the weights fixed for a solve
+    # (every block: constant, attention / hard_attention / mixed weights are computed once per forward)
+    affine = True
+
+    def rhs_stage(self, t, x, stage, linear=False):
         """forward(t, x) with the solver's stage combination fused into the K1
-        epilogue (gnpde.integrator, no-grad fixed-grid solvers)."""
+        epilogue (gnpde.integrator, no-grad fixed-grid solvers).  linear=True
+        evaluates the linear part sigma(alpha)(A - I) x alone (no source term):
+        the adaptive solvers' affine stage derivatives (Stage.f_lin)."""
         if self.nfe > self.opt["max_nfe"]:
             raise MaxNFEException
         self.nfe += 1
         g = self.graph_for(x)
         w, tag = self._weights_tensor()
-        add_source = bool(self.opt.get('add_source', False))
+        add_source = bool(self.opt.get('add_source', False)) and not linear
         x0 = self.stable_x0(x) if add_source else None
         ops.spmm_rhs(g, self.csr_weights(g, w, tag), x, x0=x0, alpha=self.alpha_train.detach(),
                      beta=self.beta_train.detach(), rhs=True, alpha_sigmoid=not self.opt.get('no_alpha_sigmoid', False),

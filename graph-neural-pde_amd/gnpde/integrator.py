@@ -406,6 +406,13 @@ def _graph_cache_key(func, method, y, state):
             tuple(id(o) for o in state))
 
 
+def _replayable(func):
+    """Steps of ``func`` may be captured and replayed as hipGraphs: no collective per RHS
+    (graph_capturable) and f(t, x) independent of t (autonomous) — a replay passes the
+    stage times recorded at capture."""
+    return getattr(func, 'graph_capturable', True) and getattr(func, 'autonomous', False)
+
+
 def _nfe_headroom(func, n):
     """True when n more RHS calls cannot trip the MaxNFEException guard (the
     eager path raises at the exact call, as the reference does)."""
@@ -833,7 +840,7 @@ def _solve_fused(func, y0, t_h, steps, method, graph):
     n = len(steps)
     if graph is None:
         # a RHS with a collective inside (dist.RowShardedLaplacian) opts out of capture
-        graph = n >= GRAPH_MIN_STEPS and getattr(func, 'graph_capturable', True)
+        graph = n >= GRAPH_MIN_STEPS and _replayable(func)
     sol = torch.empty((len(t_h),) + tuple(y0.shape), dtype=y0.dtype, device=y0.device)
     pool = _state_pool(func, y0)
     bufs, ws = pool.bufs, pool.ws
@@ -938,14 +945,29 @@ class _RKAdaptive(object):
         dev = y0.device
         self.func, self.y0, self.combine, self.norm = func, y0, combine, norm
         self.dtype = dtype
-        self.rtol = torch.as_tensor(rtol, dtype=dtype, device=dev)
-        self.atol = torch.as_tensor(atol, dtype=dtype, device=dev)
-        self.safety = torch.as_tensor(safety, dtype=dtype, device=dev)
-        self.ifactor = torch.as_tensor(ifactor, dtype=dtype, device=dev)
-        self.dfactor = torch.as_tensor(dfactor, dtype=dtype, device=dev)
-        self.first_step = None if first_step is None else torch.as_tensor(first_step, dtype=dtype, device=dev)
+        # the controller's scalars as given; their device tensors (the torch restatement's
+        # arithmetic) are made on first use, so the fused solver (host floats) moves none
+        self._scalars = {'rtol': rtol, 'atol': atol, 'safety': safety, 'ifactor': ifactor, 'dfactor': dfactor,
+                         'first_step': first_step}
+        self._tensors = {}
+        self._dev = dev
         self.max_num_steps = max_num_steps
         self.n_steps = 0
+
+    def _scalar_tensor(self, name):
+        v = self._tensors.get(name)
+        if v is None:
+            raw = self._scalars[name]
+            v = None if raw is None else torch.as_tensor(raw, dtype=self.dtype, device=self._dev)
+            self._tensors[name] = v
+        return v
+
+    rtol = property(lambda self: self._scalar_tensor('rtol'))
+    atol = property(lambda self: self._scalar_tensor('atol'))
+    safety = property(lambda self: self._scalar_tensor('safety'))
+    ifactor = property(lambda self: self._scalar_tensor('ifactor'))
+    dfactor = property(lambda self: self._scalar_tensor('dfactor'))
+    first_step = property(lambda self: self._scalar_tensor('first_step'))
 
     def _select_initial_step(self, t0, f0):
         y0, rtol, atol, norm, func = self.y0, self.rtol, self.atol, self.norm, self.func
@@ -1179,6 +1201,7 @@ def _fused_adaptive_ok(func, y0, combine, options):
 # step costs one graph launch and one host read.  GNPDE_ADAPTIVE_GRAPH=0 runs
 # every step eagerly.
 ADAPTIVE_GRAPH = os.environ.get('GNPDE_ADAPTIVE_GRAPH', '1') != '0'
+AFFINE_STAGE = os.environ.get('GNPDE_AFFINE_STAGE', '1') != '0'
 _ADAPTIVE_CACHE = weakref.WeakKeyDictionary()  # module -> (key, _AdaptiveState)
 
 
@@ -1201,6 +1224,14 @@ class _AdaptiveState(object):
         # the step size the stage coefficients are scaled by (device fp32 scalar; the host-stage
         # test RHS objects apply it in their own precision)
         self.scale = torch.zeros((), dtype=torch.float32 if not host else torch.float64, device=y0.device)
+        # the device controller's step size (fp64) and its record {ratio, dt, next dt} (device solves)
+        # h = {h0, d1, first step} of the device initial-step selection; dt is h[2] (a view), so
+        # the first step's size and scale are in place when the selection ends
+        self.h = None if host else torch.zeros(3, dtype=torch.float64, device=y0.device)
+        self.dt = None if host else self.h[2]
+        self.rec = None if host else torch.zeros(4, dtype=torch.float64, device=y0.device)
+        self.ws = None if host else torch.empty(_lib.fn("gnpde_dot_workspace_bytes")(), dtype=torch.uint8,
+                                                device=y0.device)
         self.graphs = {}   # (id Y, id K0, mid) -> (graph, error-sum tensor)
         self.mempool = None
         self.warm = False
@@ -1220,6 +1251,13 @@ class _RKAdaptiveFused(_RKAdaptive):
         self.plan = _adaptive_plan(method)
         self.host = not y0.is_cuda
         self.rtol_f, self.atol_f = float(rtol), float(atol)
+        # f(y) = L y + s (func.affine): the step's first stage derivative is k0 + dt b00 L k0 from
+        # a launch over k0 (Stage.f_lin) — no X0 = y0 + dt b00 k0 pass.  Needs k0 = f(y0): the FSAL
+        # pairs (dopri5, bosh3); torchdiffeq's non-FSAL pairs carry k0 = the last stage of the previous
+        # step instead.  GNPDE_AFFINE_STAGE=0 disables it.
+        self.affine = bool(getattr(func, 'affine', False)) and AFFINE_STAGE and self.plan.fsal
+        sc = self._scalars
+        self.safety_f, self.ifactor_f, self.dfactor_f = float(sc['safety']), float(sc['ifactor']), float(sc['dfactor'])
 
     # ---- device primitives (host-stage RHS objects supply CPU versions: tests only)
     def _apply(self, stage, f, x, like):
@@ -1250,36 +1288,89 @@ class _RKAdaptiveFused(_RKAdaptive):
         P = self.plan
         bufs = st.bufs
         L = P.launches[i]
+        lin = self.affine and i == 0
+        if lin:
+            # the affine first stage: the launch reads k0 and forms k1 = k0 + dt b00 L k0 (Stage.f_lin),
+            # never X0 = y0 + dt b00 k0; its combinations on X0 are restated on y0 (X0 = y0 + dt b00 k0)
+            x = bufs['K0']
         outs = []
         for key, dst in (('next', 'X%d' % (i + 1)), ('y1', 'Y1'), ('epart', 'E')):
             if L[key] is not None:
-                b, cb, cf, ks = self._combo(L[key], bufs, x)
+                spec = self._on_y0(L[key]) if lin else L[key]
+                b, cb, cf, ks = self._combo(spec, bufs, x)
                 outs.append((bufs[dst], b, cb, cf, ks))
         err = None
         if L['err'] is not None:
-            b, cb, cf, ks = self._combo(L['err'], bufs, x)
+            spec = self._on_y0(L['err']) if lin else L['err']
+            if lin and L['y1'] is None:
+                raise RuntimeError("gnpde: an affine one-stage tableau needs its y1 output for the tolerance")
+            b, cb, cf, ks = self._combo(spec, bufs, x)
             err = (st.rows, (b, cb, cf, ks), bufs['Y'], 0 if L['y1'] is not None else -1, self.atol_f, self.rtol_f)
         j = i + 1
         f_out = bufs['K%d' % j] if (j in P.store or (mid and j in P.store_mid)) else None
-        self.func.rhs_stage(t, x, ops.Stage(f_out=f_out, outs=outs, err=err, scale=st.scale))
+        if lin:
+            self.func.rhs_stage(t, x, ops.Stage(f_out=f_out, outs=outs, err=err, scale=st.scale,
+                                                f_lin=P.beta[0][0]), linear=True)
+        else:
+            self.func.rhs_stage(t, x, ops.Stage(f_out=f_out, outs=outs, err=err, scale=st.scale))
+
+    def _on_y0(self, spec):
+        """A launch-0 combination on base X0 restated on y0: X0 + dt(sum d_j k_j + cf f)
+        = y0 + dt((b00 + d_0) k0 + ...) (X0 = y0 + dt b00 k0)."""
+        base, terms, cf = spec
+        if base != 'X':
+            return spec
+        b00 = self.plan.beta[0][0]
+        d = dict(terms)
+        d['K0'] = d.get('K0', 0.0) + b00
+        return ('Y', [(k, c) for k, c in d.items() if c != 0.0], cf)
 
     def _step(self, st, t_cur, dt, mid):
         """Enqueue one step (stage-input pass, RHS launches, error reduction); returns
         the device error sum."""
         P = self.plan
         bufs = st.bufs
-        self._apply(ops.Stage(outs=[(bufs['X0'], bufs['Y'], 1.0, 0.0, [(bufs['K0'], P.beta[0][0])])],
-                              scale=st.scale), None, None, bufs['Y'])
+        if not self.affine:  # the first stage input X0 = y0 + dt b00 k0 (the affine mode never forms it)
+            self._apply(ops.Stage(outs=[(bufs['X0'], bufs['Y'], 1.0, 0.0, [(bufs['K0'], P.beta[0][0])])],
+                                  scale=st.scale), None, None, bufs['Y'])
         for i in range(P.ns):
             ti = t_cur + dt if P.alpha[i] == 1. else t_cur + P.alpha[i] * dt
             self._launch(i, st, bufs['X%d' % i], ti, mid)
+        if self._dev_control():  # the error sum and the controller: two launches, no host work
+            ops.adaptive_control(st.rows, st.rows.numel() * self.C, self.order, self.safety_f, self.ifactor_f,
+                                 self.dfactor_f, st.dt, st.scale, st.rec, ws=st.ws)
+            return st.rec
         return self._err_sum(st.rows)
+
+    def _dev_control(self):
+        """The step-size controller runs on the device (a device solve with the
+        default RMS norm): the host reads {ratio, dt, next dt} once per step."""
+        return not self.host and 'norm' not in self.options
+
+    def _initial_step_device(self, st, t0):
+        """_select_initial_step on the device (gnpde_initial_step_*: the two fixed-order
+        norm reductions and the scalar rules in HIP, the probe y0 + h0 f0 as one stage
+        pass with h0 as its device coefficient scale, f1 by the RHS): one host read.
+        The probe's RHS is evaluated at t0 (the RHS is autonomous: h0 stays on the
+        device)."""
+        bufs = st.bufs
+        Y, K0 = bufs['Y'], bufs['K0']
+        h, hf = st.h, st.scale  # h[2] is st.dt: the device controller starts from it
+        ops.initial_step(Y, K0, None, self.atol_f, self.rtol_f, self.order, h, hf)
+        probe, f1 = bufs['X0'], bufs['Y1']  # free until the first step
+        if self.affine:  # f1 = f0 + h0 L f0 from a launch over f0 (no probe pass)
+            self.func.rhs_stage(t0, K0, ops.Stage(f_out=f1, scale=hf, f_lin=1.0), linear=True)
+        else:
+            ops.stage_apply(ops.Stage(outs=[(probe, Y, 1.0, 0.0, [(K0, 1.0)])], scale=hf), None, None, Y)
+            self.func.rhs_stage(t0, probe, ops.Stage(f_out=f1))
+        ops.initial_step(Y, K0, f1, self.atol_f, self.rtol_f, self.order, h, hf)
+        return float(h[2])
 
     def _state(self, y0):
         """The module's cached buffers / graphs for this shape, tolerance and graph
         state (a new entry when any of them changed)."""
         P = self.plan
-        if self.host or not ADAPTIVE_GRAPH or not getattr(self.func, 'graph_capturable', True) or \
+        if self.host or not ADAPTIVE_GRAPH or not _replayable(self.func) or \
                 'norm' in self.options:  # a sharded RHS's global norm: a collective inside the step
             return _AdaptiveState(P, y0, self.host), False
         state = _capture_state(self.func, y0)
@@ -1322,29 +1413,65 @@ class _RKAdaptiveFused(_RKAdaptive):
         return err
 
     def integrate(self, t):
+        """The adaptive loop.  A device solve of a module offering a locality numbering
+        (ops.NodeLayout, as the fixed-grid path) runs in it: the entry pass writes
+        sol[0] and the permuted state from one read of y0, every RHS launch gathers
+        from the degree-ordered rows, and outputs return to the caller's numbering
+        (the dense output's single pass stores there directly, out_rows).  Row
+        values are bit-identical to the user numbering; the error norm's fixed-order
+        sum runs over rows in the other order (fp64 rounding only)."""
         P = self.plan
-        th = [float(v) for v in t.detach().to(torch.float64).cpu().tolist()]
+        th = _host_times(t)  # cached per time tensor: no device read for an ODEblock's self.t
         y0 = self.y0.contiguous()
         self.C = y0.shape[-1]
         dev = y0.device
         sol = torch.empty((len(th),) + tuple(y0.shape), dtype=y0.dtype, device=dev)
-        sol[0].copy_(y0)
+        lay = None if self.host else _node_layout(self.func, y0)
+        self.lay = lay
+        if lay is not None:
+            self.func._layout = lay
+        try:
+            return self._integrate(th, y0, sol, lay)
+        finally:
+            if lay is not None:
+                self.func._layout = None
+
+    def _integrate(self, th, y0, sol, lay):
+        P = self.plan
+        dev = y0.device
         st, graphs_ok = self._state(y0)
         bufs = st.bufs
-        bufs['Y'].copy_(y0)
-        t0 = torch.tensor(th[0], dtype=torch.float64)
-        f0 = self.func(t0, bufs['Y'])
-        bufs['K0'].copy_(f0)
-        if self.first_step is None:
-            dt = float(self._select_initial_step(t0.to(dev) if not self.host else t0, bufs['K0']))
+        if self.host:
+            sol[0].copy_(y0)
+            bufs['Y'].copy_(y0)
         else:
-            dt = float(self.first_step)
+            _entry_copy(y0, bufs['Y'], sol[0], lay.order if lay is not None else None)
+        t0 = torch.tensor(th[0], dtype=torch.float64)
+        dev_init = not self.host and getattr(self.func, 'autonomous', False) and 'norm' not in self.options
+        if dev_init:  # f0 straight into K0 (the RHS epilogue's f_out)
+            self.func.rhs_stage(t0, bufs['Y'], ops.Stage(f_out=bufs['K0']))
+        else:
+            f0 = self.func(t0, bufs['Y'])
+            bufs['K0'].copy_(f0)
+        dt_on_device = False
+        if self._scalars['first_step'] is None:
+            if dev_init:
+                dt = self._initial_step_device(st, t0)
+                dt_on_device = True  # st.dt and st.scale hold it already
+            else:
+                dt = float(self._select_initial_step(t0.to(dev) if not self.host else t0, bufs['K0']))
+        else:
+            dt = float(self._scalars['first_step'])
         t_cur = th[0]
         last = None  # (t_prev, dt) of the last accepted step
         self._dense = None
         order = float(P.order)
-        safety, ifactor, dfactor = float(self.safety), float(self.ifactor), float(self.dfactor)
+        safety, ifactor, dfactor = self.safety_f, self.ifactor_f, self.dfactor_f
         kn = 'K%d' % P.ns
+        dev_ctl = self._dev_control()
+        if dev_ctl and not dt_on_device:  # the device controller carries dt (and the scale) from step to step
+            st.dt.fill_(dt)
+            st.scale.fill_(dt)
         for i_out in range(1, len(th)):
             next_t = th[i_out]
             while next_t > t_cur:
@@ -1353,9 +1480,13 @@ class _RKAdaptiveFused(_RKAdaptive):
                 if self.n_steps >= self.max_num_steps:
                     raise AssertionError('max_num_steps exceeded ({}>={})'.format(self.n_steps, self.max_num_steps))
                 mid = t_cur + dt >= next_t  # an accepted step would cross an output time: keep the dense-output k's
-                st.scale.fill_(dt)
+                if not dev_ctl:
+                    st.scale.fill_(dt)
                 err = self._run_step(st, graphs_ok, t_cur, dt, mid)
-                if err.dim() == 0:
+                dt_next = None
+                if dev_ctl:
+                    ratio, _dt, dt_next, _e2 = err.tolist()  # the one host read of the step
+                elif err.dim() == 0:
                     ratio = math.sqrt(float(err) / (y0.numel()))  # the one host read of the step
                 else:
                     e2, n = (float(v) for v in err.tolist())
@@ -1370,23 +1501,31 @@ class _RKAdaptiveFused(_RKAdaptive):
                     bufs['K0'], bufs[kn] = bufs[kn], bufs['K0']
                     if P.fsal:
                         bufs['X%d' % (P.ns - 1)] = bufs['Y1']
-                if ratio == 0:
+                if dt_next is not None:
+                    dt = dt_next
+                elif ratio == 0:
                     dt = dt * ifactor
                 else:
                     df = 1.0 if ratio < 1 else dfactor
                     dt = dt * min(ifactor, max(safety / ratio ** (1.0 / order), df))
                 self.n_steps += 1
             if next_t == t_cur or last is None:
-                sol[i_out].copy_(bufs['Y'])
+                if self.host:
+                    sol[i_out].copy_(bufs['Y'])
+                else:
+                    _to_user(bufs['Y'], sol[i_out], lay)
             else:
-                self._interp_into(sol[i_out], last, next_t, t_cur)
+                self._interp_into(sol[i_out], last, next_t, t_cur, lay)
         return sol
 
-    def _interp_into(self, out, last, t, t1):
+    def _interp_into(self, out, last, t, t1, lay=None):
         """torchdiffeq's 4th-order dense output (_interp_fit / _interp_evaluate, with the
-        tableau's mid-point coefficients) of the last accepted step at time t, as two
-        stage passes: y_mid = y0 + dt sum_j c_mid[j] k_j, then the polynomial, a
-        combination of y0, y1, y_mid, f0 and f1."""
+        tableau's mid-point coefficients) of the last accepted step at time t:
+        y_mid = y0 + dt sum_j c_mid[j] k_j, then the polynomial, a combination of y0,
+        y1, y_mid, f0 and f1 — folded into ONE stage pass over y0 (its base), f1 (its
+        f input) and the other rows as operands (y_mid substituted), stored in the
+        caller's numbering (out_rows); two passes when the operands exceed the
+        stage's table."""
         P = self.plan
         t0, dt = last
         d = self._dense
@@ -1394,9 +1533,6 @@ class _RKAdaptiveFused(_RKAdaptive):
             raise RuntimeError("gnpde: dense output of a step whose stage derivatives were not kept")
         y_prev, y_cur = d['Y'], d['Y1']
         f0, f1 = d['K0'], d['K%d' % P.ns]
-        ymid = torch.empty_like(out)
-        terms = [(d['K%d' % j], dt * P.c_mid[j]) for j in range(P.ns + 1) if _nz(P.c_mid[j])]
-        self._apply(ops.Stage(outs=[(ymid, y_prev, 1.0, 0.0, terms)]), None, None, y_prev)
         x = (t - t0) / (t1 - t0)
         x2, x3, x4 = x * x, x * x * x, x * x * x * x
         cy0 = 1.0 - 11.0 * x2 + 18.0 * x3 - 8.0 * x4
@@ -1404,8 +1540,49 @@ class _RKAdaptiveFused(_RKAdaptive):
         cym = 16.0 * x2 - 32.0 * x3 + 16.0 * x4
         cf0 = dt * (x - 4.0 * x2 + 5.0 * x3 - 2.0 * x4)
         cf1 = dt * (x2 - 3.0 * x3 + 2.0 * x4)
-        self._apply(ops.Stage(outs=[(out, y_prev, cy0, 0.0, [(y_cur, cy1), (ymid, cym), (f0, cf0), (f1, cf1)])]),
-                    None, None, y_prev)
+        rows = None if (lay is None or self.host) else lay.order32
+        # one pass: out = (cy0 + cym) y0 + cy1 y1 + sum_j cym dt c_mid[j] k_j + cf0 f0 + cf1 f1
+        coef = {}  # id -> [tensor, coefficient] of the operands besides y0 (base) and f1 (f input)
+        order_ = []
+
+        def add(tn, c):
+            if c == 0.0:
+                return
+            if id(tn) not in coef:
+                coef[id(tn)] = [tn, 0.0]
+                order_.append(id(tn))
+            coef[id(tn)][1] += c
+        add(y_cur, cy1)
+        for j in range(P.ns + 1):
+            if _nz(P.c_mid[j]):
+                add(d['K%d' % j] if j < P.ns else f1, cym * dt * P.c_mid[j])
+        add(f0, cf0)
+        cf_f1 = coef.pop(id(f1))[1] + cf1 if id(f1) in coef else cf1
+        terms = [tuple(coef[k]) for k in order_ if k in coef]
+        if len(terms) <= _lib.STAGE_MAX_K and (not self.host or hasattr(self.func, 'host_stage_apply')):
+            stage = ops.Stage(outs=[(out, y_prev, cy0 + cym, cf_f1, terms)], out_rows=rows)
+            if self.host:
+                self.func.host_stage_apply(stage, f1, y_prev, y_prev)
+            else:
+                ops.stage_apply(stage, f1, y_prev, y_prev)
+            return
+        ymid = torch.empty_like(out)
+        mterms = [(d['K%d' % j], dt * P.c_mid[j]) for j in range(P.ns + 1) if _nz(P.c_mid[j])]
+        self._apply(ops.Stage(outs=[(ymid, y_prev, 1.0, 0.0, mterms)]), None, None, y_prev)
+        self._apply(ops.Stage(outs=[(out, y_prev, cy0, 0.0, [(y_cur, cy1), (ymid, cym), (f0, cf0), (f1, cf1)])],
+                              out_rows=rows), None, None, y_prev)
+
+
+def adaptive_step_graph(func):
+    """A captured fused adaptive step of ``func`` (the last solve's cache entry), or
+    None: replaying it re-runs one whole step (its launches, the error reduction and
+    the device controller) on the buffers it was captured with — the measurement hook
+    of bench.py's dopri5 line and tools/pmc_run.py (not part of a solve)."""
+    hit = _ADAPTIVE_CACHE.get(func)
+    if hit is None or not hit[1].graphs:
+        return None
+    ent = next(iter(hit[1].graphs.values()))
+    return ent[0]
 
 
 def odeint(func, y0, t, rtol=1e-7, atol=1e-9, method=None, options=None, combine=None):

@@ -531,8 +531,10 @@ class Stage(object):
     in fp64 with e the combination, tol = atol + rtol * max(|y0|, |y1|), y1 = the
     RHS input (y1_out = -1) or output ``y1_out``."""
 
-    def __init__(self, f_out=None, outs=(), out_rows=None, dot=None, err=None, scale=None):
+    def __init__(self, f_out=None, outs=(), out_rows=None, dot=None, err=None, scale=None, f_lin=0.0):
         self.f_out = f_out
+        # nonzero: the RHS value becomes x + scale*f_lin*f (the affine stage derivative, ABI 5)
+        self.f_lin = float(f_lin)
         # a device fp32 0-d tensor multiplying every cf and c_j (not cb): the adaptive step size
         self.scale = scale
         self.outs = list(outs)
@@ -631,6 +633,7 @@ class Stage(object):
         if self.scale is not None:
             _require_gpu(self.scale, "coefficient scale", torch.float32)
             st.coef_scale = self.scale.data_ptr()
+        st.f_lin = self.f_lin
         return st
 
 
@@ -1208,6 +1211,48 @@ def sum_f64(v, out=None, accumulate=False):
     _lib.call("gnpde_sum_f64", v.numel(), _ptr(v), _ptr(out), int(bool(accumulate)), _ptr(ws), nbytes,
               _stream(v.device))
     return out
+
+
+def initial_step(y0, f0, f1, atol, rtol, order, h, hf=None):
+    """torchdiffeq's _select_initial_step on the device (gnpde_initial_step_*):
+    phase 0 (f1 None) writes h[0] = h0, h[1] = d1 and hf = float(h0); phase 1
+    (f1 = f(y0 + h0 f0)) writes h[2] = the first step.  h: fp64 [3], hf: fp32 0-d."""
+    dt = y0.dtype
+    if dt not in STATE_DTYPES:
+        raise TypeError("initial_step: state dtype %s" % dt)
+    for t in (y0, f0) + ((f1,) if f1 is not None else ()):
+        _require_gpu(t, "initial_step state", dt)
+        if not t.is_contiguous() or t.numel() != y0.numel():
+            raise ValueError("initial_step: y0, f0, f1 must be contiguous and shaped alike")
+    _require_gpu(h, "h", torch.float64)
+    if h.numel() < 3 or (f1 is None and hf is None):
+        raise ValueError("initial_step: h needs 3 doubles; phase 0 needs hf")
+    if hf is not None:
+        _require_gpu(hf, "hf", torch.float32)
+    nbytes = _lib.fn("gnpde_initial_step_workspace_bytes")()
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=y0.device)
+    name = "gnpde_initial_step_bf16" if dt == torch.bfloat16 else "gnpde_initial_step_f32"
+    _lib.call(name, y0.numel(), _ptr(y0), _ptr(f0), _ptr(f1), float(atol), float(rtol), float(order), _ptr(h),
+              _ptr(hf), _ptr(ws), nbytes, _stream(y0.device))
+
+
+def adaptive_control(err_rows, n, order, safety, ifactor, dfactor, dt, scale, rec, ws=None):
+    """The step's error-row sum and torchdiffeq's step-size controller on the device
+    (gnpde_adaptive_control): rec = {error ratio, dt, next dt, squared error sum};
+    dt (fp64 0-d) and scale (fp32 0-d) advance to the next step's size.  ``ws``: a
+    reusable workspace (gnpde_dot_workspace_bytes() bytes)."""
+    _require_gpu(err_rows, "err_rows", torch.float64)
+    _require_gpu(dt, "dt", torch.float64)
+    _require_gpu(scale, "scale", torch.float32)
+    _require_gpu(rec, "rec", torch.float64)
+    if rec.numel() < 4:
+        raise ValueError("adaptive_control: rec needs 4 doubles")
+    nbytes = _lib.fn("gnpde_dot_workspace_bytes")()
+    if ws is None:
+        ws = torch.empty(nbytes, dtype=torch.uint8, device=err_rows.device)
+    _lib.call("gnpde_adaptive_control", err_rows.numel(), _ptr(err_rows), float(n), float(order), float(safety),
+              float(ifactor), float(dfactor), _ptr(dt), _ptr(scale), _ptr(rec), _ptr(ws), ws.numel(),
+              _stream(err_rows.device))
 
 
 def wcolsum(x, B, N, w):

@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define GNPDE_ABI_VERSION 4
+#define GNPDE_ABI_VERSION 5
 
 #define GNPDE_OK 0
 #define GNPDE_EINVAL (-1)
@@ -196,6 +196,12 @@ size_t gnpde_plan_workspace_bytes(int64_t R);
  * outputs and of err (not cb): the step size of an adaptive solve, so the
  * launches of a step do not change with it (hipGraph-replayable, one graph per
  * step whatever dt).
+ * f_lin (0 = off): the RHS value becomes f = x + coef_scale*f_lin*f before any
+ * store or combination (x = the RHS input row): for an affine RHS f(y) = L y + s
+ * evaluated on the input k WITHOUT the source term (flags: no GNPDE_ADD_SOURCE),
+ * f(y0 + h k) = k + h L k with k = f(y0) — an adaptive step's first stage derivative
+ * without materialising its stage input y0 + h k (gnpde.integrator, ABI 5).
+ * A k operand (or base) equal to the RHS input x reuses the row already read.
  * At most 2 k operands with dot_rows; err_rows and 3..6 operands take the wide
  * epilogue (operands loaded after the aggregation), fused into the plain-weight
  * K1 (gnpde_spmm_rhs_f32 / _bf16); the attention kernels return
@@ -228,6 +234,7 @@ typedef struct {
   double atol;
   double rtol;
   const float* coef_scale;
+  float f_lin;
 } gnpde_stage_epilogue_t;
 
 /* The stage epilogue as a pass of its own, over rows [0, R) of C columns
@@ -515,6 +522,40 @@ int gnpde_sum_f64(int64_t n, const double* v, double* out, int accumulate, void*
                   void* stream);
 int gnpde_dot_f64(int64_t n, const float* a, const float* b, double* out, void* workspace, size_t workspace_bytes,
                   void* stream);
+
+/* The first step of an adaptive solve on the device: torchdiffeq's
+ * _select_initial_step (RKAdaptiveStepsizeODESolver._before_integrate, order =
+ * the tableau's order: 5 for dopri5) over n state elements, replacing the
+ * Python-side torch elementwise chain and its host syncs (gnpde.integrator):
+ *   scale = atol + |y0| rtol (fp32, as torch on an fp32 state)
+ *   phase 0 (f1 == NULL): d0 = rms(y0/scale), d1 = rms(f0/scale),
+ *     h[0] = h0 = (d0 < 1e-5 || d1 < 1e-5) ? 1e-6 : 0.01 d0/d1, h[1] = d1,
+ *     *hf = (float)h0 (the coef_scale of the probe y0 + h0 f0);
+ *   phase 1 (f1 = f(t0 + h0, y0 + h0 f0)): d2 = rms((f1 - f0)/scale)/h0,
+ *     h1 = (d1 <= 1e-15 && d2 <= 1e-15) ? max(1e-6, 1e-3 h0) : (0.01/max(d1,d2))^(1/order),
+ *     h[2] = min(100 h0, h1)  (reads h[0], h[1] of phase 0); *hf = (float)h[2] when hf
+ *     is given (the first step's coef_scale, so the host need not write it).
+ * Squares summed in fp64 in a fixed order (two launches per phase); h [3]
+ * fp64 and hf are device memory.  Workspace gnpde_initial_step_workspace_bytes(). */
+/* torchdiffeq's step-size controller after one adaptive step, on the device
+ * (rk_common.py _optimal_step_size with the loop's accept test error_ratio <= 1),
+ * fused with the reduction of the step's error rows (the stage epilogue's err_rows):
+ *   e2    = sum_r err_rows[r]   (fixed order, as gnpde_sum_f64)
+ *   ratio = sqrt(e2 / n)        (the RMS error ratio over n state elements)
+ *   next  = ratio == 0 ? dt ifactor
+ *         : dt min(ifactor, max(safety ratio^(-1/order), ratio < 1 ? 1 : dfactor))
+ * rec[0..3] = {ratio, dt, next, e2}; *dt = next; *scale = (float)next (the
+ * coef_scale of the next step's launches).  Device pointers; two launches;
+ * workspace gnpde_dot_workspace_bytes().                                    */
+int gnpde_adaptive_control(int64_t nrows, const double* err_rows, double n, double order, double safety,
+                           double ifactor, double dfactor, double* dt, float* scale, double* rec, void* workspace,
+                           size_t workspace_bytes, void* stream);
+size_t gnpde_initial_step_workspace_bytes(void);
+int gnpde_initial_step_f32(int64_t n, const float* y0, const float* f0, const float* f1, double atol, double rtol,
+                           double order, double* h, float* hf, void* workspace, size_t workspace_bytes, void* stream);
+int gnpde_initial_step_bf16(int64_t n, const uint16_t* y0, const uint16_t* f0, const uint16_t* f1, double atol,
+                            double rtol, double order, double* h, float* hf, void* workspace, size_t workspace_bytes,
+                            void* stream);
 
 /* ---------------------------------------------------------------- backward
  * Gradients of the RHS f = a (A(w) x - x) [+ b x0] and of the attention that

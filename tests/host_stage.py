@@ -18,9 +18,11 @@ def apply_stage(stage, f, x):
     if f is None:
         like = stage.outs[0][0] if stage.outs else stage.err[2]
         f = torch.zeros_like(like)
+    sc = float(stage.scale) if stage.scale is not None else 1.0
+    if getattr(stage, 'f_lin', 0.0):
+        f = x + (sc * stage.f_lin) * f
     if stage.f_out is not None:
         stage.f_out.copy_(f)
-    sc = float(stage.scale) if stage.scale is not None else 1.0
     vals = []
     for out, base, cb, cf, terms in stage.outs:
         v = _combo(base, cb, cf, terms, f, sc)
@@ -50,7 +52,9 @@ class HostLinearRHS(object):
         self.nfe += 1
         return y @ self.A.T
 
-    def rhs_stage(self, t, x, stage):
+    affine = True  # f(y) = A y: its own linear part
+
+    def rhs_stage(self, t, x, stage, linear=False):
         self.nfe += 1
         self.n_stage += 1
         apply_stage(stage, x @ self.A.T, x)

@@ -46,7 +46,7 @@ def test_library_built_from_these_sources():
 
 
 def test_abi_version():
-    assert _lib.load().gnpde_abi_version() == _lib.ABI_VERSION == 4
+    assert _lib.load().gnpde_abi_version() == _lib.ABI_VERSION == 5
 
 
 def test_library_is_gfx950_code_object():
@@ -135,8 +135,10 @@ def test_stage_struct_layout_matches_header():
     assert _lib.StageEpilogue.out_rows.offset == 16 + 2 * so + 8 + 48
     assert _lib.StageEpilogue.dot_coef.offset == _lib.StageEpilogue.out_rows.offset + 24
     assert _lib.StageEpilogue.err.offset == _lib.StageEpilogue.dot_coef.offset + 24
-    assert ctypes.sizeof(_lib.StageEpilogue) == _lib.StageEpilogue.err.offset + so + 8 + 8 + 8 + 8 + 8
+    # ... err_y0, err_y1 (padded), atol, rtol, coef_scale, f_lin (ABI 5; padded to 8)
+    assert ctypes.sizeof(_lib.StageEpilogue) == _lib.StageEpilogue.err.offset + so + 8 + 8 + 8 + 8 + 8 + 8
     assert _lib.StageEpilogue.coef_scale.offset == _lib.StageEpilogue.rtol.offset + 8
+    assert _lib.StageEpilogue.f_lin.offset == _lib.StageEpilogue.coef_scale.offset + 8
 
 
 def test_workspace_size_queries():

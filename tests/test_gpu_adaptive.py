@@ -295,3 +295,96 @@ def test_c2_dopri5_default_tolerances_vs_oracle_steps():
     print("C2 dopri5 steps: gnpde %d, oracle %d" % (n_got, n_want))
     assert n_got == n_want
     assert rel(z, want[-1]) <= RTOL
+
+
+def _init_step_ref(y0, f0, f1, atol, rtol, order):
+    """torchdiffeq's _select_initial_step (integrator._RKAdaptive) in fp64 from fp32
+    elementwise quotients (the device kernel's arithmetic): (h0, d1, first step)."""
+    y, f = y0.astype(np.float32), f0.astype(np.float32)
+    sc = np.float32(atol) + np.abs(y) * np.float32(rtol)
+    d0 = np.sqrt(np.mean(((y / sc).astype(np.float64)) ** 2))
+    d1 = np.sqrt(np.mean(((f / sc).astype(np.float64)) ** 2))
+    h0 = 1e-6 if (d0 < 1e-5 or d1 < 1e-5) else 0.01 * d0 / d1
+    if f1 is None:
+        return h0, d1, None
+    d2 = np.sqrt(np.mean((((f1.astype(np.float32) - f) / sc).astype(np.float64)) ** 2)) / h0
+    h1 = max(1e-6, h0 * 1e-3) if (d1 <= 1e-15 and d2 <= 1e-15) else (0.01 / max(d1, d2)) ** (1.0 / order)
+    return h0, d1, min(100 * h0, h1)
+
+
+@pytest.mark.parametrize("n,scale_f", [(4096 * 33, 1.0), (1001, 3.0), (64, 1e-9)])
+def test_initial_step_kernel_vs_formula(n, scale_f):
+    """gnpde_initial_step_f32 (both phases) against the formula in fp64 numpy: the
+    same h0, d1 and first step within 1e-7; the tiny-f case takes the 1e-6 branch."""
+    rng = np.random.default_rng(n)
+    y0 = rng.standard_normal(n).astype(np.float32)
+    f0 = (rng.standard_normal(n) * scale_f).astype(np.float32)
+    f1 = (f0 + rng.standard_normal(n).astype(np.float32) * 0.01).astype(np.float32)
+    atol, rtol, order = 1.1e-3, 1.1e-5, 5.0
+    h = torch.empty(3, dtype=torch.float64, device=DEV)
+    hf = torch.empty((), dtype=torch.float32, device=DEV)
+    ops.initial_step(T(y0), T(f0), None, atol, rtol, order, h, hf)
+    ops.initial_step(T(y0), T(f0), T(f1), atol, rtol, order, h)
+    h0, d1, first = _init_step_ref(y0, f0, f1, atol, rtol, order)
+    got = h.cpu().numpy()
+    # 1e-7 (two fp32 ulps): the device's fp32 quotients sit up to an ulp from numpy's
+    # correctly rounded ones (measured 1.4e-11 at n = 135k, 2.3e-9 at n = 64) and the fp64
+    # sums run in another order; the heuristic first step needs no more
+    assert abs(got[0] - h0) <= 1e-7 * abs(h0)
+    assert abs(got[1] - d1) <= 1e-7 * max(abs(d1), 1e-300)
+    assert abs(got[2] - first) <= 1e-7 * abs(first)
+    assert float(hf) == np.float32(got[0])
+
+
+@pytest.mark.parametrize("ratio", [0.0, 0.3, 0.999, 1.0, 1.7, 40.0])
+def test_adaptive_control_kernel_vs_host_controller(ratio):
+    """gnpde_adaptive_control against the host controller it replaces
+    (_RKAdaptiveFused.integrate, torchdiffeq _optimal_step_size): same ratio, same
+    next step up to pow's last bit, scale = float(next)."""
+    n = 1000.0
+    rows = torch.zeros(77, dtype=torch.float64, device=DEV)
+    rows[5] = ratio * ratio * n  # the error sum over rows (one nonzero: exact in any order)
+    dt = torch.tensor(0.37, dtype=torch.float64, device=DEV)
+    scale = torch.zeros((), dtype=torch.float32, device=DEV)
+    rec = torch.zeros(4, dtype=torch.float64, device=DEV)
+    ops.adaptive_control(rows, n, 5.0, 0.9, 10.0, 0.2, dt, scale, rec)
+    r, h, nxt, e2 = rec.tolist()
+    assert e2 == ratio * ratio * n
+    want_ratio = np.sqrt(ratio * ratio * n / n)
+    if want_ratio == 0:
+        want = 0.37 * 10.0
+    else:
+        df = 1.0 if want_ratio < 1 else 0.2
+        want = 0.37 * min(10.0, max(0.9 / want_ratio ** (1.0 / 5.0), df))
+    assert abs(r - want_ratio) <= 1e-15 * max(want_ratio, 1)
+    assert h == 0.37
+    assert abs(nxt - want) <= 4e-16 * want
+    assert float(dt) == nxt and float(scale) == np.float32(nxt)
+
+
+def test_fused_dopri5_in_node_layout_vs_user_numbering_and_oracle(monkeypatch):
+    """The fused dopri5 solve in the graph's in-degree numbering (forced on a small
+    graph): the same accepted / rejected sequence as the user numbering and as the
+    oracle, values within 1e-6 of the user numbering (the error norm sums rows in
+    another order) and 1e-5 of the oracle; outputs in the caller's numbering,
+    including the dense output's out_rows store."""
+    N, E, C = 3000, 24000, 32
+    eo, wo, rng = _graph(N, E, 37)
+    x = rng.standard_normal((1, N, C)).astype(np.float32)
+    ts = [0.0, 0.05, 0.5, 1.0]
+    tt = torch.tensor(ts, dtype=torch.float64, device=DEV)
+    with torch.no_grad():
+        plain = gi.odeint(_laplacian(C, eo, wo, alpha=0.0), T(x), tt, rtol=1e-3, atol=1e-4, method='dopri5')
+        n_plain = gi.odeint.last_n_steps
+        monkeypatch.setattr(ops, "LAYOUT_MIN_ROWS", 1)
+        monkeypatch.setattr(ops, "LAYOUT_MIN_BYTES", 1)
+        func = _laplacian(C, eo, wo, alpha=0.0)
+        assert func.node_layout(T(x)) is not None
+        got = gi.odeint(func, T(x), tt, rtol=1e-3, atol=1e-4, method='dopri5')
+        n_got = gi.odeint.last_n_steps
+        assert func._layout is None  # restored after the solve
+    f = lambda t, y: O.laplacian_rhs(eo, y, None, 0.0, 0.0, edge_weight=wo)  # noqa: E731
+    want, n_want = O.odeint_adaptive(f, x, ts, 'dopri5', 1e-3, 1e-4)
+    assert n_got == n_plain == n_want
+    assert rel(got, plain) <= 1e-6
+    assert rel(got, want) <= RTOL

@@ -76,6 +76,10 @@ def main():
             n = meta["rhs"]
             ent["per_rhs_bytes"] = sum(k["bytes"] * k["count"] for k in ks) / n
             ent["per_rhs_kernels"] = ["%s x%g" % (k["kernel"], k["count"] / n) for k in ks]
+        if "steps" in meta:
+            n = meta["steps"]
+            ent["per_step_bytes"] = sum(k["bytes"] * k["count"] for k in ks) / n
+            ent["per_step_kernels"] = ["%s x%g" % (k["kernel"], k["count"] / n) for k in ks]
         out["workloads"][meta["workload"]] = ent
         print("%-24s" % meta["workload"], ", ".join("%s x%d %.1f MB" % (k["kernel"][:50], k["count"], k["bytes"] / 1e6)
                                                    for k in ks[:6]))

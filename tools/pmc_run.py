@@ -5,7 +5,7 @@ can be attributed per kernel and per RHS evaluation (tools/pmc_reduce.py):
   tools/pmc_run.py WORKLOAD [--reps N]
 
 WORKLOAD: lap (G-arxiv rk4, fused K1 stages + plain K1 launches), grmat
-(configs[4] graph rk4), attn:<mode>_norm<k> (the transformer RHS of
+(configs[4] graph rk4), dopri5 (replays of one captured G-arxiv dopri5 step), attn:<mode>_norm<k> (the transformer RHS of
 bench.bench_attention, eager), blend_fp32 / blend_bf16 (C = 162 rk4 steps).
 Setup (graph, plans, cached weights) and two warm-up evaluations run first,
 then a marker (one gnpde_dot_f64, used by no workload), then the N measured
@@ -84,6 +84,23 @@ def main():
             meta["node_order"] = "degree" if lay is not None else "none"
             meta.update({"nodes": 169343, "edges": 1200000, "dim": 128, "heads": 2, "attention_dim": 32,
                          "rhs": reps})
+        elif wl == "dopri5":
+            # the bench's dopri5 line (G-arxiv, ogbn-arxiv best_params): warm solves, then `reps`
+            # replays of one captured step (6 RHS launches + error reduction + device controller)
+            import gnpde.integrator as integ
+            ei, w = synthetic.rw_graph(169343, 1200000, seed=0, device=dev)
+            x = synthetic.features(1, 169343, 128, seed=1, device=dev)
+            func = gnpde.LaplacianODEFunc(128, 128, dict(bench.LAP_OPT, hidden_dim=128), dev).to(dev)
+            func.edge_index, func.edge_weight = ei, w
+            T, ts = bench.ARXIV_DOPRI5
+            t = torch.tensor([0.0, T], dtype=torch.float32, device=dev)
+            for _ in range(3):
+                gnpde.odeint(func, x, t, method='dopri5', rtol=1e-9 * ts, atol=1e-7 * ts)
+            g = integ.adaptive_step_graph(func)
+            marker()
+            for _ in range(reps):
+                g.replay()
+            meta.update({"nodes": 169343, "edges": 1200000, "dim": 128, "steps": reps, "rhs_per_step": 6})
         elif wl.startswith("blend_"):
             dt = torch.bfloat16 if wl == "blend_bf16" else torch.float32
             ei, w = synthetic.rw_graph(169343, 1200000, seed=0, device=dev)
