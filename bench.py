@@ -332,6 +332,8 @@ def bench_single(args, world, rank, dev):
     if not args.no_train and rank == 0 and world == 1:
         result["block_forward"] = bench_block(ei, x, h, dev)
         result["train_rk4"] = bench_train(ei, w, x, h, dev)
+        fwd = result.get("dopri5", {}).get("garxiv_laplacian", {}).get("ms_per_solve")
+        result["train_adjoint"] = bench_train_adjoint(ei, w, x, dev, fwd)
         progress("block / train done")
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -972,6 +974,53 @@ def bench_train(ei, w, x, h, dev, steps=4, reps=5):
                       "(eager drop-in path)" % steps,
             "ms_per_train_step": round(ms, 4), "ms_per_rk4_step_fwd_bwd": round(ms / steps, 4),
             "forward_rhs": 4 * steps}
+
+
+def bench_train_adjoint(ei, w, x, dev, fwd_ms=None, reps=3):
+    """SURVEY §8(f) next-1 as the reference trains ogbn-arxiv (src/best_params.py:7, src/base_classes.py:45-49,
+    src/block_constant.py:34-44): odeint_adjoint with method dopri5 over [0, 3.676] at tol_scale 11353.6 and
+    adjoint_method rk4 with adjoint_step_size 1 — forward the fused no-grad dopri5 solve, backward the fused
+    continuous adjoint (gnpde.integrator._LaplacianAdjointFn: y and a integrated back over s = -t, eight K1
+    launches per rk4 step, the alpha gradient's row terms in the CSC epilogues).  A linear loss, backward to x
+    and alpha_train; HIP events around the whole training step."""
+    import gnpde
+    import gnpde.integrator as integ
+    C = x.shape[-1]
+    func = gnpde.LaplacianODEFunc(C, C, dict(LAP_OPT, hidden_dim=C), dev).to(dev)
+    func.edge_index, func.edge_weight = ei, w
+    T, ts = ARXIV_DOPRI5
+    t = torch.tensor([0.0, T], dtype=torch.float32, device=dev)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(9)
+    gout = torch.randn(x.shape, generator=gen, device=dev)
+
+    def one():
+        xi = x.detach().requires_grad_(True)
+        func.alpha_train.grad = None
+        y = integ.odeint_adjoint(func, xi, t, rtol=1e-9 * ts, atol=1e-7 * ts, method='dopri5',
+                                 adjoint_method='rk4', adjoint_options={'step_size': 1.0},
+                                 adjoint_rtol=1e-9, adjoint_atol=1e-7)[1]
+        (y * gout).sum().backward()
+        return xi.grad
+
+    for _ in range(2):
+        one()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    nfe0 = func.nfe
+    s.record()
+    for _ in range(reps):
+        gx = one()
+    e.record()
+    torch.cuda.synchronize()
+    ms = s.elapsed_time(e) / reps
+    assert torch.isfinite(gx).all() and func.alpha_train.grad is not None
+    return {"config": "G-arxiv laplacian (C=128), ogbn-arxiv best_params training: odeint_adjoint, dopri5 forward "
+                      "over [0, %.3f] at tol_scale %.1f, adjoint_method rk4, adjoint_step_size 1" % (T, ts),
+            "fused": integ._fused_adjoint_ok(func, x, 'rk4', tuple(p for p in func.parameters() if p.requires_grad)),
+            "ms_per_train_step": round(ms, 4), "forward_ms_per_solve": fwd_ms,
+            "train_over_forward": round(ms / fwd_ms, 3) if fwd_ms else None,
+            "rhs_evals_per_train_step": (func.nfe - nfe0) // reps}
 
 
 def cpu_baseline(ei, w, x, N, E, C, budget_s):

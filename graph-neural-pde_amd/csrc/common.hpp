@@ -284,6 +284,123 @@ __device__ __forceinline__ float unpack(const Packed<VEC, bf16>& r, int t) {
   return bf16_to_f32((t & 1) ? (r.d[t >> 1] >> 16) : (r.d[t >> 1] & 0xffffu));
 }
 
+// ------------------------------------------------------------------ streamed stage operands
+// The operand rows of the streamed stage epilogues (STG 4, the non-prefetching
+// STG 1-3, gnpde_stage_apply_*) are ISSUED TOGETHER, before any of them is used:
+// one memory round trip per epilogue.  Written as "if (j < nk) { load k[j];
+// fma }" the compiler waits for each load before the next (one round trip per
+// operand: the G-arxiv dopri5 launches with 3-6 operands ran at 172 us against
+// 92 us for the rk4 stage, round 4).  The loads are raw buffer loads whose absent
+// operands take the out-of-range offset kBufNone (no memory access, value 0),
+// so nothing in the load sequence branches.  Buffer byte offsets are 32-bit: a
+// wavefront any of whose rows lies past 4 GiB of the state takes the per-operand
+// form.
+// GNPDE_WIDE_BATCH=0 builds the per-operand form (A/B only).
+#ifndef GNPDE_WIDE_BATCH
+#define GNPDE_WIDE_BATCH 1
+#endif
+#ifndef GNPDE_WIDE_NOFB
+#define GNPDE_WIDE_NOFB 0
+#endif
+#ifndef GNPDE_STG4_PRE
+#define GNPDE_STG4_PRE 0  // wide-epilogue operand rows read before the gathers (A/B)
+#endif
+
+template <int VEC, class T>
+__device__ __forceinline__ void buf_load_packed(const void* p, uint32_t boff, Packed<VEC, T>& r) {
+  const __amdgpu_buffer_rsrc_t rs = buf_rsrc(p);
+  constexpr int B = VEC * (int)sizeof(T);
+  if constexpr (B == 32) {
+    // a dropped load (kBufNone) stays dropped: kBufNone + 16 would wrap to offset 0
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, boff, 0, 0);
+    const u32x4 u = __builtin_amdgcn_raw_buffer_load_b128(rs, boff >= kBufRecords ? kBufNone : boff + 16u, 0, 0);
+    r.d[0] = v.x;
+    r.d[1] = v.y;
+    r.d[2] = v.z;
+    r.d[3] = v.w;
+    r.d[4] = u.x;
+    r.d[5] = u.y;
+    r.d[6] = u.z;
+    r.d[7] = u.w;
+  } else if constexpr (B == 16) {
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, boff, 0, 0);
+    r.d[0] = v.x;
+    r.d[1] = v.y;
+    r.d[2] = v.z;
+    r.d[3] = v.w;
+  } else if constexpr (B == 8) {
+    const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(rs, boff, 0, 0);
+    r.d[0] = v.x;
+    r.d[1] = v.y;
+  } else if constexpr (B == 4) {
+    r.d[0] = __builtin_amdgcn_raw_buffer_load_b32(rs, boff, 0, 0);
+  } else {
+    static_assert(B == 2, "row slices are 2-16 bytes");
+    r.d[0] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(rs, boff, 0, 0);
+  }
+}
+
+// An operand row slice, or zeros for an absent operand (p == NULL, wave-uniform):
+// GNPDE_WIDE_SKIP=1 skips the absent operand's load under a scalar branch (an
+// out-of-range buffer load still costs an address-unit pass over the wavefront);
+// the waits stay at the first use after the whole batch.
+#ifndef GNPDE_WIDE_SKIP
+#define GNPDE_WIDE_SKIP 1
+#endif
+template <int VEC, class T>
+__device__ __forceinline__ void opt_load(const float* p, uint32_t bo, Packed<VEC, T>& r) {
+  if (GNPDE_WIDE_SKIP) {
+    if (p) {
+      buf_load_packed<VEC, T>(p, bo, r);
+    } else {
+#pragma unroll
+      for (int t = 0; t < Packed<VEC, T>::W; ++t) r.d[t] = 0u;
+    }
+  } else {
+    buf_load_packed<VEC, T>(p, p ? bo : kBufNone, r);
+  }
+}
+
+// Whether every row of the wavefront addresses the state with 32-bit buffer offsets
+template <int VEC, class T>
+__device__ __forceinline__ bool rows_fit_buffer(int64_t off) {
+  return __all((off + VEC) * (int64_t)sizeof(T) < (int64_t)kBufRecords);
+}
+
+// The operand slots of the wide epilogue, in consumption order: the NOUT output
+// bases, the error base, k[0..NKMAX-1], the error tolerance's y0 (ERR).  p[q] is
+// NULL for an absent operand or one equal to the RHS input xid (its values are
+// already held); cb the bases' coefficients (0 without a base).
+template <int NOUT, int NKMAX, bool ERR>
+struct WideSlots {
+  static constexpr int N = NOUT + NKMAX + (ERR ? 2 : 0);
+  const float* p[N];
+  float cb[NOUT + 1];
+  // the slot id of position q (slot ids: bases 0..NOUT-1, k rows NOUT + j, error base
+  // NOUT + NKMAX, y0 N - 1 — as the consumers below number them)
+  __device__ static constexpr int slot(int q) {
+    return q < NOUT ? q : (ERR && q == NOUT ? NOUT + NKMAX : (q < NOUT + (ERR ? 1 : 0) + NKMAX ? q - (ERR ? 1 : 0) : N - 1));
+  }
+};
+
+template <int NOUT, int NKMAX, bool ERR>
+__device__ __forceinline__ void wide_slots(const gnpde_stage_epilogue_t& st, const float* xid,
+                                           WideSlots<NOUT, NKMAX, ERR>& w) {
+  const bool has_err = ERR && st.err_rows != nullptr;
+#pragma unroll
+  for (int i = 0; i <= NOUT; ++i) {
+    if (i == NOUT && !ERR) break;
+    const bool on = i < NOUT ? i < st.n_out : has_err;
+    const gnpde_stage_out_t& so = i < NOUT ? st.o[i] : st.err;
+    const float* b = on ? so.base : nullptr;
+    w.cb[i] = b ? so.cb : 0.f;
+    w.p[i] = (b && b != xid) ? b : nullptr;  // position i: output bases, then the error base
+  }
+#pragma unroll
+  for (int j = 0; j < NKMAX; ++j) w.p[NOUT + (ERR ? 1 : 0) + j] = (j < st.nk && st.k[j] != xid) ? st.k[j] : nullptr;
+  if constexpr (ERR) w.p[WideSlots<NOUT, NKMAX, ERR>::N - 1] = has_err ? st.err_y0 : nullptr;
+}
+
 // fp32 values -> a row slice in storage form (bf16: round to nearest even); for an
 // operand that equals the RHS input, whose values are already fp32-exact in T
 template <int VEC, class T>
@@ -371,6 +488,7 @@ struct EpiPre {
   Packed<VEC, T> kv[stage_kpre<STG>() > 0 ? stage_kpre<STG>() : 1];
   Packed<VEC, T> dw;  // the stage's dot operand (dot_rows; STG 2 with GNPDE_STG2_PRE, STG 3 with GNPDE_DOT_PRE)
   double dprev;       // the row's running dot (dot_accumulate), read before the gathers
+  Packed<VEC, T> wk[(STG == 4 && GNPDE_STG4_PRE > 0) ? GNPDE_STG4_PRE : 1];  // the wide epilogue's first operands
 };
 
 // The Epi / stage pointers are declared float*; for bf16 storage they address
@@ -391,6 +509,25 @@ __device__ __forceinline__ void epi_prefetch(const Epi& e, int64_t row, int cc, 
   if (e.flags & GNPDE_ADD_SOURCE) load_packed<VEC>(as_t<T>(e.x0) + row * e.ldx0 + cc, p.x0r);
   if constexpr (stage_dot<STG>() && GNPDE_DOT_PRE)  // the running dot: its read is off the epilogue's chain
     p.dprev = (e.st.dot_rows && e.st.dot_accumulate) ? e.st.dot_rows[row] : 0.0;
+  if constexpr (STG == 4 && GNPDE_STG4_PRE > 0) {
+    // the first GNPDE_STG4_PRE present operand rows of the wide epilogue (WideSlots order)
+    const int64_t off = row * e.ldf + cc;
+    if (GNPDE_WIDE_BATCH && rows_fit_buffer<VEC, T>(off)) {
+      WideSlots<2, GNPDE_STAGE_MAX_K, true> w;
+      wide_slots<2, GNPDE_STAGE_MAX_K, true>(e.st, (need_x && e.ldx == e.ldf) ? e.x : nullptr, w);
+      const uint32_t bo = (uint32_t)(off * (int64_t)sizeof(T));
+      int cnt = 0;
+#pragma unroll
+      for (int q = 0; q < WideSlots<2, GNPDE_STAGE_MAX_K, true>::N; ++q) {
+        if (w.p[q]) {
+#pragma unroll
+          for (int c = 0; c < GNPDE_STG4_PRE; ++c)
+            if (cnt == c) buf_load_packed<VEC, T>(w.p[q], bo, p.wk[c]);
+          ++cnt;
+        }
+      }
+    }
+  }
   if constexpr (STG == 0 || STG == 4) return;
   const int64_t off = row * e.ldf + cc;
 #pragma unroll
@@ -449,129 +586,61 @@ __device__ __forceinline__ float stage_scale(const gnpde_stage_epilogue_t& st) {
   return st.coef_scale ? *st.coef_scale : 1.f;
 }
 
-// ------------------------------------------------------------------ streamed stage operands
-// The operand rows of the streamed stage epilogues (STG 4, the non-prefetching
-// STG 1-3, gnpde_stage_apply_*) are ISSUED TOGETHER, before any of them is used:
-// one memory round trip per epilogue.  Written as "if (j < nk) { load k[j];
-// fma }" the compiler waits for each load before the next (one round trip per
-// operand: the G-arxiv dopri5 launches with 3-6 operands ran at 172 us against
-// 92 us for the rk4 stage, round 4).  The loads are raw buffer loads whose absent
-// operands take the out-of-range offset kBufNone (no memory access, value 0),
-// so nothing in the load sequence branches.  Buffer byte offsets are 32-bit: a
-// wavefront any of whose rows lies past 4 GiB of the state takes the per-operand
-// form.
-// GNPDE_WIDE_BATCH=0 builds the per-operand form (A/B only).
-#ifndef GNPDE_WIDE_BATCH
-#define GNPDE_WIDE_BATCH 1
-#endif
-#ifndef GNPDE_WIDE_NOFB
-#define GNPDE_WIDE_NOFB 0
-#endif
-#ifndef GNPDE_WIDE_DEPTH
-#define GNPDE_WIDE_DEPTH 0
-#endif
-
-template <int VEC, class T>
-__device__ __forceinline__ void buf_load_packed(const void* p, uint32_t boff, Packed<VEC, T>& r) {
-  const __amdgpu_buffer_rsrc_t rs = buf_rsrc(p);
-  constexpr int B = VEC * (int)sizeof(T);
-  if constexpr (B == 32) {
-    // a dropped load (kBufNone) stays dropped: kBufNone + 16 would wrap to offset 0
-    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, boff, 0, 0);
-    const u32x4 u = __builtin_amdgcn_raw_buffer_load_b128(rs, boff >= kBufRecords ? kBufNone : boff + 16u, 0, 0);
-    r.d[0] = v.x;
-    r.d[1] = v.y;
-    r.d[2] = v.z;
-    r.d[3] = v.w;
-    r.d[4] = u.x;
-    r.d[5] = u.y;
-    r.d[6] = u.z;
-    r.d[7] = u.w;
-  } else if constexpr (B == 16) {
-    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, boff, 0, 0);
-    r.d[0] = v.x;
-    r.d[1] = v.y;
-    r.d[2] = v.z;
-    r.d[3] = v.w;
-  } else if constexpr (B == 8) {
-    const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(rs, boff, 0, 0);
-    r.d[0] = v.x;
-    r.d[1] = v.y;
-  } else if constexpr (B == 4) {
-    r.d[0] = __builtin_amdgcn_raw_buffer_load_b32(rs, boff, 0, 0);
-  } else {
-    static_assert(B == 2, "row slices are 2-16 bytes");
-    r.d[0] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(rs, boff, 0, 0);
-  }
-}
-
-// Whether every row of the wavefront addresses the state with 32-bit buffer offsets
-template <int VEC, class T>
-__device__ __forceinline__ bool rows_fit_buffer(int64_t off) {
-  return __all((off + VEC) * (int64_t)sizeof(T) < (int64_t)kBufRecords);
-}
-
 // The wide stage epilogue of one row slice (STG 4; also gnpde_stage_apply_*):
 // every output and the error combination start from cb*base (x when the base is
 // the RHS input xid, with values xv), take sc*c[j]*k[j] for j ascending, then
 // sc*cf*f — per output the same order as stage_combine, so the same bits.
 // Returns the error combination in ev (when err_rows), output values in r and,
 // when y0v is given and err_rows is set, the tolerance's y0 row slice.
-template <int VEC, class T, int NKMAX = GNPDE_STAGE_MAX_K, int NOUT = 2, bool ERR = true>
+template <int VEC, class T, int NKMAX = GNPDE_STAGE_MAX_K, int NOUT = 2, bool ERR = true, int PK = 0>
 __device__ __forceinline__ void wide_combine(const gnpde_stage_epilogue_t& st, int64_t off, const float (&o)[VEC],
                                              const float* xid, const float (&xv)[VEC], float (&r)[2][VEC],
-                                             float (&ev)[VEC], Packed<VEC, T>* y0v = nullptr) {
+                                             float (&ev)[VEC], Packed<VEC, T>* y0v = nullptr,
+                                             const Packed<VEC, T>* pre = nullptr) {
   const float sc = stage_scale(st);
   if (GNPDE_WIDE_BATCH && (GNPDE_WIDE_NOFB || rows_fit_buffer<VEC, T>(off))) {
     const bool has_err = ERR && st.err_rows != nullptr;
-    // operand table: NOUT output bases, the error base, NKMAX k rows, the tolerance's y0
-    constexpr int NE = ERR ? 2 : 0;
-    constexpr int N = NOUT + NKMAX + NE;
-    const float* p[N];
-    float cb[NOUT + 1];
-#pragma unroll
-    for (int i = 0; i <= NOUT; ++i) {
-      const bool on = i < NOUT ? i < st.n_out : has_err;
-      const gnpde_stage_out_t& so = i < NOUT ? st.o[i] : st.err;
-      const float* b = (on && (i < NOUT || ERR)) ? so.base : nullptr;
-      cb[i] = b ? so.cb : 0.f;
-      if (i < NOUT) p[i] = (b && b != xid) ? b : nullptr;
-      else if constexpr (ERR) p[NOUT + NKMAX] = (b && b != xid) ? b : nullptr;
-    }
-#pragma unroll
-    for (int j = 0; j < NKMAX; ++j) p[NOUT + j] = (j < st.nk && st.k[j] != xid) ? st.k[j] : nullptr;
-    if constexpr (ERR) p[N - 1] = has_err ? st.err_y0 : nullptr;
-    // slots: output bases [0, NOUT), the error base NOUT + NKMAX, k rows NOUT + j, y0 last;
-    // consumed in the order bases, error base, k0..k_{NKMAX-1} with at most D loads in
-    // flight (GNPDE_WIDE_DEPTH; 0 = all N issued at once)
-    constexpr int D = (GNPDE_WIDE_DEPTH > 0 && GNPDE_WIDE_DEPTH < N) ? GNPDE_WIDE_DEPTH : N;
-    int order[N];
-#pragma unroll
-    for (int i = 0; i < NOUT; ++i) order[i] = i;
-    if constexpr (ERR) order[NOUT] = NOUT + NKMAX;
-#pragma unroll
-    for (int j = 0; j < NKMAX; ++j) order[NOUT + (ERR ? 1 : 0) + j] = NOUT + j;
-    if constexpr (ERR) order[N - 1] = N - 1;
+    using WS = WideSlots<NOUT, NKMAX, ERR>;
+    constexpr int N = WS::N;
+    WS w;
+    wide_slots<NOUT, NKMAX, ERR>(st, xid, w);
     const uint32_t bo = (uint32_t)(off * (int64_t)sizeof(T));
-    Packed<VEC, T> ring[D];
-#pragma unroll
-    for (int q = 0; q < D; ++q) buf_load_packed<VEC, T>(p[order[q]], p[order[q]] ? bo : kBufNone, ring[q]);
+    // every operand row issued before any is used (one memory round trip); the first PK
+    // present ones were read before the gathers (epi_prefetch, GNPDE_STG4_PRE)
+    Packed<VEC, T> v[N];
+    int cnt = 0;
 #pragma unroll
     for (int q = 0; q < N; ++q) {
-      const int slot = order[q];
-      const Packed<VEC, T> v = ring[q % D];
-      if (q + D < N) buf_load_packed<VEC, T>(p[order[q + D]], p[order[q + D]] ? bo : kBufNone, ring[q % D]);
+      bool from_pre = false;
+      if constexpr (PK > 0) {
+        if (pre && w.p[q]) {
+#pragma unroll
+          for (int c = 0; c < PK; ++c)
+            if (cnt == c) {
+              v[q] = pre[c];
+              from_pre = true;
+            }
+        }
+      }
+      if (!from_pre) opt_load<VEC, T>(w.p[q], bo, v[q]);
+      cnt += w.p[q] != nullptr;
+    }
+    const float* cb = w.cb;
+#pragma unroll
+    for (int q = 0; q < N; ++q) {
+      const int slot = WS::slot(q);
+      const Packed<VEC, T> vq = v[q];
       if (slot < NOUT) {
         const bool isx = xid != nullptr && slot < st.n_out && st.o[slot].base == xid;
 #pragma unroll
-        for (int t = 0; t < VEC; ++t) r[slot][t] = cb[slot] * (isx ? xv[t] : unpack(v, t));
+        for (int t = 0; t < VEC; ++t) r[slot][t] = cb[slot] * (isx ? xv[t] : unpack(vq, t));
       } else if (slot < NOUT + NKMAX) {
         const int j = slot - NOUT;
         const bool on = j < st.nk;
         const bool kx = on && xid != nullptr && st.k[j] == xid;  // the RHS input row, already held
         float kv[VEC];
 #pragma unroll
-        for (int t = 0; t < VEC; ++t) kv[t] = kx ? xv[t] : unpack(v, t);
+        for (int t = 0; t < VEC; ++t) kv[t] = kx ? xv[t] : unpack(vq, t);
 #pragma unroll
         for (int i = 0; i < NOUT; ++i) {
           const float c = (on && i < st.n_out) ? st.o[i].c[j] * sc : 0.f;
@@ -587,10 +656,10 @@ __device__ __forceinline__ void wide_combine(const gnpde_stage_epilogue_t& st, i
         if constexpr (ERR) {
           const bool isx = xid != nullptr && has_err && st.err.base == xid;
 #pragma unroll
-          for (int t = 0; t < VEC; ++t) ev[t] = cb[NOUT] * (isx ? xv[t] : unpack(v, t));
+          for (int t = 0; t < VEC; ++t) ev[t] = cb[NOUT] * (isx ? xv[t] : unpack(vq, t));
         }
       } else if (y0v) {
-        *y0v = v;
+        *y0v = vq;
       }
     }
 #pragma unroll
@@ -723,7 +792,8 @@ __device__ __forceinline__ void epi_finish(const Epi& e, int64_t row, int cc, co
     Packed<VEC, T> y0v;
 #pragma unroll
     for (int t = 0; t < VEC; ++t) xv[t] = need_x ? unpack(p.xr, t) : 0.f;
-    wide_combine<VEC, T>(e.st, off, o, (need_x && e.ldx == e.ldf) ? e.x : nullptr, xv, r, ev, &y0v);
+    wide_combine<VEC, T, GNPDE_STAGE_MAX_K, 2, true, GNPDE_STG4_PRE>(
+        e.st, off, o, (need_x && e.ldx == e.ldf) ? e.x : nullptr, xv, r, ev, &y0v, GNPDE_STG4_PRE > 0 ? p.wk : nullptr);
 #pragma unroll
     for (int i = 0; i < 2; ++i)
       if (i < e.st.n_out) store_vec<VEC>(as_t<T>(e.st.o[i].out) + oo, r[i]);

@@ -1692,6 +1692,146 @@ class _OdeintAdjoint(torch.autograd.Function):
         return (ay, None, None) + tuple(ap)
 
 
+# Fused continuous adjoint of the Laplacian RHS (src/base_classes.py:45-49 with opt['adjoint'],
+# src/block_constant.py:34-44: odeint_adjoint with adjoint_method / adjoint_step_size; the
+# ogbn-arxiv and Photo best_params run adjoint_method 'rk4', src/best_params.py:6-7).
+FUSED_ADJOINT = os.environ.get('GNPDE_FUSED_ADJOINT', '1') != '0'
+
+
+class _AdjointRHS(object):
+    """The adjoint component of the augmented system in s = -t, a' = L^T a with
+    L = sigma(alpha)(A - I): K1 over the CSC with the RHS epilogue, whose dot term
+    adds coef_i <o_i, y_i> (o_i = L^T a_i, y_i the y component's input at the same
+    stage) per row in fp64 — the alpha gradient's integrand sigma'(alpha)<(A^T - I)a, y>
+    up to the factor (1 - sigma(alpha)) applied once at the end."""
+
+    def __init__(self, gr, w_csc, alpha, sig, drow):
+        self.gr, self.w_csc, self.alpha, self.sig, self.drow = gr, w_csc, alpha, sig, drow
+        self.ys, self.coefs, self.i = None, None, 0
+
+    def begin_step(self, ys, coefs):
+        self.ys, self.coefs, self.i = ys, coefs, 0
+
+    def rhs_stage(self, t, x, stage):
+        stage.dot = (self.ys[self.i], self.drow, self.coefs[self.i], True)
+        self.i += 1
+        ops.spmm_rhs(self.gr, self.w_csc, x, alpha=self.alpha, rhs=True, alpha_sigmoid=self.sig, transpose=True,
+                     stage=stage)
+
+
+def _fused_adjoint_ok(func, y0, adjoint_method, adjoint_params):
+    """odeint_adjoint of a Laplacian RHS with a fixed-grid rk4 adjoint runs fused
+    (_LaplacianAdjointFn): a device fp32 state, weights without their own gradient,
+    the sigmoid alpha, and adjoint parameters among the module's own."""
+    if not (FUSED_ADJOINT and adjoint_method == 'rk4' and y0.is_cuda and y0.dtype == torch.float32 and
+            y0.dim() == 3):
+        return False
+    fn = getattr(func, 'fixed_grid_backward_ok', None)
+    if fn is None or not fn() or func.opt.get('no_alpha_sigmoid', False) or not hasattr(func, 'rhs_stage'):
+        return False
+    own = {id(p) for p in func.parameters()}
+    return all(id(p) in own for p in adjoint_params)
+
+
+class _LaplacianAdjointFn(torch.autograd.Function):
+    """torchdiffeq.odeint_adjoint (0.2.x OdeintAdjointMethod) of f(y) = sigma(alpha)(A y - y)
+    [+ beta x0] with a fixed-grid rk4 adjoint, fused.  Forward: the no-grad solve
+    (the fused adaptive step for dopri5).  Backward, per interval [t_{i-1}, t_i] from
+    the last, the augmented system integrated over s = -t with torchdiffeq's grid
+    (adjoint_options step_size) exactly as torchdiffeq does — y restarts from the
+    forward solution at t_i and is integrated backwards too:
+        dy/ds = -f(y)                      a fused rk4 step of f with dt = -h
+        da/ds = L^T a                      a fused rk4 step over the CSC (_AdjointRHS)
+        d alpha/ds = sigma'(alpha) <(A^T - I) a, y>   row terms in the CSC epilogues (dot_rows)
+        d beta/ds  = <a, x0>               (add_source) fp64 dots of the stage inputs
+    and a += grad_y[i-1] at each output time.  Eight K1 launches per rk4 step, the
+    stage combinations in their epilogues, the state in the graph's in-degree
+    numbering; the parameter gradients summed once at the end.  The RHS counter
+    advances by one per augmented evaluation, as torchdiffeq's backward calls func."""
+
+    @staticmethod
+    def forward(ctx, y0, t, cfg, *params):
+        func, rtol, atol, method, options = cfg[:5]
+        with torch.no_grad():
+            ans = odeint(func, y0, t, rtol=rtol, atol=atol, method=method, options=options)
+        ctx.cfg = cfg
+        ctx.params = params
+        ctx.save_for_backward(t, ans)
+        return ans
+
+    @staticmethod
+    def backward(ctx, grad_y):
+        func = ctx.cfg[0]
+        a_options = ctx.cfg[8] or {}
+        t, ans = ctx.saved_tensors
+        params = ctx.params
+        t_h = _host_times(t)
+        grad_y = grad_y.contiguous()
+        with torch.no_grad():
+            lay = _node_layout(func, ans[0])
+            if lay is not None:
+                func._layout = lay
+            try:
+                gr = func.graph_for(ans[0])
+                w, tag = func._weights_tensor()
+                w_csc = gr.gather_weights(w.detach().float() if w.dtype != torch.float32 else w.detach(),
+                                          transpose=True)
+                R = ans[0].numel() // ans[0].shape[-1]
+                acc = torch.zeros(1 + R, dtype=torch.float64, device=ans.device)
+                gb, drow = acc[0], acc[1:]
+                add_source = bool(func.opt.get('add_source', False))
+                x0 = func.stable_x0(ans[0]) if add_source else None
+                arhs = _AdjointRHS(gr, w_csc, func.alpha_train.detach(), True, drow)
+                step = a_options.get('step_size')
+
+                def internal(v):
+                    if lay is None:
+                        return v.clone()
+                    return _to_internal(v, lay)
+                a = internal(grad_y[-1])
+                ws_y, ws_a = _Workspace(), _Workspace()
+                ybuf = [torch.empty_like(a), torch.empty_like(a)]
+                abuf = [torch.empty_like(a), torch.empty_like(a)]
+                for i in range(len(t_h) - 1, 0, -1):
+                    y = internal(ans[i])
+                    # torchdiffeq's grid of the flipped interval, in t's dtype (as its fixed-grid solver)
+                    s_t = torch.tensor([-t_h[i], -t_h[i - 1]], dtype=t.dtype)
+                    grid = (fixed_grid(s_t, float(step)) if step is not None else s_t).tolist()
+                    for sa, sb in zip(grid[:-1], grid[1:]):
+                        h = sb - sa
+                        if h == 0.0:
+                            continue
+                        yo = ybuf[0] if ybuf[0] is not y else ybuf[1]
+                        ao = abuf[0] if abuf[0] is not a else abuf[1]
+                        _fused_step('rk4', func, -sa, -h, -sb, y, ws_y, out=yo)
+                        ys = [y, ws_y['a'], ws_y['b'], ws_y['c']]
+                        arhs.begin_step(ys, [h / 8.0, 3.0 * h / 8.0, 3.0 * h / 8.0, h / 8.0])
+                        _fused_step('rk4', arhs, sa, h, sb, a, ws_a, out=ao)
+                        if add_source:  # d beta/ds = <a, x0> at the four stages
+                            for c, av in zip((1.0, 3.0, 3.0, 1.0), (a, ws_a['a'], ws_a['b'], ws_a['c'])):
+                                gb = gb + (c * h / 8.0) * ops.dot(av, x0)
+                        y, a = yo, ao
+                    a = a + internal(grad_y[i - 1])
+                sig = torch.sigmoid(func.alpha_train.detach()).double()
+                ga = ops.sum_f64(drow) * (1.0 - sig)
+                if lay is not None:
+                    gy = torch.empty_like(a)
+                    _to_user(a, gy, lay)
+                else:
+                    gy = a
+            finally:
+                func._layout = None
+        out = []
+        for p in params:
+            if p is func.alpha_train:
+                out.append(ga.to(p.dtype).reshape(p.shape))
+            elif p is func.beta_train and add_source:
+                out.append(gb.to(p.dtype).reshape(p.shape))
+            else:
+                out.append(torch.zeros_like(p))
+        return (gy.view(grad_y.shape[1:]), None, None) + tuple(out)
+
+
 def odeint_adjoint(func, y0, t, rtol=1e-7, atol=1e-9, method=None, options=None, adjoint_rtol=None,
                    adjoint_atol=None, adjoint_method=None, adjoint_options=None, adjoint_params=None):
     """torchdiffeq.odeint_adjoint(func, y0, t, ...) with its defaults: the adjoint
@@ -1712,6 +1852,8 @@ def odeint_adjoint(func, y0, t, rtol=1e-7, atol=1e-9, method=None, options=None,
     if not isinstance(t, torch.Tensor):
         t = torch.as_tensor(t)
     cfg = (func, rtol, atol, method, options, adjoint_rtol, adjoint_atol, adjoint_method, adjoint_options)
+    if _fused_adjoint_ok(func, y0, adjoint_method, adjoint_params):
+        return _LaplacianAdjointFn.apply(y0, t, cfg, *adjoint_params)
     return _OdeintAdjoint.apply(y0, t, cfg, *adjoint_params)
 
 
