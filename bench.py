@@ -334,6 +334,7 @@ def bench_single(args, world, rank, dev):
         result["train_rk4"] = bench_train(ei, w, x, h, dev)
         fwd = result.get("dopri5", {}).get("garxiv_laplacian", {}).get("ms_per_solve")
         result["train_adjoint"] = bench_train_adjoint(ei, w, x, dev, fwd)
+        result["hard_attention_train"] = bench_hard_attention_train(ei, x, dev)
         progress("block / train done")
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -1021,6 +1022,85 @@ def bench_train_adjoint(ei, w, x, dev, fwd_ms=None, reps=3):
             "ms_per_train_step": round(ms, 4), "forward_ms_per_solve": fwd_ms,
             "train_over_forward": round(ms / fwd_ms, 3) if fwd_ms else None,
             "rhs_evals_per_train_step": (func.nfe - nfe0) // reps}
+
+
+def bench_hard_attention_train(ei, x, dev, reps=3):
+    """The ogbn-arxiv best_params block in training mode (src/best_params.py:7: block hard_attention, heads 2,
+    attention_dim 32, attention_norm_idx 0, scaled_dot, att_samp_pct 0.8105, dopri5 over [0, 3.676] at tol_scale
+    11353.6, adjoint rk4 with step 1; src/block_transformer_hard_attention.py:37-99) on G-arxiv (C = 128):
+    one training forward — block attention, quantile threshold, sampling mask, group renormalisation, the
+    dopri5 solve — and the training step with its adjoint backward.  The sampled graph is the full CSR with
+    zero weights on the dropped edges (gnpde_threshold_mask_f32): no per-forward graph rebuild."""
+    import gnpde
+    C = x.shape[-1]
+    N = x.shape[1]
+    T, ts = ARXIV_DOPRI5
+    opt = dict(LAP_OPT, hidden_dim=C, block='hard_attention', function='laplacian', heads=2, attention_dim=32,
+               attention_norm_idx=0, attention_type='scaled_dot', att_samp_pct=0.8105268910037231, method='dopri5',
+               step_size=1, tol_scale=ts, adjoint=True, adjoint_method='rk4', adjoint_step_size=1,
+               tol_scale_adjoint=1.0, max_iters=100, self_loop_weight=1.0, data_norm='rw', leaky_relu_slope=0.2,
+               reweight_attention=False, square_plus=False, mix_features=False, beltrami=False, use_flux=False,
+               augment=False)
+    blk = gnpde.HardAttODEblock(gnpde.LaplacianODEFunc, [], opt, dev,
+                                t=torch.tensor([0.0, T], device=dev)).to(dev).train()
+    data = gnpde.GraphData()
+    raw = ei[:, :, :ei.shape[2] - N]  # synthetic.rw_graph appended N self loops; the block adds its own
+    data.new_graph(raw, N)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(13)
+    gout = torch.randn(x.shape, generator=gen, device=dev)
+    import contextlib
+    import io
+
+    def fwd():
+        blk.set_x0(x)
+        with contextlib.redirect_stdout(io.StringIO()):  # the reference's 'retaining ...' line per forward
+            return blk(x, data)
+
+    def sample():
+        with contextlib.redirect_stdout(io.StringIO()):
+            blk.sample_edges(x)
+
+    def step():
+        xi = x.detach().requires_grad_(True)
+        blk.set_x0(xi)
+        with contextlib.redirect_stdout(io.StringIO()):
+            z = blk(xi, data)
+        (z * gout).sum().backward()
+        return xi.grad
+
+    def timed(fn, with_grad):
+        for _ in range(2):
+            if with_grad:
+                fn()
+            else:
+                with torch.no_grad():
+                    fn()
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(reps):
+            if with_grad:
+                fn()
+            else:
+                with torch.no_grad():
+                    fn()
+        e.record()
+        torch.cuda.synchronize()
+        return s.elapsed_time(e) / reps
+
+    ms_fwd = timed(fwd, False)
+    ms_sample = timed(sample, False)
+    ms_step = timed(step, True)
+    return {"config": "HardAttODEblock.forward (training), ogbn-arxiv best_params on G-arxiv (C=128): heads 2, "
+                      "attention_dim 32, att_samp_pct 0.81, dopri5 over [0, %.3f], adjoint rk4 step 1" % T,
+            "ms_per_forward": round(ms_fwd, 4), "ms_sampling": round(ms_sample, 4),
+            "sampling_share": round(ms_sample / ms_fwd, 4), "graph_rebuild_ms": 0.0,
+            "retained_edges": int(blk.retained), "edges": int(raw.shape[2] + N),
+            "ms_per_train_step": round(ms_step, 4),
+            "basis": "sampling = block attention + head mean + quantile + threshold mask + group renormalisation "
+                     "(one host read for the reference's 'retaining' line); the sampled graph reuses the full "
+                     "graph's CSR / plans with zero weights (no rebuild)"}
 
 
 def cpu_baseline(ei, w, x, N, E, C, budget_s):

@@ -54,6 +54,29 @@ __global__ void group_normalize_kernel(const int32_t* __restrict__ rowptr, const
   }
 }
 
+// The hard-attention sampling mask as weights over the FULL graph
+// (src/block_transformer_hard_attention.py:52-55): out[i] = v[i] if v[i] > *thr
+// else 0, and *count = the retained edges (one atomic per wavefront).  Zero-weight
+// edges add exact zeros to every row sum and group sum, so the RHS over the full
+// graph with these weights equals the RHS over the compacted edge list — without
+// building a new CSR / plan for every training forward.
+__global__ void threshold_mask_kernel(const float* __restrict__ v, int64_t n, const float* __restrict__ thr,
+                                      float* __restrict__ out, unsigned long long* __restrict__ count) {
+  const float t = *thr;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  unsigned long long kept = 0;
+  for (int64_t base = blockIdx.x * (int64_t)blockDim.x + (threadIdx.x & ~(kWave - 1)); base < n; base += stride) {
+    const int64_t i = base + lane;
+    const bool live = i < n;
+    const float x = live ? v[i] : 0.f;
+    const bool keep = live && x > t;
+    if (live) out[i] = keep ? x : 0.f;
+    kept += __popcll(__ballot(keep));
+  }
+  if (lane == 0 && kept) atomicAdd(count, kept);
+}
+
 // torch.quantile(v, q) (linear interpolation) on a sorted copy:
 // rank = q*(n-1) in fp32, lo = floor, hi = ceil, w = rank - lo,
 // lerp(a, b, w) = w < 0.5 ? a + w (b - a) : b - (b - a)(1 - w)   (ATen's lerp).
@@ -115,6 +138,18 @@ int gnpde_group_normalize_f32(const int32_t* rowptr, const int32_t* perm, int64_
   const int64_t blocks = ceil_div(R, (int64_t)kWavesPerBlock);
   group_normalize_kernel<<<(int)(blocks < 8192 ? blocks : 8192), kBlock, 0, as_stream(stream)>>>(rowptr, perm, R,
                                                                                                    w_in, w_out);
+  GNPDE_LAUNCH_CHECK();
+  return GNPDE_OK;
+}
+
+int gnpde_threshold_mask_f32(const float* v, int64_t n, const float* thr, float* out, int64_t* count, void* stream) {
+  GNPDE_REQUIRE(n >= 0 && thr && count && (n == 0 || (v && out)), GNPDE_EINVAL, "threshold_mask: bad arguments");
+  hipStream_t s = as_stream(stream);
+  GNPDE_HIP(hipMemsetAsync(count, 0, sizeof(int64_t), s));
+  if (n == 0) return GNPDE_OK;
+  const int64_t blocks = ceil_div(n, kBlock);
+  threshold_mask_kernel<<<(int)(blocks < 4096 ? blocks : 4096), kBlock, 0, s>>>(
+      v, n, thr, out, reinterpret_cast<unsigned long long*>(count));
   GNPDE_LAUNCH_CHECK();
   return GNPDE_OK;
 }

@@ -73,6 +73,7 @@ SIGNATURES = {
     "gnpde_attn_dot_rhs_bf16": (_int, [_vp, _i64, _vp, _i64, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _i64, _vp, _i64, _vp,
                                       _i64, _vp, _vp, _int, _vp, _i64, _vp, _i64, ctypes.POINTER(StageEpilogue), _vp]),
     "gnpde_rows_copy": (_int, [_vp, _i64, _i64, _vp, _vp, _vp, _vp]),
+    "gnpde_threshold_mask_f32": (_int, [_vp, _i64, _vp, _vp, _vp, _vp]),
     "gnpde_initial_step_workspace_bytes": (_size, []),
     "gnpde_adaptive_control": (_int, [_i64, _vp, _f64, _f64, _f64, _f64, _f64, _vp, _vp, _vp, _vp, _size, _vp]),
     "gnpde_initial_step_f32": (_int, [_i64, _vp, _vp, _vp, _f64, _f64, _f64, _vp, _vp, _vp, _size, _vp]),

@@ -8,7 +8,8 @@ quantile are kept and their weights renormalised per softmax group (:32-35);
 the RHS then integrates over the sampled graph.  The threshold is a device
 radix sort + torch.quantile's interpolation (gnpde_quantile_f32), the
 renormalisation a fixed-order per-group pass (gnpde_group_normalize_f32); the
-edge compaction is a torch boolean index on the device.  The sampling runs
+dropped edges keep weight 0 on the full graph (gnpde_threshold_mask_f32) instead
+of a compacted edge list, so no graph is rebuilt per forward.  The sampling runs
 under no_grad exactly as in the reference, so training differentiates the RHS
 through x, alpha_train and beta_train only — which the Laplacian backward
 provides.
@@ -59,7 +60,17 @@ class HardAttODEblock(ODEblock):
         return ops.group_normalize(grouped, attention.reshape(-1)).reshape(attention.shape)
 
     def sample_edges(self, x):
-        """Training-mode attention sampling (:42-57): (edge_index [1,2,E'], weights [1,E'])."""
+        """Training-mode attention sampling (:42-57): (edge_index [1,2,E], weights [1,E]).
+
+        The retained edges are those whose mean attention exceeds the
+        (1 - att_samp_pct) quantile; the module keeps the FULL edge list and gives
+        the dropped edges weight 0 (gnpde_threshold_mask_f32), renormalising per
+        softmax group over the full graph.  Zero weights add exact zeros to every
+        row and group sum, so the integrated RHS is the RHS over the compacted edge
+        list of the reference (:54-56) — while the CSR, the work plans and the
+        node numbering built once per graph serve every training forward (no
+        per-forward graph rebuild, no host-syncing boolean index; one host read
+        for the reference's 'retaining' line)."""
         if self.opt.get('use_flux', False):
             raise NotImplementedError("gnpde: use_flux is broken in the reference (broadcasts [B,1,E] against "
                                       "[1,1,C], block_transformer_hard_attention.py:46-50)")
@@ -70,12 +81,12 @@ class HardAttODEblock(ODEblock):
         with torch.no_grad():
             mean_att = ops.mix_weights(self.get_attention_weights(x))
             threshold = ops.quantile(mean_att, 1 - self.opt['att_samp_pct'])
-            mask = mean_att[0] > threshold
-            edge_index = ei[:, :, mask]
-            self.odefunc.edge_index = edge_index
-            weights = self.renormalise_attention(mean_att[:, mask])
-        print('retaining {} of {} edges'.format(edge_index.shape[2], ei.shape[2]))
-        return edge_index, weights
+            masked, kept = ops.threshold_mask(mean_att, threshold)
+            self.odefunc.edge_index = ei
+            weights = self.renormalise_attention(masked)
+        self.retained = kept
+        print('retaining {} of {} edges'.format(int(kept), ei.shape[2]))
+        return ei, weights
 
     def forward(self, x, graph_data, y=None):
         self.reset_graph_data(graph_data, x.dtype, y)

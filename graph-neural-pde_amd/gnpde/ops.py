@@ -494,6 +494,18 @@ def quantile(v, q):
     return out
 
 
+def threshold_mask(v, thr):
+    """(v with every entry <= *thr set to 0, device int64 count of the kept ones):
+    the hard-attention sampling as weights over the full graph (gnpde_threshold_mask_f32)."""
+    _require_gpu(v, "values", torch.float32)
+    _require_gpu(thr, "threshold", torch.float32)
+    v = v.contiguous()
+    out = torch.empty_like(v)
+    count = torch.empty(1, dtype=torch.int64, device=v.device)
+    _lib.call("gnpde_threshold_mask_f32", _ptr(v), v.numel(), _ptr(thr), _ptr(out), _ptr(count), _stream(v.device))
+    return out, count
+
+
 # --------------------------------------------------------------------------- epilogue helpers
 def _flags(rhs, alpha_sigmoid, add_source):
     f = 0

@@ -114,6 +114,14 @@ size_t gnpde_quantile_workspace_bytes(int64_t n);
 int gnpde_quantile_f32(const float* v, int64_t n, double q, float* out, void* workspace, size_t workspace_bytes,
                        void* stream);
 
+/* The training-mode attention sampling as a weight mask over the full edge list
+ * (src/block_transformer_hard_attention.py:52-55): out[i] = v[i] > *thr ? v[i] : 0,
+ * *count (device int64) = the retained edges.  With these weights the RHS over the
+ * full graph equals the RHS over the compacted edge list (zero weights add exact
+ * zeros), so a training forward needs no new CSR / plan.  thr: device (the
+ * gnpde_quantile_f32 output).                                                 */
+int gnpde_threshold_mask_f32(const float* v, int64_t n, const float* thr, float* out, int64_t* count, void* stream);
+
 /* deg[r] = #{p : idx[p] == r}, r < R (memset + integer atomics: deterministic).
  * With idx = the aggregation CSR's col this is the in-degree used by the
  * reference-mode key sum.                                                   */

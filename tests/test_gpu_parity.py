@@ -924,8 +924,9 @@ def test_hard_attention_block_eval_vs_oracle():
 
 @pytest.mark.parametrize("norm_idx", [0, 1])
 def test_hard_attention_block_training_sampling_vs_oracle(norm_idx):
-    """Training forward: quantile threshold, edge sampling, group renormalisation,
-    then rk4 over the sampled graph; plus gradients through x / alpha (Laplacian backward)."""
+    """Training forward: quantile threshold, edge sampling (a weight mask over the full
+    graph), group renormalisation, then rk4 over the sampled graph (against the oracle
+    on the compacted edge list); plus gradients through x / alpha (Laplacian backward)."""
     N, E, C, h, att = 1200, 8000, 16, 2, 16
     rng = np.random.default_rng(51 + norm_idx)
     ei = rng.integers(0, N, size=(1, 2, E))
@@ -946,9 +947,15 @@ def test_hard_attention_block_training_sampling_vs_oracle(norm_idx):
     # sample from the kernel's own fp32 attention: the mask is a strict comparison,
     # so it is compared bit-exactly given identical inputs (H = 2: the head mean is one add)
     es, ws = O.hard_attention_sample(eo, att_gpu, 0.6, norm_idx, N)
+    # the block keeps the full edge list with weight 0 on the dropped edges (gnpde_threshold_mask_f32):
+    # the retained set, its renormalised weights and the count equal the oracle's compacted sample
     got_ei = blk.odefunc.edge_index.cpu().numpy()
-    assert got_ei.shape == es.shape and (got_ei == es).all()
-    assert np.abs(blk.odefunc.attention_weights.double().cpu().numpy() - ws).max() <= 2e-6
+    assert got_ei.shape == eo.shape and (got_ei == eo).all()
+    gw = blk.odefunc.attention_weights.double().cpu().numpy()[0]
+    keep = gw > 0
+    assert int(blk.retained) == es.shape[2] == int(keep.sum())
+    assert (eo[:, :, keep] == es).all()
+    assert np.abs(gw[keep] - ws[0]).max() <= 2e-6
     f = lambda t, y: O.laplacian_rhs(es, y, None, 0.0, 0.0, block='hard_attention', attention_weights=ws)  # noqa
     want = O.odeint_fixed(f, x, 0.0, 1.0, 'rk4', 0.5)
     assert rel(z, want) <= RTOL
