@@ -163,8 +163,9 @@ class RowShardedLaplacian(object):
 
     On a large graph (ops.LAYOUT_MIN_ROWS, ops.NODE_ORDER 'degree') the rows are
     those of the graph's in-degree numbering (ops.NodeLayout, as the unsharded and
-    column-striped solves): scatter() / unpad() map from / to the caller's numbering,
-    and x0_local must come from scatter(x0)."""
+    column-striped solves): scatter() / unpad() map from / to the caller's numbering.
+    The source term takes the full x0 (``x0=``, the caller's numbering; scattered
+    here) or ``x0_local`` = scatter(x0); a block of another shape is rejected."""
 
     autonomous = True  # the RHS does not read t (gnpde.base_classes.ODEFunc.autonomous)
 
@@ -173,7 +174,7 @@ class RowShardedLaplacian(object):
 
     def __init__(self, edge_index, edge_weight, num_nodes, alpha, beta=None, x0_local=None, add_source=False,
                  alpha_sigmoid=True, group=None, local_rhs=None, chunk=ops.DEFAULT_CHUNK, row_weight=0.0,
-                 local_stage=None, node_order=None):
+                 local_stage=None, node_order=None, x0=None):
         self.group = group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
@@ -181,7 +182,6 @@ class RowShardedLaplacian(object):
         self.N = int(num_nodes)
         self.R = B * self.N
         self.alpha, self.beta = alpha, beta
-        self.x0_local = x0_local
         self.add_source, self.alpha_sigmoid = add_source, alpha_sigmoid
         self.nfe = 0
         self.local_rhs = local_rhs
@@ -206,7 +206,17 @@ class RowShardedLaplacian(object):
             self.blocks = balanced_row_blocks(host_rowptr(edge_index, self.N), self.world, row_weight)
             self.nb = max(max(r1 - r0 for r0, r1 in self.blocks), 1)
         self.r0, self.r1 = self.blocks[self.rank]
-        self._full = {}    # data_ptr of a state block -> its gathered buffer (alloc_state)
+        if x0 is not None:
+            x0_local = self.scatter(x0)
+        if add_source and x0_local is not None and tuple(x0_local.shape[:1]) != (self.nb,):
+            raise ValueError("RowShardedLaplacian: x0_local must be this rank's padded block [%d, C] (scatter(x0), "
+                             "in the graph's numbering), got %s; or pass the full x0 as x0=" %
+                             (self.nb, tuple(x0_local.shape)))
+        self.x0_local = x0_local
+        # data_ptr of a state block handed out by alloc_state -> a weak reference to its
+        # gathered buffer's storage (no strong reference, so buffers the
+        # integrator drops are freed; expired entries are pruned at the next alloc_state)
+        self._blocks_out = {}
         self._gbuf = None  # the gathered buffer of other states
 
     def alloc_state(self, like):
@@ -214,18 +224,32 @@ class RowShardedLaplacian(object):
         [world*nb, C] (gnpde.integrator places its stage inputs here): the all-gather
         before each RHS then runs in place — no send copy, and at world 1 no copy at
         all."""
+        from torch.multiprocessing.reductions import StorageWeakRef
+        for k in [k for k, w in self._blocks_out.items() if w.expired()]:
+            del self._blocks_out[k]
         full = torch.empty((self.world * self.nb,) + tuple(like.shape[1:]), dtype=like.dtype, device=like.device)
         blk = full[self.rank * self.nb:(self.rank + 1) * self.nb]
-        self._full[blk.data_ptr()] = full
+        self._blocks_out[blk.data_ptr()] = StorageWeakRef(full.untyped_storage())
         return blk
+
+    def _gathered_base(self, y_local):
+        """The gathered buffer y_local is the row block of (alloc_state), else None."""
+        base = y_local._base
+        if base is None or y_local.data_ptr() not in self._blocks_out:
+            return None
+        shape = (self.world * self.nb,) + tuple(y_local.shape[1:])
+        if (tuple(base.shape) != shape or base.dtype != y_local.dtype or not base.is_contiguous() or
+                y_local.data_ptr() != base.data_ptr() + self.rank * self.nb * y_local[0].numel() * base.element_size()):
+            return None
+        return base
 
     def gather(self, y_local):
         """All-gather of the row blocks (RCCL over xGMI on ROCm): in place when
         y_local is a block of one of this object's gathered buffers (alloc_state),
         else into a persistent buffer."""
         y_local = y_local.contiguous()
-        full = self._full.get(y_local.data_ptr())
-        if full is not None and full.dtype == y_local.dtype and full.shape[1:] == y_local.shape[1:]:
+        full = self._gathered_base(y_local)
+        if full is not None:
             if self.world > 1:
                 dist.all_gather_into_tensor(full, y_local, group=self.group)
             return full
@@ -257,6 +281,18 @@ class RowShardedLaplacian(object):
             raise NotImplementedError("rhs_stage needs local_stage (or the HIP path)")
         self.part.rhs(self.g, self.w, y_full, y_local, x0=self.x0_local, alpha=self.alpha, beta=self.beta,
                       alpha_sigmoid=self.alpha_sigmoid, add_source=self.add_source, stage=stage)
+
+    def global_rms_norm(self, t):
+        """RMS over the whole state (all row blocks, the padding rows excluded): the
+        error norm an adaptive solve of the row partition must pass
+        (options=dict(norm=sh.global_rms_norm)) so every rank takes the same steps;
+        one all-reduce of 2 doubles."""
+        n = self.r1 - self.r0
+        own = t.reshape(-1, t.shape[-1])[:n]
+        v = torch.stack([own.double().pow(2).sum(), torch.tensor(float(own.numel()), dtype=torch.float64,
+                                                                  device=t.device)])
+        dist.all_reduce(v, group=self.group)
+        return (v[0] / v[1]).sqrt().to(t.dtype)
 
     def scatter(self, y):
         """Full state [R, C] (the caller's numbering) -> this rank's zero-padded block [nb, C]."""
@@ -563,6 +599,65 @@ class _RowView(object):
         self._owner = g
 
 
+class _HipRowAttentionLocal(object):
+    """A rank's arithmetic of RowShardedTransformer on the HIP path: the shares of
+    its own rows [r0, r1) (key sum, node scores, q | k projection), the softmax
+    statistics over the whole (replicated) CSC, and K1 over its rows' local plan.
+    An empty row block (a hub row can take a whole rank's share of the nnz) has
+    zero shares and no aggregation, but its rank still joins every collective
+    (ADVICE r4).  Tests inject a CPU object with the same methods."""
+
+    def __init__(self, g, r0, r1, chunk):
+        self.g, self.r0, self.r1 = g, r0, r1
+        self.n = r1 - r0
+        self.plan = _local_plan(g.csr, r0, r1, chunk)  # item rows = global row ids
+        self.view = _RowView(g, r0, r1)
+        self._uni = None
+
+    def keysum(self, own, Wk, bk):
+        if self.n == 0:
+            return torch.zeros((1, Wk.shape[0]), dtype=torch.float64, device=Wk.device)
+        return ops.ref_keysum(self.view, own, Wk, bk)
+
+    def node_scores(self, own, S, Wq, bq, heads):
+        if self.n == 0:
+            return torch.zeros((0, heads), dtype=torch.float64, device=Wq.device)
+        return ops.ref_scores_from_keysum(self.view, own, S, Wq, bq, heads)
+
+    def project(self, own, W, b):
+        if self.n == 0:
+            return torch.zeros((0, W.shape[0]), dtype=torch.float32, device=W.device)
+        return ops.linear(own, W, b)[0]
+
+    def aggregate(self, ns, norm_idx, x_full, y_local, stage=None, heads=None, **kw):
+        g = self.g
+        if self.plan is None:  # no rows: nothing to write (the block is padding)
+            return None if stage is not None else torch.zeros_like(y_local)
+        kw['stage'] = stage
+        if ns is None:  # fork scaled_dot under source-grouped softmax: 1/outdeg weights, graph-only
+            if self._uni is None:
+                un = ops.uniform_scores(heads)
+                m, rl = ops.softmax_stats(g, un, 0)
+                self._uni = ops.attn_weights(g, un, m, rl, 0)
+            return ops.spmm_rhs_rows(g, self.plan, self._uni, x_full, y_local, self.r0, **kw)
+        if ns.mode == ops._lib.SCORE_REFERENCE:  # destination-grouped (norm_idx 1)
+            if heads == 2:
+                _, _, mr = ops.softmax_stats(g, ns, 1, packed=True)
+                w = ops.RefDstWeights(ns.cs, None, None, 2, mr=mr)
+            else:
+                m, rl = ops.softmax_stats(g, ns, 1)
+                w = ops.RefDstWeights(ns.cs, m, rl, heads)
+            return ops.spmm_rhs_rows(g, self.plan, w, x_full, y_local, self.r0, **kw)
+        if ops._lib.fn("gnpde_attn_dot_supported")(ns.heads, ns.dk, x_full.shape[-1]):
+            mr = ops.softmax_stats(g, ns, 1, packed=True)[2] if norm_idx == 1 else None
+            return ops.spmm_rhs_rows(g, self.plan, None, x_full, y_local, self.r0, ns=ns, mr=mr, **kw)
+        # shapes outside the fused per-edge kernel (ADVICE r4): the head-mean weights in
+        # CSR order (K2), then the plain K1 over this rank's rows
+        m, rl = ops.softmax_stats(g, ns, norm_idx)
+        w = ops.attn_weights(g, ns, m, rl, norm_idx)
+        return ops.spmm_rhs_rows(g, self.plan, w, x_full, y_local, self.r0, **kw)
+
+
 class RowShardedTransformer(object):
     """Row-partitioned transformer attention RHS (the north star's literal 1-D
     partition): contiguous row blocks balanced by nnz
@@ -580,7 +675,11 @@ class RowShardedTransformer(object):
     * the rank's rows are aggregated by the fused kernels over a local plan
       (ops.spmm_rhs_rows), written through pointers shifted to its block.
 
-    B = 1 (one graph; batches shard as replicas, shard_batch)."""
+    Every rank takes part in every collective of an RHS, also a rank whose row
+    block is empty (zero shares).  ``local`` replaces the HIP arithmetic
+    (_HipRowAttentionLocal; tests inject a host restatement and run the
+    collectives under gloo).  B = 1 (one graph; batches shard as replicas,
+    shard_batch)."""
 
     autonomous = True  # the RHS does not read t (gnpde.base_classes.ODEFunc.autonomous)
 
@@ -589,9 +688,13 @@ class RowShardedTransformer(object):
 
     def __init__(self, edge_index, num_nodes, C, Wq, bq, Wk, bk, heads, norm_idx, alpha, score_mode='reference',
                  beta=None, x0_local=None, add_source=False, alpha_sigmoid=True, group=None,
-                 chunk=ops.DEFAULT_CHUNK, row_weight=0.0, comm=None):
+                 chunk=ops.DEFAULT_CHUNK, row_weight=0.0, comm=None, local=None):
         if edge_index.shape[0] != 1:
             raise NotImplementedError("RowShardedTransformer: one graph (B = 1); shard batches with shard_batch")
+        if int(norm_idx) not in (0, 1) or score_mode not in ('reference', 'per_edge'):
+            raise ValueError("RowShardedTransformer: norm_idx 0 | 1 and score_mode 'reference' | 'per_edge'")
+        if int(Wq.shape[0]) % int(heads):
+            raise ValueError("attention_dim %d not divisible by heads %d" % (int(Wq.shape[0]), int(heads)))
         self.group = group
         self.comm = comm if comm is not None else _Comm(group)
         self.rank = dist.get_rank(group)
@@ -607,15 +710,29 @@ class RowShardedTransformer(object):
         self.x0_local = x0_local
         self.add_source, self.alpha_sigmoid = add_source, alpha_sigmoid
         self.nfe = 0
-        self.g = ops.GraphCSR(edge_index, self.N, chunk=chunk)
-        self.blocks = balanced_row_blocks(self.g.csr.rowptr.cpu().numpy(), self.world, row_weight)
+        if local is None:
+            g = ops.GraphCSR(edge_index, self.N, chunk=chunk)
+            self.blocks = balanced_row_blocks(g.csr.rowptr.cpu().numpy(), self.world, row_weight)
+        else:
+            g = None
+            self.blocks = balanced_row_blocks(host_rowptr(edge_index, self.N), self.world, row_weight)
         self.nb = max(max(r1 - r0 for r0, r1 in self.blocks), 1)
         self.r0, self.r1 = self.blocks[self.rank]
-        self.plan = _local_plan(self.g.csr, self.r0, self.r1, chunk)  # item rows = global row ids
-        self.view = _RowView(self.g, self.r0, self.r1)
+        self.local = local if local is not None else _HipRowAttentionLocal(g, self.r0, self.r1, chunk)
         self.uniform = score_mode == 'reference' and self.norm_idx == 0
-        self._uni = None
         self.bytes_per_rhs = 0
+
+    def global_rms_norm(self, t):
+        """RMS over the whole state (all row blocks, the padding rows excluded): the
+        error norm an adaptive solve of the row partition must pass
+        (options=dict(norm=sh.global_rms_norm)) so every rank takes the same steps;
+        one all-reduce of 2 doubles."""
+        n = self.r1 - self.r0
+        own = t.reshape(-1, t.shape[-1])[:n]
+        v = torch.stack([own.double().pow(2).sum(), torch.tensor(float(own.numel()), dtype=torch.float64,
+                                                                  device=t.device)])
+        self.comm.all_reduce(v)
+        return (v[0] / v[1]).sqrt().to(t.dtype)
 
     def scatter(self, y):
         """Full state [1, N, C] or [N, C] -> this rank's zero-padded block [nb, C]."""
@@ -641,44 +758,28 @@ class RowShardedTransformer(object):
         out[:v_own.shape[0]] = v_own
         return out
 
+    def scores(self, own):
+        """The full node-level score operands from this rank's rows (collectives:
+        every rank, whatever its block holds); None for the uniform weights."""
+        if self.uniform:
+            return None, 0
+        if self.score_mode == 'reference':
+            S = self.local.keysum(own, self.Wk, self.bk)
+            self.comm.all_reduce(S)
+            cs = self._gather_rows(self._blockify(self.local.node_scores(own, S, self.Wq, self.bq, self.heads)))
+            ns = ops.NodeScores(ops._lib.SCORE_REFERENCE, self.heads, self.att // self.heads, cs=cs)
+            return ns, S.numel() * 8 + cs.numel() * 8
+        qk = self._gather_rows(self._blockify(self.local.project(own, self.Wcat, self.bcat)))  # [N, 2 att]
+        return _qk_scores(qk, self.heads, self.att), qk.numel() * qk.element_size()
+
     def _rhs(self, y_local, stage):
         self.nfe += 1
         x_full = self._gather_rows(y_local)                     # [N, C]
-        nbytes = x_full.numel() * 4
-        own = x_full[self.r0:self.r1]
-        kw = dict(x0=self.x0_local, alpha=self.alpha, beta=self.beta, alpha_sigmoid=self.alpha_sigmoid,
-                  add_source=self.add_source, stage=stage)
-        if self.plan is None:
-            self.bytes_per_rhs = nbytes
-            return None if stage is not None else torch.zeros_like(y_local)
-        if self.uniform:
-            if self._uni is None:
-                ns = ops.uniform_scores(self.heads)
-                m, rl = ops.softmax_stats(self.g, ns, 0)
-                self._uni = ops.attn_weights(self.g, ns, m, rl, 0)
-            self.bytes_per_rhs = nbytes
-            return ops.spmm_rhs_rows(self.g, self.plan, self._uni, x_full, y_local, self.r0, **kw)
-        if self.score_mode == 'reference':
-            S = ops.ref_keysum(self.view, own, self.Wk, self.bk)
-            self.comm.all_reduce(S)
-            cs = self._gather_rows(self._blockify(ops.ref_scores_from_keysum(self.view, own, S, self.Wq, self.bq,
-                                                                             self.heads)))
-            self.bytes_per_rhs = nbytes + S.numel() * 8 + cs.numel() * 8
-            ns = ops.NodeScores(ops._lib.SCORE_REFERENCE, self.heads, self.att // self.heads, cs=cs)
-            if self.norm_idx != 1:
-                raise NotImplementedError("reference scores under source-grouped softmax are uniform")
-            if self.heads == 2:
-                _, _, mr = ops.softmax_stats(self.g, ns, 1, packed=True)
-                w = ops.RefDstWeights(cs, None, None, 2, mr=mr)
-            else:
-                m, rl = ops.softmax_stats(self.g, ns, 1)
-                w = ops.RefDstWeights(cs, m, rl, self.heads)
-            return ops.spmm_rhs_rows(self.g, self.plan, w, x_full, y_local, self.r0, **kw)
-        qk = self._gather_rows(self._blockify(ops.linear(own, self.Wcat, self.bcat)[0]))  # [N, 2 att]
-        self.bytes_per_rhs = nbytes + qk.numel() * 4
-        ns = _qk_scores(qk, self.heads, self.att)
-        mr = ops.softmax_stats(self.g, ns, 1, packed=True)[2] if self.norm_idx == 1 else None
-        return ops.spmm_rhs_rows(self.g, self.plan, None, x_full, y_local, self.r0, ns=ns, mr=mr, **kw)
+        ns, nbytes = self.scores(x_full[self.r0:self.r1])
+        self.bytes_per_rhs = x_full.numel() * x_full.element_size() + nbytes
+        return self.local.aggregate(ns, self.norm_idx, x_full, y_local, stage=stage, heads=self.heads,
+                                    x0=self.x0_local, alpha=self.alpha, beta=self.beta,
+                                    alpha_sigmoid=self.alpha_sigmoid, add_source=self.add_source)
 
     def __call__(self, t, y_local):
         return self._rhs(y_local, None)

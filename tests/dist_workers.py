@@ -235,3 +235,82 @@ def attn_cols_worker(rank, world, port, score_mode, norm_idx, method, q):
         q.put((rank, err_f, float(np.abs(y_full - want).max()), sh.nfe, sh.bytes_per_rhs))
     finally:
         dist.destroy_process_group()
+
+
+class CpuRowAttentionLocal(object):
+    """The per-rank arithmetic of gnpde.dist.RowShardedTransformer restated on the
+    host in float64 (test infrastructure): the key-sum share and node scores of the
+    rank's rows [r0, r1), their q | k projection, and the rows' softmax +
+    aggregation over the whole gathered state (src/function_transformer_attention.py:
+    218-267, src/utils.py:116-127)."""
+
+    def __init__(self, ei, N, r0, r1):
+        self.full = CpuAttentionLocal(ei, N)
+        self.r0, self.r1 = r0, r1
+
+    def keysum(self, own, Wk, bk):
+        indeg = self.full.indeg[self.r0:self.r1]
+        xb = (indeg[:, None] * own.numpy()).sum(0)
+        return torch.from_numpy((Wk.numpy() @ xb + indeg.sum() * bk.numpy())[None].copy())
+
+    def node_scores(self, own, S, Wq, bq, heads):
+        return self.full.node_scores(own[None], S, Wq, bq, heads)
+
+    def project(self, own, W, b):
+        return self.full.project(own[None], W, b)
+
+    def aggregate(self, ns, norm_idx, x_full, y_local, stage=None, **kw):
+        n = self.r1 - self.r0
+        f = torch.zeros_like(y_local)
+        f[:n] = self.full.aggregate(ns, norm_idx, x_full[None], **kw)[0, self.r0:self.r1]
+        if stage is not None:
+            from host_stage import apply_stage
+            apply_stage(stage, f, y_local)
+            return None
+        return f
+
+
+def attn_rows_worker(rank, world, port, score_mode, norm_idx, method, hub, q):
+    """gnpde.dist.RowShardedTransformer under gloo with CPU arithmetic: state
+    all-gathered, key-sum shares all-reduced, node scores / q | k all-gathered, each
+    rank's rows aggregated; integrated with gnpde.odeint (fused fixed-grid stages;
+    dopri5 with the global error norm) against the oracle on the whole state.
+    ``hub``: row 0 holds most edges, so the nnz-balanced blocks leave a rank with
+    no rows — it must still join every collective."""
+    _init(rank, world, port)
+    try:
+        import gnpde_oracle as O
+        from gnpde import dist as gd, integrator as gi
+        N, E, C, h, att = 37, 260, 12, 2, 8
+        rng = np.random.default_rng(23)
+        ei = rng.integers(0, N, size=(1, 2, E))
+        if hub:
+            ei[0, 0, :220] = 0  # 85% of the rows' edges in row 0
+        x = rng.standard_normal((1, N, C))
+        Wq, Wk = [rng.standard_normal((att, C)) * 0.3 for _ in range(2)]
+        bq, bk = [rng.standard_normal(att) * 0.3 for _ in range(2)]
+        alpha = 0.35
+        T = lambda a: torch.from_numpy(np.ascontiguousarray(a))  # noqa: E731
+        blocks = gd.balanced_row_blocks(gd.host_rowptr(ei, N), world)
+        r0, r1 = blocks[rank]
+        sh = gd.RowShardedTransformer(T(ei), N, C, T(Wq), T(bq), T(Wk), T(bk), h, norm_idx, alpha,
+                                      score_mode=score_mode, local=CpuRowAttentionLocal(ei, N, r0, r1))
+        from host_stage import apply_stage
+        sh.host_stages = True
+        sh.host_stage_apply = lambda stage, f, xx, like: apply_stage(stage, f, xx)
+        y0 = sh.scatter(T(x))
+        opts = dict(step_size=0.125) if method != 'dopri5' else dict(norm=sh.global_rms_norm)
+        with torch.no_grad():
+            f = sh(None, y0)
+            y = gi.odeint(sh, y0, torch.tensor([0.0, 0.5], dtype=torch.float64), method=method, options=opts,
+                          combine=gi._Combine() if method != 'dopri5' else gi._torch_combine, rtol=1e-8, atol=1e-10)[1]
+        f_full = sh.gather(f).numpy()
+        y_full = sh.gather(y).numpy()
+        rhs = lambda t, v: O.transformer_rhs(ei, v, None, Wq, bq, Wk, bk, h, norm_idx, alpha, 0.0,  # noqa: E731
+                                             score_mode=score_mode)
+        err_f = float(np.abs(f_full - rhs(0, x)[0]).max())
+        want = O.odeint_fixed(rhs, x, 0.0, 0.5, method, 0.125) if method != 'dopri5' else \
+            O.odeint_adaptive(rhs, x, [0.0, 0.5], method, 1e-8, 1e-10)[0][-1]
+        q.put((rank, r1 - r0, err_f, float(np.abs(y_full - want[0]).max()), sh.nfe))
+    finally:
+        dist.destroy_process_group()

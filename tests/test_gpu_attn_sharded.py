@@ -195,10 +195,14 @@ def test_sharded_classes_two_ranks_one_gpu(cls, mode, norm_idx):
         assert err <= 1e-6, (rank, err)
 
 
-def test_row_sharded_laplacian_world_one_in_degree_numbering(tmp_path):
+@pytest.mark.parametrize("add_source", [False, True])
+def test_row_sharded_laplacian_world_one_in_degree_numbering(tmp_path, add_source):
     """The row partition in the graph's in-degree numbering at a
     world of one (gloo, in-process): the integrator's state blocks are the gathered
-    buffers themselves (in-place all-gather), the solve equals the unsharded one."""
+    buffers themselves (in-place all-gather), the solve equals the unsharded one.
+    With the source term the full x0 in the caller's numbering is
+    scattered into the block by the class (x0=); a block of the wrong shape is
+    rejected."""
     import torch.distributed as dist
     import gnpde
     init = not dist.is_initialized()
@@ -208,20 +212,28 @@ def test_row_sharded_laplacian_world_one_in_degree_numbering(tmp_path):
         n, e, c = 40000, 300000, 64
         ei, w = synthetic.rw_graph(n, e, seed=12, device=DEV)
         x = synthetic.features(1, n, c, seed=13, device=DEV)
-        a = torch.tensor(0.3, device=DEV)
-        opt = {'block': 'constant', 'function': 'laplacian', 'add_source': False, 'no_alpha_sigmoid': False,
+        x0 = synthetic.features(1, n, c, seed=14, device=DEV)
+        a, b = torch.tensor(0.3, device=DEV), torch.tensor(-0.4, device=DEV)
+        opt = {'block': 'constant', 'function': 'laplacian', 'add_source': add_source, 'no_alpha_sigmoid': False,
                'max_nfe': 10 ** 9, 'multi_modal': False, 'hidden_dim': c}
         func = gnpde.LaplacianODEFunc(c, c, opt, DEV).to(DEV)
         func.edge_index, func.edge_weight = ei, w
+        if add_source:
+            func.x0 = x0
         with torch.no_grad():
             func.alpha_train.fill_(0.3)
+            func.beta_train.fill_(-0.4)
             t = torch.tensor([0.0, 1.0], device=DEV)
             want = gnpde.odeint(func, x, t, method='rk4', options={'step_size': 0.25})[1]
-            sh = gd.RowShardedLaplacian(ei, w, n, a)
+            kw = dict(beta=b, add_source=True, x0=x0) if add_source else {}
+            sh = gd.RowShardedLaplacian(ei, w, n, a, **kw)
             assert sh.lay is not None  # the in-degree numbering
             y = gnpde.odeint(sh, sh.scatter(x), t, method='rk4', options={'step_size': 0.25})[1]
             got = sh.unpad(sh.gather(y)).view(want.shape)
-        assert len(sh._full) >= 2  # the solve's states were gathered in place
+            if add_source:
+                with pytest.raises(ValueError):
+                    gd.RowShardedLaplacian(ei, w, n, a, beta=b, add_source=True, x0_local=x0.view(n, c)[:100])
+        assert len(sh._blocks_out) >= 2  # the solve's states were gathered in place
         assert rel(got, want) <= 1e-6
     finally:
         if init:
