@@ -219,7 +219,10 @@ __device__ __forceinline__ void long_item_stats(int e0, int e1, const int* __res
   // one pass of kSegLongU edges per lane (more heads: passes of fewer, for registers)
   constexpr int LU = MAXH <= 2 ? kSegLongU : 2;
 #pragma unroll
-  for (int ps = 0; ps < kSegLongU / LU; ++ps) push_edges<LU, MAXH>(e0 + lane + ps * LU * kWave, kWave, e1, gidx, sa, M, L);
+  for (int ps = 0; ps < kSegLongU / LU; ++ps) {
+    if (e0 + ps * LU * kWave >= e1) break;  // wave-uniform: an item of fewer edges skips the empty passes
+    push_edges<LU, MAXH>(e0 + lane + ps * LU * kWave, kWave, e1, gidx, sa, M, L);
+  }
   wave_merge<MAXH>(M, L);
 }
 
@@ -248,7 +251,7 @@ __device__ __forceinline__ void hub_chunk_stats(int e0, int e1, int slot, int hu
   const int4 hv = heavy[hub];
   if (ticket != uniform(hv.z) - 1) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  for (int h = 0; h < H; ++h) stats_merge_store(uniform(hv.x), uniform(hv.y), uniform(hv.z), H, h, partials, m, rl, mr);
+  stats_merge_store_heads<MAXH>(uniform(hv.x), uniform(hv.y), uniform(hv.z), H, partials, m, rl, mr);
   if (lane == 0) __hip_atomic_store(&heavy[hub].w, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -364,6 +367,13 @@ __global__ __launch_bounds__(256) void seg_softmax_kernel(const int4* __restrict
 // round 4 (256-thread workgroups, hub chunks) 16.25 / 16.9 / 19.1 us (tools/ab_stats.sh)
 constexpr int kRefStatsNI = GNPDE_RS_NI;
 
+#if GNPDE_EXPERIMENTS
+__constant__ int g_rs_skip = 0;
+__device__ __forceinline__ int rs_skip() { return g_rs_skip; }
+#else
+__device__ __forceinline__ int rs_skip() { return 0; }
+#endif
+
 template <int NI, int MAXH>
 __global__ __launch_bounds__(256) void ref_stats_kernel(const int4* __restrict__ items, int n_items, int n_hub,
                                                          int n_long, const int* __restrict__ rowidx,
@@ -372,6 +382,10 @@ __global__ __launch_bounds__(256) void ref_stats_kernel(const int4* __restrict__
                                                          float* __restrict__ rl, float* __restrict__ mr) {
   const int lane = threadIdx.x & 63;
   const int wid = uniform((int)blockIdx.x * kWavesPerBlock + (int)(threadIdx.x >> 6));
+  if constexpr (GNPDE_EXPERIMENTS) {  // timing probes: 1 skips the hub / long items, 2 the short ones
+    if (rs_skip() == 1 && wid < n_hub + n_long) return;
+    if (rs_skip() == 2 && wid >= n_hub + n_long) return;
+  }
   if (wid < n_hub + n_long) {
     const int4 it = items[wid];
     if (wid < n_hub) {
@@ -432,6 +446,14 @@ template <int NI>
 static int launch_ref_stats(const int4* items, int64_t n_items, int64_t n_hub, int64_t n_long, const int* rowidx,
                             const int* gidx, const ScoreArgs& sa, int4* heavy, double* partials, double* m, float* rl,
                             float* mr, hipStream_t s) {
+#if GNPDE_EXPERIMENTS
+  static const bool once = [] {  // GNPDE_RS_SKIP: the kernel's timing probes (before any capture)
+    const char* e = std::getenv("GNPDE_RS_SKIP");
+    const int v = e ? std::atoi(e) : 0;
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_rs_skip), &v, sizeof(int)) == hipSuccess;
+  }();
+  (void)once;
+#endif
   const int64_t waves = n_hub + n_long + ceil_div(n_items - n_hub - n_long, (int64_t)NI);
   const unsigned grid = (unsigned)ceil_div(waves, (int64_t)kWavesPerBlock);
 #define GNPDE_RS(M)                                                                                            \
@@ -470,6 +492,11 @@ using namespace gnpde;
 extern "C" {
 
 int gnpde_seg_long_edges(void) { return kSegLongMax; }
+
+// edges one pass of a long statistics item covers (long_item_stats: kSegLongU edges
+// per lane up to two heads, 2 per lane beyond): the plan's long-item size when every
+// wavefront should finish in one pass (latency-bound small graphs)
+int gnpde_seg_long_pass_edges(int64_t heads) { return kWave * (heads <= 2 ? kSegLongU : 2); }
 
 int gnpde_seg_block_edges(int mode, int64_t heads, int64_t dk) {
   if (mode == GNPDE_SCORE_REFERENCE || mode == GNPDE_SCORE_UNIFORM) return kWave;

@@ -628,6 +628,11 @@ __global__ __launch_bounds__(256) void node_scores_kernel(const float* __restric
 // per grid row (gridDim.y == B).
 constexpr int kNsfPre = 16;    // Wq values per U output held in registers (dk <= 16)
 constexpr int kNsfLoads = 32;  // tile shares in flight per thread
+#ifndef GNPDE_NSF_OUTS
+#define GNPDE_NSF_OUTS 1  // 4 (the 8-head Cora shape's U in one load round): 18.9 against 16.2 us
+#endif
+constexpr int kNsfOuts = GNPDE_NSF_OUTS;
+constexpr int64_t kNsSplitRows = 50000;  // below: key_projection_kernel + node_scores_kernel  // U outputs per thread with their Wq values in registers
 
 template <int VEC, int GL, int MAXH, bool CLAMP>
 __global__ __launch_bounds__(256) void node_scores_fused_kernel(const float* __restrict__ x, int64_t N, int C,
@@ -650,20 +655,24 @@ __global__ __launch_bounds__(256) void node_scores_fused_kernel(const float* __r
   const float* __restrict__ xb = x + b * N * ldx;
   NsRing<VEC, GL, MAXH> xr;
   ns_first_rows<VEC, GL, MAXH, CLAMP>(xb, n0, n1, C, ldx, g, gl, wv, xr);
-  // this thread's operands of U (output (c, h) = (tid / MAXH, tid % MAXH); the v
-  // outputs c = Cp go to the first threads' second slot), loaded before S is known
+  // this thread's operands of U, loaded before S is known: KO outputs (c, h) =
+  // (t / MAXH, t % MAXH) at t = o * kBlock + tid, and the v outputs (c = Cp) in the
+  // first MAXH threads' extra slot (KO <= kNsfOuts; more outputs take the loop below)
+  constexpr int KO = (Cp * MAXH + kBlock - 1) / kBlock;
   const int dk = att / H;
-  const bool pre = dk <= kNsfPre && Cp * MAXH == kBlock;  // one U output per thread (+ v on the first MAXH)
-  float wq[2][kNsfPre];
+  const bool pre = dk <= kNsfPre && KO <= kNsfOuts && Cp * MAXH == KO * kBlock;
+  float wq[KO <= kNsfOuts ? KO + 1 : 1][kNsfPre];
+  if constexpr (KO <= kNsfOuts) {
 #pragma unroll
-  for (int o = 0; o < 2; ++o) {
-    const int t = o == 0 ? tid : Cp * MAXH + tid;
-    const int c = t / MAXH, h = t - c * MAXH;
-    const bool ok = pre && (o == 0 || tid < MAXH) && h < H && (c < C || c == Cp);
+    for (int o = 0; o <= KO; ++o) {
+      const int t = o < KO ? o * kBlock + tid : Cp * MAXH + tid;
+      const int c = t / MAXH, h = t - c * MAXH;
+      const bool ok = pre && (o < KO || tid < MAXH) && h < H && (c < C || c == Cp);
 #pragma unroll
-    for (int d = 0; d < kNsfPre; ++d) {
-      const int dd = h * dk + min(d, dk - 1);
-      wq[o][d] = (ok && d < dk) ? (c == Cp ? bq[dd] : Wq[(int64_t)dd * C + c]) : 0.f;
+      for (int d = 0; d < kNsfPre; ++d) {
+        const int dd = h * dk + min(d, dk - 1);
+        wq[o][d] = (ok && d < dk) ? (c == Cp ? bq[dd] : Wq[(int64_t)dd * C + c]) : 0.f;
+      }
     }
   }
   // S = sum over the tile shares: every share of the thread in flight at once
@@ -694,11 +703,11 @@ __global__ __launch_bounds__(256) void node_scores_fused_kernel(const float* __r
   }
   // U[c][h] (c < Cp; zero past C and H) and v[h] (row c = Cp)
   const double inv = 1.0 / sqrt((double)dk);
-  if (pre) {
+  if (KO <= kNsfOuts && pre) {
 #pragma unroll
-    for (int o = 0; o < 2; ++o) {
-      const int t = o == 0 ? tid : Cp * MAXH + tid;
-      if (t < (Cp + 1) * MAXH && (o == 0 || tid < MAXH)) {
+    for (int o = 0; o < (KO <= kNsfOuts ? KO + 1 : 1); ++o) {
+      const int t = o < KO ? o * kBlock + tid : Cp * MAXH + tid;
+      if (t < (Cp + 1) * MAXH && (o < KO || tid < MAXH)) {
         const int c = t / MAXH, h = t - c * MAXH;
         double a = 0.0;
 #pragma unroll
@@ -1056,7 +1065,10 @@ static int ref_node_scores_launch(const float* x, int64_t B, int64_t N, int64_t 
   const NsGeom ge = ns_geometry(vec, C, heads);
   const int64_t cp = (int64_t)ge.nch * ge.CW;
   GNPDE_REQUIRE(ns_uv_doubles(ge) <= 16 * C + 2048 + 16, GNPDE_EUNSUPPORTED, "ref_scores: node-score geometry");
-  if (ge.nch == 1 && att <= 1024 && B <= 65535 && ns_fused_enabled()) {
+  // small graphs (B N < kNsSplitRows: the launch is a handful of rows per workgroup) take
+  // the projection once, in its own workgroup, instead of in every node-score workgroup:
+  // Cora-sized 8-head scores 6.3 + 6.7 us against 16.2 us fused
+  if (ge.nch == 1 && att <= 1024 && B <= 65535 && B * N >= kNsSplitRows && ns_fused_enabled()) {
     // every node-score workgroup forms U itself (node_scores_fused_kernel): two launches
     launch_node_scores_fused(s, ge, x, B, N, (int)C, ldx, (int)heads, part, ntiles, Wq, bq, (int)att, cs);
     GNPDE_LAUNCH_CHECK();

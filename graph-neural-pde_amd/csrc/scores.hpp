@@ -144,6 +144,55 @@ __device__ __forceinline__ void stats_merge_store(int g, int first, int nch, int
   if (lane == 0) store_stats(m_out, rl_out, mr_out, g, H, h, M, L);
 }
 
+// stats_merge_store for every head at once (MAXH >= H): a lane loads all heads of
+// its chunks in one round and the heads' xor trees interleave — the same merges in
+// the same order per head, so the same bits.  (A hub group's merge ran head after
+// head, a load and a 6-step tree each: serial latency at 8 heads.)
+#ifndef GNPDE_MERGE_ALL_HEADS
+#define GNPDE_MERGE_ALL_HEADS 1
+#endif
+template <int MAXH>
+__device__ __forceinline__ void stats_merge_store_heads(int g, int first, int nch, int H,
+                                                        const double* __restrict__ partials, double* __restrict__ m_out,
+                                                        float* __restrict__ rl_out, float* __restrict__ mr_out) {
+  if constexpr (!GNPDE_MERGE_ALL_HEADS) {
+    for (int h = 0; h < H; ++h) stats_merge_store(g, first, nch, H, h, partials, m_out, rl_out, mr_out);
+    return;
+  }
+  const int lane = threadIdx.x & 63;
+  double M[MAXH];
+  float L[MAXH];
+#pragma unroll
+  for (int h = 0; h < MAXH; ++h) {
+    M[h] = -INFINITY;
+    L[h] = 0.f;
+  }
+  for (int c = lane; c < nch; c += kWave) {
+    const double* __restrict__ p = partials + (int64_t)(first + c) * 2 * H;
+    double pm[MAXH], pl[MAXH];
+#pragma unroll
+    for (int h = 0; h < MAXH; ++h) {
+      pm[h] = h < H ? p[h] : -INFINITY;
+      pl[h] = h < H ? p[H + h] : 0.0;
+    }
+#pragma unroll
+    for (int h = 0; h < MAXH; ++h)
+      if (h < H) online_merge(M[h], L[h], pm[h], (float)pl[h]);
+  }
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1)
+#pragma unroll
+    for (int h = 0; h < MAXH; ++h) {
+      const double M2 = __shfl_xor(M[h], o);
+      const float L2 = __shfl_xor(L[h], o);
+      online_merge(M[h], L[h], M2, L2);
+    }
+  if (lane == 0)
+#pragma unroll
+    for (int h = 0; h < MAXH; ++h)
+      if (h < H) store_stats(m_out, rl_out, mr_out, g, H, h, M[h], L[h]);
+}
+
 int launch_stats_fixup(const int4* heavy, int64_t n_heavy, int H, const double* partials, double* m, float* rl,
                        float* mr, hipStream_t s);
 

@@ -81,6 +81,7 @@ SIGNATURES = {
     "gnpde_stage_apply_f32": (_int, [_i64, _i64, _i64, _vp, _vp, ctypes.POINTER(StageEpilogue), _vp]),
     "gnpde_stage_apply_bf16": (_int, [_i64, _i64, _i64, _vp, _vp, ctypes.POINTER(StageEpilogue), _vp]),
     "gnpde_seg_long_edges": (_int, []),
+    "gnpde_seg_long_pass_edges": (_int, [_i64]),
     "gnpde_linear_f32": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _vp]),
     "gnpde_linear_bf16": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _vp]),
     "gnpde_linear_wgrad_workspace_bytes": (_size, [_i64, _i64, _i64]),

@@ -86,8 +86,7 @@ class ODEFunc(nn.Module):
         n = x if isinstance(x, int) else int(x.shape[1])
         key = (_tensor_key(self.edge_index), n)
         if self._graph is None or key != self._graph_key:
-            chunk = int(self.opt.get('gnpde_chunk', ops.DEFAULT_CHUNK)) if isinstance(self.opt, dict) else \
-                ops.DEFAULT_CHUNK
+            chunk = self.opt.get('gnpde_chunk') if isinstance(self.opt, dict) else None  # None: ops.auto_chunk
             self._graph = ops.GraphCSR(self.edge_index, n, chunk=chunk)
             self._graph_key = key
             self._w_cache = {}

@@ -86,7 +86,7 @@ class RowPartition(object):
     (``col``); the local plan's item rows are positions too, and the outputs are
     addressed through pointers shifted back by rank*nbmax rows."""
 
-    def __init__(self, g, world, rank, row_weight=0.0, chunk=ops.DEFAULT_CHUNK, blocks=None):
+    def __init__(self, g, world, rank, row_weight=0.0, chunk=None, blocks=None):
         self.world, self.rank = int(world), int(rank)
         rowptr = g.csr.rowptr
         self.blocks = blocks if blocks is not None else balanced_row_blocks(rowptr.cpu().numpy(), world, row_weight)
@@ -100,7 +100,7 @@ class RowPartition(object):
             blk = torch.searchsorted(starts, col, right=True) - 1
             col = col - starts[blk] + blk * self.nbmax
         self.col = col.to(torch.int32).contiguous()
-        self.plan = _local_plan(g.csr, self.r0, self.r1, chunk, self.pos0)
+        self.plan = _local_plan(g.csr, self.r0, self.r1, g.chunk if chunk is None else chunk, self.pos0)
 
     def pad_state(self, y):
         """Full state [R, C] (global row order) -> the padded [world*nbmax, C] layout."""
@@ -173,7 +173,7 @@ class RowShardedLaplacian(object):
     fused_adaptive = False    # the adaptive solvers' wide stages run in column stripes or unsharded
 
     def __init__(self, edge_index, edge_weight, num_nodes, alpha, beta=None, x0_local=None, add_source=False,
-                 alpha_sigmoid=True, group=None, local_rhs=None, chunk=ops.DEFAULT_CHUNK, row_weight=0.0,
+                 alpha_sigmoid=True, group=None, local_rhs=None, chunk=None, row_weight=0.0,
                  local_stage=None, node_order=None, x0=None):
         self.group = group
         self.rank = dist.get_rank(group)
@@ -332,7 +332,7 @@ class ColumnShardedLaplacian(object):
     autonomous = True  # the RHS does not read t (gnpde.base_classes.ODEFunc.autonomous)
 
     def __init__(self, edge_index, edge_weight, num_nodes, C, alpha, beta=None, x0_local=None, add_source=False,
-                 alpha_sigmoid=True, group=None, local_rhs=None, chunk=ops.DEFAULT_CHUNK):
+                 alpha_sigmoid=True, group=None, local_rhs=None, chunk=None):
         self.group = group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
@@ -501,7 +501,7 @@ class ColumnShardedTransformer(object):
 
     def __init__(self, edge_index, num_nodes, C, Wq, bq, Wk, bk, heads, norm_idx, alpha, score_mode='reference',
                  beta=None, x0_local=None, add_source=False, alpha_sigmoid=True, group=None, local=None,
-                 chunk=ops.DEFAULT_CHUNK, comm=None):
+                 chunk=None, comm=None):
         self.group = group
         self.comm = comm if comm is not None else _Comm(group)
         self.rank = dist.get_rank(group)
@@ -610,7 +610,7 @@ class _HipRowAttentionLocal(object):
     def __init__(self, g, r0, r1, chunk):
         self.g, self.r0, self.r1 = g, r0, r1
         self.n = r1 - r0
-        self.plan = _local_plan(g.csr, r0, r1, chunk)  # item rows = global row ids
+        self.plan = _local_plan(g.csr, r0, r1, g.chunk if chunk is None else chunk)  # item rows = global row ids
         self.view = _RowView(g, r0, r1)
         self._uni = None
 
@@ -688,7 +688,7 @@ class RowShardedTransformer(object):
 
     def __init__(self, edge_index, num_nodes, C, Wq, bq, Wk, bk, heads, norm_idx, alpha, score_mode='reference',
                  beta=None, x0_local=None, add_source=False, alpha_sigmoid=True, group=None,
-                 chunk=ops.DEFAULT_CHUNK, row_weight=0.0, comm=None, local=None):
+                 chunk=None, row_weight=0.0, comm=None, local=None):
         if edge_index.shape[0] != 1:
             raise NotImplementedError("RowShardedTransformer: one graph (B = 1); shard batches with shard_batch")
         if int(norm_idx) not in (0, 1) or score_mode not in ('reference', 'per_edge'):

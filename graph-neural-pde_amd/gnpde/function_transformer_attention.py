@@ -240,8 +240,7 @@ class SpGraphTransAttentionLayer(nn.Module):
     def graph_for(self, x, edge):
         key = (_tensor_key(edge), int(x.shape[1]))
         if self._graph is None or key != self._graph_key:
-            self._graph = ops.GraphCSR(edge, int(x.shape[1]), chunk=int(self.opt.get('gnpde_chunk',
-                                                                                      ops.DEFAULT_CHUNK)))
+            self._graph = ops.GraphCSR(edge, int(x.shape[1]), chunk=self.opt.get('gnpde_chunk'))
             self._graph_key = key
         return self._graph
 

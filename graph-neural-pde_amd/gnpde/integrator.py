@@ -1202,6 +1202,7 @@ def _fused_adaptive_ok(func, y0, combine, options):
 # every step eagerly.
 ADAPTIVE_GRAPH = os.environ.get('GNPDE_ADAPTIVE_GRAPH', '1') != '0'
 AFFINE_STAGE = os.environ.get('GNPDE_AFFINE_STAGE', '1') != '0'
+ADAPTIVE_SPEC = os.environ.get('GNPDE_ADAPTIVE_SPEC', '1') != '0'  # steps enqueued ahead (_integrate)
 _ADAPTIVE_CACHE = weakref.WeakKeyDictionary()  # module -> (key, _AdaptiveState)
 
 
@@ -1232,6 +1233,7 @@ class _AdaptiveState(object):
         self.rec = None if host else torch.zeros(4, dtype=torch.float64, device=y0.device)
         self.ws = None if host else torch.empty(_lib.fn("gnpde_dot_workspace_bytes")(), dtype=torch.uint8,
                                                 device=y0.device)
+        self.rec_host, self.rec_slot = None, 0  # pinned copies of rec (_rec_reader)
         self.graphs = {}   # (id Y, id K0, mid) -> (graph, error-sum tensor)
         self.mempool = None
         self.warm = False
@@ -1346,6 +1348,37 @@ class _RKAdaptiveFused(_RKAdaptive):
         """The step-size controller runs on the device (a device solve with the
         default RMS norm): the host reads {ratio, dt, next dt} once per step."""
         return not self.host and 'norm' not in self.options
+
+    def _rotate(self, bufs, kn, d):
+        """Advance (d = 1) or undo (d = -1) the binding of y0 / f0 after an accepted
+        step: two buffers swap; with the third (steps ahead) the three rotate."""
+        P = self.plan
+        for a, b, c in (('Y', 'Y1', 'Ys'), ('K0', kn, 'Ks')):
+            if c not in bufs:
+                bufs[a], bufs[b] = bufs[b], bufs[a]
+            elif d > 0:
+                bufs[a], bufs[b], bufs[c] = bufs[b], bufs[c], bufs[a]
+            else:
+                bufs[a], bufs[b], bufs[c] = bufs[c], bufs[a], bufs[b]
+        if P.fsal:
+            bufs['X%d' % (P.ns - 1)] = bufs['Y1']
+
+    def _rec_reader(self, st, rec):
+        """The step record {ratio, dt, next dt} copied to pinned host memory behind an
+        event (two slots: a step ahead may be in flight): a callable that waits for
+        that copy only."""
+        if st.rec_host is None:
+            st.rec_host = torch.empty((2, rec.numel()), dtype=rec.dtype, pin_memory=True)
+        h = st.rec_host[st.rec_slot]
+        st.rec_slot ^= 1
+        h.copy_(rec, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+
+        def read():
+            ev.synchronize()
+            return h.tolist()
+        return read
 
     def _initial_step_device(self, st, t0):
         """_select_initial_step on the device (gnpde_initial_step_*: the two fixed-order
@@ -1472,6 +1505,14 @@ class _RKAdaptiveFused(_RKAdaptive):
         if dev_ctl and not dt_on_device:  # the device controller carries dt (and the scale) from step to step
             st.dt.fill_(dt)
             st.scale.fill_(dt)
+        # Steps enqueued ahead (ADAPTIVE_SPEC): while the host waits for step n's record, step
+        # n+1 already runs on the binding an acceptance gives, from the device controller's dt.
+        # A third y / f0 buffer keeps step n's inputs intact, so a rejection only discards the
+        # step ahead (its RHS evaluations are not counted) and restores dt on the device.
+        spec_ok = dev_ctl and graphs_ok and ADAPTIVE_SPEC and P.fsal
+        if spec_ok and 'Ys' not in bufs:
+            bufs['Ys'], bufs['Ks'] = torch.empty_like(bufs['Y']), torch.empty_like(bufs['K0'])
+        pending = None  # the record reader of the step enqueued ahead: the current step
         for i_out in range(1, len(th)):
             next_t = th[i_out]
             while next_t > t_cur:
@@ -1480,12 +1521,23 @@ class _RKAdaptiveFused(_RKAdaptive):
                 if self.n_steps >= self.max_num_steps:
                     raise AssertionError('max_num_steps exceeded ({}>={})'.format(self.n_steps, self.max_num_steps))
                 mid = t_cur + dt >= next_t  # an accepted step would cross an output time: keep the dense-output k's
-                if not dev_ctl:
-                    st.scale.fill_(dt)
-                err = self._run_step(st, graphs_ok, t_cur, dt, mid)
+                if pending is not None:
+                    read, pending = pending, None
+                else:
+                    if not dev_ctl:
+                        st.scale.fill_(dt)
+                    err = self._run_step(st, graphs_ok, t_cur, dt, mid)
+                    read = self._rec_reader(st, err) if dev_ctl else None
+                ahead = None
+                # ahead only after a step whose k's the dense output does not need (the step ahead
+                # overwrites them); it keeps its own (mid variant: its dt is not known yet)
+                if spec_ok and st.warm and not mid and self.n_steps + 1 < self.max_num_steps and \
+                        _nfe_headroom(self.func, 2 * P.ns):
+                    self._rotate(bufs, kn, 1)
+                    ahead = self._rec_reader(st, self._run_step(st, graphs_ok, t_cur + dt, dt, True))
                 dt_next = None
                 if dev_ctl:
-                    ratio, _dt, dt_next, _e2 = err.tolist()  # the one host read of the step
+                    ratio, _dt, dt_next, _e2 = read()  # the one host read of the step
                 elif err.dim() == 0:
                     ratio = math.sqrt(float(err) / (y0.numel()))  # the one host read of the step
                 else:
@@ -1497,10 +1549,16 @@ class _RKAdaptiveFused(_RKAdaptive):
                     # a step that crossed an output time keeps its operands for the dense output (the
                     # references as they are now; the buffers are only rewritten by the next step)
                     self._dense = dict(bufs, scale=dt) if mid else None
-                    bufs['Y'], bufs['Y1'] = bufs['Y1'], bufs['Y']
-                    bufs['K0'], bufs[kn] = bufs[kn], bufs['K0']
-                    if P.fsal:
-                        bufs['X%d' % (P.ns - 1)] = bufs['Y1']
+                    if ahead is not None:
+                        pending = ahead  # already on the accepted binding
+                    else:
+                        self._rotate(bufs, kn, 1)
+                elif ahead is not None:  # rejected: discard the step ahead, step n again from its inputs
+                    self._rotate(bufs, kn, -1)
+                    st.dt.fill_(dt_next)
+                    st.scale.fill_(dt_next)
+                    if hasattr(self.func, 'nfe'):
+                        self.func.nfe -= P.ns
                 if dt_next is not None:
                     dt = dt_next
                 elif ratio == 0:

@@ -21,6 +21,27 @@ from . import _lib
 # order below, full-bench A/B on G-arxiv: 128 -> 8,048-8,200, 256 -> 8,485-8,496,
 # 384 -> 8,434-8,450 RHS/s (in row order 128 was best: 121 against 128 us per RHS)
 DEFAULT_CHUNK = int(os.environ.get("GNPDE_CHUNK", 256))
+# Small graphs (fewer rows than SMALL_GRAPH_ROWS, configs[1]'s Cora-sized graph) are
+# latency-bound: the launch is one round of short work items and its time is the
+# longest item's chain of dependent loads, so their rows split at SMALL_CHUNK edges
+# (a 256-edge item of the Cora-sized transformer RHS: 38 us of K1 alone).
+# GNPDE_CHUNK set in the environment applies to every graph.
+SMALL_GRAPH_ROWS = 50000
+SMALL_CHUNK = int(os.environ.get("GNPDE_SMALL_CHUNK", 32))
+
+
+SEG_LONG_SPLIT = os.environ.get("GNPDE_SEG_LONG_SPLIT", "1") != "0"  # small graphs: one-pass long items
+
+
+def auto_chunk(R, chunk=None):
+    """The hub-row split of a graph of R rows: ``chunk`` if given, else the
+    environment's GNPDE_CHUNK, else SMALL_CHUNK below SMALL_GRAPH_ROWS rows and
+    DEFAULT_CHUNK above."""
+    if chunk is not None:
+        return int(chunk)
+    if "GNPDE_CHUNK" in os.environ:
+        return DEFAULT_CHUNK
+    return SMALL_CHUNK if R < SMALL_GRAPH_ROWS else DEFAULT_CHUNK
 STATS_CHUNK = 64     # items of the softmax-statistics kernel (8 lanes per item)
 # K1 work items ordered by power-of-two length class, longest first, row order inside a class
 # ("classes", the default since round 2: tools/stripe_sweep2.sh, profiles/r02c_plan_order_sweep.jsonl —
@@ -113,14 +134,15 @@ class GroupedCSR(object):
             self._rowidx = ri
         return self._rowidx
 
-    def seg_plan(self, eb, long_items=False):
+    def seg_plan(self, eb, long_items=False, long_max=None):
         """Edge-block plan of the segmented-softmax kernel (K2) for blocks of at
         most ``eb`` edges (SegPlan), built once per grouped CSR and block size.
         long_items=True (reference-score statistics): groups longer than eb
-        as long items instead of eb-edge chunks + a fixup launch."""
-        key = (eb, bool(long_items))
+        as long items of at most ``long_max`` edges (default seg_long_max())
+        instead of eb-edge chunks + a fixup launch."""
+        key = (eb, bool(long_items), long_max)
         if key not in self._seg_plans:
-            self._seg_plans[key] = build_seg_plan(self.rowptr, eb, long_items)
+            self._seg_plans[key] = build_seg_plan(self.rowptr, eb, long_items, long_max)
         return self._seg_plans[key]
 
     @property
@@ -192,7 +214,7 @@ def seg_long_max():
     return int(_lib.fn("gnpde_seg_long_edges")())
 
 
-def build_seg_plan(rowptr, eb, long_items=False):
+def build_seg_plan(rowptr, eb, long_items=False, long_max=None):
     """gnpde_seg_plan_build on a host copy of rowptr (once per graph and block size).
     long_items=True (the reference statistics over the CSC): every group longer
     than eb becomes LONG item {e_begin, e_end, -2, group} (one wavefront) when it
@@ -217,7 +239,7 @@ def build_seg_plan(rowptr, eb, long_items=False):
         return torch.from_numpy(np.ascontiguousarray(a[:max(n, 1)]).reshape(-1)).to(dev)
 
     if long_items:
-        long_max = seg_long_max()
+        long_max = seg_long_max() if long_max is None else int(long_max)
         rows = heavy[:nh.value, 0].astype(np.int64)
         s0, s1 = rp[rows].astype(np.int64), rp[rows + 1].astype(np.int64)
         order = np.argsort(-(s1 - s0), kind="stable")
@@ -320,7 +342,7 @@ class GraphCSR(object):
     """All per-graph device structures the RHS needs, built once and reused by
     every RHS evaluation (the reference rebuilds a dense [B,N,N] per call)."""
 
-    def __init__(self, edge_index, num_nodes, chunk=DEFAULT_CHUNK, validate=True):
+    def __init__(self, edge_index, num_nodes, chunk=None, validate=True):
         if validate:
             validate_edge_index(edge_index, num_nodes)
         self.edge_index = edge_index
@@ -328,7 +350,7 @@ class GraphCSR(object):
         self.N = int(num_nodes)
         self.R = self.B * self.N
         self.nnz = self.B * self.E
-        self.chunk = chunk
+        self.chunk = chunk = auto_chunk(self.R, chunk)
         self.csr = build_grouped(edge_index, self.N, 0, chunk)
         self._csc = None
         self._indeg = None
@@ -985,7 +1007,12 @@ def _seg_call(g, ns, norm_idx, out_kind, packed=False):
     if ns.q is not None and (ns.ldqk % 4 or ns.q.data_ptr() % 16 or ns.k.data_ptr() % 16):
         return NotImplemented
     grouped = g.csr if norm_idx == 0 else g.csc
-    plan = grouped.seg_plan(eb, long_items=ns.mode == _lib.SCORE_REFERENCE and out_kind == 1 and norm_idx == 1)
+    long_items = ns.mode == _lib.SCORE_REFERENCE and out_kind == 1 and norm_idx == 1
+    # a small graph's statistics launch is one round of items: every long item one pass
+    # (its hub groups in one-pass chunks), so no wavefront walks a group alone
+    long_max = int(_lib.fn("gnpde_seg_long_pass_edges")(ns.heads)) if (long_items and g.R < SMALL_GRAPH_ROWS and
+                                                                        SEG_LONG_SPLIT) else None
+    plan = grouped.seg_plan(eb, long_items=long_items, long_max=long_max)
     dev = grouped.col.device
     H = ns.heads
     packed = packed and out_kind == 1
@@ -1053,6 +1080,20 @@ def attn_weights(g, ns, m, rl, norm_idx, seg=True):
     return w
 
 
+# Small graphs (SMALL_GRAPH_ROWS): the fork's scaled_dot weights under destination-grouped
+# softmax as a separate edge-parallel pass (gnpde_attn_weights_f32, every edge at once)
+# instead of in K1's gather loop, whose chain per edge (the destination's statistics, one
+# exp per head) is the launch's critical path there.  "wide": for the adaptive solvers'
+# wide stages only (then K1 fuses the stage: no stage pass); "all"; "none".
+SMALL_PRECOMPUTE = os.environ.get("GNPDE_SMALL_PRECOMPUTE", "wide")
+
+
+def _small_precompute(g, stage):
+    if g.R >= SMALL_GRAPH_ROWS or SMALL_PRECOMPUTE == "none":
+        return False
+    return SMALL_PRECOMPUTE == "all" or (stage is not None and stage.wide)
+
+
 def attn_rhs(g, ns, m, rl, norm_idx, x, x0=None, alpha=None, beta=None, rhs=True, alpha_sigmoid=True,
              add_source=False, out=None, stage=None, seg=True, fuse=True, mr=None):
     """K2 + K1: f = a*(A_att x - x) [+ b x0], A_att = head-mean softmax weights
@@ -1063,7 +1104,8 @@ def attn_rhs(g, ns, m, rl, norm_idx, x, x0=None, alpha=None, beta=None, rhs=True
     pass.  Two heads with no statistics given: the packed records.  Per-edge
     scaled_dot (fuse=True, shapes of gnpde_attn_dot_supported): one fused pass
     (attn_dot_rhs) for either grouping."""
-    if fuse and norm_idx == 1 and ns.mode == _lib.SCORE_REFERENCE and x.dtype == torch.float32:
+    if fuse and norm_idx == 1 and ns.mode == _lib.SCORE_REFERENCE and x.dtype == torch.float32 and \
+            not _small_precompute(g, stage):
         if m is None and mr is None:
             if ns.heads == 2:
                 _, _, mr = softmax_stats(g, ns, 1, seg=seg, packed=True)

@@ -481,6 +481,10 @@ int gnpde_seg_block_edges(int mode, int64_t heads, int64_t dk);
 /* Edges of one long item of the reference statistics (whole groups up to it,
  * chunks of it beyond): the plan builder's unit. */
 int gnpde_seg_long_edges(void);
+/* Edges one wavefront covers in ONE pass over a long item of `heads` heads
+ * (<= gnpde_seg_long_edges()): the long-item size of a small graph's plan, whose
+ * launch is latency-bound (every item one pass; longer groups as hub chunks). */
+int gnpde_seg_long_pass_edges(int64_t heads);
 int gnpde_seg_plan_build(const int32_t* rowptr, int64_t R, int32_t eb, int32_t* items, int64_t items_capacity,
                          int32_t* chunk_items, int64_t chunks_capacity, int32_t* heavy, int64_t heavy_capacity,
                          int64_t* n_items, int64_t* n_chunks, int64_t* n_heavy);

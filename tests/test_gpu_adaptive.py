@@ -109,7 +109,10 @@ def test_fused_adaptive_vs_unfused_loop(method, monkeypatch):
     assert n_fused == n_loop
     ns = gi._adaptive_plan(method).ns
     assert nfe == 2 + ns * n_fused  # f0, the initial-step probe, len(alpha) per step
-    assert ns <= calls['stage'] <= ns * n_fused  # the first step eagerly, later ones possibly replayed
+    # f0 and the initial-step probe, then the first step eagerly; a later step runs eagerly, is
+    # captured (its launches recorded through rhs_stage) or replays a captured graph (no call),
+    # and a step enqueued ahead may be captured too (integrator.ADAPTIVE_SPEC)
+    assert 2 + ns <= calls['stage'] <= 2 + 2 * ns * n_fused
     assert rel(fused, loop) <= 2e-6
 
 

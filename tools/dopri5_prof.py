@@ -15,22 +15,17 @@ import torch  # noqa: E402
 import bench  # noqa: E402
 
 
-def main():
-    p = argparse.ArgumentParser()
-    p.add_argument("--reps", type=int, default=5)
-    p.add_argument("--c2", action="store_true")
-    a = p.parse_args()
+def problem(c2):
     import gnpde
-    import gnpde.integrator as integ
     from gnpde import synthetic
     dev = torch.device("cuda", 0)
-    if a.c2:
+    if c2:
         N, E, C = 2708, 13264, 80
     else:
         N, E, C = 169343, 1200000, 128
     ei, w = synthetic.rw_graph(N, E, seed=0, device=dev)
     x = synthetic.features(1, N, C, seed=1, device=dev)
-    if a.c2:
+    if c2:
         opt = {'hidden_dim': C, 'heads': 8, 'attention_dim': 128, 'attention_norm_idx': 1,
                'attention_type': 'scaled_dot', 'function': 'transformer', 'add_source': False,
                'no_alpha_sigmoid': False, 'max_nfe': 10 ** 9, 'multi_modal': False, 'mix_features': False,
@@ -50,6 +45,17 @@ def main():
         T, ts = bench.ARXIV_DOPRI5
     t = torch.tensor([0.0, T], dtype=torch.float32, device=dev)
     kw = dict(method='dopri5', rtol=1e-9 * ts, atol=1e-7 * ts)
+    return func, x, t, kw
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--reps", type=int, default=5)
+    p.add_argument("--c2", action="store_true")
+    a = p.parse_args()
+    func, x, t, kw = problem(a.c2)
+    import gnpde
+    import gnpde.integrator as integ
     with torch.no_grad():
         gnpde.odeint(func, x, t, **kw)
         steps = integ.odeint.last_n_steps
