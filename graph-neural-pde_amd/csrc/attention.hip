@@ -147,6 +147,15 @@ __device__ __forceinline__ float seg_team_score(const ScoreArgs& sa, const float
 //     ticket.  Round 3 ran each hub group as one 1024-thread workgroup (mostly
 //     idle lanes, 16 wave slots held per group): the kernel took 20.9 us on
 //     G-arxiv's CSC, bound by those groups.
+// timing probes of experiment builds (GNPDE_RS_SKIP, launch_ref_stats): 1 / 2 skip the
+// hub + long / the short items, 4 stops a long item after its passes, 5 after its item load
+#if GNPDE_EXPERIMENTS
+__constant__ int g_rs_skip = 0;
+__device__ __forceinline__ int rs_skip() { return g_rs_skip; }
+#else
+__device__ __forceinline__ int rs_skip() { return 0; }
+#endif
+
 constexpr int kSegLongU = 8;                   // edges per lane
 constexpr int kSegLongMax = kWave * kSegLongU;  // 512: one pass
 
@@ -196,14 +205,7 @@ __device__ __forceinline__ void push_edges(int pb, int stride, int e1, const int
 
 template <int MAXH>
 __device__ __forceinline__ void wave_merge(double (&M)[MAXH], float (&L)[MAXH]) {
-#pragma unroll
-  for (int o = 1; o < kWave; o <<= 1)
-#pragma unroll
-    for (int h = 0; h < MAXH; ++h) {
-      const double M2 = __shfl_xor(M[h], o);
-      const float L2 = __shfl_xor(L[h], o);
-      online_merge(M[h], L[h], M2, L2);
-    }
+  lanes_merge<MAXH>(M, L);
 }
 
 // at most kSegLongMax edges [e0, e1) by one wavefront: (M, L) per head, every lane
@@ -218,11 +220,12 @@ __device__ __forceinline__ void long_item_stats(int e0, int e1, const int* __res
   }
   // one pass of kSegLongU edges per lane (more heads: passes of fewer, for registers)
   constexpr int LU = MAXH <= 2 ? kSegLongU : 2;
-#pragma unroll
+#pragma unroll(MAXH <= 2 ? kSegLongU / LU : 1)
   for (int ps = 0; ps < kSegLongU / LU; ++ps) {
     if (e0 + ps * LU * kWave >= e1) break;  // wave-uniform: an item of fewer edges skips the empty passes
     push_edges<LU, MAXH>(e0 + lane + ps * LU * kWave, kWave, e1, gidx, sa, M, L);
   }
+  if (GNPDE_EXPERIMENTS && rs_skip() == 4) return;
   wave_merge<MAXH>(M, L);
 }
 
@@ -367,13 +370,6 @@ __global__ __launch_bounds__(256) void seg_softmax_kernel(const int4* __restrict
 // round 4 (256-thread workgroups, hub chunks) 16.25 / 16.9 / 19.1 us (tools/ab_stats.sh)
 constexpr int kRefStatsNI = GNPDE_RS_NI;
 
-#if GNPDE_EXPERIMENTS
-__constant__ int g_rs_skip = 0;
-__device__ __forceinline__ int rs_skip() { return g_rs_skip; }
-#else
-__device__ __forceinline__ int rs_skip() { return 0; }
-#endif
-
 template <int NI, int MAXH>
 __global__ __launch_bounds__(256) void ref_stats_kernel(const int4* __restrict__ items, int n_items, int n_hub,
                                                          int n_long, const int* __restrict__ rowidx,
@@ -388,6 +384,11 @@ __global__ __launch_bounds__(256) void ref_stats_kernel(const int4* __restrict__
   }
   if (wid < n_hub + n_long) {
     const int4 it = items[wid];
+    if (GNPDE_EXPERIMENTS && rs_skip() == 5 && it.x == -7) return;  // (never: keeps the item load)
+    if (GNPDE_EXPERIMENTS && rs_skip() == 5) {
+      if (lane == 0 && it.y < 0) m[0] = 0.0;  // a use of the load, never taken
+      return;
+    }
     if (wid < n_hub) {
       hub_chunk_stats<MAXH>(uniform(it.x), uniform(it.y), uniform(it.z), uniform(it.w), gidx, sa, heavy, partials, m,
                             rl, mr);

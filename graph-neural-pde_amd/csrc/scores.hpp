@@ -51,7 +51,22 @@ __device__ __forceinline__ float pair_score(int mode, const float* __restrict__ 
 // (max, sum-exp) pushed one score at a time and merged pairwise in a fixed
 // order (deterministic).  fp64 max for the reference mode's fp64 node scores;
 // the float twin serves the fp32 per-edge scores of the fused kernel.
+// Branch-free (selects, one exp): the same values as the two-branch form, and no
+// basic blocks between a wave's gathers and their uses — behind branches the
+// compiler issued each score load just before its push (the 8-head long items of
+// the Cora-sized CSC statistics waited out one load latency per push).
+#ifndef GNPDE_PUSH_SELECT
+#define GNPDE_PUSH_SELECT 1
+#endif
 __device__ __forceinline__ void online_push(double& M, float& L, double s) {
+  if constexpr (GNPDE_PUSH_SELECT) {
+    const bool gt = s > M;
+    const float e = expf((float)(gt ? M - s : s - M));
+    const float up = (M == -INFINITY ? 0.f : L * e) + 1.f;
+    L = gt ? up : L + e;
+    M = gt ? s : M;
+    return;
+  }
   if (s > M) {
     L = (M == -INFINITY ? 0.f : L * expf((float)(M - s))) + 1.f;
     M = s;
@@ -144,6 +159,42 @@ __device__ __forceinline__ void stats_merge_store(int g, int first, int nch, int
   if (lane == 0) store_stats(m_out, rl_out, mr_out, g, H, h, M, L);
 }
 
+// Wave-wide (max, sum-exp) of per-lane online states, every head: beyond two heads in
+// two phases — the max over the lanes (exact, any order), then the lanes' sums
+// rescaled to it (one exp per lane and head) and added in a fixed xor tree — instead
+// of a tree of online merges (two exps per merge, six levels, head after head on one
+// SIMD: ~6 us of an 8-head long item).  Deterministic; rounding as any fixed tree
+// (the per-group kernels agree to 2e-6, tests/test_gpu_parity.py).
+template <int MAXH>
+__device__ __forceinline__ void lanes_merge(double (&M)[MAXH], float (&L)[MAXH]) {
+  if constexpr (MAXH <= 2) {
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1)
+#pragma unroll
+      for (int h = 0; h < MAXH; ++h) {
+        const double M2 = __shfl_xor(M[h], o);
+        const float L2 = __shfl_xor(L[h], o);
+        online_merge(M[h], L[h], M2, L2);
+      }
+  } else {
+    double Mx[MAXH];
+#pragma unroll
+    for (int h = 0; h < MAXH; ++h) Mx[h] = M[h];
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1)
+#pragma unroll
+      for (int h = 0; h < MAXH; ++h) Mx[h] = fmax(Mx[h], __shfl_xor(Mx[h], o));
+#pragma unroll
+    for (int h = 0; h < MAXH; ++h) L[h] = M[h] == -INFINITY ? 0.f : L[h] * expf((float)(M[h] - Mx[h]));
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1)
+#pragma unroll
+      for (int h = 0; h < MAXH; ++h) L[h] += __shfl_xor(L[h], o);
+#pragma unroll
+    for (int h = 0; h < MAXH; ++h) M[h] = Mx[h];
+  }
+}
+
 // stats_merge_store for every head at once (MAXH >= H): a lane loads all heads of
 // its chunks in one round and the heads' xor trees interleave — the same merges in
 // the same order per head, so the same bits.  (A hub group's merge ran head after
@@ -179,14 +230,7 @@ __device__ __forceinline__ void stats_merge_store_heads(int g, int first, int nc
     for (int h = 0; h < MAXH; ++h)
       if (h < H) online_merge(M[h], L[h], pm[h], (float)pl[h]);
   }
-#pragma unroll
-  for (int o = 1; o < kWave; o <<= 1)
-#pragma unroll
-    for (int h = 0; h < MAXH; ++h) {
-      const double M2 = __shfl_xor(M[h], o);
-      const float L2 = __shfl_xor(L[h], o);
-      online_merge(M[h], L[h], M2, L2);
-    }
+  lanes_merge<MAXH>(M, L);
   if (lane == 0)
 #pragma unroll
     for (int h = 0; h < MAXH; ++h)

@@ -1363,14 +1363,17 @@ class _RKAdaptiveFused(_RKAdaptive):
         if P.fsal:
             bufs['X%d' % (P.ns - 1)] = bufs['Y1']
 
-    def _rec_reader(self, st, rec):
-        """The step record {ratio, dt, next dt} copied to pinned host memory behind an
-        event (two slots: a step ahead may be in flight): a callable that waits for
-        that copy only."""
+    def _rec_reader(self, st, rec, slot=None):
+        """A device fp64 record (the step's {ratio, dt, next dt, e2}; h of the initial
+        step, slot 2) copied to pinned host memory behind an event (slots 0 / 1
+        alternate: a step ahead may be in flight): a callable that waits for that copy
+        only and returns the values."""
         if st.rec_host is None:
-            st.rec_host = torch.empty((2, rec.numel()), dtype=rec.dtype, pin_memory=True)
-        h = st.rec_host[st.rec_slot]
-        st.rec_slot ^= 1
+            st.rec_host = torch.empty((3, 4), dtype=torch.float64, pin_memory=True)
+        if slot is None:
+            slot = st.rec_slot
+            st.rec_slot ^= 1
+        h = st.rec_host[slot, :rec.numel()]
         h.copy_(rec, non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
@@ -1397,7 +1400,7 @@ class _RKAdaptiveFused(_RKAdaptive):
             ops.stage_apply(ops.Stage(outs=[(probe, Y, 1.0, 0.0, [(K0, 1.0)])], scale=hf), None, None, Y)
             self.func.rhs_stage(t0, probe, ops.Stage(f_out=f1))
         ops.initial_step(Y, K0, f1, self.atol_f, self.rtol_f, self.order, h, hf)
-        return float(h[2])
+        return self._rec_reader(st, h, slot=2)  # the first step's size: read when it is needed
 
     def _state(self, y0):
         """The module's cached buffers / graphs for this shape, tolerance and graph
@@ -1487,9 +1490,11 @@ class _RKAdaptiveFused(_RKAdaptive):
             f0 = self.func(t0, bufs['Y'])
             bufs['K0'].copy_(f0)
         dt_on_device = False
+        dt_read = None  # the device initial step's reader: the first step is enqueued before it is read
         if self._scalars['first_step'] is None:
             if dev_init:
-                dt = self._initial_step_device(st, t0)
+                dt_read = self._initial_step_device(st, t0)
+                dt = None
                 dt_on_device = True  # st.dt and st.scale hold it already
             else:
                 dt = float(self._select_initial_step(t0.to(dev) if not self.host else t0, bufs['K0']))
@@ -1509,10 +1514,17 @@ class _RKAdaptiveFused(_RKAdaptive):
         # n+1 already runs on the binding an acceptance gives, from the device controller's dt.
         # A third y / f0 buffer keeps step n's inputs intact, so a rejection only discards the
         # step ahead (its RHS evaluations are not counted) and restores dt on the device.
+        # In this mode every step keeps its dense-output k's (one variant per binding, so a
+        # solve replays three captured graphs): whether a step crosses an output time is
+        # known only once its dt is read.
         spec_ok = dev_ctl and graphs_ok and ADAPTIVE_SPEC and P.fsal
         if spec_ok and 'Ys' not in bufs:
             bufs['Ys'], bufs['Ks'] = torch.empty_like(bufs['Y']), torch.empty_like(bufs['K0'])
         pending = None  # the record reader of the step enqueued ahead: the current step
+        if dt_read is not None:
+            if spec_ok and th[-1] > th[0]:  # the first step runs while the host waits for its size
+                pending = self._rec_reader(st, self._run_step(st, graphs_ok, t_cur, 0.0, True))
+            dt = dt_read()[2]
         for i_out in range(1, len(th)):
             next_t = th[i_out]
             while next_t > t_cur:
@@ -1526,7 +1538,7 @@ class _RKAdaptiveFused(_RKAdaptive):
                 else:
                     if not dev_ctl:
                         st.scale.fill_(dt)
-                    err = self._run_step(st, graphs_ok, t_cur, dt, mid)
+                    err = self._run_step(st, graphs_ok, t_cur, dt, mid or spec_ok)
                     read = self._rec_reader(st, err) if dev_ctl else None
                 ahead = None
                 # ahead only after a step whose k's the dense output does not need (the step ahead

@@ -24,10 +24,11 @@ DEFAULT_CHUNK = int(os.environ.get("GNPDE_CHUNK", 256))
 # Small graphs (fewer rows than SMALL_GRAPH_ROWS, configs[1]'s Cora-sized graph) are
 # latency-bound: the launch is one round of short work items and its time is the
 # longest item's chain of dependent loads, so their rows split at SMALL_CHUNK edges
-# (a 256-edge item of the Cora-sized transformer RHS: 38 us of K1 alone).
+# (the Cora-sized transformer's K1: 38 us at 256-edge items, 16 at 32; its dopri5
+# step 0.358 ms at 32, 0.348 at 16, 0.428 at 64: gpurun_out/r05m, r05p).
 # GNPDE_CHUNK set in the environment applies to every graph.
 SMALL_GRAPH_ROWS = 50000
-SMALL_CHUNK = int(os.environ.get("GNPDE_SMALL_CHUNK", 32))
+SMALL_CHUNK = int(os.environ.get("GNPDE_SMALL_CHUNK", 16))
 
 
 SEG_LONG_SPLIT = os.environ.get("GNPDE_SEG_LONG_SPLIT", "1") != "0"  # small graphs: one-pass long items

@@ -96,23 +96,31 @@ def test_fused_adaptive_vs_unfused_loop(method, monkeypatch):
         calls['stage'] += 1
         return orig(*a, **k)
 
+    # A given first step: the selected one (~0.04 here) has an error ratio of ~1e-5, which is
+    # fp32 noise of the error combination, and the controller turns that noise into the next
+    # dt (x8.5 from a ratio of 1.34e-5, x8.35 from 1.46e-5), so the two implementations drifted
+    # apart to 4 and 5 steps on this case (tools/adaptive_diag.py).  From 0.2 every ratio is
+    # well above the noise and both take the same steps.  The same arithmetic on both sides:
+    # no affine first stage (integrator.AFFINE_STAGE; pinned to the oracle by the oracle tests).
+    monkeypatch.setattr(gi, "AFFINE_STAGE", False)
+    opts = {'first_step': 0.2}
     with torch.no_grad():
         func.rhs_stage = spy
         nfe0 = func.nfe
-        fused = gi.odeint(func, x, t, rtol=1e-5, atol=1e-6, method=method)
+        fused = gi.odeint(func, x, t, rtol=1e-5, atol=1e-6, method=method, options=opts)
         n_fused = gi.odeint.last_n_steps
         nfe = func.nfe - nfe0
         del func.rhs_stage
         monkeypatch.setenv("GNPDE_FUSED_ADAPTIVE", "0")
-        loop = gi.odeint(func, x, t, rtol=1e-5, atol=1e-6, method=method)
+        loop = gi.odeint(func, x, t, rtol=1e-5, atol=1e-6, method=method, options=opts)
         n_loop = gi.odeint.last_n_steps
     assert n_fused == n_loop
     ns = gi._adaptive_plan(method).ns
-    assert nfe == 2 + ns * n_fused  # f0, the initial-step probe, len(alpha) per step
-    # f0 and the initial-step probe, then the first step eagerly; a later step runs eagerly, is
-    # captured (its launches recorded through rhs_stage) or replays a captured graph (no call),
-    # and a step enqueued ahead may be captured too (integrator.ADAPTIVE_SPEC)
-    assert 2 + ns <= calls['stage'] <= 2 + 2 * ns * n_fused
+    assert nfe == 1 + ns * n_fused  # f0, len(alpha) per step
+    # f0, then the first step eagerly; a later step runs eagerly, is captured (its launches
+    # recorded through rhs_stage) or replays a captured graph (no call), and a step enqueued
+    # ahead may be captured too (integrator.ADAPTIVE_SPEC)
+    assert 1 + ns <= calls['stage'] <= 1 + 2 * ns * n_fused
     assert rel(fused, loop) <= 2e-6
 
 

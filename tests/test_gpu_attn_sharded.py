@@ -119,7 +119,7 @@ def test_row_partition_shares(arxiv, world, mode, norm_idx):
         mrd = ops.softmax_stats(g, nsd, 1, packed=True)[2] if norm_idx == 1 else None
         wts = None
     for r0, r1 in blocks:
-        plan = gd._local_plan(g.csr, r0, r1, ops.DEFAULT_CHUNK)
+        plan = gd._local_plan(g.csr, r0, r1, g.chunk)
         yl = xr[r0:r1].contiguous()
         loc = ops.spmm_rhs_rows(g, plan, wts, xr, yl, r0, alpha=a, ns=nsd, mr=mrd)
         assert rel(loc, f_full[r0:r1]) <= 1e-6, (world, r0)
