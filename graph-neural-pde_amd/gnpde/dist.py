@@ -458,11 +458,55 @@ class _HipAttentionLocal(object):
             self._uni = ops.attn_weights(self.g, ns, m, rl, 0)
         return self._uni
 
-    def aggregate(self, ns, norm_idx, x, stage=None, **kw):
+    def stats_rows(self, ns, r0, r1):
+        """The destination statistics (norm_idx 1) of groups [r0, r1) only: a list of
+        full-size tensors with those rows written (packed records for two-head
+        reference and per-edge scores, m and rl otherwise), or None outside K2."""
+        return _hip_stats_rows(self.g, ns, r0, r1)
+
+    def aggregate(self, ns, norm_idx, x, stage=None, stats=None, **kw):
         if ns is None:  # uniform weights (fork scaled_dot, norm_idx 0): graph-only
             return ops.spmm_rhs(self.g, self.uniform_weights(kw.pop('heads')), x, stage=stage, **kw)
         kw.pop('heads', None)
-        return ops.attn_rhs(self.g, ns, None, None, norm_idx, x, stage=stage, **kw)
+        m, rl, mr = _stats_args(stats)
+        return ops.attn_rhs(self.g, ns, m, rl, norm_idx, x, stage=stage, mr=mr, **kw)
+
+
+def _hip_stats_rows(g, ns, r0, r1):
+    packed = ns.heads == 2 or ns.mode != ops._lib.SCORE_REFERENCE
+    r = ops.softmax_stats(g, ns, 1, packed=packed, rows=(r0, r1))
+    if r is NotImplemented:
+        return None
+    return [r[2]] if packed else [r[0], r[1]]
+
+
+def _stats_args(stats):
+    """(m, rl, mr) for ops.attn_rhs from a gathered statistics list (None: compute them)."""
+    if stats is None:
+        return None, None, None
+    return (None, None, stats[0]) if len(stats) == 1 else (stats[0], stats[1], None)
+
+
+def _gather_row_blocks(comm, v, blocks, rank, world, nb):
+    """Rows [r0, r1) of this rank's full-size [R, k] tensor v, exchanged so every rank
+    holds all of them: padded [nb, k] blocks all-gathered, then unpadded."""
+    r0, r1 = blocks[rank]
+    if world == 1:
+        return v
+    blk = torch.zeros((nb,) + tuple(v.shape[1:]), dtype=v.dtype, device=v.device)
+    blk[:r1 - r0] = v[r0:r1]
+    pad = torch.empty((world * nb,) + tuple(v.shape[1:]), dtype=v.dtype, device=v.device)
+    comm.all_gather_into_tensor(pad, blk)
+    return torch.cat([pad[p * nb:p * nb + (b - a)] for p, (a, b) in enumerate(blocks)], 0)
+
+
+def _dst_blocks(edge_index, N, world, g=None):
+    """Destination-row blocks balanced by in-degree (the CSC's nnz): each rank forms the
+    softmax statistics of one block (norm_idx 1)."""
+    rp = g.csc.rowptr.cpu().numpy() if g is not None else host_rowptr(edge_index.flip(1) if isinstance(
+        edge_index, torch.Tensor) else edge_index[:, ::-1], N)
+    blocks = balanced_row_blocks(rp, world)
+    return blocks, max(max(b - a for a, b in blocks), 1)
 
 
 def _qk_scores(qk, heads, att):
@@ -501,7 +545,7 @@ class ColumnShardedTransformer(object):
 
     def __init__(self, edge_index, num_nodes, C, Wq, bq, Wk, bk, heads, norm_idx, alpha, score_mode='reference',
                  beta=None, x0_local=None, add_source=False, alpha_sigmoid=True, group=None, local=None,
-                 chunk=None, comm=None):
+                 chunk=None, comm=None, partition_stats=True):
         self.group = group
         self.comm = comm if comm is not None else _Comm(group)
         self.rank = dist.get_rank(group)
@@ -525,7 +569,14 @@ class ColumnShardedTransformer(object):
         self.Wcat = torch.cat([self.Wq, self.Wk], 0).contiguous()
         self.bcat = torch.cat([self.bq, self.bk], 0).contiguous()
         self.uniform = score_mode == 'reference' and self.norm_idx == 0
-        self.local = local if local is not None else _HipAttentionLocal(ops.GraphCSR(edge_index, self.N, chunk=chunk))
+        g = ops.GraphCSR(edge_index, self.N, chunk=chunk) if local is None else None
+        self.local = local if local is not None else _HipAttentionLocal(g)
+        # destination-grouped softmax (norm_idx 1): each rank forms the statistics of one block
+        # of destination rows and the blocks are all-gathered, instead of
+        # every rank forming all of them
+        self.partition_stats = bool(partition_stats) and self.norm_idx == 1 and not self.uniform
+        if self.partition_stats:
+            self.dblocks, self.dnb = _dst_blocks(edge_index, self.N, self.world, g)
         self.bytes_per_rhs = 0  # collective payload of the last RHS (bench.py)
 
     def split(self, x):
@@ -553,13 +604,29 @@ class ColumnShardedTransformer(object):
         self.bytes_per_rhs = qk.numel() * 4
         return _qk_scores(qk, self.heads, self.att)
 
+    def stats(self, ns):
+        """This rank's block of the destination statistics, all-gathered (None: the
+        aggregation forms them all itself)."""
+        if not self.partition_stats:
+            return None
+        d0, d1 = self.dblocks[self.rank]
+        st = self.local.stats_rows(ns, d0, d1)
+        if st is None:
+            return None
+        st = [_gather_row_blocks(self.comm, v, self.dblocks, self.rank, self.world, self.dnb) for v in st]
+        if self.world > 1:
+            self.bytes_per_rhs += sum(self.world * self.dnb * v[0].numel() * v.element_size() for v in st)
+        return st
+
     def __call__(self, t, x_local):
         self.nfe += 1
-        return self.local.aggregate(self.scores(x_local), self.norm_idx, x_local, **self._kw())
+        ns = self.scores(x_local)
+        return self.local.aggregate(ns, self.norm_idx, x_local, stats=self.stats(ns), **self._kw())
 
     def rhs_stage(self, t, x_local, stage):
         self.nfe += 1
-        self.local.aggregate(self.scores(x_local), self.norm_idx, x_local, stage=stage, **self._kw())
+        ns = self.scores(x_local)
+        self.local.aggregate(ns, self.norm_idx, x_local, stage=stage, stats=self.stats(ns), **self._kw())
 
     def global_rms_norm(self, t):
         v = torch.stack([t.double().pow(2).sum(), torch.tensor(float(t.numel()), dtype=torch.float64,
@@ -629,11 +696,15 @@ class _HipRowAttentionLocal(object):
             return torch.zeros((0, W.shape[0]), dtype=torch.float32, device=W.device)
         return ops.linear(own, W, b)[0]
 
-    def aggregate(self, ns, norm_idx, x_full, y_local, stage=None, heads=None, **kw):
+    def stats_rows(self, ns, r0, r1):
+        return _hip_stats_rows(self.g, ns, r0, r1)
+
+    def aggregate(self, ns, norm_idx, x_full, y_local, stage=None, heads=None, stats=None, **kw):
         g = self.g
         if self.plan is None:  # no rows: nothing to write (the block is padding)
             return None if stage is not None else torch.zeros_like(y_local)
         kw['stage'] = stage
+        m0, rl0, mr0 = _stats_args(stats)
         if ns is None:  # fork scaled_dot under source-grouped softmax: 1/outdeg weights, graph-only
             if self._uni is None:
                 un = ops.uniform_scores(heads)
@@ -641,7 +712,11 @@ class _HipRowAttentionLocal(object):
                 self._uni = ops.attn_weights(g, un, m, rl, 0)
             return ops.spmm_rhs_rows(g, self.plan, self._uni, x_full, y_local, self.r0, **kw)
         if ns.mode == ops._lib.SCORE_REFERENCE:  # destination-grouped (norm_idx 1)
-            if heads == 2:
+            if mr0 is not None:
+                w = ops.RefDstWeights(ns.cs, None, None, 2, mr=mr0)
+            elif m0 is not None:
+                w = ops.RefDstWeights(ns.cs, m0, rl0, heads)
+            elif heads == 2:
                 _, _, mr = ops.softmax_stats(g, ns, 1, packed=True)
                 w = ops.RefDstWeights(ns.cs, None, None, 2, mr=mr)
             else:
@@ -649,7 +724,9 @@ class _HipRowAttentionLocal(object):
                 w = ops.RefDstWeights(ns.cs, m, rl, heads)
             return ops.spmm_rhs_rows(g, self.plan, w, x_full, y_local, self.r0, **kw)
         if ops._lib.fn("gnpde_attn_dot_supported")(ns.heads, ns.dk, x_full.shape[-1]):
-            mr = ops.softmax_stats(g, ns, 1, packed=True)[2] if norm_idx == 1 else None
+            mr = None
+            if norm_idx == 1:
+                mr = mr0 if mr0 is not None else ops.softmax_stats(g, ns, 1, packed=True)[2]
             return ops.spmm_rhs_rows(g, self.plan, None, x_full, y_local, self.r0, ns=ns, mr=mr, **kw)
         # shapes outside the fused per-edge kernel: the head-mean weights in
         # CSR order (K2), then the plain K1 over this rank's rows
@@ -688,7 +765,7 @@ class RowShardedTransformer(object):
 
     def __init__(self, edge_index, num_nodes, C, Wq, bq, Wk, bk, heads, norm_idx, alpha, score_mode='reference',
                  beta=None, x0_local=None, add_source=False, alpha_sigmoid=True, group=None,
-                 chunk=None, row_weight=0.0, comm=None, local=None):
+                 chunk=None, row_weight=0.0, comm=None, local=None, partition_stats=True):
         if edge_index.shape[0] != 1:
             raise NotImplementedError("RowShardedTransformer: one graph (B = 1); shard batches with shard_batch")
         if int(norm_idx) not in (0, 1) or score_mode not in ('reference', 'per_edge'):
@@ -720,6 +797,11 @@ class RowShardedTransformer(object):
         self.r0, self.r1 = self.blocks[self.rank]
         self.local = local if local is not None else _HipRowAttentionLocal(g, self.r0, self.r1, chunk)
         self.uniform = score_mode == 'reference' and self.norm_idx == 0
+        # destination statistics (norm_idx 1) formed per block of destination rows and
+        # all-gathered (ColumnShardedTransformer.stats)
+        self.partition_stats = bool(partition_stats) and self.norm_idx == 1 and not self.uniform
+        if self.partition_stats:
+            self.dblocks, self.dnb = _dst_blocks(edge_index, self.N, self.world, g)
         self.bytes_per_rhs = 0
 
     def global_rms_norm(self, t):
@@ -772,12 +854,15 @@ class RowShardedTransformer(object):
         qk = self._gather_rows(self._blockify(self.local.project(own, self.Wcat, self.bcat)))  # [N, 2 att]
         return _qk_scores(qk, self.heads, self.att), qk.numel() * qk.element_size()
 
+    stats = ColumnShardedTransformer.stats
+
     def _rhs(self, y_local, stage):
         self.nfe += 1
         x_full = self._gather_rows(y_local)                     # [N, C]
         ns, nbytes = self.scores(x_full[self.r0:self.r1])
         self.bytes_per_rhs = x_full.numel() * x_full.element_size() + nbytes
-        return self.local.aggregate(ns, self.norm_idx, x_full, y_local, stage=stage, heads=self.heads,
+        st = self.stats(ns) if ns is not None else None
+        return self.local.aggregate(ns, self.norm_idx, x_full, y_local, stage=stage, heads=self.heads, stats=st,
                                     x0=self.x0_local, alpha=self.alpha, beta=self.beta,
                                     alpha_sigmoid=self.alpha_sigmoid, add_source=self.add_source)
 

@@ -146,6 +146,15 @@ class GroupedCSR(object):
             self._seg_plans[key] = build_seg_plan(self.rowptr, eb, long_items, long_max)
         return self._seg_plans[key]
 
+    def seg_plan_rows(self, r0, r1, eb, long_items=False, long_max=None):
+        """seg_plan over the groups [r0, r1) only (their group ids the CSR's): the
+        statistics of one rank's block of destination rows (softmax_stats(rows=))."""
+        key = ('rows', int(r0), int(r1), eb, bool(long_items), long_max)
+        if key not in self._seg_plans:
+            self._seg_plans[key] = build_seg_plan(self.rowptr[int(r0):int(r1) + 1], eb, long_items, long_max,
+                                                  group_offset=r0)
+        return self._seg_plans[key]
+
     @property
     def stats_plan(self):
         """Plan with small chunks for the 8-lanes-per-group statistics kernel."""
@@ -215,7 +224,7 @@ def seg_long_max():
     return int(_lib.fn("gnpde_seg_long_edges")())
 
 
-def build_seg_plan(rowptr, eb, long_items=False, long_max=None):
+def build_seg_plan(rowptr, eb, long_items=False, long_max=None, group_offset=0):
     """gnpde_seg_plan_build on a host copy of rowptr (once per graph and block size).
     long_items=True (the reference statistics over the CSC): every group longer
     than eb becomes LONG item {e_begin, e_end, -2, group} (one wavefront) when it
@@ -223,7 +232,9 @@ def build_seg_plan(rowptr, eb, long_items=False, long_max=None):
     {e_begin, e_end, slot, hub} with a hub table entry {group, first_slot,
     n_chunks, 0} (``heavy``: arrival tickets, the last chunk merges); hub chunks
     first (longest hubs first), then long items longest first, then the packed
-    short items."""
+    short items.  ``rowptr`` may be a row range [r0, r1] of a grouped CSR (edge
+    positions stay absolute): ``group_offset`` = r0 then turns the plan's group ids
+    into the CSR's (the statistics of one rank's destination rows, gnpde.dist)."""
     rp = np.ascontiguousarray(rowptr.cpu().numpy().astype(np.int32))
     R = rp.shape[0] - 1
     nnz = int(rp[-1])
@@ -239,6 +250,8 @@ def build_seg_plan(rowptr, eb, long_items=False, long_max=None):
     def dev32(a, n):
         return torch.from_numpy(np.ascontiguousarray(a[:max(n, 1)]).reshape(-1)).to(dev)
 
+    go = int(group_offset)
+    items[:ni.value, 3] += go  # first group of a short item
     if long_items:
         long_max = seg_long_max() if long_max is None else int(long_max)
         rows = heavy[:nh.value, 0].astype(np.int64)
@@ -251,8 +264,8 @@ def build_seg_plan(rowptr, eb, long_items=False, long_max=None):
             first = len(hub_chunks)
             for c0 in range(int(s0[i]), int(s1[i]), long_max):
                 hub_chunks.append((c0, min(c0 + long_max, int(s1[i])), len(hub_chunks), len(hubs)))
-            hubs.append((int(rows[i]), first, len(hub_chunks) - first, 0))
-        longs = [(int(s0[i]), int(s1[i]), -2, int(rows[i])) for i in order if s1[i] - s0[i] <= long_max]
+            hubs.append((int(rows[i]) + go, first, len(hub_chunks) - first, 0))
+        longs = [(int(s0[i]), int(s1[i]), -2, int(rows[i]) + go) for i in order if s1[i] - s0[i] <= long_max]
         front = np.asarray(hub_chunks + longs, np.int32).reshape(-1, 4)
         all_items = np.concatenate([front, items[:ni.value]], 0)
         table = np.asarray(hubs, np.int32).reshape(-1, 4)
@@ -262,6 +275,8 @@ def build_seg_plan(rowptr, eb, long_items=False, long_max=None):
         plan.n_slots = len(hub_chunks)
         return plan
 
+    chunks[:nc.value, 3] += go
+    heavy[:nh.value, 0] += go
     # items and chunk items back to back in one buffer: K2 then covers both in one launch
     both = dev32(np.concatenate([items[:ni.value], chunks[:max(nc.value, 1)]], 0), ni.value + max(nc.value, 1))
     it_view = both[:max(ni.value, 1) * 4] if ni.value else dev32(items, 0)
@@ -995,7 +1010,7 @@ def stats_record_floats(heads):
     return (2 * heads + 3) & ~3
 
 
-def _seg_call(g, ns, norm_idx, out_kind, packed=False):
+def _seg_call(g, ns, norm_idx, out_kind, packed=False, rows=None):
     """K2 (gnpde_seg_softmax_f32) over the grouped CSR of the softmax groups:
     out_kind 0 -> head-mean weights in aggregation-CSR order (norm_idx 0 only);
     1 -> (m, rl), or with packed=True (None, None, mr): the packed statistics
@@ -1013,7 +1028,12 @@ def _seg_call(g, ns, norm_idx, out_kind, packed=False):
     # (its hub groups in one-pass chunks), so no wavefront walks a group alone
     long_max = int(_lib.fn("gnpde_seg_long_pass_edges")(ns.heads)) if (long_items and g.R < SMALL_GRAPH_ROWS and
                                                                         SEG_LONG_SPLIT) else None
-    plan = grouped.seg_plan(eb, long_items=long_items, long_max=long_max)
+    if rows is not None:  # the groups of rows [r0, r1) only (outputs: full-size, those rows written)
+        if out_kind != 1:
+            return NotImplemented
+        plan = grouped.seg_plan_rows(rows[0], rows[1], eb, long_items=long_items, long_max=long_max)
+    else:
+        plan = grouped.seg_plan(eb, long_items=long_items, long_max=long_max)
     dev = grouped.col.device
     H = ns.heads
     packed = packed and out_kind == 1
@@ -1037,13 +1057,17 @@ def _seg_call(g, ns, norm_idx, out_kind, packed=False):
     return (None, None, mr) if packed else (m, rl)
 
 
-def softmax_stats(g, ns, norm_idx, seg=True, packed=False):
+def softmax_stats(g, ns, norm_idx, seg=True, packed=False, rows=None):
     """m [R,h] fp64, rl [R,h]: per-group max and 1/(sum-exp + 1e-16)
     (utils.softmax, src/utils.py:116-127).  seg=True: the edge-block kernel K2;
     shapes outside it (and seg=False) use the per-group kernels
     (gnpde_softmax_stats_f32).  packed=True returns (None, None, mr): the same
     statistics as packed records [R, stats_record_floats(h)] fp32 only (the form
-    the fused-weight K1 reads in one cache line per edge)."""
+    the fused-weight K1 reads in one cache line per edge).  rows=(r0, r1): only
+    the groups [r0, r1) are formed (K2; full-size outputs with those rows written,
+    the same values as the full launch) — NotImplemented outside K2's shapes."""
+    if rows is not None:
+        return _seg_call(g, ns, norm_idx, 1, packed=packed, rows=rows) if seg else NotImplemented
     if seg:
         r = _seg_call(g, ns, norm_idx, 1, packed=packed)
         if r is not NotImplemented:

@@ -171,20 +171,41 @@ class CpuAttentionLocal(object):
     def project(self, x, W, b):
         return torch.from_numpy(x[0].numpy() @ W.numpy().T + b.numpy())
 
-    def aggregate(self, ns, norm_idx, x, stage=None, **kw):
-        import gnpde_oracle as O
-        heads = kw['heads']
+    def _scores(self, ns, heads):
         src, dst = self.ei[0, 0], self.ei[0, 1]
         if ns is None:  # uniform
-            s = np.zeros((len(src), heads))
-        elif ns.cs is not None:
-            s = ns.cs.numpy()[src]
+            return np.zeros((len(src), heads))
+        if ns.cs is not None:
+            return ns.cs.numpy()[src]
+        q, k = ns.q.numpy(), ns.k.numpy()
+        dk = ns.dk
+        return np.stack([(q[src, h * dk:(h + 1) * dk] * k[dst, h * dk:(h + 1) * dk]).sum(1) / np.sqrt(dk)
+                         for h in range(heads)], 1)
+
+    def stats_rows(self, ns, r0, r1):
+        """The destination groups [r0, r1)'s max and sum-exp (the rest 0): the block a
+        rank forms and all-gathers (partitioned statistics, norm_idx 1)."""
+        s = self._scores(ns, ns.heads)
+        grp = self.ei[0, 1]
+        sel = (grp >= r0) & (grp < r1)
+        mx = np.full((self.N, ns.heads), -np.inf)
+        np.maximum.at(mx, grp[sel], s[sel])
+        sm = np.zeros((self.N, ns.heads))
+        np.add.at(sm, grp[sel], np.exp(s[sel] - mx[grp[sel]]))
+        m, l = np.zeros_like(mx), np.zeros_like(sm)
+        m[r0:r1], l[r0:r1] = mx[r0:r1], sm[r0:r1]
+        return [torch.from_numpy(m), torch.from_numpy(l)]
+
+    def aggregate(self, ns, norm_idx, x, stage=None, stats=None, **kw):
+        import gnpde_oracle as O
+        heads = kw['heads']
+        s = self._scores(ns, heads)
+        if stats is not None:  # the all-gathered blocks of the destination statistics
+            grp = self.ei[0, norm_idx]
+            mx, sm = stats[0].numpy(), stats[1].numpy()
+            att = (np.exp(s - mx[grp]) / (sm[grp] + 1e-16))[None]
         else:
-            q, k = ns.q.numpy(), ns.k.numpy()
-            dk = ns.dk
-            s = np.stack([(q[src, h * dk:(h + 1) * dk] * k[dst, h * dk:(h + 1) * dk]).sum(1) / np.sqrt(dk)
-                          for h in range(heads)], 1)
-        att = O.edge_softmax(s[None], self.ei[:, norm_idx], self.N)
+            att = O.edge_softmax(s[None], self.ei[:, norm_idx], self.N)
         f = O.rhs_epilogue(O.aggregate(self.ei, att.mean(axis=2), x.numpy()), x.numpy(), None, kw['alpha'], 0.0,
                            False, False)
         f = torch.from_numpy(f)
@@ -232,7 +253,8 @@ def attn_cols_worker(rank, world, port, score_mode, norm_idx, method, q):
         err_f = float(np.abs(f_full - rhs(0, x)).max())
         want = O.odeint_fixed(rhs, x, 0.0, 0.5, method, 0.125) if method != 'dopri5' else \
             O.odeint_adaptive(rhs, x, [0.0, 0.5], method, 1e-8, 1e-10)[0][-1]
-        q.put((rank, err_f, float(np.abs(y_full - want).max()), sh.nfe, sh.bytes_per_rhs))
+        q.put((rank, err_f, float(np.abs(y_full - want).max()), sh.nfe, sh.bytes_per_rhs,
+               sh.dnb if sh.partition_stats else 0))
     finally:
         dist.destroy_process_group()
 
@@ -258,6 +280,9 @@ class CpuRowAttentionLocal(object):
 
     def project(self, own, W, b):
         return self.full.project(own[None], W, b)
+
+    def stats_rows(self, ns, r0, r1):
+        return self.full.stats_rows(ns, r0, r1)
 
     def aggregate(self, ns, norm_idx, x_full, y_local, stage=None, **kw):
         n = self.r1 - self.r0

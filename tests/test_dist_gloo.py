@@ -107,15 +107,19 @@ def test_column_sharded_transformer_matches_single_process(score_mode, norm_idx,
     whole state; integrated (rk4 through the fused stages, dopri5 through the
     global error norm) it matches the single-process integration."""
     res = _run(W.attn_cols_worker, score_mode, norm_idx, method)
-    for rank, err_f, err_y, nfe, nbytes in res:
+    for rank, err_f, err_y, nfe, nbytes, dnb in res:
         assert err_f < 1e-12
         assert err_y < 1e-9
+        # norm_idx 1: each rank forms the statistics of a block of dnb destination rows, and
+        # the blocks (max and sum-exp, [dnb, heads] fp64 each on this host path) are all-gathered
+        stats = 2 * 2 * dnb * 2 * 8 if norm_idx == 1 else 0
+        assert (dnb > 0) == (norm_idx == 1 and not (score_mode == "reference" and norm_idx == 0))
         if score_mode == "reference" and norm_idx == 0:
             assert nbytes == 0  # uniform 1/outdeg weights: no collective at all
         elif score_mode == "reference":
-            assert nbytes == (8 + 41 * 2) * 8  # S [1, att] + cs [N, heads], fp64
+            assert nbytes == (8 + 41 * 2) * 8 + stats  # S [1, att] + cs [N, heads], fp64
         else:
-            assert nbytes == 41 * 16 * 4  # q | k [N, 2 att], fp32
+            assert nbytes == 41 * 16 * 4 + stats  # q | k [N, 2 att], fp32
 
 
 @pytest.mark.parametrize("score_mode,norm_idx,method,world,hub", [

@@ -125,6 +125,26 @@ def test_row_partition_shares(arxiv, world, mode, norm_idx):
         assert rel(loc, f_full[r0:r1]) <= 1e-6, (world, r0)
 
 
+@pytest.mark.parametrize("world,mode", [(2, 'reference'), (8, 'reference'), (4, 'per_edge'), (8, 'per_edge')])
+def test_partitioned_destination_statistics(arxiv, world, mode):
+    """the destination statistics (norm_idx 1) formed per block of
+    destination rows (gnpde.dist: each rank one block, then all-gathered) — K2 over a
+    row-range plan — equal the statistics of the whole CSC bit for bit."""
+    ei, g, x, Wq, bq, Wk, bk = arxiv
+    kw = dict(wcat=(torch.cat([Wq, Wk], 0), torch.cat([bq, bk], 0))) if mode == 'per_edge' else {}
+    ns = ops.node_scores(g, x, Wq, bq, Wk, bk, H, 'scaled_dot', mode, **kw)
+    _, _, mr = ops.softmax_stats(g, ns, 1, packed=True)
+    blocks, nb = gd._dst_blocks(ei, N, world, g)
+    assert blocks[0][0] == 0 and blocks[-1][1] == N and max(b - a for a, b in blocks) == nb
+    got = torch.full_like(mr, float('nan'))
+    for r0, r1 in blocks:
+        part = gd._hip_stats_rows(g, ns, r0, r1)
+        assert part is not None and len(part) == 1
+        got[r0:r1] = part[0][r0:r1]
+    nz = torch.diff(g.csc.rowptr) > 0
+    assert torch.equal(got[nz], mr[nz])
+
+
 def _two_rank_worker(rank, world, port, cls, mode, norm_idx, q):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
