@@ -244,11 +244,15 @@ def test_bf16_unfused_adaptive_loop_combines_in_hip(monkeypatch):
 
 
 def test_attention_rhs_dopri5_fused_vs_unfused(monkeypatch):
-    """The transformer RHS (fork scaled_dot, norm_idx 1: weights formed inside K1 from
-    the statistics records, a policy the wide epilogue is not fused with) under
-    dopri5: f then the stage pass; same steps as the tableau loop and the same values
-    to the suite's 1e-5 (the softmax RHS amplifies the rounding differences of the
-    two combination orders: 2.9e-6 measured)."""
+    """The transformer RHS (fork scaled_dot, norm_idx 1) under dopri5, the fused step
+    (on this small graph the weights precomputed and the stage in K1's wide epilogue,
+    ops.SMALL_PRECOMPUTE; on large graphs weights inside K1, then the stage pass)
+    against the tableau loop: the same steps, values within the suite's RTOL = 1e-5
+    (north_star's fp32 tolerance).  Why not tighter: the two sides form the same stage
+    values in different fp32 summation orders (fused epilogue vs torch combinations and
+    norm), a few ulp per stage, and the softmax RHS carries them through ~10 steps of 6
+    stages with growth; round 4 measured 2.896e-6 (gpurun_out/r04c), above the 2e-6
+    first written, so the bar is the suite's tolerance, not a fitted one."""
     N, E, C, h, att = 2708, 10556, 80, 8, 128
     rng = np.random.default_rng(41)
     ei = rng.integers(0, N, size=(1, 2, E))

@@ -129,7 +129,10 @@ def test_row_partition_shares(arxiv, world, mode, norm_idx):
 def test_partitioned_destination_statistics(arxiv, world, mode):
     """the destination statistics (norm_idx 1) formed per block of
     destination rows (gnpde.dist: each rank one block, then all-gathered) — K2 over a
-    row-range plan — equal the statistics of the whole CSC bit for bit."""
+    row-range plan — equal the statistics of the whole CSC: the max bit for bit, the
+    reciprocal sums within 1e-6 (a group's segmented sum runs in a lane order that
+    depends on where the item packing put it, and a block boundary moves the packing:
+    1-ulp differences on 2-4 of 169k rows measured, tools/dbg_stats.py)."""
     ei, g, x, Wq, bq, Wk, bk = arxiv
     kw = dict(wcat=(torch.cat([Wq, Wk], 0), torch.cat([bq, bk], 0))) if mode == 'per_edge' else {}
     ns = ops.node_scores(g, x, Wq, bq, Wk, bk, H, 'scaled_dot', mode, **kw)
@@ -142,7 +145,8 @@ def test_partitioned_destination_statistics(arxiv, world, mode):
         assert part is not None and len(part) == 1
         got[r0:r1] = part[0][r0:r1]
     nz = torch.diff(g.csc.rowptr) > 0
-    assert torch.equal(got[nz], mr[nz])
+    assert torch.equal(got[nz, :H], mr[nz, :H])  # the max (stored fp32-exact)
+    assert torch.allclose(got[nz, H:2 * H], mr[nz, H:2 * H], rtol=1e-6, atol=0)
 
 
 def _two_rank_worker(rank, world, port, cls, mode, norm_idx, q):
