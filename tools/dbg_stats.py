@@ -1,3 +1,7 @@
+"""Per-block destination statistics (gnpde.dist partitioned statistics, per-edge
+scaled_dot on G-arxiv) against the whole-CSC launch: rows that differ, their degree
+and values, at 2 / 4 / 8 blocks (tests/test_gpu_attn_sharded.py's bar).
+  python tools/dbg_stats.py"""
 import sys, os, torch
 sys.path.insert(0, "graph-neural-pde_amd"); sys.path.insert(0, ".")
 from gnpde import ops, synthetic, dist as gd
