@@ -734,18 +734,24 @@ __global__ __launch_bounds__(256) void node_scores_fused_kernel(const float* __r
   ns_block_resident<VEC, GL, MAXH, CLAMP, true>(U, xb, rcs, n0, n1, C, ldx, H, Cp, g, gl, wv, xr);
 }
 
-// S[b][d] = sum of the tile shares part[b][tile][d] in tile order (one thread per
-// (b, d)): the key sum of gnpde_ref_keysum_f32, handed to the caller (a sharded
-// solve all-reduces it over the column stripes before the node scores).
+// S[b][d] = the sum of the tile shares part[b][tile][d]: the key sum of
+// gnpde_ref_keysum_f32, handed to the caller (a sharded solve all-reduces it over the
+// column stripes before the node scores).  One wavefront per (b, d): lane l sums tiles
+// l, l + 64, ... in order, then a fixed xor tree (one thread walking all ~256 tiles in
+// a chain of dependent loads took 62 us on G-arxiv, the sharded reference RHS's
+// slowest launch).
 __global__ __launch_bounds__(256) void keysum_reduce_kernel(const double* __restrict__ part, int ntiles, int att,
                                                              int64_t B, double* __restrict__ S) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t i = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
   if (i >= B * att) return;
+  const int lane = threadIdx.x & 63;
   const int64_t b = i / att, d = i - b * att;
   const double* __restrict__ pb = part + b * (int64_t)ntiles * att + d;
   double acc = 0.0;
-  for (int t = 0; t < ntiles; ++t) acc += pb[(int64_t)t * att];
-  S[i] = acc;
+  for (int t = lane; t < ntiles; t += kWave) acc += pb[(int64_t)t * att];
+#pragma unroll
+  for (int o = kWave / 2; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+  if (lane == 0) S[i] = acc;
 }
 
 // ------------------------------------------------------------------ host helpers
@@ -1121,7 +1127,8 @@ int gnpde_ref_keysum_f32(const float* x, int64_t B, int64_t N, int64_t C, int64_
   int ntiles = 0;
   rc = ref_keysum_launch(x, B, N, C, ldx, indeg, Wk, bk, att, part, s, &ntiles);
   if (rc) return rc;
-  keysum_reduce_kernel<<<(unsigned)ceil_div(B * att, (int64_t)kBlock), kBlock, 0, s>>>(part, ntiles, (int)att, B, S);
+  keysum_reduce_kernel<<<(unsigned)ceil_div(B * att, (int64_t)kWavesPerBlock), kBlock, 0, s>>>(part, ntiles, (int)att,
+                                                                                                 B, S);
   GNPDE_LAUNCH_CHECK();
   return GNPDE_OK;
 }

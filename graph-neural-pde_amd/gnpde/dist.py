@@ -26,11 +26,29 @@ communication pattern — including the fused-stage path the integrator runs
 (``rhs_stage``) — is exercised with the gloo backend; the default is the HIP path.
 """
 import math
+import os
 
 import torch
 import torch.distributed as dist
 
 from . import ops
+
+# Step graphs that capture the RHS's collectives (RCCL through torch.distributed into
+# the hipGraph: tools/rccl_capture_check.py replays all_reduce / all_gather_into_tensor
+# correctly).  A sharded RHS on the nccl backend is captured at a world of one (its
+# collectives then run in the graph) and, with GNPDE_CAPTURE_COLLECTIVES=1, at any
+# world — opt-in there: the multi-rank capture has not run on this build's hardware.
+CAPTURE_COLLECTIVES = os.environ.get('GNPDE_CAPTURE_COLLECTIVES', '0') == '1'
+
+
+def _capturable(group, world, collectives=True):
+    """Whether a sharded RHS's steps may be captured and replayed: no collective in the
+    RHS at all, or RCCL collectives at a world of one (or GNPDE_CAPTURE_COLLECTIVES)."""
+    if not collectives:
+        return True
+    if dist.get_backend(group) != 'nccl':
+        return False
+    return world == 1 or CAPTURE_COLLECTIVES
 
 
 def row_blocks(R, world):
@@ -169,8 +187,23 @@ class RowShardedLaplacian(object):
 
     autonomous = True  # the RHS does not read t (gnpde.base_classes.ODEFunc.autonomous)
 
-    graph_capturable = False  # an RCCL all-gather per RHS: the integrator runs it eagerly
     fused_adaptive = False    # the adaptive solvers' wide stages run in column stripes or unsharded
+
+    @property
+    def graph_capturable(self):
+        """An all-gather per RHS (none at a world of one: the state blocks are the
+        gathered buffers): captured at a world of one, or with GNPDE_CAPTURE_COLLECTIVES
+        on RCCL; injected host arithmetic never."""
+        if self.part is None:
+            return False
+        return self.world == 1 or _capturable(self.group, self.world)
+
+    def graph_capture_state(self, y):
+        """What a captured step reads besides its state buffers (integrator._capture_state)."""
+        return (self.g, self.w, self.part.col, self.part.plan) + ((self.x0_local,) if self.add_source else ())
+
+    def capture_key_tensors(self):
+        return tuple(t for t in (self.alpha, self.beta) if isinstance(t, torch.Tensor))
 
     def __init__(self, edge_index, edge_weight, num_nodes, alpha, beta=None, x0_local=None, add_source=False,
                  alpha_sigmoid=True, group=None, local_rhs=None, chunk=None, row_weight=0.0,
@@ -257,7 +290,10 @@ class RowShardedLaplacian(object):
         out = self._gbuf
         if out is None or tuple(out.shape) != shape or out.dtype != y_local.dtype or out.device != y_local.device:
             out = self._gbuf = torch.empty(shape, dtype=y_local.dtype, device=y_local.device)
-        dist.all_gather_into_tensor(out, y_local, group=self.group)
+        if self.world == 1:
+            out.copy_(y_local)  # no collective at a world of one (whatever the backend)
+        else:
+            dist.all_gather_into_tensor(out, y_local, group=self.group)
         return out
 
     def __call__(self, t, y_local):
@@ -541,7 +577,21 @@ class ColumnShardedTransformer(object):
 
     autonomous = True  # the RHS does not read t (gnpde.base_classes.ODEFunc.autonomous)
 
-    graph_capturable = False  # collectives per RHS
+    @property
+    def graph_capturable(self):
+        """Collectives per RHS (the uniform weights have none): captured on RCCL at a
+        world of one, or at any world with GNPDE_CAPTURE_COLLECTIVES=1."""
+        if not isinstance(self.local, _HipAttentionLocal):
+            return False
+        return _capturable(self.group, self.world, collectives=not self.uniform)
+
+    def graph_capture_state(self, y):
+        """The derived objects a captured step reads (integrator._capture_state)."""
+        return (self.local.g, self.Wq, self.Wk, self.bq, self.bk, self.Wcat, self.bcat) + \
+            ((self.x0_local,) if self.add_source else ())
+
+    def capture_key_tensors(self):
+        return tuple(t for t in (self.alpha, self.beta) if isinstance(t, torch.Tensor))
 
     def __init__(self, edge_index, num_nodes, C, Wq, bq, Wk, bk, heads, norm_idx, alpha, score_mode='reference',
                  beta=None, x0_local=None, add_source=False, alpha_sigmoid=True, group=None, local=None,
@@ -760,8 +810,22 @@ class RowShardedTransformer(object):
 
     autonomous = True  # the RHS does not read t (gnpde.base_classes.ODEFunc.autonomous)
 
-    graph_capturable = False  # collectives per RHS
     fused_adaptive = False    # the adaptive solvers' wide stages run in column stripes or unsharded
+
+    @property
+    def graph_capturable(self):
+        """The state all-gather and the score collectives per RHS: captured on RCCL at a
+        world of one, or at any world with GNPDE_CAPTURE_COLLECTIVES=1."""
+        if not isinstance(self.local, _HipRowAttentionLocal):
+            return False
+        return _capturable(self.group, self.world)
+
+    def graph_capture_state(self, y):
+        lc = self.local
+        return (lc.g, lc.plan, self.Wq, self.Wk, self.bq, self.bk, self.Wcat, self.bcat) + \
+            ((self.x0_local,) if self.add_source else ())
+
+    capture_key_tensors = ColumnShardedTransformer.capture_key_tensors
 
     def __init__(self, edge_index, num_nodes, C, Wq, bq, Wk, bk, heads, norm_idx, alpha, score_mode='reference',
                  beta=None, x0_local=None, add_source=False, alpha_sigmoid=True, group=None,
