@@ -888,11 +888,14 @@ class RowShardedTransformer(object):
         return out
 
     def _gather_rows(self, v_local):
-        """Padded blocks [nb, K] of every rank -> [R, K] in global row order."""
+        """Padded blocks [nb, K] of every rank -> [R, K] in global row order (a view of
+        the gathered buffer when there is no padding to drop: a world of one)."""
         v_local = v_local.contiguous()
         pad = torch.empty((self.world * self.nb,) + tuple(v_local.shape[1:]), dtype=v_local.dtype,
                           device=v_local.device)
         self.comm.all_gather_into_tensor(pad, v_local)
+        if all(b - a == self.nb for a, b in self.blocks):
+            return pad
         return torch.cat([pad[p * self.nb:p * self.nb + (b - a)] for p, (a, b) in enumerate(self.blocks)], 0)
 
     def gather(self, y_local):
@@ -900,6 +903,8 @@ class RowShardedTransformer(object):
         return self._gather_rows(y_local)
 
     def _blockify(self, v_own):
+        if v_own.shape[0] == self.nb and v_own.is_contiguous():
+            return v_own  # a full block: sent as it is
         out = torch.zeros((self.nb,) + tuple(v_own.shape[1:]), dtype=v_own.dtype, device=v_own.device)
         out[:v_own.shape[0]] = v_own
         return out
