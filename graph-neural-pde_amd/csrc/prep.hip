@@ -26,29 +26,64 @@ int grid_of(int64_t n, int block = 256, int cap = 4096) {
 
 size_t align_up(size_t v, size_t a = 256) { return (v + a - 1) / a * a; }
 
-// flags[i] = 1 for a non-loop edge (row != col); the per-batch counts from a
-// wavefront ballot: one integer atomic per wavefront and batch element (a
-// per-edge atomicAdd on counts[b] serialised every edge on one address: 12.4 ms
-// per call at G-arxiv, round 4).  The grid-stride loop is wavefront-uniform.
+// flags[i] = 1 for a non-loop edge (row != col); the per-batch counts from
+// wavefront ballots, kept in a register while the wavefront stays in one batch
+// element and added with one integer atomic when it leaves it (and at the end), on a
+// grid of at most kFlagBlocks workgroups.  (Round 4 did one atomicAdd per edge on
+// counts[b]: 12.4 ms per call at G-arxiv; one per wavefront and step of a 4096-block
+// grid: 197 us, still one contended address.)  The grid-stride loop is wavefront-uniform.
+constexpr int kFlagBlocks = 256;
+
 __global__ void loop_flags_kernel(const int64_t* __restrict__ ei, int64_t B, int64_t E, int32_t* __restrict__ flags,
                                   unsigned long long* __restrict__ counts) {
   const int64_t n = B * E;
   const int lane = threadIdx.x & 63;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t cur = -1;             // the batch element whose count is held (wavefront-uniform)
+  unsigned long long held = 0;
   for (int64_t base = blockIdx.x * (int64_t)blockDim.x + (threadIdx.x & ~63); base < n; base += stride) {
     const int64_t i = base + lane;
     const bool valid = i < n;
-    const int64_t b = valid ? i / E : -1;
+    const int64_t b = valid ? (B == 1 ? 0 : i / E) : -1;  // (no 64-bit division for one graph)
     const int64_t e = valid ? i - b * E : 0;
     const bool keep = valid && ei[(b * 2 + 0) * E + e] != ei[(b * 2 + 1) * E + e];
     if (flags && valid) flags[i] = keep;
     // the wavefront's 64 edges span batch elements b0 <= b <= b0 + ceil(64 / E): one ballot each
-    const int64_t b0 = base / E;
-    const int64_t blast = (base + 63 < n ? base + 63 : n - 1) / E;
+    const int64_t b0 = B == 1 ? 0 : base / E;
+    const int64_t blast = B == 1 ? 0 : (base + 63 < n ? base + 63 : n - 1) / E;
     for (int64_t bb = b0; bb <= blast; ++bb) {
       const unsigned long long m = __ballot(keep && b == bb);
-      if (lane == 0 && m) atomicAdd(&counts[bb], (unsigned long long)__popcll(m));
+      if (bb != cur) {
+        if (lane == 0 && held) atomicAdd(&counts[cur], held);
+        cur = bb;
+        held = 0;
+      }
+      held += (unsigned long long)__popcll(m);
     }
+  }
+  // the workgroup's wavefronts merged in LDS first: one atomic per batch element and
+  // workgroup (usually one per workgroup) instead of one per wavefront
+  __shared__ long long wb[kBlock / 64];
+  __shared__ unsigned long long wc[kBlock / 64];
+  const int wv = threadIdx.x >> 6;
+  if (lane == 0) {
+    wb[wv] = held ? cur : -1;
+    wc[wv] = held;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    long long pb = -1;
+    unsigned long long pc = 0;
+    for (int k = 0; k < kBlock / 64; ++k) {
+      if (wb[k] < 0) continue;
+      if (wb[k] != pb) {
+        if (pc) atomicAdd(&counts[pb], pc);
+        pb = wb[k];
+        pc = 0;
+      }
+      pc += wc[k];
+    }
+    if (pc) atomicAdd(&counts[pb], pc);
   }
 }
 
@@ -89,18 +124,26 @@ __global__ void emit_loops_kernel(const int64_t* __restrict__ ei, const float* _
 }
 
 // deg[r] = sum of w over the row's edges, sequentially in COO order (perm of a
-// stable grouped CSR), then the normalisation factor of the mode.  One wavefront
-// per 64 rows: a lane sums its own row when it has at most kDegLane edges; longer
-// rows (power-law hubs: 7.4k edges at G-arxiv) are taken by the whole wavefront,
-// 64 weights gathered per load (the next chunk in flight while one is summed) and
-// added IN ORDER through readlane — the same sequential fp32 additions as a lane
-// walking the row (and as torch's CPU scatter_add_), without its 7.4k-deep chain
-// of dependent loads (1.58 ms per call at G-arxiv, round 4).
+// stable grouped CSR), then the normalisation factor of the mode.  A lane sums its
+// own row when it has at most kDegLane edges; longer rows (power-law hubs: 7.4k
+// edges at G-arxiv) are taken by a wavefront each (degree_long_kernel), 64 weights
+// gathered per load and added IN ORDER through readlane — the same sequential fp32
+// additions as a lane walking the row (and as torch's CPU scatter_add_), without its
+// 7.4k-deep chain of dependent loads (1.58 ms per call at G-arxiv, round 4).
 constexpr int kDegLane = 64;
 
 __device__ __forceinline__ float deg_weight(const float* __restrict__ w, const int32_t* __restrict__ perm, int32_t p,
                                             int32_t end) {
   return p < end ? (w ? w[perm[p]] : 1.0f) : 0.0f;
+}
+
+__device__ __forceinline__ void store_fac(float* __restrict__ fac, int64_t r, int mode, float d) {
+  if (mode == GNPDE_NORM_GCN) {
+    const float v = 1.0f / sqrtf(d);  // deg.pow_(-0.5), src/utils.py:192; inf -> 0 (:193)
+    fac[r] = isinf(v) ? 0.f : v;
+  } else {
+    fac[r] = 1.0f / d;  // deg.pow_(-1), src/utils.py:231
+  }
 }
 
 __global__ void degree_kernel(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ perm, int64_t R,
@@ -115,28 +158,37 @@ __global__ void degree_kernel(const int32_t* __restrict__ rowptr, const int32_t*
   float d = 0.f;
   if (valid && !longr)
     for (int32_t p = b; p < e; ++p) d += w ? w[perm[p]] : 1.0f;
-  unsigned long long lm = __ballot(longr);
-  while (lm) {  // wavefront-uniform
-    const int j = __ffsll((long long)lm) - 1;
-    lm &= lm - 1;
-    const int32_t bb = __builtin_amdgcn_readlane(b, j), ee = __builtin_amdgcn_readlane(e, j);
-    float acc = 0.f;
-    float v = deg_weight(w, perm, bb + lane, ee);
-    for (int32_t p0 = bb; p0 < ee; p0 += 64) {
-      const float nv = deg_weight(w, perm, p0 + 64 + lane, ee);  // the next chunk, in flight
-      const int cnt = ee - p0 < 64 ? ee - p0 : 64;
+  if (!valid || longr) return;  // long rows: degree_long_kernel
+  store_fac(fac, r, mode, d);
+}
+
+// The rows longer than kDegLane edges, one wavefront per row (in one wavefront the
+// hub rows of a 64-row block — RMAT puts them together at low ids — were summed one
+// after another: 1.56 ms per call at G-arxiv).  The wave's 64 weights per load are
+// added in order through readlane (the sequential sum), the next chunk in flight.
+__global__ void degree_long_kernel(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ perm, int64_t R,
+                                   const float* __restrict__ w, int mode, float* __restrict__ fac) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+  if (r >= R) return;
+  const int32_t bb = rowptr[r], ee = rowptr[r + 1];
+  if (ee - bb <= kDegLane) return;  // wavefront-uniform: degree_kernel's lanes took it
+  float acc = 0.f;
+  float v = deg_weight(w, perm, bb + lane, ee);
+  for (int32_t p0 = bb; p0 < ee; p0 += 64) {
+    const float nv = deg_weight(w, perm, p0 + 64 + lane, ee);  // the next chunk, in flight
+    const int cnt = ee - p0 < 64 ? ee - p0 : 64;
+    if (cnt == 64) {
+      // whole chunks: constant lane indices, no loop counter between the dependent adds
+      // (a counted readlane loop cost ~120 cycles per edge: 370 us for G-arxiv's hubs)
+#pragma unroll
+      for (int k = 0; k < 64; ++k) acc += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), k));
+    } else {
       for (int k = 0; k < cnt; ++k) acc += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), k));
-      v = nv;
     }
-    if (lane == j) d = acc;
+    v = nv;
   }
-  if (!valid) return;
-  if (mode == GNPDE_NORM_GCN) {
-    float v = 1.0f / sqrtf(d);  // deg.pow_(-0.5), src/utils.py:192; inf -> 0 (:193)
-    fac[r] = isinf(v) ? 0.f : v;
-  } else {
-    fac[r] = 1.0f / d;  // deg.pow_(-1), src/utils.py:231
-  }
+  if (lane == 0) store_fac(fac, r, mode, acc);
 }
 
 __global__ void scale_kernel(const int64_t* __restrict__ ei, const float* __restrict__ w, int64_t B, int64_t E,
@@ -184,7 +236,7 @@ int gnpde_self_loops_count(const int64_t* edge_index, int64_t B, int64_t E, int6
   GNPDE_HIP(hipMemsetAsync(counts, 0, sizeof(unsigned long long) * B, s));
   if (B * E > 0) {
     GNPDE_REQUIRE(edge_index != nullptr, GNPDE_EINVAL, "self_loops_count: NULL edge_index");
-    loop_flags_kernel<<<grid_of(B * E), 256, 0, s>>>(edge_index, B, E, nullptr, counts);
+    loop_flags_kernel<<<grid_of(B * E, 256, kFlagBlocks), 256, 0, s>>>(edge_index, B, E, nullptr, counts);
     GNPDE_LAUNCH_CHECK();
   }
   GNPDE_HIP(hipMemcpyAsync(nonloop, counts, sizeof(unsigned long long) * B, hipMemcpyDeviceToHost, s));
@@ -215,7 +267,7 @@ int gnpde_add_self_loops(const int64_t* edge_index, const float* w, int64_t B, i
   GNPDE_HIP(hipMemsetAsync(counts, 0, sizeof(unsigned long long) * B, s));
   if (B * E > 0) {
     GNPDE_REQUIRE(edge_index != nullptr, GNPDE_EINVAL, "add_self_loops: NULL edge_index");
-    loop_flags_kernel<<<grid_of(B * E), 256, 0, s>>>(edge_index, B, E, flags, counts);
+    loop_flags_kernel<<<grid_of(B * E, 256, kFlagBlocks), 256, 0, s>>>(edge_index, B, E, flags, counts);
     GNPDE_LAUNCH_CHECK();
     last_loop_kernel<<<grid_of(B * E), 256, 0, s>>>(edge_index, B, E, N, last);
     GNPDE_LAUNCH_CHECK();
@@ -237,6 +289,9 @@ int gnpde_norm_weights_f32(const int64_t* edge_index, const float* w, int64_t B,
                 "norm_weights: NULL pointer");
   hipStream_t s = as_stream(stream);
   degree_kernel<<<(unsigned)ceil_div(B * N, 256), 256, 0, s>>>(rowptr, perm, B * N, w, mode, fac);
+  GNPDE_LAUNCH_CHECK();
+  degree_long_kernel<<<(unsigned)ceil_div(B * N, (int64_t)kWavesPerBlock), 256, 0, s>>>(rowptr, perm, B * N, w, mode,
+                                                                                        fac);
   GNPDE_LAUNCH_CHECK();
   if (B * E > 0) {
     scale_kernel<<<grid_of(B * E), 256, 0, s>>>(edge_index, w, B, E, N, mode, fac, w_out);

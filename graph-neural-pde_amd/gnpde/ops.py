@@ -379,11 +379,12 @@ class GraphCSR(object):
 
     @property
     def indeg(self):
+        """In-degree per row: the CSC's row lengths (the reference scores' key sum is
+        the only reader and runs with the CSC's statistics; a per-edge atomic count
+        contends on the hub columns: 0.3-1.9 ms per graph)."""
         if self._indeg is None:
-            deg = torch.empty(self.R, dtype=torch.int32, device=self.edge_index.device)
-            _lib.call("gnpde_indegree_i32", _ptr(self.csr.col), self.nnz, self.R, _ptr(deg),
-                      _stream(deg.device))
-            self._indeg = deg
+            rp = self.csc.rowptr
+            self._indeg = (rp[1:] - rp[:-1]).to(torch.int32).contiguous()
         return self._indeg
 
     def gather_weights(self, w, transpose=False, out=None):
