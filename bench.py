@@ -824,7 +824,10 @@ def bench_dopri5(ei, w, x, dev, k1_stage_ms, k1_plain_ms, reps=3):
     ms_step = el * 1e3 / max(steps, 1)
     r, wr = plan.state_passes()
     affine = bool(getattr(func, 'affine', False)) and integ.AFFINE_STAGE
-    if affine:  # no first stage-input pass (y0 and k0 read, X0 written): launch 0 reads k0 as its input
+    krylov = affine and integ.KRYLOV_STEP
+    if krylov:  # the Krylov step (integrator._KrylovPlan): only the last launch reads / writes more
+        r, wr = integ._KrylovPlan(plan).state_passes()
+    elif affine:  # no first stage-input pass (y0 and k0 read, X0 written): launch 0 reads k0 as its input
         r, wr = r - 2, wr - 1
     # device time of one step: a captured step (6 RHS launches, the error reduction and the device
     # controller) replayed back to back between HIP events on the launch stream
@@ -849,8 +852,10 @@ def bench_dopri5(ei, w, x, dev, k1_stage_ms, k1_plain_ms, reps=3):
     rl = None
     if dev_ms:
         t = dev_ms * 1e-3
-        rl = {"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s", "kernel": "one replayed dopri5 step (2 STG1 + 4 "
-              "STG4 agg_kernel launches, sum_partial_kernel, adaptive_control_kernel)", "step_ms": round(dev_ms, 4),
+        kern = ("5 STG1 + 1 STG4 agg_kernel launches (Krylov step)" if krylov else
+                "2 STG1 + 4 STG4 agg_kernel launches")
+        rl = {"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s", "kernel": "one replayed dopri5 step (%s, "
+              "sum_partial_kernel, adaptive_control_kernel)" % kern, "step_ms": round(dev_ms, 4),
               "algorithmic_bytes_per_step": int(alg), "algorithmic_frac": round(alg / t / 1e9 / HBM_PEAK_GBS, 4)}
         if tb:
             rl.update({"traffic": int(tb), "achieved": round(tb / t / 1e9, 1),
@@ -869,11 +874,12 @@ def bench_dopri5(ei, w, x, dev, k1_stage_ms, k1_plain_ms, reps=3):
         "step_ms_device": round(dev_ms, 4) if dev_ms else None,
         "state_passes_per_step": {"reads": r, "writes": wr},
         "affine_first_stage": affine,
+        "krylov_step": krylov,
         "roofline": rl,
         "basis": "ms_per_step = whole solve (entry copy, initial-step selection, steps, dense output) / steps; "
-                 "per step: 6 RHS launches carrying the stage combinations and the error rows (the first stage's "
-                 "input never formed: f affine) + the error reduction with the device step-size controller, one "
-                 "host read; rhs_stage_ms = the rk4 fused-stage K1 launch time"}
+                 "per step: 6 RHS launches (Krylov step, f affine: u_{p+1} = dt L u_p, the last launch forming y1, "
+                 "f1 and the error rows from u_0..u_5) + the error reduction with the device step-size "
+                 "controller, one host read; rhs_stage_ms = the rk4 fused-stage K1 launch time"}
     progress("dopri5 G-arxiv: %.3f ms/step, %d steps" % (ms_step, steps))
     # configs[1] shape
     N, E, Cc, h, att = 2708, 13264, 80, 8, 128  # Cora: 10,556 edges + 2,708 self loops

@@ -398,7 +398,13 @@ __device__ __forceinline__ void wide_slots(const gnpde_stage_epilogue_t& st, con
   }
 #pragma unroll
   for (int j = 0; j < NKMAX; ++j) w.p[NOUT + (ERR ? 1 : 0) + j] = (j < st.nk && st.k[j] != xid) ? st.k[j] : nullptr;
-  if constexpr (ERR) w.p[WideSlots<NOUT, NKMAX, ERR>::N - 1] = has_err ? st.err_y0 : nullptr;
+  if constexpr (ERR) {
+    // the tolerance's y0: not loaded again when it is a loaded output base (wide_combine copies it)
+    bool dup = false;
+#pragma unroll
+    for (int i = 0; i < NOUT; ++i) dup = dup || (w.p[i] != nullptr && w.p[i] == st.err_y0);
+    w.p[WideSlots<NOUT, NKMAX, ERR>::N - 1] = (has_err && !dup) ? st.err_y0 : nullptr;
+  }
 }
 
 // fp32 values -> a row slice in storage form (bf16: round to nearest even); for an
@@ -586,6 +592,11 @@ __device__ __forceinline__ float stage_scale(const gnpde_stage_epilogue_t& st) {
   return st.coef_scale ? *st.coef_scale : 1.f;
 }
 
+// output i's coefficient scale: sc, or 1 when its bit in unscaled_outs is set (ABI 6)
+__device__ __forceinline__ float out_scale(const gnpde_stage_epilogue_t& st, int i, float sc) {
+  return (st.unscaled_outs >> i) & 1 ? 1.f : sc;
+}
+
 // The wide stage epilogue of one row slice (STG 4; also gnpde_stage_apply_*):
 // every output and the error combination start from cb*base (x when the base is
 // the RHS input xid, with values xv), take sc*c[j]*k[j] for j ascending, then
@@ -598,6 +609,9 @@ __device__ __forceinline__ void wide_combine(const gnpde_stage_epilogue_t& st, i
                                              float (&ev)[VEC], Packed<VEC, T>* y0v = nullptr,
                                              const Packed<VEC, T>* pre = nullptr) {
   const float sc = stage_scale(st);
+  float sco[NOUT];  // the outputs' coefficient scales (the error term's is sc)
+#pragma unroll
+  for (int i = 0; i < NOUT; ++i) sco[i] = out_scale(st, i, sc);
   if (GNPDE_WIDE_BATCH && (GNPDE_WIDE_NOFB || rows_fit_buffer<VEC, T>(off))) {
     const bool has_err = ERR && st.err_rows != nullptr;
     using WS = WideSlots<NOUT, NKMAX, ERR>;
@@ -634,6 +648,7 @@ __device__ __forceinline__ void wide_combine(const gnpde_stage_epilogue_t& st, i
         const bool isx = xid != nullptr && slot < st.n_out && st.o[slot].base == xid;
 #pragma unroll
         for (int t = 0; t < VEC; ++t) r[slot][t] = cb[slot] * (isx ? xv[t] : unpack(vq, t));
+        if (ERR && y0v && has_err && w.p[q] != nullptr && w.p[q] == st.err_y0) *y0v = vq;  // y0 = this base
       } else if (slot < NOUT + NKMAX) {
         const int j = slot - NOUT;
         const bool on = j < st.nk;
@@ -643,7 +658,7 @@ __device__ __forceinline__ void wide_combine(const gnpde_stage_epilogue_t& st, i
         for (int t = 0; t < VEC; ++t) kv[t] = kx ? xv[t] : unpack(vq, t);
 #pragma unroll
         for (int i = 0; i < NOUT; ++i) {
-          const float c = (on && i < st.n_out) ? st.o[i].c[j] * sc : 0.f;
+          const float c = (on && i < st.n_out) ? st.o[i].c[j] * sco[i] : 0.f;
 #pragma unroll
           for (int t = 0; t < VEC; ++t) r[i][t] = fmaf(c, kv[t], r[i][t]);
         }
@@ -658,13 +673,13 @@ __device__ __forceinline__ void wide_combine(const gnpde_stage_epilogue_t& st, i
 #pragma unroll
           for (int t = 0; t < VEC; ++t) ev[t] = cb[NOUT] * (isx ? xv[t] : unpack(vq, t));
         }
-      } else if (y0v) {
+      } else if (y0v && w.p[q] != nullptr) {  // (NULL: deduplicated against a base, copied above)
         *y0v = vq;
       }
     }
 #pragma unroll
     for (int i = 0; i < NOUT; ++i) {
-      const float cf = i < st.n_out ? st.o[i].cf * sc : 0.f;
+      const float cf = i < st.n_out ? st.o[i].cf * sco[i] : 0.f;
 #pragma unroll
       for (int t = 0; t < VEC; ++t) r[i][t] = fmaf(cf, o[t], r[i][t]);
     }
@@ -690,6 +705,7 @@ __device__ __forceinline__ void wide_combine(const gnpde_stage_epilogue_t& st, i
     }
   };
   const bool has_err = ERR && st.err_rows != nullptr;
+  if (y0v && has_err) load_packed<VEC>(as_t<T>(st.err_y0) + off, *y0v);  // err_terms reads it from y0v
 #pragma unroll
   for (int i = 0; i < NOUT; ++i)
     if (i < st.n_out) base_term(st.o[i], r[i]);
@@ -708,7 +724,7 @@ __device__ __forceinline__ void wide_combine(const gnpde_stage_epilogue_t& st, i
 #pragma unroll
       for (int i = 0; i < NOUT; ++i) {
         if (i < st.n_out) {
-          const float c = st.o[i].c[j] * sc;
+          const float c = st.o[i].c[j] * sco[i];
 #pragma unroll
           for (int t = 0; t < VEC; ++t) r[i][t] = fmaf(c, unpack(kv, t), r[i][t]);
         }
@@ -723,7 +739,7 @@ __device__ __forceinline__ void wide_combine(const gnpde_stage_epilogue_t& st, i
 #pragma unroll
   for (int i = 0; i < NOUT; ++i) {
     if (i < st.n_out) {
-      const float cf = st.o[i].cf * sc;
+      const float cf = st.o[i].cf * sco[i];
 #pragma unroll
       for (int t = 0; t < VEC; ++t) r[i][t] = fmaf(cf, o[t], r[i][t]);
     }
@@ -843,7 +859,7 @@ __device__ __forceinline__ void epi_finish(const Epi& e, int64_t row, int cc, co
       for (int i = 0; i < stage_nout<STG>(); ++i) {
         if (i >= e.st.n_out) break;
         float r[VEC];
-        stage_combine<VEC, NK, T>(e, e.st.o[i], off, o, p.xr, &p.base[i], kval, sc, r);
+        stage_combine<VEC, NK, T>(e, e.st.o[i], off, o, p.xr, &p.base[i], kval, out_scale(e.st, i, sc), r);
         store_vec<VEC>(as_t<T>(e.st.o[i].out) + oo, r);
       }
     }

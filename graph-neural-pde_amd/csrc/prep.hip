@@ -131,6 +131,8 @@ __global__ void emit_loops_kernel(const int64_t* __restrict__ ei, const float* _
 // additions as a lane walking the row (and as torch's CPU scatter_add_), without its
 // 7.4k-deep chain of dependent loads (1.58 ms per call at G-arxiv, round 4).
 constexpr int kDegLane = 64;
+constexpr int kDegUnroll = 64;
+constexpr int kDegBatch = 8;
 
 __device__ __forceinline__ float deg_weight(const float* __restrict__ w, const int32_t* __restrict__ perm, int32_t p,
                                             int32_t end) {
@@ -155,10 +157,25 @@ __global__ void degree_kernel(const int32_t* __restrict__ rowptr, const int32_t*
   const bool valid = r < R;
   const int32_t b = valid ? rowptr[r] : 0, e = valid ? rowptr[r + 1] : 0;
   const bool longr = e - b > kDegLane;
-  float d = 0.f;
-  if (valid && !longr)
-    for (int32_t p = b; p < e; ++p) d += w ? w[perm[p]] : 1.0f;
   if (!valid || longr) return;  // long rows: degree_long_kernel
+  float d = 0.f;
+  if (!w) {
+    d = (float)(e - b);  // unit weights: the in-order sum of at most 64 ones
+  } else {
+    // kDegBatch positions' perm entries, then their weights, in flight at once; the adds
+    // stay in COO order (the chain of dependent loads was the cost: 32 us at G-arxiv)
+    for (int32_t p0 = b; p0 < e; p0 += kDegBatch) {
+      int32_t q[kDegBatch];
+#pragma unroll
+      for (int k = 0; k < kDegBatch; ++k) q[k] = p0 + k < e ? perm[p0 + k] : -1;
+      float v[kDegBatch];
+#pragma unroll
+      for (int k = 0; k < kDegBatch; ++k) v[k] = q[k] >= 0 ? w[q[k]] : 0.f;
+#pragma unroll
+      for (int k = 0; k < kDegBatch; ++k)
+        if (p0 + k < e) d += v[k];
+    }
+  }
   store_fac(fac, r, mode, d);
 }
 
@@ -173,6 +190,39 @@ __global__ void degree_long_kernel(const int32_t* __restrict__ rowptr, const int
   if (r >= R) return;
   const int32_t bb = rowptr[r], ee = rowptr[r + 1];
   if (ee - bb <= kDegLane) return;  // wavefront-uniform: degree_kernel's lanes took it
+  // Integral weights whose |w| sum stays below 2^24 (unit weights: any row shorter than
+  // 2^24): every partial sum in ANY order is an exactly representable integer, so lane-
+  // strided sums and a tree give the sequential sum's bits.  kDegUnroll loads per lane in
+  // flight (perm, then the weights); the fp32 sum of |w| is monotone in its addends, so
+  // it reaches 2^24 exactly when the true sum does.
+  {
+    float s = 0.f, a = 0.f;
+    bool ok = true;
+    for (int32_t p0 = bb; p0 < ee; p0 += 64 * kDegUnroll) {
+      int32_t q[kDegUnroll];
+#pragma unroll
+      for (int k = 0; k < kDegUnroll; ++k) {
+        const int32_t p = p0 + k * 64 + lane;
+        q[k] = p < ee ? (w ? perm[p] : 0) : -1;
+      }
+#pragma unroll
+      for (int k = 0; k < kDegUnroll; ++k) {
+        const float v = q[k] < 0 ? 0.f : (w ? w[q[k]] : 1.0f);
+        s += v;
+        a += fabsf(v);
+        ok = ok && v == rintf(v);
+      }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      s += __shfl_xor(s, off);
+      a += __shfl_xor(a, off);
+    }
+    if (__ballot(!ok) == 0 && a < 16777216.0f) {  // wavefront-uniform (a is lane-equal after the tree)
+      if (lane == 0) store_fac(fac, r, mode, s);
+      return;
+    }
+  }
   float acc = 0.f;
   float v = deg_weight(w, perm, bb + lane, ee);
   for (int32_t p0 = bb; p0 < ee; p0 += 64) {

@@ -137,7 +137,7 @@ __global__ __launch_bounds__(256) void rows_copy_kernel(const uint4* __restrict_
 // the row's lanes by the same xor tree.
 // NKMAX / NOUT / ERR: the operands, outputs and error term an instantiation holds
 // registers for (the plain combinations of the adaptive step — its first stage input,
-// the dense output — take the light one: more waves, more bytes in flight).
+// the dense output — take the lighter ones: more waves, more bytes in flight).
 template <int VEC, int GL, class T, int NKMAX, int NOUT, bool ERR>
 __global__ __launch_bounds__(256) void stage_apply_kernel(int64_t R, int C, int64_t ld, const T* __restrict__ f,
                                                            const T* __restrict__ x, gnpde_stage_epilogue_t st) {
@@ -306,9 +306,12 @@ static int launch_stage_apply(int64_t R, int C, int64_t ld, const T* f, const T*
   const int64_t waves = [&](int rpw) { return ceil_div(R, (int64_t)rpw); }(lanes <= 16 ? 4 : (lanes <= 32 ? 2 : 1));
   const unsigned grid = (unsigned)std::max<int64_t>(1, ceil_div(waves, kWavesPerBlock));
   const bool light = !st.err_rows && st.n_out <= 1 && st.nk <= 2;
+  const bool one_out = !st.err_rows && st.n_out <= 1;  // the dense output over many operands
 #define GNPDE_SA(GL)                                                                                  \
   if (light)                                                                                          \
     stage_apply_kernel<VEC, GL, T, 2, 1, false><<<grid, kBlock, 0, s>>>(R, C, ld, f, x, st);          \
+  else if (one_out)                                                                                   \
+    stage_apply_kernel<VEC, GL, T, GNPDE_STAGE_MAX_K, 1, false><<<grid, kBlock, 0, s>>>(R, C, ld, f, x, st); \
   else                                                                                                \
     stage_apply_kernel<VEC, GL, T, GNPDE_STAGE_MAX_K, 2, true><<<grid, kBlock, 0, s>>>(R, C, ld, f, x, st)
   if (lanes <= 16) {

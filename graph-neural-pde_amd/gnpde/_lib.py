@@ -32,7 +32,7 @@ class StageEpilogue(ctypes.Structure):
                 ("dot_coef", ctypes.c_double), ("dot_accumulate", ctypes.c_int),
                 ("err_rows", ctypes.c_void_p), ("err", StageOut), ("err_y0", ctypes.c_void_p), ("err_y1", ctypes.c_int),
                 ("atol", ctypes.c_double), ("rtol", ctypes.c_double), ("coef_scale", ctypes.c_void_p),
-                ("f_lin", ctypes.c_float)]
+                ("f_lin", ctypes.c_float), ("unscaled_outs", ctypes.c_int)]
 
 
 c_i32p = ctypes.POINTER(ctypes.c_int32)
@@ -125,7 +125,7 @@ SIGNATURES = {
 }
 
 # constants mirrored from include/gnpde.h
-ABI_VERSION = 5
+ABI_VERSION = 6
 OK = 0
 EINVAL = -1
 EHIP = -2

@@ -1179,6 +1179,66 @@ def _adaptive_plan(method):
     return p
 
 
+class _KrylovPlan(object):
+    """The step of an FSAL tableau for an affine RHS f(y) = L y + s in the Krylov basis
+    u_p = (dt L)^p f0 (u_0 = f0 = f(y0)).  Every stage derivative is a fixed
+    combination of them: k_0 = u_0, k_{i+1} = f(y0 + dt sum_j beta[i][j] k_j)
+    = k_0 + sum_j beta[i][j] (dt L) k_j, so k_i = sum_p B[i][p] u_p with
+    B[i+1][p] = sum_j beta[i][j] B[j][p-1].  A step is ns launches of the linear part,
+    u_{p+1} = dt L u_p, each reading only its own input (no stage operand); the last
+    (over u_{ns-1}, with f_lin = 1: f' = u_{ns-1} + u_ns) forms
+      y1  = y0 + dt sum_p G[p] u_p,                 G[p]   = sum_j c_sol[j] B[j][p]
+      f1  = sum_p B[ns][p] u_p                      (the next step's f0: unscaled)
+      e   = dt sum_p Eps[p] u_p,                    Eps[p] = sum_j c_err[j] B[j][p]
+    with u_ns = f' - u_{ns-1} substituted.  Mathematically the tableau's step; Eps[p]
+    vanishes exactly for p below the embedded order (the order conditions of the
+    linear problem), which the fp64 sums leave at rounding level and the plan zeroes,
+    so the error estimate carries no stage-combination cancellation noise.  Dense
+    output: y_mid = y0 + dt (sum_p Mu[p] u_p + c_mid[ns] f1), Mu[p] = sum_{j<ns}
+    c_mid[j] B[j][p], with y1 restated on the u_p (one pass over ns + 2 rows)."""
+
+    def __init__(self, plan):
+        ns, beta = plan.ns, plan.beta
+        B = [[1.0]]
+        for i in range(ns):
+            B.append([1.0] + [sum(beta[i][j] * B[j][p - 1] for j in range(p - 1, i + 1))
+                              for p in range(1, i + 2)])
+        self.B = B
+
+        def comb(c, upto):
+            v = [sum(c[j] * B[j][p] for j in range(p, upto)) for p in range(ns + 1)]
+            big = max(1.0, max(abs(x) for x in v))
+            return [0.0 if abs(x) < 1e-12 * big else x for x in v]
+        self.G = comb(plan.c_sol, ns + 1)
+        self.Eps = comb(plan.c_err, ns + 1)
+        self.Mu = comb(plan.c_mid, ns)
+        self.Bn = list(B[ns])
+        self.ns = ns
+
+    def last_launch_terms(self):
+        """(y1 terms, (f1 terms, f1 cf), (error terms, error cf)) of the last launch over
+        u_{ns-1}, as [(p, coefficient)] with u_ns = f' - u_{ns-1} substituted."""
+        ns = self.ns
+
+        def sub(v):
+            t = [(p, v[p]) for p in range(ns - 1) if v[p] != 0.0]
+            c = v[ns - 1] - v[ns]
+            if c != 0.0:
+                t.append((ns - 1, c))
+            return t, v[ns]
+        y1 = [(p, self.G[p]) for p in range(ns) if self.G[p] != 0.0]
+        return y1, sub(self.Bn), sub(self.Eps)
+
+    def state_passes(self):
+        """Full-state reads / writes per step beyond each launch's gathers, input row
+        and one output: the last launch reads y0 (the y1 base and the tolerance) and
+        u_0 .. u_{ns-2}, and writes a second output (f1)."""
+        return self.ns, 1
+
+
+KRYLOV_STEP = os.environ.get('GNPDE_KRYLOV_STEP', '1') != '0'
+
+
 def _fused_adaptive_ok(func, y0, combine, options):
     """The fused adaptive step applies: a gnpde RHS (rhs_stage) without autograd, a
     device state (or a host-stage test RHS on CPU), torchdiffeq's RMS norm (or a
@@ -1258,6 +1318,13 @@ class _RKAdaptiveFused(_RKAdaptive):
         # pairs (dopri5, bosh3); torchdiffeq's non-FSAL pairs carry k0 = the last stage of the previous
         # step instead.  GNPDE_AFFINE_STAGE=0 disables it.
         self.affine = bool(getattr(func, 'affine', False)) and AFFINE_STAGE and self.plan.fsal
+        # the affine step in the Krylov basis (_KrylovPlan): ns launches, no stage operands
+        # before the last; its u_1 .. u_{ns-1} live in the K1 .. K{ns-1} buffers
+        P = self.plan
+        self.krylov = None
+        if self.affine and KRYLOV_STEP and P.ns <= _lib.STAGE_MAX_K and \
+                set(range(1, P.ns + 1)) <= (P.store | P.store_mid):
+            self.krylov = _KrylovPlan(P)
         sc = self._scalars
         self.safety_f, self.ifactor_f, self.dfactor_f = float(sc['safety']), float(sc['ifactor']), float(sc['dfactor'])
 
@@ -1332,17 +1399,38 @@ class _RKAdaptiveFused(_RKAdaptive):
         the device error sum."""
         P = self.plan
         bufs = st.bufs
-        if not self.affine:  # the first stage input X0 = y0 + dt b00 k0 (the affine mode never forms it)
-            self._apply(ops.Stage(outs=[(bufs['X0'], bufs['Y'], 1.0, 0.0, [(bufs['K0'], P.beta[0][0])])],
-                                  scale=st.scale), None, None, bufs['Y'])
-        for i in range(P.ns):
-            ti = t_cur + dt if P.alpha[i] == 1. else t_cur + P.alpha[i] * dt
-            self._launch(i, st, bufs['X%d' % i], ti, mid)
+        if self.krylov is not None:
+            self._krylov_launches(st, t_cur)
+        else:
+            if not self.affine:  # the first stage input X0 = y0 + dt b00 k0 (the affine mode never forms it)
+                self._apply(ops.Stage(outs=[(bufs['X0'], bufs['Y'], 1.0, 0.0, [(bufs['K0'], P.beta[0][0])])],
+                                      scale=st.scale), None, None, bufs['Y'])
+            for i in range(P.ns):
+                ti = t_cur + dt if P.alpha[i] == 1. else t_cur + P.alpha[i] * dt
+                self._launch(i, st, bufs['X%d' % i], ti, mid)
         if self._dev_control():  # the error sum and the controller: two launches, no host work
             ops.adaptive_control(st.rows, st.rows.numel() * self.C, self.order, self.safety_f, self.ifactor_f,
                                  self.dfactor_f, st.dt, st.scale, st.rec, ws=st.ws)
             return st.rec
         return self._err_sum(st.rows)
+
+    def _krylov_launches(self, st, t):
+        """The launches of one affine step in the Krylov basis (_KrylovPlan): u_{p+1} =
+        dt L u_p into K{p+1} for p < ns - 1, then the launch over u_{ns-1} that writes y1,
+        f1 (K{ns}) and the error rows.  The RHS is autonomous: every launch at t."""
+        K = self.krylov
+        ns = K.ns
+        bufs = st.bufs
+        u = [bufs['K0']] + [bufs['K%d' % p] for p in range(1, ns)]
+        for p in range(ns - 1):
+            self.func.rhs_stage(t, u[p], ops.Stage(outs=[(u[p + 1], None, 0.0, 1.0, [])], scale=st.scale),
+                                linear=True)
+        y1t, (ft, fcf), (et, ecf) = K.last_launch_terms()
+        outs = [(bufs['Y1'], bufs['Y'], 1.0, 0.0, [(u[p], c) for p, c in y1t]),
+                (bufs['K%d' % ns], None, 0.0, fcf, [(u[p], c) for p, c in ft])]
+        err = (st.rows, (None, 0.0, ecf, [(u[p], c) for p, c in et]), bufs['Y'], 0, self.atol_f, self.rtol_f)
+        self.func.rhs_stage(t, u[ns - 1], ops.Stage(outs=outs, err=err, scale=st.scale, f_lin=1.0, unscaled=(1,)),
+                            linear=True)
 
     def _dev_control(self):
         """The step-size controller runs on the device (a device solve with the
@@ -1410,7 +1498,7 @@ class _RKAdaptiveFused(_RKAdaptive):
                 'norm' in self.options:  # a sharded RHS's global norm: a collective inside the step
             return _AdaptiveState(P, y0, self.host), False
         state = _capture_state(self.func, y0)
-        key = _graph_cache_key(self.func, 'adaptive:' + P.method, y0, state)
+        key = _graph_cache_key(self.func, 'adaptive:' + P.method + (':krylov' if self.krylov is not None else ''), y0, state)
         if key is None:
             return _AdaptiveState(P, y0, self.host), False
         key = key + (self.atol_f, self.rtol_f, torch.cuda.current_stream(y0.device).cuda_stream,
@@ -1611,6 +1699,21 @@ class _RKAdaptiveFused(_RKAdaptive):
         cf0 = dt * (x - 4.0 * x2 + 5.0 * x3 - 2.0 * x4)
         cf1 = dt * (x2 - 3.0 * x3 + 2.0 * x4)
         rows = None if (lay is None or self.host) else lay.order32
+        K = self.krylov
+        if K is not None:
+            # y1 and y_mid restated on the u_p (K0 .. K{ns-1}): one pass over y0, the u_p and f1
+            terms = []
+            for p in range(P.ns):
+                c = cy1 * dt * K.G[p] + cym * dt * K.Mu[p] + (cf0 if p == 0 else 0.0)
+                if c != 0.0:
+                    terms.append((d['K%d' % p], c))
+            stage = ops.Stage(outs=[(out, y_prev, cy0 + cy1 + cym, cym * dt * P.c_mid[P.ns] + cf1, terms)],
+                              out_rows=rows)
+            if self.host:
+                self.func.host_stage_apply(stage, f1, y_prev, y_prev)
+            else:
+                ops.stage_apply(stage, f1, y_prev, y_prev)
+            return
         # one pass: out = (cy0 + cym) y0 + cy1 y1 + sum_j cym dt c_mid[j] k_j + cf0 f0 + cf1 f1
         coef = {}  # id -> [tensor, coefficient] of the operands besides y0 (base) and f1 (f input)
         order_ = []

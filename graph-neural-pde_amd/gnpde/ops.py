@@ -582,8 +582,11 @@ class Stage(object):
     in fp64 with e the combination, tol = atol + rtol * max(|y0|, |y1|), y1 = the
     RHS input (y1_out = -1) or output ``y1_out``."""
 
-    def __init__(self, f_out=None, outs=(), out_rows=None, dot=None, err=None, scale=None, f_lin=0.0):
+    def __init__(self, f_out=None, outs=(), out_rows=None, dot=None, err=None, scale=None, f_lin=0.0,
+                 unscaled=()):
         self.f_out = f_out
+        # indices of the outputs whose cf / c_j do NOT take ``scale`` (ABI 6 unscaled_outs)
+        self.unscaled = tuple(unscaled)
         # nonzero: the RHS value becomes x + scale*f_lin*f (the affine stage derivative, ABI 5)
         self.f_lin = float(f_lin)
         # a device fp32 0-d tensor multiplying every cf and c_j (not cb): the adaptive step size
@@ -685,6 +688,7 @@ class Stage(object):
             _require_gpu(self.scale, "coefficient scale", torch.float32)
             st.coef_scale = self.scale.data_ptr()
         st.f_lin = self.f_lin
+        st.unscaled_outs = sum(1 << i for i in self.unscaled)
         return st
 
 

@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define GNPDE_ABI_VERSION 5
+#define GNPDE_ABI_VERSION 6
 
 #define GNPDE_OK 0
 #define GNPDE_EINVAL (-1)
@@ -209,6 +209,10 @@ size_t gnpde_plan_workspace_bytes(int64_t R);
  * evaluated on the input k WITHOUT the source term (flags: no GNPDE_ADD_SOURCE),
  * f(y0 + h k) = k + h L k with k = f(y0) — an adaptive step's first stage derivative
  * without materialising its stage input y0 + h k (gnpde.integrator, ABI 5).
+ * unscaled_outs (0 = none; ABI 6): bit i set — output i takes its cf and c[j]
+ * WITHOUT coef_scale (the error term always takes it): a combination whose
+ * operands already carry the step size, e.g. the next step's f0 = sum_p B[p] u_p
+ * of the affine Krylov step (u_p = (h L)^p f0, gnpde.integrator).
  * A k operand (or base) equal to the RHS input x reuses the row already read.
  * At most 2 k operands with dot_rows; err_rows and 3..6 operands take the wide
  * epilogue (operands loaded after the aggregation), fused into the plain-weight
@@ -243,6 +247,7 @@ typedef struct {
   double rtol;
   const float* coef_scale;
   float f_lin;
+  int unscaled_outs;
 } gnpde_stage_epilogue_t;
 
 /* The stage epilogue as a pass of its own, over rows [0, R) of C columns

@@ -24,8 +24,9 @@ def apply_stage(stage, f, x):
     if stage.f_out is not None:
         stage.f_out.copy_(f)
     vals = []
-    for out, base, cb, cf, terms in stage.outs:
-        v = _combo(base, cb, cf, terms, f, sc)
+    unscaled = getattr(stage, 'unscaled', ())
+    for i, (out, base, cb, cf, terms) in enumerate(stage.outs):
+        v = _combo(base, cb, cf, terms, f, 1.0 if i in unscaled else sc)
         vals.append(v)
         out.copy_(v)
     if stage.err is not None:

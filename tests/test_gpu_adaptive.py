@@ -163,6 +163,41 @@ def test_stage_apply_vs_torch(dtype, C):
     assert X.shape == F.shape
 
 
+@pytest.mark.parametrize("fused", [False, True])
+def test_unscaled_output_with_coefficient_scale(fused):
+    """ABI 6 unscaled_outs: output 1 takes its cf / c_j without the device scale while
+    output 0 and the error term take it; the tolerance's y0 is output 1's base (loaded
+    once, shared).  Through the stage pass and the fused wide epilogue (K1, f_lin = 1
+    as the Krylov step's last launch), against torch."""
+    N, E, C = 3000, 30000, 64
+    eo, wo, rng = _graph(N, E, 34)
+    gen = torch.Generator(device=DEV)
+    gen.manual_seed(9)
+    st, ks, x, y0 = _random_stage(N, C, torch.float32, gen, err_y1=0)
+    sc = torch.tensor(0.37, device=DEV)
+    st.scale, st.unscaled = sc, (1,)
+    if fused:
+        g = ops.GraphCSR(T(eo), N)
+        w = g.gather_weights(T(wo.astype(np.float32)))
+        a = torch.tensor(0.2, device=DEV)
+        st.f_lin = 1.0
+        ops.spmm_rhs(g, w, x, alpha=a, stage=st)
+        F = x + 0.37 * ops.spmm_rhs(g, w, x, alpha=a).view(N, C)  # f' = x + sc f_lin f
+    else:
+        f = torch.randn(N, C, generator=gen, device=DEV)
+        ops.stage_apply(st, f, x, x)
+        F = f
+    vals = []
+    for i, (out, base, cb, cf, terms) in enumerate(st.outs):
+        s_ = 1.0 if i == 1 else 0.37
+        want = cb * base + sum((c * s_) * k for k, c in terms) + (cf * s_) * F
+        vals.append(want)
+        assert rel(out, want) <= 2e-6
+    e = sum((1e-3 * (j - 2) * 0.37) * k for j, k in enumerate(ks)) + (1e-3 * 0.37) * F
+    tol = 1e-4 + 1e-3 * torch.maximum(y0.abs(), vals[0].abs())
+    assert rel(st.err[0], ((e.double() / tol.double()) ** 2).sum(-1)) <= 1e-5
+
+
 def test_wide_epilogue_bit_equal_to_stage_pass():
     """The fused wide epilogue (K1, STG 4) and the stage pass applied to K1's f give
     the same bits (same per-element arithmetic in the same order), error rows
@@ -241,6 +276,39 @@ def test_bf16_unfused_adaptive_loop_combines_in_hip(monkeypatch):
         zb = gi.odeint(func, y0, t, rtol=1e-3, atol=1e-4, method='dopri5')[1]
     assert zb.dtype == torch.bfloat16
     assert rel(zb.float(), z32) <= 2e-2
+
+
+@pytest.mark.parametrize("rtol,first", [(1e-5, 0.2), (1e-3, None), (1e-4, None)])
+def test_krylov_step_vs_stage_step(monkeypatch, rtol, first):
+    """The affine dopri5 step in the Krylov basis (integrator._KrylovPlan, default) against
+    the stage-combination plan (GNPDE_KRYLOV_STEP=0) on the same HIP RHS with a source
+    term and a hub row: same step count, values within fp32 rounding of each other (the
+    two evaluate the same polynomial in dt L in different bases), and within RTOL of the
+    fp64 oracle's solve with its step count.  (At rtol 1e-7 the fp32 error estimate of
+    the stage combinations is noise of the size of the tolerance and the two take
+    8 and 9 steps: not a comparison of the methods.)"""
+    N, E, C = 5000, 60000, 64
+    eo, wo, rng = _graph(N, E, 35)
+    x = rng.standard_normal((1, N, C)).astype(np.float32)
+    x0 = rng.standard_normal((1, N, C)).astype(np.float32)
+    func = _laplacian(C, eo, wo, alpha=0.3, add_source=True, x0=T(x0))
+    ts = [0.0, 0.3, 1.0, 1.5]
+    opts = {} if first is None else {'first_step': first}
+    got = []
+    for kry in (True, False):
+        monkeypatch.setattr(gi, "KRYLOV_STEP", kry)
+        with torch.no_grad():
+            z = gi.odeint(func, T(x), torch.tensor(ts, dtype=torch.float64, device=DEV), rtol=rtol,
+                          atol=rtol * 0.1, method='dopri5', options=opts)
+        got.append((z, gi.odeint.last_n_steps))
+    (zk, nk), (zs, ns_) = got
+    assert nk == ns_
+    assert rel(zk, zs) <= 2e-6
+    f = lambda t, y: O.laplacian_rhs(eo, y, x0, 0.3, 0.4, edge_weight=wo, add_source=True)  # noqa: E731
+    if first is None:
+        want, n_want = O.odeint_adaptive(f, x, ts, 'dopri5', rtol, rtol * 0.1)
+        assert nk == n_want
+        assert rel(zk, want) <= RTOL
 
 
 def test_attention_rhs_dopri5_fused_vs_unfused(monkeypatch):

@@ -202,13 +202,16 @@ def test_add_source_new_x0_each_forward_replays_with_new_x0():
 
 @pytest.mark.parametrize("fn,kw", [("get_rw_adj", dict(norm_dim=1)), ("get_rw_adj", dict(norm_dim=0)),
                                    ("gcn_norm_fill_val", {})])
-@pytest.mark.parametrize("weighted", [False, True])
+@pytest.mark.parametrize("weighted", [None, "frac", "int", "bigint"])
 def test_graph_normalisation_kernels_bit_exact_vs_host(fn, kw, weighted):
     """csrc/prep.hip (self loops + rw / gcn weights) equals the host restatement
     in gnpde.utils bit for bit: same edge order, the node's last existing loop
     weight, degrees added in COO order (= torch's CPU scatter_add_); and the
     fp64 oracle within fp32 rounding.  Batched, duplicated edges, repeated
-    loops on one node, an isolated node."""
+    loops on one node, an isolated node, hub rows and columns longer than one
+    wavefront (degree_long_kernel: the parallel sum for integral weights below
+    2^24 — unit and small integer weights — the in-order sum for fractional ones
+    and for integers whose sum reaches 2^24, where the order changes the bits)."""
     from gnpde import utils as gu
     rng = np.random.default_rng(107)
     B, N, E = 2, 500, 4000
@@ -218,8 +221,17 @@ def test_graph_normalisation_kernels_bit_exact_vs_host(fn, kw, weighted):
     ei[:, 0, :30] = 4
     ei[:, 1, :30] = 4  # 30 loops on node 4 with different weights: the last one wins
     ei[:, :, 100:200] = ei[:, :, 200:300]  # duplicates
-    w = rng.uniform(0.1, 2.0, size=(B, E)).astype(np.float32) if weighted else None
-    args = dict(fill_value=1.5, num_nodes=N, **kw)
+    ei[:, 0, 300:1300] = 7  # a hub row and a hub column (1000 edges)
+    ei[:, 1, 1300:2300] = 9
+    ei[:, 1, 300:1300][ei[:, 1, 300:1300] == 7] = 8
+    ei[:, 0, 1300:2300][ei[:, 0, 1300:2300] == 9] = 8
+    w = {None: None,
+         "frac": lambda: rng.uniform(0.1, 2.0, size=(B, E)),
+         "int": lambda: rng.integers(1, 5, size=(B, E)),
+         "bigint": lambda: rng.integers(1, 2 ** 20, size=(B, E))}[weighted]
+    w = None if w is None else w().astype(np.float32)
+    # an integral loop fill keeps integral rows integral (the parallel path)
+    args = dict(fill_value=1.5 if weighted == "frac" else 2.0, num_nodes=N, **kw)
     ge, gw = getattr(gu, fn)(T(ei), edge_weight=None if w is None else T(w), **args)
     he, hw = getattr(gu, fn)(torch.from_numpy(ei), edge_weight=None if w is None else torch.from_numpy(w), **args)
     assert torch.equal(ge.cpu(), he)

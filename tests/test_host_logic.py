@@ -417,3 +417,44 @@ def test_fused_adaptive_plan_dopri5_operands():
     assert P.launches[4]['epart'] is not None and P.launches[5]['err'][0] == 'E'
     assert P.reads[5] == set()
     assert P.store == {1, 2, 3, 4, 6} and P.store_mid == {5}
+
+
+def test_krylov_plan_dopri5_coefficients():
+    """_KrylovPlan (the affine dopri5 step in the basis u_p = (dt L)^p f0): y1's
+    coefficients are the exponential's 1/(p+1)! through the method's order, the
+    error combination vanishes below the embedded order (exact zeros, no
+    cancellation left to the fp32 sums), f1 = sum_p B[6][p] u_p is the stage
+    derivative at y1 (FSAL: B[6] = [1] + G[:6] shifted)."""
+    import math
+    K = gode._KrylovPlan(gode._adaptive_plan('dopri5'))
+    for p in range(5):
+        assert abs(K.G[p] - 1.0 / math.factorial(p + 1)) < 1e-15
+    assert K.G[6] == 0.0
+    assert K.Eps[:4] == [0.0, 0.0, 0.0, 0.0] and all(K.Eps[p] != 0.0 for p in (4, 5, 6))
+    assert K.Bn[0] == 1.0 and all(abs(K.Bn[p + 1] - K.G[p]) < 1e-15 for p in range(6))
+    y1, (ft, fcf), (et, ecf) = K.last_launch_terms()
+    assert [p for p, _ in et] == [4, 5] and ecf == K.Eps[6]
+    assert len({p for p, _ in y1} | {p for p, _ in ft}) <= 6  # u_0 .. u_5: the stage's operand table
+
+
+@pytest.mark.parametrize("tol", [1e-3, 1e-7])
+def test_krylov_step_matches_stage_step(monkeypatch, tol):
+    """The fused dopri5 solve of an affine RHS with the Krylov step (default) and
+    with the stage-combination plan (GNPDE_KRYLOV_STEP=0): the same accepted step
+    sequence and the same values to fp64 rounding, dense outputs included."""
+    from host_stage import HostLinearRHS
+    rng = np.random.default_rng(11)
+    C = 5
+    A = torch.from_numpy(rng.standard_normal((C, C)) * 0.9)
+    y0 = torch.from_numpy(rng.standard_normal((1, 30, C)))
+    ts = torch.tensor([0.0, 0.05, 0.7, 2.0], dtype=torch.float64)
+    runs = []
+    for kry in (True, False):
+        monkeypatch.setattr(gode, "KRYLOV_STEP", kry)
+        f = HostLinearRHS(A)
+        with torch.no_grad():
+            got = gode.odeint(f, y0, ts, method='dopri5', rtol=tol, atol=tol * 0.1, combine=gode._Combine())
+        runs.append((got, gode.odeint.last_n_steps, f.nfe))
+    (a, na, fa), (b, nb, fb) = runs
+    assert na == nb and fa == fb
+    assert float((a - b).abs().max()) <= 1e-11 * max(1.0, float(b.abs().max()))
