@@ -131,7 +131,7 @@ __global__ void emit_loops_kernel(const int64_t* __restrict__ ei, const float* _
 // additions as a lane walking the row (and as torch's CPU scatter_add_), without its
 // 7.4k-deep chain of dependent loads (1.58 ms per call at G-arxiv, round 4).
 constexpr int kDegLane = 64;
-constexpr int kDegUnroll = 64;
+constexpr int kDegUnroll = 16;
 constexpr int kDegBatch = 8;
 
 __device__ __forceinline__ float deg_weight(const float* __restrict__ w, const int32_t* __restrict__ perm, int32_t p,
