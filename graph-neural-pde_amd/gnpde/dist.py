@@ -494,11 +494,12 @@ class _HipAttentionLocal(object):
             self._uni = ops.attn_weights(self.g, ns, m, rl, 0)
         return self._uni
 
-    def stats_rows(self, ns, r0, r1):
+    def stats_rows(self, ns, r0, r1, packed=None):
         """The destination statistics (norm_idx 1) of groups [r0, r1) only: a list of
         full-size tensors with those rows written (packed records for two-head
-        reference and per-edge scores, m and rl otherwise), or None outside K2."""
-        return _hip_stats_rows(self.g, ns, r0, r1)
+        reference and per-edge scores, m and rl otherwise or with packed=False), or
+        None outside K2."""
+        return _hip_stats_rows(self.g, ns, r0, r1, packed)
 
     def aggregate(self, ns, norm_idx, x, stage=None, stats=None, **kw):
         if ns is None:  # uniform weights (fork scaled_dot, norm_idx 0): graph-only
@@ -507,9 +508,36 @@ class _HipAttentionLocal(object):
         m, rl, mr = _stats_args(stats)
         return ops.attn_rhs(self.g, ns, m, rl, norm_idx, x, stage=stage, mr=mr, **kw)
 
+    def n_edges(self):
+        return self.g.nnz
 
-def _hip_stats_rows(g, ns, r0, r1):
-    packed = ns.heads == 2 or ns.mode != ops._lib.SCORE_REFERENCE
+    def edge_blocks(self, world):
+        """Blocks of CSR positions, one per rank, aligned to CSR rows and balanced by
+        nnz: under source-grouped softmax (norm_idx 0) a block holds whole groups.
+        Returns ([(e0, e1)], [(r0, r1)])."""
+        rp = self.g.csr.rowptr.cpu().numpy()
+        rows = balanced_row_blocks(rp, world)
+        return [(int(rp[a]), int(rp[b])) for a, b in rows], rows
+
+    def src_stats(self, ns, r0, r1):
+        """The source-grouped statistics (norm_idx 0) of rows [r0, r1): [m, rl] full-size
+        with those rows written (K2 over a row-range plan), or None outside K2."""
+        r = ops.softmax_stats(self.g, ns, 0, packed=False, rows=(r0, r1))
+        return None if r is NotImplemented else [r[0], r[1]]
+
+    def edge_weights(self, ns, norm_idx, stats, e0, e1):
+        """The head-mean weights of CSR positions [e0, e1) from the gathered m, rl."""
+        return ops.attn_weights(self.g, ns, stats[0], stats[1], norm_idx, edges=(e0, e1))
+
+    def weighted(self, w, x, stage=None, **kw):
+        """K1 over this rank's columns with the gathered [nnz] weights."""
+        kw.pop('heads', None)
+        return ops.spmm_rhs(self.g, w, x, stage=stage, **kw)
+
+
+def _hip_stats_rows(g, ns, r0, r1, packed=None):
+    if packed is None:
+        packed = ns.heads == 2 or ns.mode != ops._lib.SCORE_REFERENCE
     r = ops.softmax_stats(g, ns, 1, packed=packed, rows=(r0, r1))
     if r is NotImplemented:
         return None
@@ -532,6 +560,19 @@ def _gather_row_blocks(comm, v, blocks, rank, world, nb):
     blk = torch.zeros((nb,) + tuple(v.shape[1:]), dtype=v.dtype, device=v.device)
     blk[:r1 - r0] = v[r0:r1]
     pad = torch.empty((world * nb,) + tuple(v.shape[1:]), dtype=v.dtype, device=v.device)
+    comm.all_gather_into_tensor(pad, blk)
+    return torch.cat([pad[p * nb:p * nb + (b - a)] for p, (a, b) in enumerate(blocks)], 0)
+
+
+def _gather_edge_blocks(comm, w, blocks, world):
+    """This rank's weights of CSR positions [e0, e1), exchanged so every rank holds all
+    nnz of them: padded blocks all-gathered, then unpadded (one copy of E floats)."""
+    if world == 1:
+        return w
+    nb = max(max(b - a for a, b in blocks), 1)
+    blk = torch.zeros(nb, dtype=w.dtype, device=w.device)
+    blk[:w.numel()] = w
+    pad = torch.empty(world * nb, dtype=w.dtype, device=w.device)
     comm.all_gather_into_tensor(pad, blk)
     return torch.cat([pad[p * nb:p * nb + (b - a)] for p, (a, b) in enumerate(blocks)], 0)
 
@@ -569,9 +610,12 @@ class ColumnShardedTransformer(object):
     * per-edge scaled_dot: the projection q | k [R, 2 att] (fp32, the stripe's
       columns of [Wq; Wk]) all-reduced — R 2 att 4 bytes per RHS.
 
-    The biases enter on rank 0 only.  Every rank then runs the same softmax
-    statistics (replicated, they are graph- and score-sized) and aggregates its
-    own columns with the fused kernels.  Drops into gnpde.odeint: __call__ /
+    The biases enter on rank 0 only.  Under destination-grouped softmax (norm_idx
+    1) each rank forms the statistics of one block of destination rows and the
+    blocks are all-gathered; with ``edge_weights`` (default at world > 1) each
+    rank also forms the head-mean weights of one block of edges, all-gathered
+    (E x 4 bytes), and aggregates its own columns with the plain-weight K1;
+    otherwise it aggregates with the fused kernels.  Drops into gnpde.odeint: __call__ /
     rhs_stage (fixed-grid fused stages, the adaptive solvers' wide stages),
     global_rms_norm / reduce_error_sq (dopri5's error norm over all stripes)."""
 
@@ -595,7 +639,7 @@ class ColumnShardedTransformer(object):
 
     def __init__(self, edge_index, num_nodes, C, Wq, bq, Wk, bk, heads, norm_idx, alpha, score_mode='reference',
                  beta=None, x0_local=None, add_source=False, alpha_sigmoid=True, group=None, local=None,
-                 chunk=None, comm=None, partition_stats=True):
+                 chunk=None, comm=None, partition_stats=True, edge_weights=None):
         self.group = group
         self.comm = comm if comm is not None else _Comm(group)
         self.rank = dist.get_rank(group)
@@ -627,6 +671,20 @@ class ColumnShardedTransformer(object):
         self.partition_stats = bool(partition_stats) and self.norm_idx == 1 and not self.uniform
         if self.partition_stats:
             self.dblocks, self.dnb = _dst_blocks(edge_index, self.N, self.world, g)
+        # edge-sharded weights (norm_idx 1, the statistics partitioned): each rank forms the
+        # head-mean weights of one block of CSR positions from the gathered statistics, the
+        # blocks are all-gathered (E x 4 bytes) and every rank aggregates its columns with the
+        # plain-weight K1 — the per-edge work (scores, exponentials, the statistics' loads)
+        # divided by the world instead of repeated in every rank's fused K1.  Default: on for
+        # world > 1 on the HIP path (at one rank the fused K1 is faster).
+        # Under source-grouped softmax (norm_idx 0, per-edge scores) the blocks are whole CSR
+        # rows: a rank forms its rows' statistics and their weights, and only the weights are
+        # exchanged.
+        if edge_weights is None:
+            edge_weights = self.world > 1 and isinstance(self.local, _HipAttentionLocal)
+        self.edge_weights = bool(edge_weights) and not self.uniform and (self.partition_stats or self.norm_idx == 0)
+        if self.edge_weights:
+            self.eblocks, self.erows = self.local.edge_blocks(self.world)
         self.bytes_per_rhs = 0  # collective payload of the last RHS (bench.py)
 
     def split(self, x):
@@ -660,7 +718,8 @@ class ColumnShardedTransformer(object):
         if not self.partition_stats:
             return None
         d0, d1 = self.dblocks[self.rank]
-        st = self.local.stats_rows(ns, d0, d1)
+        st = self.local.stats_rows(ns, d0, d1, packed=False) if getattr(self, 'edge_weights', False) else \
+            self.local.stats_rows(ns, d0, d1)
         if st is None:
             return None
         st = [_gather_row_blocks(self.comm, v, self.dblocks, self.rank, self.world, self.dnb) for v in st]
@@ -668,15 +727,35 @@ class ColumnShardedTransformer(object):
             self.bytes_per_rhs += sum(self.world * self.dnb * v[0].numel() * v.element_size() for v in st)
         return st
 
+    def weights(self, ns, stats):
+        """This rank's block of the [nnz] weights from the gathered statistics, all-gathered."""
+        e0, e1 = self.eblocks[self.rank]
+        w = self.local.edge_weights(ns, self.norm_idx, stats, e0, e1)
+        w = _gather_edge_blocks(self.comm, w, self.eblocks, self.world)
+        if self.world > 1:
+            self.bytes_per_rhs += self.world * max(max(b - a for a, b in self.eblocks), 1) * 4
+        return w
+
+    def _aggregate(self, x_local, stage):
+        ns = self.scores(x_local)
+        if self.edge_weights and self.norm_idx == 0:
+            st = self.local.src_stats(ns, *self.erows[self.rank])  # this rank's groups: no exchange
+            if st is not None:
+                return self.local.weighted(self.weights(ns, st), x_local, stage=stage, **self._kw())
+            stats = None
+        else:
+            stats = self.stats(ns)
+        if self.edge_weights and stats is not None:
+            return self.local.weighted(self.weights(ns, stats), x_local, stage=stage, **self._kw())
+        return self.local.aggregate(ns, self.norm_idx, x_local, stage=stage, stats=stats, **self._kw())
+
     def __call__(self, t, x_local):
         self.nfe += 1
-        ns = self.scores(x_local)
-        return self.local.aggregate(ns, self.norm_idx, x_local, stats=self.stats(ns), **self._kw())
+        return self._aggregate(x_local, None)
 
     def rhs_stage(self, t, x_local, stage):
         self.nfe += 1
-        ns = self.scores(x_local)
-        self.local.aggregate(ns, self.norm_idx, x_local, stage=stage, stats=self.stats(ns), **self._kw())
+        self._aggregate(x_local, stage)
 
     def global_rms_norm(self, t):
         v = torch.stack([t.double().pow(2).sum(), torch.tensor(float(t.numel()), dtype=torch.float64,

@@ -1091,18 +1091,30 @@ def softmax_stats(g, ns, norm_idx, seg=True, packed=False, rows=None):
     return (None, None, mr) if packed else (m, rl)
 
 
-def attn_weights(g, ns, m, rl, norm_idx, seg=True):
+def attn_weights(g, ns, m, rl, norm_idx, seg=True, edges=None):
     """Head-mean softmax weights in aggregation-CSR order [nnz].  norm_idx 0:
     K2 computes them straight from the scores (m, rl unused, may be None);
     norm_idx 1 (and shapes outside K2): edge-parallel from the group
-    statistics (gnpde_attn_weights_f32)."""
+    statistics (gnpde_attn_weights_f32).  edges=(e0, e1): only the CSR
+    positions [e0, e1), edge-parallel from the given m, rl ([e1 - e0] weights,
+    the same values as the full pass: gnpde.dist's edge-sharded weights)."""
+    dev = g.csr.col.device
+    if edges is not None:
+        e0, e1 = (int(v) for v in edges)
+        if m is None or rl is None or not 0 <= e0 <= e1 <= g.nnz:
+            raise ValueError("attn_weights: edges needs the statistics m, rl and 0 <= e0 <= e1 <= nnz")
+        w = torch.empty(max(e1 - e0, 1), dtype=torch.float32, device=dev)
+        if e1 > e0:
+            _lib.call("gnpde_attn_weights_f32", _ptr(g.csr.rowidx[e0:e1]), _ptr(g.csr.col[e0:e1]), e1 - e0,
+                      int(norm_idx), ns.mode, ns.heads, ns.dk, _ptr(ns.cs), _ptr(ns.q), _ptr(ns.k), ns.ldqk, ns.p0,
+                      ns.p1, _ptr(m), _ptr(rl), _ptr(w), _stream(dev))
+        return w[:e1 - e0]
     if seg and norm_idx == 0:
         w = _seg_call(g, ns, 0, 0)
         if w is not NotImplemented:
             return w
     if m is None:
         m, rl = softmax_stats(g, ns, norm_idx, seg=seg)
-    dev = g.csr.col.device
     w = torch.empty(max(g.nnz, 1), dtype=torch.float32, device=dev)
     _lib.call("gnpde_attn_weights_f32", _ptr(g.csr.rowidx), _ptr(g.csr.col), g.nnz, int(norm_idx), ns.mode, ns.heads,
               ns.dk, _ptr(ns.cs), _ptr(ns.q), _ptr(ns.k), ns.ldqk, ns.p0, ns.p1, _ptr(m), _ptr(rl), _ptr(w),

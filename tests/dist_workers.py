@@ -182,7 +182,44 @@ class CpuAttentionLocal(object):
         return np.stack([(q[src, h * dk:(h + 1) * dk] * k[dst, h * dk:(h + 1) * dk]).sum(1) / np.sqrt(dk)
                          for h in range(heads)], 1)
 
-    def stats_rows(self, ns, r0, r1):
+    def n_edges(self):
+        return self.ei.shape[-1]
+
+    def edge_blocks(self, world):
+        """Even blocks of the COO edges (this host double's edge order); every rank's
+        source statistics cover all rows (src_stats), so any split is whole."""
+        ne = self.ei.shape[-1]
+        return [(ne * p // world, ne * (p + 1) // world) for p in range(world)], [(0, self.N)] * world
+
+    def src_stats(self, ns, r0, r1):
+        """Source-grouped max and sum-exp of every row (norm_idx 0)."""
+        s = self._scores(ns, ns.heads)
+        grp = self.ei[0, 0]
+        mx = np.full((self.N, ns.heads), -np.inf)
+        np.maximum.at(mx, grp, s)
+        sm = np.zeros((self.N, ns.heads))
+        np.add.at(sm, grp, np.exp(s - mx[grp]))
+        return [torch.from_numpy(mx), torch.from_numpy(sm)]
+
+    def edge_weights(self, ns, norm_idx, stats, e0, e1):
+        """Head-mean weights of COO edges [e0, e1) from the gathered statistics (the
+        edge-sharded weights of ColumnShardedTransformer)."""
+        s = self._scores(ns, ns.heads)[e0:e1]
+        grp = self.ei[0, norm_idx, e0:e1]
+        mx, sm = stats[0].numpy(), stats[1].numpy()
+        return torch.from_numpy((np.exp(s - mx[grp]) / (sm[grp] + 1e-16)).mean(axis=1))
+
+    def weighted(self, w, x, stage=None, **kw):
+        import gnpde_oracle as O
+        f = torch.from_numpy(O.rhs_epilogue(O.aggregate(self.ei, w.numpy()[None], x.numpy()), x.numpy(), None,
+                                            kw['alpha'], 0.0, False, False))
+        if stage is not None:
+            from host_stage import apply_stage
+            apply_stage(stage, f, x)
+            return None
+        return f
+
+    def stats_rows(self, ns, r0, r1, packed=None):
         """The destination groups [r0, r1)'s max and sum-exp (the rest 0): the block a
         rank forms and all-gathers (partitioned statistics, norm_idx 1)."""
         s = self._scores(ns, ns.heads)
@@ -216,7 +253,7 @@ class CpuAttentionLocal(object):
         return f
 
 
-def attn_cols_worker(rank, world, port, score_mode, norm_idx, method, q):
+def attn_cols_worker(rank, world, port, score_mode, norm_idx, method, edge_weights, q):
     """gnpde.dist.ColumnShardedTransformer under gloo with CPU arithmetic: the
     stripes' key-sum / node-score / projection shares all-reduced, the stripes
     aggregated, integrated with gnpde.odeint (fused fixed-grid stages), against
@@ -234,7 +271,8 @@ def attn_cols_worker(rank, world, port, score_mode, norm_idx, method, q):
         alpha = 0.35
         T = lambda a: torch.from_numpy(np.ascontiguousarray(a))  # noqa: E731
         sh = gd.ColumnShardedTransformer(T(ei), N, C, T(Wq), T(bq), T(Wk), T(bk), h, norm_idx, alpha,
-                                         score_mode=score_mode, local=CpuAttentionLocal(ei, N))
+                                         score_mode=score_mode, local=CpuAttentionLocal(ei, N),
+                                         edge_weights=edge_weights)
         # the injected aggregation writes the fused stage outputs on the host (fixed-grid and
         # adaptive stages; the adaptive step's own passes through host_stage_apply)
         from host_stage import apply_stage
@@ -254,7 +292,7 @@ def attn_cols_worker(rank, world, port, score_mode, norm_idx, method, q):
         want = O.odeint_fixed(rhs, x, 0.0, 0.5, method, 0.125) if method != 'dopri5' else \
             O.odeint_adaptive(rhs, x, [0.0, 0.5], method, 1e-8, 1e-10)[0][-1]
         q.put((rank, err_f, float(np.abs(y_full - want).max()), sh.nfe, sh.bytes_per_rhs,
-               sh.dnb if sh.partition_stats else 0))
+               sh.dnb if sh.partition_stats else 0, sh.edge_weights))
     finally:
         dist.destroy_process_group()
 

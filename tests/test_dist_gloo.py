@@ -106,10 +106,11 @@ def test_column_sharded_transformer_matches_single_process(score_mode, norm_idx,
     (per-edge) all-reduced, the stripes aggregated — equals the oracle RHS of the
     whole state; integrated (rk4 through the fused stages, dopri5 through the
     global error norm) it matches the single-process integration."""
-    res = _run(W.attn_cols_worker, score_mode, norm_idx, method)
-    for rank, err_f, err_y, nfe, nbytes, dnb in res:
+    res = _run(W.attn_cols_worker, score_mode, norm_idx, method, False)
+    for rank, err_f, err_y, nfe, nbytes, dnb, ew in res:
         assert err_f < 1e-12
         assert err_y < 1e-9
+        assert not ew  # a CPU local: the fused aggregation unless asked
         # norm_idx 1: each rank forms the statistics of a block of dnb destination rows, and
         # the blocks (max and sum-exp, [dnb, heads] fp64 each on this host path) are all-gathered
         stats = 2 * 2 * dnb * 2 * 8 if norm_idx == 1 else 0
@@ -120,6 +121,24 @@ def test_column_sharded_transformer_matches_single_process(score_mode, norm_idx,
             assert nbytes == (8 + 41 * 2) * 8 + stats  # S [1, att] + cs [N, heads], fp64
         else:
             assert nbytes == 41 * 16 * 4 + stats  # q | k [N, 2 att], fp32
+
+
+@pytest.mark.parametrize("score_mode,norm_idx", [("reference", 1), ("per_edge", 1), ("per_edge", 0)])
+@pytest.mark.parametrize("method", ["rk4", "dopri5"])
+def test_column_sharded_transformer_edge_weights(score_mode, norm_idx, method):
+    """Edge-sharded weights: each rank forms the head-mean weights of one block of
+    edges — from the gathered destination statistics (norm_idx 1) or its own source
+    groups' (norm_idx 0, no statistics exchanged) — the blocks are all-gathered and
+    every rank aggregates its columns with them: equals the oracle RHS of the whole
+    state and the single-process integration; the payload adds the padded E x 4 bytes."""
+    res = _run(W.attn_cols_worker, score_mode, norm_idx, method, True)
+    for rank, err_f, err_y, nfe, nbytes, dnb, ew in res:
+        assert ew
+        assert err_f < 1e-12
+        assert err_y < 1e-9
+        stats = 2 * 2 * dnb * 2 * 8 if norm_idx == 1 else 0
+        base = (8 + 41 * 2) * 8 if score_mode == "reference" else 41 * 16 * 4
+        assert nbytes == base + stats + 2 * 150 * 4  # two ranks, 300 edges: blocks of 150
 
 
 @pytest.mark.parametrize("score_mode,norm_idx,method,world,hub", [

@@ -149,6 +149,40 @@ def test_partitioned_destination_statistics(arxiv, world, mode):
     assert torch.allclose(got[nz, H:2 * H], mr[nz, H:2 * H], rtol=1e-6, atol=0)
 
 
+@pytest.mark.parametrize("world,mode,norm_idx", [(2, 'reference', 1), (8, 'reference', 1), (4, 'per_edge', 1),
+                                                 (8, 'per_edge', 0)])
+def test_edge_sharded_weights_shares(arxiv, world, mode, norm_idx):
+    """The edge-sharded weights of ColumnShardedTransformer: each rank's block of CSR
+    positions (whole CSR rows, balanced by nnz) weighted edge-parallel
+    (gnpde_attn_weights_f32 over [e0, e1)) from the statistics — the gathered
+    destination ones (norm_idx 1) or its own rows' source ones from a row-range K2
+    (norm_idx 0) — equals that block of the whole-graph weights bit for bit (norm_idx
+    1) / within 1e-6 (norm_idx 0: the row-range K2's lane order); the stripes
+    aggregated with the gathered weights equal the unsharded RHS within 1e-6."""
+    ei, g, x, Wq, bq, Wk, bk = arxiv
+    a = torch.tensor(0.3, device=DEV)
+    kw = dict(wcat=(torch.cat([Wq, Wk], 0), torch.cat([bq, bk], 0))) if mode == 'per_edge' else {}
+    ns = ops.node_scores(g, x, Wq, bq, Wk, bk, H, 'scaled_dot', mode, **kw)
+    f_full = ops.attn_rhs(g, ns, None, None, norm_idx, x, alpha=a)
+    m, rl = ops.softmax_stats(g, ns, norm_idx, seg=False)
+    w_full = ops.attn_weights(g, ns, m, rl, norm_idx, seg=False)
+    blocks, rows = gd._HipAttentionLocal(g).edge_blocks(world)
+    assert blocks[0][0] == 0 and blocks[-1][1] == g.nnz
+    parts = []
+    for (e0, e1), (r0, r1) in zip(blocks, rows):
+        if norm_idx == 0:
+            ms, rls = gd._HipAttentionLocal(g).src_stats(ns, r0, r1)
+            wp = ops.attn_weights(g, ns, ms, rls, 0, edges=(e0, e1))
+            assert torch.allclose(wp, w_full[e0:e1], rtol=1e-6, atol=0)
+        else:
+            wp = ops.attn_weights(g, ns, m, rl, 1, edges=(e0, e1))
+            assert torch.equal(wp, w_full[e0:e1])
+        parts.append(wp)
+    w = torch.cat(parts)
+    f = torch.cat([ops.spmm_rhs(g, w, x[..., c0:c1].contiguous(), alpha=a) for c0, c1 in gd.col_blocks(C, world)], -1)
+    assert rel(f, f_full) <= 1e-6
+
+
 def _two_rank_worker(rank, world, port, cls, mode, norm_idx, q):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
@@ -204,7 +238,7 @@ def _two_rank_worker(rank, world, port, cls, mode, norm_idx, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("cls,mode,norm_idx", [("cols", "reference", 1), ("cols", "per_edge", 0),
+@pytest.mark.parametrize("cls,mode,norm_idx", [("cols", "reference", 1), ("cols", "per_edge", 0), ("cols", "per_edge", 1),
                                                ("rows", "reference", 1), ("rows", "per_edge", 1),
                                                ("rows", "reference", 0)])
 def test_sharded_classes_two_ranks_one_gpu(cls, mode, norm_idx):

@@ -9,6 +9,12 @@ Column stripes (gnpde.dist.ColumnShardedTransformer / ColumnShardedLaplacian) on
     columns with the full scores;
   * per-edge scaled_dot, norm_idx 0: its stripe's q|k projection share, the one-pass
     per-edge K1 over its columns with the full q|k;
+  * reference scaled_dot, norm_idx 1, edge-sharded weights (ColumnShardedTransformer
+    edge_weights, the default at world > 1): the score shares and statistics block as
+    above, the head-mean weights of its block of E / N edges, the plain-weight K1 over its
+    columns with the gathered weights;
+  * per-edge scaled_dot, norm_idx 0, edge-sharded weights: the q|k share, its CSR rows'
+    source statistics (row-range K2) and their edges' weights, the plain-weight K1;
   * Laplacian: the plain K1 over its columns.
 Each share's launches are captured in one hipGraph and replayed (median of 3 x 20
 replays).  The collectives are listed with their payloads; their time is not modelled
@@ -72,7 +78,13 @@ def main():
         qk_full = ops.linear(x, Wc, bc)[0]
         ns_dot = gd._qk_scores(qk_full, H, ATT)
         _, _, mr_full = ops.softmax_stats(g, ns_full, 1, packed=True)
-        for wl in ("reference_norm1", "per_edge_norm0", "laplacian"):
+        m_full, rl_full = ops.softmax_stats(g, ns_full, 1)
+        w_full = ops.attn_weights(g, ns_full, m_full, rl_full, 1)
+        m0, rl0 = ops.softmax_stats(g, ns_dot, 0)
+        w_dot0 = ops.attn_weights(g, ns_dot, m0, rl0, 0)
+        loc = gd._HipAttentionLocal(g)
+        for wl in ("reference_norm1", "reference_norm1_edges", "per_edge_norm0", "per_edge_norm0_edges",
+                   "laplacian"):
             res = {"workload": wl, "graph": "G-arxiv N=%d E'=%d C=%d" % (N, E, C), "ranks": {}}
             for world in worlds:
                 cols = gd.col_blocks(C, world)
@@ -92,6 +104,30 @@ def main():
                             ops.ref_scores_from_keysum(g, xs, S, Wqs, bqs, H)
                             ops.softmax_stats(g, ns_full, 1, packed=True, rows=(d0, d1))
                             ops.attn_rhs(g, ns_full, None, None, 1, xs, alpha=a0, mr=mr_full)
+                    elif wl == "reference_norm1_edges":
+                        Wks, Wqs = Wk[:, c0:c1].contiguous(), Wq[:, c0:c1].contiguous()
+                        bks = bk if first else torch.zeros_like(bk)
+                        bqs = bq if first else torch.zeros_like(bq)
+                        d0, d1 = dblocks[p]
+                        ne = g.nnz
+                        eb = (ne * p // world, ne * (p + 1) // world)
+
+                        def share():
+                            S = ops.ref_keysum(g, xs, Wks, bks)
+                            ops.ref_scores_from_keysum(g, xs, S, Wqs, bqs, H)
+                            ops.softmax_stats(g, ns_full, 1, packed=False, rows=(d0, d1))
+                            ops.attn_weights(g, ns_full, m_full, rl_full, 1, edges=eb)
+                            ops.spmm_rhs(g, w_full, xs, alpha=a0)
+                    elif wl == "per_edge_norm0_edges":
+                        Wcs = Wc[:, c0:c1].contiguous()
+                        bcs = bc if first else torch.zeros_like(bc)
+                        (eb,), (rb,) = [v[p:p + 1] for v in loc.edge_blocks(world)]
+
+                        def share():
+                            ops.linear(xs, Wcs, bcs)
+                            ms, rls = loc.src_stats(ns_dot, *rb)
+                            ops.attn_weights(g, ns_dot, ms, rls, 0, edges=eb)
+                            ops.spmm_rhs(g, w_dot0, xs, alpha=a0)
                     elif wl == "per_edge_norm0":
                         Wcs = Wc[:, c0:c1].contiguous()
                         bcs = bc if first else torch.zeros_like(bc)
@@ -105,7 +141,11 @@ def main():
                     per_rank.append(replay_ms(share))
                 coll = {"reference_norm1": {"all_reduce S": 8 * ATT, "all_reduce cs": 8 * N * H,
                                             "all_gather stats records": 4 * ops.stats_record_floats(H) * N},
+                        "reference_norm1_edges": {"all_reduce S": 8 * ATT, "all_reduce cs": 8 * N * H,
+                                                  "all_gather stats m, rl": 12 * H * N,
+                                                  "all_gather weights": 4 * g.nnz},
                         "per_edge_norm0": {"all_reduce q|k": 4 * N * 2 * ATT},
+                        "per_edge_norm0_edges": {"all_reduce q|k": 4 * N * 2 * ATT, "all_gather weights": 4 * g.nnz},
                         "laplacian": {}}[wl]
                 res["ranks"][world] = {"rank_ms": [round(v, 4) for v in per_rank], "max_ms": round(max(per_rank), 4),
                                        "collective_bytes": coll if world > 1 else {}}
