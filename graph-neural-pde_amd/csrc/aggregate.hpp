@@ -552,6 +552,12 @@ static int launch_agg_vec(const int4* items, int64_t n_items, int4* heavy, int64
         if (lanes <= 8) return GNPDE_AGG(8, 1, 4, 2);
         if (lanes <= 16) return GNPDE_AGG(16, 1, 4, 1);
         break;
+      // narrow stripes (the column layout at 4-8 ranks): edge groups per row x unroll
+      case 20: if (lanes <= 4) return GNPDE_AGG(4, 1, 8, 4); if (lanes <= 8) return GNPDE_AGG(8, 1, 4, 4); break;
+      case 21: if (lanes <= 4) return GNPDE_AGG(4, 1, 2, 4); if (lanes <= 8) return GNPDE_AGG(8, 1, 8, 2); break;
+      case 22: if (lanes <= 4) return GNPDE_AGG(4, 1, 4, 8); if (lanes <= 8) return GNPDE_AGG(8, 1, 4, 2); break;
+      case 23: if (lanes <= 4) return GNPDE_AGG(4, 1, 8, 2); if (lanes <= 8) return GNPDE_AGG(8, 1, 2, 4); break;
+      case 24: if (lanes <= 4) return GNPDE_AGG(4, 1, 4, 2); if (lanes <= 8) return GNPDE_AGG(8, 1, 8, 8); break;
       case 2: if (lanes > 16 && lanes <= 32) return GNPDE_AGG(32, 1, 2, 1); break;
       case 3:
         if (lanes > 16 && lanes <= 32) return GNPDE_AGG(32, 1, 8, 1);
