@@ -304,10 +304,18 @@ class RowShardedLaplacian(object):
         return self.part.rhs(self.g, self.w, y_full, y_local, x0=self.x0_local, alpha=self.alpha, beta=self.beta,
                              alpha_sigmoid=self.alpha_sigmoid, add_source=self.add_source)
 
-    def rhs_stage(self, t, y_local, stage):
+    @property
+    def affine(self):
+        """f = σ(α)(A − I) y [+ β x0] is affine in y (gnpde.integrator: the adaptive
+        solvers' affine first stage and Krylov step) — on the HIP path; an injected
+        test RHS is taken as it is."""
+        return self.local_rhs is None and self.local_stage is None
+
+    def rhs_stage(self, t, y_local, stage, linear=False):
         """One RHS with the solver's stage combination in the epilogue (the path
-        gnpde.integrator's fused fixed-grid solve takes): all-gather, then K1
-        over this rank's rows writing the stage outputs."""
+        gnpde.integrator's fused solves take): all-gather, then K1 over this rank's
+        rows writing the stage outputs.  linear=True: the linear part alone (no
+        source term; Stage.f_lin, the Krylov step)."""
         self.nfe += 1
         y_full = self.gather(y_local)
         if self.local_stage is not None:
@@ -315,8 +323,9 @@ class RowShardedLaplacian(object):
             return
         if self.local_rhs is not None:
             raise NotImplementedError("rhs_stage needs local_stage (or the HIP path)")
-        self.part.rhs(self.g, self.w, y_full, y_local, x0=self.x0_local, alpha=self.alpha, beta=self.beta,
-                      alpha_sigmoid=self.alpha_sigmoid, add_source=self.add_source, stage=stage)
+        src = self.add_source and not linear
+        self.part.rhs(self.g, self.w, y_full, y_local, x0=self.x0_local if src else None, alpha=self.alpha,
+                      beta=self.beta, alpha_sigmoid=self.alpha_sigmoid, add_source=src, stage=stage)
 
     def global_rms_norm(self, t):
         """RMS over the whole state (all row blocks, the padding rows excluded): the
@@ -429,13 +438,22 @@ class ColumnShardedLaplacian(object):
         return ops.spmm_rhs(self.g, self.w, x_local, x0=self.x0_local, alpha=self.alpha, beta=self.beta,
                             alpha_sigmoid=self.alpha_sigmoid, add_source=self.add_source)
 
-    def rhs_stage(self, t, x_local, stage):
+    @property
+    def affine(self):
+        """f is affine in the stripe (gnpde.integrator's affine first stage and Krylov
+        step) on the HIP path."""
+        return self.local_rhs is None
+
+    def rhs_stage(self, t, x_local, stage, linear=False):
+        """One RHS with the stage combination in the epilogue; linear=True: the linear
+        part alone (no source term)."""
         self.nfe += 1
         if self.local_rhs is not None:
             raise NotImplementedError
         g, w, x0 = self._operands()
-        ops.spmm_rhs(g, w, x_local, x0=x0, alpha=self.alpha, beta=self.beta,
-                     alpha_sigmoid=self.alpha_sigmoid, add_source=self.add_source, stage=stage)
+        src = self.add_source and not linear
+        ops.spmm_rhs(g, w, x_local, x0=x0 if src else None, alpha=self.alpha, beta=self.beta,
+                     alpha_sigmoid=self.alpha_sigmoid, add_source=src, stage=stage)
 
     def global_rms_norm(self, t):
         """RMS over the full state (all stripes): one all-reduce of 2 doubles."""

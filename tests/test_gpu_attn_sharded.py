@@ -296,3 +296,50 @@ def test_row_sharded_laplacian_world_one_in_degree_numbering(tmp_path, add_sourc
     finally:
         if init:
             dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("cls", ["rows", "cols"])
+def test_sharded_laplacian_dopri5_krylov_world_one(tmp_path, cls):
+    """The sharded Laplacians are affine on the HIP path: an adaptive solve with their
+    global error norm takes the affine first stage and the Krylov step
+    (integrator._KrylovPlan; linear=True drops the source term) — at a world of one
+    (gloo, in-process) the same step count as the unsharded solve and its values within
+    1e-6, with a source term."""
+    import torch.distributed as dist
+    import gnpde
+    from gnpde import integrator as gi
+    init = not dist.is_initialized()
+    if init:
+        dist.init_process_group("gloo", init_method="file://%s" % (tmp_path / "pg"), rank=0, world_size=1)
+    try:
+        n, e, c = 40000, 300000, 64
+        ei, w = synthetic.rw_graph(n, e, seed=15, device=DEV)
+        x = synthetic.features(1, n, c, seed=16, device=DEV)
+        x0 = synthetic.features(1, n, c, seed=17, device=DEV)
+        a, b = torch.tensor(0.3, device=DEV), torch.tensor(-0.4, device=DEV)
+        opt = {'block': 'constant', 'function': 'laplacian', 'add_source': True, 'no_alpha_sigmoid': False,
+               'max_nfe': 10 ** 9, 'multi_modal': False, 'hidden_dim': c}
+        func = gnpde.LaplacianODEFunc(c, c, opt, DEV).to(DEV)
+        func.edge_index, func.edge_weight = ei, w
+        func.x0 = x0
+        t = torch.tensor([0.0, 1.0], device=DEV)
+        kw = dict(method='dopri5', rtol=1e-4, atol=1e-5)
+        with torch.no_grad():
+            func.alpha_train.fill_(0.3)
+            func.beta_train.fill_(-0.4)
+            want = gnpde.odeint(func, x, t, **kw)[1]
+            n_want = gi.odeint.last_n_steps
+            if cls == "rows":
+                sh = gd.RowShardedLaplacian(ei, w, n, a, beta=b, add_source=True, x0=x0)
+                y0 = sh.scatter(x)
+            else:
+                sh = gd.ColumnShardedLaplacian(ei, w, n, c, a, beta=b, add_source=True, x0_local=x0)
+                y0 = sh.split(x)
+            assert sh.affine
+            y = gnpde.odeint(sh, y0, t, options=dict(norm=sh.global_rms_norm), **kw)[1]
+            got = sh.unpad(sh.gather(y)).view(want.shape) if cls == "rows" else y.view(want.shape)
+        assert gi.odeint.last_n_steps == n_want
+        assert rel(got, want) <= 1e-6
+    finally:
+        if init:
+            dist.destroy_process_group()
