@@ -1022,12 +1022,58 @@ def bench_train_adjoint(ei, w, x, dev, fwd_ms=None, reps=3):
     torch.cuda.synchronize()
     ms = s.elapsed_time(e) / reps
     assert torch.isfinite(gx).all() and func.alpha_train.grad is not None
-    return {"config": "G-arxiv laplacian (C=128), ogbn-arxiv best_params training: odeint_adjoint, dopri5 forward "
-                      "over [0, %.3f] at tol_scale %.1f, adjoint_method rk4, adjoint_step_size 1" % (T, ts),
-            "fused": integ._fused_adjoint_ok(func, x, 'rk4', tuple(p for p in func.parameters() if p.requires_grad)),
-            "ms_per_train_step": round(ms, 4), "forward_ms_per_solve": fwd_ms,
-            "train_over_forward": round(ms / fwd_ms, 3) if fwd_ms else None,
-            "rhs_evals_per_train_step": (func.nfe - nfe0) // reps}
+    out = {"config": "G-arxiv laplacian (C=128), ogbn-arxiv best_params training: odeint_adjoint, dopri5 forward "
+                     "over [0, %.3f] at tol_scale %.1f, adjoint_method rk4, adjoint_step_size 1" % (T, ts),
+           "fused": integ._fused_adjoint_ok(func, x, 'rk4', tuple(p for p in func.parameters() if p.requires_grad)),
+           "ms_per_train_step": round(ms, 4), "forward_ms_per_solve": fwd_ms,
+           "train_over_forward": round(ms / fwd_ms, 3) if fwd_ms else None,
+           "rhs_evals_per_train_step": (func.nfe - nfe0) // reps}
+    out["adaptive_adjoint"] = _train_adaptive_adjoint(func, x, gout, dev, reps)
+    return out
+
+
+# CoauthorCS best_params (src/best_params.py:4): dopri5 over [0, T] at tol_scale, adjoint dopri5 at
+# tol_scale_adjoint (src/base_classes.py: rtol = 1e-9 tol_scale, atol = 1e-7 tol_scale)
+COAUTHOR_ADJ = (3.126400580172773, 9348.983916372074, 6599.1250595331385)
+
+
+def _train_adaptive_adjoint(func, x, gout, dev, reps):
+    """The adaptive adjoint of best_params (CoauthorCS / Computers: adjoint_method dopri5) on the G-arxiv
+    Laplacian: torchdiffeq's adjoint loop (integrator._OdeintAdjoint) with the augmented RHS by K1 launches
+    (integrator._laplacian_aug) — and, for reference, with autograd vector-Jacobian products
+    (GNPDE_FUSED_ADJOINT=0)."""
+    import gnpde.integrator as integ
+    T, ts, tsa = COAUTHOR_ADJ
+    t = torch.tensor([0.0, T], dtype=torch.float32, device=dev)
+
+    def one():
+        xi = x.detach().requires_grad_(True)
+        func.alpha_train.grad = None
+        y = integ.odeint_adjoint(func, xi, t, rtol=1e-9 * ts, atol=1e-7 * ts, method='dopri5',
+                                 adjoint_method='dopri5', adjoint_rtol=1e-9 * tsa, adjoint_atol=1e-7 * tsa)[1]
+        (y * gout).sum().backward()
+        return xi.grad
+    res = {"config": "CoauthorCS best_params adjoint on G-arxiv: dopri5 over [0, %.3f] at tol_scale %.1f, "
+                     "adjoint_method dopri5 at tol_scale_adjoint %.1f" % (T, ts, tsa)}
+    saved = integ.FUSED_ADJOINT
+    try:
+        for name, flag in (("direct", True), ("autograd", False)):
+            integ.FUSED_ADJOINT = flag
+            one()
+            torch.cuda.synchronize()
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            nfe0 = func.nfe
+            s.record()
+            for _ in range(reps):
+                gx = one()
+            e.record()
+            torch.cuda.synchronize()
+            assert torch.isfinite(gx).all()
+            res[name] = {"ms_per_train_step": round(s.elapsed_time(e) / reps, 4),
+                         "rhs_evals_per_train_step": (func.nfe - nfe0) // reps}
+    finally:
+        integ.FUSED_ADJOINT = saved
+    return res
 
 
 def bench_hard_attention_train(ei, x, dev, reps=3):

@@ -1804,6 +1804,64 @@ def _mixed_norm_fn(sizes):
     return norm
 
 
+def _laplacian_aug(func, params, y_shape, ny, ans):
+    """The augmented RHS of _OdeintAdjoint for the Laplacian (src/function_laplacian_diffusion.py,
+    f = sigma(alpha)(A y - y) [+ beta x0]) without autograd: per evaluation two K1 launches
+    and at most one dot,
+        dy/ds     = -f(y)                          K1 over the CSR, its epilogue storing -f
+        da/ds     = L^T a                          K1 over the CSC (L = sigma(alpha)(A - I))
+        dalpha/ds = (1 - sigma(alpha)) <L^T a, y>  fp64 row terms in that launch's epilogue
+        dbeta/ds  = <a, x0>                        (add_source) one fp64 dot
+    written into one output buffer in the packed layout [y | a | params]; the other
+    parameters' components are 0.  For the adaptive adjoint methods (torchdiffeq's
+    solver loop, the mixed norm); the fixed-grid rk4 adjoint runs _LaplacianAdjointFn.
+    None when the RHS is not the HIP Laplacian on a device fp32 state."""
+    fn = getattr(func, 'fixed_grid_backward_ok', None)
+    if not (FUSED_ADJOINT and fn is not None and fn() and hasattr(func, 'rhs_stage')) or \
+            func.opt.get('no_alpha_sigmoid', False) or not ans.is_cuda or ans.dtype != torch.float32 or \
+            len(y_shape) != 3:
+        return None
+    own = {id(p) for p in func.parameters()}
+    if not all(id(p) in own for p in params):
+        return None
+    y0 = ans[0]
+    g = func.graph_for(y0)
+    w, tag = func._weights_tensor()
+    w_csr = func.csr_weights(g, w, tag)
+    w_csc = g.gather_weights(w.detach().float() if w.dtype != torch.float32 else w.detach(), transpose=True)
+    add_source = bool(func.opt.get('add_source', False))
+    x0 = func.stable_x0(y0) if add_source else None
+    alpha, beta = func.alpha_train.detach(), func.beta_train.detach()
+    R = y0.numel() // y0.shape[-1]
+    drow = torch.empty(R, dtype=torch.float64, device=y0.device)
+    slots = {}
+    o = 2 * ny
+    for p in params:
+        slots[id(p)] = (o, p.numel())
+        o += p.numel()
+
+    def aug(s, z):
+        func.nfe += 1  # one RHS evaluation per augmented one, as torchdiffeq's backward calls func
+        y = z[:ny].view(y_shape)
+        a = z[ny:2 * ny].view(y_shape)
+        out = torch.empty_like(z)
+        ops.spmm_rhs(g, w_csr, y, x0=x0, alpha=alpha, beta=beta, rhs=True, alpha_sigmoid=True,
+                     add_source=add_source, stage=ops.Stage(outs=[(out[:ny].view(y_shape), None, 0.0, -1.0, [])]))
+        ops.spmm_rhs(g, w_csc, a, alpha=alpha, rhs=True, alpha_sigmoid=True, transpose=True,
+                     stage=ops.Stage(outs=[(out[ny:2 * ny].view(y_shape), None, 0.0, 1.0, [])],
+                                     dot=(y, drow, 1.0, False)))
+        out[2 * ny:].zero_()
+        if id(func.alpha_train) in slots:
+            oa, _ = slots[id(func.alpha_train)]
+            ga = ops.sum_f64(drow) * (1.0 - torch.sigmoid(alpha.double()))
+            out[oa:oa + 1].copy_(ga.reshape(1))
+        if add_source and id(func.beta_train) in slots:
+            ob, _ = slots[id(func.beta_train)]
+            out[ob:ob + 1].copy_(ops.dot(a, x0).reshape(1))
+        return out
+    return aug
+
+
 class _OdeintAdjoint(torch.autograd.Function):
     """torchdiffeq.odeint_adjoint (0.2.x OdeintAdjointMethod) restated: the
     forward integrates without recording; the backward integrates the augmented
@@ -1846,6 +1904,9 @@ class _OdeintAdjoint(torch.autograd.Function):
             vjp_p = [torch.zeros_like(p) if g is None else g for g, p in zip(grads[1:], params)]
             return -pack(f.detach(), vjp_y, vjp_p)  # d/ds = -d/dt
 
+        direct = _laplacian_aug(func, params, y_shape, ny, ans)
+        if direct is not None:
+            aug = direct  # noqa: F811 — the Laplacian's VJPs by K1 launches, no autograd
         opts = dict(a_options or {})
         if a_method in ADAPTIVE_METHODS and 'norm' not in opts:
             opts['norm'] = _mixed_norm_fn(sizes)
