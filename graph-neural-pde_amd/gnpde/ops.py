@@ -1036,6 +1036,12 @@ def _seg_call(g, ns, norm_idx, out_kind, packed=False, rows=None):
     if rows is not None:  # the groups of rows [r0, r1) only (outputs: full-size, those rows written)
         if out_kind != 1:
             return NotImplemented
+        if rows[1] <= rows[0]:  # an empty block (a rank with no groups): nothing to form
+            dev, H = grouped.col.device, ns.heads
+            if packed:
+                return None, None, torch.zeros(g.R, stats_record_floats(H), dtype=torch.float32, device=dev)
+            return (torch.zeros(g.R, H, dtype=torch.float64, device=dev),
+                    torch.zeros(g.R, H, dtype=torch.float32, device=dev))
         plan = grouped.seg_plan_rows(rows[0], rows[1], eb, long_items=long_items, long_max=long_max)
     else:
         plan = grouped.seg_plan(eb, long_items=long_items, long_max=long_max)

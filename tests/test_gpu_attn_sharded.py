@@ -343,3 +343,17 @@ def test_sharded_laplacian_dopri5_krylov_world_one(tmp_path, cls):
     finally:
         if init:
             dist.destroy_process_group()
+
+
+def test_empty_row_range_statistics_and_edge_block(arxiv):
+    """A rank whose block is empty (balanced_row_blocks gives equal cuts when one hub row
+    holds more than 1/world of the nnz): the row-range statistics return full-size
+    arrays without a launch, and the weights of an empty edge range are empty."""
+    ei, g, x, Wq, bq, Wk, bk = arxiv
+    ns = ops.node_scores(g, x, Wq, bq, Wk, bk, H, 'scaled_dot', 'reference')
+    m, rl = ops.softmax_stats(g, ns, 1, packed=False, rows=(7, 7))
+    assert m.shape == (N, H) and rl.shape == (N, H)
+    _, _, mr = ops.softmax_stats(g, ns, 1, packed=True, rows=(7, 7))
+    assert mr.shape[0] == N
+    w = ops.attn_weights(g, ns, m, rl, 1, edges=(100, 100))
+    assert w.numel() == 0
