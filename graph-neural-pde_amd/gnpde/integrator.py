@@ -1893,7 +1893,7 @@ class _OdeintAdjoint(torch.autograd.Function):
         def pack(y, ay, ap):
             return torch.cat([y.reshape(-1).float(), ay.reshape(-1).float()] + [a.reshape(-1).float() for a in ap])
 
-        def aug(s, z):
+        def aug_autograd(s, z):
             y = z[:ny].view(y_shape)
             ay = z[ny:2 * ny].view(y_shape)
             with torch.enable_grad():
@@ -1904,9 +1904,8 @@ class _OdeintAdjoint(torch.autograd.Function):
             vjp_p = [torch.zeros_like(p) if g is None else g for g, p in zip(grads[1:], params)]
             return -pack(f.detach(), vjp_y, vjp_p)  # d/ds = -d/dt
 
-        direct = _laplacian_aug(func, params, y_shape, ny, ans)
-        if direct is not None:
-            aug = direct  # noqa: F811 — the Laplacian's VJPs by K1 launches, no autograd
+        # the Laplacian's vector-Jacobian products by K1 launches (no autograd), else autograd's
+        aug = _laplacian_aug(func, params, y_shape, ny, ans) or aug_autograd
         opts = dict(a_options or {})
         if a_method in ADAPTIVE_METHODS and 'norm' not in opts:
             opts['norm'] = _mixed_norm_fn(sizes)
