@@ -1609,6 +1609,7 @@ class _RKAdaptiveFused(_RKAdaptive):
         if spec_ok and 'Ys' not in bufs:
             bufs['Ys'], bufs['Ks'] = torch.empty_like(bufs['Y']), torch.empty_like(bufs['K0'])
         pending = None  # the record reader of the step enqueued ahead: the current step
+        pre_interp = None  # (output index, t0, dt) of a dense output enqueued ahead of its step's record
         if dt_read is not None:
             if spec_ok and th[-1] > th[0]:  # the first step runs while the host waits for its size
                 pending = self._rec_reader(st, self._run_step(st, graphs_ok, t_cur, 0.0, True))
@@ -1635,6 +1636,14 @@ class _RKAdaptiveFused(_RKAdaptive):
                         _nfe_headroom(self.func, 2 * P.ns):
                     self._rotate(bufs, kn, 1)
                     ahead = self._rec_reader(st, self._run_step(st, graphs_ok, t_cur + dt, dt, True))
+                # the step crossing next_t (steps-ahead mode, its k's kept): its dense output is
+                # enqueued before its record is read, so the pass follows the step on the device
+                # without the host's round trip; used if the step is accepted (a rejected step's
+                # successor writes the output again)
+                if spec_ok and mid and ahead is None and t_cur + dt > next_t:
+                    self._dense = dict(bufs, scale=dt)
+                    self._interp_into(sol[i_out], (t_cur, dt), next_t, t_cur + dt, lay)
+                    pre_interp = (i_out, t_cur, dt)
                 dt_next = None
                 if dev_ctl:
                     ratio, _dt, dt_next, _e2 = read()  # the one host read of the step
@@ -1672,7 +1681,7 @@ class _RKAdaptiveFused(_RKAdaptive):
                     sol[i_out].copy_(bufs['Y'])
                 else:
                     _to_user(bufs['Y'], sol[i_out], lay)
-            else:
+            elif pre_interp != (i_out,) + tuple(last):  # (not already enqueued for this step)
                 self._interp_into(sol[i_out], last, next_t, t_cur, lay)
         return sol
 
