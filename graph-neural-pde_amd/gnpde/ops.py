@@ -1437,6 +1437,8 @@ def rows_copy(src, dst, order=None, dst_copy=None):
     _lib.call("gnpde_rows_copy", _ptr(src), rows, C * src.element_size(), _ptr(order), _ptr(dst), _ptr(dst_copy),
               _stream(src.device))
     return dst
+
+
 def rk_combine(y0, ks, coefs, scale, out=None):
     """out = y0 + scale * sum_j coefs[j] * ks[j]  (one fused pass; y0=None means 0)."""
     ref = y0 if y0 is not None else ks[0]
