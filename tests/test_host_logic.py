@@ -458,3 +458,29 @@ def test_krylov_step_matches_stage_step(monkeypatch, tol):
     (a, na, fa), (b, nb, fb) = runs
     assert na == nb and fa == fb
     assert float((a - b).abs().max()) <= 1e-11 * max(1.0, float(b.abs().max()))
+
+
+def test_krylov_step_selection():
+    """The Krylov step is taken for an affine RHS under dopri5 (FSAL, every k kept);
+    bosh3 (its k2 not kept), the non-FSAL pairs, a non-affine RHS and
+    GNPDE_KRYLOV_STEP=0 keep the stage plan."""
+    from host_stage import HostLinearRHS
+    A = torch.eye(3, dtype=torch.float64)
+    y0 = torch.zeros(1, 4, 3, dtype=torch.float64)
+    comb = gode._Combine()
+
+    def solver(method, func):
+        return gode._RKAdaptiveFused(func, y0, 1e-6, 1e-8, comb, method=method)
+    assert solver('dopri5', HostLinearRHS(A)).krylov is not None
+    for m in ('bosh3', 'fehlberg2', 'adaptive_heun'):
+        assert solver(m, HostLinearRHS(A)).krylov is None, m
+
+    class NotAffine(HostLinearRHS):
+        affine = False
+    assert solver('dopri5', NotAffine(A)).krylov is None
+    old = gode.KRYLOV_STEP
+    try:
+        gode.KRYLOV_STEP = False
+        assert solver('dopri5', HostLinearRHS(A)).krylov is None
+    finally:
+        gode.KRYLOV_STEP = old
