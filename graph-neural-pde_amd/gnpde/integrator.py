@@ -30,6 +30,7 @@ import torch
 
 from . import _lib, ops
 from ._cache import _tensor_key
+from .utils import MaxNFEException
 
 # Dormand-Prince-Shampine (torchdiffeq dopri5.py)
 _DP_ALPHA = [1 / 5, 3 / 10, 4 / 5, 8 / 9, 1., 1.]
@@ -1850,7 +1851,10 @@ def _laplacian_aug(func, params, y_shape, ny, ans):
         o += p.numel()
 
     def aug(s, z):
-        func.nfe += 1  # one RHS evaluation per augmented one, as torchdiffeq's backward calls func
+        # one RHS evaluation per augmented one, as torchdiffeq's backward calls func (and its guard)
+        if func.nfe > func.opt["max_nfe"]:
+            raise MaxNFEException
+        func.nfe += 1
         y = z[:ny].view(y_shape)
         a = z[ny:2 * ny].view(y_shape)
         out = torch.empty_like(z)
