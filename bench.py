@@ -1028,51 +1028,86 @@ def bench_train_adjoint(ei, w, x, dev, fwd_ms=None, reps=3):
            "ms_per_train_step": round(ms, 4), "forward_ms_per_solve": fwd_ms,
            "train_over_forward": round(ms / fwd_ms, 3) if fwd_ms else None,
            "rhs_evals_per_train_step": (func.nfe - nfe0) // reps}
-    out["adaptive_adjoint"] = _train_adaptive_adjoint(func, x, gout, dev, reps)
+    out["adaptive_adjoint"] = _train_adaptive_adjoint(ei, x, gout, dev, reps)
     return out
 
 
-# CoauthorCS best_params (src/best_params.py:4): dopri5 over [0, T] at tol_scale, adjoint dopri5 at
-# tol_scale_adjoint (src/base_classes.py: rtol = 1e-9 tol_scale, atol = 1e-7 tol_scale)
+# best_params of the attention-block datasets trained with an ADAPTIVE adjoint (src/best_params.py:3-4;
+# src/base_classes.py set_tol: rtol = 1e-9 tol_scale, atol = 1e-7 tol_scale, the adjoint's from tol_scale_adjoint)
 COAUTHOR_ADJ = (3.126400580172773, 9348.983916372074, 6599.1250595331385)
+PUBMED_ADJ = (12.942327880200853, 1991.0688305523001, 16324.368093998313)
+ADJ_BLOCKS = {
+    # CoauthorCS (:4): block attention, scaled_dot heads 4 / attention_dim 8, norm_idx 1, dopri5 adjoint
+    "coauthorcs": (COAUTHOR_ADJ, dict(heads=4, attention_dim=8, attention_norm_idx=1, attention_type='scaled_dot',
+                                      leaky_relu_slope=0.7181389780997276, adjoint_method='dopri5', add_source=False)),
+    # Pubmed (:3): block attention, cosine_sim heads 1 / attention_dim 16, norm_idx 0, adaptive_heun adjoint, add_source
+    "pubmed": (PUBMED_ADJ, dict(heads=1, attention_dim=16, attention_norm_idx=0, attention_type='cosine_sim',
+                                leaky_relu_slope=0.2, adjoint_method='adaptive_heun', add_source=True)),
+}
 
 
-def _train_adaptive_adjoint(func, x, gout, dev, reps):
-    """The adaptive adjoint of best_params (CoauthorCS / Computers: adjoint_method dopri5) on the G-arxiv
-    Laplacian: torchdiffeq's adjoint loop (integrator._OdeintAdjoint) with the augmented RHS by K1 launches
-    (integrator._laplacian_aug) — and, for reference, with autograd vector-Jacobian products
-    (GNPDE_FUSED_ADJOINT=0)."""
+def _adjoint_block(case, x, ei, dev):
+    import gnpde
+    C, N = x.shape[-1], x.shape[1]
+    (T, ts, tsa), extra = ADJ_BLOCKS[case]
+    opt = dict(LAP_OPT, hidden_dim=C, block='attention', function='laplacian', method='dopri5', adjoint=True,
+               tol_scale=ts, tol_scale_adjoint=tsa, self_loop_weight=1.0, data_norm='rw', reweight_attention=False,
+               square_plus=False, mix_features=False, beltrami=False, augment=False, max_iters=100, step_size=1,
+               adjoint_step_size=1, **extra)
+    torch.manual_seed(17)
+    blk = gnpde.AttODEblock(gnpde.LaplacianODEFunc, [], opt, dev, t=torch.tensor([0.0, T], device=dev)).to(dev).train()
+    data = gnpde.GraphData()
+    data.new_graph(ei[:, :, :ei.shape[2] - N], N)  # synthetic.rw_graph appended N self loops; the block adds its own
+    return blk, data, opt
+
+
+def _train_adaptive_adjoint(ei, x, gout, dev, reps):
+    """AttODEblock training steps as best_params runs them with an adaptive adjoint (src/best_params.py:3-4,
+    src/block_transformer_attention.py:40-50, src/base_classes.py:45-49) on the G-arxiv graph (C = 128): the block
+    attention, the dopri5 forward under no_grad, odeint_adjoint's backward with the attention weights a constant
+    of it (torchdiffeq's semantics).  Backward paths: 'fused' (gnpde.adjoint_adaptive: stage combinations, error
+    rows and the alpha integrand in the K1 epilogues), 'direct' (the restated torchdiffeq loop with the augmented
+    RHS by K1 launches, GNPDE_FUSED_ADAPTIVE_ADJOINT=0), 'autograd' (that loop with autograd VJPs)."""
     import gnpde.integrator as integ
-    T, ts, tsa = COAUTHOR_ADJ
-    t = torch.tensor([0.0, T], dtype=torch.float32, device=dev)
-
-    def one():
-        xi = x.detach().requires_grad_(True)
-        func.alpha_train.grad = None
-        y = integ.odeint_adjoint(func, xi, t, rtol=1e-9 * ts, atol=1e-7 * ts, method='dopri5',
-                                 adjoint_method='dopri5', adjoint_rtol=1e-9 * tsa, adjoint_atol=1e-7 * tsa)[1]
-        (y * gout).sum().backward()
-        return xi.grad
-    res = {"config": "CoauthorCS best_params adjoint on G-arxiv: dopri5 over [0, %.3f] at tol_scale %.1f, "
-                     "adjoint_method dopri5 at tol_scale_adjoint %.1f" % (T, ts, tsa)}
-    saved = integ.FUSED_ADJOINT
+    res = {}
+    saved = (integ.FUSED_ADJOINT, integ.FUSED_ADAPTIVE_ADJOINT)
     try:
-        for name, flag in (("direct", True), ("autograd", False)):
-            integ.FUSED_ADJOINT = flag
-            one()
-            torch.cuda.synchronize()
-            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            nfe0 = func.nfe
-            s.record()
-            for _ in range(reps):
-                gx = one()
-            e.record()
-            torch.cuda.synchronize()
-            assert torch.isfinite(gx).all()
-            res[name] = {"ms_per_train_step": round(s.elapsed_time(e) / reps, 4),
-                         "rhs_evals_per_train_step": (func.nfe - nfe0) // reps}
+        for case in ("coauthorcs", "pubmed"):
+            blk, data, opt = _adjoint_block(case, x, ei, dev)
+            (T, ts, tsa), _ = ADJ_BLOCKS[case]
+            ent = {"config": "AttODEblock (%s best_params: heads %d, attention_dim %d, %s, norm_idx %d, add_source %s) "
+                             "on G-arxiv, dopri5 over [0, %.3f] at tol_scale %.1f, adjoint %s at tol_scale_adjoint %.1f"
+                             % (case, opt['heads'], opt['attention_dim'], opt['attention_type'],
+                                opt['attention_norm_idx'], opt['add_source'], T, ts, opt['adjoint_method'], tsa)}
+
+            def one():
+                xi = x.detach().requires_grad_(True)
+                blk.odefunc.alpha_train.grad = None
+                blk.set_x0(xi)
+                z = blk(xi, data)
+                (z * gout).sum().backward()
+                return xi.grad
+            modes = (("fused", True, True), ("direct", True, False)) + \
+                ((("autograd", False, False),) if case == "coauthorcs" else ())
+            for name, fa, faa in modes:
+                integ.FUSED_ADJOINT, integ.FUSED_ADAPTIVE_ADJOINT = fa, faa
+                one()
+                torch.cuda.synchronize()
+                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                nfe0 = blk.odefunc.nfe
+                s.record()
+                for _ in range(reps):
+                    gx = one()
+                e.record()
+                torch.cuda.synchronize()
+                assert torch.isfinite(gx).all()
+                ent[name] = {"ms_per_train_step": round(s.elapsed_time(e) / reps, 4),
+                             "rhs_evals_per_train_step": (blk.odefunc.nfe - nfe0) // reps,
+                             "backward_path": integ._OdeintAdjoint.last_path}
+                progress("adaptive adjoint %s %s: %.3f ms" % (case, name, ent[name]["ms_per_train_step"]))
+            res[case] = ent
     finally:
-        integ.FUSED_ADJOINT = saved
+        integ.FUSED_ADJOINT, integ.FUSED_ADAPTIVE_ADJOINT = saved
     return res
 
 

@@ -120,7 +120,7 @@ __device__ __forceinline__ void hub_combine(int row, int first, int nch, int C, 
   const int g = lane / GL, gl = lane % GL;
   const float a = (ep.flags & GNPDE_EPI_RHS) ? epi_alpha(ep) : 1.f;
   const float b = (ep.flags & GNPDE_ADD_SOURCE) ? *ep.beta : 0.f;
-  double dpart = 0.0;
+  double dpart[2] = {0.0, 0.0};
   for (int c0 = 0; c0 < C; c0 += GL * VEC) {
     const int cc = c0 + gl * VEC;
     const bool live = cc < C;
@@ -143,10 +143,9 @@ __device__ __forceinline__ void hub_combine(int row, int first, int nch, int C, 
     for (int o = GL; o < kWave; o <<= 1)
 #pragma unroll
       for (int t = 0; t < VEC; ++t) s[t] += __shfl_xor(s[t], o);
-    if (g == 0 && live) epilogue_store<VEC, STG, T>(ep, row, cc, s, a, b, &dpart);
+    if (g == 0 && live) epilogue_store<VEC, STG, T>(ep, row, cc, s, a, b, dpart);
   }
-  if constexpr (stage_rowsum<STG, T>())
-    if (ep.st.dot_rows || ep.st.err_rows) epi_rowsum_store<GL>(ep, row, dpart, lane == 0);  // wave-uniform
+  epi_rowsums<GL, STG, T>(ep, row, dpart, 0, lane == 0);  // wave-uniform
 }
 
 // The sum of the nch chunk partials of a hub row (slots first .. first+nch-1),
@@ -436,24 +435,22 @@ __global__ __launch_bounds__(256) void agg_kernel(const int4* __restrict__ items
   }
   const float a = (ep.flags & GNPDE_EPI_RHS) ? epi_alpha(ep) : 1.f;
   const float b = (ep.flags & GNPDE_ADD_SOURCE) ? *ep.beta : 0.f;
-  double dpart = 0.0;
+  double dpart[2] = {0.0, 0.0};
 #pragma unroll
   for (int ch = 0; ch < NCH; ++ch) {
     const int cc = (ch * GL + gl) * VEC;
     if (cc < C) {
       if constexpr (PRE)
-        epi_finish<VEC, STG, T>(ep, erow, cc, acc[ch], a, b, pre[ch], &dpart);
+        epi_finish<VEC, STG, T>(ep, erow, cc, acc[ch], a, b, pre[ch], dpart);
       else
-        epilogue_store<VEC, STG, T>(ep, erow, cc, acc[ch], a, b, &dpart);
+        epilogue_store<VEC, STG, T>(ep, erow, cc, acc[ch], a, b, dpart);
     }
   }
   // the row's owner lanes (g == 0: lanes [rs*SL, rs*SL + GL)) are all here
   if constexpr (stage_rowsum<STG, T>()) {
-    if (ep.st.dot_rows || ep.st.err_rows) {
-      const double* prev = nullptr;
-      if constexpr (PRE && stage_dot<STG>() && GNPDE_DOT_PRE) prev = &pre[0].dprev;
-      epi_rowsum_store_any<GL>(ep, erow, dpart, rs * SL, gl == 0, prev);
-    }
+    const double* prev = nullptr;
+    if constexpr (PRE && stage_dot<STG>() && GNPDE_DOT_PRE) prev = &pre[0].dprev;
+    epi_rowsums<GL, STG, T>(ep, erow, dpart, rs * SL, gl == 0, prev);
   }
 }
 

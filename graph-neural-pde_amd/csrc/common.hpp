@@ -773,7 +773,8 @@ __device__ __forceinline__ double err_terms(const gnpde_stage_epilogue_t& st, in
 
 // f = a*(ax - x) [+ b*x0]  (function_laplacian_diffusion.py:69-77) or f = ax,
 // then either store f or emit the fused Runge-Kutta stage outputs.  dpart
-// accumulates the row's dot term (STG 2, 3) or error term (STG 4) of this slice.
+// accumulates the row's dot term (STG 2, 3) or error term (STG 4) of this slice;
+// STG 4 takes dpart[2]: the error term in dpart[0], its dot term in dpart[1].
 template <int VEC, int STG, class T = float>
 __device__ __forceinline__ void epi_finish(const Epi& e, int64_t row, int cc, const float (&ax)[VEC], float a,
                                            float b, const EpiPre<VEC, T, STG>& p, double* dpart = nullptr) {
@@ -817,7 +818,17 @@ __device__ __forceinline__ void epi_finish(const Epi& e, int64_t row, int cc, co
       float y1[VEC];
 #pragma unroll
       for (int t = 0; t < VEC; ++t) y1[t] = e.st.err_y1 == 1 ? r[1][t] : (e.st.err_y1 == 0 ? r[0][t] : xv[t]);
-      *dpart += err_terms<VEC, T>(e.st, off, ev, y1, &y0v);
+      dpart[0] += err_terms<VEC, T>(e.st, off, ev, y1, &y0v);
+    }
+    // the dot term of the wide epilogue (its second row sum, dpart[1]): <f, dot_with> of the
+    // row slice, f as the other epilogues take it (after f_lin)
+    if constexpr (sizeof(T) == 4) {  // (fp32 state only: the bf16 K1 rejects dot terms)
+      if (e.st.dot_rows && dpart) {
+        Packed<VEC, T> dw;
+        load_packed<VEC>(as_t<T>(e.st.dot_with) + off, dw);
+#pragma unroll
+        for (int t = 0; t < VEC; ++t) dpart[1] = fma((double)o[t], (double)unpack(dw, t), dpart[1]);
+      }
     }
     return;
   } else {
@@ -908,9 +919,11 @@ __device__ __forceinline__ double group_sum64(double v) {
   return v;
 }
 
-// prev: the row's running dot read before the gathers (GNPDE_DOT_PRE), or nullptr
-__device__ __forceinline__ void epi_rowsum_write(const Epi& e, int64_t row, double v, const double* prev = nullptr) {
-  if (e.st.err_rows) {
+// prev: the row's running dot read before the gathers (GNPDE_DOT_PRE), or nullptr;
+// dot_ch: the dot channel whatever err_rows says (the wide epilogue's second row sum)
+__device__ __forceinline__ void epi_rowsum_write(const Epi& e, int64_t row, double v, const double* prev = nullptr,
+                                                 bool dot_ch = false) {
+  if (e.st.err_rows && !dot_ch) {
     e.st.err_rows[row] = v;
   } else if (e.st.dot_rows) {
     double* d = e.st.dot_rows + row;
@@ -925,25 +938,42 @@ __device__ __forceinline__ void epi_rowsum_write(const Epi& e, int64_t row, doub
 // (convergent).
 template <int GL>
 __device__ __forceinline__ void epi_rowsum_store(const Epi& e, int64_t row, double dpart, bool store,
-                                                 const double* prev = nullptr) {
+                                                 const double* prev = nullptr, bool dot_ch = false) {
   static_assert((GL & (GL - 1)) == 0, "the xor tree needs power-of-two row lanes");
   if constexpr (GNPDE_DOT_DIAG == 2) return;
   dpart = group_sum64<GL>(dpart);
-  if (store) epi_rowsum_write(e, row, dpart, prev);
+  if (store) epi_rowsum_write(e, row, dpart, prev, dot_ch);
 }
 
 // The same for any GL (e.g. 21 lanes: three bf16 rows of 168 columns per wavefront):
 // the first owner lane sums the slot's lanes base .. base + GL - 1 in order.
 template <int GL>
 __device__ __forceinline__ void epi_rowsum_store_any(const Epi& e, int64_t row, double dpart, int base, bool store,
-                                                     const double* prev = nullptr) {
+                                                     const double* prev = nullptr, bool dot_ch = false) {
   if constexpr ((GL & (GL - 1)) == 0) {
-    epi_rowsum_store<GL>(e, row, dpart, store, prev);
+    epi_rowsum_store<GL>(e, row, dpart, store, prev, dot_ch);
   } else {
     double tot = 0.0;
 #pragma unroll
     for (int j = 0; j < GL; ++j) tot += __shfl(dpart, base + j);
-    if (store) epi_rowsum_write(e, row, tot, prev);
+    if (store) epi_rowsum_write(e, row, tot, prev, dot_ch);
+  }
+}
+
+// The row sums of an epilogue (wave-uniform branches; called by every lane of the
+// row's slot): STG 2 / 3 the dot term (dpart[0]); STG 4 the error rows (dpart[0])
+// and the dot term (dpart[1]).
+template <int GL, int STG, class T>
+__device__ __forceinline__ void epi_rowsums(const Epi& e, int64_t row, const double* dpart, int base, bool store,
+                                            const double* prev = nullptr) {
+  if constexpr (stage_rowsum<STG, T>()) {
+    if constexpr (STG == 4) {
+      if (e.st.err_rows) epi_rowsum_store_any<GL>(e, row, dpart[0], base, store);
+      if constexpr (sizeof(T) == 4)
+        if (e.st.dot_rows) epi_rowsum_store_any<GL>(e, row, dpart[1], base, store, nullptr, true);
+    } else {
+      if (e.st.dot_rows || e.st.err_rows) epi_rowsum_store_any<GL>(e, row, dpart[0], base, store, prev);
+    }
   }
 }
 

@@ -57,8 +57,8 @@ inline int check_stage(const gnpde_stage_epilogue_t& st) {
   for (int i = 0; i < st.n_out; ++i) GNPDE_REQUIRE(st.o[i].out, GNPDE_EINVAL, "stage: output %d is NULL", i);
   GNPDE_REQUIRE(st.f_out || st.n_out > 0 || st.err_rows, GNPDE_EINVAL, "stage: the epilogue stores nothing");
   GNPDE_REQUIRE(!st.dot_rows || st.dot_with, GNPDE_EINVAL, "stage: dot_rows without dot_with");
-  GNPDE_REQUIRE(!(st.dot_rows && st.err_rows), GNPDE_EINVAL, "stage: dot_rows and err_rows together");
-  GNPDE_REQUIRE(!st.dot_rows || st.nk <= 2, GNPDE_EUNSUPPORTED, "stage: dot_rows with more than 2 operands");
+  // a dot term beside error rows or more than kStagePre operands: the wide epilogue (STG 4)
+  // carries it as a second row sum (the adaptive adjoint's alpha integrand, gnpde.integrator)
   if (st.err_rows) {
     GNPDE_REQUIRE(st.err_y0 != nullptr, GNPDE_EINVAL, "stage: err_rows without err_y0");
     GNPDE_REQUIRE(st.err_y1 >= -1 && st.err_y1 < st.n_out, GNPDE_EINVAL, "stage: err_y1=%d names no output",

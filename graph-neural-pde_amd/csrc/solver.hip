@@ -485,6 +485,96 @@ extern "C" int gnpde_initial_step_bf16(int64_t n, const uint16_t* y0, const uint
                             stream);
 }
 
+// The two squared sums of init_step_partial_kernel, stored as they are (the mixed norm
+// of the adjoint's augmented state combines them per component on the host)
+__global__ __launch_bounds__(256) void pair_sum_final_kernel(const double* __restrict__ part, int nb,
+                                                              double* __restrict__ out) {
+  __shared__ double red[kBlock / kWave];
+  double a0 = 0.0, a1 = 0.0;
+  for (int i = threadIdx.x; i < nb; i += blockDim.x) {
+    a0 += part[2 * i];
+    a1 += part[2 * i + 1];
+  }
+  const double s0 = block_sum_f64(a0, red);
+  __syncthreads();
+  const double s1 = block_sum_f64(a1, red);
+  if (threadIdx.x == 0) {
+    out[0] = s0;
+    out[1] = s1;
+  }
+}
+
+extern "C" int gnpde_scaled_sq_sums_f32(int64_t n, const float* y0, const float* f0, const float* f1, double atol,
+                                        double rtol, double* out, void* workspace, size_t ws_bytes, void* stream) {
+  GNPDE_REQUIRE(n >= 1 && y0 && f0 && out && workspace, GNPDE_EINVAL, "scaled_sq_sums: bad arguments");
+  GNPDE_REQUIRE(ws_bytes >= 2 * sizeof(double) * kDotBlocks, GNPDE_EINVAL, "scaled_sq_sums: workspace too small");
+  hipStream_t s = as_stream(stream);
+  double* part = static_cast<double*>(workspace);
+  const float a = (float)atol, r = (float)rtol;
+  auto al = [&](const void* p) { return p == nullptr || reinterpret_cast<uintptr_t>(p) % 16 == 0; };
+  const bool v4 = n % 4 == 0 && al(y0) && al(f0) && al(f1);
+  if (f1 == nullptr) {
+    if (v4)
+      init_step_partial_kernel<float, 4, 0><<<kDotBlocks, kBlock, 0, s>>>(n, y0, f0, f1, a, r, part);
+    else
+      init_step_partial_kernel<float, 1, 0><<<kDotBlocks, kBlock, 0, s>>>(n, y0, f0, f1, a, r, part);
+  } else {
+    if (v4)
+      init_step_partial_kernel<float, 4, 1><<<kDotBlocks, kBlock, 0, s>>>(n, y0, f0, f1, a, r, part);
+    else
+      init_step_partial_kernel<float, 1, 1><<<kDotBlocks, kBlock, 0, s>>>(n, y0, f0, f1, a, r, part);
+  }
+  GNPDE_LAUNCH_CHECK();
+  pair_sum_final_kernel<<<1, kBlock, 0, s>>>(part, kDotBlocks, out);
+  GNPDE_LAUNCH_CHECK();
+  return GNPDE_OK;
+}
+
+// Segment sums: kSegSumBlocks blocks per segment (blockIdx.y = segment), each thread
+// summing a fixed stride of its segment in order, a fixed tree per block, then one
+// block per segment summing its block partials in order (deterministic).
+constexpr int kSegSumBlocks = 128;
+
+__global__ __launch_bounds__(256) void seg_sum_partial_kernel(int64_t len, const double* __restrict__ v,
+                                                               double* __restrict__ part) {
+  __shared__ double red[kBlock / kWave];
+  const double* seg = v + (int64_t)blockIdx.y * len;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  double acc = 0.0;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < len; i += stride) acc += seg[i];
+  const double t = block_sum_f64(acc, red);
+  if (threadIdx.x == 0) part[(int64_t)blockIdx.y * gridDim.x + blockIdx.x] = t;
+}
+
+__global__ __launch_bounds__(256) void seg_sum_final_kernel(const double* __restrict__ part, int nb,
+                                                             double* __restrict__ out) {
+  __shared__ double red[kBlock / kWave];
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < nb; i += blockDim.x) acc += part[(int64_t)blockIdx.x * nb + i];
+  const double t = block_sum_f64(acc, red);
+  if (threadIdx.x == 0) out[blockIdx.x] = t;
+}
+
+extern "C" size_t gnpde_segment_sums_workspace_bytes(int64_t nseg) {
+  return sizeof(double) * (size_t)kSegSumBlocks * (size_t)(nseg > 0 ? nseg : 0);
+}
+
+extern "C" int gnpde_segment_sums_f64(int64_t nseg, int64_t len, const double* v, double* out, void* workspace,
+                                      size_t workspace_bytes, void* stream) {
+  GNPDE_REQUIRE(nseg >= 0 && nseg <= 65535 && len >= 0 && out && workspace && (v || nseg * len == 0), GNPDE_EINVAL,
+                "segment_sums: bad arguments");
+  GNPDE_REQUIRE(workspace_bytes >= gnpde_segment_sums_workspace_bytes(nseg), GNPDE_EINVAL,
+                "segment_sums: workspace too small");
+  if (nseg == 0) return GNPDE_OK;
+  hipStream_t s = as_stream(stream);
+  double* part = static_cast<double*>(workspace);
+  seg_sum_partial_kernel<<<dim3(kSegSumBlocks, (unsigned)nseg), kBlock, 0, s>>>(len, v, part);
+  GNPDE_LAUNCH_CHECK();
+  seg_sum_final_kernel<<<(unsigned)nseg, kBlock, 0, s>>>(part, kSegSumBlocks, out);
+  GNPDE_LAUNCH_CHECK();
+  return GNPDE_OK;
+}
+
 // torchdiffeq's step-size controller (rk_common.py _optimal_step_size, the adaptive
 // loop's accept test) on the device, fused with the last level of the step's error
 // reduction (the same fixed order as gnpde_sum_f64): the host reads rec = {error

@@ -77,6 +77,9 @@ SIGNATURES = {
     "gnpde_initial_step_workspace_bytes": (_size, []),
     "gnpde_adaptive_control": (_int, [_i64, _vp, _f64, _f64, _f64, _f64, _f64, _vp, _vp, _vp, _vp, _size, _vp]),
     "gnpde_initial_step_f32": (_int, [_i64, _vp, _vp, _vp, _f64, _f64, _f64, _vp, _vp, _vp, _size, _vp]),
+    "gnpde_scaled_sq_sums_f32": (_int, [_i64, _vp, _vp, _vp, _f64, _f64, _vp, _vp, _size, _vp]),
+    "gnpde_segment_sums_workspace_bytes": (_size, [_i64]),
+    "gnpde_segment_sums_f64": (_int, [_i64, _i64, _vp, _vp, _vp, _size, _vp]),
     "gnpde_initial_step_bf16": (_int, [_i64, _vp, _vp, _vp, _f64, _f64, _f64, _vp, _vp, _vp, _size, _vp]),
     "gnpde_stage_apply_f32": (_int, [_i64, _i64, _i64, _vp, _vp, ctypes.POINTER(StageEpilogue), _vp]),
     "gnpde_stage_apply_bf16": (_int, [_i64, _i64, _i64, _vp, _vp, ctypes.POINTER(StageEpilogue), _vp]),
@@ -125,7 +128,7 @@ SIGNATURES = {
 }
 
 # constants mirrored from include/gnpde.h
-ABI_VERSION = 6
+ABI_VERSION = 7
 OK = 0
 EINVAL = -1
 EHIP = -2

@@ -78,6 +78,10 @@ class LaplacianODEFunc(ODEFunc):
         self.d = nn.Parameter(torch.zeros(opt['hidden_dim']) + 1)
         self.alpha_sc = nn.Parameter(torch.ones(1))
         self.beta_sc = nn.Parameter(torch.ones(1))
+        # set by integrator._OdeintAdjoint's backward while the weights are a constant of it
+        # (adjoint_direct_ok): forward() then hands autograd the detached weights, so its
+        # vector-Jacobian products form no weight gradient (the SDDMM) only to drop it
+        self.adjoint_const_weights = False
         if opt.get('multi_modal', False):
             raise NotImplementedError("gnpde: multi_modal is broken in the reference (torch.nn.softmax, "
                                       "function_laplacian_diffusion.py:63) and out of scope")
@@ -106,6 +110,18 @@ class LaplacianODEFunc(ODEFunc):
         blocks training through the weights) keeps the per-RHS autograd path."""
         w, _ = self._weights_tensor()
         return not w.requires_grad
+
+    def adjoint_direct_ok(self, adjoint_params):
+        """The adjoint's augmented RHS may be evaluated by K1 launches (integrator.
+        _LaplacianAdjointFn, _laplacian_aug) when the weights are not an adjoint
+        parameter.  torchdiffeq's odeint_adjoint propagates into y0 and
+        adjoint_params only (its forward runs under no_grad; the backward takes
+        vector-Jacobian products with respect to those tensors alone), so a weight
+        tensor the RHS closes over — AttODEblock's attention (src/block_transformer_
+        attention.py:40-50), requiring grad in training — is a constant of the
+        backward, exactly as upstream: its gradient from the ODE is dropped there too."""
+        w, _ = self._weights_tensor()
+        return all(p is not w for p in adjoint_params)
 
     def supports_node_layout(self):
         """Weights are per edge in COO order, x0 per node: the fixed-grid
@@ -176,6 +192,7 @@ class LaplacianODEFunc(ODEFunc):
                 raise NotImplementedError("gnpde: bf16 state is inference-only; run under torch.no_grad()")
             return ops.spmm_rhs(g, w_csr, x, x0=x0, alpha=self.alpha_train.detach(), beta=self.beta_train.detach(),
                                 rhs=True, alpha_sigmoid=alpha_sigmoid, add_source=add_source)
-        return _LaplacianRHS.apply(x, self.alpha_train, self.beta_train, w, g, w_csr,
+        w_src = w.detach() if self.adjoint_const_weights else w
+        return _LaplacianRHS.apply(x, self.alpha_train, self.beta_train, w_src, g, w_csr,
                                    lambda: self.csr_weights(g, w, tag, transpose=True), x0, alpha_sigmoid,
                                    add_source)

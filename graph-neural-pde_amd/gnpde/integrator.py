@@ -1826,8 +1826,8 @@ def _laplacian_aug(func, params, y_shape, ny, ans):
     parameters' components are 0.  For the adaptive adjoint methods (torchdiffeq's
     solver loop, the mixed norm); the fixed-grid rk4 adjoint runs _LaplacianAdjointFn.
     None when the RHS is not the HIP Laplacian on a device fp32 state."""
-    fn = getattr(func, 'fixed_grid_backward_ok', None)
-    if not (FUSED_ADJOINT and fn is not None and fn() and hasattr(func, 'rhs_stage')) or \
+    fn = getattr(func, 'adjoint_direct_ok', None)
+    if not (FUSED_ADJOINT and fn is not None and fn(params) and hasattr(func, 'rhs_stage')) or \
             func.opt.get('no_alpha_sigmoid', False) or not ans.is_cuda or ans.dtype != torch.float32 or \
             len(y_shape) != 3:
         return None
@@ -1875,6 +1875,26 @@ def _laplacian_aug(func, params, y_shape, ny, ans):
     return aug
 
 
+FUSED_ADAPTIVE_ADJOINT = os.environ.get('GNPDE_FUSED_ADAPTIVE_ADJOINT', '1') != '0'
+
+
+def _adaptive_adjoint_ok(func, ans, a_method, params, a_options):
+    """The adaptive adjoint of a Laplacian RHS runs fused (gnpde.adjoint_adaptive): an
+    adaptive adjoint method with torchdiffeq's default adjoint norm (no user 'norm'),
+    a device fp32 state, weights that are not adjoint parameters, the sigmoid alpha,
+    and adjoint parameters among the module's own."""
+    if not (FUSED_ADJOINT and FUSED_ADAPTIVE_ADJOINT and a_method in ADAPTIVE_METHODS) or \
+            'norm' in (a_options or {}):
+        return False
+    if not (ans.is_cuda and ans.dtype == torch.float32 and ans.dim() == 4):
+        return False
+    fn = getattr(func, 'adjoint_direct_ok', None)
+    if fn is None or not fn(params) or func.opt.get('no_alpha_sigmoid', False) or not hasattr(func, 'rhs_stage'):
+        return False
+    own = {id(p) for p in func.parameters()}
+    return all(id(p) in own for p in params)
+
+
 class _OdeintAdjoint(torch.autograd.Function):
     """torchdiffeq.odeint_adjoint (0.2.x OdeintAdjointMethod) restated: the
     forward integrates without recording; the backward integrates the augmented
@@ -1899,6 +1919,20 @@ class _OdeintAdjoint(torch.autograd.Function):
         func, _rtol, _atol, _method, _options, a_rtol, a_atol, a_method, a_options = ctx.cfg
         t, ans = ctx.saved_tensors
         params = ctx.params
+        if _adaptive_adjoint_ok(func, ans, a_method, params, a_options):
+            # the Laplacian's adaptive adjoint, fused (gnpde.adjoint_adaptive): the same loop with the
+            # packed state's stage combinations, error rows and alpha integrand in the K1 epilogues
+            from .adjoint_adaptive import AdaptiveAdjoint
+            with torch.no_grad():
+                solver = AdaptiveAdjoint(func, params, a_method, a_rtol, a_atol, a_options)
+                gy, pg = solver.run(_host_times(t), ans, grad_y)
+            _OdeintAdjoint.last_path = 'fused_adaptive'
+            out = []
+            for p in params:
+                v = pg.get(id(p))
+                out.append(torch.zeros_like(p) if v is None else
+                           torch.full(p.shape, v, dtype=p.dtype, device=p.device))
+            return (gy.view(grad_y.shape[1:]).to(grad_y.dtype), None, None) + tuple(out)
         y_shape = ans.shape[1:]
         ny = ans[0].numel()
         sizes = [ny, ny] + [p.numel() for p in params]
@@ -1918,24 +1952,38 @@ class _OdeintAdjoint(torch.autograd.Function):
             return -pack(f.detach(), vjp_y, vjp_p)  # d/ds = -d/dt
 
         # the Laplacian's vector-Jacobian products by K1 launches (no autograd), else autograd's
-        aug = _laplacian_aug(func, params, y_shape, ny, ans) or aug_autograd
+        aug = _laplacian_aug(func, params, y_shape, ny, ans)
+        _OdeintAdjoint.last_path = 'direct_aug' if aug is not None else 'autograd'
+        aug = aug or aug_autograd
         opts = dict(a_options or {})
         if a_method in ADAPTIVE_METHODS and 'norm' not in opts:
             opts['norm'] = _mixed_norm_fn(sizes)
         ay = grad_y[-1]
         ap = [torch.zeros_like(p) for p in params]
-        with torch.no_grad():
-            for i in range(len(t) - 1, 0, -1):
-                z0 = pack(ans[i], ay, ap)
-                s = torch.stack([-t[i], -t[i - 1]])
-                z1 = odeint(aug, z0, s, rtol=a_rtol, atol=a_atol, method=a_method, options=opts)[1]
-                ay = z1[ny:2 * ny].view(y_shape).to(grad_y.dtype) + grad_y[i - 1]
-                o = 2 * ny
-                ap = []
-                for p in params:
-                    ap.append(z1[o:o + p.numel()].view(p.shape).to(p.dtype))
-                    o += p.numel()
+        # weights the RHS closes over are constants of the backward (torchdiffeq: VJPs w.r.t. y and
+        # adjoint_params only): the autograd VJPs see them detached
+        const_w = hasattr(func, 'adjoint_const_weights') and func.adjoint_direct_ok(params)
+        try:
+            if const_w:
+                func.adjoint_const_weights = True
+            with torch.no_grad():
+                for i in range(len(t) - 1, 0, -1):
+                    z0 = pack(ans[i], ay, ap)
+                    s = torch.stack([-t[i], -t[i - 1]])
+                    z1 = odeint(aug, z0, s, rtol=a_rtol, atol=a_atol, method=a_method, options=opts)[1]
+                    ay = z1[ny:2 * ny].view(y_shape).to(grad_y.dtype) + grad_y[i - 1]
+                    o = 2 * ny
+                    ap = []
+                    for p in params:
+                        ap.append(z1[o:o + p.numel()].view(p.shape).to(p.dtype))
+                        o += p.numel()
+        finally:
+            if const_w:
+                func.adjoint_const_weights = False
         return (ay, None, None) + tuple(ap)
+
+
+_OdeintAdjoint.last_path = None  # which backward the last one ran: 'fused_adaptive', 'direct_aug' or 'autograd'
 
 
 # Fused continuous adjoint of the Laplacian RHS (src/base_classes.py:45-49 with opt['adjoint'],
@@ -1972,8 +2020,9 @@ def _fused_adjoint_ok(func, y0, adjoint_method, adjoint_params):
     if not (FUSED_ADJOINT and adjoint_method == 'rk4' and y0.is_cuda and y0.dtype == torch.float32 and
             y0.dim() == 3):
         return False
-    fn = getattr(func, 'fixed_grid_backward_ok', None)
-    if fn is None or not fn() or func.opt.get('no_alpha_sigmoid', False) or not hasattr(func, 'rhs_stage'):
+    fn = getattr(func, 'adjoint_direct_ok', None)
+    if fn is None or not fn(adjoint_params) or func.opt.get('no_alpha_sigmoid', False) or \
+            not hasattr(func, 'rhs_stage'):
         return False
     own = {id(p) for p in func.parameters()}
     return all(id(p) in own for p in adjoint_params)

@@ -1286,15 +1286,21 @@ def segment_sum(grouped, vals):
     return out
 
 
-def dot(a, b):
+def dot(a, b, out=None):
     """<a, b> of two fp32 device tensors of the same size, accumulated in fp64
-    (gnpde_dot_f64, fixed order): 0-d float64 tensor on the device."""
+    (gnpde_dot_f64, fixed order): 0-d float64 tensor on the device (``out``: a
+    one-element fp64 device tensor, e.g. a slot of a record, written in place)."""
     _require_gpu(a, "a", torch.float32)
     _require_gpu(b, "b", torch.float32)
     if a.numel() != b.numel():
         raise ValueError("dot: sizes differ (%d, %d)" % (a.numel(), b.numel()))
     a, b = a.contiguous(), b.contiguous()
-    out = torch.empty((), dtype=torch.float64, device=a.device)
+    if out is None:
+        out = torch.empty((), dtype=torch.float64, device=a.device)
+    else:
+        _require_gpu(out, "dot out", torch.float64)
+        if out.numel() != 1:
+            raise ValueError("dot: out must hold one fp64")
     nbytes = _lib.fn("gnpde_dot_workspace_bytes")()
     ws = torch.empty(nbytes, dtype=torch.uint8, device=a.device)
     _lib.call("gnpde_dot_f64", a.numel(), _ptr(a), _ptr(b), _ptr(out), _ptr(ws), nbytes, _stream(a.device))
@@ -1313,6 +1319,39 @@ def sum_f64(v, out=None, accumulate=False):
     _lib.call("gnpde_sum_f64", v.numel(), _ptr(v), _ptr(out), int(bool(accumulate)), _ptr(ws), nbytes,
               _stream(v.device))
     return out
+
+
+def scaled_sq_sums(y0, f0, f1, atol, rtol, out):
+    """The squared sums of the initial-step selection for one component of a mixed
+    norm (gnpde_scaled_sq_sums_f32): f1 None -> out[0] = sum (y0/sc)^2, out[1] =
+    sum (f0/sc)^2; else out[0] = sum ((f1 - f0)/sc)^2; sc = atol + |y0| rtol.
+    out: fp64 device [2] (a view is fine)."""
+    for t in (y0, f0) + ((f1,) if f1 is not None else ()):
+        _require_gpu(t, "scaled_sq_sums operand", torch.float32)
+        if not t.is_contiguous() or t.numel() != y0.numel():
+            raise ValueError("scaled_sq_sums: operands must be contiguous and shaped alike")
+    _require_gpu(out, "scaled_sq_sums out", torch.float64)
+    if out.numel() < 2 or not out.is_contiguous():
+        raise ValueError("scaled_sq_sums: out needs 2 contiguous doubles")
+    nbytes = _lib.fn("gnpde_initial_step_workspace_bytes")()
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=y0.device)
+    _lib.call("gnpde_scaled_sq_sums_f32", y0.numel(), _ptr(y0), _ptr(f0), _ptr(f1), float(atol), float(rtol),
+              _ptr(out), _ptr(ws), nbytes, _stream(y0.device))
+
+
+def segment_sums(v, out):
+    """out[s] = sum of row s of the fp64 device matrix v [nseg, len] (gnpde_segment_sums_f64,
+    fixed order per segment): several epilogue row channels reduced in one pass."""
+    _require_gpu(v, "segment_sums v", torch.float64)
+    _require_gpu(out, "segment_sums out", torch.float64)
+    if v.dim() != 2 or not v.is_contiguous():
+        raise ValueError("segment_sums: v must be a contiguous [nseg, len] matrix")
+    if out.numel() < v.shape[0] or not out.is_contiguous():
+        raise ValueError("segment_sums: out needs nseg contiguous doubles")
+    nbytes = _lib.fn("gnpde_segment_sums_workspace_bytes")(v.shape[0])
+    ws = torch.empty(max(nbytes, 8), dtype=torch.uint8, device=v.device)
+    _lib.call("gnpde_segment_sums_f64", v.shape[0], v.shape[1], _ptr(v), _ptr(out), _ptr(ws), nbytes,
+              _stream(v.device))
 
 
 def initial_step(y0, f0, f1, atol, rtol, order, h, hf=None):

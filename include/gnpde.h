@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define GNPDE_ABI_VERSION 6
+#define GNPDE_ABI_VERSION 7
 
 #define GNPDE_OK 0
 #define GNPDE_EINVAL (-1)
@@ -214,8 +214,11 @@ size_t gnpde_plan_workspace_bytes(int64_t R);
  * operands already carry the step size, e.g. the next step's f0 = sum_p B[p] u_p
  * of the affine Krylov step (u_p = (h L)^p f0, gnpde.integrator).
  * A k operand (or base) equal to the RHS input x reuses the row already read.
- * At most 2 k operands with dot_rows; err_rows and 3..6 operands take the wide
- * epilogue (operands loaded after the aggregation), fused into the plain-weight
+ * err_rows and 3..6 operands take the wide epilogue (operands loaded after the
+ * aggregation); since ABI 7 it carries dot_rows too, beside err_rows or with up to
+ * 6 operands (a second fp64 row sum: the adaptive adjoint's alpha integrand
+ * <L^T a_i, y_i> in the launch that forms the next adjoint stage input and its
+ * error rows, gnpde.integrator), fused into the plain-weight
  * K1 (gnpde_spmm_rhs_f32 / _bf16); the attention kernels return
  * GNPDE_EUNSUPPORTED for it (the caller applies it with gnpde_stage_apply_*).  */
 #define GNPDE_STAGE_MAX_OUT 2
@@ -568,6 +571,22 @@ int gnpde_adaptive_control(int64_t nrows, const double* err_rows, double n, doub
                            double ifactor, double dfactor, double* dt, float* scale, double* rec, void* workspace,
                            size_t workspace_bytes, void* stream);
 size_t gnpde_initial_step_workspace_bytes(void);
+/* The squared sums of gnpde_initial_step_f32 without its scalar rules (ABI 7): the
+ * per-component pieces of a mixed norm (torchdiffeq's adjoint norm: the max over the
+ * components [y | adj_y | adj_params] of their RMS norms), the caller combining them:
+ *   f1 == NULL: out[0] = sum (y0/scale)^2, out[1] = sum (f0/scale)^2
+ *   else:       out[0] = sum ((f1 - f0)/scale)^2, out[1] = 0
+ * scale = atol + |y0| rtol in fp32, squares in fp64, the fixed order of
+ * gnpde_initial_step_f32.  Workspace gnpde_initial_step_workspace_bytes().     */
+int gnpde_scaled_sq_sums_f32(int64_t n, const float* y0, const float* f0, const float* f1, double atol, double rtol,
+                             double* out, void* workspace, size_t workspace_bytes, void* stream);
+/* out[s] = sum_{i < len} v[s*len + i] for s < nseg (ABI 7): the row sums of several
+ * epilogue channels of one adaptive step (the y and adjoint error rows, the alpha
+ * integrand's rows of every stage) in one pass, each in a fixed order
+ * (deterministic).  Workspace gnpde_segment_sums_workspace_bytes(nseg).        */
+size_t gnpde_segment_sums_workspace_bytes(int64_t nseg);
+int gnpde_segment_sums_f64(int64_t nseg, int64_t len, const double* v, double* out, void* workspace,
+                           size_t workspace_bytes, void* stream);
 int gnpde_initial_step_f32(int64_t n, const float* y0, const float* f0, const float* f1, double atol, double rtol,
                            double order, double* h, float* hf, void* workspace, size_t workspace_bytes, void* stream);
 int gnpde_initial_step_bf16(int64_t n, const uint16_t* y0, const uint16_t* f0, const uint16_t* f1, double atol,

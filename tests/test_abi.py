@@ -46,7 +46,7 @@ def test_library_built_from_these_sources():
 
 
 def test_abi_version():
-    assert _lib.load().gnpde_abi_version() == _lib.ABI_VERSION == 6
+    assert _lib.load().gnpde_abi_version() == _lib.ABI_VERSION == 7
 
 
 def test_library_is_gfx950_code_object():
