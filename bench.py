@@ -1111,83 +1111,110 @@ def _train_adaptive_adjoint(ei, x, gout, dev, reps):
     return res
 
 
+# HardAttODEblock best_params (src/best_params.py:5,7): ogbn-arxiv (heads 2, attention_dim 32, att_samp_pct 0.81,
+# adjoint rk4 step 1) and Computers (heads 4, attention_dim 64, att_samp_pct 0.573, adjoint dopri5)
+HARD_BLOCKS = {
+    "arxiv": dict(T=ARXIV_DOPRI5[0], tol_scale=ARXIV_DOPRI5[1], heads=2, attention_dim=32,
+                  att_samp_pct=0.8105268910037231, adjoint_method='rk4', tol_scale_adjoint=1.0),
+    "computers": dict(T=3.249016177876166, tol_scale=127.46369887079446, heads=4, attention_dim=64,
+                      att_samp_pct=0.572918052062338, adjoint_method='dopri5', tol_scale_adjoint=443.81436775321754),
+}
+
+
 def bench_hard_attention_train(ei, x, dev, reps=3):
-    """The ogbn-arxiv best_params block in training mode (src/best_params.py:7: block hard_attention, heads 2,
-    attention_dim 32, attention_norm_idx 0, scaled_dot, att_samp_pct 0.8105, dopri5 over [0, 3.676] at tol_scale
-    11353.6, adjoint rk4 with step 1; src/block_transformer_hard_attention.py:37-99) on G-arxiv (C = 128):
-    one training forward — block attention, quantile threshold, sampling mask, group renormalisation, the
-    dopri5 solve — and the training step with its adjoint backward.  The sampled graph is the full CSR with
-    zero weights on the dropped edges (gnpde_threshold_mask_f32): no per-forward graph rebuild."""
+    """HardAttODEblock in training mode as best_params runs it (src/block_transformer_hard_attention.py:37-99) on
+    G-arxiv (C = 128) at ogbn-arxiv's and Computers' parameters: one training forward — block attention, quantile
+    threshold, sampling mask, group renormalisation, the dopri5 solve — and the training step with its adjoint
+    backward.  The sampled graph reuses the full graph's CSR and plans: K1 gathers the retained edges only,
+    compacted inside the plan's items on the device (gnpde_compact_items_f32, ops.CompactWeights); the forward is
+    also timed over the masked full graph (GNPDE_COMPACT_SAMPLED=0) for comparison."""
+    import contextlib
+    import io
+
     import gnpde
+    import gnpde.base_classes as bc
     C = x.shape[-1]
     N = x.shape[1]
-    T, ts = ARXIV_DOPRI5
-    opt = dict(LAP_OPT, hidden_dim=C, block='hard_attention', function='laplacian', heads=2, attention_dim=32,
-               attention_norm_idx=0, attention_type='scaled_dot', att_samp_pct=0.8105268910037231, method='dopri5',
-               step_size=1, tol_scale=ts, adjoint=True, adjoint_method='rk4', adjoint_step_size=1,
-               tol_scale_adjoint=1.0, max_iters=100, self_loop_weight=1.0, data_norm='rw', leaky_relu_slope=0.2,
-               reweight_attention=False, square_plus=False, mix_features=False, beltrami=False, use_flux=False,
-               augment=False)
-    blk = gnpde.HardAttODEblock(gnpde.LaplacianODEFunc, [], opt, dev,
-                                t=torch.tensor([0.0, T], device=dev)).to(dev).train()
-    data = gnpde.GraphData()
     raw = ei[:, :, :ei.shape[2] - N]  # synthetic.rw_graph appended N self loops; the block adds its own
+    data = gnpde.GraphData()
     data.new_graph(raw, N)
     gen = torch.Generator(device=dev)
     gen.manual_seed(13)
     gout = torch.randn(x.shape, generator=gen, device=dev)
-    import contextlib
-    import io
+    out = {}
+    for case, prm in HARD_BLOCKS.items():
+        T = prm['T']
+        opt = dict(LAP_OPT, hidden_dim=C, block='hard_attention', function='laplacian', heads=prm['heads'],
+                   attention_dim=prm['attention_dim'], attention_norm_idx=0, attention_type='scaled_dot',
+                   att_samp_pct=prm['att_samp_pct'], method='dopri5', step_size=1, tol_scale=prm['tol_scale'],
+                   adjoint=True, adjoint_method=prm['adjoint_method'], adjoint_step_size=1,
+                   tol_scale_adjoint=prm['tol_scale_adjoint'], max_iters=100, self_loop_weight=1.0, data_norm='rw',
+                   leaky_relu_slope=0.2, reweight_attention=False, square_plus=False, mix_features=False,
+                   beltrami=False, use_flux=False, augment=False)
+        torch.manual_seed(19)
+        blk = gnpde.HardAttODEblock(gnpde.LaplacianODEFunc, [], opt, dev,
+                                    t=torch.tensor([0.0, T], device=dev)).to(dev).train()
 
-    def fwd():
-        blk.set_x0(x)
-        with contextlib.redirect_stdout(io.StringIO()):  # the reference's 'retaining ...' line per forward
-            return blk(x, data)
+        def fwd():
+            blk.set_x0(x)
+            with contextlib.redirect_stdout(io.StringIO()):  # the reference's 'retaining ...' line per forward
+                return blk(x, data)
 
-    def sample():
-        with contextlib.redirect_stdout(io.StringIO()):
-            blk.sample_edges(x)
+        def sample():
+            with contextlib.redirect_stdout(io.StringIO()):
+                blk.sample_edges(x)
 
-    def step():
-        xi = x.detach().requires_grad_(True)
-        blk.set_x0(xi)
-        with contextlib.redirect_stdout(io.StringIO()):
-            z = blk(xi, data)
-        (z * gout).sum().backward()
-        return xi.grad
+        def step():
+            xi = x.detach().requires_grad_(True)
+            blk.set_x0(xi)
+            with contextlib.redirect_stdout(io.StringIO()):
+                z = blk(xi, data)
+            (z * gout).sum().backward()
+            return xi.grad
 
-    def timed(fn, with_grad):
-        for _ in range(2):
-            if with_grad:
-                fn()
-            else:
-                with torch.no_grad():
+        def timed(fn, with_grad):
+            for _ in range(2):
+                if with_grad:
                     fn()
-        torch.cuda.synchronize()
-        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        s.record()
-        for _ in range(reps):
-            if with_grad:
-                fn()
-            else:
-                with torch.no_grad():
+                else:
+                    with torch.no_grad():
+                        fn()
+            torch.cuda.synchronize()
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(reps):
+                if with_grad:
                     fn()
-        e.record()
-        torch.cuda.synchronize()
-        return s.elapsed_time(e) / reps
+                else:
+                    with torch.no_grad():
+                        fn()
+            e.record()
+            torch.cuda.synchronize()
+            return s.elapsed_time(e) / reps
 
-    ms_fwd = timed(fwd, False)
-    ms_sample = timed(sample, False)
-    ms_step = timed(step, True)
-    return {"config": "HardAttODEblock.forward (training), ogbn-arxiv best_params on G-arxiv (C=128): heads 2, "
-                      "attention_dim 32, att_samp_pct 0.81, dopri5 over [0, %.3f], adjoint rk4 step 1" % T,
-            "ms_per_forward": round(ms_fwd, 4), "ms_sampling": round(ms_sample, 4),
-            "sampling_share": round(ms_sample / ms_fwd, 4), "graph_rebuild_ms": 0.0,
-            "retained_edges": int(blk.retained), "edges": int(raw.shape[2] + N),
-            "ms_per_train_step": round(ms_step, 4),
-            "basis": "sampling = block attention + head mean + quantile + threshold mask + group renormalisation "
-                     "(one host read for the reference's 'retaining' line); the sampled graph reuses the full "
-                     "graph's CSR / plans with zero weights (no rebuild)"}
+        ms_fwd = timed(fwd, False)
+        ms_sample = timed(sample, False)
+        ms_step = timed(step, True)
+        saved = bc.COMPACT_SAMPLED
+        try:
+            bc.COMPACT_SAMPLED = False
+            ms_fwd_masked = timed(fwd, False)
+        finally:
+            bc.COMPACT_SAMPLED = saved
+        out[case] = {"config": "HardAttODEblock.forward (training), %s best_params on G-arxiv (C=128): heads %d, "
+                               "attention_dim %d, att_samp_pct %.3f, dopri5 over [0, %.3f] at tol_scale %.1f, adjoint %s"
+                               % (case, prm['heads'], prm['attention_dim'], prm['att_samp_pct'], T, prm['tol_scale'],
+                                  prm['adjoint_method']),
+                     "ms_per_forward": round(ms_fwd, 4), "ms_per_forward_masked_full_graph": round(ms_fwd_masked, 4),
+                     "ms_sampling": round(ms_sample, 4), "sampling_share": round(ms_sample / ms_fwd, 4),
+                     "graph_rebuild_ms": 0.0, "retained_edges": int(blk.retained), "edges": int(raw.shape[2] + N),
+                     "ms_per_train_step": round(ms_step, 4)}
+        progress("hard attention %s: forward %.3f (masked %.3f) ms, step %.3f ms" % (case, ms_fwd, ms_fwd_masked,
+                                                                                    ms_step))
+    out["basis"] = ("sampling = block attention + head mean + quantile + threshold mask + group renormalisation (one "
+                    "host read for the reference's 'retaining' line); the sampled graph reuses the full graph's CSR / "
+                    "plans, its retained edges compacted inside the plan's items on the device (no rebuild)")
+    return out
 
 
 def cpu_baseline(ei, w, x, N, E, C, budget_s):

@@ -88,6 +88,39 @@ __global__ void threshold_mask_kernel(const float* __restrict__ v, int64_t n, co
   }
 }
 
+// The sampled graph of hard attention in the plan's own structure: every work item
+// (row, edge_begin, edge_end, slot) keeps its row, slot and edge_begin, and its
+// edges with a nonzero weight are moved to the front of its range in their order
+// (a stable partition by ballot, one wavefront per item), edge_end shrinking to
+// edge_begin + the kept count.  The aggregation then gathers only retained edges,
+// in the order and hub chunks of the full plan: the same sums as over the masked
+// full graph (a dropped edge added an exact 0), no plan rebuild and no host read.
+__global__ __launch_bounds__(256) void compact_items_kernel(const int4* __restrict__ items, int n_items,
+                                                            const int* __restrict__ col, const float* __restrict__ w,
+                                                            int* __restrict__ col_out, float* __restrict__ w_out,
+                                                            int4* __restrict__ items_out) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int item = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+  if (item >= n_items) return;
+  const int4 it = items[item];
+  int kept = 0;
+  for (int e0 = it.y; e0 < it.z; e0 += kWave) {
+    const int p = e0 + lane;
+    const bool live = p < it.z;
+    const float v = live ? w[p] : 0.f;
+    const int c = live ? col[p] : 0;
+    const bool keep = live && v != 0.f;
+    const unsigned long long m = __ballot(keep);
+    const int before = __popcll(m & ((1ull << lane) - 1ull));
+    if (keep) {
+      col_out[it.y + kept + before] = c;
+      w_out[it.y + kept + before] = v;
+    }
+    kept += __popcll(m);
+  }
+  if (lane == 0) items_out[item] = make_int4(it.x, it.y, it.y + kept, it.w);
+}
+
 // torch.quantile(v, q) (linear interpolation) on a sorted copy:
 // rank = q*(n-1) in fp32, lo = floor, hi = ceil, w = rank - lo,
 // lerp(a, b, w) = w < 0.5 ? a + w (b - a) : b - (b - a)(1 - w)   (ATen's lerp).
@@ -161,6 +194,21 @@ int gnpde_threshold_mask_f32(const float* v, int64_t n, const float* thr, float*
   const int64_t blocks = ceil_div(n, kBlock);
   threshold_mask_kernel<<<(int)(blocks < kMaskBlocks ? blocks : kMaskBlocks), kBlock, 0, s>>>(
       v, n, thr, out, reinterpret_cast<unsigned long long*>(count));
+  GNPDE_LAUNCH_CHECK();
+  return GNPDE_OK;
+}
+
+int gnpde_compact_items_f32(const int32_t* items, int64_t n_items, const int32_t* col, const float* w,
+                            int32_t* col_out, float* w_out, int32_t* items_out, void* stream) {
+  GNPDE_REQUIRE(n_items >= 0 && n_items < INT32_MAX && (n_items == 0 || (items && col && w && col_out && w_out &&
+                items_out)), GNPDE_EINVAL, "compact_items: bad arguments");
+  GNPDE_REQUIRE(items_out != items && col_out != col && w_out != w, GNPDE_EINVAL,
+                "compact_items: outputs may not alias the inputs");
+  if (n_items == 0) return GNPDE_OK;
+  const unsigned grid = (unsigned)ceil_div(n_items, (int64_t)kWavesPerBlock);
+  compact_items_kernel<<<grid, kBlock, 0, as_stream(stream)>>>(reinterpret_cast<const int4*>(items), (int)n_items,
+                                                                col, w, col_out, w_out,
+                                                                reinterpret_cast<int4*>(items_out));
   GNPDE_LAUNCH_CHECK();
   return GNPDE_OK;
 }

@@ -80,6 +80,7 @@ SIGNATURES = {
     "gnpde_scaled_sq_sums_f32": (_int, [_i64, _vp, _vp, _vp, _f64, _f64, _vp, _vp, _size, _vp]),
     "gnpde_segment_sums_workspace_bytes": (_size, [_i64]),
     "gnpde_segment_sums_f64": (_int, [_i64, _i64, _vp, _vp, _vp, _size, _vp]),
+    "gnpde_compact_items_f32": (_int, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp]),
     "gnpde_initial_step_bf16": (_int, [_i64, _vp, _vp, _vp, _f64, _f64, _f64, _vp, _vp, _vp, _size, _vp]),
     "gnpde_stage_apply_f32": (_int, [_i64, _i64, _i64, _vp, _vp, ctypes.POINTER(StageEpilogue), _vp]),
     "gnpde_stage_apply_bf16": (_int, [_i64, _i64, _i64, _vp, _vp, ctypes.POINTER(StageEpilogue), _vp]),

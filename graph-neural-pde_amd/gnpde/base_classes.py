@@ -24,6 +24,8 @@ loop use them unchanged:
   ``GNN.getNFE`` (src/base_classes.py:174-176) sums the two counters.
 * ``GraphData`` — src/base_classes.py:100-113.
 """
+import os
+
 import torch
 from torch import nn
 
@@ -31,6 +33,10 @@ from . import ops
 from ._cache import _tensor_key  # noqa: F401  (re-exported for the function modules)
 from .integrator import odeint, odeint_adjoint
 from .utils import get_rw_adj, gcn_norm_fill_val
+
+
+# GNPDE_COMPACT_SAMPLED=0: the sampled hard-attention graph stays the masked full graph
+COMPACT_SAMPLED = os.environ.get('GNPDE_COMPACT_SAMPLED', '1') != '0'
 
 
 class GraphData(object):
@@ -76,6 +82,9 @@ class ODEFunc(nn.Module):
         self._graph_key = None
         self._w_cache = {}
         self._layout = None  # the NodeLayout a fixed-grid solve runs in (gnpde.integrator), else None
+        # weights with zeros on dropped edges (HardAttODEblock training's sampled graph): csr_weights
+        # hands K1 the retained edges compacted inside the plan's items (ops.CompactWeights)
+        self.compact_sampled = False
 
     def graph_for(self, x):
         """Device CSR of ``self.edge_index`` for node count x.shape[1] (or x, an
@@ -120,7 +129,8 @@ class ODEFunc(nn.Module):
         buffer, so they keep replaying with the new weights instead of being
         re-captured every forward.  Buffers an autograd call has seen are never
         overwritten (its backward may still read them)."""
-        tag = (tag, transpose)
+        compact = bool(self.compact_sampled) and COMPACT_SAMPLED
+        tag = (tag, transpose, compact)
         key = (tag, _tensor_key(w), id(g))
         hit = self._w_cache.get(tag)
         grad = torch.is_grad_enabled()
@@ -129,10 +139,15 @@ class ODEFunc(nn.Module):
                 self._w_cache[tag] = (hit[0], hit[1], False)
             return hit[1]
         src = w.detach().float() if w.dtype != torch.float32 else w.detach()
-        if hit is not None and hit[2] and not grad and hit[0][2] == id(g):
-            wc = g.gather_weights(src, transpose=transpose, out=hit[1])
+        reuse = hit is not None and hit[2] and not grad and hit[0][2] == id(g)
+        prev = hit[1] if reuse else None
+        if compact:
+            # the sampled graph (HardAttODEblock training): the retained edges compacted inside the
+            # plan's items on the device (ops.CompactWeights), refreshed in place like the weights
+            full = g.gather_weights(src, transpose=transpose, out=prev.full if prev is not None else None)
+            wc = ops.compact_weights(g.csc if transpose else g.csr, full, transpose, out=prev)
         else:
-            wc = g.gather_weights(src, transpose=transpose)
+            wc = g.gather_weights(src, transpose=transpose, out=prev)
         self._w_cache[tag] = (key, wc, not grad)
         return wc
 

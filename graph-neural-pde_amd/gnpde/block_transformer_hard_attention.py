@@ -7,12 +7,16 @@ Training (:42-57): edges whose mean attention exceeds the (1 - att_samp_pct)
 quantile are kept and their weights renormalised per softmax group (:32-35);
 the RHS then integrates over the sampled graph.  The threshold is a device
 radix sort + torch.quantile's interpolation (gnpde_quantile_f32), the
-renormalisation a fixed-order per-group pass (gnpde_group_normalize_f32); the
-dropped edges keep weight 0 on the full graph (gnpde_threshold_mask_f32) instead
-of a compacted edge list, so no graph is rebuilt per forward.  The sampling runs
-under no_grad exactly as in the reference, so training differentiates the RHS
-through x, alpha_train and beta_train only — which the Laplacian backward
-provides.
+renormalisation a fixed-order per-group pass (gnpde_group_normalize_f32).  With
+the Laplacian RHS (which reads ``attention_weights``) the dropped edges keep weight
+0 on the full graph (gnpde_threshold_mask_f32) and K1 gathers the retained edges
+only, compacted inside the full plan's items on the device (gnpde_compact_items_f32,
+ops.CompactWeights): no graph rebuilt per forward, no host read.  The transformer /
+GAT RHS recomputes its attention over ``odefunc.edge_index`` at every evaluation
+(src/function_transformer_attention.py:49), so there the edge list itself is
+compacted (:54), as in the reference.  The sampling runs under no_grad exactly as
+in the reference, so training differentiates the RHS through x, alpha_train and
+beta_train only — which the Laplacian backward provides.
 
 The fork's training branch cannot run as written (SURVEY.md §0.5 family): it
 indexes the batched [B,2,E] edge list with ``mask.T`` (:54) and takes
@@ -81,15 +85,31 @@ class HardAttODEblock(ODEblock):
         with torch.no_grad():
             mean_att = ops.mix_weights(self.get_attention_weights(x))
             threshold = ops.quantile(mean_att, 1 - self.opt['att_samp_pct'])
-            masked, kept = ops.threshold_mask(mean_att, threshold)
-            self.odefunc.edge_index = ei
-            weights = self.renormalise_attention(masked)
+            if self.reads_weights():
+                masked, kept = ops.threshold_mask(mean_att, threshold)
+                self.odefunc.edge_index = ei
+                weights = self.renormalise_attention(masked)
+            else:
+                # the transformer / GAT RHS attends over odefunc.edge_index itself: the compacted list (:54)
+                mask = (mean_att > threshold).reshape(-1)
+                ei = ei[:, :, mask]
+                kept = ei.shape[2]
+                self.odefunc.edge_index = ei
+                weights = self.renormalise_attention(mean_att.reshape(1, -1)[:, mask])
         self.retained = kept
-        print('retaining {} of {} edges'.format(int(kept), ei.shape[2]))
+        print('retaining {} of {} edges'.format(int(kept), self.data_edge_index.shape[2]))
         return ei, weights
+
+    def reads_weights(self):
+        """Whether the integrated RHS reads ``attention_weights`` (the Laplacian) rather than
+        recomputing its attention over ``edge_index`` (ODEFuncTransformerAtt / GAT)."""
+        return hasattr(self.odefunc, '_weights_tensor')
 
     def forward(self, x, graph_data, y=None):
         self.reset_graph_data(graph_data, x.dtype, y)
+        # the sampled graph's zero weights: K1 over the retained edges only (ops.CompactWeights)
+        for f in (self.odefunc, self.reg_odefunc.odefunc):
+            f.compact_sampled = bool(self.training) and self.reads_weights()
         if self.training:
             edge_index, weights = self.sample_edges(x)
             self.odefunc.edge_index = edge_index

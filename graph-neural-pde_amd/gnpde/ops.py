@@ -755,11 +755,16 @@ def spmm_rhs(g, w_csr, x, x0=None, alpha=None, beta=None, rhs=True, alpha_sigmoi
     plan.order_launch(dev)
     epi = (C, _ptr(xr), C, _ptr(x0r), C, _ptr(a), _ptr(b), _flags(rhs, alpha_sigmoid, add_source), _ptr(out), C,
            _ptr(partials), plan.n_slots, st, _stream(dev))
+    items, col = plan.items, grouped.col
+    if isinstance(w_csr, CompactWeights):  # the sampled graph: the plan's items over the retained edges
+        if w_csr.grouped is not grouped or w_csr.transpose != bool(transpose):
+            raise ValueError("spmm_rhs: compacted weights of another grouped CSR")
+        items, col, w_csr = w_csr.items, w_csr.col, w_csr.w
     if dt == torch.bfloat16:
         if isinstance(w_csr, RefDstWeights):
             raise ValueError("bf16 storage takes precomputed weights (attn_rhs(..., fuse=False))")
-        _lib.call("gnpde_spmm_rhs_bf16", _ptr(plan.items), plan.n_items, _ptr(plan.heavy), plan.n_heavy,
-                  _ptr(grouped.col), _ptr(w_csr), *epi)
+        _lib.call("gnpde_spmm_rhs_bf16", _ptr(items), plan.n_items, _ptr(plan.heavy), plan.n_heavy,
+                  _ptr(col), _ptr(w_csr), *epi)
     elif isinstance(w_csr, RefDstWeights):
         if transpose:
             raise ValueError("on-the-fly attention weights aggregate over the CSR only")
@@ -767,9 +772,42 @@ def spmm_rhs(g, w_csr, x, x0=None, alpha=None, beta=None, rhs=True, alpha_sigmoi
                   _ptr(grouped.col), _ptr(w_csr.cs), _ptr(w_csr.m), _ptr(w_csr.rl), _ptr(w_csr.mr), w_csr.heads,
                   *epi)
     else:
-        _lib.call("gnpde_spmm_rhs_f32", _ptr(plan.items), plan.n_items, _ptr(plan.heavy), plan.n_heavy,
-                  _ptr(grouped.col), _ptr(w_csr), *epi)
+        _lib.call("gnpde_spmm_rhs_f32", _ptr(items), plan.n_items, _ptr(plan.heavy), plan.n_heavy,
+                  _ptr(col), _ptr(w_csr), *epi)
     return None if stage is not None else out.view(shape)
+
+
+class CompactWeights(object):
+    """Grouped-order weights with zeros (the sampled graph of HardAttODEblock training,
+    src/block_transformer_hard_attention.py:52-56) compacted inside the plan's items
+    (gnpde_compact_items_f32): ``items`` / ``col`` / ``w`` replace the grouped CSR's
+    for K1, which then gathers the retained edges only, in the full plan's order and
+    hub chunks (the masked full graph's sums: dropped edges added exact zeros).
+    ``full`` is the uncompacted grouped-order weights.  Refreshed in place
+    (compact_weights(..., out=)), so captured step graphs keep replaying."""
+
+    def __init__(self, grouped, transpose, full, col, w, items):
+        self.grouped, self.transpose = grouped, transpose
+        self.full, self.col, self.w, self.items = full, col, w, items
+
+
+def compact_weights(grouped, w_full, transpose, out=None):
+    """CompactWeights of grouped-order weights ``w_full`` [nnz] over ``grouped`` (a
+    GroupedCSR: the CSR, or the CSC with transpose=True); ``out``: an earlier
+    CompactWeights of the same grouped CSR refreshed in place."""
+    plan = grouped.plan
+    dev = w_full.device
+    _require_gpu(w_full, "w_full", torch.float32)
+    if out is None:
+        out = CompactWeights(grouped, transpose, w_full, torch.empty_like(grouped.col),
+                             torch.empty(max(grouped.nnz, 1), dtype=torch.float32, device=dev),
+                             torch.empty_like(plan.items))
+    elif out.grouped is not grouped or out.transpose != transpose:
+        raise ValueError("compact_weights: out belongs to another grouped CSR")
+    out.full = w_full
+    _lib.call("gnpde_compact_items_f32", _ptr(plan.items), plan.n_items, _ptr(grouped.col), _ptr(w_full),
+              _ptr(out.col), _ptr(out.w), _ptr(out.items), _stream(dev))
+    return out
 
 
 # byte offsets of the hub partial stores are 32-bit (buffer addressing, csrc/common.hpp kBufRecords)
@@ -812,6 +850,8 @@ def spmm_rhs_rows(g, plan, w_csr, x_src, x_rows, row0, x0=None, alpha=None, beta
     whole state (q, k rows at the positions of x_src; ``mr``: destination
     statistics records for norm_idx 1, None for source-grouped softmax: the fused
     gnpde_attn_dot_rhs_f32)."""
+    if isinstance(w_csr, CompactWeights):
+        raise ValueError("spmm_rhs_rows: compacted (sampled-graph) weights take the whole-graph K1 (spmm_rhs)")
     xs = _rows(x_src, "x_src")
     xl = _rows(x_rows, "x_rows")
     C = xs.shape[1]

@@ -121,6 +121,19 @@ int gnpde_quantile_f32(const float* v, int64_t n, double q, float* out, void* wo
  * zeros), so a training forward needs no new CSR / plan.  thr: device (the
  * gnpde_quantile_f32 output).                                                 */
 int gnpde_threshold_mask_f32(const float* v, int64_t n, const float* thr, float* out, int64_t* count, void* stream);
+/* The sampled graph of HardAttODEblock training over a work plan (ABI 7;
+ * src/block_transformer_hard_attention.py:52-56 keeps the edges above the
+ * threshold and integrates over that edge list): for every plan item
+ * {row, edge_begin, edge_end, slot} of gnpde_plan_build, the positions of
+ * [edge_begin, edge_end) whose weight w (grouped order, e.g. gnpde_threshold_mask_f32
+ * then gnpde_gather_weights_f32) is nonzero are written, in order, to
+ * col_out / w_out from edge_begin on, and items_out = {row, edge_begin,
+ * edge_begin + kept, slot}.  Launching K1 with items_out / col_out / w_out (and the
+ * plan's heavy entries unchanged) aggregates the retained edges only, in the
+ * order and hub chunks of the full plan: the same result as the masked full graph.
+ * No host synchronisation; outputs the size of the inputs; no aliasing.        */
+int gnpde_compact_items_f32(const int32_t* items, int64_t n_items, const int32_t* col, const float* w,
+                            int32_t* col_out, float* w_out, int32_t* items_out, void* stream);
 
 /* deg[r] = #{p : idx[p] == r}, r < R (memset + integer atomics: deterministic).
  * With idx = the aggregation CSR's col this is the in-degree used by the

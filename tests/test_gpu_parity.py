@@ -964,6 +964,100 @@ def test_hard_attention_block_training_sampling_vs_oracle(norm_idx):
     assert blk.odefunc.alpha_train.grad is not None
 
 
+@pytest.mark.parametrize("C", [128, 32])
+@pytest.mark.parametrize("method,pct", [("rk4", 0.81), ("dopri5", 0.573)])
+def test_hard_attention_compacted_graph_bit_equal(method, pct, C, monkeypatch):
+    """The sampled graph of HardAttODEblock training (ogbn-arxiv's / Computers' att_samp_pct,
+    src/best_params.py:5,7) as K1 runs it: the retained edges compacted inside the full
+    plan's items on the device (gnpde_compact_items_f32) — every item keeps its hub chunk
+    and the order of its retained edges, so the sums are those of the masked full graph
+    (a dropped edge adds an exact 0) and the solve, its gradients and the NFE are BIT-EQUAL
+    to the uncompacted run (GNPDE_COMPACT_SAMPLED=0) wherever K1 sums a row's edges in one
+    sequence — rows of 65-128 fp32 columns (G-arxiv's C = 128) take one edge group per
+    row slot.  Narrow rows (C = 32: two edge groups per slot, edges dealt by their parity
+    in the item) re-associate the sum: within 1e-6 there.  The compacted items cover
+    exactly the retained edges of each item, in order."""
+    import gnpde.base_classes as bc
+    N, E, h, att = 3000, 30000, 2, 16
+    rng = np.random.default_rng(71)
+    ei = rng.integers(0, N, size=(1, 2, E))
+    ei[0, 0, :1200] = 7  # a hub row: chunked in the plan
+    ei[0, 1, 1200:2000] = 11  # a hub destination: chunked in the CSC
+    x = rng.standard_normal((1, N, C)).astype(np.float32)
+    opt = dict(OPT, hidden_dim=C, heads=h, attention_dim=att, block='hard_attention', attention_norm_idx=0,
+               att_samp_pct=pct, method=method, step_size=0.25, tol_scale=100.0)
+    data = gnpde.GraphData()
+    data.new_graph(T(ei), N)
+    res = []
+    for compact in (True, False):
+        monkeypatch.setattr(bc, "COMPACT_SAMPLED", compact)
+        torch.manual_seed(0)
+        blk = gnpde.HardAttODEblock(gnpde.LaplacianODEFunc, [], opt, DEV, t=torch.tensor([0, 1.0])).to(DEV).train()
+        _set_qk(blk.multihead_att_layer, np.random.default_rng(3), C, att, scale=0.3)
+        with torch.no_grad():
+            blk.odefunc.alpha_train.fill_(0.4)
+        xt = T(x).requires_grad_(True)
+        z = blk(xt, data)
+        z.sum().backward()
+        if compact:
+            f = blk.odefunc
+            g = f.graph_for(N)
+            wc = f.csr_weights(g, f.attention_weights, 'att')
+            assert isinstance(wc, ops.CompactWeights)
+            full = wc.full.cpu().numpy()
+            col, cw = g.csr.col.cpu().numpy(), full
+            ccol, cwc = wc.col.cpu().numpy(), wc.w.cpu().numpy()
+            it0 = g.csr.plan.items[:g.csr.plan.n_items * 4].view(-1, 4).cpu().numpy()
+            it1 = wc.items[:g.csr.plan.n_items * 4].view(-1, 4).cpu().numpy()
+            assert (it0[:, [0, 1, 3]] == it1[:, [0, 1, 3]]).all()
+            for (r, b0, e0, _), (_, b1, e1, _) in zip(it0, it1):
+                keep = cw[b0:e0] != 0
+                assert e1 - b1 == int(keep.sum())
+                assert (ccol[b1:e1] == col[b0:e0][keep]).all() and (cwc[b1:e1] == cw[b0:e0][keep]).all()
+        res.append((z.detach(), xt.grad, blk.odefunc.alpha_train.grad, blk.odefunc.nfe))
+    (z0, g0, a0, n0), (z1, g1, a1, n1) = res
+    diag = (float((z0 - z1).abs().max()), float((g0 - g1).abs().max()), float((a0 - a1).abs()), n0, n1)
+    if C == 128:
+        assert torch.equal(z0, z1) and torch.equal(g0, g1) and torch.equal(a0, a1) and n0 == n1, diag
+    else:
+        assert rel(z0, z1.double().cpu().numpy()) <= 1e-6 and rel(g0, g1.double().cpu().numpy()) <= 1e-6, diag
+        assert abs(float(a0) - float(a1)) <= 1e-6 * max(1.0, abs(float(a1))) and abs(n0 - n1) <= 6, diag
+
+
+@pytest.mark.parametrize("norm_idx", [0, 1])
+def test_hard_attention_transformer_training_vs_oracle(norm_idx):
+    """HardAttODEblock with the transformer RHS in training: the block samples
+    with the odefunc's own attention layer (src/block_transformer_hard_attention.py:29),
+    and the RHS recomputes its attention over odefunc.edge_index at every evaluation
+    (src/function_transformer_attention.py:49), so the edge list itself is compacted
+    (:54) and the transformer RHS attends over the sampled subgraph only — against the
+    oracle's sample and its transformer RHS over that subgraph (rk4)."""
+    N, E, C, h, att = 1200, 8000, 16, 2, 16
+    rng = np.random.default_rng(81 + norm_idx)
+    ei = rng.integers(0, N, size=(1, 2, E))
+    x = rng.standard_normal((1, N, C)).astype(np.float32)
+    opt = dict(OPT, hidden_dim=C, heads=h, attention_dim=att, block='hard_attention', function='transformer',
+               attention_norm_idx=norm_idx, att_samp_pct=0.6, method='rk4', step_size=0.5)
+    blk = gnpde.HardAttODEblock(gnpde.ODEFuncTransformerAtt, [], opt, DEV, t=torch.tensor([0, 1])).to(DEV).train()
+    Wq, bq, Wk, bk = _set_qk(blk.odefunc.multihead_att_layer, rng, C, att, scale=0.3)
+    with torch.no_grad():
+        blk.odefunc.alpha_train.fill_(0.3)
+    data = gnpde.GraphData()
+    data.new_graph(T(ei), N)
+    with torch.no_grad():
+        z = blk(T(x), data)
+        att_gpu = blk.get_attention_weights(T(x)).cpu().numpy()
+    eo, wo = _prep_oracle(ei, N)
+    attn = O.transformer_attention(x, eo, Wq, bq, Wk, bk, h, norm_idx)
+    assert np.abs(att_gpu - attn).max() <= 2e-5
+    es, ws = O.hard_attention_sample(eo, att_gpu, 0.6, norm_idx, N)
+    got = blk.odefunc.edge_index.cpu().numpy()
+    assert got.shape == es.shape and (got == es).all() and int(blk.retained) == es.shape[2]
+    f = lambda t, y: O.transformer_rhs(es, y, None, Wq, bq, Wk, bk, h, norm_idx, 0.3, 0.0)  # noqa: E731
+    want = O.odeint_fixed(f, x, 0.0, 1.0, 'rk4', 0.5)
+    assert rel(z, want) <= RTOL
+
+
 # ---------------------------------------------------------------- hipGraph replay of fixed-grid steps
 @pytest.mark.parametrize("method", ["euler", "midpoint", "rk4"])
 def test_graph_replay_matches_eager_bitwise(method):
