@@ -306,9 +306,11 @@ class RowShardedLaplacian(object):
 
     @property
     def affine(self):
-        """f = σ(α)(A − I) y [+ β x0] is affine in y (gnpde.integrator: the adaptive
-        solvers' affine first stage and Krylov step) — on the HIP path; an injected
-        test RHS is taken as it is."""
+        """f = σ(α)(A − I) y [+ β x0] is affine in y — on the HIP path; an injected
+        test RHS is taken as it is.  The fused adaptive loop that would use it (the
+        affine first stage, the Krylov step) is not taken by the row partition
+        (fused_adaptive = False: its adaptive solves run the restated loop with the
+        global norm); the flag serves its fixed-grid stages and the column stripes."""
         return self.local_rhs is None and self.local_stage is None
 
     def rhs_stage(self, t, y_local, stage, linear=False):

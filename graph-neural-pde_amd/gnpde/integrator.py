@@ -1787,8 +1787,10 @@ def odeint(func, y0, t, rtol=1e-7, atol=1e-9, method=None, options=None, combine
                   max_num_steps=options.get('max_num_steps', 2 ** 31 - 1), norm=options.get('norm', _rms_norm))
         if _fused_adaptive_ok(func, y0, combine, options):
             solver = _RKAdaptiveFused(func, y0, rtol, atol, combine, options=options, **kw)
+            odeint.last_path = 'fused_krylov' if solver.krylov is not None else 'fused_stage'
         else:
             solver = _RKAdaptive(func, y0, rtol, atol, combine, **kw)
+            odeint.last_path = 'restated'
         out = solver.integrate(t)
         odeint.last_n_steps = solver.n_steps
         return out
@@ -1797,6 +1799,7 @@ def odeint(func, y0, t, rtol=1e-7, atol=1e-9, method=None, options=None, combine
 
 
 odeint.last_n_steps = 0
+odeint.last_path = None  # the last adaptive solve's loop: 'fused_krylov', 'fused_stage' or 'restated'
 
 
 # --------------------------------------------------------------------------- adjoint

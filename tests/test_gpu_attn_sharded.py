@@ -300,11 +300,13 @@ def test_row_sharded_laplacian_world_one_in_degree_numbering(tmp_path, add_sourc
 
 @pytest.mark.parametrize("cls", ["rows", "cols"])
 def test_sharded_laplacian_dopri5_krylov_world_one(tmp_path, cls):
-    """The sharded Laplacians are affine on the HIP path: an adaptive solve with their
-    global error norm takes the affine first stage and the Krylov step
-    (integrator._KrylovPlan; linear=True drops the source term) — at a world of one
-    (gloo, in-process) the same step count as the unsharded solve and its values within
-    1e-6, with a source term."""
+    """Adaptive solves of the sharded Laplacians with their global error norm, at a world
+    of one (gloo, in-process): the column stripes run the fused loop with the Krylov step
+    (integrator._KrylovPlan; linear=True drops the source term); the row partition runs
+    the restated torch loop (RowShardedLaplacian.fused_adaptive is False: its per-RHS
+    all-gather sits between the wide stages) — which path ran is asserted.
+    Both: the same step count as the unsharded solve and its values within 1e-6, with a
+    source term."""
     import torch.distributed as dist
     import gnpde
     from gnpde import integrator as gi
@@ -338,6 +340,8 @@ def test_sharded_laplacian_dopri5_krylov_world_one(tmp_path, cls):
             assert sh.affine
             y = gnpde.odeint(sh, y0, t, options=dict(norm=sh.global_rms_norm), **kw)[1]
             got = sh.unpad(sh.gather(y)).view(want.shape) if cls == "rows" else y.view(want.shape)
+            path = gi.odeint.last_path
+        assert path == ('restated' if cls == "rows" else 'fused_krylov'), path
         assert gi.odeint.last_n_steps == n_want
         assert rel(got, want) <= 1e-6
     finally:
