@@ -335,6 +335,7 @@ def bench_single(args, world, rank, dev):
         fwd = result.get("dopri5", {}).get("garxiv_laplacian", {}).get("ms_per_solve")
         result["train_adjoint"] = bench_train_adjoint(ei, w, x, dev, fwd)
         result["hard_attention_train"] = bench_hard_attention_train(ei, x, dev)
+        result["train_cora"] = bench_train_cora(dev)
         progress("block / train done")
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -1214,6 +1215,82 @@ def bench_hard_attention_train(ei, x, dev, reps=3):
     out["basis"] = ("sampling = block attention + head mean + quantile + threshold mask + group renormalisation (one "
                     "host read for the reference's 'retaining' line); the sampled graph reuses the full graph's CSR / "
                     "plans, its retained edges compacted inside the plan's items on the device (no rebuild)")
+    return out
+
+
+# Cora best_params (src/best_params.py:1): block attention over the Laplacian, heads 8, attention_dim 128,
+# attention_norm_idx 1, scaled_dot, add_source, dopri5 over [0, 18.29] at tol_scale 822, direct backprop
+# (adjoint False), hidden_dim 80, max_nfe 2000
+CORA_TRAIN = dict(heads=8, attention_dim=128, attention_norm_idx=1, attention_type='scaled_dot', add_source=True,
+                  leaky_relu_slope=0.2, max_nfe=2000)
+
+
+def bench_train_cora(dev, reps=5):
+    """One AttODEblock training step at Cora's best_params on a Cora-sized synthetic graph
+    (2,708 nodes, 10,556 edges; the block adds self loops, rw normalisation; C = 80): the block attention
+    (autograd-tracked), the dopri5 solve with autograd through every RHS (backprop, as Cora trains), a linear
+    loss and the backward to x, alpha / beta and Q / K.  The dataset is absent (no network): synthetic data, so
+    Cora's accuracy stays unpinned."""
+    import gnpde
+    import gnpde.integrator as integ
+    from gnpde import synthetic
+    N, E, C = 2708, 10556, 80
+    T, ts = CORA_DOPRI5
+    ei, _ = synthetic.rw_graph(N, E + N, seed=5, device=dev)
+    raw = ei[:, :, :E]
+    x = synthetic.features(1, N, C, seed=6, device=dev)
+    opt = dict(LAP_OPT, hidden_dim=C, block='attention', function='laplacian', method='dopri5', step_size=1,
+               tol_scale=ts, adjoint=False, self_loop_weight=1.0, data_norm='rw', reweight_attention=False,
+               square_plus=False, mix_features=False, beltrami=False, augment=False, max_iters=100, **CORA_TRAIN)
+    torch.manual_seed(23)
+    blk = gnpde.AttODEblock(gnpde.LaplacianODEFunc, [], opt, dev, t=torch.tensor([0.0, T], device=dev)).to(dev).train()
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(24)
+    with torch.no_grad():
+        for lin in (blk.multihead_att_layer.Q, blk.multihead_att_layer.K):
+            lin.weight.copy_(torch.randn(lin.weight.shape, generator=gen, device=dev) * 0.03)
+    data = gnpde.GraphData()
+    data.new_graph(raw, N)
+    gout = torch.randn(x.shape, generator=gen, device=dev)
+
+    def fwd():
+        blk.set_x0(x)
+        return blk(x, data)
+
+    def step():
+        xi = x.detach().requires_grad_(True)
+        blk.zero_grad(set_to_none=True)
+        blk.set_x0(xi)
+        z = blk(xi, data)
+        (z * gout).sum().backward()
+        return xi.grad
+
+    def timed(fn, grad):
+        with torch.set_grad_enabled(grad):
+            for _ in range(2):
+                fn()
+            torch.cuda.synchronize()
+            nfe0 = blk.odefunc.nfe
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(reps):
+                out = fn()
+            e.record()
+            torch.cuda.synchronize()
+        assert torch.isfinite(out).all()
+        return s.elapsed_time(e) / reps, (blk.odefunc.nfe - nfe0) // reps
+    ms_step, nfe_step = timed(step, True)
+    steps_train = integ.odeint.last_n_steps
+    ms_fwd_grad, _ = timed(fwd, True)
+    ms_eval, nfe_eval = timed(fwd, False)
+    out = {"config": "AttODEblock training step, Cora best_params (heads 8, attention_dim 128, norm_idx 1, scaled_dot, "
+                     "add_source, dopri5 over [0, %.2f] at tol_scale %.1f, backprop) on a Cora-sized synthetic graph "
+                     "(N=%d, E=%d + self loops, C=%d)" % (T, ts, N, E, C),
+           "ms_per_train_step": round(ms_step, 4), "rhs_evals_per_train_step": nfe_step, "steps": steps_train,
+           "ms_forward_with_grad": round(ms_fwd_grad, 4), "ms_forward_no_grad": round(ms_eval, 4),
+           "rhs_evals_no_grad": nfe_eval, "forward_path": integ.odeint.last_path,
+           "accuracy": "unpinned (the Cora dataset is absent: no network)"}
+    progress("train cora: %.3f ms per step (%d RHS), no-grad forward %.3f ms" % (ms_step, nfe_step, ms_eval))
     return out
 
 

@@ -1,5 +1,5 @@
 """One part of bench.py on its own (G-arxiv, C = 128): python tools/bench_part.py PART [reps]
-PART: adaptive_adjoint | hard_attention | dopri5 | train_adjoint | train_rk4 -> one JSON line."""
+PART: adaptive_adjoint | hard_attention | dopri5 | train_adjoint | train_cora | train_rk4 -> one JSON line."""
 import json
 import os
 import sys
@@ -32,6 +32,8 @@ def main():
         res = bench.bench_dopri5(ei, w, x, dev, 0.0888, 0.0760, reps)
     elif part == "train_adjoint":
         res = bench.bench_train_adjoint(ei, w, x, dev, None, reps)
+    elif part == "train_cora":
+        res = bench.bench_train_cora(dev, reps)
     elif part == "train_rk4":
         res = bench.bench_train(ei, w, x, 0.25, dev)
     else:
