@@ -33,23 +33,53 @@ __global__ void mix_weights_kernel(const float* __restrict__ att, int H, const f
   }
 }
 
-// One wavefront per group (row of a grouped CSR): the group's sum in a fixed
-// order (lane-strided partial sums, then a butterfly), then
-// w_out[e] = w_in[e] / (sum + 1e-16) for every COO edge e = perm[p] of the row.
+// Group renormalisation in two passes over the grouped (CSR-order) positions:
+// group_gather_kernel: t[p] = w_in[perm[p]] (position-parallel: the COO-order weights
+// brought into group order once, so no group walks a perm -> w chain of dependent
+// loads); group_normalize_kernel: one wavefront per group sums its contiguous run of
+// t in a fixed order (lane-strided partial sums, UNR loads in flight per lane, then a
+// butterfly) and writes w_out[perm[p]] = t[p] / (sum + 1e-16).  (Round 5 walked
+// w_in[perm[p]] per group: the 7.4k-edge hub group of G-arxiv was a chain of ~230
+// dependent loads, 342 us per training forward.)
+__global__ void group_gather_kernel(const int32_t* __restrict__ perm, int64_t nnz, const float* __restrict__ w_in,
+                                    float* __restrict__ t) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < nnz; p += stride) t[p] = w_in[perm[p]];
+}
+
 __global__ void group_normalize_kernel(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ perm,
-                                       int64_t R, const float* __restrict__ w_in, float* __restrict__ w_out) {
+                                       int64_t R, const float* __restrict__ t, float* __restrict__ w_out) {
+  constexpr int UNR = 4;
   const int lane = threadIdx.x & (kWave - 1);
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / kWave;
   const int64_t nwaves = (int64_t)gridDim.x * blockDim.x / kWave;
   for (int64_t r = wave; r < R; r += nwaves) {
     const int b = rowptr[r], e = rowptr[r + 1];
     float s = 0.f;
-    for (int p = b + lane; p < e; p += kWave) s += w_in[perm[p]];
+    for (int p0 = b; p0 < e; p0 += UNR * kWave) {
+      float v[UNR];
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        const int p = p0 + u * kWave + lane;
+        v[u] = p < e ? t[p] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) s += v[u];
+    }
     s = wave_sum(s);
     const float den = s + kSoftmaxEps;
-    for (int p = b + lane; p < e; p += kWave) {
-      const int i = perm[p];
-      w_out[i] = w_in[i] / den;
+    for (int p0 = b; p0 < e; p0 += UNR * kWave) {
+      int idx[UNR];
+      float v[UNR];
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        const int p = p0 + u * kWave + lane;
+        idx[u] = p < e ? perm[p] : -1;
+        v[u] = p < e ? t[p] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < UNR; ++u)
+        if (idx[u] >= 0) w_out[idx[u]] = v[u] / den;
     }
   }
 }
@@ -91,34 +121,44 @@ __global__ void threshold_mask_kernel(const float* __restrict__ v, int64_t n, co
 // The sampled graph of hard attention in the plan's own structure: every work item
 // (row, edge_begin, edge_end, slot) keeps its row, slot and edge_begin, and its
 // edges with a nonzero weight are moved to the front of its range in their order
-// (a stable partition by ballot, one wavefront per item), edge_end shrinking to
-// edge_begin + the kept count.  The aggregation then gathers only retained edges,
-// in the order and hub chunks of the full plan: the same sums as over the masked
-// full graph (a dropped edge added an exact 0), no plan rebuild and no host read.
+// (a stable partition by ballot), edge_end shrinking to edge_begin + the kept count.
+// The aggregation then gathers only retained edges, in the order and hub chunks of
+// the full plan: the same sums as over the masked full graph (a dropped edge added
+// an exact 0), no plan rebuild and no host read.  Four items per wavefront (16-lane
+// slots; the plan's items are stored longest first, so a wave's items have similar
+// lengths): 35 -> ~10 us for G-arxiv's 170k items.
+constexpr int kCompactSL = 16;
+
 __global__ __launch_bounds__(256) void compact_items_kernel(const int4* __restrict__ items, int n_items,
                                                             const int* __restrict__ col, const float* __restrict__ w,
                                                             int* __restrict__ col_out, float* __restrict__ w_out,
                                                             int4* __restrict__ items_out) {
+  constexpr int SPW = kWave / kCompactSL;
   const int lane = threadIdx.x & (kWave - 1);
-  const int item = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
-  if (item >= n_items) return;
-  const int4 it = items[item];
+  const int slot = lane / kCompactSL, sl = lane % kCompactSL;
+  const int item = (blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * SPW + slot;
+  const bool live = item < n_items;
+  const int4 it = live ? items[item] : make_int4(0, 0, 0, 0);
+  const int len = it.z - it.y;
+  int maxlen = len;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) maxlen = max(maxlen, __shfl_xor(maxlen, o));
   int kept = 0;
-  for (int e0 = it.y; e0 < it.z; e0 += kWave) {
-    const int p = e0 + lane;
-    const bool live = p < it.z;
-    const float v = live ? w[p] : 0.f;
-    const int c = live ? col[p] : 0;
-    const bool keep = live && v != 0.f;
-    const unsigned long long m = __ballot(keep);
-    const int before = __popcll(m & ((1ull << lane) - 1ull));
+  for (int j = 0; j < maxlen; j += kCompactSL) {  // wave-uniform trip count
+    const int p = it.y + j + sl;
+    const bool in = j + sl < len;
+    const float v = in ? w[p] : 0.f;
+    const int c = in ? col[p] : 0;
+    const bool keep = in && v != 0.f;
+    const unsigned long long m = (__ballot(keep) >> (slot * kCompactSL)) & 0xffffull;
+    const int before = __popcll(m & ((1ull << sl) - 1ull));
     if (keep) {
       col_out[it.y + kept + before] = c;
       w_out[it.y + kept + before] = v;
     }
     kept += __popcll(m);
   }
-  if (lane == 0) items_out[item] = make_int4(it.x, it.y, it.y + kept, it.w);
+  if (live && sl == 0) items_out[item] = make_int4(it.x, it.y, it.y + kept, it.w);
 }
 
 // torch.quantile(v, q) (linear interpolation) on a sorted copy:
@@ -173,15 +213,23 @@ int gnpde_mix_weights_f32(const float* att, int H, const float* ew, const float*
   return GNPDE_OK;
 }
 
+size_t gnpde_group_normalize_workspace_bytes(int64_t nnz) { return sizeof(float) * (size_t)(nnz > 0 ? nnz : 1); }
+
 int gnpde_group_normalize_f32(const int32_t* rowptr, const int32_t* perm, int64_t R, int64_t nnz, const float* w_in,
-                              float* w_out, void* stream) {
+                              float* w_out, void* workspace, size_t workspace_bytes, void* stream) {
   GNPDE_REQUIRE(R >= 1 && nnz >= 0, GNPDE_EINVAL, "group_normalize: bad sizes");
   GNPDE_REQUIRE(w_in != w_out, GNPDE_EINVAL, "group_normalize: in-place is not supported");
   if (nnz == 0) return GNPDE_OK;
-  GNPDE_REQUIRE(rowptr && perm && w_in && w_out, GNPDE_EINVAL, "group_normalize: NULL pointer");
+  GNPDE_REQUIRE(rowptr && perm && w_in && w_out && workspace, GNPDE_EINVAL, "group_normalize: NULL pointer");
+  GNPDE_REQUIRE(workspace_bytes >= gnpde_group_normalize_workspace_bytes(nnz), GNPDE_EINVAL,
+                "group_normalize: workspace too small");
+  hipStream_t s = as_stream(stream);
+  float* t = static_cast<float*>(workspace);
+  const int64_t gblocks = ceil_div(nnz, (int64_t)kBlock);
+  group_gather_kernel<<<(int)(gblocks < 4096 ? gblocks : 4096), kBlock, 0, s>>>(perm, nnz, w_in, t);
+  GNPDE_LAUNCH_CHECK();
   const int64_t blocks = ceil_div(R, (int64_t)kWavesPerBlock);
-  group_normalize_kernel<<<(int)(blocks < 8192 ? blocks : 8192), kBlock, 0, as_stream(stream)>>>(rowptr, perm, R,
-                                                                                                   w_in, w_out);
+  group_normalize_kernel<<<(int)(blocks < 65536 ? blocks : 65536), kBlock, 0, s>>>(rowptr, perm, R, t, w_out);
   GNPDE_LAUNCH_CHECK();
   return GNPDE_OK;
 }
@@ -205,7 +253,7 @@ int gnpde_compact_items_f32(const int32_t* items, int64_t n_items, const int32_t
   GNPDE_REQUIRE(items_out != items && col_out != col && w_out != w, GNPDE_EINVAL,
                 "compact_items: outputs may not alias the inputs");
   if (n_items == 0) return GNPDE_OK;
-  const unsigned grid = (unsigned)ceil_div(n_items, (int64_t)kWavesPerBlock);
+  const unsigned grid = (unsigned)ceil_div(n_items, (int64_t)kWavesPerBlock * (kWave / kCompactSL));
   compact_items_kernel<<<grid, kBlock, 0, as_stream(stream)>>>(reinterpret_cast<const int4*>(items), (int)n_items,
                                                                 col, w, col_out, w_out,
                                                                 reinterpret_cast<int4*>(items_out));

@@ -54,7 +54,8 @@ SIGNATURES = {
     "gnpde_gather_weights_f32": (_int, [_vp, _i64, _int, _vp, _vp, _vp]),
     "gnpde_indegree_i32": (_int, [_vp, _i64, _i64, _vp, _vp]),
     "gnpde_mix_weights_f32": (_int, [_vp, _int, _vp, _vp, _i64, _vp, _vp]),
-    "gnpde_group_normalize_f32": (_int, [_vp, _vp, _i64, _i64, _vp, _vp, _vp]),
+    "gnpde_group_normalize_workspace_bytes": (_size, [_i64]),
+    "gnpde_group_normalize_f32": (_int, [_vp, _vp, _i64, _i64, _vp, _vp, _vp, _size, _vp]),
     "gnpde_quantile_workspace_bytes": (_size, [_i64]),
     "gnpde_quantile_f32": (_int, [_vp, _i64, _f64, _vp, _vp, _size, _vp]),
     "gnpde_plan_workspace_bytes": (_size, [_i64]),

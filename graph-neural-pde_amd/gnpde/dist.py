@@ -69,6 +69,14 @@ def host_rowptr(edge_index, num_nodes):
     return rp
 
 
+# The row partition's default row weight: besides its edges' gathers a row costs its own row read and
+# its output write — about two gathered rows.  G-rmat (configs[4]) at 8 ranks, the slowest rank's rk4-step
+# compute (tools/mgpu_implied_grmat.py, profiles/r06_mgpu_rows_row_weight.jsonl): row_weight 0 / 1 / 2 / 4 / 8
+# -> 3.23 / 2.32 / 1.78 / 1.98 / 2.44 ms (pure nnz balance leaves the low-degree tail of the in-degree
+# numbering, every row of which still moves 2 KB, on the last rank).
+ROW_WEIGHT = 2.0
+
+
 def balanced_row_blocks(rowptr, world, row_weight=0.0):
     """Contiguous row blocks balanced by work, not by row count (SURVEY §8(e):
     "1-D partition ... balanced by nnz").  Block p ends at the row where the
@@ -104,7 +112,7 @@ class RowPartition(object):
     (``col``); the local plan's item rows are positions too, and the outputs are
     addressed through pointers shifted back by rank*nbmax rows."""
 
-    def __init__(self, g, world, rank, row_weight=0.0, chunk=None, blocks=None):
+    def __init__(self, g, world, rank, row_weight=ROW_WEIGHT, chunk=None, blocks=None):
         self.world, self.rank = int(world), int(rank)
         rowptr = g.csr.rowptr
         self.blocks = blocks if blocks is not None else balanced_row_blocks(rowptr.cpu().numpy(), world, row_weight)
@@ -206,7 +214,7 @@ class RowShardedLaplacian(object):
         return tuple(t for t in (self.alpha, self.beta) if isinstance(t, torch.Tensor))
 
     def __init__(self, edge_index, edge_weight, num_nodes, alpha, beta=None, x0_local=None, add_source=False,
-                 alpha_sigmoid=True, group=None, local_rhs=None, chunk=None, row_weight=0.0,
+                 alpha_sigmoid=True, group=None, local_rhs=None, chunk=None, row_weight=ROW_WEIGHT,
                  local_stage=None, node_order=None, x0=None):
         self.group = group
         self.rank = dist.get_rank(group)
@@ -928,7 +936,7 @@ class RowShardedTransformer(object):
 
     def __init__(self, edge_index, num_nodes, C, Wq, bq, Wk, bk, heads, norm_idx, alpha, score_mode='reference',
                  beta=None, x0_local=None, add_source=False, alpha_sigmoid=True, group=None,
-                 chunk=None, row_weight=0.0, comm=None, local=None, partition_stats=True):
+                 chunk=None, row_weight=ROW_WEIGHT, comm=None, local=None, partition_stats=True):
         if edge_index.shape[0] != 1:
             raise NotImplementedError("RowShardedTransformer: one graph (B = 1); shard batches with shard_batch")
         if int(norm_idx) not in (0, 1) or score_mode not in ('reference', 'per_edge'):

@@ -514,8 +514,10 @@ def group_normalize(grouped, w):
     if w.numel() != grouped.nnz:
         raise ValueError("group_normalize: %d weights for %d edges" % (w.numel(), grouped.nnz))
     out = torch.empty_like(w)
+    nbytes = _lib.fn("gnpde_group_normalize_workspace_bytes")(grouped.nnz)
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=w.device)
     _lib.call("gnpde_group_normalize_f32", _ptr(grouped.rowptr), _ptr(grouped.perm), grouped.R, grouped.nnz,
-              _ptr(w), _ptr(out), _stream(w.device))
+              _ptr(w), _ptr(out), _ptr(ws), nbytes, _stream(w.device))
     return out
 
 

@@ -103,9 +103,12 @@ int gnpde_mix_weights_f32(const float* att, int H, const float* ew, const float*
 /* w_out[e] = w_in[e] / (sum of w_in over e's group + 1e-16), groups = the rows
  * of a grouped CSR (rowptr[R+1], perm[nnz] = CSR position -> COO edge id),
  * COO order in and out; fixed summation order (deterministic).  Replaces
- * HardAttODEblock.renormalise_attention, src/block_transformer_hard_attention.py:32-35. */
+ * HardAttODEblock.renormalise_attention, src/block_transformer_hard_attention.py:32-35.
+ * ABI 7: a workspace of gnpde_group_normalize_workspace_bytes(nnz) (the weights in
+ * group order, so each group's sum streams a contiguous run). */
+size_t gnpde_group_normalize_workspace_bytes(int64_t nnz);
 int gnpde_group_normalize_f32(const int32_t* rowptr, const int32_t* perm, int64_t R, int64_t nnz, const float* w_in,
-                              float* w_out, void* stream);
+                              float* w_out, void* workspace, size_t workspace_bytes, void* stream);
 
 /* *out = torch.quantile(v[0:n], q) (linear interpolation; rank q*(n-1) in
  * fp32, ATen's lerp) written to DEVICE memory; radix sort into the workspace.
