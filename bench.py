@@ -1281,6 +1281,7 @@ def bench_train_cora(dev, reps=5):
         return s.elapsed_time(e) / reps, (blk.odefunc.nfe - nfe0) // reps
     ms_step, nfe_step = timed(step, True)
     steps_train = integ.odeint.last_n_steps
+    train_path = integ.odeint.last_path
     ms_fwd_grad, _ = timed(fwd, True)
     ms_eval, nfe_eval = timed(fwd, False)
     out = {"config": "AttODEblock training step, Cora best_params (heads 8, attention_dim 128, norm_idx 1, scaled_dot, "
@@ -1288,7 +1289,9 @@ def bench_train_cora(dev, reps=5):
                      "(N=%d, E=%d + self loops, C=%d)" % (T, ts, N, E, C),
            "ms_per_train_step": round(ms_step, 4), "rhs_evals_per_train_step": nfe_step, "steps": steps_train,
            "ms_forward_with_grad": round(ms_fwd_grad, 4), "ms_forward_no_grad": round(ms_eval, 4),
-           "rhs_evals_no_grad": nfe_eval, "forward_path": integ.odeint.last_path,
+           "rhs_evals_no_grad": nfe_eval, "train_path": train_path, "eval_path": integ.odeint.last_path,
+           "basis": "train_path 'fused_backprop': the solve and its discrete adjoint as one autograd node "
+                    "(gnpde.adaptive_backprop); 'restated': autograd through every RHS (GNPDE_ADAPTIVE_BACKPROP=0)",
            "accuracy": "unpinned (the Cora dataset is absent: no network)"}
     progress("train cora: %.3f ms per step (%d RHS), no-grad forward %.3f ms" % (ms_step, nfe_step, ms_eval))
     return out

@@ -1256,6 +1256,58 @@ def _fused_adaptive_ok(func, y0, combine, options):
     return bool(getattr(func, 'host_stages', False)) and hasattr(func, 'host_stage_apply')
 
 
+# Backprop through adaptive solves of the Laplacian (gnpde.adaptive_backprop; GNPDE_ADAPTIVE_BACKPROP=0: the
+# restated loop with autograd through every RHS and stage combination)
+ADAPTIVE_BACKPROP = os.environ.get('GNPDE_ADAPTIVE_BACKPROP', '1') != '0'
+
+
+def _adaptive_backprop_ok(func, y0, combine, options):
+    """An adaptive solve under autograd of a gnpde LaplacianODEFunc on a device fp32
+    state with torchdiffeq's RMS norm, the sigmoid alpha and something to differentiate."""
+    if not (ADAPTIVE_BACKPROP and torch.is_grad_enabled() and isinstance(combine, _Combine)):
+        return False
+    if not (hasattr(func, '_weights_tensor') and hasattr(func, 'rhs_stage')) or 'norm' in options:
+        return False
+    if not (y0.is_cuda and y0.dtype == torch.float32 and y0.dim() == 3) or getattr(func, '_layout', None) is not None:
+        return False
+    if func.opt.get('no_alpha_sigmoid', False):
+        return False
+    w, _ = func._weights_tensor()
+    return any(v.requires_grad for v in (y0, func.alpha_train, func.beta_train, w))
+
+
+class _LaplacianAdaptiveFn(torch.autograd.Function):
+    """An adaptive solve of f(y) = sigma(alpha)(A(w) y - y) [+ beta x0] with its discrete
+    adjoint (gnpde.adaptive_backprop): gradients to y0, alpha_train, beta_train and the
+    weights (the attention an AttODEblock hands the Laplacian)."""
+
+    @staticmethod
+    def forward(ctx, y0, alpha_train, beta_train, w, func, t_h, method, rtol, atol, first_step, max_num_steps):
+        from .adaptive_backprop import AdaptiveBackprop
+        with torch.no_grad():
+            solver = AdaptiveBackprop(func, y0.detach(), t_h, method, rtol, atol, first_step, max_num_steps)
+            sol = solver.forward()
+        odeint.last_n_steps = solver.n_steps
+        ctx.solver = solver
+        ctx.shapes = (alpha_train.shape, alpha_train.dtype, beta_train.shape, beta_train.dtype)
+        return sol
+
+    @staticmethod
+    def backward(ctx, g):
+        with torch.no_grad():
+            ybar, ga, gb, gw = ctx.solver.backward(g)
+        ctx.solver = None
+        ash, adt, bsh, bdt = ctx.shapes
+        need = ctx.needs_input_grad
+        gy = ybar.view(g.shape[1:]) if need[0] else None
+        gal = ga.to(adt).reshape(ash) if need[1] else None
+        gbe = None
+        if need[2]:
+            gbe = gb.to(bdt).reshape(bsh) if gb is not None else torch.zeros(bsh, dtype=bdt, device=g.device)
+        gwo = gw if need[3] else None
+        return (gy, gal, gbe, gwo) + (None,) * 7
+
+
 # Captured adaptive steps (hipGraph): one graph per (buffer binding, dense-output
 # variant) replays a whole step — the stage-input pass, the RHS launches and the
 # error reduction — whatever dt (the coefficients scale by a device scalar), so a
@@ -1788,6 +1840,13 @@ def odeint(func, y0, t, rtol=1e-7, atol=1e-9, method=None, options=None, combine
         if _fused_adaptive_ok(func, y0, combine, options):
             solver = _RKAdaptiveFused(func, y0, rtol, atol, combine, options=options, **kw)
             odeint.last_path = 'fused_krylov' if solver.krylov is not None else 'fused_stage'
+        elif _adaptive_backprop_ok(func, y0, combine, options):
+            # backprop through the adaptive solve of the Laplacian as one node (gnpde.adaptive_backprop)
+            w, _ = func._weights_tensor()
+            out = _LaplacianAdaptiveFn.apply(y0, func.alpha_train, func.beta_train, w, func, _host_times(t), method,
+                                             rtol, atol, options.get('first_step'), kw['max_num_steps'])
+            odeint.last_path = 'fused_backprop'
+            return out
         else:
             solver = _RKAdaptive(func, y0, rtol, atol, combine, **kw)
             odeint.last_path = 'restated'
