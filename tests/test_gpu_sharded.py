@@ -66,8 +66,10 @@ def test_row_partition_bit_equal_to_unsharded(grmat, world):
     parts = [gd.RowPartition(g, world, r) for r in range(world)]
     blocks = parts[0].blocks
     assert blocks[0][0] == 0 and blocks[-1][1] == N
-    work = [int(rp[b] - rp[a]) for a, b in blocks]
-    assert max(work) <= 1.05 * E / world + int(np.diff(rp).max())  # nnz-balanced up to one row
+    # balanced by nnz + ROW_WEIGHT x rows (each row also moves its own row and output) up to one row
+    rw = gd.ROW_WEIGHT
+    work = [int(rp[b] - rp[a]) + rw * (b - a) for a, b in blocks]
+    assert max(work) <= 1.05 * (E + rw * N) / world + int(np.diff(rp).max()) + rw
     y_full = parts[0].pad_state(x)
     assert torch.equal(parts[0].unpad_state(y_full), x)
     for p in parts:
