@@ -1,5 +1,5 @@
 """One part of bench.py on its own (G-arxiv, C = 128): python tools/bench_part.py PART [reps]
-PART: adaptive_adjoint | hard_attention | dopri5 | train_adjoint | train_cora | train_rk4 -> one JSON line."""
+PART: adaptive_adjoint | hard_attention | dopri5 | train_adjoint | train_cora | train_rk4 | blend -> one JSON line."""
 import json
 import os
 import sys
@@ -36,6 +36,13 @@ def main():
         res = bench.bench_train_cora(dev, reps)
     elif part == "train_rk4":
         res = bench.bench_train(ei, w, x, 0.25, dev)
+    elif part == "blend":
+        import gnpde
+        func = gnpde.LaplacianODEFunc(C, C, dict(bench.LAP_OPT, hidden_dim=C), dev).to(dev)
+        func.edge_index, func.edge_weight = ei, w
+        with torch.no_grad():
+            g = func.graph_for(x)
+        res = bench.bench_blend(g, dev)
     else:
         raise SystemExit("unknown part %r" % part)
     print(json.dumps(res), flush=True)

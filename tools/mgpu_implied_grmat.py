@@ -54,6 +54,8 @@ def main():
     p.add_argument("--worlds", default="1,2,4,8")
     p.add_argument("--bus-gbs", type=float, default=300.0)
     p.add_argument("--steps", type=int, default=8)
+    p.add_argument("--row-weights", default="0", help="balanced_row_blocks row_weight values to try (rows layout)")
+    p.add_argument("--rows-only", action="store_true")
     a = p.parse_args()
     worlds = [int(v) for v in a.worlds.split(",")]
     import bench
@@ -68,7 +70,7 @@ def main():
            "rows": {}}
     # column stripes: one rk4 step of each stripe's solve (a stripe is an independent LaplacianODEFunc of C/N
     # columns on the shared graph: exactly the work ColumnShardedLaplacian gives a rank, no collective per RHS)
-    for world in worlds:
+    for world in ([] if a.rows_only else worlds):
         per = []
         for (c0, c1) in gd.col_blocks(C, world)[:1] if world > 1 else [(0, C)]:
             xs = x[..., c0:c1].contiguous()
@@ -90,8 +92,9 @@ def main():
     g = lay.graph if lay is not None else func.graph_for(x)
     xi = lay.to_internal(x) if lay is not None else x
     wc = g.gather_weights(w)
-    for world in worlds:
-        blocks = gd.balanced_row_blocks(g.csr.rowptr.cpu().numpy(), world)
+    rws = [float(v) for v in a.row_weights.split(",")]
+    for rw, world in [(r, n) for r in rws for n in worlds]:
+        blocks = gd.balanced_row_blocks(g.csr.rowptr.cpu().numpy(), world, row_weight=rw)
         per = []
         for (r0, r1) in blocks:
             plan = gd._local_plan(g.csr, r0, r1, g.chunk)
@@ -104,13 +107,15 @@ def main():
                 ops.spmm_rhs_rows(g, plan, wc, xi.view(-1, C), xr, r0, alpha=a0)
             per.append(4 * replay_ms(share))
         gather = 4 * (world - 1) / world * N * C * 4 / (a.bus_gbs * 1e9) * 1e3 if world > 1 else 0.0
-        out["rows"][world] = {"rk4_step_compute_ms_per_rank": round(max(per), 4),
-                              "per_rk4_step_all_gathers_ms_modelled": round(gather, 3),
-                              "rk4_step_ms_implied": round(max(per) + gather, 4),
-                              "rank_compute_ms": [round(v, 4) for v in per]}
-        print(json.dumps({"rows": world, **{k: v for k, v in out["rows"][world].items() if k != "rank_compute_ms"}}),
-              flush=True)
-    b1 = out["cols"][worlds[0]]["rk4_step_ms_per_rank"] if worlds[0] == 1 else None
+        ent = {"row_weight": rw, "rk4_step_compute_ms_per_rank": round(max(per), 4),
+               "per_rk4_step_all_gathers_ms_modelled": round(gather, 3),
+               "rk4_step_ms_implied": round(max(per) + gather, 4), "rank_compute_ms": [round(v, 4) for v in per]}
+        if rw == rws[0]:
+            out["rows"][world] = ent
+        else:
+            out.setdefault("rows_row_weight", {}).setdefault(str(rw), {})[world] = ent
+        print(json.dumps({"rows": world, **{k: v for k, v in ent.items() if k != "rank_compute_ms"}}), flush=True)
+    b1 = out["cols"][worlds[0]]["rk4_step_ms_per_rank"] if (worlds[0] == 1 and out["cols"]) else None
     if b1:
         for world in worlds:
             c = out["cols"][world]
