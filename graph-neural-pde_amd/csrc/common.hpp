@@ -690,18 +690,20 @@ __device__ __forceinline__ void wide_combine(const gnpde_stage_epilogue_t& st, i
     }
     return;
   }
+  // (the fallback for rows past the buffer range: an operand equal to the RHS input is
+  // loaded like any other and its value replaced by the held row — a branch between the
+  // held row and a load is folded into a load through a selected pointer, which puts xv
+  // in scratch memory for every row of the kernel)
   auto base_term = [&](const gnpde_stage_out_t& so, float (&acc)[VEC]) {
     if (so.base == nullptr) {
 #pragma unroll
       for (int t = 0; t < VEC; ++t) acc[t] = 0.f;
-    } else if (xid != nullptr && so.base == xid) {
-#pragma unroll
-      for (int t = 0; t < VEC; ++t) acc[t] = so.cb * xv[t];
     } else {
+      const bool isx = xid != nullptr && so.base == xid;
       Packed<VEC, T> bv;
       load_packed<VEC>(as_t<T>(so.base) + off, bv);
 #pragma unroll
-      for (int t = 0; t < VEC; ++t) acc[t] = so.cb * unpack(bv, t);
+      for (int t = 0; t < VEC; ++t) acc[t] = so.cb * (isx ? xv[t] : unpack(bv, t));
     }
   };
   const bool has_err = ERR && st.err_rows != nullptr;
@@ -713,26 +715,24 @@ __device__ __forceinline__ void wide_combine(const gnpde_stage_epilogue_t& st, i
 #pragma unroll
   for (int j = 0; j < NKMAX; ++j) {
     if (j < st.nk) {
-      Packed<VEC, T> kv;
-      if (xid != nullptr && st.k[j] == xid) {
+      const bool kx = xid != nullptr && st.k[j] == xid;
+      Packed<VEC, T> kp;
+      load_packed<VEC>(as_t<T>(st.k[j]) + off, kp);
+      float kv[VEC];
 #pragma unroll
-        for (int t = 0; t < Packed<VEC, T>::W; ++t) kv.d[t] = 0u;
-        pack_into<VEC, T>(xv, kv);
-      } else {
-        load_packed<VEC>(as_t<T>(st.k[j]) + off, kv);
-      }
+      for (int t = 0; t < VEC; ++t) kv[t] = kx ? xv[t] : unpack(kp, t);
 #pragma unroll
       for (int i = 0; i < NOUT; ++i) {
         if (i < st.n_out) {
           const float c = st.o[i].c[j] * sco[i];
 #pragma unroll
-          for (int t = 0; t < VEC; ++t) r[i][t] = fmaf(c, unpack(kv, t), r[i][t]);
+          for (int t = 0; t < VEC; ++t) r[i][t] = fmaf(c, kv[t], r[i][t]);
         }
       }
       if (has_err) {
         const float c = st.err.c[j] * sc;
 #pragma unroll
-        for (int t = 0; t < VEC; ++t) ev[t] = fmaf(c, unpack(kv, t), ev[t]);
+        for (int t = 0; t < VEC; ++t) ev[t] = fmaf(c, kv[t], ev[t]);
       }
     }
   }
