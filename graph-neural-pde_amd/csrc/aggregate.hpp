@@ -290,6 +290,12 @@ __device__ __forceinline__ void hub_arrive_slots(int4* heavy, int n_heavy, bool 
   }
 }
 
+// The folded dense output's crossing flag and coefficients (dense_coefs) ahead of the
+// launch that applies them (ABI 8 dense_out).
+static __global__ __launch_bounds__(64) void dense_coef_kernel(gnpde_stage_epilogue_t st) {
+  if (threadIdx.x == 0) dense_coefs(st, st.dense_tab);
+}
+
 // ------------------------------------------------------------------ aggregation kernel
 // Lane layout: RPW row slots of SL = 64/RPW lanes per wavefront (one plan item
 // each); inside a slot lane = g*GL + gl: G = SL/GL edges are gathered side by
@@ -491,8 +497,13 @@ static int launch_agg_cfg(const int4* items, int64_t n_items, int4* heavy, int64
       // the adaptive solvers' wide epilogue: plain weights only (the Laplacian RHS and
       // precomputed attention weights); the callers apply it after the other policies
       if constexpr (std::is_same<WP, PlainWeights>::value) {
-        agg_kernel<VEC, GL, NCH, U, RPW, 4, PlainWeights, T><<<grid, kBlock, 0, s>>>(
-            items, (int)n_items, heavy, nh, col, as_plain(wp), C, ep, partials);
+        if (ep.st.dense_out) {  // + the step's folded dense output (ABI 8): its coefficients first
+          dense_coef_kernel<<<1, kWave, 0, s>>>(ep.st);
+          agg_kernel<VEC, GL, NCH, U, RPW, 5, PlainWeights, T><<<grid, kBlock, 0, s>>>(
+              items, (int)n_items, heavy, nh, col, as_plain(wp), C, ep, partials);
+        } else
+          agg_kernel<VEC, GL, NCH, U, RPW, 4, PlainWeights, T><<<grid, kBlock, 0, s>>>(
+              items, (int)n_items, heavy, nh, col, as_plain(wp), C, ep, partials);
       } else {
         set_error("rhs: the wide (adaptive-solver) stage epilogue is fused with plain weights only; "
                   "apply it with gnpde_stage_apply_*");

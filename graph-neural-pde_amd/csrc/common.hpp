@@ -434,9 +434,15 @@ __device__ __forceinline__ void pack_into(const float (&v)[VEC], Packed<VEC, T>&
 //   2: the general fixed-grid epilogue (two outputs, dot term);
 //   4: the wide epilogue of the adaptive solvers: two outputs, up to
 //      GNPDE_STAGE_MAX_K operands and the embedded pair's error rows, every stage
-//      operand loaded after the aggregation (nothing held across the gathers).
+//      operand loaded after the aggregation (nothing held across the gathers);
+//   5: the wide epilogue plus the step's folded dense output (ABI 8 dense_out: the
+//      last launch of an affine Krylov step that may cross an output time).
 // An instantiation only holds registers for what it can emit.
 constexpr int kStagePre = 2;
+template <int STG>
+constexpr bool stage_wide() {
+  return STG == 4 || STG == 5;
+}
 // A/B knobs: whether the STG 1 / 2 / 3 instantiations prefetch their stage
 // operands before the gathers (1) or stream them after the aggregation (0, as STG 4)
 #ifndef GNPDE_STG1_PRE
@@ -459,7 +465,7 @@ constexpr int kStagePre = 2;
 #endif
 template <int STG>
 constexpr int stage_nout() {
-  return (STG == 2 || STG == 4) ? 2 : 1;
+  return (STG == 2 || stage_wide<STG>()) ? 2 : 1;
 }
 template <int STG>
 constexpr bool stage_prefetch() {
@@ -483,7 +489,7 @@ constexpr bool stage_dw_pre() {  // the dot operand read before the gathers
 }
 template <int STG>
 constexpr bool stage_err() {
-  return STG == 4;
+  return stage_wide<STG>();
 }
 
 template <int VEC, class T, int STG>
@@ -494,7 +500,7 @@ struct EpiPre {
   Packed<VEC, T> kv[stage_kpre<STG>() > 0 ? stage_kpre<STG>() : 1];
   Packed<VEC, T> dw;  // the stage's dot operand (dot_rows; STG 2 with GNPDE_STG2_PRE, STG 3 with GNPDE_DOT_PRE)
   double dprev;       // the row's running dot (dot_accumulate), read before the gathers
-  Packed<VEC, T> wk[(STG == 4 && GNPDE_STG4_PRE > 0) ? GNPDE_STG4_PRE : 1];  // the wide epilogue's first operands
+  Packed<VEC, T> wk[(stage_wide<STG>() && GNPDE_STG4_PRE > 0) ? GNPDE_STG4_PRE : 1];  // the wide epilogue's first operands
 };
 
 // The Epi / stage pointers are declared float*; for bf16 storage they address
@@ -515,7 +521,7 @@ __device__ __forceinline__ void epi_prefetch(const Epi& e, int64_t row, int cc, 
   if (e.flags & GNPDE_ADD_SOURCE) load_packed<VEC>(as_t<T>(e.x0) + row * e.ldx0 + cc, p.x0r);
   if constexpr (stage_dot<STG>() && GNPDE_DOT_PRE)  // the running dot: its read is off the epilogue's chain
     p.dprev = (e.st.dot_rows && e.st.dot_accumulate) ? e.st.dot_rows[row] : 0.0;
-  if constexpr (STG == 4 && GNPDE_STG4_PRE > 0) {
+  if constexpr (stage_wide<STG>() && GNPDE_STG4_PRE > 0) {
     // the first GNPDE_STG4_PRE present operand rows of the wide epilogue (WideSlots order)
     const int64_t off = row * e.ldf + cc;
     if (GNPDE_WIDE_BATCH && rows_fit_buffer<VEC, T>(off)) {
@@ -534,7 +540,7 @@ __device__ __forceinline__ void epi_prefetch(const Epi& e, int64_t row, int cc, 
       }
     }
   }
-  if constexpr (STG == 0 || STG == 4) return;
+  if constexpr (STG == 0 || stage_wide<STG>()) return;
   const int64_t off = row * e.ldf + cc;
 #pragma unroll
   for (int i = 0; i < stage_bpre<STG>(); ++i) {
@@ -597,17 +603,62 @@ __device__ __forceinline__ float out_scale(const gnpde_stage_epilogue_t& st, int
   return (st.unscaled_outs >> i) & 1 ? 1.f : sc;
 }
 
+// The folded dense output of an adaptive step (ABI 8 dense_out, STG 5): whether the
+// step crosses the output time, and the fp32 coefficients of its operands — [0] the
+// base of output 0 (y0), [1 + j] k[j], [GNPDE_STAGE_MAX_K + 1] f — formed in fp64
+// from the device step start, output time and step size by dense_coef_kernel (one
+// wavefront ahead of the launch) into dense_tab = {crossing, c[0..7]}, which the
+// launch reads into scalar registers (wave-uniform values).
+constexpr int kDenseSlots = GNPDE_STAGE_MAX_K + 2;
+struct DenseCoef {
+  bool on;
+  float c[kDenseSlots];
+};
+
+__device__ __forceinline__ DenseCoef dense_load(const gnpde_stage_epilogue_t& st) {
+  DenseCoef d;
+  const float* tab = st.dense_tab;
+  d.on = __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, tab[0])) != 0;
+#pragma unroll
+  for (int q = 0; q < kDenseSlots; ++q)
+    d.c[q] = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, tab[1 + q])));
+  return d;
+}
+
+__device__ __forceinline__ void dense_coefs(const gnpde_stage_epilogue_t& st, float* tab) {
+  const double t0 = st.dense_t[0], tout = st.dense_t[1], h = *st.dense_dt;
+  const bool on = t0 < tout && tout <= t0 + h;
+  const double x = on ? (tout - t0) / h : 0.0;
+  const double x2 = x * x, x3 = x2 * x, x4 = x2 * x2;
+  const double cy0 = 1.0 - 11.0 * x2 + 18.0 * x3 - 8.0 * x4;
+  const double cy1 = -5.0 * x2 + 14.0 * x3 - 8.0 * x4;
+  const double cym = 16.0 * x2 - 32.0 * x3 + 16.0 * x4;
+  const double w[GNPDE_DENSE_BASIS] = {cy0 + cy1 + cym, h * cy1, h * cym, h * (x - 4.0 * x2 + 5.0 * x3 - 2.0 * x4),
+                                       h * (x2 - 3.0 * x3 + 2.0 * x4)};
+  tab[0] = __builtin_bit_cast(float, on ? 1 : 0);
+#pragma unroll
+  for (int q = 0; q < kDenseSlots; ++q) {
+    double c = 0.0;
+#pragma unroll
+    for (int m = 0; m < GNPDE_DENSE_BASIS; ++m) c = fma(w[m], (double)st.dense_m[m][q], c);
+    tab[1 + q] = (float)c;
+  }
+}
+
 // The wide stage epilogue of one row slice (STG 4; also gnpde_stage_apply_*):
 // every output and the error combination start from cb*base (x when the base is
 // the RHS input xid, with values xv), take sc*c[j]*k[j] for j ascending, then
 // sc*cf*f — per output the same order as stage_combine, so the same bits.
 // Returns the error combination in ev (when err_rows), output values in r and,
-// when y0v is given and err_rows is set, the tolerance's y0 row slice.
-template <int VEC, class T, int NKMAX = GNPDE_STAGE_MAX_K, int NOUT = 2, bool ERR = true, int PK = 0>
+// when y0v is given and err_rows is set, the tolerance's y0 row slice.  DENSE (STG
+// 5): also the dense output sum_q dc[q] * operand q in rd (base of output 0, k[j], f).
+template <int VEC, class T, int NKMAX = GNPDE_STAGE_MAX_K, int NOUT = 2, bool ERR = true, int PK = 0,
+          bool DENSE = false>
 __device__ __forceinline__ void wide_combine(const gnpde_stage_epilogue_t& st, int64_t off, const float (&o)[VEC],
                                              const float* xid, const float (&xv)[VEC], float (&r)[2][VEC],
                                              float (&ev)[VEC], Packed<VEC, T>* y0v = nullptr,
-                                             const Packed<VEC, T>* pre = nullptr) {
+                                             const Packed<VEC, T>* pre = nullptr, const float* dc = nullptr,
+                                             float* rd = nullptr) {
   const float sc = stage_scale(st);
   float sco[NOUT];  // the outputs' coefficient scales (the error term's is sc)
 #pragma unroll
@@ -648,6 +699,13 @@ __device__ __forceinline__ void wide_combine(const gnpde_stage_epilogue_t& st, i
         const bool isx = xid != nullptr && slot < st.n_out && st.o[slot].base == xid;
 #pragma unroll
         for (int t = 0; t < VEC; ++t) r[slot][t] = cb[slot] * (isx ? xv[t] : unpack(vq, t));
+        if constexpr (DENSE) {
+          if (slot == 0) {
+            const bool on = st.n_out > 0 && st.o[0].base != nullptr;
+#pragma unroll
+            for (int t = 0; t < VEC; ++t) rd[t] = on ? dc[0] * (isx ? xv[t] : unpack(vq, t)) : 0.f;
+          }
+        }
         if (ERR && y0v && has_err && w.p[q] != nullptr && w.p[q] == st.err_y0) *y0v = vq;  // y0 = this base
       } else if (slot < NOUT + NKMAX) {
         const int j = slot - NOUT;
@@ -661,6 +719,11 @@ __device__ __forceinline__ void wide_combine(const gnpde_stage_epilogue_t& st, i
           const float c = (on && i < st.n_out) ? st.o[i].c[j] * sco[i] : 0.f;
 #pragma unroll
           for (int t = 0; t < VEC; ++t) r[i][t] = fmaf(c, kv[t], r[i][t]);
+        }
+        if constexpr (DENSE) {
+          const float c = on ? dc[1 + j] : 0.f;
+#pragma unroll
+          for (int t = 0; t < VEC; ++t) rd[t] = fmaf(c, kv[t], rd[t]);
         }
         if constexpr (ERR) {
           const float c = (on && has_err) ? st.err.c[j] * sc : 0.f;
@@ -688,6 +751,10 @@ __device__ __forceinline__ void wide_combine(const gnpde_stage_epilogue_t& st, i
 #pragma unroll
       for (int t = 0; t < VEC; ++t) ev[t] = fmaf(cf, o[t], ev[t]);
     }
+    if constexpr (DENSE) {
+#pragma unroll
+      for (int t = 0; t < VEC; ++t) rd[t] = fmaf(dc[kDenseSlots - 1], o[t], rd[t]);
+    }
     return;
   }
   // (the fallback for rows past the buffer range: an operand equal to the RHS input is
@@ -712,6 +779,16 @@ __device__ __forceinline__ void wide_combine(const gnpde_stage_epilogue_t& st, i
   for (int i = 0; i < NOUT; ++i)
     if (i < st.n_out) base_term(st.o[i], r[i]);
   if (has_err) base_term(st.err, ev);
+  if constexpr (DENSE) {
+    if (st.n_out > 0) {
+      gnpde_stage_out_t so = st.o[0];
+      so.cb = dc[0];
+      base_term(so, *reinterpret_cast<float(*)[VEC]>(rd));
+    } else {
+#pragma unroll
+      for (int t = 0; t < VEC; ++t) rd[t] = 0.f;
+    }
+  }
 #pragma unroll
   for (int j = 0; j < NKMAX; ++j) {
     if (j < st.nk) {
@@ -734,6 +811,10 @@ __device__ __forceinline__ void wide_combine(const gnpde_stage_epilogue_t& st, i
 #pragma unroll
         for (int t = 0; t < VEC; ++t) ev[t] = fmaf(c, kv[t], ev[t]);
       }
+      if constexpr (DENSE) {
+#pragma unroll
+        for (int t = 0; t < VEC; ++t) rd[t] = fmaf(dc[1 + j], kv[t], rd[t]);
+      }
     }
   }
 #pragma unroll
@@ -748,6 +829,10 @@ __device__ __forceinline__ void wide_combine(const gnpde_stage_epilogue_t& st, i
     const float cf = st.err.cf * sc;
 #pragma unroll
     for (int t = 0; t < VEC; ++t) ev[t] = fmaf(cf, o[t], ev[t]);
+  }
+  if constexpr (DENSE) {
+#pragma unroll
+    for (int t = 0; t < VEC; ++t) rd[t] = fmaf(dc[kDenseSlots - 1], o[t], rd[t]);
   }
 }
 
@@ -804,16 +889,27 @@ __device__ __forceinline__ void epi_finish(const Epi& e, int64_t row, int cc, co
   if (e.st.f_out) store_vec<VEC>(as_t<T>(e.st.f_out) + off, o);
   // the stage outputs' row (out_rows: the last step of a renumbered solve writes the caller's numbering)
   const int64_t oo = e.st.out_rows ? (int64_t)e.st.out_rows[row] * e.ldf + cc : off;
-  if constexpr (STG == 4) {
-    float xv[VEC], r[2][VEC], ev[VEC];
+  if constexpr (stage_wide<STG>()) {
+    constexpr bool DENSE = STG == 5;
+    float xv[VEC], r[2][VEC], ev[VEC], rd[VEC];
     Packed<VEC, T> y0v;
 #pragma unroll
     for (int t = 0; t < VEC; ++t) xv[t] = need_x ? unpack(p.xr, t) : 0.f;
-    wide_combine<VEC, T, GNPDE_STAGE_MAX_K, 2, true, GNPDE_STG4_PRE>(
-        e.st, off, o, (need_x && e.ldx == e.ldf) ? e.x : nullptr, xv, r, ev, &y0v, GNPDE_STG4_PRE > 0 ? p.wk : nullptr);
+    DenseCoef dc;
+    if constexpr (DENSE) dc = dense_load(e.st);
+    wide_combine<VEC, T, GNPDE_STAGE_MAX_K, 2, true, GNPDE_STG4_PRE, DENSE>(
+        e.st, off, o, (need_x && e.ldx == e.ldf) ? e.x : nullptr, xv, r, ev, &y0v, GNPDE_STG4_PRE > 0 ? p.wk : nullptr,
+        DENSE ? dc.c : nullptr, DENSE ? rd : nullptr);
 #pragma unroll
     for (int i = 0; i < 2; ++i)
       if (i < e.st.n_out) store_vec<VEC>(as_t<T>(e.st.o[i].out) + oo, r[i]);
+    if constexpr (DENSE) {
+      if (dc.on) {  // wave-uniform: the step crosses the output time
+        T* dout = reinterpret_cast<T*>(*e.st.dense_out);
+        const int64_t od = e.st.dense_rows ? (int64_t)e.st.dense_rows[row] * e.ldf + cc : off;
+        store_vec<VEC>(dout + od, rd);
+      }
+    }
     if (e.st.err_rows && dpart) {
       float y1[VEC];
 #pragma unroll
@@ -967,7 +1063,7 @@ template <int GL, int STG, class T>
 __device__ __forceinline__ void epi_rowsums(const Epi& e, int64_t row, const double* dpart, int base, bool store,
                                             const double* prev = nullptr) {
   if constexpr (stage_rowsum<STG, T>()) {
-    if constexpr (STG == 4) {
+    if constexpr (stage_wide<STG>()) {
       if (e.st.err_rows) epi_rowsum_store_any<GL>(e, row, dpart[0], base, store);
       if constexpr (sizeof(T) == 4)
         if (e.st.dot_rows) epi_rowsum_store_any<GL>(e, row, dpart[1], base, store, nullptr, true);
@@ -986,7 +1082,7 @@ inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 // the adaptive solvers).
 inline int epi_stage_kind(const Epi& e) {
   if (!e.has_stage) return 0;
-  if (e.st.err_rows || e.st.nk > kStagePre) return 4;
+  if (e.st.err_rows || e.st.nk > kStagePre || e.st.dense_out) return 4;  // (5 = 4 + dense_out: launch_agg_cfg)
   if (e.st.n_out <= 1) return e.st.dot_rows ? 3 : 1;
   return 2;
 }

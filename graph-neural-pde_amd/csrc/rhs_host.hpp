@@ -66,6 +66,10 @@ inline int check_stage(const gnpde_stage_epilogue_t& st) {
     GNPDE_REQUIRE(st.atol >= 0.0 && st.rtol >= 0.0 && (st.atol > 0.0 || st.rtol > 0.0), GNPDE_EINVAL,
                   "stage: tolerances must be >= 0 and not both 0");
   }
+  // the folded dense output (ABI 8): its device slot, times and step size
+  if (st.dense_out)
+    GNPDE_REQUIRE(st.dense_t && st.dense_dt && st.dense_tab, GNPDE_EINVAL,
+                  "stage: dense_out without dense_t / dense_dt / dense_tab");
   return GNPDE_OK;
 }
 

@@ -335,6 +335,7 @@ static int stage_apply(int64_t R, int64_t C, int64_t ld, const T* f, const T* x,
   if (rc) return rc;
   const gnpde_stage_epilogue_t& st = *stage;
   GNPDE_REQUIRE(!st.dot_rows, GNPDE_EUNSUPPORTED, "stage_apply: dot_rows are fused into the RHS kernels only");
+  GNPDE_REQUIRE(!st.dense_out, GNPDE_EUNSUPPORTED, "stage_apply: dense_out is fused into the RHS kernel only");
   bool needs_x = st.err_rows && st.err_y1 < 0;
   for (int i = 0; i < st.n_out; ++i)
     GNPDE_REQUIRE(st.o[i].out != reinterpret_cast<const float*>(x), GNPDE_EINVAL, "stage_apply: output %d aliases x",
@@ -583,7 +584,8 @@ extern "C" int gnpde_segment_sums_f64(int64_t nseg, int64_t len, const double* v
 // steps, no separate sum launch).
 __global__ __launch_bounds__(256) void adaptive_control_kernel(const double* __restrict__ part, int nb, double n,
                                                                 double order, double safety, double ifactor,
-                                                                double dfactor, double* dt, float* scale, double* rec) {
+                                                                double dfactor, double* dt, float* scale, double* rec,
+                                                                double* t) {
   __shared__ double red[kBlock / kWave];
   double acc = 0.0;
   for (int i = threadIdx.x; i < nb; i += blockDim.x) acc += part[i];
@@ -604,11 +606,12 @@ __global__ __launch_bounds__(256) void adaptive_control_kernel(const double* __r
   rec[3] = e2;
   *dt = next;
   *scale = (float)next;
+  if (t && ratio <= 1.0) *t += h;  // the accepted step's end: the next step's start (dense_t)
 }
 
 extern "C" int gnpde_adaptive_control(int64_t nrows, const double* err_rows, double n, double order, double safety,
                                       double ifactor, double dfactor, double* dt, float* scale, double* rec,
-                                      void* workspace, size_t workspace_bytes, void* stream) {
+                                      double* t, void* workspace, size_t workspace_bytes, void* stream) {
   GNPDE_REQUIRE(nrows >= 0 && (err_rows || nrows == 0) && dt && scale && rec && workspace && order > 0.0,
                 GNPDE_EINVAL, "adaptive_control: bad arguments");
   GNPDE_REQUIRE(workspace_bytes >= sizeof(double) * kDotBlocks, GNPDE_EINVAL, "adaptive_control: workspace too small");
@@ -616,7 +619,8 @@ extern "C" int gnpde_adaptive_control(int64_t nrows, const double* err_rows, dou
   double* part = static_cast<double*>(workspace);
   sum_partial_kernel<<<kDotBlocks, kBlock, 0, s>>>(nrows, err_rows, part);
   GNPDE_LAUNCH_CHECK();
-  adaptive_control_kernel<<<1, kBlock, 0, s>>>(part, kDotBlocks, n, order, safety, ifactor, dfactor, dt, scale, rec);
+  adaptive_control_kernel<<<1, kBlock, 0, s>>>(part, kDotBlocks, n, order, safety, ifactor, dfactor, dt, scale, rec,
+                                               t);
   GNPDE_LAUNCH_CHECK();
   return GNPDE_OK;
 }

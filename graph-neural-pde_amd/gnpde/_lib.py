@@ -16,6 +16,8 @@ LIB_PATH = os.environ.get("GNPDE_LIB", os.path.join(_HERE, "libgnpde.so"))
 STAGE_MAX_OUT = 2
 STAGE_MAX_K = 6
 STAGE_PRE_K = 2  # operands the fixed-grid epilogues prefetch (csrc/common.hpp kStagePre)
+DENSE_BASIS = 5  # the folded dense output's basis polynomials (ABI 8)
+DENSE_SLOTS = STAGE_MAX_K + 2  # its operand slots: output 0's base, k[0..5], f
 
 
 class StageOut(ctypes.Structure):
@@ -32,7 +34,9 @@ class StageEpilogue(ctypes.Structure):
                 ("dot_coef", ctypes.c_double), ("dot_accumulate", ctypes.c_int),
                 ("err_rows", ctypes.c_void_p), ("err", StageOut), ("err_y0", ctypes.c_void_p), ("err_y1", ctypes.c_int),
                 ("atol", ctypes.c_double), ("rtol", ctypes.c_double), ("coef_scale", ctypes.c_void_p),
-                ("f_lin", ctypes.c_float), ("unscaled_outs", ctypes.c_int)]
+                ("f_lin", ctypes.c_float), ("unscaled_outs", ctypes.c_int),
+                ("dense_out", ctypes.c_void_p), ("dense_rows", ctypes.c_void_p), ("dense_t", ctypes.c_void_p),
+                ("dense_dt", ctypes.c_void_p), ("dense_tab", ctypes.c_void_p), ("dense_m", (ctypes.c_float * DENSE_SLOTS) * DENSE_BASIS)]
 
 
 c_i32p = ctypes.POINTER(ctypes.c_int32)
@@ -76,7 +80,7 @@ SIGNATURES = {
     "gnpde_rows_copy": (_int, [_vp, _i64, _i64, _vp, _vp, _vp, _vp]),
     "gnpde_threshold_mask_f32": (_int, [_vp, _i64, _vp, _vp, _vp, _vp]),
     "gnpde_initial_step_workspace_bytes": (_size, []),
-    "gnpde_adaptive_control": (_int, [_i64, _vp, _f64, _f64, _f64, _f64, _f64, _vp, _vp, _vp, _vp, _size, _vp]),
+    "gnpde_adaptive_control": (_int, [_i64, _vp, _f64, _f64, _f64, _f64, _f64, _vp, _vp, _vp, _vp, _vp, _size, _vp]),
     "gnpde_initial_step_f32": (_int, [_i64, _vp, _vp, _vp, _f64, _f64, _f64, _vp, _vp, _vp, _size, _vp]),
     "gnpde_scaled_sq_sums_f32": (_int, [_i64, _vp, _vp, _vp, _f64, _f64, _vp, _vp, _size, _vp]),
     "gnpde_segment_sums_workspace_bytes": (_size, [_i64]),
@@ -130,7 +134,7 @@ SIGNATURES = {
 }
 
 # constants mirrored from include/gnpde.h
-ABI_VERSION = 7
+ABI_VERSION = 8
 OK = 0
 EINVAL = -1
 EHIP = -2

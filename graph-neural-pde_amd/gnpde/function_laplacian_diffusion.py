@@ -157,6 +157,9 @@ class LaplacianODEFunc(ODEFunc):
     # f(x) = sigma(alpha)(A - I) x [+ beta x0] is affine in x with the weights fixed for a solve
     # (every block: constant, attention / hard_attention / mixed weights are computed once per forward)
     affine = True
+    # rhs_stage takes Stage.dense (the plain-weight K1): an adaptive solve in the Krylov basis may fold
+    # its dense output into the steps' last launch (integrator.DENSE_FOLD)
+    fold_dense = True
 
     def rhs_stage(self, t, x, stage, linear=False):
         """forward(t, x) with the solver's stage combination fused into the K1

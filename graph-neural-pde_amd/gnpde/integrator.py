@@ -1238,6 +1238,19 @@ class _KrylovPlan(object):
 
 
 KRYLOV_STEP = os.environ.get('GNPDE_KRYLOV_STEP', '1') != '0'
+_KRYLOV_PLANS = {}
+
+
+def _krylov_plan(plan):
+    """The _KrylovPlan of a tableau plan, built once (its fp64 sums cost ~50 us of host
+    time, which every solve paid before its first launch)."""
+    k = _KRYLOV_PLANS.get(plan.method)
+    if k is None:
+        k = _KRYLOV_PLANS[plan.method] = _KrylovPlan(plan)
+    return k
+# The dense output of a one-output-time Krylov solve folded into its steps' last launch
+# (ABI 8 Stage.dense; GNPDE_DENSE_FOLD=0: the separate pass of _interp_into)
+DENSE_FOLD = os.environ.get('GNPDE_DENSE_FOLD', '1') != '0'
 
 
 def _fused_adaptive_ok(func, y0, combine, options):
@@ -1347,7 +1360,18 @@ class _AdaptiveState(object):
         self.ws = None if host else torch.empty(_lib.fn("gnpde_dot_workspace_bytes")(), dtype=torch.uint8,
                                                 device=y0.device)
         self.rec_host, self.rec_slot = None, 0  # pinned copies of rec (_rec_reader)
-        self.graphs = {}   # (id Y, id K0, mid) -> (graph, error-sum tensor)
+        # the folded dense output (DENSE_FOLD): the device time {step start, output time} the controller
+        # advances, the slot holding the output array's address, the output row map (a copy: the
+        # captured launch reads this buffer whatever layout object the solve has)
+        # one device record {t0, t_out, output address} (fp64 / fp64 / int64 views) set per solve by one
+        # copy from a pinned host twin
+        self.dsc = None if host else torch.zeros(3, dtype=torch.float64, device=y0.device)
+        self.dsc_host = None if host else torch.zeros(3, dtype=torch.float64, pin_memory=True)
+        self.tdev = None if host else self.dsc[:2]
+        self.dslot = None if host else self.dsc[2:].view(torch.int64)
+        self.dtab = None if host else torch.zeros(_lib.DENSE_SLOTS + 1, dtype=torch.float32, device=y0.device)
+        self.drows, self.drows_src = None, None
+        self.graphs = {}   # (id Y, id K0, mid, fold, renumbered) -> (graph, error-sum tensor)
         self.mempool = None
         self.warm = False
 
@@ -1377,9 +1401,11 @@ class _RKAdaptiveFused(_RKAdaptive):
         self.krylov = None
         if self.affine and KRYLOV_STEP and P.ns <= _lib.STAGE_MAX_K and \
                 set(range(1, P.ns + 1)) <= (P.store | P.store_mid):
-            self.krylov = _KrylovPlan(P)
+            self.krylov = _krylov_plan(P)
         sc = self._scalars
         self.safety_f, self.ifactor_f, self.dfactor_f = float(sc['safety']), float(sc['ifactor']), float(sc['dfactor'])
+        self.fold = False  # this solve's dense output folded into the Krylov steps (_integrate)
+        self.lay = None
 
     # ---- device primitives (host-stage RHS objects supply CPU versions: tests only)
     def _apply(self, stage, f, x, like):
@@ -1463,7 +1489,7 @@ class _RKAdaptiveFused(_RKAdaptive):
                 self._launch(i, st, bufs['X%d' % i], ti, mid)
         if self._dev_control():  # the error sum and the controller: two launches, no host work
             ops.adaptive_control(st.rows, st.rows.numel() * self.C, self.order, self.safety_f, self.ifactor_f,
-                                 self.dfactor_f, st.dt, st.scale, st.rec, ws=st.ws)
+                                 self.dfactor_f, st.dt, st.scale, st.rec, ws=st.ws, t=st.tdev)
             return st.rec
         return self._err_sum(st.rows)
 
@@ -1482,8 +1508,31 @@ class _RKAdaptiveFused(_RKAdaptive):
         outs = [(bufs['Y1'], bufs['Y'], 1.0, 0.0, [(u[p], c) for p, c in y1t]),
                 (bufs['K%d' % ns], None, 0.0, fcf, [(u[p], c) for p, c in ft])]
         err = (st.rows, (None, 0.0, ecf, [(u[p], c) for p, c in et]), bufs['Y'], 0, self.atol_f, self.rtol_f)
-        self.func.rhs_stage(t, u[ns - 1], ops.Stage(outs=outs, err=err, scale=st.scale, f_lin=1.0, unscaled=(1,)),
-                            linear=True)
+        dense = None
+        if self.fold:
+            dense = (st.dslot, st.drows if self.lay is not None else None, st.tdev, st.dt, st.dtab,
+                     self._dense_table(u, ft, fcf))
+        self.func.rhs_stage(t, u[ns - 1], ops.Stage(outs=outs, err=err, scale=st.scale, f_lin=1.0, unscaled=(1,),
+                                                    dense=dense), linear=True)
+
+    def _dense_table(self, u, ft, fcf):
+        """The basis coefficients of the step's dense output over the last Krylov launch's
+        operands (ABI 8 Stage.dense): with w = (cy0 + cy1 + cym, h cy1, h cym, cf0, cf1),
+        out = w0 y0 + sum_p [w1 G[p] + w2 (Mu[p] + c_mid[ns] f1_p) + w3 [p = 0] + w4 f1_p] u_p
+              + (w2 c_mid[ns] + w4) fcf f'
+        where f1 = sum_p f1_p u_p + fcf f' is the next step's f0 (u_ns substituted) — the
+        combination _interp_into forms from y0, the u_p and f1 in a pass of its own."""
+        K, P = self.krylov, self.plan
+        ns = K.ns
+        cm = P.c_mid[ns]
+        f1 = dict(ft)
+        table = {'base': [1.0, 0.0, 0.0, 0.0, 0.0], 'f': [0.0, 0.0, cm * fcf, 0.0, fcf]}
+        for p in range(ns):
+            b = f1.get(p, 0.0)
+            w = [0.0, K.G[p], K.Mu[p] + cm * b, 1.0 if p == 0 else 0.0, b]
+            if any(v != 0.0 for v in w):
+                table[u[p]] = w
+        return table
 
     def _dev_control(self):
         """The step-size controller runs on the device (a device solve with the
@@ -1568,7 +1617,7 @@ class _RKAdaptiveFused(_RKAdaptive):
         on first use once the module is warm), eagerly otherwise."""
         P = self.plan
         if graphs_ok and st.warm and _nfe_headroom(self.func, P.ns):
-            gk = (id(st.bufs['Y']), id(st.bufs['K0']), bool(mid))
+            gk = (id(st.bufs['Y']), id(st.bufs['K0']), bool(mid), self.fold, self.lay is not None)
             ent = st.graphs.get(gk)
             if ent is None:
                 nfe = getattr(self.func, 'nfe', None)
@@ -1618,6 +1667,25 @@ class _RKAdaptiveFused(_RKAdaptive):
         dev = y0.device
         st, graphs_ok = self._state(y0)
         bufs = st.bufs
+        # The dense output folded into the last launch of every step (DENSE_FOLD; ABI 8): a
+        # solve to one output time in the Krylov basis under the device controller.  Each
+        # step's launch writes the interpolant at th[1] straight into sol[1] (the caller's
+        # numbering) when the step crosses it, by the device time the controller advances;
+        # the accepted crossing step writes last (a rejected or discarded step either does
+        # not cross or is followed by one that does), so no dense-output pass follows.
+        self.fold = (DENSE_FOLD and not self.host and self.krylov is not None and self._dev_control() and
+                     len(th) == 2 and th[1] > th[0] and getattr(self.func, 'fold_dense', False))
+        if not self.host:
+            hv = st.dsc_host
+            hv[0], hv[1] = th[0], th[-1]
+            hv[2:].view(torch.int64)[0] = sol[1].data_ptr() if self.fold else 0
+            st.dsc.copy_(hv, non_blocking=True)
+        if self.fold:
+            if lay is not None and st.drows_src is not lay.order32:
+                if st.drows is None:
+                    st.drows = torch.empty_like(lay.order32)
+                st.drows.copy_(lay.order32)
+                st.drows_src = lay.order32
         if self.host:
             sol[0].copy_(y0)
             bufs['Y'].copy_(y0)
@@ -1693,7 +1761,7 @@ class _RKAdaptiveFused(_RKAdaptive):
                 # enqueued before its record is read, so the pass follows the step on the device
                 # without the host's round trip; used if the step is accepted (a rejected step's
                 # successor writes the output again)
-                if spec_ok and mid and ahead is None and t_cur + dt > next_t:
+                if spec_ok and mid and ahead is None and t_cur + dt > next_t and not self.fold:
                     self._dense = dict(bufs, scale=dt)
                     self._interp_into(sol[i_out], (t_cur, dt), next_t, t_cur + dt, lay)
                     pre_interp = (i_out, t_cur, dt)
@@ -1719,6 +1787,7 @@ class _RKAdaptiveFused(_RKAdaptive):
                     self._rotate(bufs, kn, -1)
                     st.dt.fill_(dt_next)
                     st.scale.fill_(dt_next)
+                    st.tdev[0].fill_(t_cur)  # (the discarded step's controller may have advanced it)
                     if hasattr(self.func, 'nfe'):
                         self.func.nfe -= P.ns
                 if dt_next is not None:
@@ -1734,7 +1803,7 @@ class _RKAdaptiveFused(_RKAdaptive):
                     sol[i_out].copy_(bufs['Y'])
                 else:
                     _to_user(bufs['Y'], sol[i_out], lay)
-            elif pre_interp != (i_out,) + tuple(last):  # (not already enqueued for this step)
+            elif pre_interp != (i_out,) + tuple(last) and not self.fold:  # (not already enqueued / folded)
                 self._interp_into(sol[i_out], last, next_t, t_cur, lay)
         return sol
 
@@ -1852,6 +1921,7 @@ def odeint(func, y0, t, rtol=1e-7, atol=1e-9, method=None, options=None, combine
             odeint.last_path = 'restated'
         out = solver.integrate(t)
         odeint.last_n_steps = solver.n_steps
+        odeint.last_dense_fold = bool(getattr(solver, 'fold', False))
         return out
     raise NotImplementedError("gnpde.odeint: method %r not supported (supported: %s)" %
                               (method, ', '.join(FIXED_METHODS + ADAPTIVE_METHODS)))
@@ -1859,6 +1929,7 @@ def odeint(func, y0, t, rtol=1e-7, atol=1e-9, method=None, options=None, combine
 
 odeint.last_n_steps = 0
 odeint.last_path = None  # the last adaptive solve's loop: 'fused_krylov', 'fused_stage' or 'restated'
+odeint.last_dense_fold = False  # whether its dense output was folded into the steps (DENSE_FOLD)
 
 
 # --------------------------------------------------------------------------- adjoint

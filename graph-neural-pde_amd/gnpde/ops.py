@@ -582,10 +582,18 @@ class Stage(object):
     ``err`` (the adaptive solvers' embedded-pair error rows): (rows, (base, cb,
     cf, [(k_j, c_j)...]), y0, y1_out, atol, rtol) -> rows[r] = sum_c (e / tol)^2
     in fp64 with e the combination, tol = atol + rtol * max(|y0|, |y1|), y1 = the
-    RHS input (y1_out = -1) or output ``y1_out``."""
+    RHS input (y1_out = -1) or output ``y1_out``.
+
+    ``dense`` (ABI 8, the plain-weight K1 only): the step's dense output folded into
+    the launch — (slot, rows, t, dt, tab, table): ``slot`` a device int64 holding the
+    output array's address, ``rows`` its int32 row map or None, ``t`` device fp64
+    {step start, output time}, ``dt`` the device fp64 step size, ``tab`` device fp32
+    scratch of STAGE_MAX_K + 3 (the launch's coefficients), ``table`` the
+    basis coefficients: {'base': [5], 'f': [5], k tensor: [5]} over w = (cy0 + cy1 +
+    cym, h cy1, h cym, cf0, cf1) of torchdiffeq's interpolant (include/gnpde.h)."""
 
     def __init__(self, f_out=None, outs=(), out_rows=None, dot=None, err=None, scale=None, f_lin=0.0,
-                 unscaled=()):
+                 unscaled=(), dense=None):
         self.f_out = f_out
         # indices of the outputs whose cf / c_j do NOT take ``scale`` (ABI 6 unscaled_outs)
         self.unscaled = tuple(unscaled)
@@ -598,11 +606,14 @@ class Stage(object):
         # (y, rows, coef, accumulate) or None: rows[r] (+)= coef * <f[r], y[r]> in fp64 (fp32 state)
         self.dot = dot
         self.err = err
+        self.dense = dense
 
     def _operands(self):
         """The distinct k tensors of every combination, in first-use order."""
         ks, seen = [], set()
         combos = [o[4] for o in self.outs] + ([self.err[1][3]] if self.err is not None else [])
+        if self.dense is not None:
+            combos.append([(k, 0.0) for k in self.dense[5] if isinstance(k, torch.Tensor)])
         for terms in combos:
             for k, _ in terms:
                 if k.data_ptr() not in seen:
@@ -691,6 +702,32 @@ class Stage(object):
             st.coef_scale = self.scale.data_ptr()
         st.f_lin = self.f_lin
         st.unscaled_outs = sum(1 << i for i in self.unscaled)
+        if self.dense is not None:
+            dslot, drows, dtt, ddt, dtab, table = self.dense
+            _require_gpu(dslot, "dense slot", torch.int64)
+            _require_gpu(dtab, "dense coefficient scratch", torch.float32)
+            if dtab.numel() < _lib.DENSE_SLOTS + 1:
+                raise ValueError("dense: coefficient scratch of %d floats" % (_lib.DENSE_SLOTS + 1))
+            st.dense_tab = dtab.data_ptr()
+            _require_gpu(dtt, "dense times", torch.float64)
+            _require_gpu(ddt, "dense step", torch.float64)
+            if shift or not self.outs or dtt.numel() < 2:
+                raise ValueError("dense: needs output 0 (its base is y0), two times and unshifted buffers")
+            st.dense_out, st.dense_t, st.dense_dt = dslot.data_ptr(), dtt.data_ptr(), ddt.data_ptr()
+            if drows is not None:
+                _require_gpu(drows, "dense rows", torch.int32)
+                if drows.numel() * ref.shape[-1] != ref.numel():
+                    raise ValueError("dense rows must hold one row index per RHS row")
+                st.dense_rows = drows.data_ptr()
+            for key, w in table.items():
+                if isinstance(key, str):
+                    q = {'base': 0, 'f': _lib.DENSE_SLOTS - 1}[key]
+                else:
+                    q = 1 + slot[key.data_ptr()]
+                if len(w) != _lib.DENSE_BASIS:
+                    raise ValueError("dense: %d basis coefficients per operand" % _lib.DENSE_BASIS)
+                for m, v in enumerate(w):
+                    st.dense_m[m][q] += float(v)
         return st
 
 
@@ -1419,22 +1456,26 @@ def initial_step(y0, f0, f1, atol, rtol, order, h, hf=None):
               _ptr(hf), _ptr(ws), nbytes, _stream(y0.device))
 
 
-def adaptive_control(err_rows, n, order, safety, ifactor, dfactor, dt, scale, rec, ws=None):
+def adaptive_control(err_rows, n, order, safety, ifactor, dfactor, dt, scale, rec, ws=None, t=None):
     """The step's error-row sum and torchdiffeq's step-size controller on the device
     (gnpde_adaptive_control): rec = {error ratio, dt, next dt, squared error sum};
-    dt (fp64 0-d) and scale (fp32 0-d) advance to the next step's size.  ``ws``: a
-    reusable workspace (gnpde_dot_workspace_bytes() bytes)."""
+    dt (fp64 0-d) and scale (fp32 0-d) advance to the next step's size; ``t`` (fp64,
+    optional: its first element) advances by the step when it is accepted (the step
+    start a folded dense output reads, Stage.dense).  ``ws``: a reusable workspace
+    (gnpde_dot_workspace_bytes() bytes)."""
     _require_gpu(err_rows, "err_rows", torch.float64)
     _require_gpu(dt, "dt", torch.float64)
     _require_gpu(scale, "scale", torch.float32)
     _require_gpu(rec, "rec", torch.float64)
     if rec.numel() < 4:
         raise ValueError("adaptive_control: rec needs 4 doubles")
+    if t is not None:
+        _require_gpu(t, "t", torch.float64)
     nbytes = _lib.fn("gnpde_dot_workspace_bytes")()
     if ws is None:
         ws = torch.empty(nbytes, dtype=torch.uint8, device=err_rows.device)
     _lib.call("gnpde_adaptive_control", err_rows.numel(), _ptr(err_rows), float(n), float(order), float(safety),
-              float(ifactor), float(dfactor), _ptr(dt), _ptr(scale), _ptr(rec), _ptr(ws), ws.numel(),
+              float(ifactor), float(dfactor), _ptr(dt), _ptr(scale), _ptr(rec), _ptr(t), _ptr(ws), ws.numel(),
               _stream(err_rows.device))
 
 

@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define GNPDE_ABI_VERSION 7
+#define GNPDE_ABI_VERSION 8
 
 #define GNPDE_OK 0
 #define GNPDE_EINVAL (-1)
@@ -236,9 +236,26 @@ size_t gnpde_plan_workspace_bytes(int64_t R);
  * <L^T a_i, y_i> in the launch that forms the next adjoint stage input and its
  * error rows, gnpde.integrator), fused into the plain-weight
  * K1 (gnpde_spmm_rhs_f32 / _bf16); the attention kernels return
- * GNPDE_EUNSUPPORTED for it (the caller applies it with gnpde_stage_apply_*).  */
+ * GNPDE_EUNSUPPORTED for it (the caller applies it with gnpde_stage_apply_*).
+ * dense_out (NULL = none; ABI 8; plain-weight K1 with err_rows only): the dense
+ * output of the adaptive step folded into its last launch.  With the device
+ * fp64 scalars t0 = dense_t[0] (the step's start), t_out = dense_t[1] and
+ * h = *dense_dt (the step size), when t0 < t_out <= t0 + h (the step crosses the
+ * output time; wave-uniform, nothing is written otherwise):
+ *   x = (t_out - t0)/h, the basis w = {cy0 + cy1 + cym, h cy1, h cym, cf0, cf1}
+ *   of torchdiffeq's 4th-order interpolant (cy0 = 1 - 11x^2 + 18x^3 - 8x^4,
+ *   cy1 = -5x^2 + 14x^3 - 8x^4, cym = 16x^2 - 32x^3 + 16x^4,
+ *   cf0 = h (x - 4x^2 + 5x^3 - 2x^4), cf1 = h (x^2 - 3x^3 + 2x^4)),
+ *   out[dense_rows[r]] = sum_m w[m] (dense_m[m][0] o[0].base[r]
+ *                        + sum_{j<nk} dense_m[m][1+j] k[j][r] + dense_m[m][7] f[r])
+ * (coefficients formed in fp64, applied in fp32; f after f_lin), out = *dense_out
+ * (a device slot holding the output array: the launch can be captured once and
+ * its output redirected per solve).  dense_tab: device scratch of
+ * GNPDE_STAGE_MAX_K + 3 floats (the crossing flag and the coefficients, formed by
+ * a one-wavefront launch ahead of the aggregation).                          */
 #define GNPDE_STAGE_MAX_OUT 2
 #define GNPDE_STAGE_MAX_K 6
+#define GNPDE_DENSE_BASIS 5
 typedef struct {
   float* out;
   const float* base;
@@ -267,6 +284,12 @@ typedef struct {
   const float* coef_scale;
   float f_lin;
   int unscaled_outs;
+  float* const* dense_out;
+  const int32_t* dense_rows;
+  const double* dense_t;
+  const double* dense_dt;
+  float* dense_tab;
+  float dense_m[GNPDE_DENSE_BASIS][GNPDE_STAGE_MAX_K + 2];
 } gnpde_stage_epilogue_t;
 
 /* The stage epilogue as a pass of its own, over rows [0, R) of C columns
@@ -581,11 +604,13 @@ int gnpde_dot_f64(int64_t n, const float* a, const float* b, double* out, void* 
  *   next  = ratio == 0 ? dt ifactor
  *         : dt min(ifactor, max(safety ratio^(-1/order), ratio < 1 ? 1 : dfactor))
  * rec[0..3] = {ratio, dt, next, e2}; *dt = next; *scale = (float)next (the
- * coef_scale of the next step's launches).  Device pointers; two launches;
- * workspace gnpde_dot_workspace_bytes().                                    */
+ * coef_scale of the next step's launches); t (ABI 8, NULL = none): the device
+ * time of the solve, *t += dt when the step is accepted (ratio <= 1) — the step
+ * start a folded dense output reads (stage dense_t).  Device pointers; two
+ * launches; workspace gnpde_dot_workspace_bytes().                           */
 int gnpde_adaptive_control(int64_t nrows, const double* err_rows, double n, double order, double safety,
-                           double ifactor, double dfactor, double* dt, float* scale, double* rec, void* workspace,
-                           size_t workspace_bytes, void* stream);
+                           double ifactor, double dfactor, double* dt, float* scale, double* rec, double* t,
+                           void* workspace, size_t workspace_bytes, void* stream);
 size_t gnpde_initial_step_workspace_bytes(void);
 /* The squared sums of gnpde_initial_step_f32 without its scalar rules (ABI 7): the
  * per-component pieces of a mixed norm (torchdiffeq's adjoint norm: the max over the

@@ -450,13 +450,14 @@ ADAPTIVE_TABLEAUS = {
 }
 
 
-def odeint_adaptive(func, y0, ts, method, rtol, atol):
+def odeint_adaptive(func, y0, ts, method, rtol, atol, first_step=None):
     """torchdiffeq 0.2.x ``RKAdaptiveStepsizeODESolver`` in float64 numpy: initial
     step from ``_select_initial_step`` (Hairer's d0/d1/d2 rule), RMS error ratio
     over ``atol + rtol*max(|y0|,|y1|)``, step factor ``min(10, max(0.9 r^(-1/order),
     0.2 if rejected else 1))``, the next step's f0 = the last stage (as torchdiffeq,
     also for the non-FSAL pairs) and the quartic ``_interp_fit`` dense output at
-    every requested time.  Returns (solution [len(ts), ...], n_steps).  Parity
+    every requested time.  ``first_step`` replaces the initial-step rule (torchdiffeq's
+    options['first_step']).  Returns (solution [len(ts), ...], n_steps).  Parity
     unpinned (torchdiffeq absent): checked against exact flows."""
     order, A, b, e, mid = ADAPTIVE_TABLEAUS[method]
     fsal = b[-1] == 0 and list(b[:-1]) == list(A[-1])
@@ -470,7 +471,7 @@ def odeint_adaptive(func, y0, ts, method, rtol, atol):
     f_probe = func(ts[0] + h0, y + h0 * f)
     d2 = rms((f_probe - f) / sc) / h0
     h1 = max(1e-6, h0 * 1e-3) if (d1 <= 1e-15 and d2 <= 1e-15) else (0.01 / max(d1, d2)) ** (1.0 / order)
-    h = min(100 * h0, h1)
+    h = min(100 * h0, h1) if first_step is None else float(first_step)
     t = ts[0]
     out = [y]
     seg = None  # (t_a, t_b, y_a, y_b, f_a, f_b, y_mid) of the last accepted step

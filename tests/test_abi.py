@@ -46,7 +46,7 @@ def test_library_built_from_these_sources():
 
 
 def test_abi_version():
-    assert _lib.load().gnpde_abi_version() == _lib.ABI_VERSION == 7
+    assert _lib.load().gnpde_abi_version() == _lib.ABI_VERSION == 8
 
 
 def test_library_is_gfx950_code_object():
@@ -136,11 +136,14 @@ def test_stage_struct_layout_matches_header():
     assert _lib.StageEpilogue.dot_coef.offset == _lib.StageEpilogue.out_rows.offset + 24
     assert _lib.StageEpilogue.err.offset == _lib.StageEpilogue.dot_coef.offset + 24
     # ... err_y0, err_y1 (padded), atol, rtol, coef_scale, f_lin, unscaled_outs
-    assert ctypes.sizeof(_lib.StageEpilogue) == _lib.StageEpilogue.err.offset + so + 8 + 8 + 8 + 8 + 8 + 8
+    assert _lib.StageEpilogue.dense_out.offset == _lib.StageEpilogue.err.offset + so + 8 + 8 + 8 + 8 + 8 + 8
     assert _lib.StageEpilogue.coef_scale.offset == _lib.StageEpilogue.rtol.offset + 8
     assert _lib.StageEpilogue.f_lin.offset == _lib.StageEpilogue.coef_scale.offset + 8
-    # unscaled_outs (ABI 6) fills f_lin's padding: the size is ABI 5's
+    # unscaled_outs (ABI 6) fills f_lin's padding
     assert _lib.StageEpilogue.unscaled_outs.offset == _lib.StageEpilogue.f_lin.offset + 4
+    # ABI 8: dense_out, dense_rows, dense_t, dense_dt, dense_tab, dense_m[5][8] floats
+    assert _lib.StageEpilogue.dense_m.offset == _lib.StageEpilogue.dense_out.offset + 5 * 8
+    assert ctypes.sizeof(_lib.StageEpilogue) == _lib.StageEpilogue.dense_m.offset + 5 * 8 * 4
 
 
 def test_workspace_size_queries():
@@ -168,14 +171,17 @@ def test_c_header_struct_layout_with_gcc(tmp_path):
                    'offsetof(gnpde_stage_epilogue_t, dot_coef), offsetof(gnpde_stage_epilogue_t, dot_accumulate),'
                    'offsetof(gnpde_stage_epilogue_t, err), offsetof(gnpde_stage_epilogue_t, err_y1),'
                    'offsetof(gnpde_stage_epilogue_t, rtol), offsetof(gnpde_stage_epilogue_t, coef_scale),'
-                   'offsetof(gnpde_stage_epilogue_t, unscaled_outs));return 0;}\n')
+                   'offsetof(gnpde_stage_epilogue_t, unscaled_outs));'
+                   'printf("%zu %zu %zu\\n", offsetof(gnpde_stage_epilogue_t, dense_out),'
+                   'offsetof(gnpde_stage_epilogue_t, dense_tab), offsetof(gnpde_stage_epilogue_t, dense_m));return 0;}\n')
     exe = tmp_path / "layout"
     subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
     got = [int(v) for v in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()]
     E = _lib.StageEpilogue
     assert got == [ctypes.sizeof(_lib.StageOut), _lib.StageOut.c.offset, ctypes.sizeof(E), E.nk.offset, E.k.offset,
                    E.out_rows.offset, E.dot_coef.offset, E.dot_accumulate.offset, E.err.offset, E.err_y1.offset,
-                   E.rtol.offset, E.coef_scale.offset, E.unscaled_outs.offset]
+                   E.rtol.offset, E.coef_scale.offset, E.unscaled_outs.offset, E.dense_out.offset, E.dense_tab.offset,
+                   E.dense_m.offset]
 
 
 def test_stale_library_is_refused(monkeypatch):

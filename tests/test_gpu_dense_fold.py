@@ -1,0 +1,98 @@
+"""The dense output of a one-output-time Krylov dopri5 solve folded into the steps'
+last launch (ABI 8 gnpde_stage_epilogue_t.dense_out, integrator.DENSE_FOLD; reference
+anchor src/block_constant.py:46-51 — ODEblock.forward integrates to its one output
+time self.t[1] and torchdiffeq interpolates there).  The launch that writes y1, f1 and
+the error rows also writes torchdiffeq's 4th-order interpolant at the output time
+straight into sol[1] (in the caller's numbering) when the device time the controller
+advances says the step crosses it.
+
+Checked against the separate dense-output pass (GNPDE_DENSE_FOLD=0): the same step
+sequence, values within fp32 rounding of it (the coefficients are formed in fp64 on
+the device instead of the host, then rounded to fp32); against the oracle's float64
+restatement of torchdiffeq's loop with its step count; replayed solves bit-equal to
+the first; rejected steps (and discarded steps ahead) never leave their interpolant."""
+import numpy as np
+import pytest
+import torch
+
+import gnpde_oracle as O
+from gnpde import integrator as gi, ops
+
+from test_gpu_adaptive import DEV, RTOL, T, _graph, _laplacian, rel
+
+pytestmark = pytest.mark.gpu
+
+
+def _solve(func, x, ts, rtol, atol, opts=None):
+    tt = torch.tensor(ts, dtype=torch.float64, device=DEV)
+    with torch.no_grad():
+        z = gi.odeint(func, T(x), tt, rtol=rtol, atol=atol, method='dopri5', options=opts or {})
+    torch.cuda.synchronize()
+    return z.clone(), gi.odeint.last_n_steps, gi.odeint.last_dense_fold, gi.odeint.last_path
+
+
+@pytest.mark.parametrize("layout", [False, True])
+@pytest.mark.parametrize("add_source", [False, True])
+@pytest.mark.parametrize("rtol,T1", [(1e-3, 1.7), (1e-5, 2.3), (3e-2, 4.0)])
+def test_dense_fold_vs_pass_and_oracle(monkeypatch, layout, add_source, rtol, T1):
+    N, E, C = 4000, 40000, 64
+    eo, wo, rng = _graph(N, E, 41)
+    x = rng.standard_normal((1, N, C)).astype(np.float32)
+    x0 = rng.standard_normal((1, N, C)).astype(np.float32)
+    if layout:
+        monkeypatch.setattr(ops, "LAYOUT_MIN_ROWS", 1)
+        monkeypatch.setattr(ops, "LAYOUT_MIN_BYTES", 1)
+    ts = [0.0, T1]
+    res = {}
+    for fold in (False, True):
+        monkeypatch.setattr(gi, "DENSE_FOLD", fold)
+        func = _laplacian(C, eo, wo, alpha=0.3, add_source=add_source, x0=T(x0) if add_source else None)
+        if layout:
+            assert func.node_layout(T(x)) is not None
+        runs = [_solve(func, x, ts, rtol, rtol * 0.1) for _ in range(3)]  # eager, captured, replayed
+        for z, n, f, path in runs:
+            assert path == 'fused_krylov' and f == fold
+        assert all(torch.equal(runs[0][0], r[0]) and runs[0][1] == r[1] for r in runs[1:])
+        res[fold] = runs[0]
+    (zp, npass, _, _), (zf, nfold, _, _) = res[False], res[True]
+    assert nfold == npass
+    assert torch.equal(zf[0], zp[0])
+    assert rel(zf[1], zp[1]) <= 1e-6
+    f = lambda t, y: O.laplacian_rhs(eo, y, x0, 0.3, 0.4, edge_weight=wo, add_source=add_source)  # noqa: E731
+    want, n_want = O.odeint_adaptive(f, x, ts, 'dopri5', rtol, rtol * 0.1)
+    assert nfold == n_want
+    assert rel(zf, want) <= RTOL
+
+
+def test_dense_fold_rejections_and_steps_ahead(monkeypatch):
+    """A large first step (options first_step) forces rejections right away, with the
+    steps-ahead loop discarding a step already enqueued: the fold's output equals the
+    pass's, and the device time restored on each rejection keeps later crossings right."""
+    N, E, C = 3000, 30000, 32
+    eo, wo, rng = _graph(N, E, 43)
+    x = rng.standard_normal((1, N, C)).astype(np.float32)
+    out = {}
+    for fold in (False, True):
+        monkeypatch.setattr(gi, "DENSE_FOLD", fold)
+        func = _laplacian(C, eo, wo, alpha=2.0)
+        runs = [_solve(func, x, [0.0, 3.0], 1e-6, 1e-7, {'first_step': 2.5}) for _ in range(2)]
+        assert runs[1][2] == fold and torch.equal(runs[0][0], runs[1][0])
+        out[fold] = runs[1]
+    assert out[True][1] == out[False][1] and out[True][1] > 3
+    assert rel(out[True][0][1], out[False][0][1]) <= 1e-6
+    f = lambda t, y: O.laplacian_rhs(eo, y, None, 2.0, 0.0, edge_weight=wo)  # noqa: E731
+    want, n_want = O.odeint_adaptive(f, x, [0.0, 3.0], 'dopri5', 1e-6, 1e-7, first_step=2.5)
+    assert out[True][1] == n_want
+    assert rel(out[True][0], want) <= RTOL
+
+
+def test_dense_fold_only_for_one_output_time(monkeypatch):
+    """Several output times keep the dense-output pass (the device predicate knows one
+    output time); the fold is on by default for one."""
+    N, E, C = 2000, 16000, 32
+    eo, wo, rng = _graph(N, E, 47)
+    x = rng.standard_normal((1, N, C)).astype(np.float32)
+    func = _laplacian(C, eo, wo)
+    _, _, f2, _ = _solve(func, x, [0.0, 0.4, 1.0], 1e-4, 1e-5)
+    _, _, f1, _ = _solve(func, x, [0.0, 1.0], 1e-4, 1e-5)
+    assert not f2 and f1
