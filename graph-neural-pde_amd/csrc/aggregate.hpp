@@ -290,12 +290,6 @@ __device__ __forceinline__ void hub_arrive_slots(int4* heavy, int n_heavy, bool 
   }
 }
 
-// The folded dense output's crossing flag and coefficients (dense_coefs) ahead of the
-// launch that applies them (ABI 8 dense_out).
-static __global__ __launch_bounds__(64) void dense_coef_kernel(gnpde_stage_epilogue_t st) {
-  if (threadIdx.x == 0) dense_coefs(st, st.dense_tab);
-}
-
 // ------------------------------------------------------------------ aggregation kernel
 // Lane layout: RPW row slots of SL = 64/RPW lanes per wavefront (one plan item
 // each); inside a slot lane = g*GL + gl: G = SL/GL edges are gathered side by
@@ -318,6 +312,10 @@ __global__ __launch_bounds__(256) void agg_kernel(const int4* __restrict__ items
   const int g = sl / GL, gl = sl % GL;
   const int wid = uniform(xcd_block(ep.xcd_remap) * kWavesPerBlock + (threadIdx.x >> 6));
   const int item = wid * RPW + rs;
+  // the step's folded dense-output coefficients, for its last launch (ABI 8: a stage with
+  // dense_tab but no dense_out); kernel-argument branch
+  if (ep.has_stage && ep.st.dense_tab && !ep.st.dense_out && blockIdx.x == 0 && threadIdx.x == 0)
+    dense_coefs(ep.st, ep.st.dense_tab);
   if (wid * RPW >= n_items) return;
   // RPW = 3 (SL = 21): lane 63 is in no slot
   const bool live = item < n_items && rs < RPW;
@@ -497,11 +495,10 @@ static int launch_agg_cfg(const int4* items, int64_t n_items, int4* heavy, int64
       // the adaptive solvers' wide epilogue: plain weights only (the Laplacian RHS and
       // precomputed attention weights); the callers apply it after the other policies
       if constexpr (std::is_same<WP, PlainWeights>::value) {
-        if (ep.st.dense_out) {  // + the step's folded dense output (ABI 8): its coefficients first
-          dense_coef_kernel<<<1, kWave, 0, s>>>(ep.st);
+        if (ep.st.dense_out)  // + the step's folded dense output (ABI 8)
           agg_kernel<VEC, GL, NCH, U, RPW, 5, PlainWeights, T><<<grid, kBlock, 0, s>>>(
               items, (int)n_items, heavy, nh, col, as_plain(wp), C, ep, partials);
-        } else
+        else
           agg_kernel<VEC, GL, NCH, U, RPW, 4, PlainWeights, T><<<grid, kBlock, 0, s>>>(
               items, (int)n_items, heavy, nh, col, as_plain(wp), C, ep, partials);
       } else {

@@ -403,7 +403,8 @@ __device__ __forceinline__ void wide_slots(const gnpde_stage_epilogue_t& st, con
     bool dup = false;
 #pragma unroll
     for (int i = 0; i < NOUT; ++i) dup = dup || (w.p[i] != nullptr && w.p[i] == st.err_y0);
-    w.p[WideSlots<NOUT, NKMAX, ERR>::N - 1] = (has_err && !dup) ? st.err_y0 : nullptr;
+    // (nor when it is the RHS input: its values are held, wide_combine packs them)
+    w.p[WideSlots<NOUT, NKMAX, ERR>::N - 1] = (has_err && !dup && st.err_y0 != xid) ? st.err_y0 : nullptr;
   }
 }
 
@@ -459,6 +460,11 @@ constexpr bool stage_wide() {
 #endif
 #ifndef GNPDE_DOT_DIAG
 #define GNPDE_DOT_DIAG 0  // diagnostics only (wrong results): 1 no dot arithmetic, 2 no row reduction / store
+#endif
+#ifndef GNPDE_ERR_DIAG
+#define GNPDE_ERR_DIAG 0  // diagnostics only (wrong results): bit 1 no error-term arithmetic, bit 2 no row sum
+// (G-arxiv K1 with error rows and no output, round 6: 116 us; bit 1: 106; bit 2: 91 — the per-row
+// error sum at the end of every wave costs ~20 us of a launch; whole-granule row stores: no change)
 #endif
 #ifndef GNPDE_STG2_DW
 #define GNPDE_STG2_DW 1   // STG 2 prefetches its dot operand too (with GNPDE_DOT_PRE)
@@ -736,8 +742,12 @@ __device__ __forceinline__ void wide_combine(const gnpde_stage_epilogue_t& st, i
 #pragma unroll
           for (int t = 0; t < VEC; ++t) ev[t] = cb[NOUT] * (isx ? xv[t] : unpack(vq, t));
         }
-      } else if (y0v && w.p[q] != nullptr) {  // (NULL: deduplicated against a base, copied above)
-        *y0v = vq;
+      } else if (y0v) {  // the tolerance's y0
+        if (w.p[q] != nullptr)
+          *y0v = vq;
+        else if (ERR && has_err && xid != nullptr && st.err_y0 == xid)  // the RHS input row, held
+          pack_into<VEC, T>(xv, *y0v);
+        // (otherwise NULL: deduplicated against a base, copied above)
       }
     }
 #pragma unroll
@@ -836,24 +846,39 @@ __device__ __forceinline__ void wide_combine(const gnpde_stage_epilogue_t& st, i
   }
 }
 
-// sum_t (e_t / tol_t)^2 in fp64 with tol = atol + rtol * max(|y0|, |y1|): the
-// slice's share of the embedded pair's squared error norm.
+// sum_t (e_t / tol_t)^2 with tol = atol + rtol * max(|y0|, |y1|): the slice's share of
+// the embedded pair's squared error norm.  tol and the quotient in fp32 as torchdiffeq
+// forms them on an fp32 state (_compute_error_ratio: the 0-d fp64 atol / rtol do not
+// promote it), the squares summed in fp64 (round 6; the quotient was fp64, whose
+// division sequence cost the f0 / probe launches of the initial step 40-50 us each).
+// err_y1 = -2: tol = atol + rtol |y0| (y1 ignored).  aux (scale_rows): += sum (y0 / tol)^2.
 template <int VEC, class T>
 __device__ __forceinline__ double err_terms(const gnpde_stage_epilogue_t& st, int64_t off, const float (&ev)[VEC],
-                                            const float (&y1)[VEC], const Packed<VEC, T>* y0pre = nullptr) {
+                                            const float (&y1)[VEC], const Packed<VEC, T>* y0pre = nullptr,
+                                            double* aux = nullptr) {
   Packed<VEC, T> y0v;
   if (GNPDE_WIDE_BATCH && y0pre)  // loaded with the operands (wide_combine)
     y0v = *y0pre;
   else
     load_packed<VEC>(as_t<T>(st.err_y0) + off, y0v);
-  double d = 0.0;
+  if constexpr (GNPDE_ERR_DIAG & 1) return (double)ev[0] + (double)unpack(y0v, 0);
+  const bool y0only = st.err_y1 == -2;
+  const float at = (float)st.atol, rt = (float)st.rtol;
+  float d = 0.f, a = 0.f;
 #pragma unroll
   for (int t = 0; t < VEC; ++t) {
-    const double tol = st.atol + st.rtol * (double)fmaxf(fabsf(unpack(y0v, t)), fabsf(y1[t]));
-    const double q = (double)ev[t] / tol;
-    d = fma(q, q, d);
+    const float y = unpack(y0v, t);
+    const float ay0 = fabsf(y);
+    const float tol = __fadd_rn(at, __fmul_rn(rt, y0only ? ay0 : fmaxf(ay0, fabsf(y1[t]))));  // no fma: torch rounds twice
+    const float q = ev[t] / tol;
+    d = fmaf(q, q, d);
+    if (aux) {  // (the f0 launch of an adaptive solve only: tol is then atol + rtol |y0|)
+      const float qy = y / tol;
+      a = fmaf(qy, qy, a);
+    }
   }
-  return d;
+  if (aux) *aux += (double)a;
+  return (double)d;
 }
 
 // f = a*(ax - x) [+ b*x0]  (function_laplacian_diffusion.py:69-77) or f = ax,
@@ -914,7 +939,7 @@ __device__ __forceinline__ void epi_finish(const Epi& e, int64_t row, int cc, co
       float y1[VEC];
 #pragma unroll
       for (int t = 0; t < VEC; ++t) y1[t] = e.st.err_y1 == 1 ? r[1][t] : (e.st.err_y1 == 0 ? r[0][t] : xv[t]);
-      dpart[0] += err_terms<VEC, T>(e.st, off, ev, y1, &y0v);
+      dpart[0] += err_terms<VEC, T>(e.st, off, ev, y1, &y0v, e.st.scale_rows ? &dpart[1] : nullptr);
     }
     // the dot term of the wide epilogue (its second row sum, dpart[1]): <f, dot_with> of the
     // row slice, f as the other epilogues take it (after f_lin)
@@ -1015,11 +1040,32 @@ __device__ __forceinline__ double group_sum64(double v) {
   return v;
 }
 
+// The same in fp32 (the error / scale rows of the wide epilogue: fp32 quotients whose
+// squares torchdiffeq itself sums in fp32): one DPP add per step, one permute per
+// further doubling — a shorter chain at the end of every wave than the fp64 tree.
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov32(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xf, 0xf, false));
+}
+
+template <int GL>
+__device__ __forceinline__ float group_sum32(float v) {
+  if constexpr (GL >= 2) v += dpp_mov32<0xB1>(v);
+  if constexpr (GL >= 4) v += dpp_mov32<0x4E>(v);
+  if constexpr (GL >= 8) v += dpp_mov32<0x141>(v);
+  if constexpr (GL >= 16) v += dpp_mov32<0x140>(v);
+#pragma unroll
+  for (int o = 16; o < GL; o <<= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
 // prev: the row's running dot read before the gathers (GNPDE_DOT_PRE), or nullptr;
 // dot_ch: the dot channel whatever err_rows says (the wide epilogue's second row sum)
 __device__ __forceinline__ void epi_rowsum_write(const Epi& e, int64_t row, double v, const double* prev = nullptr,
                                                  bool dot_ch = false) {
-  if (e.st.err_rows && !dot_ch) {
+  if (dot_ch && e.st.scale_rows) {  // the wide epilogue's second row sum as scale_rows (ABI 8)
+    e.st.scale_rows[row] = v;
+  } else if (e.st.err_rows && !dot_ch) {
     e.st.err_rows[row] = v;
   } else if (e.st.dot_rows) {
     double* d = e.st.dot_rows + row;
@@ -1032,22 +1078,25 @@ __device__ __forceinline__ void epi_rowsum_write(const Epi& e, int64_t row, doub
 // of the wavefront, GL a power of two, base a multiple of GL) summed by a fixed
 // xor tree, stored by the first of them.  Called by every lane of the row's slot
 // (convergent).
-template <int GL>
+template <int GL, bool F32 = false>
 __device__ __forceinline__ void epi_rowsum_store(const Epi& e, int64_t row, double dpart, bool store,
                                                  const double* prev = nullptr, bool dot_ch = false) {
   static_assert((GL & (GL - 1)) == 0, "the xor tree needs power-of-two row lanes");
   if constexpr (GNPDE_DOT_DIAG == 2) return;
-  dpart = group_sum64<GL>(dpart);
+  if constexpr (F32)
+    dpart = (double)group_sum32<GL>((float)dpart);
+  else
+    dpart = group_sum64<GL>(dpart);
   if (store) epi_rowsum_write(e, row, dpart, prev, dot_ch);
 }
 
 // The same for any GL (e.g. 21 lanes: three bf16 rows of 168 columns per wavefront):
 // the first owner lane sums the slot's lanes base .. base + GL - 1 in order.
-template <int GL>
+template <int GL, bool F32 = false>
 __device__ __forceinline__ void epi_rowsum_store_any(const Epi& e, int64_t row, double dpart, int base, bool store,
                                                      const double* prev = nullptr, bool dot_ch = false) {
   if constexpr ((GL & (GL - 1)) == 0) {
-    epi_rowsum_store<GL>(e, row, dpart, store, prev, dot_ch);
+    epi_rowsum_store<GL, F32>(e, row, dpart, store, prev, dot_ch);
   } else {
     double tot = 0.0;
 #pragma unroll
@@ -1064,9 +1113,14 @@ __device__ __forceinline__ void epi_rowsums(const Epi& e, int64_t row, const dou
                                             const double* prev = nullptr) {
   if constexpr (stage_rowsum<STG, T>()) {
     if constexpr (stage_wide<STG>()) {
-      if (e.st.err_rows) epi_rowsum_store_any<GL>(e, row, dpart[0], base, store);
-      if constexpr (sizeof(T) == 4)
+      if constexpr (GNPDE_ERR_DIAG & 2) return;
+      // the error / scale rows: fp32 slice sums (err_terms), reduced in fp32 and stored as fp64
+      if (e.st.err_rows) epi_rowsum_store_any<GL, true>(e, row, dpart[0], base, store);
+      if (e.st.scale_rows) {
+        epi_rowsum_store_any<GL, true>(e, row, dpart[1], base, store, nullptr, true);
+      } else if constexpr (sizeof(T) == 4) {
         if (e.st.dot_rows) epi_rowsum_store_any<GL>(e, row, dpart[1], base, store, nullptr, true);
+      }
     } else {
       if (e.st.dot_rows || e.st.err_rows) epi_rowsum_store_any<GL>(e, row, dpart[0], base, store, prev);
     }

@@ -61,15 +61,18 @@ inline int check_stage(const gnpde_stage_epilogue_t& st) {
   // carries it as a second row sum (the adaptive adjoint's alpha integrand, gnpde.integrator)
   if (st.err_rows) {
     GNPDE_REQUIRE(st.err_y0 != nullptr, GNPDE_EINVAL, "stage: err_rows without err_y0");
-    GNPDE_REQUIRE(st.err_y1 >= -1 && st.err_y1 < st.n_out, GNPDE_EINVAL, "stage: err_y1=%d names no output",
+    GNPDE_REQUIRE(st.err_y1 >= -2 && st.err_y1 < st.n_out, GNPDE_EINVAL, "stage: err_y1=%d names no output",
                   st.err_y1);
     GNPDE_REQUIRE(st.atol >= 0.0 && st.rtol >= 0.0 && (st.atol > 0.0 || st.rtol > 0.0), GNPDE_EINVAL,
                   "stage: tolerances must be >= 0 and not both 0");
   }
-  // the folded dense output (ABI 8): its device slot, times and step size
-  if (st.dense_out)
-    GNPDE_REQUIRE(st.dense_t && st.dense_dt && st.dense_tab, GNPDE_EINVAL,
-                  "stage: dense_out without dense_t / dense_dt / dense_tab");
+  // the folded dense output (ABI 8): its device slot and coefficient table; the launch
+  // that forms the table: its times and step size
+  if (st.dense_out) GNPDE_REQUIRE(st.dense_tab, GNPDE_EINVAL, "stage: dense_out without dense_tab");
+  if (st.dense_tab && !st.dense_out)
+    GNPDE_REQUIRE(st.dense_t && st.dense_dt, GNPDE_EINVAL, "stage: dense_tab without dense_t / dense_dt");
+  GNPDE_REQUIRE(!st.scale_rows || (st.err_rows && !st.dot_rows), GNPDE_EINVAL,
+                "stage: scale_rows needs err_rows and no dot_rows");
   return GNPDE_OK;
 }
 

@@ -146,7 +146,7 @@ __global__ __launch_bounds__(256) void stage_apply_kernel(int64_t R, int C, int6
   const int rs = lane / GL, gl = lane % GL;
   const int64_t row = ((int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * RPW + rs;
   const bool live = row < R;
-  double dpart = 0.0;
+  float dpart = 0.f;  // the error row's slice sums: fp32, as the fused epilogue (err_terms, epi_rowsums)
   for (int c0 = 0; c0 < C; c0 += GL * VEC) {
     const int cc = c0 + gl * VEC;
     if (!live || cc >= C) continue;
@@ -182,13 +182,13 @@ __global__ __launch_bounds__(256) void stage_apply_kernel(int64_t R, int C, int6
       float y1[VEC];
 #pragma unroll
       for (int t = 0; t < VEC; ++t) y1[t] = st.err_y1 == 1 ? r[1][t] : (st.err_y1 == 0 ? r[0][t] : xv[t]);
-      dpart += err_terms<VEC, T>(st, off, ev, y1, &y0v);
+      dpart += (float)err_terms<VEC, T>(st, off, ev, y1, &y0v);
     }
   }
   if (ERR && st.err_rows) {  // kernel-uniform
 #pragma unroll
     for (int o = 1; o < GL; o <<= 1) dpart += __shfl_xor(dpart, o);
-    if (live && gl == 0) st.err_rows[row] = dpart;
+    if (live && gl == 0) st.err_rows[row] = (double)dpart;
   }
 }
 
@@ -239,8 +239,9 @@ __global__ __launch_bounds__(256) void init_step_partial_kernel(int64_t n, const
 }
 
 // h[0] = h0, h[1] = d1 (phase 0; hf = (float)h0, the probe's coefficient scale);
-// h[2] = the first step (phase 1)
-template <int PHASE>
+// h[2] = the first step (phase 1; DIVH: the sums are of (f1 - f0)/scale, divided by h0 —
+// else of L f0 / scale, gnpde_initial_step_rows)
+template <int PHASE, bool DIVH = true>
 __global__ __launch_bounds__(256) void init_step_final_kernel(const double* __restrict__ part, int nb, double n,
                                                                double order, double* h, float* hf) {
   __shared__ double red[kBlock / kWave];
@@ -261,7 +262,7 @@ __global__ __launch_bounds__(256) void init_step_final_kernel(const double* __re
     *hf = (float)h0;
   } else {
     const double h0 = h[0], d1 = h[1];
-    const double d2 = sqrt(s0 / n) / h0;
+    const double d2 = DIVH ? sqrt(s0 / n) / h0 : sqrt(s0 / n);
     const double h1 = (d1 <= 1e-15 && d2 <= 1e-15) ? fmax(1e-6, h0 * 1e-3) : pow(0.01 / fmax(d1, d2), 1.0 / order);
     h[2] = fmin(100.0 * h0, h1);
     if (hf) *hf = (float)h[2];  // the first step's coefficient scale, in place for its launches
@@ -297,6 +298,28 @@ static int initial_step(int64_t n, const T* y0, const T* f0, const T* f1, double
   }
   GNPDE_LAUNCH_CHECK();
   return GNPDE_OK;
+}
+
+// Block partials of the row sums of gnpde_initial_step_rows: part[2b] = sum y (rows_b,
+// the y0 channel; rows_a in phase 1), part[2b + 1] = sum rows_a (the f0 channel; 0 in
+// phase 1) — the layout init_step_final_kernel reads.
+__global__ __launch_bounds__(256) void init_rows_partial_kernel(int64_t n, const double* __restrict__ a,
+                                                                 const double* __restrict__ b,
+                                                                 double* __restrict__ part) {
+  __shared__ double red[kBlock / kWave];
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  double sa = 0.0, sb = 0.0;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride) {
+    sa += a[i];
+    if (b) sb += b[i];
+  }
+  const double ta = block_sum_f64(sa, red);
+  __syncthreads();
+  const double tb = b ? block_sum_f64(sb, red) : 0.0;
+  if (threadIdx.x == 0) {
+    part[2 * blockIdx.x] = b ? tb : ta;
+    part[2 * blockIdx.x + 1] = b ? ta : 0.0;
+  }
 }
 
 template <int VEC, class T>
@@ -335,7 +358,8 @@ static int stage_apply(int64_t R, int64_t C, int64_t ld, const T* f, const T* x,
   if (rc) return rc;
   const gnpde_stage_epilogue_t& st = *stage;
   GNPDE_REQUIRE(!st.dot_rows, GNPDE_EUNSUPPORTED, "stage_apply: dot_rows are fused into the RHS kernels only");
-  GNPDE_REQUIRE(!st.dense_out, GNPDE_EUNSUPPORTED, "stage_apply: dense_out is fused into the RHS kernel only");
+  GNPDE_REQUIRE(!st.dense_out && !st.dense_tab && !st.scale_rows, GNPDE_EUNSUPPORTED,
+                "stage_apply: dense_out / dense_tab / scale_rows are fused into the RHS kernel only");
   bool needs_x = st.err_rows && st.err_y1 < 0;
   for (int i = 0; i < st.n_out; ++i)
     GNPDE_REQUIRE(st.o[i].out != reinterpret_cast<const float*>(x), GNPDE_EINVAL, "stage_apply: output %d aliases x",
@@ -476,6 +500,26 @@ extern "C" int gnpde_initial_step_f32(int64_t n, const float* y0, const float* f
                                       double rtol, double order, double* h, float* hf, void* workspace,
                                       size_t workspace_bytes, void* stream) {
   return initial_step<float>(n, y0, f0, f1, atol, rtol, order, h, hf, workspace, workspace_bytes, stream);
+}
+
+extern "C" int gnpde_initial_step_rows(int64_t nrows, const double* rows_a, const double* rows_b, double n,
+                                       double order, double* h, float* hf, void* workspace, size_t workspace_bytes,
+                                       void* stream) {
+  GNPDE_REQUIRE(nrows >= 1 && rows_a && h && n > 0.0 && order > 0.0 && workspace,
+                GNPDE_EINVAL, "initial_step_rows: bad arguments");
+  GNPDE_REQUIRE(rows_b == nullptr || hf != nullptr, GNPDE_EINVAL, "initial_step_rows: phase 0 needs hf");
+  GNPDE_REQUIRE(workspace_bytes >= 2 * sizeof(double) * kDotBlocks, GNPDE_EINVAL,
+                "initial_step_rows: workspace too small");
+  hipStream_t s = as_stream(stream);
+  double* part = static_cast<double*>(workspace);
+  init_rows_partial_kernel<<<kDotBlocks, kBlock, 0, s>>>(nrows, rows_a, rows_b, part);
+  GNPDE_LAUNCH_CHECK();
+  if (rows_b)
+    init_step_final_kernel<0><<<1, kBlock, 0, s>>>(part, kDotBlocks, n, order, h, hf);
+  else
+    init_step_final_kernel<1, false><<<1, kBlock, 0, s>>>(part, kDotBlocks, n, order, h, hf);
+  GNPDE_LAUNCH_CHECK();
+  return GNPDE_OK;
 }
 
 extern "C" int gnpde_initial_step_bf16(int64_t n, const uint16_t* y0, const uint16_t* f0, const uint16_t* f1,

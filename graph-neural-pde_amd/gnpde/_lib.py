@@ -36,7 +36,8 @@ class StageEpilogue(ctypes.Structure):
                 ("atol", ctypes.c_double), ("rtol", ctypes.c_double), ("coef_scale", ctypes.c_void_p),
                 ("f_lin", ctypes.c_float), ("unscaled_outs", ctypes.c_int),
                 ("dense_out", ctypes.c_void_p), ("dense_rows", ctypes.c_void_p), ("dense_t", ctypes.c_void_p),
-                ("dense_dt", ctypes.c_void_p), ("dense_tab", ctypes.c_void_p), ("dense_m", (ctypes.c_float * DENSE_SLOTS) * DENSE_BASIS)]
+                ("dense_dt", ctypes.c_void_p), ("dense_tab", ctypes.c_void_p),
+                ("dense_m", (ctypes.c_float * DENSE_SLOTS) * DENSE_BASIS), ("scale_rows", ctypes.c_void_p)]
 
 
 c_i32p = ctypes.POINTER(ctypes.c_int32)
@@ -82,6 +83,7 @@ SIGNATURES = {
     "gnpde_initial_step_workspace_bytes": (_size, []),
     "gnpde_adaptive_control": (_int, [_i64, _vp, _f64, _f64, _f64, _f64, _f64, _vp, _vp, _vp, _vp, _vp, _size, _vp]),
     "gnpde_initial_step_f32": (_int, [_i64, _vp, _vp, _vp, _f64, _f64, _f64, _vp, _vp, _vp, _size, _vp]),
+    "gnpde_initial_step_rows": (_int, [_i64, _vp, _vp, _f64, _f64, _vp, _vp, _vp, _size, _vp]),
     "gnpde_scaled_sq_sums_f32": (_int, [_i64, _vp, _vp, _vp, _f64, _f64, _vp, _vp, _size, _vp]),
     "gnpde_segment_sums_workspace_bytes": (_size, [_i64]),
     "gnpde_segment_sums_f64": (_int, [_i64, _i64, _vp, _vp, _vp, _size, _vp]),

@@ -1251,6 +1251,12 @@ def _krylov_plan(plan):
 # The dense output of a one-output-time Krylov solve folded into its steps' last launch
 # (ABI 8 Stage.dense; GNPDE_DENSE_FOLD=0: the separate pass of _interp_into)
 DENSE_FOLD = os.environ.get('GNPDE_DENSE_FOLD', '1') != '0'
+# The initial-step selection of an affine RHS from row sums the f0 and probe launches form
+# (ABI 8 scale_rows, err_y1 = -2, gnpde_initial_step_rows; GNPDE_INIT_ROWS=0: the passes of
+# gnpde_initial_step_f32 over y0, f0 and f1 = f(y0 + h0 f0), in torch's fp32 arithmetic).
+# Off by default: the wide epilogue the two launches then take costs more than the passes
+# it saves (G-arxiv: f0 launch 80 -> 124 us, probe 76 -> 109 us)
+INIT_ROWS = os.environ.get('GNPDE_INIT_ROWS', '0') == '1'
 
 
 def _fused_adaptive_ok(func, y0, combine, options):
@@ -1371,6 +1377,9 @@ class _AdaptiveState(object):
         self.dslot = None if host else self.dsc[2:].view(torch.int64)
         self.dtab = None if host else torch.zeros(_lib.DENSE_SLOTS + 1, dtype=torch.float32, device=y0.device)
         self.drows, self.drows_src = None, None
+        # the initial-step selection from the f0 / probe launches' row sums (INIT_ROWS): a second
+        # row array (the f0 launch's scale_rows) and the reduction's workspace
+        self.rows2, self.iws = None, None
         self.graphs = {}   # (id Y, id K0, mid, fold, renumbered) -> (graph, error-sum tensor)
         self.mempool = None
         self.warm = False
@@ -1405,6 +1414,7 @@ class _RKAdaptiveFused(_RKAdaptive):
         sc = self._scalars
         self.safety_f, self.ifactor_f, self.dfactor_f = float(sc['safety']), float(sc['ifactor']), float(sc['dfactor'])
         self.fold = False  # this solve's dense output folded into the Krylov steps (_integrate)
+        self.init_rows = False  # its initial step from the f0 / probe launches' row sums (_integrate)
         self.lay = None
 
     # ---- device primitives (host-stage RHS objects supply CPU versions: tests only)
@@ -1501,19 +1511,20 @@ class _RKAdaptiveFused(_RKAdaptive):
         ns = K.ns
         bufs = st.bufs
         u = [bufs['K0']] + [bufs['K%d' % p] for p in range(1, ns)]
-        for p in range(ns - 1):
-            self.func.rhs_stage(t, u[p], ops.Stage(outs=[(u[p + 1], None, 0.0, 1.0, [])], scale=st.scale),
-                                linear=True)
         y1t, (ft, fcf), (et, ecf) = K.last_launch_terms()
         outs = [(bufs['Y1'], bufs['Y'], 1.0, 0.0, [(u[p], c) for p, c in y1t]),
                 (bufs['K%d' % ns], None, 0.0, fcf, [(u[p], c) for p, c in ft])]
         err = (st.rows, (None, 0.0, ecf, [(u[p], c) for p, c in et]), bufs['Y'], 0, self.atol_f, self.rtol_f)
-        dense = None
-        if self.fold:
-            dense = (st.dslot, st.drows if self.lay is not None else None, st.tdev, st.dt, st.dtab,
-                     self._dense_table(u, ft, fcf))
-        self.func.rhs_stage(t, u[ns - 1], ops.Stage(outs=outs, err=err, scale=st.scale, f_lin=1.0, unscaled=(1,),
-                                                    dense=dense), linear=True)
+        last = ops.Stage(outs=outs, err=err, scale=st.scale, f_lin=1.0, unscaled=(1,))
+        form = None  # the folded dense output: launch 0 forms its coefficients, the last applies them
+        if self.fold and ns >= 2:
+            last.dense = (st.dslot, st.drows if self.lay is not None else None, None, None, st.dtab,
+                          self._dense_table(u, ft, fcf))
+            form = (None, None, st.tdev, st.dt, st.dtab, last.dense_matrix())
+        for p in range(ns - 1):
+            self.func.rhs_stage(t, u[p], ops.Stage(outs=[(u[p + 1], None, 0.0, 1.0, [])], scale=st.scale,
+                                                   dense=form if p == 0 else None), linear=True)
+        self.func.rhs_stage(t, u[ns - 1], last, linear=True)
 
     def _dense_table(self, u, ft, fcf):
         """The basis coefficients of the step's dense output over the last Krylov launch's
@@ -1582,6 +1593,15 @@ class _RKAdaptiveFused(_RKAdaptive):
         bufs = st.bufs
         Y, K0 = bufs['Y'], bufs['K0']
         h, hf = st.h, st.scale  # h[2] is st.dt: the device controller starts from it
+        if self.init_rows:
+            # from the f0 launch's rows; then the rows of L f0 (the probe's linear part on f0, no
+            # output): d2 = rms(L f0 / scale) = rms((f1 - f0) / scale) / h0 for f1 = f(y0 + h0 f0)
+            n = float(st.rows.numel() * self.C)
+            ops.initial_step_rows(st.rows, st.rows2, n, self.order, h, hf, ws=st.iws)
+            self.func.rhs_stage(t0, K0, ops.Stage(err=(st.rows, (None, 0.0, 1.0, []), Y, -2, self.atol_f,
+                                                       self.rtol_f)), linear=True)
+            ops.initial_step_rows(st.rows, None, n, self.order, h, hf, ws=st.iws)
+            return self._rec_reader(st, h, slot=2)
         ops.initial_step(Y, K0, None, self.atol_f, self.rtol_f, self.order, h, hf)
         probe, f1 = bufs['X0'], bufs['Y1']  # free until the first step
         if self.affine:  # f1 = f0 + h0 L f0 from a launch over f0 (no probe pass)
@@ -1673,7 +1693,8 @@ class _RKAdaptiveFused(_RKAdaptive):
         # numbering) when the step crosses it, by the device time the controller advances;
         # the accepted crossing step writes last (a rejected or discarded step either does
         # not cross or is followed by one that does), so no dense-output pass follows.
-        self.fold = (DENSE_FOLD and not self.host and self.krylov is not None and self._dev_control() and
+        self.fold = (DENSE_FOLD and not self.host and self.krylov is not None and self.krylov.ns >= 2 and
+                     self._dev_control() and
                      len(th) == 2 and th[1] > th[0] and getattr(self.func, 'fold_dense', False))
         if not self.host:
             hv = st.dsc_host
@@ -1693,7 +1714,20 @@ class _RKAdaptiveFused(_RKAdaptive):
             _entry_copy(y0, bufs['Y'], sol[0], lay.order if lay is not None else None)
         t0 = torch.tensor(th[0], dtype=torch.float64)
         dev_init = not self.host and getattr(self.func, 'autonomous', False) and 'norm' not in self.options
-        if dev_init:  # f0 straight into K0 (the RHS epilogue's f_out)
+        # the initial-step selection's squared sums formed by the f0 and probe launches themselves
+        # (an affine RHS: the probe is the linear part on f0), no passes over y0, f0, f1
+        self.init_rows = (INIT_ROWS and dev_init and self.affine and self._scalars['first_step'] is None)
+        if self.init_rows:
+            if st.rows2 is None:
+                st.rows2 = torch.empty_like(st.rows)
+                st.iws = torch.empty(_lib.fn("gnpde_initial_step_workspace_bytes")(), dtype=torch.uint8,
+                                     device=dev)
+            # f0 into K0 with the rows sum (f0 / scale)^2 (err) and sum (y0 / scale)^2 (scale_rows),
+            # scale = atol + rtol |y0| (err_y1 = -2)
+            self.func.rhs_stage(t0, bufs['Y'], ops.Stage(
+                f_out=bufs['K0'], err=(st.rows, (None, 0.0, 1.0, []), bufs['Y'], -2, self.atol_f, self.rtol_f),
+                scale_rows=st.rows2))
+        elif dev_init:  # f0 straight into K0 (the RHS epilogue's f_out)
             self.func.rhs_stage(t0, bufs['Y'], ops.Stage(f_out=bufs['K0']))
         else:
             f0 = self.func(t0, bufs['Y'])

@@ -590,10 +590,13 @@ class Stage(object):
     {step start, output time}, ``dt`` the device fp64 step size, ``tab`` device fp32
     scratch of STAGE_MAX_K + 3 (the launch's coefficients), ``table`` the
     basis coefficients: {'base': [5], 'f': [5], k tensor: [5]} over w = (cy0 + cy1 +
-    cym, h cy1, h cym, cf0, cf1) of torchdiffeq's interpolant (include/gnpde.h)."""
+    cym, h cy1, h cym, cf0, cf1) of torchdiffeq's interpolant (include/gnpde.h).
+    The launch that applies them has a ``slot``; an earlier launch of the step forms
+    ``tab``: slot None and ``table`` the applying stage's ``dense_matrix()``.
+    ``scale_rows`` (ABI 8, with ``err``): fp64 [R], rows[r] = sum_c (y0 / tol)^2."""
 
     def __init__(self, f_out=None, outs=(), out_rows=None, dot=None, err=None, scale=None, f_lin=0.0,
-                 unscaled=(), dense=None):
+                 unscaled=(), dense=None, scale_rows=None):
         self.f_out = f_out
         # indices of the outputs whose cf / c_j do NOT take ``scale`` (ABI 6 unscaled_outs)
         self.unscaled = tuple(unscaled)
@@ -607,13 +610,15 @@ class Stage(object):
         self.dot = dot
         self.err = err
         self.dense = dense
+        self.scale_rows = scale_rows
 
     def _operands(self):
         """The distinct k tensors of every combination, in first-use order."""
         ks, seen = [], set()
         combos = [o[4] for o in self.outs] + ([self.err[1][3]] if self.err is not None else [])
         if self.dense is not None:
-            combos.append([(k, 0.0) for k in self.dense[5] if isinstance(k, torch.Tensor)])
+            if isinstance(self.dense[5], dict):
+                combos.append([(k, 0.0) for k in self.dense[5] if isinstance(k, torch.Tensor)])
         for terms in combos:
             for k, _ in terms:
                 if k.data_ptr() not in seen:
@@ -702,33 +707,60 @@ class Stage(object):
             st.coef_scale = self.scale.data_ptr()
         st.f_lin = self.f_lin
         st.unscaled_outs = sum(1 << i for i in self.unscaled)
+        if self.scale_rows is not None:
+            _require_gpu(self.scale_rows, "scale rows", torch.float64)
+            if self.err is None or self.dot is not None or self.scale_rows.numel() * ref.shape[-1] != ref.numel():
+                raise ValueError("scale rows: one fp64 per RHS row, with err and without dot")
+            st.scale_rows = self.scale_rows.data_ptr()
         if self.dense is not None:
             dslot, drows, dtt, ddt, dtab, table = self.dense
-            _require_gpu(dslot, "dense slot", torch.int64)
             _require_gpu(dtab, "dense coefficient scratch", torch.float32)
             if dtab.numel() < _lib.DENSE_SLOTS + 1:
                 raise ValueError("dense: coefficient scratch of %d floats" % (_lib.DENSE_SLOTS + 1))
             st.dense_tab = dtab.data_ptr()
-            _require_gpu(dtt, "dense times", torch.float64)
-            _require_gpu(ddt, "dense step", torch.float64)
-            if shift or not self.outs or dtt.numel() < 2:
-                raise ValueError("dense: needs output 0 (its base is y0), two times and unshifted buffers")
-            st.dense_out, st.dense_t, st.dense_dt = dslot.data_ptr(), dtt.data_ptr(), ddt.data_ptr()
-            if drows is not None:
-                _require_gpu(drows, "dense rows", torch.int32)
-                if drows.numel() * ref.shape[-1] != ref.numel():
-                    raise ValueError("dense rows must hold one row index per RHS row")
-                st.dense_rows = drows.data_ptr()
-            for key, w in table.items():
-                if isinstance(key, str):
-                    q = {'base': 0, 'f': _lib.DENSE_SLOTS - 1}[key]
-                else:
-                    q = 1 + slot[key.data_ptr()]
-                if len(w) != _lib.DENSE_BASIS:
-                    raise ValueError("dense: %d basis coefficients per operand" % _lib.DENSE_BASIS)
-                for m, v in enumerate(w):
-                    st.dense_m[m][q] += float(v)
+            if shift:
+                raise ValueError("dense: unshifted buffers only")
+            if dslot is not None:  # the launch that applies the coefficients
+                _require_gpu(dslot, "dense slot", torch.int64)
+                if not self.outs:
+                    raise ValueError("dense: needs output 0 (its base is y0)")
+                st.dense_out = dslot.data_ptr()
+                if drows is not None:
+                    _require_gpu(drows, "dense rows", torch.int32)
+                    if drows.numel() * ref.shape[-1] != ref.numel():
+                        raise ValueError("dense rows must hold one row index per RHS row")
+                    st.dense_rows = drows.data_ptr()
+            if dtt is not None:  # the times: the launch that forms the coefficients
+                _require_gpu(dtt, "dense times", torch.float64)
+                _require_gpu(ddt, "dense step", torch.float64)
+                if dtt.numel() < 2:
+                    raise ValueError("dense: two times")
+                st.dense_t, st.dense_dt = dtt.data_ptr(), ddt.data_ptr()
+            mat = table if not isinstance(table, dict) else self._dense_matrix(table, slot)
+            for m in range(_lib.DENSE_BASIS):
+                for q in range(_lib.DENSE_SLOTS):
+                    st.dense_m[m][q] = float(mat[m][q])
         return st
+
+    @staticmethod
+    def _dense_matrix(table, slot):
+        mat = [[0.0] * _lib.DENSE_SLOTS for _ in range(_lib.DENSE_BASIS)]
+        for key, w in table.items():
+            if isinstance(key, str):
+                q = {'base': 0, 'f': _lib.DENSE_SLOTS - 1}[key]
+            else:
+                q = 1 + slot[key.data_ptr()]
+            if len(w) != _lib.DENSE_BASIS:
+                raise ValueError("dense: %d basis coefficients per operand" % _lib.DENSE_BASIS)
+            for m, v in enumerate(w):
+                mat[m][q] += float(v)
+        return mat
+
+    def dense_matrix(self):
+        """The basis-coefficient matrix [DENSE_BASIS][DENSE_SLOTS] of this stage's dense
+        table over its own operand slots (what the launch forming the coefficients carries)."""
+        ks = self._operands()
+        return self._dense_matrix(self.dense[5], {k.data_ptr(): j for j, k in enumerate(ks)})
 
 
 def stage_apply(stage, f, x, like):
@@ -1454,6 +1486,23 @@ def initial_step(y0, f0, f1, atol, rtol, order, h, hf=None):
     name = "gnpde_initial_step_bf16" if dt == torch.bfloat16 else "gnpde_initial_step_f32"
     _lib.call(name, y0.numel(), _ptr(y0), _ptr(f0), _ptr(f1), float(atol), float(rtol), float(order), _ptr(h),
               _ptr(hf), _ptr(ws), nbytes, _stream(y0.device))
+
+
+def initial_step_rows(rows_a, rows_b, n, order, h, hf, ws=None):
+    """gnpde_initial_step_rows: the initial-step rules from the squared-sum rows of the f0
+    launch (phase 0: rows_a its err_rows, rows_b its scale_rows) or of the launch over L f0
+    (phase 1: rows_b None).  h: fp64 [3], hf: fp32 0-d (device)."""
+    _require_gpu(rows_a, "rows", torch.float64)
+    if rows_b is not None:
+        _require_gpu(rows_b, "rows", torch.float64)
+    _require_gpu(h, "h", torch.float64)
+    if hf is not None:
+        _require_gpu(hf, "hf", torch.float32)
+    nbytes = _lib.fn("gnpde_initial_step_workspace_bytes")()
+    if ws is None or ws.numel() < nbytes:
+        ws = torch.empty(nbytes, dtype=torch.uint8, device=rows_a.device)
+    _lib.call("gnpde_initial_step_rows", rows_a.numel(), _ptr(rows_a), _ptr(rows_b), float(n), float(order), _ptr(h),
+              _ptr(hf), _ptr(ws), ws.numel(), _stream(rows_a.device))
 
 
 def adaptive_control(err_rows, n, order, safety, ifactor, dfactor, dt, scale, rec, ws=None, t=None):

@@ -212,10 +212,16 @@ size_t gnpde_plan_workspace_bytes(int64_t R);
  * err_rows (NULL = none): the error estimate of an embedded Runge-Kutta pair
  * (torchdiffeq's RKAdaptiveStepsizeODESolver: error_ratio = RMS(e / tol)):
  *   e      = err.cb*err.base + err.cf*f + sum_{j<nk} err.c[j]*k[j]   (err.out unused)
- *   y1     = the RHS input x (err_y1 = -1) or the value of output err_y1
+ *   y1     = the RHS input x (err_y1 = -1), err_y0 itself (err_y1 = -2, ABI 8: tol =
+ *            atol + rtol |y0|, the scale of torchdiffeq's initial-step selection) or
+ *            the value of output err_y1
  *   tol    = atol + rtol * max(|err_y0|, |y1|)
  *   err_rows[r] = sum_c (e / tol)^2     (fp64, the row's lanes in a fixed order)
  * which the caller sums (gnpde_sum_f64) into the squared norm of one step.
+ * scale_rows (NULL = none; ABI 8; with err_rows, the plain-weight K1 only, not beside
+ * dot_rows): scale_rows[r] = sum_c (err_y0 / tol)^2 — with e = f and err_y1 = -2 the
+ * f0 launch of an adaptive solve yields both squared sums of the initial-step
+ * selection (gnpde_initial_step_rows).
  * coef_scale (NULL = 1): a device fp32 scalar multiplying every cf and c[j] of the
  * outputs and of err (not cb): the step size of an adaptive solve, so the
  * launches of a step do not change with it (hipGraph-replayable, one graph per
@@ -251,8 +257,11 @@ size_t gnpde_plan_workspace_bytes(int64_t R);
  * (coefficients formed in fp64, applied in fp32; f after f_lin), out = *dense_out
  * (a device slot holding the output array: the launch can be captured once and
  * its output redirected per solve).  dense_tab: device scratch of
- * GNPDE_STAGE_MAX_K + 3 floats (the crossing flag and the coefficients, formed by
- * a one-wavefront launch ahead of the aggregation).                          */
+ * GNPDE_STAGE_MAX_K + 3 floats holding the crossing flag and the coefficients of
+ * the launch's step, which an EARLIER launch of the same step forms: a K1 launch
+ * whose stage sets dense_tab, dense_t, dense_dt and dense_m but not dense_out writes
+ * them (one thread, before its aggregation) — the first launch of the step, so
+ * the one that applies them reads them from memory into scalar registers.     */
 #define GNPDE_STAGE_MAX_OUT 2
 #define GNPDE_STAGE_MAX_K 6
 #define GNPDE_DENSE_BASIS 5
@@ -290,6 +299,7 @@ typedef struct {
   const double* dense_dt;
   float* dense_tab;
   float dense_m[GNPDE_DENSE_BASIS][GNPDE_STAGE_MAX_K + 2];
+  double* scale_rows;
 } gnpde_stage_epilogue_t;
 
 /* The stage epilogue as a pass of its own, over rows [0, R) of C columns
@@ -612,6 +622,17 @@ int gnpde_adaptive_control(int64_t nrows, const double* err_rows, double n, doub
                            double ifactor, double dfactor, double* dt, float* scale, double* rec, double* t,
                            void* workspace, size_t workspace_bytes, void* stream);
 size_t gnpde_initial_step_workspace_bytes(void);
+/* gnpde_initial_step_f32's scalar rules from per-row squared sums formed by the RHS
+ * launches themselves (ABI 8; an affine RHS f(y) = L y + s): phase 0 (rows_b given)
+ * with rows_a = the f0 launch's err_rows (e = f0, err_y1 = -2: sum (f0/scale)^2) and
+ * rows_b = its scale_rows (sum (y0/scale)^2); phase 1 (rows_b NULL) with rows_a =
+ * the err_rows of a launch evaluating L f0 (the linear part on f0, e = f): then
+ *   d2 = rms(L f0 / scale)   (= rms((f1 - f0)/scale)/h0 for f1 = f(y0 + h0 f0))
+ * and h[2], *hf as gnpde_initial_step_f32's phase 1.  scale = atol + rtol |y0| in
+ * fp64 (the epilogue's tolerance), n the state's element count.  Two launches;
+ * workspace gnpde_initial_step_workspace_bytes().                             */
+int gnpde_initial_step_rows(int64_t nrows, const double* rows_a, const double* rows_b, double n, double order,
+                            double* h, float* hf, void* workspace, size_t workspace_bytes, void* stream);
 /* The squared sums of gnpde_initial_step_f32 without its scalar rules (ABI 7): the
  * per-component pieces of a mixed norm (torchdiffeq's adjoint norm: the max over the
  * components [y | adj_y | adj_params] of their RMS norms), the caller combining them:

@@ -143,7 +143,8 @@ def test_stage_struct_layout_matches_header():
     assert _lib.StageEpilogue.unscaled_outs.offset == _lib.StageEpilogue.f_lin.offset + 4
     # ABI 8: dense_out, dense_rows, dense_t, dense_dt, dense_tab, dense_m[5][8] floats
     assert _lib.StageEpilogue.dense_m.offset == _lib.StageEpilogue.dense_out.offset + 5 * 8
-    assert ctypes.sizeof(_lib.StageEpilogue) == _lib.StageEpilogue.dense_m.offset + 5 * 8 * 4
+    assert _lib.StageEpilogue.scale_rows.offset == _lib.StageEpilogue.dense_m.offset + 5 * 8 * 4
+    assert ctypes.sizeof(_lib.StageEpilogue) == _lib.StageEpilogue.scale_rows.offset + 8
 
 
 def test_workspace_size_queries():
@@ -172,8 +173,9 @@ def test_c_header_struct_layout_with_gcc(tmp_path):
                    'offsetof(gnpde_stage_epilogue_t, err), offsetof(gnpde_stage_epilogue_t, err_y1),'
                    'offsetof(gnpde_stage_epilogue_t, rtol), offsetof(gnpde_stage_epilogue_t, coef_scale),'
                    'offsetof(gnpde_stage_epilogue_t, unscaled_outs));'
-                   'printf("%zu %zu %zu\\n", offsetof(gnpde_stage_epilogue_t, dense_out),'
-                   'offsetof(gnpde_stage_epilogue_t, dense_tab), offsetof(gnpde_stage_epilogue_t, dense_m));return 0;}\n')
+                   'printf("%zu %zu %zu %zu\\n", offsetof(gnpde_stage_epilogue_t, dense_out),'
+                   'offsetof(gnpde_stage_epilogue_t, dense_tab), offsetof(gnpde_stage_epilogue_t, dense_m),'
+                   'offsetof(gnpde_stage_epilogue_t, scale_rows));return 0;}\n')
     exe = tmp_path / "layout"
     subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
     got = [int(v) for v in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()]
@@ -181,7 +183,7 @@ def test_c_header_struct_layout_with_gcc(tmp_path):
     assert got == [ctypes.sizeof(_lib.StageOut), _lib.StageOut.c.offset, ctypes.sizeof(E), E.nk.offset, E.k.offset,
                    E.out_rows.offset, E.dot_coef.offset, E.dot_accumulate.offset, E.err.offset, E.err_y1.offset,
                    E.rtol.offset, E.coef_scale.offset, E.unscaled_outs.offset, E.dense_out.offset, E.dense_tab.offset,
-                   E.dense_m.offset]
+                   E.dense_m.offset, E.scale_rows.offset]
 
 
 def test_stale_library_is_refused(monkeypatch):

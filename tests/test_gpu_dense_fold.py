@@ -96,3 +96,45 @@ def test_dense_fold_only_for_one_output_time(monkeypatch):
     _, _, f2, _ = _solve(func, x, [0.0, 0.4, 1.0], 1e-4, 1e-5)
     _, _, f1, _ = _solve(func, x, [0.0, 1.0], 1e-4, 1e-5)
     assert not f2 and f1
+
+
+@pytest.mark.parametrize("add_source", [False, True])
+@pytest.mark.parametrize("rtol", [1e-3, 1e-6])
+def test_initial_step_from_launch_rows(monkeypatch, add_source, rtol):
+    """The first step of an affine solve from the row sums of the f0 launch (err rows of f0
+    and scale_rows of y0, tol = atol + rtol |y0|) and of the probe launch over L f0
+    (integrator.INIT_ROWS, gnpde_initial_step_rows) against torchdiffeq's
+    _select_initial_step restated in fp64 on the oracle's RHS (src/block_constant.py:46-51
+    solves with the solver's default first step): within 1e-6 relative — the fp32 path
+    (GNPDE_INIT_ROWS=0) forms (f1 - f0) / h0 in fp32, the rows path L f0 itself."""
+    N, E, C = 3000, 30000, 48
+    eo, wo, rng = _graph(N, E, 53)
+    x = rng.standard_normal((1, N, C)).astype(np.float32)
+    x0 = rng.standard_normal((1, N, C)).astype(np.float32)
+    func = _laplacian(C, eo, wo, alpha=0.7, add_source=add_source, x0=T(x0) if add_source else None)
+    atol = rtol * 0.1
+    monkeypatch.setattr(gi, "INIT_ROWS", True)
+    seen = {}
+    orig = gi._RKAdaptiveFused._initial_step_device
+
+    def spy(self, st, t0):
+        read = orig(self, st, t0)
+        seen['h'] = st.h.clone()
+        seen['rows'] = self.init_rows
+        return read
+    monkeypatch.setattr(gi._RKAdaptiveFused, "_initial_step_device", spy)
+    _solve(func, x, [0.0, 0.5], rtol, atol)
+    assert seen['rows']
+    h = seen['h'].cpu().numpy()
+    f = lambda y: O.laplacian_rhs(eo, y, x0, 0.7, 0.4, edge_weight=wo, add_source=add_source)  # noqa: E731
+    y = x.astype(np.float64)
+    f0 = f(y)
+    sc = atol + np.abs(y) * rtol
+    rms = lambda v: np.sqrt(np.mean(np.square(v)))  # noqa: E731
+    d0, d1 = rms(y / sc), rms(f0 / sc)
+    h0 = 1e-6 if (d0 < 1e-5 or d1 < 1e-5) else 0.01 * d0 / d1
+    d2 = rms((f(y + h0 * f0) - f0) / sc) / h0
+    h1 = max(1e-6, h0 * 1e-3) if (d1 <= 1e-15 and d2 <= 1e-15) else (0.01 / max(d1, d2)) ** (1.0 / 5)
+    want = min(100 * h0, h1)
+    assert abs(h[0] - h0) <= 1e-6 * h0 and abs(h[1] - d1) <= 1e-6 * d1
+    assert abs(h[2] - want) <= 1e-6 * want
