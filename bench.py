@@ -703,6 +703,15 @@ def bench_attention(g, x, dev, ops, reps=50):
                                  "replayed RHS time" % (TRAFFIC_FILE, mode, norm_idx)})
         else:
             ent.update({"traffic": None, "frac": None, "basis": "no PMC traffic in %s" % TRAFFIC_FILE})
+        # the RHS inside the adaptive solve the reference runs (dopri5 at ogbn-arxiv's best_params
+        # T / tol_scale): the fused step's stage pass and error reduction included
+        T, ts = ARXIV_DOPRI5
+        func.nfe = 0
+        el, steps, nfe = _timed_dopri5(func, x, T, ts, dev, 3)
+        ent["dopri5"] = {"ms_per_solve": round(el * 1e3, 4), "steps": steps, "rhs_evals": nfe,
+                         "dopri5_ms_per_step": round(el * 1e3 / max(steps, 1), 4),
+                         "ms_per_rhs_in_solve": round(el * 1e3 / max(nfe, 1), 4),
+                         "config": "dopri5 over [0, %.3f] at tol_scale %.1f (ogbn-arxiv best_params)" % (T, ts)}
         out["%s_norm%d" % (mode, norm_idx)] = ent
     return out
 

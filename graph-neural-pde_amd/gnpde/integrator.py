@@ -26,6 +26,7 @@ import math
 import os
 import weakref
 
+import numpy as np
 import torch
 
 from . import _lib, ops
@@ -1327,6 +1328,19 @@ class _LaplacianAdaptiveFn(torch.autograd.Function):
         return (gy, gal, gbe, gwo) + (None,) * 7
 
 
+class _HostRecord(object):
+    """A pinned host copy of a step's device record that its step graph writes."""
+    __slots__ = ('buf',)
+
+    def __init__(self, buf):
+        self.buf = buf
+
+
+# The replayed step graph copies the controller's record to pinned memory itself
+# (GNPDE_GRAPH_RECORD_COPY=0: a copy enqueued behind each replay)
+GRAPH_RECORD_COPY = os.environ.get('GNPDE_GRAPH_RECORD_COPY', '1') != '0'
+
+
 # Captured adaptive steps (hipGraph): one graph per (buffer binding, dense-output
 # variant) replays a whole step — the stage-input pass, the RHS launches and the
 # error reduction — whatever dt (the coefficients scale by a device scalar), so a
@@ -1373,6 +1387,7 @@ class _AdaptiveState(object):
         # copy from a pinned host twin
         self.dsc = None if host else torch.zeros(3, dtype=torch.float64, device=y0.device)
         self.dsc_host = None if host else torch.zeros(3, dtype=torch.float64, pin_memory=True)
+        self.dsc_np = None if host else self.dsc_host.numpy()  # (host writes through numpy: no torch ops)
         self.tdev = None if host else self.dsc[:2]
         self.dslot = None if host else self.dsc[2:].view(torch.int64)
         self.dtab = None if host else torch.zeros(_lib.DENSE_SLOTS + 1, dtype=torch.float32, device=y0.device)
@@ -1569,6 +1584,15 @@ class _RKAdaptiveFused(_RKAdaptive):
         step, slot 2) copied to pinned host memory behind an event (slots 0 / 1
         alternate: a step ahead may be in flight): a callable that waits for that copy
         only and returns the values."""
+        if isinstance(rec, _HostRecord):  # copied by the replayed step graph itself
+            ev = torch.cuda.Event()
+            ev.record()
+            hb = rec.buf
+
+            def read_graph():
+                ev.synchronize()
+                return hb.tolist()
+            return read_graph
         if st.rec_host is None:
             st.rec_host = torch.empty((3, 4), dtype=torch.float64, pin_memory=True)
         if slot is None:
@@ -1637,18 +1661,25 @@ class _RKAdaptiveFused(_RKAdaptive):
         on first use once the module is warm), eagerly otherwise."""
         P = self.plan
         if graphs_ok and st.warm and _nfe_headroom(self.func, P.ns):
-            gk = (id(st.bufs['Y']), id(st.bufs['K0']), bool(mid), self.fold, self.lay is not None)
+            gk = (id(st.bufs['Y']), id(st.bufs['K0']), bool(mid), self.fold, self.lay is not None, GRAPH_RECORD_COPY)
             ent = st.graphs.get(gk)
             if ent is None:
                 nfe = getattr(self.func, 'nfe', None)
                 g = torch.cuda.CUDAGraph()
+                # the device controller's record copied to a pinned buffer of this graph by the graph
+                # itself (GRAPH_RECORD_COPY): no separate copy behind the replay (the same graph is
+                # replayed again only after its record was read: the bindings rotate through three)
+                hb = torch.empty(4, dtype=torch.float64, pin_memory=True) \
+                    if (GRAPH_RECORD_COPY and self._dev_control()) else None
                 with torch.cuda.graph(g, pool=st.mempool):
                     err = self._step(st, t_cur, dt, mid)
+                    if hb is not None:
+                        hb.copy_(err, non_blocking=True)
                 if st.mempool is None:
                     st.mempool = g.pool()
                 if nfe is not None:
                     self.func.nfe = nfe  # capture records launches, it evaluates nothing
-                ent = (g, err)
+                ent = (g, err if hb is None else _HostRecord(hb))
                 st.graphs[gk] = ent
             ent[0].replay()
             if hasattr(self.func, 'nfe'):
@@ -1697,10 +1728,10 @@ class _RKAdaptiveFused(_RKAdaptive):
                      self._dev_control() and
                      len(th) == 2 and th[1] > th[0] and getattr(self.func, 'fold_dense', False))
         if not self.host:
-            hv = st.dsc_host
+            hv = st.dsc_np
             hv[0], hv[1] = th[0], th[-1]
-            hv[2:].view(torch.int64)[0] = sol[1].data_ptr() if self.fold else 0
-            st.dsc.copy_(hv, non_blocking=True)
+            hv[2:].view(np.int64)[0] = sol[1].data_ptr() if self.fold else 0
+            st.dsc.copy_(st.dsc_host, non_blocking=True)
         if self.fold:
             if lay is not None and st.drows_src is not lay.order32:
                 if st.drows is None:
