@@ -214,8 +214,8 @@ __global__ __launch_bounds__(256) void init_step_partial_kernel(int64_t n, const
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n / VEC; i += stride) {
     float y[VEC], f[VEC], g[VEC];
     load_vec<VEC>(y0 + i * VEC, y);
-    load_vec<VEC>(f0 + i * VEC, f);
-    if constexpr (PHASE == 1) load_vec<VEC>(f1 + i * VEC, g);
+    if constexpr (PHASE != 2) load_vec<VEC>(f0 + i * VEC, f);
+    if constexpr (PHASE >= 1) load_vec<VEC>(f1 + i * VEC, g);
 #pragma unroll
     for (int t = 0; t < VEC; ++t) {
       const float sc = __fadd_rn(atol, __fmul_rn(fabsf(y[t]), rtol));  // no fma: torch rounds twice
@@ -223,8 +223,11 @@ __global__ __launch_bounds__(256) void init_step_partial_kernel(int64_t n, const
         const double q0 = (double)(y[t] / sc), q1 = (double)(f[t] / sc);
         a0 = fma(q0, q0, a0);
         a1 = fma(q1, q1, a1);
-      } else {
+      } else if constexpr (PHASE == 1) {
         const double q = (double)((g[t] - f[t]) / sc);
+        a0 = fma(q, q, a0);
+      } else {  // PHASE 2: g = L f0 itself (gnpde_initial_step_lin_*)
+        const double q = (double)(g[t] / sc);
         a0 = fma(q, q, a0);
       }
     }
@@ -500,6 +503,41 @@ extern "C" int gnpde_initial_step_f32(int64_t n, const float* y0, const float* f
                                       double rtol, double order, double* h, float* hf, void* workspace,
                                       size_t workspace_bytes, void* stream) {
   return initial_step<float>(n, y0, f0, f1, atol, rtol, order, h, hf, workspace, workspace_bytes, stream);
+}
+
+// phase 1 of the initial step from v = L f0 (the linear part of an affine RHS on f0):
+// d2 = rms(v / scale), the quotient in fp32 as gnpde_initial_step_f32's
+template <class T>
+static int initial_step_lin(int64_t n, const T* y0, const T* v, double atol, double rtol, double order, double* h,
+                            float* hf, void* workspace, size_t ws_bytes, void* stream) {
+  GNPDE_REQUIRE(n >= 1 && y0 && v && h && workspace && order > 0.0, GNPDE_EINVAL, "initial_step_lin: bad arguments");
+  GNPDE_REQUIRE(ws_bytes >= 2 * sizeof(double) * kDotBlocks, GNPDE_EINVAL, "initial_step_lin: workspace too small");
+  hipStream_t s = as_stream(stream);
+  double* part = static_cast<double*>(workspace);
+  const float a = (float)atol, r = (float)rtol;
+  const size_t vb = 4 * sizeof(T);
+  const bool v4 = n % 4 == 0 && reinterpret_cast<uintptr_t>(y0) % vb == 0 && reinterpret_cast<uintptr_t>(v) % vb == 0;
+  if (v4)
+    init_step_partial_kernel<T, 4, 2><<<kDotBlocks, kBlock, 0, s>>>(n, y0, nullptr, v, a, r, part);
+  else
+    init_step_partial_kernel<T, 1, 2><<<kDotBlocks, kBlock, 0, s>>>(n, y0, nullptr, v, a, r, part);
+  GNPDE_LAUNCH_CHECK();
+  init_step_final_kernel<1, false><<<1, kBlock, 0, s>>>(part, kDotBlocks, (double)n, order, h, hf);
+  GNPDE_LAUNCH_CHECK();
+  return GNPDE_OK;
+}
+
+extern "C" int gnpde_initial_step_lin_f32(int64_t n, const float* y0, const float* v, double atol, double rtol,
+                                          double order, double* h, float* hf, void* workspace, size_t workspace_bytes,
+                                          void* stream) {
+  return initial_step_lin<float>(n, y0, v, atol, rtol, order, h, hf, workspace, workspace_bytes, stream);
+}
+
+extern "C" int gnpde_initial_step_lin_bf16(int64_t n, const uint16_t* y0, const uint16_t* v, double atol, double rtol,
+                                           double order, double* h, float* hf, void* workspace,
+                                           size_t workspace_bytes, void* stream) {
+  return initial_step_lin<bf16>(n, reinterpret_cast<const bf16*>(y0), reinterpret_cast<const bf16*>(v), atol, rtol,
+                                order, h, hf, workspace, workspace_bytes, stream);
 }
 
 extern "C" int gnpde_initial_step_rows(int64_t nrows, const double* rows_a, const double* rows_b, double n,

@@ -84,6 +84,8 @@ SIGNATURES = {
     "gnpde_adaptive_control": (_int, [_i64, _vp, _f64, _f64, _f64, _f64, _f64, _vp, _vp, _vp, _vp, _vp, _size, _vp]),
     "gnpde_initial_step_f32": (_int, [_i64, _vp, _vp, _vp, _f64, _f64, _f64, _vp, _vp, _vp, _size, _vp]),
     "gnpde_initial_step_rows": (_int, [_i64, _vp, _vp, _f64, _f64, _vp, _vp, _vp, _size, _vp]),
+    "gnpde_initial_step_lin_f32": (_int, [_i64, _vp, _vp, _f64, _f64, _f64, _vp, _vp, _vp, _size, _vp]),
+    "gnpde_initial_step_lin_bf16": (_int, [_i64, _vp, _vp, _f64, _f64, _f64, _vp, _vp, _vp, _size, _vp]),
     "gnpde_scaled_sq_sums_f32": (_int, [_i64, _vp, _vp, _vp, _f64, _f64, _vp, _vp, _size, _vp]),
     "gnpde_segment_sums_workspace_bytes": (_size, [_i64]),
     "gnpde_segment_sums_f64": (_int, [_i64, _i64, _vp, _vp, _vp, _size, _vp]),

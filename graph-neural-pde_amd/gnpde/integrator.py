@@ -1258,6 +1258,11 @@ DENSE_FOLD = os.environ.get('GNPDE_DENSE_FOLD', '1') != '0'
 # Off by default: the wide epilogue the two launches then take costs more than the passes
 # it saves (G-arxiv: f0 launch 80 -> 124 us, probe 76 -> 109 us)
 INIT_ROWS = os.environ.get('GNPDE_INIT_ROWS', '0') == '1'
+# The initial-step probe of an affine Krylov solve as v = L f0 (gnpde_initial_step_lin_*: d2 =
+# rms(v / scale)), run beside the phase-0 reduction on a second stream; v is the first step's
+# u_1 / dt, so that step scales it in place instead of launching K1 (GNPDE_LIN_INIT=0: the probe
+# f0 + h0 L f0 after phase 0 and a first step like the others)
+LIN_INIT = os.environ.get('GNPDE_LIN_INIT', '1') != '0'
 
 
 def _fused_adaptive_ok(func, y0, combine, options):
@@ -1395,6 +1400,7 @@ class _AdaptiveState(object):
         # the initial-step selection from the f0 / probe launches' row sums (INIT_ROWS): a second
         # row array (the f0 launch's scale_rows) and the reduction's workspace
         self.rows2, self.iws = None, None
+        self.side = None  # the second stream of the initial step (LIN_INIT)
         self.graphs = {}   # (id Y, id K0, mid, fold, renumbered) -> (graph, error-sum tensor)
         self.mempool = None
         self.warm = False
@@ -1430,6 +1436,8 @@ class _RKAdaptiveFused(_RKAdaptive):
         self.safety_f, self.ifactor_f, self.dfactor_f = float(sc['safety']), float(sc['ifactor']), float(sc['dfactor'])
         self.fold = False  # this solve's dense output folded into the Krylov steps (_integrate)
         self.init_rows = False  # its initial step from the f0 / probe launches' row sums (_integrate)
+        self.lin_init = False   # its probe v = L f0, reused as the first step's u_1 (_integrate)
+        self._first = False     # the next step is the first attempt after a lin_init probe
         self.lay = None
 
     # ---- device primitives (host-stage RHS objects supply CPU versions: tests only)
@@ -1498,13 +1506,13 @@ class _RKAdaptiveFused(_RKAdaptive):
         d['K0'] = d.get('K0', 0.0) + b00
         return ('Y', [(k, c) for k, c in d.items() if c != 0.0], cf)
 
-    def _step(self, st, t_cur, dt, mid):
+    def _step(self, st, t_cur, dt, mid, first=False):
         """Enqueue one step (stage-input pass, RHS launches, error reduction); returns
         the device error sum."""
         P = self.plan
         bufs = st.bufs
         if self.krylov is not None:
-            self._krylov_launches(st, t_cur)
+            self._krylov_launches(st, t_cur, first)
         else:
             if not self.affine:  # the first stage input X0 = y0 + dt b00 k0 (the affine mode never forms it)
                 self._apply(ops.Stage(outs=[(bufs['X0'], bufs['Y'], 1.0, 0.0, [(bufs['K0'], P.beta[0][0])])],
@@ -1518,7 +1526,7 @@ class _RKAdaptiveFused(_RKAdaptive):
             return st.rec
         return self._err_sum(st.rows)
 
-    def _krylov_launches(self, st, t):
+    def _krylov_launches(self, st, t, first=False):
         """The launches of one affine step in the Krylov basis (_KrylovPlan): u_{p+1} =
         dt L u_p into K{p+1} for p < ns - 1, then the launch over u_{ns-1} that writes y1,
         f1 (K{ns}) and the error rows.  The RHS is autonomous: every launch at t."""
@@ -1531,14 +1539,22 @@ class _RKAdaptiveFused(_RKAdaptive):
                 (bufs['K%d' % ns], None, 0.0, fcf, [(u[p], c) for p, c in ft])]
         err = (st.rows, (None, 0.0, ecf, [(u[p], c) for p, c in et]), bufs['Y'], 0, self.atol_f, self.rtol_f)
         last = ops.Stage(outs=outs, err=err, scale=st.scale, f_lin=1.0, unscaled=(1,))
-        form = None  # the folded dense output: launch 0 forms its coefficients, the last applies them
+        # the first attempt after a lin_init probe: u_1 = dt v in place (v = L f0 in K1, the same
+        # fp32 product the launch over u_0 would store), the K1 launches from u_1 on
+        p0 = 1 if first else 0
+        if first:
+            if hasattr(self.func, 'nfe'):  # the reference evaluates it: the counter keeps torchdiffeq's NFE
+                self.func.nfe += 1
+            ops.stage_apply(ops.Stage(outs=[(u[1], None, 0.0, 0.0, [(u[1], 1.0)])], scale=st.scale), None, None,
+                            u[1])
+        form = None  # the folded dense output: the step's first launch forms its coefficients, the last applies them
         if self.fold and ns >= 2:
             last.dense = (st.dslot, st.drows if self.lay is not None else None, None, None, st.dtab,
                           self._dense_table(u, ft, fcf))
             form = (None, None, st.tdev, st.dt, st.dtab, last.dense_matrix())
-        for p in range(ns - 1):
+        for p in range(p0, ns - 1):
             self.func.rhs_stage(t, u[p], ops.Stage(outs=[(u[p + 1], None, 0.0, 1.0, [])], scale=st.scale,
-                                                   dense=form if p == 0 else None), linear=True)
+                                                   dense=form if p == p0 else None), linear=True)
         self.func.rhs_stage(t, u[ns - 1], last, linear=True)
 
     def _dense_table(self, u, ft, fcf):
@@ -1617,6 +1633,21 @@ class _RKAdaptiveFused(_RKAdaptive):
         bufs = st.bufs
         Y, K0 = bufs['Y'], bufs['K0']
         h, hf = st.h, st.scale  # h[2] is st.dt: the device controller starts from it
+        if self.lin_init:
+            # phase 0 (y0, f0 -> h0, d1) on a second stream beside the probe v = L f0 (it needs no h0),
+            # then phase 1 from v; v lands in K1, the first step's u_1 buffer (_krylov_launches)
+            v = bufs['K1']
+            main = torch.cuda.current_stream(Y.device)
+            if st.side is None:
+                st.side = torch.cuda.Stream(Y.device)
+            st.side.wait_stream(main)
+            with torch.cuda.stream(st.side):
+                ops.initial_step(Y, K0, None, self.atol_f, self.rtol_f, self.order, h, hf)
+            self.func.rhs_stage(t0, K0, ops.Stage(f_out=v), linear=True)
+            main.wait_stream(st.side)
+            ops.initial_step_lin(Y, v, self.atol_f, self.rtol_f, self.order, h, hf)
+            self._first = True
+            return self._rec_reader(st, h, slot=2)
         if self.init_rows:
             # from the f0 launch's rows; then the rows of L f0 (the probe's linear part on f0, no
             # output): d2 = rms(L f0 / scale) = rms((f1 - f0) / scale) / h0 for f1 = f(y0 + h0 f0)
@@ -1658,10 +1689,13 @@ class _RKAdaptiveFused(_RKAdaptive):
 
     def _run_step(self, st, graphs_ok, t_cur, dt, mid):
         """One step: replayed from its graph when the binding's graph exists (captured
-        on first use once the module is warm), eagerly otherwise."""
+        on first use once the module is warm), eagerly otherwise.  The first attempt after
+        a lin_init probe takes its own variant (u_1 from the probe)."""
         P = self.plan
+        first, self._first = self._first, False
         if graphs_ok and st.warm and _nfe_headroom(self.func, P.ns):
-            gk = (id(st.bufs['Y']), id(st.bufs['K0']), bool(mid), self.fold, self.lay is not None, GRAPH_RECORD_COPY)
+            gk = (id(st.bufs['Y']), id(st.bufs['K0']), bool(mid), self.fold, self.lay is not None, GRAPH_RECORD_COPY,
+                  first)
             ent = st.graphs.get(gk)
             if ent is None:
                 nfe = getattr(self.func, 'nfe', None)
@@ -1672,7 +1706,7 @@ class _RKAdaptiveFused(_RKAdaptive):
                 hb = torch.empty(4, dtype=torch.float64, pin_memory=True) \
                     if (GRAPH_RECORD_COPY and self._dev_control()) else None
                 with torch.cuda.graph(g, pool=st.mempool):
-                    err = self._step(st, t_cur, dt, mid)
+                    err = self._step(st, t_cur, dt, mid, first)
                     if hb is not None:
                         hb.copy_(err, non_blocking=True)
                 if st.mempool is None:
@@ -1685,7 +1719,7 @@ class _RKAdaptiveFused(_RKAdaptive):
             if hasattr(self.func, 'nfe'):
                 self.func.nfe += P.ns
             return ent[1]
-        err = self._step(st, t_cur, dt, mid)
+        err = self._step(st, t_cur, dt, mid, first)
         st.warm = True
         return err
 
@@ -1748,6 +1782,8 @@ class _RKAdaptiveFused(_RKAdaptive):
         # the initial-step selection's squared sums formed by the f0 and probe launches themselves
         # (an affine RHS: the probe is the linear part on f0), no passes over y0, f0, f1
         self.init_rows = (INIT_ROWS and dev_init and self.affine and self._scalars['first_step'] is None)
+        self.lin_init = (LIN_INIT and not self.init_rows and dev_init and self.krylov is not None and
+                         self.krylov.ns >= 3 and self._scalars['first_step'] is None)
         if self.init_rows:
             if st.rows2 is None:
                 st.rows2 = torch.empty_like(st.rows)

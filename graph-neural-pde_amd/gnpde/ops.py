@@ -1488,6 +1488,27 @@ def initial_step(y0, f0, f1, atol, rtol, order, h, hf=None):
               _ptr(hf), _ptr(ws), nbytes, _stream(y0.device))
 
 
+def initial_step_lin(y0, v, atol, rtol, order, h, hf=None, ws=None):
+    """Phase 1 of the device initial step from v = L f0 (gnpde_initial_step_lin_*):
+    d2 = rms(v / scale); writes h[2] (and hf).  h: fp64 [3] after phase 0."""
+    dt = y0.dtype
+    if dt not in STATE_DTYPES:
+        raise TypeError("initial_step_lin: state dtype %s" % dt)
+    for t in (y0, v):
+        _require_gpu(t, "initial_step state", dt)
+        if not t.is_contiguous() or t.numel() != y0.numel():
+            raise ValueError("initial_step_lin: y0 and v must be contiguous and shaped alike")
+    _require_gpu(h, "h", torch.float64)
+    if hf is not None:
+        _require_gpu(hf, "hf", torch.float32)
+    nbytes = _lib.fn("gnpde_initial_step_workspace_bytes")()
+    if ws is None or ws.numel() < nbytes:
+        ws = torch.empty(nbytes, dtype=torch.uint8, device=y0.device)
+    name = "gnpde_initial_step_lin_f32" if dt == torch.float32 else "gnpde_initial_step_lin_bf16"
+    _lib.call(name, y0.numel(), _ptr(y0), _ptr(v), float(atol), float(rtol), float(order), _ptr(h), _ptr(hf),
+              _ptr(ws), ws.numel(), _stream(y0.device))
+
+
 def initial_step_rows(rows_a, rows_b, n, order, h, hf, ws=None):
     """gnpde_initial_step_rows: the initial-step rules from the squared-sum rows of the f0
     launch (phase 0: rows_a its err_rows, rows_b its scale_rows) or of the launch over L f0

@@ -622,6 +622,18 @@ int gnpde_adaptive_control(int64_t nrows, const double* err_rows, double n, doub
                            double ifactor, double dfactor, double* dt, float* scale, double* rec, double* t,
                            void* workspace, size_t workspace_bytes, void* stream);
 size_t gnpde_initial_step_workspace_bytes(void);
+/* Phase 1 of gnpde_initial_step_f32 for an affine RHS f(y) = L y + s (ABI 8), from
+ * v = L f0 (the linear part evaluated on f0, which is also the first step's u_1 / dt):
+ *   d2 = rms(v / scale)   (= rms((f1 - f0)/scale)/h0 for f1 = f(y0 + h0 f0), without the
+ *                          fp32 cancellation of f1 - f0)
+ * then h[2] and *hf (when given) as phase 1; reads h[0], h[1] of phase 0.  scale, the
+ * quotient and the fp64 squares as gnpde_initial_step_f32.  Two launches; workspace
+ * gnpde_initial_step_workspace_bytes().                                        */
+int gnpde_initial_step_lin_f32(int64_t n, const float* y0, const float* v, double atol, double rtol, double order,
+                               double* h, float* hf, void* workspace, size_t workspace_bytes, void* stream);
+int gnpde_initial_step_lin_bf16(int64_t n, const uint16_t* y0, const uint16_t* v, double atol, double rtol,
+                                double order, double* h, float* hf, void* workspace, size_t workspace_bytes,
+                                void* stream);
 /* gnpde_initial_step_f32's scalar rules from per-row squared sums formed by the RHS
  * launches themselves (ABI 8; an affine RHS f(y) = L y + s): phase 0 (rows_b given)
  * with rows_a = the f0 launch's err_rows (e = f0, err_y1 = -2: sum (f0/scale)^2) and

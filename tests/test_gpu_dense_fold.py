@@ -98,33 +98,37 @@ def test_dense_fold_only_for_one_output_time(monkeypatch):
     assert not f2 and f1
 
 
+@pytest.mark.parametrize("path", ["rows", "lin"])
 @pytest.mark.parametrize("add_source", [False, True])
 @pytest.mark.parametrize("rtol", [1e-3, 1e-6])
-def test_initial_step_from_launch_rows(monkeypatch, add_source, rtol):
+def test_initial_step_from_launch_rows(monkeypatch, path, add_source, rtol):
     """The first step of an affine solve from the row sums of the f0 launch (err rows of f0
     and scale_rows of y0, tol = atol + rtol |y0|) and of the probe launch over L f0
     (integrator.INIT_ROWS, gnpde_initial_step_rows) against torchdiffeq's
     _select_initial_step restated in fp64 on the oracle's RHS (src/block_constant.py:46-51
     solves with the solver's default first step): within 1e-6 relative — the fp32 path
-    (GNPDE_INIT_ROWS=0) forms (f1 - f0) / h0 in fp32, the rows path L f0 itself."""
+    (GNPDE_INIT_ROWS=0) forms (f1 - f0) / h0 in fp32, the rows path L f0 itself.  path 'lin'
+    (integrator.LIN_INIT, the default): phase 0 beside the probe v = L f0 on a second stream,
+    d2 = rms(v / scale) (gnpde_initial_step_lin_f32)."""
     N, E, C = 3000, 30000, 48
     eo, wo, rng = _graph(N, E, 53)
     x = rng.standard_normal((1, N, C)).astype(np.float32)
     x0 = rng.standard_normal((1, N, C)).astype(np.float32)
     func = _laplacian(C, eo, wo, alpha=0.7, add_source=add_source, x0=T(x0) if add_source else None)
     atol = rtol * 0.1
-    monkeypatch.setattr(gi, "INIT_ROWS", True)
+    monkeypatch.setattr(gi, "INIT_ROWS", path == "rows")
+    monkeypatch.setattr(gi, "LIN_INIT", path == "lin")
     seen = {}
     orig = gi._RKAdaptiveFused._initial_step_device
 
     def spy(self, st, t0):
         read = orig(self, st, t0)
         seen['h'] = st.h.clone()
-        seen['rows'] = self.init_rows
+        seen['path'] = 'rows' if self.init_rows else ('lin' if self.lin_init else None)
         return read
     monkeypatch.setattr(gi._RKAdaptiveFused, "_initial_step_device", spy)
     _solve(func, x, [0.0, 0.5], rtol, atol)
-    assert seen['rows']
+    assert seen['path'] == path
     h = seen['h'].cpu().numpy()
     f = lambda y: O.laplacian_rhs(eo, y, x0, 0.7, 0.4, edge_weight=wo, add_source=add_source)  # noqa: E731
     y = x.astype(np.float64)
@@ -138,3 +142,34 @@ def test_initial_step_from_launch_rows(monkeypatch, add_source, rtol):
     want = min(100 * h0, h1)
     assert abs(h[0] - h0) <= 1e-6 * h0 and abs(h[1] - d1) <= 1e-6 * d1
     assert abs(h[2] - want) <= 1e-6 * want
+
+
+@pytest.mark.parametrize("add_source", [False, True])
+def test_lin_init_first_step_vs_probe_path(monkeypatch, add_source):
+    """The first step after the lin_init probe (u_1 = dt v scaled in place, v = L f0 from
+    the probe) against the probe path (GNPDE_LIN_INIT=0: probe f0 + h0 L f0, first step
+    like the others): the same step count and NFE (the reused evaluation is counted, as
+    torchdiffeq evaluates it), values within 1e-6 (the first step sizes differ by the
+    fp32 cancellation the probe path carries), both within RTOL of the oracle; replayed
+    solves bit-equal."""
+    N, E, C = 4000, 40000, 64
+    eo, wo, rng = _graph(N, E, 59)
+    x = rng.standard_normal((1, N, C)).astype(np.float32)
+    x0 = rng.standard_normal((1, N, C)).astype(np.float32)
+    res = {}
+    for lin in (False, True):
+        monkeypatch.setattr(gi, "LIN_INIT", lin)
+        func = _laplacian(C, eo, wo, alpha=0.3, add_source=add_source, x0=T(x0) if add_source else None)
+        runs = []
+        for _ in range(3):
+            n0 = func.nfe
+            z, n, _, path = _solve(func, x, [0.0, 2.0], 1e-4, 1e-5)
+            runs.append((z, n, func.nfe - n0))
+        assert torch.equal(runs[1][0], runs[2][0]) and runs[1][1:] == runs[2][1:]
+        res[lin] = runs[2]
+    assert res[True][1] == res[False][1] and res[True][2] == res[False][2]
+    assert rel(res[True][0], res[False][0]) <= 1e-6
+    f = lambda t, y: O.laplacian_rhs(eo, y, x0, 0.3, 0.4, edge_weight=wo, add_source=add_source)  # noqa: E731
+    want, n_want = O.odeint_adaptive(f, x, [0.0, 2.0], 'dopri5', 1e-4, 1e-5)
+    assert res[True][1] == n_want
+    assert rel(res[True][0], want) <= RTOL
