@@ -403,9 +403,29 @@ def _graph_cache_key(func, method, y, state):
     else:  # a plain RHS object (gnpde.dist shards): the scalars it reads by pointer
         tens = [_tensor_key(t) for t in getattr(func, 'capture_key_tensors', lambda: ())()]
     opt = getattr(func, 'opt', None)
-    okey = repr(sorted(opt.items(), key=lambda kv: str(kv[0]))) if isinstance(opt, dict) else None
+    okey = _opt_key(opt) if isinstance(opt, dict) else None
     return (method, tuple(y.shape), tuple(y.stride()), y.dtype, str(y.device), okey, tuple(tens),
             tuple(id(o) for o in state))
+
+
+_OPT_KEYS = {}  # id(opt dict) -> (its items when keyed, key string)
+
+
+def _opt_key(opt):
+    """The options part of a graph cache key: the sorted repr of the dict, recomputed only
+    when its items changed (an in-place edit of the module's opt changes them)."""
+    items = tuple(opt.items())
+    hit = _OPT_KEYS.get(id(opt))
+    try:
+        if hit is not None and hit[0] == items:
+            return hit[1]
+    except (TypeError, ValueError):  # values without a plain equality (arrays): no cache
+        return repr(sorted(opt.items(), key=lambda kv: str(kv[0])))
+    key = repr(sorted(opt.items(), key=lambda kv: str(kv[0])))
+    if len(_OPT_KEYS) > 256:
+        _OPT_KEYS.clear()
+    _OPT_KEYS[id(opt)] = (items, key)
+    return key
 
 
 def _replayable(func):
@@ -1401,6 +1421,7 @@ class _AdaptiveState(object):
         # row array (the f0 launch's scale_rows) and the reduction's workspace
         self.rows2, self.iws = None, None
         self.side = None  # the second stream of the initial step (LIN_INIT)
+        self.canon = None  # the y / f0 buffer binding every solve starts from (_integrate)
         self.graphs = {}   # (id Y, id K0, mid, fold, renumbered) -> (graph, error-sum tensor)
         self.mempool = None
         self.warm = False
@@ -1752,6 +1773,11 @@ class _RKAdaptiveFused(_RKAdaptive):
         dev = y0.device
         st, graphs_ok = self._state(y0)
         bufs = st.bufs
+        if st.canon is not None:
+            # every solve starts from the same binding of the rotating y / f0 buffers, so it walks
+            # the same sequence of bindings and replays the same step graphs (a solve starting
+            # where the last one ended met bindings whose graphs were not captured yet)
+            bufs.update(st.canon)
         # The dense output folded into the last launch of every step (DENSE_FOLD; ABI 8): a
         # solve to one output time in the Krylov basis under the device controller.  Each
         # step's launch writes the interpolant at th[1] straight into sol[1] (the caller's
@@ -1830,6 +1856,8 @@ class _RKAdaptiveFused(_RKAdaptive):
         spec_ok = dev_ctl and graphs_ok and ADAPTIVE_SPEC and P.fsal
         if spec_ok and 'Ys' not in bufs:
             bufs['Ys'], bufs['Ks'] = torch.empty_like(bufs['Y']), torch.empty_like(bufs['K0'])
+        if st.canon is None or len(st.canon) < len(bufs):  # (no step has rotated them in this solve yet)
+            st.canon = dict(bufs)
         pending = None  # the record reader of the step enqueued ahead: the current step
         pre_interp = None  # (output index, t0, dt) of a dense output enqueued ahead of its step's record
         if dt_read is not None:
