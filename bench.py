@@ -793,7 +793,7 @@ CORA_DOPRI5 = (18.294754260552843, 821.9773048827274)
 
 
 def _timed_dopri5(func, x, T, tol_scale, dev, reps):
-    """One warm-up solve, then `reps` solves of dopri5 over [0, T] timed between
+    """Two warm-up solves, then `reps` solves of dopri5 over [0, T] timed between
     device syncs (the step's one host read is inside)."""
     import gnpde
     import gnpde.integrator as integ
@@ -863,7 +863,8 @@ def bench_dopri5(ei, w, x, dev, k1_stage_ms, k1_plain_ms, reps=3):
     rl = None
     if dev_ms:
         t = dev_ms * 1e-3
-        kern = ("5 STG1 + 1 STG4 agg_kernel launches (Krylov step)" if krylov else
+        kern = ("5 STG1 + 1 STG5 agg_kernel launches (Krylov step; STG5: STG4 + the folded dense output)"
+                if krylov else
                 "2 STG1 + 4 STG4 agg_kernel launches")
         rl = {"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s", "kernel": "one replayed dopri5 step (%s, "
               "sum_partial_kernel, adaptive_control_kernel)" % kern, "step_ms": round(dev_ms, 4),
@@ -889,8 +890,10 @@ def bench_dopri5(ei, w, x, dev, k1_stage_ms, k1_plain_ms, reps=3):
         "roofline": rl,
         "basis": "ms_per_step = whole solve (entry copy, initial-step selection, steps, dense output) / steps; "
                  "per step: 6 RHS launches (Krylov step, f affine: u_{p+1} = dt L u_p, the last launch forming y1, "
-                 "f1 and the error rows from u_0..u_5) + the error reduction with the device step-size "
-                 "controller, one host read; rhs_stage_ms = the rk4 fused-stage K1 launch time"}
+                 "f1, the error rows and — in the step crossing the output time — the dense output, from "
+                 "u_0..u_5) + the error reduction with the device step-size controller, one host read; the "
+                 "initial step's probe v = L f0 is the first step's u_1 / dt; rhs_stage_ms = the rk4 fused-stage "
+                 "K1 launch time"}
     progress("dopri5 G-arxiv: %.3f ms/step, %d steps" % (ms_step, steps))
     # configs[1] shape
     N, E, Cc, h, att = 2708, 13264, 80, 8, 128  # Cora: 10,556 edges + 2,708 self loops

@@ -2014,8 +2014,9 @@ def adaptive_step_graph(func):
     hit = _ADAPTIVE_CACHE.get(func)
     if hit is None or not hit[1].graphs:
         return None
-    ent = next(iter(hit[1].graphs.values()))
-    return ent[0]
+    # a step like most of a solve's: not the first attempt after a lin_init probe (key[-1])
+    ents = [e for k, e in hit[1].graphs.items() if not k[-1]] or list(hit[1].graphs.values())
+    return ents[0][0]
 
 
 def odeint(func, y0, t, rtol=1e-7, atol=1e-9, method=None, options=None, combine=None):
