@@ -1247,7 +1247,15 @@ def attn_weights(g, ns, m, rl, norm_idx, seg=True, edges=None):
 SMALL_PRECOMPUTE = os.environ.get("GNPDE_SMALL_PRECOMPUTE", "wide")
 
 
+# Any graph: the adaptive solvers' wide stages take the weights pass too, so the plain-weight
+# K1 fuses the stage (STG 4) instead of forming f and applying the stage in a second pass
+# over f and its operands (gnpde_stage_apply_f32) — GNPDE_WIDE_PRECOMPUTE=0: the pass.
+WIDE_PRECOMPUTE = os.environ.get("GNPDE_WIDE_PRECOMPUTE", "1") != "0"
+
+
 def _small_precompute(g, stage):
+    if WIDE_PRECOMPUTE and stage is not None and stage.wide:
+        return True
     if g.R >= SMALL_GRAPH_ROWS or SMALL_PRECOMPUTE == "none":
         return False
     return SMALL_PRECOMPUTE == "all" or (stage is not None and stage.wide)
