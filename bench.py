@@ -793,8 +793,9 @@ CORA_DOPRI5 = (18.294754260552843, 821.9773048827274)
 
 
 def _timed_dopri5(func, x, T, tol_scale, dev, reps):
-    """Two warm-up solves, then `reps` solves of dopri5 over [0, T] timed between
-    device syncs (the step's one host read is inside)."""
+    """Two warm-up solves, then `reps` solves of dopri5 over [0, T], each timed from its
+    call to a device sync after it (the steps' host reads inside); the median solve
+    (a box's occasional slow solve — host preemption — does not move it)."""
     import gnpde
     import gnpde.integrator as integ
     t = torch.tensor([0.0, T], dtype=torch.float32, device=dev)
@@ -804,18 +805,20 @@ def _timed_dopri5(func, x, T, tol_scale, dev, reps):
             z = gnpde.odeint(func, x, t, **kw)[1]
         torch.cuda.synchronize()
         nfe0 = func.nfe
-        t0 = time.perf_counter()
+        els = []
         for _ in range(reps):
+            t0 = time.perf_counter()
             z = gnpde.odeint(func, x, t, **kw)[1]
-        torch.cuda.synchronize()
-        el = (time.perf_counter() - t0) / reps
+            torch.cuda.synchronize()
+            els.append(time.perf_counter() - t0)
+        el = sorted(els)[len(els) // 2]
     assert torch.isfinite(z).all()
     steps = integ.odeint.last_n_steps
     nfe = (func.nfe - nfe0) // reps
     return el, steps, nfe
 
 
-def bench_dopri5(ei, w, x, dev, k1_stage_ms, k1_plain_ms, reps=3):
+def bench_dopri5(ei, w, x, dev, k1_stage_ms, k1_plain_ms, reps=9):
     """dopri5 as the reference runs it (src/best_params.py): the fused adaptive step
     (gnpde.integrator._RKAdaptiveFused: stage combinations and error rows in the RHS
     epilogues, one fixed-order norm reduction and one host read per step).
