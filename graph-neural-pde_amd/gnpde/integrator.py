@@ -1283,6 +1283,10 @@ INIT_ROWS = os.environ.get('GNPDE_INIT_ROWS', '0') == '1'
 # u_1 / dt, so that step scales it in place instead of launching K1 (GNPDE_LIN_INIT=0: the probe
 # f0 + h0 L f0 after phase 0 and a first step like the others)
 LIN_INIT = os.environ.get('GNPDE_LIN_INIT', '1') != '0'
+# The f0 launch and the lin_init initial step replayed as one captured graph once warm
+# (GNPDE_PROLOGUE_GRAPH=1).  Off by default: measured no faster (G-arxiv 2.705 against 2.698 ms
+# per solve) — once the first launch runs, the host stays ahead of the device anyway.
+PROLOGUE_GRAPH = os.environ.get('GNPDE_PROLOGUE_GRAPH', '0') == '1'
 
 
 def _fused_adaptive_ok(func, y0, combine, options):
@@ -1421,6 +1425,10 @@ class _AdaptiveState(object):
         # row array (the f0 launch's scale_rows) and the reduction's workspace
         self.rows2, self.iws = None, None
         self.side = None  # the second stream of the initial step (LIN_INIT)
+        # the captured prologue of a lin_init solve (f0 and the initial-step launches) and the
+        # workspaces of its two reductions (phase 0 runs beside the probe: two buffers)
+        self.pro = None
+        self.iws0 = self.iws1 = None
         self.canon = None  # the y / f0 buffer binding every solve starts from (_integrate)
         self.graphs = {}   # (id Y, id K0, mid, fold, renumbered) -> (graph, error-sum tensor)
         self.mempool = None
@@ -1645,6 +1653,50 @@ class _RKAdaptiveFused(_RKAdaptive):
             return h.tolist()
         return read
 
+    def _lin_init_launches(self, st, t0):
+        """The lin_init initial step: phase 0 (y0, f0 -> h0, d1) on a second stream beside the
+        probe v = L f0 (it needs no h0), then phase 1 from v; v lands in K1, the first step's
+        u_1 buffer (_krylov_launches).  No host read (capturable: _prologue)."""
+        bufs = st.bufs
+        Y, K0, v = bufs['Y'], bufs['K0'], bufs['K1']
+        h, hf = st.h, st.scale
+        if st.iws0 is None:
+            nb = _lib.fn("gnpde_initial_step_workspace_bytes")()
+            st.iws0 = torch.empty(nb, dtype=torch.uint8, device=Y.device)
+            st.iws1 = torch.empty(nb, dtype=torch.uint8, device=Y.device)
+        main = torch.cuda.current_stream(Y.device)
+        if st.side is None:
+            st.side = torch.cuda.Stream(Y.device)
+        st.side.wait_stream(main)
+        with torch.cuda.stream(st.side):
+            ops.initial_step(Y, K0, None, self.atol_f, self.rtol_f, self.order, h, hf, ws=st.iws0)
+        self.func.rhs_stage(t0, K0, ops.Stage(f_out=v), linear=True)
+        main.wait_stream(st.side)
+        ops.initial_step_lin(Y, v, self.atol_f, self.rtol_f, self.order, h, hf, ws=st.iws1)
+
+    def _prologue(self, st, graphs_ok, t0):
+        """f0 into K0 and the lin_init initial step as ONE captured graph (PROLOGUE_GRAPH) once
+        the module is warm.  Returns True when replayed (the caller reads h)."""
+        if not (PROLOGUE_GRAPH and graphs_ok and st.warm and _nfe_headroom(self.func, 2)):
+            return False
+        bufs = st.bufs
+        if st.pro is None:
+            nfe = getattr(self.func, 'nfe', None)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=st.mempool):
+                self.func.rhs_stage(t0, bufs['Y'], ops.Stage(f_out=bufs['K0']))
+                self._lin_init_launches(st, t0)
+            if st.mempool is None:
+                st.mempool = g.pool()
+            if nfe is not None:
+                self.func.nfe = nfe  # capture records launches, it evaluates nothing
+            st.pro = g
+        st.pro.replay()
+        if hasattr(self.func, 'nfe'):
+            self.func.nfe += 2
+        self._first = True
+        return True
+
     def _initial_step_device(self, st, t0):
         """_select_initial_step on the device (gnpde_initial_step_*: the two fixed-order
         norm reductions and the scalar rules in HIP, the probe y0 + h0 f0 as one stage
@@ -1655,18 +1707,7 @@ class _RKAdaptiveFused(_RKAdaptive):
         Y, K0 = bufs['Y'], bufs['K0']
         h, hf = st.h, st.scale  # h[2] is st.dt: the device controller starts from it
         if self.lin_init:
-            # phase 0 (y0, f0 -> h0, d1) on a second stream beside the probe v = L f0 (it needs no h0),
-            # then phase 1 from v; v lands in K1, the first step's u_1 buffer (_krylov_launches)
-            v = bufs['K1']
-            main = torch.cuda.current_stream(Y.device)
-            if st.side is None:
-                st.side = torch.cuda.Stream(Y.device)
-            st.side.wait_stream(main)
-            with torch.cuda.stream(st.side):
-                ops.initial_step(Y, K0, None, self.atol_f, self.rtol_f, self.order, h, hf)
-            self.func.rhs_stage(t0, K0, ops.Stage(f_out=v), linear=True)
-            main.wait_stream(st.side)
-            ops.initial_step_lin(Y, v, self.atol_f, self.rtol_f, self.order, h, hf)
+            self._lin_init_launches(st, t0)
             self._first = True
             return self._rec_reader(st, h, slot=2)
         if self.init_rows:
@@ -1810,6 +1851,7 @@ class _RKAdaptiveFused(_RKAdaptive):
         self.init_rows = (INIT_ROWS and dev_init and self.affine and self._scalars['first_step'] is None)
         self.lin_init = (LIN_INIT and not self.init_rows and dev_init and self.krylov is not None and
                          self.krylov.ns >= 3 and self._scalars['first_step'] is None)
+        dt_read = None  # the device initial step's reader: the first step is enqueued before it is read
         if self.init_rows:
             if st.rows2 is None:
                 st.rows2 = torch.empty_like(st.rows)
@@ -1820,16 +1862,18 @@ class _RKAdaptiveFused(_RKAdaptive):
             self.func.rhs_stage(t0, bufs['Y'], ops.Stage(
                 f_out=bufs['K0'], err=(st.rows, (None, 0.0, 1.0, []), bufs['Y'], -2, self.atol_f, self.rtol_f),
                 scale_rows=st.rows2))
+        elif dev_init and self.lin_init and self._prologue(st, graphs_ok, t0):
+            dt_read = self._rec_reader(st, st.h, slot=2)  # f0 and the initial step replayed
         elif dev_init:  # f0 straight into K0 (the RHS epilogue's f_out)
             self.func.rhs_stage(t0, bufs['Y'], ops.Stage(f_out=bufs['K0']))
         else:
             f0 = self.func(t0, bufs['Y'])
             bufs['K0'].copy_(f0)
         dt_on_device = False
-        dt_read = None  # the device initial step's reader: the first step is enqueued before it is read
         if self._scalars['first_step'] is None:
             if dev_init:
-                dt_read = self._initial_step_device(st, t0)
+                if dt_read is None:
+                    dt_read = self._initial_step_device(st, t0)
                 dt = None
                 dt_on_device = True  # st.dt and st.scale hold it already
             else:

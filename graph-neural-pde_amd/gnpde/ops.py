@@ -1473,7 +1473,7 @@ def segment_sums(v, out):
               _stream(v.device))
 
 
-def initial_step(y0, f0, f1, atol, rtol, order, h, hf=None):
+def initial_step(y0, f0, f1, atol, rtol, order, h, hf=None, ws=None):
     """torchdiffeq's _select_initial_step on the device (gnpde_initial_step_*):
     phase 0 (f1 None) writes h[0] = h0, h[1] = d1 and hf = float(h0); phase 1
     (f1 = f(y0 + h0 f0)) writes h[2] = the first step.  h: fp64 [3], hf: fp32 0-d."""
@@ -1490,7 +1490,8 @@ def initial_step(y0, f0, f1, atol, rtol, order, h, hf=None):
     if hf is not None:
         _require_gpu(hf, "hf", torch.float32)
     nbytes = _lib.fn("gnpde_initial_step_workspace_bytes")()
-    ws = torch.empty(nbytes, dtype=torch.uint8, device=y0.device)
+    if ws is None or ws.numel() < nbytes:
+        ws = torch.empty(nbytes, dtype=torch.uint8, device=y0.device)
     name = "gnpde_initial_step_bf16" if dt == torch.bfloat16 else "gnpde_initial_step_f32"
     _lib.call(name, y0.numel(), _ptr(y0), _ptr(f0), _ptr(f1), float(atol), float(rtol), float(order), _ptr(h),
               _ptr(hf), _ptr(ws), nbytes, _stream(y0.device))

@@ -12,10 +12,10 @@ import dopri5_prof  # noqa: E402
 import torch  # noqa: E402
 
 CONFIGS = {
-    "default": dict(DENSE_FOLD=True, INIT_ROWS=False, GRAPH_RECORD_COPY=True, LIN_INIT=True),
-    "no-lin": dict(DENSE_FOLD=True, INIT_ROWS=False, GRAPH_RECORD_COPY=True, LIN_INIT=False),
-    "rows": dict(DENSE_FOLD=True, INIT_ROWS=True, GRAPH_RECORD_COPY=True, LIN_INIT=False),
-    "round5": dict(DENSE_FOLD=False, INIT_ROWS=False, GRAPH_RECORD_COPY=False, LIN_INIT=False),
+    "default": dict(DENSE_FOLD=True, INIT_ROWS=False, GRAPH_RECORD_COPY=True, LIN_INIT=True, PROLOGUE_GRAPH=True),
+    "no-pro": dict(DENSE_FOLD=True, INIT_ROWS=False, GRAPH_RECORD_COPY=True, LIN_INIT=True, PROLOGUE_GRAPH=False),
+    "no-lin": dict(DENSE_FOLD=True, INIT_ROWS=False, GRAPH_RECORD_COPY=True, LIN_INIT=False, PROLOGUE_GRAPH=False),
+    "round5": dict(DENSE_FOLD=False, INIT_ROWS=False, GRAPH_RECORD_COPY=False, LIN_INIT=False, PROLOGUE_GRAPH=False),
 }
 
 
