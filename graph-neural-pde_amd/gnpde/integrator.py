@@ -2089,6 +2089,7 @@ def odeint(func, y0, t, rtol=1e-7, atol=1e-9, method=None, options=None, combine
             out = _LaplacianAdaptiveFn.apply(y0, func.alpha_train, func.beta_train, w, func, _host_times(t), method,
                                              rtol, atol, options.get('first_step'), kw['max_num_steps'])
             odeint.last_path = 'fused_backprop'
+            odeint.last_dense_fold = False
             return out
         else:
             solver = _RKAdaptive(func, y0, rtol, atol, combine, **kw)

@@ -484,3 +484,47 @@ def test_krylov_step_selection():
         assert solver('dopri5', HostLinearRHS(A)).krylov is None
     finally:
         gode.KRYLOV_STEP = old
+
+
+@pytest.mark.parametrize("method", ["dopri5", "bosh3"])
+def test_dense_fold_table_matches_host_interpolant(method):
+    """The folded dense output's basis table (integrator._RKAdaptiveFused._dense_table, ABI 8
+    dense_m) evaluated at a step's theta and dt — the combination the K1 epilogue forms
+    (csrc dense_coefs) — equals the interpolant the separate pass forms (_interp_into's
+    Krylov branch: y0, the u_p and f1 = sum_p f1_p u_p + fcf f'), coefficient by coefficient,
+    and reproduces torchdiffeq's quartic on random u_p (a float64 restatement of the oracle's
+    _interp_fit on the same step)."""
+    P = gode._adaptive_plan(method)
+    K = gode._krylov_plan(P)
+    ns = K.ns
+    rng = np.random.default_rng(7)
+    u = [rng.standard_normal(5) for _ in range(ns + 1)]  # u_0 .. u_ns (u_ns = (dt L) u_{ns-1})
+    y0 = rng.standard_normal(5)
+    fp = u[ns - 1] + u[ns]  # f' of the last launch (f_lin = 1)
+    y1t, (ft, fcf), _ = K.last_launch_terms()
+    fake = gode._RKAdaptiveFused.__new__(gode._RKAdaptiveFused)
+    fake.krylov, fake.plan = K, P
+    keys = ["u%d" % p for p in range(ns)]
+    table = fake._dense_table(keys, ft, fcf)
+    for theta, dt in ((0.3, 0.7), (0.85, 1.9), (1.0, 0.25)):
+        x2, x3, x4 = theta ** 2, theta ** 3, theta ** 4
+        cy0 = 1 - 11 * x2 + 18 * x3 - 8 * x4
+        cy1 = -5 * x2 + 14 * x3 - 8 * x4
+        cym = 16 * x2 - 32 * x3 + 16 * x4
+        cf0 = dt * (theta - 4 * x2 + 5 * x3 - 2 * x4)
+        cf1 = dt * (x2 - 3 * x3 + 2 * x4)
+        w = [cy0 + cy1 + cym, dt * cy1, dt * cym, cf0, cf1]
+        coef = lambda key: sum(wm * c for wm, c in zip(w, table.get(key, [0.0] * 5)))  # noqa: E731
+        dense = coef('base') * y0 + sum(coef(k) * u[p] for p, k in enumerate(keys)) + coef('f') * fp
+        # the host pass: y1, y_mid and f1 from the u_p, then the quartic
+        y1 = y0 + dt * sum(K.G[p] * u[p] for p in range(ns))
+        f1 = sum(c * u[p] for p, c in ft) + fcf * fp
+        ymid = y0 + dt * (sum(K.Mu[p] * u[p] for p in range(ns)) + P.c_mid[ns] * f1)
+        want = cy0 * y0 + cy1 * y1 + cym * ymid + cf0 * u[0] + cf1 * f1
+        assert np.allclose(dense, want, rtol=1e-12, atol=1e-12)
+        # torchdiffeq's _interp_fit form (oracle.odeint_adaptive): the same polynomial
+        p4 = 2 * dt * (f1 - u[0]) - 8 * (y1 + y0) + 16 * ymid
+        p3 = dt * (5 * u[0] - 3 * f1) + 18 * y0 + 14 * y1 - 32 * ymid
+        p2 = dt * (f1 - 4 * u[0]) - 11 * y0 - 5 * y1 + 16 * ymid
+        quartic = y0 + theta * (dt * u[0]) + x2 * p2 + x3 * p3 + x4 * p4
+        assert np.allclose(dense, quartic, rtol=1e-12, atol=1e-12)
