@@ -290,6 +290,14 @@ __device__ __forceinline__ void hub_arrive_slots(int4* heavy, int n_heavy, bool 
   }
 }
 
+// The folded dense output's crossing flag and coefficients (dense_coefs), formed ahead of
+// the launch whose stage asks for them (ABI 8: dense_tab without dense_out) for the step's
+// last launch.  A launch of its own: the same branch at the top of the aggregation kernel
+// cost every instantiation (BLEND's fp32 rk4 step 0.556 -> 0.583 ms).
+static __global__ __launch_bounds__(64) void dense_coef_kernel(gnpde_stage_epilogue_t st) {
+  if (threadIdx.x == 0) dense_coefs(st, st.dense_tab);
+}
+
 // ------------------------------------------------------------------ aggregation kernel
 // Lane layout: RPW row slots of SL = 64/RPW lanes per wavefront (one plan item
 // each); inside a slot lane = g*GL + gl: G = SL/GL edges are gathered side by
@@ -312,10 +320,6 @@ __global__ __launch_bounds__(256) void agg_kernel(const int4* __restrict__ items
   const int g = sl / GL, gl = sl % GL;
   const int wid = uniform(xcd_block(ep.xcd_remap) * kWavesPerBlock + (threadIdx.x >> 6));
   const int item = wid * RPW + rs;
-  // the step's folded dense-output coefficients, for its last launch (ABI 8: a stage with
-  // dense_tab but no dense_out); kernel-argument branch
-  if (ep.has_stage && ep.st.dense_tab && !ep.st.dense_out && blockIdx.x == 0 && threadIdx.x == 0)
-    dense_coefs(ep.st, ep.st.dense_tab);
   if (wid * RPW >= n_items) return;
   // RPW = 3 (SL = 21): lane 63 is in no slot
   const bool live = item < n_items && rs < RPW;
@@ -488,6 +492,10 @@ static int launch_agg_cfg(const int4* items, int64_t n_items, int4* heavy, int64
   // leaner instantiation: 56-60 VGPRs, 8 waves per SIMD; the dot terms of the adjoint
   // stages alone cost the general one 40+ VGPRs (fused rk4 K1 92.9 -> 107 us at 4 waves)
   int stg = epi_stage_kind(ep);
+  if (ep.has_stage && ep.st.dense_tab && !ep.st.dense_out) {  // the step's dense-output coefficients
+    dense_coef_kernel<<<1, kWave, 0, s>>>(ep.st);
+    GNPDE_LAUNCH_CHECK();
+  }
   if (n_items > 0) {
     // the one-output adjoint stages: fp32 plain weights only (the transposed aggregation)
     if (stg == 3 && !(std::is_same<WP, PlainWeights>::value && sizeof(T) == 4)) stg = 2;

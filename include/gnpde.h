@@ -260,8 +260,8 @@ size_t gnpde_plan_workspace_bytes(int64_t R);
  * GNPDE_STAGE_MAX_K + 3 floats holding the crossing flag and the coefficients of
  * the launch's step, which an EARLIER launch of the same step forms: a K1 launch
  * whose stage sets dense_tab, dense_t, dense_dt and dense_m but not dense_out writes
- * them (one thread, before its aggregation) — the first launch of the step, so
- * the one that applies them reads them from memory into scalar registers.     */
+ * them (a one-wavefront launch ahead of its aggregation) — the first launch of
+ * the step, so the one that applies them reads them into scalar registers.    */
 #define GNPDE_STAGE_MAX_OUT 2
 #define GNPDE_STAGE_MAX_K 6
 #define GNPDE_DENSE_BASIS 5
